@@ -1,0 +1,135 @@
+/*
+ * tbgpu.h — C ABI of the MI355X batch-commit engine for TigerBeetle's create_accounts /
+ * create_transfers state-machine path.
+ *
+ * Drop-in boundary: these entry points are what a Zig `StateMachineType` wrapper binds through
+ * `@cImport` to replace the reference's synchronous commit:
+ *
+ *   reference interface                                   replaced by
+ *   ----------------------------------------------------  ----------------------------------------
+ *   StateMachine.init(allocator, grid, options)            tbgpu_init
+ *     (src/state_machine.zig:264-278)
+ *   StateMachine.deinit / reset (:280-299)                 tbgpu_deinit / tbgpu_reset
+ *   StateMachine.commit(client, op, timestamp, operation,  tbgpu_commit (one prepare) and
+ *     input, output) -> usize (:508-540)                     tbgpu_commit_many (N prepares, one
+ *                                                             device pass; same bytes as N commits)
+ *   execute_lookup_accounts / _transfers (:700-736)        tbgpu_commit with operation 130 / 131
+ *   `setup` action of the table tests (:1398-1407)         tbgpu_test_set_balances (test only)
+ *   StateMachine.commit_timestamp field (:251)             tbgpu_commit_timestamp
+ *
+ * Layouts are the reference's extern structs (src/tigerbeetle.zig:7-249), identical to the C
+ * client header (src/clients/c/tb_client.h:25-64,150-158): Account and Transfer are 128-byte
+ * little-endian records, results are {uint32 index, uint32 result} pairs, only non-ok events,
+ * ascending index.  Operation numbers: 128 create_accounts, 129 create_transfers,
+ * 130 lookup_accounts, 131 lookup_transfers (src/state_machine.zig:208-214).
+ *
+ * Conventions (src/state_machine.zig:508-540):
+ *   - Every call is synchronous unless its name ends in _async; calls never overlap.
+ *   - Invalid input is reported through result codes, never through the status.
+ *   - A non-zero status is TBGPU_STATUS_INVALID (bad arguments: the reference could not have
+ *     been called that way), TBGPU_STATUS_PANIC (the reference would have trapped: an overflow
+ *     assert, a failed invariant, `timestamp <= commit_timestamp`), or TBGPU_STATUS_DEVICE
+ *     (a HIP error).  The Zig wrapper turns PANIC/DEVICE into @panic.
+ *   - No allocation after tbgpu_init.
+ */
+#ifndef TBGPU_H
+#define TBGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TBGPU_STATUS_OK 0
+#define TBGPU_STATUS_INVALID 1
+#define TBGPU_STATUS_PANIC 2
+#define TBGPU_STATUS_DEVICE 3
+
+#define TBGPU_OPERATION_CREATE_ACCOUNTS 128
+#define TBGPU_OPERATION_CREATE_TRANSFERS 129
+#define TBGPU_OPERATION_LOOKUP_ACCOUNTS 130
+#define TBGPU_OPERATION_LOOKUP_TRANSFERS 131
+
+/* batch_max.create_transfers for the production config (src/state_machine.zig:46-65). */
+#define TBGPU_BATCH_EVENTS_MAX 8191u
+
+/* Config flags. */
+#define TBGPU_CONFIG_PROFILE (1u << 0) /* time every kernel with HIP events (tbgpu_get_stats) */
+
+typedef struct tbgpu_config {
+    uint64_t accounts_max;      /* HBM account table capacity (the groove's object count) */
+    uint64_t transfers_max;     /* HBM transfer store capacity */
+    uint32_t pass_events_max;   /* max events in one device pass (tbgpu_commit_many) */
+    uint32_t pass_batches_max;  /* max prepares in one device pass */
+    int32_t device;             /* HIP device ordinal */
+    uint32_t flags;             /* TBGPU_CONFIG_* */
+} tbgpu_config;
+
+typedef struct tbgpu tbgpu_t;
+
+/* StateMachine.init: allocates every HBM table up front (static allocation). */
+int tbgpu_init(const tbgpu_config* config, tbgpu_t** out);
+void tbgpu_deinit(tbgpu_t* engine);
+/* StateMachine.reset: empties every table, commit_timestamp = 0. */
+int tbgpu_reset(tbgpu_t* engine);
+
+/* StateMachine.commit for one prepare.  `input` holds `input_len` bytes (a multiple of 128 for
+ * creates, of 16 for lookups); `output` receives the reply body and `*out_len` its size.
+ * Byte-identical to the reference for every operation. */
+int tbgpu_commit(tbgpu_t* engine, uint8_t operation, uint64_t timestamp, const void* input,
+                 uint32_t input_len, void* output, uint32_t output_cap, uint32_t* out_len);
+
+/* N consecutive prepares of the same create operation in one device pass; identical results to
+ * N sequential tbgpu_commit calls (timestamps strictly increasing). */
+int tbgpu_commit_many(tbgpu_t* engine, uint8_t operation, uint32_t n, const uint64_t* timestamps,
+                      const void* const* inputs, const uint32_t* input_lens, void* const* outputs,
+                      uint32_t* out_lens);
+
+/* Device-resident throughput entry point: `events_dev` holds sum(batch_lens) events back to back
+ * in HBM; batch k's reply is written to results_dev + 8*offset_k (offset_k = sum of earlier
+ * batch lengths) and its byte count to reply_bytes_dev[k].  Enqueued on the engine's stream;
+ * call tbgpu_sync() to wait and collect the status. */
+int tbgpu_commit_device_async(tbgpu_t* engine, uint8_t operation, uint32_t n_batches,
+                              const uint64_t* timestamps, const uint32_t* batch_lens,
+                              const void* events_dev, void* results_dev, uint32_t* reply_bytes_dev);
+int tbgpu_sync(tbgpu_t* engine);
+
+/* StateMachine.commit_timestamp (src/state_machine.zig:251). */
+uint64_t tbgpu_commit_timestamp(tbgpu_t* engine);
+
+/* Test-only: the table harness `setup` action (src/state_machine.zig:1398-1407).
+ * balances = {dp_lo, dp_hi, dpost_lo, dpost_hi, cp_lo, cp_hi, cpost_lo, cpost_hi}. */
+int tbgpu_test_set_balances(tbgpu_t* engine, uint64_t id_lo, uint64_t id_hi,
+                            const uint64_t balances[8]);
+
+/* Parity read-back: every live record, sorted by id ascending; *count = records written. */
+int tbgpu_export_accounts(tbgpu_t* engine, void* out, uint64_t cap, uint64_t* count);
+int tbgpu_export_transfers(tbgpu_t* engine, void* out, uint64_t cap, uint64_t* count);
+/* Posted groove (src/state_machine.zig:185-198): {pending_timestamp, fulfillment} pairs, sorted. */
+int tbgpu_export_posted(tbgpu_t* engine, uint64_t* out_pairs, uint64_t cap, uint64_t* count);
+
+typedef struct tbgpu_stats {
+    uint64_t passes;
+    uint64_t events;
+    uint64_t dependent_events;   /* events replayed by the ordered fallback kernel */
+    uint64_t accounts;           /* live accounts */
+    uint64_t transfers;          /* live transfers */
+    /* With TBGPU_CONFIG_PROFILE: total device ms and launch count per kernel. */
+    double ms_validate;          /* tb_transfers_validate / tb_accounts_validate */
+    double ms_resolve;           /* tb_*_resolve (classify + chains + apply + replies) */
+    double ms_replay;            /* tb_replay (ordered fallback) */
+    double ms_clear;             /* dedup table clears */
+    uint64_t launches_validate, launches_resolve, launches_replay, launches_clear;
+} tbgpu_stats;
+
+int tbgpu_get_stats(tbgpu_t* engine, tbgpu_stats* stats);
+void tbgpu_reset_stats(tbgpu_t* engine);
+
+/* Last error message (thread-local, static storage). */
+const char* tbgpu_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,44 @@
+/*
+ * tbgpu_bench.h — synthetic workload generation for bench.py and the parity tests (same library
+ * as tbgpu.h).  Not part of the StateMachine boundary.
+ */
+#ifndef TBGPU_BENCH_H
+#define TBGPU_BENCH_H
+
+#include <stdint.h>
+
+#include "tbgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tbgpu_workload {
+    uint64_t seed;
+    uint64_t account_count;    /* accounts 0..account_count-1 exist (ids by IdPermutation.inversion) */
+    uint32_t kind;             /* 0: uniform dr != cr, no flags (BASELINE config C2) */
+    uint32_t limit_permille;   /* accounts with debits_must_not_exceed_credits, per mille */
+} tbgpu_workload;
+
+/* Write `count` Account events for account indices [first, first+count) into device memory. */
+int tbgpu_bench_generate_accounts(tbgpu_t* engine, void* out_dev, uint64_t first, uint64_t count,
+                                  const tbgpu_workload* w);
+/* Write `count` Transfer events for transfer indices [first, first+count) into device memory. */
+int tbgpu_bench_generate_transfers(tbgpu_t* engine, void* out_dev, uint64_t first, uint64_t count,
+                                   const tbgpu_workload* w);
+
+/* Device memory helpers for callers without a device allocator (ctypes users). */
+int tbgpu_device_alloc(tbgpu_t* engine, uint64_t bytes, void** out);
+int tbgpu_device_free(tbgpu_t* engine, void* ptr);
+int tbgpu_copy_to_host(tbgpu_t* engine, void* dst, const void* src_dev, uint64_t bytes);
+int tbgpu_copy_to_device(tbgpu_t* engine, void* dst_dev, const void* src, uint64_t bytes);
+
+/* Device-side timing of the last tbgpu_sync'ed work: elapsed ms between two markers recorded on
+ * the engine stream. */
+int tbgpu_marker(tbgpu_t* engine, uint32_t slot);          /* slot < 16 */
+double tbgpu_marker_elapsed_ms(tbgpu_t* engine, uint32_t a, uint32_t b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

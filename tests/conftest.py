@@ -13,3 +13,22 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running parity sweep")
+
+
+@pytest.fixture
+def gpu_engine_factory():
+    """Fresh small engines on cuda:0 (the HIP library must be built; no fallback)."""
+    from tigerbeetle_amd.state_machine import Engine, Options
+
+    made = []
+
+    def make(**kw):
+        opts = dict(accounts_max=4096, transfers_max=1 << 15, pass_events_max=8192 * 4, pass_batches_max=64)
+        opts.update(kw)
+        e = Engine(Options(**opts))
+        made.append(e)
+        return e
+
+    yield make
+    for e in made:
+        e.close()

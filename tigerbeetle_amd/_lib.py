@@ -1,0 +1,121 @@
+"""Loader for the in-tree HIP engine library (libtbgpu.so) and its C ABI (include/tbgpu.h).
+
+The library is built in-tree by `tigerbeetle_amd.build` (hipcc --offload-arch=gfx950).  There is
+no CPU fallback: if the library is missing or no GPU is visible, calls fail loudly.
+"""
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libtbgpu.so")
+
+STATUS_OK, STATUS_INVALID, STATUS_PANIC, STATUS_DEVICE = 0, 1, 2, 3
+
+CONFIG_PROFILE = 1
+
+
+class tbgpu_config(ctypes.Structure):
+    _fields_ = [
+        ("accounts_max", ctypes.c_uint64),
+        ("transfers_max", ctypes.c_uint64),
+        ("pass_events_max", ctypes.c_uint32),
+        ("pass_batches_max", ctypes.c_uint32),
+        ("device", ctypes.c_int32),
+        ("flags", ctypes.c_uint32),
+    ]
+
+
+class tbgpu_stats(ctypes.Structure):
+    _fields_ = [
+        ("passes", ctypes.c_uint64),
+        ("events", ctypes.c_uint64),
+        ("dependent_events", ctypes.c_uint64),
+        ("accounts", ctypes.c_uint64),
+        ("transfers", ctypes.c_uint64),
+        ("ms_validate", ctypes.c_double),
+        ("ms_resolve", ctypes.c_double),
+        ("ms_replay", ctypes.c_double),
+        ("ms_clear", ctypes.c_double),
+        ("launches_validate", ctypes.c_uint64),
+        ("launches_resolve", ctypes.c_uint64),
+        ("launches_replay", ctypes.c_uint64),
+        ("launches_clear", ctypes.c_uint64),
+    ]
+
+
+class tbgpu_workload(ctypes.Structure):
+    _fields_ = [
+        ("seed", ctypes.c_uint64),
+        ("account_count", ctypes.c_uint64),
+        ("kind", ctypes.c_uint32),
+        ("limit_permille", ctypes.c_uint32),
+    ]
+
+
+# Every symbol declared in include/tbgpu.h and include/tbgpu_bench.h: (name, restype, argtypes).
+_P = ctypes.c_void_p
+_U8, _U32, _U64 = ctypes.c_uint8, ctypes.c_uint32, ctypes.c_uint64
+SIGNATURES = [
+    ("tbgpu_init", ctypes.c_int, [ctypes.POINTER(tbgpu_config), ctypes.POINTER(_P)]),
+    ("tbgpu_deinit", None, [_P]),
+    ("tbgpu_reset", ctypes.c_int, [_P]),
+    ("tbgpu_commit", ctypes.c_int, [_P, _U8, _U64, _P, _U32, _P, _U32, ctypes.POINTER(_U32)]),
+    ("tbgpu_commit_many", ctypes.c_int, [_P, _U8, _U32, ctypes.POINTER(_U64), ctypes.POINTER(_P),
+                                         ctypes.POINTER(_U32), ctypes.POINTER(_P), ctypes.POINTER(_U32)]),
+    ("tbgpu_commit_device_async", ctypes.c_int, [_P, _U8, _U32, ctypes.POINTER(_U64), ctypes.POINTER(_U32),
+                                                 _P, _P, _P]),
+    ("tbgpu_sync", ctypes.c_int, [_P]),
+    ("tbgpu_commit_timestamp", _U64, [_P]),
+    ("tbgpu_test_set_balances", ctypes.c_int, [_P, _U64, _U64, ctypes.POINTER(_U64)]),
+    ("tbgpu_export_accounts", ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
+    ("tbgpu_export_transfers", ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
+    ("tbgpu_export_posted", ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
+    ("tbgpu_get_stats", ctypes.c_int, [_P, ctypes.POINTER(tbgpu_stats)]),
+    ("tbgpu_reset_stats", None, [_P]),
+    ("tbgpu_last_error", ctypes.c_char_p, []),
+    ("tbgpu_bench_generate_accounts", ctypes.c_int, [_P, _P, _U64, _U64, ctypes.POINTER(tbgpu_workload)]),
+    ("tbgpu_bench_generate_transfers", ctypes.c_int, [_P, _P, _U64, _U64, ctypes.POINTER(tbgpu_workload)]),
+    ("tbgpu_device_alloc", ctypes.c_int, [_P, _U64, ctypes.POINTER(_P)]),
+    ("tbgpu_device_free", ctypes.c_int, [_P, _P]),
+    ("tbgpu_copy_to_host", ctypes.c_int, [_P, _P, _P, _U64]),
+    ("tbgpu_copy_to_device", ctypes.c_int, [_P, _P, _P, _U64]),
+    ("tbgpu_marker", ctypes.c_int, [_P, _U32]),
+    ("tbgpu_marker_elapsed_ms", ctypes.c_double, [_P, _U32, _U32]),
+]
+
+_lib = None
+
+
+class EngineError(RuntimeError):
+    def __init__(self, status, message):
+        super().__init__("tbgpu status %d: %s" % (status, message))
+        self.status = status
+
+
+class EnginePanic(EngineError):
+    """The reference would have panicked (assert / ReleaseSafe overflow trap)."""
+
+
+def load():
+    """Load libtbgpu.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("tigerbeetle_amd: %s is missing — run `python -c 'import __graft_entry__ as g; "
+                              "g.build()'` (hipcc --offload-arch=gfx950)" % LIB_PATH)
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(status):
+    if status == STATUS_OK:
+        return
+    msg = load().tbgpu_last_error().decode(errors="replace")
+    if status == STATUS_PANIC:
+        raise EnginePanic(status, msg)
+    raise EngineError(status, msg)

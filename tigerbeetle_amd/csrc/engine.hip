@@ -1,0 +1,773 @@
+// engine.hip — host side of the MI355X commit engine: the C ABI of include/tbgpu.h.
+//
+// One engine = one HIP device + one stream + HBM tables allocated at init (static allocation, as
+// the reference's grooves: src/lsm/groove.zig:486-555).  A commit call is split into device passes
+// of up to pass_events_max events / pass_batches_max prepares; each pass is three kernels
+// (validate, resolve, replay — see pass.h) enqueued without host synchronisation.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/tbgpu.h"
+#include "../../include/tbgpu_bench.h"
+#include "k_aux.h"
+#include "k_replay.h"
+#include "k_workload.h"
+
+static thread_local std::string g_err;
+
+static int fail(int status, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+static int fail(int status, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return status;
+}
+
+#define HIPCK(x)                                                                                   \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "%s: %s (%s:%d)", #x,               \
+                                          hipGetErrorString(e_), __FILE__, __LINE__);              \
+    } while (0)
+
+static u64 pow2_at_least(u64 v) {
+    u64 c = 1;
+    while (c < v) c <<= 1;
+    return c;
+}
+
+enum { K_VALIDATE = 0, K_RESOLVE = 1, K_REPLAY = 2, K_CLEAR = 3, K_COUNT = 4 };
+
+struct ProfilePair {
+    int kind;
+    hipEvent_t a, b;
+};
+
+struct tbgpu {
+    tbgpu_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+
+    Tables T{};
+    Globals* g = nullptr;
+    u64 account_cap = 0, transfer_cap = 0;
+
+    // Pass scratch.
+    u32 pe_max = 0, pb_max = 0;
+    u32 *info = nullptr, *dr = nullptr, *cr = nullptr, *ps = nullptr;
+    u32 *dep_list = nullptr, *dep_count = nullptr;
+    u64 *amt = nullptr, *kid = nullptr, *kpid = nullptr;
+    u64* dedup = nullptr;
+    u64 dedup_cap = 0;
+    u64* sum_shards = nullptr;
+    UndoEntry* undo = nullptr;
+    u32 undo_cap = 0;
+
+    // Host-path staging.
+    u8* staging = nullptr;
+    u32* results = nullptr;
+    u32* reply_bytes = nullptr;
+    u64* meta = nullptr;   // device: [meta_cap + 1] offsets then [meta_cap] timestamps
+    u64 meta_cap = 0;
+    u64* h_meta = nullptr; // pinned mirror
+    u64* lookup_ids = nullptr;
+    u8* lookup_out = nullptr;
+    u8* lookup_found = nullptr;
+    u32 lookup_cap = 0;
+    u32* d_status = nullptr;
+
+    u32 epoch = 0;
+    u64 commit_ts = 0;       // exact after every synchronous call
+    u64 last_batch_ts = 0;   // upper bound for async calls
+    bool pending = false;    // an async call was enqueued and not yet synced
+
+    bool profile = false;
+    std::vector<hipEvent_t> event_pool;
+    size_t event_next = 0;
+    std::vector<ProfilePair> prof;
+    double prof_ms[K_COUNT] = {};
+    u64 prof_n[K_COUNT] = {};
+    u64 passes = 0, events = 0;
+
+    hipEvent_t markers[16] = {};
+};
+
+static int ev_get(tbgpu* E, hipEvent_t* out) {
+    if (E->event_next == E->event_pool.size()) {
+        hipEvent_t e;
+        HIPCK(hipEventCreate(&e));
+        E->event_pool.push_back(e);
+    }
+    *out = E->event_pool[E->event_next++];
+    return 0;
+}
+
+static int prof_begin(tbgpu* E, ProfilePair* p, int kind) {
+    if (!E->profile) return 0;
+    p->kind = kind;
+    int st = ev_get(E, &p->a);
+    if (st) return st;
+    st = ev_get(E, &p->b);
+    if (st) return st;
+    HIPCK(hipEventRecord(p->a, E->stream));
+    return 0;
+}
+
+static int prof_end(tbgpu* E, ProfilePair* p) {
+    if (!E->profile) return 0;
+    HIPCK(hipEventRecord(p->b, E->stream));
+    E->prof.push_back(*p);
+    return 0;
+}
+
+static int prof_collect(tbgpu* E) {
+    for (const ProfilePair& p : E->prof) {
+        float ms = 0;
+        HIPCK(hipEventElapsedTime(&ms, p.a, p.b));
+        E->prof_ms[p.kind] += ms;
+        E->prof_n[p.kind] += 1;
+    }
+    E->prof.clear();
+    E->event_next = 0;
+    return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+
+static int engine_clear(tbgpu* E) {
+    HIPCK(hipMemsetAsync(E->T.accounts, 0, E->account_cap * sizeof(Account), E->stream));
+    HIPCK(hipMemsetAsync(E->T.account_mark, 0, E->account_cap * sizeof(u32), E->stream));
+    HIPCK(hipMemsetAsync(E->T.transfers, 0, E->transfer_cap * sizeof(Transfer), E->stream));
+    HIPCK(hipMemsetAsync(E->T.posted, 0, E->transfer_cap, E->stream));
+    HIPCK(hipMemsetAsync(E->g, 0, sizeof(Globals), E->stream));
+    HIPCK(hipStreamSynchronize(E->stream));
+    E->epoch = 0;
+    E->commit_ts = 0;
+    E->last_batch_ts = 0;
+    E->pending = false;
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
+    *out = nullptr;
+    if (!config || config->accounts_max == 0 || config->transfers_max == 0 || config->pass_events_max == 0 ||
+        config->pass_batches_max == 0) {
+        return fail(TBGPU_STATUS_INVALID, "tbgpu_init: invalid config");
+    }
+    if (config->accounts_max > (1ULL << 31) || config->transfers_max > (1ULL << 31)) {
+        return fail(TBGPU_STATUS_INVALID, "tbgpu_init: table capacity above 2^31 objects per device");
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        return fail(TBGPU_STATUS_DEVICE, "tbgpu_init: no HIP device visible");
+    }
+    if (config->device < 0 || config->device >= ndev) {
+        return fail(TBGPU_STATUS_INVALID, "tbgpu_init: device %d out of range (%d devices)", config->device, ndev);
+    }
+    tbgpu* E = new tbgpu();
+    E->cfg = *config;
+    E->device = config->device;
+    E->profile = (config->flags & TBGPU_CONFIG_PROFILE) != 0;
+    int st = TBGPU_STATUS_OK;
+#define INIT_CK(x)                                                                                 \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) {                                                                    \
+            st = fail(TBGPU_STATUS_DEVICE, "%s: %s", #x, hipGetErrorString(e_));                   \
+            tbgpu_deinit(E);                                                                       \
+            return st;                                                                             \
+        }                                                                                          \
+    } while (0)
+    INIT_CK(hipSetDevice(E->device));
+    INIT_CK(hipStreamCreateWithFlags(&E->stream, hipStreamNonBlocking));
+
+    E->account_cap = pow2_at_least(std::max<u64>(2 * config->accounts_max, 1024));
+    E->transfer_cap = pow2_at_least(std::max<u64>(2 * config->transfers_max, 1024));
+    E->pe_max = config->pass_events_max;
+    E->pb_max = config->pass_batches_max;
+    E->dedup_cap = pow2_at_least(std::max<u64>(4ULL * E->pe_max, 64));
+    E->undo_cap = 4 * (BATCH_EVENTS_MAX + 1);
+    E->meta_cap = std::max<u64>(E->pb_max, 1 << 16);
+    E->lookup_cap = 1 << 16;
+
+    size_t free_b = 0, total_b = 0;
+    INIT_CK(hipMemGetInfo(&free_b, &total_b));
+    const u64 need = E->account_cap * (sizeof(Account) + 4) + E->transfer_cap * (sizeof(Transfer) + 1) +
+                     (u64)E->pe_max * (4 * 4 + 8 * 4 + 128 + 8 + 4) + E->dedup_cap * 8;
+    if (need > free_b) {
+        st = fail(TBGPU_STATUS_INVALID, "tbgpu_init: needs %llu bytes of HBM, %llu free",
+                  (unsigned long long)need, (unsigned long long)free_b);
+        tbgpu_deinit(E);
+        return st;
+    }
+
+    INIT_CK(hipMalloc(&E->T.accounts, E->account_cap * sizeof(Account)));
+    INIT_CK(hipMalloc(&E->T.account_mark, E->account_cap * sizeof(u32)));
+    INIT_CK(hipMalloc(&E->T.transfers, E->transfer_cap * sizeof(Transfer)));
+    INIT_CK(hipMalloc(&E->T.posted, E->transfer_cap));
+    INIT_CK(hipMalloc(&E->g, sizeof(Globals)));
+    E->T.account_mask = E->account_cap - 1;
+    E->T.transfer_mask = E->transfer_cap - 1;
+    E->T.g = E->g;
+
+    const u64 pe = E->pe_max;
+    INIT_CK(hipMalloc(&E->info, pe * 4));
+    INIT_CK(hipMalloc(&E->dr, pe * 4));
+    INIT_CK(hipMalloc(&E->cr, pe * 4));
+    INIT_CK(hipMalloc(&E->ps, pe * 4));
+    INIT_CK(hipMalloc(&E->dep_list, pe * 4));
+    INIT_CK(hipMalloc(&E->dep_count, (u64)E->pb_max * 4));
+    INIT_CK(hipMalloc(&E->amt, pe * 16));
+    INIT_CK(hipMalloc(&E->kid, pe * 8));
+    INIT_CK(hipMalloc(&E->kpid, pe * 8));
+    INIT_CK(hipMalloc(&E->dedup, E->dedup_cap * 8));
+    INIT_CK(hipMalloc(&E->sum_shards, SUM_WORDS * 8));
+    INIT_CK(hipMalloc(&E->undo, (u64)E->undo_cap * sizeof(UndoEntry)));
+    INIT_CK(hipMalloc(&E->staging, pe * 128));
+    INIT_CK(hipMalloc(&E->results, pe * 8));
+    INIT_CK(hipMalloc(&E->reply_bytes, E->meta_cap * 4));
+    INIT_CK(hipMalloc(&E->meta, (2 * E->meta_cap + 1) * 8));
+    INIT_CK(hipHostMalloc(&E->h_meta, (2 * E->meta_cap + 1) * 8, hipHostMallocDefault));
+    INIT_CK(hipMalloc(&E->lookup_ids, (u64)E->lookup_cap * 16));
+    INIT_CK(hipMalloc(&E->lookup_out, (u64)E->lookup_cap * 128));
+    INIT_CK(hipMalloc(&E->lookup_found, E->lookup_cap));
+    INIT_CK(hipMalloc(&E->d_status, 16));
+    for (int i = 0; i < 16; i++) INIT_CK(hipEventCreate(&E->markers[i]));
+#undef INIT_CK
+    st = engine_clear(E);
+    if (st) {
+        tbgpu_deinit(E);
+        return st;
+    }
+    *out = E;
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" void tbgpu_deinit(tbgpu_t* E) {
+    if (!E) return;
+    (void)hipSetDevice(E->device);
+    if (E->stream) (void)hipStreamSynchronize(E->stream);
+    void* bufs[] = {E->T.accounts, E->T.account_mark, E->T.transfers, E->T.posted, E->g, E->info, E->dr,
+                    E->cr, E->ps, E->dep_list, E->dep_count, E->amt, E->kid, E->kpid, E->dedup,
+                    E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
+                    E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status};
+    for (void* p : bufs) if (p) (void)hipFree(p);
+    if (E->h_meta) (void)hipHostFree(E->h_meta);
+    for (hipEvent_t e : E->event_pool) (void)hipEventDestroy(e);
+    for (int i = 0; i < 16; i++) if (E->markers[i]) (void)hipEventDestroy(E->markers[i]);
+    if (E->stream) (void)hipStreamDestroy(E->stream);
+    delete E;
+}
+
+extern "C" int tbgpu_reset(tbgpu_t* E) {
+    HIPCK(hipSetDevice(E->device));
+    return engine_clear(E);
+}
+
+// Read back commit_timestamp and the panic word after the stream drained.
+static int engine_sync(tbgpu* E) {
+    HIPCK(hipStreamSynchronize(E->stream));
+    Globals g;
+    HIPCK(hipMemcpy(&g, E->g, sizeof(Globals), hipMemcpyDeviceToHost));
+    E->commit_ts = g.commit_timestamp;
+    E->pending = false;
+    int st = prof_collect(E);
+    if (st) return st;
+    if (g.panic) return fail(TBGPU_STATUS_PANIC, "device panic 0x%llx (the reference would have trapped)",
+                             (unsigned long long)g.panic);
+    return TBGPU_STATUS_OK;
+}
+
+// Enqueue every pass of one call.  meta (device) already holds the call's offsets/timestamps.
+static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* events_dev, u32* results_dev,
+                        u32* reply_bytes_dev) {
+    const u64* d_off = E->meta;
+    const u64* d_ts = E->meta + (nb + 1);
+    u32 b0 = 0;
+    while (b0 < nb) {
+        u32 b1 = b0;
+        while (b1 < nb && b1 - b0 < E->pb_max && h_off[b1 + 1] - h_off[b0] <= E->pe_max) b1++;
+        if (b1 == b0) return fail(TBGPU_STATUS_INVALID, "batch larger than pass_events_max");
+        const u64 n = h_off[b1] - h_off[b0];
+        E->epoch++;
+        if (E->epoch == 0) {  // wrapped: clear stale balancing marks
+            HIPCK(hipMemsetAsync(E->T.account_mark, 0, E->account_cap * sizeof(u32), E->stream));
+            E->epoch = 1;
+        }
+        PassArgs P{};
+        P.op = op;
+        P.epoch = E->epoch;
+        P.b0 = b0;
+        P.b1 = b1;
+        P.e0 = h_off[b0];
+        P.n = (u32)n;
+        P.batch_off = d_off;
+        P.batch_ts = d_ts;
+        P.events = events_dev;
+        P.results = results_dev;
+        P.reply_bytes = reply_bytes_dev;
+        P.info = E->info;
+        P.dr = E->dr;
+        P.cr = E->cr;
+        P.ps = E->ps;
+        P.amt = E->amt;
+        P.kid = E->kid;
+        P.kpid = E->kpid;
+        P.dep_list = E->dep_list;
+        P.dep_count = E->dep_count;
+        P.dedup = E->dedup;
+        P.dedup_mask = std::min<u64>(pow2_at_least(std::max<u64>(4 * n, 64)), E->dedup_cap) - 1;
+        P.sum_shards = E->sum_shards;
+        P.T = E->T;
+
+        ProfilePair pp;
+        int st = prof_begin(E, &pp, K_CLEAR);
+        if (st) return st;
+        HIPCK(hipMemsetAsync(E->dedup, 0, (P.dedup_mask + 1) * 8, E->stream));
+        HIPCK(hipMemsetAsync(E->sum_shards, 0, SUM_WORDS * 8, E->stream));
+        if ((st = prof_end(E, &pp))) return st;
+
+        if (n > 0) {
+            if ((st = prof_begin(E, &pp, K_VALIDATE))) return st;
+            const u32 grid = (u32)((n + VALIDATE_THREADS - 1) / VALIDATE_THREADS);
+            if (op == OP_CREATE_TRANSFERS) {
+                hipLaunchKernelGGL(tb_transfers_validate, dim3(grid), dim3(VALIDATE_THREADS), 0, E->stream, P);
+            } else {
+                hipLaunchKernelGGL(tb_accounts_validate, dim3(grid), dim3(VALIDATE_THREADS), 0, E->stream, P);
+            }
+            HIPCK(hipGetLastError());
+            if ((st = prof_end(E, &pp))) return st;
+        }
+        if ((st = prof_begin(E, &pp, K_RESOLVE))) return st;
+        if (op == OP_CREATE_TRANSFERS) {
+            hipLaunchKernelGGL(tb_resolve<OP_CREATE_TRANSFERS>, dim3(b1 - b0), dim3(RESOLVE_THREADS), 0, E->stream, P);
+        } else {
+            hipLaunchKernelGGL(tb_resolve<OP_CREATE_ACCOUNTS>, dim3(b1 - b0), dim3(RESOLVE_THREADS), 0, E->stream, P);
+        }
+        HIPCK(hipGetLastError());
+        if ((st = prof_end(E, &pp))) return st;
+        if ((st = prof_begin(E, &pp, K_REPLAY))) return st;
+        if (op == OP_CREATE_TRANSFERS) {
+            hipLaunchKernelGGL(tb_replay<OP_CREATE_TRANSFERS>, dim3(1), dim3(REPLAY_THREADS), 0, E->stream, P,
+                               E->undo, E->undo_cap);
+        } else {
+            hipLaunchKernelGGL(tb_replay<OP_CREATE_ACCOUNTS>, dim3(1), dim3(REPLAY_THREADS), 0, E->stream, P,
+                               E->undo, E->undo_cap);
+        }
+        HIPCK(hipGetLastError());
+        if ((st = prof_end(E, &pp))) return st;
+        E->passes++;
+        E->events += n;
+        b0 = b1;
+    }
+    return TBGPU_STATUS_OK;
+}
+
+// Host-side checks of the commit asserts (state_machine.zig:518-519, :645, :739, :780) and
+// upload of the call metadata.
+static int prepare_call(tbgpu* E, u8 op, u32 nb, const u64* timestamps, const u32* lens, u64 floor_ts,
+                        u64* total_events) {
+    if (op != OP_CREATE_ACCOUNTS && op != OP_CREATE_TRANSFERS) {
+        return fail(TBGPU_STATUS_INVALID, "operation %u is not a create operation", op);
+    }
+    if (nb == 0) return fail(TBGPU_STATUS_INVALID, "no batches");
+    if (nb > E->meta_cap) return fail(TBGPU_STATUS_INVALID, "too many batches in one call (%u > %llu)", nb,
+                                      (unsigned long long)E->meta_cap);
+    if (E->pending) {  // the pinned metadata mirror may still be in flight
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    u64* h_off = E->h_meta;
+    u64* h_ts = E->h_meta + (nb + 1);
+    u64 prev = floor_ts;
+    h_off[0] = 0;
+    for (u32 k = 0; k < nb; k++) {
+        const u64 ts = timestamps[k];
+        const u32 L = lens[k];
+        if (L > BATCH_EVENTS_MAX) return fail(TBGPU_STATUS_INVALID, "batch %u has %u events (max %u)", k, L, BATCH_EVENTS_MAX);
+        if (!(ts > prev)) return fail(TBGPU_STATUS_PANIC, "timestamp %llu <= commit timestamp %llu",
+                                      (unsigned long long)ts, (unsigned long long)prev);
+        if (L > 0) {
+            if (ts < L) return fail(TBGPU_STATUS_PANIC, "timestamp %llu < batch length %u", (unsigned long long)ts, L);
+            if (!(ts - L + 1 > prev)) return fail(TBGPU_STATUS_PANIC, "first event timestamp <= commit timestamp");
+        }
+        prev = ts;
+        h_off[k + 1] = h_off[k] + L;
+        h_ts[k] = ts;
+    }
+    HIPCK(hipMemcpyAsync(E->meta, E->h_meta, (2 * (u64)nb + 1) * 8, hipMemcpyHostToDevice, E->stream));
+    E->last_batch_ts = prev;
+    *total_events = h_off[nb];
+    return TBGPU_STATUS_OK;
+}
+
+static int commit_lookup(tbgpu* E, bool accounts, const void* input, uint32_t input_len, void* output,
+                         uint32_t output_cap, uint32_t* out_len) {
+    if (input_len % 16 != 0) return fail(TBGPU_STATUS_INVALID, "lookup body not a multiple of 16");
+    const u32 n = input_len / 16;
+    if (n > E->lookup_cap) return fail(TBGPU_STATUS_INVALID, "too many ids");
+    if (n == 0) return TBGPU_STATUS_OK;
+    HIPCK(hipMemcpyAsync(E->lookup_ids, input, input_len, hipMemcpyHostToDevice, E->stream));
+    if (accounts) {
+        hipLaunchKernelGGL(tb_lookup<true>, dim3((n + 255) / 256), dim3(256), 0, E->stream, E->T, E->lookup_ids, n,
+                           E->lookup_out, E->lookup_found);
+    } else {
+        hipLaunchKernelGGL(tb_lookup<false>, dim3((n + 255) / 256), dim3(256), 0, E->stream, E->T, E->lookup_ids, n,
+                           E->lookup_out, E->lookup_found);
+    }
+    HIPCK(hipGetLastError());
+    std::vector<u8> found(n);
+    std::vector<u8> recs((u64)n * 128);
+    HIPCK(hipMemcpyAsync(found.data(), E->lookup_found, n, hipMemcpyDeviceToHost, E->stream));
+    HIPCK(hipMemcpyAsync(recs.data(), E->lookup_out, (u64)n * 128, hipMemcpyDeviceToHost, E->stream));
+    HIPCK(hipStreamSynchronize(E->stream));
+    const u32 slots = output_cap / 128;
+    u32 m = 0;
+    for (u32 i = 0; i < n; i++) {
+        if (found[i] && m < slots) {
+            memcpy((u8*)output + (u64)m * 128, recs.data() + (u64)i * 128, 128);
+            m++;
+        }
+    }
+    *out_len = m * 128;
+    return TBGPU_STATUS_OK;
+}
+
+static int commit_host(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const void* const* inputs,
+                       const uint32_t* input_lens, void* const* outputs, uint32_t* out_lens, const uint32_t* out_caps) {
+    std::vector<u32> lens(n);
+    for (u32 k = 0; k < n; k++) {
+        if (input_lens[k] % 128 != 0) return fail(TBGPU_STATUS_INVALID, "create body not a multiple of 128");
+        lens[k] = input_lens[k] / 128;
+        if (out_caps && (u64)out_caps[k] < (u64)lens[k] * 8) return fail(TBGPU_STATUS_INVALID, "output too small");
+    }
+    // Split into calls whose events fit the staging buffer.
+    u32 k0 = 0;
+    while (k0 < n) {
+        u32 k1 = k0;
+        u64 ev = 0;
+        while (k1 < n && k1 - k0 < E->meta_cap && ev + lens[k1] <= E->pe_max) ev += lens[k1++];
+        if (k1 == k0) return fail(TBGPU_STATUS_INVALID, "batch larger than pass_events_max");
+        u64 total = 0;
+        int st = prepare_call(E, op, k1 - k0, timestamps + k0, lens.data() + k0, E->commit_ts, &total);
+        if (st) return st;
+        u64 off = 0;
+        for (u32 k = k0; k < k1; k++) {
+            if (lens[k]) HIPCK(hipMemcpyAsync(E->staging + off * 128, inputs[k], (u64)lens[k] * 128,
+                                              hipMemcpyHostToDevice, E->stream));
+            off += lens[k];
+        }
+        std::vector<u64> h_off(E->h_meta, E->h_meta + (k1 - k0) + 1);
+        if ((st = enqueue_call(E, op, k1 - k0, h_off.data(), E->staging, E->results, E->reply_bytes))) return st;
+        std::vector<u32> rb(k1 - k0);
+        HIPCK(hipMemcpyAsync(rb.data(), E->reply_bytes, (u64)(k1 - k0) * 4, hipMemcpyDeviceToHost, E->stream));
+        if ((st = engine_sync(E))) return st;
+        for (u32 k = k0; k < k1; k++) {
+            const u32 bytes = rb[k - k0];
+            if (bytes) HIPCK(hipMemcpy(outputs[k], E->results + 2 * h_off[k - k0], bytes, hipMemcpyDeviceToHost));
+            out_lens[k] = bytes;
+        }
+        k0 = k1;
+    }
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_commit(tbgpu_t* E, uint8_t operation, uint64_t timestamp, const void* input,
+                            uint32_t input_len, void* output, uint32_t output_cap, uint32_t* out_len) {
+    *out_len = 0;
+    HIPCK(hipSetDevice(E->device));
+    if (operation < OP_CREATE_ACCOUNTS || operation > OP_LOOKUP_TRANSFERS) {
+        return fail(TBGPU_STATUS_INVALID, "unknown operation %u", operation);
+    }
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    if (!(timestamp > E->commit_ts)) {  // state_machine.zig:519
+        return fail(TBGPU_STATUS_PANIC, "timestamp %llu <= commit timestamp %llu", (unsigned long long)timestamp,
+                    (unsigned long long)E->commit_ts);
+    }
+    if (operation == OP_LOOKUP_ACCOUNTS || operation == OP_LOOKUP_TRANSFERS) {
+        return commit_lookup(E, operation == OP_LOOKUP_ACCOUNTS, input, input_len, output, output_cap, out_len);
+    }
+    if (input_len == 0) {  // empty batch: nothing to execute (execute loops zero times)
+        return TBGPU_STATUS_OK;
+    }
+    const void* ins[1] = {input};
+    void* outs[1] = {output};
+    return commit_host(E, operation, 1, &timestamp, ins, &input_len, outs, out_len, &output_cap);
+}
+
+extern "C" int tbgpu_commit_many(tbgpu_t* E, uint8_t operation, uint32_t n, const uint64_t* timestamps,
+                                 const void* const* inputs, const uint32_t* input_lens, void* const* outputs,
+                                 uint32_t* out_lens) {
+    HIPCK(hipSetDevice(E->device));
+    for (u32 k = 0; k < n; k++) out_lens[k] = 0;
+    if (n == 0) return TBGPU_STATUS_OK;
+    return commit_host(E, operation, n, timestamps, inputs, input_lens, outputs, out_lens, nullptr);
+}
+
+extern "C" int tbgpu_commit_device_async(tbgpu_t* E, uint8_t operation, uint32_t n_batches,
+                                         const uint64_t* timestamps, const uint32_t* batch_lens,
+                                         const void* events_dev, void* results_dev, uint32_t* reply_bytes_dev) {
+    HIPCK(hipSetDevice(E->device));
+    const u64 floor_ts = std::max(E->commit_ts, E->pending ? E->last_batch_ts : 0);
+    u64 total = 0;
+    int st = prepare_call(E, operation, n_batches, timestamps, batch_lens, floor_ts, &total);
+    if (st) return st;
+    std::vector<u64> h_off(E->h_meta, E->h_meta + n_batches + 1);
+    st = enqueue_call(E, operation, n_batches, h_off.data(), (const u8*)events_dev, (u32*)results_dev, reply_bytes_dev);
+    if (st) return st;
+    E->pending = true;
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_sync(tbgpu_t* E) {
+    HIPCK(hipSetDevice(E->device));
+    return engine_sync(E);
+}
+
+extern "C" uint64_t tbgpu_commit_timestamp(tbgpu_t* E) {
+    if (E->pending) engine_sync(E);
+    return E->commit_ts;
+}
+
+extern "C" int tbgpu_test_set_balances(tbgpu_t* E, uint64_t id_lo, uint64_t id_hi, const uint64_t b[8]) {
+    HIPCK(hipSetDevice(E->device));
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    hipLaunchKernelGGL(tb_set_balances, dim3(1), dim3(1), 0, E->stream, E->T, id_lo, id_hi, b[0], b[1], b[2], b[3],
+                       b[4], b[5], b[6], b[7], E->d_status);
+    HIPCK(hipGetLastError());
+    u32 status = 0;
+    HIPCK(hipMemcpyAsync(&status, E->d_status, 4, hipMemcpyDeviceToHost, E->stream));
+    HIPCK(hipStreamSynchronize(E->stream));
+    if (status) return fail(TBGPU_STATUS_PANIC, "setup of a missing account");
+    return TBGPU_STATUS_OK;
+}
+
+static bool id_less(const u8* a, const u8* b) {
+    const u64* x = (const u64*)a;
+    const u64* y = (const u64*)b;
+    return x[1] != y[1] ? x[1] < y[1] : x[0] < y[0];
+}
+
+// Export live records in chunks of slots (no large temporary), then sort by id.
+template <bool ACCOUNTS>
+static int export_records(tbgpu* E, std::vector<u8>& recs, std::vector<u64>* posted) {
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    const u64 cap = ACCOUNTS ? E->account_cap : E->transfer_cap;
+    const u64 chunk = std::min<u64>(cap, 1ULL << 20);
+    u8* d_out = nullptr;
+    u64* d_cnt = nullptr;
+    u64* d_posted = nullptr;
+    HIPCK(hipMalloc(&d_out, chunk * 128));
+    HIPCK(hipMalloc(&d_cnt, 16));
+    HIPCK(hipMalloc(&d_posted, chunk * 16));
+    int st = TBGPU_STATUS_OK;
+    for (u64 s = 0; s < cap && st == TBGPU_STATUS_OK; s += chunk) {
+        Tables T = E->T;
+        if (ACCOUNTS) T.accounts += s;
+        else {
+            T.transfers += s;
+            T.posted += s;
+        }
+        hipError_t e = hipMemsetAsync(d_cnt, 0, 16, E->stream);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(tb_export<ACCOUNTS>, dim3((unsigned)((chunk + 255) / 256)), dim3(256), 0, E->stream, T,
+                               chunk, d_out, d_cnt, d_posted, d_cnt + 1);
+            e = hipGetLastError();
+        }
+        u64 cnt[2] = {0, 0};
+        if (e == hipSuccess) e = hipMemcpyAsync(cnt, d_cnt, 16, hipMemcpyDeviceToHost, E->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(E->stream);
+        if (e == hipSuccess && cnt[0]) {
+            const size_t at = recs.size();
+            recs.resize(at + cnt[0] * 128);
+            e = hipMemcpy(recs.data() + at, d_out, cnt[0] * 128, hipMemcpyDeviceToHost);
+        }
+        if (e == hipSuccess && posted && cnt[1]) {
+            const size_t at = posted->size();
+            posted->resize(at + cnt[1] * 2);
+            e = hipMemcpy(posted->data() + at, d_posted, cnt[1] * 16, hipMemcpyDeviceToHost);
+        }
+        if (e != hipSuccess) st = fail(TBGPU_STATUS_DEVICE, "export: %s", hipGetErrorString(e));
+    }
+    (void)hipFree(d_out);
+    (void)hipFree(d_cnt);
+    (void)hipFree(d_posted);
+    if (st) return st;
+    const u64 n = recs.size() / 128;
+    std::vector<u64> idx(n);
+    for (u64 i = 0; i < n; i++) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](u64 a, u64 b) { return id_less(&recs[a * 128], &recs[b * 128]); });
+    std::vector<u8> sorted(recs.size());
+    for (u64 i = 0; i < n; i++) memcpy(&sorted[i * 128], &recs[idx[i] * 128], 128);
+    recs.swap(sorted);
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_export_accounts(tbgpu_t* E, void* out, uint64_t cap, uint64_t* count) {
+    HIPCK(hipSetDevice(E->device));
+    std::vector<u8> recs;
+    int st = export_records<true>(E, recs, nullptr);
+    if (st) return st;
+    const u64 n = std::min<u64>(recs.size() / 128, cap);
+    memcpy(out, recs.data(), n * 128);
+    *count = n;
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_export_transfers(tbgpu_t* E, void* out, uint64_t cap, uint64_t* count) {
+    HIPCK(hipSetDevice(E->device));
+    std::vector<u8> recs;
+    int st = export_records<false>(E, recs, nullptr);
+    if (st) return st;
+    const u64 n = std::min<u64>(recs.size() / 128, cap);
+    memcpy(out, recs.data(), n * 128);
+    *count = n;
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_export_posted(tbgpu_t* E, uint64_t* out_pairs, uint64_t cap, uint64_t* count) {
+    HIPCK(hipSetDevice(E->device));
+    std::vector<u8> recs;
+    std::vector<u64> posted;
+    int st = export_records<false>(E, recs, &posted);
+    if (st) return st;
+    const u64 n = posted.size() / 2;
+    std::vector<std::pair<u64, u64>> pairs(n);
+    for (u64 i = 0; i < n; i++) pairs[i] = {posted[2 * i], posted[2 * i + 1]};
+    std::sort(pairs.begin(), pairs.end());
+    const u64 m = std::min<u64>(n, cap);
+    for (u64 i = 0; i < m; i++) {
+        out_pairs[2 * i] = pairs[i].first;
+        out_pairs[2 * i + 1] = pairs[i].second;
+    }
+    *count = m;
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
+    HIPCK(hipSetDevice(E->device));
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    Globals g;
+    HIPCK(hipMemcpy(&g, E->g, sizeof(Globals), hipMemcpyDeviceToHost));
+    memset(s, 0, sizeof(*s));
+    s->passes = E->passes;
+    s->events = E->events;
+    s->dependent_events = g.dependent_all;
+    s->ms_validate = E->prof_ms[K_VALIDATE];
+    s->ms_resolve = E->prof_ms[K_RESOLVE];
+    s->ms_replay = E->prof_ms[K_REPLAY];
+    s->ms_clear = E->prof_ms[K_CLEAR];
+    s->launches_validate = E->prof_n[K_VALIDATE];
+    s->launches_resolve = E->prof_n[K_RESOLVE];
+    s->launches_replay = E->prof_n[K_REPLAY];
+    s->launches_clear = E->prof_n[K_CLEAR];
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" void tbgpu_reset_stats(tbgpu_t* E) {
+    for (int k = 0; k < K_COUNT; k++) {
+        E->prof_ms[k] = 0;
+        E->prof_n[k] = 0;
+    }
+    E->passes = 0;
+    E->events = 0;
+}
+
+extern "C" const char* tbgpu_last_error(void) { return g_err.c_str(); }
+
+// ------------------------------------------------------------------------------------------------
+// tbgpu_bench.h
+// ------------------------------------------------------------------------------------------------
+
+static WorkloadParams workload_params(const tbgpu_workload* w, u64 first) {
+    WorkloadParams W{};
+    W.seed = w->seed;
+    W.account_count = w->account_count;
+    W.first_index = first;
+    W.kind = w->kind;
+    W.limit_permille = w->limit_permille;
+    W.zipf_s = 1.2;
+    return W;
+}
+
+extern "C" int tbgpu_bench_generate_accounts(tbgpu_t* E, void* out_dev, uint64_t first, uint64_t count,
+                                             const tbgpu_workload* w) {
+    HIPCK(hipSetDevice(E->device));
+    if (count == 0) return TBGPU_STATUS_OK;
+    hipLaunchKernelGGL(tb_gen_accounts, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, E->stream,
+                       (u8*)out_dev, first, count, workload_params(w, first));
+    HIPCK(hipGetLastError());
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_bench_generate_transfers(tbgpu_t* E, void* out_dev, uint64_t first, uint64_t count,
+                                              const tbgpu_workload* w) {
+    HIPCK(hipSetDevice(E->device));
+    if (count == 0) return TBGPU_STATUS_OK;
+    if (w->account_count < 2) return fail(TBGPU_STATUS_INVALID, "need at least two accounts");
+    hipLaunchKernelGGL(tb_gen_transfers, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, E->stream,
+                       (u8*)out_dev, count, workload_params(w, first));
+    HIPCK(hipGetLastError());
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_device_alloc(tbgpu_t* E, uint64_t bytes, void** out) {
+    HIPCK(hipSetDevice(E->device));
+    HIPCK(hipMalloc(out, bytes));
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_device_free(tbgpu_t* E, void* ptr) {
+    HIPCK(hipSetDevice(E->device));
+    HIPCK(hipFree(ptr));
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_copy_to_host(tbgpu_t* E, void* dst, const void* src_dev, uint64_t bytes) {
+    HIPCK(hipSetDevice(E->device));
+    HIPCK(hipStreamSynchronize(E->stream));
+    HIPCK(hipMemcpy(dst, src_dev, bytes, hipMemcpyDeviceToHost));
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_copy_to_device(tbgpu_t* E, void* dst_dev, const void* src, uint64_t bytes) {
+    HIPCK(hipSetDevice(E->device));
+    HIPCK(hipStreamSynchronize(E->stream));
+    HIPCK(hipMemcpy(dst_dev, src, bytes, hipMemcpyHostToDevice));
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_marker(tbgpu_t* E, uint32_t slot) {
+    if (slot >= 16) return fail(TBGPU_STATUS_INVALID, "marker slot");
+    HIPCK(hipEventRecord(E->markers[slot], E->stream));
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" double tbgpu_marker_elapsed_ms(tbgpu_t* E, uint32_t a, uint32_t b) {
+    float ms = -1;
+    if (a >= 16 || b >= 16) return -1;
+    if (hipEventSynchronize(E->markers[b]) != hipSuccess) return -1;
+    if (hipEventElapsedTime(&ms, E->markers[a], E->markers[b]) != hipSuccess) return -1;
+    return ms;
+}

@@ -1,0 +1,427 @@
+// k_replay.h — kernel 3 of a pass: the ordered fallback.
+//
+// One workgroup.  Lane 0 replays the dependent events of the pass in batch order with the
+// reference's sequential logic (execute state_machine.zig:612-698, create_transfer :779-884,
+// post_or_void_pending_transfer :907-1014, create_account :738-765) directly on the HBM tables.
+// Linked-chain scopes keep an undo log and roll back LIFO on discard (cache_map.zig:266-309).
+// Every event that can observe a dependent event's effect is itself dependent (see k_resolve.h),
+// so replaying only this subsequence reproduces the sequential results exactly.  Afterwards the
+// workgroup writes the replies of the batches that had dependent events.
+#pragma once
+
+#include "k_resolve.h"
+
+enum : u32 { UNDO_ACCOUNT_INSERT = 1, UNDO_ACCOUNT_UPDATE = 2, UNDO_TRANSFER_INSERT = 3, UNDO_POSTED = 4 };
+
+struct alignas(16) UndoEntry {
+    u32 kind;
+    u32 slot;
+    u64 pad;
+    Account before;
+};
+
+struct Replay {
+    Tables T;
+    UndoEntry* undo;
+    u32 undo_len;
+    u32 undo_cap;
+    bool scope;
+    bool failed;  // a panic was raised: stop
+};
+
+__device__ static inline void rp_panic(Replay& R, u32 code) {
+    tb_panic(R.T.g, code);
+    R.failed = true;
+}
+
+__device__ static inline void rp_push(Replay& R, u32 kind, u32 slot, const Account* before) {
+    if (!R.scope) return;
+    if (R.undo_len == R.undo_cap) {
+        rp_panic(R, PANIC_UNDO_FULL);
+        return;
+    }
+    UndoEntry& e = R.undo[R.undo_len++];
+    e.kind = kind;
+    e.slot = slot;
+    if (before) e.before = *before;
+}
+
+__device__ static inline void rp_scope_close(Replay& R, bool persist) {
+    if (!persist) {
+        while (R.undo_len > 0) {
+            const UndoEntry& e = R.undo[--R.undo_len];
+            switch (e.kind) {
+            case UNDO_ACCOUNT_INSERT: {  // tombstone: id = 0, timestamp kept
+                u64* w = (u64*)&R.T.accounts[e.slot].id;
+                w[0] = 0;
+                w[1] = 0;
+                break;
+            }
+            case UNDO_ACCOUNT_UPDATE: R.T.accounts[e.slot] = e.before; break;
+            case UNDO_TRANSFER_INSERT: {
+                u64* w = (u64*)&R.T.transfers[e.slot].id;
+                w[0] = 0;
+                w[1] = 0;
+                break;
+            }
+            case UNDO_POSTED: R.T.posted[e.slot] = POSTED_NONE; break;
+            }
+        }
+    }
+    R.undo_len = 0;
+    R.scope = false;
+}
+
+// Checked `+` (ReleaseSafe trap).
+__device__ static inline u128 rp_add(Replay& R, u128 a, u128 b) {
+    u128 r;
+    if (tb_add_overflows(a, b, &r)) rp_panic(R, PANIC_OVERFLOW);
+    return r;
+}
+
+__device__ static inline void rp_account_update(Replay& R, u32 slot, const Account& next) {
+    rp_push(R, UNDO_ACCOUNT_UPDATE, slot, &R.T.accounts[slot]);
+    R.T.accounts[slot] = next;
+}
+
+__device__ static inline u32 rp_transfer_insert(Replay& R, const Transfer& t) {
+    const u32 slot = tb_transfer_claim(R.T, tb_lo(t.id), tb_hi(t.id), t.timestamp);
+    if (slot == TB_NOT_FOUND) {
+        R.failed = true;
+        return slot;
+    }
+    R.T.transfers[slot] = t;
+    rp_push(R, UNDO_TRANSFER_INSERT, slot, nullptr);
+    return slot;
+}
+
+__device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t) {
+    const Tables& T = R.T;
+    const u16 f = t.flags;
+    if ((f & TF_POST) && (f & TF_VOID)) return CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    if (f & TF_PENDING) return CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    if (f & TF_BAL_DEBIT) return CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    if (f & TF_BAL_CREDIT) return CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    if (t.pending_id == 0) return CT_PENDING_ID_MUST_NOT_BE_ZERO;
+    if (t.pending_id == TB_U128_MAX) return CT_PENDING_ID_MUST_NOT_BE_INT_MAX;
+    if (t.pending_id == t.id) return CT_PENDING_ID_MUST_BE_DIFFERENT;
+    if (t.timeout != 0) return CT_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+
+    const u32 pslot = tb_transfer_find(T, tb_lo(t.pending_id), tb_hi(t.pending_id));
+    if (pslot == TB_NOT_FOUND) return CT_PENDING_TRANSFER_NOT_FOUND;
+    const Transfer p = T.transfers[pslot];
+    if (!(p.flags & TF_PENDING)) return CT_PENDING_TRANSFER_NOT_PENDING;
+    const u32 drs = tb_account_find(T, tb_lo(p.debit_account_id), tb_hi(p.debit_account_id));
+    const u32 crs = tb_account_find(T, tb_lo(p.credit_account_id), tb_hi(p.credit_account_id));
+    if (drs == TB_NOT_FOUND || crs == TB_NOT_FOUND) {
+        rp_panic(R, PANIC_ASSERT);
+        return R_OK;
+    }
+    if (t.debit_account_id > 0 && t.debit_account_id != p.debit_account_id) {
+        return CT_PENDING_TRANSFER_HAS_DIFFERENT_DEBIT_ACCOUNT_ID;
+    }
+    if (t.credit_account_id > 0 && t.credit_account_id != p.credit_account_id) {
+        return CT_PENDING_TRANSFER_HAS_DIFFERENT_CREDIT_ACCOUNT_ID;
+    }
+    if (t.ledger > 0 && t.ledger != p.ledger) return CT_PENDING_TRANSFER_HAS_DIFFERENT_LEDGER;
+    if (t.code > 0 && t.code != p.code) return CT_PENDING_TRANSFER_HAS_DIFFERENT_CODE;
+    const u128 amount = t.amount > 0 ? t.amount : p.amount;
+    if (amount > p.amount) return CT_EXCEEDS_PENDING_TRANSFER_AMOUNT;
+    if ((f & TF_VOID) && amount < p.amount) return CT_PENDING_TRANSFER_HAS_DIFFERENT_AMOUNT;
+
+    const u32 es = tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id));
+    if (es != TB_NOT_FOUND) return tb_post_void_exists(t, T.transfers[es], p);
+    const u8 posted = T.posted[pslot];
+    if (posted == POSTED_POSTED) return CT_PENDING_TRANSFER_ALREADY_POSTED;
+    if (posted == POSTED_VOIDED) return CT_PENDING_TRANSFER_ALREADY_VOIDED;
+    if (!(p.timestamp < t.timestamp)) {
+        rp_panic(R, PANIC_ASSERT);
+        return R_OK;
+    }
+    if (p.timeout > 0) {
+        const u64 timeout_ns = (u64)p.timeout * 1000000000ULL;
+        const u64 expiry = p.timestamp + timeout_ns;
+        if (expiry < p.timestamp) {
+            rp_panic(R, PANIC_OVERFLOW);
+            return R_OK;
+        }
+        if (t.timestamp >= expiry) return CT_PENDING_TRANSFER_EXPIRED;
+    }
+
+    Transfer r;
+    r.id = t.id;
+    r.debit_account_id = p.debit_account_id;
+    r.credit_account_id = p.credit_account_id;
+    r.user_data_128 = t.user_data_128 > 0 ? t.user_data_128 : p.user_data_128;
+    r.user_data_64 = t.user_data_64 > 0 ? t.user_data_64 : p.user_data_64;
+    r.user_data_32 = t.user_data_32 > 0 ? t.user_data_32 : p.user_data_32;
+    r.ledger = p.ledger;
+    r.code = p.code;
+    r.pending_id = t.pending_id;
+    r.timeout = 0;
+    r.timestamp = t.timestamp;
+    r.flags = t.flags;
+    r.amount = amount;
+    rp_transfer_insert(R, r);
+    if (R.failed) return R_OK;
+
+    rp_push(R, UNDO_POSTED, pslot, nullptr);
+    T.posted[pslot] = (f & TF_POST) ? POSTED_POSTED : POSTED_VOIDED;
+
+    Account dr = T.accounts[drs];
+    Account cr = T.accounts[crs];
+    if (dr.debits_pending < p.amount || cr.credits_pending < p.amount) {
+        rp_panic(R, PANIC_OVERFLOW);
+        return R_OK;
+    }
+    dr.debits_pending -= p.amount;
+    cr.credits_pending -= p.amount;
+    if (f & TF_POST) {
+        dr.debits_posted = rp_add(R, dr.debits_posted, amount);
+        cr.credits_posted = rp_add(R, cr.credits_posted, amount);
+    }
+    rp_account_update(R, drs, dr);
+    rp_account_update(R, crs, cr);
+    return R_OK;
+}
+
+__device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t) {
+    const Tables& T = R.T;
+    const u16 f = t.flags;
+    if (f & TF_PADDING) return CT_RESERVED_FLAG;
+    if (t.id == 0) return CT_ID_MUST_NOT_BE_ZERO;
+    if (t.id == TB_U128_MAX) return CT_ID_MUST_NOT_BE_INT_MAX;
+    if (f & (TF_POST | TF_VOID)) return rp_post_or_void(R, t);
+
+    if (t.debit_account_id == 0) return CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (t.debit_account_id == TB_U128_MAX) return CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (t.credit_account_id == 0) return CT_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (t.credit_account_id == TB_U128_MAX) return CT_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (t.credit_account_id == t.debit_account_id) return CT_ACCOUNTS_MUST_BE_DIFFERENT;
+    if (t.pending_id != 0) return CT_PENDING_ID_MUST_BE_ZERO;
+    if (!(f & TF_PENDING)) {
+        if (t.timeout != 0) return CT_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+    }
+    if (!(f & (TF_BAL_DEBIT | TF_BAL_CREDIT))) {
+        if (t.amount == 0) return CT_AMOUNT_MUST_NOT_BE_ZERO;
+    }
+    if (t.ledger == 0) return CT_LEDGER_MUST_NOT_BE_ZERO;
+    if (t.code == 0) return CT_CODE_MUST_NOT_BE_ZERO;
+
+    const u32 drs = tb_account_find(T, tb_lo(t.debit_account_id), tb_hi(t.debit_account_id));
+    if (drs == TB_NOT_FOUND) return CT_DEBIT_ACCOUNT_NOT_FOUND;
+    const u32 crs = tb_account_find(T, tb_lo(t.credit_account_id), tb_hi(t.credit_account_id));
+    if (crs == TB_NOT_FOUND) return CT_CREDIT_ACCOUNT_NOT_FOUND;
+    Account dr = T.accounts[drs];
+    Account cr = T.accounts[crs];
+    if (!(t.timestamp > dr.timestamp) || !(t.timestamp > cr.timestamp)) {
+        rp_panic(R, PANIC_ASSERT);
+        return R_OK;
+    }
+    if (dr.ledger != cr.ledger) return CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+    if (t.ledger != dr.ledger) return CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+
+    const u32 es = tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id));
+    if (es != TB_NOT_FOUND) return tb_transfer_exists(t, T.transfers[es]);
+
+    u128 amount = t.amount;
+    if (f & (TF_BAL_DEBIT | TF_BAL_CREDIT)) {
+        if (amount == 0) amount = (u128)UINT64_MAX;  // maxInt(u64) (:829)
+    }
+    if (f & TF_BAL_DEBIT) {
+        const u128 bal = rp_add(R, dr.debits_posted, dr.debits_pending);
+        const u128 room = dr.credits_posted > bal ? dr.credits_posted - bal : 0;  // -|
+        if (room < amount) amount = room;
+        if (amount == 0) return CT_EXCEEDS_CREDITS;
+    }
+    if (f & TF_BAL_CREDIT) {
+        const u128 bal = rp_add(R, cr.credits_posted, cr.credits_pending);
+        const u128 room = cr.debits_posted > bal ? cr.debits_posted - bal : 0;
+        if (room < amount) amount = room;
+        if (amount == 0) return CT_EXCEEDS_DEBITS;
+    }
+    if (R.failed) return R_OK;
+
+    u128 r;
+    if (f & TF_PENDING) {
+        if (tb_add_overflows(amount, dr.debits_pending, &r)) return CT_OVERFLOWS_DEBITS_PENDING;
+        if (tb_add_overflows(amount, cr.credits_pending, &r)) return CT_OVERFLOWS_CREDITS_PENDING;
+    }
+    if (tb_add_overflows(amount, dr.debits_posted, &r)) return CT_OVERFLOWS_DEBITS_POSTED;
+    if (tb_add_overflows(amount, cr.credits_posted, &r)) return CT_OVERFLOWS_CREDITS_POSTED;
+    if (tb_add_overflows(amount, rp_add(R, dr.debits_pending, dr.debits_posted), &r)) return CT_OVERFLOWS_DEBITS;
+    if (tb_add_overflows(amount, rp_add(R, cr.credits_pending, cr.credits_posted), &r)) return CT_OVERFLOWS_CREDITS;
+    if (R.failed) return R_OK;
+    const u64 timeout_ns = (u64)t.timeout * 1000000000ULL;
+    if (t.timestamp + timeout_ns < t.timestamp) return CT_OVERFLOWS_TIMEOUT;
+    // debits_exceed_credits / credits_exceed_debits (tigerbeetle.zig:31-39).
+    if ((dr.flags & AF_DEBITS_MUST_NOT_EXCEED_CREDITS) &&
+        rp_add(R, rp_add(R, dr.debits_pending, dr.debits_posted), amount) > dr.credits_posted) {
+        return CT_EXCEEDS_CREDITS;
+    }
+    if ((cr.flags & AF_CREDITS_MUST_NOT_EXCEED_DEBITS) &&
+        rp_add(R, rp_add(R, cr.credits_pending, cr.credits_posted), amount) > cr.debits_posted) {
+        return CT_EXCEEDS_DEBITS;
+    }
+    if (R.failed) return R_OK;
+
+    Transfer t2 = t;
+    t2.amount = amount;
+    rp_transfer_insert(R, t2);
+    if (R.failed) return R_OK;
+    if (f & TF_PENDING) {
+        dr.debits_pending = rp_add(R, dr.debits_pending, amount);
+        cr.credits_pending = rp_add(R, cr.credits_pending, amount);
+    } else {
+        dr.debits_posted = rp_add(R, dr.debits_posted, amount);
+        cr.credits_posted = rp_add(R, cr.credits_posted, amount);
+    }
+    rp_account_update(R, drs, dr);
+    rp_account_update(R, crs, cr);
+    return R_OK;
+}
+
+__device__ static inline u32 rp_create_account(Replay& R, const Account& a) {
+    const u32 code = tb_account_stateless(a);
+    if (code != R_OK) return code;
+    const u32 es = tb_account_find(R.T, tb_lo(a.id), tb_hi(a.id));
+    if (es != TB_NOT_FOUND) return tb_account_exists(a, R.T.accounts[es]);
+    const u32 slot = tb_account_claim(R.T, tb_lo(a.id), tb_hi(a.id), a.timestamp);
+    if (slot == TB_NOT_FOUND) {
+        R.failed = true;
+        return R_OK;
+    }
+    R.T.accounts[slot] = a;
+    rp_push(R, UNDO_ACCOUNT_INSERT, slot, nullptr);
+    return R_OK;
+}
+
+// Replay the dependent events of batch b (lane 0 only).  Returns the max ok timestamp.
+template <u8 OP>
+__device__ static inline u64 rp_batch(const PassArgs& P, Replay& R, u32 b) {
+    const u64 boff = P.batch_off[b];
+    const u32 L = (u32)(P.batch_off[b + 1] - boff);
+    const u32 pbase = (u32)(boff - P.e0);
+    const u64 ts0 = P.batch_ts[b] - L + 1;
+    const u32 nd = P.dep_count[b - P.b0];
+    const u32* list = P.dep_list + pbase;
+    u64 tsmax = 0;
+    bool in_chain = false, broken = false;
+    u32 chain_k = 0;
+    for (u32 k = 0; k < nd && !R.failed; k++) {
+        const u32 i = list[k];
+        const u8* ev = P.events + (boff + i) * 128;
+        const u16 flags = *(const u16*)(ev + 118);
+        const u64 evts = *(const u64*)(ev + 120);
+        const bool linked = flags & 1;
+        u32 result;
+        if (linked && !in_chain) {
+            in_chain = true;
+            chain_k = k;
+            R.scope = true;
+            R.undo_len = 0;
+        }
+        if (linked && i == L - 1) {
+            result = R_LINKED_EVENT_CHAIN_OPEN;
+        } else if (broken) {
+            result = R_LINKED_EVENT_FAILED;
+        } else if (evts != 0) {
+            result = R_TIMESTAMP_MUST_BE_ZERO;
+        } else {
+            const u64 ts = ts0 + i;
+            if (OP == OP_CREATE_TRANSFERS) {
+                Transfer t = *(const Transfer*)ev;
+                t.timestamp = ts;
+                result = rp_create_transfer(R, t);
+            } else {
+                Account a = *(const Account*)ev;
+                a.timestamp = ts;
+                result = rp_create_account(R, a);
+            }
+            if (result == R_OK && !R.failed) tsmax = ts;
+        }
+        if (R.failed) break;
+        if (result != R_OK && in_chain && !broken) {
+            broken = true;
+            rp_scope_close(R, false);
+            for (u32 kk = chain_k; kk < k; kk++) {
+                u32* w = &P.info[pbase + list[kk]];
+                *w = (*w & 0xFFFFFF00u) | R_LINKED_EVENT_FAILED;
+            }
+        }
+        u32* w = &P.info[pbase + i];
+        *w = (*w & 0xFFFFFF00u) | result;
+        if (in_chain && (!linked || result == R_LINKED_EVENT_CHAIN_OPEN)) {
+            if (!broken) rp_scope_close(R, true);
+            in_chain = false;
+            broken = false;
+        }
+    }
+    return tsmax;
+}
+
+template <u8 OP>
+__global__ __launch_bounds__(REPLAY_THREADS) void tb_replay(PassArgs P, UndoEntry* undo, u32 undo_cap) {
+    __shared__ u8 s_code[BATCH_LDS];
+    __shared__ u32 s_wave[REPLAY_THREADS / 64];
+    __shared__ u32 s_list[REPLAY_THREADS];
+    __shared__ u32 s_nlist;
+    __shared__ u32 s_failed;
+    Globals* g = P.T.g;
+    const u32 nb = P.b1 - P.b0;
+    if (threadIdx.x == 0) s_failed = 0;
+    __syncthreads();
+    const bool any = *(volatile u64*)&g->dependent_total != 0;
+    if (any) {
+        Replay R;
+        R.T = P.T;
+        R.undo = undo;
+        R.undo_len = 0;
+        R.undo_cap = undo_cap;
+        R.scope = false;
+        R.failed = false;
+        u64 tsmax = 0;
+        for (u32 c = 0; c < nb; c += REPLAY_THREADS) {
+            const u32 k = c + threadIdx.x;
+            const bool has = k < nb && P.dep_count[k] > 0;
+            u32 total;
+            const u32 r = tb_block_rank(has, s_wave, total);
+            if (has) s_list[r] = k;
+            if (threadIdx.x == 0) s_nlist = total;
+            __syncthreads();
+            const u32 nl = s_nlist;
+            for (u32 q = 0; q < nl; q++) {
+                const u32 b = P.b0 + s_list[q];
+                if (threadIdx.x == 0) {
+                    if (!s_failed) {
+                        const u64 m = rp_batch<OP>(P, R, b);
+                        tsmax = max(tsmax, m);
+                        if (R.failed) s_failed = 1;
+                    }
+                }
+                __syncthreads();
+                // The batch's final codes are in P.info now; write its reply.
+                const u64 boff = P.batch_off[b];
+                const u32 L = (u32)(P.batch_off[b + 1] - boff);
+                const u32 pbase = (u32)(boff - P.e0);
+                for (u32 i = threadIdx.x; i < L; i += REPLAY_THREADS) s_code[i] = (u8)(P.info[pbase + i] & 0xFF);
+                __syncthreads();
+                tb_write_replies(P, b, L, s_code, s_wave);
+                __syncthreads();
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0 && tsmax > g->commit_timestamp) g->commit_timestamp = tsmax;
+    }
+    if (threadIdx.x == 0) {
+        // Close the pass: bound += S, reset the dependent counter.
+        if (P.op == OP_CREATE_TRANSFERS) {
+            const u128 S = tb_sum_total(P.sum_shards);
+            const u128 nb2 = tb_sat_add(tb_u128(g->bound_lo, g->bound_hi), S);
+            g->bound_lo = tb_lo(nb2);
+            g->bound_hi = tb_hi(nb2);
+        }
+        g->dependent_all += g->dependent_total;
+        g->dependent_total = 0;
+    }
+}

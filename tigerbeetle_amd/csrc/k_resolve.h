@@ -1,0 +1,292 @@
+// k_resolve.h — kernel 2 of a pass: one 1024-thread workgroup per prepare (batch).
+//
+//  a. classify: an event is DEPENDENT when its intrinsic result (kernel 1, pre-pass state) may
+//     differ from the sequential result: its id / pending id collides with another event of the
+//     pass; or it would change or read the balance of a constrained account (limit flags
+//     tigerbeetle.zig:31-39, a balancing event's account :826-846, or an account whose balances
+//     could overflow u128 this pass — the certificate below); or it is a balancing event.
+//  b. linked chains (execute, state_machine.zig:628-692): a chain with a dependent member is
+//     dependent as a whole; an independent chain resolves from its first failing member: that
+//     member keeps its result, every other member becomes linked_event_failed (the last event of
+//     the batch keeps linked_event_chain_open).
+//  c. apply: independent ok events are inserted into the HBM transfer/account table and their
+//     balance deltas added with exact u128 atomics (sums commute, so the order does not matter).
+//  d. replies: non-ok results of a batch with no dependent event, ascending index (the reference's
+//     FIFO back-fill of linked_event_failed also yields ascending order).  Batches with dependent
+//     events are answered by the replay kernel.
+//
+// Overflow certificate: with S = Σ of every potential debit/credit increment of the pass and
+// `bound` >= dp+dpost, cp+cpost of every account, no overflow check of create_transfer
+// (:848-861) can fire in this pass if bound + S fits in u128.  Otherwise each account is checked
+// individually (its own sums + S).
+#pragma once
+
+#include "k_validate.h"
+
+// Ordered compaction helper: position of this thread's element among the true predicates of the
+// block (ascending threadIdx), and the block total.  Every thread of the block must call it.
+__device__ static inline u32 tb_block_rank(bool pred, u32* s_wave, u32& total) {
+    const u64 m = __ballot(pred);
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+    const u32 before = __popcll(m & ((1ULL << lane) - 1));
+    if (lane == 0) s_wave[wave] = __popcll(m);
+    __syncthreads();
+    u32 wb = 0, tot = 0;
+    for (u32 k = 0; k < nwaves; k++) {
+        const u32 c = s_wave[k];
+        wb += (k < wave) ? c : 0;
+        tot += c;
+    }
+    __syncthreads();
+    total = tot;
+    return wb + before;
+}
+
+__device__ static inline bool tb_account_cert_fails(const Account* a, u128 S) {
+    u128 d, c, r;
+    if (tb_add_overflows(a->debits_pending, a->debits_posted, &d)) return true;
+    if (tb_add_overflows(a->credits_pending, a->credits_posted, &c)) return true;
+    if (tb_add_overflows(d, S, &r)) return true;
+    if (tb_add_overflows(c, S, &r)) return true;
+    return false;
+}
+
+// Write the sparse reply of batch b from LDS codes.
+__device__ static inline void tb_write_replies(const PassArgs& P, u32 b, u32 L, const u8* s_code, u32* s_wave) {
+    u32* out = P.results + 2 * P.batch_off[b];
+    u32 running = 0;
+    for (u32 c = 0; c < L; c += blockDim.x) {
+        const u32 i = c + threadIdx.x;
+        const u32 code = i < L ? s_code[i] : R_OK;
+        u32 total;
+        const u32 r = tb_block_rank(code != R_OK, s_wave, total);
+        if (code != R_OK) {
+            out[2 * (running + r)] = i;
+            out[2 * (running + r) + 1] = code;
+        }
+        running += total;
+    }
+    if (threadIdx.x == 0) P.reply_bytes[b] = running * 8;
+}
+
+// Apply one independent ok transfer (create_transfer :866-882, post_or_void :971-1012).
+__device__ static inline void tb_apply_transfer(const PassArgs& P, u32 pe, u32 info, u64 ts) {
+    const Tables& T = P.T;
+    const Transfer* ev = (const Transfer*)(P.events + (P.e0 + pe) * 128);
+    Transfer t = *ev;
+    t.timestamp = ts;
+    const Account* dr = &T.accounts[P.dr[pe]];
+    const Account* cr = &T.accounts[P.cr[pe]];
+    const u128 amount = tb_u128(P.amt[2 * pe], P.amt[2 * pe + 1]);
+    if (info & HZ_POSTVOID) {
+        const u32 pslot = P.ps[pe];
+        const Transfer& p = T.transfers[pslot];
+        Transfer r;
+        r.id = t.id;
+        r.debit_account_id = p.debit_account_id;
+        r.credit_account_id = p.credit_account_id;
+        r.amount = (t.flags & TF_POST) ? amount : (t.amount > 0 ? t.amount : p.amount);
+        r.pending_id = t.pending_id;
+        r.user_data_128 = t.user_data_128 > 0 ? t.user_data_128 : p.user_data_128;
+        r.user_data_64 = t.user_data_64 > 0 ? t.user_data_64 : p.user_data_64;
+        r.user_data_32 = t.user_data_32 > 0 ? t.user_data_32 : p.user_data_32;
+        r.timeout = 0;
+        r.ledger = p.ledger;
+        r.code = p.code;
+        r.flags = t.flags;
+        r.timestamp = ts;
+        const u128 neg = (u128)0 - p.amount;
+        const u32 slot = tb_transfer_claim(T, tb_lo(r.id), tb_hi(r.id), ts);
+        if (slot == TB_NOT_FOUND) return;
+        T.transfers[slot] = r;
+        T.posted[pslot] = (t.flags & TF_POST) ? POSTED_POSTED : POSTED_VOIDED;
+        tb_atomic_add_u128((u8*)dr + ACCOUNT_OFF_DEBITS_PENDING, neg);
+        tb_atomic_add_u128((u8*)cr + ACCOUNT_OFF_CREDITS_PENDING, neg);
+        if (t.flags & TF_POST) {
+            tb_atomic_add_u128((u8*)dr + ACCOUNT_OFF_DEBITS_POSTED, amount);
+            tb_atomic_add_u128((u8*)cr + ACCOUNT_OFF_CREDITS_POSTED, amount);
+        }
+    } else {
+        t.amount = amount;
+        const u32 slot = tb_transfer_claim(T, tb_lo(t.id), tb_hi(t.id), ts);
+        if (slot == TB_NOT_FOUND) return;
+        T.transfers[slot] = t;
+        if (t.flags & TF_PENDING) {
+            tb_atomic_add_u128((u8*)dr + ACCOUNT_OFF_DEBITS_PENDING, amount);
+            tb_atomic_add_u128((u8*)cr + ACCOUNT_OFF_CREDITS_PENDING, amount);
+        } else {
+            tb_atomic_add_u128((u8*)dr + ACCOUNT_OFF_DEBITS_POSTED, amount);
+            tb_atomic_add_u128((u8*)cr + ACCOUNT_OFF_CREDITS_POSTED, amount);
+        }
+    }
+}
+
+// Apply one independent ok account (create_account :762, groove insert).
+__device__ static inline void tb_apply_account(const PassArgs& P, u32 pe, u64 ts) {
+    const Account* ev = (const Account*)(P.events + (P.e0 + pe) * 128);
+    Account a = *ev;
+    a.timestamp = ts;
+    const u32 slot = tb_account_claim(P.T, tb_lo(a.id), tb_hi(a.id), ts);
+    if (slot == TB_NOT_FOUND) return;
+    P.T.accounts[slot] = a;
+}
+
+template <u8 OP>
+__global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
+    __shared__ u8 s_code[BATCH_LDS];
+    __shared__ u8 s_fl[BATCH_LDS];   // bit0 linked, bit1 dependent
+    __shared__ u16 s_seg[BATCH_LDS]; // segment (chain) start
+    __shared__ u32 s_key[BATCH_LDS]; // per segment start: min over members (0 = dependent member)
+    __shared__ u32 s_wave[RESOLVE_THREADS / 64];
+    __shared__ u64 s_tsmax[RESOLVE_THREADS / 64];
+
+    const Tables& T = P.T;
+    const u32 b = P.b0 + blockIdx.x;
+    const u64 boff = P.batch_off[b];
+    const u32 L = (u32)(P.batch_off[b + 1] - boff);
+    const u32 pbase = (u32)(boff - P.e0);
+    const u64 ts0 = P.batch_ts[b] - L + 1;  // timestamp of event 0 (:645)
+
+    u128 S = 0;
+    bool cert_global = true;
+    if (OP == OP_CREATE_TRANSFERS) {
+        S = tb_sum_total(P.sum_shards);
+        u128 r;
+        cert_global = !tb_add_overflows(tb_u128(T.g->bound_lo, T.g->bound_hi), S, &r);
+    }
+
+    // a. classify
+    bool local_linked = false;
+    for (u32 i = threadIdx.x; i < L; i += RESOLVE_THREADS) {
+        const u32 pe = pbase + i;
+        const u32 info = P.info[pe];
+        const u32 code = info & 0xFF;
+        bool dep = false;
+        if ((info & HZ_KEYS) && (tb_dedup_is_dup(P.dedup, P.dedup_mask, P.kid[pe]) ||
+                                 (P.kpid[pe] && tb_dedup_is_dup(P.dedup, P.dedup_mask, P.kpid[pe])))) {
+            dep = true;
+        }
+        if (OP == OP_CREATE_TRANSFERS && !dep && (info & HZ_ACCTS) &&
+            (code == R_OK || code == CT_OVERFLOWS_TIMEOUT)) {
+            const u32 drs = P.dr[pe], crs = P.cr[pe];
+            if (code == R_OK) {
+                if (info & (HZ_BAL | HZ_LIMIT)) dep = true;
+                else if (T.account_mark[drs] == P.epoch || T.account_mark[crs] == P.epoch) dep = true;
+            }
+            if (!dep && !cert_global &&
+                (tb_account_cert_fails(&T.accounts[drs], S) || tb_account_cert_fails(&T.accounts[crs], S))) {
+                dep = true;
+            }
+        }
+        const bool linked = (info >> 16) & 1;
+        local_linked |= linked;
+        s_code[i] = (u8)code;
+        s_fl[i] = (linked ? 1 : 0) | (dep ? 2 : 0);
+        s_key[i] = 0xFFFFFFFFu;
+    }
+    const bool any_linked = __syncthreads_or(local_linked);
+
+    // b. linked chains
+    if (any_linked) {
+        u32 carry = 0;
+        for (u32 c = 0; c < L; c += RESOLVE_THREADS) {
+            const u32 i = c + threadIdx.x;
+            u32 v = 0;
+            if (i < L) v = (i == 0 || !(s_fl[i - 1] & 1)) ? i : 0;
+            const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+            for (u32 off = 1; off < 64; off <<= 1) {
+                const u32 o = __shfl_up(v, off);
+                if (lane >= off) v = max(v, o);
+            }
+            if (lane == 63) s_wave[wave] = v;
+            __syncthreads();
+            u32 prefix = carry;
+            for (u32 k = 0; k < wave; k++) prefix = max(prefix, s_wave[k]);
+            v = max(v, prefix);
+            if (i < L) s_seg[i] = (u16)v;
+            __syncthreads();
+            carry = s_seg[min(c + RESOLVE_THREADS, L) - 1];
+            __syncthreads();
+        }
+        for (u32 i = threadIdx.x; i < L; i += RESOLVE_THREADS) {
+            const u32 s = s_seg[i];
+            if (s_fl[s] & 1) {  // member of a chain
+                const u32 key = (s_fl[i] & 2) ? 0u : (s_code[i] != R_OK ? i + 1 : 0xFFFFFFFFu);
+                if (key != 0xFFFFFFFFu) atomicMin(&s_key[s], key);
+            }
+        }
+        __syncthreads();
+    }
+
+    // Final results, dependent list, apply.
+    u64 tsmax = 0;
+    u32 ndep = 0;
+    u32* dep_out = P.dep_list + pbase;
+    for (u32 c = 0; c < L; c += RESOLVE_THREADS) {
+        const u32 i = c + threadIdx.x;
+        bool dep = false, eval_ok = false;
+        u32 fin = R_OK;
+        if (i < L) {
+            const u32 code = s_code[i];
+            dep = (s_fl[i] & 2) != 0;
+            fin = code;
+            const u32 s = any_linked ? s_seg[i] : i;
+            if (any_linked && (s_fl[s] & 1)) {
+                const u32 key = s_key[s];
+                if (key == 0) {
+                    dep = true;
+                } else if (key == 0xFFFFFFFFu) {
+                    fin = R_OK;
+                    eval_ok = true;
+                } else {
+                    const u32 ff = key - 1;
+                    if (i == ff) {
+                        fin = code;
+                    } else if (i < ff) {
+                        fin = R_LINKED_EVENT_FAILED;
+                        eval_ok = true;
+                    } else {
+                        fin = ((s_fl[i] & 1) && i == L - 1) ? R_LINKED_EVENT_CHAIN_OPEN : R_LINKED_EVENT_FAILED;
+                    }
+                }
+            } else {
+                eval_ok = code == R_OK;
+            }
+            if (!dep) {
+                if (fin == TB_CODE_PANIC) tb_panic(T.g, PANIC_ASSERT);
+                s_code[i] = (u8)fin;
+                const u32 pe = pbase + i;
+                const u32 info = P.info[pe];
+                P.info[pe] = (info & 0xFFFFFF00u) | fin | (eval_ok ? HZ_EVAL_OK : 0);
+                const u64 ts = ts0 + i;
+                if (eval_ok) tsmax = ts;  // increasing in i
+                if (fin == R_OK) {
+                    if (OP == OP_CREATE_TRANSFERS) tb_apply_transfer(P, pe, info, ts);
+                    else tb_apply_account(P, pe, ts);
+                }
+            } else {
+                P.info[pbase + i] |= HZ_DEP;
+            }
+        }
+        u32 total;
+        const u32 r = tb_block_rank(dep, s_wave, total);
+        if (dep) dep_out[ndep + r] = i;
+        ndep += total;
+    }
+
+    // commit_timestamp: max over events that returned ok when evaluated (:763, :882, :1012).
+    u64 m = tsmax;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (u64)__shfl_xor((unsigned long long)m, off));
+    if ((threadIdx.x & 63) == 0) s_tsmax[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u64 mm = 0;
+        for (u32 k = 0; k < RESOLVE_THREADS / 64; k++) mm = max(mm, s_tsmax[k]);
+        if (mm) atomicMax((unsigned long long*)&T.g->commit_timestamp, (unsigned long long)mm);
+        P.dep_count[blockIdx.x] = ndep;
+        if (ndep) atomicAdd((unsigned long long*)&T.g->dependent_total, (unsigned long long)ndep);
+    }
+    if (ndep == 0) tb_write_replies(P, b, L, s_code, s_wave);
+}

@@ -1,0 +1,308 @@
+// k_validate.h — kernel 1 of a pass: one event per lane.
+//
+// Computes each event's *intrinsic* result against the pre-pass HBM state, in the reference's code
+// order (create_transfer state_machine.zig:779-884, post_or_void_pending_transfer :907-1014,
+// create_account :738-765), plus the hazard bits the resolve kernel needs to decide whether that
+// result can be trusted (see DESIGN.md "Dependence").
+#pragma once
+
+#include "pass.h"
+
+#define TB_CODE_PANIC 63u  // the reference would trap if this event were evaluated in sequence
+
+struct TransferScratch {
+    u32 hz = 0;
+    u32 dr = TB_NOT_FOUND, cr = TB_NOT_FOUND, ps = TB_NOT_FOUND;
+    u128 amount = 0;       // amount applied by an independent ok event (post: posted amount)
+    u128 contrib = 0;      // contribution to S (overflow certificate)
+    u64 kid = 0, kpid = 0;
+};
+
+// create_transfer_exists (state_machine.zig:886-905).
+__device__ static inline u32 tb_transfer_exists(const Transfer& t, const Transfer& e) {
+    if (t.flags != e.flags) return CT_EXISTS_WITH_DIFFERENT_FLAGS;
+    if (t.debit_account_id != e.debit_account_id) return CT_EXISTS_WITH_DIFFERENT_DEBIT_ACCOUNT_ID;
+    if (t.credit_account_id != e.credit_account_id) return CT_EXISTS_WITH_DIFFERENT_CREDIT_ACCOUNT_ID;
+    if (t.amount != e.amount) return CT_EXISTS_WITH_DIFFERENT_AMOUNT;
+    if (t.user_data_128 != e.user_data_128) return CT_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    if (t.user_data_64 != e.user_data_64) return CT_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    if (t.user_data_32 != e.user_data_32) return CT_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    if (t.timeout != e.timeout) return CT_EXISTS_WITH_DIFFERENT_TIMEOUT;
+    if (t.code != e.code) return CT_EXISTS_WITH_DIFFERENT_CODE;
+    return CT_EXISTS;
+}
+
+// post_or_void_pending_transfer_exists (state_machine.zig:1016-1077).
+__device__ static inline u32 tb_post_void_exists(const Transfer& t, const Transfer& e, const Transfer& p) {
+    if (t.flags != e.flags) return CT_EXISTS_WITH_DIFFERENT_FLAGS;
+    if (t.amount == 0) {
+        if (e.amount != p.amount) return CT_EXISTS_WITH_DIFFERENT_AMOUNT;
+    } else {
+        if (t.amount != e.amount) return CT_EXISTS_WITH_DIFFERENT_AMOUNT;
+    }
+    if (t.pending_id != e.pending_id) return CT_EXISTS_WITH_DIFFERENT_PENDING_ID;
+    if (t.user_data_128 == 0) {
+        if (e.user_data_128 != p.user_data_128) return CT_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    } else {
+        if (t.user_data_128 != e.user_data_128) return CT_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    }
+    if (t.user_data_64 == 0) {
+        if (e.user_data_64 != p.user_data_64) return CT_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    } else {
+        if (t.user_data_64 != e.user_data_64) return CT_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    }
+    if (t.user_data_32 == 0) {
+        if (e.user_data_32 != p.user_data_32) return CT_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    } else {
+        if (t.user_data_32 != e.user_data_32) return CT_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    }
+    return CT_EXISTS;
+}
+
+__device__ static inline u32 tb_validate_post_void(const PassArgs& P, const Transfer& t, u64 ts,
+                                                   TransferScratch& s) {
+    const Tables& T = P.T;
+    const u16 f = t.flags;
+    if ((f & TF_POST) && (f & TF_VOID)) return CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    if (f & TF_PENDING) return CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    if (f & TF_BAL_DEBIT) return CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    if (f & TF_BAL_CREDIT) return CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    if (t.pending_id == 0) return CT_PENDING_ID_MUST_NOT_BE_ZERO;
+    if (t.pending_id == TB_U128_MAX) return CT_PENDING_ID_MUST_NOT_BE_INT_MAX;
+    if (t.pending_id == t.id) return CT_PENDING_ID_MUST_BE_DIFFERENT;
+    if (t.timeout != 0) return CT_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+
+    // From here the result reads the state of pending_id and of id: register both keys.
+    s.hz |= HZ_POSTVOID | HZ_KEYS;
+    s.kid = tb_dedup_key(tb_lo(t.id), tb_hi(t.id));
+    s.kpid = tb_dedup_key(tb_lo(t.pending_id), tb_hi(t.pending_id));
+    tb_dedup_insert(P.dedup, P.dedup_mask, s.kid);
+    tb_dedup_insert(P.dedup, P.dedup_mask, s.kpid);
+
+    const u32 pslot = tb_transfer_find(T, tb_lo(t.pending_id), tb_hi(t.pending_id));
+    if (pslot == TB_NOT_FOUND) return CT_PENDING_TRANSFER_NOT_FOUND;
+    const Transfer p = T.transfers[pslot];
+    if (!(p.flags & TF_PENDING)) return CT_PENDING_TRANSFER_NOT_PENDING;
+
+    const u32 drs = tb_account_find(T, tb_lo(p.debit_account_id), tb_hi(p.debit_account_id));
+    const u32 crs = tb_account_find(T, tb_lo(p.credit_account_id), tb_hi(p.credit_account_id));
+    if (drs == TB_NOT_FOUND || crs == TB_NOT_FOUND) return TB_CODE_PANIC;  // `.?` at :929-930
+
+    if (t.debit_account_id > 0 && t.debit_account_id != p.debit_account_id) {
+        return CT_PENDING_TRANSFER_HAS_DIFFERENT_DEBIT_ACCOUNT_ID;
+    }
+    if (t.credit_account_id > 0 && t.credit_account_id != p.credit_account_id) {
+        return CT_PENDING_TRANSFER_HAS_DIFFERENT_CREDIT_ACCOUNT_ID;
+    }
+    if (t.ledger > 0 && t.ledger != p.ledger) return CT_PENDING_TRANSFER_HAS_DIFFERENT_LEDGER;
+    if (t.code > 0 && t.code != p.code) return CT_PENDING_TRANSFER_HAS_DIFFERENT_CODE;
+
+    const u128 amount = t.amount > 0 ? t.amount : p.amount;
+    if (amount > p.amount) return CT_EXCEEDS_PENDING_TRANSFER_AMOUNT;
+    if ((f & TF_VOID) && amount < p.amount) return CT_PENDING_TRANSFER_HAS_DIFFERENT_AMOUNT;
+
+    const u32 es = tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id));
+    if (es != TB_NOT_FOUND) return tb_post_void_exists(t, T.transfers[es], p);
+
+    const u8 posted = T.posted[pslot];
+    if (posted == POSTED_POSTED) return CT_PENDING_TRANSFER_ALREADY_POSTED;
+    if (posted == POSTED_VOIDED) return CT_PENDING_TRANSFER_ALREADY_VOIDED;
+
+    if (!(p.timestamp < ts)) return TB_CODE_PANIC;
+    if (p.timeout > 0) {
+        const u64 timeout_ns = (u64)p.timeout * 1000000000ULL;
+        const u64 expiry = p.timestamp + timeout_ns;
+        if (expiry < p.timestamp) return TB_CODE_PANIC;  // checked `+` at :968
+        if (ts >= expiry) return CT_PENDING_TRANSFER_EXPIRED;
+    }
+
+    s.dr = drs;
+    s.cr = crs;
+    s.ps = pslot;
+    s.hz |= HZ_ACCTS;
+    if ((T.accounts[drs].flags | T.accounts[crs].flags) & AF_LIMITS) s.hz |= HZ_LIMIT;
+    s.amount = (f & TF_POST) ? amount : 0;
+    // A post moves <= p.amount from pending to posted: dp + dpost never grows, so no S term.
+    return R_OK;
+}
+
+__device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Transfer& t, u64 ts,
+                                                  TransferScratch& s) {
+    const Tables& T = P.T;
+    const u16 f = t.flags;
+    if (f & TF_PADDING) return CT_RESERVED_FLAG;
+    if (t.id == 0) return CT_ID_MUST_NOT_BE_ZERO;
+    if (t.id == TB_U128_MAX) return CT_ID_MUST_NOT_BE_INT_MAX;
+
+    if (f & (TF_POST | TF_VOID)) return tb_validate_post_void(P, t, ts, s);
+
+    if (t.debit_account_id == 0) return CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (t.debit_account_id == TB_U128_MAX) return CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (t.credit_account_id == 0) return CT_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (t.credit_account_id == TB_U128_MAX) return CT_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (t.credit_account_id == t.debit_account_id) return CT_ACCOUNTS_MUST_BE_DIFFERENT;
+    if (t.pending_id != 0) return CT_PENDING_ID_MUST_BE_ZERO;
+    if (!(f & TF_PENDING)) {
+        if (t.timeout != 0) return CT_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+    }
+    if (!(f & (TF_BAL_DEBIT | TF_BAL_CREDIT))) {
+        if (t.amount == 0) return CT_AMOUNT_MUST_NOT_BE_ZERO;
+    }
+    if (t.ledger == 0) return CT_LEDGER_MUST_NOT_BE_ZERO;
+    if (t.code == 0) return CT_CODE_MUST_NOT_BE_ZERO;
+
+    const u32 drs = tb_account_find(T, tb_lo(t.debit_account_id), tb_hi(t.debit_account_id));
+    if (drs == TB_NOT_FOUND) return CT_DEBIT_ACCOUNT_NOT_FOUND;
+    const u32 crs = tb_account_find(T, tb_lo(t.credit_account_id), tb_hi(t.credit_account_id));
+    if (crs == TB_NOT_FOUND) return CT_CREDIT_ACCOUNT_NOT_FOUND;
+    const Account* dr = &T.accounts[drs];
+    const Account* cr = &T.accounts[crs];
+    const u32 dr_ledger = dr->ledger, cr_ledger = cr->ledger;
+    const u16 acct_flags = dr->flags | cr->flags;
+    if (!(ts > dr->timestamp) || !(ts > cr->timestamp)) return TB_CODE_PANIC;  // :817-818
+    if (dr_ledger != cr_ledger) return CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+    if (t.ledger != dr_ledger) return CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+
+    // From here the result reads the state of `id`.
+    s.hz |= HZ_KEYS;
+    s.kid = tb_dedup_key(tb_lo(t.id), tb_hi(t.id));
+    tb_dedup_insert(P.dedup, P.dedup_mask, s.kid);
+    const u32 es = tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id));
+    if (es != TB_NOT_FOUND) return tb_transfer_exists(t, T.transfers[es]);
+
+    s.dr = drs;
+    s.cr = crs;
+    s.hz |= HZ_ACCTS;
+    if (acct_flags & AF_LIMITS) s.hz |= HZ_LIMIT;
+    if (f & (TF_BAL_DEBIT | TF_BAL_CREDIT)) {
+        // The amount depends on the running balance (:826-846): dependent, and so is every event
+        // touching the balanced account in this pass.
+        s.hz |= HZ_BAL;
+        if (f & TF_BAL_DEBIT) P.T.account_mark[drs] = P.epoch;
+        if (f & TF_BAL_CREDIT) P.T.account_mark[crs] = P.epoch;
+        s.contrib = t.amount == 0 ? (u128)UINT64_MAX : t.amount;
+        return R_OK;
+    }
+    s.amount = t.amount;
+    s.contrib = t.amount;
+    // Overflow checks (:848-861) are certified impossible or the event is dependent (resolve);
+    // then the timeout check (:862) is the next possible failure.
+    const u64 timeout_ns = (u64)t.timeout * 1000000000ULL;
+    if (ts + timeout_ns < ts) return CT_OVERFLOWS_TIMEOUT;
+    return R_OK;
+}
+
+// Kernel 1 (create_transfers).
+__global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassArgs P) {
+    __shared__ __attribute__((aligned(16))) u8 stage[VALIDATE_THREADS * STAGE_STRIDE];
+    __shared__ u64 s_sum[2 * (VALIDATE_THREADS / 64)];
+
+    const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
+    const u32 count = min((u32)VALIDATE_THREADS, P.n - tile0);
+    tb_stage_events(P.events + (P.e0 + tile0) * 128, count, stage);
+
+    const u32 pe = tile0 + threadIdx.x;  // pass-relative event
+    TransferScratch s;
+    if (threadIdx.x < count) {
+        const Transfer t = tb_read_staged<Transfer>(stage);
+        const u64 e = P.e0 + pe;
+        const u32 b = tb_batch_of(P, e);
+        const u32 L = (u32)(P.batch_off[b + 1] - P.batch_off[b]);
+        const u32 j = (u32)(e - P.batch_off[b]);
+        u32 code;
+        if ((t.flags & TF_LINKED) && j == L - 1) {
+            code = R_LINKED_EVENT_CHAIN_OPEN;  // execute :632-640
+        } else if (t.timestamp != 0) {
+            code = R_TIMESTAMP_MUST_BE_ZERO;  // :643
+        } else {
+            const u64 ts = P.batch_ts[b] - L + j + 1;  // :645
+            code = tb_validate_transfer(P, t, ts, s);
+        }
+        P.info[pe] = code | s.hz | ((u32)t.flags << 16);
+        P.dr[pe] = s.dr;
+        P.cr[pe] = s.cr;
+        P.ps[pe] = s.ps;
+        P.amt[2 * pe] = tb_lo(s.amount);
+        P.amt[2 * pe + 1] = tb_hi(s.amount);
+        P.kid[pe] = s.kid;
+        P.kpid[pe] = s.kpid;
+        if (code != R_OK) s.contrib = 0;
+    }
+    // Block partial of S (saturating), then one sharded atomic per block.
+    const u128 w = tb_wave_sum_u128(s.contrib);
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        s_sum[2 * wave] = tb_lo(w);
+        s_sum[2 * wave + 1] = tb_hi(w);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u128 total = 0;
+        for (u32 k = 0; k < VALIDATE_THREADS / 64; k++) total = tb_sat_add(total, tb_u128(s_sum[2 * k], s_sum[2 * k + 1]));
+        tb_sum_publish(P, total);
+    }
+}
+
+// create_account_exists (state_machine.zig:767-777).
+__device__ static inline u32 tb_account_exists(const Account& a, const Account& e) {
+    if (a.flags != e.flags) return CA_EXISTS_WITH_DIFFERENT_FLAGS;
+    if (a.user_data_128 != e.user_data_128) return CA_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    if (a.user_data_64 != e.user_data_64) return CA_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    if (a.user_data_32 != e.user_data_32) return CA_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    if (a.ledger != e.ledger) return CA_EXISTS_WITH_DIFFERENT_LEDGER;
+    if (a.code != e.code) return CA_EXISTS_WITH_DIFFERENT_CODE;
+    return CA_EXISTS;
+}
+
+// Stateless prefix of create_account (state_machine.zig:741-756).
+__device__ static inline u32 tb_account_stateless(const Account& a) {
+    if (a.reserved != 0) return CA_RESERVED_FIELD;
+    if (a.flags & AF_PADDING) return CA_RESERVED_FLAG;
+    if (a.id == 0) return CA_ID_MUST_NOT_BE_ZERO;
+    if (a.id == TB_U128_MAX) return CA_ID_MUST_NOT_BE_INT_MAX;
+    if ((a.flags & AF_DEBITS_MUST_NOT_EXCEED_CREDITS) && (a.flags & AF_CREDITS_MUST_NOT_EXCEED_DEBITS)) {
+        return CA_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    }
+    if (a.debits_pending != 0) return CA_DEBITS_PENDING_MUST_BE_ZERO;
+    if (a.debits_posted != 0) return CA_DEBITS_POSTED_MUST_BE_ZERO;
+    if (a.credits_pending != 0) return CA_CREDITS_PENDING_MUST_BE_ZERO;
+    if (a.credits_posted != 0) return CA_CREDITS_POSTED_MUST_BE_ZERO;
+    if (a.ledger == 0) return CA_LEDGER_MUST_NOT_BE_ZERO;
+    if (a.code == 0) return CA_CODE_MUST_NOT_BE_ZERO;
+    return R_OK;
+}
+
+// Kernel 1 (create_accounts).
+__global__ __launch_bounds__(VALIDATE_THREADS) void tb_accounts_validate(PassArgs P) {
+    __shared__ __attribute__((aligned(16))) u8 stage[VALIDATE_THREADS * STAGE_STRIDE];
+    const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
+    const u32 count = min((u32)VALIDATE_THREADS, P.n - tile0);
+    tb_stage_events(P.events + (P.e0 + tile0) * 128, count, stage);
+    if (threadIdx.x >= count) return;
+
+    const u32 pe = tile0 + threadIdx.x;
+    const Account a = tb_read_staged<Account>(stage);
+    const u64 e = P.e0 + pe;
+    const u32 b = tb_batch_of(P, e);
+    const u32 L = (u32)(P.batch_off[b + 1] - P.batch_off[b]);
+    const u32 j = (u32)(e - P.batch_off[b]);
+    u32 code, hz = 0;
+    u64 kid = 0;
+    if ((a.flags & AF_LINKED) && j == L - 1) {
+        code = R_LINKED_EVENT_CHAIN_OPEN;
+    } else if (a.timestamp != 0) {
+        code = R_TIMESTAMP_MUST_BE_ZERO;
+    } else {
+        code = tb_account_stateless(a);
+        if (code == R_OK) {
+            hz |= HZ_KEYS;
+            kid = tb_dedup_key(tb_lo(a.id), tb_hi(a.id));
+            tb_dedup_insert(P.dedup, P.dedup_mask, kid);
+            const u32 slot = tb_account_find(P.T, tb_lo(a.id), tb_hi(a.id));
+            if (slot != TB_NOT_FOUND) code = tb_account_exists(a, P.T.accounts[slot]);
+        }
+    }
+    P.info[pe] = code | hz | ((u32)a.flags << 16);
+    P.kid[pe] = kid;
+    P.kpid[pe] = 0;
+}

@@ -1,0 +1,126 @@
+// pass.h — one device pass = N consecutive prepares (batches) of one create operation.
+//
+// Kernels of a pass (all on the engine stream, no host synchronisation between them):
+//   1. tb_{transfers,accounts}_validate  one event per lane: stateless checks in the reference's
+//      code order, hash probes of the HBM tables, the event's intrinsic result, hazard bits,
+//      dedup-set inserts, balancing marks and the overflow-certificate sum S.
+//   2. tb_resolve<op>                     one workgroup per prepare: dependence classification,
+//      linked-chain resolution, in-place apply of independent ok events, sparse replies.
+//   3. tb_replay<op>                      one workgroup: the ordered fallback — replays the
+//      dependent events in batch order with the reference logic and an undo log, then writes
+//      the replies of the prepares that had dependent events.
+#pragma once
+
+#include "tb_device.h"
+
+// info word per event: [7:0] result code, [15:8] hazard bits, [31:16] event flags.
+enum : u32 {
+    HZ_KEYS = 1u << 8,       // inserted dedup keys (kid/kpid) — check for collisions
+    HZ_LIMIT = 1u << 9,      // touches an account with a limit flag (tigerbeetle.zig:31-39)
+    HZ_BAL = 1u << 10,       // balancing_debit / balancing_credit event
+    HZ_ACCTS = 1u << 11,     // dr/cr slots valid (marks + certificate apply)
+    HZ_POSTVOID = 1u << 12,  // post_pending_transfer / void_pending_transfer
+    HZ_DEP = 1u << 13,       // dependent: resolved by the ordered replay
+    HZ_EVAL_OK = 1u << 14,   // returned ok when evaluated (feeds commit_timestamp)
+};
+
+#define SUM_SHARDS 64
+#define VALIDATE_THREADS 256
+#define RESOLVE_THREADS 1024
+#define REPLAY_THREADS 256
+#define BATCH_EVENTS_MAX 8191
+#define BATCH_LDS 8192
+
+struct PassArgs {
+    u8 op;
+    u32 epoch;             // pass number (never 0): balancing marks
+    u32 b0, b1;            // batches [b0, b1) of the call
+    u64 e0;                // first event of the pass (call-relative)
+    u32 n;                 // events in the pass
+    const u64* batch_off;  // [nb_call + 1] call-relative event offsets
+    const u64* batch_ts;   // [nb_call] prepare timestamps
+    const u8* events;      // call events (128 B each)
+    u32* results;          // call reply area: batch k at results + 2*batch_off[k]
+    u32* reply_bytes;      // [nb_call]
+    // scratch, pass-relative
+    u32* info;
+    u32* dr;
+    u32* cr;
+    u32* ps;
+    u64* amt;              // 2 words per event
+    u64* kid;
+    u64* kpid;
+    u32* dep_list;         // pass-relative: batch k's dependent events at dep_list + (off[k]-e0)
+    u32* dep_count;        // per batch (call-relative index - b0)
+    u64* dedup;
+    u64 dedup_mask;
+    u64* sum_shards;       // [SUM_SHARDS][2]
+    Tables T;
+};
+
+// Batch of a call-relative event index (binary search over batch_off[b0..b1]).
+__device__ static inline u32 tb_batch_of(const PassArgs& P, u64 e) {
+    u32 lo = P.b0, hi = P.b1;  // invariant: off[lo] <= e < off[hi]
+    while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if (P.batch_off[mid] <= e) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// Stage VALIDATE_THREADS 128-byte events through LDS with 16-byte coalesced loads; row stride
+// 144 B so the per-lane ds_read_b128 of one record is bank-conflict free.
+#define STAGE_STRIDE 144
+__device__ static inline void tb_stage_events(const u8* src, u32 count, u8* lds) {
+    const u32 t = threadIdx.x;
+#pragma unroll
+    for (u32 r = 0; r < 8; r++) {
+        const u32 c = t + r * VALIDATE_THREADS;  // 16-byte chunk index within the tile
+        const u32 ev = c >> 3, part = c & 7;
+        if (ev < count) {
+            const uint4 v = *(const uint4*)(src + (u64)c * 16);
+            *(uint4*)(lds + ev * STAGE_STRIDE + part * 16) = v;
+        }
+    }
+    __syncthreads();
+}
+
+template <typename R>
+__device__ static inline R tb_read_staged(const u8* lds) {
+    R r;
+    const u8* p = lds + threadIdx.x * STAGE_STRIDE;
+#pragma unroll
+    for (int k = 0; k < 8; k++) ((uint4*)&r)[k] = *(const uint4*)(p + k * 16);
+    return r;
+}
+
+// Wave-level sum of a u128 (64 lanes).
+__device__ static inline u128 tb_wave_sum_u128(u128 v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const u64 lo = __shfl_xor((unsigned long long)tb_lo(v), off);
+        const u64 hi = __shfl_xor((unsigned long long)tb_hi(v), off);
+        v = tb_sat_add(v, tb_u128(lo, hi));
+    }
+    return v;
+}
+
+// Add a block's partial S into one of SUM_SHARDS shards (no single hot word).  A partial at or
+// above 2^100 sets the HUGE word instead, which keeps every shard total below 2^124 (at most 2^24
+// blocks per pass) so the mod-2^128 shard atomics never wrap.
+#define SUM_WORDS (2 * SUM_SHARDS + 2)
+__device__ static inline void tb_sum_publish(const PassArgs& P, u128 block_sum) {
+    if (block_sum == 0) return;
+    if (tb_hi(block_sum) >> 36) {
+        atomicOr((unsigned long long*)&P.sum_shards[2 * SUM_SHARDS], 1ULL);
+        return;
+    }
+    tb_atomic_add_u128(P.sum_shards + 2 * (blockIdx.x % SUM_SHARDS), block_sum);
+}
+
+__device__ static inline u128 tb_sum_total(const u64* shards) {
+    if (shards[2 * SUM_SHARDS]) return TB_U128_MAX;
+    u128 s = 0;
+    for (int i = 0; i < SUM_SHARDS; i++) s = tb_sat_add(s, tb_u128(shards[2 * i], shards[2 * i + 1]));
+    return s;
+}

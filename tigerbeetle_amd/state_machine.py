@@ -1,0 +1,230 @@
+"""Host-side mirror of the reference's StateMachine plugin interface, backed by the MI355X engine.
+
+The reference's replica drives a comptime duck-typed `StateMachineType`
+(src/state_machine.zig:28-1150; the contract is listed in SURVEY.md §8b):
+
+    init(allocator, grid, options) / deinit / reset
+    prepare(operation, input)                    -> prepare_timestamp += len(events)   (:336-343)
+    prefetch(callback, op, operation, input)     -> async staging of objects          (:345-506)
+    commit(client, op, timestamp, operation, input, output) -> reply bytes             (:508-540)
+    compact(callback, op) / checkpoint(callback)                                        (:542-582)
+    fields prepare_timestamp, commit_timestamp
+
+`StateMachine` below keeps that shape; `commit` crosses into HIP through the C ABI
+(include/tbgpu.h).  Objects live in HBM, so `prefetch` completes immediately (its callback fires
+synchronously, which the reference allows: src/lsm/groove.zig:723-742), and `compact` /
+`checkpoint` have nothing to persist (durability is out of scope this round).
+"""
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .types import ACCOUNT_DTYPE, BATCH_MAX, TRANSFER_DTYPE, U64_MAX, Operation
+
+
+@dataclass
+class Options:
+    """StateMachine.Options (state_machine.zig:216-221) plus the HBM sizing the engine needs."""
+    accounts_max: int = 1 << 16
+    transfers_max: int = 1 << 20
+    pass_events_max: int = 8190 * 64
+    pass_batches_max: int = 512
+    device: int = 0
+    profile: bool = False
+    # Reference cache options are accepted for interface parity; the HBM tables hold every object.
+    lsm_forest_node_count: int = 0
+    cache_entries_accounts: int = 0
+    cache_entries_transfers: int = 0
+    cache_entries_posted: int = 0
+
+
+class Engine:
+    """Thin ctypes handle over one tbgpu engine (one GPU)."""
+
+    def __init__(self, options=None, **kw):
+        options = options or Options(**kw)
+        self.options = options
+        self.lib = _lib.load()
+        cfg = _lib.tbgpu_config(options.accounts_max, options.transfers_max, options.pass_events_max,
+                                options.pass_batches_max, options.device,
+                                _lib.CONFIG_PROFILE if options.profile else 0)
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.tbgpu_init(ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.tbgpu_deinit(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self):
+        _lib.check(self.lib.tbgpu_reset(self.h))
+
+    # -- commit ------------------------------------------------------------------------------
+    def commit(self, operation, timestamp, body):
+        """StateMachine.commit: returns the reply body bytes."""
+        body = bytes(body)
+        op = int(operation)
+        if op in (Operation.lookup_accounts, Operation.lookup_transfers):
+            cap = max(len(body) // 16 * 128, 128)
+        else:
+            cap = max(len(body) // 128 * 8, 8)
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_uint32(0)
+        src = ctypes.create_string_buffer(body, len(body)) if body else None
+        _lib.check(self.lib.tbgpu_commit(self.h, op, timestamp, src, len(body), out, cap, ctypes.byref(n)))
+        return out.raw[:n.value]
+
+    def commit_many(self, operation, timestamps, bodies):
+        """N prepares in one device pass; returns the N reply bodies."""
+        n = len(bodies)
+        if n == 0:
+            return []
+        bufs = [ctypes.create_string_buffer(bytes(b), len(b)) if len(b) else None for b in bodies]
+        outs = [ctypes.create_string_buffer(max(len(b) // 128 * 8, 8)) for b in bodies]
+        ts = (ctypes.c_uint64 * n)(*timestamps)
+        ins = (ctypes.c_void_p * n)(*[ctypes.cast(b, ctypes.c_void_p) if b is not None else None for b in bufs])
+        lens = (ctypes.c_uint32 * n)(*[len(b) for b in bodies])
+        outp = (ctypes.c_void_p * n)(*[ctypes.cast(o, ctypes.c_void_p) for o in outs])
+        out_lens = (ctypes.c_uint32 * n)()
+        _lib.check(self.lib.tbgpu_commit_many(self.h, int(operation), n, ts, ins, lens, outp, out_lens))
+        return [outs[k].raw[:out_lens[k]] for k in range(n)]
+
+    def commit_device_async(self, operation, timestamps, lens, events_dev, results_dev, reply_bytes_dev):
+        n = len(lens)
+        ts = (ctypes.c_uint64 * n)(*[int(t) for t in timestamps])
+        ls = (ctypes.c_uint32 * n)(*[int(x) for x in lens])
+        _lib.check(self.lib.tbgpu_commit_device_async(self.h, int(operation), n, ts, ls, events_dev, results_dev,
+                                                      reply_bytes_dev))
+
+    def sync(self):
+        _lib.check(self.lib.tbgpu_sync(self.h))
+
+    @property
+    def commit_timestamp(self):
+        return self.lib.tbgpu_commit_timestamp(self.h)
+
+    def set_balances(self, account_id, dp, dpost, cp, cpost):
+        arr = (ctypes.c_uint64 * 8)()
+        for i, v in enumerate((dp, dpost, cp, cpost)):
+            arr[2 * i] = v & U64_MAX
+            arr[2 * i + 1] = v >> 64
+        _lib.check(self.lib.tbgpu_test_set_balances(self.h, account_id & U64_MAX, account_id >> 64, arr))
+
+    # -- parity read-back --------------------------------------------------------------------
+    def _export(self, fn, dtype, cap):
+        out = np.zeros(max(cap, 1), dtype=dtype)
+        n = ctypes.c_uint64(0)
+        _lib.check(fn(self.h, out.ctypes.data, cap, ctypes.byref(n)))
+        return out[:n.value]
+
+    def export_accounts(self, cap=None):
+        return self._export(self.lib.tbgpu_export_accounts, ACCOUNT_DTYPE, cap or self.options.accounts_max)
+
+    def export_transfers(self, cap=None):
+        return self._export(self.lib.tbgpu_export_transfers, TRANSFER_DTYPE, cap or self.options.transfers_max)
+
+    def export_posted(self, cap=None):
+        cap = cap or self.options.transfers_max
+        out = np.zeros((max(cap, 1), 2), dtype=np.uint64)
+        n = ctypes.c_uint64(0)
+        _lib.check(self.lib.tbgpu_export_posted(self.h, out.ctypes.data, cap, ctypes.byref(n)))
+        return out[:n.value]
+
+    def stats(self):
+        s = _lib.tbgpu_stats()
+        _lib.check(self.lib.tbgpu_get_stats(self.h, ctypes.byref(s)))
+        return {f: getattr(s, f) for f, _ in s._fields_}
+
+    def reset_stats(self):
+        self.lib.tbgpu_reset_stats(self.h)
+
+    # -- device memory + workload generation (bench) -----------------------------------------
+    def alloc(self, nbytes):
+        p = ctypes.c_void_p()
+        _lib.check(self.lib.tbgpu_device_alloc(self.h, nbytes, ctypes.byref(p)))
+        return p.value
+
+    def free(self, ptr):
+        _lib.check(self.lib.tbgpu_device_free(self.h, ptr))
+
+    def to_host(self, ptr, nbytes):
+        out = np.empty(nbytes, dtype=np.uint8)
+        _lib.check(self.lib.tbgpu_copy_to_host(self.h, out.ctypes.data, ptr, nbytes))
+        return out
+
+    def to_device(self, ptr, array):
+        array = np.ascontiguousarray(array)
+        _lib.check(self.lib.tbgpu_copy_to_device(self.h, ptr, array.ctypes.data, array.nbytes))
+
+    def generate_accounts(self, out_dev, first, count, seed=42, limit_permille=0):
+        w = _lib.tbgpu_workload(seed, 0, 0, limit_permille)
+        _lib.check(self.lib.tbgpu_bench_generate_accounts(self.h, out_dev, first, count, ctypes.byref(w)))
+
+    def generate_transfers(self, out_dev, first, count, account_count, seed=42, kind=0):
+        w = _lib.tbgpu_workload(seed, account_count, kind, 0)
+        _lib.check(self.lib.tbgpu_bench_generate_transfers(self.h, out_dev, first, count, ctypes.byref(w)))
+
+    def marker(self, slot):
+        _lib.check(self.lib.tbgpu_marker(self.h, slot))
+
+    def marker_elapsed_ms(self, a, b):
+        return self.lib.tbgpu_marker_elapsed_ms(self.h, a, b)
+
+
+class StateMachine:
+    """The reference's StateMachine interface over one Engine."""
+
+    Operation = Operation
+    batch_max = BATCH_MAX
+
+    def __init__(self, options=None, **kw):
+        self.engine = Engine(options, **kw)
+        self.prepare_timestamp = 0
+        self.commit_timestamp = 0
+
+    def deinit(self):
+        self.engine.close()
+
+    def reset(self):
+        self.engine.reset()
+        self.prepare_timestamp = 0
+        self.commit_timestamp = 0
+
+    @staticmethod
+    def event_count(operation, body):
+        if operation in (Operation.create_accounts, Operation.create_transfers):
+            return len(body) // 128
+        return 0
+
+    def prepare(self, operation, body):
+        """state_machine.zig:336-343."""
+        self.prepare_timestamp += self.event_count(Operation(operation), body)
+
+    def prefetch(self, callback, op, operation, body):
+        """state_machine.zig:345-506.  Every object is HBM-resident: complete synchronously."""
+        assert op != 0
+        callback(self)
+
+    def commit(self, client, op, timestamp, operation, body):
+        """state_machine.zig:508-540.  Returns the reply body (bytes)."""
+        del client
+        assert op != 0
+        reply = self.engine.commit(int(operation), timestamp, body)
+        self.commit_timestamp = self.engine.commit_timestamp
+        return reply
+
+    def compact(self, callback, op):
+        del op
+        callback(self)
+
+    def checkpoint(self, callback):
+        callback(self)
