@@ -1,0 +1,308 @@
+"""Headline benchmark: committed create_transfers per second, bit-exact, on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): 1M accounts, 100M uniform-random transfers (dr != cr,
+no flags), prepares of 8190 events, synthetic data generated on the GPU (tigerbeetle_amd
+k_workload.h, shapes of the reference benchmark client src/benchmark.zig:223-327).
+
+A step = committing all 100M transfers (12,211 prepares) from the post-account-creation state,
+inputs already resident in HBM.  Between steps the transfer store and balances are restored
+(untimed), so every step commits the same 100M transfers.  Each timed step is bracketed by a
+barrier + torch.cuda.synchronize(); value = transfers committed by all ranks / Σ step time (max
+over ranks).
+
+--gpus N (torchrun): one process per GPU; each rank commits its own shard (its own accounts and
+transfers, no cross-shard transfer), so scaling is weak.  The cross-shard all-to-all path of
+BASELINE config C5 is not built yet.
+
+The JSON line also carries:
+  roofline      the dominant kernel's algorithmic bytes per launch / its average launch time
+                (HIP events on the engine stream, inside the timed steps) against 8 TB/s;
+                `traffic` comes from profiles/pmc_<round>.json (rocprofv3 PMC) when present.
+  cpu_baseline  the C oracle (reference semantics restated, single thread) timed on this host on
+                a bounded prefix of the same workload.
+  parity        the same prefix committed on the GPU from a fresh state and compared with the
+                oracle byte for byte (replies, every account, every transfer); for the full run,
+                every reply empty, no dependent event, debits == credits in total.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "transfers/sec committed (whole node, bit-exact results) + p99 batch latency"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--accounts", type=int, default=1_000_000)
+    p.add_argument("--transfers", type=int, default=100_000_000)
+    p.add_argument("--batch", type=int, default=8190)
+    p.add_argument("--pass-batches", type=int, default=512)
+    p.add_argument("--cpu-sample", type=int, default=12_285_000, help="transfers in the CPU baseline / parity sample (0: skip)")
+    p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--profile", type=int, default=1, help="time kernels with HIP events (roofline)")
+    return p.parse_args()
+
+
+def batches(total, batch):
+    q, r = divmod(total, batch)
+    return [batch] * q + ([r] if r else [])
+
+
+def timestamps(lens, start):
+    """Prepare timestamps: t_k = t_{k-1} + 1 + len_k (state_machine.zig:1483-1485)."""
+    ts, t = [], start
+    for L in lens:
+        t += 1 + L
+        ts.append(t)
+    return ts, t
+
+
+def expected_unique(accounts, legs):
+    """Expected number of distinct accounts touched by `legs` uniform draws."""
+    return accounts * (1.0 - math.exp(-legs / accounts))
+
+
+def run_cpu_baseline(engine, args, acct_lens, acct_ts, events_dev, sample_lens, sample_ts):
+    """Oracle (single thread) on the sample; returns (result dict, oracle engine, replies)."""
+    from tests.harness.oracle import OracleEngine
+
+    n_acct = args.accounts
+    acct_dev = engine.alloc(n_acct * 128)
+    engine.generate_accounts(acct_dev, 0, n_acct, seed=args.seed)
+    acct_events = engine.to_host(acct_dev, n_acct * 128)
+    engine.free(acct_dev)
+    n_sample = sum(sample_lens)
+    events = engine.to_host(events_dev, n_sample * 128)
+
+    oracle = OracleEngine(n_acct, n_sample)
+    off = 0
+    for L, ts in zip(acct_lens, acct_ts):
+        r = oracle.commit(128, ts, acct_events[off * 128:(off + L) * 128].tobytes())
+        assert r == b"", "account creation failed on the oracle"
+        off += L
+    replies = []
+    off = 0
+    lat = []
+    t0 = time.perf_counter()
+    for L, ts in zip(sample_lens, sample_ts):
+        b0 = time.perf_counter()
+        replies.append(oracle.commit(129, ts, events[off * 128:(off + L) * 128].tobytes()))
+        lat.append(time.perf_counter() - b0)
+        off += L
+    dt = time.perf_counter() - t0
+    lat = np.array(lat) * 1e3
+    return {
+        "value": n_sample / dt,
+        "unit": "transfers/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": "first %d transfers (%d prepares of %d) of the same workload; C oracle oracle/tb_oracle.c "
+                  "(reference semantics restated, in-memory hash-map grooves, no LSM/WAL/network), one thread, "
+                  "%s" % (n_sample, len(sample_lens), args.batch, cpu_model()),
+        "p99_batch_latency_ms": float(np.percentile(lat, 99)),
+        "seconds": dt,
+    }, oracle, replies
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return "host CPU: %s, nproc %d" % (line.split(":", 1)[1].strip(), os.cpu_count())
+    except OSError:
+        pass
+    return "nproc %d" % os.cpu_count()
+
+
+def load_pmc(kernel):
+    """HBM traffic per launch of `kernel` from a committed rocprofv3 PMC summary, if any."""
+    prof_dir = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(prof_dir):
+        return None
+    for name in sorted(os.listdir(prof_dir), reverse=True):
+        if name.startswith("pmc_") and name.endswith(".json"):
+            try:
+                d = json.load(open(os.path.join(prof_dir, name)))
+            except (OSError, ValueError):
+                continue
+            k = d.get("kernels", {}).get(kernel)
+            if k and "hbm_bytes_per_launch" in k:
+                return k["hbm_bytes_per_launch"]
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def allmax(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    from tigerbeetle_amd.state_machine import Engine, Options
+
+    pass_events = args.pass_batches * args.batch
+    engine = Engine(Options(accounts_max=args.accounts, transfers_max=args.transfers, pass_events_max=pass_events,
+                            pass_batches_max=args.pass_batches, device=local_rank, profile=bool(args.profile)))
+    seed = args.seed + 1000003 * rank  # each rank: its own ledger shard
+
+    # -- accounts (create_accounts through the engine) --------------------------------------
+    acct_lens = batches(args.accounts, args.batch)
+    acct_ts, t_end = timestamps(acct_lens, 1_000_000_000)
+    acct_dev = engine.alloc(args.accounts * 128)
+    engine.generate_accounts(acct_dev, 0, args.accounts, seed=seed)
+    res_dev = engine.alloc(max(args.accounts, args.transfers) * 8)
+    rb_dev = engine.alloc(max(len(acct_lens), args.transfers // args.batch + 2) * 4)
+    engine.commit_device_async(128, acct_ts, acct_lens, acct_dev, res_dev, rb_dev)
+    engine.sync()
+    rb = engine.to_host(rb_dev, len(acct_lens) * 4).view(np.uint32)
+    assert rb.sum() == 0, "account creation returned errors"
+    engine.free(acct_dev)
+
+    # -- transfers (synthetic, resident in HBM) ----------------------------------------------
+    xfer_lens = batches(args.transfers, args.batch)
+    events_dev = engine.alloc(args.transfers * 128)
+    engine.generate_transfers(events_dev, 0, args.transfers, args.accounts, seed=seed)
+    engine.sync()
+
+    step_ms = []
+    t_cursor = t_end
+    for step in range(args.warmup + args.steps):
+        timed = step >= args.warmup
+        engine.reset_transfers()
+        ts, t_cursor = timestamps(xfer_lens, t_cursor + 10)
+        if timed and step == args.warmup:
+            engine.reset_stats()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        engine.commit_device_async(129, ts, xfer_lens, events_dev, res_dev, rb_dev)
+        engine.sync()
+        torch.cuda.synchronize()
+        barrier()
+        dt = time.perf_counter() - t0
+        if timed:
+            step_ms.append(allmax(dt * 1e3))
+    stats = engine.stats()
+    pass_lat = engine.pass_latencies()
+
+    # -- full-run checks (size-independent properties) ---------------------------------------
+    rb = engine.to_host(rb_dev, len(xfer_lens) * 4).view(np.uint32)
+    accts = engine.export_accounts()
+    dpost = sum(int(x) for x in accts["debits_posted_lo"]) + (sum(int(x) for x in accts["debits_posted_hi"]) << 64)
+    cpost = sum(int(x) for x in accts["credits_posted_lo"]) + (sum(int(x) for x in accts["credits_posted_hi"]) << 64)
+    full_ok = bool(rb.sum() == 0 and stats["transfers"] == args.transfers and dpost == cpost and dpost > 0
+                   and len(accts) == args.accounts)
+
+    total_ms = sum(step_ms)
+    n_total = args.transfers * world * args.steps
+    value = n_total / (total_ms / 1e3)
+
+    # -- roofline: dominant kernel -----------------------------------------------------------
+    kernels = {
+        "tb_transfers_validate": (stats["ms_validate"], stats["launches_validate"]),
+        "tb_resolve": (stats["ms_resolve"], stats["launches_resolve"]),
+        "tb_replay": (stats["ms_replay"], stats["launches_replay"]),
+    }
+    dom = max(kernels, key=lambda k: kernels[k][0])
+    ms_dom, n_dom = kernels[dom]
+    per_pass = pass_events
+    u_over_t = expected_unique(args.accounts, 2 * per_pass) / per_pass
+    # B = 296 + 256·U/T per transfer; validate's share reads the event (128),
+    # probes the id (16) and reads each touched account once (128·U/T); resolve's share writes the
+    # record (128), the result slot (8), the id (16) and writes each touched account back (128·U/T).
+    b_validate = 144 + 128 * u_over_t
+    b_resolve = 152 + 128 * u_over_t
+    per_launch_transfers = args.transfers / max(1, stats["launches_validate"] / max(1, args.steps))
+    alg_bytes = {"tb_transfers_validate": b_validate, "tb_resolve": b_resolve, "tb_replay": 0.0}[dom] * per_launch_transfers
+    roof = None
+    if n_dom:
+        avg_s = ms_dom / n_dom / 1e3
+        achieved = alg_bytes / avg_s / 1e9
+        traffic = load_pmc(dom)
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
+                "avg_launch_ms": round(ms_dom / n_dom, 4), "alg_bytes_per_transfer": round(alg_bytes / per_launch_transfers, 1),
+                "path_bytes_per_transfer": round(296 + 256 * u_over_t, 1),
+                "path_achieved_GBs": round((296 + 256 * u_over_t) * args.transfers * args.steps / (total_ms / 1e3) / 1e9, 1)}
+
+    # -- CPU baseline + bit-exact sample parity (rank 0, N=1 only) ---------------------------
+    cpu = None
+    parity = {"full_run_properties": full_ok}
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        sample_lens = batches(min(args.cpu_sample, args.transfers), args.batch)
+        sample_ts, t_cursor = timestamps(sample_lens, t_cursor + 10)
+        cpu, oracle, expected = run_cpu_baseline(engine, args, acct_lens, acct_ts, events_dev, sample_lens, sample_ts)
+        engine.reset_transfers()
+        engine.commit_device_async(129, sample_ts, sample_lens, events_dev, res_dev, rb_dev)
+        engine.sync()
+        rb = engine.to_host(rb_dev, len(sample_lens) * 4).view(np.uint32)
+        replies_equal = all(e == b"" for e in expected) and int(rb.sum()) == 0
+        acc_equal = engine.export_accounts().tobytes() == oracle.export_accounts().tobytes()
+        xfer_equal = engine.export_transfers(cap=sum(sample_lens)).tobytes() == oracle.export_transfers().tobytes()
+        parity.update({"sample_transfers": sum(sample_lens), "replies_equal": replies_equal,
+                       "accounts_equal": acc_equal, "transfers_equal": xfer_equal})
+        cpu.pop("seconds")
+
+    lat = np.array(pass_lat) if len(pass_lat) else np.array([float("nan")])
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "transfers/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(total_ms / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u128",
+        "data": "synthetic (device-generated, reference benchmark shapes)",
+        "config": {"workload": "C2 (BASELINE.json configs[1]): %d accounts, %d uniform transfers/GPU, no flags, "
+                               "prepares of %d" % (args.accounts, args.transfers, args.batch),
+                   "prepares_per_step": len(xfer_lens), "pass_prepares": args.pass_batches,
+                   "parallelism": "shard%d" % world if world > 1 else "single"},
+        "p99_batch_latency_ms": round(float(np.percentile(lat, 99)), 3),
+        "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3), "p100": round(float(lat.max()), 3),
+                             "definition": "device time of the pass that answers the prepare (%d prepares/pass)" % args.pass_batches},
+        "dependent_events": stats["dependent_events"],
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "parity": parity,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    engine.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

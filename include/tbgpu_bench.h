@@ -27,6 +27,13 @@ int tbgpu_bench_generate_accounts(tbgpu_t* engine, void* out_dev, uint64_t first
 int tbgpu_bench_generate_transfers(tbgpu_t* engine, void* out_dev, uint64_t first, uint64_t count,
                                    const tbgpu_workload* w);
 
+/* Restore the post-account-creation state between bench steps: empty the transfer store and the
+ * posted groove, zero every account balance.  Accounts and commit_timestamp are kept. */
+int tbgpu_bench_reset_transfers(tbgpu_t* engine);
+/* Device duration (ms) of every pass since the last tbgpu_reset_stats (TBGPU_CONFIG_PROFILE):
+ * a prepare's reply is available when its pass completes, so this is the batch latency. */
+int tbgpu_bench_pass_latencies(tbgpu_t* engine, double* out_ms, uint64_t cap, uint64_t* count);
+
 /* Device memory helpers for callers without a device allocator (ctypes users). */
 int tbgpu_device_alloc(tbgpu_t* engine, uint64_t bytes, void** out);
 int tbgpu_device_free(tbgpu_t* engine, void* ptr);

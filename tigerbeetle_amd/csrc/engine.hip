@@ -45,7 +45,7 @@ static u64 pow2_at_least(u64 v) {
     return c;
 }
 
-enum { K_VALIDATE = 0, K_RESOLVE = 1, K_REPLAY = 2, K_CLEAR = 3, K_COUNT = 4 };
+enum { K_VALIDATE = 0, K_RESOLVE = 1, K_REPLAY = 2, K_CLEAR = 3, K_PASS = 4, K_COUNT = 5 };
 
 struct ProfilePair {
     int kind;
@@ -97,6 +97,7 @@ struct tbgpu {
     double prof_ms[K_COUNT] = {};
     u64 prof_n[K_COUNT] = {};
     u64 passes = 0, events = 0;
+    std::vector<double> pass_ms;  // device duration of every profiled pass (batch latency)
 
     hipEvent_t markers[16] = {};
 };
@@ -135,6 +136,7 @@ static int prof_collect(tbgpu* E) {
         HIPCK(hipEventElapsedTime(&ms, p.a, p.b));
         E->prof_ms[p.kind] += ms;
         E->prof_n[p.kind] += 1;
+        if (p.kind == K_PASS) E->pass_ms.push_back(ms);
     }
     E->prof.clear();
     E->event_next = 0;
@@ -329,9 +331,11 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.sum_shards = E->sum_shards;
         P.T = E->T;
 
-        ProfilePair pp;
-        int st = prof_begin(E, &pp, K_CLEAR);
+        ProfilePair pass_pp;
+        int st = prof_begin(E, &pass_pp, K_PASS);
         if (st) return st;
+        ProfilePair pp;
+        if ((st = prof_begin(E, &pp, K_CLEAR))) return st;
         HIPCK(hipMemsetAsync(E->dedup, 0, (P.dedup_mask + 1) * 8, E->stream));
         HIPCK(hipMemsetAsync(E->sum_shards, 0, SUM_WORDS * 8, E->stream));
         if ((st = prof_end(E, &pp))) return st;
@@ -365,6 +369,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         }
         HIPCK(hipGetLastError());
         if ((st = prof_end(E, &pp))) return st;
+        if ((st = prof_end(E, &pass_pp))) return st;
         E->passes++;
         E->events += n;
         b0 = b1;
@@ -674,6 +679,8 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     s->passes = E->passes;
     s->events = E->events;
     s->dependent_events = g.dependent_all;
+    s->accounts = g.account_count;
+    s->transfers = g.transfer_count;
     s->ms_validate = E->prof_ms[K_VALIDATE];
     s->ms_resolve = E->prof_ms[K_RESOLVE];
     s->ms_replay = E->prof_ms[K_REPLAY];
@@ -692,6 +699,7 @@ extern "C" void tbgpu_reset_stats(tbgpu_t* E) {
     }
     E->passes = 0;
     E->events = 0;
+    E->pass_ms.clear();
 }
 
 extern "C" const char* tbgpu_last_error(void) { return g_err.c_str(); }
@@ -755,6 +763,32 @@ extern "C" int tbgpu_copy_to_device(tbgpu_t* E, void* dst_dev, const void* src, 
     HIPCK(hipSetDevice(E->device));
     HIPCK(hipStreamSynchronize(E->stream));
     HIPCK(hipMemcpy(dst_dev, src, bytes, hipMemcpyHostToDevice));
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_bench_reset_transfers(tbgpu_t* E) {
+    HIPCK(hipSetDevice(E->device));
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    HIPCK(hipMemsetAsync(E->T.transfers, 0, E->transfer_cap * sizeof(Transfer), E->stream));
+    HIPCK(hipMemsetAsync(E->T.posted, 0, E->transfer_cap, E->stream));
+    hipLaunchKernelGGL(tb_zero_balances, dim3((unsigned)((E->account_cap + 255) / 256)), dim3(256), 0, E->stream, E->T,
+                       E->account_cap);
+    HIPCK(hipGetLastError());
+    HIPCK(hipStreamSynchronize(E->stream));
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_bench_pass_latencies(tbgpu_t* E, double* out_ms, uint64_t cap, uint64_t* count) {
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    const u64 n = std::min<u64>(cap, E->pass_ms.size());
+    for (u64 i = 0; i < n; i++) out_ms[i] = E->pass_ms[i];
+    *count = n;
     return TBGPU_STATUS_OK;
 }
 

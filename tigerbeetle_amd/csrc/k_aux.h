@@ -67,3 +67,21 @@ __global__ void tb_set_balances(Tables T, u64 lo, u64 hi, u64 dp_lo, u64 dp_hi, 
     T.g->bound_hi = tb_hi(bound);
     *status = 0;
 }
+
+// Bench reset between steps: zero every live account's balances, drop the transfer count and the
+// balance bound (the transfer table itself is cleared with a memset).
+__global__ void tb_zero_balances(Tables T, u64 cap) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        T.g->transfer_count = 0;
+        T.g->bound_lo = 0;
+        T.g->bound_hi = 0;
+    }
+    if (i >= cap) return;
+    Account* a = &T.accounts[i];
+    if (a->timestamp == 0) return;
+    a->debits_pending = 0;
+    a->debits_posted = 0;
+    a->credits_pending = 0;
+    a->credits_posted = 0;
+}

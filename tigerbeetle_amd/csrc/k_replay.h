@@ -55,6 +55,7 @@ __device__ static inline void rp_scope_close(Replay& R, bool persist) {
                 u64* w = (u64*)&R.T.accounts[e.slot].id;
                 w[0] = 0;
                 w[1] = 0;
+                R.T.g->account_count--;
                 break;
             }
             case UNDO_ACCOUNT_UPDATE: R.T.accounts[e.slot] = e.before; break;
@@ -62,6 +63,7 @@ __device__ static inline void rp_scope_close(Replay& R, bool persist) {
                 u64* w = (u64*)&R.T.transfers[e.slot].id;
                 w[0] = 0;
                 w[1] = 0;
+                R.T.g->transfer_count--;
                 break;
             }
             case UNDO_POSTED: R.T.posted[e.slot] = POSTED_NONE; break;
@@ -91,6 +93,7 @@ __device__ static inline u32 rp_transfer_insert(Replay& R, const Transfer& t) {
         return slot;
     }
     R.T.transfers[slot] = t;
+    R.T.g->transfer_count++;
     rp_push(R, UNDO_TRANSFER_INSERT, slot, nullptr);
     return slot;
 }
@@ -292,6 +295,7 @@ __device__ static inline u32 rp_create_account(Replay& R, const Account& a) {
         return R_OK;
     }
     R.T.accounts[slot] = a;
+    R.T.g->account_count++;
     rp_push(R, UNDO_ACCOUNT_INSERT, slot, nullptr);
     return R_OK;
 }

@@ -139,6 +139,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     __shared__ u32 s_key[BATCH_LDS]; // per segment start: min over members (0 = dependent member)
     __shared__ u32 s_wave[RESOLVE_THREADS / 64];
     __shared__ u64 s_tsmax[RESOLVE_THREADS / 64];
+    __shared__ u32 s_applied;
 
     const Tables& T = P.T;
     const u32 b = P.b0 + blockIdx.x;
@@ -155,6 +156,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         cert_global = !tb_add_overflows(tb_u128(T.g->bound_lo, T.g->bound_hi), S, &r);
     }
 
+    if (threadIdx.x == 0) s_applied = 0;
     // a. classify
     bool local_linked = false;
     for (u32 i = threadIdx.x; i < L; i += RESOLVE_THREADS) {
@@ -264,6 +266,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                 if (fin == R_OK) {
                     if (OP == OP_CREATE_TRANSFERS) tb_apply_transfer(P, pe, info, ts);
                     else tb_apply_account(P, pe, ts);
+                    atomicAdd(&s_applied, 1u);
                 }
             } else {
                 P.info[pbase + i] |= HZ_DEP;
@@ -285,6 +288,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         u64 mm = 0;
         for (u32 k = 0; k < RESOLVE_THREADS / 64; k++) mm = max(mm, s_tsmax[k]);
         if (mm) atomicMax((unsigned long long*)&T.g->commit_timestamp, (unsigned long long)mm);
+        if (s_applied) {
+            atomicAdd((unsigned long long*)(OP == OP_CREATE_TRANSFERS ? &T.g->transfer_count : &T.g->account_count),
+                      (unsigned long long)s_applied);
+        }
         P.dep_count[blockIdx.x] = ndep;
         if (ndep) atomicAdd((unsigned long long*)&T.g->dependent_total, (unsigned long long)ndep);
     }

@@ -173,6 +173,15 @@ class Engine:
         w = _lib.tbgpu_workload(seed, account_count, kind, 0)
         _lib.check(self.lib.tbgpu_bench_generate_transfers(self.h, out_dev, first, count, ctypes.byref(w)))
 
+    def reset_transfers(self):
+        _lib.check(self.lib.tbgpu_bench_reset_transfers(self.h))
+
+    def pass_latencies(self, cap=1 << 20):
+        out = np.zeros(cap, dtype=np.float64)
+        n = ctypes.c_uint64(0)
+        _lib.check(self.lib.tbgpu_bench_pass_latencies(self.h, out.ctypes.data, cap, ctypes.byref(n)))
+        return out[:n.value]
+
     def marker(self, slot):
         _lib.check(self.lib.tbgpu_marker(self.h, slot))
 
