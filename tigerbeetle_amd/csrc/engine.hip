@@ -63,7 +63,7 @@ struct tbgpu {
 
     // Pass scratch.
     u32 pe_max = 0, pb_max = 0;
-    u32 *info = nullptr, *dr = nullptr, *cr = nullptr, *ps = nullptr;
+    u32 *info = nullptr, *dr = nullptr, *cr = nullptr, *ps = nullptr, *rs = nullptr;
     u32 *dep_list = nullptr, *dep_count = nullptr;
     u64 *amt = nullptr, *kid = nullptr, *kpid = nullptr;
     u64* dedup = nullptr;
@@ -226,6 +226,7 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     INIT_CK(hipMalloc(&E->dr, pe * 4));
     INIT_CK(hipMalloc(&E->cr, pe * 4));
     INIT_CK(hipMalloc(&E->ps, pe * 4));
+    INIT_CK(hipMalloc(&E->rs, pe * 4));
     INIT_CK(hipMalloc(&E->dep_list, pe * 4));
     INIT_CK(hipMalloc(&E->dep_count, (u64)E->pb_max * 4));
     INIT_CK(hipMalloc(&E->amt, pe * 16));
@@ -259,7 +260,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
     (void)hipSetDevice(E->device);
     if (E->stream) (void)hipStreamSynchronize(E->stream);
     void* bufs[] = {E->T.accounts, E->T.account_mark, E->T.transfers, E->T.posted, E->g, E->info, E->dr,
-                    E->cr, E->ps, E->dep_list, E->dep_count, E->amt, E->kid, E->kpid, E->dedup,
+                    E->cr, E->ps, E->rs, E->dep_list, E->dep_count, E->amt, E->kid, E->kpid, E->dedup,
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
                     E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status};
     for (void* p : bufs) if (p) (void)hipFree(p);
@@ -321,6 +322,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.dr = E->dr;
         P.cr = E->cr;
         P.ps = E->ps;
+        P.rs = E->rs;
         P.amt = E->amt;
         P.kid = E->kid;
         P.kpid = E->kpid;

@@ -32,7 +32,7 @@ __global__ void tb_export(Tables T, u64 cap_slots, u8* out, u64* count, u64* pos
     const u8* rec = ACCOUNTS ? (const u8*)&T.accounts[i] : (const u8*)&T.transfers[i];
     const u64 ts = *(const u64*)(rec + 120);
     const u64* idw = (const u64*)rec;
-    if (ts == 0 || (idw[0] == 0 && idw[1] == 0)) return;
+    if (ts == 0 || (idw[0] == 0 && idw[1] == 0) || (idw[0] == ~0ULL && idw[1] == ~0ULL)) return;
     const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
     uint4* dst = (uint4*)(out + k * 128);
 #pragma unroll

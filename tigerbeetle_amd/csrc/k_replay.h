@@ -51,18 +51,14 @@ __device__ static inline void rp_scope_close(Replay& R, bool persist) {
         while (R.undo_len > 0) {
             const UndoEntry& e = R.undo[--R.undo_len];
             switch (e.kind) {
-            case UNDO_ACCOUNT_INSERT: {  // tombstone: id = 0, timestamp kept
-                u64* w = (u64*)&R.T.accounts[e.slot].id;
-                w[0] = 0;
-                w[1] = 0;
+            case UNDO_ACCOUNT_INSERT: {  // tombstone (id = maxInt), timestamp kept
+                tb_tombstone(&R.T.accounts[e.slot]);
                 R.T.g->account_count--;
                 break;
             }
             case UNDO_ACCOUNT_UPDATE: R.T.accounts[e.slot] = e.before; break;
             case UNDO_TRANSFER_INSERT: {
-                u64* w = (u64*)&R.T.transfers[e.slot].id;
-                w[0] = 0;
-                w[1] = 0;
+                tb_tombstone(&R.T.transfers[e.slot]);
                 R.T.g->transfer_count--;
                 break;
             }

@@ -69,55 +69,36 @@ __device__ static inline void tb_write_replies(const PassArgs& P, u32 b, u32 L, 
     if (threadIdx.x == 0) P.reply_bytes[b] = running * 8;
 }
 
-// Apply one independent ok transfer (create_transfer :866-882, post_or_void :971-1012).
-__device__ static inline void tb_apply_transfer(const PassArgs& P, u32 pe, u32 info, u64 ts) {
+// Apply the balance effects of one independent ok transfer whose record kernel 1 already inserted
+// (create_transfer :870-880, post_or_void :987-1010).  With the 64-bit certificate (no balance
+// can reach 2^64 this pass) the adds are fire-and-forget low-word atomics.
+__device__ static inline void tb_apply_transfer(const PassArgs& P, u32 pe, u32 info, bool cert64) {
     const Tables& T = P.T;
-    const Transfer* ev = (const Transfer*)(P.events + (P.e0 + pe) * 128);
-    Transfer t = *ev;
-    t.timestamp = ts;
-    const Account* dr = &T.accounts[P.dr[pe]];
-    const Account* cr = &T.accounts[P.cr[pe]];
+    u8* dr = (u8*)&T.accounts[P.dr[pe]];
+    u8* cr = (u8*)&T.accounts[P.cr[pe]];
     const u128 amount = tb_u128(P.amt[2 * pe], P.amt[2 * pe + 1]);
+    const u16 flags = (u16)(info >> 16);
     if (info & HZ_POSTVOID) {
         const u32 pslot = P.ps[pe];
-        const Transfer& p = T.transfers[pslot];
-        Transfer r;
-        r.id = t.id;
-        r.debit_account_id = p.debit_account_id;
-        r.credit_account_id = p.credit_account_id;
-        r.amount = (t.flags & TF_POST) ? amount : (t.amount > 0 ? t.amount : p.amount);
-        r.pending_id = t.pending_id;
-        r.user_data_128 = t.user_data_128 > 0 ? t.user_data_128 : p.user_data_128;
-        r.user_data_64 = t.user_data_64 > 0 ? t.user_data_64 : p.user_data_64;
-        r.user_data_32 = t.user_data_32 > 0 ? t.user_data_32 : p.user_data_32;
-        r.timeout = 0;
-        r.ledger = p.ledger;
-        r.code = p.code;
-        r.flags = t.flags;
-        r.timestamp = ts;
-        const u128 neg = (u128)0 - p.amount;
-        const u32 slot = tb_transfer_claim(T, tb_lo(r.id), tb_hi(r.id), ts);
-        if (slot == TB_NOT_FOUND) return;
-        T.transfers[slot] = r;
-        T.posted[pslot] = (t.flags & TF_POST) ? POSTED_POSTED : POSTED_VOIDED;
-        tb_atomic_add_u128((u8*)dr + ACCOUNT_OFF_DEBITS_PENDING, neg);
-        tb_atomic_add_u128((u8*)cr + ACCOUNT_OFF_CREDITS_PENDING, neg);
-        if (t.flags & TF_POST) {
-            tb_atomic_add_u128((u8*)dr + ACCOUNT_OFF_DEBITS_POSTED, amount);
-            tb_atomic_add_u128((u8*)cr + ACCOUNT_OFF_CREDITS_POSTED, amount);
+        const u128 pamount = T.transfers[pslot].amount;
+        T.posted[pslot] = (flags & TF_POST) ? POSTED_POSTED : POSTED_VOIDED;
+        const u128 neg = (u128)0 - pamount;  // dp -= p.amount (mod 2^128, exact in aggregate)
+        tb_atomic_add_u128(dr + ACCOUNT_OFF_DEBITS_PENDING, neg);
+        tb_atomic_add_u128(cr + ACCOUNT_OFF_CREDITS_PENDING, neg);
+        if (flags & TF_POST) {
+            tb_atomic_add_u128(dr + ACCOUNT_OFF_DEBITS_POSTED, amount);
+            tb_atomic_add_u128(cr + ACCOUNT_OFF_CREDITS_POSTED, amount);
         }
+        return;
+    }
+    const u32 off_d = (flags & TF_PENDING) ? ACCOUNT_OFF_DEBITS_PENDING : ACCOUNT_OFF_DEBITS_POSTED;
+    const u32 off_c = (flags & TF_PENDING) ? ACCOUNT_OFF_CREDITS_PENDING : ACCOUNT_OFF_CREDITS_POSTED;
+    if (cert64) {
+        tb_atomic_add_lo_noret(dr + off_d, tb_lo(amount));
+        tb_atomic_add_lo_noret(cr + off_c, tb_lo(amount));
     } else {
-        t.amount = amount;
-        const u32 slot = tb_transfer_claim(T, tb_lo(t.id), tb_hi(t.id), ts);
-        if (slot == TB_NOT_FOUND) return;
-        T.transfers[slot] = t;
-        if (t.flags & TF_PENDING) {
-            tb_atomic_add_u128((u8*)dr + ACCOUNT_OFF_DEBITS_PENDING, amount);
-            tb_atomic_add_u128((u8*)cr + ACCOUNT_OFF_CREDITS_PENDING, amount);
-        } else {
-            tb_atomic_add_u128((u8*)dr + ACCOUNT_OFF_DEBITS_POSTED, amount);
-            tb_atomic_add_u128((u8*)cr + ACCOUNT_OFF_CREDITS_POSTED, amount);
-        }
+        tb_atomic_add_u128(dr + off_d, amount);
+        tb_atomic_add_u128(cr + off_c, amount);
     }
 }
 
@@ -149,11 +130,15 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     const u64 ts0 = P.batch_ts[b] - L + 1;  // timestamp of event 0 (:645)
 
     u128 S = 0;
-    bool cert_global = true;
+    bool cert_global = true, cert64 = true;
+    bool any_dup = true, any_bal = true;
     if (OP == OP_CREATE_TRANSFERS) {
         S = tb_sum_total(P.sum_shards);
         u128 r;
         cert_global = !tb_add_overflows(tb_u128(T.g->bound_lo, T.g->bound_hi), S, &r);
+        cert64 = cert_global && tb_hi(r) == 0;
+        any_dup = P.sum_shards[PW_DUP] != 0;
+        any_bal = P.sum_shards[PW_BAL] != 0;
     }
 
     if (threadIdx.x == 0) s_applied = 0;
@@ -164,8 +149,9 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         const u32 info = P.info[pe];
         const u32 code = info & 0xFF;
         bool dep = false;
-        if ((info & HZ_KEYS) && (tb_dedup_is_dup(P.dedup, P.dedup_mask, P.kid[pe]) ||
-                                 (P.kpid[pe] && tb_dedup_is_dup(P.dedup, P.dedup_mask, P.kpid[pe])))) {
+        if (any_dup && (info & HZ_KEYS) &&
+            (tb_dedup_is_dup(P.dedup, P.dedup_mask, P.kid[pe]) ||
+             (P.kpid[pe] && tb_dedup_is_dup(P.dedup, P.dedup_mask, P.kpid[pe])))) {
             dep = true;
         }
         if (OP == OP_CREATE_TRANSFERS && !dep && (info & HZ_ACCTS) &&
@@ -173,7 +159,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
             const u32 drs = P.dr[pe], crs = P.cr[pe];
             if (code == R_OK) {
                 if (info & (HZ_BAL | HZ_LIMIT)) dep = true;
-                else if (T.account_mark[drs] == P.epoch || T.account_mark[crs] == P.epoch) dep = true;
+                else if (any_bal && (T.account_mark[drs] == P.epoch || T.account_mark[crs] == P.epoch)) dep = true;
             }
             if (!dep && !cert_global &&
                 (tb_account_cert_fails(&T.accounts[drs], S) || tb_account_cert_fails(&T.accounts[crs], S))) {
@@ -255,21 +241,26 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
             } else {
                 eval_ok = code == R_OK;
             }
+            const u32 pe = pbase + i;
+            const u32 info = P.info[pe];
             if (!dep) {
                 if (fin == TB_CODE_PANIC) tb_panic(T.g, PANIC_ASSERT);
                 s_code[i] = (u8)fin;
-                const u32 pe = pbase + i;
-                const u32 info = P.info[pe];
                 P.info[pe] = (info & 0xFFFFFF00u) | fin | (eval_ok ? HZ_EVAL_OK : 0);
                 const u64 ts = ts0 + i;
                 if (eval_ok) tsmax = ts;  // increasing in i
                 if (fin == R_OK) {
-                    if (OP == OP_CREATE_TRANSFERS) tb_apply_transfer(P, pe, info, ts);
+                    if (OP == OP_CREATE_TRANSFERS) tb_apply_transfer(P, pe, info, cert64);
                     else tb_apply_account(P, pe, ts);
                     atomicAdd(&s_applied, 1u);
                 }
             } else {
-                P.info[pbase + i] |= HZ_DEP;
+                P.info[pe] = info | HZ_DEP;
+            }
+            // Withdraw a speculative record whose event did not commit here (failed, rolled back,
+            // or left to the ordered replay, which inserts it itself in order).
+            if (OP == OP_CREATE_TRANSFERS && (info & HZ_SPEC) && (dep || fin != R_OK)) {
+                tb_tombstone(&T.transfers[P.rs[pe]]);
             }
         }
         u32 total;

@@ -12,7 +12,7 @@
 
 struct TransferScratch {
     u32 hz = 0;
-    u32 dr = TB_NOT_FOUND, cr = TB_NOT_FOUND, ps = TB_NOT_FOUND;
+    u32 dr = TB_NOT_FOUND, cr = TB_NOT_FOUND, ps = TB_NOT_FOUND, rs = TB_NOT_FOUND;
     u128 amount = 0;       // amount applied by an independent ok event (post: posted amount)
     u128 contrib = 0;      // contribution to S (overflow certificate)
     u64 kid = 0, kpid = 0;
@@ -59,6 +59,14 @@ __device__ static inline u32 tb_post_void_exists(const Transfer& t, const Transf
     return CT_EXISTS;
 }
 
+__device__ static inline void tb_spec_insert(const PassArgs& P, const Transfer& r, TransferScratch& s) {
+    const u32 slot = tb_transfer_claim(P.T, tb_lo(r.id), tb_hi(r.id), r.timestamp);
+    if (slot == TB_NOT_FOUND) return;
+    P.T.transfers[slot] = r;
+    s.rs = slot;
+    s.hz |= HZ_SPEC;
+}
+
 __device__ static inline u32 tb_validate_post_void(const PassArgs& P, const Transfer& t, u64 ts,
                                                    TransferScratch& s) {
     const Tables& T = P.T;
@@ -76,8 +84,9 @@ __device__ static inline u32 tb_validate_post_void(const PassArgs& P, const Tran
     s.hz |= HZ_POSTVOID | HZ_KEYS;
     s.kid = tb_dedup_key(tb_lo(t.id), tb_hi(t.id));
     s.kpid = tb_dedup_key(tb_lo(t.pending_id), tb_hi(t.pending_id));
-    tb_dedup_insert(P.dedup, P.dedup_mask, s.kid);
-    tb_dedup_insert(P.dedup, P.dedup_mask, s.kpid);
+    const bool c1 = tb_dedup_insert(P.dedup, P.dedup_mask, s.kid);
+    const bool c2 = tb_dedup_insert(P.dedup, P.dedup_mask, s.kpid);
+    if (c1 || c2) P.sum_shards[PW_DUP] = 1;
 
     const u32 pslot = tb_transfer_find(T, tb_lo(t.pending_id), tb_hi(t.pending_id));
     if (pslot == TB_NOT_FOUND) return CT_PENDING_TRANSFER_NOT_FOUND;
@@ -123,6 +132,24 @@ __device__ static inline u32 tb_validate_post_void(const PassArgs& P, const Tran
     if ((T.accounts[drs].flags | T.accounts[crs].flags) & AF_LIMITS) s.hz |= HZ_LIMIT;
     s.amount = (f & TF_POST) ? amount : 0;
     // A post moves <= p.amount from pending to posted: dp + dpost never grows, so no S term.
+
+    // Speculative insert of the composed record (:971-985); kernel 2 withdraws it (tombstone) if
+    // the event ends up failing or dependent.
+    Transfer r;
+    r.id = t.id;
+    r.debit_account_id = p.debit_account_id;
+    r.credit_account_id = p.credit_account_id;
+    r.amount = amount;
+    r.pending_id = t.pending_id;
+    r.user_data_128 = t.user_data_128 > 0 ? t.user_data_128 : p.user_data_128;
+    r.user_data_64 = t.user_data_64 > 0 ? t.user_data_64 : p.user_data_64;
+    r.user_data_32 = t.user_data_32 > 0 ? t.user_data_32 : p.user_data_32;
+    r.timeout = 0;
+    r.ledger = p.ledger;
+    r.code = p.code;
+    r.flags = t.flags;
+    r.timestamp = ts;
+    tb_spec_insert(P, r, s);
     return R_OK;
 }
 
@@ -166,7 +193,7 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     // From here the result reads the state of `id`.
     s.hz |= HZ_KEYS;
     s.kid = tb_dedup_key(tb_lo(t.id), tb_hi(t.id));
-    tb_dedup_insert(P.dedup, P.dedup_mask, s.kid);
+    if (tb_dedup_insert(P.dedup, P.dedup_mask, s.kid)) P.sum_shards[PW_DUP] = 1;
     const u32 es = tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id));
     if (es != TB_NOT_FOUND) return tb_transfer_exists(t, T.transfers[es]);
 
@@ -180,6 +207,7 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
         s.hz |= HZ_BAL;
         if (f & TF_BAL_DEBIT) P.T.account_mark[drs] = P.epoch;
         if (f & TF_BAL_CREDIT) P.T.account_mark[crs] = P.epoch;
+        P.sum_shards[PW_BAL] = 1;
         s.contrib = t.amount == 0 ? (u128)UINT64_MAX : t.amount;
         return R_OK;
     }
@@ -189,6 +217,9 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     // then the timeout check (:862) is the next possible failure.
     const u64 timeout_ns = (u64)t.timeout * 1000000000ULL;
     if (ts + timeout_ns < ts) return CT_OVERFLOWS_TIMEOUT;
+    Transfer r = t;
+    r.timestamp = ts;
+    tb_spec_insert(P, r, s);
     return R_OK;
 }
 
@@ -222,6 +253,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
         P.dr[pe] = s.dr;
         P.cr[pe] = s.cr;
         P.ps[pe] = s.ps;
+        P.rs[pe] = s.rs;
         P.amt[2 * pe] = tb_lo(s.amount);
         P.amt[2 * pe + 1] = tb_hi(s.amount);
         P.kid[pe] = s.kid;

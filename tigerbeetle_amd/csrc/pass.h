@@ -22,6 +22,7 @@ enum : u32 {
     HZ_POSTVOID = 1u << 12,  // post_pending_transfer / void_pending_transfer
     HZ_DEP = 1u << 13,       // dependent: resolved by the ordered replay
     HZ_EVAL_OK = 1u << 14,   // returned ok when evaluated (feeds commit_timestamp)
+    HZ_SPEC = 1u << 15,      // record speculatively inserted at rs[] by kernel 1
 };
 
 #define SUM_SHARDS 64
@@ -47,6 +48,7 @@ struct PassArgs {
     u32* dr;
     u32* cr;
     u32* ps;
+    u32* rs;               // slot of the speculatively inserted transfer record
     u64* amt;              // 2 words per event
     u64* kid;
     u64* kpid;
@@ -108,18 +110,23 @@ __device__ static inline u128 tb_wave_sum_u128(u128 v) {
 // Add a block's partial S into one of SUM_SHARDS shards (no single hot word).  A partial at or
 // above 2^100 sets the HUGE word instead, which keeps every shard total below 2^124 (at most 2^24
 // blocks per pass) so the mod-2^128 shard atomics never wrap.
-#define SUM_WORDS (2 * SUM_SHARDS + 2)
+// Pass words after the shards: HUGE (S >= 2^100 somewhere), DUP (a dedup collision happened),
+// BAL (a tentatively-ok balancing event exists).  Written with idempotent stores.
+#define PW_HUGE (2 * SUM_SHARDS)
+#define PW_DUP (2 * SUM_SHARDS + 1)
+#define PW_BAL (2 * SUM_SHARDS + 2)
+#define SUM_WORDS (2 * SUM_SHARDS + 4)
 __device__ static inline void tb_sum_publish(const PassArgs& P, u128 block_sum) {
     if (block_sum == 0) return;
     if (tb_hi(block_sum) >> 36) {
-        atomicOr((unsigned long long*)&P.sum_shards[2 * SUM_SHARDS], 1ULL);
+        atomicOr((unsigned long long*)&P.sum_shards[PW_HUGE], 1ULL);
         return;
     }
     tb_atomic_add_u128(P.sum_shards + 2 * (blockIdx.x % SUM_SHARDS), block_sum);
 }
 
 __device__ static inline u128 tb_sum_total(const u64* shards) {
-    if (shards[2 * SUM_SHARDS]) return TB_U128_MAX;
+    if (shards[PW_HUGE]) return TB_U128_MAX;
     u128 s = 0;
     for (int i = 0; i < SUM_SHARDS; i++) s = tb_sat_add(s, tb_u128(shards[2 * i], shards[2 * i + 1]));
     return s;

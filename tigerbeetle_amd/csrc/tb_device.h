@@ -162,18 +162,22 @@ __device__ static inline u128 tb_sat_add(u128 a, u128 b) {
 // Engine state in HBM.
 //
 // Both object tables are open-addressing hash tables whose slots ARE the 128-byte records
-// (record-in-table): one probe line carries id, ledger, flags and balances, so resolving an
-// account costs one HBM line instead of an index line plus a record line.
-//   * empty slot:     timestamp == 0 (event timestamps are always >= 1)
-//   * claimed/live:   timestamp != 0; the id words are written after the claim
-//   * tombstone:      timestamp != 0 and id == 0 (a rolled-back linked-chain insert; ids are
-//                     never 0 for live objects, id_must_not_be_zero)
-// Slots are claimed with a 64-bit CAS on the timestamp word; tombstones are never reclaimed.
+// (record-in-table): a hit costs one HBM line, and a transfer probe reads only the first 64-byte
+// sector (the id).
+//   * empty slot:  id == 0 (ids are never 0 for live objects: id_must_not_be_zero)
+//   * live slot:   id != 0, id != maxInt; timestamp != 0
+//   * tombstone:   id == maxInt(u128) (never a live id: id_must_not_be_int_max) — a rolled-back or
+//                  withdrawn insert; probes continue past it, it is never reclaimed
+// Inserts claim an empty slot with a 64-bit CAS of the timestamp word (0 -> ts) and then write the
+// record; a slot claimed in the current kernel may still read id == 0 to a concurrent prober, which
+// can only be a prober of an id that is absent from the pre-kernel table (a claimed slot was empty,
+// so it never lies on the probe path of an older key) — every such pair of events collides in the
+// pass dedup set and is resolved by the ordered replay.
 // ------------------------------------------------------------------------------------------------
 struct Globals {
     u64 commit_timestamp;     // max timestamp of an event that returned ok when evaluated
     u64 panic;                // PANIC_* bits
-    u64 sum_lo, sum_hi;       // S: Σ potential balance increments of this pass (overflow certificate)
+    u64 sum_lo, sum_hi;       // (unused)
     u64 bound_lo, bound_hi;   // upper bound of dp+dpost and cp+cpost over every account
     u64 dependent_total;      // dependent events of this pass
     u64 dependent_all;        // cumulative
@@ -197,31 +201,36 @@ __device__ static inline void tb_panic(Globals* g, u32 code) {
     atomicOr((unsigned long long*)&g->panic, (unsigned long long)code);
 }
 
-// Probe for a live account.  Returns the slot or TB_NOT_FOUND.
-__device__ static inline u32 tb_account_find(const Tables& T, u64 lo, u64 hi) {
-    u64 pos = tb_hash_id(lo, hi) & T.account_mask;
-    for (u64 n = 0; n <= T.account_mask; n++) {
-        const Account* a = &T.accounts[pos];
-        const u64 ts = a->timestamp;
-        if (ts == 0) return TB_NOT_FOUND;
-        const u64* idw = (const u64*)&a->id;
-        if (idw[0] == lo && idw[1] == hi) return (u32)pos;
-        pos = (pos + 1) & T.account_mask;
+// Probe a record-in-table for a live id.  Returns the slot or TB_NOT_FOUND.
+template <typename R>
+__device__ static inline u32 tb_find(const R* table, u64 mask, u64 lo, u64 hi) {
+    // 0 marks an empty slot and maxInt a tombstone: neither is ever a live id.
+    if ((lo | hi) == 0 || (lo & hi) == ~0ULL) return TB_NOT_FOUND;
+    u64 pos = tb_hash_id(lo, hi) & mask;
+    for (u64 n = 0; n <= mask; n++) {
+        const u64* idw = (const u64*)&table[pos];
+        const u64 a = idw[0], b = idw[1];
+        if (a == lo && b == hi) return (u32)pos;
+        if ((a | b) == 0) return TB_NOT_FOUND;
+        pos = (pos + 1) & mask;
     }
     return TB_NOT_FOUND;
 }
 
+__device__ static inline u32 tb_account_find(const Tables& T, u64 lo, u64 hi) {
+    return tb_find(T.accounts, T.account_mask, lo, hi);
+}
+
 __device__ static inline u32 tb_transfer_find(const Tables& T, u64 lo, u64 hi) {
-    u64 pos = tb_hash_id(lo, hi) & T.transfer_mask;
-    for (u64 n = 0; n <= T.transfer_mask; n++) {
-        const Transfer* t = &T.transfers[pos];
-        const u64 ts = t->timestamp;
-        if (ts == 0) return TB_NOT_FOUND;
-        const u64* idw = (const u64*)&t->id;
-        if (idw[0] == lo && idw[1] == hi) return (u32)pos;
-        pos = (pos + 1) & T.transfer_mask;
-    }
-    return TB_NOT_FOUND;
+    return tb_find(T.transfers, T.transfer_mask, lo, hi);
+}
+
+// Tombstone a slot (id = maxInt), keeping its timestamp so it is never reclaimed.
+template <typename R>
+__device__ static inline void tb_tombstone(R* rec) {
+    u64* w = (u64*)rec;
+    w[0] = ~0ULL;
+    w[1] = ~0ULL;
 }
 
 // Claim an empty slot for a key that is known to be absent; CAS the timestamp word 0 -> ts.
@@ -262,6 +271,13 @@ __device__ static inline void tb_atomic_add_u128(void* field, u128 v) {
     if (hi + carry != 0) atomicAdd(&w[1], (unsigned long long)(hi + carry));
 }
 
+// Fire-and-forget add to the low word only: valid when no low word can carry this pass (the
+// 64-bit certificate: bound + S < 2^64, so every balance stays below 2^64).
+__device__ static inline void tb_atomic_add_lo_noret(void* field, u64 v) {
+    __hip_atomic_fetch_add((unsigned long long*)field, (unsigned long long)v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ------------------------------------------------------------------------------------------------
 // Per-pass dedup set of 63-bit id fingerprints: collisions between the ids / pending ids of two
 // events of one pass mark both events dependent (ordered fallback).  0 = empty, bit 63 = DUP.
@@ -275,20 +291,22 @@ __device__ static inline u64 tb_dedup_key(u64 lo, u64 hi) {
     return (h >> 1) | 1;  // nonzero, bit 63 clear
 }
 
-__device__ static inline void tb_dedup_insert(u64* table, u64 mask, u64 key) {
+// Returns true when the key was already present (a collision: both events become dependent).
+__device__ static inline bool tb_dedup_insert(u64* table, u64 mask, u64 key) {
     u64 pos = tb_mix64(key) & mask;
     for (u64 n = 0; n <= mask; n++) {
         u64 cur = *(volatile u64*)&table[pos];
         if (cur == 0) {
             cur = atomicCAS((unsigned long long*)&table[pos], 0ULL, (unsigned long long)key);
-            if (cur == 0) return;
+            if (cur == 0) return false;
         }
         if ((cur & ~DEDUP_DUP) == key) {
             if (!(cur & DEDUP_DUP)) atomicOr((unsigned long long*)&table[pos], (unsigned long long)DEDUP_DUP);
-            return;
+            return true;
         }
         pos = (pos + 1) & mask;
     }
+    return true;
 }
 
 __device__ static inline bool tb_dedup_is_dup(const u64* table, u64 mask, u64 key) {
