@@ -23,7 +23,7 @@ def gpu_engine_factory():
     made = []
 
     def make(**kw):
-        opts = dict(accounts_max=4096, transfers_max=1 << 15, pass_events_max=8192 * 4, pass_batches_max=64)
+        opts = dict(accounts_max=4096, transfers_max=1 << 17, pass_events_max=8192 * 4, pass_batches_max=64)
         opts.update(kw)
         e = Engine(Options(**opts))
         made.append(e)

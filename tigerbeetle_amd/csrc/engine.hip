@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -59,10 +60,12 @@ struct tbgpu {
 
     Tables T{};
     Globals* g = nullptr;
-    u64 account_cap = 0, transfer_cap = 0;
+    u64 account_cap = 0, xidx_cap = 0, xlog_cap = 0;
+    u64 log_next = 0;  // next free transfer-log position (host-owned)
 
     // Pass scratch.
     u32 pe_max = 0, pb_max = 0;
+    u16* eflags = nullptr;
     u32 *info = nullptr, *dr = nullptr, *cr = nullptr, *ps = nullptr, *rs = nullptr;
     u32 *dep_list = nullptr, *dep_count = nullptr;
     u64 *amt = nullptr, *kid = nullptr, *kpid = nullptr;
@@ -91,6 +94,7 @@ struct tbgpu {
     bool pending = false;    // an async call was enqueued and not yet synced
 
     bool profile = false;
+    u32 ablate = 0;
     std::vector<hipEvent_t> event_pool;
     size_t event_next = 0;
     std::vector<ProfilePair> prof;
@@ -146,10 +150,13 @@ static int prof_collect(tbgpu* E) {
 // ------------------------------------------------------------------------------------------------
 
 static int engine_clear(tbgpu* E) {
-    HIPCK(hipMemsetAsync(E->T.accounts, 0, E->account_cap * sizeof(Account), E->stream));
+    HIPCK(hipMemsetAsync(E->T.acct_hot, 0, E->account_cap * sizeof(AccountHot), E->stream));
+    HIPCK(hipMemsetAsync(E->T.acct_bal, 0, E->account_cap * sizeof(AccountBal), E->stream));
+    HIPCK(hipMemsetAsync(E->T.acct_cold, 0, E->account_cap * sizeof(AccountCold), E->stream));
     HIPCK(hipMemsetAsync(E->T.account_mark, 0, E->account_cap * sizeof(u32), E->stream));
-    HIPCK(hipMemsetAsync(E->T.transfers, 0, E->transfer_cap * sizeof(Transfer), E->stream));
-    HIPCK(hipMemsetAsync(E->T.posted, 0, E->transfer_cap, E->stream));
+    HIPCK(hipMemsetAsync(E->T.xidx, 0, E->xidx_cap * sizeof(XIndex), E->stream));
+    HIPCK(hipMemsetAsync(E->T.xposted, 0, E->xlog_cap, E->stream));
+    E->log_next = 0;
     HIPCK(hipMemsetAsync(E->g, 0, sizeof(Globals), E->stream));
     HIPCK(hipStreamSynchronize(E->stream));
     E->epoch = 0;
@@ -179,6 +186,7 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     E->cfg = *config;
     E->device = config->device;
     E->profile = (config->flags & TBGPU_CONFIG_PROFILE) != 0;
+    if (const char* ab = getenv("TBGPU_ABLATE")) E->ablate = (u32)strtoul(ab, nullptr, 0);  // timing experiments only
     int st = TBGPU_STATUS_OK;
 #define INIT_CK(x)                                                                                 \
     do {                                                                                           \
@@ -193,7 +201,9 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     INIT_CK(hipStreamCreateWithFlags(&E->stream, hipStreamNonBlocking));
 
     E->account_cap = pow2_at_least(std::max<u64>(2 * config->accounts_max, 1024));
-    E->transfer_cap = pow2_at_least(std::max<u64>(2 * config->transfers_max, 1024));
+    // The index is sized for 2x the log so tombstones of withdrawn speculative inserts leave room.
+    E->xlog_cap = std::max<u64>(config->transfers_max, 1024);
+    E->xidx_cap = pow2_at_least(std::max<u64>(2 * E->xlog_cap, 2048));
     E->pe_max = config->pass_events_max;
     E->pb_max = config->pass_batches_max;
     E->dedup_cap = pow2_at_least(std::max<u64>(4ULL * E->pe_max, 64));
@@ -203,7 +213,8 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
 
     size_t free_b = 0, total_b = 0;
     INIT_CK(hipMemGetInfo(&free_b, &total_b));
-    const u64 need = E->account_cap * (sizeof(Account) + 4) + E->transfer_cap * (sizeof(Transfer) + 1) +
+    const u64 need = E->account_cap * (sizeof(Account) + 4) + E->xlog_cap * (sizeof(Transfer) + 1) +
+                     E->xidx_cap * sizeof(XIndex) +
                      (u64)E->pe_max * (4 * 4 + 8 * 4 + 128 + 8 + 4) + E->dedup_cap * 8;
     if (need > free_b) {
         st = fail(TBGPU_STATUS_INVALID, "tbgpu_init: needs %llu bytes of HBM, %llu free",
@@ -212,17 +223,22 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         return st;
     }
 
-    INIT_CK(hipMalloc(&E->T.accounts, E->account_cap * sizeof(Account)));
+    INIT_CK(hipMalloc(&E->T.acct_hot, E->account_cap * sizeof(AccountHot)));
+    INIT_CK(hipMalloc(&E->T.acct_bal, E->account_cap * sizeof(AccountBal)));
+    INIT_CK(hipMalloc(&E->T.acct_cold, E->account_cap * sizeof(AccountCold)));
     INIT_CK(hipMalloc(&E->T.account_mark, E->account_cap * sizeof(u32)));
-    INIT_CK(hipMalloc(&E->T.transfers, E->transfer_cap * sizeof(Transfer)));
-    INIT_CK(hipMalloc(&E->T.posted, E->transfer_cap));
+    INIT_CK(hipMalloc(&E->T.xidx, E->xidx_cap * sizeof(XIndex)));
+    INIT_CK(hipMalloc(&E->T.xlog, E->xlog_cap * sizeof(Transfer)));
+    INIT_CK(hipMalloc(&E->T.xposted, E->xlog_cap));
     INIT_CK(hipMalloc(&E->g, sizeof(Globals)));
     E->T.account_mask = E->account_cap - 1;
-    E->T.transfer_mask = E->transfer_cap - 1;
+    E->T.xidx_mask = E->xidx_cap - 1;
+    E->T.xlog_cap = E->xlog_cap;
     E->T.g = E->g;
 
     const u64 pe = E->pe_max;
     INIT_CK(hipMalloc(&E->info, pe * 4));
+    INIT_CK(hipMalloc(&E->eflags, pe * 2));
     INIT_CK(hipMalloc(&E->dr, pe * 4));
     INIT_CK(hipMalloc(&E->cr, pe * 4));
     INIT_CK(hipMalloc(&E->ps, pe * 4));
@@ -259,7 +275,8 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
     if (!E) return;
     (void)hipSetDevice(E->device);
     if (E->stream) (void)hipStreamSynchronize(E->stream);
-    void* bufs[] = {E->T.accounts, E->T.account_mark, E->T.transfers, E->T.posted, E->g, E->info, E->dr,
+    void* bufs[] = {E->T.acct_hot, E->T.acct_bal, E->T.acct_cold, E->T.account_mark, E->T.xidx, E->T.xlog,
+                    E->T.xposted, E->g, E->info, E->eflags, E->dr,
                     E->cr, E->ps, E->rs, E->dep_list, E->dep_count, E->amt, E->kid, E->kpid, E->dedup,
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
                     E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status};
@@ -319,6 +336,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.results = results_dev;
         P.reply_bytes = reply_bytes_dev;
         P.info = E->info;
+        P.eflags = E->eflags;
         P.dr = E->dr;
         P.cr = E->cr;
         P.ps = E->ps;
@@ -331,7 +349,10 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.dedup = E->dedup;
         P.dedup_mask = std::min<u64>(pow2_at_least(std::max<u64>(4 * n, 64)), E->dedup_cap) - 1;
         P.sum_shards = E->sum_shards;
+        P.pass_words = E->sum_shards;
+        P.log_base = E->log_next;
         P.T = E->T;
+        P.ablate = E->ablate;
 
         ProfilePair pass_pp;
         int st = prof_begin(E, &pass_pp, K_PASS);
@@ -374,6 +395,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         if ((st = prof_end(E, &pass_pp))) return st;
         E->passes++;
         E->events += n;
+        if (op == OP_CREATE_TRANSFERS) E->log_next += n;
         b0 = b1;
     }
     return TBGPU_STATUS_OK;
@@ -410,6 +432,10 @@ static int prepare_call(tbgpu* E, u8 op, u32 nb, const u64* timestamps, const u3
         prev = ts;
         h_off[k + 1] = h_off[k] + L;
         h_ts[k] = ts;
+    }
+    if (op == OP_CREATE_TRANSFERS && E->log_next + h_off[nb] > E->xlog_cap) {
+        return fail(TBGPU_STATUS_INVALID, "transfer log full (%llu + %llu events > capacity %llu)",
+                    (unsigned long long)E->log_next, (unsigned long long)h_off[nb], (unsigned long long)E->xlog_cap);
     }
     HIPCK(hipMemcpyAsync(E->meta, E->h_meta, (2 * (u64)nb + 1) * 8, hipMemcpyHostToDevice, E->stream));
     E->last_batch_ts = prev;
@@ -570,14 +596,14 @@ static bool id_less(const u8* a, const u8* b) {
     return x[1] != y[1] ? x[1] < y[1] : x[0] < y[0];
 }
 
-// Export live records in chunks of slots (no large temporary), then sort by id.
+// Export live records in chunks (bounded temporaries), then sort by id.
 template <bool ACCOUNTS>
 static int export_records(tbgpu* E, std::vector<u8>& recs, std::vector<u64>* posted) {
     if (E->pending) {
         int st = engine_sync(E);
         if (st) return st;
     }
-    const u64 cap = ACCOUNTS ? E->account_cap : E->transfer_cap;
+    const u64 cap = ACCOUNTS ? E->account_cap : E->xidx_cap;
     const u64 chunk = std::min<u64>(cap, 1ULL << 20);
     u8* d_out = nullptr;
     u64* d_cnt = nullptr;
@@ -587,16 +613,16 @@ static int export_records(tbgpu* E, std::vector<u8>& recs, std::vector<u64>* pos
     HIPCK(hipMalloc(&d_posted, chunk * 16));
     int st = TBGPU_STATUS_OK;
     for (u64 s = 0; s < cap && st == TBGPU_STATUS_OK; s += chunk) {
-        Tables T = E->T;
-        if (ACCOUNTS) T.accounts += s;
-        else {
-            T.transfers += s;
-            T.posted += s;
-        }
+        const u64 n = std::min<u64>(chunk, cap - s);
         hipError_t e = hipMemsetAsync(d_cnt, 0, 16, E->stream);
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(tb_export<ACCOUNTS>, dim3((unsigned)((chunk + 255) / 256)), dim3(256), 0, E->stream, T,
-                               chunk, d_out, d_cnt, d_posted, d_cnt + 1);
+            if (ACCOUNTS) {
+                hipLaunchKernelGGL(tb_export_accounts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T,
+                                   s, s + n, d_out, d_cnt);
+            } else {
+                hipLaunchKernelGGL(tb_export_transfers, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T,
+                                   s, n, d_out, d_cnt, d_posted, d_cnt + 1);
+            }
             e = hipGetLastError();
         }
         u64 cnt[2] = {0, 0};
@@ -774,10 +800,11 @@ extern "C" int tbgpu_bench_reset_transfers(tbgpu_t* E) {
         int st = engine_sync(E);
         if (st) return st;
     }
-    HIPCK(hipMemsetAsync(E->T.transfers, 0, E->transfer_cap * sizeof(Transfer), E->stream));
-    HIPCK(hipMemsetAsync(E->T.posted, 0, E->transfer_cap, E->stream));
+    HIPCK(hipMemsetAsync(E->T.xidx, 0, E->xidx_cap * sizeof(XIndex), E->stream));
+    HIPCK(hipMemsetAsync(E->T.xposted, 0, E->xlog_cap, E->stream));
     hipLaunchKernelGGL(tb_zero_balances, dim3((unsigned)((E->account_cap + 255) / 256)), dim3(256), 0, E->stream, E->T,
                        E->account_cap);
+    E->log_next = 0;
     HIPCK(hipGetLastError());
     HIPCK(hipStreamSynchronize(E->stream));
     return TBGPU_STATUS_OK;

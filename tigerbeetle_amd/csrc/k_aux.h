@@ -11,36 +11,44 @@ __global__ void tb_lookup(Tables T, const u64* ids, u32 n, u8* out, u8* found) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u64 lo = ids[2 * i], hi = ids[2 * i + 1];
-    u32 slot;
-    if (ACCOUNTS) slot = tb_account_find(T, lo, hi);
-    else slot = tb_transfer_find(T, lo, hi);
-    found[i] = slot != TB_NOT_FOUND;
-    if (slot != TB_NOT_FOUND) {
-        const uint4* src = ACCOUNTS ? (const uint4*)&T.accounts[slot] : (const uint4*)&T.transfers[slot];
-        uint4* dst = (uint4*)(out + (u64)i * 128);
-#pragma unroll
-        for (int k = 0; k < 8; k++) dst[k] = src[k];
+    if (ACCOUNTS) {
+        const u32 slot = tb_account_find(T, lo, hi);
+        found[i] = slot != TB_NOT_FOUND;
+        if (slot != TB_NOT_FOUND) *(Account*)(out + (u64)i * 128) = tb_account_load(T, slot);
+    } else {
+        const u32 pos = tb_transfer_find(T, lo, hi);
+        found[i] = pos != TB_NOT_FOUND;
+        if (pos != TB_NOT_FOUND) *(Transfer*)(out + (u64)i * 128) = T.xlog[pos];
     }
 }
 
-// Compact every live record (timestamp != 0, id != 0) into out (order unspecified; the host
-// sorts by id).  For transfers, also emit the posted groove as {pending timestamp, fulfillment}.
-template <bool ACCOUNTS>
-__global__ void tb_export(Tables T, u64 cap_slots, u8* out, u64* count, u64* posted_out, u64* posted_count) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= cap_slots) return;
-    const u8* rec = ACCOUNTS ? (const u8*)&T.accounts[i] : (const u8*)&T.transfers[i];
-    const u64 ts = *(const u64*)(rec + 120);
-    const u64* idw = (const u64*)rec;
-    if (ts == 0 || (idw[0] == 0 && idw[1] == 0) || (idw[0] == ~0ULL && idw[1] == ~0ULL)) return;
+// Compact every live account (slots [0, cap)) into out; order unspecified (the host sorts by id).
+__global__ void tb_export_accounts(Tables T, u64 first, u64 cap, u8* out, u64* count) {
+    const u64 i = first + (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap) return;
+    const AccountHot& h = T.acct_hot[i];
+    if (h.timestamp == 0 || tb_id_reserved(h.id_lo, h.id_hi)) return;
     const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
-    uint4* dst = (uint4*)(out + k * 128);
-#pragma unroll
-    for (int w = 0; w < 8; w++) dst[w] = ((const uint4*)rec)[w];
-    if (!ACCOUNTS && T.posted[i] != POSTED_NONE) {
+    *(Account*)(out + k * 128) = tb_account_load(T, (u32)i);
+}
+
+// Compact every live transfer (index entries [first, first+n)); also the posted groove as
+// {pending timestamp, fulfillment} pairs.
+__global__ void tb_export_transfers(Tables T, u64 first, u64 n, u8* out, u64* count, u64* posted_out,
+                                    u64* posted_count) {
+    const u64 i = first + (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= first + n) return;
+    const XIndex e = T.xidx[i];
+    if (e.fp == 0 || (u32)e.word1 == 0 || (e.word1 & XI_TOMB)) return;
+    const u32 pos = tb_xi_pos(e.word1);
+    const Transfer& t = T.xlog[pos];
+    const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
+    *(Transfer*)(out + k * 128) = t;
+    const u8 st = T.xposted[pos];
+    if (st != POSTED_NONE) {
         const u64 q = atomicAdd((unsigned long long*)posted_count, 1ULL);
-        posted_out[2 * q] = ts;
-        posted_out[2 * q + 1] = T.posted[i] == POSTED_POSTED ? 0 : 1;
+        posted_out[2 * q] = t.timestamp;
+        posted_out[2 * q + 1] = st == POSTED_POSTED ? 0 : 1;
     }
 }
 
@@ -53,7 +61,7 @@ __global__ void tb_set_balances(Tables T, u64 lo, u64 hi, u64 dp_lo, u64 dp_hi, 
         *status = 1;
         return;
     }
-    Account* a = &T.accounts[slot];
+    AccountBal* a = &T.acct_bal[slot];
     a->debits_pending = tb_u128(dp_lo, dp_hi);
     a->debits_posted = tb_u128(dpo_lo, dpo_hi);
     a->credits_pending = tb_u128(cp_lo, cp_hi);
@@ -68,8 +76,8 @@ __global__ void tb_set_balances(Tables T, u64 lo, u64 hi, u64 dp_lo, u64 dp_hi, 
     *status = 0;
 }
 
-// Bench reset between steps: zero every live account's balances, drop the transfer count and the
-// balance bound (the transfer table itself is cleared with a memset).
+// Bench reset between steps: zero every balance, drop the transfer count and the balance bound
+// (the transfer index and posted groove are cleared with memsets).
 __global__ void tb_zero_balances(Tables T, u64 cap) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) {
@@ -78,10 +86,5 @@ __global__ void tb_zero_balances(Tables T, u64 cap) {
         T.g->bound_hi = 0;
     }
     if (i >= cap) return;
-    Account* a = &T.accounts[i];
-    if (a->timestamp == 0) return;
-    a->debits_pending = 0;
-    a->debits_posted = 0;
-    a->credits_pending = 0;
-    a->credits_posted = 0;
+    T.acct_bal[i] = AccountBal{0, 0, 0, 0};
 }

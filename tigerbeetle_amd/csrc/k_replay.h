@@ -11,13 +11,13 @@
 
 #include "k_resolve.h"
 
-enum : u32 { UNDO_ACCOUNT_INSERT = 1, UNDO_ACCOUNT_UPDATE = 2, UNDO_TRANSFER_INSERT = 3, UNDO_POSTED = 4 };
+enum : u32 { UNDO_ACCOUNT_INSERT = 1, UNDO_BALANCE_UPDATE = 2, UNDO_TRANSFER_INSERT = 3, UNDO_POSTED = 4 };
 
 struct alignas(16) UndoEntry {
     u32 kind;
-    u32 slot;
+    u32 slot;  // account slot / index entry / log position
     u64 pad;
-    Account before;
+    AccountBal before;
 };
 
 struct Replay {
@@ -25,6 +25,7 @@ struct Replay {
     UndoEntry* undo;
     u32 undo_len;
     u32 undo_cap;
+    u64 log_base;
     bool scope;
     bool failed;  // a panic was raised: stop
 };
@@ -34,7 +35,7 @@ __device__ static inline void rp_panic(Replay& R, u32 code) {
     R.failed = true;
 }
 
-__device__ static inline void rp_push(Replay& R, u32 kind, u32 slot, const Account* before) {
+__device__ static inline void rp_push(Replay& R, u32 kind, u32 slot, const AccountBal* before) {
     if (!R.scope) return;
     if (R.undo_len == R.undo_cap) {
         rp_panic(R, PANIC_UNDO_FULL);
@@ -51,18 +52,16 @@ __device__ static inline void rp_scope_close(Replay& R, bool persist) {
         while (R.undo_len > 0) {
             const UndoEntry& e = R.undo[--R.undo_len];
             switch (e.kind) {
-            case UNDO_ACCOUNT_INSERT: {  // tombstone (id = maxInt), timestamp kept
-                tb_tombstone(&R.T.accounts[e.slot]);
+            case UNDO_ACCOUNT_INSERT:  // tombstone (id = maxInt), timestamp kept
+                tb_account_tombstone(R.T, e.slot);
                 R.T.g->account_count--;
                 break;
-            }
-            case UNDO_ACCOUNT_UPDATE: R.T.accounts[e.slot] = e.before; break;
-            case UNDO_TRANSFER_INSERT: {
-                tb_tombstone(&R.T.transfers[e.slot]);
+            case UNDO_BALANCE_UPDATE: R.T.acct_bal[e.slot] = e.before; break;
+            case UNDO_TRANSFER_INSERT:
+                tb_xindex_tombstone(R.T, e.slot);
                 R.T.g->transfer_count--;
                 break;
-            }
-            case UNDO_POSTED: R.T.posted[e.slot] = POSTED_NONE; break;
+            case UNDO_POSTED: R.T.xposted[e.slot] = POSTED_NONE; break;
             }
         }
     }
@@ -77,24 +76,31 @@ __device__ static inline u128 rp_add(Replay& R, u128 a, u128 b) {
     return r;
 }
 
-__device__ static inline void rp_account_update(Replay& R, u32 slot, const Account& next) {
-    rp_push(R, UNDO_ACCOUNT_UPDATE, slot, &R.T.accounts[slot]);
-    R.T.accounts[slot] = next;
+__device__ static inline void rp_balance_update(Replay& R, u32 slot, const AccountBal& next) {
+    rp_push(R, UNDO_BALANCE_UPDATE, slot, &R.T.acct_bal[slot]);
+    R.T.acct_bal[slot] = next;
 }
 
-__device__ static inline u32 rp_transfer_insert(Replay& R, const Transfer& t) {
-    const u32 slot = tb_transfer_claim(R.T, tb_lo(t.id), tb_hi(t.id), t.timestamp);
-    if (slot == TB_NOT_FOUND) {
-        R.failed = true;
-        return slot;
+// Insert a transfer record at the event's own log position (after an exact find said "absent").
+__device__ static inline void rp_transfer_insert(Replay& R, const Transfer& t, u32 log_pos) {
+    const Tables& T = R.T;
+    const u64 fp = tb_fingerprint(tb_lo(t.id), tb_hi(t.id));
+    u64 pos = tb_hash_id(tb_lo(t.id), tb_hi(t.id)) & T.xidx_mask;
+    for (u64 n = 0; n <= T.xidx_mask; n++) {
+        XIndex* e = &T.xidx[pos];
+        if (e->fp == 0 && atomicCAS((unsigned long long*)&e->fp, 0ULL, (unsigned long long)fp) == 0ULL) {
+            T.xlog[log_pos] = t;
+            atomicOr((unsigned long long*)&e->word1, (unsigned long long)log_pos + 1);
+            T.g->transfer_count++;
+            rp_push(R, UNDO_TRANSFER_INSERT, (u32)pos, nullptr);
+            return;
+        }
+        pos = (pos + 1) & T.xidx_mask;
     }
-    R.T.transfers[slot] = t;
-    R.T.g->transfer_count++;
-    rp_push(R, UNDO_TRANSFER_INSERT, slot, nullptr);
-    return slot;
+    rp_panic(R, PANIC_TABLE_FULL);
 }
 
-__device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t) {
+__device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t, u32 log_pos) {
     const Tables& T = R.T;
     const u16 f = t.flags;
     if ((f & TF_POST) && (f & TF_VOID)) return CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
@@ -108,7 +114,7 @@ __device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t) {
 
     const u32 pslot = tb_transfer_find(T, tb_lo(t.pending_id), tb_hi(t.pending_id));
     if (pslot == TB_NOT_FOUND) return CT_PENDING_TRANSFER_NOT_FOUND;
-    const Transfer p = T.transfers[pslot];
+    const Transfer p = T.xlog[pslot];
     if (!(p.flags & TF_PENDING)) return CT_PENDING_TRANSFER_NOT_PENDING;
     const u32 drs = tb_account_find(T, tb_lo(p.debit_account_id), tb_hi(p.debit_account_id));
     const u32 crs = tb_account_find(T, tb_lo(p.credit_account_id), tb_hi(p.credit_account_id));
@@ -129,8 +135,8 @@ __device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t) {
     if ((f & TF_VOID) && amount < p.amount) return CT_PENDING_TRANSFER_HAS_DIFFERENT_AMOUNT;
 
     const u32 es = tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id));
-    if (es != TB_NOT_FOUND) return tb_post_void_exists(t, T.transfers[es], p);
-    const u8 posted = T.posted[pslot];
+    if (es != TB_NOT_FOUND) return tb_post_void_exists(t, T.xlog[es], p);
+    const u8 posted = T.xposted[pslot];
     if (posted == POSTED_POSTED) return CT_PENDING_TRANSFER_ALREADY_POSTED;
     if (posted == POSTED_VOIDED) return CT_PENDING_TRANSFER_ALREADY_VOIDED;
     if (!(p.timestamp < t.timestamp)) {
@@ -161,14 +167,14 @@ __device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t) {
     r.timestamp = t.timestamp;
     r.flags = t.flags;
     r.amount = amount;
-    rp_transfer_insert(R, r);
+    rp_transfer_insert(R, r, log_pos);
     if (R.failed) return R_OK;
 
     rp_push(R, UNDO_POSTED, pslot, nullptr);
-    T.posted[pslot] = (f & TF_POST) ? POSTED_POSTED : POSTED_VOIDED;
+    T.xposted[pslot] = (f & TF_POST) ? POSTED_POSTED : POSTED_VOIDED;
 
-    Account dr = T.accounts[drs];
-    Account cr = T.accounts[crs];
+    AccountBal dr = T.acct_bal[drs];
+    AccountBal cr = T.acct_bal[crs];
     if (dr.debits_pending < p.amount || cr.credits_pending < p.amount) {
         rp_panic(R, PANIC_OVERFLOW);
         return R_OK;
@@ -179,18 +185,18 @@ __device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t) {
         dr.debits_posted = rp_add(R, dr.debits_posted, amount);
         cr.credits_posted = rp_add(R, cr.credits_posted, amount);
     }
-    rp_account_update(R, drs, dr);
-    rp_account_update(R, crs, cr);
+    rp_balance_update(R, drs, dr);
+    rp_balance_update(R, crs, cr);
     return R_OK;
 }
 
-__device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t) {
+__device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u32 log_pos) {
     const Tables& T = R.T;
     const u16 f = t.flags;
     if (f & TF_PADDING) return CT_RESERVED_FLAG;
     if (t.id == 0) return CT_ID_MUST_NOT_BE_ZERO;
     if (t.id == TB_U128_MAX) return CT_ID_MUST_NOT_BE_INT_MAX;
-    if (f & (TF_POST | TF_VOID)) return rp_post_or_void(R, t);
+    if (f & (TF_POST | TF_VOID)) return rp_post_or_void(R, t, log_pos);
 
     if (t.debit_account_id == 0) return CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
     if (t.debit_account_id == TB_U128_MAX) return CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
@@ -211,17 +217,19 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t) {
     if (drs == TB_NOT_FOUND) return CT_DEBIT_ACCOUNT_NOT_FOUND;
     const u32 crs = tb_account_find(T, tb_lo(t.credit_account_id), tb_hi(t.credit_account_id));
     if (crs == TB_NOT_FOUND) return CT_CREDIT_ACCOUNT_NOT_FOUND;
-    Account dr = T.accounts[drs];
-    Account cr = T.accounts[crs];
-    if (!(t.timestamp > dr.timestamp) || !(t.timestamp > cr.timestamp)) {
+    const AccountHot dh = T.acct_hot[drs];
+    const AccountHot ch = T.acct_hot[crs];
+    AccountBal dr = T.acct_bal[drs];
+    AccountBal cr = T.acct_bal[crs];
+    if (!(t.timestamp > dh.timestamp) || !(t.timestamp > ch.timestamp)) {
         rp_panic(R, PANIC_ASSERT);
         return R_OK;
     }
-    if (dr.ledger != cr.ledger) return CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
-    if (t.ledger != dr.ledger) return CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+    if (dh.ledger != ch.ledger) return CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+    if (t.ledger != dh.ledger) return CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
 
     const u32 es = tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id));
-    if (es != TB_NOT_FOUND) return tb_transfer_exists(t, T.transfers[es]);
+    if (es != TB_NOT_FOUND) return tb_transfer_exists(t, T.xlog[es]);
 
     u128 amount = t.amount;
     if (f & (TF_BAL_DEBIT | TF_BAL_CREDIT)) {
@@ -254,11 +262,11 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t) {
     const u64 timeout_ns = (u64)t.timeout * 1000000000ULL;
     if (t.timestamp + timeout_ns < t.timestamp) return CT_OVERFLOWS_TIMEOUT;
     // debits_exceed_credits / credits_exceed_debits (tigerbeetle.zig:31-39).
-    if ((dr.flags & AF_DEBITS_MUST_NOT_EXCEED_CREDITS) &&
+    if ((dh.flags & AF_DEBITS_MUST_NOT_EXCEED_CREDITS) &&
         rp_add(R, rp_add(R, dr.debits_pending, dr.debits_posted), amount) > dr.credits_posted) {
         return CT_EXCEEDS_CREDITS;
     }
-    if ((cr.flags & AF_CREDITS_MUST_NOT_EXCEED_DEBITS) &&
+    if ((ch.flags & AF_CREDITS_MUST_NOT_EXCEED_DEBITS) &&
         rp_add(R, rp_add(R, cr.credits_pending, cr.credits_posted), amount) > cr.debits_posted) {
         return CT_EXCEEDS_DEBITS;
     }
@@ -266,7 +274,7 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t) {
 
     Transfer t2 = t;
     t2.amount = amount;
-    rp_transfer_insert(R, t2);
+    rp_transfer_insert(R, t2, log_pos);
     if (R.failed) return R_OK;
     if (f & TF_PENDING) {
         dr.debits_pending = rp_add(R, dr.debits_pending, amount);
@@ -275,8 +283,8 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t) {
         dr.debits_posted = rp_add(R, dr.debits_posted, amount);
         cr.credits_posted = rp_add(R, cr.credits_posted, amount);
     }
-    rp_account_update(R, drs, dr);
-    rp_account_update(R, crs, cr);
+    rp_balance_update(R, drs, dr);
+    rp_balance_update(R, crs, cr);
     return R_OK;
 }
 
@@ -284,13 +292,13 @@ __device__ static inline u32 rp_create_account(Replay& R, const Account& a) {
     const u32 code = tb_account_stateless(a);
     if (code != R_OK) return code;
     const u32 es = tb_account_find(R.T, tb_lo(a.id), tb_hi(a.id));
-    if (es != TB_NOT_FOUND) return tb_account_exists(a, R.T.accounts[es]);
+    if (es != TB_NOT_FOUND) return tb_account_exists(a, tb_account_load(R.T, es));
     const u32 slot = tb_account_claim(R.T, tb_lo(a.id), tb_hi(a.id), a.timestamp);
     if (slot == TB_NOT_FOUND) {
         R.failed = true;
         return R_OK;
     }
-    R.T.accounts[slot] = a;
+    tb_account_store_new(R.T, slot, a);
     R.T.g->account_count++;
     rp_push(R, UNDO_ACCOUNT_INSERT, slot, nullptr);
     return R_OK;
@@ -311,7 +319,7 @@ __device__ static inline u64 rp_batch(const PassArgs& P, Replay& R, u32 b) {
     for (u32 k = 0; k < nd && !R.failed; k++) {
         const u32 i = list[k];
         const u8* ev = P.events + (boff + i) * 128;
-        const u16 flags = *(const u16*)(ev + 118);
+        const u16 flags = P.eflags[pbase + i];
         const u64 evts = *(const u64*)(ev + 120);
         const bool linked = flags & 1;
         u32 result;
@@ -332,7 +340,7 @@ __device__ static inline u64 rp_batch(const PassArgs& P, Replay& R, u32 b) {
             if (OP == OP_CREATE_TRANSFERS) {
                 Transfer t = *(const Transfer*)ev;
                 t.timestamp = ts;
-                result = rp_create_transfer(R, t);
+                result = rp_create_transfer(R, t, (u32)(R.log_base + pbase + i));
             } else {
                 Account a = *(const Account*)ev;
                 a.timestamp = ts;
@@ -380,6 +388,7 @@ __global__ __launch_bounds__(REPLAY_THREADS) void tb_replay(PassArgs P, UndoEntr
         R.undo_cap = undo_cap;
         R.scope = false;
         R.failed = false;
+        R.log_base = P.log_base;
         u64 tsmax = 0;
         for (u32 c = 0; c < nb; c += REPLAY_THREADS) {
             const u32 k = c + threadIdx.x;

@@ -42,7 +42,7 @@ __device__ static inline u32 tb_block_rank(bool pred, u32* s_wave, u32& total) {
     return wb + before;
 }
 
-__device__ static inline bool tb_account_cert_fails(const Account* a, u128 S) {
+__device__ static inline bool tb_account_cert_fails(const AccountBal* a, u128 S) {
     u128 d, c, r;
     if (tb_add_overflows(a->debits_pending, a->debits_posted, &d)) return true;
     if (tb_add_overflows(a->credits_pending, a->credits_posted, &c)) return true;
@@ -69,30 +69,29 @@ __device__ static inline void tb_write_replies(const PassArgs& P, u32 b, u32 L, 
     if (threadIdx.x == 0) P.reply_bytes[b] = running * 8;
 }
 
-// Apply the balance effects of one independent ok transfer whose record kernel 1 already inserted
+// Apply the balance effects of one independent ok transfer whose record kernel 1 already wrote
 // (create_transfer :870-880, post_or_void :987-1010).  With the 64-bit certificate (no balance
 // can reach 2^64 this pass) the adds are fire-and-forget low-word atomics.
-__device__ static inline void tb_apply_transfer(const PassArgs& P, u32 pe, u32 info, bool cert64) {
+__device__ static inline void tb_apply_transfer(const PassArgs& P, u32 pe, u32 info, u16 flags, bool cert64) {
     const Tables& T = P.T;
-    u8* dr = (u8*)&T.accounts[P.dr[pe]];
-    u8* cr = (u8*)&T.accounts[P.cr[pe]];
+    u8* dr = (u8*)&T.acct_bal[P.dr[pe]];
+    u8* cr = (u8*)&T.acct_bal[P.cr[pe]];
     const u128 amount = tb_u128(P.amt[2 * pe], P.amt[2 * pe + 1]);
-    const u16 flags = (u16)(info >> 16);
     if (info & HZ_POSTVOID) {
         const u32 pslot = P.ps[pe];
-        const u128 pamount = T.transfers[pslot].amount;
-        T.posted[pslot] = (flags & TF_POST) ? POSTED_POSTED : POSTED_VOIDED;
+        const u128 pamount = T.xlog[pslot].amount;
+        T.xposted[pslot] = (flags & TF_POST) ? POSTED_POSTED : POSTED_VOIDED;
         const u128 neg = (u128)0 - pamount;  // dp -= p.amount (mod 2^128, exact in aggregate)
-        tb_atomic_add_u128(dr + ACCOUNT_OFF_DEBITS_PENDING, neg);
-        tb_atomic_add_u128(cr + ACCOUNT_OFF_CREDITS_PENDING, neg);
+        tb_atomic_add_u128(dr + BAL_OFF_DEBITS_PENDING, neg);
+        tb_atomic_add_u128(cr + BAL_OFF_CREDITS_PENDING, neg);
         if (flags & TF_POST) {
-            tb_atomic_add_u128(dr + ACCOUNT_OFF_DEBITS_POSTED, amount);
-            tb_atomic_add_u128(cr + ACCOUNT_OFF_CREDITS_POSTED, amount);
+            tb_atomic_add_u128(dr + BAL_OFF_DEBITS_POSTED, amount);
+            tb_atomic_add_u128(cr + BAL_OFF_CREDITS_POSTED, amount);
         }
         return;
     }
-    const u32 off_d = (flags & TF_PENDING) ? ACCOUNT_OFF_DEBITS_PENDING : ACCOUNT_OFF_DEBITS_POSTED;
-    const u32 off_c = (flags & TF_PENDING) ? ACCOUNT_OFF_CREDITS_PENDING : ACCOUNT_OFF_CREDITS_POSTED;
+    const u32 off_d = (flags & TF_PENDING) ? BAL_OFF_DEBITS_PENDING : BAL_OFF_DEBITS_POSTED;
+    const u32 off_c = (flags & TF_PENDING) ? BAL_OFF_CREDITS_PENDING : BAL_OFF_CREDITS_POSTED;
     if (cert64) {
         tb_atomic_add_lo_noret(dr + off_d, tb_lo(amount));
         tb_atomic_add_lo_noret(cr + off_c, tb_lo(amount));
@@ -104,12 +103,47 @@ __device__ static inline void tb_apply_transfer(const PassArgs& P, u32 pe, u32 i
 
 // Apply one independent ok account (create_account :762, groove insert).
 __device__ static inline void tb_apply_account(const PassArgs& P, u32 pe, u64 ts) {
-    const Account* ev = (const Account*)(P.events + (P.e0 + pe) * 128);
-    Account a = *ev;
+    Account a = *(const Account*)(P.events + (P.e0 + pe) * 128);
     a.timestamp = ts;
     const u32 slot = tb_account_claim(P.T, tb_lo(a.id), tb_hi(a.id), ts);
     if (slot == TB_NOT_FOUND) return;
-    P.T.accounts[slot] = a;
+    tb_account_store_new(P.T, slot, a);
+}
+
+// Is an event dependent (see the header)?  Kernel 1's intrinsic result `code` is trusted otherwise.
+template <u8 OP>
+__device__ static inline bool tb_classify(const PassArgs& P, u32 pe, u32 info, u32 code, u128 S, bool cert_global,
+                                          bool any_dup, bool any_bal, bool any_pv) {
+    const Tables& T = P.T;
+    if (OP == OP_CREATE_ACCOUNTS) {
+        return any_dup && (info & HZ_KEYS) && tb_dedup_is_dup(P.dedup, P.dedup_mask, P.kid[pe]);
+    }
+    if (info & HZ_SELFDEP) return true;
+    if (any_dup) {
+        if ((info & HZ_SPEC) && (T.xidx[P.rs[pe]].word1 & XI_DUP)) return true;
+        if ((info & HZ_PV_KEY) && tb_dedup_is_dup(P.dedup, P.dedup_mask, P.kpid[pe])) return true;
+    }
+    if (any_pv) {
+        // Some post/void of this pass names a pending id: an event whose id is one of them, or a
+        // post/void whose pending transfer was created in this pass, is dependent.
+        const u64 kid = P.kid[pe];
+        if (kid && tb_dedup_is_dup_or_present(P.dedup, P.dedup_mask, kid)) return true;
+        if (info & HZ_PV_KEY) {
+            const Transfer* ev = (const Transfer*)(P.events + (P.e0 + pe) * 128);
+            if (tb_transfer_claimed_in_pass(T, tb_lo(ev->pending_id), tb_hi(ev->pending_id), P.log_base)) return true;
+        }
+    }
+    if ((info & HZ_ACCTS) && (code == R_OK || code == CT_OVERFLOWS_TIMEOUT)) {
+        const u32 drs = P.dr[pe], crs = P.cr[pe];
+        if (code == R_OK) {
+            if (info & (HZ_BAL | HZ_LIMIT)) return true;
+            if (any_bal && (T.account_mark[drs] == P.epoch || T.account_mark[crs] == P.epoch)) return true;
+        }
+        if (!cert_global && (tb_account_cert_fails(&T.acct_bal[drs], S) || tb_account_cert_fails(&T.acct_bal[crs], S))) {
+            return true;
+        }
+    }
+    return false;
 }
 
 template <u8 OP>
@@ -131,14 +165,14 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
 
     u128 S = 0;
     bool cert_global = true, cert64 = true;
-    bool any_dup = true, any_bal = true;
+    const bool any_dup = P.pass_words[PW_DUP] != 0;
+    const bool any_bal = P.pass_words[PW_BAL] != 0;
+    const bool any_pv = P.pass_words[PW_PV] != 0;
     if (OP == OP_CREATE_TRANSFERS) {
         S = tb_sum_total(P.sum_shards);
         u128 r;
         cert_global = !tb_add_overflows(tb_u128(T.g->bound_lo, T.g->bound_hi), S, &r);
         cert64 = cert_global && tb_hi(r) == 0;
-        any_dup = P.sum_shards[PW_DUP] != 0;
-        any_bal = P.sum_shards[PW_BAL] != 0;
     }
 
     if (threadIdx.x == 0) s_applied = 0;
@@ -148,25 +182,8 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         const u32 pe = pbase + i;
         const u32 info = P.info[pe];
         const u32 code = info & 0xFF;
-        bool dep = false;
-        if (any_dup && (info & HZ_KEYS) &&
-            (tb_dedup_is_dup(P.dedup, P.dedup_mask, P.kid[pe]) ||
-             (P.kpid[pe] && tb_dedup_is_dup(P.dedup, P.dedup_mask, P.kpid[pe])))) {
-            dep = true;
-        }
-        if (OP == OP_CREATE_TRANSFERS && !dep && (info & HZ_ACCTS) &&
-            (code == R_OK || code == CT_OVERFLOWS_TIMEOUT)) {
-            const u32 drs = P.dr[pe], crs = P.cr[pe];
-            if (code == R_OK) {
-                if (info & (HZ_BAL | HZ_LIMIT)) dep = true;
-                else if (any_bal && (T.account_mark[drs] == P.epoch || T.account_mark[crs] == P.epoch)) dep = true;
-            }
-            if (!dep && !cert_global &&
-                (tb_account_cert_fails(&T.accounts[drs], S) || tb_account_cert_fails(&T.accounts[crs], S))) {
-                dep = true;
-            }
-        }
-        const bool linked = (info >> 16) & 1;
+        const bool dep = tb_classify<OP>(P, pe, info, code, S, cert_global, any_dup, any_bal, any_pv);
+        const bool linked = P.eflags[pe] & 1;
         local_linked |= linked;
         s_code[i] = (u8)code;
         s_fl[i] = (linked ? 1 : 0) | (dep ? 2 : 0);
@@ -250,7 +267,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                 const u64 ts = ts0 + i;
                 if (eval_ok) tsmax = ts;  // increasing in i
                 if (fin == R_OK) {
-                    if (OP == OP_CREATE_TRANSFERS) tb_apply_transfer(P, pe, info, cert64);
+                    if (OP == OP_CREATE_TRANSFERS) tb_apply_transfer(P, pe, info, P.eflags[pe], cert64);
                     else tb_apply_account(P, pe, ts);
                     atomicAdd(&s_applied, 1u);
                 }
@@ -260,7 +277,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
             // Withdraw a speculative record whose event did not commit here (failed, rolled back,
             // or left to the ordered replay, which inserts it itself in order).
             if (OP == OP_CREATE_TRANSFERS && (info & HZ_SPEC) && (dep || fin != R_OK)) {
-                tb_tombstone(&T.transfers[P.rs[pe]]);
+                tb_xindex_tombstone(T, P.rs[pe]);
             }
         }
         u32 total;

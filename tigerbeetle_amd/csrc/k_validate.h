@@ -12,10 +12,12 @@
 
 struct TransferScratch {
     u32 hz = 0;
-    u32 dr = TB_NOT_FOUND, cr = TB_NOT_FOUND, ps = TB_NOT_FOUND, rs = TB_NOT_FOUND;
-    u128 amount = 0;       // amount applied by an independent ok event (post: posted amount)
-    u128 contrib = 0;      // contribution to S (overflow certificate)
-    u64 kid = 0, kpid = 0;
+    u32 dr = TB_NOT_FOUND, cr = TB_NOT_FOUND;
+    u32 ps = TB_NOT_FOUND;  // log position of the pending transfer (post/void)
+    u32 rs = TB_NOT_FOUND;  // index entry claimed by the speculative insert
+    u128 amount = 0;        // amount applied by an independent ok event (post: posted amount)
+    u128 contrib = 0;       // contribution to S (overflow certificate)
+    u64 kid = 0, kpid = 0;  // dedup keys of id / pending_id
 };
 
 // create_transfer_exists (state_machine.zig:886-905).
@@ -59,15 +61,28 @@ __device__ static inline u32 tb_post_void_exists(const Transfer& t, const Transf
     return CT_EXISTS;
 }
 
-__device__ static inline void tb_spec_insert(const PassArgs& P, const Transfer& r, TransferScratch& s) {
-    const u32 slot = tb_transfer_claim(P.T, tb_lo(r.id), tb_hi(r.id), r.timestamp);
-    if (slot == TB_NOT_FOUND) return;
-    P.T.transfers[slot] = r;
-    s.rs = slot;
-    s.hz |= HZ_SPEC;
+// The `id` existence check of create_transfer (:824) / post_or_void (:954) fused with the
+// speculative index claim.  Returns R_OK (claimed, record to be written by the caller),
+// a pseudo "exists" marker via *exists_pos, or CLAIM_COLLIDED (dependent).
+__device__ static inline u32 tb_claim_id(const PassArgs& P, const Transfer& t, u32 pe, TransferScratch& s,
+                                         u32* exists_pos) {
+    s.kid = tb_dedup_key(tb_lo(t.id), tb_hi(t.id));
+    if (P.ablate & ABL_SPEC) return CLAIM_NEW;
+    u32 entry = TB_NOT_FOUND;
+    const u32 r = tb_transfer_claim(P.T, tb_lo(t.id), tb_hi(t.id), P.log_base + pe, P.log_base, exists_pos, &entry);
+    if (r == CLAIM_NEW) {
+        s.rs = entry;
+        s.hz |= HZ_SPEC;
+    } else if (r == CLAIM_COLLIDED) {
+        s.hz |= HZ_SELFDEP;
+        P.pass_words[PW_DUP] = 1;
+    }
+    return r;
 }
 
-__device__ static inline u32 tb_validate_post_void(const PassArgs& P, const Transfer& t, u64 ts,
+// Claims are never withdrawn here: an entry claimed by an event that then fails stays claimed
+// until kernel 2 tombstones it, so it keeps detecting same-pass collisions on its id.
+__device__ static inline u32 tb_validate_post_void(const PassArgs& P, const Transfer& t, u64 ts, u32 pe,
                                                    TransferScratch& s) {
     const Tables& T = P.T;
     const u16 f = t.flags;
@@ -80,17 +95,24 @@ __device__ static inline u32 tb_validate_post_void(const PassArgs& P, const Tran
     if (t.pending_id == t.id) return CT_PENDING_ID_MUST_BE_DIFFERENT;
     if (t.timeout != 0) return CT_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
 
-    // From here the result reads the state of pending_id and of id: register both keys.
-    s.hz |= HZ_POSTVOID | HZ_KEYS;
-    s.kid = tb_dedup_key(tb_lo(t.id), tb_hi(t.id));
+    // From here the result reads the state of pending_id and of id.  Register both now (the
+    // pending-dependent checks below may change under the replay): pending_id in the pass pending
+    // set, id by claiming its index entry.
+    s.hz |= HZ_POSTVOID | HZ_PV_KEY;
+    P.pass_words[PW_PV] = 1;
     s.kpid = tb_dedup_key(tb_lo(t.pending_id), tb_hi(t.pending_id));
-    const bool c1 = tb_dedup_insert(P.dedup, P.dedup_mask, s.kid);
-    const bool c2 = tb_dedup_insert(P.dedup, P.dedup_mask, s.kpid);
-    if (c1 || c2) P.sum_shards[PW_DUP] = 1;
+    if (tb_dedup_insert(P.dedup, P.dedup_mask, s.kpid)) P.pass_words[PW_DUP] = 1;
+    u32 es = TB_NOT_FOUND;
+    const u32 claim = tb_claim_id(P, t, pe, s, &es);
+    if (claim == CLAIM_COLLIDED) return R_OK;  // dependent: the replay decides
 
     const u32 pslot = tb_transfer_find(T, tb_lo(t.pending_id), tb_hi(t.pending_id));
+    if (pslot != TB_NOT_FOUND && (u64)pslot >= P.log_base) {  // pending created in this pass
+        s.hz |= HZ_SELFDEP;
+        return R_OK;
+    }
     if (pslot == TB_NOT_FOUND) return CT_PENDING_TRANSFER_NOT_FOUND;
-    const Transfer p = T.transfers[pslot];
+    const Transfer p = T.xlog[pslot];
     if (!(p.flags & TF_PENDING)) return CT_PENDING_TRANSFER_NOT_PENDING;
 
     const u32 drs = tb_account_find(T, tb_lo(p.debit_account_id), tb_hi(p.debit_account_id));
@@ -110,10 +132,9 @@ __device__ static inline u32 tb_validate_post_void(const PassArgs& P, const Tran
     if (amount > p.amount) return CT_EXCEEDS_PENDING_TRANSFER_AMOUNT;
     if ((f & TF_VOID) && amount < p.amount) return CT_PENDING_TRANSFER_HAS_DIFFERENT_AMOUNT;
 
-    const u32 es = tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id));
-    if (es != TB_NOT_FOUND) return tb_post_void_exists(t, T.transfers[es], p);
+    if (claim == CLAIM_EXISTS) return tb_post_void_exists(t, T.xlog[es], p);
 
-    const u8 posted = T.posted[pslot];
+    const u8 posted = T.xposted[pslot];
     if (posted == POSTED_POSTED) return CT_PENDING_TRANSFER_ALREADY_POSTED;
     if (posted == POSTED_VOIDED) return CT_PENDING_TRANSFER_ALREADY_VOIDED;
 
@@ -129,12 +150,11 @@ __device__ static inline u32 tb_validate_post_void(const PassArgs& P, const Tran
     s.cr = crs;
     s.ps = pslot;
     s.hz |= HZ_ACCTS;
-    if ((T.accounts[drs].flags | T.accounts[crs].flags) & AF_LIMITS) s.hz |= HZ_LIMIT;
+    if ((T.acct_hot[drs].flags | T.acct_hot[crs].flags) & AF_LIMITS) s.hz |= HZ_LIMIT;
     s.amount = (f & TF_POST) ? amount : 0;
     // A post moves <= p.amount from pending to posted: dp + dpost never grows, so no S term.
 
-    // Speculative insert of the composed record (:971-985); kernel 2 withdraws it (tombstone) if
-    // the event ends up failing or dependent.
+    // Speculative record (composed as at :971-985); kernel 2 withdraws it if the event fails.
     Transfer r;
     r.id = t.id;
     r.debit_account_id = p.debit_account_id;
@@ -149,11 +169,11 @@ __device__ static inline u32 tb_validate_post_void(const PassArgs& P, const Tran
     r.code = p.code;
     r.flags = t.flags;
     r.timestamp = ts;
-    tb_spec_insert(P, r, s);
+    if (s.hz & HZ_SPEC) T.xlog[P.log_base + pe] = r;
     return R_OK;
 }
 
-__device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Transfer& t, u64 ts,
+__device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Transfer& t, u64 ts, u32 pe,
                                                   TransferScratch& s) {
     const Tables& T = P.T;
     const u16 f = t.flags;
@@ -161,7 +181,7 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     if (t.id == 0) return CT_ID_MUST_NOT_BE_ZERO;
     if (t.id == TB_U128_MAX) return CT_ID_MUST_NOT_BE_INT_MAX;
 
-    if (f & (TF_POST | TF_VOID)) return tb_validate_post_void(P, t, ts, s);
+    if (f & (TF_POST | TF_VOID)) return tb_validate_post_void(P, t, ts, pe, s);
 
     if (t.debit_account_id == 0) return CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
     if (t.debit_account_id == TB_U128_MAX) return CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
@@ -178,48 +198,53 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     if (t.ledger == 0) return CT_LEDGER_MUST_NOT_BE_ZERO;
     if (t.code == 0) return CT_CODE_MUST_NOT_BE_ZERO;
 
-    const u32 drs = tb_account_find(T, tb_lo(t.debit_account_id), tb_hi(t.debit_account_id));
+    // Both probes are issued before either result is consumed.
+    const bool fake = P.ablate & ABL_ACCTS;
+    const u32 drs = fake ? (u32)(tb_lo(t.debit_account_id) & 1023)
+                         : tb_account_find(T, tb_lo(t.debit_account_id), tb_hi(t.debit_account_id));
+    const u32 crs = fake ? (u32)(tb_lo(t.credit_account_id) & 1023)
+                         : tb_account_find(T, tb_lo(t.credit_account_id), tb_hi(t.credit_account_id));
     if (drs == TB_NOT_FOUND) return CT_DEBIT_ACCOUNT_NOT_FOUND;
-    const u32 crs = tb_account_find(T, tb_lo(t.credit_account_id), tb_hi(t.credit_account_id));
     if (crs == TB_NOT_FOUND) return CT_CREDIT_ACCOUNT_NOT_FOUND;
-    const Account* dr = &T.accounts[drs];
-    const Account* cr = &T.accounts[crs];
-    const u32 dr_ledger = dr->ledger, cr_ledger = cr->ledger;
-    const u16 acct_flags = dr->flags | cr->flags;
-    if (!(ts > dr->timestamp) || !(ts > cr->timestamp)) return TB_CODE_PANIC;  // :817-818
-    if (dr_ledger != cr_ledger) return CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
-    if (t.ledger != dr_ledger) return CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+    const AccountHot dr = T.acct_hot[drs];
+    const AccountHot cr = T.acct_hot[crs];
+    if (!(ts > dr.timestamp) || !(ts > cr.timestamp)) return TB_CODE_PANIC;  // :817-818
+    if (dr.ledger != cr.ledger) return CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+    if (t.ledger != dr.ledger) return CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
 
-    // From here the result reads the state of `id`.
-    s.hz |= HZ_KEYS;
-    s.kid = tb_dedup_key(tb_lo(t.id), tb_hi(t.id));
-    if (tb_dedup_insert(P.dedup, P.dedup_mask, s.kid)) P.sum_shards[PW_DUP] = 1;
-    const u32 es = tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id));
-    if (es != TB_NOT_FOUND) return tb_transfer_exists(t, T.transfers[es]);
-
+    // From here the event may end up ok: account for it in S and mark balancing accounts before
+    // the id check, so that a dependent (colliding) event is covered too.
+    const bool balancing = (f & (TF_BAL_DEBIT | TF_BAL_CREDIT)) != 0;
+    s.contrib = balancing && t.amount == 0 ? (u128)UINT64_MAX : t.amount;
     s.dr = drs;
     s.cr = crs;
     s.hz |= HZ_ACCTS;
-    if (acct_flags & AF_LIMITS) s.hz |= HZ_LIMIT;
-    if (f & (TF_BAL_DEBIT | TF_BAL_CREDIT)) {
+    if ((dr.flags | cr.flags) & AF_LIMITS) s.hz |= HZ_LIMIT;
+    if (balancing) {
         // The amount depends on the running balance (:826-846): dependent, and so is every event
         // touching the balanced account in this pass.
         s.hz |= HZ_BAL;
         if (f & TF_BAL_DEBIT) P.T.account_mark[drs] = P.epoch;
         if (f & TF_BAL_CREDIT) P.T.account_mark[crs] = P.epoch;
-        P.sum_shards[PW_BAL] = 1;
-        s.contrib = t.amount == 0 ? (u128)UINT64_MAX : t.amount;
-        return R_OK;
+        P.pass_words[PW_BAL] = 1;
     }
+
+    // The existence check of `id` (:824) fused with the speculative claim of its index entry.
+    u32 es = TB_NOT_FOUND;
+    const u32 claim = tb_claim_id(P, t, pe, s, &es);
+    if (claim == CLAIM_EXISTS) return tb_transfer_exists(t, T.xlog[es]);
+    if (claim == CLAIM_COLLIDED || balancing) return R_OK;  // dependent: the replay decides
+
     s.amount = t.amount;
-    s.contrib = t.amount;
     // Overflow checks (:848-861) are certified impossible or the event is dependent (resolve);
     // then the timeout check (:862) is the next possible failure.
     const u64 timeout_ns = (u64)t.timeout * 1000000000ULL;
-    if (ts + timeout_ns < ts) return CT_OVERFLOWS_TIMEOUT;
-    Transfer r = t;
-    r.timestamp = ts;
-    tb_spec_insert(P, r, s);
+    if (ts + timeout_ns < ts) return CT_OVERFLOWS_TIMEOUT;  // entry withdrawn by kernel 2
+    if (s.hz & HZ_SPEC) {
+        Transfer r = t;
+        r.timestamp = ts;
+        T.xlog[P.log_base + pe] = r;
+    }
     return R_OK;
 }
 
@@ -247,9 +272,10 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
             code = R_TIMESTAMP_MUST_BE_ZERO;  // :643
         } else {
             const u64 ts = P.batch_ts[b] - L + j + 1;  // :645
-            code = tb_validate_transfer(P, t, ts, s);
+            code = tb_validate_transfer(P, t, ts, pe, s);
         }
-        P.info[pe] = code | s.hz | ((u32)t.flags << 16);
+        P.info[pe] = code | s.hz;
+        P.eflags[pe] = t.flags;
         P.dr[pe] = s.dr;
         P.cr[pe] = s.cr;
         P.ps[pe] = s.ps;
@@ -329,12 +355,13 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_accounts_validate(PassArg
         if (code == R_OK) {
             hz |= HZ_KEYS;
             kid = tb_dedup_key(tb_lo(a.id), tb_hi(a.id));
-            tb_dedup_insert(P.dedup, P.dedup_mask, kid);
+            if (tb_dedup_insert(P.dedup, P.dedup_mask, kid)) P.pass_words[PW_DUP] = 1;
             const u32 slot = tb_account_find(P.T, tb_lo(a.id), tb_hi(a.id));
-            if (slot != TB_NOT_FOUND) code = tb_account_exists(a, P.T.accounts[slot]);
+            if (slot != TB_NOT_FOUND) code = tb_account_exists(a, tb_account_load(P.T, slot));
         }
     }
-    P.info[pe] = code | hz | ((u32)a.flags << 16);
+    P.info[pe] = code | hz;
+    P.eflags[pe] = a.flags;
     P.kid[pe] = kid;
     P.kpid[pe] = 0;
 }

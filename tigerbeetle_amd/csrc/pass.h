@@ -13,16 +13,18 @@
 
 #include "tb_device.h"
 
-// info word per event: [7:0] result code, [15:8] hazard bits, [31:16] event flags.
+// info word per event: [7:0] result code, [31:8] hazard bits (event flags live in eflags[]).
 enum : u32 {
-    HZ_KEYS = 1u << 8,       // inserted dedup keys (kid/kpid) — check for collisions
+    HZ_KEYS = 1u << 8,       // create_accounts: inserted its id into the pass dedup set
     HZ_LIMIT = 1u << 9,      // touches an account with a limit flag (tigerbeetle.zig:31-39)
     HZ_BAL = 1u << 10,       // balancing_debit / balancing_credit event
     HZ_ACCTS = 1u << 11,     // dr/cr slots valid (marks + certificate apply)
     HZ_POSTVOID = 1u << 12,  // post_pending_transfer / void_pending_transfer
     HZ_DEP = 1u << 13,       // dependent: resolved by the ordered replay
     HZ_EVAL_OK = 1u << 14,   // returned ok when evaluated (feeds commit_timestamp)
-    HZ_SPEC = 1u << 15,      // record speculatively inserted at rs[] by kernel 1
+    HZ_SPEC = 1u << 15,      // index entry rs[] claimed, record written at log_base + event
+    HZ_SELFDEP = 1u << 16,   // kernel 1 already knows the event is dependent (id collision)
+    HZ_PV_KEY = 1u << 17,    // post/void: pending id registered in the pass pending set
 };
 
 #define SUM_SHARDS 64
@@ -45,10 +47,11 @@ struct PassArgs {
     u32* reply_bytes;      // [nb_call]
     // scratch, pass-relative
     u32* info;
+    u16* eflags;           // event flags
     u32* dr;
     u32* cr;
-    u32* ps;
-    u32* rs;               // slot of the speculatively inserted transfer record
+    u32* ps;               // log position of the pending transfer (post/void)
+    u32* rs;               // index entry claimed by the speculative insert
     u64* amt;              // 2 words per event
     u64* kid;
     u64* kpid;
@@ -56,9 +59,14 @@ struct PassArgs {
     u32* dep_count;        // per batch (call-relative index - b0)
     u64* dedup;
     u64 dedup_mask;
-    u64* sum_shards;       // [SUM_SHARDS][2]
+    u64* sum_shards;       // [SUM_SHARDS][2] then the pass words (PW_*)
+    u64* pass_words;       // == sum_shards
+    u64 log_base;          // transfer-log position of event 0 of the pass
     Tables T;
+    u32 ablate;            // timing-only ablation bits (TBGPU_ABLATE env, never in a parity run)
 };
+
+enum : u32 { ABL_DEDUP = 1, ABL_SPEC = 2, ABL_ACCTS = 4, ABL_XFIND = 8, ABL_STAGE = 16 };
 
 // Batch of a call-relative event index (binary search over batch_off[b0..b1]).
 __device__ static inline u32 tb_batch_of(const PassArgs& P, u64 e) {
@@ -110,11 +118,13 @@ __device__ static inline u128 tb_wave_sum_u128(u128 v) {
 // Add a block's partial S into one of SUM_SHARDS shards (no single hot word).  A partial at or
 // above 2^100 sets the HUGE word instead, which keeps every shard total below 2^124 (at most 2^24
 // blocks per pass) so the mod-2^128 shard atomics never wrap.
-// Pass words after the shards: HUGE (S >= 2^100 somewhere), DUP (a dedup collision happened),
-// BAL (a tentatively-ok balancing event exists).  Written with idempotent stores.
+// Pass words after the shards: HUGE (S >= 2^100 somewhere), DUP (an id or pending-id collision
+// happened), BAL (a tentatively-ok balancing event exists), PV (a post/void event registered its
+// pending id).  Written with idempotent stores.
 #define PW_HUGE (2 * SUM_SHARDS)
 #define PW_DUP (2 * SUM_SHARDS + 1)
 #define PW_BAL (2 * SUM_SHARDS + 2)
+#define PW_PV (2 * SUM_SHARDS + 3)
 #define SUM_WORDS (2 * SUM_SHARDS + 4)
 __device__ static inline void tb_sum_publish(const PassArgs& P, u128 block_sum) {
     if (block_sum == 0) return;

@@ -50,11 +50,6 @@ struct alignas(16) Transfer {
 static_assert(sizeof(Account) == 128, "Account is 128 bytes");
 static_assert(sizeof(Transfer) == 128, "Transfer is 128 bytes");
 
-// Byte offsets used by the in-place balance atomics.
-#define ACCOUNT_OFF_DEBITS_PENDING 16
-#define ACCOUNT_OFF_DEBITS_POSTED 32
-#define ACCOUNT_OFF_CREDITS_PENDING 48
-#define ACCOUNT_OFF_CREDITS_POSTED 64
 
 // AccountFlags (tigerbeetle.zig:42-62), TransferFlags (:91-104).
 enum : u16 {
@@ -161,23 +156,28 @@ __device__ static inline u128 tb_sat_add(u128 a, u128 b) {
 // ------------------------------------------------------------------------------------------------
 // Engine state in HBM.
 //
-// Both object tables are open-addressing hash tables whose slots ARE the 128-byte records
-// (record-in-table): a hit costs one HBM line, and a transfer probe reads only the first 64-byte
-// sector (the id).
-//   * empty slot:  id == 0 (ids are never 0 for live objects: id_must_not_be_zero)
-//   * live slot:   id != 0, id != maxInt; timestamp != 0
-//   * tombstone:   id == maxInt(u128) (never a live id: id_must_not_be_int_max) — a rolled-back or
-//                  withdrawn insert; probes continue past it, it is never reclaimed
-// Inserts claim an empty slot with a 64-bit CAS of the timestamp word (0 -> ts) and then write the
-// record; a slot claimed in the current kernel may still read id == 0 to a concurrent prober, which
-// can only be a prober of an id that is absent from the pre-kernel table (a claimed slot was empty,
-// so it never lies on the probe path of an older key) — every such pair of events collides in the
-// pass dedup set and is resolved by the ordered replay.
+// Accounts: open-addressing hash table of 32-byte HOT entries {id, ledger, code, flags, timestamp}
+// (one 64-byte sector holds two entries, so a probe step costs one sector), with the balances
+// (64 B) and the cold fields (user_data_*, reserved; 32 B) in parallel arrays at the same slot.
+//   * empty:     id == 0 (never a live id: id_must_not_be_zero)
+//   * tombstone: id == maxInt(u128) (never a live id: id_must_not_be_int_max) — a rolled-back
+//                insert; probes continue past it and it is never reclaimed
+//   Inserts claim an empty entry with a 64-bit CAS of its timestamp word (0 -> ts; timestamps are
+//   always >= 1), then write the id.
+//
+// Transfers: an append LOG of 128-byte records — event e of a pass is written at log position
+// pass_base + e, so kernel 1 stores records fully coalesced — plus a 16-byte INDEX entry per
+// record {fingerprint u64 (0 = empty), word1 = (log position + 1) | state << 32}.  A probe compares
+// fingerprints and confirms a match against the log record's id.  An index entry is claimed with a
+// CAS of its fingerprint word; a second event of the same pass with the same id meets the claimed
+// fingerprint on its probe path (or loses the CAS to it) — that is how same-pass duplicate ids are
+// detected, with no separate dedup set.  Withdrawn entries get the TOMB state.
 // ------------------------------------------------------------------------------------------------
 struct Globals {
     u64 commit_timestamp;     // max timestamp of an event that returned ok when evaluated
     u64 panic;                // PANIC_* bits
-    u64 sum_lo, sum_hi;       // (unused)
+    u64 log_next;             // next free transfer-log position
+    u64 unused;
     u64 bound_lo, bound_hi;   // upper bound of dp+dpost and cp+cpost over every account
     u64 dependent_total;      // dependent events of this pass
     u64 dependent_all;        // cumulative
@@ -187,13 +187,47 @@ struct Globals {
     u64 pad[5];
 };
 
+struct AccountHot {
+    u64 id_lo, id_hi;
+    u32 ledger;
+    u16 code;
+    u16 flags;
+    u64 timestamp;
+};
+struct AccountBal {
+    u128 debits_pending, debits_posted, credits_pending, credits_posted;
+};
+struct AccountCold {
+    u128 user_data_128;
+    u64 user_data_64;
+    u32 user_data_32;
+    u32 reserved;
+};
+static_assert(sizeof(AccountHot) == 32 && sizeof(AccountBal) == 64 && sizeof(AccountCold) == 32, "account split");
+
+#define BAL_OFF_DEBITS_PENDING 0
+#define BAL_OFF_DEBITS_POSTED 16
+#define BAL_OFF_CREDITS_PENDING 32
+#define BAL_OFF_CREDITS_POSTED 48
+
+struct XIndex {
+    u64 fp;     // fingerprint of the id, never 0; 0 = empty entry
+    u64 word1;  // (log position + 1) in the low 32 bits (0 = claim in flight), state in the high 32
+};
+#define XI_DUP (1ULL << 32)   // another event of the same pass claimed this id too
+#define XI_TOMB (2ULL << 32)  // withdrawn (failed / dependent / rolled back)
+
 struct Tables {
-    Account* accounts;        // [account_cap]
+    AccountHot* acct_hot;     // [account_cap]
+    AccountBal* acct_bal;     // [account_cap]
+    AccountCold* acct_cold;   // [account_cap]
     u32* account_mark;        // [account_cap] pass epoch of the last balancing mark
     u64 account_mask;         // account_cap - 1
-    Transfer* transfers;      // [transfer_cap]
-    u8* posted;               // [transfer_cap] POSTED_* of the pending transfer in that slot
-    u64 transfer_mask;
+    XIndex* xidx;             // [xidx_cap]
+    u64 xidx_mask;
+    Transfer* xlog;           // [xlog_cap]
+    u8* xposted;              // [xlog_cap] POSTED_* of the pending transfer at that log position
+    u64 xlog_cap;
     Globals* g;
 };
 
@@ -201,61 +235,176 @@ __device__ static inline void tb_panic(Globals* g, u32 code) {
     atomicOr((unsigned long long*)&g->panic, (unsigned long long)code);
 }
 
-// Probe a record-in-table for a live id.  Returns the slot or TB_NOT_FOUND.
-template <typename R>
-__device__ static inline u32 tb_find(const R* table, u64 mask, u64 lo, u64 hi) {
-    // 0 marks an empty slot and maxInt a tombstone: neither is ever a live id.
-    if ((lo | hi) == 0 || (lo & hi) == ~0ULL) return TB_NOT_FOUND;
-    u64 pos = tb_hash_id(lo, hi) & mask;
-    for (u64 n = 0; n <= mask; n++) {
-        const u64* idw = (const u64*)&table[pos];
-        const u64 a = idw[0], b = idw[1];
+__host__ __device__ static inline bool tb_id_reserved(u64 lo, u64 hi) {
+    return (lo | hi) == 0 || (lo & hi) == ~0ULL;  // 0 or maxInt: never a live id
+}
+
+// ---- accounts -----------------------------------------------------------------------------------
+__device__ static inline u32 tb_account_find(const Tables& T, u64 lo, u64 hi) {
+    if (tb_id_reserved(lo, hi)) return TB_NOT_FOUND;
+    u64 pos = tb_hash_id(lo, hi) & T.account_mask;
+    for (u64 n = 0; n <= T.account_mask; n++) {
+        const AccountHot* h = &T.acct_hot[pos];
+        const u64 a = h->id_lo, b = h->id_hi;
         if (a == lo && b == hi) return (u32)pos;
         if ((a | b) == 0) return TB_NOT_FOUND;
-        pos = (pos + 1) & mask;
+        pos = (pos + 1) & T.account_mask;
     }
-    return TB_NOT_FOUND;
-}
-
-__device__ static inline u32 tb_account_find(const Tables& T, u64 lo, u64 hi) {
-    return tb_find(T.accounts, T.account_mask, lo, hi);
-}
-
-__device__ static inline u32 tb_transfer_find(const Tables& T, u64 lo, u64 hi) {
-    return tb_find(T.transfers, T.transfer_mask, lo, hi);
-}
-
-// Tombstone a slot (id = maxInt), keeping its timestamp so it is never reclaimed.
-template <typename R>
-__device__ static inline void tb_tombstone(R* rec) {
-    u64* w = (u64*)rec;
-    w[0] = ~0ULL;
-    w[1] = ~0ULL;
-}
-
-// Claim an empty slot for a key that is known to be absent; CAS the timestamp word 0 -> ts.
-__device__ static inline u32 tb_claim_slot(u64* ts_word0, size_t stride_words, u64 mask, u64 hash, u64 ts,
-                                           Globals* g) {
-    u64 pos = hash & mask;
-    for (u64 n = 0; n <= mask; n++) {
-        u64* w = ts_word0 + pos * stride_words;
-        if (*(volatile u64*)w == 0) {
-            if (atomicCAS((unsigned long long*)w, 0ULL, (unsigned long long)ts) == 0ULL) return (u32)pos;
-        }
-        pos = (pos + 1) & mask;
-    }
-    tb_panic(g, PANIC_TABLE_FULL);
     return TB_NOT_FOUND;
 }
 
 __device__ static inline u32 tb_account_claim(const Tables& T, u64 lo, u64 hi, u64 ts) {
-    return tb_claim_slot((u64*)&T.accounts[0].timestamp, sizeof(Account) / 8, T.account_mask,
-                         tb_hash_id(lo, hi), ts, T.g);
+    u64 pos = tb_hash_id(lo, hi) & T.account_mask;
+    for (u64 n = 0; n <= T.account_mask; n++) {
+        u64* w = &T.acct_hot[pos].timestamp;
+        if (*(volatile u64*)w == 0 &&
+            atomicCAS((unsigned long long*)w, 0ULL, (unsigned long long)ts) == 0ULL) {
+            return (u32)pos;
+        }
+        pos = (pos + 1) & T.account_mask;
+    }
+    tb_panic(T.g, PANIC_TABLE_FULL);
+    return TB_NOT_FOUND;
 }
 
-__device__ static inline u32 tb_transfer_claim(const Tables& T, u64 lo, u64 hi, u64 ts) {
-    return tb_claim_slot((u64*)&T.transfers[0].timestamp, sizeof(Transfer) / 8, T.transfer_mask,
-                         tb_hash_id(lo, hi), ts, T.g);
+__device__ static inline void tb_account_tombstone(const Tables& T, u32 slot) {
+    T.acct_hot[slot].id_lo = ~0ULL;
+    T.acct_hot[slot].id_hi = ~0ULL;
+}
+
+__device__ static inline Account tb_account_load(const Tables& T, u32 slot) {
+    const AccountHot h = T.acct_hot[slot];
+    const AccountBal b = T.acct_bal[slot];
+    const AccountCold c = T.acct_cold[slot];
+    Account a;
+    a.id = tb_u128(h.id_lo, h.id_hi);
+    a.debits_pending = b.debits_pending;
+    a.debits_posted = b.debits_posted;
+    a.credits_pending = b.credits_pending;
+    a.credits_posted = b.credits_posted;
+    a.user_data_128 = c.user_data_128;
+    a.user_data_64 = c.user_data_64;
+    a.user_data_32 = c.user_data_32;
+    a.reserved = c.reserved;
+    a.ledger = h.ledger;
+    a.code = h.code;
+    a.flags = h.flags;
+    a.timestamp = h.timestamp;
+    return a;
+}
+
+// Write every field of a claimed slot (the timestamp word was set by the claim).
+__device__ static inline void tb_account_store_new(const Tables& T, u32 slot, const Account& a) {
+    AccountCold c;
+    c.user_data_128 = a.user_data_128;
+    c.user_data_64 = a.user_data_64;
+    c.user_data_32 = a.user_data_32;
+    c.reserved = a.reserved;
+    T.acct_cold[slot] = c;
+    AccountBal b;
+    b.debits_pending = a.debits_pending;
+    b.debits_posted = a.debits_posted;
+    b.credits_pending = a.credits_pending;
+    b.credits_posted = a.credits_posted;
+    T.acct_bal[slot] = b;
+    AccountHot* h = &T.acct_hot[slot];
+    h->ledger = a.ledger;
+    h->code = a.code;
+    h->flags = a.flags;
+    h->id_lo = tb_lo(a.id);
+    h->id_hi = tb_hi(a.id);
+}
+
+// ---- transfers ----------------------------------------------------------------------------------
+__host__ __device__ static inline u64 tb_fingerprint(u64 lo, u64 hi) {
+    const u64 f = tb_mix64(hi ^ tb_mix64(lo ^ 0x6a09e667f3bcc909ULL));
+    return f ? f : 1;
+}
+
+__device__ static inline u32 tb_xi_pos(u64 word1) { return (u32)word1 - 1; }
+
+// Find a live transfer; returns its log position or TB_NOT_FOUND.  Entries whose claim is still
+// in flight (word1 == 0) only exist for ids claimed by the running kernel; they are skipped.
+__device__ static inline u32 tb_transfer_find(const Tables& T, u64 lo, u64 hi) {
+    if (tb_id_reserved(lo, hi)) return TB_NOT_FOUND;
+    const u64 fp = tb_fingerprint(lo, hi);
+    u64 pos = tb_hash_id(lo, hi) & T.xidx_mask;
+    for (u64 n = 0; n <= T.xidx_mask; n++) {
+        const XIndex e = T.xidx[pos];
+        if (e.fp == 0) return TB_NOT_FOUND;
+        if (e.fp == fp && !(e.word1 & XI_TOMB) && (u32)e.word1 != 0) {
+            const u32 lp = tb_xi_pos(e.word1);
+            const u64* idw = (const u64*)&T.xlog[lp];
+            if (idw[0] == lo && idw[1] == hi) return lp;
+        }
+        pos = (pos + 1) & T.xidx_mask;
+    }
+    return TB_NOT_FOUND;
+}
+
+enum : u32 { CLAIM_NEW = 0, CLAIM_EXISTS = 1, CLAIM_COLLIDED = 2, CLAIM_FULL = 3 };
+
+// Find-or-claim for `id` at log position `log_pos`.
+//  CLAIM_EXISTS:   a live record from an earlier pass has this id (*found = its log position)
+//  CLAIM_COLLIDED: another event of this pass (log position >= pass_base, or claim in flight)
+//                  holds the same fingerprint — both events become dependent (the holder's entry
+//                  gets XI_DUP)
+//  CLAIM_NEW:      entry claimed (*entry = index position); the caller writes the record
+__device__ static inline u32 tb_transfer_claim(const Tables& T, u64 lo, u64 hi, u32 log_pos, u64 pass_base,
+                                               u32* found, u32* entry) {
+    const u64 fp = tb_fingerprint(lo, hi);
+    u64 pos = tb_hash_id(lo, hi) & T.xidx_mask;
+    for (u64 n = 0; n <= T.xidx_mask; n++) {
+        XIndex* e = &T.xidx[pos];
+        u64 cur = *(volatile u64*)&e->fp;
+        if (cur == 0) {
+            cur = atomicCAS((unsigned long long*)&e->fp, 0ULL, (unsigned long long)fp);
+            if (cur == 0) {
+                // OR, not store: a colliding event may already have set XI_DUP on this entry.
+                atomicOr((unsigned long long*)&e->word1, (unsigned long long)log_pos + 1);
+                *entry = (u32)pos;
+                return CLAIM_NEW;
+            }
+        }
+        if (cur == fp) {
+            const u64 w1 = *(volatile u64*)&e->word1;
+            if (!(w1 & XI_TOMB)) {
+                const u32 lo32 = (u32)w1;
+                if (lo32 == 0 || (u64)tb_xi_pos(w1) >= pass_base) {
+                    atomicOr((unsigned long long*)&e->word1, (unsigned long long)XI_DUP);
+                    return CLAIM_COLLIDED;
+                }
+                const u32 lp = tb_xi_pos(w1);
+                const u64* idw = (const u64*)&T.xlog[lp];
+                if (idw[0] == lo && idw[1] == hi) {
+                    *found = lp;
+                    return CLAIM_EXISTS;
+                }
+            }
+        }
+        pos = (pos + 1) & T.xidx_mask;
+    }
+    tb_panic(T.g, PANIC_TABLE_FULL);
+    return CLAIM_FULL;
+}
+
+// Did any event of the current pass (log positions >= pass_base) claim this id — whether its
+// entry is live, withdrawn (tombstoned) or still in flight?  Fingerprint-level, so conservative.
+__device__ static inline bool tb_transfer_claimed_in_pass(const Tables& T, u64 lo, u64 hi, u64 pass_base) {
+    if (tb_id_reserved(lo, hi)) return false;
+    const u64 fp = tb_fingerprint(lo, hi);
+    u64 pos = tb_hash_id(lo, hi) & T.xidx_mask;
+    for (u64 n = 0; n <= T.xidx_mask; n++) {
+        const XIndex e = T.xidx[pos];
+        if (e.fp == 0) return false;
+        if (e.fp == fp && ((u32)e.word1 == 0 || (u64)tb_xi_pos(e.word1) >= pass_base)) return true;
+        pos = (pos + 1) & T.xidx_mask;
+    }
+    return true;
+}
+
+__device__ static inline void tb_xindex_tombstone(const Tables& T, u32 entry) {
+    atomicOr((unsigned long long*)&T.xidx[entry].word1, (unsigned long long)XI_TOMB);
 }
 
 // In-place u128 atomic add (mod 2^128) on a balance field: exact for any interleaving because
@@ -304,6 +453,18 @@ __device__ static inline bool tb_dedup_insert(u64* table, u64 mask, u64 key) {
             if (!(cur & DEDUP_DUP)) atomicOr((unsigned long long*)&table[pos], (unsigned long long)DEDUP_DUP);
             return true;
         }
+        pos = (pos + 1) & mask;
+    }
+    return true;
+}
+
+// True when `key` is in the set (inserted by anyone).
+__device__ static inline bool tb_dedup_is_dup_or_present(const u64* table, u64 mask, u64 key) {
+    u64 pos = tb_mix64(key) & mask;
+    for (u64 n = 0; n <= mask; n++) {
+        const u64 cur = table[pos];
+        if (cur == 0) return false;
+        if ((cur & ~DEDUP_DUP) == key) return true;
         pos = (pos + 1) & mask;
     }
     return true;
