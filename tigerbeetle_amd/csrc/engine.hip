@@ -154,7 +154,8 @@ static int engine_clear(tbgpu* E) {
     HIPCK(hipMemsetAsync(E->T.acct_bal, 0, E->account_cap * sizeof(AccountBal), E->stream));
     HIPCK(hipMemsetAsync(E->T.acct_cold, 0, E->account_cap * sizeof(AccountCold), E->stream));
     HIPCK(hipMemsetAsync(E->T.account_mark, 0, E->account_cap * sizeof(u32), E->stream));
-    HIPCK(hipMemsetAsync(E->T.xidx, 0, E->xidx_cap * sizeof(XIndex), E->stream));
+    HIPCK(hipMemsetAsync(E->T.xidx, 0, E->xidx_cap * sizeof(u64), E->stream));
+    HIPCK(hipMemsetAsync(E->T.xdup, 0, E->xidx_cap, E->stream));
     HIPCK(hipMemsetAsync(E->T.xposted, 0, E->xlog_cap, E->stream));
     E->log_next = 0;
     HIPCK(hipMemsetAsync(E->g, 0, sizeof(Globals), E->stream));
@@ -214,7 +215,7 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     size_t free_b = 0, total_b = 0;
     INIT_CK(hipMemGetInfo(&free_b, &total_b));
     const u64 need = E->account_cap * (sizeof(Account) + 4) + E->xlog_cap * (sizeof(Transfer) + 1) +
-                     E->xidx_cap * sizeof(XIndex) +
+                     E->xidx_cap * (sizeof(u64) + 1) +
                      (u64)E->pe_max * (4 * 4 + 8 * 4 + 128 + 8 + 4) + E->dedup_cap * 8;
     if (need > free_b) {
         st = fail(TBGPU_STATUS_INVALID, "tbgpu_init: needs %llu bytes of HBM, %llu free",
@@ -227,7 +228,8 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     INIT_CK(hipMalloc(&E->T.acct_bal, E->account_cap * sizeof(AccountBal)));
     INIT_CK(hipMalloc(&E->T.acct_cold, E->account_cap * sizeof(AccountCold)));
     INIT_CK(hipMalloc(&E->T.account_mark, E->account_cap * sizeof(u32)));
-    INIT_CK(hipMalloc(&E->T.xidx, E->xidx_cap * sizeof(XIndex)));
+    INIT_CK(hipMalloc(&E->T.xidx, E->xidx_cap * sizeof(u64)));
+    INIT_CK(hipMalloc(&E->T.xdup, E->xidx_cap));
     INIT_CK(hipMalloc(&E->T.xlog, E->xlog_cap * sizeof(Transfer)));
     INIT_CK(hipMalloc(&E->T.xposted, E->xlog_cap));
     INIT_CK(hipMalloc(&E->g, sizeof(Globals)));
@@ -275,7 +277,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
     if (!E) return;
     (void)hipSetDevice(E->device);
     if (E->stream) (void)hipStreamSynchronize(E->stream);
-    void* bufs[] = {E->T.acct_hot, E->T.acct_bal, E->T.acct_cold, E->T.account_mark, E->T.xidx, E->T.xlog,
+    void* bufs[] = {E->T.acct_hot, E->T.acct_bal, E->T.acct_cold, E->T.account_mark, E->T.xidx, E->T.xdup, E->T.xlog,
                     E->T.xposted, E->g, E->info, E->eflags, E->dr,
                     E->cr, E->ps, E->rs, E->dep_list, E->dep_count, E->amt, E->kid, E->kpid, E->dedup,
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
@@ -800,7 +802,8 @@ extern "C" int tbgpu_bench_reset_transfers(tbgpu_t* E) {
         int st = engine_sync(E);
         if (st) return st;
     }
-    HIPCK(hipMemsetAsync(E->T.xidx, 0, E->xidx_cap * sizeof(XIndex), E->stream));
+    HIPCK(hipMemsetAsync(E->T.xidx, 0, E->xidx_cap * sizeof(u64), E->stream));
+    HIPCK(hipMemsetAsync(E->T.xdup, 0, E->xidx_cap, E->stream));
     HIPCK(hipMemsetAsync(E->T.xposted, 0, E->xlog_cap, E->stream));
     hipLaunchKernelGGL(tb_zero_balances, dim3((unsigned)((E->account_cap + 255) / 256)), dim3(256), 0, E->stream, E->T,
                        E->account_cap);

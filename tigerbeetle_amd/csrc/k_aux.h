@@ -38,9 +38,9 @@ __global__ void tb_export_transfers(Tables T, u64 first, u64 n, u8* out, u64* co
                                     u64* posted_count) {
     const u64 i = first + (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= first + n) return;
-    const XIndex e = T.xidx[i];
-    if (e.fp == 0 || (u32)e.word1 == 0 || (e.word1 & XI_TOMB)) return;
-    const u32 pos = tb_xi_pos(e.word1);
+    const u64 e = T.xidx[i];
+    if (e == 0 || (e & XI_TOMB)) return;
+    const u32 pos = tb_xi_pos(e);
     const Transfer& t = T.xlog[pos];
     const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
     *(Transfer*)(out + k * 128) = t;

@@ -83,21 +83,14 @@ __device__ static inline void rp_balance_update(Replay& R, u32 slot, const Accou
 
 // Insert a transfer record at the event's own log position (after an exact find said "absent").
 __device__ static inline void rp_transfer_insert(Replay& R, const Transfer& t, u32 log_pos) {
-    const Tables& T = R.T;
-    const u64 fp = tb_fingerprint(tb_lo(t.id), tb_hi(t.id));
-    u64 pos = tb_hash_id(tb_lo(t.id), tb_hi(t.id)) & T.xidx_mask;
-    for (u64 n = 0; n <= T.xidx_mask; n++) {
-        XIndex* e = &T.xidx[pos];
-        if (e->fp == 0 && atomicCAS((unsigned long long*)&e->fp, 0ULL, (unsigned long long)fp) == 0ULL) {
-            T.xlog[log_pos] = t;
-            atomicOr((unsigned long long*)&e->word1, (unsigned long long)log_pos + 1);
-            T.g->transfer_count++;
-            rp_push(R, UNDO_TRANSFER_INSERT, (u32)pos, nullptr);
-            return;
-        }
-        pos = (pos + 1) & T.xidx_mask;
+    R.T.xlog[log_pos] = t;
+    const u32 entry = tb_transfer_claim_new(R.T, tb_lo(t.id), tb_hi(t.id), log_pos);
+    if (entry == TB_NOT_FOUND) {
+        R.failed = true;
+        return;
     }
-    rp_panic(R, PANIC_TABLE_FULL);
+    R.T.g->transfer_count++;
+    rp_push(R, UNDO_TRANSFER_INSERT, entry, nullptr);
 }
 
 __device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t, u32 log_pos) {

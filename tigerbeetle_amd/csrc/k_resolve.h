@@ -120,7 +120,7 @@ __device__ static inline bool tb_classify(const PassArgs& P, u32 pe, u32 info, u
     }
     if (info & HZ_SELFDEP) return true;
     if (any_dup) {
-        if ((info & HZ_SPEC) && (T.xidx[P.rs[pe]].word1 & XI_DUP)) return true;
+        if ((info & HZ_SPEC) && T.xdup[P.rs[pe]]) return true;
         if ((info & HZ_PV_KEY) && tb_dedup_is_dup(P.dedup, P.dedup_mask, P.kpid[pe])) return true;
     }
     if (any_pv) {

@@ -65,11 +65,17 @@ __device__ static inline u32 tb_post_void_exists(const Transfer& t, const Transf
 // speculative index claim.  Returns R_OK (claimed, record to be written by the caller),
 // a pseudo "exists" marker via *exists_pos, or CLAIM_COLLIDED (dependent).
 __device__ static inline u32 tb_claim_id(const PassArgs& P, const Transfer& t, u32 pe, TransferScratch& s,
-                                         u32* exists_pos) {
+                                         u32* exists_pos, u64 first = ~0ULL) {
     s.kid = tb_dedup_key(tb_lo(t.id), tb_hi(t.id));
     if (P.ablate & ABL_SPEC) return CLAIM_NEW;
     u32 entry = TB_NOT_FOUND;
-    const u32 r = tb_transfer_claim(P.T, tb_lo(t.id), tb_hi(t.id), P.log_base + pe, P.log_base, exists_pos, &entry);
+    if (P.ablate & ABL_CAS) {  // timing only: no atomic claim
+        s.rs = (u32)(tb_hash_id(tb_lo(t.id), tb_hi(t.id)) & P.T.xidx_mask);
+        s.hz |= HZ_SPEC;
+        return CLAIM_NEW;
+    }
+    const u32 r = tb_transfer_claim(P.T, tb_lo(t.id), tb_hi(t.id), P.log_base + pe, P.log_base, exists_pos, &entry,
+                                    first);
     if (r == CLAIM_NEW) {
         s.rs = entry;
         s.hz |= HZ_SPEC;
@@ -198,12 +204,22 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     if (t.ledger == 0) return CT_LEDGER_MUST_NOT_BE_ZERO;
     if (t.code == 0) return CT_CODE_MUST_NOT_BE_ZERO;
 
-    // Both probes are issued before either result is consumed.
+    // The first probe of both accounts and of the id index entry are independent loads: issue them
+    // together, before any result is consumed.
+    const u64 dlo = tb_lo(t.debit_account_id), dhi = tb_hi(t.debit_account_id);
+    const u64 clo = tb_lo(t.credit_account_id), chi = tb_hi(t.credit_account_id);
+    const u64 dpos = tb_hash_id(dlo, dhi) & T.account_mask;
+    const u64 cpos = tb_hash_id(clo, chi) & T.account_mask;
+    const u64 xpos = tb_hash_id(tb_lo(t.id), tb_hi(t.id)) & T.xidx_mask;
     const bool fake = P.ablate & ABL_ACCTS;
-    const u32 drs = fake ? (u32)(tb_lo(t.debit_account_id) & 1023)
-                         : tb_account_find(T, tb_lo(t.debit_account_id), tb_hi(t.debit_account_id));
-    const u32 crs = fake ? (u32)(tb_lo(t.credit_account_id) & 1023)
-                         : tb_account_find(T, tb_lo(t.credit_account_id), tb_hi(t.credit_account_id));
+    AccountHot d0 = {}, c0 = {};
+    if (!fake) {
+        d0 = T.acct_hot[dpos];
+        c0 = T.acct_hot[cpos];
+    }
+    const u64 x0 = (P.ablate & (ABL_SPEC | ABL_CAS)) ? ~0ULL : T.xidx[xpos];
+    const u32 drs = fake ? (u32)(dlo & 1023) : tb_account_find_from(T, dlo, dhi, dpos, d0);
+    const u32 crs = fake ? (u32)(clo & 1023) : tb_account_find_from(T, clo, chi, cpos, c0);
     if (drs == TB_NOT_FOUND) return CT_DEBIT_ACCOUNT_NOT_FOUND;
     if (crs == TB_NOT_FOUND) return CT_CREDIT_ACCOUNT_NOT_FOUND;
     const AccountHot dr = T.acct_hot[drs];
@@ -231,7 +247,7 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
 
     // The existence check of `id` (:824) fused with the speculative claim of its index entry.
     u32 es = TB_NOT_FOUND;
-    const u32 claim = tb_claim_id(P, t, pe, s, &es);
+    const u32 claim = tb_claim_id(P, t, pe, s, &es, x0);
     if (claim == CLAIM_EXISTS) return tb_transfer_exists(t, T.xlog[es]);
     if (claim == CLAIM_COLLIDED || balancing) return R_OK;  // dependent: the replay decides
 
@@ -240,10 +256,10 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     // then the timeout check (:862) is the next possible failure.
     const u64 timeout_ns = (u64)t.timeout * 1000000000ULL;
     if (ts + timeout_ns < ts) return CT_OVERFLOWS_TIMEOUT;  // entry withdrawn by kernel 2
-    if (s.hz & HZ_SPEC) {
+    if ((s.hz & HZ_SPEC) && !(P.ablate & ABL_RECORD)) {
         Transfer r = t;
         r.timestamp = ts;
-        T.xlog[P.log_base + pe] = r;
+        tb_store_record(&T.xlog[P.log_base + pe], r, P.ablate & EXP_NT);
     }
     return R_OK;
 }
@@ -252,17 +268,18 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
 __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassArgs P) {
     __shared__ __attribute__((aligned(16))) u8 stage[VALIDATE_THREADS * STAGE_STRIDE];
     __shared__ u64 s_sum[2 * (VALIDATE_THREADS / 64)];
+    __shared__ u32 s_range[2];
 
     const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
     const u32 count = min((u32)VALIDATE_THREADS, P.n - tile0);
-    tb_stage_events(P.events + (P.e0 + tile0) * 128, count, stage);
+    tb_stage_events(P.events + (P.e0 + tile0) * 128, count, stage, P.ablate & EXP_NT);
 
     const u32 pe = tile0 + threadIdx.x;  // pass-relative event
+    const u64 e = P.e0 + pe;
+    const u32 b = tb_tile_batch(P, P.e0 + tile0, count, e, s_range);
     TransferScratch s;
     if (threadIdx.x < count) {
         const Transfer t = tb_read_staged<Transfer>(stage);
-        const u64 e = P.e0 + pe;
-        const u32 b = tb_batch_of(P, e);
         const u32 L = (u32)(P.batch_off[b + 1] - P.batch_off[b]);
         const u32 j = (u32)(e - P.batch_off[b]);
         u32 code;
@@ -333,15 +350,16 @@ __device__ static inline u32 tb_account_stateless(const Account& a) {
 // Kernel 1 (create_accounts).
 __global__ __launch_bounds__(VALIDATE_THREADS) void tb_accounts_validate(PassArgs P) {
     __shared__ __attribute__((aligned(16))) u8 stage[VALIDATE_THREADS * STAGE_STRIDE];
+    __shared__ u32 s_range[2];
     const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
     const u32 count = min((u32)VALIDATE_THREADS, P.n - tile0);
     tb_stage_events(P.events + (P.e0 + tile0) * 128, count, stage);
+    const u32 pe = tile0 + threadIdx.x;
+    const u64 e = P.e0 + pe;
+    const u32 b = tb_tile_batch(P, P.e0 + tile0, count, e, s_range);
     if (threadIdx.x >= count) return;
 
-    const u32 pe = tile0 + threadIdx.x;
     const Account a = tb_read_staged<Account>(stage);
-    const u64 e = P.e0 + pe;
-    const u32 b = tb_batch_of(P, e);
     const u32 L = (u32)(P.batch_off[b + 1] - P.batch_off[b]);
     const u32 j = (u32)(e - P.batch_off[b]);
     u32 code, hz = 0;

@@ -66,33 +66,56 @@ struct PassArgs {
     u32 ablate;            // timing-only ablation bits (TBGPU_ABLATE env, never in a parity run)
 };
 
-enum : u32 { ABL_DEDUP = 1, ABL_SPEC = 2, ABL_ACCTS = 4, ABL_XFIND = 8, ABL_STAGE = 16 };
+enum : u32 { ABL_DEDUP = 1, ABL_SPEC = 2, ABL_ACCTS = 4, ABL_XFIND = 8, ABL_STAGE = 16, ABL_RECORD = 32, ABL_CAS = 64, EXP_NT = 128 };
 
-// Batch of a call-relative event index (binary search over batch_off[b0..b1]).
-__device__ static inline u32 tb_batch_of(const PassArgs& P, u64 e) {
-    u32 lo = P.b0, hi = P.b1;  // invariant: off[lo] <= e < off[hi]
+// Batch of a call-relative event index: binary search over batch_off[lo..hi) (off[lo] <= e < off[hi]).
+__device__ static inline u32 tb_batch_search(const u64* off, u32 lo, u32 hi, u64 e) {
     while (hi - lo > 1) {
         const u32 mid = (lo + hi) >> 1;
-        if (P.batch_off[mid] <= e) lo = mid; else hi = mid;
+        if (off[mid] <= e) lo = mid; else hi = mid;
     }
     return lo;
+}
+
+// Batch of every event of a VALIDATE_THREADS tile: one lane searches for the tile's first and last
+// events, then each lane searches only that (usually one- or two-batch) range.
+__device__ static inline u32 tb_tile_batch(const PassArgs& P, u64 e_first, u32 count, u64 e, u32* s_range) {
+    if (threadIdx.x == 0) {
+        s_range[0] = tb_batch_search(P.batch_off, P.b0, P.b1, e_first);
+        s_range[1] = tb_batch_search(P.batch_off, s_range[0], P.b1, e_first + count - 1) + 1;
+    }
+    __syncthreads();
+    return tb_batch_search(P.batch_off, s_range[0], s_range[1], e);
 }
 
 // Stage VALIDATE_THREADS 128-byte events through LDS with 16-byte coalesced loads; row stride
 // 144 B so the per-lane ds_read_b128 of one record is bank-conflict free.
 #define STAGE_STRIDE 144
-__device__ static inline void tb_stage_events(const u8* src, u32 count, u8* lds) {
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ static inline void tb_stage_events(const u8* src, u32 count, u8* lds, bool nt = false) {
     const u32 t = threadIdx.x;
 #pragma unroll
     for (u32 r = 0; r < 8; r++) {
         const u32 c = t + r * VALIDATE_THREADS;  // 16-byte chunk index within the tile
         const u32 ev = c >> 3, part = c & 7;
         if (ev < count) {
-            const uint4 v = *(const uint4*)(src + (u64)c * 16);
-            *(uint4*)(lds + ev * STAGE_STRIDE + part * 16) = v;
+            const u32x4* g = (const u32x4*)(src + (u64)c * 16);
+            const u32x4 v = nt ? __builtin_nontemporal_load(g) : *g;
+            *(u32x4*)(lds + ev * STAGE_STRIDE + part * 16) = v;
         }
     }
     __syncthreads();
+}
+
+// 128-byte record store, optionally non-temporal (streamed once, keep it out of the caches).
+template <typename R>
+__device__ static inline void tb_store_record(R* dst, const R& r, bool nt) {
+    if (nt) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) __builtin_nontemporal_store(((const u32x4*)&r)[k], ((u32x4*)dst) + k);
+    } else {
+        *dst = r;
+    }
 }
 
 template <typename R>

@@ -166,12 +166,12 @@ __device__ static inline u128 tb_sat_add(u128 a, u128 b) {
 //   always >= 1), then write the id.
 //
 // Transfers: an append LOG of 128-byte records — event e of a pass is written at log position
-// pass_base + e, so kernel 1 stores records fully coalesced — plus a 16-byte INDEX entry per
-// record {fingerprint u64 (0 = empty), word1 = (log position + 1) | state << 32}.  A probe compares
-// fingerprints and confirms a match against the log record's id.  An index entry is claimed with a
-// CAS of its fingerprint word; a second event of the same pass with the same id meets the claimed
-// fingerprint on its probe path (or loses the CAS to it) — that is how same-pass duplicate ids are
-// detected, with no separate dedup set.  Withdrawn entries get the TOMB state.
+// pass_base + e, so kernel 1 stores records fully coalesced — plus an 8-byte INDEX entry per
+// record: {fingerprint32 (never 0) << 32 | (log position + 1)}, 0 = empty, bit 31 of the low word
+// = TOMB (withdrawn).  One 64-bit CAS publishes a whole entry.  A probe compares fingerprints and
+// confirms a match against the log record's id.  A second event of the same pass with the same id
+// meets the claimed fingerprint on its probe path (or loses the CAS to it) — that is how same-pass
+// duplicate ids are detected, with no separate dedup set.
 // ------------------------------------------------------------------------------------------------
 struct Globals {
     u64 commit_timestamp;     // max timestamp of an event that returned ok when evaluated
@@ -210,12 +210,8 @@ static_assert(sizeof(AccountHot) == 32 && sizeof(AccountBal) == 64 && sizeof(Acc
 #define BAL_OFF_CREDITS_PENDING 32
 #define BAL_OFF_CREDITS_POSTED 48
 
-struct XIndex {
-    u64 fp;     // fingerprint of the id, never 0; 0 = empty entry
-    u64 word1;  // (log position + 1) in the low 32 bits (0 = claim in flight), state in the high 32
-};
-#define XI_DUP (1ULL << 32)   // another event of the same pass claimed this id too
-#define XI_TOMB (2ULL << 32)  // withdrawn (failed / dependent / rolled back)
+#define XI_TOMB (1ULL << 31)  // withdrawn (failed / dependent / rolled back)
+#define XI_POS_MASK 0x7FFFFFFFULL
 
 struct Tables {
     AccountHot* acct_hot;     // [account_cap]
@@ -223,7 +219,8 @@ struct Tables {
     AccountCold* acct_cold;   // [account_cap]
     u32* account_mark;        // [account_cap] pass epoch of the last balancing mark
     u64 account_mask;         // account_cap - 1
-    XIndex* xidx;             // [xidx_cap]
+    u64* xidx;                // [xidx_cap] index entries
+    u8* xdup;                 // [xidx_cap] 1: another event of the claiming pass met this entry
     u64 xidx_mask;
     Transfer* xlog;           // [xlog_cap]
     u8* xposted;              // [xlog_cap] POSTED_* of the pending transfer at that log position
@@ -244,6 +241,21 @@ __device__ static inline u32 tb_account_find(const Tables& T, u64 lo, u64 hi) {
     if (tb_id_reserved(lo, hi)) return TB_NOT_FOUND;
     u64 pos = tb_hash_id(lo, hi) & T.account_mask;
     for (u64 n = 0; n <= T.account_mask; n++) {
+        const AccountHot* h = &T.acct_hot[pos];
+        const u64 a = h->id_lo, b = h->id_hi;
+        if (a == lo && b == hi) return (u32)pos;
+        if ((a | b) == 0) return TB_NOT_FOUND;
+        pos = (pos + 1) & T.account_mask;
+    }
+    return TB_NOT_FOUND;
+}
+
+// Continue an account probe whose first entry (at `pos`) was already loaded.
+__device__ static inline u32 tb_account_find_from(const Tables& T, u64 lo, u64 hi, u64 pos, const AccountHot& first) {
+    if (first.id_lo == lo && first.id_hi == hi) return (u32)pos;
+    if ((first.id_lo | first.id_hi) == 0 || tb_id_reserved(lo, hi)) return TB_NOT_FOUND;
+    pos = (pos + 1) & T.account_mask;
+    for (u64 n = 1; n <= T.account_mask; n++) {
         const AccountHot* h = &T.acct_hot[pos];
         const u64 a = h->id_lo, b = h->id_hi;
         if (a == lo && b == hi) return (u32)pos;
@@ -321,19 +333,19 @@ __host__ __device__ static inline u64 tb_fingerprint(u64 lo, u64 hi) {
     return f ? f : 1;
 }
 
-__device__ static inline u32 tb_xi_pos(u64 word1) { return (u32)word1 - 1; }
+__host__ __device__ static inline u64 tb_fp32(u64 lo, u64 hi) { return (tb_fingerprint(lo, hi) >> 32) | 1; }
+__device__ static inline u32 tb_xi_pos(u64 e) { return (u32)((e & XI_POS_MASK) - 1); }
 
-// Find a live transfer; returns its log position or TB_NOT_FOUND.  Entries whose claim is still
-// in flight (word1 == 0) only exist for ids claimed by the running kernel; they are skipped.
+// Find a live transfer; returns its log position or TB_NOT_FOUND.
 __device__ static inline u32 tb_transfer_find(const Tables& T, u64 lo, u64 hi) {
     if (tb_id_reserved(lo, hi)) return TB_NOT_FOUND;
-    const u64 fp = tb_fingerprint(lo, hi);
+    const u64 fp = tb_fp32(lo, hi);
     u64 pos = tb_hash_id(lo, hi) & T.xidx_mask;
     for (u64 n = 0; n <= T.xidx_mask; n++) {
-        const XIndex e = T.xidx[pos];
-        if (e.fp == 0) return TB_NOT_FOUND;
-        if (e.fp == fp && !(e.word1 & XI_TOMB) && (u32)e.word1 != 0) {
-            const u32 lp = tb_xi_pos(e.word1);
+        const u64 e = T.xidx[pos];
+        if (e == 0) return TB_NOT_FOUND;
+        if ((e >> 32) == fp && !(e & XI_TOMB)) {
+            const u32 lp = tb_xi_pos(e);
             const u64* idw = (const u64*)&T.xlog[lp];
             if (idw[0] == lo && idw[1] == hi) return lp;
         }
@@ -346,40 +358,36 @@ enum : u32 { CLAIM_NEW = 0, CLAIM_EXISTS = 1, CLAIM_COLLIDED = 2, CLAIM_FULL = 3
 
 // Find-or-claim for `id` at log position `log_pos`.
 //  CLAIM_EXISTS:   a live record from an earlier pass has this id (*found = its log position)
-//  CLAIM_COLLIDED: another event of this pass (log position >= pass_base, or claim in flight)
-//                  holds the same fingerprint — both events become dependent (the holder's entry
-//                  gets XI_DUP)
+//  CLAIM_COLLIDED: another event of this pass (log position >= pass_base) holds the same
+//                  fingerprint — both events become dependent (xdup[] marks the holder's entry;
+//                  kernel 2 reads it)
 //  CLAIM_NEW:      entry claimed (*entry = index position); the caller writes the record
+// `first` is the home entry if the caller already loaded it, else ~0.
 __device__ static inline u32 tb_transfer_claim(const Tables& T, u64 lo, u64 hi, u32 log_pos, u64 pass_base,
-                                               u32* found, u32* entry) {
-    const u64 fp = tb_fingerprint(lo, hi);
+                                               u32* found, u32* entry, u64 first = ~0ULL) {
+    const u64 fp = tb_fp32(lo, hi);
+    const u64 mine = (fp << 32) | ((u64)log_pos + 1);
     u64 pos = tb_hash_id(lo, hi) & T.xidx_mask;
     for (u64 n = 0; n <= T.xidx_mask; n++) {
-        XIndex* e = &T.xidx[pos];
-        u64 cur = *(volatile u64*)&e->fp;
+        u64* e = &T.xidx[pos];
+        u64 cur = (n == 0 && first != ~0ULL) ? first : *(volatile u64*)e;
         if (cur == 0) {
-            cur = atomicCAS((unsigned long long*)&e->fp, 0ULL, (unsigned long long)fp);
+            cur = atomicCAS((unsigned long long*)e, 0ULL, (unsigned long long)mine);
             if (cur == 0) {
-                // OR, not store: a colliding event may already have set XI_DUP on this entry.
-                atomicOr((unsigned long long*)&e->word1, (unsigned long long)log_pos + 1);
                 *entry = (u32)pos;
                 return CLAIM_NEW;
             }
         }
-        if (cur == fp) {
-            const u64 w1 = *(volatile u64*)&e->word1;
-            if (!(w1 & XI_TOMB)) {
-                const u32 lo32 = (u32)w1;
-                if (lo32 == 0 || (u64)tb_xi_pos(w1) >= pass_base) {
-                    atomicOr((unsigned long long*)&e->word1, (unsigned long long)XI_DUP);
-                    return CLAIM_COLLIDED;
-                }
-                const u32 lp = tb_xi_pos(w1);
-                const u64* idw = (const u64*)&T.xlog[lp];
-                if (idw[0] == lo && idw[1] == hi) {
-                    *found = lp;
-                    return CLAIM_EXISTS;
-                }
+        if ((cur >> 32) == fp && !(cur & XI_TOMB)) {
+            const u32 lp = tb_xi_pos(cur);
+            if ((u64)lp >= pass_base) {
+                T.xdup[pos] = 1;
+                return CLAIM_COLLIDED;
+            }
+            const u64* idw = (const u64*)&T.xlog[lp];
+            if (idw[0] == lo && idw[1] == hi) {
+                *found = lp;
+                return CLAIM_EXISTS;
             }
         }
         pos = (pos + 1) & T.xidx_mask;
@@ -388,23 +396,36 @@ __device__ static inline u32 tb_transfer_claim(const Tables& T, u64 lo, u64 hi, 
     return CLAIM_FULL;
 }
 
-// Did any event of the current pass (log positions >= pass_base) claim this id — whether its
-// entry is live, withdrawn (tombstoned) or still in flight?  Fingerprint-level, so conservative.
-__device__ static inline bool tb_transfer_claimed_in_pass(const Tables& T, u64 lo, u64 hi, u64 pass_base) {
-    if (tb_id_reserved(lo, hi)) return false;
-    const u64 fp = tb_fingerprint(lo, hi);
+// Claim the first empty entry for an id known to be absent (the ordered replay).
+__device__ static inline u32 tb_transfer_claim_new(const Tables& T, u64 lo, u64 hi, u32 log_pos) {
+    const u64 mine = (tb_fp32(lo, hi) << 32) | ((u64)log_pos + 1);
     u64 pos = tb_hash_id(lo, hi) & T.xidx_mask;
     for (u64 n = 0; n <= T.xidx_mask; n++) {
-        const XIndex e = T.xidx[pos];
-        if (e.fp == 0) return false;
-        if (e.fp == fp && ((u32)e.word1 == 0 || (u64)tb_xi_pos(e.word1) >= pass_base)) return true;
+        u64* e = &T.xidx[pos];
+        if (*e == 0 && atomicCAS((unsigned long long*)e, 0ULL, (unsigned long long)mine) == 0ULL) return (u32)pos;
+        pos = (pos + 1) & T.xidx_mask;
+    }
+    tb_panic(T.g, PANIC_TABLE_FULL);
+    return TB_NOT_FOUND;
+}
+
+// Did any event of the current pass (log positions >= pass_base) claim this id — whether its
+// entry is live or withdrawn (tombstoned)?  Fingerprint-level, so conservative.
+__device__ static inline bool tb_transfer_claimed_in_pass(const Tables& T, u64 lo, u64 hi, u64 pass_base) {
+    if (tb_id_reserved(lo, hi)) return false;
+    const u64 fp = tb_fp32(lo, hi);
+    u64 pos = tb_hash_id(lo, hi) & T.xidx_mask;
+    for (u64 n = 0; n <= T.xidx_mask; n++) {
+        const u64 e = T.xidx[pos];
+        if (e == 0) return false;
+        if ((e >> 32) == fp && (u64)tb_xi_pos(e) >= pass_base) return true;
         pos = (pos + 1) & T.xidx_mask;
     }
     return true;
 }
 
 __device__ static inline void tb_xindex_tombstone(const Tables& T, u32 entry) {
-    atomicOr((unsigned long long*)&T.xidx[entry].word1, (unsigned long long)XI_TOMB);
+    atomicOr((unsigned long long*)&T.xidx[entry], (unsigned long long)XI_TOMB);
 }
 
 // In-place u128 atomic add (mod 2^128) on a balance field: exact for any interleaving because
