@@ -138,8 +138,10 @@ def load_pmc(kernel):
             except (OSError, ValueError):
                 continue
             k = d.get("kernels", {}).get(kernel)
-            if k and "hbm_bytes_per_launch" in k:
-                return k["hbm_bytes_per_launch"]
+            if k and "hbm_bytes_per_launch_raw" in k:
+                return {"bytes_per_launch": round(k["hbm_bytes_per_launch_raw"]), "source": "profiles/" + name,
+                        "counters": "FETCH_SIZE + WRITE_SIZE (raw; FETCH_SIZE may read up to 2x low on gfx950)",
+                        "bytes_per_launch_fetch_x2": round(k["hbm_bytes_per_launch"])}
     return None
 
 
@@ -228,8 +230,8 @@ def main():
     # -- roofline: dominant kernel -----------------------------------------------------------
     kernels = {
         "tb_transfers_validate": (stats["ms_validate"], stats["launches_validate"]),
-        "tb_resolve": (stats["ms_resolve"], stats["launches_resolve"]),
-        "tb_replay": (stats["ms_replay"], stats["launches_replay"]),
+        "tb_resolve<129>": (stats["ms_resolve"], stats["launches_resolve"]),
+        "tb_replay<129>": (stats["ms_replay"], stats["launches_replay"]),
     }
     dom = max(kernels, key=lambda k: kernels[k][0])
     ms_dom, n_dom = kernels[dom]
@@ -241,7 +243,7 @@ def main():
     b_validate = 144 + 128 * u_over_t
     b_resolve = 152 + 128 * u_over_t
     per_launch_transfers = args.transfers / max(1, stats["launches_validate"] / max(1, args.steps))
-    alg_bytes = {"tb_transfers_validate": b_validate, "tb_resolve": b_resolve, "tb_replay": 0.0}[dom] * per_launch_transfers
+    alg_bytes = {"tb_transfers_validate": b_validate, "tb_resolve<129>": b_resolve, "tb_replay<129>": 0.0}[dom] * per_launch_transfers
     roof = None
     if n_dom:
         avg_s = ms_dom / n_dom / 1e3
