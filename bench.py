@@ -237,11 +237,12 @@ def main():
     ms_dom, n_dom = kernels[dom]
     per_pass = pass_events
     u_over_t = expected_unique(args.accounts, 2 * per_pass) / per_pass
-    # B = 296 + 256·U/T per transfer; validate's share reads the event (128),
-    # probes the id (16) and reads each touched account once (128·U/T); resolve's share writes the
-    # record (128), the result slot (8), the id (16) and writes each touched account back (128·U/T).
-    b_validate = 144 + 128 * u_over_t
-    b_resolve = 152 + 128 * u_over_t
+    # B = 296 + 256·U/T per transfer, split by where the work happens:
+    # validate reads the event (128), probes + claims the id (32), writes the record (128) and reads
+    # each touched account once (128·U/T); resolve writes the result slot (8) and each touched
+    # account back (128·U/T).
+    b_validate = 288 + 128 * u_over_t
+    b_resolve = 8 + 128 * u_over_t
     per_launch_transfers = args.transfers / max(1, stats["launches_validate"] / max(1, args.steps))
     alg_bytes = {"tb_transfers_validate": b_validate, "tb_resolve<129>": b_resolve, "tb_replay<129>": 0.0}[dom] * per_launch_transfers
     roof = None
