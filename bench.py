@@ -10,9 +10,12 @@ inputs already resident in HBM.  Between steps the transfer store and balances a
 barrier + torch.cuda.synchronize(); value = transfers committed by all ranks / Σ step time (max
 over ranks).
 
---gpus N (torchrun): one process per GPU; each rank commits its own shard (its own accounts and
-transfers, no cross-shard transfer), so scaling is weak.  The cross-shard all-to-all path of
-BASELINE config C5 is not built yet.
+--gpus N (torchrun): one process per GPU over RCCL (tigerbeetle_amd.sharded).  The
+accounts are replicated (every rank commits the same create_accounts prepares); every rank
+submits its own 100M transfers (global transfer index r*100M + k), and every pass routes each
+transfer to its home GPU (tbgpu_home of its id) with an all-to-all over xGMI, commits it there and
+routes the result codes back.  The global prepare order of a pass is rank-major.  Per-GPU work is
+fixed as N grows: scaling is weak.
 
 The JSON line also carries:
   roofline      the dominant kernel's algorithmic bytes per launch / its average launch time
@@ -52,6 +55,8 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=12_285_000, help="transfers in the CPU baseline / parity sample (0: skip)")
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--profile", type=int, default=1, help="time kernels with HIP events (roofline)")
+    p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (rehearsal on one GPU)")
+    p.add_argument("--same-device", action="store_true", help="rehearsal: every rank on cuda:0")
     return p.parse_args()
 
 
@@ -154,8 +159,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        if args.same_device:
+            local_rank = 0
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(args.dist_backend)
+        return run_sharded(args, world, rank, local_rank)
 
     def barrier():
         if world > 1:
@@ -228,33 +239,9 @@ def main():
     value = n_total / (total_ms / 1e3)
 
     # -- roofline: dominant kernel -----------------------------------------------------------
-    kernels = {
-        "tb_transfers_validate": (stats["ms_validate"], stats["launches_validate"]),
-        "tb_resolve<129>": (stats["ms_resolve"], stats["launches_resolve"]),
-        "tb_replay<129>": (stats["ms_replay"], stats["launches_replay"]),
-    }
-    dom = max(kernels, key=lambda k: kernels[k][0])
-    ms_dom, n_dom = kernels[dom]
-    per_pass = pass_events
-    u_over_t = expected_unique(args.accounts, 2 * per_pass) / per_pass
-    # B = 296 + 256·U/T per transfer, split by where the work happens:
-    # validate reads the event (128), probes + claims the id (32), writes the record (128) and reads
-    # each touched account once (128·U/T); resolve writes the result slot (8) and each touched
-    # account back (128·U/T).
-    b_validate = 288 + 128 * u_over_t
-    b_resolve = 8 + 128 * u_over_t
     per_launch_transfers = args.transfers / max(1, stats["launches_validate"] / max(1, args.steps))
-    alg_bytes = {"tb_transfers_validate": b_validate, "tb_resolve<129>": b_resolve, "tb_replay<129>": 0.0}[dom] * per_launch_transfers
-    roof = None
-    if n_dom:
-        avg_s = ms_dom / n_dom / 1e3
-        achieved = alg_bytes / avg_s / 1e9
-        traffic = load_pmc(dom)
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
-                "avg_launch_ms": round(ms_dom / n_dom, 4), "alg_bytes_per_transfer": round(alg_bytes / per_launch_transfers, 1),
-                "path_bytes_per_transfer": round(296 + 256 * u_over_t, 1),
-                "path_achieved_GBs": round((296 + 256 * u_over_t) * args.transfers * args.steps / (total_ms / 1e3) / 1e9, 1)}
+    u_over_t = expected_unique(args.accounts, 2 * pass_events) / pass_events
+    roof = roofline(stats, u_over_t, per_launch_transfers, args, total_ms)
 
     # -- CPU baseline + bit-exact sample parity (rank 0, N=1 only) ---------------------------
     cpu = None
@@ -305,6 +292,150 @@ def main():
     engine.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def run_sharded(args, world, rank, local_rank):
+    """N>1: the routed multi-GPU commit (clean passes: all-to-all of events to their home GPU)."""
+    import torch
+    import torch.distributed as dist
+
+    from tigerbeetle_amd.sharded import GpuShard, ShardedStateMachine
+    from tigerbeetle_amd.state_machine import Engine, Options
+
+    dev = torch.device("cuda", local_rank)
+    pass_events = args.pass_batches * args.batch
+    # A home receives about 1/N of every rank's pass: size for imbalance.
+    recv_max = int(pass_events * 1.25) + 8192
+    engine = Engine(Options(accounts_max=args.accounts, transfers_max=int(args.transfers * 1.05) + recv_max,
+                            pass_events_max=recv_max, pass_batches_max=recv_max // 8190 + 2, device=local_rank,
+                            profile=bool(args.profile)))
+    backend = GpuShard(engine, world, events_max=pass_events, device=dev)
+    sm = ShardedStateMachine(backend)
+
+    # Accounts: replicated — every rank commits the same prepares (same seed).
+    acct_lens = batches(args.accounts, args.batch)
+    acct_ts, t_end = timestamps(acct_lens, 1_000_000_000)
+    acct = torch.empty((args.accounts, 128), dtype=torch.uint8, device=dev)
+    engine.generate_accounts(acct.data_ptr(), 0, args.accounts, seed=args.seed)
+    res = torch.empty(args.accounts * 2, dtype=torch.int32, device=dev)
+    rb = torch.empty(len(acct_lens), dtype=torch.int32, device=dev)
+    engine.commit_device_async(128, acct_ts, acct_lens, acct.data_ptr(), res.data_ptr(), rb.data_ptr())
+    engine.sync()
+    assert int(rb.sum().item()) == 0, "account creation returned errors"
+    del acct, res, rb
+    sm.commit_timestamp = engine.commit_timestamp
+
+    # Transfers: this rank's share of the global sequence, resident in HBM.
+    events = torch.empty((args.transfers, 128), dtype=torch.uint8, device=dev)
+    engine.generate_transfers(events.data_ptr(), rank * args.transfers, args.transfers, args.accounts, seed=args.seed)
+    engine.sync()
+    lens = batches(args.transfers, args.batch)
+    passes = [lens[i:i + args.pass_batches] for i in range(0, len(lens), args.pass_batches)]
+
+    step_ms = []
+    t_cursor = t_end
+    errors = torch.zeros(1, dtype=torch.int64, device=dev)
+    for step in range(args.warmup + args.steps):
+        timed = step >= args.warmup
+        engine.reset_transfers()
+        if timed and step == args.warmup:
+            engine.reset_stats()
+            sm.passes_clean = sm.passes_dirty = 0
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        off = 0
+        for plens in passes:
+            n = sum(plens)
+            mine = None
+            for r in range(world):  # rank-major global order of the pass
+                ts, t_cursor = timestamps(plens, t_cursor)
+                if r == rank:
+                    mine = ts
+            out = sm.commit(129, mine, plens, events[off:off + n])
+            errors += out.reply_bytes.sum()
+            off += n
+        torch.cuda.synchronize()
+        dist.barrier()
+        dt = time.perf_counter() - t0
+        if timed:
+            t = torch.tensor([dt * 1e3], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            step_ms.append(float(t.item()))
+        t_cursor += 10
+    stats = engine.stats()
+    pass_lat = engine.pass_latencies()
+
+    # Full-run properties: every reply empty, every transfer stored once somewhere, debits == credits.
+    tot = torch.tensor([int(errors.item()), stats["transfers"]], dtype=torch.int64, device=dev)
+    dist.all_reduce(tot)
+    accts = sm.export_accounts()
+    dpost = sum(int(x) for x in accts["debits_posted_lo"]) + (sum(int(x) for x in accts["debits_posted_hi"]) << 64)
+    cpost = sum(int(x) for x in accts["credits_posted_lo"]) + (sum(int(x) for x in accts["credits_posted_hi"]) << 64)
+    full_ok = bool(int(tot[0]) == 0 and int(tot[1]) == args.transfers * world and dpost == cpost and dpost > 0
+                   and sm.passes_dirty == 0)
+
+    total_ms = sum(step_ms)
+    value = args.transfers * world * args.steps / (total_ms / 1e3)
+    recv_per_launch = args.transfers / max(1, stats["launches_validate"] / max(1, args.steps))
+    u_over_t = expected_unique(args.accounts, 2 * recv_per_launch) / recv_per_launch
+    roof = roofline(stats, u_over_t, recv_per_launch, args, total_ms)
+    lat = np.array(pass_lat) if len(pass_lat) else np.array([float("nan")])
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "transfers/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(total_ms / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u128",
+        "data": "synthetic (device-generated, reference benchmark shapes)",
+        "config": {"workload": "C2 per GPU, routed across GPUs (C5 shape): %d replicated accounts, %d uniform "
+                               "transfers submitted per GPU, home GPU = hash(id), prepares of %d"
+                               % (args.accounts, args.transfers, args.batch),
+                   "prepares_per_step": len(lens) * world, "pass_prepares_per_gpu": args.pass_batches,
+                   "parallelism": "route%d (all-to-all over RCCL)" % world},
+        "p99_batch_latency_ms": round(float(np.percentile(lat, 99)), 3),
+        "batch_latency_ms": {"definition": "device time of the home commit pass (rank 0); excludes the all-to-all"},
+        "passes": {"clean": sm.passes_clean, "dirty": sm.passes_dirty},
+        "roofline": roof,
+        "cpu_baseline": None,
+        "parity": {"full_run_properties": full_ok},
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    engine.close()
+    dist.destroy_process_group()
+
+
+def roofline(stats, u_over_t, per_launch_transfers, args, total_ms):
+    kernels = {
+        "tb_transfers_validate": (stats["ms_validate"], stats["launches_validate"]),
+        "tb_resolve<129>": (stats["ms_resolve"], stats["launches_resolve"]),
+        "tb_replay<129>": (stats["ms_replay"], stats["launches_replay"]),
+    }
+    dom = max(kernels, key=lambda k: kernels[k][0])
+    ms_dom, n_dom = kernels[dom]
+    # SURVEY.md §8(d): B = 296 + 256·U/T per transfer, split by where the work happens (DESIGN.md §4):
+    # validate reads the event (128), probes + claims the id (32), writes the record (128) and reads
+    # each touched account once (128·U/T); resolve writes the result slot (8) and each touched
+    # account back (128·U/T).
+    b_validate = 288 + 128 * u_over_t
+    b_resolve = 8 + 128 * u_over_t
+    alg_bytes = {"tb_transfers_validate": b_validate, "tb_resolve<129>": b_resolve, "tb_replay<129>": 0.0}[dom] * per_launch_transfers
+    if not n_dom:
+        return None
+    avg_s = ms_dom / n_dom / 1e3
+    achieved = alg_bytes / avg_s / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc(dom), "kernel": dom,
+            "avg_launch_ms": round(ms_dom / n_dom, 4), "alg_bytes_per_transfer": round(alg_bytes / per_launch_transfers, 1),
+            "path_bytes_per_transfer": round(296 + 256 * u_over_t, 1),
+            "path_achieved_GBs": round((296 + 256 * u_over_t) * args.transfers * args.steps / (total_ms / 1e3) / 1e9, 1)}
 
 
 if __name__ == "__main__":

@@ -897,3 +897,104 @@ int tbo_sum_overflows_u64(uint64_t a, uint64_t b) { return sum_overflows_u64(a, 
 int tbo_sum_overflows_u128(uint64_t a_lo, uint64_t a_hi, uint64_t b_lo, uint64_t b_hi) {
     return sum_overflows_u128(((u128)a_hi << 64) | a_lo, ((u128)b_hi << 64) | b_lo);
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* Shard test double support (tests/harness/shard_double.py): the per-rank primitives of       */
+/* include/tbgpu_shard.h restated on the CPU state, so the multi-GPU router's collectives and  */
+/* fallback logic can be tested with gloo on CPU.                                              */
+/* ------------------------------------------------------------------------------------------ */
+
+int tbo_commit_routed(tbo_state* s, uint64_t n, const void* events, const uint64_t* ts, uint8_t* codes) {
+    if (setjmp(s->panic_jmp)) return TBO_STATUS_PANIC;
+    for (u64 i = 0; i < n; i++) {
+        transfer_t t;
+        memcpy(&t, (const u8*)events + i * 128, 128);
+        if (t.flags & (1 | 4 | 8 | 16 | 32)) return TBO_STATUS_INVALID; /* never routed */
+        if (!(ts[i] > s->commit_timestamp)) return TBO_STATUS_PANIC;
+        if (t.timestamp != 0) {
+            codes[i] = CT_TIMESTAMP_MUST_BE_ZERO;
+            continue;
+        }
+        t.timestamp = ts[i];
+        codes[i] = (uint8_t)create_transfer(s, &t);
+    }
+    return TBO_STATUS_OK;
+}
+
+int tbo_fetch_accounts(const tbo_state* s, const uint64_t* ids, uint32_t n, void* out, uint8_t* found) {
+    for (u32 i = 0; i < n; i++) {
+        const u128 id = ((u128)ids[2 * i + 1] << 64) | ids[2 * i];
+        const account_t* a = accounts_get(s, id);
+        found[i] = a != NULL;
+        if (a) memcpy((u8*)out + (u64)i * 128, a, 128);
+        else memset((u8*)out + (u64)i * 128, 0, 128);
+    }
+    return TBO_STATUS_OK;
+}
+
+int tbo_fetch_transfers(const tbo_state* s, const uint64_t* ids, uint32_t n, void* out, uint8_t* state) {
+    for (u32 i = 0; i < n; i++) {
+        const u128 id = ((u128)ids[2 * i + 1] << 64) | ids[2 * i];
+        const transfer_t* t = transfers_get(s, id);
+        if (t) {
+            memcpy((u8*)out + (u64)i * 128, t, 128);
+            state[i] = (uint8_t)(1 + posted_get(s, t->timestamp));
+        } else {
+            memset((u8*)out + (u64)i * 128, 0, 128);
+            state[i] = 0;
+        }
+    }
+    return TBO_STATUS_OK;
+}
+
+int tbo_upsert_accounts(tbo_state* s, const void* records, uint32_t n) {
+    if (setjmp(s->panic_jmp)) return TBO_STATUS_PANIC;
+    for (u32 i = 0; i < n; i++) {
+        account_t a;
+        memcpy(&a, (const u8*)records + (u64)i * 128, 128);
+        map_slot* m = map_find(&s->account_ids, a.id);
+        if (m) {
+            account_t* cur = &s->accounts[m->value];
+            cur->debits_pending = a.debits_pending;
+            cur->debits_posted = a.debits_posted;
+            cur->credits_pending = a.credits_pending;
+            cur->credits_posted = a.credits_posted;
+        } else {
+            accounts_insert(s, &a);
+        }
+    }
+    return TBO_STATUS_OK;
+}
+
+int tbo_upsert_transfers(tbo_state* s, const void* records, const uint8_t* state, uint32_t n) {
+    if (setjmp(s->panic_jmp)) return TBO_STATUS_PANIC;
+    for (u32 i = 0; i < n; i++) {
+        transfer_t t;
+        memcpy(&t, (const u8*)records + (u64)i * 128, 128);
+        const transfer_t* cur = transfers_get(s, t.id);
+        if (!cur) transfers_insert(s, &t);
+        const u64 ts = cur ? cur->timestamp : t.timestamp;
+        if (state[i] >= 2) {
+            if (map_find(&s->posted, ts)) map_remove(&s->posted, ts);
+            map_put(&s->posted, ts, (u64)(state[i] - 2));
+        } else if (state[i] == 1 && map_find(&s->posted, ts)) {
+            map_remove(&s->posted, ts);
+        }
+    }
+    return TBO_STATUS_OK;
+}
+
+void tbo_balance_bound(const tbo_state* s, uint64_t out[2]) {
+    u128 bound = 0;
+    const u128 MAX = ~(u128)0;
+    for (u64 i = 0; i < s->accounts_len; i++) {
+        const account_t* a = &s->accounts[i];
+        u128 d, c;
+        if (__builtin_add_overflow(a->debits_pending, a->debits_posted, &d)) d = MAX;
+        if (__builtin_add_overflow(a->credits_pending, a->credits_posted, &c)) c = MAX;
+        if (d > bound) bound = d;
+        if (c > bound) bound = c;
+    }
+    out[0] = (u64)bound;
+    out[1] = (u64)(bound >> 64);
+}

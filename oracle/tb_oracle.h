@@ -69,6 +69,18 @@ uint64_t tbo_export_transfers(const tbo_state* s, void* out, uint64_t cap);
  * sorted by timestamp. */
 uint64_t tbo_export_posted(const tbo_state* s, uint64_t* out_pairs, uint64_t cap);
 
+/* Shard test double (tests/harness/shard_double.py): CPU restatements of the per-rank primitives
+ * of include/tbgpu_shard.h.  commit_routed: create_transfer for each event with the given
+ * timestamp (execute's per-event body, state_machine.zig:641-662), codes[i] = its result;
+ * linked/post/void/balancing events are rejected (TBO_STATUS_INVALID).  fetch/upsert: as the
+ * tbgpu_* calls of the same name.  balance_bound: max over accounts of dp+dpost, cp+cpost. */
+int tbo_commit_routed(tbo_state* s, uint64_t n, const void* events, const uint64_t* ts, uint8_t* codes);
+int tbo_fetch_accounts(const tbo_state* s, const uint64_t* ids, uint32_t n, void* out, uint8_t* found);
+int tbo_fetch_transfers(const tbo_state* s, const uint64_t* ids, uint32_t n, void* out, uint8_t* state);
+int tbo_upsert_accounts(tbo_state* s, const void* records, uint32_t n);
+int tbo_upsert_transfers(tbo_state* s, const void* records, const uint8_t* state, uint32_t n);
+void tbo_balance_bound(const tbo_state* s, uint64_t out[2]);
+
 /* sum_overflows (state_machine.zig:1152-1157) exposed for its known-answer vectors. */
 int tbo_sum_overflows_u64(uint64_t a, uint64_t b);
 int tbo_sum_overflows_u128(uint64_t a_lo, uint64_t a_hi, uint64_t b_lo, uint64_t b_hi);

@@ -49,6 +49,17 @@ def lib():
             getattr(L, name).argtypes = [c.c_void_p, c.c_void_p, c.c_uint64]
         L.tbo_export_posted.restype = c.c_uint64
         L.tbo_export_posted.argtypes = [c.c_void_p, c.c_void_p, c.c_uint64]
+        L.tbo_commit_routed.restype = c.c_int
+        L.tbo_commit_routed.argtypes = [c.c_void_p, c.c_uint64, c.c_void_p, c.c_void_p, c.c_void_p]
+        for name in ("tbo_fetch_accounts", "tbo_fetch_transfers"):
+            getattr(L, name).restype = c.c_int
+            getattr(L, name).argtypes = [c.c_void_p, c.c_void_p, c.c_uint32, c.c_void_p, c.c_void_p]
+        L.tbo_upsert_accounts.restype = c.c_int
+        L.tbo_upsert_accounts.argtypes = [c.c_void_p, c.c_void_p, c.c_uint32]
+        L.tbo_upsert_transfers.restype = c.c_int
+        L.tbo_upsert_transfers.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32]
+        L.tbo_balance_bound.restype = None
+        L.tbo_balance_bound.argtypes = [c.c_void_p, c.c_void_p]
         L.tbo_sum_overflows_u64.restype = c.c_int
         L.tbo_sum_overflows_u64.argtypes = [c.c_uint64, c.c_uint64]
         L.tbo_sum_overflows_u128.restype = c.c_int
@@ -128,3 +139,54 @@ class OracleEngine:
         out = np.zeros((max(n, 1), 2), dtype=np.uint64)
         m = self.L.tbo_export_posted(self.h, out.ctypes.data, n)
         return out[:m]
+
+    # -- shard test double primitives (tbo_* restatements of include/tbgpu_shard.h) -----------
+    def commit_routed(self, events, ts):
+        events = np.ascontiguousarray(events, dtype=np.uint8)
+        ts = np.ascontiguousarray(ts, dtype=np.uint64)
+        n = len(ts)
+        codes = np.zeros(max(n, 1), dtype=np.uint8)
+        st = self.L.tbo_commit_routed(self.h, n, events.ctypes.data, ts.ctypes.data, codes.ctypes.data)
+        if st == STATUS_PANIC:
+            raise OraclePanic("oracle panic in a routed commit")
+        if st != STATUS_OK:
+            raise RuntimeError("routed commit status %d" % st)
+        return codes[:n]
+
+    def fetch_accounts(self, ids):
+        ids = np.ascontiguousarray(ids, dtype=np.uint64).reshape(-1, 2)
+        out = np.zeros(len(ids), dtype=ACCOUNT_DTYPE)
+        found = np.zeros(len(ids), dtype=np.uint8)
+        if len(ids):
+            self.L.tbo_fetch_accounts(self.h, ids.ctypes.data, len(ids), out.ctypes.data, found.ctypes.data)
+        return out, found
+
+    def fetch_transfers(self, ids):
+        ids = np.ascontiguousarray(ids, dtype=np.uint64).reshape(-1, 2)
+        out = np.zeros(len(ids), dtype=TRANSFER_DTYPE)
+        state = np.zeros(len(ids), dtype=np.uint8)
+        if len(ids):
+            self.L.tbo_fetch_transfers(self.h, ids.ctypes.data, len(ids), out.ctypes.data, state.ctypes.data)
+        return out, state
+
+    def upsert_accounts(self, records):
+        records = np.ascontiguousarray(records, dtype=ACCOUNT_DTYPE)
+        if len(records) and self.L.tbo_upsert_accounts(self.h, records.ctypes.data, len(records)) != STATUS_OK:
+            raise OraclePanic("upsert_accounts")
+
+    def upsert_transfers(self, records, state):
+        records = np.ascontiguousarray(records, dtype=TRANSFER_DTYPE)
+        state = np.ascontiguousarray(state, dtype=np.uint8)
+        if len(records) and self.L.tbo_upsert_transfers(self.h, records.ctypes.data, state.ctypes.data,
+                                                        len(records)) != STATUS_OK:
+            raise OraclePanic("upsert_transfers")
+
+    def balance_bound(self):
+        out = (ctypes.c_uint64 * 2)()
+        self.L.tbo_balance_bound(self.h, out)
+        return (out[1] << 64) | out[0]
+
+    def commit_many(self, operation, timestamps, bodies):
+        return [self.commit(operation, t, b) for t, b in zip(timestamps, bodies)]
+
+    commit_batches = commit_many

@@ -1,0 +1,111 @@
+"""CPU test double of one rank's multi-GPU backend (tigerbeetle_amd.sharded.GpuShard) — TEST
+INFRASTRUCTURE ONLY.
+
+It implements the same per-rank primitives (include/tbgpu_shard.h) over the CPU oracle, with the
+routing kernels (tb_route_classify / _scatter / _replies, k_route.h) restated in numpy, so the
+collective protocol of ShardedStateMachine — clean routed passes, the dirty-pass prefetch /
+scratch commit / write-back, lookups and exports — runs with gloo on CPU at world_size 2.  The
+GPU backend itself is covered by tests/test_gpu_sharded.py.
+"""
+import numpy as np
+import torch
+
+from tigerbeetle_amd import _lib
+from tigerbeetle_amd.sharded import _ROUTED_NEVER, PassResult, RoutePlan
+from tigerbeetle_amd.types import TRANSFER_DTYPE, U128_MAX, AccountFlags
+
+from .oracle import OracleEngine
+
+_LIMITS = int(AccountFlags.debits_must_not_exceed_credits | AccountFlags.credits_must_not_exceed_debits)
+
+
+def homes_of(ids, world):
+    lib = _lib.load()
+    ids = np.ascontiguousarray(ids, dtype=np.uint64).reshape(-1, 2)
+    out = np.zeros(len(ids), dtype=np.uint32)
+    if len(ids):
+        lib.tbgpu_homes(ids.ctypes.data, len(ids), world, out.ctypes.data)
+    return out
+
+
+class OracleShard:
+    def __init__(self, world):
+        self.world = world
+        self.device = torch.device("cpu")
+        self.o = OracleEngine(1 << 12, 1 << 14)
+
+    def plan(self, timestamps, lens, events):
+        ev = events.numpy().reshape(-1).view(TRANSFER_DTYPE)
+        n = len(ev)
+        homes = homes_of(np.stack([ev["id_lo"], ev["id_hi"]], axis=1), self.world)
+        dirty = 0
+        if n:
+            if np.any(ev["flags"] & _ROUTED_NEVER):
+                dirty |= _lib.DIRTY_FLAGS
+            clean = (ev["flags"] & _ROUTED_NEVER) == 0
+            for side in ("debit_account_id", "credit_account_id"):
+                ids = np.stack([ev[side + "_lo"][clean], ev[side + "_hi"][clean]], axis=1)
+                recs, found = self.o.fetch_accounts(ids)
+                if np.any(((recs["flags"] & _LIMITS) != 0) & found.astype(bool)):
+                    dirty |= _lib.DIRTY_LIMIT
+        S = 0
+        for lo, hi in zip(ev["amount_lo"], ev["amount_hi"]):
+            S = min(S + ((int(hi) << 64) | int(lo)), U128_MAX)
+        ts = np.zeros(n, dtype=np.int64)
+        o = 0
+        for t, L in zip(timestamps, lens):
+            ts[o:o + L] = int(t) - L + 1 + np.arange(L)
+            o += L
+        order = np.argsort(homes, kind="stable")
+        slots = np.empty(n, dtype=np.int32)
+        slots[order] = np.arange(n, dtype=np.int32)
+        counts = np.bincount(homes, minlength=self.world).tolist() if n else [0] * self.world
+        plan = RoutePlan(counts, S, self.o.balance_bound(), dirty)
+        return plan, events[torch.from_numpy(order)], torch.from_numpy(ts[order]), torch.from_numpy(slots)
+
+    def commit_routed(self, events, ts, ts_max, cert):
+        del ts_max, cert
+        codes = self.o.commit_routed(events.numpy().reshape(-1), ts.numpy().view(np.uint64))
+        return torch.from_numpy(codes.copy())
+
+    def replies(self, lens, slots, codes_back):
+        codes = codes_back.numpy()[slots.numpy()] if len(slots) else np.zeros(0, dtype=np.uint8)
+        out, o = [], 0
+        for L in lens:
+            c = codes[o:o + L]
+            nz = np.nonzero(c)[0]
+            pairs = np.stack([nz.astype(np.uint32), c[nz].astype(np.uint32)], axis=1)
+            out.append(pairs.tobytes())
+            o += L
+        return PassResult.from_bytes(out, lens, self.device)
+
+    def commit_batches(self, operation, timestamps, bodies):
+        return self.o.commit_many(operation, timestamps, bodies)
+
+    def fetch_accounts(self, ids):
+        return self.o.fetch_accounts(ids)
+
+    def fetch_transfers(self, ids):
+        return self.o.fetch_transfers(ids)
+
+    def upsert_accounts(self, records):
+        self.o.upsert_accounts(records)
+
+    def upsert_transfers(self, records, state):
+        self.o.upsert_transfers(records, state)
+
+    @property
+    def commit_timestamp(self):
+        return self.o.commit_timestamp
+
+    def export_accounts(self):
+        return self.o.export_accounts()
+
+    def export_transfers(self):
+        return self.o.export_transfers()
+
+    def export_posted(self):
+        return self.o.export_posted()
+
+    def scratch(self, accounts, transfers):
+        return OracleEngine(accounts, transfers)

@@ -13,7 +13,7 @@ from tigerbeetle_amd import _lib, types
 
 def declared_functions():
     names = set()
-    for h in ("tbgpu.h", "tbgpu_bench.h"):
+    for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
         text = open(os.path.join(ROOT, "include", h)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         names |= set(re.findall(r"\b(tbgpu_\w+)\s*\(", text))
@@ -46,6 +46,17 @@ def test_exports_are_plain_c_symbols(lib):
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r"\b(tbgpu_\w+)$", out, flags=re.M))
     assert set(declared_functions()) <= exported  # unmangled extern "C"
+
+
+def test_home_function_is_host_side(lib):
+    # tbgpu_home needs no device: the router and the tests compute homes on the host.
+    homes = [lib.tbgpu_home(i, 0, 8) for i in range(1, 2001)]
+    assert set(homes) == set(range(8))
+    assert all(lib.tbgpu_home(i, 0, 1) == 0 for i in range(1, 100))
+    ids = (ctypes.c_uint64 * 4000)(*[v for i in range(1, 2001) for v in (i, 0)])
+    out = (ctypes.c_uint32 * 2000)()
+    lib.tbgpu_homes(ids, 2000, 8, out)
+    assert list(out) == homes
 
 
 def test_struct_layouts_match_reference():

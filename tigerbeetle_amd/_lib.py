@@ -52,7 +52,24 @@ class tbgpu_workload(ctypes.Structure):
     ]
 
 
-# Every symbol declared in include/tbgpu.h and include/tbgpu_bench.h: (name, restype, argtypes).
+WORLD_MAX = 64
+DIRTY_FLAGS, DIRTY_LIMIT = 1, 2
+CERT_U128, CERT_U64 = 1, 2
+
+
+class tbgpu_route_plan(ctypes.Structure):
+    _fields_ = [
+        ("send_counts", ctypes.c_uint64 * WORLD_MAX),
+        ("sum_lo", ctypes.c_uint64),
+        ("sum_hi", ctypes.c_uint64),
+        ("bound_lo", ctypes.c_uint64),
+        ("bound_hi", ctypes.c_uint64),
+        ("dirty", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+    ]
+
+
+# Every symbol declared in include/*.h: (name, restype, argtypes).
 _P = ctypes.c_void_p
 _U8, _U32, _U64 = ctypes.c_uint8, ctypes.c_uint32, ctypes.c_uint64
 SIGNATURES = [
@@ -83,6 +100,18 @@ SIGNATURES = [
     ("tbgpu_copy_to_device", ctypes.c_int, [_P, _P, _P, _U64]),
     ("tbgpu_marker", ctypes.c_int, [_P, _U32]),
     ("tbgpu_marker_elapsed_ms", ctypes.c_double, [_P, _U32, _U32]),
+    # include/tbgpu_shard.h
+    ("tbgpu_home", _U32, [_U64, _U64, _U32]),
+    ("tbgpu_homes", None, [_P, _U64, _U32, _P]),
+    ("tbgpu_route_init", ctypes.c_int, [_P, _U32, _U64]),
+    ("tbgpu_route_plan_build", ctypes.c_int, [_P, _U32, ctypes.POINTER(_U64), ctypes.POINTER(_U32), _P, _P, _P, _P,
+                                              ctypes.POINTER(tbgpu_route_plan)]),
+    ("tbgpu_commit_routed_async", ctypes.c_int, [_P, _U64, _P, _P, _U64, _U32, _P]),
+    ("tbgpu_route_replies_async", ctypes.c_int, [_P, _U32, ctypes.POINTER(_U32), _P, _P, _P, _P]),
+    ("tbgpu_fetch_accounts", ctypes.c_int, [_P, _P, _U32, _P, _P]),
+    ("tbgpu_fetch_transfers", ctypes.c_int, [_P, _P, _U32, _P, _P]),
+    ("tbgpu_upsert_accounts", ctypes.c_int, [_P, _P, _U32]),
+    ("tbgpu_upsert_transfers", ctypes.c_int, [_P, _P, _P, _U32]),
 ]
 
 _lib = None

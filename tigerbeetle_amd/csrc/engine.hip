@@ -16,8 +16,10 @@
 
 #include "../../include/tbgpu.h"
 #include "../../include/tbgpu_bench.h"
+#include "../../include/tbgpu_shard.h"
 #include "k_aux.h"
 #include "k_replay.h"
+#include "k_route.h"
 #include "k_workload.h"
 
 static thread_local std::string g_err;
@@ -104,6 +106,15 @@ struct tbgpu {
     std::vector<double> pass_ms;  // device duration of every profiled pass (batch latency)
 
     hipEvent_t markers[16] = {};
+
+    // Multi-GPU routing scratch (tbgpu_route_init).
+    u32 route_world = 0;
+    u64 route_events_max = 0;
+    u8* r_home = nullptr;
+    u32* r_block_counts = nullptr;
+    u64* r_words = nullptr;
+    u64* r_meta = nullptr;    // device [meta_cap + 1] offsets then [meta_cap] timestamps
+    u64* h_rmeta = nullptr;   // pinned mirror
 };
 
 static int ev_get(tbgpu* E, hipEvent_t* out) {
@@ -281,9 +292,11 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->T.xposted, E->g, E->info, E->eflags, E->dr,
                     E->cr, E->ps, E->rs, E->dep_list, E->dep_count, E->amt, E->kid, E->kpid, E->dedup,
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
-                    E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status};
+                    E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->r_home,
+                    E->r_block_counts, E->r_words, E->r_meta};
     for (void* p : bufs) if (p) (void)hipFree(p);
     if (E->h_meta) (void)hipHostFree(E->h_meta);
+    if (E->h_rmeta) (void)hipHostFree(E->h_rmeta);
     for (hipEvent_t e : E->event_pool) (void)hipEventDestroy(e);
     for (int i = 0; i < 16; i++) if (E->markers[i]) (void)hipEventDestroy(E->markers[i]);
     if (E->stream) (void)hipStreamDestroy(E->stream);
@@ -310,8 +323,10 @@ static int engine_sync(tbgpu* E) {
 }
 
 // Enqueue every pass of one call.  meta (device) already holds the call's offsets/timestamps.
+// Routed mode (a shard of a multi-GPU pass): ev_ts = per-event timestamps, codes = dense result
+// codes instead of sparse replies, cert_ext = the router's certificate.
 static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* events_dev, u32* results_dev,
-                        u32* reply_bytes_dev) {
+                        u32* reply_bytes_dev, const u64* ev_ts = nullptr, u8* codes = nullptr, u32 cert_ext = 0) {
     const u64* d_off = E->meta;
     const u64* d_ts = E->meta + (nb + 1);
     u32 b0 = 0;
@@ -355,6 +370,9 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.log_base = E->log_next;
         P.T = E->T;
         P.ablate = E->ablate;
+        P.ev_ts = ev_ts;
+        P.codes = codes;
+        P.cert_ext = cert_ext;
 
         ProfilePair pass_pp;
         int st = prof_begin(E, &pass_pp, K_PASS);
@@ -836,4 +854,268 @@ extern "C" double tbgpu_marker_elapsed_ms(tbgpu_t* E, uint32_t a, uint32_t b) {
     if (hipEventSynchronize(E->markers[b]) != hipSuccess) return -1;
     if (hipEventElapsedTime(&ms, E->markers[a], E->markers[b]) != hipSuccess) return -1;
     return ms;
+}
+
+// ------------------------------------------------------------------------------------------------
+// tbgpu_shard.h
+// ------------------------------------------------------------------------------------------------
+
+extern "C" uint32_t tbgpu_home(uint64_t id_lo, uint64_t id_hi, uint32_t world) { return tb_home(id_lo, id_hi, world); }
+
+extern "C" void tbgpu_homes(const uint64_t* ids, uint64_t n, uint32_t world, uint32_t* out) {
+    for (u64 i = 0; i < n; i++) out[i] = tb_home(ids[2 * i], ids[2 * i + 1], world);
+}
+
+extern "C" int tbgpu_route_init(tbgpu_t* E, uint32_t world, uint64_t events_max) {
+    HIPCK(hipSetDevice(E->device));
+    if (world == 0 || world > ROUTE_WORLD_MAX) return fail(TBGPU_STATUS_INVALID, "world %u out of range", world);
+    if (E->r_home) return fail(TBGPU_STATUS_INVALID, "tbgpu_route_init called twice");
+    if (events_max == 0 || events_max >= (1ULL << 32)) return fail(TBGPU_STATUS_INVALID, "route events_max out of range");
+    E->route_world = world;
+    E->route_events_max = events_max;
+    const u64 nblocks = (events_max + ROUTE_THREADS - 1) / ROUTE_THREADS;
+    HIPCK(hipMalloc(&E->r_home, events_max));
+    HIPCK(hipMalloc(&E->r_block_counts, nblocks * world * 4));
+    HIPCK(hipMalloc(&E->r_words, ROUTE_WORDS * 8));
+    HIPCK(hipMalloc(&E->r_meta, (2 * E->meta_cap + 1) * 8));
+    HIPCK(hipHostMalloc(&E->h_rmeta, (2 * E->meta_cap + 1) * 8, hipHostMallocDefault));
+    return TBGPU_STATUS_OK;
+}
+
+// Upload a local batch structure (offsets, timestamps) to r_meta; returns total events.
+static int route_meta(tbgpu* E, u32 nb, const u64* timestamps, const u32* lens, u64* total) {
+    if (nb > E->meta_cap) return fail(TBGPU_STATUS_INVALID, "too many batches (%u)", nb);
+    HIPCK(hipStreamSynchronize(E->stream));  // the pinned mirror may still be in flight
+    u64* off = E->h_rmeta;
+    u64* ts = E->h_rmeta + nb + 1;
+    off[0] = 0;
+    for (u32 k = 0; k < nb; k++) {
+        if (lens[k] > BATCH_EVENTS_MAX) return fail(TBGPU_STATUS_INVALID, "batch %u has %u events", k, lens[k]);
+        off[k + 1] = off[k] + lens[k];
+        ts[k] = timestamps ? timestamps[k] : 0;
+        if (timestamps && lens[k] && timestamps[k] < lens[k]) return fail(TBGPU_STATUS_PANIC, "timestamp < batch length");
+    }
+    HIPCK(hipMemcpyAsync(E->r_meta, E->h_rmeta, (2 * (u64)nb + 1) * 8, hipMemcpyHostToDevice, E->stream));
+    *total = off[nb];
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_route_plan_build(tbgpu_t* E, uint32_t nb, const uint64_t* timestamps, const uint32_t* lens,
+                                      const void* events_dev, void* send_events_dev, uint64_t* send_ts_dev,
+                                      uint32_t* slot_dev, tbgpu_route_plan* plan) {
+    HIPCK(hipSetDevice(E->device));
+    if (!E->r_home) return fail(TBGPU_STATUS_INVALID, "tbgpu_route_init was not called");
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    u64 n = 0;
+    int st = route_meta(E, nb, timestamps, lens, &n);
+    if (st) return st;
+    if (n > E->route_events_max) return fail(TBGPU_STATUS_INVALID, "pass has %llu events > route capacity %llu",
+                                             (unsigned long long)n, (unsigned long long)E->route_events_max);
+    memset(plan, 0, sizeof(*plan));
+    HIPCK(hipMemsetAsync(E->r_words, 0, ROUTE_WORDS * 8, E->stream));
+    RouteArgs A{};
+    A.events = (const u8*)events_dev;
+    A.n = (u32)n;
+    A.nb = nb;
+    A.batch_off = E->r_meta;
+    A.batch_ts = E->r_meta + nb + 1;
+    A.world = E->route_world;
+    A.nblocks = (u32)((n + ROUTE_THREADS - 1) / ROUTE_THREADS);
+    A.home = E->r_home;
+    A.block_counts = E->r_block_counts;
+    A.words = E->r_words;
+    A.T = E->T;
+    if (n > 0) {
+        hipLaunchKernelGGL(tb_route_classify, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, E->stream, A);
+        HIPCK(hipGetLastError());
+        hipLaunchKernelGGL(tb_route_offsets, dim3(1), dim3(1024), 0, E->stream, A);
+        HIPCK(hipGetLastError());
+        hipLaunchKernelGGL(tb_route_scatter, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, E->stream, A, (u8*)send_events_dev,
+                           (u64*)send_ts_dev, (u32*)slot_dev);
+        HIPCK(hipGetLastError());
+    }
+    std::vector<u64> words(ROUTE_WORDS);
+    HIPCK(hipMemcpyAsync(words.data(), E->r_words, ROUTE_WORDS * 8, hipMemcpyDeviceToHost, E->stream));
+    Globals g;
+    HIPCK(hipMemcpyAsync(&g, E->g, sizeof(Globals), hipMemcpyDeviceToHost, E->stream));
+    HIPCK(hipStreamSynchronize(E->stream));
+    unsigned __int128 S = 0;
+    bool huge = words[RW_HUGE] != 0;
+    for (int i = 0; i < SUM_SHARDS && !huge; i++) {
+        const unsigned __int128 v = ((unsigned __int128)words[2 * i + 1] << 64) | words[2 * i];
+        const unsigned __int128 r = S + v;
+        if (r < S) huge = true;
+        S = r;
+    }
+    if (huge) S = ~(unsigned __int128)0;
+    plan->sum_lo = (u64)S;
+    plan->sum_hi = (u64)(S >> 64);
+    plan->bound_lo = g.bound_lo;
+    plan->bound_hi = g.bound_hi;
+    plan->dirty = (u32)words[RW_DIRTY];
+    for (u32 h = 0; h < E->route_world; h++) plan->send_counts[h] = words[RW_COUNTS + h];
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_commit_routed_async(tbgpu_t* E, uint64_t n, const void* events_dev, const uint64_t* ts_dev,
+                                         uint64_t ts_max, uint32_t cert, uint8_t* codes_dev) {
+    HIPCK(hipSetDevice(E->device));
+    if (cert != TBGPU_CERT_U128 && cert != TBGPU_CERT_U64) return fail(TBGPU_STATUS_INVALID, "routed commit needs a certificate");
+    if (n == 0) return TBGPU_STATUS_OK;
+    if (E->pending) {  // the pinned metadata mirror may still be in flight
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    // Pseudo-prepares of up to 8190 events: the events are independent (no chains), so the split
+    // only sizes the resolve workgroups.
+    const u64 per = BATCH_EVENTS_MAX - 1;
+    const u64 nb = (n + per - 1) / per;
+    if (nb > E->meta_cap) return fail(TBGPU_STATUS_INVALID, "routed call too large");
+    if (E->log_next + n > E->xlog_cap) {
+        return fail(TBGPU_STATUS_INVALID, "transfer log full (%llu + %llu events > capacity %llu)",
+                    (unsigned long long)E->log_next, (unsigned long long)n, (unsigned long long)E->xlog_cap);
+    }
+    u64* h_off = E->h_meta;
+    u64* h_ts = E->h_meta + nb + 1;
+    h_off[0] = 0;
+    for (u64 k = 0; k < nb; k++) {
+        h_off[k + 1] = std::min<u64>(n, h_off[k] + per);
+        h_ts[k] = ts_max;
+    }
+    HIPCK(hipMemcpyAsync(E->meta, E->h_meta, (2 * nb + 1) * 8, hipMemcpyHostToDevice, E->stream));
+    std::vector<u64> off(h_off, h_off + nb + 1);
+    int st = enqueue_call(E, OP_CREATE_TRANSFERS, (u32)nb, off.data(), (const u8*)events_dev, E->results,
+                          E->reply_bytes, ts_dev, codes_dev, cert);
+    if (st) return st;
+    E->last_batch_ts = std::max(E->last_batch_ts, ts_max);
+    E->pending = true;
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_route_replies_async(tbgpu_t* E, uint32_t nb, const uint32_t* lens, const uint32_t* slot_dev,
+                                         const uint8_t* codes_dev, void* results_dev, uint32_t* reply_bytes_dev) {
+    HIPCK(hipSetDevice(E->device));
+    if (!E->r_meta) return fail(TBGPU_STATUS_INVALID, "tbgpu_route_init was not called");
+    if (nb == 0) return TBGPU_STATUS_OK;
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    u64 n = 0;
+    int st = route_meta(E, nb, nullptr, lens, &n);
+    if (st) return st;
+    hipLaunchKernelGGL(tb_route_replies, dim3(nb), dim3(1024), 0, E->stream, E->r_meta, slot_dev, codes_dev,
+                       (u32*)results_dev, reply_bytes_dev);
+    HIPCK(hipGetLastError());
+    E->pending = true;
+    return TBGPU_STATUS_OK;
+}
+
+// Host <-> device staging through the lookup buffers, in chunks of lookup_cap.
+extern "C" int tbgpu_fetch_accounts(tbgpu_t* E, const uint64_t* ids, uint32_t n, void* out, uint8_t* found) {
+    HIPCK(hipSetDevice(E->device));
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    for (u32 c = 0; c < n; c += E->lookup_cap) {
+        const u32 m = std::min<u32>(E->lookup_cap, n - c);
+        HIPCK(hipMemcpyAsync(E->lookup_ids, ids + 2 * (u64)c, (u64)m * 16, hipMemcpyHostToDevice, E->stream));
+        HIPCK(hipMemsetAsync(E->lookup_out, 0, (u64)m * 128, E->stream));
+        hipLaunchKernelGGL(tb_lookup<true>, dim3((m + 255) / 256), dim3(256), 0, E->stream, E->T, E->lookup_ids, m,
+                           E->lookup_out, E->lookup_found);
+        HIPCK(hipGetLastError());
+        HIPCK(hipMemcpyAsync((u8*)out + (u64)c * 128, E->lookup_out, (u64)m * 128, hipMemcpyDeviceToHost, E->stream));
+        HIPCK(hipMemcpyAsync(found + c, E->lookup_found, m, hipMemcpyDeviceToHost, E->stream));
+        HIPCK(hipStreamSynchronize(E->stream));
+    }
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_fetch_transfers(tbgpu_t* E, const uint64_t* ids, uint32_t n, void* out, uint8_t* state) {
+    HIPCK(hipSetDevice(E->device));
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    for (u32 c = 0; c < n; c += E->lookup_cap) {
+        const u32 m = std::min<u32>(E->lookup_cap, n - c);
+        HIPCK(hipMemcpyAsync(E->lookup_ids, ids + 2 * (u64)c, (u64)m * 16, hipMemcpyHostToDevice, E->stream));
+        HIPCK(hipMemsetAsync(E->lookup_out, 0, (u64)m * 128, E->stream));
+        hipLaunchKernelGGL(tb_fetch_transfers, dim3((m + 255) / 256), dim3(256), 0, E->stream, E->T, E->lookup_ids, m,
+                           E->lookup_out, E->lookup_found);
+        HIPCK(hipGetLastError());
+        HIPCK(hipMemcpyAsync((u8*)out + (u64)c * 128, E->lookup_out, (u64)m * 128, hipMemcpyDeviceToHost, E->stream));
+        HIPCK(hipMemcpyAsync(state + c, E->lookup_found, m, hipMemcpyDeviceToHost, E->stream));
+        HIPCK(hipStreamSynchronize(E->stream));
+    }
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_upsert_accounts(tbgpu_t* E, const void* records, uint32_t n) {
+    HIPCK(hipSetDevice(E->device));
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    // Keep `bound` >= dp+dpost, cp+cpost of every account (saturating).
+    Globals g;
+    HIPCK(hipMemcpy(&g, E->g, sizeof(Globals), hipMemcpyDeviceToHost));
+    typedef unsigned __int128 h128;
+    const h128 MAX = ~(h128)0;
+    h128 bound = ((h128)g.bound_hi << 64) | g.bound_lo;
+    for (u32 i = 0; i < n; i++) {
+        const u64* w = (const u64*)((const u8*)records + (u64)i * 128);
+        const h128 dp = ((h128)w[3] << 64) | w[2], dpo = ((h128)w[5] << 64) | w[4];
+        const h128 cp = ((h128)w[7] << 64) | w[6], cpo = ((h128)w[9] << 64) | w[8];
+        const h128 d = dp + dpo < dp ? MAX : dp + dpo;
+        const h128 c = cp + cpo < cp ? MAX : cp + cpo;
+        bound = std::max(bound, std::max(d, c));
+    }
+    u32 status = 0;
+    HIPCK(hipMemsetAsync(E->d_status, 0, 4, E->stream));
+    for (u32 c = 0; c < n; c += E->lookup_cap) {
+        const u32 m = std::min<u32>(E->lookup_cap, n - c);
+        HIPCK(hipMemcpyAsync(E->lookup_out, (const u8*)records + (u64)c * 128, (u64)m * 128, hipMemcpyHostToDevice,
+                             E->stream));
+        hipLaunchKernelGGL(tb_upsert_accounts, dim3((m + 255) / 256), dim3(256), 0, E->stream, E->T, E->lookup_out, m,
+                           E->d_status);
+        HIPCK(hipGetLastError());
+        HIPCK(hipStreamSynchronize(E->stream));
+    }
+    const u64 bw[2] = {(u64)bound, (u64)(bound >> 64)};
+    HIPCK(hipMemcpy(&E->g->bound_lo, bw, 16, hipMemcpyHostToDevice));
+    HIPCK(hipMemcpy(&status, E->d_status, 4, hipMemcpyDeviceToHost));
+    if (status) return fail(TBGPU_STATUS_PANIC, "account table full");
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_upsert_transfers(tbgpu_t* E, const void* records, const uint8_t* state, uint32_t n) {
+    HIPCK(hipSetDevice(E->device));
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    HIPCK(hipMemsetAsync(E->d_status, 0, 8, E->stream));
+    for (u32 c = 0; c < n; c += E->lookup_cap) {
+        const u32 m = std::min<u32>(E->lookup_cap, n - c);
+        HIPCK(hipMemcpyAsync(E->lookup_out, (const u8*)records + (u64)c * 128, (u64)m * 128, hipMemcpyHostToDevice,
+                             E->stream));
+        HIPCK(hipMemcpyAsync(E->lookup_found, state + c, m, hipMemcpyHostToDevice, E->stream));
+        HIPCK(hipMemsetAsync(E->d_status + 1, 0, 4, E->stream));
+        hipLaunchKernelGGL(tb_upsert_transfers, dim3((m + 255) / 256), dim3(256), 0, E->stream, E->T, E->lookup_out,
+                           E->lookup_found, m, E->log_next, E->d_status + 1, E->d_status);
+        HIPCK(hipGetLastError());
+        u32 added = 0;
+        HIPCK(hipMemcpyAsync(&added, E->d_status + 1, 4, hipMemcpyDeviceToHost, E->stream));
+        HIPCK(hipStreamSynchronize(E->stream));
+        E->log_next += added;
+    }
+    u32 status = 0;
+    HIPCK(hipMemcpy(&status, E->d_status, 4, hipMemcpyDeviceToHost));
+    if (status) return fail(TBGPU_STATUS_PANIC, "transfer log or index full");
+    return TBGPU_STATUS_OK;
 }

@@ -303,7 +303,6 @@ __device__ static inline u64 rp_batch(const PassArgs& P, Replay& R, u32 b) {
     const u64 boff = P.batch_off[b];
     const u32 L = (u32)(P.batch_off[b + 1] - boff);
     const u32 pbase = (u32)(boff - P.e0);
-    const u64 ts0 = P.batch_ts[b] - L + 1;
     const u32 nd = P.dep_count[b - P.b0];
     const u32* list = P.dep_list + pbase;
     u64 tsmax = 0;
@@ -329,7 +328,7 @@ __device__ static inline u64 rp_batch(const PassArgs& P, Replay& R, u32 b) {
         } else if (evts != 0) {
             result = R_TIMESTAMP_MUST_BE_ZERO;
         } else {
-            const u64 ts = ts0 + i;
+            const u64 ts = tb_event_ts(P, b, boff, L, i);
             if (OP == OP_CREATE_TRANSFERS) {
                 Transfer t = *(const Transfer*)ev;
                 t.timestamp = ts;

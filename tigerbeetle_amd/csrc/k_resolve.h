@@ -53,6 +53,11 @@ __device__ static inline bool tb_account_cert_fails(const AccountBal* a, u128 S)
 
 // Write the sparse reply of batch b from LDS codes.
 __device__ static inline void tb_write_replies(const PassArgs& P, u32 b, u32 L, const u8* s_code, u32* s_wave) {
+    if (P.codes) {  // routed mode: dense per-event codes, the router compacts them per prepare
+        u8* dst = P.codes + P.batch_off[b];
+        for (u32 i = threadIdx.x; i < L; i += blockDim.x) dst[i] = s_code[i];
+        return;
+    }
     u32* out = P.results + 2 * P.batch_off[b];
     u32 running = 0;
     for (u32 c = 0; c < L; c += blockDim.x) {
@@ -161,7 +166,6 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     const u64 boff = P.batch_off[b];
     const u32 L = (u32)(P.batch_off[b + 1] - boff);
     const u32 pbase = (u32)(boff - P.e0);
-    const u64 ts0 = P.batch_ts[b] - L + 1;  // timestamp of event 0 (:645)
 
     u128 S = 0;
     bool cert_global = true, cert64 = true;
@@ -173,6 +177,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         u128 r;
         cert_global = !tb_add_overflows(tb_u128(T.g->bound_lo, T.g->bound_hi), S, &r);
         cert64 = cert_global && tb_hi(r) == 0;
+        if (P.cert_ext) {  // routed shard: the router certified the global bound + S
+            cert_global = true;
+            cert64 = P.cert_ext == CERT_EXT_U64;
+        }
     }
 
     if (threadIdx.x == 0) s_applied = 0;
@@ -264,7 +272,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                 if (fin == TB_CODE_PANIC) tb_panic(T.g, PANIC_ASSERT);
                 s_code[i] = (u8)fin;
                 P.info[pe] = (info & 0xFFFFFF00u) | fin | (eval_ok ? HZ_EVAL_OK : 0);
-                const u64 ts = ts0 + i;
+                const u64 ts = tb_event_ts(P, b, boff, L, i);
                 if (eval_ok) tsmax = ts;  // increasing in i
                 if (fin == R_OK) {
                     if (OP == OP_CREATE_TRANSFERS) tb_apply_transfer(P, pe, info, P.eflags[pe], cert64);

@@ -1,0 +1,276 @@
+// k_route.h — multi-GPU routing of a create_transfers pass (include/tbgpu_shard.h).
+//
+// Partition: account records are replicated on every rank, account balances are
+// per-rank partial sums, and a transfer (record, id index entry, posted state) lives on
+// home(id).  A CLEAN pass — no linked / post / void / balancing event, no limit-flag account,
+// global overflow certificate — is decided entirely by each event's home: id uniqueness and the
+// exists checks are home-local and no free account's balance is read by create_transfer
+// (state_machine.zig:779-884 reads balances only for balancing :826-846, the overflow checks
+// :848-861 and the limit checks :863-868).  So a clean pass is
+//   1. tb_route_classify + tb_route_offsets + tb_route_scatter on every rank: the rank's events
+//      grouped by home (stable: global order survives), each with its execute timestamp
+//      (:645) — one send buffer for the all-to-all;
+//   2. a routed commit on every home (the normal validate/resolve/replay kernels in routed mode);
+//   3. tb_route_replies: the codes that came back, compacted into per-prepare sparse replies.
+// Dirty passes use the prefetch/write-back kernels at the bottom (tb_fetch_*, tb_upsert_*).
+#pragma once
+
+#include "pass.h"
+
+#define ROUTE_THREADS 256
+#define ROUTE_WORLD_MAX 64
+
+enum : u32 { ROUTE_DIRTY_FLAGS = 1, ROUTE_DIRTY_LIMIT = 2 };
+
+// home(id): the top 32 bits of the id hash scaled to [0, world) — independent of the low hash bits
+// that pick the index position, so each home's index stays uniformly loaded.
+__host__ __device__ static inline u32 tb_home(u64 lo, u64 hi, u32 world) {
+    return (u32)(((tb_hash_id(lo, hi) >> 32) * (u64)world) >> 32);
+}
+
+struct RouteArgs {
+    const u8* events;      // this rank's events of the pass, back to back
+    u32 n;
+    u32 nb;
+    const u64* batch_off;  // [nb + 1]
+    const u64* batch_ts;   // [nb]
+    u32 world;
+    u32 nblocks;
+    u8* home;              // [n]
+    u32* block_counts;     // [nblocks][world] (then rewritten as exclusive bases)
+    u64* words;            // [2*SUM_SHARDS] S shards, [2*SUM_SHARDS] HUGE, [+1] dirty bits, [+2..] counts
+    Tables T;
+};
+#define RW_HUGE (2 * SUM_SHARDS)
+#define RW_DIRTY (2 * SUM_SHARDS + 1)
+#define RW_COUNTS (2 * SUM_SHARDS + 2)
+#define ROUTE_WORDS (RW_COUNTS + ROUTE_WORLD_MAX)
+
+// Pass 1: home of every event, dirty bits, S (saturating sum of amounts: every potential
+// increment of any balance), per-block home histogram.
+__global__ __launch_bounds__(ROUTE_THREADS) void tb_route_classify(RouteArgs A) {
+    __shared__ u32 s_cnt[ROUTE_WORLD_MAX];
+    __shared__ u64 s_sum[2 * (ROUTE_THREADS / 64)];
+    __shared__ u32 s_dirty;
+    if (threadIdx.x < A.world) s_cnt[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_dirty = 0;
+    __syncthreads();
+    const u64 e = (u64)blockIdx.x * ROUTE_THREADS + threadIdx.x;
+    u128 amount = 0;
+    if (e < A.n) {
+        const u64* w = (const u64*)(A.events + e * 128);
+        const u64 id_lo = w[0], id_hi = w[1];
+        const u16 flags = *(const u16*)(A.events + e * 128 + 118);
+        const u32 h = tb_home(id_lo, id_hi, A.world);
+        A.home[e] = (u8)h;
+        atomicAdd(&s_cnt[h], 1u);
+        amount = tb_u128(w[6], w[7]);
+        u32 dirty = 0;
+        if (flags & (TF_LINKED | TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT)) {
+            dirty = ROUTE_DIRTY_FLAGS;
+        } else {
+            const u32 d = tb_account_find(A.T, w[2], w[3]);
+            const u32 c = tb_account_find(A.T, w[4], w[5]);
+            const u16 lim = AF_DEBITS_MUST_NOT_EXCEED_CREDITS | AF_CREDITS_MUST_NOT_EXCEED_DEBITS;
+            if ((d != TB_NOT_FOUND && (A.T.acct_hot[d].flags & lim)) ||
+                (c != TB_NOT_FOUND && (A.T.acct_hot[c].flags & lim))) {
+                dirty = ROUTE_DIRTY_LIMIT;
+            }
+        }
+        if (dirty) atomicOr(&s_dirty, dirty);
+    }
+    const u128 ws = tb_wave_sum_u128(amount);
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        s_sum[2 * wave] = tb_lo(ws);
+        s_sum[2 * wave + 1] = tb_hi(ws);
+    }
+    __syncthreads();
+    if (threadIdx.x < A.world) A.block_counts[(u64)blockIdx.x * A.world + threadIdx.x] = s_cnt[threadIdx.x];
+    if (threadIdx.x == 0) {
+        u128 total = 0;
+        for (u32 k = 0; k < ROUTE_THREADS / 64; k++) total = tb_sat_add(total, tb_u128(s_sum[2 * k], s_sum[2 * k + 1]));
+        if (total != 0) {
+            if (tb_hi(total) >> 36) atomicOr((unsigned long long*)&A.words[RW_HUGE], 1ULL);
+            else tb_atomic_add_u128(A.words + 2 * (blockIdx.x % SUM_SHARDS), total);
+        }
+        if (s_dirty) atomicOr((unsigned long long*)&A.words[RW_DIRTY], (unsigned long long)s_dirty);
+    }
+}
+
+// Pass 2 (one workgroup): exclusive bases.  block_counts[blk][h] becomes the send-buffer position
+// of block blk's first event for home h: homes in rank order, blocks in order within a home.
+__global__ __launch_bounds__(1024) void tb_route_offsets(RouteArgs A) {
+    __shared__ u32 s_part[1024];
+    __shared__ u64 s_home_base;
+    if (threadIdx.x == 0) s_home_base = 0;
+    __syncthreads();
+    for (u32 h = 0; h < A.world; h++) {
+        // Each thread owns a contiguous run of blocks.
+        const u32 per = (A.nblocks + 1023) / 1024;
+        const u32 b0 = threadIdx.x * per, b1 = min(A.nblocks, b0 + per);
+        u32 local = 0;
+        for (u32 b = b0; b < b1; b++) local += A.block_counts[(u64)b * A.world + h];
+        s_part[threadIdx.x] = local;
+        __syncthreads();
+        // Inclusive scan over the 1024 partials (Hillis-Steele; tiny).
+        for (u32 off = 1; off < 1024; off <<= 1) {
+            const u32 v = threadIdx.x >= off ? s_part[threadIdx.x - off] : 0;
+            __syncthreads();
+            s_part[threadIdx.x] += v;
+            __syncthreads();
+        }
+        const u64 base = s_home_base;
+        u64 run = base + (threadIdx.x ? s_part[threadIdx.x - 1] : 0);
+        for (u32 b = b0; b < b1; b++) {
+            u32* c = &A.block_counts[(u64)b * A.world + h];
+            const u32 v = *c;
+            *c = (u32)run;
+            run += v;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            A.words[RW_COUNTS + h] = s_part[1023];
+            s_home_base = base + s_part[1023];
+        }
+        __syncthreads();
+    }
+}
+
+// Pass 3: stable scatter into the send buffer, with the execute timestamp of every event.
+__global__ __launch_bounds__(ROUTE_THREADS) void tb_route_scatter(RouteArgs A, u8* send_events, u64* send_ts,
+                                                                 u32* slot) {
+    __shared__ __attribute__((aligned(16))) u8 stage[ROUTE_THREADS * STAGE_STRIDE];
+    __shared__ u32 s_wcnt[ROUTE_THREADS / 64][ROUTE_WORLD_MAX];
+    __shared__ u32 s_range[2];
+    const u64 tile0 = (u64)blockIdx.x * ROUTE_THREADS;
+    const u32 count = (u32)min((u64)ROUTE_THREADS, A.n - tile0);
+    tb_stage_events(A.events + tile0 * 128, count, stage);
+    const u64 e = tile0 + threadIdx.x;
+    const bool live = threadIdx.x < count;
+    const u32 h = live ? A.home[e] : 0xFFFFFFFFu;
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u32 before = 0;
+    for (u32 k = 0; k < A.world; k++) {
+        const u64 m = __ballot(h == k);
+        if (h == k) before = __popcll(m & ((1ULL << lane) - 1));
+        if (lane == 0) s_wcnt[wave][k] = __popcll(m);
+    }
+    // Batch of every event (for its timestamp).
+    if (threadIdx.x == 0) {
+        s_range[0] = tb_batch_search(A.batch_off, 0, A.nb, tile0);
+        s_range[1] = tb_batch_search(A.batch_off, s_range[0], A.nb, tile0 + count - 1) + 1;
+    }
+    __syncthreads();
+    if (!live) return;
+    u32 pos = A.block_counts[(u64)blockIdx.x * A.world + h] + before;
+    for (u32 w = 0; w < wave; w++) pos += s_wcnt[w][h];
+    const u32 b = tb_batch_search(A.batch_off, s_range[0], s_range[1], e);
+    const u64 boff = A.batch_off[b];
+    const u32 L = (u32)(A.batch_off[b + 1] - boff);
+    send_ts[pos] = A.batch_ts[b] - L + 1 + (e - boff);  // execute, state_machine.zig:645
+    slot[e] = pos;
+    const u8* src = stage + threadIdx.x * STAGE_STRIDE;
+    u32x4* dst = (u32x4*)(send_events + (u64)pos * 128);
+#pragma unroll
+    for (int k = 0; k < 8; k++) dst[k] = *(const u32x4*)(src + k * 16);
+}
+
+// Per-prepare sparse replies from the codes that came back (in send order): ascending index,
+// non-ok only (tb_write_replies' layout).  One workgroup per prepare.
+__global__ __launch_bounds__(1024) void tb_route_replies(const u64* batch_off, const u32* slot, const u8* codes,
+                                                        u32* results, u32* reply_bytes) {
+    __shared__ u32 s_wave[1024 / 64];
+    const u32 b = blockIdx.x;
+    const u64 boff = batch_off[b];
+    const u32 L = (u32)(batch_off[b + 1] - boff);
+    u32* out = results + 2 * boff;
+    u32 running = 0;
+    for (u32 c = 0; c < L; c += blockDim.x) {
+        const u32 i = c + threadIdx.x;
+        const u32 code = i < L ? codes[slot[boff + i]] : R_OK;
+        const u64 m = __ballot(code != R_OK);
+        const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        if (lane == 0) s_wave[wave] = __popcll(m);
+        __syncthreads();
+        u32 wb = 0, tot = 0;
+        for (u32 k = 0; k < blockDim.x / 64; k++) {
+            wb += k < wave ? s_wave[k] : 0;
+            tot += s_wave[k];
+        }
+        if (code != R_OK) {
+            const u32 r = running + wb + __popcll(m & ((1ULL << lane) - 1));
+            out[2 * r] = i;
+            out[2 * r + 1] = code;
+        }
+        running += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) reply_bytes[b] = running * 8;
+}
+
+// ---- dirty-pass prefetch / write-back ----------------------------------------------------------
+
+// Prefetch of transfers by id (groove get, state_machine.zig:1079-1082): record + state
+// (0 absent, 1 + POSTED_* otherwise: the posted groove entry, :1084-1089).
+__global__ void tb_fetch_transfers(Tables T, const u64* ids, u32 n, u8* out, u8* state) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32 pos = tb_transfer_find(T, ids[2 * i], ids[2 * i + 1]);
+    if (pos == TB_NOT_FOUND) {
+        state[i] = 0;
+        return;
+    }
+    *(Transfer*)(out + (u64)i * 128) = T.xlog[pos];
+    state[i] = 1 + T.xposted[pos];
+}
+
+// Insert accounts verbatim (metadata + balances + timestamp), or overwrite the balances of an
+// existing one.  Ids within one call are distinct.  status: bit0 table full.
+__global__ void tb_upsert_accounts(Tables T, const u8* recs, u32 n, u32* status) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Account a = *(const Account*)(recs + (u64)i * 128);
+    u32 slot = tb_account_find(T, tb_lo(a.id), tb_hi(a.id));
+    if (slot != TB_NOT_FOUND) {
+        AccountBal b;
+        b.debits_pending = a.debits_pending;
+        b.debits_posted = a.debits_posted;
+        b.credits_pending = a.credits_pending;
+        b.credits_posted = a.credits_posted;
+        T.acct_bal[slot] = b;
+        return;
+    }
+    slot = tb_account_claim(T, tb_lo(a.id), tb_hi(a.id), a.timestamp);
+    if (slot == TB_NOT_FOUND) {
+        atomicOr(status, 1u);
+        return;
+    }
+    tb_account_store_new(T, slot, a);
+    atomicAdd((unsigned long long*)&T.g->account_count, 1ULL);
+}
+
+// Insert transfers verbatim at the end of the log (state = 1 + POSTED_*), or set the posted state
+// of an existing one (state != 0).  Ids within one call are distinct.
+__global__ void tb_upsert_transfers(Tables T, const u8* recs, const u8* state, u32 n, u64 log_base, u32* counter,
+                                    u32* status) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Transfer& t = *(const Transfer*)(recs + (u64)i * 128);
+    const u32 pos = tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id));
+    const u8 st = state[i];
+    if (pos != TB_NOT_FOUND) {
+        if (st) T.xposted[pos] = st - 1;
+        return;
+    }
+    const u64 lp = log_base + atomicAdd(counter, 1u);
+    if (lp >= T.xlog_cap) {
+        atomicOr(status, 1u);
+        return;
+    }
+    T.xlog[lp] = t;
+    T.xposted[lp] = st ? st - 1 : POSTED_NONE;
+    __threadfence();
+    if (tb_transfer_claim_new(T, tb_lo(t.id), tb_hi(t.id), (u32)lp) == TB_NOT_FOUND) atomicOr(status, 1u);
+    atomicAdd((unsigned long long*)&T.g->transfer_count, 1ULL);
+}

@@ -1,0 +1,564 @@
+"""Multi-GPU commit of the create_accounts / create_transfers path.
+
+One engine per GPU, one process per GPU, collectives over torch.distributed (backend "nccl" =
+RCCL over xGMI on an MI355X node; "gloo" for the CPU tests and for several ranks sharing one GPU).
+The partition and the pass protocol are documented in include/tbgpu_shard.h and DESIGN.md §6:
+
+* account records are replicated (every rank commits every create_accounts prepare);
+* account balances are per-rank partial sums (true balance = sum over ranks);
+* a transfer lives on its home rank, tbgpu_home(id, world).
+
+Global order.  A collective pass takes every rank's prepares.  The global prepare order is rank 0's
+prepares, then rank 1's, ..., and timestamps must increase in that order: the results are exactly
+those of one StateMachine committing the concatenation (src/state_machine.zig:508-540).
+
+A clean create_transfers pass is routed: one all-to-all of events (+ their execute timestamps) to
+their homes, a routed commit on every home, one all-to-all of result codes back.  A dirty pass
+(linked / post / void / balancing event, limit-flag account, or no global overflow certificate)
+is committed by rank 0 on a scratch engine after prefetching the referenced transfers from their
+homes and the summed balances of the touched accounts (the reference's prefetch -> commit split,
+src/state_machine.zig:345-506), then its effects are written back.
+"""
+import dataclasses
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from .types import ACCOUNT_DTYPE, TRANSFER_DTYPE, U64_MAX, Operation, TransferFlags
+
+U64 = 1 << 64
+U128 = 1 << 128
+_BAL_FIELDS = ("debits_pending", "debits_posted", "credits_pending", "credits_posted")
+_ROUTED_NEVER = int(TransferFlags.linked | TransferFlags.post_pending_transfer | TransferFlags.void_pending_transfer
+                    | TransferFlags.balancing_debit | TransferFlags.balancing_credit)
+
+
+@dataclasses.dataclass
+class RoutePlan:
+    counts: list  # events for each home rank
+    S: int        # saturating sum of every amount of this rank's share of the pass
+    bound: int    # this engine's balance bound
+    dirty: int    # _lib.DIRTY_* bits
+
+
+class PassResult:
+    """Replies of this rank's prepares of one pass.  Prepare k's reply is the {index, result} u32
+    pairs results[2*offsets[k] : 2*offsets[k] + reply_bytes[k] // 4] (tensors, possibly on the GPU)."""
+
+    def __init__(self, results, reply_bytes, offsets):
+        self.results = results
+        self.reply_bytes = reply_bytes
+        self.offsets = offsets
+
+    def replies(self):
+        rb = self.reply_bytes.cpu().numpy().astype(np.int64)
+        if rb.sum() == 0:
+            return [b""] * len(rb)
+        res = self.results.cpu().numpy().view(np.uint32)
+        out = []
+        for k, nbytes in enumerate(rb):
+            o = 2 * int(self.offsets[k])
+            out.append(res[o:o + nbytes // 4].tobytes())
+        return out
+
+    @staticmethod
+    def from_bytes(replies, lens, device):
+        offsets = np.concatenate([[0], np.cumsum(lens, dtype=np.int64)])
+        results = np.zeros(2 * max(int(offsets[-1]), 1), dtype=np.uint32)
+        rb = np.zeros(len(lens), dtype=np.int32)
+        for k, r in enumerate(replies):
+            a = np.frombuffer(r, dtype=np.uint32)
+            results[2 * offsets[k]:2 * offsets[k] + len(a)] = a
+            rb[k] = len(r)
+        return PassResult(torch.from_numpy(results.view(np.int32)).to(device), torch.from_numpy(rb).to(device), offsets)
+
+
+def _events_np(events):
+    return events.cpu().numpy().reshape(-1).view(TRANSFER_DTYPE)
+
+
+def _u128(lo, hi):
+    return (int(hi) << 64) | int(lo)
+
+
+def _ids(lo, hi):
+    return np.stack([np.asarray(lo, dtype=np.uint64), np.asarray(hi, dtype=np.uint64)], axis=1)
+
+
+def _unique_ids(ids):
+    ids = ids[~(((ids[:, 0] == 0) & (ids[:, 1] == 0)) | ((ids[:, 0] == U64_MAX) & (ids[:, 1] == U64_MAX)))]
+    if len(ids) == 0:
+        return ids.reshape(0, 2)
+    return np.unique(ids, axis=0)
+
+
+class GpuShard:
+    """Backend of one rank: the HIP engine on this rank's GPU (include/tbgpu_shard.h)."""
+
+    def __init__(self, engine, world, events_max, device=None):
+        self.engine = engine
+        self.lib = engine.lib
+        self.world = world
+        self.device = device if device is not None else torch.device("cuda", engine.options.device)
+        self.events_max = events_max
+        engine.route_init(world, events_max)
+        self._scratch = None
+
+    # -- clean pass ------------------------------------------------------------------------
+    def plan(self, timestamps, lens, events):
+        import ctypes
+        n = events.shape[0]
+        nb = len(lens)
+        send_events = torch.empty_like(events)
+        send_ts = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        slots = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        p = _lib.tbgpu_route_plan()
+        ts = (ctypes.c_uint64 * max(nb, 1))(*[int(t) for t in timestamps])
+        ls = (ctypes.c_uint32 * max(nb, 1))(*[int(x) for x in lens])
+        torch.cuda.synchronize(self.device)
+        _lib.check(self.lib.tbgpu_route_plan_build(self.engine.h, nb, ts, ls, events.data_ptr(), send_events.data_ptr(),
+                                                   send_ts.data_ptr(), slots.data_ptr(), ctypes.byref(p)))
+        plan = RoutePlan([int(p.send_counts[i]) for i in range(self.world)], _u128(p.sum_lo, p.sum_hi),
+                         _u128(p.bound_lo, p.bound_hi), int(p.dirty))
+        return plan, send_events, send_ts[:n], slots[:n]
+
+    def commit_routed(self, events, ts, ts_max, cert):
+        m = events.shape[0]
+        codes = torch.empty(max(m, 1), dtype=torch.uint8, device=self.device)
+        if m:
+            torch.cuda.synchronize(self.device)
+            _lib.check(self.lib.tbgpu_commit_routed_async(self.engine.h, m, events.data_ptr(), ts.data_ptr(), ts_max,
+                                                          cert, codes.data_ptr()))
+            self.engine.sync()
+        return codes[:m]
+
+    def replies(self, lens, slots, codes_back):
+        import ctypes
+        nb = len(lens)
+        n = int(sum(lens))
+        results = torch.empty(2 * max(n, 1), dtype=torch.int32, device=self.device)
+        reply_bytes = torch.zeros(max(nb, 1), dtype=torch.int32, device=self.device)
+        if nb:
+            ls = (ctypes.c_uint32 * nb)(*[int(x) for x in lens])
+            torch.cuda.synchronize(self.device)
+            _lib.check(self.lib.tbgpu_route_replies_async(self.engine.h, nb, ls, slots.data_ptr(), codes_back.data_ptr(),
+                                                          results.data_ptr(), reply_bytes.data_ptr()))
+            self.engine.sync()
+        offsets = np.concatenate([[0], np.cumsum(lens, dtype=np.int64)])
+        return PassResult(results, reply_bytes[:nb], offsets)
+
+    # -- host-side primitives ----------------------------------------------------------------
+    def commit_batches(self, operation, timestamps, bodies):
+        return self.engine.commit_many(operation, timestamps, bodies)
+
+    def fetch_accounts(self, ids):
+        return self.engine.fetch_accounts(ids)
+
+    def fetch_transfers(self, ids):
+        return self.engine.fetch_transfers(ids)
+
+    def upsert_accounts(self, records):
+        self.engine.upsert_accounts(records)
+
+    def upsert_transfers(self, records, state):
+        self.engine.upsert_transfers(records, state)
+
+    @property
+    def commit_timestamp(self):
+        return self.engine.commit_timestamp
+
+    def export_accounts(self):
+        return self.engine.export_accounts()
+
+    def export_transfers(self):
+        return self.engine.export_transfers()
+
+    def export_posted(self):
+        return self.engine.export_posted()
+
+    def scratch(self, accounts, transfers):
+        """A scratch engine on this GPU for dirty passes, sized for the pass (grown on demand)."""
+        from .state_machine import Engine, Options
+        need_a = max(1024, 1 << int(accounts).bit_length())
+        need_t = max(1024, 1 << int(transfers).bit_length())
+        s = self._scratch
+        if s is None or s.options.accounts_max < need_a or s.options.transfers_max < need_t:
+            if s is not None:
+                s.close()
+            o = self.engine.options
+            s = Engine(Options(accounts_max=need_a, transfers_max=need_t, pass_events_max=8190 * 64,
+                               pass_batches_max=512, device=o.device))
+            self._scratch = s
+        else:
+            s.reset()
+        return _ScratchGpu(s)
+
+
+class _ScratchGpu:
+    def __init__(self, engine):
+        self.engine = engine
+
+    def upsert_accounts(self, records):
+        self.engine.upsert_accounts(records)
+
+    def upsert_transfers(self, records, state):
+        self.engine.upsert_transfers(records, state)
+
+    def fetch_accounts(self, ids):
+        return self.engine.fetch_accounts(ids)
+
+    def fetch_transfers(self, ids):
+        return self.engine.fetch_transfers(ids)
+
+    def commit_batches(self, operation, timestamps, bodies):
+        return self.engine.commit_many(operation, timestamps, bodies)
+
+    @property
+    def commit_timestamp(self):
+        return self.engine.commit_timestamp
+
+
+class ShardedStateMachine:
+    """Collective create/lookup over every rank of a process group (one backend per rank)."""
+
+    def __init__(self, backend, group=None):
+        self.b = backend
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        assert backend.world == self.world
+        self.comm_device = torch.device("cpu") if dist.get_backend(group) == "gloo" else backend.device
+        self.commit_timestamp = 0
+        self.passes_clean = 0
+        self.passes_dirty = 0
+
+    # -- collectives helpers -----------------------------------------------------------------
+    def _all_gather_i64(self, values):
+        t = torch.tensor(values, dtype=torch.int64, device=self.comm_device)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t, group=self.group)
+        return np.stack([o.cpu().numpy() for o in out])
+
+    def _a2a(self, send, send_counts, recv_counts):
+        """all_to_all_single on rows; `send` rows grouped by destination rank.  Returns the received
+        rows (grouped by source rank) on the backend device."""
+        shape = tuple(send.shape[1:])
+        out = torch.empty((int(sum(recv_counts)),) + shape, dtype=send.dtype, device=self.comm_device)
+        src = send.to(self.comm_device)
+        if self.comm_device.type == "cuda":
+            torch.cuda.synchronize(self.comm_device)
+        dist.all_to_all_single(out, src.contiguous(), [int(c) for c in recv_counts], [int(c) for c in send_counts],
+                               group=self.group)
+        return out.to(self.b.device)
+
+    def _bcast_np(self, arr, dtype):
+        """Broadcast a numpy array (root 0) of `dtype`; returns it on every rank."""
+        dtype = np.dtype(dtype)
+        raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1) if self.rank == 0 else None
+        size = torch.tensor([raw.size if raw is not None else 0], dtype=torch.int64, device=self.comm_device)
+        dist.broadcast(size, 0, group=self.group)
+        n = int(size.item())
+        t = (torch.from_numpy(raw.copy()).to(self.comm_device) if self.rank == 0
+             else torch.empty(n, dtype=torch.uint8, device=self.comm_device))
+        if n:
+            dist.broadcast(t, 0, group=self.group)
+        return t.cpu().numpy().view(dtype)
+
+    def _gather_np(self, arr, dtype):
+        """Gather a numpy array from every rank to rank 0 (list by rank there, None elsewhere)."""
+        dtype = np.dtype(dtype)
+        raw = np.ascontiguousarray(arr, dtype=dtype).view(np.uint8).reshape(-1)
+        sizes = self._all_gather_i64([raw.size])[:, 0]
+        send_counts = [raw.size if r == 0 else 0 for r in range(self.world)]
+        recv_counts = list(sizes) if self.rank == 0 else [0] * self.world
+        out = self._a2a(torch.from_numpy(raw.copy()), send_counts, recv_counts).cpu().numpy()
+        if self.rank != 0:
+            return None
+        parts, o = [], 0
+        for s in sizes:
+            parts.append(out[o:o + s].view(dtype))
+            o += s
+        return parts
+
+    def _sum_balances(self, records):
+        """Records identical on every rank but the balances: sum the balances over ranks (mod 2^128)."""
+        n = len(records)
+        if n == 0:
+            return records
+        limbs = np.zeros((n, 4, 4), dtype=np.int64)
+        for f, name in enumerate(_BAL_FIELDS):
+            lo = records[name + "_lo"].astype(np.uint64)
+            hi = records[name + "_hi"].astype(np.uint64)
+            limbs[:, f, 0] = (lo & 0xFFFFFFFF).astype(np.int64)
+            limbs[:, f, 1] = (lo >> np.uint64(32)).astype(np.int64)
+            limbs[:, f, 2] = (hi & 0xFFFFFFFF).astype(np.int64)
+            limbs[:, f, 3] = (hi >> np.uint64(32)).astype(np.int64)
+        t = torch.from_numpy(limbs).to(self.comm_device)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        s = t.cpu().numpy()
+        for k in range(3):  # carry propagation; the top limb wraps (mod 2^128)
+            s[:, :, k + 1] += s[:, :, k] >> 32
+            s[:, :, k] &= 0xFFFFFFFF
+        s[:, :, 3] &= 0xFFFFFFFF
+        out = records.copy()
+        su = s.astype(np.uint64)
+        for f, name in enumerate(_BAL_FIELDS):
+            out[name + "_lo"] = su[:, f, 0] | (su[:, f, 1] << np.uint64(32))
+            out[name + "_hi"] = su[:, f, 2] | (su[:, f, 3] << np.uint64(32))
+        return out
+
+    def _homes(self, ids):
+        lib = _lib.load()
+        ids = np.ascontiguousarray(ids, dtype=np.uint64).reshape(-1, 2)
+        out = np.zeros(len(ids), dtype=np.uint32)
+        if len(ids):
+            lib.tbgpu_homes(ids.ctypes.data, len(ids), self.world, out.ctypes.data)
+        return out
+
+    def _finish(self, local_ts):
+        t = torch.tensor([int(local_ts)], dtype=torch.int64, device=self.comm_device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        self.commit_timestamp = max(self.commit_timestamp, int(t.item()))
+
+    # -- commit ------------------------------------------------------------------------------
+    def commit(self, operation, timestamps, lens, events):
+        """Collective: commit this rank's prepares (batch k = lens[k] events at timestamps[k],
+        back to back in `events`, a uint8 [n, 128] tensor on the backend device).  Returns a
+        PassResult for this rank's prepares."""
+        operation = Operation(int(operation))
+        lens = [int(x) for x in lens]
+        timestamps = [int(t) for t in timestamps]
+        assert events.shape[0] == sum(lens) and len(lens) == len(timestamps)
+        self._check_order(timestamps, lens)
+        if operation == Operation.create_accounts:
+            return self._commit_replicated(operation, timestamps, lens, events)
+        if operation != Operation.create_transfers:
+            raise ValueError("commit: create operations only (use lookup_accounts / lookup_transfers)")
+        plan, send_events, send_ts, slots = self.b.plan(timestamps, lens, events)
+        g = self._all_gather_i64([plan.dirty, plan.S & 0xFFFFFFFF, (plan.S >> 32) & 0xFFFFFFFF,
+                                  (plan.S >> 64) & 0xFFFFFFFF, plan.S >> 96, plan.bound & 0xFFFFFFFF,
+                                  (plan.bound >> 32) & 0xFFFFFFFF, (plan.bound >> 64) & 0xFFFFFFFF, plan.bound >> 96])
+        dirty = int(np.bitwise_or.reduce(g[:, 0]))
+        total = 0
+        for r in range(self.world):
+            total += sum(int(g[r, 1 + k]) << (32 * k) for k in range(4))
+            total += sum(int(g[r, 5 + k]) << (32 * k) for k in range(4))
+        if dirty or total >= U128:
+            self.passes_dirty += 1
+            return self._commit_dirty(operation, timestamps, lens, events)
+        self.passes_clean += 1
+        cert = _lib.CERT_U64 if total < U64 else _lib.CERT_U128
+        return self._commit_routed(plan, send_events, send_ts, slots, lens, cert)
+
+    def _check_order(self, timestamps, lens):
+        first = timestamps[0] - lens[0] + 1 if lens else 0
+        prev = None
+        for t, L in zip(timestamps, lens):
+            if prev is not None and not (t - L + 1 > prev and t > prev):
+                raise _lib.EnginePanic(_lib.STATUS_PANIC, "prepare timestamps not increasing")
+            prev = t
+        g = self._all_gather_i64([len(lens), first, timestamps[-1] if lens else 0])
+        last = self.commit_timestamp
+        for r in range(self.world):
+            if g[r, 0] == 0:
+                continue
+            if not (g[r, 1] > last and g[r, 2] > last):
+                raise _lib.EnginePanic(_lib.STATUS_PANIC, "timestamp <= commit timestamp (rank %d)" % r)
+            last = int(g[r, 2])
+        self._pass_ts_max = last
+
+    def _commit_routed(self, plan, send_events, send_ts, slots, lens, cert):
+        recv_counts = self._a2a(torch.tensor(plan.counts, dtype=torch.int64), [1] * self.world,
+                                [1] * self.world).cpu().numpy()
+        recv_events = self._a2a(send_events, plan.counts, recv_counts)
+        recv_ts = self._a2a(send_ts, plan.counts, recv_counts)
+        codes = self.b.commit_routed(recv_events, recv_ts, self._pass_ts_max, cert)
+        codes_back = self._a2a(codes, recv_counts, plan.counts)
+        result = self.b.replies(lens, slots, codes_back)
+        self._finish(self.b.commit_timestamp)
+        return result
+
+    def _commit_replicated(self, operation, timestamps, lens, events):
+        """create_accounts: every rank commits every prepare of the pass (records are replicated)."""
+        meta = self._all_gather_i64([len(lens), events.shape[0]])
+        ts_all = self._gather_all_np(np.asarray(timestamps, dtype=np.uint64), meta[:, 0])
+        lens_all = self._gather_all_np(np.asarray(lens, dtype=np.uint64), meta[:, 0])
+        n_max = int(meta[:, 1].max())
+        padded = torch.zeros((max(n_max, 1), 128), dtype=torch.uint8, device=self.comm_device)
+        padded[:events.shape[0]] = events.to(self.comm_device)
+        parts = [torch.empty_like(padded) for _ in range(self.world)]
+        dist.all_gather(parts, padded, group=self.group)
+        bodies, stamps, own = [], [], None
+        for r in range(self.world):
+            ev = parts[r][:int(meta[r, 1])].cpu().numpy().reshape(-1)
+            o = 0
+            if r == self.rank:
+                own = (len(bodies), len(bodies) + int(meta[r, 0]))
+            for t, L in zip(ts_all[r], lens_all[r]):
+                bodies.append(ev[o:o + int(L) * 128].tobytes())
+                stamps.append(int(t))
+                o += int(L) * 128
+        replies = self.b.commit_batches(int(operation), stamps, bodies) if bodies else []
+        self._finish(self.b.commit_timestamp)
+        return PassResult.from_bytes(replies[own[0]:own[1]], lens, self.b.device)
+
+    def _gather_all_np(self, arr, counts):
+        """All-gather a 1-D uint64 array of per-rank length counts[r]."""
+        m = max(int(counts.max()), 1)
+        pad = np.zeros(m, dtype=np.int64)
+        pad[:len(arr)] = arr.view(np.int64)
+        g = self._all_gather_i64(list(pad))
+        return [g[r, :int(counts[r])].view(np.uint64) for r in range(self.world)]
+
+    # -- dirty pass: prefetch on rank 0, commit on a scratch engine, write back -----------------
+    def _commit_dirty(self, operation, timestamps, lens, events):
+        W, root = self.world, self.rank == 0
+        meta = self._all_gather_i64([len(lens), events.shape[0]])
+        ts_all = self._gather_all_np(np.asarray(timestamps, dtype=np.uint64), meta[:, 0])
+        lens_all = self._gather_all_np(np.asarray(lens, dtype=np.uint64), meta[:, 0])
+        send_counts = [events.shape[0] if r == 0 else 0 for r in range(W)]
+        recv_counts = list(meta[:, 1]) if root else [0] * W
+        gathered = self._a2a(events, send_counts, recv_counts)
+
+        # 1. transfers the pass reads: every event id, and the pending id of post/void events.
+        if root:
+            ev = _events_np(gathered)
+            pv = (ev["flags"] & (TransferFlags.post_pending_transfer | TransferFlags.void_pending_transfer)) != 0
+            tids = _unique_ids(np.concatenate([_ids(ev["id_lo"], ev["id_hi"]),
+                                               _ids(ev["pending_id_lo"][pv], ev["pending_id_hi"][pv])]))
+        tids = self._bcast_np(tids if root else None, np.uint64).reshape(-1, 2)
+        homes = self._homes(tids)
+        mine = np.nonzero(homes == self.rank)[0]
+        recs, state = self.b.fetch_transfers(tids[mine])
+        recs_parts = self._gather_np(recs, TRANSFER_DTYPE)
+        state_parts = self._gather_np(state, np.uint8)
+        if root:
+            fetched = np.zeros(len(tids), dtype=TRANSFER_DTYPE)
+            fstate = np.zeros(len(tids), dtype=np.uint8)
+            for r in range(W):
+                idx = np.nonzero(homes == r)[0]
+                fetched[idx] = recs_parts[r]
+                fstate[idx] = state_parts[r]
+            present = fstate != 0
+            aids = _unique_ids(np.concatenate([
+                _ids(ev["debit_account_id_lo"], ev["debit_account_id_hi"]),
+                _ids(ev["credit_account_id_lo"], ev["credit_account_id_hi"]),
+                _ids(fetched["debit_account_id_lo"][present], fetched["debit_account_id_hi"][present]),
+                _ids(fetched["credit_account_id_lo"][present], fetched["credit_account_id_hi"][present])]))
+
+        # 2. the touched accounts with their true (summed) balances.
+        aids = self._bcast_np(aids if root else None, np.uint64).reshape(-1, 2)
+        accts, afound = self.b.fetch_accounts(aids)
+        accts = self._sum_balances(accts)
+        afound = afound.astype(bool)
+
+        # 3. rank 0 commits the pass on the scratch engine.
+        if root:
+            scratch = self.b.scratch(int(afound.sum()) + 1, int(present.sum()) + len(ev) + 1)
+            scratch.upsert_accounts(accts[afound])
+            scratch.upsert_transfers(fetched[present], fstate[present])
+            bodies, stamps, o = [], [], 0
+            evb = gathered.cpu().numpy().reshape(-1)
+            for r in range(W):
+                for t, L in zip(ts_all[r], lens_all[r]):
+                    bodies.append(evb[o:o + int(L) * 128].tobytes())
+                    stamps.append(int(t))
+                    o += int(L) * 128
+            replies = scratch.commit_batches(int(operation), stamps, bodies)
+            after, astate = scratch.fetch_transfers(tids)
+            changed = (astate != 0) & (astate != fstate)
+            wb_t, wb_s = after[changed], astate[changed]
+            acc_after, _ = scratch.fetch_accounts(aids[afound])
+            local_ts = scratch.commit_timestamp
+            rlens = np.asarray([len(r) for r in replies], dtype=np.int64)
+            rbytes = np.frombuffer(b"".join(replies), dtype=np.uint8)
+        else:
+            local_ts = 0
+
+        # 4. write back: new transfers and posted states to their homes, balances collected on
+        #    rank 0 (every other rank's partial of a touched account becomes 0).
+        wb_t = self._bcast_np(wb_t if root else None, TRANSFER_DTYPE)
+        wb_s = self._bcast_np(wb_s if root else None, np.uint8)
+        if len(wb_t):
+            h = self._homes(_ids(wb_t["id_lo"], wb_t["id_hi"]))
+            sel = h == self.rank
+            self.b.upsert_transfers(wb_t[sel], wb_s[sel])
+        if root:
+            self.b.upsert_accounts(acc_after)
+        else:
+            zero = accts[afound].copy()
+            for name in _BAL_FIELDS:
+                zero[name + "_lo"] = 0
+                zero[name + "_hi"] = 0
+            self.b.upsert_accounts(zero)
+
+        # 5. replies back to their ranks.
+        rlens = self._bcast_np(rlens if root else None, np.int64)
+        rbytes = self._bcast_np(rbytes if root else None, np.uint8)
+        first = int(meta[:self.rank, 0].sum())
+        offs = np.concatenate([[0], np.cumsum(rlens)])
+        mine_r = [rbytes[offs[k]:offs[k + 1]].tobytes() for k in range(first, first + len(lens))]
+        self._finish(local_ts)
+        return PassResult.from_bytes(mine_r, lens, self.b.device)
+
+    def test_set_balances(self, account_id, dp, dpost, cp, cpost):
+        """Collective test-only `setup` action (state_machine.zig:1398-1407): rank 0's partial holds
+        the balances, every other rank's partial becomes 0."""
+        ids = np.array([[account_id & U64_MAX, account_id >> 64]], dtype=np.uint64)
+        recs, found = self.b.fetch_accounts(ids)
+        if not found[0]:
+            raise _lib.EnginePanic(_lib.STATUS_PANIC, "setup of a missing account")
+        for name, v in zip(_BAL_FIELDS, (dp, dpost, cp, cpost)):
+            v = v if self.rank == 0 else 0
+            recs[name + "_lo"] = v & U64_MAX
+            recs[name + "_hi"] = v >> 64
+        self.b.upsert_accounts(recs)
+
+    # -- lookups (execute_lookup_accounts / _transfers, state_machine.zig:700-736) -------------
+    def lookup_accounts(self, ids):
+        """Collective: found accounts in input order, with the summed balances."""
+        ids = np.ascontiguousarray(ids, dtype=np.uint64).reshape(-1, 2)
+        recs, found = self.b.fetch_accounts(ids)
+        recs = self._sum_balances(recs)
+        return recs[found.astype(bool)]
+
+    def lookup_transfers(self, ids):
+        """Collective: found transfers in input order (each lives on exactly one home)."""
+        ids = np.ascontiguousarray(ids, dtype=np.uint64).reshape(-1, 2)
+        homes = self._homes(ids)
+        recs = np.zeros(len(ids), dtype=TRANSFER_DTYPE)
+        mine = np.nonzero(homes == self.rank)[0]
+        r, st = self.b.fetch_transfers(ids[mine])
+        found = np.zeros(len(ids), dtype=np.int64)
+        recs[mine] = r
+        found[mine] = st != 0
+        words = torch.from_numpy(recs.view(np.int64).reshape(-1).copy()).to(self.comm_device)
+        f = torch.from_numpy(found).to(self.comm_device)
+        dist.all_reduce(words, op=dist.ReduceOp.SUM, group=self.group)  # one non-zero term per id
+        dist.all_reduce(f, op=dist.ReduceOp.SUM, group=self.group)
+        out = words.cpu().numpy().view(TRANSFER_DTYPE)
+        return out[f.cpu().numpy() != 0]
+
+    # -- parity read-back ------------------------------------------------------------------------
+    def export_accounts(self):
+        """Collective: every account (sorted by id) with summed balances."""
+        return self._sum_balances(self.b.export_accounts())
+
+    def export_transfers(self):
+        """Collective: rank 0 receives every transfer sorted by id (None elsewhere)."""
+        parts = self._gather_np(self.b.export_transfers(), TRANSFER_DTYPE)
+        if parts is None:
+            return None
+        t = np.concatenate(parts)
+        order = np.lexsort((t["id_lo"], t["id_hi"]))
+        return t[order]
+
+    def export_posted(self):
+        """Collective: rank 0 receives the posted groove {pending timestamp, fulfillment}, sorted."""
+        parts = self._gather_np(np.ascontiguousarray(self.b.export_posted(), dtype=np.uint64).reshape(-1), np.uint64)
+        if parts is None:
+            return None
+        p = np.concatenate(parts).reshape(-1, 2)
+        return p[np.lexsort((p[:, 1], p[:, 0]))]

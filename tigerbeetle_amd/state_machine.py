@@ -147,6 +147,41 @@ class Engine:
     def reset_stats(self):
         self.lib.tbgpu_reset_stats(self.h)
 
+    # -- multi-GPU primitives (include/tbgpu_shard.h; driven by tigerbeetle_amd.sharded) -------
+    def route_init(self, world, events_max):
+        _lib.check(self.lib.tbgpu_route_init(self.h, world, events_max))
+
+    def fetch_accounts(self, ids):
+        """ids: uint64 [n, 2] (lo, hi).  Returns (ACCOUNT_DTYPE[n], found uint8[n])."""
+        ids = np.ascontiguousarray(ids, dtype=np.uint64).reshape(-1, 2)
+        n = ids.shape[0]
+        out = np.zeros(n, dtype=ACCOUNT_DTYPE)
+        found = np.zeros(n, dtype=np.uint8)
+        if n:
+            _lib.check(self.lib.tbgpu_fetch_accounts(self.h, ids.ctypes.data, n, out.ctypes.data, found.ctypes.data))
+        return out, found
+
+    def fetch_transfers(self, ids):
+        """ids: uint64 [n, 2].  Returns (TRANSFER_DTYPE[n], state uint8[n]: 0 absent, 1 + posted)."""
+        ids = np.ascontiguousarray(ids, dtype=np.uint64).reshape(-1, 2)
+        n = ids.shape[0]
+        out = np.zeros(n, dtype=TRANSFER_DTYPE)
+        state = np.zeros(n, dtype=np.uint8)
+        if n:
+            _lib.check(self.lib.tbgpu_fetch_transfers(self.h, ids.ctypes.data, n, out.ctypes.data, state.ctypes.data))
+        return out, state
+
+    def upsert_accounts(self, records):
+        records = np.ascontiguousarray(records, dtype=ACCOUNT_DTYPE)
+        if len(records):
+            _lib.check(self.lib.tbgpu_upsert_accounts(self.h, records.ctypes.data, len(records)))
+
+    def upsert_transfers(self, records, state):
+        records = np.ascontiguousarray(records, dtype=TRANSFER_DTYPE)
+        state = np.ascontiguousarray(state, dtype=np.uint8)
+        if len(records):
+            _lib.check(self.lib.tbgpu_upsert_transfers(self.h, records.ctypes.data, state.ctypes.data, len(records)))
+
     # -- device memory + workload generation (bench) -----------------------------------------
     def alloc(self, nbytes):
         p = ctypes.c_void_p()
