@@ -18,7 +18,7 @@
  * result then depends only on state its home holds (create_transfer reads balances only for
  * balancing :826-846, overflow :848-861 and limits :863-868), so a clean pass is:
  *     tbgpu_route_plan         (every rank: classify + group its events by home)
- *     all-to-all of events and timestamps
+ *     all-to-all of the events (each carrying its execute timestamp)
  *     tbgpu_commit_routed_async (every home: the normal kernels, per-event timestamps and codes)
  *     all-to-all of the result codes back
  *     tbgpu_route_replies_async (every rank: sparse replies per prepare).
@@ -65,18 +65,20 @@ typedef struct tbgpu_route_plan {
 
 /* Classify this rank's share of a create_transfers pass (n_batches prepares of batch_lens[k]
  * events at timestamps[k], back to back in events_dev) and group it by home: send_events_dev
- * (128 B per event) and send_ts_dev (its execute timestamp, state_machine.zig:645) receive the
- * events home by home, each home's run in input order; slot_dev[e] = event e's send position.
+ * receives the events home by home (128 B each, the timestamp field set to the event's execute
+ * timestamp, state_machine.zig:645), each home's run in input order; slot_dev[e] = event e's send
+ * position, or 0xFFFFFFFF for an event whose timestamp field was non-zero (it fails with
+ * timestamp_must_be_zero, :643, before reading any state: answered here, never routed).
  * Synchronous (the plan is needed on the host for the collectives). */
 int tbgpu_route_plan_build(tbgpu_t* engine, uint32_t n_batches, const uint64_t* timestamps,
                            const uint32_t* batch_lens, const void* events_dev, void* send_events_dev,
-                           uint64_t* send_ts_dev, uint32_t* slot_dev, tbgpu_route_plan* plan);
+                           uint32_t* slot_dev, tbgpu_route_plan* plan);
 
-/* Commit `n` routed events (this home's share of a clean pass, in global order) with per-event
- * timestamps; codes_dev[i] = result code of event i.  `cert` = TBGPU_CERT_*.  `ts_max` = the last
- * timestamp of the global pass (host-side ordering state).  Enqueued; tbgpu_sync() waits. */
-int tbgpu_commit_routed_async(tbgpu_t* engine, uint64_t n, const void* events_dev, const uint64_t* ts_dev,
-                              uint64_t ts_max, uint32_t cert, uint8_t* codes_dev);
+/* Commit `n` routed events (this home's share of a clean pass, in global order, each carrying its
+ * execute timestamp); codes_dev[i] = result code of event i.  `cert` = TBGPU_CERT_*.  `ts_max` =
+ * the last timestamp of the global pass (host-side ordering state).  Enqueued; tbgpu_sync() waits. */
+int tbgpu_commit_routed_async(tbgpu_t* engine, uint64_t n, const void* events_dev, uint64_t ts_max,
+                              uint32_t cert, uint8_t* codes_dev);
 
 /* Sparse per-prepare replies from the returned codes (codes_dev in send order): batch k's reply
  * at results_dev + 8*offset_k, its size in reply_bytes_dev[k]. Enqueued. */

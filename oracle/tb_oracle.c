@@ -904,18 +904,13 @@ int tbo_sum_overflows_u128(uint64_t a_lo, uint64_t a_hi, uint64_t b_lo, uint64_t
 /* fallback logic can be tested with gloo on CPU.                                              */
 /* ------------------------------------------------------------------------------------------ */
 
-int tbo_commit_routed(tbo_state* s, uint64_t n, const void* events, const uint64_t* ts, uint8_t* codes) {
+int tbo_commit_routed(tbo_state* s, uint64_t n, const void* events, uint8_t* codes) {
     if (setjmp(s->panic_jmp)) return TBO_STATUS_PANIC;
     for (u64 i = 0; i < n; i++) {
-        transfer_t t;
+        transfer_t t; /* t.timestamp = the execute timestamp assigned by the source */
         memcpy(&t, (const u8*)events + i * 128, 128);
         if (t.flags & (1 | 4 | 8 | 16 | 32)) return TBO_STATUS_INVALID; /* never routed */
-        if (!(ts[i] > s->commit_timestamp)) return TBO_STATUS_PANIC;
-        if (t.timestamp != 0) {
-            codes[i] = CT_TIMESTAMP_MUST_BE_ZERO;
-            continue;
-        }
-        t.timestamp = ts[i];
+        if (!(t.timestamp > s->commit_timestamp)) return TBO_STATUS_PANIC;
         codes[i] = (uint8_t)create_transfer(s, &t);
     }
     return TBO_STATUS_OK;

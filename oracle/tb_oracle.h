@@ -70,11 +70,12 @@ uint64_t tbo_export_transfers(const tbo_state* s, void* out, uint64_t cap);
 uint64_t tbo_export_posted(const tbo_state* s, uint64_t* out_pairs, uint64_t cap);
 
 /* Shard test double (tests/harness/shard_double.py): CPU restatements of the per-rank primitives
- * of include/tbgpu_shard.h.  commit_routed: create_transfer for each event with the given
- * timestamp (execute's per-event body, state_machine.zig:641-662), codes[i] = its result;
+ * of include/tbgpu_shard.h.  commit_routed: create_transfer for each event, whose timestamp
+ * field holds its execute timestamp (execute's per-event body, state_machine.zig:641-662),
+ * codes[i] = its result;
  * linked/post/void/balancing events are rejected (TBO_STATUS_INVALID).  fetch/upsert: as the
  * tbgpu_* calls of the same name.  balance_bound: max over accounts of dp+dpost, cp+cpost. */
-int tbo_commit_routed(tbo_state* s, uint64_t n, const void* events, const uint64_t* ts, uint8_t* codes);
+int tbo_commit_routed(tbo_state* s, uint64_t n, const void* events, uint8_t* codes);
 int tbo_fetch_accounts(const tbo_state* s, const uint64_t* ids, uint32_t n, void* out, uint8_t* found);
 int tbo_fetch_transfers(const tbo_state* s, const uint64_t* ids, uint32_t n, void* out, uint8_t* state);
 int tbo_upsert_accounts(tbo_state* s, const void* records, uint32_t n);

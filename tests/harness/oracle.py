@@ -50,7 +50,7 @@ def lib():
         L.tbo_export_posted.restype = c.c_uint64
         L.tbo_export_posted.argtypes = [c.c_void_p, c.c_void_p, c.c_uint64]
         L.tbo_commit_routed.restype = c.c_int
-        L.tbo_commit_routed.argtypes = [c.c_void_p, c.c_uint64, c.c_void_p, c.c_void_p, c.c_void_p]
+        L.tbo_commit_routed.argtypes = [c.c_void_p, c.c_uint64, c.c_void_p, c.c_void_p]
         for name in ("tbo_fetch_accounts", "tbo_fetch_transfers"):
             getattr(L, name).restype = c.c_int
             getattr(L, name).argtypes = [c.c_void_p, c.c_void_p, c.c_uint32, c.c_void_p, c.c_void_p]
@@ -141,12 +141,11 @@ class OracleEngine:
         return out[:m]
 
     # -- shard test double primitives (tbo_* restatements of include/tbgpu_shard.h) -----------
-    def commit_routed(self, events, ts):
-        events = np.ascontiguousarray(events, dtype=np.uint8)
-        ts = np.ascontiguousarray(ts, dtype=np.uint64)
-        n = len(ts)
+    def commit_routed(self, events):
+        events = np.ascontiguousarray(events, dtype=np.uint8).reshape(-1)
+        n = events.size // 128
         codes = np.zeros(max(n, 1), dtype=np.uint8)
-        st = self.L.tbo_commit_routed(self.h, n, events.ctypes.data, ts.ctypes.data, codes.ctypes.data)
+        st = self.L.tbo_commit_routed(self.h, n, events.ctypes.data, codes.ctypes.data)
         if st == STATUS_PANIC:
             raise OraclePanic("oracle panic in a routed commit")
         if st != STATUS_OK:

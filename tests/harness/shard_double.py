@@ -48,28 +48,36 @@ class OracleShard:
                 recs, found = self.o.fetch_accounts(ids)
                 if np.any(((recs["flags"] & _LIMITS) != 0) & found.astype(bool)):
                     dirty |= _lib.DIRTY_LIMIT
-        S = 0
-        for lo, hi in zip(ev["amount_lo"], ev["amount_hi"]):
-            S = min(S + ((int(hi) << 64) | int(lo)), U128_MAX)
-        ts = np.zeros(n, dtype=np.int64)
+        ts = np.zeros(n, dtype=np.uint64)
         o = 0
         for t, L in zip(timestamps, lens):
-            ts[o:o + L] = int(t) - L + 1 + np.arange(L)
+            ts[o:o + L] = int(t) - L + 1 + np.arange(L, dtype=np.uint64)
             o += L
+        local = ev["timestamp"] != 0  # timestamp_must_be_zero: answered here, never routed
+        homes = np.where(local, self.world, homes)
         order = np.argsort(homes, kind="stable")
-        slots = np.empty(n, dtype=np.int32)
-        slots[order] = np.arange(n, dtype=np.int32)
-        counts = np.bincount(homes, minlength=self.world).tolist() if n else [0] * self.world
+        slots = np.empty(n, dtype=np.int64)
+        slots[order] = np.arange(n)
+        slots[local] = -1
+        routed = ev.copy()
+        routed["timestamp"] = ts
+        counts = np.bincount(homes[~local], minlength=self.world).tolist() if n else [0] * self.world
+        S = 0
+        for lo, hi in zip(ev["amount_lo"][~local], ev["amount_hi"][~local]):
+            S = min(S + ((int(hi) << 64) | int(lo)), U128_MAX)
         plan = RoutePlan(counts, S, self.o.balance_bound(), dirty)
-        return plan, events[torch.from_numpy(order)], torch.from_numpy(ts[order]), torch.from_numpy(slots)
+        send = torch.from_numpy(routed.view(np.uint8).reshape(-1, 128)[order[:sum(counts)]].copy())
+        return plan, send, torch.from_numpy(slots)
 
-    def commit_routed(self, events, ts, ts_max, cert):
+    def commit_routed(self, events, ts_max, cert):
         del ts_max, cert
-        codes = self.o.commit_routed(events.numpy().reshape(-1), ts.numpy().view(np.uint64))
-        return torch.from_numpy(codes.copy())
+        return torch.from_numpy(self.o.commit_routed(events.numpy()).copy())
 
     def replies(self, lens, slots, codes_back):
-        codes = codes_back.numpy()[slots.numpy()] if len(slots) else np.zeros(0, dtype=np.uint8)
+        s = slots.numpy()
+        cb = codes_back.numpy()
+        codes = np.where(s < 0, 3, cb[np.maximum(s, 0)] if len(cb) else 0).astype(np.uint8) if len(s) \
+            else np.zeros(0, dtype=np.uint8)
         out, o = [], 0
         for L in lens:
             c = codes[o:o + L]

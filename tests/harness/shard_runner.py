@@ -71,6 +71,7 @@ def run_rank(rank, world, port, kind, scenario_kw, max_prepares, result_path):
             if rank == 0:
                 for p in parts:
                     replies.extend(p)
+        sm.sync_commit_timestamp()
         accounts = sm.export_accounts()
         transfers = sm.export_transfers()
         posted = sm.export_posted()

@@ -323,10 +323,10 @@ static int engine_sync(tbgpu* E) {
 }
 
 // Enqueue every pass of one call.  meta (device) already holds the call's offsets/timestamps.
-// Routed mode (a shard of a multi-GPU pass): ev_ts = per-event timestamps, codes = dense result
-// codes instead of sparse replies, cert_ext = the router's certificate.
+// Routed mode (a shard of a multi-GPU pass): events carry their execute timestamps, codes = dense
+// result codes instead of sparse replies, cert_ext = the router's certificate.
 static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* events_dev, u32* results_dev,
-                        u32* reply_bytes_dev, const u64* ev_ts = nullptr, u8* codes = nullptr, u32 cert_ext = 0) {
+                        u32* reply_bytes_dev, bool routed = false, u8* codes = nullptr, u32 cert_ext = 0) {
     const u64* d_off = E->meta;
     const u64* d_ts = E->meta + (nb + 1);
     u32 b0 = 0;
@@ -370,7 +370,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.log_base = E->log_next;
         P.T = E->T;
         P.ablate = E->ablate;
-        P.ev_ts = ev_ts;
+        P.routed = routed ? 1 : 0;
         P.codes = codes;
         P.cert_ext = cert_ext;
 
@@ -901,8 +901,8 @@ static int route_meta(tbgpu* E, u32 nb, const u64* timestamps, const u32* lens, 
 }
 
 extern "C" int tbgpu_route_plan_build(tbgpu_t* E, uint32_t nb, const uint64_t* timestamps, const uint32_t* lens,
-                                      const void* events_dev, void* send_events_dev, uint64_t* send_ts_dev,
-                                      uint32_t* slot_dev, tbgpu_route_plan* plan) {
+                                      const void* events_dev, void* send_events_dev, uint32_t* slot_dev,
+                                      tbgpu_route_plan* plan) {
     HIPCK(hipSetDevice(E->device));
     if (!E->r_home) return fail(TBGPU_STATUS_INVALID, "tbgpu_route_init was not called");
     if (E->pending) {
@@ -934,7 +934,7 @@ extern "C" int tbgpu_route_plan_build(tbgpu_t* E, uint32_t nb, const uint64_t* t
         hipLaunchKernelGGL(tb_route_offsets, dim3(1), dim3(1024), 0, E->stream, A);
         HIPCK(hipGetLastError());
         hipLaunchKernelGGL(tb_route_scatter, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, E->stream, A, (u8*)send_events_dev,
-                           (u64*)send_ts_dev, (u32*)slot_dev);
+                           (u32*)slot_dev);
         HIPCK(hipGetLastError());
     }
     std::vector<u64> words(ROUTE_WORDS);
@@ -960,8 +960,8 @@ extern "C" int tbgpu_route_plan_build(tbgpu_t* E, uint32_t nb, const uint64_t* t
     return TBGPU_STATUS_OK;
 }
 
-extern "C" int tbgpu_commit_routed_async(tbgpu_t* E, uint64_t n, const void* events_dev, const uint64_t* ts_dev,
-                                         uint64_t ts_max, uint32_t cert, uint8_t* codes_dev) {
+extern "C" int tbgpu_commit_routed_async(tbgpu_t* E, uint64_t n, const void* events_dev, uint64_t ts_max,
+                                         uint32_t cert, uint8_t* codes_dev) {
     HIPCK(hipSetDevice(E->device));
     if (cert != TBGPU_CERT_U128 && cert != TBGPU_CERT_U64) return fail(TBGPU_STATUS_INVALID, "routed commit needs a certificate");
     if (n == 0) return TBGPU_STATUS_OK;
@@ -988,7 +988,7 @@ extern "C" int tbgpu_commit_routed_async(tbgpu_t* E, uint64_t n, const void* eve
     HIPCK(hipMemcpyAsync(E->meta, E->h_meta, (2 * nb + 1) * 8, hipMemcpyHostToDevice, E->stream));
     std::vector<u64> off(h_off, h_off + nb + 1);
     int st = enqueue_call(E, OP_CREATE_TRANSFERS, (u32)nb, off.data(), (const u8*)events_dev, E->results,
-                          E->reply_bytes, ts_dev, codes_dev, cert);
+                          E->reply_bytes, true, codes_dev, cert);
     if (st) return st;
     E->last_batch_ts = std::max(E->last_batch_ts, ts_max);
     E->pending = true;

@@ -8,8 +8,10 @@
 // (state_machine.zig:779-884 reads balances only for balancing :826-846, the overflow checks
 // :848-861 and the limit checks :863-868).  So a clean pass is
 //   1. tb_route_classify + tb_route_offsets + tb_route_scatter on every rank: the rank's events
-//      grouped by home (stable: global order survives), each with its execute timestamp
-//      (:645) — one send buffer for the all-to-all;
+//      grouped by home (stable: global order survives), each carrying its execute timestamp
+//      (:645) in its timestamp field — one send buffer for the all-to-all.  An event whose
+//      timestamp field is non-zero fails with timestamp_must_be_zero before touching any state
+//      (execute :643), so its source answers it and never routes it;
 //   2. a routed commit on every home (the normal validate/resolve/replay kernels in routed mode);
 //   3. tb_route_replies: the codes that came back, compacted into per-prepare sparse replies.
 // Dirty passes use the prefetch/write-back kernels at the bottom (tb_fetch_*, tb_upsert_*).
@@ -19,6 +21,8 @@
 
 #define ROUTE_THREADS 256
 #define ROUTE_WORLD_MAX 64
+#define ROUTE_LOCAL 0xFF
+#define SLOT_LOCAL 0xFFFFFFFFu
 
 enum : u32 { ROUTE_DIRTY_FLAGS = 1, ROUTE_DIRTY_LIMIT = 2 };
 
@@ -36,7 +40,7 @@ struct RouteArgs {
     const u64* batch_ts;   // [nb]
     u32 world;
     u32 nblocks;
-    u8* home;              // [n]
+    u8* home;              // [n] home rank, or ROUTE_LOCAL (answered by the source)
     u32* block_counts;     // [nblocks][world] (then rewritten as exclusive bases)
     u64* words;            // [2*SUM_SHARDS] S shards, [2*SUM_SHARDS] HUGE, [+1] dirty bits, [+2..] counts
     Tables T;
@@ -61,10 +65,14 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_route_classify(RouteArgs A) 
         const u64* w = (const u64*)(A.events + e * 128);
         const u64 id_lo = w[0], id_hi = w[1];
         const u16 flags = *(const u16*)(A.events + e * 128 + 118);
-        const u32 h = tb_home(id_lo, id_hi, A.world);
-        A.home[e] = (u8)h;
-        atomicAdd(&s_cnt[h], 1u);
-        amount = tb_u128(w[6], w[7]);
+        if (w[15] != 0) {
+            A.home[e] = ROUTE_LOCAL;  // timestamp_must_be_zero, answered at the source
+        } else {
+            const u32 h = tb_home(id_lo, id_hi, A.world);
+            A.home[e] = (u8)h;
+            atomicAdd(&s_cnt[h], 1u);
+            amount = tb_u128(w[6], w[7]);
+        }
         u32 dirty = 0;
         if (flags & (TF_LINKED | TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT)) {
             dirty = ROUTE_DIRTY_FLAGS;
@@ -138,8 +146,7 @@ __global__ __launch_bounds__(1024) void tb_route_offsets(RouteArgs A) {
 }
 
 // Pass 3: stable scatter into the send buffer, with the execute timestamp of every event.
-__global__ __launch_bounds__(ROUTE_THREADS) void tb_route_scatter(RouteArgs A, u8* send_events, u64* send_ts,
-                                                                 u32* slot) {
+__global__ __launch_bounds__(ROUTE_THREADS) void tb_route_scatter(RouteArgs A, u8* send_events, u32* slot) {
     __shared__ __attribute__((aligned(16))) u8 stage[ROUTE_THREADS * STAGE_STRIDE];
     __shared__ u32 s_wcnt[ROUTE_THREADS / 64][ROUTE_WORLD_MAX];
     __shared__ u32 s_range[2];
@@ -163,14 +170,18 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_route_scatter(RouteArgs A, u
     }
     __syncthreads();
     if (!live) return;
+    if (h == ROUTE_LOCAL) {
+        slot[e] = SLOT_LOCAL;
+        return;
+    }
     u32 pos = A.block_counts[(u64)blockIdx.x * A.world + h] + before;
     for (u32 w = 0; w < wave; w++) pos += s_wcnt[w][h];
     const u32 b = tb_batch_search(A.batch_off, s_range[0], s_range[1], e);
     const u64 boff = A.batch_off[b];
     const u32 L = (u32)(A.batch_off[b + 1] - boff);
-    send_ts[pos] = A.batch_ts[b] - L + 1 + (e - boff);  // execute, state_machine.zig:645
     slot[e] = pos;
-    const u8* src = stage + threadIdx.x * STAGE_STRIDE;
+    u8* src = stage + threadIdx.x * STAGE_STRIDE;
+    *(u64*)(src + 120) = A.batch_ts[b] - L + 1 + (e - boff);  // execute, state_machine.zig:645
     u32x4* dst = (u32x4*)(send_events + (u64)pos * 128);
 #pragma unroll
     for (int k = 0; k < 8; k++) dst[k] = *(const u32x4*)(src + k * 16);
@@ -188,7 +199,11 @@ __global__ __launch_bounds__(1024) void tb_route_replies(const u64* batch_off, c
     u32 running = 0;
     for (u32 c = 0; c < L; c += blockDim.x) {
         const u32 i = c + threadIdx.x;
-        const u32 code = i < L ? codes[slot[boff + i]] : R_OK;
+        u32 code = R_OK;
+        if (i < L) {
+            const u32 s = slot[boff + i];
+            code = s == SLOT_LOCAL ? R_TIMESTAMP_MUST_BE_ZERO : codes[s];
+        }
         const u64 m = __ballot(code != R_OK);
         const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
         if (lane == 0) s_wave[wave] = __popcll(m);

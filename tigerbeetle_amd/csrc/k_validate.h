@@ -279,19 +279,24 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
     const u32 b = tb_tile_batch(P, P.e0 + tile0, count, e, s_range);
     TransferScratch s;
     if (threadIdx.x < count) {
-        const Transfer t = tb_read_staged<Transfer>(stage);
+        Transfer t = tb_read_staged<Transfer>(stage);
         const u32 L = (u32)(P.batch_off[b + 1] - P.batch_off[b]);
         const u32 j = (u32)(e - P.batch_off[b]);
         u32 code;
-        if (P.ev_ts && (t.flags & (TF_LINKED | TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT))) {
-            tb_panic(P.T.g, PANIC_ASSERT);  // routed shards never receive these (router bug)
+        u64 routed_ts = 0;
+        if (P.routed) {
+            if (t.flags & (TF_LINKED | TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT)) {
+                tb_panic(P.T.g, PANIC_ASSERT);  // routed shards never receive these (router bug)
+            }
+            routed_ts = t.timestamp;
+            t.timestamp = 0;
         }
         if ((t.flags & TF_LINKED) && j == L - 1) {
             code = R_LINKED_EVENT_CHAIN_OPEN;  // execute :632-640
         } else if (t.timestamp != 0) {
             code = R_TIMESTAMP_MUST_BE_ZERO;  // :643
         } else {
-            const u64 ts = tb_event_ts(P, b, P.batch_off[b], L, j);  // :645
+            const u64 ts = P.routed ? routed_ts : P.batch_ts[b] - L + j + 1;  // :645
             code = tb_validate_transfer(P, t, ts, pe, s);
         }
         P.info[pe] = code | s.hz;

@@ -66,16 +66,18 @@ struct PassArgs {
     u32 ablate;            // timing-only ablation bits (TBGPU_ABLATE env, never in a parity run)
     // Routed mode (tbgpu_commit_routed_async, a shard of a multi-GPU pass): the events are this
     // shard's share of the global pass, in global order, with no linked/post/void/balancing event.
-    const u64* ev_ts;      // call-relative per-event timestamps (null: derived from batch_ts)
+    u32 routed;            // 1: each event carries its execute timestamp in its timestamp field
     u8* codes;             // call-relative dense result codes instead of sparse replies (or null)
     u32 cert_ext;          // 0: certificate from this engine's bound; CERT_EXT_*: given by the caller
 };
 
 enum : u32 { CERT_EXT_U128 = 1, CERT_EXT_U64 = 2 };
 
-// Timestamp of event i of batch b (execute, state_machine.zig:645), or the routed per-event one.
+// Timestamp of event i of batch b (execute, state_machine.zig:645).  A routed event carries the
+// timestamp its source assigned (the source answered timestamp_must_be_zero itself and never
+// routed such an event).
 __device__ static inline u64 tb_event_ts(const PassArgs& P, u32 b, u64 boff, u32 L, u32 i) {
-    return P.ev_ts ? P.ev_ts[boff + i] : P.batch_ts[b] - L + 1 + i;
+    return P.routed ? *(const u64*)(P.events + (boff + i) * 128 + 120) : P.batch_ts[b] - L + 1 + i;
 }
 
 enum : u32 { ABL_DEDUP = 1, ABL_SPEC = 2, ABL_ACCTS = 4, ABL_XFIND = 8, ABL_STAGE = 16, ABL_RECORD = 32, ABL_CAS = 64, EXP_NT = 128 };

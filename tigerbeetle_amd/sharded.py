@@ -112,25 +112,24 @@ class GpuShard:
         n = events.shape[0]
         nb = len(lens)
         send_events = torch.empty_like(events)
-        send_ts = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
         slots = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
         p = _lib.tbgpu_route_plan()
         ts = (ctypes.c_uint64 * max(nb, 1))(*[int(t) for t in timestamps])
         ls = (ctypes.c_uint32 * max(nb, 1))(*[int(x) for x in lens])
         torch.cuda.synchronize(self.device)
         _lib.check(self.lib.tbgpu_route_plan_build(self.engine.h, nb, ts, ls, events.data_ptr(), send_events.data_ptr(),
-                                                   send_ts.data_ptr(), slots.data_ptr(), ctypes.byref(p)))
+                                                   slots.data_ptr(), ctypes.byref(p)))
         plan = RoutePlan([int(p.send_counts[i]) for i in range(self.world)], _u128(p.sum_lo, p.sum_hi),
                          _u128(p.bound_lo, p.bound_hi), int(p.dirty))
-        return plan, send_events, send_ts[:n], slots[:n]
+        return plan, send_events[:sum(plan.counts)], slots[:n]
 
-    def commit_routed(self, events, ts, ts_max, cert):
+    def commit_routed(self, events, ts_max, cert):
         m = events.shape[0]
         codes = torch.empty(max(m, 1), dtype=torch.uint8, device=self.device)
         if m:
             torch.cuda.synchronize(self.device)
-            _lib.check(self.lib.tbgpu_commit_routed_async(self.engine.h, m, events.data_ptr(), ts.data_ptr(), ts_max,
-                                                          cert, codes.data_ptr()))
+            _lib.check(self.lib.tbgpu_commit_routed_async(self.engine.h, m, events.data_ptr(), ts_max, cert,
+                                                          codes.data_ptr()))
             self.engine.sync()
         return codes[:m]
 
@@ -331,35 +330,40 @@ class ShardedStateMachine:
         lens = [int(x) for x in lens]
         timestamps = [int(t) for t in timestamps]
         assert events.shape[0] == sum(lens) and len(lens) == len(timestamps)
-        self._check_order(timestamps, lens)
         if operation == Operation.create_accounts:
+            self._check_order(self._all_gather_i64(self._order_row(timestamps, lens)))
             return self._commit_replicated(operation, timestamps, lens, events)
         if operation != Operation.create_transfers:
             raise ValueError("commit: create operations only (use lookup_accounts / lookup_transfers)")
-        plan, send_events, send_ts, slots = self.b.plan(timestamps, lens, events)
-        g = self._all_gather_i64([plan.dirty, plan.S & 0xFFFFFFFF, (plan.S >> 32) & 0xFFFFFFFF,
-                                  (plan.S >> 64) & 0xFFFFFFFF, plan.S >> 96, plan.bound & 0xFFFFFFFF,
-                                  (plan.bound >> 32) & 0xFFFFFFFF, (plan.bound >> 64) & 0xFFFFFFFF, plan.bound >> 96])
-        dirty = int(np.bitwise_or.reduce(g[:, 0]))
-        total = 0
-        for r in range(self.world):
-            total += sum(int(g[r, 1 + k]) << (32 * k) for k in range(4))
-            total += sum(int(g[r, 5 + k]) << (32 * k) for k in range(4))
+        # One all-gather carries the ordering check, every rank's plan and the home count matrix.
+        plan, send_events, slots = self.b.plan(timestamps, lens, events)
+        limbs = lambda v: [(v >> (32 * k)) & 0xFFFFFFFF for k in range(4)]  # noqa: E731
+        g = self._all_gather_i64(self._order_row(timestamps, lens) + [plan.dirty] + limbs(plan.S) + limbs(plan.bound)
+                                 + plan.counts)
+        self._check_order(g[:, :4])
+        dirty = int(np.bitwise_or.reduce(g[:, 4]))
+        total = sum(int(g[r, 5 + k]) << (32 * (k % 4)) for r in range(self.world) for k in range(8))
         if dirty or total >= U128:
             self.passes_dirty += 1
             return self._commit_dirty(operation, timestamps, lens, events)
         self.passes_clean += 1
         cert = _lib.CERT_U64 if total < U64 else _lib.CERT_U128
-        return self._commit_routed(plan, send_events, send_ts, slots, lens, cert)
+        return self._commit_routed(plan, send_events, slots, lens, g[:, 13 + self.rank], cert)
 
-    def _check_order(self, timestamps, lens):
-        first = timestamps[0] - lens[0] + 1 if lens else 0
+    def _order_row(self, timestamps, lens):
         prev = None
         for t, L in zip(timestamps, lens):
             if prev is not None and not (t - L + 1 > prev and t > prev):
                 raise _lib.EnginePanic(_lib.STATUS_PANIC, "prepare timestamps not increasing")
             prev = t
-        g = self._all_gather_i64([len(lens), first, timestamps[-1] if lens else 0])
+        first = timestamps[0] - lens[0] + 1 if lens else 0
+        return [len(lens), first, timestamps[-1] if lens else 0, int(self.b.commit_timestamp)]
+
+    def _check_order(self, g):
+        """g[r] = [prepares, first event timestamp, last prepare timestamp, engine commit ts]: the
+        global order is rank-major and must start after the global commit timestamp
+        (state_machine.zig:518-519, :645)."""
+        self.commit_timestamp = max(self.commit_timestamp, int(g[:, 3].max()))
         last = self.commit_timestamp
         for r in range(self.world):
             if g[r, 0] == 0:
@@ -369,16 +373,16 @@ class ShardedStateMachine:
             last = int(g[r, 2])
         self._pass_ts_max = last
 
-    def _commit_routed(self, plan, send_events, send_ts, slots, lens, cert):
-        recv_counts = self._a2a(torch.tensor(plan.counts, dtype=torch.int64), [1] * self.world,
-                                [1] * self.world).cpu().numpy()
-        recv_events = self._a2a(send_events, plan.counts, recv_counts)
-        recv_ts = self._a2a(send_ts, plan.counts, recv_counts)
-        codes = self.b.commit_routed(recv_events, recv_ts, self._pass_ts_max, cert)
-        codes_back = self._a2a(codes, recv_counts, plan.counts)
-        result = self.b.replies(lens, slots, codes_back)
+    def sync_commit_timestamp(self):
+        """Collective: the global commit_timestamp (max over every engine) after the last pass."""
         self._finish(self.b.commit_timestamp)
-        return result
+        return self.commit_timestamp
+
+    def _commit_routed(self, plan, send_events, slots, lens, recv_counts, cert):
+        recv_events = self._a2a(send_events, plan.counts, recv_counts)
+        codes = self.b.commit_routed(recv_events, self._pass_ts_max, cert)
+        codes_back = self._a2a(codes, recv_counts, plan.counts)
+        return self.b.replies(lens, slots, codes_back)
 
     def _commit_replicated(self, operation, timestamps, lens, events):
         """create_accounts: every rank commits every prepare of the pass (records are replicated)."""
