@@ -18,8 +18,9 @@ FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Werr
 
 
 def _sources():
+    inc = os.path.join(ROOT, "include")
     return [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC)) if f.endswith((".hip", ".h"))] + [
-        os.path.join(ROOT, "include", "tbgpu.h"), os.path.join(ROOT, "include", "tbgpu_bench.h")]
+        os.path.join(inc, f) for f in sorted(os.listdir(inc)) if f.endswith(".h")]
 
 
 def _stale(target, sources):
@@ -40,8 +41,31 @@ def build_engine(force=False, verbose=True):
     return LIB
 
 
+HOST = os.path.join(PKG_DIR, "host")
+RUNNER = os.path.join(HOST, "tb_table_runner")
+CXX = os.environ.get("CXX", shutil.which("g++") or "g++")
+
+
+def build_host(force=False, verbose=True):
+    """The C++ host mirror (host/state_machine.*) and its golden-table runner, linked against the
+    in-tree engine (rpath $ORIGIN/..)."""
+    srcs = [os.path.join(HOST, f) for f in ("state_machine.cpp", "table_runner.cpp")]
+    deps = srcs + [os.path.join(HOST, "state_machine.hpp"), os.path.join(ROOT, "include", "tbgpu.h"), LIB]
+    if not force and not _stale(RUNNER, deps):
+        return RUNNER
+    cmd = [CXX, "-O2", "-std=c++17", "-Wall", "-Wextra", "-o", RUNNER + ".tmp"] + srcs + [
+        "-L" + PKG_DIR, "-ltbgpu", "-Wl,-rpath,$ORIGIN/.."]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(RUNNER + ".tmp", RUNNER)
+    return RUNNER
+
+
 def build(force=False, verbose=True):
-    return build_engine(force=force, verbose=verbose)
+    lib = build_engine(force=force, verbose=verbose)
+    build_host(force=force, verbose=verbose)
+    return lib
 
 
 if __name__ == "__main__":

@@ -1,0 +1,138 @@
+// state_machine.cpp — tb::StateMachine over the C ABI (include/tbgpu.h).  See state_machine.hpp.
+#include "state_machine.hpp"
+
+#include <cstring>
+
+namespace tb {
+
+const std::vector<std::string>& create_account_result_names() {
+    static const std::vector<std::string> names = {
+        "ok", "linked_event_failed", "linked_event_chain_open", "timestamp_must_be_zero", "reserved_field",
+        "reserved_flag", "id_must_not_be_zero", "id_must_not_be_int_max", "flags_are_mutually_exclusive",
+        "debits_pending_must_be_zero", "debits_posted_must_be_zero", "credits_pending_must_be_zero",
+        "credits_posted_must_be_zero", "ledger_must_not_be_zero", "code_must_not_be_zero",
+        "exists_with_different_flags", "exists_with_different_user_data_128", "exists_with_different_user_data_64",
+        "exists_with_different_user_data_32", "exists_with_different_ledger", "exists_with_different_code", "exists",
+    };
+    return names;
+}
+
+const std::vector<std::string>& create_transfer_result_names() {
+    static const std::vector<std::string> names = {
+        "ok", "linked_event_failed", "linked_event_chain_open", "timestamp_must_be_zero", "reserved_flag",
+        "id_must_not_be_zero", "id_must_not_be_int_max", "flags_are_mutually_exclusive",
+        "debit_account_id_must_not_be_zero", "debit_account_id_must_not_be_int_max",
+        "credit_account_id_must_not_be_zero", "credit_account_id_must_not_be_int_max", "accounts_must_be_different",
+        "pending_id_must_be_zero", "pending_id_must_not_be_zero", "pending_id_must_not_be_int_max",
+        "pending_id_must_be_different", "timeout_reserved_for_pending_transfer", "amount_must_not_be_zero",
+        "ledger_must_not_be_zero", "code_must_not_be_zero", "debit_account_not_found", "credit_account_not_found",
+        "accounts_must_have_the_same_ledger", "transfer_must_have_the_same_ledger_as_accounts",
+        "pending_transfer_not_found", "pending_transfer_not_pending", "pending_transfer_has_different_debit_account_id",
+        "pending_transfer_has_different_credit_account_id", "pending_transfer_has_different_ledger",
+        "pending_transfer_has_different_code", "exceeds_pending_transfer_amount",
+        "pending_transfer_has_different_amount", "pending_transfer_already_posted", "pending_transfer_already_voided",
+        "pending_transfer_expired", "exists_with_different_flags", "exists_with_different_debit_account_id",
+        "exists_with_different_credit_account_id", "exists_with_different_amount", "exists_with_different_pending_id",
+        "exists_with_different_user_data_128", "exists_with_different_user_data_64",
+        "exists_with_different_user_data_32", "exists_with_different_timeout", "exists_with_different_code", "exists",
+        "overflows_debits_pending", "overflows_credits_pending", "overflows_debits_posted", "overflows_credits_posted",
+        "overflows_debits", "overflows_credits", "overflows_timeout", "exceeds_credits", "exceeds_debits",
+    };
+    return names;
+}
+
+void StateMachine::check(int status, const char* what) const {
+    if (status == TBGPU_STATUS_OK) return;
+    const std::string msg = std::string(what) + ": " + tbgpu_last_error();
+    if (status == TBGPU_STATUS_PANIC) throw Panic(msg);
+    if (status == TBGPU_STATUS_DEVICE) throw DeviceError(msg);
+    throw std::invalid_argument(msg);
+}
+
+StateMachine::StateMachine(const Options& o) {
+    tbgpu_config cfg{};
+    cfg.accounts_max = o.accounts_max;
+    cfg.transfers_max = o.transfers_max;
+    cfg.pass_events_max = o.pass_events_max;
+    cfg.pass_batches_max = o.pass_batches_max;
+    cfg.device = o.device;
+    cfg.flags = o.profile ? TBGPU_CONFIG_PROFILE : 0;
+    const int st = tbgpu_init(&cfg, &engine_);
+    if (st != TBGPU_STATUS_OK) {
+        // init is the reference's only fallible call (`!StateMachine`).
+        throw DeviceError(std::string("tbgpu_init: ") + tbgpu_last_error());
+    }
+}
+
+StateMachine::~StateMachine() { tbgpu_deinit(engine_); }
+
+void StateMachine::reset() {
+    check(tbgpu_reset(engine_), "reset");
+    prepare_timestamp = 0;
+    commit_timestamp = 0;
+}
+
+void StateMachine::open(const Callback& callback) { callback(*this); }
+
+void StateMachine::prepare(Operation operation, const void* input, size_t input_len) {
+    (void)input;
+    // state_machine.zig:336-343: creates advance prepare_timestamp by the event count.
+    if (operation == Operation::create_accounts || operation == Operation::create_transfers) {
+        prepare_timestamp += input_len / 128;
+    }
+}
+
+void StateMachine::prefetch(const Callback& callback, uint64_t op, Operation operation, const void* input,
+                            size_t input_len) {
+    (void)operation, (void)input, (void)input_len;
+    if (op == 0) throw Panic("prefetch: op == 0");
+    // Every object is HBM-resident: the prefetch completes at once (the reference allows the
+    // callback to fire inside the call, src/lsm/groove.zig:723-742).
+    callback(*this);
+}
+
+size_t StateMachine::commit(u128 client, uint64_t op, uint64_t timestamp, Operation operation, const void* input,
+                            size_t input_len, void* output) {
+    (void)client;
+    if (op == 0) throw Panic("commit: op == 0");  // state_machine.zig:518
+    if (input_len > message_body_size_max) throw std::invalid_argument("commit: body larger than a message");
+    uint32_t out_len = 0;
+    check(tbgpu_commit(engine_, static_cast<uint8_t>(operation), timestamp, input, static_cast<uint32_t>(input_len),
+                       output, static_cast<uint32_t>(message_body_size_max), &out_len),
+          "commit");
+    commit_timestamp = tbgpu_commit_timestamp(engine_);
+    return out_len;
+}
+
+std::vector<size_t> StateMachine::commit_many(Operation operation, const std::vector<uint64_t>& timestamps,
+                                              const std::vector<const void*>& inputs,
+                                              const std::vector<size_t>& input_lens,
+                                              const std::vector<void*>& outputs) {
+    const size_t n = timestamps.size();
+    if (inputs.size() != n || input_lens.size() != n || outputs.size() != n) {
+        throw std::invalid_argument("commit_many: argument lengths differ");
+    }
+    std::vector<uint32_t> lens(n), out_lens(n);
+    for (size_t k = 0; k < n; k++) lens[k] = static_cast<uint32_t>(input_lens[k]);
+    check(tbgpu_commit_many(engine_, static_cast<uint8_t>(operation), static_cast<uint32_t>(n), timestamps.data(),
+                            inputs.data(), lens.data(), outputs.data(), out_lens.data()),
+          "commit_many");
+    commit_timestamp = tbgpu_commit_timestamp(engine_);
+    return std::vector<size_t>(out_lens.begin(), out_lens.end());
+}
+
+void StateMachine::compact(const Callback& callback, uint64_t op) {
+    (void)op;
+    // Durability (groove write-back to the LSM forest) is out of scope this round.
+    callback(*this);
+}
+
+void StateMachine::checkpoint(const Callback& callback) { callback(*this); }
+
+void StateMachine::test_set_balances(u128 id, u128 dp, u128 dpost, u128 cp, u128 cpost) {
+    const uint64_t b[8] = {(uint64_t)dp, (uint64_t)(dp >> 64), (uint64_t)dpost, (uint64_t)(dpost >> 64),
+                           (uint64_t)cp, (uint64_t)(cp >> 64), (uint64_t)cpost, (uint64_t)(cpost >> 64)};
+    check(tbgpu_test_set_balances(engine_, (uint64_t)id, (uint64_t)(id >> 64), b), "test_set_balances");
+}
+
+}  // namespace tb

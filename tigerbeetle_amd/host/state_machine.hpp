@@ -1,0 +1,181 @@
+// state_machine.hpp — C++ host mirror of the reference's StateMachine plugin interface, backed by
+// the MI355X engine's C ABI (include/tbgpu.h).
+//
+// The reference's replica drives a comptime duck-typed `StateMachineType`
+// (src/state_machine.zig:28-1150; contract in SURVEY.md §8b).  The host side stays in the
+// reference's language there (Zig); no Zig toolchain exists in this image, so this is the same
+// interface in C++ — what a Zig `@cImport` wrapper would call, one level up:
+//
+//   reference member (src/state_machine.zig)          here
+//   ------------------------------------------------  ---------------------------------------------
+//   Operation (:208-214)                               tb::Operation
+//   Options (:216-221)                                 tb::Options (+ HBM sizing)
+//   init(allocator, grid, options) !Self (:264-278)    StateMachine(const Options&) (throws DeviceError)
+//   deinit (:280-289) / reset (:291-317)                ~StateMachine() / reset()
+//   open(callback) (:319-334)                          open(cb)
+//   prepare(operation, input) (:336-343)               prepare(op, input, len)
+//   prefetch(callback, op, operation, input) (:345)    prefetch(cb, op, operation, input, len)
+//   commit(client, op, timestamp, operation, input,    commit(client, op, timestamp, operation, input,
+//          output) usize (:508-540)                           len, output) -> bytes written
+//   compact(callback, op) / checkpoint(callback)       compact(cb, op) / checkpoint(cb)
+//     (:542-582)
+//   prepare_timestamp / commit_timestamp (:250-251)    prepare_timestamp / commit_timestamp
+//
+// Error behaviour follows the reference: invalid events are result codes; an invariant the
+// reference asserts (or an integer overflow it would trap on in ReleaseSafe) throws tb::Panic —
+// the replica's @panic; a HIP failure throws tb::DeviceError.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <functional>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+extern "C" {
+#include "../../include/tbgpu.h"
+}
+
+namespace tb {
+
+using u128 = unsigned __int128;
+
+// src/state_machine.zig:208-214 (vsr_operations_reserved = 128).
+enum class Operation : uint8_t {
+    create_accounts = 128,
+    create_transfers = 129,
+    lookup_accounts = 130,
+    lookup_transfers = 131,
+};
+
+// config.zig:137 / vsr.zig:401: message_size_max (1 MiB) - header (128 B).
+constexpr size_t message_body_size_max = (1u << 20) - 128;
+// batch_max (state_machine.zig:46-65): body / max(sizeof(Event), sizeof(Result)) = 8191 for every
+// operation of the production config.
+constexpr uint32_t batch_max = message_body_size_max / 128;
+
+// src/tigerbeetle.zig:7-29.
+struct alignas(16) Account {
+    u128 id;
+    u128 debits_pending;
+    u128 debits_posted;
+    u128 credits_pending;
+    u128 credits_posted;
+    u128 user_data_128;
+    uint64_t user_data_64;
+    uint32_t user_data_32;
+    uint32_t reserved;
+    uint32_t ledger;
+    uint16_t code;
+    uint16_t flags;
+    uint64_t timestamp;
+};
+static_assert(sizeof(Account) == 128, "Account is a 128-byte extern struct");
+
+// src/tigerbeetle.zig:64-89.
+struct alignas(16) Transfer {
+    u128 id;
+    u128 debit_account_id;
+    u128 credit_account_id;
+    u128 amount;
+    u128 pending_id;
+    u128 user_data_128;
+    uint64_t user_data_64;
+    uint32_t user_data_32;
+    uint32_t timeout;
+    uint32_t ledger;
+    uint16_t code;
+    uint16_t flags;
+    uint64_t timestamp;
+};
+static_assert(sizeof(Transfer) == 128, "Transfer is a 128-byte extern struct");
+
+// Create*sResult (tigerbeetle.zig:224-249): {index, result}, only non-ok events.
+struct CreateResult {
+    uint32_t index;
+    uint32_t result;
+};
+static_assert(sizeof(CreateResult) == 8, "8-byte result");
+
+namespace AccountFlags {  // tigerbeetle.zig:31-62
+constexpr uint16_t linked = 1 << 0;
+constexpr uint16_t debits_must_not_exceed_credits = 1 << 1;
+constexpr uint16_t credits_must_not_exceed_debits = 1 << 2;
+}  // namespace AccountFlags
+
+namespace TransferFlags {  // tigerbeetle.zig:91-104
+constexpr uint16_t linked = 1 << 0;
+constexpr uint16_t pending = 1 << 1;
+constexpr uint16_t post_pending_transfer = 1 << 2;
+constexpr uint16_t void_pending_transfer = 1 << 3;
+constexpr uint16_t balancing_debit = 1 << 4;
+constexpr uint16_t balancing_credit = 1 << 5;
+}  // namespace TransferFlags
+
+// Result names in declaration order (value == index, tigerbeetle.zig:109-249).
+const std::vector<std::string>& create_account_result_names();
+const std::vector<std::string>& create_transfer_result_names();
+
+struct Options {
+    // Reference options (state_machine.zig:216-221): accepted for interface parity; the HBM
+    // tables hold every object, so there is no cache to size.
+    uint32_t lsm_forest_node_count = 0;
+    uint32_t cache_entries_accounts = 0;
+    uint32_t cache_entries_transfers = 0;
+    uint32_t cache_entries_posted = 0;
+    // HBM sizing (static allocation at init, as the reference's grooves).
+    uint64_t accounts_max = 1 << 16;
+    uint64_t transfers_max = 1 << 20;
+    uint32_t pass_events_max = 8190 * 64;
+    uint32_t pass_batches_max = 512;
+    int32_t device = 0;
+    bool profile = false;
+};
+
+struct Panic : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+struct DeviceError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+class StateMachine {
+public:
+    using Callback = std::function<void(StateMachine&)>;
+
+    explicit StateMachine(const Options& options);
+    ~StateMachine();
+    StateMachine(const StateMachine&) = delete;
+    StateMachine& operator=(const StateMachine&) = delete;
+
+    void reset();
+    void open(const Callback& callback);
+    // Input / output buffers are the prepare body and the reply body (align 16 in the reference).
+    void prepare(Operation operation, const void* input, size_t input_len);
+    void prefetch(const Callback& callback, uint64_t op, Operation operation, const void* input, size_t input_len);
+    size_t commit(u128 client, uint64_t op, uint64_t timestamp, Operation operation, const void* input,
+                  size_t input_len, void* output);
+    // N consecutive prepares of one create operation in one device pass: identical results to N
+    // commit() calls (the throughput entry point; the replica may batch committed prepares).
+    std::vector<size_t> commit_many(Operation operation, const std::vector<uint64_t>& timestamps,
+                                    const std::vector<const void*>& inputs, const std::vector<size_t>& input_lens,
+                                    const std::vector<void*>& outputs);
+    void compact(const Callback& callback, uint64_t op);
+    void checkpoint(const Callback& callback);
+
+    // Test-only: the table harness `setup` action (state_machine.zig:1398-1407).
+    void test_set_balances(u128 account_id, u128 debits_pending, u128 debits_posted, u128 credits_pending,
+                           u128 credits_posted);
+
+    uint64_t prepare_timestamp = 0;
+    uint64_t commit_timestamp = 0;
+
+    tbgpu_t* engine() const { return engine_; }
+
+private:
+    void check(int status, const char* what) const;
+    tbgpu_t* engine_ = nullptr;
+};
+
+}  // namespace tb
