@@ -417,22 +417,28 @@ def roofline(stats, u_over_t, per_launch_transfers, args, total_ms):
         "tb_transfers_validate": (stats["ms_validate"], stats["launches_validate"]),
         "tb_resolve<129>": (stats["ms_resolve"], stats["launches_resolve"]),
         "tb_replay<129>": (stats["ms_replay"], stats["launches_replay"]),
+        "tb_apply_legs": (stats["ms_apply"], stats["launches_apply"]),
     }
     dom = max(kernels, key=lambda k: kernels[k][0])
     ms_dom, n_dom = kernels[dom]
     # B = 296 + 256·U/T per transfer, split by where the work happens:
     # validate reads the event (128), probes + claims the id (32), writes the record (128) and reads
     # each touched account once (128·U/T); resolve writes the result slot (8) and each touched
-    # account back (128·U/T).
+    # account back (128·U/T) — or, with the legs path, tb_apply_legs writes the accounts back.
+    legs = stats["launches_apply"] > 0
     b_validate = 288 + 128 * u_over_t
-    b_resolve = 8 + 128 * u_over_t
-    alg_bytes = {"tb_transfers_validate": b_validate, "tb_resolve<129>": b_resolve, "tb_replay<129>": 0.0}[dom] * per_launch_transfers
+    b_resolve = 8 + (0 if legs else 128 * u_over_t)
+    b_apply = 128 * u_over_t if legs else 0.0
+    alg_bytes = {"tb_transfers_validate": b_validate, "tb_resolve<129>": b_resolve, "tb_replay<129>": 0.0,
+                 "tb_apply_legs": b_apply}[dom] * per_launch_transfers
     if not n_dom:
         return None
     avg_s = ms_dom / n_dom / 1e3
     achieved = alg_bytes / avg_s / 1e9
+    per_kernel = {k: {"launches": int(n), "avg_launch_ms": round(ms / n, 4)} for k, (ms, n) in kernels.items() if n}
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc(dom), "kernel": dom,
+            "kernels": per_kernel,
             "avg_launch_ms": round(ms_dom / n_dom, 4), "alg_bytes_per_transfer": round(alg_bytes / per_launch_transfers, 1),
             "path_bytes_per_transfer": round(296 + 256 * u_over_t, 1),
             "path_achieved_GBs": round((296 + 256 * u_over_t) * args.transfers * args.steps / (total_ms / 1e3) / 1e9, 1)}

@@ -121,6 +121,8 @@ typedef struct tbgpu_stats {
     double ms_replay;            /* tb_replay (ordered fallback) */
     double ms_clear;             /* dedup table clears */
     uint64_t launches_validate, launches_resolve, launches_replay, launches_clear;
+    double ms_apply;             /* tb_apply_legs (per-account sums of the balance legs) */
+    uint64_t launches_apply;
 } tbgpu_stats;
 
 int tbgpu_get_stats(tbgpu_t* engine, tbgpu_stats* stats);

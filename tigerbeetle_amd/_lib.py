@@ -40,6 +40,8 @@ class tbgpu_stats(ctypes.Structure):
         ("launches_resolve", ctypes.c_uint64),
         ("launches_replay", ctypes.c_uint64),
         ("launches_clear", ctypes.c_uint64),
+        ("ms_apply", ctypes.c_double),
+        ("launches_apply", ctypes.c_uint64),
     ]
 
 

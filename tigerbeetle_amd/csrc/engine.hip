@@ -17,6 +17,7 @@
 #include "../../include/tbgpu.h"
 #include "../../include/tbgpu_bench.h"
 #include "../../include/tbgpu_shard.h"
+#include "k_apply.h"
 #include "k_aux.h"
 #include "k_replay.h"
 #include "k_route.h"
@@ -48,7 +49,7 @@ static u64 pow2_at_least(u64 v) {
     return c;
 }
 
-enum { K_VALIDATE = 0, K_RESOLVE = 1, K_REPLAY = 2, K_CLEAR = 3, K_PASS = 4, K_COUNT = 5 };
+enum { K_VALIDATE = 0, K_RESOLVE = 1, K_REPLAY = 2, K_CLEAR = 3, K_PASS = 4, K_APPLY = 5, K_COUNT = 6 };
 
 struct ProfilePair {
     int kind;
@@ -76,6 +77,12 @@ struct tbgpu {
     u64* sum_shards = nullptr;
     UndoEntry* undo = nullptr;
     u32 undo_cap = 0;
+    // Balance legs (k_apply.h); legs_ok = false: resolve applies every leg with atomics.
+    bool legs_ok = false;
+    u32 leg_shift = 0, leg_buckets = 0;
+    u64* leg_ev = nullptr;
+    u64* leg_w = nullptr;
+    u32* leg_off = nullptr;
 
     // Host-path staging.
     u8* staging = nullptr;
@@ -222,6 +229,14 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     E->undo_cap = 4 * (BATCH_EVENTS_MAX + 1);
     E->meta_cap = std::max<u64>(E->pb_max, 1 << 16);
     E->lookup_cap = 1 << 16;
+    // Legs buckets: about LEG_BUCKETS_PREF buckets, at most LEG_SLOTS_MAX slots (LDS) each.
+    {
+        u32 shift = 0;
+        while ((E->account_cap >> shift) > LEG_BUCKETS_PREF && (1u << shift) < LEG_SLOTS_MAX) shift++;
+        E->leg_shift = shift;
+        E->leg_buckets = (u32)(E->account_cap >> shift);
+        E->legs_ok = E->leg_buckets <= LEG_BUCKETS_MAX;
+    }
 
     size_t free_b = 0, total_b = 0;
     INIT_CK(hipMemGetInfo(&free_b, &total_b));
@@ -264,6 +279,11 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     INIT_CK(hipMalloc(&E->dedup, E->dedup_cap * 8));
     INIT_CK(hipMalloc(&E->sum_shards, SUM_WORDS * 8));
     INIT_CK(hipMalloc(&E->undo, (u64)E->undo_cap * sizeof(UndoEntry)));
+    if (E->legs_ok) {
+        INIT_CK(hipMalloc(&E->leg_ev, pe * 2 * 8));
+        INIT_CK(hipMalloc(&E->leg_w, pe * 2 * 8));
+        INIT_CK(hipMalloc(&E->leg_off, (u64)std::min<u32>(E->pb_max, LEG_PREPARES_MAX) * (E->leg_buckets + 1) * 4));
+    }
     INIT_CK(hipMalloc(&E->staging, pe * 128));
     INIT_CK(hipMalloc(&E->results, pe * 8));
     INIT_CK(hipMalloc(&E->reply_bytes, E->meta_cap * 4));
@@ -293,7 +313,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->cr, E->ps, E->rs, E->dep_list, E->dep_count, E->amt, E->kid, E->kpid, E->dedup,
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
                     E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->r_home,
-                    E->r_block_counts, E->r_words, E->r_meta};
+                    E->r_block_counts, E->r_words, E->r_meta, E->leg_ev, E->leg_w, E->leg_off};
     for (void* p : bufs) if (p) (void)hipFree(p);
     if (E->h_meta) (void)hipHostFree(E->h_meta);
     if (E->h_rmeta) (void)hipHostFree(E->h_rmeta);
@@ -373,6 +393,12 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.routed = routed ? 1 : 0;
         P.codes = codes;
         P.cert_ext = cert_ext;
+        P.legs = (op == OP_CREATE_TRANSFERS && E->legs_ok && b1 - b0 <= LEG_PREPARES_MAX && !(E->ablate & ABL_LEGS)) ? 1 : 0;
+        P.leg_shift = E->leg_shift;
+        P.leg_buckets = E->leg_buckets;
+        P.leg_ev = E->leg_ev;
+        P.leg_w = E->leg_w;
+        P.leg_off = E->leg_off;
 
         ProfilePair pass_pp;
         int st = prof_begin(E, &pass_pp, K_PASS);
@@ -402,6 +428,12 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         }
         HIPCK(hipGetLastError());
         if ((st = prof_end(E, &pp))) return st;
+        if (P.legs) {
+            if ((st = prof_begin(E, &pp, K_APPLY))) return st;
+            hipLaunchKernelGGL(tb_apply_legs, dim3(E->leg_buckets), dim3(APPLY_THREADS), 0, E->stream, P);
+            HIPCK(hipGetLastError());
+            if ((st = prof_end(E, &pp))) return st;
+        }
         if ((st = prof_begin(E, &pp, K_REPLAY))) return st;
         if (op == OP_CREATE_TRANSFERS) {
             hipLaunchKernelGGL(tb_replay<OP_CREATE_TRANSFERS>, dim3(1), dim3(REPLAY_THREADS), 0, E->stream, P,
@@ -737,6 +769,8 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     s->launches_resolve = E->prof_n[K_RESOLVE];
     s->launches_replay = E->prof_n[K_REPLAY];
     s->launches_clear = E->prof_n[K_CLEAR];
+    s->ms_apply = E->prof_ms[K_APPLY];
+    s->launches_apply = E->prof_n[K_APPLY];
     return TBGPU_STATUS_OK;
 }
 

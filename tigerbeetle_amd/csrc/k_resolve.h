@@ -52,7 +52,13 @@ __device__ static inline bool tb_account_cert_fails(const AccountBal* a, u128 S)
 }
 
 // Write the sparse reply of batch b from LDS codes.
-__device__ static inline void tb_write_replies(const PassArgs& P, u32 b, u32 L, const u8* s_code, u32* s_wave) {
+// n_fail: the number of non-ok codes (0: the reply is empty, no compaction needed).
+__device__ static inline void tb_write_replies(const PassArgs& P, u32 b, u32 L, const u8* s_code, u32* s_wave,
+                                               u32 n_fail = ~0u) {
+    if (n_fail == 0 && !P.codes) {
+        if (threadIdx.x == 0) P.reply_bytes[b] = 0;
+        return;
+    }
     if (P.codes) {  // routed mode: dense per-event codes, the router compacts them per prepare
         u8* dst = P.codes + P.batch_off[b];
         for (u32 i = threadIdx.x; i < L; i += blockDim.x) dst[i] = s_code[i];
@@ -104,6 +110,37 @@ __device__ static inline void tb_apply_transfer(const PassArgs& P, u32 pe, u32 i
         tb_atomic_add_u128(dr + off_d, amount);
         tb_atomic_add_u128(cr + off_c, amount);
     }
+}
+
+// Legs of this workgroup's prepare (see k_apply.h): s_hist holds the legs per bucket.  Publish the
+// bucket starts (exclusive scan) as the prepare's leg_off row, then write every leg of an
+// independent ok create_transfer into the prepare's leg region [2*pbase, 2*pbase + 2L), grouped by
+// bucket: debit side into debits_pending / debits_posted, credit side into credits_pending /
+// credits_posted (:870-880).  The order inside a bucket is unspecified: the sums commute.
+// The final-results loop wrote each leg word in event order (leg_ev, coalesced); the counting sort
+// runs in LDS (s_perm: sorted position -> event << 1 | side, 2 B per leg) and the grouped copy is
+// stored in order, coalesced (scattering the words straight to their sorted places cost 4x the
+// whole sort: partial-line stores).
+__device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 L, u32 legmask, u32* s_hist,
+                                           u16* s_perm, u32* s_wave) {
+    if (P.ablate & ABL_LEG_WORK) return;
+    __syncthreads();  // every count is in; s_perm's LDS is free
+    tb_block_scan_lds(s_hist, P.leg_buckets, s_wave);
+    const u32 nlegs = s_hist[P.leg_buckets];
+    u32* row = P.leg_off + (u64)blockIdx.x * (P.leg_buckets + 1);
+    for (u32 k = threadIdx.x; k <= P.leg_buckets; k += blockDim.x) row[k] = s_hist[k];
+    __syncthreads();  // the row is read before the starts advance as cursors
+    for (u32 c = 0; c < L; c += blockDim.x) {
+        if (!((legmask >> (c / blockDim.x)) & 1)) continue;
+        const u32 i = c + threadIdx.x;
+        const u32 drs = P.dr[pbase + i], crs = P.cr[pbase + i];
+        s_perm[atomicAdd(&s_hist[drs >> P.leg_shift], 1u)] = (u16)(i << 1);
+        s_perm[atomicAdd(&s_hist[crs >> P.leg_shift], 1u)] = (u16)((i << 1) | 1);
+    }
+    __syncthreads();
+    if (P.ablate & ABL_LEG_STORES) return;
+    const u64 base = 2ULL * pbase;
+    for (u32 j = threadIdx.x; j < nlegs; j += blockDim.x) P.leg_w[base + j] = P.leg_ev[base + s_perm[j]];
 }
 
 // Apply one independent ok account (create_account :762, groove insert).
@@ -160,6 +197,8 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     __shared__ u32 s_wave[RESOLVE_THREADS / 64];
     __shared__ u64 s_tsmax[RESOLVE_THREADS / 64];
     __shared__ u32 s_applied;
+    __shared__ u32 s_failed;  // non-ok final results of independent events
+    __shared__ u32 s_hist[OP == OP_CREATE_TRANSFERS ? LEG_BUCKETS_MAX + 1 : 1];  // legs per bucket
 
     const Tables& T = P.T;
     const u32 b = P.b0 + blockIdx.x;
@@ -172,20 +211,18 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     const bool any_dup = P.pass_words[PW_DUP] != 0;
     const bool any_bal = P.pass_words[PW_BAL] != 0;
     const bool any_pv = P.pass_words[PW_PV] != 0;
-    if (OP == OP_CREATE_TRANSFERS) {
-        S = tb_sum_total(P.sum_shards);
-        u128 r;
-        cert_global = !tb_add_overflows(tb_u128(T.g->bound_lo, T.g->bound_hi), S, &r);
-        cert64 = cert_global && tb_hi(r) == 0;
-        if (P.cert_ext) {  // routed shard: the router certified the global bound + S
-            cert_global = true;
-            cert64 = P.cert_ext == CERT_EXT_U64;
-        }
+    if (OP == OP_CREATE_TRANSFERS) tb_pass_cert(P, S, cert_global, cert64);
+    const bool use_legs = OP == OP_CREATE_TRANSFERS && P.legs && cert64;
+    if (use_legs) {
+        for (u32 k = threadIdx.x; k < P.leg_buckets; k += RESOLVE_THREADS) s_hist[k] = 0;
     }
 
-    if (threadIdx.x == 0) s_applied = 0;
+    if (threadIdx.x == 0) {
+        s_applied = 0;
+        s_failed = 0;
+    }
     // a. classify
-    bool local_linked = false;
+    bool local_linked = false, local_dep = false;
     for (u32 i = threadIdx.x; i < L; i += RESOLVE_THREADS) {
         const u32 pe = pbase + i;
         const u32 info = P.info[pe];
@@ -193,11 +230,14 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         const bool dep = tb_classify<OP>(P, pe, info, code, S, cert_global, any_dup, any_bal, any_pv);
         const bool linked = P.eflags[pe] & 1;
         local_linked |= linked;
+        local_dep |= dep;
         s_code[i] = (u8)code;
         s_fl[i] = (linked ? 1 : 0) | (dep ? 2 : 0);
         s_key[i] = 0xFFFFFFFFu;
     }
     const bool any_linked = __syncthreads_or(local_linked);
+    // A chain is dependent only through a dependent member, so no classified dependent means none.
+    const bool any_dep = __syncthreads_or(local_dep);
 
     // b. linked chains
     if (any_linked) {
@@ -235,6 +275,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     // Final results, dependent list, apply.
     u64 tsmax = 0;
     u32 ndep = 0;
+    u32 legmask = 0;  // bit k: this thread's event of chunk k contributes two legs
     u32* dep_out = P.dep_list + pbase;
     for (u32 c = 0; c < L; c += RESOLVE_THREADS) {
         const u32 i = c + threadIdx.x;
@@ -275,9 +316,28 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                 const u64 ts = tb_event_ts(P, b, boff, L, i);
                 if (eval_ok) tsmax = ts;  // increasing in i
                 if (fin == R_OK) {
-                    if (OP == OP_CREATE_TRANSFERS) tb_apply_transfer(P, pe, info, P.eflags[pe], cert64);
-                    else tb_apply_account(P, pe, ts);
+                    if (OP == OP_CREATE_TRANSFERS) {
+                        if (use_legs && !(info & HZ_POSTVOID) && P.amt[2 * pe + 1] == 0 &&
+                            P.amt[2 * pe] <= LEG_AMT_MASK) {
+                            const u32 drs = P.dr[pe], crs = P.cr[pe];
+                            const u64 pend = (P.eflags[pe] & TF_PENDING) ? 0 : 1;  // field: pending / posted
+                            const u32 mask = (1u << P.leg_shift) - 1;
+                            P.leg_ev[2 * (u64)pe] = ((((u64)(drs & mask) << 2) | pend) << LEG_AMT_BITS) | P.amt[2 * pe];
+                            P.leg_ev[2 * (u64)pe + 1] = ((((u64)(crs & mask) << 2) | 2 | pend) << LEG_AMT_BITS) | P.amt[2 * pe];
+                            if (!(P.ablate & ABL_LEG_WORK)) {
+                                atomicAdd(&s_hist[drs >> P.leg_shift], 1u);
+                                atomicAdd(&s_hist[crs >> P.leg_shift], 1u);
+                            }
+                            legmask |= 1u << (c / RESOLVE_THREADS);
+                        } else {
+                            tb_apply_transfer(P, pe, info, P.eflags[pe], cert64);
+                        }
+                    } else {
+                        tb_apply_account(P, pe, ts);
+                    }
                     atomicAdd(&s_applied, 1u);
+                } else {
+                    atomicAdd(&s_failed, 1u);
                 }
             } else {
                 P.info[pe] = info | HZ_DEP;
@@ -288,10 +348,12 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                 tb_xindex_tombstone(T, P.rs[pe]);
             }
         }
-        u32 total;
-        const u32 r = tb_block_rank(dep, s_wave, total);
-        if (dep) dep_out[ndep + r] = i;
-        ndep += total;
+        if (any_dep) {
+            u32 total;
+            const u32 r = tb_block_rank(dep, s_wave, total);
+            if (dep) dep_out[ndep + r] = i;
+            ndep += total;
+        }
     }
 
     // commit_timestamp: max over events that returned ok when evaluated (:763, :882, :1012).
@@ -311,5 +373,6 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         P.dep_count[blockIdx.x] = ndep;
         if (ndep) atomicAdd((unsigned long long*)&T.g->dependent_total, (unsigned long long)ndep);
     }
-    if (ndep == 0) tb_write_replies(P, b, L, s_code, s_wave);
+    if (use_legs) tb_emit_legs(P, pbase, L, legmask, s_hist, (u16*)s_key, s_wave);  // s_key is dead here
+    if (ndep == 0) tb_write_replies(P, b, L, s_code, s_wave, s_failed);
 }

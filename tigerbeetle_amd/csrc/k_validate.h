@@ -87,7 +87,8 @@ __device__ static inline u32 tb_claim_id(const PassArgs& P, const Transfer& t, u
 }
 
 // Claims are never withdrawn here: an entry claimed by an event that then fails stays claimed
-// until kernel 2 tombstones it, so it keeps detecting same-pass collisions on its id.
+// until kernel 2 tombstones it, so it keeps detecting same-pass collisions on its id (a later
+// same-id event collides with it and both are replayed in order).
 __device__ static inline u32 tb_validate_post_void(const PassArgs& P, const Transfer& t, u64 ts, u32 pe,
                                                    TransferScratch& s) {
     const Tables& T = P.T;
@@ -204,8 +205,9 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     if (t.ledger == 0) return CT_LEDGER_MUST_NOT_BE_ZERO;
     if (t.code == 0) return CT_CODE_MUST_NOT_BE_ZERO;
 
-    // The first probe of both accounts and of the id index entry are independent loads: issue them
-    // together, before any result is consumed.
+    // The first probe of both accounts and the claim of the id's home index entry are independent:
+    // issue them together, before any result is consumed.  The claim is speculative (the id check
+    // comes after the account checks, :813-824); if the event fails first, kernel 2 withdraws it.
     const u64 dlo = tb_lo(t.debit_account_id), dhi = tb_hi(t.debit_account_id);
     const u64 clo = tb_lo(t.credit_account_id), chi = tb_hi(t.credit_account_id);
     const u64 dpos = tb_hash_id(dlo, dhi) & T.account_mask;
@@ -217,7 +219,14 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
         d0 = T.acct_hot[dpos];
         c0 = T.acct_hot[cpos];
     }
-    const u64 x0 = (P.ablate & (ABL_SPEC | ABL_CAS)) ? ~0ULL : T.xidx[xpos];
+    u64 x0 = ~0ULL;
+    if (!(P.ablate & (ABL_SPEC | ABL_CAS))) {
+        x0 = tb_transfer_cas_home(T, tb_lo(t.id), tb_hi(t.id), (u32)(P.log_base + pe), xpos);
+        if (x0 == 0) {
+            s.rs = (u32)xpos;
+            s.hz |= HZ_SPEC;
+        }
+    }
     const u32 drs = fake ? (u32)(dlo & 1023) : tb_account_find_from(T, dlo, dhi, dpos, d0);
     const u32 crs = fake ? (u32)(clo & 1023) : tb_account_find_from(T, clo, chi, cpos, c0);
     if (drs == TB_NOT_FOUND) return CT_DEBIT_ACCOUNT_NOT_FOUND;

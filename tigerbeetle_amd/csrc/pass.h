@@ -69,9 +69,32 @@ struct PassArgs {
     u32 routed;            // 1: each event carries its execute timestamp in its timestamp field
     u8* codes;             // call-relative dense result codes instead of sparse replies (or null)
     u32 cert_ext;          // 0: certificate from this engine's bound; CERT_EXT_*: given by the caller
+    // Balance legs (k_apply.h): with the 64-bit certificate, the balance deltas of independent ok
+    // create_transfer events are written as legs, bucketed by account slot per prepare, and summed
+    // per account by tb_apply_legs instead of being added with one global atomic per leg.
+    u32 legs;              // 1: the legs path is enabled for this pass (the host checked the sizes)
+    u32 leg_shift;         // bucket of an account slot = slot >> leg_shift (2^leg_shift slots each)
+    u32 leg_buckets;       // account_cap >> leg_shift
+    u64* leg_ev;           // [2 * pass events] leg word of event pe's side s at 2*pe+s (event order)
+    u64* leg_w;            // [2 * pass events] the same leg words grouped by bucket per prepare
+
+    u32* leg_off;          // [prepares of the pass][leg_buckets + 1] bucket starts in the prepare's legs
 };
 
 enum : u32 { CERT_EXT_U128 = 1, CERT_EXT_U64 = 2 };
+
+// Legs limits: a bucket's accumulators live in LDS (4 fields x 8 B per slot), the per-prepare
+// bucket histogram in the resolve workgroup's LDS, the per-prepare segment table in the apply
+// workgroup's LDS.
+#define LEG_SLOTS_MAX 1024
+#define LEG_BUCKETS_PREF 2048
+#define LEG_BUCKETS_MAX 2048  // keeps tb_resolve's LDS under 80 KB: two workgroups per CU
+#define LEG_PREPARES_MAX 1024
+#define APPLY_THREADS 256
+// Leg word: ((slot within its bucket) << 2 | balance field (BAL_OFF / 16)) << LEG_AMT_BITS | amount.
+// An amount of 2^LEG_AMT_BITS or more is applied by the resolve kernel with an atomic instead.
+#define LEG_AMT_BITS 52
+#define LEG_AMT_MASK ((1ULL << LEG_AMT_BITS) - 1)
 
 // Timestamp of event i of batch b (execute, state_machine.zig:645).  A routed event carries the
 // timestamp its source assigned (the source answered timestamp_must_be_zero itself and never
@@ -80,7 +103,8 @@ __device__ static inline u64 tb_event_ts(const PassArgs& P, u32 b, u64 boff, u32
     return P.routed ? *(const u64*)(P.events + (boff + i) * 128 + 120) : P.batch_ts[b] - L + 1 + i;
 }
 
-enum : u32 { ABL_DEDUP = 1, ABL_SPEC = 2, ABL_ACCTS = 4, ABL_XFIND = 8, ABL_STAGE = 16, ABL_RECORD = 32, ABL_CAS = 64, EXP_NT = 128 };
+enum : u32 { ABL_DEDUP = 1, ABL_SPEC = 2, ABL_ACCTS = 4, ABL_XFIND = 8, ABL_STAGE = 16, ABL_RECORD = 32, ABL_CAS = 64, EXP_NT = 128,
+             ABL_LEGS = 256, ABL_LEG_STORES = 512, ABL_LEG_WORK = 1024 };  // ABL_LEG_*: timing only (wrong balances)
 
 // Batch of a call-relative event index: binary search over batch_off[lo..hi) (off[lo] <= e < off[hi]).
 __device__ static inline u32 tb_batch_search(const u64* off, u32 lo, u32 hi, u64 e) {
@@ -177,4 +201,60 @@ __device__ static inline u128 tb_sum_total(const u64* shards) {
     u128 s = 0;
     for (int i = 0; i < SUM_SHARDS; i++) s = tb_sat_add(s, tb_u128(shards[2 * i], shards[2 * i + 1]));
     return s;
+}
+
+// The pass's overflow certificate (k_resolve.h header).  Every kernel of the pass between validate
+// and replay computes the same answer: S is final after validate and `bound` only moves at the end
+// of the replay kernel.
+//   cert_global: bound + S fits in u128 — no overflow check of create_transfer can fire;
+//   cert64:      bound + S < 2^64 — no balance word can carry this pass.
+__device__ static inline void tb_pass_cert(const PassArgs& P, u128& S, bool& cert_global, bool& cert64) {
+    S = tb_sum_total(P.sum_shards);
+    u128 r;
+    cert_global = !tb_add_overflows(tb_u128(P.T.g->bound_lo, P.T.g->bound_hi), S, &r);
+    cert64 = cert_global && tb_hi(r) == 0;
+    if (P.cert_ext) {  // routed shard: the router certified the global bound + S
+        cert_global = true;
+        cert64 = P.cert_ext == CERT_EXT_U64;
+    }
+}
+
+// Exclusive prefix sum of one u32 per thread over the workgroup; *total = the sum.  Every thread
+// calls it; s_wave holds blockDim.x / 64 words.
+__device__ static inline u32 tb_block_excl_sum(u32 v, u32* s_wave, u32* total) {
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+    u32 x = v;
+#pragma unroll
+    for (u32 off = 1; off < 64; off <<= 1) {
+        const u32 o = __shfl_up(x, off);
+        if (lane >= off) x += o;
+    }
+    if (lane == 63) s_wave[wave] = x;
+    __syncthreads();
+    u32 before = 0, tot = 0;
+    for (u32 k = 0; k < nwaves; k++) {
+        const u32 c = s_wave[k];
+        before += k < wave ? c : 0;
+        tot += c;
+    }
+    __syncthreads();
+    *total = tot;
+    return before + x - v;
+}
+
+// In-place exclusive scan of s[0, n) in LDS, s[n] = the total.  Every thread calls it.
+__device__ static inline void tb_block_scan_lds(u32* s, u32 n, u32* s_wave) {
+    const u32 per = (n + blockDim.x - 1) / blockDim.x;
+    const u32 k0 = min(n, threadIdx.x * per), k1 = min(n, k0 + per);
+    u32 local = 0;
+    for (u32 k = k0; k < k1; k++) local += s[k];
+    u32 total;
+    u32 run = tb_block_excl_sum(local, s_wave, &total);
+    for (u32 k = k0; k < k1; k++) {
+        const u32 c = s[k];
+        s[k] = run;
+        run += c;
+    }
+    if (threadIdx.x == 0) s[n] = total;
+    __syncthreads();
 }

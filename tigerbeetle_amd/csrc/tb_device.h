@@ -362,7 +362,7 @@ enum : u32 { CLAIM_NEW = 0, CLAIM_EXISTS = 1, CLAIM_COLLIDED = 2, CLAIM_FULL = 3
 //                  fingerprint — both events become dependent (xdup[] marks the holder's entry;
 //                  kernel 2 reads it)
 //  CLAIM_NEW:      entry claimed (*entry = index position); the caller writes the record
-// `first` is the home entry if the caller already loaded it, else ~0.
+// `first` is the value the caller's home-entry CAS (tb_transfer_cas_home) returned, else ~0.
 __device__ static inline u32 tb_transfer_claim(const Tables& T, u64 lo, u64 hi, u32 log_pos, u64 pass_base,
                                                u32* found, u32* entry, u64 first = ~0ULL) {
     const u64 fp = tb_fp32(lo, hi);
@@ -370,7 +370,12 @@ __device__ static inline u32 tb_transfer_claim(const Tables& T, u64 lo, u64 hi, 
     u64 pos = tb_hash_id(lo, hi) & T.xidx_mask;
     for (u64 n = 0; n <= T.xidx_mask; n++) {
         u64* e = &T.xidx[pos];
-        u64 cur = (n == 0 && first != ~0ULL) ? first : *(volatile u64*)e;
+        const bool home_cas = n == 0 && first != ~0ULL;
+        if (home_cas && first == 0) {  // the home CAS already claimed the entry
+            *entry = (u32)pos;
+            return CLAIM_NEW;
+        }
+        u64 cur = home_cas ? first : *(volatile u64*)e;
         if (cur == 0) {
             cur = atomicCAS((unsigned long long*)e, 0ULL, (unsigned long long)mine);
             if (cur == 0) {
@@ -394,6 +399,15 @@ __device__ static inline u32 tb_transfer_claim(const Tables& T, u64 lo, u64 hi, 
     }
     tb_panic(T.g, PANIC_TABLE_FULL);
     return CLAIM_FULL;
+}
+
+// Speculative claim of the home entry, issued before the event's account checks: for a new id
+// (the common case) the whole claim is one memory-side atomic, with no probe read in front of it.
+// Returns the entry's previous value (0: claimed).  A claim whose event then fails is withdrawn by
+// the resolve kernel like any other failed speculative insert.
+__device__ static inline u64 tb_transfer_cas_home(const Tables& T, u64 lo, u64 hi, u32 log_pos, u64 xpos) {
+    const u64 mine = (tb_fp32(lo, hi) << 32) | ((u64)log_pos + 1);
+    return atomicCAS((unsigned long long*)&T.xidx[xpos], 0ULL, (unsigned long long)mine);
 }
 
 // Claim the first empty entry for an id known to be absent (the ordered replay).
