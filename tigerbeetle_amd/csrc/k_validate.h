@@ -18,6 +18,8 @@ struct TransferScratch {
     u128 amount = 0;        // amount applied by an independent ok event (post: posted amount)
     u128 contrib = 0;       // contribution to S (overflow certificate)
     u64 kid = 0, kpid = 0;  // dedup keys of id / pending_id
+    u64 rec_ts = 0;         // != 0: the event's record is the event with this timestamp (written
+                            // from the LDS stage by the whole workgroup, coalesced)
 };
 
 // create_transfer_exists (state_machine.zig:886-905).
@@ -227,12 +229,11 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
             s.hz |= HZ_SPEC;
         }
     }
-    const u32 drs = fake ? (u32)(dlo & 1023) : tb_account_find_from(T, dlo, dhi, dpos, d0);
-    const u32 crs = fake ? (u32)(clo & 1023) : tb_account_find_from(T, clo, chi, cpos, c0);
+    AccountHot dr = {}, cr = {};
+    const u32 drs = fake ? (u32)(dlo & 1023) : tb_account_find_from(T, dlo, dhi, dpos, d0, &dr);
+    const u32 crs = fake ? (u32)(clo & 1023) : tb_account_find_from(T, clo, chi, cpos, c0, &cr);
     if (drs == TB_NOT_FOUND) return CT_DEBIT_ACCOUNT_NOT_FOUND;
     if (crs == TB_NOT_FOUND) return CT_CREDIT_ACCOUNT_NOT_FOUND;
-    const AccountHot dr = T.acct_hot[drs];
-    const AccountHot cr = T.acct_hot[crs];
     if (!(ts > dr.timestamp) || !(ts > cr.timestamp)) return TB_CODE_PANIC;  // :817-818
     if (dr.ledger != cr.ledger) return CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
     if (t.ledger != dr.ledger) return CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
@@ -265,11 +266,7 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     // then the timeout check (:862) is the next possible failure.
     const u64 timeout_ns = (u64)t.timeout * 1000000000ULL;
     if (ts + timeout_ns < ts) return CT_OVERFLOWS_TIMEOUT;  // entry withdrawn by kernel 2
-    if ((s.hz & HZ_SPEC) && !(P.ablate & ABL_RECORD)) {
-        Transfer r = t;
-        r.timestamp = ts;
-        tb_store_record(&T.xlog[P.log_base + pe], r, P.ablate & EXP_NT);
-    }
+    if ((s.hz & HZ_SPEC) && !(P.ablate & ABL_RECORD)) s.rec_ts = ts;
     return R_OK;
 }
 
@@ -277,6 +274,7 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
 __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassArgs P) {
     __shared__ __attribute__((aligned(16))) u8 stage[VALIDATE_THREADS * STAGE_STRIDE];
     __shared__ u64 s_sum[2 * (VALIDATE_THREADS / 64)];
+    __shared__ u64 s_rec[VALIDATE_THREADS / 64];  // per wave: lanes whose record is their staged event
     __shared__ u32 s_range[2];
 
     const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
@@ -319,15 +317,31 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
         P.kid[pe] = s.kid;
         P.kpid[pe] = s.kpid;
         if (code != R_OK) s.contrib = 0;
+        // The record (create_transfer :870) is the event as staged, with its timestamp.
+        if (s.rec_ts) *(u64*)(stage + threadIdx.x * STAGE_STRIDE + 120) = s.rec_ts;
     }
     // Block partial of S (saturating), then one sharded atomic per block.
     const u128 w = tb_wave_sum_u128(s.contrib);
+    const u64 rec = __ballot(s.rec_ts != 0);
     const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) {
         s_sum[2 * wave] = tb_lo(w);
         s_sum[2 * wave + 1] = tb_hi(w);
+        s_rec[wave] = rec;
     }
     __syncthreads();
+    // Records of the tile: consecutive lanes store consecutive 16-B chunks of consecutive records.
+#pragma unroll
+    for (u32 r = 0; r < 8; r++) {
+        const u32 c = threadIdx.x + r * VALIDATE_THREADS;
+        const u32 ev = c >> 3, part = c & 7;
+        if ((s_rec[ev >> 6] >> (ev & 63)) & 1) {
+            const u32x4 v = *(const u32x4*)(stage + ev * STAGE_STRIDE + part * 16);
+            u32x4* dst = (u32x4*)&P.T.xlog[P.log_base + tile0 + ev] + part;
+            if (P.ablate & EXP_NT) __builtin_nontemporal_store(v, dst);
+            else *dst = v;
+        }
+    }
     if (threadIdx.x == 0) {
         u128 total = 0;
         for (u32 k = 0; k < VALIDATE_THREADS / 64; k++) total = tb_sat_add(total, tb_u128(s_sum[2 * k], s_sum[2 * k + 1]));

@@ -145,17 +145,6 @@ __device__ static inline void tb_stage_events(const u8* src, u32 count, u8* lds,
     __syncthreads();
 }
 
-// 128-byte record store, optionally non-temporal (streamed once, keep it out of the caches).
-template <typename R>
-__device__ static inline void tb_store_record(R* dst, const R& r, bool nt) {
-    if (nt) {
-#pragma unroll
-        for (int k = 0; k < 8; k++) __builtin_nontemporal_store(((const u32x4*)&r)[k], ((u32x4*)dst) + k);
-    } else {
-        *dst = r;
-    }
-}
-
 template <typename R>
 __device__ static inline R tb_read_staged(const u8* lds) {
     R r;

@@ -250,16 +250,23 @@ __device__ static inline u32 tb_account_find(const Tables& T, u64 lo, u64 hi) {
     return TB_NOT_FOUND;
 }
 
-// Continue an account probe whose first entry (at `pos`) was already loaded.
-__device__ static inline u32 tb_account_find_from(const Tables& T, u64 lo, u64 hi, u64 pos, const AccountHot& first) {
-    if (first.id_lo == lo && first.id_hi == hi) return (u32)pos;
+// Continue an account probe whose first entry (at `pos`) was already loaded; *hit = the matching
+// entry (no second load of it).
+__device__ static inline u32 tb_account_find_from(const Tables& T, u64 lo, u64 hi, u64 pos, const AccountHot& first,
+                                                  AccountHot* hit) {
+    if (first.id_lo == lo && first.id_hi == hi) {
+        *hit = first;
+        return (u32)pos;
+    }
     if ((first.id_lo | first.id_hi) == 0 || tb_id_reserved(lo, hi)) return TB_NOT_FOUND;
     pos = (pos + 1) & T.account_mask;
     for (u64 n = 1; n <= T.account_mask; n++) {
-        const AccountHot* h = &T.acct_hot[pos];
-        const u64 a = h->id_lo, b = h->id_hi;
-        if (a == lo && b == hi) return (u32)pos;
-        if ((a | b) == 0) return TB_NOT_FOUND;
+        const AccountHot h = T.acct_hot[pos];
+        if (h.id_lo == lo && h.id_hi == hi) {
+            *hit = h;
+            return (u32)pos;
+        }
+        if ((h.id_lo | h.id_hi) == 0) return TB_NOT_FOUND;
         pos = (pos + 1) & T.account_mask;
     }
     return TB_NOT_FOUND;
