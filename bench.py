@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--pass-batches", type=int, default=512)
     p.add_argument("--cpu-sample", type=int, default=12_285_000, help="transfers in the CPU baseline / parity sample (0: skip)")
     p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"],
+                   help="BASELINE.json shape: c2 (headline, default), c3 Zipf + limit accounts, c4 chains + two-phase")
     p.add_argument("--profile", type=int, default=1, help="time kernels with HIP events (roofline)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (rehearsal on one GPU)")
     p.add_argument("--same-device", action="store_true", help="rehearsal: every rank on cuda:0")
@@ -65,13 +67,11 @@ def batches(total, batch):
     return [batch] * q + ([r] if r else [])
 
 
-def timestamps(lens, start):
-    """Prepare timestamps: t_k = t_{k-1} + 1 + len_k (state_machine.zig:1483-1485)."""
-    ts, t = [], start
-    for L in lens:
-        t += 1 + L
-        ts.append(t)
-    return ts, t
+def timestamps(lens, start, gap_every=0):
+    """Prepare timestamps: t_k = t_{k-1} + 1 + len_k (state_machine.zig:1483-1485), plus the C4
+    expiry gaps (tests/harness/configs.py)."""
+    from tests.harness.configs import timestamps as ts_gaps
+    return ts_gaps(lens, start, gap_every)
 
 
 def expected_unique(accounts, legs):
@@ -81,11 +81,12 @@ def expected_unique(accounts, legs):
 
 def run_cpu_baseline(engine, args, acct_lens, acct_ts, events_dev, sample_lens, sample_ts):
     """Oracle (single thread) on the sample; returns (result dict, oracle engine, replies)."""
+    from tests.harness.configs import SETTINGS
     from tests.harness.oracle import OracleEngine
 
     n_acct = args.accounts
     acct_dev = engine.alloc(n_acct * 128)
-    engine.generate_accounts(acct_dev, 0, n_acct, seed=args.seed)
+    engine.generate_accounts(acct_dev, 0, n_acct, seed=args.seed, limit_permille=SETTINGS[args.workload]["limit_permille"])
     acct_events = engine.to_host(acct_dev, n_acct * 128)
     engine.free(acct_dev)
     n_sample = sum(sample_lens)
@@ -150,6 +151,16 @@ def load_pmc(kernel):
     return None
 
 
+WORKLOAD_TEXT = {
+    "c2": "C2 (BASELINE.json configs[1]): %d accounts, %d uniform transfers/GPU, no flags, prepares of %d",
+    "c3": "C3 (BASELINE.json configs[2]): %d accounts (10%% debits_must_not_exceed_credits, funded by a bank "
+          "account), %d transfers with Zipf(1.2) dr/cr, prepares of %d",
+    "c4": "C4 (BASELINE.json configs[3]): %d accounts, %d transfers: ~20%% in linked chains (5%% chain-breaking), "
+          "30%% pending with 0..10 s timeouts, 15%% post/void of earlier transfers, 0.5%% balancing, a 2 s "
+          "timestamp gap every 64 prepares; prepares of %d",
+}
+
+
 def main():
     args = parse()
     import torch
@@ -159,6 +170,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        assert args.workload == "c2", "the multi-GPU bench runs the C2/C5 shape"
         if args.same_device:
             local_rank = 0
         torch.cuda.set_device(local_rank)
@@ -179,8 +191,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    from tests.harness.configs import KINDS, SETTINGS
     from tigerbeetle_amd.state_machine import Engine, Options
 
+    wl = SETTINGS[args.workload]
     pass_events = args.pass_batches * args.batch
     engine = Engine(Options(accounts_max=args.accounts, transfers_max=args.transfers, pass_events_max=pass_events,
                             pass_batches_max=args.pass_batches, device=local_rank, profile=bool(args.profile)))
@@ -190,7 +204,7 @@ def main():
     acct_lens = batches(args.accounts, args.batch)
     acct_ts, t_end = timestamps(acct_lens, 1_000_000_000)
     acct_dev = engine.alloc(args.accounts * 128)
-    engine.generate_accounts(acct_dev, 0, args.accounts, seed=seed)
+    engine.generate_accounts(acct_dev, 0, args.accounts, seed=seed, limit_permille=wl["limit_permille"])
     res_dev = engine.alloc(max(args.accounts, args.transfers) * 8)
     rb_dev = engine.alloc(max(len(acct_lens), args.transfers // args.batch + 2) * 4)
     engine.commit_device_async(128, acct_ts, acct_lens, acct_dev, res_dev, rb_dev)
@@ -202,7 +216,8 @@ def main():
     # -- transfers (synthetic, resident in HBM) ----------------------------------------------
     xfer_lens = batches(args.transfers, args.batch)
     events_dev = engine.alloc(args.transfers * 128)
-    engine.generate_transfers(events_dev, 0, args.transfers, args.accounts, seed=seed)
+    engine.generate_transfers(events_dev, 0, args.transfers, args.accounts, seed=seed, kind=KINDS[args.workload],
+                              limit_permille=wl["limit_permille"])
     engine.sync()
 
     step_ms = []
@@ -210,7 +225,7 @@ def main():
     for step in range(args.warmup + args.steps):
         timed = step >= args.warmup
         engine.reset_transfers()
-        ts, t_cursor = timestamps(xfer_lens, t_cursor + 10)
+        ts, t_cursor = timestamps(xfer_lens, t_cursor + 10, wl["gap_every"])
         if timed and step == args.warmup:
             engine.reset_stats()
         barrier()
@@ -229,10 +244,17 @@ def main():
     # -- full-run checks (size-independent properties) ---------------------------------------
     rb = engine.to_host(rb_dev, len(xfer_lens) * 4).view(np.uint32)
     accts = engine.export_accounts()
-    dpost = sum(int(x) for x in accts["debits_posted_lo"]) + (sum(int(x) for x in accts["debits_posted_hi"]) << 64)
-    cpost = sum(int(x) for x in accts["credits_posted_lo"]) + (sum(int(x) for x in accts["credits_posted_hi"]) << 64)
-    full_ok = bool(rb.sum() == 0 and stats["transfers"] == args.transfers and dpost == cpost and dpost > 0
-                   and len(accts) == args.accounts)
+
+    def total(field):
+        return sum(int(x) for x in accts[field + "_lo"]) + (sum(int(x) for x in accts[field + "_hi"]) << 64)
+
+    dpost, cpost = total("debits_posted"), total("credits_posted")
+    n_failed = int(rb.sum()) // 8
+    # C2: every transfer commits.  Every config: each committed transfer is one record; debits equal
+    # credits in total, posted and pending.
+    full_ok = bool(stats["transfers"] == args.transfers - n_failed and dpost == cpost and dpost > 0
+                   and total("debits_pending") == total("credits_pending") and len(accts) == args.accounts
+                   and (n_failed == 0 or args.workload != "c2"))
 
     total_ms = sum(step_ms)
     n_total = args.transfers * world * args.steps
@@ -248,13 +270,18 @@ def main():
     parity = {"full_run_properties": full_ok}
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         sample_lens = batches(min(args.cpu_sample, args.transfers), args.batch)
-        sample_ts, t_cursor = timestamps(sample_lens, t_cursor + 10)
+        sample_ts, t_cursor = timestamps(sample_lens, t_cursor + 10, wl["gap_every"])
         cpu, oracle, expected = run_cpu_baseline(engine, args, acct_lens, acct_ts, events_dev, sample_lens, sample_ts)
         engine.reset_transfers()
         engine.commit_device_async(129, sample_ts, sample_lens, events_dev, res_dev, rb_dev)
         engine.sync()
         rb = engine.to_host(rb_dev, len(sample_lens) * 4).view(np.uint32)
-        replies_equal = all(e == b"" for e in expected) and int(rb.sum()) == 0
+        results = engine.to_host(res_dev, sum(sample_lens) * 8)
+        got, off = [], 0
+        for L, nb in zip(sample_lens, rb):  # sparse replies at the prepare's event offset
+            got.append(bytes(results[off * 8:off * 8 + int(nb)]))
+            off += L
+        replies_equal = got == expected
         acc_equal = engine.export_accounts().tobytes() == oracle.export_accounts().tobytes()
         xfer_equal = engine.export_transfers(cap=sum(sample_lens)).tobytes() == oracle.export_transfers().tobytes()
         parity.update({"sample_transfers": sum(sample_lens), "replies_equal": replies_equal,
@@ -275,14 +302,14 @@ def main():
         "vs_baseline": None,
         "dtype": "u128",
         "data": "synthetic (device-generated, reference benchmark shapes)",
-        "config": {"workload": "C2 (BASELINE.json configs[1]): %d accounts, %d uniform transfers/GPU, no flags, "
-                               "prepares of %d" % (args.accounts, args.transfers, args.batch),
+        "config": {"workload": WORKLOAD_TEXT[args.workload] % (args.accounts, args.transfers, args.batch),
                    "prepares_per_step": len(xfer_lens), "pass_prepares": args.pass_batches,
                    "parallelism": "shard%d" % world if world > 1 else "single"},
         "p99_batch_latency_ms": round(float(np.percentile(lat, 99)), 3),
         "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3), "p100": round(float(lat.max()), 3),
                              "definition": "device time of the pass that answers the prepare (%d prepares/pass)" % args.pass_batches},
         "dependent_events": stats["dependent_events"],
+        "failed_events": n_failed,
         "roofline": roof,
         "cpu_baseline": cpu,
         "parity": parity,

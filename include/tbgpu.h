@@ -123,6 +123,8 @@ typedef struct tbgpu_stats {
     uint64_t launches_validate, launches_resolve, launches_replay, launches_clear;
     double ms_apply;             /* tb_apply_legs (per-account sums of the balance legs) */
     uint64_t launches_apply;
+    uint64_t flow_passes;        /* passes whose dependent events ran on the parallel flow path */
+    uint64_t flow_units;         /* chains / single dependent events the flow path executed */
 } tbgpu_stats;
 
 int tbgpu_get_stats(tbgpu_t* engine, tbgpu_stats* stats);

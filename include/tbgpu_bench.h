@@ -16,8 +16,13 @@ extern "C" {
 typedef struct tbgpu_workload {
     uint64_t seed;
     uint64_t account_count;    /* accounts 0..account_count-1 exist (ids by IdPermutation.inversion) */
-    uint32_t kind;             /* 0: uniform dr != cr, no flags (BASELINE config C2) */
+    uint32_t kind;             /* 0: uniform dr != cr, no flags (BASELINE config C2)
+                                  1: Zipf(zipf_s) dr/cr over a rank permutation; the first transfers
+                                     fund every limit account from account 0 (C3)
+                                  2: uniform, 20% linked chains (5% chain-breaking), pending with
+                                     timeouts, post/void of earlier transfers, balancing (C4) */
     uint32_t limit_permille;   /* accounts with debits_must_not_exceed_credits, per mille */
+    double zipf_s;             /* kind 1: Zipf exponent (BASELINE C3: 1.2) */
 } tbgpu_workload;
 
 /* Write `count` Account events for account indices [first, first+count) into device memory. */

@@ -1,0 +1,44 @@
+"""GPU vs oracle on the BASELINE.json workload shapes at reduced size (C2 uniform; C3 Zipf s=1.2
+with 10% debits_must_not_exceed_credits accounts funded by a bank account; C4 linked chains,
+pending transfers with timeouts, post/void of earlier transfers across expiry gaps, balancing).
+Inputs come from the engine's device generator; both sides commit identical prepares, through
+multi-prepare device passes.  Bit-exact: replies, accounts, transfers, posted groove,
+commit_timestamp."""
+import pytest
+
+from tests.harness.configs import SETTINGS, batches, generate, split, timestamps
+from tests.harness.oracle import OracleEngine
+from tests.test_gpu_differential import assert_same_state
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("config,n_accounts,n_transfers,pass_batches", [
+    ("c2", 20_000, 200_000, 8),
+    ("c3", 20_000, 200_000, 8),
+    ("c3", 2_000, 100_000, 16),   # hotter: long per-account segments, many exceeds_credits
+    ("c4", 20_000, 200_000, 8),
+    ("c4", 1_000, 100_000, 16),   # dense two-phase traffic per account
+])
+def test_config_parity(config, n_accounts, n_transfers, pass_batches, gpu_engine_factory):
+    batch = 8190
+    engine = gpu_engine_factory(accounts_max=n_accounts, transfers_max=n_transfers,
+                                pass_events_max=pass_batches * batch, pass_batches_max=pass_batches)
+    accts, xfers = generate(engine, config, n_accounts, n_transfers, seed=7)
+    a_lens = batches(n_accounts, batch)
+    a_ts, t = timestamps(a_lens, 10**12)
+    x_lens = batches(n_transfers, batch)
+    x_ts, _ = timestamps(x_lens, t + 10, gap_every=SETTINGS[config]["gap_every"])
+
+    oracle = OracleEngine(n_accounts, n_transfers)
+    for e in (oracle, engine):
+        assert all(r == b"" for r in e.commit_many(128, a_ts, split(accts, a_lens)))
+    expected = oracle.commit_many(129, x_ts, split(xfers, x_lens))
+    actual = engine.commit_many(129, x_ts, split(xfers, x_lens))
+    for k, (e, a) in enumerate(zip(expected, actual)):
+        assert e == a, "reply of prepare %d differs" % k
+    assert_same_state(oracle, engine)
+    if config != "c2":  # the shape really exercises the dependent paths, on the parallel flow path
+        st = engine.stats()
+        assert st["dependent_events"] > 0 and st["flow_passes"] > 0 and st["flow_units"] > 0
+        assert sum(len(r) for r in expected) > 0

@@ -42,6 +42,8 @@ class tbgpu_stats(ctypes.Structure):
         ("launches_clear", ctypes.c_uint64),
         ("ms_apply", ctypes.c_double),
         ("launches_apply", ctypes.c_uint64),
+        ("flow_passes", ctypes.c_uint64),
+        ("flow_units", ctypes.c_uint64),
     ]
 
 
@@ -51,6 +53,7 @@ class tbgpu_workload(ctypes.Structure):
         ("account_count", ctypes.c_uint64),
         ("kind", ctypes.c_uint32),
         ("limit_permille", ctypes.c_uint32),
+        ("zipf_s", ctypes.c_double),
     ]
 
 

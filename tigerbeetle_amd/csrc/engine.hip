@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <numeric>
 #include <string>
 #include <vector>
 
@@ -18,6 +19,7 @@
 #include "../../include/tbgpu_bench.h"
 #include "../../include/tbgpu_shard.h"
 #include "k_apply.h"
+#include "k_flow.h"
 #include "k_aux.h"
 #include "k_replay.h"
 #include "k_route.h"
@@ -83,6 +85,11 @@ struct tbgpu {
     u64* leg_ev = nullptr;
     u64* leg_w = nullptr;
     u32* leg_off = nullptr;
+    // Parallel ordered fallback (k_flow.h): create_transfers passes run tb_flow instead of
+    // tb_replay while no balance was set directly (the post/void assert argument, k_replay.h).
+    bool flow_ok = false;
+    bool balances_set = false;
+    FlowArgs F{};
 
     // Host-path staging.
     u8* staging = nullptr;
@@ -182,6 +189,7 @@ static int engine_clear(tbgpu* E) {
     E->commit_ts = 0;
     E->last_batch_ts = 0;
     E->pending = false;
+    E->balances_set = false;
     return TBGPU_STATUS_OK;
 }
 
@@ -259,6 +267,26 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     INIT_CK(hipMalloc(&E->T.xlog, E->xlog_cap * sizeof(Transfer)));
     INIT_CK(hipMalloc(&E->T.xposted, E->xlog_cap));
     INIT_CK(hipMalloc(&E->g, sizeof(Globals)));
+    {
+        // tb_flow: one 1024-thread workgroup per CU, all resident (cooperative launch).
+        hipDeviceProp_t prop;
+        int occ = 0;
+        if (hipGetDeviceProperties(&prop, E->device) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&tb_flow), FLOW_THREADS, 0) ==
+                hipSuccess &&
+            occ >= 1 && prop.cooperativeLaunch) {
+            E->F.grid = (u32)std::min(prop.multiProcessorCount, 256);
+            int khz = 0;
+            if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, E->device) != hipSuccess) khz = 0;
+            khz = std::max(khz, 100000);  // s_memrealtime: 100 MHz on gfx9 parts; never trust a lower figure
+            E->F.stall_ticks = 60ULL * 1000ULL * (u64)khz;  // 60 s
+            if (getenv("TBGPU_DEBUG")) {
+                fprintf(stderr, "tbgpu: flow grid %u, occupancy %d, wall clock %d kHz, stall ticks %llu\n", E->F.grid,
+                        occ, khz, (unsigned long long)E->F.stall_ticks);
+            }
+            E->flow_ok = E->pb_max <= FLOW_NB_MAX && getenv("TBGPU_NO_FLOW") == nullptr;
+        }
+    }
     E->T.account_mask = E->account_cap - 1;
     E->T.xidx_mask = E->xidx_cap - 1;
     E->T.xlog_cap = E->xlog_cap;
@@ -283,6 +311,24 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         INIT_CK(hipMalloc(&E->leg_ev, pe * 2 * 8));
         INIT_CK(hipMalloc(&E->leg_w, pe * 2 * 8));
         INIT_CK(hipMalloc(&E->leg_off, (u64)std::min<u32>(E->pb_max, LEG_PREPARES_MAX) * (E->leg_buckets + 1) * 4));
+    }
+    if (E->flow_ok) {
+        FlowArgs& F = E->F;
+        INIT_CK(hipMalloc(&F.f_pe, pe * 4));
+        INIT_CK(hipMalloc(&F.f_batch, pe * 4));
+        INIT_CK(hipMalloc(&F.f_len, pe * 4));
+        INIT_CK(hipMalloc(&F.need, pe * 4));
+        INIT_CK(hipMalloc(&F.nsucc, pe * 4));
+        INIT_CK(hipMalloc(&F.queue, pe * 4));
+        INIT_CK(hipMalloc(&F.uflags, pe * 4));
+        INIT_CK(hipMalloc(&F.succ, pe * 4 * FLOW_RMAX));
+        for (int k = 0; k < 2; k++) {
+            INIT_CK(hipMalloc(&F.keys[k], pe * 4 * FLOW_RMAX));
+            INIT_CK(hipMalloc(&F.vals[k], pe * 4 * FLOW_RMAX));
+        }
+        INIT_CK(hipMalloc(&F.hist, (u64)F.grid * 256 * 4));
+        INIT_CK(hipMalloc(&F.words, FW_WORDS * 4));
+        INIT_CK(hipMalloc(&F.undo, pe * 4 * sizeof(UndoEntry)));
     }
     INIT_CK(hipMalloc(&E->staging, pe * 128));
     INIT_CK(hipMalloc(&E->results, pe * 8));
@@ -313,7 +359,9 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->cr, E->ps, E->rs, E->dep_list, E->dep_count, E->amt, E->kid, E->kpid, E->dedup,
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
                     E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->r_home,
-                    E->r_block_counts, E->r_words, E->r_meta, E->leg_ev, E->leg_w, E->leg_off};
+                    E->r_block_counts, E->r_words, E->r_meta, E->leg_ev, E->leg_w, E->leg_off,
+                    E->F.f_pe, E->F.f_batch, E->F.f_len, E->F.need, E->F.nsucc, E->F.queue, E->F.uflags, E->F.succ,
+                    E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo};
     for (void* p : bufs) if (p) (void)hipFree(p);
     if (E->h_meta) (void)hipHostFree(E->h_meta);
     if (E->h_rmeta) (void)hipHostFree(E->h_rmeta);
@@ -399,6 +447,9 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.leg_ev = E->leg_ev;
         P.leg_w = E->leg_w;
         P.leg_off = E->leg_off;
+        const bool flow = op == OP_CREATE_TRANSFERS && E->flow_ok && !E->balances_set && !(E->ablate & ABL_FLOW) &&
+                          b1 - b0 <= FLOW_NB_MAX;
+        P.flow_words = E->flow_ok ? E->F.words : nullptr;
 
         ProfilePair pass_pp;
         int st = prof_begin(E, &pass_pp, K_PASS);
@@ -435,7 +486,13 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
             if ((st = prof_end(E, &pp))) return st;
         }
         if ((st = prof_begin(E, &pp, K_REPLAY))) return st;
-        if (op == OP_CREATE_TRANSFERS) {
+        if (flow) {
+            UndoEntry* seq_undo = E->undo;
+            u32 seq_cap = E->undo_cap;
+            void* args[] = {&P, &E->F, &seq_undo, &seq_cap};
+            HIPCK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&tb_flow), dim3(E->F.grid), dim3(FLOW_THREADS),
+                                             args, 0, E->stream));
+        } else if (op == OP_CREATE_TRANSFERS) {
             hipLaunchKernelGGL(tb_replay<OP_CREATE_TRANSFERS>, dim3(1), dim3(REPLAY_THREADS), 0, E->stream, P,
                                E->undo, E->undo_cap);
         } else {
@@ -632,6 +689,7 @@ extern "C" int tbgpu_test_set_balances(tbgpu_t* E, uint64_t id_lo, uint64_t id_h
         int st = engine_sync(E);
         if (st) return st;
     }
+    E->balances_set = true;  // the flow path's post/void argument needs consistent pending balances
     hipLaunchKernelGGL(tb_set_balances, dim3(1), dim3(1), 0, E->stream, E->T, id_lo, id_hi, b[0], b[1], b[2], b[3],
                        b[4], b[5], b[6], b[7], E->d_status);
     HIPCK(hipGetLastError());
@@ -771,6 +829,8 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     s->launches_clear = E->prof_n[K_CLEAR];
     s->ms_apply = E->prof_ms[K_APPLY];
     s->launches_apply = E->prof_n[K_APPLY];
+    s->flow_passes = g.flow_passes;
+    s->flow_units = g.flow_units;
     return TBGPU_STATUS_OK;
 }
 
@@ -797,7 +857,14 @@ static WorkloadParams workload_params(const tbgpu_workload* w, u64 first) {
     W.first_index = first;
     W.kind = w->kind;
     W.limit_permille = w->limit_permille;
-    W.zipf_s = 1.2;
+    W.zipf_s = w->zipf_s > 0 ? w->zipf_s : 1.2;
+    // Rank permutation r -> (a r + b) mod n with gcd(a, n) = 1.
+    const u64 n = std::max<u64>(w->account_count, 1);
+    u64 a = (0x9E3779B97F4A7C15ULL ^ w->seed) % n;
+    if (a == 0) a = 1;
+    while (std::gcd(a, n) != 1) a = a + 1 == n ? 1 : a + 1;
+    W.perm_a = a;
+    W.perm_b = tb_splitmix(w->seed ^ 0x5bd1e995ULL) % n;
     return W;
 }
 
@@ -1091,6 +1158,7 @@ extern "C" int tbgpu_fetch_transfers(tbgpu_t* E, const uint64_t* ids, uint32_t n
 
 extern "C" int tbgpu_upsert_accounts(tbgpu_t* E, const void* records, uint32_t n) {
     HIPCK(hipSetDevice(E->device));
+    E->balances_set = true;  // balances loaded from elsewhere: the sequential replay stays exact
     if (E->pending) {
         int st = engine_sync(E);
         if (st) return st;

@@ -1,0 +1,529 @@
+// k_flow.h — kernel 3 of a create_transfers pass, parallel form: the ordered fallback as a
+// dependency DAG executed by many lanes at once.
+//
+// The dependent events of a pass (k_resolve.h) must see each other's effects in batch order
+// (execute, state_machine.zig:612-698).  They interact only through RESOURCES:
+//   * the balance of a constrained account — a limit flag (tigerbeetle.zig:31-39), a balancing
+//     mark of this pass (:826-846), or any account when the global overflow certificate fails
+//     (:848-861);
+//   * a transfer id: the event's own id (exists / insert, :824, :954) and, for a post/void, its
+//     pending id (pending lookup, posted status, :927-964).
+// A post/void also writes the balances of its pending transfer's accounts (:987-1010): when one of
+// them is constrained it is a resource of the post/void too, found from the pending transfer
+// (an earlier pass's record, or the event of this pass that creates it).  Balances of free
+// accounts feed no check and take commutative atomic deltas (k_replay.h, FLOW = true).
+//
+// A UNIT is a linked chain (executed whole, with its undo log: chains roll back as one,
+// :661-692) or a single event.  Two units that share a resource run in batch order; units that
+// share none commute.  The kernel:
+//   plan   every workgroup: list the pass's dependent events in order, emit (resource key, unit)
+//          pairs, radix-sort them by key (stable, so each key's units stay in batch order) and
+//          link every unit to its successor on each of its resources (need[] = predecessors);
+//   run    workgroup 0, 1024 lanes: a ticket queue of ready units; a lane executes its unit with
+//          the reference logic, then releases its successors, queueing those with no
+//          predecessor left.  The result equals the sequential replay's: every unit sees exactly
+//          the effects of the units before it on its resources, and nothing else it reads can
+//          differ.
+// Grid-wide phases are separated by a counter barrier (cooperative launch: every workgroup is
+// resident).  Cases the planner does not cover (a chain longer than FLOW_CHAIN_MAX, a pending id
+// whose creator in this pass is ambiguous) set a flag, and workgroup 0 runs the sequential replay
+// for the pass instead.  Every wait is bounded: a stall raises PANIC_FLOW_STALL, never a hang.
+#pragma once
+
+#include "k_replay.h"
+
+#define FLOW_THREADS 1024
+#define FLOW_RMAX 6             // resources per event: id, pending id, two accounts (+2 inherited)
+#define FLOW_CHAIN_MAX 64       // longer chains: sequential replay
+#define FLOW_NB_MAX 4096        // prepares per pass the planner handles (LDS prefix)
+#define FLOW_SENT 0xFFFFFFFFu   // empty pair slot
+
+enum : u32 { FW_NUNITS = 0, FW_QTAIL = 1, FW_SEQ = 2, FW_WORDS = 8 };
+enum : u32 { UF_ID_SINGLE = 1 };  // the unit is the only dependent event of the pass naming its id
+
+struct FlowArgs {
+    u32* f_pe;      // [pass events] flat dependent f -> pass-relative event
+    u32* f_batch;   // [pass events] f -> call-relative batch
+    u32* f_len;     // [pass events] unit heads: members; other members: 0
+    u32* need;      // [pass events] per unit head: predecessors not yet done
+    u32* nsucc;     // [pass events] per unit head: successors
+    u32* succ;      // [FLOW_RMAX * pass events] unit u's successors at FLOW_RMAX * u
+    u32* queue;     // [pass events] ready units (head + 1; 0 = not yet published)
+    u32* uflags;    // [pass events] per unit head: UF_*
+    u32* keys[2];   // [FLOW_RMAX * pass events] radix-sort ping-pong buffers
+    u32* vals[2];
+    u32* hist;      // [grid * 256]
+    u32* words;     // [FW_WORDS], zeroed by tb_resolve every pass
+    UndoEntry* undo;  // [4 * pass events] chain of head u: [4u, 4u + 4 * len)
+    u32 grid;
+    u64 stall_ticks;  // wall_clock64 ticks after which a wait is taken as an engine bug (PANIC_FLOW_STALL)
+};
+
+// Every wait of the kernel is bounded by wall time (s_memrealtime) since the wait began.
+__device__ static inline u64 fl_now() {
+    u64 t = (u64)wall_clock64();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    return t;
+}
+__device__ static inline bool fl_expired(const FlowArgs& F, u64 w0) {
+    const u64 now = fl_now();
+    return now > w0 && now - w0 > F.stall_ticks;
+}
+
+// Resource keys: an account slot (< 2^31) or 2^31 | a 31-bit hash of a transfer id.  Two ids that
+// share a hash only add an ordering edge, never lose one.
+__device__ static inline u32 fl_key_id(u64 lo, u64 hi) {
+    return 0x80000000u | (u32)(tb_mix64(lo ^ tb_mix64(hi ^ 0x9e3779b97f4a7c15ULL)) % 0x7FFFFFFFu);
+}
+
+__device__ static inline void fl_grid_sync(Globals* g, u32 nblocks, u32& gen, const FlowArgs& F) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the barrier
+    __syncthreads();
+    gen++;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(&g->flow_barrier, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u32 target = gen * nblocks;
+        const u64 w0 = fl_now();
+        while (__hip_atomic_load(&g->flow_barrier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (fl_expired(F, w0)) {
+                tb_panic(g, PANIC_FLOW_STALL);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
+__device__ static inline bool fl_stalled(Globals* g) {
+    return (__hip_atomic_load(&g->panic, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & PANIC_FLOW_STALL) != 0;
+}
+
+// Resources a post/void inherits from its pending transfer: the constrained accounts of an
+// earlier pass's pending record, and those of the event of this pass that claimed the pending id
+// (its creator; the ordering on the pending id puts the post/void after it).  Returns false when
+// the creator is ambiguous (its id collided in this pass).
+__device__ static inline bool fl_pending_accounts(const PassArgs& P, u64 lo, u64 hi, bool cert_global, u32* keys,
+                                                  u32& nk) {
+    const Tables& T = P.T;
+    if (tb_id_reserved(lo, hi)) return true;
+    const u64 fp = tb_fp32(lo, hi);
+    u64 pos = tb_hash_id(lo, hi) & T.xidx_mask;
+    for (u64 n = 0; n <= T.xidx_mask; n++) {
+        const u64 e = T.xidx[pos];
+        if (e == 0) return true;
+        if ((e >> 32) == fp) {
+            const u32 lp = tb_xi_pos(e);
+            u32 drs = TB_NOT_FOUND, crs = TB_NOT_FOUND;
+            if ((u64)lp < P.log_base) {
+                if (!(e & XI_TOMB)) {
+                    const Transfer& p = T.xlog[lp];
+                    if (p.id == tb_u128(lo, hi)) {
+                        drs = tb_account_find(T, tb_lo(p.debit_account_id), tb_hi(p.debit_account_id));
+                        crs = tb_account_find(T, tb_lo(p.credit_account_id), tb_hi(p.credit_account_id));
+                    }
+                }
+            } else {
+                const u32 c = (u32)(lp - P.log_base);
+                const Transfer& ce = *(const Transfer*)(P.events + (P.e0 + c) * 128);
+                if (ce.id == tb_u128(lo, hi)) {
+                    if (T.xdup[pos]) return false;  // its id collided in this pass: creator ambiguous
+                    if (!(P.eflags[c] & (TF_POST | TF_VOID)) && (P.info[c] & HZ_ACCTS)) {
+                        drs = P.dr[c];
+                        crs = P.cr[c];
+                    }
+                }
+            }
+            if (drs != TB_NOT_FOUND && fl_account_is_resource(T, drs, P.epoch, cert_global)) keys[nk++] = drs;
+            if (crs != TB_NOT_FOUND && fl_account_is_resource(T, crs, P.epoch, cert_global)) keys[nk++] = crs;
+            if (nk > FLOW_RMAX - 2) return false;  // several matching records: keep it simple
+        }
+        pos = (pos + 1) & T.xidx_mask;
+    }
+    return true;
+}
+
+// Execute one unit (a chain or a single event) with the reference logic; returns the max
+// timestamp of its events that returned ok.
+__device__ static inline u64 fl_run_unit(const PassArgs& P, const FlowArgs& F, Replay& R, u32 u) {
+    const u32 m = F.f_len[u];
+    R.undo = F.undo + 4ULL * u;
+    R.undo_cap = 4 * m;
+    R.undo_len = 0;
+    R.scope = false;
+    u64 tsmax = 0;
+    bool in_chain = false, broken = false;
+    for (u32 j = 0; j < m && !R.failed; j++) {
+        const u32 f = u + j;
+        const u32 pe = F.f_pe[f];
+        const u32 b = F.f_batch[f];
+        const u64 boff = P.batch_off[b];
+        const u32 L = (u32)(P.batch_off[b + 1] - boff);
+        const u32 i = (u32)(P.e0 + pe - boff);
+        const u8* ev = P.events + (boff + i) * 128;
+        const u16 flags = P.eflags[pe];
+        const u64 evts = P.routed ? 0 : *(const u64*)(ev + 120);
+        const bool linked = flags & TF_LINKED;
+        u32 result;
+        if (linked && !in_chain) {
+            in_chain = true;
+            R.scope = true;
+            R.undo_len = 0;
+        }
+        if (linked && i == L - 1) {
+            result = R_LINKED_EVENT_CHAIN_OPEN;
+        } else if (broken) {
+            result = R_LINKED_EVENT_FAILED;
+        } else if (evts != 0) {
+            result = R_TIMESTAMP_MUST_BE_ZERO;
+        } else {
+            const u64 ts = tb_event_ts(P, b, boff, L, i);
+            Transfer t = *(const Transfer*)ev;
+            t.timestamp = ts;
+            const u32 info = P.info[pe];
+            FastHint hint;
+            const bool fast = m == 1 && (F.uflags[u] & UF_ID_SINGLE) && (info & HZ_SPEC) && (info & HZ_ACCTS) &&
+                              !(flags & (TF_POST | TF_VOID));
+            if (fast) {
+                hint.drs = P.dr[pe];
+                hint.crs = P.cr[pe];
+                hint.entry = P.rs[pe];
+            }
+            result = rp_create_transfer<true>(R, t, (u32)(R.log_base + pe), fast ? &hint : nullptr);
+            if (result == R_OK && !R.failed) tsmax = ts;
+        }
+        if (R.failed) break;
+        if (result != R_OK && in_chain && !broken) {
+            broken = true;
+            rp_scope_close<true>(R, false);  // commit_timestamp keeps their timestamps (:763, :882)
+            for (u32 jj = 0; jj < j; jj++) {
+                u32* w = &P.info[F.f_pe[u + jj]];
+                *w = (*w & 0xFFFFFF00u) | R_LINKED_EVENT_FAILED;
+            }
+        }
+        u32* w = &P.info[pe];
+        *w = (*w & 0xFFFFFF00u) | result;
+        if (in_chain && (!linked || result == R_LINKED_EVENT_CHAIN_OPEN)) {
+            if (!broken) rp_scope_close<true>(R, true);
+            in_chain = false;
+            broken = false;
+        }
+    }
+    return tsmax;
+}
+
+// Replies of every prepare with dependent events (their final codes are in P.info), then close
+// the pass: bound += S, reset the dependent counter.  Workgroup 0, every thread.
+__device__ static inline void fl_finish(const PassArgs& P, u8* s_code, u32* s_wave, u64 tsmax_block) {
+    Globals* g = P.T.g;
+    const u32 nb = P.b1 - P.b0;
+    for (u32 k = 0; k < nb; k++) {
+        if (P.dep_count[k] == 0) continue;
+        const u32 b = P.b0 + k;
+        const u64 boff = P.batch_off[b];
+        const u32 L = (u32)(P.batch_off[b + 1] - boff);
+        const u32 pbase = (u32)(boff - P.e0);
+        for (u32 i = threadIdx.x; i < L; i += blockDim.x) s_code[i] = (u8)(P.info[pbase + i] & 0xFF);
+        __syncthreads();
+        tb_write_replies(P, b, L, s_code, s_wave);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (tsmax_block > g->commit_timestamp) g->commit_timestamp = tsmax_block;
+        const u128 S = tb_sum_total(P.sum_shards);
+        const u128 nb2 = tb_sat_add(tb_u128(g->bound_lo, g->bound_hi), S);
+        g->bound_lo = tb_lo(nb2);
+        g->bound_hi = tb_hi(nb2);
+        g->dependent_all += g->dependent_total;
+        g->dependent_total = 0;
+    }
+}
+
+__global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, UndoEntry* seq_undo, u32 seq_undo_cap) {
+    __shared__ u32 s_dpre[FLOW_NB_MAX + 1];
+    __shared__ u32 s_wave[FLOW_THREADS / 64];
+    __shared__ u32 s_hist[256];
+    __shared__ u32 s_base[256];
+    __shared__ u32 s_wcnt[FLOW_THREADS / 64][256];
+    __shared__ u8 s_code[BATCH_LDS];
+    __shared__ u32 s_qhead, s_qtail, s_nunits, s_done;
+    __shared__ u64 s_tsmax[FLOW_THREADS / 64];
+
+    Globals* g = P.T.g;
+    const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid;
+    const u32 nb = P.b1 - P.b0;
+    if (__hip_atomic_load(&g->dependent_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        if (blockIdx.x == 0) fl_finish(P, s_code, s_wave, 0);
+        return;
+    }
+    u128 S;
+    bool cert_global, cert64;
+    tb_pass_cert(P, S, cert_global, cert64);
+    u32 gen = 0;
+
+    // ---- plan 1: flat list of dependent events, units, resource pairs ------------------------
+    for (u32 k = tid; k < nb; k += NT) s_dpre[k] = P.dep_count[k];
+    __syncthreads();
+    tb_block_scan_lds(s_dpre, nb, s_wave);
+    const u32 ndep = s_dpre[nb];
+    const u32 N = FLOW_RMAX * ndep;
+    for (u32 f = blockIdx.x * NT + tid; f < ndep; f += G * NT) {
+        u32 lo = 0, hi = nb;  // the batch k with s_dpre[k] <= f < s_dpre[k + 1]
+        while (hi - lo > 1) {
+            const u32 mid = (lo + hi) >> 1;
+            if (s_dpre[mid] <= f) lo = mid; else hi = mid;
+        }
+        const u32 b = P.b0 + lo;
+        const u64 boff = P.batch_off[b];
+        const u32 L = (u32)(P.batch_off[b + 1] - boff);
+        const u32 pbase = (u32)(boff - P.e0);
+        const u32 i = P.dep_list[pbase + (f - s_dpre[lo])];
+        const u32 pe = pbase + i;
+        F.f_pe[f] = pe;
+        F.f_batch[f] = b;
+        F.need[f] = 0;
+        F.nsucc[f] = 0;
+        F.queue[f] = 0;
+        F.uflags[f] = 0;
+        // Unit: the chain (execute :628-692) this event belongs to, headed by its first member.
+        u32 i0 = i;
+        while (i0 > 0 && (P.eflags[pbase + i0 - 1] & TF_LINKED)) {
+            i0--;
+            if (i - i0 > FLOW_CHAIN_MAX) break;
+        }
+        const bool seq = i - i0 > FLOW_CHAIN_MAX;
+        const u32 unit = f - (i - i0);
+        u32 m = 0;
+        if (unit == f) {
+            m = 1;
+            for (u32 j = i; (P.eflags[pbase + j] & TF_LINKED) && j + 1 < L && m <= FLOW_CHAIN_MAX; j++) m++;
+            atomicAdd(&F.words[FW_NUNITS], 1u);
+        }
+        F.f_len[f] = m;
+        // Resources.
+        u32 keys[FLOW_RMAX];
+        u32 nk = 0;
+        bool ok = !seq && m <= FLOW_CHAIN_MAX;
+        const Transfer* ev = (const Transfer*)(P.events + (P.e0 + pe) * 128);
+        const u16 fl = P.eflags[pe];
+        const u32 info = P.info[pe];
+        keys[nk++] = fl_key_id(tb_lo(ev->id), tb_hi(ev->id));
+        if (fl & (TF_POST | TF_VOID)) {
+            keys[nk++] = fl_key_id(tb_lo(ev->pending_id), tb_hi(ev->pending_id));
+            ok = ok && fl_pending_accounts(P, tb_lo(ev->pending_id), tb_hi(ev->pending_id), cert_global, keys, nk);
+        } else if (info & HZ_ACCTS) {
+            if (fl_account_is_resource(P.T, P.dr[pe], P.epoch, cert_global)) keys[nk++] = P.dr[pe];
+            if (fl_account_is_resource(P.T, P.cr[pe], P.epoch, cert_global)) keys[nk++] = P.cr[pe];
+        }
+        if (!ok) atomicOr(&F.words[FW_SEQ], 1u);
+#pragma unroll
+        for (u32 k = 0; k < FLOW_RMAX; k++) {
+            F.keys[0][FLOW_RMAX * f + k] = k < nk ? keys[k] : FLOW_SENT;
+            F.vals[0][FLOW_RMAX * f + k] = unit;
+        }
+    }
+    fl_grid_sync(g, G, gen, F);
+    if (fl_stalled(g)) return;
+    const bool sequential = *(volatile u32*)&F.words[FW_SEQ] != 0;
+
+    if (!sequential) {
+        // ---- plan 2: stable LSD radix sort of the pairs by key (4 x 8 bits) ---------------------
+        const u32 tile = ((N + G - 1) / G + NT - 1) / NT * NT;
+        const u32 t0 = min(N, blockIdx.x * tile), t1 = min(N, t0 + tile);
+        const u32 lane = tid & 63, wave = tid >> 6;
+        for (u32 pass = 0; pass < 4; pass++) {
+            const u32 shift = 8 * pass;
+            const u32* sk = F.keys[pass & 1];
+            const u32* sv = F.vals[pass & 1];
+            u32* dk = F.keys[(pass + 1) & 1];
+            u32* dv = F.vals[(pass + 1) & 1];
+            if (tid < 256) s_hist[tid] = 0;
+            __syncthreads();
+            for (u32 q = t0 + tid; q < t1; q += NT) atomicAdd(&s_hist[(sk[q] >> shift) & 255], 1u);
+            __syncthreads();
+            if (tid < 256) F.hist[blockIdx.x * 256 + tid] = s_hist[tid];
+            fl_grid_sync(g, G, gen, F);
+            if (fl_stalled(g)) return;
+            u32 tot = 0, before = 0;
+            if (tid < 256) {
+                for (u32 w = 0; w < G; w++) {
+                    const u32 c = F.hist[w * 256 + tid];
+                    tot += c;
+                    before += w < blockIdx.x ? c : 0;
+                }
+                s_hist[tid] = tot;
+            }
+            __syncthreads();
+            if (tid < 256) {  // exclusive scan of the digit totals (256 entries, one wave per 64)
+                u32 start = 0;
+                for (u32 d = 0; d < tid; d++) start += s_hist[d];
+                s_base[tid] = start + before;
+            }
+            __syncthreads();
+            for (u32 c0 = t0; c0 < t1; c0 += NT) {
+                const u32 q = c0 + tid;
+                const bool valid = q < t1;
+                const u32 key = valid ? sk[q] : 0, val = valid ? sv[q] : 0;
+                const u32 d = (key >> shift) & 255;
+                for (u32 k = tid; k < (NT / 64) * 256; k += NT) (&s_wcnt[0][0])[k] = 0;
+                u64 peers = __ballot(valid);
+#pragma unroll
+                for (u32 bit = 0; bit < 8; bit++) {
+                    const u64 m = __ballot((d >> bit) & 1);
+                    peers &= ((d >> bit) & 1) ? m : ~m;
+                }
+                const u32 rank = __popcll(peers & ((1ULL << lane) - 1));
+                __syncthreads();
+                if (valid && rank == 0) s_wcnt[wave][d] = __popcll(peers);
+                __syncthreads();
+                if (tid < 256) {
+                    u32 run = s_base[tid];
+                    for (u32 w = 0; w < NT / 64; w++) {
+                        const u32 c = s_wcnt[w][tid];
+                        s_wcnt[w][tid] = run;
+                        run += c;
+                    }
+                    s_base[tid] = run;
+                }
+                __syncthreads();
+                if (valid) {
+                    const u32 pos = s_wcnt[wave][d] + rank;
+                    dk[pos] = key;
+                    dv[pos] = val;
+                }
+                __syncthreads();
+            }
+            fl_grid_sync(g, G, gen, F);
+            if (fl_stalled(g)) return;
+        }
+
+        // ---- plan 3: link each unit to its successor on every resource --------------------------
+        const u32* K = F.keys[0];
+        const u32* V = F.vals[0];
+        for (u32 q = blockIdx.x * NT + tid; q < N; q += G * NT) {
+            const u32 key = K[q];
+            if (key == FLOW_SENT) continue;
+            const bool first = q == 0 || K[q - 1] != key;
+            if (first && (key & 0x80000000u) && (q + 1 == N || K[q + 1] != key)) atomicOr(&F.uflags[V[q]], UF_ID_SINGLE);
+            if (first) continue;
+            const u32 u = V[q], v = V[q - 1];
+            if (u == v) continue;  // the same unit holds this resource twice
+            atomicAdd(&F.need[u], 1u);
+            const u32 slot = atomicAdd(&F.nsucc[v], 1u);
+            F.succ[FLOW_RMAX * v + slot] = u;
+        }
+        fl_grid_sync(g, G, gen, F);
+        if (fl_stalled(g)) return;
+        for (u32 f = blockIdx.x * NT + tid; f < ndep; f += G * NT) {
+            if (F.f_len[f] && F.need[f] == 0) {
+                const u32 pos = atomicAdd(&F.words[FW_QTAIL], 1u);
+                F.queue[pos] = f + 1;
+            }
+        }
+        fl_grid_sync(g, G, gen, F);
+        if (fl_stalled(g)) return;
+    }
+    if (blockIdx.x != 0) return;
+
+    // ---- run (workgroup 0) ---------------------------------------------------------------------
+    u64 tsmax = 0;
+    if (sequential) {
+        Replay R;
+        R.T = P.T;
+        R.undo = seq_undo;
+        R.undo_len = 0;
+        R.undo_cap = seq_undo_cap;
+        R.scope = false;
+        R.failed = false;
+        R.log_base = P.log_base;
+        R.epoch = P.epoch;
+        R.cert_global = cert_global;
+        if (tid == 0) {
+            for (u32 k = 0; k < nb && !R.failed; k++) {
+                if (P.dep_count[k] == 0) continue;
+                tsmax = max(tsmax, rp_batch<OP_CREATE_TRANSFERS>(P, R, P.b0 + k));
+            }
+        }
+    } else {
+        if (tid == 0) {
+            s_qhead = 0;
+            s_qtail = F.words[FW_QTAIL];
+            s_nunits = F.words[FW_NUNITS];
+            s_done = 0;
+        }
+        __syncthreads();
+        const u32 nunits = s_nunits;
+        Replay R;
+        R.T = P.T;
+        R.failed = false;
+        R.log_base = P.log_base;
+        R.epoch = P.epoch;
+        R.cert_global = cert_global;
+        R.cert64 = cert64;
+        // Each lane: take a ticket (a queue position), wait for its unit, run it, release its
+        // successors; the lane continues with the first successor that became ready (a chain of
+        // units on one hot resource then never goes through the queue) and queues the others.
+        // Not every ticket is filled (continued units skip the queue): a lane stops when all
+        // units are done.
+        u32 ticket = FLOW_SENT, spins = 0, next = FLOW_SENT;
+        u64 w0 = 0;
+        while (true) {
+            u32 u;
+            if (next != FLOW_SENT) {
+                u = next;
+                next = FLOW_SENT;
+            } else {
+                if (ticket == FLOW_SENT) ticket = atomicAdd(&s_qhead, 1u);
+                const u32 item = ticket < nunits
+                                     ? __hip_atomic_load(&F.queue[ticket], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : 0;
+                if (item == 0) {
+                    if (*(volatile u32*)&s_done >= nunits) break;
+                    if (spins++ == 0) w0 = fl_now();
+                    if (spins % 256 == 0 && (fl_expired(F, w0) || fl_stalled(g))) {
+                        tb_panic(g, PANIC_FLOW_STALL);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                spins = 0;
+                ticket = FLOW_SENT;
+                u = item - 1;
+            }
+            tsmax = max(tsmax, fl_run_unit(P, F, R, u));
+            R.failed = false;  // a panic is recorded in g->panic; keep releasing successors
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this unit's writes land first
+            const u32 ns = F.nsucc[u];
+            for (u32 k = 0; k < ns; k++) {
+                const u32 s = F.succ[FLOW_RMAX * u + k];
+                if (atomicSub(&F.need[s], 1u) == 1u) {
+                    if (next == FLOW_SENT) {
+                        next = s;
+                    } else {
+                        const u32 pos = atomicAdd(&s_qtail, 1u);
+                        __hip_atomic_store(&F.queue[pos], s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+            }
+            atomicAdd(&s_done, 1u);
+        }
+        if (tid == 0) {
+            atomicAdd(&g->flow_passes, 1u);
+            atomicAdd((unsigned long long*)&g->flow_units, (unsigned long long)nunits);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    u64 m = tsmax;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (u64)__shfl_xor((unsigned long long)m, off));
+    if ((tid & 63) == 0) s_tsmax[tid >> 6] = m;
+    __syncthreads();
+    u64 mm = 0;
+    for (u32 k = 0; k < NT / 64; k++) mm = max(mm, s_tsmax[k]);
+    fl_finish(P, s_code, s_wave, mm);
+}

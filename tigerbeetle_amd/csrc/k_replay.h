@@ -11,15 +11,24 @@
 
 #include "k_resolve.h"
 
-enum : u32 { UNDO_ACCOUNT_INSERT = 1, UNDO_BALANCE_UPDATE = 2, UNDO_TRANSFER_INSERT = 3, UNDO_POSTED = 4 };
+enum : u32 {
+    UNDO_ACCOUNT_INSERT = 1, UNDO_BALANCE_UPDATE = 2, UNDO_TRANSFER_INSERT = 3, UNDO_POSTED = 4,
+    UNDO_FREE_DELTA = 5,  // flow path: the four balance deltas added (atomically) to a free account
+};
 
 struct alignas(16) UndoEntry {
     u32 kind;
     u32 slot;  // account slot / index entry / log position
     u64 pad;
-    AccountBal before;
+    AccountBal before;  // UNDO_FREE_DELTA: the deltas
 };
 
+// Replay state of one lane.  FLOW = false: the sequential replay (one lane of one workgroup owns
+// every table it touches).  FLOW = true: one of many lanes of the parallel flow path (k_flow.h):
+// every read of state another lane may have written goes through L1-bypassing agent-scope loads,
+// and balances of FREE accounts (no limit flag, not balancing-marked, under the global overflow
+// certificate: no check reads them) are changed only by atomic deltas, since lanes that do not
+// share a resource run concurrently.
 struct Replay {
     Tables T;
     UndoEntry* undo;
@@ -28,7 +37,70 @@ struct Replay {
     u64 log_base;
     bool scope;
     bool failed;  // a panic was raised: stop
+    // flow path
+    u32 epoch;
+    bool cert_global;
+    bool cert64;  // no balance word can carry this pass: free-account deltas are low-word adds
 };
+
+// Flow path, single-event unit whose lookups kernel 1 already did exactly (k_flow.h): the account
+// slots (accounts never change in a create_transfers pass) and the id's absence (its speculative
+// claim was a new entry, and no other dependent event of the pass names this id).  The insert then
+// revives that entry instead of claiming a new one.
+struct FastHint {
+    u32 drs, crs;
+    u32 entry;  // index entry claimed by kernel 1 (tombstoned by kernel 2)
+};
+
+__device__ static inline u64 fl_ld64(const void* p) {
+    return __hip_atomic_load((const u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ static inline u128 fl_ld128(const void* p) {
+    const u64* w = (const u64*)p;
+    return tb_u128(fl_ld64(w), fl_ld64(w + 1));
+}
+template <bool FLOW, typename R>
+__device__ static inline R rp_load(const R* p) {
+    static_assert(sizeof(R) % 8 == 0, "8-byte words");
+    if (!FLOW) return *p;
+    R r;
+    u64* d = (u64*)&r;
+#pragma unroll
+    for (u32 k = 0; k < sizeof(R) / 8; k++) d[k] = fl_ld64((const u64*)p + k);
+    return r;
+}
+template <bool FLOW>
+__device__ static inline u8 rp_load_posted(const Tables& T, u32 pos) {
+    if (!FLOW) return T.xposted[pos];
+    const u32 w = __hip_atomic_load((const u32*)(T.xposted + (pos & ~3u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (u8)(w >> (8 * (pos & 3)));
+}
+
+// Flow path: is this account's balance an ordering resource (k_flow.h)?  Must agree with the
+// planner's choice.
+__device__ static inline bool fl_account_is_resource(const Tables& T, u32 slot, u32 epoch, bool cert_global) {
+    return !cert_global || (T.acct_hot[slot].flags & AF_LIMITS) || T.account_mark[slot] == epoch;
+}
+
+// tb_transfer_find with agent-scope loads (entries and records may be new from another lane).
+template <bool FLOW>
+__device__ static inline u32 rp_transfer_find(const Tables& T, u64 lo, u64 hi) {
+    if (!FLOW) return tb_transfer_find(T, lo, hi);
+    if (tb_id_reserved(lo, hi)) return TB_NOT_FOUND;
+    const u64 fp = tb_fp32(lo, hi);
+    u64 pos = tb_hash_id(lo, hi) & T.xidx_mask;
+    for (u64 n = 0; n <= T.xidx_mask; n++) {
+        const u64 e = fl_ld64(&T.xidx[pos]);
+        if (e == 0) return TB_NOT_FOUND;
+        if ((e >> 32) == fp && !(e & XI_TOMB)) {
+            const u32 lp = tb_xi_pos(e);
+            const u64* idw = (const u64*)&T.xlog[lp];
+            if (fl_ld64(idw) == lo && fl_ld64(idw + 1) == hi) return lp;
+        }
+        pos = (pos + 1) & T.xidx_mask;
+    }
+    return TB_NOT_FOUND;
+}
 
 __device__ static inline void rp_panic(Replay& R, u32 code) {
     tb_panic(R.T.g, code);
@@ -47,6 +119,22 @@ __device__ static inline void rp_push(Replay& R, u32 kind, u32 slot, const Accou
     if (before) e.before = *before;
 }
 
+__device__ static inline void rp_add_free_delta(Replay& R, u32 slot, const AccountBal& d) {
+    u8* a = (u8*)&R.T.acct_bal[slot];
+    if (R.cert64) {  // every balance stays below 2^64: the low word alone is exact, no carry to wait for
+        if (d.debits_pending) tb_atomic_add_lo_noret(a + BAL_OFF_DEBITS_PENDING, tb_lo(d.debits_pending));
+        if (d.debits_posted) tb_atomic_add_lo_noret(a + BAL_OFF_DEBITS_POSTED, tb_lo(d.debits_posted));
+        if (d.credits_pending) tb_atomic_add_lo_noret(a + BAL_OFF_CREDITS_PENDING, tb_lo(d.credits_pending));
+        if (d.credits_posted) tb_atomic_add_lo_noret(a + BAL_OFF_CREDITS_POSTED, tb_lo(d.credits_posted));
+        return;
+    }
+    if (d.debits_pending) tb_atomic_add_u128(a + BAL_OFF_DEBITS_PENDING, d.debits_pending);
+    if (d.debits_posted) tb_atomic_add_u128(a + BAL_OFF_DEBITS_POSTED, d.debits_posted);
+    if (d.credits_pending) tb_atomic_add_u128(a + BAL_OFF_CREDITS_PENDING, d.credits_pending);
+    if (d.credits_posted) tb_atomic_add_u128(a + BAL_OFF_CREDITS_POSTED, d.credits_posted);
+}
+
+template <bool FLOW>
 __device__ static inline void rp_scope_close(Replay& R, bool persist) {
     if (!persist) {
         while (R.undo_len > 0) {
@@ -57,9 +145,19 @@ __device__ static inline void rp_scope_close(Replay& R, bool persist) {
                 R.T.g->account_count--;
                 break;
             case UNDO_BALANCE_UPDATE: R.T.acct_bal[e.slot] = e.before; break;
+            case UNDO_FREE_DELTA: {
+                AccountBal neg;
+                neg.debits_pending = (u128)0 - e.before.debits_pending;
+                neg.debits_posted = (u128)0 - e.before.debits_posted;
+                neg.credits_pending = (u128)0 - e.before.credits_pending;
+                neg.credits_posted = (u128)0 - e.before.credits_posted;
+                rp_add_free_delta(R, e.slot, neg);
+                break;
+            }
             case UNDO_TRANSFER_INSERT:
                 tb_xindex_tombstone(R.T, e.slot);
-                R.T.g->transfer_count--;
+                if (FLOW) atomicAdd((unsigned long long*)&R.T.g->transfer_count, ~0ULL);
+                else R.T.g->transfer_count--;
                 break;
             case UNDO_POSTED: R.T.xposted[e.slot] = POSTED_NONE; break;
             }
@@ -76,23 +174,52 @@ __device__ static inline u128 rp_add(Replay& R, u128 a, u128 b) {
     return r;
 }
 
-__device__ static inline void rp_balance_update(Replay& R, u32 slot, const AccountBal& next) {
-    rp_push(R, UNDO_BALANCE_UPDATE, slot, &R.T.acct_bal[slot]);
+// A free account on the flow path is not read at all (zeros, *free = true): under the global
+// certificate no check its value feeds can fire (overflows :848-861), and the others read only
+// constrained accounts (balancing :826-846, limits :863-868); rp_balance_update then applies the
+// difference as a delta.
+template <bool FLOW>
+__device__ static inline AccountBal rp_balance_load(Replay& R, u32 slot, bool* free) {
+    *free = FLOW && !fl_account_is_resource(R.T, slot, R.epoch, R.cert_global);
+    if (*free) return AccountBal{};
+    return rp_load<FLOW>(&R.T.acct_bal[slot]);
+}
+
+// Write an account's balances (`before` = what rp_balance_load returned).  A free account on the
+// flow path gets the difference as atomic deltas: other lanes may be adding to it concurrently,
+// and its value is read by no check (see Replay).
+template <bool FLOW>
+__device__ static inline void rp_balance_update(Replay& R, u32 slot, const AccountBal& before, const AccountBal& next) {
+    if (FLOW && !fl_account_is_resource(R.T, slot, R.epoch, R.cert_global)) {
+        AccountBal d;
+        d.debits_pending = next.debits_pending - before.debits_pending;
+        d.debits_posted = next.debits_posted - before.debits_posted;
+        d.credits_pending = next.credits_pending - before.credits_pending;
+        d.credits_posted = next.credits_posted - before.credits_posted;
+        rp_push(R, UNDO_FREE_DELTA, slot, &d);
+        rp_add_free_delta(R, slot, d);
+        return;
+    }
+    rp_push(R, UNDO_BALANCE_UPDATE, slot, &before);
     R.T.acct_bal[slot] = next;
 }
 
 // Insert a transfer record at the event's own log position (after an exact find said "absent").
+template <bool FLOW>
 __device__ static inline void rp_transfer_insert(Replay& R, const Transfer& t, u32 log_pos) {
     R.T.xlog[log_pos] = t;
+    if (FLOW) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record before its index entry
     const u32 entry = tb_transfer_claim_new(R.T, tb_lo(t.id), tb_hi(t.id), log_pos);
     if (entry == TB_NOT_FOUND) {
         R.failed = true;
         return;
     }
-    R.T.g->transfer_count++;
+    if (FLOW) atomicAdd((unsigned long long*)&R.T.g->transfer_count, 1ULL);
+    else R.T.g->transfer_count++;
     rp_push(R, UNDO_TRANSFER_INSERT, entry, nullptr);
 }
 
+template <bool FLOW>
 __device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t, u32 log_pos) {
     const Tables& T = R.T;
     const u16 f = t.flags;
@@ -105,9 +232,9 @@ __device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t, u32 l
     if (t.pending_id == t.id) return CT_PENDING_ID_MUST_BE_DIFFERENT;
     if (t.timeout != 0) return CT_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
 
-    const u32 pslot = tb_transfer_find(T, tb_lo(t.pending_id), tb_hi(t.pending_id));
+    const u32 pslot = rp_transfer_find<FLOW>(T, tb_lo(t.pending_id), tb_hi(t.pending_id));
     if (pslot == TB_NOT_FOUND) return CT_PENDING_TRANSFER_NOT_FOUND;
-    const Transfer p = T.xlog[pslot];
+    const Transfer p = rp_load<FLOW>(&T.xlog[pslot]);
     if (!(p.flags & TF_PENDING)) return CT_PENDING_TRANSFER_NOT_PENDING;
     const u32 drs = tb_account_find(T, tb_lo(p.debit_account_id), tb_hi(p.debit_account_id));
     const u32 crs = tb_account_find(T, tb_lo(p.credit_account_id), tb_hi(p.credit_account_id));
@@ -127,9 +254,9 @@ __device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t, u32 l
     if (amount > p.amount) return CT_EXCEEDS_PENDING_TRANSFER_AMOUNT;
     if ((f & TF_VOID) && amount < p.amount) return CT_PENDING_TRANSFER_HAS_DIFFERENT_AMOUNT;
 
-    const u32 es = tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id));
-    if (es != TB_NOT_FOUND) return tb_post_void_exists(t, T.xlog[es], p);
-    const u8 posted = T.xposted[pslot];
+    const u32 es = rp_transfer_find<FLOW>(T, tb_lo(t.id), tb_hi(t.id));
+    if (es != TB_NOT_FOUND) return tb_post_void_exists(t, rp_load<FLOW>(&T.xlog[es]), p);
+    const u8 posted = rp_load_posted<FLOW>(T, pslot);
     if (posted == POSTED_POSTED) return CT_PENDING_TRANSFER_ALREADY_POSTED;
     if (posted == POSTED_VOIDED) return CT_PENDING_TRANSFER_ALREADY_VOIDED;
     if (!(p.timestamp < t.timestamp)) {
@@ -160,15 +287,20 @@ __device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t, u32 l
     r.timestamp = t.timestamp;
     r.flags = t.flags;
     r.amount = amount;
-    rp_transfer_insert(R, r, log_pos);
+    rp_transfer_insert<FLOW>(R, r, log_pos);
     if (R.failed) return R_OK;
 
     rp_push(R, UNDO_POSTED, pslot, nullptr);
     T.xposted[pslot] = (f & TF_POST) ? POSTED_POSTED : POSTED_VOIDED;
 
-    AccountBal dr = T.acct_bal[drs];
-    AccountBal cr = T.acct_bal[crs];
-    if (dr.debits_pending < p.amount || cr.credits_pending < p.amount) {
+    bool dfree, cfree;
+    const AccountBal dr0 = rp_balance_load<FLOW>(R, drs, &dfree);
+    const AccountBal cr0 = rp_balance_load<FLOW>(R, crs, &cfree);
+    AccountBal dr = dr0, cr = cr0;
+    // The `-=` asserts (:991-992).  A free account on the flow path is not read: its pending
+    // balance covers every outstanding pending transfer (the engine runs the flow path only while
+    // no balance was set directly), this one included.
+    if ((!dfree && dr.debits_pending < p.amount) || (!cfree && cr.credits_pending < p.amount)) {
         rp_panic(R, PANIC_OVERFLOW);
         return R_OK;
     }
@@ -178,18 +310,20 @@ __device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t, u32 l
         dr.debits_posted = rp_add(R, dr.debits_posted, amount);
         cr.credits_posted = rp_add(R, cr.credits_posted, amount);
     }
-    rp_balance_update(R, drs, dr);
-    rp_balance_update(R, crs, cr);
+    rp_balance_update<FLOW>(R, drs, dr0, dr);
+    rp_balance_update<FLOW>(R, crs, cr0, cr);
     return R_OK;
 }
 
-__device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u32 log_pos) {
+template <bool FLOW>
+__device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u32 log_pos,
+                                                const FastHint* hint = nullptr) {
     const Tables& T = R.T;
     const u16 f = t.flags;
     if (f & TF_PADDING) return CT_RESERVED_FLAG;
     if (t.id == 0) return CT_ID_MUST_NOT_BE_ZERO;
     if (t.id == TB_U128_MAX) return CT_ID_MUST_NOT_BE_INT_MAX;
-    if (f & (TF_POST | TF_VOID)) return rp_post_or_void(R, t, log_pos);
+    if (f & (TF_POST | TF_VOID)) return rp_post_or_void<FLOW>(R, t, log_pos);
 
     if (t.debit_account_id == 0) return CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
     if (t.debit_account_id == TB_U128_MAX) return CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
@@ -206,14 +340,16 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u3
     if (t.ledger == 0) return CT_LEDGER_MUST_NOT_BE_ZERO;
     if (t.code == 0) return CT_CODE_MUST_NOT_BE_ZERO;
 
-    const u32 drs = tb_account_find(T, tb_lo(t.debit_account_id), tb_hi(t.debit_account_id));
+    const u32 drs = hint ? hint->drs : tb_account_find(T, tb_lo(t.debit_account_id), tb_hi(t.debit_account_id));
     if (drs == TB_NOT_FOUND) return CT_DEBIT_ACCOUNT_NOT_FOUND;
-    const u32 crs = tb_account_find(T, tb_lo(t.credit_account_id), tb_hi(t.credit_account_id));
+    const u32 crs = hint ? hint->crs : tb_account_find(T, tb_lo(t.credit_account_id), tb_hi(t.credit_account_id));
     if (crs == TB_NOT_FOUND) return CT_CREDIT_ACCOUNT_NOT_FOUND;
     const AccountHot dh = T.acct_hot[drs];
     const AccountHot ch = T.acct_hot[crs];
-    AccountBal dr = T.acct_bal[drs];
-    AccountBal cr = T.acct_bal[crs];
+    bool dfree, cfree;
+    const AccountBal dr0 = rp_balance_load<FLOW>(R, drs, &dfree);
+    const AccountBal cr0 = rp_balance_load<FLOW>(R, crs, &cfree);
+    AccountBal dr = dr0, cr = cr0;
     if (!(t.timestamp > dh.timestamp) || !(t.timestamp > ch.timestamp)) {
         rp_panic(R, PANIC_ASSERT);
         return R_OK;
@@ -221,8 +357,8 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u3
     if (dh.ledger != ch.ledger) return CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
     if (t.ledger != dh.ledger) return CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
 
-    const u32 es = tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id));
-    if (es != TB_NOT_FOUND) return tb_transfer_exists(t, T.xlog[es]);
+    const u32 es = hint ? TB_NOT_FOUND : rp_transfer_find<FLOW>(T, tb_lo(t.id), tb_hi(t.id));
+    if (es != TB_NOT_FOUND) return tb_transfer_exists(t, rp_load<FLOW>(&T.xlog[es]));
 
     u128 amount = t.amount;
     if (f & (TF_BAL_DEBIT | TF_BAL_CREDIT)) {
@@ -242,6 +378,8 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u3
     }
     if (R.failed) return R_OK;
 
+    // Overflow checks (:848-861).  A free account on the flow path reads as zero here; the global
+    // certificate holds, so none of these could fire for its real value either.
     u128 r;
     if (f & TF_PENDING) {
         if (tb_add_overflows(amount, dr.debits_pending, &r)) return CT_OVERFLOWS_DEBITS_PENDING;
@@ -267,7 +405,14 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u3
 
     Transfer t2 = t;
     t2.amount = amount;
-    rp_transfer_insert(R, t2, log_pos);
+    if (hint) {  // revive kernel 1's entry (a single event: no scope to undo)
+        R.T.xlog[log_pos] = t2;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record before its index entry
+        atomicAnd((unsigned long long*)&R.T.xidx[hint->entry], ~(unsigned long long)XI_TOMB);
+        atomicAdd((unsigned long long*)&R.T.g->transfer_count, 1ULL);
+    } else {
+        rp_transfer_insert<FLOW>(R, t2, log_pos);
+    }
     if (R.failed) return R_OK;
     if (f & TF_PENDING) {
         dr.debits_pending = rp_add(R, dr.debits_pending, amount);
@@ -276,8 +421,8 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u3
         dr.debits_posted = rp_add(R, dr.debits_posted, amount);
         cr.credits_posted = rp_add(R, cr.credits_posted, amount);
     }
-    rp_balance_update(R, drs, dr);
-    rp_balance_update(R, crs, cr);
+    rp_balance_update<FLOW>(R, drs, dr0, dr);
+    rp_balance_update<FLOW>(R, crs, cr0, cr);
     return R_OK;
 }
 
@@ -332,7 +477,7 @@ __device__ static inline u64 rp_batch(const PassArgs& P, Replay& R, u32 b) {
             if (OP == OP_CREATE_TRANSFERS) {
                 Transfer t = *(const Transfer*)ev;
                 t.timestamp = ts;
-                result = rp_create_transfer(R, t, (u32)(R.log_base + pbase + i));
+                result = rp_create_transfer<false>(R, t, (u32)(R.log_base + pbase + i));
             } else {
                 Account a = *(const Account*)ev;
                 a.timestamp = ts;
@@ -343,7 +488,7 @@ __device__ static inline u64 rp_batch(const PassArgs& P, Replay& R, u32 b) {
         if (R.failed) break;
         if (result != R_OK && in_chain && !broken) {
             broken = true;
-            rp_scope_close(R, false);
+            rp_scope_close<false>(R, false);
             for (u32 kk = chain_k; kk < k; kk++) {
                 u32* w = &P.info[pbase + list[kk]];
                 *w = (*w & 0xFFFFFF00u) | R_LINKED_EVENT_FAILED;
@@ -352,7 +497,7 @@ __device__ static inline u64 rp_batch(const PassArgs& P, Replay& R, u32 b) {
         u32* w = &P.info[pbase + i];
         *w = (*w & 0xFFFFFF00u) | result;
         if (in_chain && (!linked || result == R_LINKED_EVENT_CHAIN_OPEN)) {
-            if (!broken) rp_scope_close(R, true);
+            if (!broken) rp_scope_close<false>(R, true);
             in_chain = false;
             broken = false;
         }

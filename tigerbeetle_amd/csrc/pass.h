@@ -79,6 +79,7 @@ struct PassArgs {
     u64* leg_w;            // [2 * pass events] the same leg words grouped by bucket per prepare
 
     u32* leg_off;          // [prepares of the pass][leg_buckets + 1] bucket starts in the prepare's legs
+    u32* flow_words;       // tb_flow's per-pass counters (k_flow.h), zeroed by tb_resolve (or null)
 };
 
 enum : u32 { CERT_EXT_U128 = 1, CERT_EXT_U64 = 2 };
@@ -104,7 +105,8 @@ __device__ static inline u64 tb_event_ts(const PassArgs& P, u32 b, u64 boff, u32
 }
 
 enum : u32 { ABL_DEDUP = 1, ABL_SPEC = 2, ABL_ACCTS = 4, ABL_XFIND = 8, ABL_STAGE = 16, ABL_RECORD = 32, ABL_CAS = 64, EXP_NT = 128,
-             ABL_LEGS = 256, ABL_LEG_STORES = 512, ABL_LEG_WORK = 1024 };  // ABL_LEG_*: timing only (wrong balances)
+             ABL_LEGS = 256, ABL_LEG_STORES = 512, ABL_LEG_WORK = 1024,  // ABL_LEG_*: timing only (wrong balances)
+             ABL_FLOW = 2048 };  // sequential replay instead of the parallel flow path (exact either way)
 
 // Batch of a call-relative event index: binary search over batch_off[lo..hi) (off[lo] <= e < off[hi]).
 __device__ static inline u32 tb_batch_search(const u64* off, u32 lo, u32 hi, u64 e) {

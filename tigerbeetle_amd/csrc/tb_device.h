@@ -117,6 +117,7 @@ enum : u8 { POSTED_NONE = 0, POSTED_POSTED = 1, POSTED_VOIDED = 2 };
 // Device panic codes (the reference would trap).
 enum : u32 {
     PANIC_NONE = 0, PANIC_OVERFLOW = 1, PANIC_ASSERT = 2, PANIC_TABLE_FULL = 4, PANIC_UNDO_FULL = 8,
+    PANIC_FLOW_STALL = 16,  // engine bug guard: a flow-path wait exceeded its bound
 };
 
 #define TB_NOT_FOUND 0xFFFFFFFFu
@@ -184,7 +185,10 @@ struct Globals {
     u64 account_count;
     u64 transfer_count;
     u64 export_count;
-    u64 pad[5];
+    u32 flow_barrier;         // tb_flow grid-barrier arrivals (reset by tb_resolve each pass)
+    u32 flow_passes;          // passes whose dependent events ran on the parallel flow path
+    u64 flow_units;           // cumulative units (chains / single events) the flow path executed
+    u64 pad[3];
 };
 
 struct AccountHot {

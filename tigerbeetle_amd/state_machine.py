@@ -201,11 +201,14 @@ class Engine:
         _lib.check(self.lib.tbgpu_copy_to_device(self.h, ptr, array.ctypes.data, array.nbytes))
 
     def generate_accounts(self, out_dev, first, count, seed=42, limit_permille=0):
-        w = _lib.tbgpu_workload(seed, 0, 0, limit_permille)
+        w = _lib.tbgpu_workload(seed, 0, 0, limit_permille, 0.0)
         _lib.check(self.lib.tbgpu_bench_generate_accounts(self.h, out_dev, first, count, ctypes.byref(w)))
 
-    def generate_transfers(self, out_dev, first, count, account_count, seed=42, kind=0):
-        w = _lib.tbgpu_workload(seed, account_count, kind, 0)
+    def generate_transfers(self, out_dev, first, count, account_count, seed=42, kind=0, limit_permille=0,
+                           zipf_s=1.2):
+        """kind 0: C2 uniform; 1: C3 Zipf + limit-account funding; 2: C4 chains / two-phase / balancing
+        (include/tbgpu_bench.h).  limit_permille must match generate_accounts' for kind 1."""
+        w = _lib.tbgpu_workload(seed, account_count, kind, limit_permille, zipf_s)
         _lib.check(self.lib.tbgpu_bench_generate_transfers(self.h, out_dev, first, count, ctypes.byref(w)))
 
     def reset_transfers(self):
