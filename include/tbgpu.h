@@ -125,6 +125,8 @@ typedef struct tbgpu_stats {
     uint64_t launches_apply;
     uint64_t flow_passes;        /* passes whose dependent events ran on the parallel flow path */
     uint64_t flow_units;         /* chains / single dependent events the flow path executed */
+    uint64_t flow_runs;          /* runs: single-resource sequences walked with the balance in registers */
+    uint64_t flow_run_units;     /* units covered by runs */
 } tbgpu_stats;
 
 int tbgpu_get_stats(tbgpu_t* engine, tbgpu_stats* stats);

@@ -44,6 +44,8 @@ class tbgpu_stats(ctypes.Structure):
         ("launches_apply", ctypes.c_uint64),
         ("flow_passes", ctypes.c_uint64),
         ("flow_units", ctypes.c_uint64),
+        ("flow_runs", ctypes.c_uint64),
+        ("flow_run_units", ctypes.c_uint64),
     ]
 
 

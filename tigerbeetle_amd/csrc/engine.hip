@@ -88,6 +88,7 @@ struct tbgpu {
     // Parallel ordered fallback (k_flow.h): create_transfers passes run tb_flow instead of
     // tb_replay while no balance was set directly (the post/void assert argument, k_replay.h).
     bool flow_ok = false;
+    bool flow_coop = false;  // TBGPU_FLOW_COOP: hipLaunchCooperativeKernel (default: plain launch, same residency)
     bool balances_set = false;
     FlowArgs F{};
 
@@ -275,7 +276,11 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&tb_flow), FLOW_THREADS, 0) ==
                 hipSuccess &&
             occ >= 1 && prop.cooperativeLaunch) {
-            E->F.grid = (u32)std::min(prop.multiProcessorCount, 256);
+            // A quarter of the CUs at most: co-residency of the grid then holds even with a few
+            // engines (processes) sharing the device, each with a tb_flow in flight.
+            E->F.grid = (u32)std::max(1, std::min(prop.multiProcessorCount / 4, 64));
+            E->flow_coop = getenv("TBGPU_FLOW_COOP") != nullptr;
+            if (const char* gs = getenv("TBGPU_FLOW_GRID")) E->F.grid = std::max(1u, std::min(E->F.grid, (u32)atoi(gs)));
             int khz = 0;
             if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, E->device) != hipSuccess) khz = 0;
             khz = std::max(khz, 100000);  // s_memrealtime: 100 MHz on gfx9 parts; never trust a lower figure
@@ -321,6 +326,8 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         INIT_CK(hipMalloc(&F.nsucc, pe * 4));
         INIT_CK(hipMalloc(&F.queue, pe * 4));
         INIT_CK(hipMalloc(&F.uflags, pe * 4));
+        INIT_CK(hipMalloc(&F.nacct, pe * 4));
+        INIT_CK(hipMalloc(&F.rpos, pe * 4));
         INIT_CK(hipMalloc(&F.succ, pe * 4 * FLOW_RMAX));
         for (int k = 0; k < 2; k++) {
             INIT_CK(hipMalloc(&F.keys[k], pe * 4 * FLOW_RMAX));
@@ -360,7 +367,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
                     E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->r_home,
                     E->r_block_counts, E->r_words, E->r_meta, E->leg_ev, E->leg_w, E->leg_off,
-                    E->F.f_pe, E->F.f_batch, E->F.f_len, E->F.need, E->F.nsucc, E->F.queue, E->F.uflags, E->F.succ,
+                    E->F.f_pe, E->F.f_batch, E->F.f_len, E->F.need, E->F.nsucc, E->F.queue, E->F.uflags, E->F.nacct, E->F.rpos, E->F.succ,
                     E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo};
     for (void* p : bufs) if (p) (void)hipFree(p);
     if (E->h_meta) (void)hipHostFree(E->h_meta);
@@ -489,9 +496,14 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         if (flow) {
             UndoEntry* seq_undo = E->undo;
             u32 seq_cap = E->undo_cap;
-            void* args[] = {&P, &E->F, &seq_undo, &seq_cap};
-            HIPCK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&tb_flow), dim3(E->F.grid), dim3(FLOW_THREADS),
-                                             args, 0, E->stream));
+            if (E->flow_coop) {
+                void* args[] = {&P, &E->F, &seq_undo, &seq_cap};
+                HIPCK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&tb_flow), dim3(E->F.grid),
+                                                 dim3(FLOW_THREADS), args, 0, E->stream));
+            } else {
+                hipLaunchKernelGGL(tb_flow, dim3(E->F.grid), dim3(FLOW_THREADS), 0, E->stream, P, E->F, seq_undo, seq_cap);
+                HIPCK(hipGetLastError());
+            }
         } else if (op == OP_CREATE_TRANSFERS) {
             hipLaunchKernelGGL(tb_replay<OP_CREATE_TRANSFERS>, dim3(1), dim3(REPLAY_THREADS), 0, E->stream, P,
                                E->undo, E->undo_cap);
@@ -831,6 +843,8 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     s->launches_apply = E->prof_n[K_APPLY];
     s->flow_passes = g.flow_passes;
     s->flow_units = g.flow_units;
+    s->flow_runs = g.flow_runs;
+    s->flow_run_units = g.flow_run_units;
     return TBGPU_STATUS_OK;
 }
 

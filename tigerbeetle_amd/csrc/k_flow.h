@@ -50,6 +50,8 @@ struct FlowArgs {
     u32* succ;      // [FLOW_RMAX * pass events] unit u's successors at FLOW_RMAX * u
     u32* queue;     // [pass events] ready units (head + 1; 0 = not yet published)
     u32* uflags;    // [pass events] per unit head: UF_*
+    u32* nacct;     // [pass events] per unit head: account resources
+    u32* rpos;      // [pass events] per unit head: sorted position of its (last) account resource
     u32* keys[2];   // [FLOW_RMAX * pass events] radix-sort ping-pong buffers
     u32* vals[2];
     u32* hist;      // [grid * 256]
@@ -216,21 +218,141 @@ __device__ static inline u64 fl_run_unit(const PassArgs& P, const FlowArgs& F, R
     return tsmax;
 }
 
+// A RUN: consecutive units on one account resource r that each are a single plain create_transfer
+// whose only other state is free — kernel 1 validated it fully (code ok through the timeout check,
+// :779-862), its id is new and named by no other dependent event, r is its only constrained
+// account, and it is not balancing.  The only open check is r's limit (tigerbeetle.zig:31-39)
+// against r's running balance: a lane keeps r's balances in registers and walks the run down r's
+// sorted resource list, eight units per step with their loads issued together.  Kernel 1 already
+// wrote each record; an ok unit revives its index entry, adds its amount to r (registers) and to
+// its free account (atomic delta); a failed one gets exceeds_credits / exceeds_debits.
+__device__ static inline bool fl_run_member(const PassArgs& P, const FlowArgs& F, u32 u, u32 pe) {
+    const u32 info = P.info[pe];
+    return F.f_len[u] == 1 && F.nacct[u] == 1 && (F.uflags[u] & UF_ID_SINGLE) && (info & HZ_SPEC) &&
+           (info & HZ_ACCTS) && (info & 0xFF) == R_OK &&
+           !(P.eflags[pe] & (TF_LINKED | TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT));
+}
+
+#define FLOW_RUN_STEP 8
+
+// Runs the run headed by unit u (a run member); returns the last unit it ran (its successors are
+// released by the caller), *count = units run, *tsmax = max ok timestamp.
+__device__ static inline u32 fl_run_run(const PassArgs& P, const FlowArgs& F, const Replay& R, u32 u, u32 N,
+                                        u32* count, u64* tsmax) {
+    const Tables& T = P.T;
+    const u32* K = F.keys[0];
+    const u32* V = F.vals[0];
+    u32 q = F.rpos[u];
+    const u32 r = K[q];
+    AccountBal B = rp_load<true>(&T.acct_bal[r]);
+    const u16 rflags = T.acct_hot[r].flags;
+    u32 n = 0, n_ok = 0, last = u, last_ok_pe = TB_NOT_FOUND;
+    bool more = true;
+    while (more) {
+        // Three dependent load levels for eight candidates at once: list entry, unit, event.
+        u32 cu[FLOW_RUN_STEP], cpe[FLOW_RUN_STEP], cdr[FLOW_RUN_STEP], ccr[FLOW_RUN_STEP], crs_[FLOW_RUN_STEP];
+        u64 camt[FLOW_RUN_STEP], camt_hi[FLOW_RUN_STEP];
+        u16 cfl[FLOW_RUN_STEP];
+        bool ok[FLOW_RUN_STEP];
+#pragma unroll
+        for (u32 j = 0; j < FLOW_RUN_STEP; j++) {
+            ok[j] = q + j < N && K[q + j] == r;
+            cu[j] = ok[j] ? V[q + j] : 0;
+        }
+#pragma unroll
+        for (u32 j = 0; j < FLOW_RUN_STEP; j++) {
+            cpe[j] = ok[j] ? F.f_pe[cu[j]] : 0;
+            ok[j] = ok[j] && F.f_len[cu[j]] == 1 && F.nacct[cu[j]] == 1 && (F.uflags[cu[j]] & UF_ID_SINGLE);
+        }
+#pragma unroll
+        for (u32 j = 0; j < FLOW_RUN_STEP; j++) {
+            const u32 pe = cpe[j];
+            const u32 info = ok[j] ? P.info[pe] : 0;
+            cfl[j] = ok[j] ? P.eflags[pe] : 0;
+            cdr[j] = ok[j] ? P.dr[pe] : 0;
+            ccr[j] = ok[j] ? P.cr[pe] : 0;
+            crs_[j] = ok[j] ? P.rs[pe] : 0;
+            camt[j] = ok[j] ? P.amt[2 * pe] : 0;
+            camt_hi[j] = ok[j] ? P.amt[2 * pe + 1] : 0;
+            ok[j] = ok[j] && (info & HZ_SPEC) && (info & HZ_ACCTS) && (info & 0xFF) == R_OK &&
+                    !(cfl[j] & (TF_LINKED | TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT));
+        }
+        u32 j = 0;
+        for (; j < FLOW_RUN_STEP && ok[j]; j++) {
+            const u32 pe = cpe[j];
+            const u32 drs = cdr[j], crs = ccr[j];
+            const bool debit = drs == r;  // else r is the credit side
+            const bool pend = cfl[j] & TF_PENDING;
+            const u128 amount = tb_u128(camt[j], camt_hi[j]);
+            u32 code = R_OK;
+            if (debit && (rflags & AF_DEBITS_MUST_NOT_EXCEED_CREDITS) &&
+                B.debits_pending + B.debits_posted + amount > B.credits_posted) {
+                code = CT_EXCEEDS_CREDITS;
+            } else if (!debit && (rflags & AF_CREDITS_MUST_NOT_EXCEED_DEBITS) &&
+                       B.credits_pending + B.credits_posted + amount > B.debits_posted) {
+                code = CT_EXCEEDS_DEBITS;
+            }
+            if (code == R_OK) {
+                u128* rf = debit ? (pend ? &B.debits_pending : &B.debits_posted)
+                                 : (pend ? &B.credits_pending : &B.credits_posted);
+                *rf += amount;
+                // The free side: one field, +amount (exact in any order).
+                u8* fb = (u8*)&T.acct_bal[debit ? crs : drs];
+                const u32 off = debit ? (pend ? BAL_OFF_CREDITS_PENDING : BAL_OFF_CREDITS_POSTED)
+                                      : (pend ? BAL_OFF_DEBITS_PENDING : BAL_OFF_DEBITS_POSTED);
+                if (R.cert64) tb_atomic_add_lo_noret(fb + off, tb_lo(amount));
+                else tb_atomic_add_u128(fb + off, amount);
+                __hip_atomic_fetch_and(&T.xidx[crs_[j]], ~(u64)XI_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                n_ok++;
+                last_ok_pe = pe;
+            } else {
+                P.info[pe] = (P.info[pe] & 0xFFFFFF00u) | code;
+            }
+            last = cu[j];
+            n++;
+        }
+        more = j == FLOW_RUN_STEP;
+        q += FLOW_RUN_STEP;
+    }
+    T.acct_bal[r] = B;
+    if (n_ok) atomicAdd((unsigned long long*)&T.g->transfer_count, (unsigned long long)n_ok);
+    if (last_ok_pe != TB_NOT_FOUND) {  // commit_timestamp: the run's last ok event is its latest
+        u32 lo = P.b0, hi = P.b1;
+        const u64 e = P.e0 + last_ok_pe;
+        while (hi - lo > 1) {
+            const u32 mid = (lo + hi) >> 1;
+            if (P.batch_off[mid] <= e) lo = mid; else hi = mid;
+        }
+        const u64 boff = P.batch_off[lo];
+        *tsmax = tb_event_ts(P, lo, boff, (u32)(P.batch_off[lo + 1] - boff), (u32)(e - boff));
+    }
+    *count = n;
+    return last;
+}
+
 // Replies of every prepare with dependent events (their final codes are in P.info), then close
 // the pass: bound += S, reset the dependent counter.  Workgroup 0, every thread.
-__device__ static inline void fl_finish(const PassArgs& P, u8* s_code, u32* s_wave, u64 tsmax_block) {
+__device__ static inline void fl_finish(const PassArgs& P, u8* s_code, u32* s_wave, u32* s_list, u64 tsmax_block,
+                                         bool any) {
     Globals* g = P.T.g;
     const u32 nb = P.b1 - P.b0;
-    for (u32 k = 0; k < nb; k++) {
-        if (P.dep_count[k] == 0) continue;
-        const u32 b = P.b0 + k;
-        const u64 boff = P.batch_off[b];
-        const u32 L = (u32)(P.batch_off[b + 1] - boff);
-        const u32 pbase = (u32)(boff - P.e0);
-        for (u32 i = threadIdx.x; i < L; i += blockDim.x) s_code[i] = (u8)(P.info[pbase + i] & 0xFF);
+    for (u32 c = 0; any && c < nb; c += blockDim.x) {
+        const u32 k = c + threadIdx.x;
+        const bool has = k < nb && P.dep_count[k] > 0;
+        u32 total;
+        const u32 r = tb_block_rank(has, s_wave, total);
+        if (has) s_list[r] = k;
         __syncthreads();
-        tb_write_replies(P, b, L, s_code, s_wave);
-        __syncthreads();
+        for (u32 q = 0; q < total; q++) {
+            const u32 b = P.b0 + s_list[q];
+            const u64 boff = P.batch_off[b];
+            const u32 L = (u32)(P.batch_off[b + 1] - boff);
+            const u32 pbase = (u32)(boff - P.e0);
+            for (u32 i = threadIdx.x; i < L; i += blockDim.x) s_code[i] = (u8)(P.info[pbase + i] & 0xFF);
+            __syncthreads();
+            tb_write_replies(P, b, L, s_code, s_wave);
+            __syncthreads();
+        }
     }
     if (threadIdx.x == 0) {
         if (tsmax_block > g->commit_timestamp) g->commit_timestamp = tsmax_block;
@@ -250,6 +372,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     __shared__ u32 s_base[256];
     __shared__ u32 s_wcnt[FLOW_THREADS / 64][256];
     __shared__ u8 s_code[BATCH_LDS];
+    __shared__ u32 s_list[FLOW_THREADS];
     __shared__ u32 s_qhead, s_qtail, s_nunits, s_done;
     __shared__ u64 s_tsmax[FLOW_THREADS / 64];
 
@@ -257,7 +380,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid;
     const u32 nb = P.b1 - P.b0;
     if (__hip_atomic_load(&g->dependent_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        if (blockIdx.x == 0) fl_finish(P, s_code, s_wave, 0);
+        if (blockIdx.x == 0) fl_finish(P, s_code, s_wave, s_list, 0, false);
         return;
     }
     u128 S;
@@ -289,6 +412,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
         F.nsucc[f] = 0;
         F.queue[f] = 0;
         F.uflags[f] = 0;
+        F.nacct[f] = 0;
         // Unit: the chain (execute :628-692) this event belongs to, headed by its first member.
         u32 i0 = i;
         while (i0 > 0 && (P.eflags[pbase + i0 - 1] & TF_LINKED)) {
@@ -408,10 +532,15 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
             const u32 key = K[q];
             if (key == FLOW_SENT) continue;
             const bool first = q == 0 || K[q - 1] != key;
-            if (first && (key & 0x80000000u) && (q + 1 == N || K[q + 1] != key)) atomicOr(&F.uflags[V[q]], UF_ID_SINGLE);
+            const u32 u = V[q];
+            if (first && (key & 0x80000000u) && (q + 1 == N || K[q + 1] != key)) atomicOr(&F.uflags[u], UF_ID_SINGLE);
+            if (!first && V[q - 1] == u) continue;  // the same unit holds this resource twice
+            if (!(key & 0x80000000u)) {
+                atomicAdd(&F.nacct[u], 1u);
+                F.rpos[u] = q;
+            }
             if (first) continue;
-            const u32 u = V[q], v = V[q - 1];
-            if (u == v) continue;  // the same unit holds this resource twice
+            const u32 v = V[q - 1];
             atomicAdd(&F.need[u], 1u);
             const u32 slot = atomicAdd(&F.nsucc[v], 1u);
             F.succ[FLOW_RMAX * v + slot] = u;
@@ -471,6 +600,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
         // units are done.
         u32 ticket = FLOW_SENT, spins = 0, next = FLOW_SENT;
         u64 w0 = 0;
+        u32 runs = 0, run_units = 0;
         while (true) {
             u32 u;
             if (next != FLOW_SENT) {
@@ -495,7 +625,16 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
                 ticket = FLOW_SENT;
                 u = item - 1;
             }
-            tsmax = max(tsmax, fl_run_unit(P, F, R, u));
+            u32 ran = 1;
+            if (fl_run_member(P, F, u, F.f_pe[u])) {
+                u64 ts = 0;
+                u = fl_run_run(P, F, R, u, N, &ran, &ts);
+                tsmax = max(tsmax, ts);
+                runs++;
+                run_units += ran;
+            } else {
+                tsmax = max(tsmax, fl_run_unit(P, F, R, u));
+            }
             R.failed = false;  // a panic is recorded in g->panic; keep releasing successors
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this unit's writes land first
             const u32 ns = F.nsucc[u];
@@ -510,7 +649,11 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
                     }
                 }
             }
-            atomicAdd(&s_done, 1u);
+            atomicAdd(&s_done, ran);
+        }
+        if (runs) {
+            atomicAdd((unsigned long long*)&g->flow_runs, (unsigned long long)runs);
+            atomicAdd((unsigned long long*)&g->flow_run_units, (unsigned long long)run_units);
         }
         if (tid == 0) {
             atomicAdd(&g->flow_passes, 1u);
@@ -525,5 +668,5 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     __syncthreads();
     u64 mm = 0;
     for (u32 k = 0; k < NT / 64; k++) mm = max(mm, s_tsmax[k]);
-    fl_finish(P, s_code, s_wave, mm);
+    fl_finish(P, s_code, s_wave, s_list, mm, true);
 }

@@ -188,7 +188,9 @@ struct Globals {
     u32 flow_barrier;         // tb_flow grid-barrier arrivals (reset by tb_resolve each pass)
     u32 flow_passes;          // passes whose dependent events ran on the parallel flow path
     u64 flow_units;           // cumulative units (chains / single events) the flow path executed
-    u64 pad[3];
+    u64 flow_runs;            // runs (k_flow.h) and the units they covered
+    u64 flow_run_units;
+    u64 pad[1];
 };
 
 struct AccountHot {

@@ -21,5 +21,5 @@ t0 = time.time()
 e.commit_many(129, x_ts, split(xfers, x_lens))
 dt = time.time() - t0
 s = e.stats()
-print(config, "wall %.3fs" % dt, {k: s[k] for k in ("passes", "dependent_events", "flow_passes", "flow_units",
+print(config, "wall %.3fs" % dt, {k: s[k] for k in ("passes", "dependent_events", "flow_passes", "flow_units", "flow_runs", "flow_run_units",
                                                    "ms_replay", "launches_replay", "ms_validate", "ms_resolve")})

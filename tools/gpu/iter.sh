@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
-summ() { python -c 'import json,sys; d=json.loads(open(sys.argv[1]).readlines()[-1]); r=d["roofline"]; print(sys.argv[2], d["value"], d["ms_per_step"], r["kernel"], r["frac"], {k: v["avg_launch_ms"] for k, v in r["kernels"].items()})' "$1" "$2"; }
+summ() { python tools/gpu/summ.py "$1" "$2"; }
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
   tail -2 gpurun_out/pytest_gpu.log
