@@ -228,7 +228,12 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     INIT_CK(hipSetDevice(E->device));
     INIT_CK(hipStreamCreateWithFlags(&E->stream, hipStreamNonBlocking));
 
-    E->account_cap = pow2_at_least(std::max<u64>(2 * config->accounts_max, 1024));
+    // Account table slots per account (load factor <= 1/2).  4 slots shorten the probes (validate
+    // -2..10 % at C2, box to box) but double the legs buckets (tb_apply_legs +40 %): a net loss.
+    // TBGPU_ACCOUNT_SLOTS overrides (experiments).
+    u64 load = 2;
+    if (const char* s = getenv("TBGPU_ACCOUNT_SLOTS")) load = std::max<u64>(2, strtoull(s, nullptr, 0));
+    E->account_cap = pow2_at_least(std::max<u64>(load * config->accounts_max, 1024));
     // The index is sized for 2x the log so tombstones of withdrawn speculative inserts leave room.
     E->xlog_cap = std::max<u64>(config->transfers_max, 1024);
     E->xidx_cap = pow2_at_least(std::max<u64>(2 * E->xlog_cap, 2048));
@@ -488,7 +493,8 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         if ((st = prof_end(E, &pp))) return st;
         if (P.legs) {
             if ((st = prof_begin(E, &pp, K_APPLY))) return st;
-            hipLaunchKernelGGL(tb_apply_legs, dim3(E->leg_buckets), dim3(APPLY_THREADS), 0, E->stream, P);
+            hipLaunchKernelGGL(tb_apply_legs, dim3(E->leg_buckets), dim3(APPLY_THREADS), (4u << E->leg_shift) * 8, E->stream,
+                               P);
             HIPCK(hipGetLastError());
             if ((st = prof_end(E, &pp))) return st;
         }

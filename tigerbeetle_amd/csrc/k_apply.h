@@ -17,7 +17,7 @@
 #include "k_resolve.h"
 
 __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
-    __shared__ u64 s_acc[LEG_SLOTS_MAX * 4];        // per (slot, field) sum
+    extern __shared__ u64 s_acc[];                  // [4 << leg_shift] per (slot, field) sum (dynamic)
     __shared__ u32 s_start[LEG_PREPARES_MAX];       // the bucket's first leg in each prepare
     __shared__ u32 s_pref[LEG_PREPARES_MAX + 1];    // exclusive prefix of the segment lengths
     __shared__ u32 s_wave[APPLY_THREADS / 64];

@@ -121,21 +121,29 @@ __device__ static inline void tb_apply_transfer(const PassArgs& P, u32 pe, u32 i
 // runs in LDS (s_perm: sorted position -> event << 1 | side, 2 B per leg) and the grouped copy is
 // stored in order, coalesced (scattering the words straight to their sorted places cost 4x the
 // whole sort: partial-line stores).
+// Per-bucket leg counter of a prepare: 16 bits each, two per LDS word (a prepare has at most
+// 16382 legs), so 4096 buckets fit in 8 KB.  Returns the counter's previous value.
+__device__ static inline u32 tb_hist16_inc(u32* s_hist, u32 bucket) {
+    const u32 sh = 16 * (bucket & 1);
+    return (atomicAdd(&s_hist[bucket >> 1], 1u << sh) >> sh) & 0xFFFF;
+}
+
 __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 L, u32 legmask, u32* s_hist,
                                            u16* s_perm, u32* s_wave) {
     if (P.ablate & ABL_LEG_WORK) return;
     __syncthreads();  // every count is in; s_perm's LDS is free
-    tb_block_scan_lds(s_hist, P.leg_buckets, s_wave);
-    const u32 nlegs = s_hist[P.leg_buckets];
+    tb_block_scan_lds((u16*)s_hist, P.leg_buckets, s_wave);
+    const u16* h = (const u16*)s_hist;
+    const u32 nlegs = h[P.leg_buckets];
     u32* row = P.leg_off + (u64)blockIdx.x * (P.leg_buckets + 1);
-    for (u32 k = threadIdx.x; k <= P.leg_buckets; k += blockDim.x) row[k] = s_hist[k];
+    for (u32 k = threadIdx.x; k <= P.leg_buckets; k += blockDim.x) row[k] = h[k];
     __syncthreads();  // the row is read before the starts advance as cursors
     for (u32 c = 0; c < L; c += blockDim.x) {
         if (!((legmask >> (c / blockDim.x)) & 1)) continue;
         const u32 i = c + threadIdx.x;
         const u32 drs = P.dr[pbase + i], crs = P.cr[pbase + i];
-        s_perm[atomicAdd(&s_hist[drs >> P.leg_shift], 1u)] = (u16)(i << 1);
-        s_perm[atomicAdd(&s_hist[crs >> P.leg_shift], 1u)] = (u16)((i << 1) | 1);
+        s_perm[tb_hist16_inc(s_hist, drs >> P.leg_shift)] = (u16)(i << 1);
+        s_perm[tb_hist16_inc(s_hist, crs >> P.leg_shift)] = (u16)((i << 1) | 1);
     }
     __syncthreads();
     if (P.ablate & ABL_LEG_STORES) return;
@@ -198,7 +206,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     __shared__ u64 s_tsmax[RESOLVE_THREADS / 64];
     __shared__ u32 s_applied;
     __shared__ u32 s_failed;  // non-ok final results of independent events
-    __shared__ u32 s_hist[OP == OP_CREATE_TRANSFERS ? LEG_BUCKETS_MAX + 1 : 1];  // legs per bucket
+    __shared__ u32 s_hist[OP == OP_CREATE_TRANSFERS ? LEG_BUCKETS_MAX / 2 + 1 : 1];  // legs per bucket (u16 pairs)
 
     const Tables& T = P.T;
     const u32 b = P.b0 + blockIdx.x;
@@ -214,7 +222,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     if (OP == OP_CREATE_TRANSFERS) tb_pass_cert(P, S, cert_global, cert64);
     const bool use_legs = OP == OP_CREATE_TRANSFERS && P.legs && cert64;
     if (use_legs) {
-        for (u32 k = threadIdx.x; k < P.leg_buckets; k += RESOLVE_THREADS) s_hist[k] = 0;
+        for (u32 k = threadIdx.x; k <= P.leg_buckets / 2; k += RESOLVE_THREADS) s_hist[k] = 0;
     }
 
     if (threadIdx.x == 0) {
@@ -329,8 +337,8 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                             P.leg_ev[2 * (u64)pe] = ((((u64)(drs & mask) << 2) | pend) << LEG_AMT_BITS) | P.amt[2 * pe];
                             P.leg_ev[2 * (u64)pe + 1] = ((((u64)(crs & mask) << 2) | 2 | pend) << LEG_AMT_BITS) | P.amt[2 * pe];
                             if (!(P.ablate & ABL_LEG_WORK)) {
-                                atomicAdd(&s_hist[drs >> P.leg_shift], 1u);
-                                atomicAdd(&s_hist[crs >> P.leg_shift], 1u);
+                                tb_hist16_inc(s_hist, drs >> P.leg_shift);
+                                tb_hist16_inc(s_hist, crs >> P.leg_shift);
                             }
                             legmask |= 1u << (c / RESOLVE_THREADS);
                         } else {

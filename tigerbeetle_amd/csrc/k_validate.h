@@ -216,10 +216,15 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     const u64 cpos = tb_hash_id(clo, chi) & T.account_mask;
     const u64 xpos = tb_hash_id(tb_lo(t.id), tb_hi(t.id)) & T.xidx_mask;
     const bool fake = P.ablate & ABL_ACCTS;
-    AccountHot d0 = {}, c0 = {};
+    AccountHot d0 = {}, c0 = {}, d1 = {}, c1 = {};
+    const bool pair = P.ablate & EXP_PAIR;
     if (!fake) {
         d0 = T.acct_hot[dpos];
         c0 = T.acct_hot[cpos];
+        if (pair) {  // the next slot too: no dependent second probe on a displaced entry
+            d1 = T.acct_hot[(dpos + 1) & T.account_mask];
+            c1 = T.acct_hot[(cpos + 1) & T.account_mask];
+        }
     }
     u64 x0 = ~0ULL;
     if (!(P.ablate & (ABL_SPEC | ABL_CAS))) {
@@ -230,8 +235,8 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
         }
     }
     AccountHot dr = {}, cr = {};
-    const u32 drs = fake ? (u32)(dlo & 1023) : tb_account_find_from(T, dlo, dhi, dpos, d0, &dr);
-    const u32 crs = fake ? (u32)(clo & 1023) : tb_account_find_from(T, clo, chi, cpos, c0, &cr);
+    const u32 drs = fake ? (u32)(dlo & 1023) : tb_account_find_from(T, dlo, dhi, dpos, d0, &dr, pair ? &d1 : nullptr);
+    const u32 crs = fake ? (u32)(clo & 1023) : tb_account_find_from(T, clo, chi, cpos, c0, &cr, pair ? &c1 : nullptr);
     if (drs == TB_NOT_FOUND) return CT_DEBIT_ACCOUNT_NOT_FOUND;
     if (crs == TB_NOT_FOUND) return CT_CREDIT_ACCOUNT_NOT_FOUND;
     if (!(ts > dr.timestamp) || !(ts > cr.timestamp)) return TB_CODE_PANIC;  // :817-818

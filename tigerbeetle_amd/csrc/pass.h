@@ -89,13 +89,14 @@ enum : u32 { CERT_EXT_U128 = 1, CERT_EXT_U64 = 2 };
 // workgroup's LDS.
 #define LEG_SLOTS_MAX 1024
 #define LEG_BUCKETS_PREF 2048
-#define LEG_BUCKETS_MAX 2048  // keeps tb_resolve's LDS under 80 KB: two workgroups per CU
+#define LEG_BUCKETS_MAX 4096  // u16 counters: 8 KB of tb_resolve's LDS (under 80 KB: two workgroups per CU)
 #define LEG_PREPARES_MAX 1024
 #define APPLY_THREADS 256
 // Leg word: ((slot within its bucket) << 2 | balance field (BAL_OFF / 16)) << LEG_AMT_BITS | amount.
 // An amount of 2^LEG_AMT_BITS or more is applied by the resolve kernel with an atomic instead.
-#define LEG_AMT_BITS 52
+#define LEG_AMT_BITS 52  // leaves 12 bits: slot-in-bucket (<= 10, LEG_SLOTS_MAX) + field (2)
 #define LEG_AMT_MASK ((1ULL << LEG_AMT_BITS) - 1)
+static_assert((1u << (64 - LEG_AMT_BITS - 2)) >= LEG_SLOTS_MAX, "leg word: slot-in-bucket field too narrow");
 
 // Timestamp of event i of batch b (execute, state_machine.zig:645).  A routed event carries the
 // timestamp its source assigned (the source answered timestamp_must_be_zero itself and never
@@ -106,7 +107,7 @@ __device__ static inline u64 tb_event_ts(const PassArgs& P, u32 b, u64 boff, u32
 
 enum : u32 { ABL_DEDUP = 1, ABL_SPEC = 2, ABL_ACCTS = 4, ABL_XFIND = 8, ABL_STAGE = 16, ABL_RECORD = 32, ABL_CAS = 64, EXP_NT = 128,
              ABL_LEGS = 256, ABL_LEG_STORES = 512, ABL_LEG_WORK = 1024,  // ABL_LEG_*: timing only (wrong balances)
-             ABL_FLOW = 2048 };  // sequential replay instead of the parallel flow path (exact either way)
+             ABL_FLOW = 2048, EXP_PAIR = 4096 };  // sequential replay instead of the parallel flow path (exact either way)
 
 // Batch of a call-relative event index: binary search over batch_off[lo..hi) (off[lo] <= e < off[hi]).
 __device__ static inline u32 tb_batch_search(const u64* off, u32 lo, u32 hi, u64 e) {
@@ -233,8 +234,10 @@ __device__ static inline u32 tb_block_excl_sum(u32 v, u32* s_wave, u32* total) {
     return before + x - v;
 }
 
-// In-place exclusive scan of s[0, n) in LDS, s[n] = the total.  Every thread calls it.
-__device__ static inline void tb_block_scan_lds(u32* s, u32 n, u32* s_wave) {
+// In-place exclusive scan of s[0, n) in LDS, s[n] = the total (which must fit T).  Every thread
+// calls it.
+template <typename T>
+__device__ static inline void tb_block_scan_lds(T* s, u32 n, u32* s_wave) {
     const u32 per = (n + blockDim.x - 1) / blockDim.x;
     const u32 k0 = min(n, threadIdx.x * per), k1 = min(n, k0 + per);
     u32 local = 0;
@@ -243,9 +246,9 @@ __device__ static inline void tb_block_scan_lds(u32* s, u32 n, u32* s_wave) {
     u32 run = tb_block_excl_sum(local, s_wave, &total);
     for (u32 k = k0; k < k1; k++) {
         const u32 c = s[k];
-        s[k] = run;
+        s[k] = (T)run;
         run += c;
     }
-    if (threadIdx.x == 0) s[n] = total;
+    if (threadIdx.x == 0) s[n] = (T)total;
     __syncthreads();
 }
