@@ -220,14 +220,23 @@ def main():
                               limit_permille=wl["limit_permille"])
     engine.sync()
 
+    # Warmup steps time every kernel (the per-kernel breakdown); timed steps time only the kernel
+    # the roofline is quoted on (validate) and whole passes (batch latency): every HIP event pair on
+    # the stream costs a little (all six kernels timed: ~9 % of a step).
     step_ms = []
     t_cursor = t_end
+    breakdown = None
+    if args.warmup:
+        engine.profile_mask(engine.PROF_ALL)
     for step in range(args.warmup + args.steps):
         timed = step >= args.warmup
         engine.reset_transfers()
         ts, t_cursor = timestamps(xfer_lens, t_cursor + 10, wl["gap_every"])
         if timed and step == args.warmup:
+            if args.warmup:
+                breakdown = engine.stats()
             engine.reset_stats()
+            engine.profile_mask(engine.PROF_VALIDATE | engine.PROF_PASS | engine.PROF_REPLAY)
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -263,7 +272,7 @@ def main():
     # -- roofline: dominant kernel -----------------------------------------------------------
     per_launch_transfers = args.transfers / max(1, stats["launches_validate"] / max(1, args.steps))
     u_over_t = expected_unique(args.accounts, 2 * pass_events) / pass_events
-    roof = roofline(stats, u_over_t, per_launch_transfers, args, total_ms)
+    roof = roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown)
 
     # -- CPU baseline + bit-exact sample parity (rank 0, N=1 only) ---------------------------
     cpu = None
@@ -439,34 +448,43 @@ def run_sharded(args, world, rank, local_rank):
     dist.destroy_process_group()
 
 
-def roofline(stats, u_over_t, per_launch_transfers, args, total_ms):
-    kernels = {
-        "tb_transfers_validate": (stats["ms_validate"], stats["launches_validate"]),
-        "tb_resolve<129>": (stats["ms_resolve"], stats["launches_resolve"]),
-        # the ordered fallback of create_transfers passes: tb_flow (or tb_replay<129> when disabled)
-        "tb_flow": (stats["ms_replay"], stats["launches_replay"]),
-        "tb_apply_legs": (stats["ms_apply"], stats["launches_apply"]),
-    }
+def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=None):
+    """The dominant kernel of the timed steps against the HBM peak; `kernels` = every kernel's mean
+    launch time (from the warmup steps when given: the timed steps time only validate, replay/flow
+    and whole passes)."""
+    def kernel_table(stats):
+        return {
+            "tb_transfers_validate": (stats["ms_validate"], stats["launches_validate"]),
+            "tb_resolve<129>": (stats["ms_resolve"], stats["launches_resolve"]),
+            # the ordered fallback of create_transfers passes: tb_flow (or tb_replay<129> when disabled)
+            "tb_flow": (stats["ms_replay"], stats["launches_replay"]),
+            "memset(dedup,sums)": (stats["ms_clear"], stats["launches_clear"]),
+            "tb_apply_legs": (stats["ms_apply"], stats["launches_apply"]),
+        }
+
+    kernels = kernel_table(stats)
     dom = max(kernels, key=lambda k: kernels[k][0])
     ms_dom, n_dom = kernels[dom]
     # SURVEY.md §8(d): B = 296 + 256·U/T per transfer, split by where the work happens (DESIGN.md §4):
     # validate reads the event (128), probes + claims the id (32), writes the record (128) and reads
     # each touched account once (128·U/T); resolve writes the result slot (8) and each touched
     # account back (128·U/T) — or, with the legs path, tb_apply_legs writes the accounts back.
-    legs = stats["launches_apply"] > 0
+    legs = (breakdown or stats)["launches_apply"] > 0
     b_validate = 288 + 128 * u_over_t
     b_resolve = 8 + (0 if legs else 128 * u_over_t)
     b_apply = 128 * u_over_t if legs else 0.0
     alg_bytes = {"tb_transfers_validate": b_validate, "tb_resolve<129>": b_resolve, "tb_flow": 0.0,
+                 "memset(dedup,sums)": 0.0,
                  "tb_apply_legs": b_apply}[dom] * per_launch_transfers
     if not n_dom:
         return None
     avg_s = ms_dom / n_dom / 1e3
     achieved = alg_bytes / avg_s / 1e9
-    per_kernel = {k: {"launches": int(n), "avg_launch_ms": round(ms / n, 4)} for k, (ms, n) in kernels.items() if n}
+    src = kernel_table(breakdown) if breakdown else kernels
+    per_kernel = {k: {"launches": int(n), "avg_launch_ms": round(ms / n, 4)} for k, (ms, n) in src.items() if n}
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc(dom), "kernel": dom,
-            "kernels": per_kernel,
+            "kernels": per_kernel, "kernels_timed_in": "warmup steps (every kernel)" if breakdown else "timed steps",
             "avg_launch_ms": round(ms_dom / n_dom, 4), "alg_bytes_per_transfer": round(alg_bytes / per_launch_transfers, 1),
             "path_bytes_per_transfer": round(296 + 256 * u_over_t, 1),
             "path_achieved_GBs": round((296 + 256 * u_over_t) * args.transfers * args.steps / (total_ms / 1e3) / 1e9, 1)}

@@ -39,6 +39,13 @@ int tbgpu_bench_reset_transfers(tbgpu_t* engine);
  * a prepare's reply is available when its pass completes, so this is the batch latency. */
 int tbgpu_bench_pass_latencies(tbgpu_t* engine, double* out_ms, uint64_t cap, uint64_t* count);
 
+/* Which kernels TBGPU_CONFIG_PROFILE times with HIP events (every event pair on the stream costs
+ * a little): bit 1 << kind, kinds 0 validate, 1 resolve, 2 replay/flow, 3 clears, 4 whole pass,
+ * 5 apply_legs.  Default: all. */
+enum { TBGPU_PROF_VALIDATE = 1, TBGPU_PROF_RESOLVE = 2, TBGPU_PROF_REPLAY = 4, TBGPU_PROF_CLEAR = 8,
+       TBGPU_PROF_PASS = 16, TBGPU_PROF_APPLY = 32, TBGPU_PROF_ALL = 63 };
+int tbgpu_bench_profile_mask(tbgpu_t* engine, uint32_t mask);
+
 /* Device memory helpers for callers without a device allocator (ctypes users). */
 int tbgpu_device_alloc(tbgpu_t* engine, uint64_t bytes, void** out);
 int tbgpu_device_free(tbgpu_t* engine, void* ptr);

@@ -101,6 +101,7 @@ SIGNATURES = [
     ("tbgpu_bench_generate_transfers", ctypes.c_int, [_P, _P, _U64, _U64, ctypes.POINTER(tbgpu_workload)]),
     ("tbgpu_bench_reset_transfers", ctypes.c_int, [_P]),
     ("tbgpu_bench_pass_latencies", ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
+    ("tbgpu_bench_profile_mask", ctypes.c_int, [_P, _U32]),
     ("tbgpu_device_alloc", ctypes.c_int, [_P, _U64, ctypes.POINTER(_P)]),
     ("tbgpu_device_free", ctypes.c_int, [_P, _P]),
     ("tbgpu_copy_to_host", ctypes.c_int, [_P, _P, _P, _U64]),

@@ -111,6 +111,7 @@ struct tbgpu {
     bool pending = false;    // an async call was enqueued and not yet synced
 
     bool profile = false;
+    u32 prof_mask = ~0u;  // kernels timed when profiling (1 << K_*; tbgpu_bench_profile_mask)
     u32 ablate = 0;
     std::vector<hipEvent_t> event_pool;
     size_t event_next = 0;
@@ -143,7 +144,8 @@ static int ev_get(tbgpu* E, hipEvent_t* out) {
 }
 
 static int prof_begin(tbgpu* E, ProfilePair* p, int kind) {
-    if (!E->profile) return 0;
+    p->kind = -1;
+    if (!E->profile || !(E->prof_mask & (1u << kind))) return 0;
     p->kind = kind;
     int st = ev_get(E, &p->a);
     if (st) return st;
@@ -154,7 +156,7 @@ static int prof_begin(tbgpu* E, ProfilePair* p, int kind) {
 }
 
 static int prof_end(tbgpu* E, ProfilePair* p) {
-    if (!E->profile) return 0;
+    if (!E->profile || p->kind < 0) return 0;
     HIPCK(hipEventRecord(p->b, E->stream));
     E->prof.push_back(*p);
     return 0;
@@ -906,6 +908,11 @@ extern "C" int tbgpu_bench_generate_transfers(tbgpu_t* E, void* out_dev, uint64_
     hipLaunchKernelGGL(tb_gen_transfers, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, E->stream,
                        (u8*)out_dev, count, workload_params(w, first));
     HIPCK(hipGetLastError());
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_bench_profile_mask(tbgpu_t* E, uint32_t mask) {
+    E->prof_mask = mask;
     return TBGPU_STATUS_OK;
 }
 

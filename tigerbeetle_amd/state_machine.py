@@ -147,6 +147,12 @@ class Engine:
     def reset_stats(self):
         self.lib.tbgpu_reset_stats(self.h)
 
+    PROF_VALIDATE, PROF_RESOLVE, PROF_REPLAY, PROF_CLEAR, PROF_PASS, PROF_APPLY, PROF_ALL = 1, 2, 4, 8, 16, 32, 63
+
+    def profile_mask(self, mask):
+        """Kernels timed with HIP events when profiling (include/tbgpu_bench.h)."""
+        _lib.check(self.lib.tbgpu_bench_profile_mask(self.h, mask))
+
     # -- multi-GPU primitives (include/tbgpu_shard.h; driven by tigerbeetle_amd.sharded) -------
     def route_init(self, world, events_max):
         _lib.check(self.lib.tbgpu_route_init(self.h, world, events_max))
