@@ -180,11 +180,10 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_route_scatter(RouteArgs A, u
     const u64 boff = A.batch_off[b];
     const u32 L = (u32)(A.batch_off[b + 1] - boff);
     slot[e] = pos;
-    u8* src = stage + threadIdx.x * STAGE_STRIDE;
-    *(u64*)(src + 120) = A.batch_ts[b] - L + 1 + (e - boff);  // execute, state_machine.zig:645
+    *(u64*)(stage + tb_stage_off(threadIdx.x, 7) + 8) = A.batch_ts[b] - L + 1 + (e - boff);  // execute, :645
     u32x4* dst = (u32x4*)(send_events + (u64)pos * 128);
 #pragma unroll
-    for (int k = 0; k < 8; k++) dst[k] = *(const u32x4*)(src + k * 16);
+    for (u32 k = 0; k < 8; k++) dst[k] = *(const u32x4*)(stage + tb_stage_off(threadIdx.x, k));
 }
 
 // Per-prepare sparse replies from the codes that came back (in send order): ascending index,

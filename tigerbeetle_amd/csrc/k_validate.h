@@ -323,7 +323,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
         P.kpid[pe] = s.kpid;
         if (code != R_OK) s.contrib = 0;
         // The record (create_transfer :870) is the event as staged, with its timestamp.
-        if (s.rec_ts) *(u64*)(stage + threadIdx.x * STAGE_STRIDE + 120) = s.rec_ts;
+        if (s.rec_ts) *(u64*)(stage + tb_stage_off(threadIdx.x, 7) + 8) = s.rec_ts;  // timestamp @120
     }
     // Block partial of S (saturating), then one sharded atomic per block.
     const u128 w = tb_wave_sum_u128(s.contrib);
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
         const u32 c = threadIdx.x + r * VALIDATE_THREADS;
         const u32 ev = c >> 3, part = c & 7;
         if ((s_rec[ev >> 6] >> (ev & 63)) & 1) {
-            const u32x4 v = *(const u32x4*)(stage + ev * STAGE_STRIDE + part * 16);
+            const u32x4 v = *(const u32x4*)(stage + tb_stage_off(ev, part));
             u32x4* dst = (u32x4*)&P.T.xlog[P.log_base + tile0 + ev] + part;
             if (P.ablate & EXP_NT) __builtin_nontemporal_store(v, dst);
             else *dst = v;

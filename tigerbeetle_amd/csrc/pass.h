@@ -129,9 +129,11 @@ __device__ static inline u32 tb_tile_batch(const PassArgs& P, u64 e_first, u32 c
     return tb_batch_search(P.batch_off, s_range[0], s_range[1], e);
 }
 
-// Stage VALIDATE_THREADS 128-byte events through LDS with 16-byte coalesced loads; row stride
-// 144 B so the per-lane ds_read_b128 of one record is bank-conflict free.
-#define STAGE_STRIDE 144
+// Stage VALIDATE_THREADS 128-byte events through LDS with 16-byte coalesced loads.  Rows are 128 B
+// with the 16-B chunks of row r XOR-swizzled by r & 7, so the per-lane ds_read_b128 of one record
+// spreads over the banks without padding (32 KB per 256 events: five validate workgroups per CU).
+#define STAGE_STRIDE 128
+__device__ static inline u32 tb_stage_off(u32 row, u32 chunk) { return row * STAGE_STRIDE + ((chunk ^ (row & 7)) << 4); }
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ static inline void tb_stage_events(const u8* src, u32 count, u8* lds, bool nt = false) {
     const u32 t = threadIdx.x;
@@ -142,7 +144,7 @@ __device__ static inline void tb_stage_events(const u8* src, u32 count, u8* lds,
         if (ev < count) {
             const u32x4* g = (const u32x4*)(src + (u64)c * 16);
             const u32x4 v = nt ? __builtin_nontemporal_load(g) : *g;
-            *(u32x4*)(lds + ev * STAGE_STRIDE + part * 16) = v;
+            *(u32x4*)(lds + tb_stage_off(ev, part)) = v;
         }
     }
     __syncthreads();
@@ -151,9 +153,8 @@ __device__ static inline void tb_stage_events(const u8* src, u32 count, u8* lds,
 template <typename R>
 __device__ static inline R tb_read_staged(const u8* lds) {
     R r;
-    const u8* p = lds + threadIdx.x * STAGE_STRIDE;
 #pragma unroll
-    for (int k = 0; k < 8; k++) ((uint4*)&r)[k] = *(const uint4*)(p + k * 16);
+    for (u32 k = 0; k < 8; k++) ((uint4*)&r)[k] = *(const uint4*)(lds + tb_stage_off(threadIdx.x, k));
     return r;
 }
 
