@@ -216,15 +216,10 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     const u64 cpos = tb_hash_id(clo, chi) & T.account_mask;
     const u64 xpos = tb_hash_id(tb_lo(t.id), tb_hi(t.id)) & T.xidx_mask;
     const bool fake = P.ablate & ABL_ACCTS;
-    AccountHot d0 = {}, c0 = {}, d1 = {}, c1 = {};
-    const bool pair = P.ablate & EXP_PAIR;
+    AccountHot d0 = {}, c0 = {};
     if (!fake) {
         d0 = T.acct_hot[dpos];
         c0 = T.acct_hot[cpos];
-        if (pair) {  // the next slot too: no dependent second probe on a displaced entry
-            d1 = T.acct_hot[(dpos + 1) & T.account_mask];
-            c1 = T.acct_hot[(cpos + 1) & T.account_mask];
-        }
     }
     u64 x0 = ~0ULL;
     if (!(P.ablate & (ABL_SPEC | ABL_CAS))) {
@@ -235,8 +230,8 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
         }
     }
     AccountHot dr = {}, cr = {};
-    const u32 drs = fake ? (u32)(dlo & 1023) : tb_account_find_from(T, dlo, dhi, dpos, d0, &dr, pair ? &d1 : nullptr);
-    const u32 crs = fake ? (u32)(clo & 1023) : tb_account_find_from(T, clo, chi, cpos, c0, &cr, pair ? &c1 : nullptr);
+    const u32 drs = fake ? (u32)(dlo & 1023) : tb_account_find_from(T, dlo, dhi, dpos, d0, &dr);
+    const u32 crs = fake ? (u32)(clo & 1023) : tb_account_find_from(T, clo, chi, cpos, c0, &cr);
     if (drs == TB_NOT_FOUND) return CT_DEBIT_ACCOUNT_NOT_FOUND;
     if (crs == TB_NOT_FOUND) return CT_CREDIT_ACCOUNT_NOT_FOUND;
     if (!(ts > dr.timestamp) || !(ts > cr.timestamp)) return TB_CODE_PANIC;  // :817-818
@@ -276,11 +271,11 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
 }
 
 // Kernel 1 (create_transfers).
+// LDS is the 32 KB stage only (five workgroups per CU): the batch search runs on the scalar unit,
+// each wave stores its own records, and the block's S partials go through the stage rows their
+// waves have finished with.
 __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassArgs P) {
     __shared__ __attribute__((aligned(16))) u8 stage[VALIDATE_THREADS * STAGE_STRIDE];
-    __shared__ u64 s_sum[2 * (VALIDATE_THREADS / 64)];
-    __shared__ u64 s_rec[VALIDATE_THREADS / 64];  // per wave: lanes whose record is their staged event
-    __shared__ u32 s_range[2];
 
     const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
     const u32 count = min((u32)VALIDATE_THREADS, P.n - tile0);
@@ -288,7 +283,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
 
     const u32 pe = tile0 + threadIdx.x;  // pass-relative event
     const u64 e = P.e0 + pe;
-    const u32 b = tb_tile_batch(P, P.e0 + tile0, count, e, s_range);
+    const u32 b = tb_wave_batch(P.batch_off, P.b0, P.b1, P.e0 + tile0, count, e);
     TransferScratch s;
     if (threadIdx.x < count) {
         Transfer t = tb_read_staged<Transfer>(stage);
@@ -325,31 +320,41 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
         // The record (create_transfer :870) is the event as staged, with its timestamp.
         if (s.rec_ts) *(u64*)(stage + tb_stage_off(threadIdx.x, 7) + 8) = s.rec_ts;  // timestamp @120
     }
-    // Block partial of S (saturating), then one sharded atomic per block.
     const u128 w = tb_wave_sum_u128(s.contrib);
     const u64 rec = __ballot(s.rec_ts != 0);
-    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) {
-        s_sum[2 * wave] = tb_lo(w);
-        s_sum[2 * wave + 1] = tb_hi(w);
-        s_rec[wave] = rec;
-    }
-    __syncthreads();
-    // Records of the tile: consecutive lanes store consecutive 16-B chunks of consecutive records.
+    const u32 lane = threadIdx.x & 63, w0 = threadIdx.x & ~63u;
+    // The wave's records (its own 64 stage rows): consecutive lanes store consecutive 16-B chunks
+    // of consecutive records.  LDS operations of one wave complete in order, so the timestamps
+    // written above are visible here without a workgroup barrier.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (u32 r = 0; r < 8; r++) {
-        const u32 c = threadIdx.x + r * VALIDATE_THREADS;
-        const u32 ev = c >> 3, part = c & 7;
-        if ((s_rec[ev >> 6] >> (ev & 63)) & 1) {
-            const u32x4 v = *(const u32x4*)(stage + tb_stage_off(ev, part));
-            u32x4* dst = (u32x4*)&P.T.xlog[P.log_base + tile0 + ev] + part;
+        const u32 c = lane + r * 64;
+        const u32 row = c >> 3, part = c & 7;
+        if ((rec >> row) & 1) {
+            const u32x4 v = *(const u32x4*)(stage + tb_stage_off(w0 + row, part));
+            u32x4* dst = (u32x4*)&P.T.xlog[P.log_base + tile0 + w0 + row] + part;
             if (P.ablate & EXP_NT) __builtin_nontemporal_store(v, dst);
             else *dst = v;
         }
     }
+    // Block partial of S (saturating), then one sharded atomic per block.  Each wave parks its
+    // partial in the first row of its own stage rows, which it has finished reading.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+        *(u64*)(stage + w0 * STAGE_STRIDE) = tb_lo(w);
+        *(u64*)(stage + w0 * STAGE_STRIDE + 8) = tb_hi(w);
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
         u128 total = 0;
-        for (u32 k = 0; k < VALIDATE_THREADS / 64; k++) total = tb_sat_add(total, tb_u128(s_sum[2 * k], s_sum[2 * k + 1]));
+        for (u32 k = 0; k < VALIDATE_THREADS / 64; k++) {
+            const u8* q = stage + k * 64 * STAGE_STRIDE;
+            total = tb_sat_add(total, tb_u128(*(const u64*)q, *(const u64*)(q + 8)));
+        }
         tb_sum_publish(P, total);
     }
 }
@@ -386,13 +391,12 @@ __device__ static inline u32 tb_account_stateless(const Account& a) {
 // Kernel 1 (create_accounts).
 __global__ __launch_bounds__(VALIDATE_THREADS) void tb_accounts_validate(PassArgs P) {
     __shared__ __attribute__((aligned(16))) u8 stage[VALIDATE_THREADS * STAGE_STRIDE];
-    __shared__ u32 s_range[2];
     const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
     const u32 count = min((u32)VALIDATE_THREADS, P.n - tile0);
     tb_stage_events(P.events + (P.e0 + tile0) * 128, count, stage);
     const u32 pe = tile0 + threadIdx.x;
     const u64 e = P.e0 + pe;
-    const u32 b = tb_tile_batch(P, P.e0 + tile0, count, e, s_range);
+    const u32 b = tb_wave_batch(P.batch_off, P.b0, P.b1, P.e0 + tile0, count, e);
     if (threadIdx.x >= count) return;
 
     const Account a = tb_read_staged<Account>(stage);

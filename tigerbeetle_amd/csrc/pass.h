@@ -107,7 +107,7 @@ __device__ static inline u64 tb_event_ts(const PassArgs& P, u32 b, u64 boff, u32
 
 enum : u32 { ABL_DEDUP = 1, ABL_SPEC = 2, ABL_ACCTS = 4, ABL_XFIND = 8, ABL_STAGE = 16, ABL_RECORD = 32, ABL_CAS = 64, EXP_NT = 128,
              ABL_LEGS = 256, ABL_LEG_STORES = 512, ABL_LEG_WORK = 1024,  // ABL_LEG_*: timing only (wrong balances)
-             ABL_FLOW = 2048, EXP_PAIR = 4096 };  // sequential replay instead of the parallel flow path (exact either way)
+             ABL_FLOW = 2048 };  // sequential replay instead of the parallel flow path (exact either way)
 
 // Batch of a call-relative event index: binary search over batch_off[lo..hi) (off[lo] <= e < off[hi]).
 __device__ static inline u32 tb_batch_search(const u64* off, u32 lo, u32 hi, u64 e) {
@@ -127,6 +127,18 @@ __device__ static inline u32 tb_tile_batch(const PassArgs& P, u64 e_first, u32 c
     }
     __syncthreads();
     return tb_batch_search(P.batch_off, s_range[0], s_range[1], e);
+}
+
+// Batch of every event of a wave: the wave's first and last events are wave-uniform, so their
+// searches run on the scalar unit (s_load, no LDS, no barrier); each lane then searches only that
+// (usually one- or two-batch) range.  `count` = events of the workgroup's tile.
+__device__ static inline u32 tb_wave_batch(const u64* off, u32 lo, u32 hi, u64 tile_e0, u32 count, u64 e) {
+    const u32 w0 = (u32)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 64;
+    if (w0 >= count) return lo;
+    const u64 first = tile_e0 + w0, last = tile_e0 + min(count, w0 + 64) - 1;
+    const u32 a = tb_batch_search(off, lo, hi, first);
+    const u32 z = tb_batch_search(off, a, hi, last) + 1;
+    return tb_batch_search(off, a, z, e);
 }
 
 // Stage VALIDATE_THREADS 128-byte events through LDS with 16-byte coalesced loads.  Rows are 128 B

@@ -259,21 +259,13 @@ __device__ static inline u32 tb_account_find(const Tables& T, u64 lo, u64 hi) {
 // Continue an account probe whose first entry (at `pos`) was already loaded; *hit = the matching
 // entry (no second load of it).
 __device__ static inline u32 tb_account_find_from(const Tables& T, u64 lo, u64 hi, u64 pos, const AccountHot& first,
-                                                  AccountHot* hit, const AccountHot* second = nullptr) {
+                                                  AccountHot* hit) {
     if (first.id_lo == lo && first.id_hi == hi) {
         *hit = first;
         return (u32)pos;
     }
     if ((first.id_lo | first.id_hi) == 0 || tb_id_reserved(lo, hi)) return TB_NOT_FOUND;
     pos = (pos + 1) & T.account_mask;
-    if (second) {  // the caller loaded the next slot together with the first
-        if (second->id_lo == lo && second->id_hi == hi) {
-            *hit = *second;
-            return (u32)pos;
-        }
-        if ((second->id_lo | second->id_hi) == 0) return TB_NOT_FOUND;
-        pos = (pos + 1) & T.account_mask;
-    }
     for (u64 n = 1; n <= T.account_mask; n++) {
         const AccountHot h = T.acct_hot[pos];
         if (h.id_lo == lo && h.id_hi == hi) {
