@@ -458,7 +458,7 @@ def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=No
             "tb_resolve<129>": (stats["ms_resolve"], stats["launches_resolve"]),
             # the ordered fallback of create_transfers passes: tb_flow (or tb_replay<129> when disabled)
             "tb_flow": (stats["ms_replay"], stats["launches_replay"]),
-            "memset(dedup,sums)": (stats["ms_clear"], stats["launches_clear"]),
+            "tb_pass_clear": (stats["ms_clear"], stats["launches_clear"]),
             "tb_apply_legs": (stats["ms_apply"], stats["launches_apply"]),
         }
 
@@ -474,7 +474,7 @@ def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=No
     b_resolve = 8 + (0 if legs else 128 * u_over_t)
     b_apply = 128 * u_over_t if legs else 0.0
     alg_bytes = {"tb_transfers_validate": b_validate, "tb_resolve<129>": b_resolve, "tb_flow": 0.0,
-                 "memset(dedup,sums)": 0.0,
+                 "tb_pass_clear": 0.0,
                  "tb_apply_legs": b_apply}[dom] * per_launch_transfers
     if not n_dom:
         return None

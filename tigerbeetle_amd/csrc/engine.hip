@@ -106,6 +106,7 @@ struct tbgpu {
     u32* d_status = nullptr;
 
     u32 epoch = 0;
+    bool dedup_force = true;  // the next pass clears the whole dedup set (init, reset, epoch wrap)
     u64 commit_ts = 0;       // exact after every synchronous call
     u64 last_batch_ts = 0;   // upper bound for async calls
     bool pending = false;    // an async call was enqueued and not yet synced
@@ -189,6 +190,7 @@ static int engine_clear(tbgpu* E) {
     HIPCK(hipMemsetAsync(E->g, 0, sizeof(Globals), E->stream));
     HIPCK(hipStreamSynchronize(E->stream));
     E->epoch = 0;
+    E->dedup_force = true;
     E->commit_ts = 0;
     E->last_batch_ts = 0;
     E->pending = false;
@@ -421,6 +423,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         if (E->epoch == 0) {  // wrapped: clear stale balancing marks
             HIPCK(hipMemsetAsync(E->T.account_mark, 0, E->account_cap * sizeof(u32), E->stream));
             E->epoch = 1;
+            E->dedup_force = true;
         }
         PassArgs P{};
         P.op = op;
@@ -470,8 +473,10 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         if (st) return st;
         ProfilePair pp;
         if ((st = prof_begin(E, &pp, K_CLEAR))) return st;
-        HIPCK(hipMemsetAsync(E->dedup, 0, (P.dedup_mask + 1) * 8, E->stream));
-        HIPCK(hipMemsetAsync(E->sum_shards, 0, SUM_WORDS * 8, E->stream));
+        hipLaunchKernelGGL(tb_pass_clear, dim3(1024), dim3(256), 0, E->stream, E->dedup, E->dedup_cap, E->sum_shards,
+                           E->g, E->epoch, E->dedup_force ? 1u : 0u);
+        HIPCK(hipGetLastError());
+        E->dedup_force = false;
         if ((st = prof_end(E, &pp))) return st;
 
         if (n > 0) {

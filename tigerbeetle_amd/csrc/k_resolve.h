@@ -128,8 +128,10 @@ __device__ static inline u32 tb_hist16_inc(u32* s_hist, u32 bucket) {
     return (atomicAdd(&s_hist[bucket >> 1], 1u << sh) >> sh) & 0xFFFF;
 }
 
-__device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 L, u32 legmask, u32* s_hist,
-                                           u16* s_perm, u32* s_wave) {
+#define RESOLVE_K (BATCH_LDS / RESOLVE_THREADS)  // events per thread of a prepare
+
+__device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 L, u32 legmask, const u32* r_dr,
+                                           const u32* r_cr, u32* s_hist, u16* s_perm, u32* s_wave) {
     if (P.ablate & ABL_LEG_WORK) return;
     __syncthreads();  // every count is in; s_perm's LDS is free
     tb_block_scan_lds((u16*)s_hist, P.leg_buckets, s_wave);
@@ -138,12 +140,12 @@ __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 L, 
     u32* row = P.leg_off + (u64)blockIdx.x * (P.leg_buckets + 1);
     for (u32 k = threadIdx.x; k <= P.leg_buckets; k += blockDim.x) row[k] = h[k];
     __syncthreads();  // the row is read before the starts advance as cursors
-    for (u32 c = 0; c < L; c += blockDim.x) {
-        if (!((legmask >> (c / blockDim.x)) & 1)) continue;
-        const u32 i = c + threadIdx.x;
-        const u32 drs = P.dr[pbase + i], crs = P.cr[pbase + i];
-        s_perm[tb_hist16_inc(s_hist, drs >> P.leg_shift)] = (u16)(i << 1);
-        s_perm[tb_hist16_inc(s_hist, crs >> P.leg_shift)] = (u16)((i << 1) | 1);
+#pragma unroll
+    for (u32 k = 0; k < RESOLVE_K; k++) {
+        if (!((legmask >> k) & 1)) continue;
+        const u32 i = k * RESOLVE_THREADS + threadIdx.x;
+        s_perm[tb_hist16_inc(s_hist, r_dr[k] >> P.leg_shift)] = (u16)(i << 1);
+        s_perm[tb_hist16_inc(s_hist, r_cr[k] >> P.leg_shift)] = (u16)((i << 1) | 1);
     }
     __syncthreads();
     if (P.ablate & ABL_LEG_STORES) return;
@@ -233,14 +235,26 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
             if (P.flow_words) for (u32 k = 0; k < 8; k++) P.flow_words[k] = 0;
         }
     }
-    // a. classify
+    // a. classify.  Each thread owns events tid + k*RESOLVE_THREADS; their scratch words are loaded
+    // for every k before any is used (one memory round trip instead of one per k).
+    u32 r_info[RESOLVE_K];
+    u16 r_fl[RESOLVE_K];
+#pragma unroll
+    for (u32 k = 0; k < RESOLVE_K; k++) {
+        const u32 i = k * RESOLVE_THREADS + threadIdx.x;
+        r_info[k] = i < L ? P.info[pbase + i] : 0u;
+        r_fl[k] = i < L ? P.eflags[pbase + i] : (u16)0;
+    }
     bool local_linked = false, local_dep = false;
-    for (u32 i = threadIdx.x; i < L; i += RESOLVE_THREADS) {
+#pragma unroll
+    for (u32 k = 0; k < RESOLVE_K; k++) {
+        const u32 i = k * RESOLVE_THREADS + threadIdx.x;
+        if (i >= L) continue;
         const u32 pe = pbase + i;
-        const u32 info = P.info[pe];
+        const u32 info = r_info[k];
         const u32 code = info & 0xFF;
         const bool dep = tb_classify<OP>(P, pe, info, code, S, cert_global, any_dup, any_bal, any_pv);
-        const bool linked = P.eflags[pe] & 1;
+        const bool linked = r_fl[k] & 1;
         local_linked |= linked;
         local_dep |= dep;
         s_code[i] = (u8)code;
@@ -284,13 +298,27 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         __syncthreads();
     }
 
-    // Final results, dependent list, apply.
+    // Final results, dependent list, apply.  The account slots and amounts of every event of the
+    // thread are loaded up front as well.
+    u32 r_dr[RESOLVE_K], r_cr[RESOLVE_K];
+    u64 r_amt[RESOLVE_K][2];
+#pragma unroll
+    for (u32 k = 0; k < RESOLVE_K; k++) {
+        const u32 i = k * RESOLVE_THREADS + threadIdx.x;
+        const bool want = OP == OP_CREATE_TRANSFERS && i < L && (r_info[k] & HZ_ACCTS);
+        const u32 pe = pbase + i;
+        r_dr[k] = want ? P.dr[pe] : 0u;
+        r_cr[k] = want ? P.cr[pe] : 0u;
+        r_amt[k][0] = want ? P.amt[2 * pe] : 0ULL;
+        r_amt[k][1] = want ? P.amt[2 * pe + 1] : 0ULL;
+    }
     u64 tsmax = 0;
     u32 ndep = 0;
-    u32 legmask = 0;  // bit k: this thread's event of chunk k contributes two legs
+    u32 legmask = 0;  // bit k: this thread's event k contributes two legs
     u32* dep_out = P.dep_list + pbase;
-    for (u32 c = 0; c < L; c += RESOLVE_THREADS) {
-        const u32 i = c + threadIdx.x;
+#pragma unroll
+    for (u32 k = 0; k < RESOLVE_K; k++) {
+        const u32 i = k * RESOLVE_THREADS + threadIdx.x;
         bool dep = false, eval_ok = false;
         u32 fin = R_OK;
         if (i < L) {
@@ -320,7 +348,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                 eval_ok = code == R_OK;
             }
             const u32 pe = pbase + i;
-            const u32 info = P.info[pe];
+            const u32 info = r_info[k];
             if (!dep) {
                 if (fin == TB_CODE_PANIC) tb_panic(T.g, PANIC_ASSERT);
                 s_code[i] = (u8)fin;
@@ -329,20 +357,19 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                 if (eval_ok) tsmax = ts;  // increasing in i
                 if (fin == R_OK) {
                     if (OP == OP_CREATE_TRANSFERS) {
-                        if (use_legs && !(info & HZ_POSTVOID) && P.amt[2 * pe + 1] == 0 &&
-                            P.amt[2 * pe] <= LEG_AMT_MASK) {
-                            const u32 drs = P.dr[pe], crs = P.cr[pe];
-                            const u64 pend = (P.eflags[pe] & TF_PENDING) ? 0 : 1;  // field: pending / posted
+                        if (use_legs && !(info & HZ_POSTVOID) && r_amt[k][1] == 0 && r_amt[k][0] <= LEG_AMT_MASK) {
+                            const u32 drs = r_dr[k], crs = r_cr[k];
+                            const u64 pend = (r_fl[k] & TF_PENDING) ? 0 : 1;  // field: pending / posted
                             const u32 mask = (1u << P.leg_shift) - 1;
-                            P.leg_ev[2 * (u64)pe] = ((((u64)(drs & mask) << 2) | pend) << LEG_AMT_BITS) | P.amt[2 * pe];
-                            P.leg_ev[2 * (u64)pe + 1] = ((((u64)(crs & mask) << 2) | 2 | pend) << LEG_AMT_BITS) | P.amt[2 * pe];
+                            P.leg_ev[2 * (u64)pe] = ((((u64)(drs & mask) << 2) | pend) << LEG_AMT_BITS) | r_amt[k][0];
+                            P.leg_ev[2 * (u64)pe + 1] = ((((u64)(crs & mask) << 2) | 2 | pend) << LEG_AMT_BITS) | r_amt[k][0];
                             if (!(P.ablate & ABL_LEG_WORK)) {
                                 tb_hist16_inc(s_hist, drs >> P.leg_shift);
                                 tb_hist16_inc(s_hist, crs >> P.leg_shift);
                             }
-                            legmask |= 1u << (c / RESOLVE_THREADS);
+                            legmask |= 1u << k;
                         } else {
-                            tb_apply_transfer(P, pe, info, P.eflags[pe], cert64);
+                            tb_apply_transfer(P, pe, info, r_fl[k], cert64);
                         }
                     } else {
                         tb_apply_account(P, pe, ts);
@@ -385,6 +412,6 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         P.dep_count[blockIdx.x] = ndep;
         if (ndep) atomicAdd((unsigned long long*)&T.g->dependent_total, (unsigned long long)ndep);
     }
-    if (use_legs) tb_emit_legs(P, pbase, L, legmask, s_hist, (u16*)s_key, s_wave);  // s_key is dead here
+    if (use_legs) tb_emit_legs(P, pbase, L, legmask, r_dr, r_cr, s_hist, (u16*)s_key, s_wave);  // s_key is dead here
     if (ndep == 0) tb_write_replies(P, b, L, s_code, s_wave, s_failed);
 }

@@ -110,6 +110,7 @@ __device__ static inline u32 tb_validate_post_void(const PassArgs& P, const Tran
     s.hz |= HZ_POSTVOID | HZ_PV_KEY;
     P.pass_words[PW_PV] = 1;
     s.kpid = tb_dedup_key(tb_lo(t.pending_id), tb_hi(t.pending_id));
+    tb_dedup_mark(P);
     if (tb_dedup_insert(P.dedup, P.dedup_mask, s.kpid)) P.pass_words[PW_DUP] = 1;
     u32 es = TB_NOT_FOUND;
     const u32 claim = tb_claim_id(P, t, pe, s, &es);
@@ -413,6 +414,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_accounts_validate(PassArg
         if (code == R_OK) {
             hz |= HZ_KEYS;
             kid = tb_dedup_key(tb_lo(a.id), tb_hi(a.id));
+            tb_dedup_mark(P);
             if (tb_dedup_insert(P.dedup, P.dedup_mask, kid)) P.pass_words[PW_DUP] = 1;
             const u32 slot = tb_account_find(P.T, tb_lo(a.id), tb_hi(a.id));
             if (slot != TB_NOT_FOUND) code = tb_account_exists(a, tb_account_load(P.T, slot));

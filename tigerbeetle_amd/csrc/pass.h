@@ -201,6 +201,27 @@ __device__ static inline void tb_sum_publish(const PassArgs& P, u128 block_sum) 
     tb_atomic_add_u128(P.sum_shards + 2 * (blockIdx.x % SUM_SHARDS), block_sum);
 }
 
+// The pass dedup set is cleared lazily: a pass that inserts records its epoch and extent, and the
+// next pass's tb_pass_clear zeroes that extent only then (a pass without post/void or
+// create_accounts events leaves the set clean, and the next clear is a no-op).
+__device__ static inline void tb_dedup_mark(const PassArgs& P) {
+    P.T.g->dedup_dirty = ((u64)P.epoch << 8) | (u64)(64 - __clzll((long long)P.dedup_mask));
+}
+
+// Before kernel 1 of pass `epoch`: zero the S shards and pass words, and the dedup entries the
+// previous pass may have written (all `cap` entries when `force`).
+__global__ __launch_bounds__(256) void tb_pass_clear(u64* dedup, u64 cap, u64* sum_shards, const Globals* g, u32 epoch,
+                                                     u32 force) {
+    if (blockIdx.x == 0 && threadIdx.x < SUM_WORDS) sum_shards[threadIdx.x] = 0;
+    const u64 w = g->dedup_dirty;
+    u64 n = 0;
+    if (force) n = cap;
+    else if ((u32)(w >> 8) == epoch - 1 && w != 0) n = min(cap, 1ULL << (w & 255));
+    typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+    const v4 z = {0, 0, 0, 0};
+    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; 2 * i < n; i += (u64)gridDim.x * 256) ((v4*)dedup)[i] = z;
+}
+
 __device__ static inline u128 tb_sum_total(const u64* shards) {
     if (shards[PW_HUGE]) return TB_U128_MAX;
     u128 s = 0;

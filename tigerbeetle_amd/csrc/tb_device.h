@@ -178,7 +178,7 @@ struct Globals {
     u64 commit_timestamp;     // max timestamp of an event that returned ok when evaluated
     u64 panic;                // PANIC_* bits
     u64 log_next;             // next free transfer-log position
-    u64 unused;
+    u64 dedup_dirty;          // (pass epoch << 8) | log2(entries) of the last pass that inserted into the dedup set
     u64 bound_lo, bound_hi;   // upper bound of dp+dpost and cp+cpost over every account
     u64 dependent_total;      // dependent events of this pass
     u64 dependent_all;        // cumulative
