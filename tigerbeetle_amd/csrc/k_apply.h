@@ -54,16 +54,27 @@ __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
     if (threadIdx.x == 0) s_pref[nb] = total;
     __syncthreads();
 
-    // Gather: consecutive legs of a segment go to consecutive lanes (coalesced reads).
-    for (u32 j = threadIdx.x; j < total; j += APPLY_THREADS) {
-        u32 lo = 0, hi = nb;  // the last prepare whose segment starts at or before j
-        while (hi - lo > 1) {
-            const u32 mid = (lo + hi) >> 1;
-            if (s_pref[mid] <= j) lo = mid; else hi = mid;
+    // Gather: consecutive legs of a segment go to consecutive lanes (coalesced reads), four legs
+    // per thread in flight before their LDS adds.
+    for (u32 j0 = 0; j0 < total; j0 += 4 * APPLY_THREADS) {
+        u64 w[4];
+#pragma unroll
+        for (u32 q = 0; q < 4; q++) {
+            const u32 j = j0 + q * APPLY_THREADS + threadIdx.x;
+            w[q] = 0;
+            if (j < total) {
+                u32 lo = 0, hi = nb;  // the last prepare whose segment starts at or before j
+                while (hi - lo > 1) {
+                    const u32 mid = (lo + hi) >> 1;
+                    if (s_pref[mid] <= j) lo = mid; else hi = mid;
+                }
+                w[q] = P.leg_w[(u64)s_start[lo] + (j - s_pref[lo])];
+            }
         }
-        const u64 idx = (u64)s_start[lo] + (j - s_pref[lo]);
-        const u64 w = P.leg_w[idx];
-        atomicAdd((unsigned long long*)&s_acc[w >> LEG_AMT_BITS], (unsigned long long)(w & LEG_AMT_MASK));
+#pragma unroll
+        for (u32 q = 0; q < 4; q++) {
+            if (w[q]) atomicAdd((unsigned long long*)&s_acc[w[q] >> LEG_AMT_BITS], (unsigned long long)(w[q] & LEG_AMT_MASK));
+        }
     }
     __syncthreads();
 

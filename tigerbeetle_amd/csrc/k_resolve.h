@@ -149,8 +149,23 @@ __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 L, 
     }
     __syncthreads();
     if (P.ablate & ABL_LEG_STORES) return;
-    const u64 base = 2ULL * pbase;
-    for (u32 j = threadIdx.x; j < nlegs; j += blockDim.x) P.leg_w[base + j] = P.leg_ev[base + s_perm[j]];
+    // Gather in groups of four (the loads of a group are in flight together: leg_w and leg_ev are
+    // both u64 arrays, so the compiler would otherwise order each load after the previous store).
+    const u64* __restrict__ ev = P.leg_ev + 2ULL * pbase;
+    u64* __restrict__ w = P.leg_w + 2ULL * pbase;
+    for (u32 j0 = 0; j0 < nlegs; j0 += 4 * blockDim.x) {
+        u64 v[4];
+#pragma unroll
+        for (u32 q = 0; q < 4; q++) {
+            const u32 j = j0 + q * blockDim.x + threadIdx.x;
+            v[q] = j < nlegs ? ev[s_perm[j]] : 0;
+        }
+#pragma unroll
+        for (u32 q = 0; q < 4; q++) {
+            const u32 j = j0 + q * blockDim.x + threadIdx.x;
+            if (j < nlegs) w[j] = v[q];
+        }
+    }
 }
 
 // Apply one independent ok account (create_account :762, groove insert).
