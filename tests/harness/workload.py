@@ -26,7 +26,7 @@ def account_id(i):
 
 def make_scenario(seed, *, n_accounts=64, n_account_batches=2, n_transfer_batches=8, batch_len=(1, 200),
                   p_limit=0.1, p_linked=0.1, p_pending=0.2, p_post_void=0.2, p_balancing=0.05,
-                  p_dup=0.05, p_invalid=0.05, p_timeout=0.5, id_space=None, near_overflow=False,
+                  p_dup=0.05, p_invalid=0.05, p_timeout=0.5, id_space=None, near_overflow=False, p_huge=0.0,
                   ledgers=(1, 2), start_ts=10**12):
     rng = random.Random(seed)
     sc = Scenario()
@@ -105,6 +105,8 @@ def make_scenario(seed, *, n_accounts=64, n_account_batches=2, n_transfer_batche
                     cr = (cr + 1) % n_accounts
                 ledger = ledgers[dr % len(ledgers)]
                 amount = rng.choice([1, 2, 3, 10, 100, rng.randrange(1, 1000), rng.randrange(1, 1 << 40)])
+                if rng.random() < p_huge:  # sums past 2^128 on fresh balances (saturated certificate)
+                    amount = rng.choice([U128_MAX, 1 << 127, (1 << 126) + rng.randrange(1 << 20)])
                 if rng.random() < p_pending:
                     flags |= TF.pending
                 if rng.random() < p_balancing:

@@ -20,6 +20,7 @@ CONFIGS = {
     "clean": dict(p_limit=0, p_linked=0, p_pending=0, p_post_void=0, p_balancing=0, p_dup=0, p_invalid=0,
                   n_accounts=256, batch_len=(500, 2000), id_space=1 << 60),
     "overflow": dict(near_overflow=True, p_limit=0.2, n_accounts=32),
+    "huge_amounts": dict(p_huge=0.05, p_limit=0.1, n_accounts=24),
     "big_batches": dict(batch_len=(4000, 8190), n_transfer_batches=4, n_accounts=512, id_space=1 << 20),
 }
 

@@ -67,3 +67,10 @@ def test_sharded_near_overflow_balances(tmp_path):
     v = run_world(tmp_path, "oracle", 2, dict(seed=5, n_accounts=32, n_transfer_batches=6, near_overflow=True,
                                               **CLEAN))
     assert v["ok"], v["problems"]
+
+
+def test_sharded_huge_amounts_fresh_balances(tmp_path):
+    # Amounts near 2^127 on zero balances: a rank's saturated S must make the pass dirty (no
+    # certificate), so the overflow checks run in order on the scratch engine.
+    v = run_world(tmp_path, "oracle", 2, dict(seed=9, n_accounts=16, n_transfer_batches=6, p_huge=0.08, **CLEAN))
+    assert v["ok"], v["problems"]

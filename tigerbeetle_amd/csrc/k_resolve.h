@@ -43,6 +43,7 @@ __device__ static inline u32 tb_block_rank(bool pred, u32* s_wave, u32& total) {
 }
 
 __device__ static inline bool tb_account_cert_fails(const AccountBal* a, u128 S) {
+    if (S == TB_U128_MAX) return true;  // saturated: the true S is unknown (tb_pass_cert)
     u128 d, c, r;
     if (tb_add_overflows(a->debits_pending, a->debits_posted, &d)) return true;
     if (tb_add_overflows(a->credits_pending, a->credits_posted, &c)) return true;

@@ -237,7 +237,9 @@ __device__ static inline u128 tb_sum_total(const u64* shards) {
 __device__ static inline void tb_pass_cert(const PassArgs& P, u128& S, bool& cert_global, bool& cert64) {
     S = tb_sum_total(P.sum_shards);
     u128 r;
-    cert_global = !tb_add_overflows(tb_u128(P.T.g->bound_lo, P.T.g->bound_hi), S, &r);
+    // S saturates at maxInt(u128) (and the HUGE word reads as maxInt): such an S is a lower bound
+    // of the true sum, not an upper one, so it certifies nothing.
+    cert_global = S != TB_U128_MAX && !tb_add_overflows(tb_u128(P.T.g->bound_lo, P.T.g->bound_hi), S, &r);
     cert64 = cert_global && tb_hi(r) == 0;
     if (P.cert_ext) {  // routed shard: the router certified the global bound + S
         cert_global = true;
