@@ -91,7 +91,7 @@ def make_scenario(seed, *, n_accounts=64, n_account_batches=2, n_transfer_batche
             if pendings and rng.random() < p_post_void:
                 pid, pdr, pcr, pamt, pled = rng.choice(pendings)
                 flags = TF.post_pending_transfer if rng.random() < 0.6 else TF.void_pending_transfer
-                amount = rng.choice([0, 0, pamt, max(1, pamt - 1), pamt + 1])
+                amount = rng.choice([0, 0, pamt, max(1, pamt - 1), min(pamt + 1, U128_MAX)])
                 ev = dict(id=rng.randrange(1, id_space), pending_id=pid, amount=amount, flags=int(flags),
                           debit_account_id=rng.choice([0, 0, pdr, account_id(rng.randrange(n_accounts))]),
                           credit_account_id=rng.choice([0, 0, pcr]), ledger=rng.choice([0, 0, pled]),
