@@ -105,7 +105,7 @@ def make_scenario(seed, *, n_accounts=64, n_account_batches=2, n_transfer_batche
                     cr = (cr + 1) % n_accounts
                 ledger = ledgers[dr % len(ledgers)]
                 amount = rng.choice([1, 2, 3, 10, 100, rng.randrange(1, 1000), rng.randrange(1, 1 << 40)])
-                if rng.random() < p_huge:  # sums past 2^128 on fresh balances (saturated certificate)
+                if p_huge and rng.random() < p_huge:  # (no draw at 0: keeps older seeds' streams) sums past 2^128 on fresh balances (saturated certificate)
                     amount = rng.choice([U128_MAX, 1 << 127, (1 << 126) + rng.randrange(1 << 20)])
                 if rng.random() < p_pending:
                     flags |= TF.pending
