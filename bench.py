@@ -59,6 +59,8 @@ def parse():
     p.add_argument("--profile", type=int, default=1, help="time kernels with HIP events (roofline)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (rehearsal on one GPU)")
     p.add_argument("--same-device", action="store_true", help="rehearsal: every rank on cuda:0")
+    p.add_argument("--host-prepares", type=int, default=600,
+                   help="prepares committed one per tbgpu_commit call from host memory (the replica's call; 0: skip)")
     return p.parse_args()
 
 
@@ -77,6 +79,54 @@ def timestamps(lens, start, gap_every=0):
 def expected_unique(accounts, legs):
     """Expected number of distinct accounts touched by `legs` uniform draws."""
     return accounts * (1.0 - math.exp(-legs / accounts))
+
+
+def run_host_commits(engine, args, events_dev, t_cursor):
+    """The replica's own call pattern: one prepare per tbgpu_commit, body in host memory, reply
+    bytes back in host memory (state_machine.zig:508-540 as replica.zig:3654 calls it).  The
+    latency includes PCIe both ways; measured with the host clock around each call, first from
+    pageable memory, then from memory registered once (tbgpu_register_host: the message pool)."""
+    import ctypes
+    from tigerbeetle_amd import _lib
+
+    lib = engine.lib
+    L = args.batch
+    n = min(args.host_prepares, args.transfers // L)
+    body = np.ascontiguousarray(engine.to_host(events_dev, n * L * 128))
+    out = np.zeros(L * 8, dtype=np.uint8)
+    out_len = ctypes.c_uint32(0)
+    res = {"prepares": n, "events_per_prepare": L, "call": "tbgpu_commit (one prepare per call, host buffers)"}
+    engine.profile_mask(0)  # no HIP event pairs around the kernels
+    for mode in ("pageable", "registered"):
+        if mode == "registered":
+            _lib.check(lib.tbgpu_register_host(engine.h, body.ctypes.data, body.nbytes))
+        engine.reset_transfers()
+        engine.sync()
+        lat = []
+        for k in range(n):
+            t_cursor += 1 + L
+            t0 = time.perf_counter()
+            _lib.check(lib.tbgpu_commit(engine.h, 129, t_cursor, ctypes.c_void_p(body.ctypes.data + k * L * 128),
+                                        L * 128, out.ctypes.data, out.nbytes, ctypes.byref(out_len)))
+            lat.append(time.perf_counter() - t0)
+            assert out_len.value == 0, "C2 prepare returned errors"
+        lat = np.array(lat[min(20, n // 10):]) * 1e3  # first calls warm the path
+        res[mode] = {"transfers_per_s": round(L / (lat.mean() / 1e3), 1), "p50_ms": round(float(np.percentile(lat, 50)), 4),
+                     "p99_ms": round(float(np.percentile(lat, 99)), 4), "p100_ms": round(float(lat.max()), 4)}
+    # Per-kernel device time of the same calls (HIP event pairs: a separate, shorter run).
+    engine.reset_transfers()
+    engine.profile_mask(engine.PROF_ALL)
+    engine.reset_stats()
+    for k in range(min(n, 200)):
+        t_cursor += 1 + L
+        _lib.check(lib.tbgpu_commit(engine.h, 129, t_cursor, ctypes.c_void_p(body.ctypes.data + k * L * 128),
+                                    L * 128, out.ctypes.data, out.nbytes, ctypes.byref(out_len)))
+    st = engine.stats()
+    res["device_ms_per_call"] = {name: round(st["ms_" + key] / max(1, st["launches_" + key]), 4)
+                                 for name, key in (("validate", "validate"), ("resolve", "resolve"), ("apply_legs", "apply"),
+                                                   ("flow", "replay"), ("pass_clear", "clear"))}
+    _lib.check(lib.tbgpu_unregister_host(engine.h, body.ctypes.data))
+    return res, t_cursor + 10
 
 
 def run_cpu_baseline(engine, args, acct_lens, acct_ts, events_dev, sample_lens, sample_ts):
@@ -297,6 +347,10 @@ def main():
                        "accounts_equal": acc_equal, "transfers_equal": xfer_equal})
         cpu.pop("seconds")
 
+    host = None
+    if rank == 0 and world == 1 and args.host_prepares > 0:
+        host, t_cursor = run_host_commits(engine, args, events_dev, t_cursor)
+
     lat = np.array(pass_lat) if len(pass_lat) else np.array([float("nan")])
     line = {
         "metric": METRIC,
@@ -322,6 +376,7 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
         "parity": parity,
+        "host_commit": host,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -95,6 +95,11 @@ int tbgpu_commit_device_async(tbgpu_t* engine, uint8_t operation, uint32_t n_bat
                               const void* events_dev, void* results_dev, uint32_t* reply_bytes_dev);
 int tbgpu_sync(tbgpu_t* engine);
 
+/* Host-memory registration for the replica's message pool (allocated once at init, like every
+ * reference buffer): prepare bodies inside registered memory reach HBM by direct DMA. */
+int tbgpu_register_host(tbgpu_t* engine, void* ptr, uint64_t bytes);
+int tbgpu_unregister_host(tbgpu_t* engine, void* ptr);
+
 /* StateMachine.commit_timestamp (src/state_machine.zig:251). */
 uint64_t tbgpu_commit_timestamp(tbgpu_t* engine);
 

@@ -45,6 +45,10 @@ int tbgpu_bench_pass_latencies(tbgpu_t* engine, double* out_ms, uint64_t cap, ui
 enum { TBGPU_PROF_VALIDATE = 1, TBGPU_PROF_RESOLVE = 2, TBGPU_PROF_REPLAY = 4, TBGPU_PROF_CLEAR = 8,
        TBGPU_PROF_PASS = 16, TBGPU_PROF_APPLY = 32, TBGPU_PROF_ALL = 63 };
 int tbgpu_bench_profile_mask(tbgpu_t* engine, uint32_t mask);
+/* Passes of at least this many create_transfers events apply balances through sorted legs
+ * (k_apply.h), smaller ones with atomics (default 262144; tests set 0 to cover legs on small
+ * passes).  Exact either way. */
+int tbgpu_bench_legs_min_events(tbgpu_t* engine, uint32_t events);
 
 /* Device memory helpers for callers without a device allocator (ctypes users). */
 int tbgpu_device_alloc(tbgpu_t* engine, uint64_t bytes, void** out);

@@ -102,9 +102,12 @@ SIGNATURES = [
     ("tbgpu_bench_reset_transfers", ctypes.c_int, [_P]),
     ("tbgpu_bench_pass_latencies", ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
     ("tbgpu_bench_profile_mask", ctypes.c_int, [_P, _U32]),
+    ("tbgpu_bench_legs_min_events", ctypes.c_int, [_P, _U32]),
     ("tbgpu_device_alloc", ctypes.c_int, [_P, _U64, ctypes.POINTER(_P)]),
     ("tbgpu_device_free", ctypes.c_int, [_P, _P]),
     ("tbgpu_copy_to_host", ctypes.c_int, [_P, _P, _P, _U64]),
+    ("tbgpu_register_host", ctypes.c_int, [_P, _P, _U64]),
+    ("tbgpu_unregister_host", ctypes.c_int, [_P, _P]),
     ("tbgpu_copy_to_device", ctypes.c_int, [_P, _P, _P, _U64]),
     ("tbgpu_marker", ctypes.c_int, [_P, _U32]),
     ("tbgpu_marker_elapsed_ms", ctypes.c_double, [_P, _U32, _U32]),

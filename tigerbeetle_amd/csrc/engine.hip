@@ -99,6 +99,10 @@ struct tbgpu {
     u64* meta = nullptr;   // device: [meta_cap + 1] offsets then [meta_cap] timestamps
     u64 meta_cap = 0;
     u64* h_meta = nullptr; // pinned mirror
+    Globals* h_globals = nullptr;  // pinned: read back by engine_sync
+    u32* h_rb = nullptr;           // pinned: reply bytes of one host call
+    u8* h_results = nullptr;       // pinned: the results of a host call of <= h_results_events events
+    u64 h_results_events = 0;
     u64* lookup_ids = nullptr;
     u8* lookup_out = nullptr;
     u8* lookup_found = nullptr;
@@ -107,11 +111,13 @@ struct tbgpu {
 
     u32 epoch = 0;
     bool dedup_force = true;  // the next pass clears the whole dedup set (init, reset, epoch wrap)
+    u64 dedup_prev = 0;       // dedup entries the previous pass could have written (its mask + 1)
     u64 commit_ts = 0;       // exact after every synchronous call
     u64 last_batch_ts = 0;   // upper bound for async calls
     bool pending = false;    // an async call was enqueued and not yet synced
 
     bool profile = false;
+    u32 legs_min = LEGS_MIN_EVENTS;
     u32 prof_mask = ~0u;  // kernels timed when profiling (1 << K_*; tbgpu_bench_profile_mask)
     u32 ablate = 0;
     std::vector<hipEvent_t> event_pool;
@@ -351,6 +357,10 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     INIT_CK(hipMalloc(&E->reply_bytes, E->meta_cap * 4));
     INIT_CK(hipMalloc(&E->meta, (2 * E->meta_cap + 1) * 8));
     INIT_CK(hipHostMalloc(&E->h_meta, (2 * E->meta_cap + 1) * 8, hipHostMallocDefault));
+    INIT_CK(hipHostMalloc(&E->h_globals, sizeof(Globals), hipHostMallocDefault));
+    INIT_CK(hipHostMalloc(&E->h_rb, E->meta_cap * 4, hipHostMallocDefault));
+    E->h_results_events = std::min<u64>(E->pe_max, 1ULL << 16);
+    INIT_CK(hipHostMalloc(&E->h_results, E->h_results_events * 8, hipHostMallocDefault));
     INIT_CK(hipMalloc(&E->lookup_ids, (u64)E->lookup_cap * 16));
     INIT_CK(hipMalloc(&E->lookup_out, (u64)E->lookup_cap * 128));
     INIT_CK(hipMalloc(&E->lookup_found, E->lookup_cap));
@@ -380,6 +390,9 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo};
     for (void* p : bufs) if (p) (void)hipFree(p);
     if (E->h_meta) (void)hipHostFree(E->h_meta);
+    if (E->h_globals) (void)hipHostFree(E->h_globals);
+    if (E->h_rb) (void)hipHostFree(E->h_rb);
+    if (E->h_results) (void)hipHostFree(E->h_results);
     if (E->h_rmeta) (void)hipHostFree(E->h_rmeta);
     for (hipEvent_t e : E->event_pool) (void)hipEventDestroy(e);
     for (int i = 0; i < 16; i++) if (E->markers[i]) (void)hipEventDestroy(E->markers[i]);
@@ -394,9 +407,10 @@ extern "C" int tbgpu_reset(tbgpu_t* E) {
 
 // Read back commit_timestamp and the panic word after the stream drained.
 static int engine_sync(tbgpu* E) {
+    // One round trip: the globals come back on the stream, behind the call's kernels.
+    HIPCK(hipMemcpyAsync(E->h_globals, E->g, sizeof(Globals), hipMemcpyDeviceToHost, E->stream));
     HIPCK(hipStreamSynchronize(E->stream));
-    Globals g;
-    HIPCK(hipMemcpy(&g, E->g, sizeof(Globals), hipMemcpyDeviceToHost));
+    const Globals g = *E->h_globals;
     E->commit_ts = g.commit_timestamp;
     E->pending = false;
     int st = prof_collect(E);
@@ -458,7 +472,12 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.routed = routed ? 1 : 0;
         P.codes = codes;
         P.cert_ext = cert_ext;
-        P.legs = (op == OP_CREATE_TRANSFERS && E->legs_ok && b1 - b0 <= LEG_PREPARES_MAX && !(E->ablate & ABL_LEGS)) ? 1 : 0;
+        // Legs pay a fixed ~30 us (one workgroup per bucket, LDS sums) that no-return atomics in
+        // the resolve kernel (~20 G/s) only cost beyond ~LEGS_MIN_EVENTS events: the replica's
+        // one-prepare commits take the atomics.
+        P.legs = (op == OP_CREATE_TRANSFERS && E->legs_ok && b1 - b0 <= LEG_PREPARES_MAX && n >= E->legs_min &&
+                  !(E->ablate & ABL_LEGS)) ? 1 : 0;
+        P.apply_late = (op == OP_CREATE_TRANSFERS && !P.legs) ? 1 : 0;
         P.leg_shift = E->leg_shift;
         P.leg_buckets = E->leg_buckets;
         P.leg_ev = E->leg_ev;
@@ -473,10 +492,15 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         if (st) return st;
         ProfilePair pp;
         if ((st = prof_begin(E, &pp, K_CLEAR))) return st;
-        hipLaunchKernelGGL(tb_pass_clear, dim3(1024), dim3(256), 0, E->stream, E->dedup, E->dedup_cap, E->sum_shards,
+        // Grid sized to what may need zeroing: the previous pass's dedup extent (2 entries per
+        // thread per step), or the whole set when forced.
+        const u64 clear_n = E->dedup_force ? E->dedup_cap : E->dedup_prev;
+        const u32 clear_grid = (u32)std::min<u64>(1024, std::max<u64>(1, clear_n / 2048));
+        hipLaunchKernelGGL(tb_pass_clear, dim3(clear_grid), dim3(256), 0, E->stream, E->dedup, E->dedup_cap, E->sum_shards,
                            E->g, E->epoch, E->dedup_force ? 1u : 0u);
         HIPCK(hipGetLastError());
         E->dedup_force = false;
+        E->dedup_prev = P.dedup_mask + 1;
         if ((st = prof_end(E, &pp))) return st;
 
         if (n > 0) {
@@ -498,10 +522,14 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         }
         HIPCK(hipGetLastError());
         if ((st = prof_end(E, &pp))) return st;
-        if (P.legs) {
+        if (P.legs || P.apply_late) {
             if ((st = prof_begin(E, &pp, K_APPLY))) return st;
-            hipLaunchKernelGGL(tb_apply_legs, dim3(E->leg_buckets), dim3(APPLY_THREADS), (4u << E->leg_shift) * 8, E->stream,
-                               P);
+            if (P.legs) {
+                hipLaunchKernelGGL(tb_apply_legs, dim3(E->leg_buckets), dim3(APPLY_THREADS), (4u << E->leg_shift) * 8,
+                                   E->stream, P);
+            } else if (n > 0) {
+                hipLaunchKernelGGL(tb_apply_events, dim3((u32)((n + 255) / 256)), dim3(256), 0, E->stream, P);
+            }
             HIPCK(hipGetLastError());
             if ((st = prof_end(E, &pp))) return st;
         }
@@ -635,12 +663,19 @@ static int commit_host(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const
         }
         std::vector<u64> h_off(E->h_meta, E->h_meta + (k1 - k0) + 1);
         if ((st = enqueue_call(E, op, k1 - k0, h_off.data(), E->staging, E->results, E->reply_bytes))) return st;
-        std::vector<u32> rb(k1 - k0);
-        HIPCK(hipMemcpyAsync(rb.data(), E->reply_bytes, (u64)(k1 - k0) * 4, hipMemcpyDeviceToHost, E->stream));
+        // Reply sizes and (for calls of up to h_results_events events: every prepare the replica
+        // commits) the result slots come back on the stream with the globals: one round trip.
+        const u32* rb = E->h_rb;
+        HIPCK(hipMemcpyAsync(E->h_rb, E->reply_bytes, (u64)(k1 - k0) * 4, hipMemcpyDeviceToHost, E->stream));
+        const bool whole = total <= E->h_results_events;
+        if (whole && total) {
+            HIPCK(hipMemcpyAsync(E->h_results, E->results, total * 8, hipMemcpyDeviceToHost, E->stream));
+        }
         if ((st = engine_sync(E))) return st;
         for (u32 k = k0; k < k1; k++) {
             const u32 bytes = rb[k - k0];
-            if (bytes) HIPCK(hipMemcpy(outputs[k], E->results + 2 * h_off[k - k0], bytes, hipMemcpyDeviceToHost));
+            if (bytes && whole) memcpy(outputs[k], E->h_results + 8 * h_off[k - k0], bytes);
+            else if (bytes) HIPCK(hipMemcpy(outputs[k], E->results + 2 * h_off[k - k0], bytes, hipMemcpyDeviceToHost));
             out_lens[k] = bytes;
         }
         k0 = k1;
@@ -916,6 +951,11 @@ extern "C" int tbgpu_bench_generate_transfers(tbgpu_t* E, void* out_dev, uint64_
     return TBGPU_STATUS_OK;
 }
 
+extern "C" int tbgpu_bench_legs_min_events(tbgpu_t* E, uint32_t events) {
+    E->legs_min = events;
+    return TBGPU_STATUS_OK;
+}
+
 extern "C" int tbgpu_bench_profile_mask(tbgpu_t* E, uint32_t mask) {
     E->prof_mask = mask;
     return TBGPU_STATUS_OK;
@@ -930,6 +970,20 @@ extern "C" int tbgpu_device_alloc(tbgpu_t* E, uint64_t bytes, void** out) {
 extern "C" int tbgpu_device_free(tbgpu_t* E, void* ptr) {
     HIPCK(hipSetDevice(E->device));
     HIPCK(hipFree(ptr));
+    return TBGPU_STATUS_OK;
+}
+
+// The replica's message pool is allocated once at init (static allocation); registering it lets
+// the prepare bodies go to HBM by DMA straight from the message, with no staging copy.
+extern "C" int tbgpu_register_host(tbgpu_t* E, void* ptr, uint64_t bytes) {
+    HIPCK(hipSetDevice(E->device));
+    HIPCK(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_unregister_host(tbgpu_t* E, void* ptr) {
+    HIPCK(hipSetDevice(E->device));
+    HIPCK(hipHostUnregister(ptr));
     return TBGPU_STATUS_OK;
 }
 

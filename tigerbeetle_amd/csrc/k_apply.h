@@ -85,3 +85,17 @@ __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
         if (v != 0) *(u64*)(bal + (u64)k * 16) += v;  // low word: no carry under the certificate
     }
 }
+
+// Kernel 2b of a small pass (no legs): the balance effects of every independent ok transfer, one
+// event per lane.  The resolve kernel has one workgroup per prepare; left there, a one-prepare
+// pass (the replica's commit) would issue all 16K atomics of its prepare from a single CU.
+__global__ __launch_bounds__(256) void tb_apply_events(PassArgs P) {
+    const u32 pe = blockIdx.x * 256 + threadIdx.x;
+    if (pe >= P.n) return;
+    const u32 info = P.info[pe];
+    if ((info & HZ_DEP) || (info & 0xFF) != R_OK || !(info & HZ_ACCTS)) return;
+    u128 S;
+    bool cert_global, cert64;
+    tb_pass_cert(P, S, cert_global, cert64);
+    tb_apply_transfer(P, pe, info, P.eflags[pe], cert64);
+}

@@ -384,7 +384,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                                 tb_hist16_inc(s_hist, crs >> P.leg_shift);
                             }
                             legmask |= 1u << k;
-                        } else {
+                        } else if (!P.apply_late) {
                             tb_apply_transfer(P, pe, info, r_fl[k], cert64);
                         }
                     } else {

@@ -73,6 +73,7 @@ struct PassArgs {
     // create_transfer events are written as legs, bucketed by account slot per prepare, and summed
     // per account by tb_apply_legs instead of being added with one global atomic per leg.
     u32 legs;              // 1: the legs path is enabled for this pass (the host checked the sizes)
+    u32 apply_late;        // 1: tb_apply_events applies the independent ok transfers (small passes)
     u32 leg_shift;         // bucket of an account slot = slot >> leg_shift (2^leg_shift slots each)
     u32 leg_buckets;       // account_cap >> leg_shift
     u64* leg_ev;           // [2 * pass events] leg word of event pe's side s at 2*pe+s (event order)
@@ -91,6 +92,7 @@ enum : u32 { CERT_EXT_U128 = 1, CERT_EXT_U64 = 2 };
 #define LEG_BUCKETS_PREF 2048
 #define LEG_BUCKETS_MAX 4096  // u16 counters: 8 KB of tb_resolve's LDS (under 80 KB: two workgroups per CU)
 #define LEG_PREPARES_MAX 1024
+#define LEGS_MIN_EVENTS (1u << 18)  // smaller passes apply balances with atomics (engine.hip)
 #define APPLY_THREADS 256
 // Leg word: ((slot within its bucket) << 2 | balance field (BAL_OFF / 16)) << LEG_AMT_BITS | amount.
 // An amount of 2^LEG_AMT_BITS or more is applied by the resolve kernel with an atomic instead.

@@ -149,6 +149,10 @@ class Engine:
 
     PROF_VALIDATE, PROF_RESOLVE, PROF_REPLAY, PROF_CLEAR, PROF_PASS, PROF_APPLY, PROF_ALL = 1, 2, 4, 8, 16, 32, 63
 
+    def legs_min_events(self, events):
+        """Passes of >= events transfers use the sorted balance legs (0: every pass)."""
+        _lib.check(self.lib.tbgpu_bench_legs_min_events(self.h, int(events)))
+
     def profile_mask(self, mask):
         """Kernels timed with HIP events when profiling (include/tbgpu_bench.h)."""
         _lib.check(self.lib.tbgpu_bench_profile_mask(self.h, mask))
