@@ -103,6 +103,12 @@ struct tbgpu {
     u32* h_rb = nullptr;           // pinned: reply bytes of one host call
     u8* h_results = nullptr;       // pinned: the results of a host call of <= h_results_events events
     u64 h_results_events = 0;
+    struct HostRegion {
+        const u8* ptr;
+        u64 bytes;
+        const u8* dev;  // its device mapping
+    };
+    std::vector<HostRegion> host_regions;  // tbgpu_register_host
     u64* lookup_ids = nullptr;
     u8* lookup_out = nullptr;
     u8* lookup_found = nullptr;
@@ -424,7 +430,8 @@ static int engine_sync(tbgpu* E) {
 // Routed mode (a shard of a multi-GPU pass): events carry their execute timestamps, codes = dense
 // result codes instead of sparse replies, cert_ext = the router's certificate.
 static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* events_dev, u32* results_dev,
-                        u32* reply_bytes_dev, bool routed = false, u8* codes = nullptr, u32 cert_ext = 0) {
+                        u32* reply_bytes_dev, bool routed = false, u8* codes = nullptr, u32 cert_ext = 0,
+                        const u8* events_src = nullptr) {
     const u64* d_off = E->meta;
     const u64* d_ts = E->meta + (nb + 1);
     u32 b0 = 0;
@@ -449,6 +456,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.batch_off = d_off;
         P.batch_ts = d_ts;
         P.events = events_dev;
+        P.events_src = events_src;
         P.results = results_dev;
         P.reply_bytes = reply_bytes_dev;
         P.info = E->info;
@@ -655,14 +663,26 @@ static int commit_host(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const
         u64 total = 0;
         int st = prepare_call(E, op, k1 - k0, timestamps + k0, lens.data() + k0, E->commit_ts, &total);
         if (st) return st;
+        // One prepare in registered memory (the replica's commit): kernel 1 reads it over PCIe and
+        // writes it through to staging — no copy ahead of the kernels.  Otherwise a DMA per input.
+        const u8* src = nullptr;
+        if (k1 - k0 == 1 && lens[k0]) {
+            const u8* in = (const u8*)inputs[k0];
+            for (const auto& r : E->host_regions) {
+                if (in >= r.ptr && in + (u64)lens[k0] * 128 <= r.ptr + r.bytes) src = r.dev + (in - r.ptr);
+            }
+        }
         u64 off = 0;
-        for (u32 k = k0; k < k1; k++) {
+        for (u32 k = k0; k < k1 && !src; k++) {
             if (lens[k]) HIPCK(hipMemcpyAsync(E->staging + off * 128, inputs[k], (u64)lens[k] * 128,
                                               hipMemcpyHostToDevice, E->stream));
             off += lens[k];
         }
         std::vector<u64> h_off(E->h_meta, E->h_meta + (k1 - k0) + 1);
-        if ((st = enqueue_call(E, op, k1 - k0, h_off.data(), E->staging, E->results, E->reply_bytes))) return st;
+        if ((st = enqueue_call(E, op, k1 - k0, h_off.data(), E->staging, E->results, E->reply_bytes, false, nullptr, 0,
+                               src))) {
+            return st;
+        }
         // Reply sizes and (for calls of up to h_results_events events: every prepare the replica
         // commits) the result slots come back on the stream with the globals: one round trip.
         const u32* rb = E->h_rb;
@@ -977,12 +997,26 @@ extern "C" int tbgpu_device_free(tbgpu_t* E, void* ptr) {
 // the prepare bodies go to HBM by DMA straight from the message, with no staging copy.
 extern "C" int tbgpu_register_host(tbgpu_t* E, void* ptr, uint64_t bytes) {
     HIPCK(hipSetDevice(E->device));
-    HIPCK(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    HIPCK(hipHostRegister(ptr, bytes, hipHostRegisterMapped));
+    void* dev = nullptr;
+    HIPCK(hipHostGetDevicePointer(&dev, ptr, 0));
+    E->host_regions.push_back({(const u8*)ptr, bytes, (const u8*)dev});
     return TBGPU_STATUS_OK;
 }
 
 extern "C" int tbgpu_unregister_host(tbgpu_t* E, void* ptr) {
     HIPCK(hipSetDevice(E->device));
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    HIPCK(hipStreamSynchronize(E->stream));
+    for (size_t i = 0; i < E->host_regions.size(); i++) {
+        if (E->host_regions[i].ptr == (const u8*)ptr) {
+            E->host_regions.erase(E->host_regions.begin() + i);
+            break;
+        }
+    }
     HIPCK(hipHostUnregister(ptr));
     return TBGPU_STATUS_OK;
 }

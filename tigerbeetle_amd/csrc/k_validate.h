@@ -280,7 +280,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
 
     const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
     const u32 count = min((u32)VALIDATE_THREADS, P.n - tile0);
-    tb_stage_events(P.events + (P.e0 + tile0) * 128, count, stage, P.ablate & EXP_NT);
+    tb_stage_tile(P, tile0, count, stage, P.ablate & EXP_NT);
 
     const u32 pe = tile0 + threadIdx.x;  // pass-relative event
     const u64 e = P.e0 + pe;
@@ -394,7 +394,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_accounts_validate(PassArg
     __shared__ __attribute__((aligned(16))) u8 stage[VALIDATE_THREADS * STAGE_STRIDE];
     const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
     const u32 count = min((u32)VALIDATE_THREADS, P.n - tile0);
-    tb_stage_events(P.events + (P.e0 + tile0) * 128, count, stage);
+    tb_stage_tile(P, tile0, count, stage);
     const u32 pe = tile0 + threadIdx.x;
     const u64 e = P.e0 + pe;
     const u32 b = tb_wave_batch(P.batch_off, P.b0, P.b1, P.e0 + tile0, count, e);

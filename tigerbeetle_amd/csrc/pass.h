@@ -43,6 +43,8 @@ struct PassArgs {
     const u64* batch_off;  // [nb_call + 1] call-relative event offsets
     const u64* batch_ts;   // [nb_call] prepare timestamps
     const u8* events;      // call events (128 B each)
+    const u8* events_src;  // != null: kernel 1 reads the events here (registered host memory, over
+                           // PCIe) and writes them through to `events` for the later kernels
     u32* results;          // call reply area: batch k at results + 2*batch_off[k]
     u32* reply_bytes;      // [nb_call]
     // scratch, pass-relative
@@ -149,7 +151,7 @@ __device__ static inline u32 tb_wave_batch(const u64* off, u32 lo, u32 hi, u64 t
 #define STAGE_STRIDE 128
 __device__ static inline u32 tb_stage_off(u32 row, u32 chunk) { return row * STAGE_STRIDE + ((chunk ^ (row & 7)) << 4); }
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-__device__ static inline void tb_stage_events(const u8* src, u32 count, u8* lds, bool nt = false) {
+__device__ static inline void tb_stage_events(const u8* src, u32 count, u8* lds, bool nt = false, u8* copy = nullptr) {
     const u32 t = threadIdx.x;
 #pragma unroll
     for (u32 r = 0; r < 8; r++) {
@@ -159,9 +161,17 @@ __device__ static inline void tb_stage_events(const u8* src, u32 count, u8* lds,
             const u32x4* g = (const u32x4*)(src + (u64)c * 16);
             const u32x4 v = nt ? __builtin_nontemporal_load(g) : *g;
             *(u32x4*)(lds + tb_stage_off(ev, part)) = v;
+            if (copy) *(u32x4*)(copy + (u64)c * 16) = v;
         }
     }
     __syncthreads();
+}
+
+// Kernel 1's tile: from the call's events, or read through from registered host memory.
+__device__ static inline void tb_stage_tile(const PassArgs& P, u32 tile0, u32 count, u8* lds, bool nt = false) {
+    const u64 off = (P.e0 + tile0) * 128;
+    if (P.events_src) tb_stage_events(P.events_src + off, count, lds, nt, const_cast<u8*>(P.events) + off);
+    else tb_stage_events(P.events + off, count, lds, nt);
 }
 
 template <typename R>
