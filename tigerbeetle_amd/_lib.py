@@ -8,6 +8,8 @@ import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libtbgpu.so")
+# A/B timing experiments (tools/gpu/ab.sh) load an older build of the same library.
+AB_PATH = os.environ.get("TBGPU_AB_LIB")
 
 STATUS_OK, STATUS_INVALID, STATUS_PANIC, STATUS_DEVICE = 0, 1, 2, 3
 
@@ -145,8 +147,10 @@ def load():
         if not os.path.exists(LIB_PATH):
             raise ImportError("tigerbeetle_amd: %s is missing — run `python -c 'import __graft_entry__ as g; "
                               "g.build()'` (hipcc --offload-arch=gfx950)" % LIB_PATH)
-        lib = ctypes.CDLL(LIB_PATH)
+        lib = ctypes.CDLL(AB_PATH or LIB_PATH)
         for name, res, args in SIGNATURES:
+            if AB_PATH and not hasattr(lib, name):
+                continue  # an older build: symbols added since are absent
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

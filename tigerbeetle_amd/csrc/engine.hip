@@ -515,9 +515,17 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
             if ((st = prof_begin(E, &pp, K_VALIDATE))) return st;
             const u32 grid = (u32)((n + VALIDATE_THREADS - 1) / VALIDATE_THREADS);
             if (op == OP_CREATE_TRANSFERS) {
-                hipLaunchKernelGGL(tb_transfers_validate, dim3(grid), dim3(VALIDATE_THREADS), 0, E->stream, P);
+                if (P.events_src) {
+                    hipLaunchKernelGGL(tb_transfers_validate<true>, dim3(grid), dim3(VALIDATE_THREADS), 0, E->stream, P);
+                } else {
+                    hipLaunchKernelGGL(tb_transfers_validate<false>, dim3(grid), dim3(VALIDATE_THREADS), 0, E->stream, P);
+                }
             } else {
-                hipLaunchKernelGGL(tb_accounts_validate, dim3(grid), dim3(VALIDATE_THREADS), 0, E->stream, P);
+                if (P.events_src) {
+                    hipLaunchKernelGGL(tb_accounts_validate<true>, dim3(grid), dim3(VALIDATE_THREADS), 0, E->stream, P);
+                } else {
+                    hipLaunchKernelGGL(tb_accounts_validate<false>, dim3(grid), dim3(VALIDATE_THREADS), 0, E->stream, P);
+                }
             }
             HIPCK(hipGetLastError());
             if ((st = prof_end(E, &pp))) return st;

@@ -60,6 +60,7 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_route_classify(RouteArgs A) 
     if (threadIdx.x == 0) s_dirty = 0;
     __syncthreads();
     const u64 e = (u64)blockIdx.x * ROUTE_THREADS + threadIdx.x;
+    const bool limits = A.T.g->limit_accounts != 0;
     u128 amount = 0;
     if (e < A.n) {
         const u64* w = (const u64*)(A.events + e * 128);
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_route_classify(RouteArgs A) 
         u32 dirty = 0;
         if (flags & (TF_LINKED | TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT)) {
             dirty = ROUTE_DIRTY_FLAGS;
-        } else {
+        } else if (limits) {  // no limit account exists (C2/C5): no account probe at all
             const u32 d = tb_account_find(A.T, w[2], w[3]);
             const u32 c = tb_account_find(A.T, w[4], w[5]);
             const u16 lim = AF_DEBITS_MUST_NOT_EXCEED_CREDITS | AF_CREDITS_MUST_NOT_EXCEED_DEBITS;

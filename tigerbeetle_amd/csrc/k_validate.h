@@ -275,12 +275,13 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
 // LDS is the 32 KB stage only (five workgroups per CU): the batch search runs on the scalar unit,
 // each wave stores its own records, and the block's S partials go through the stage rows their
 // waves have finished with.
+template <bool SRC>
 __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassArgs P) {
     __shared__ __attribute__((aligned(16))) u8 stage[VALIDATE_THREADS * STAGE_STRIDE];
 
     const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
     const u32 count = min((u32)VALIDATE_THREADS, P.n - tile0);
-    tb_stage_tile(P, tile0, count, stage, P.ablate & EXP_NT);
+    tb_stage_tile<SRC>(P, tile0, count, stage, P.ablate & EXP_NT);
 
     const u32 pe = tile0 + threadIdx.x;  // pass-relative event
     const u64 e = P.e0 + pe;
@@ -390,11 +391,12 @@ __device__ static inline u32 tb_account_stateless(const Account& a) {
 }
 
 // Kernel 1 (create_accounts).
+template <bool SRC>
 __global__ __launch_bounds__(VALIDATE_THREADS) void tb_accounts_validate(PassArgs P) {
     __shared__ __attribute__((aligned(16))) u8 stage[VALIDATE_THREADS * STAGE_STRIDE];
     const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
     const u32 count = min((u32)VALIDATE_THREADS, P.n - tile0);
-    tb_stage_tile(P, tile0, count, stage);
+    tb_stage_tile<SRC>(P, tile0, count, stage);
     const u32 pe = tile0 + threadIdx.x;
     const u64 e = P.e0 + pe;
     const u32 b = tb_wave_batch(P.batch_off, P.b0, P.b1, P.e0 + tile0, count, e);

@@ -167,10 +167,12 @@ __device__ static inline void tb_stage_events(const u8* src, u32 count, u8* lds,
     __syncthreads();
 }
 
-// Kernel 1's tile: from the call's events, or read through from registered host memory.
+// Kernel 1's tile: from the call's events, or (SRC, a separate instantiation so the HBM path's
+// code is untouched) read through from registered host memory.
+template <bool SRC>
 __device__ static inline void tb_stage_tile(const PassArgs& P, u32 tile0, u32 count, u8* lds, bool nt = false) {
     const u64 off = (P.e0 + tile0) * 128;
-    if (P.events_src) tb_stage_events(P.events_src + off, count, lds, nt, const_cast<u8*>(P.events) + off);
+    if (SRC) tb_stage_events(P.events_src + off, count, lds, false, const_cast<u8*>(P.events) + off);
     else tb_stage_events(P.events + off, count, lds, nt);
 }
 

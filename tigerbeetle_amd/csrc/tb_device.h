@@ -190,7 +190,7 @@ struct Globals {
     u64 flow_units;           // cumulative units (chains / single events) the flow path executed
     u64 flow_runs;            // runs (k_flow.h) and the units they covered
     u64 flow_run_units;
-    u64 pad[1];
+    u64 limit_accounts;       // accounts ever created with a limit flag (never decremented: an upper bound)
 };
 
 struct AccountHot {
@@ -332,6 +332,7 @@ __device__ static inline void tb_account_store_new(const Tables& T, u32 slot, co
     b.credits_pending = a.credits_pending;
     b.credits_posted = a.credits_posted;
     T.acct_bal[slot] = b;
+    if (a.flags & AF_LIMITS) atomicAdd((unsigned long long*)&T.g->limit_accounts, 1ULL);
     AccountHot* h = &T.acct_hot[slot];
     h->ledger = a.ledger;
     h->code = a.code;
