@@ -141,6 +141,7 @@ struct tbgpu {
     u64 route_events_max = 0;
     u8* r_home = nullptr;
     u32* r_block_counts = nullptr;
+    u64 r_block_cap = 0;
     u64* r_words = nullptr;
     u64* r_meta = nullptr;    // device [meta_cap + 1] offsets then [meta_cap] timestamps
     u64* h_rmeta = nullptr;   // pinned mirror
@@ -1104,7 +1105,8 @@ extern "C" int tbgpu_route_init(tbgpu_t* E, uint32_t world, uint64_t events_max)
     E->route_events_max = events_max;
     const u64 nblocks = (events_max + ROUTE_THREADS - 1) / ROUTE_THREADS;
     HIPCK(hipMalloc(&E->r_home, events_max));
-    HIPCK(hipMalloc(&E->r_block_counts, nblocks * world * 4));
+    HIPCK(hipMalloc(&E->r_block_counts, 2 * nblocks * world * 4));  // counts, then bases
+    E->r_block_cap = nblocks * world;
     HIPCK(hipMalloc(&E->r_words, ROUTE_WORDS * 8));
     HIPCK(hipMalloc(&E->r_meta, (2 * E->meta_cap + 1) * 8));
     HIPCK(hipHostMalloc(&E->h_rmeta, (2 * E->meta_cap + 1) * 8, hipHostMallocDefault));
@@ -1155,12 +1157,13 @@ extern "C" int tbgpu_route_plan_build(tbgpu_t* E, uint32_t nb, const uint64_t* t
     A.nblocks = (u32)((n + ROUTE_THREADS - 1) / ROUTE_THREADS);
     A.home = E->r_home;
     A.block_counts = E->r_block_counts;
+    A.block_base = E->r_block_counts + E->r_block_cap;
     A.words = E->r_words;
     A.T = E->T;
     if (n > 0) {
         hipLaunchKernelGGL(tb_route_classify, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, E->stream, A);
         HIPCK(hipGetLastError());
-        hipLaunchKernelGGL(tb_route_offsets, dim3(1), dim3(1024), 0, E->stream, A);
+        hipLaunchKernelGGL(tb_route_offsets, dim3(A.world), dim3(1024), 0, E->stream, A);
         HIPCK(hipGetLastError());
         hipLaunchKernelGGL(tb_route_scatter, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, E->stream, A, (u8*)send_events_dev,
                            (u32*)slot_dev);

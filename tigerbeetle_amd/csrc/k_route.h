@@ -41,7 +41,8 @@ struct RouteArgs {
     u32 world;
     u32 nblocks;
     u8* home;              // [n] home rank, or ROUTE_LOCAL (answered by the source)
-    u32* block_counts;     // [nblocks][world] (then rewritten as exclusive bases)
+    u32* block_counts;     // [nblocks][world] events of block blk for home h
+    u32* block_base;       // [nblocks][world] send-buffer position of those events
     u64* words;            // [2*SUM_SHARDS] S shards, [2*SUM_SHARDS] HUGE, [+1] dirty bits, [+2..] counts
     Tables T;
 };
@@ -107,43 +108,34 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_route_classify(RouteArgs A) 
     }
 }
 
-// Pass 2 (one workgroup): exclusive bases.  block_counts[blk][h] becomes the send-buffer position
-// of block blk's first event for home h: homes in rank order, blocks in order within a home.
+// Pass 2: exclusive bases, one workgroup per home (all homes at once).  block_base[blk][h] is the
+// send-buffer position of block blk's first event for home h: homes in rank order, blocks in order
+// within a home.  Workgroup h scans its home's column and sums the columns of the homes before it
+// (its base) in the same sweep; each thread owns a contiguous run of blocks (one contiguous span of
+// counts), and the scan is a shuffle scan (two barriers).
 __global__ __launch_bounds__(1024) void tb_route_offsets(RouteArgs A) {
-    __shared__ u32 s_part[1024];
-    __shared__ u64 s_home_base;
-    if (threadIdx.x == 0) s_home_base = 0;
-    __syncthreads();
-    for (u32 h = 0; h < A.world; h++) {
-        // Each thread owns a contiguous run of blocks.
-        const u32 per = (A.nblocks + 1023) / 1024;
-        const u32 b0 = threadIdx.x * per, b1 = min(A.nblocks, b0 + per);
-        u32 local = 0;
-        for (u32 b = b0; b < b1; b++) local += A.block_counts[(u64)b * A.world + h];
-        s_part[threadIdx.x] = local;
-        __syncthreads();
-        // Inclusive scan over the 1024 partials (Hillis-Steele; tiny).
-        for (u32 off = 1; off < 1024; off <<= 1) {
-            const u32 v = threadIdx.x >= off ? s_part[threadIdx.x - off] : 0;
-            __syncthreads();
-            s_part[threadIdx.x] += v;
-            __syncthreads();
+    __shared__ u32 s_wave[1024 / 64];
+    const u32 h = blockIdx.x;
+    const u32 per = (A.nblocks + 1023) / 1024;
+    const u32 b0 = min(A.nblocks, threadIdx.x * per), b1 = min(A.nblocks, b0 + per);
+    u32 local = 0, before = 0;
+    for (u32 b = b0; b < b1; b++) {
+        const u32* row = A.block_counts + (u64)b * A.world;
+        for (u32 k = 0; k <= h; k++) {
+            const u32 v = row[k];
+            if (k < h) before += v;
+            else local += v;
         }
-        const u64 base = s_home_base;
-        u64 run = base + (threadIdx.x ? s_part[threadIdx.x - 1] : 0);
-        for (u32 b = b0; b < b1; b++) {
-            u32* c = &A.block_counts[(u64)b * A.world + h];
-            const u32 v = *c;
-            *c = (u32)run;
-            run += v;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            A.words[RW_COUNTS + h] = s_part[1023];
-            s_home_base = base + s_part[1023];
-        }
-        __syncthreads();
     }
+    u32 home_total, base;
+    const u32 run0 = tb_block_excl_sum(local, s_wave, &home_total);
+    tb_block_excl_sum(before, s_wave, &base);
+    u32 run = base + run0;
+    for (u32 b = b0; b < b1; b++) {
+        A.block_base[(u64)b * A.world + h] = run;
+        run += A.block_counts[(u64)b * A.world + h];
+    }
+    if (threadIdx.x == 0) A.words[RW_COUNTS + h] = home_total;
 }
 
 // Pass 3: stable scatter into the send buffer, with the execute timestamp of every event.
@@ -175,7 +167,7 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_route_scatter(RouteArgs A, u
         slot[e] = SLOT_LOCAL;
         return;
     }
-    u32 pos = A.block_counts[(u64)blockIdx.x * A.world + h] + before;
+    u32 pos = A.block_base[(u64)blockIdx.x * A.world + h] + before;
     for (u32 w = 0; w < wave; w++) pos += s_wcnt[w][h];
     const u32 b = tb_batch_search(A.batch_off, s_range[0], s_range[1], e);
     const u64 boff = A.batch_off[b];
