@@ -15,8 +15,13 @@ import sys
 
 
 def short(name):
-    """'void tb_resolve<(unsigned char)129>(PassArgs)' -> 'tb_resolve<129>'."""
+    """'void tb_resolve<(unsigned char)129>(PassArgs)' -> 'tb_resolve<129>'; the validate kernels'
+    HBM instantiation <false> keeps the plain name, the read-through one <true> gets '_src'."""
     base = name.split("(")[0].replace("void ", "").strip()
+    if base.endswith("validate<false>"):
+        return base[:-len("<false>")]
+    if base.endswith("validate<true>"):
+        return base[:-len("<true>")] + "_src"
     if "<" in name.split("(PassArgs")[0]:
         arg = name.split("<", 1)[1].split(">", 1)[0].replace("(unsigned char)", "")
         base = base.split("<")[0] + "<" + arg + ">"
