@@ -114,6 +114,21 @@ int tbgpu_export_transfers(tbgpu_t* engine, void* out, uint64_t cap, uint64_t* c
 /* Posted groove (src/state_machine.zig:185-198): {pending_timestamp, fulfillment} pairs, sorted. */
 int tbgpu_export_posted(tbgpu_t* engine, uint64_t* out_pairs, uint64_t cap, uint64_t* count);
 
+/* Groove write-back for a durable replica (StateMachine.checkpoint / compact,
+ * src/state_machine.zig:542-582; groove insert / upsert, src/lsm/groove.zig:902-963): the objects
+ * changed since the previous call (or since init / reset) — accounts created or re-balanced (full
+ * records, by id), transfers created (by timestamp), posted-groove entries created or changed
+ * ({pending timestamp, fulfillment} pairs, by timestamp).  If a buffer is too small the call
+ * returns TBGPU_STATUS_INVALID with the sizes needed in *counts and nothing advances. */
+typedef struct tbgpu_delta_counts {
+    uint64_t accounts;
+    uint64_t transfers;
+    uint64_t posted;
+} tbgpu_delta_counts;
+int tbgpu_checkpoint_delta(tbgpu_t* engine, void* accounts_out, uint64_t accounts_cap, void* transfers_out,
+                           uint64_t transfers_cap, uint64_t* posted_out, uint64_t posted_cap,
+                           tbgpu_delta_counts* counts);
+
 typedef struct tbgpu_stats {
     uint64_t passes;
     uint64_t events;

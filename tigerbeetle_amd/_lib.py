@@ -27,6 +27,10 @@ class tbgpu_config(ctypes.Structure):
     ]
 
 
+class tbgpu_delta_counts(ctypes.Structure):
+    _fields_ = [("accounts", ctypes.c_uint64), ("transfers", ctypes.c_uint64), ("posted", ctypes.c_uint64)]
+
+
 class tbgpu_stats(ctypes.Structure):
     _fields_ = [
         ("passes", ctypes.c_uint64),
@@ -109,6 +113,7 @@ SIGNATURES = [
     ("tbgpu_device_free", ctypes.c_int, [_P, _P]),
     ("tbgpu_copy_to_host", ctypes.c_int, [_P, _P, _P, _U64]),
     ("tbgpu_register_host", ctypes.c_int, [_P, _P, _U64]),
+    ("tbgpu_checkpoint_delta", ctypes.c_int, [_P, _P, _U64, _P, _U64, _P, _U64, _P]),
     ("tbgpu_unregister_host", ctypes.c_int, [_P, _P]),
     ("tbgpu_copy_to_device", ctypes.c_int, [_P, _P, _P, _U64]),
     ("tbgpu_marker", ctypes.c_int, [_P, _U32]),

@@ -124,6 +124,12 @@ struct tbgpu {
 
     bool profile = false;
     u32 legs_min = LEGS_MIN_EVENTS;
+    // Groove write-back snapshot (tbgpu_checkpoint_delta), allocated on first use.
+    AccountBal* ckpt_bal = nullptr;  // balances at the previous write-back
+    u8* ckpt_posted = nullptr;       // posted bytes at the previous write-back
+    u64 ckpt_pos = 0;                // log position of the first transfer not yet written back
+    u64 ckpt_ts = 0;                 // commit timestamp at the previous write-back
+    bool ckpt_valid = false;         // false: the snapshot is the empty state (zeroes)
     u32 prof_mask = ~0u;  // kernels timed when profiling (1 << K_*; tbgpu_bench_profile_mask)
     u32 ablate = 0;
     std::vector<hipEvent_t> event_pool;
@@ -387,7 +393,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
     if (!E) return;
     (void)hipSetDevice(E->device);
     if (E->stream) (void)hipStreamSynchronize(E->stream);
-    void* bufs[] = {E->T.acct_hot, E->T.acct_bal, E->T.acct_cold, E->T.account_mark, E->T.xidx, E->T.xdup, E->T.xlog,
+    void* bufs[] = {E->ckpt_bal, E->ckpt_posted, E->T.acct_hot, E->T.acct_bal, E->T.acct_cold, E->T.account_mark, E->T.xidx, E->T.xdup, E->T.xlog,
                     E->T.xposted, E->g, E->info, E->eflags, E->dr,
                     E->cr, E->ps, E->rs, E->dep_list, E->dep_count, E->amt, E->kid, E->kpid, E->dedup,
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
@@ -409,6 +415,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
 
 extern "C" int tbgpu_reset(tbgpu_t* E) {
     HIPCK(hipSetDevice(E->device));
+    E->ckpt_valid = false;
     return engine_clear(E);
 }
 
@@ -894,6 +901,107 @@ extern "C" int tbgpu_export_posted(tbgpu_t* E, uint64_t* out_pairs, uint64_t cap
     return TBGPU_STATUS_OK;
 }
 
+// Groove write-back: everything a durable replica's checkpoint / compact must insert or upsert into
+// its forest since the previous call (or since init / reset) — state_machine.zig:542-582 with the
+// groove semantics of src/lsm/groove.zig:902-963.  Accounts by id, transfers and posted pairs by
+// timestamp.  If a buffer is too small nothing advances: *counts holds the sizes needed.
+extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, uint64_t accounts_cap, void* transfers_out,
+                                      uint64_t transfers_cap, uint64_t* posted_out, uint64_t posted_cap,
+                                      tbgpu_delta_counts* counts) {
+    HIPCK(hipSetDevice(E->device));
+    memset(counts, 0, sizeof(*counts));
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    if (!E->ckpt_bal) {
+        HIPCK(hipMalloc(&E->ckpt_bal, E->account_cap * sizeof(AccountBal)));
+        HIPCK(hipMalloc(&E->ckpt_posted, E->xlog_cap));
+    }
+    if (!E->ckpt_valid) {  // the previous write-back is the empty state
+        HIPCK(hipMemsetAsync(E->ckpt_bal, 0, E->account_cap * sizeof(AccountBal), E->stream));
+        HIPCK(hipMemsetAsync(E->ckpt_posted, 0, E->xlog_cap, E->stream));
+        E->ckpt_pos = 0;
+        E->ckpt_ts = 0;
+    }
+    const u64 chunk = 1ULL << 20;
+    std::vector<u8> accts, xfers;
+    std::vector<u64> posted;
+    u8* d_out = nullptr;
+    u64* d_cnt = nullptr;
+    u64* d_posted = nullptr;
+    hipError_t err = hipMalloc(&d_out, chunk * 128);
+    if (err == hipSuccess) err = hipMalloc(&d_cnt, 24);
+    if (err == hipSuccess) err = hipMalloc(&d_posted, chunk * 16);
+    for (int pass = 0; pass < 2 && err == hipSuccess; pass++) {
+        const u64 cap = pass == 0 ? E->account_cap : E->xidx_cap;
+        for (u64 s = 0; s < cap && err == hipSuccess; s += chunk) {
+            const u64 n = std::min<u64>(chunk, cap - s);
+            err = hipMemsetAsync(d_cnt, 0, 24, E->stream);
+            if (err != hipSuccess) break;
+            if (pass == 0) {
+                hipLaunchKernelGGL(tb_delta_accounts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T,
+                                   E->ckpt_bal, E->ckpt_ts, s, s + n, d_out, chunk, d_cnt);
+            } else {
+                hipLaunchKernelGGL(tb_delta_transfers, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T,
+                                   E->ckpt_posted, E->ckpt_pos, s, n, d_out, chunk, d_cnt, d_posted, chunk, d_cnt + 1);
+            }
+            err = hipGetLastError();
+            u64 cnt[2] = {0, 0};
+            if (err == hipSuccess) err = hipMemcpyAsync(cnt, d_cnt, 16, hipMemcpyDeviceToHost, E->stream);
+            if (err == hipSuccess) err = hipStreamSynchronize(E->stream);
+            std::vector<u8>& recs = pass == 0 ? accts : xfers;
+            if (err == hipSuccess && cnt[0]) {  // one chunk of slots holds at most `chunk` objects
+                const size_t at = recs.size();
+                recs.resize(at + cnt[0] * 128);
+                err = hipMemcpy(recs.data() + at, d_out, cnt[0] * 128, hipMemcpyDeviceToHost);
+            }
+            if (err == hipSuccess && cnt[1]) {
+                const size_t at = posted.size();
+                posted.resize(at + cnt[1] * 2);
+                err = hipMemcpy(posted.data() + at, d_posted, cnt[1] * 16, hipMemcpyDeviceToHost);
+            }
+        }
+    }
+    (void)hipFree(d_out);
+    (void)hipFree(d_cnt);
+    (void)hipFree(d_posted);
+    if (err != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "checkpoint delta: %s", hipGetErrorString(err));
+    const u64 na = accts.size() / 128, nt = xfers.size() / 128, np = posted.size() / 2;
+    counts->accounts = na;
+    counts->transfers = nt;
+    counts->posted = np;
+    if (na > accounts_cap || nt > transfers_cap || np > posted_cap) {
+        return fail(TBGPU_STATUS_INVALID, "checkpoint delta: needs %llu accounts, %llu transfers, %llu posted",
+                    (unsigned long long)na, (unsigned long long)nt, (unsigned long long)np);
+    }
+    auto ts_of = [](const u8* r) { return *(const u64*)(r + 120); };
+    std::vector<u64> idx(na);
+    for (u64 i = 0; i < na; i++) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](u64 a, u64 b) { return id_less(&accts[a * 128], &accts[b * 128]); });
+    for (u64 i = 0; i < na; i++) memcpy((u8*)accounts_out + i * 128, &accts[idx[i] * 128], 128);
+    idx.resize(nt);
+    for (u64 i = 0; i < nt; i++) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](u64 a, u64 b) { return ts_of(&xfers[a * 128]) < ts_of(&xfers[b * 128]); });
+    for (u64 i = 0; i < nt; i++) memcpy((u8*)transfers_out + i * 128, &xfers[idx[i] * 128], 128);
+    std::vector<std::pair<u64, u64>> pairs(np);
+    for (u64 i = 0; i < np; i++) pairs[i] = {posted[2 * i], posted[2 * i + 1]};
+    std::sort(pairs.begin(), pairs.end());
+    for (u64 i = 0; i < np; i++) {
+        posted_out[2 * i] = pairs[i].first;
+        posted_out[2 * i + 1] = pairs[i].second;
+    }
+    // Advance the snapshot.
+    HIPCK(hipMemcpyAsync(E->ckpt_bal, E->T.acct_bal, E->account_cap * sizeof(AccountBal), hipMemcpyDeviceToDevice,
+                         E->stream));
+    if (E->log_next) HIPCK(hipMemcpyAsync(E->ckpt_posted, E->T.xposted, E->log_next, hipMemcpyDeviceToDevice, E->stream));
+    HIPCK(hipStreamSynchronize(E->stream));
+    E->ckpt_pos = E->log_next;
+    E->ckpt_ts = E->commit_ts;
+    E->ckpt_valid = true;
+    return TBGPU_STATUS_OK;
+}
+
 extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     HIPCK(hipSetDevice(E->device));
     if (E->pending) {
@@ -1056,6 +1164,7 @@ extern "C" int tbgpu_bench_reset_transfers(tbgpu_t* E) {
     hipLaunchKernelGGL(tb_zero_balances, dim3((unsigned)((E->account_cap + 255) / 256)), dim3(256), 0, E->stream, E->T,
                        E->account_cap);
     E->log_next = 0;
+    E->ckpt_valid = false;
     HIPCK(hipGetLastError());
     HIPCK(hipStreamSynchronize(E->stream));
     return TBGPU_STATUS_OK;

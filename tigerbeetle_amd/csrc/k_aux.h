@@ -88,3 +88,46 @@ __global__ void tb_zero_balances(Tables T, u64 cap) {
     if (i >= cap) return;
     T.acct_bal[i] = AccountBal{0, 0, 0, 0};
 }
+
+// ---- groove write-back (StateMachine.checkpoint, state_machine.zig:542-582) --------------------
+// The objects a durable replica must insert / upsert into its forest since the previous write-back:
+// accounts created since (timestamp > ts0) or whose balances differ from the snapshot taken then,
+// transfers created since (log position >= pos0), and posted-groove entries whose state changed.
+// The snapshot is a copy of the balance array and of the posted bytes: a diff stream instead of a
+// dirty mark in every balance-writing kernel of the hot path.  Counts past `cap` are still counted
+// (the host retries with room).
+__global__ void tb_delta_accounts(Tables T, const AccountBal* snap, u64 ts0, u64 first, u64 last, u8* out, u64 cap,
+                                  u64* count) {
+    const u64 i = first + (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= last) return;
+    const AccountHot& h = T.acct_hot[i];
+    if (h.timestamp == 0 || tb_id_reserved(h.id_lo, h.id_hi)) return;
+    const AccountBal b = T.acct_bal[i], s = snap[i];
+    const bool same = b.debits_pending == s.debits_pending && b.debits_posted == s.debits_posted &&
+                      b.credits_pending == s.credits_pending && b.credits_posted == s.credits_posted;
+    if (h.timestamp <= ts0 && same) return;
+    const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
+    if (k < cap) *(Account*)(out + k * 128) = tb_account_load(T, (u32)i);
+}
+
+__global__ void tb_delta_transfers(Tables T, const u8* snap_posted, u64 pos0, u64 first, u64 n, u8* out, u64 cap,
+                                   u64* count, u64* posted_out, u64 posted_cap, u64* posted_count) {
+    const u64 i = first + (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= first + n) return;
+    const u64 e = T.xidx[i];
+    if (e == 0 || (e & XI_TOMB)) return;
+    const u32 pos = tb_xi_pos(e);
+    const Transfer& t = T.xlog[pos];
+    if (pos >= pos0) {
+        const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
+        if (k < cap) *(Transfer*)(out + k * 128) = t;
+    }
+    const u8 st = T.xposted[pos];
+    if (st != snap_posted[pos]) {
+        const u64 q = atomicAdd((unsigned long long*)posted_count, 1ULL);
+        if (q < posted_cap) {
+            posted_out[2 * q] = t.timestamp;
+            posted_out[2 * q + 1] = st == POSTED_POSTED ? 0 : 1;
+        }
+    }
+}

@@ -12,8 +12,9 @@ The reference's replica drives a comptime duck-typed `StateMachineType`
 
 `StateMachine` below keeps that shape; `commit` crosses into HIP through the C ABI
 (include/tbgpu.h).  Objects live in HBM, so `prefetch` completes immediately (its callback fires
-synchronously, which the reference allows: src/lsm/groove.zig:723-742), and `compact` /
-`checkpoint` have nothing to persist (durability is out of scope this round).
+synchronously, which the reference allows: src/lsm/groove.zig:723-742).  `checkpoint` hands the
+objects changed since the previous checkpoint (tbgpu_checkpoint_delta) to an optional write-back
+sink — what a durable replica inserts / upserts into its forest; `compact` has nothing to do.
 """
 import ctypes
 from dataclasses import dataclass
@@ -149,6 +150,24 @@ class Engine:
 
     PROF_VALIDATE, PROF_RESOLVE, PROF_REPLAY, PROF_CLEAR, PROF_PASS, PROF_APPLY, PROF_ALL = 1, 2, 4, 8, 16, 32, 63
 
+    def checkpoint_delta(self):
+        """Objects changed since the previous call (groove write-back): a Delta of accounts (by
+        id), transfers (by timestamp) and posted pairs {pending timestamp, fulfillment}."""
+        counts = _lib.tbgpu_delta_counts()
+        caps = [1024, 1024, 1024]
+        while True:
+            a = np.zeros(caps[0], dtype=ACCOUNT_DTYPE)
+            t = np.zeros(caps[1], dtype=TRANSFER_DTYPE)
+            p = np.zeros((caps[2], 2), dtype=np.uint64)
+            st = self.lib.tbgpu_checkpoint_delta(self.h, a.ctypes.data, caps[0], t.ctypes.data, caps[1], p.ctypes.data,
+                                                 caps[2], ctypes.byref(counts))
+            need = [counts.accounts, counts.transfers, counts.posted]
+            if st == _lib.STATUS_INVALID and any(n > c for n, c in zip(need, caps)):
+                caps = [max(c, n) for c, n in zip(caps, need)]
+                continue
+            _lib.check(st)
+            return Delta(a[:need[0]], t[:need[1]], p[:need[2]])
+
     def legs_min_events(self, events):
         """Passes of >= events transfers use the sorted balance legs (0: every pass)."""
         _lib.check(self.lib.tbgpu_bench_legs_min_events(self.h, int(events)))
@@ -237,14 +256,23 @@ class Engine:
         return self.lib.tbgpu_marker_elapsed_ms(self.h, a, b)
 
 
+@dataclass
+class Delta:
+    """One groove write-back (tbgpu_checkpoint_delta)."""
+    accounts: np.ndarray
+    transfers: np.ndarray
+    posted: np.ndarray
+
+
 class StateMachine:
     """The reference's StateMachine interface over one Engine."""
 
     Operation = Operation
     batch_max = BATCH_MAX
 
-    def __init__(self, options=None, **kw):
+    def __init__(self, options=None, write_back=None, **kw):
         self.engine = Engine(options, **kw)
+        self.write_back = write_back  # called by checkpoint with a Delta
         self.prepare_timestamp = 0
         self.commit_timestamp = 0
 
@@ -284,4 +312,7 @@ class StateMachine:
         callback(self)
 
     def checkpoint(self, callback):
+        delta = self.engine.checkpoint_delta()
+        if self.write_back is not None:
+            self.write_back(delta)
         callback(self)
