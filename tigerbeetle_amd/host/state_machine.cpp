@@ -1,6 +1,7 @@
 // state_machine.cpp — tb::StateMachine over the C ABI (include/tbgpu.h).  See state_machine.hpp.
 #include "state_machine.hpp"
 
+#include <algorithm>
 #include <cstring>
 
 namespace tb {
@@ -123,11 +124,40 @@ std::vector<size_t> StateMachine::commit_many(Operation operation, const std::ve
 
 void StateMachine::compact(const Callback& callback, uint64_t op) {
     (void)op;
-    // Durability (groove write-back to the LSM forest) is out of scope this round.
+    // The HBM tables need no compaction; the forest write-back happens at checkpoint().
     callback(*this);
 }
 
-void StateMachine::checkpoint(const Callback& callback) { callback(*this); }
+Delta StateMachine::checkpoint_delta() {
+    Delta d;
+    tbgpu_delta_counts counts{1024, 1024, 1024};
+    for (;;) {
+        d.accounts.resize(counts.accounts * 128);
+        d.transfers.resize(counts.transfers * 128);
+        d.posted.resize(counts.posted * 2);
+        const uint64_t caps[3] = {counts.accounts, counts.transfers, counts.posted};
+        const int st = tbgpu_checkpoint_delta(engine_, d.accounts.data(), caps[0], d.transfers.data(), caps[1],
+                                              d.posted.data(), caps[2], &counts);
+        if (st == TBGPU_STATUS_INVALID &&
+            (counts.accounts > caps[0] || counts.transfers > caps[1] || counts.posted > caps[2])) {
+            counts.accounts = std::max(counts.accounts, caps[0]);
+            counts.transfers = std::max(counts.transfers, caps[1]);
+            counts.posted = std::max(counts.posted, caps[2]);
+            continue;  // room for everything, then retry (nothing advanced)
+        }
+        check(st, "checkpoint_delta");
+        d.accounts.resize(counts.accounts * 128);
+        d.transfers.resize(counts.transfers * 128);
+        d.posted.resize(counts.posted * 2);
+        return d;
+    }
+}
+
+void StateMachine::checkpoint(const Callback& callback) {
+    const Delta d = checkpoint_delta();
+    if (write_back) write_back(d);
+    callback(*this);
+}
 
 void StateMachine::test_set_balances(u128 id, u128 dp, u128 dpost, u128 cp, u128 cpost) {
     const uint64_t b[8] = {(uint64_t)dp, (uint64_t)(dp >> 64), (uint64_t)dpost, (uint64_t)(dpost >> 64),

@@ -140,9 +140,19 @@ struct DeviceError : std::runtime_error {
     using std::runtime_error::runtime_error;
 };
 
+// One groove write-back (tbgpu_checkpoint_delta): what checkpoint() hands to the durable
+// replica's forest — accounts (128-B records, by id), transfers (by timestamp), posted pairs
+// {pending timestamp, fulfillment} (by timestamp).
+struct Delta {
+    std::vector<uint8_t> accounts;
+    std::vector<uint8_t> transfers;
+    std::vector<uint64_t> posted;
+};
+
 class StateMachine {
 public:
     using Callback = std::function<void(StateMachine&)>;
+    using WriteBack = std::function<void(const Delta&)>;
 
     explicit StateMachine(const Options& options);
     ~StateMachine();
@@ -162,7 +172,11 @@ public:
                                     const std::vector<const void*>& inputs, const std::vector<size_t>& input_lens,
                                     const std::vector<void*>& outputs);
     void compact(const Callback& callback, uint64_t op);
+    // Hands the objects changed since the previous checkpoint to `write_back` (if set), then calls
+    // back (state_machine.zig:565-582).
     void checkpoint(const Callback& callback);
+    Delta checkpoint_delta();
+    WriteBack write_back;
 
     // Test-only: the table harness `setup` action (state_machine.zig:1398-1407).
     void test_set_balances(u128 account_id, u128 debits_pending, u128 debits_posted, u128 credits_pending,
