@@ -231,8 +231,13 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
         }
     }
     AccountHot dr = {}, cr = {};
-    const u32 drs = fake ? (u32)(dlo & 1023) : tb_account_find_from(T, dlo, dhi, dpos, d0, &dr);
-    const u32 crs = fake ? (u32)(clo & 1023) : tb_account_find_from(T, clo, chi, cpos, c0, &cr);
+    u32 drs, crs;
+    if (fake) {
+        drs = (u32)(dlo & 1023);
+        crs = (u32)(clo & 1023);
+    } else {
+        tb_account_find2(T, dlo, dhi, dpos, d0, clo, chi, cpos, c0, &drs, &crs, &dr, &cr);
+    }
     if (drs == TB_NOT_FOUND) return CT_DEBIT_ACCOUNT_NOT_FOUND;
     if (crs == TB_NOT_FOUND) return CT_CREDIT_ACCOUNT_NOT_FOUND;
     if (!(ts > dr.timestamp) || !(ts > cr.timestamp)) return TB_CODE_PANIC;  // :817-818

@@ -278,6 +278,80 @@ __device__ static inline u32 tb_account_find_from(const Tables& T, u64 lo, u64 h
     return TB_NOT_FOUND;
 }
 
+// Both accounts of a transfer at once (kernel 1).  Their first entries were loaded together; the
+// two chains then advance together — a wave waits for the longer chain, not for the sum of both —
+// two entries per account per round, reading only the 16-B ids (one 32-B span); a hit found in the
+// chain has its full entry read once at the end (its line was just fetched).  At load 1/2 the
+// longest of 128 chains in a wave is ~8 entries: ~4 rounds instead of ~2 x 8.
+__device__ static inline void tb_account_find2(const Tables& T, u64 dlo, u64 dhi, u64 dpos, const AccountHot& d0,
+                                               u64 clo, u64 chi, u64 cpos, const AccountHot& c0, u32* drs, u32* crs,
+                                               AccountHot* dh, AccountHot* ch) {
+    const u64 mask = T.account_mask;
+    u32 ds = TB_NOT_FOUND, cs = TB_NOT_FOUND;
+    bool dgo = false, cgo = false, dlate = false, clate = false;
+    if (d0.id_lo == dlo && d0.id_hi == dhi) {
+        ds = (u32)dpos;
+        *dh = d0;
+    } else {
+        dgo = (d0.id_lo | d0.id_hi) != 0;
+    }
+    if (c0.id_lo == clo && c0.id_hi == chi) {
+        cs = (u32)cpos;
+        *ch = c0;
+    } else {
+        cgo = (c0.id_lo | c0.id_hi) != 0;
+    }
+    u64 dp = (dpos + 1) & mask, cp = (cpos + 1) & mask;
+    for (u64 n = 0; (dgo || cgo) && n <= mask; n += 2) {
+        ulonglong2 da = {0, 0}, db = {0, 0}, ca = {0, 0}, cb = {0, 0};
+        const u64 dq = (dp + 1) & mask, cq = (cp + 1) & mask;
+        if (dgo) {
+            da = *(const ulonglong2*)&T.acct_hot[dp];
+            db = *(const ulonglong2*)&T.acct_hot[dq];
+        }
+        if (cgo) {
+            ca = *(const ulonglong2*)&T.acct_hot[cp];
+            cb = *(const ulonglong2*)&T.acct_hot[cq];
+        }
+        if (dgo) {
+            if (da.x == dlo && da.y == dhi) {
+                ds = (u32)dp;
+                dgo = false;
+                dlate = true;
+            } else if ((da.x | da.y) == 0) {
+                dgo = false;
+            } else if (db.x == dlo && db.y == dhi) {
+                ds = (u32)dq;
+                dgo = false;
+                dlate = true;
+            } else if ((db.x | db.y) == 0) {
+                dgo = false;
+            }
+            dp = (dp + 2) & mask;
+        }
+        if (cgo) {
+            if (ca.x == clo && ca.y == chi) {
+                cs = (u32)cp;
+                cgo = false;
+                clate = true;
+            } else if ((ca.x | ca.y) == 0) {
+                cgo = false;
+            } else if (cb.x == clo && cb.y == chi) {
+                cs = (u32)cq;
+                cgo = false;
+                clate = true;
+            } else if ((cb.x | cb.y) == 0) {
+                cgo = false;
+            }
+            cp = (cp + 2) & mask;
+        }
+    }
+    if (dlate) *dh = T.acct_hot[ds];
+    if (clate) *ch = T.acct_hot[cs];
+    *drs = ds;
+    *crs = cs;
+}
+
 __device__ static inline u32 tb_account_claim(const Tables& T, u64 lo, u64 hi, u64 ts) {
     u64 pos = tb_hash_id(lo, hi) & T.account_mask;
     for (u64 n = 0; n <= T.account_mask; n++) {
