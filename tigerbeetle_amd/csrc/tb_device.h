@@ -455,26 +455,21 @@ __device__ static inline u32 tb_transfer_claim(const Tables& T, u64 lo, u64 hi, 
                                                u32* found, u32* entry, u64 first = ~0ULL) {
     const u64 fp = tb_fp32(lo, hi);
     const u64 mine = (fp << 32) | ((u64)log_pos + 1);
-    u64 pos = tb_hash_id(lo, hi) & T.xidx_mask;
-    for (u64 n = 0; n <= T.xidx_mask; n++) {
-        u64* e = &T.xidx[pos];
-        const bool home_cas = n == 0 && first != ~0ULL;
-        if (home_cas && first == 0) {  // the home CAS already claimed the entry
-            *entry = (u32)pos;
-            return CLAIM_NEW;
-        }
-        u64 cur = home_cas ? first : *(volatile u64*)e;
+    const u64 mask = T.xidx_mask;
+    u64 pos = tb_hash_id(lo, hi) & mask;
+    // One entry: claim it if empty, else decide on its fingerprint.  Returns CLAIM_FULL to go on.
+    auto step = [&](u64 p, u64 cur) -> u32 {
         if (cur == 0) {
-            cur = atomicCAS((unsigned long long*)e, 0ULL, (unsigned long long)mine);
+            cur = atomicCAS((unsigned long long*)&T.xidx[p], 0ULL, (unsigned long long)mine);
             if (cur == 0) {
-                *entry = (u32)pos;
+                *entry = (u32)p;
                 return CLAIM_NEW;
             }
         }
         if ((cur >> 32) == fp && !(cur & XI_TOMB)) {
             const u32 lp = tb_xi_pos(cur);
             if ((u64)lp >= pass_base) {
-                T.xdup[pos] = 1;
+                T.xdup[p] = 1;
                 return CLAIM_COLLIDED;
             }
             const u64* idw = (const u64*)&T.xlog[lp];
@@ -483,7 +478,30 @@ __device__ static inline u32 tb_transfer_claim(const Tables& T, u64 lo, u64 hi, 
                 return CLAIM_EXISTS;
             }
         }
-        pos = (pos + 1) & T.xidx_mask;
+        return CLAIM_FULL;
+    };
+    u64 n = 0;
+    if (first != ~0ULL) {  // the caller's home CAS returned `first`
+        if (first == 0) {
+            *entry = (u32)pos;
+            return CLAIM_NEW;
+        }
+        const u32 r = step(pos, first);
+        if (r != CLAIM_FULL) return r;
+        pos = (pos + 1) & mask;
+        n = 1;
+    }
+    // The chain, two entries per read round (entries never return to empty, so a value read before
+    // the first one's CAS is still a valid lower bound for the second).
+    for (; n <= mask; n += 2) {
+        const u64 q = (pos + 1) & mask;
+        const u64 e0 = *(volatile u64*)&T.xidx[pos];
+        const u64 e1 = *(volatile u64*)&T.xidx[q];
+        u32 r = step(pos, e0);
+        if (r != CLAIM_FULL) return r;
+        r = step(q, e1);
+        if (r != CLAIM_FULL) return r;
+        pos = (q + 1) & mask;
     }
     tb_panic(T.g, PANIC_TABLE_FULL);
     return CLAIM_FULL;
