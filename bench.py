@@ -372,6 +372,8 @@ def main():
         "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3), "p100": round(float(lat.max()), 3),
                              "definition": "device time of the pass that answers the prepare (%d prepares/pass)" % args.pass_batches},
         "dependent_events": stats["dependent_events"],
+        "flow": {k: (round(stats[k], 3) if isinstance(stats[k], float) else stats[k])
+                 for k in ("flow_units", "flow_runs", "flow_run_units", "flow_plan_ms", "flow_run_ms")},
         "failed_events": n_failed,
         "roofline": roof,
         "cpu_baseline": cpu,

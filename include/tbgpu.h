@@ -147,6 +147,8 @@ typedef struct tbgpu_stats {
     uint64_t flow_units;         /* chains / single dependent events the flow path executed */
     uint64_t flow_runs;          /* runs: single-resource sequences walked with the balance in registers */
     uint64_t flow_run_units;     /* units covered by runs */
+    double flow_plan_ms;         /* tb_flow wall time planning the dependent events (workgroup 0) */
+    double flow_run_ms;          /* tb_flow wall time executing them in order (workgroup 0) */
 } tbgpu_stats;
 
 int tbgpu_get_stats(tbgpu_t* engine, tbgpu_stats* stats);

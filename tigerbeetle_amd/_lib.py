@@ -52,6 +52,8 @@ class tbgpu_stats(ctypes.Structure):
         ("flow_units", ctypes.c_uint64),
         ("flow_runs", ctypes.c_uint64),
         ("flow_run_units", ctypes.c_uint64),
+        ("flow_plan_ms", ctypes.c_double),
+        ("flow_run_ms", ctypes.c_double),
     ]
 
 

@@ -124,6 +124,7 @@ struct tbgpu {
 
     bool profile = false;
     u32 legs_min = LEGS_MIN_EVENTS;
+    u64 wall_khz = 0;  // device wall clock (flow phase timing)
     // Groove write-back snapshot (tbgpu_checkpoint_delta), allocated on first use.
     AccountBal* ckpt_bal = nullptr;  // balances at the previous write-back
     u8* ckpt_posted = nullptr;       // posted bytes at the previous write-back
@@ -313,6 +314,7 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
             if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, E->device) != hipSuccess) khz = 0;
             khz = std::max(khz, 100000);  // s_memrealtime: 100 MHz on gfx9 parts; never trust a lower figure
             E->F.stall_ticks = 60ULL * 1000ULL * (u64)khz;  // 60 s
+            E->wall_khz = (u64)khz;
             if (getenv("TBGPU_DEBUG")) {
                 fprintf(stderr, "tbgpu: flow grid %u, occupancy %d, wall clock %d kHz, stall ticks %llu\n", E->F.grid,
                         occ, khz, (unsigned long long)E->F.stall_ticks);
@@ -357,6 +359,7 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         INIT_CK(hipMalloc(&F.nacct, pe * 4));
         INIT_CK(hipMalloc(&F.rpos, pe * 4));
         INIT_CK(hipMalloc(&F.succ, pe * 4 * FLOW_RMAX));
+        INIT_CK(hipMalloc(&F.run, pe * sizeof(RunEntry) * FLOW_RMAX));
         for (int k = 0; k < 2; k++) {
             INIT_CK(hipMalloc(&F.keys[k], pe * 4 * FLOW_RMAX));
             INIT_CK(hipMalloc(&F.vals[k], pe * 4 * FLOW_RMAX));
@@ -400,7 +403,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->r_home,
                     E->r_block_counts, E->r_words, E->r_meta, E->leg_ev, E->leg_w, E->leg_off,
                     E->F.f_pe, E->F.f_batch, E->F.f_len, E->F.need, E->F.nsucc, E->F.queue, E->F.uflags, E->F.nacct, E->F.rpos, E->F.succ,
-                    E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo};
+                    E->F.run, E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo};
     for (void* p : bufs) if (p) (void)hipFree(p);
     if (E->h_meta) (void)hipHostFree(E->h_meta);
     if (E->h_globals) (void)hipHostFree(E->h_globals);
@@ -1030,6 +1033,8 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     s->flow_units = g.flow_units;
     s->flow_runs = g.flow_runs;
     s->flow_run_units = g.flow_run_units;
+    s->flow_plan_ms = E->wall_khz ? (double)g.flow_plan_ticks / E->wall_khz : 0.0;
+    s->flow_run_ms = E->wall_khz ? (double)g.flow_run_ticks / E->wall_khz : 0.0;
     return TBGPU_STATUS_OK;
 }
 

@@ -41,6 +41,15 @@
 enum : u32 { FW_NUNITS = 0, FW_QTAIL = 1, FW_SEQ = 2, FW_WORDS = 8 };
 enum : u32 { UF_ID_SINGLE = 1 };  // the unit is the only dependent event of the pass naming its id
 
+// Everything a run needs of the unit at sorted position q, packed by the planner so the run walker
+// reads one level (the list entry) instead of three (list entry -> unit -> event).
+struct RunEntry {
+    u32 u, pe, dr, cr, rs;
+    u32 flags;  // event flags | RUN_MEMBER
+    u64 amt_lo, amt_hi;
+};
+#define RUN_MEMBER (1u << 16)
+
 struct FlowArgs {
     u32* f_pe;      // [pass events] flat dependent f -> pass-relative event
     u32* f_batch;   // [pass events] f -> call-relative batch
@@ -52,6 +61,7 @@ struct FlowArgs {
     u32* uflags;    // [pass events] per unit head: UF_*
     u32* nacct;     // [pass events] per unit head: account resources
     u32* rpos;      // [pass events] per unit head: sorted position of its (last) account resource
+    RunEntry* run;  // [FLOW_RMAX * pass events] per sorted position (account resources)
     u32* keys[2];   // [FLOW_RMAX * pass events] radix-sort ping-pong buffers
     u32* vals[2];
     u32* hist;      // [grid * 256]
@@ -249,7 +259,7 @@ __device__ static inline u32 fl_run_run(const PassArgs& P, const FlowArgs& F, co
     u32 n = 0, n_ok = 0, last = u, last_ok_pe = TB_NOT_FOUND;
     bool more = true;
     while (more) {
-        // Three dependent load levels for eight candidates at once: list entry, unit, event.
+        // One load level for eight candidates at once: the planner's packed entries (RunEntry).
         u32 cu[FLOW_RUN_STEP], cpe[FLOW_RUN_STEP], cdr[FLOW_RUN_STEP], ccr[FLOW_RUN_STEP], crs_[FLOW_RUN_STEP];
         u64 camt[FLOW_RUN_STEP], camt_hi[FLOW_RUN_STEP];
         u16 cfl[FLOW_RUN_STEP];
@@ -257,25 +267,17 @@ __device__ static inline u32 fl_run_run(const PassArgs& P, const FlowArgs& F, co
 #pragma unroll
         for (u32 j = 0; j < FLOW_RUN_STEP; j++) {
             ok[j] = q + j < N && K[q + j] == r;
-            cu[j] = ok[j] ? V[q + j] : 0;
-        }
-#pragma unroll
-        for (u32 j = 0; j < FLOW_RUN_STEP; j++) {
-            cpe[j] = ok[j] ? F.f_pe[cu[j]] : 0;
-            ok[j] = ok[j] && F.f_len[cu[j]] == 1 && F.nacct[cu[j]] == 1 && (F.uflags[cu[j]] & UF_ID_SINGLE);
-        }
-#pragma unroll
-        for (u32 j = 0; j < FLOW_RUN_STEP; j++) {
-            const u32 pe = cpe[j];
-            const u32 info = ok[j] ? P.info[pe] : 0;
-            cfl[j] = ok[j] ? P.eflags[pe] : 0;
-            cdr[j] = ok[j] ? P.dr[pe] : 0;
-            ccr[j] = ok[j] ? P.cr[pe] : 0;
-            crs_[j] = ok[j] ? P.rs[pe] : 0;
-            camt[j] = ok[j] ? P.amt[2 * pe] : 0;
-            camt_hi[j] = ok[j] ? P.amt[2 * pe + 1] : 0;
-            ok[j] = ok[j] && (info & HZ_SPEC) && (info & HZ_ACCTS) && (info & 0xFF) == R_OK &&
-                    !(cfl[j] & (TF_LINKED | TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT));
+            RunEntry x = {};
+            if (ok[j]) x = F.run[q + j];
+            cu[j] = x.u;
+            cpe[j] = x.pe;
+            cdr[j] = x.dr;
+            ccr[j] = x.cr;
+            crs_[j] = x.rs;
+            cfl[j] = (u16)x.flags;
+            camt[j] = x.amt_lo;
+            camt_hi[j] = x.amt_hi;
+            ok[j] = ok[j] && (x.flags & RUN_MEMBER);
         }
         u32 j = 0;
         for (; j < FLOW_RUN_STEP && ok[j]; j++) {
@@ -387,6 +389,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     bool cert_global, cert64;
     tb_pass_cert(P, S, cert_global, cert64);
     u32 gen = 0;
+    const u64 ft0 = (blockIdx.x == 0 && tid == 0) ? fl_now() : 0;
 
     // ---- plan 1: flat list of dependent events, units, resource pairs ------------------------
     for (u32 k = tid; k < nb; k += NT) s_dpre[k] = P.dep_count[k];
@@ -553,10 +556,33 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
                 F.queue[pos] = f + 1;
             }
         }
+        // Pack the run walker's view of every account-resource position (unit flags are final now).
+        for (u32 q = blockIdx.x * NT + tid; q < N; q += G * NT) {
+            const u32 key = K[q];
+            if (key == FLOW_SENT || (key & 0x80000000u)) continue;
+            const u32 u = V[q];
+            const u32 pe = F.f_pe[u];
+            RunEntry x;
+            x.u = u;
+            x.pe = pe;
+            const bool unit_ok = F.f_len[u] == 1 && F.nacct[u] == 1 && (F.uflags[u] & UF_ID_SINGLE);
+            const u32 info = P.info[pe];
+            const u16 fl = P.eflags[pe];
+            x.dr = P.dr[pe];
+            x.cr = P.cr[pe];
+            x.rs = P.rs[pe];
+            x.amt_lo = P.amt[2 * pe];
+            x.amt_hi = P.amt[2 * pe + 1];
+            const bool member = unit_ok && (info & HZ_SPEC) && (info & HZ_ACCTS) && (info & 0xFF) == R_OK &&
+                                !(fl & (TF_LINKED | TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT));
+            x.flags = fl | (member ? RUN_MEMBER : 0u);
+            F.run[q] = x;
+        }
         fl_grid_sync(g, G, gen, F);
         if (fl_stalled(g)) return;
     }
     if (blockIdx.x != 0) return;
+    const u64 ft1 = tid == 0 ? fl_now() : 0;
 
     // ---- run (workgroup 0) ---------------------------------------------------------------------
     u64 tsmax = 0;
@@ -668,5 +694,10 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     __syncthreads();
     u64 mm = 0;
     for (u32 k = 0; k < NT / 64; k++) mm = max(mm, s_tsmax[k]);
+    if (tid == 0) {
+        const u64 ft2 = fl_now();
+        atomicAdd((unsigned long long*)&g->flow_plan_ticks, (unsigned long long)(ft1 - ft0));
+        atomicAdd((unsigned long long*)&g->flow_run_ticks, (unsigned long long)(ft2 - ft1));
+    }
     fl_finish(P, s_code, s_wave, s_list, mm, true);
 }

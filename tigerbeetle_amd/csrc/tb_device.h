@@ -191,6 +191,8 @@ struct Globals {
     u64 flow_runs;            // runs (k_flow.h) and the units they covered
     u64 flow_run_units;
     u64 limit_accounts;       // accounts ever created with a limit flag (never decremented: an upper bound)
+    u64 flow_plan_ticks;      // tb_flow wall-clock ticks (workgroup 0): planning, then the ordered run
+    u64 flow_run_ticks;
 };
 
 struct AccountHot {
