@@ -236,24 +236,15 @@ __device__ static inline u64 fl_run_unit(const PassArgs& P, const FlowArgs& F, R
 // sorted resource list, eight units per step with their loads issued together.  Kernel 1 already
 // wrote each record; an ok unit revives its index entry, adds its amount to r (registers) and to
 // its free account (atomic delta); a failed one gets exceeds_credits / exceeds_debits.
-__device__ static inline bool fl_run_member(const PassArgs& P, const FlowArgs& F, u32 u, u32 pe) {
-    const u32 info = P.info[pe];
-    return F.f_len[u] == 1 && F.nacct[u] == 1 && (F.uflags[u] & UF_ID_SINGLE) && (info & HZ_SPEC) &&
-           (info & HZ_ACCTS) && (info & 0xFF) == R_OK &&
-           !(P.eflags[pe] & (TF_LINKED | TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT));
-}
-
 #define FLOW_RUN_STEP 8
 
 // Runs the run headed by unit u (a run member); returns the last unit it ran (its successors are
 // released by the caller), *count = units run, *tsmax = max ok timestamp.
+// (q, r): the head's sorted position and its account resource, already read by the caller.
 __device__ static inline u32 fl_run_run(const PassArgs& P, const FlowArgs& F, const Replay& R, u32 u, u32 N,
-                                        u32* count, u64* tsmax) {
+                                        u32 q, u32 r, u32* count, u64* tsmax) {
     const Tables& T = P.T;
     const u32* K = F.keys[0];
-    const u32* V = F.vals[0];
-    u32 q = F.rpos[u];
-    const u32 r = K[q];
     AccountBal B = rp_load<true>(&T.acct_bal[r]);
     const u16 rflags = T.acct_hot[r].flags;
     u32 n = 0, n_ok = 0, last = u, last_ok_pe = TB_NOT_FOUND;
@@ -652,9 +643,20 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
                 u = item - 1;
             }
             u32 ran = 1;
-            if (fl_run_member(P, F, u, F.f_pe[u])) {
+            // Run head?  Two load levels through the packed entry (position, then entry + resource)
+            // instead of the unit's and the event's words.
+            const u32 rq = F.rpos[u];
+            const bool one_acct = F.nacct[u] == 1;
+            bool head = false;
+            u32 rr = 0;
+            if (one_acct && rq < N) {
+                const RunEntry& x = F.run[rq];
+                rr = F.keys[0][rq];
+                head = x.u == u && (x.flags & RUN_MEMBER) && rr != FLOW_SENT && !(rr & 0x80000000u);
+            }
+            if (head) {
                 u64 ts = 0;
-                u = fl_run_run(P, F, R, u, N, &ran, &ts);
+                u = fl_run_run(P, F, R, u, N, rq, rr, &ran, &ts);
                 tsmax = max(tsmax, ts);
                 runs++;
                 run_units += ran;
