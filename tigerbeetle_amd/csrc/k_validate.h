@@ -317,12 +317,16 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
         P.eflags[pe] = t.flags;
         P.dr[pe] = s.dr;
         P.cr[pe] = s.cr;
-        P.ps[pe] = s.ps;
+        // ps and kpid are read only for post/void events (HZ_POSTVOID / HZ_PV_KEY): 12 B per event
+        // of scratch writes skipped for the others.
+        if (s.hz & (HZ_POSTVOID | HZ_PV_KEY)) {
+            P.ps[pe] = s.ps;
+            P.kpid[pe] = s.kpid;
+        }
         P.rs[pe] = s.rs;
         P.amt[2 * pe] = tb_lo(s.amount);
         P.amt[2 * pe + 1] = tb_hi(s.amount);
         P.kid[pe] = s.kid;
-        P.kpid[pe] = s.kpid;
         if (code != R_OK) s.contrib = 0;
         // The record (create_transfer :870) is the event as staged, with its timestamp.
         if (s.rec_ts) *(u64*)(stage + tb_stage_off(threadIdx.x, 7) + 8) = s.rec_ts;  // timestamp @120
