@@ -4,11 +4,15 @@ Workload (BASELINE.json configs[1], "C2"): 1M accounts, 100M uniform-random tran
 no flags), prepares of 8190 events, synthetic data generated on the GPU (tigerbeetle_amd
 k_workload.h, shapes of the reference benchmark client src/benchmark.zig:223-327).
 
-A step = committing all 100M transfers (12,211 prepares) from the post-account-creation state,
-inputs already resident in HBM.  Between steps the transfer store and balances are restored
-(untimed), so every step commits the same 100M transfers.  Each timed step is bracketed by a
-barrier + torch.cuda.synchronize(); value = transfers committed by all ranks / Σ step time (max
-over ranks).
+A step = committing all 100M transfers (12,211 prepares) from the post-account-creation state, as
+the metric defines it: from the first H2D to the last reply D2H.  The prepare
+bodies sit in host memory registered once (the replica's message pool); tbgpu_commit_pipelined
+moves chunk c+1 (64 prepares) over PCIe while chunk c commits, and each chunk's replies land in
+host memory as soon as it is committed.  Between steps the transfer store and balances are
+restored (untimed), so every step commits the same 100M transfers.  Each timed step is bracketed
+by a barrier + torch.cuda.synchronize(); value = transfers committed by all ranks / Σ step time
+(max over ranks).  `device_resident` is the same commit with the prepares already in HBM (the
+engine's own rate, no PCIe); `pcie` is the host-link rate the headline reaches.
 
 --gpus N (torchrun): one process per GPU over RCCL (tigerbeetle_amd.sharded).  The
 accounts are replicated (every rank commits the same create_accounts prepares); every rank
@@ -41,6 +45,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "transfers/sec committed (whole node, bit-exact results) + p99 batch latency"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+PCIE_PEAK_GBS = 63.0   # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s spec
 
 
 def parse():
@@ -51,7 +56,10 @@ def parse():
     p.add_argument("--accounts", type=int, default=1_000_000)
     p.add_argument("--transfers", type=int, default=100_000_000)
     p.add_argument("--batch", type=int, default=8190)
-    p.add_argument("--pass-batches", type=int, default=512)
+    p.add_argument("--pass-batches", type=int, default=512, help="prepares per device pass (device-resident leg)")
+    p.add_argument("--chunk-prepares", type=int, default=64,
+                   help="prepares per pipelined chunk of the headline (host memory -> PCIe -> commit -> reply)")
+    p.add_argument("--device-steps", type=int, default=3, help="timed steps of the HBM-resident secondary leg")
     p.add_argument("--cpu-sample", type=int, default=12_285_000, help="transfers in the CPU baseline / parity sample (0: skip)")
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"],
@@ -79,6 +87,19 @@ def timestamps(lens, start, gap_every=0):
 def expected_unique(accounts, legs):
     """Expected number of distinct accounts touched by `legs` uniform draws."""
     return accounts * (1.0 - math.exp(-legs / accounts))
+
+
+def ref_percentile(sorted_ms, p):
+    """The reference's percentile pick (src/benchmark.zig:454-471): latencies[len * p / 100 -| 1]."""
+    if len(sorted_ms) == 0:
+        return float("nan")
+    return float(sorted_ms[max(0, len(sorted_ms) * p // 100 - 1)])
+
+
+def deciles(sorted_ms):
+    out = {"p%02d" % (10 * d): round(ref_percentile(sorted_ms, 10 * d), 3) for d in range(11)}
+    out["p99"] = round(ref_percentile(sorted_ms, 99), 3)
+    return out
 
 
 def run_host_commits(engine, args, events_dev, t_cursor):
@@ -169,7 +190,35 @@ def run_cpu_baseline(engine, args, acct_lens, acct_ts, events_dev, sample_lens, 
                   "%s" % (n_sample, len(sample_lens), args.batch, cpu_model()),
         "p99_batch_latency_ms": float(np.percentile(lat, 99)),
         "seconds": dt,
+        "c1": run_cpu_c1(engine, args),
     }, oracle, replies
+
+
+def run_cpu_c1(engine, args):
+    """BASELINE.json configs[0] (scripts/benchmark.sh, src/benchmark.zig:22-24): 10k accounts, 1M
+    uniform transfers in prepares of 8190, committed by the oracle on one host core."""
+    from tests.harness.configs import generate, split
+    from tests.harness.oracle import OracleEngine
+
+    n_acct, n_xfer = 10_000, 1_000_000
+    accts, xfers = generate(engine, "c2", n_acct, n_xfer, seed=args.seed)
+    a_lens, x_lens = batches(n_acct, args.batch), batches(n_xfer, args.batch)
+    a_ts, t = timestamps(a_lens, 10**12)
+    x_ts, _ = timestamps(x_lens, t + 10)
+    oracle = OracleEngine(n_acct, n_xfer)
+    assert all(r == b"" for r in oracle.commit_many(128, a_ts, split(accts, a_lens)))
+    bodies = split(xfers, x_lens)
+    lat = []
+    t0 = time.perf_counter()
+    for ts, body in zip(x_ts, bodies):
+        b0 = time.perf_counter()
+        assert oracle.commit(129, ts, body) == b"", "C1 transfer failed on the oracle"
+        lat.append(time.perf_counter() - b0)
+    dt = time.perf_counter() - t0
+    lat = np.sort(np.array(lat) * 1e3)
+    return {"value": round(n_xfer / dt, 1), "unit": "transfers/s", "cores": 1, "kind": "port",
+            "sample": "C1 in full: 10000 accounts, 1000000 transfers, %d prepares of %d" % (len(x_lens), args.batch),
+            "p99_batch_latency_ms": round(ref_percentile(lat, 99), 3)}
 
 
 def cpu_model():
@@ -270,10 +319,14 @@ def main():
                               limit_permille=wl["limit_permille"])
     engine.sync()
 
-    # Warmup steps time every kernel (the per-kernel breakdown); timed steps time only the kernel
-    # the roofline is quoted on (validate) and whole passes (batch latency): every HIP event pair on
-    # the stream costs a little (all six kernels timed: ~9 % of a step).
-    step_ms = []
+    # -- headline: the replica's batched commit from host memory (PCIe both ways) --------------
+    # throughput = transfers / wall time from the first H2D to the last reply D2H.
+    # The prepares sit in host memory registered once (the replica's message pool), and
+    # tbgpu_commit_pipelined moves chunk c+1 over PCIe while chunk c commits.
+    host_events = engine.to_host(events_dev, args.transfers * 128)
+    engine.register_host(host_events)
+    replies = np.empty(args.transfers * 8, dtype=np.uint8)
+    step_ms, lat_all = [], []
     t_cursor = t_end
     breakdown = None
     if args.warmup:
@@ -286,18 +339,42 @@ def main():
             if args.warmup:
                 breakdown = engine.stats()
             engine.reset_stats()
-            engine.profile_mask(engine.PROF_VALIDATE | engine.PROF_PASS | engine.PROF_REPLAY)
+            engine.profile_mask(engine.PROF_VALIDATE | engine.PROF_REPLAY)
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        engine.commit_device_async(129, ts, xfer_lens, events_dev, res_dev, rb_dev)
-        engine.sync()
+        rb_h, _, lat = engine.commit_pipelined(129, ts, xfer_lens, host_events, chunk_batches=args.chunk_prepares,
+                                               latency=True, replies=replies)
         torch.cuda.synchronize()
         barrier()
         dt = time.perf_counter() - t0
         if timed:
             step_ms.append(allmax(dt * 1e3))
+            lat_all.append(lat)
     stats = engine.stats()
+    n_failed_host = int(rb_h.sum()) // 8
+    engine.unregister_host(host_events)
+    del host_events
+    lat = np.sort(np.concatenate(lat_all))
+
+    # -- secondary: the same commits with the prepares already resident in HBM ----------------
+    dev_ms = []
+    engine.profile_mask(engine.PROF_VALIDATE | engine.PROF_PASS | engine.PROF_REPLAY)
+    dev_stats = None
+    for step in range(1 + args.device_steps):
+        engine.reset_transfers()
+        ts, t_cursor = timestamps(xfer_lens, t_cursor + 10, wl["gap_every"])
+        if step == 1:
+            engine.reset_stats()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        engine.commit_device_async(129, ts, xfer_lens, events_dev, res_dev, rb_dev)
+        engine.sync()
+        torch.cuda.synchronize()
+        if step >= 1:
+            dev_ms.append((time.perf_counter() - t0) * 1e3)
+    if args.device_steps:
+        dev_stats = engine.stats()
     pass_lat = engine.pass_latencies()
 
     # -- full-run checks (size-independent properties) ---------------------------------------
@@ -308,7 +385,7 @@ def main():
         return sum(int(x) for x in accts[field + "_lo"]) + (sum(int(x) for x in accts[field + "_hi"]) << 64)
 
     dpost, cpost = total("debits_posted"), total("credits_posted")
-    n_failed = int(rb.sum()) // 8
+    n_failed = int(rb.sum()) // 8 if dev_ms else n_failed_host
     # C2: every transfer commits.  Every config: each committed transfer is one record; debits equal
     # credits in total, posted and pending.
     full_ok = bool(stats["transfers"] == args.transfers - n_failed and dpost == cpost and dpost > 0
@@ -318,11 +395,28 @@ def main():
     total_ms = sum(step_ms)
     n_total = args.transfers * world * args.steps
     value = n_total / (total_ms / 1e3)
+    full_ok = full_ok and n_failed_host == n_failed
 
-    # -- roofline: dominant kernel -----------------------------------------------------------
+    # -- roofline: the dominant kernel of the headline's timed steps ---------------------------
     per_launch_transfers = args.transfers / max(1, stats["launches_validate"] / max(1, args.steps))
-    u_over_t = expected_unique(args.accounts, 2 * pass_events) / pass_events
+    u_over_t = expected_unique(args.accounts, 2 * per_launch_transfers) / per_launch_transfers
     roof = roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown)
+    pcie_gbs = args.transfers * 128 * args.steps / (total_ms / 1e3) / 1e9
+    pcie = {"h2d_bytes_per_transfer": 128, "achieved": round(pcie_gbs, 2), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
+            "frac": round(pcie_gbs / PCIE_PEAK_GBS, 4),
+            "note": "host link (PCIe Gen5 x16, MI355X_MICROARCH.md); the bound of the PCIe-inclusive value"}
+    device_resident = None
+    if dev_ms:
+        dev_total = sum(dev_ms)
+        per_launch_dev = args.transfers / max(1, dev_stats["launches_validate"] / max(1, args.device_steps))
+        u_dev = expected_unique(args.accounts, 2 * per_launch_dev) / per_launch_dev
+        device_resident = {
+            "value": round(args.transfers * args.device_steps / (dev_total / 1e3), 1), "unit": "transfers/s",
+            "steps": args.device_steps, "ms_per_step": round(dev_total / args.device_steps, 3),
+            "pass_prepares": args.pass_batches,
+            "definition": "tbgpu_commit_device_async: the same prepares already resident in HBM (no PCIe)",
+            "roofline": roofline(dev_stats, u_dev, per_launch_dev, args, dev_total, None, steps=args.device_steps),
+        }
 
     # -- CPU baseline + bit-exact sample parity (rank 0, N=1 only) ---------------------------
     cpu = None
@@ -351,7 +445,7 @@ def main():
     if rank == 0 and world == 1 and args.host_prepares > 0:
         host, t_cursor = run_host_commits(engine, args, events_dev, t_cursor)
 
-    lat = np.array(pass_lat) if len(pass_lat) else np.array([float("nan")])
+    pass_lat = np.array(pass_lat) if len(pass_lat) else np.array([float("nan")])
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -364,13 +458,18 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u128",
-        "data": "synthetic (device-generated, reference benchmark shapes)",
+        "data": "synthetic (generated on the GPU in the reference benchmark's shapes, copied to host memory before timing)",
         "config": {"workload": WORKLOAD_TEXT[args.workload] % (args.accounts, args.transfers, args.batch),
-                   "prepares_per_step": len(xfer_lens), "pass_prepares": args.pass_batches,
-                   "parallelism": "shard%d" % world if world > 1 else "single"},
-        "p99_batch_latency_ms": round(float(np.percentile(lat, 99)), 3),
-        "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3), "p100": round(float(lat.max()), 3),
-                             "definition": "device time of the pass that answers the prepare (%d prepares/pass)" % args.pass_batches},
+                   "prepares_per_step": len(xfer_lens), "chunk_prepares": args.chunk_prepares,
+                   "input": "prepare bodies in registered host memory; PCIe H2D and reply D2H inside the timed region",
+                   "parallelism": "single"},
+        "p99_batch_latency_ms": round(ref_percentile(lat, 99), 3),
+        "batch_latency_ms": dict(deciles(lat), definition=(
+            "per prepare, submit to reply: from the start of its chunk's PCIe copy to its reply landing in host "
+            "memory (device clock; %d-prepare chunks, 3 in flight); percentiles by src/benchmark.zig:454-471"
+            % args.chunk_prepares)),
+        "pcie": pcie,
+        "device_resident": device_resident,
         "dependent_events": stats["dependent_events"],
         "flow": {k: (round(stats[k], 3) if isinstance(stats[k], float) else stats[k])
                  for k in ("flow_units", "flow_runs", "flow_run_units", "flow_plan_ms", "flow_run_ms")},
@@ -473,7 +572,7 @@ def run_sharded(args, world, rank, local_rank):
     recv_per_launch = args.transfers / max(1, stats["launches_validate"] / max(1, args.steps))
     u_over_t = expected_unique(args.accounts, 2 * recv_per_launch) / recv_per_launch
     roof = roofline(stats, u_over_t, recv_per_launch, args, total_ms)
-    lat = np.array(pass_lat) if len(pass_lat) else np.array([float("nan")])
+    pass_lat = np.array(pass_lat) if len(pass_lat) else np.array([float("nan")])
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -505,7 +604,7 @@ def run_sharded(args, world, rank, local_rank):
     dist.destroy_process_group()
 
 
-def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=None):
+def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=None, steps=None):
     """The dominant kernel of the timed steps against the HBM peak; `kernels` = every kernel's mean
     launch time (from the warmup steps when given: the timed steps time only validate, replay/flow
     and whole passes)."""
@@ -544,7 +643,7 @@ def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=No
             "kernels": per_kernel, "kernels_timed_in": "warmup steps (every kernel)" if breakdown else "timed steps",
             "avg_launch_ms": round(ms_dom / n_dom, 4), "alg_bytes_per_transfer": round(alg_bytes / per_launch_transfers, 1),
             "path_bytes_per_transfer": round(296 + 256 * u_over_t, 1),
-            "path_achieved_GBs": round((296 + 256 * u_over_t) * args.transfers * args.steps / (total_ms / 1e3) / 1e9, 1)}
+            "path_achieved_GBs": round((296 + 256 * u_over_t) * args.transfers * (steps or args.steps) / (total_ms / 1e3) / 1e9, 1)}
 
 
 if __name__ == "__main__":

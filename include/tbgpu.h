@@ -80,11 +80,24 @@ int tbgpu_reset(tbgpu_t* engine);
 int tbgpu_commit(tbgpu_t* engine, uint8_t operation, uint64_t timestamp, const void* input,
                  uint32_t input_len, void* output, uint32_t output_cap, uint32_t* out_len);
 
-/* N consecutive prepares of the same create operation in one device pass; identical results to
- * N sequential tbgpu_commit calls (timestamps strictly increasing). */
+/* N consecutive prepares of the same create operation, pass_batches_max prepares per device pass
+ * (tbgpu_commit_pipelined with chunk_batches = 0); identical results to N sequential tbgpu_commit
+ * calls (timestamps strictly increasing). */
 int tbgpu_commit_many(tbgpu_t* engine, uint8_t operation, uint32_t n, const uint64_t* timestamps,
                       const void* const* inputs, const uint32_t* input_lens, void* const* outputs,
                       uint32_t* out_lens);
+
+/* Pipelined commit of N prepares from host memory: the replica's prefetch -> commit overlap
+ * (src/state_machine.zig:345-506, src/vsr/replica.zig:3324-3665) with the objects HBM-resident.
+ * Prepares are grouped into chunks of up to `chunk_batches` prepares (0: pass_batches_max); chunk
+ * c+1's bodies cross PCIe while chunk c commits, and chunk c's replies come back as soon as it is
+ * committed.  Bodies in memory registered with tbgpu_register_host (or otherwise pinned) move by
+ * DMA; runs of address-contiguous prepares move as one copy.  Results are identical to N sequential
+ * tbgpu_commit calls.  latency_ms (optional, N entries): per-prepare submit-to-reply time, from the
+ * start of its chunk's PCIe copy to its reply landing in host memory (device clock). */
+int tbgpu_commit_pipelined(tbgpu_t* engine, uint8_t operation, uint32_t n, const uint64_t* timestamps,
+                           const void* const* inputs, const uint32_t* input_lens, void* const* outputs,
+                           uint32_t* out_lens, uint32_t chunk_batches, double* latency_ms);
 
 /* Device-resident throughput entry point: `events_dev` holds sum(batch_lens) events back to back
  * in HBM; batch k's reply is written to results_dev + 8*offset_k (offset_k = sum of earlier

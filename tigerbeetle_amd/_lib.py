@@ -94,6 +94,8 @@ SIGNATURES = [
     ("tbgpu_commit", ctypes.c_int, [_P, _U8, _U64, _P, _U32, _P, _U32, ctypes.POINTER(_U32)]),
     ("tbgpu_commit_many", ctypes.c_int, [_P, _U8, _U32, ctypes.POINTER(_U64), ctypes.POINTER(_P),
                                          ctypes.POINTER(_U32), ctypes.POINTER(_P), ctypes.POINTER(_U32)]),
+    ("tbgpu_commit_pipelined", ctypes.c_int, [_P, _U8, _U32, ctypes.POINTER(_U64), ctypes.POINTER(_P),
+                                              ctypes.POINTER(_U32), ctypes.POINTER(_P), ctypes.POINTER(_U32), _U32, _P]),
     ("tbgpu_commit_device_async", ctypes.c_int, [_P, _U8, _U32, ctypes.POINTER(_U64), ctypes.POINTER(_U32),
                                                  _P, _P, _P]),
     ("tbgpu_sync", ctypes.c_int, [_P]),

@@ -51,6 +51,8 @@ static u64 pow2_at_least(u64 v) {
     return c;
 }
 
+#define PIPE_SLOTS 3
+
 enum { K_VALIDATE = 0, K_RESOLVE = 1, K_REPLAY = 2, K_CLEAR = 3, K_PASS = 4, K_APPLY = 5, K_COUNT = 6 };
 
 struct ProfilePair {
@@ -109,6 +111,18 @@ struct tbgpu {
         const u8* dev;  // its device mapping
     };
     std::vector<HostRegion> host_regions;  // tbgpu_register_host
+    // Pipelined host commits (tbgpu_commit_pipelined): PIPE_SLOTS chunks in flight.  Slot s has its
+    // own staging area, call metadata and pinned reply arena; chunk c+1's bodies cross PCIe on
+    // copy_stream while chunk c commits on `stream`.
+    hipStream_t copy_stream = nullptr;
+    struct PipeSlot {
+        u8* staging = nullptr;      // device: pe_max events (slot 0 aliases `staging`)
+        u64* meta = nullptr;        // device: offsets then timestamps
+        u64* h_meta = nullptr;      // pinned mirror
+        u8* h_reply = nullptr;      // pinned, mapped: [2] head {panic, commit_ts}, [meta_cap] reply bytes, results
+        u8* d_reply = nullptr;      // its device mapping
+        hipEvent_t start = nullptr, copied = nullptr, done = nullptr;
+    } pipe[PIPE_SLOTS];
     u64* lookup_ids = nullptr;
     u8* lookup_out = nullptr;
     u8* lookup_found = nullptr;
@@ -153,6 +167,10 @@ struct tbgpu {
     u64* r_meta = nullptr;    // device [meta_cap + 1] offsets then [meta_cap] timestamps
     u64* h_rmeta = nullptr;   // pinned mirror
 };
+
+// Pinned reply arena of one pipeline slot: head {panic, commit_ts}, reply bytes per prepare, then
+// the results of every event of the chunk (8 B each, the worst case).
+static u64 pipe_reply_bytes(const tbgpu* E) { return 16 + E->meta_cap * 4 + (u64)E->pe_max * 8; }
 
 static int ev_get(tbgpu* E, hipEvent_t* out) {
     if (E->event_next == E->event_pool.size()) {
@@ -280,7 +298,7 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     INIT_CK(hipMemGetInfo(&free_b, &total_b));
     const u64 need = E->account_cap * (sizeof(Account) + 4) + E->xlog_cap * (sizeof(Transfer) + 1) +
                      E->xidx_cap * (sizeof(u64) + 1) +
-                     (u64)E->pe_max * (4 * 4 + 8 * 4 + 128 + 8 + 4) + E->dedup_cap * 8;
+                     (u64)E->pe_max * (4 * 4 + 8 * 4 + 128 * PIPE_SLOTS + 8 + 4) + E->dedup_cap * 8;
     if (need > free_b) {
         st = fail(TBGPU_STATUS_INVALID, "tbgpu_init: needs %llu bytes of HBM, %llu free",
                   (unsigned long long)need, (unsigned long long)free_b);
@@ -377,6 +395,19 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     INIT_CK(hipHostMalloc(&E->h_rb, E->meta_cap * 4, hipHostMallocDefault));
     E->h_results_events = std::min<u64>(E->pe_max, 1ULL << 16);
     INIT_CK(hipHostMalloc(&E->h_results, E->h_results_events * 8, hipHostMallocDefault));
+    INIT_CK(hipStreamCreateWithFlags(&E->copy_stream, hipStreamNonBlocking));
+    for (int k = 0; k < PIPE_SLOTS; k++) {
+        tbgpu::PipeSlot& S = E->pipe[k];
+        if (k == 0) S.staging = E->staging;
+        else INIT_CK(hipMalloc(&S.staging, pe * 128));
+        INIT_CK(hipMalloc(&S.meta, (2 * E->meta_cap + 1) * 8));
+        INIT_CK(hipHostMalloc(&S.h_meta, (2 * E->meta_cap + 1) * 8, hipHostMallocDefault));
+        INIT_CK(hipHostMalloc(&S.h_reply, pipe_reply_bytes(E), hipHostMallocMapped));
+        INIT_CK(hipHostGetDevicePointer((void**)&S.d_reply, S.h_reply, 0));
+        INIT_CK(hipEventCreate(&S.start));
+        INIT_CK(hipEventCreate(&S.copied));
+        INIT_CK(hipEventCreate(&S.done));
+    }
     INIT_CK(hipMalloc(&E->lookup_ids, (u64)E->lookup_cap * 16));
     INIT_CK(hipMalloc(&E->lookup_out, (u64)E->lookup_cap * 128));
     INIT_CK(hipMalloc(&E->lookup_found, E->lookup_cap));
@@ -405,6 +436,15 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->F.f_pe, E->F.f_batch, E->F.f_len, E->F.need, E->F.nsucc, E->F.queue, E->F.uflags, E->F.nacct, E->F.rpos, E->F.succ,
                     E->F.run, E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo};
     for (void* p : bufs) if (p) (void)hipFree(p);
+    for (int k = 0; k < PIPE_SLOTS; k++) {
+        tbgpu::PipeSlot& S = E->pipe[k];
+        if (k > 0 && S.staging) (void)hipFree(S.staging);
+        if (S.meta) (void)hipFree(S.meta);
+        if (S.h_meta) (void)hipHostFree(S.h_meta);
+        if (S.h_reply) (void)hipHostFree(S.h_reply);
+        for (hipEvent_t e : {S.start, S.copied, S.done}) if (e) (void)hipEventDestroy(e);
+    }
+    if (E->copy_stream) (void)hipStreamDestroy(E->copy_stream);
     if (E->h_meta) (void)hipHostFree(E->h_meta);
     if (E->h_globals) (void)hipHostFree(E->h_globals);
     if (E->h_rb) (void)hipHostFree(E->h_rb);
@@ -442,9 +482,9 @@ static int engine_sync(tbgpu* E) {
 // result codes instead of sparse replies, cert_ext = the router's certificate.
 static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* events_dev, u32* results_dev,
                         u32* reply_bytes_dev, bool routed = false, u8* codes = nullptr, u32 cert_ext = 0,
-                        const u8* events_src = nullptr) {
-    const u64* d_off = E->meta;
-    const u64* d_ts = E->meta + (nb + 1);
+                        const u8* events_src = nullptr, const u64* d_meta = nullptr) {
+    const u64* d_off = d_meta ? d_meta : E->meta;
+    const u64* d_ts = d_off + (nb + 1);
     u32 b0 = 0;
     while (b0 < nb) {
         u32 b1 = b0;
@@ -722,6 +762,145 @@ static int commit_host(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const
     return TBGPU_STATUS_OK;
 }
 
+// Pipelined commit of n prepares from host memory (the replica's prefetch → commit overlap,
+// src/state_machine.zig:345-506 / src/vsr/replica.zig:3324-3665, with the objects HBM-resident):
+// prepares are grouped into chunks of up to `chunk_batches` prepares (and pe_max events); chunk
+// c+1's bodies cross PCIe on copy_stream while chunk c commits on the engine stream, and chunk c's
+// replies land in its slot's pinned arena (tb_reply_out) as soon as it is committed.  The host
+// reads chunk c's replies before it reuses the slot for chunk c + PIPE_SLOTS.  Results are those
+// of n sequential commits.  latency_ms[k] (optional): device-clock time from the start of prepare
+// k's chunk crossing PCIe to its reply landing in host memory.
+static int commit_pipelined(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const void* const* inputs,
+                            const uint32_t* input_lens, void* const* outputs, uint32_t* out_lens,
+                            const uint32_t* out_caps, u32 chunk_batches, double* latency_ms) {
+    if (op != OP_CREATE_ACCOUNTS && op != OP_CREATE_TRANSFERS) {
+        return fail(TBGPU_STATUS_INVALID, "operation %u is not a create operation", op);
+    }
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    std::vector<u32> lens(n);
+    u64 prev = E->commit_ts, total = 0;
+    for (u32 k = 0; k < n; k++) {  // the commit asserts of every prepare, before anything runs
+        if (input_lens[k] % 128 != 0) return fail(TBGPU_STATUS_INVALID, "create body not a multiple of 128");
+        const u32 L = input_lens[k] / 128;
+        if (L > BATCH_EVENTS_MAX) return fail(TBGPU_STATUS_INVALID, "batch %u has %u events (max %u)", k, L, BATCH_EVENTS_MAX);
+        if (out_caps && (u64)out_caps[k] < (u64)L * 8) return fail(TBGPU_STATUS_INVALID, "output too small");
+        const u64 ts = timestamps[k];
+        if (!(ts > prev)) return fail(TBGPU_STATUS_PANIC, "timestamp %llu <= commit timestamp %llu",
+                                      (unsigned long long)ts, (unsigned long long)prev);
+        if (L > 0) {
+            if (ts < L) return fail(TBGPU_STATUS_PANIC, "timestamp %llu < batch length %u", (unsigned long long)ts, L);
+            if (!(ts - L + 1 > prev)) return fail(TBGPU_STATUS_PANIC, "first event timestamp <= commit timestamp");
+        }
+        prev = ts;
+        lens[k] = L;
+        total += L;
+        out_lens[k] = 0;
+    }
+    if (op == OP_CREATE_TRANSFERS && E->log_next + total > E->xlog_cap) {
+        return fail(TBGPU_STATUS_INVALID, "transfer log full (%llu + %llu events > capacity %llu)",
+                    (unsigned long long)E->log_next, (unsigned long long)total, (unsigned long long)E->xlog_cap);
+    }
+    const u32 per_chunk = std::max<u32>(1, std::min<u32>(chunk_batches ? chunk_batches : E->pb_max, E->pb_max));
+    struct Chunk {
+        u32 k0, k1;
+    };
+    std::vector<Chunk> chunks;
+    for (u32 k0 = 0; k0 < n;) {
+        u32 k1 = k0;
+        u64 ev = 0;
+        while (k1 < n && k1 - k0 < per_chunk && k1 - k0 < E->meta_cap && ev + lens[k1] <= E->pe_max) ev += lens[k1++];
+        if (k1 == k0) return fail(TBGPU_STATUS_INVALID, "batch larger than pass_events_max");
+        chunks.push_back({k0, k1});
+        k0 = k1;
+    }
+    int status = TBGPU_STATUS_OK;
+    // Read chunk c's replies out of its slot (its done event has fired or is waited for here).
+    auto consume = [&](size_t c) -> int {
+        tbgpu::PipeSlot& S = E->pipe[c % PIPE_SLOTS];
+        HIPCK(hipEventSynchronize(S.done));
+        const Chunk& C = chunks[c];
+        const u32 nb = C.k1 - C.k0;
+        const u64* head = (const u64*)S.h_reply;
+        const u32* rb = (const u32*)(S.h_reply + 16);
+        const u8* res = S.h_reply + 16 + (u64)nb * 4;
+        float ms = 0;
+        if (latency_ms) HIPCK(hipEventElapsedTime(&ms, S.start, S.done));
+        for (u32 k = C.k0; k < C.k1; k++) {
+            const u32 bytes = rb[k - C.k0];
+            if (bytes) memcpy(outputs[k], res + 8 * S.h_meta[k - C.k0], bytes);
+            out_lens[k] = bytes;
+            if (latency_ms) latency_ms[k] = ms;
+        }
+        E->commit_ts = std::max(E->commit_ts, head[1]);
+        if (head[0]) {
+            return fail(TBGPU_STATUS_PANIC, "device panic 0x%llx (the reference would have trapped)",
+                        (unsigned long long)head[0]);
+        }
+        return TBGPU_STATUS_OK;
+    };
+    size_t issued = 0, consumed = 0;
+    for (; issued < chunks.size() && status == TBGPU_STATUS_OK; issued++) {
+        const size_t c = issued;
+        if (c >= PIPE_SLOTS) {
+            status = consume(consumed++);
+            if (status) break;
+        }
+        tbgpu::PipeSlot& S = E->pipe[c % PIPE_SLOTS];
+        const Chunk& C = chunks[c];
+        const u32 nb = C.k1 - C.k0;
+        u64* h_off = S.h_meta;
+        u64* h_ts = S.h_meta + (nb + 1);
+        h_off[0] = 0;
+        for (u32 k = C.k0; k < C.k1; k++) {
+            h_off[k - C.k0 + 1] = h_off[k - C.k0] + lens[k];
+            h_ts[k - C.k0] = timestamps[k];
+        }
+        // Copy stream: metadata, then the bodies (runs of address-contiguous prepares as one DMA).
+        HIPCK(hipEventRecord(S.start, E->copy_stream));
+        HIPCK(hipMemcpyAsync(S.meta, S.h_meta, (2 * (u64)nb + 1) * 8, hipMemcpyHostToDevice, E->copy_stream));
+        for (u32 k = C.k0; k < C.k1;) {
+            u32 j = k + 1;
+            const u8* base = (const u8*)inputs[k];
+            u64 bytes = (u64)lens[k] * 128;
+            while (j < C.k1 && (const u8*)inputs[j] == base + bytes) bytes += (u64)lens[j++] * 128;
+            if (bytes) HIPCK(hipMemcpyAsync(S.staging + h_off[k - C.k0] * 128, base, bytes, hipMemcpyHostToDevice,
+                                            E->copy_stream));
+            k = j;
+        }
+        HIPCK(hipEventRecord(S.copied, E->copy_stream));
+        // Engine stream: the chunk's passes, then its replies into the pinned arena.
+        HIPCK(hipStreamWaitEvent(E->stream, S.copied, 0));
+        E->last_batch_ts = timestamps[C.k1 - 1];
+        status = enqueue_call(E, op, nb, h_off, S.staging, E->results, E->reply_bytes, false, nullptr, 0, nullptr, S.meta);
+        if (status) break;
+        hipLaunchKernelGGL(tb_reply_out, dim3(nb), dim3(64), 0, E->stream, S.meta, nb, E->reply_bytes, E->results, E->g,
+                           S.d_reply);
+        HIPCK(hipGetLastError());
+        HIPCK(hipEventRecord(S.done, E->stream));
+    }
+    // Drain what is in flight (also after a failure: every enqueued chunk has finished before the
+    // call returns, as after any synchronous call).
+    while (consumed < issued) {
+        const int st = consume(consumed++);
+        if (status == TBGPU_STATUS_OK) status = st;
+    }
+    HIPCK(hipStreamSynchronize(E->copy_stream));
+    const int st = engine_sync(E);
+    return status ? status : st;
+}
+
+extern "C" int tbgpu_commit_pipelined(tbgpu_t* E, uint8_t operation, uint32_t n, const uint64_t* timestamps,
+                                      const void* const* inputs, const uint32_t* input_lens, void* const* outputs,
+                                      uint32_t* out_lens, uint32_t chunk_batches, double* latency_ms) {
+    HIPCK(hipSetDevice(E->device));
+    if (n == 0) return TBGPU_STATUS_OK;
+    return commit_pipelined(E, operation, n, timestamps, inputs, input_lens, outputs, out_lens, nullptr, chunk_batches,
+                            latency_ms);
+}
+
 extern "C" int tbgpu_commit(tbgpu_t* E, uint8_t operation, uint64_t timestamp, const void* input,
                             uint32_t input_len, void* output, uint32_t output_cap, uint32_t* out_len) {
     *out_len = 0;
@@ -754,7 +933,8 @@ extern "C" int tbgpu_commit_many(tbgpu_t* E, uint8_t operation, uint32_t n, cons
     HIPCK(hipSetDevice(E->device));
     for (u32 k = 0; k < n; k++) out_lens[k] = 0;
     if (n == 0) return TBGPU_STATUS_OK;
-    return commit_host(E, operation, n, timestamps, inputs, input_lens, outputs, out_lens, nullptr);
+    if (n == 1) return commit_host(E, operation, n, timestamps, inputs, input_lens, outputs, out_lens, nullptr);
+    return commit_pipelined(E, operation, n, timestamps, inputs, input_lens, outputs, out_lens, nullptr, 0, nullptr);
 }
 
 extern "C" int tbgpu_commit_device_async(tbgpu_t* E, uint8_t operation, uint32_t n_batches,

@@ -131,3 +131,26 @@ __global__ void tb_delta_transfers(Tables T, const u8* snap_posted, u64 pos0, u6
         }
     }
 }
+
+// ---- pipelined host commits (tbgpu_commit_pipelined) -------------------------------------------
+// After a chunk's passes: copy what the host needs straight into the slot's pinned reply arena
+// (mapped host memory): the panic word and commit timestamp, every prepare's reply size and the
+// non-empty replies.  Only bytes that exist cross PCIe (4 B per prepare for an all-ok chunk); the
+// host reads the arena once the chunk's `done` event fired.  One workgroup per prepare.
+__global__ __launch_bounds__(64) void tb_reply_out(const u64* batch_off, u32 nb, const u32* reply_bytes,
+                                                   const u32* results, const Globals* g, u8* arena) {
+    u64* head = (u64*)arena;
+    u32* rb = (u32*)(arena + 16);
+    const u32 k = blockIdx.x;
+    if (k == 0 && threadIdx.x == 0) {
+        head[0] = g->panic;
+        head[1] = g->commit_timestamp;
+    }
+    if (k >= nb) return;
+    const u32 bytes = reply_bytes[k];
+    if (threadIdx.x == 0) rb[k] = bytes;
+    if (bytes == 0) return;
+    u32* out = (u32*)(arena + 16 + (u64)nb * 4 + 8 * batch_off[k]);  // 4-B aligned: nb words before
+    const u32* in = results + 2 * batch_off[k];
+    for (u32 w = threadIdx.x; w < bytes / 4; w += 64) out[w] = in[w];
+}

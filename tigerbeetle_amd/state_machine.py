@@ -99,6 +99,41 @@ class Engine:
         _lib.check(self.lib.tbgpu_commit_many(self.h, int(operation), n, ts, ins, lens, outp, out_lens))
         return [outs[k].raw[:out_lens[k]] for k in range(n)]
 
+    def commit_pipelined(self, operation, timestamps, lens, events, chunk_batches=0, latency=False, replies=None):
+        """tbgpu_commit_pipelined over prepares stored back to back in the host array `events`
+        (uint8; register it with register_host for DMA at full PCIe rate).  Returns (reply_bytes
+        uint32[n], replies uint8 buffer with prepare k's reply at 8 * its first event, latency_ms
+        float64[n] or None)."""
+        n = len(lens)
+        lens = np.asarray(lens, dtype=np.uint64)
+        first = np.zeros(n, dtype=np.uint64)
+        if n > 1:
+            first[1:] = np.cumsum(lens[:-1])
+        total = int(lens.sum())
+        assert events.dtype == np.uint8 and events.flags["C_CONTIGUOUS"] and events.nbytes >= total * 128
+        if replies is None or replies.nbytes < total * 8:
+            replies = np.empty(max(total, 1) * 8, dtype=np.uint8)
+        ts = np.ascontiguousarray(timestamps, dtype=np.uint64)
+        ins = (first * 128 + np.uint64(events.ctypes.data)).astype(np.uint64)
+        outs = (first * 8 + np.uint64(replies.ctypes.data)).astype(np.uint64)
+        in_lens = (lens * 128).astype(np.uint32)
+        out_lens = np.zeros(n, dtype=np.uint32)
+        lat = np.zeros(n, dtype=np.float64) if latency else None
+        P = ctypes.c_void_p
+        _lib.check(self.lib.tbgpu_commit_pipelined(
+            self.h, int(operation), n, ts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+            ins.ctypes.data_as(ctypes.POINTER(P)), in_lens.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+            outs.ctypes.data_as(ctypes.POINTER(P)), out_lens.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+            int(chunk_batches), lat.ctypes.data if lat is not None else None))
+        return out_lens, replies, lat
+
+    def register_host(self, array):
+        """Pin a host array for DMA (the replica's message pool; tbgpu_register_host)."""
+        _lib.check(self.lib.tbgpu_register_host(self.h, array.ctypes.data, array.nbytes))
+
+    def unregister_host(self, array):
+        _lib.check(self.lib.tbgpu_unregister_host(self.h, array.ctypes.data))
+
     def commit_device_async(self, operation, timestamps, lens, events_dev, results_dev, reply_bytes_dev):
         n = len(lens)
         ts = (ctypes.c_uint64 * n)(*[int(t) for t in timestamps])
