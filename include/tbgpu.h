@@ -56,6 +56,9 @@ extern "C" {
 
 /* Config flags. */
 #define TBGPU_CONFIG_PROFILE (1u << 0) /* time every kernel with HIP events (tbgpu_get_stats) */
+/* Ordered fallback on one lane in batch order (tb_replay) instead of the parallel flow path
+ * (tb_flow); identical results, for cross-checking the two. */
+#define TBGPU_CONFIG_SEQUENTIAL_FALLBACK (1u << 1)
 
 typedef struct tbgpu_config {
     uint64_t accounts_max;      /* HBM account table capacity (the groove's object count) */
@@ -166,6 +169,11 @@ typedef struct tbgpu_stats {
 
 int tbgpu_get_stats(tbgpu_t* engine, tbgpu_stats* stats);
 void tbgpu_reset_stats(tbgpu_t* engine);
+
+/* vsr.checksum (src/vsr/checksum.zig:50-74): Aegis-128L MAC, zero key and nonce, 16 tag bytes
+ * (the u128 in little-endian order).  Host-only (touches no device): the AOF reader verifies
+ * header and body checksums with it (src/aof.zig:214-218, src/vsr.zig:405-437). */
+void tbgpu_checksum(const void* data, uint64_t len, uint8_t out[16]);
 
 /* Last error message (thread-local, static storage). */
 const char* tbgpu_last_error(void);

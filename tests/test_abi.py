@@ -79,3 +79,16 @@ def test_init_without_gpu_fails_loudly(lib):
     st = lib.tbgpu_init(ctypes.byref(cfg), ctypes.byref(h))
     assert st != _lib.STATUS_OK and not h.value
     assert lib.tbgpu_last_error()
+
+
+def test_init_refuses_capacities_past_the_engine_limits(lib):
+    """Capacity contract: a device holds at most 2^31 accounts and 2^31 transfer-log
+    positions (31-bit positions in the 8-B index entries).  init refuses more with INVALID before it
+    touches any device, so this runs without a GPU."""
+    h = ctypes.c_void_p()
+    for accounts, transfers in (((1 << 31) + 1, 1024), (1024, (1 << 31) + 1), (0, 1024), (1024, 0)):
+        cfg = _lib.tbgpu_config(accounts, transfers, 8192, 1, 0, 0)
+        assert lib.tbgpu_init(ctypes.byref(cfg), ctypes.byref(h)) == _lib.STATUS_INVALID
+        assert not h.value
+        if accounts and transfers:
+            assert b"2^31" in lib.tbgpu_last_error()

@@ -40,11 +40,18 @@ def test_format_errors(tmp_path):
     data = bytearray(path.read_bytes())
     second = aof._sector_ceil(aof.META + aof.HEADER + len(prepares[0].body))
     broken = bytearray(data)
-    broken[second + 4096 + 32] ^= 1  # parent of entry 2
+    broken[second + 4096 + 32] ^= 1  # parent of entry 2 (covered by its header checksum)
     path.write_bytes(bytes(broken))
-    with pytest.raises(aof.AofError, match="chain"):
+    with pytest.raises(aof.AofError, match="header checksum"):
         aof.read_prepares(path)
-    assert len(aof.read_prepares(path, validate_chain=False)) == len(prepares)
+    with pytest.raises(aof.AofError, match="chain"):
+        aof.read_prepares(path, validate_checksums=False)
+    assert len(aof.read_prepares(path, validate_chain=False, validate_checksums=False)) == len(prepares)
+    broken = bytearray(data)
+    broken[second + 4096 + 128 + 5] ^= 1  # a body byte of entry 2 (src/aof.zig:218)
+    path.write_bytes(bytes(broken))
+    with pytest.raises(aof.AofError, match="body checksum"):
+        aof.read_prepares(path)
     broken = bytearray(data)
     broken[second] ^= 1  # magic of entry 2
     path.write_bytes(bytes(broken))
@@ -66,6 +73,29 @@ def test_duplicates_and_order(tmp_path):
     aof.write_aof(path, bad)
     with pytest.raises(aof.AofError, match="twice"):
         aof.read_prepares(path, validate_chain=False)
+
+
+def test_op_gap_refused(tmp_path):
+    _, prepares = scenario_prepares(6)
+    path = tmp_path / "gap.aof"
+    aof.write_aof(path, prepares[:3] + prepares[4:])  # op 4 missing; the chain stays consistent
+    with pytest.raises(aof.AofError, match="gaps"):
+        aof.read_prepares(path)
+    # VSR-reserved prepares (operation < 128) fill their ops: no gap, and they are not replayed.
+    reserved = aof.AofPrepare(op=4, timestamp=prepares[3].timestamp, operation=3, body=b"")
+    aof.write_aof(path, prepares[:3] + [reserved] + prepares[4:])
+    assert [p.op for p in aof.read_prepares(path)] == [p.op for p in prepares if p.op != 4]
+
+
+def test_written_checksums_verify(tmp_path):
+    from tigerbeetle_amd._lib import checksum
+    _, prepares = scenario_prepares(7)
+    path = tmp_path / "ck.aof"
+    aof.write_aof(path, prepares[:2])
+    data = path.read_bytes()
+    hdr = data[4096:4096 + 128]
+    assert checksum(hdr[16:]).to_bytes(16, "little") == hdr[:16]
+    assert checksum(prepares[0].body).to_bytes(16, "little") == hdr[16:32]
 
 
 @pytest.mark.parametrize("seed", [11, 12])

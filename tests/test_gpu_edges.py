@@ -225,3 +225,29 @@ def test_gpu_edges(name, many, gpu_engine_factory):
     actual = run_many(sc, engine) if many else run_oracle(sc, engine)
     assert actual == expected
     assert _state(engine) == _state(oracle)
+
+
+@pytest.mark.gpu
+def test_transfer_log_full_is_refused_whole(gpu_engine_factory):
+    """Capacity contract: the transfer log is sized at init (every stored transfer
+    and every speculative record of a pass takes a position).  A commit that would overflow it is
+    refused with INVALID before anything runs — no prepare of the call commits — and the engine
+    keeps working for calls that fit."""
+    from tigerbeetle_amd._lib import EngineError
+
+    engine = gpu_engine_factory(accounts_max=64, transfers_max=1024, pass_events_max=2048, pass_batches_max=4)
+    oracle = OracleEngine()
+    b = _Builder().commit(128, _accounts(4))
+    first = [pack_transfer(id=100 + i, debit_account_id=1 + i % 4, credit_account_id=1 + (i + 1) % 4, amount=1,
+                           ledger=LEDGER, code=1) for i in range(1000)]
+    b.commit(129, first)
+    assert run_oracle(b.sc, oracle) == run_oracle(b.sc, engine)
+    over = [pack_transfer(id=5000 + i, debit_account_id=1, credit_account_id=2, amount=1, ledger=LEDGER, code=1)
+            for i in range(100)]
+    with pytest.raises(EngineError, match="transfer log full"):
+        engine.commit(129, b.ts + 200, b"".join(over))
+    from tests.test_gpu_differential import assert_same_state as assert_same
+    assert_same(oracle, engine)
+    fits = b"".join(over[:20])
+    assert engine.commit(129, b.ts + 300, fits) == oracle.commit(129, b.ts + 300, fits)
+    assert_same(oracle, engine)

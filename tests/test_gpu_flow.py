@@ -1,9 +1,8 @@
 """The parallel ordered fallback (csrc/k_flow.h) against the oracle and against the sequential
 replay it replaces: linked chains longer than the planner takes (the in-kernel sequential
 fallback), engines whose balances were set directly (sequential replay by design), and the same
-BASELINE C4-shaped workload with the flow path on and off (TBGPU_ABLATE=2048), byte for byte."""
-import os
-
+BASELINE C4-shaped workload with the flow path on and off (TBGPU_CONFIG_SEQUENTIAL_FALLBACK),
+both against the oracle, byte for byte."""
 import pytest
 
 from tests.harness.configs import SETTINGS, batches, generate, split, timestamps
@@ -30,8 +29,8 @@ def test_set_balances_keeps_sequential_replay(gpu_engine_factory):
     assert engine.stats()["flow_passes"] == 0
 
 
-def _c4(engine, n_accounts=5000, n_transfers=150_000):
-    accts, xfers = generate(engine, "c4", n_accounts, n_transfers, seed=3)
+def _c4(engine, data, n_accounts=5000, n_transfers=150_000):
+    accts, xfers = data
     a_lens = batches(n_accounts, 8190)
     a_ts, t = timestamps(a_lens, 10**12)
     x_lens = batches(n_transfers, 8190)
@@ -40,14 +39,16 @@ def _c4(engine, n_accounts=5000, n_transfers=150_000):
     return engine.commit_many(129, x_ts, split(xfers, x_lens))
 
 
-def test_flow_equals_sequential_replay(gpu_engine_factory, monkeypatch):
+def test_flow_equals_sequential_replay(gpu_engine_factory):
     kw = dict(accounts_max=5000, transfers_max=150_000, pass_events_max=8 * 8190, pass_batches_max=8)
     flow = gpu_engine_factory(**kw)
-    got_flow = _c4(flow)
+    data = generate(flow, "c4", 5000, 150_000, seed=3)
+    got_flow = _c4(flow, data)
     assert flow.stats()["flow_passes"] > 0
-    monkeypatch.setenv("TBGPU_ABLATE", str(2048))  # ABL_FLOW, read at tbgpu_init
-    seq = gpu_engine_factory(**kw)
-    got_seq = _c4(seq)
-    assert seq.stats()["flow_passes"] == 0
-    assert got_flow == got_seq
-    assert_same_state(seq, flow)  # same accounts, transfers, posted groove, commit_timestamp
+    seq = gpu_engine_factory(sequential_fallback=True, **kw)
+    got_seq = _c4(seq, data)
+    assert seq.stats()["flow_passes"] == 0 and seq.stats()["dependent_events"] > 0
+    oracle = OracleEngine(5000, 150_000)
+    assert _c4(oracle, data) == got_flow == got_seq
+    assert_same_state(oracle, flow)  # same accounts, transfers, posted groove, commit_timestamp
+    assert_same_state(oracle, seq)

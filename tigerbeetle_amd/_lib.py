@@ -14,6 +14,7 @@ AB_PATH = os.environ.get("TBGPU_AB_LIB")
 STATUS_OK, STATUS_INVALID, STATUS_PANIC, STATUS_DEVICE = 0, 1, 2, 3
 
 CONFIG_PROFILE = 1
+CONFIG_SEQUENTIAL_FALLBACK = 2
 
 
 class tbgpu_config(ctypes.Structure):
@@ -107,6 +108,7 @@ SIGNATURES = [
     ("tbgpu_get_stats", ctypes.c_int, [_P, ctypes.POINTER(tbgpu_stats)]),
     ("tbgpu_reset_stats", None, [_P]),
     ("tbgpu_last_error", ctypes.c_char_p, []),
+    ("tbgpu_checksum", None, [_P, _U64, _P]),
     ("tbgpu_bench_generate_accounts", ctypes.c_int, [_P, _P, _U64, _U64, ctypes.POINTER(tbgpu_workload)]),
     ("tbgpu_bench_generate_transfers", ctypes.c_int, [_P, _P, _U64, _U64, ctypes.POINTER(tbgpu_workload)]),
     ("tbgpu_bench_reset_transfers", ctypes.c_int, [_P]),
@@ -174,3 +176,11 @@ def check(status):
     if status == STATUS_PANIC:
         raise EnginePanic(status, msg)
     raise EngineError(status, msg)
+
+
+def checksum(data):
+    """vsr.checksum (src/vsr/checksum.zig:50) of bytes -> int (u128), computed by the library."""
+    data = bytes(data)
+    out = ctypes.create_string_buffer(16)
+    load().tbgpu_checksum(data, len(data), out)
+    return int.from_bytes(out.raw, "little")

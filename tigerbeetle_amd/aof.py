@@ -19,15 +19,18 @@ On-disk format restated from the reference (data layout only):
   replica u8 @124, command u8 @125 (`prepare` = 6, `:111-121`), operation u8 @126, version u8
   @127.  The body follows the header (`size` includes the header).
 
-Checksums are Aegis128L MACs (`vsr.checksum`); they are not recomputed here (no Aegis
-implementation in this repo), so a reader checks the magic number, the sizes and the hash chain
-(`parent` == previous entry's `checksum`, as the reference's iterator does, `:221-226`) but not
-the MAC values themselves — parity on a recorded AOF is pinned by the replay, not by the MACs.
-`write_aof` writes the same layout with placeholder (non-MAC) checksums that keep the chain
-consistent; it exists to make fixtures.
+Checksums are `vsr.checksum` (Aegis-128L MAC, zero key: `src/vsr/checksum.zig`), computed by the
+engine library's host-side `tbgpu_checksum` (pinned by the reference's checksum vectors,
+tests/test_checksum.py).  The reader verifies what the reference's iterator verifies
+(`src/aof.zig:197-233`): the magic number, the sizes, the header checksum (over header bytes
+[16, 128), `src/vsr.zig:405-411`), the body checksum (`:413-420`) and the hash chain (`parent` ==
+the previous entry's `checksum`, `:221-226`); `read_prepares` also refuses a gap in the op
+sequence.  `write_aof` writes the same layout with real checksums; it makes fixtures.
 """
 import struct
 from dataclasses import dataclass
+
+from ._lib import checksum as vsr_checksum
 
 MAGIC = 312960301372567410560647846651901451202  # src/aof.zig:24
 SECTOR = 4096
@@ -60,7 +63,7 @@ def _sector_ceil(n):
     return (n + SECTOR - 1) // SECTOR * SECTOR
 
 
-def read_entries(path, validate_chain=True):
+def read_entries(path, validate_chain=True, validate_checksums=True):
     """Every entry of an AOF file, in file order (AOF.Iterator.next, src/aof.zig:197-233)."""
     with open(path, "rb") as f:
         data = f.read()
@@ -80,6 +83,12 @@ def read_entries(path, validate_chain=True):
         disk = _sector_ceil(META + size)
         if off + disk > len(data):
             raise AofError("short read at offset %d" % off)
+        if validate_checksums:
+            header = data[off + META:off + META + HEADER]
+            if vsr_checksum(header[16:]).to_bytes(16, "little") != checksum:
+                raise AofError("header checksum mismatch at offset %d" % off)
+            if vsr_checksum(data[off + META + HEADER:off + META + size]).to_bytes(16, "little") != _cbody:
+                raise AofError("body checksum mismatch at op %d" % op)
         if validate_chain and last is not None and parent != last:
             raise AofError("checksum chain mismatch at op %d" % op)
         last = checksum
@@ -89,31 +98,41 @@ def read_entries(path, validate_chain=True):
     return out
 
 
-def read_prepares(path, validate_chain=True):
+def read_prepares(path, validate_chain=True, validate_checksums=True):
     """The committed prepares of an AOF in op order: `prepare` entries of state-machine operations
     (the replay skips VSR-reserved ones, src/aof.zig:349-350), one per op (duplicates — an AOF
-    can backtrack, :80-84 — must be identical)."""
-    by_op = {}
-    for command, p in read_entries(path, validate_chain):
-        if command != COMMAND_PREPARE or p.operation < VSR_OPERATIONS_RESERVED:
+    can backtrack, :80-84 — must be identical).  The prepare ops, VSR-reserved ones included, must
+    form one contiguous range: a missing op would replay a different history."""
+    by_op, all_ops = {}, set()
+    for command, p in read_entries(path, validate_chain, validate_checksums):
+        if command != COMMAND_PREPARE:
+            continue
+        all_ops.add(p.op)
+        if p.operation < VSR_OPERATIONS_RESERVED:
             continue
         prev = by_op.get(p.op)
         if prev is not None and (prev.timestamp, prev.operation, prev.body) != (p.timestamp, p.operation, p.body):
             raise AofError("op %d logged twice with different contents" % p.op)
         by_op[p.op] = p
+    if all_ops and len(all_ops) != max(all_ops) - min(all_ops) + 1:
+        missing = sorted(set(range(min(all_ops), max(all_ops) + 1)) - all_ops)
+        raise AofError("op sequence has gaps (first missing op %d, %d missing)" % (missing[0], len(missing)))
     return [by_op[k] for k in sorted(by_op)]
 
 
 def write_aof(path, prepares, replica=0, primary=0):
-    """Write prepares (op, timestamp, operation, body) in the AOF layout; placeholder checksums
-    (op-derived, not Aegis MACs) chained through `parent`."""
+    """Write prepares (op, timestamp, operation, body) in the AOF layout, with real checksums
+    (body, then header: set_checksum_body / set_checksum, src/vsr.zig:422-429) chained through
+    `parent`."""
     parent = b"\0" * 16
     with open(path, "wb") as f:
         for p in prepares:
             size = HEADER + len(p.body)
-            checksum = struct.pack("<QQ", 0x41_4F_46_00 ^ p.op, p.timestamp)
-            hdr = _HDR.pack(checksum, b"\0" * 16, parent, b"\0" * 16, b"\0" * 16, 0, 0, 0, 0, p.op, p.op, p.timestamp,
-                            size, replica, COMMAND_PREPARE, p.operation, 0)
+            cbody = vsr_checksum(p.body).to_bytes(16, "little")
+            rest = _HDR.pack(b"\0" * 16, cbody, parent, b"\0" * 16, b"\0" * 16, 0, 0, 0, 0, p.op, p.op, p.timestamp,
+                             size, replica, COMMAND_PREPARE, p.operation, 0)[16:]
+            checksum = vsr_checksum(rest).to_bytes(16, "little")
+            hdr = checksum + rest
             meta = MAGIC.to_bytes(16, "little") + struct.pack("<QQ", primary, replica) + b"\0" * 4064
             entry = meta + hdr + p.body
             f.write(entry + b"\0" * (_sector_ceil(len(entry)) - len(entry)))
@@ -121,6 +140,15 @@ def write_aof(path, prepares, replica=0, primary=0):
 
 
 def replay(prepares, state_machine):
-    """Commit every prepare into `state_machine` (anything with commit(operation, timestamp, body))
-    in op order; returns the replies."""
+    """Commit every prepare into `state_machine` in op order; returns the replies.  A StateMachine
+    (the reference interface: prepare / prefetch / commit(client, op, timestamp, operation, body),
+    src/state_machine.zig:336-540) is driven the way the replica drives it; an Engine or the oracle
+    takes commit(operation, timestamp, body)."""
+    if hasattr(state_machine, "prefetch"):
+        out = []
+        for p in prepares:
+            state_machine.prepare(p.operation, p.body)
+            state_machine.prefetch(lambda _sm: None, p.op, p.operation, p.body)
+            out.append(state_machine.commit(0, p.op, p.timestamp, p.operation, p.body))
+        return out
     return [state_machine.commit(p.operation, p.timestamp, p.body) for p in prepares]

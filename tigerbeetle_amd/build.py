@@ -15,6 +15,10 @@ LIB = os.path.join(PKG_DIR, "libtbgpu.so")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Werror=return-type"]
+# A/B timing builds only (tools/gpu/iter.sh): TBGPU_TIMING_KNOBS=1 compiles in the TBGPU_ABLATE /
+# TBGPU_FLOW_GRID / TBGPU_NO_FLOW / TBGPU_ACCOUNT_SLOTS environment knobs (csrc/pass.h TB_ABL).
+if os.environ.get("TBGPU_TIMING_KNOBS") == "1":
+    FLAGS.append("-DTBGPU_TIMING_KNOBS")
 
 
 def _sources():

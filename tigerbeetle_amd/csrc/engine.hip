@@ -24,6 +24,7 @@
 #include "k_replay.h"
 #include "k_route.h"
 #include "k_workload.h"
+#include "checksum.h"
 
 static thread_local std::string g_err;
 
@@ -90,7 +91,6 @@ struct tbgpu {
     // Parallel ordered fallback (k_flow.h): create_transfers passes run tb_flow instead of
     // tb_replay while no balance was set directly (the post/void assert argument, k_replay.h).
     bool flow_ok = false;
-    bool flow_coop = false;  // TBGPU_FLOW_COOP: hipLaunchCooperativeKernel (default: plain launch, same residency)
     bool balances_set = false;
     FlowArgs F{};
 
@@ -146,7 +146,7 @@ struct tbgpu {
     u64 ckpt_ts = 0;                 // commit timestamp at the previous write-back
     bool ckpt_valid = false;         // false: the snapshot is the empty state (zeroes)
     u32 prof_mask = ~0u;  // kernels timed when profiling (1 << K_*; tbgpu_bench_profile_mask)
-    u32 ablate = 0;
+    u32 ablate = 0;  // TBGPU_TIMING_KNOBS builds only
     std::vector<hipEvent_t> event_pool;
     size_t event_next = 0;
     std::vector<ProfilePair> prof;
@@ -256,7 +256,9 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     E->cfg = *config;
     E->device = config->device;
     E->profile = (config->flags & TBGPU_CONFIG_PROFILE) != 0;
+#ifdef TBGPU_TIMING_KNOBS
     if (const char* ab = getenv("TBGPU_ABLATE")) E->ablate = (u32)strtoul(ab, nullptr, 0);  // timing experiments only
+#endif
     int st = TBGPU_STATUS_OK;
 #define INIT_CK(x)                                                                                 \
     do {                                                                                           \
@@ -274,7 +276,9 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     // -2..10 % at C2, box to box) but double the legs buckets (tb_apply_legs +40 %): a net loss.
     // TBGPU_ACCOUNT_SLOTS overrides (experiments).
     u64 load = 2;
+#ifdef TBGPU_TIMING_KNOBS
     if (const char* s = getenv("TBGPU_ACCOUNT_SLOTS")) load = std::max<u64>(2, strtoull(s, nullptr, 0));
+#endif
     E->account_cap = pow2_at_least(std::max<u64>(load * config->accounts_max, 1024));
     // The index is sized for 2x the log so tombstones of withdrawn speculative inserts leave room.
     E->xlog_cap = std::max<u64>(config->transfers_max, 1024);
@@ -326,18 +330,26 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
             // A quarter of the CUs at most: co-residency of the grid then holds even with a few
             // engines (processes) sharing the device, each with a tb_flow in flight.
             E->F.grid = (u32)std::max(1, std::min(prop.multiProcessorCount / 4, 64));
-            E->flow_coop = getenv("TBGPU_FLOW_COOP") != nullptr;
+#ifdef TBGPU_TIMING_KNOBS
             if (const char* gs = getenv("TBGPU_FLOW_GRID")) E->F.grid = std::max(1u, std::min(E->F.grid, (u32)atoi(gs)));
+#endif
+            // tb_flow's grid barrier needs every workgroup resident: the launch is cooperative, so
+            // the runtime refuses it (an error status, never a spin) when the grid cannot be
+            // co-resident.  The grid is at most occupancy x CUs.
+            E->F.grid = (u32)std::min<u64>(E->F.grid, (u64)occ * prop.multiProcessorCount);
             int khz = 0;
             if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, E->device) != hipSuccess) khz = 0;
             khz = std::max(khz, 100000);  // s_memrealtime: 100 MHz on gfx9 parts; never trust a lower figure
             E->F.stall_ticks = 60ULL * 1000ULL * (u64)khz;  // 60 s
             E->wall_khz = (u64)khz;
-            if (getenv("TBGPU_DEBUG")) {
+            if (getenv("TBGPU_DEBUG")) {  // diagnostics only: changes no behaviour
                 fprintf(stderr, "tbgpu: flow grid %u, occupancy %d, wall clock %d kHz, stall ticks %llu\n", E->F.grid,
                         occ, khz, (unsigned long long)E->F.stall_ticks);
             }
-            E->flow_ok = E->pb_max <= FLOW_NB_MAX && getenv("TBGPU_NO_FLOW") == nullptr;
+            E->flow_ok = E->pb_max <= FLOW_NB_MAX && !(config->flags & TBGPU_CONFIG_SEQUENTIAL_FALLBACK);
+#ifdef TBGPU_TIMING_KNOBS
+            if (getenv("TBGPU_NO_FLOW")) E->flow_ok = false;
+#endif
         }
     }
     E->T.account_mask = E->account_cap - 1;
@@ -604,14 +616,9 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         if (flow) {
             UndoEntry* seq_undo = E->undo;
             u32 seq_cap = E->undo_cap;
-            if (E->flow_coop) {
-                void* args[] = {&P, &E->F, &seq_undo, &seq_cap};
-                HIPCK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&tb_flow), dim3(E->F.grid),
-                                                 dim3(FLOW_THREADS), args, 0, E->stream));
-            } else {
-                hipLaunchKernelGGL(tb_flow, dim3(E->F.grid), dim3(FLOW_THREADS), 0, E->stream, P, E->F, seq_undo, seq_cap);
-                HIPCK(hipGetLastError());
-            }
+            void* args[] = {&P, &E->F, &seq_undo, &seq_cap};
+            HIPCK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&tb_flow), dim3(E->F.grid), dim3(FLOW_THREADS),
+                                             args, 0, E->stream));
         } else if (op == OP_CREATE_TRANSFERS) {
             hipLaunchKernelGGL(tb_replay<OP_CREATE_TRANSFERS>, dim3(1), dim3(REPLAY_THREADS), 0, E->stream, P,
                                E->undo, E->undo_cap);
@@ -1229,6 +1236,11 @@ extern "C" void tbgpu_reset_stats(tbgpu_t* E) {
 }
 
 extern "C" const char* tbgpu_last_error(void) { return g_err.c_str(); }
+
+// vsr.checksum (src/vsr/checksum.zig:50): host only, no device or engine needed.
+extern "C" void tbgpu_checksum(const void* data, uint64_t len, uint8_t out[16]) {
+    tbck::checksum((const u8*)data, len, out);
+}
 
 // ------------------------------------------------------------------------------------------------
 // tbgpu_bench.h

@@ -25,7 +25,7 @@ __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
     u128 S;
     bool cert_global, cert64;
     tb_pass_cert(P, S, cert_global, cert64);
-    if (!cert64 || (P.ablate & ABL_LEG_WORK)) return;  // the resolve kernel applied every leg with u128 atomics
+    if (!cert64 || TB_ABL(P, ABL_LEG_WORK)) return;  // the resolve kernel applied every leg with u128 atomics
 
     const u32 g = blockIdx.x;
     const u32 W = 1u << P.leg_shift;

@@ -133,7 +133,7 @@ __device__ static inline u32 tb_hist16_inc(u32* s_hist, u32 bucket) {
 
 __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 L, u32 legmask, const u32* r_dr,
                                            const u32* r_cr, u32* s_hist, u16* s_perm, u32* s_wave) {
-    if (P.ablate & ABL_LEG_WORK) return;
+    if (TB_ABL(P, ABL_LEG_WORK)) return;
     __syncthreads();  // every count is in; s_perm's LDS is free
     tb_block_scan_lds((u16*)s_hist, P.leg_buckets, s_wave);
     const u16* h = (const u16*)s_hist;
@@ -149,7 +149,7 @@ __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 L, 
         s_perm[tb_hist16_inc(s_hist, r_cr[k] >> P.leg_shift)] = (u16)((i << 1) | 1);
     }
     __syncthreads();
-    if (P.ablate & ABL_LEG_STORES) return;
+    if (TB_ABL(P, ABL_LEG_STORES)) return;
     // Gather in groups of four (the loads of a group are in flight together: leg_w and leg_ev are
     // both u64 arrays, so the compiler would otherwise order each load after the previous store).
     const u64* __restrict__ ev = P.leg_ev + 2ULL * pbase;
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                             const u32 mask = (1u << P.leg_shift) - 1;
                             P.leg_ev[2 * (u64)pe] = ((((u64)(drs & mask) << 2) | pend) << LEG_AMT_BITS) | r_amt[k][0];
                             P.leg_ev[2 * (u64)pe + 1] = ((((u64)(crs & mask) << 2) | 2 | pend) << LEG_AMT_BITS) | r_amt[k][0];
-                            if (!(P.ablate & ABL_LEG_WORK)) {
+                            if (!TB_ABL(P, ABL_LEG_WORK)) {
                                 tb_hist16_inc(s_hist, drs >> P.leg_shift);
                                 tb_hist16_inc(s_hist, crs >> P.leg_shift);
                             }

@@ -69,9 +69,9 @@ __device__ static inline u32 tb_post_void_exists(const Transfer& t, const Transf
 __device__ static inline u32 tb_claim_id(const PassArgs& P, const Transfer& t, u32 pe, TransferScratch& s,
                                          u32* exists_pos, u64 first = ~0ULL) {
     s.kid = tb_dedup_key(tb_lo(t.id), tb_hi(t.id));
-    if (P.ablate & ABL_SPEC) return CLAIM_NEW;
+    if (TB_ABL(P, ABL_SPEC)) return CLAIM_NEW;
     u32 entry = TB_NOT_FOUND;
-    if (P.ablate & ABL_CAS) {  // timing only: no atomic claim
+    if (TB_ABL(P, ABL_CAS)) {  // timing only: no atomic claim
         s.rs = (u32)(tb_hash_id(tb_lo(t.id), tb_hi(t.id)) & P.T.xidx_mask);
         s.hz |= HZ_SPEC;
         return CLAIM_NEW;
@@ -216,14 +216,14 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     const u64 dpos = tb_hash_id(dlo, dhi) & T.account_mask;
     const u64 cpos = tb_hash_id(clo, chi) & T.account_mask;
     const u64 xpos = tb_hash_id(tb_lo(t.id), tb_hi(t.id)) & T.xidx_mask;
-    const bool fake = P.ablate & ABL_ACCTS;
+    const bool fake = TB_ABL(P, ABL_ACCTS);
     AccountHot d0 = {}, c0 = {};
     if (!fake) {
         d0 = T.acct_hot[dpos];
         c0 = T.acct_hot[cpos];
     }
     u64 x0 = ~0ULL;
-    if (!(P.ablate & (ABL_SPEC | ABL_CAS))) {
+    if (!TB_ABL(P, ABL_SPEC | ABL_CAS)) {
         x0 = tb_transfer_cas_home(T, tb_lo(t.id), tb_hi(t.id), (u32)(P.log_base + pe), xpos);
         if (x0 == 0) {
             s.rs = (u32)xpos;
@@ -272,7 +272,7 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     // then the timeout check (:862) is the next possible failure.
     const u64 timeout_ns = (u64)t.timeout * 1000000000ULL;
     if (ts + timeout_ns < ts) return CT_OVERFLOWS_TIMEOUT;  // entry withdrawn by kernel 2
-    if ((s.hz & HZ_SPEC) && !(P.ablate & ABL_RECORD)) s.rec_ts = ts;
+    if ((s.hz & HZ_SPEC) && !TB_ABL(P, ABL_RECORD)) s.rec_ts = ts;
     return R_OK;
 }
 
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
 
     const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
     const u32 count = min((u32)VALIDATE_THREADS, P.n - tile0);
-    tb_stage_tile<SRC>(P, tile0, count, stage, P.ablate & EXP_NT);
+    tb_stage_tile<SRC>(P, tile0, count, stage, TB_ABL(P, EXP_NT));
 
     const u32 pe = tile0 + threadIdx.x;  // pass-relative event
     const u64 e = P.e0 + pe;
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
         if ((rec >> row) & 1) {
             const u32x4 v = *(const u32x4*)(stage + tb_stage_off(w0 + row, part));
             u32x4* dst = (u32x4*)&P.T.xlog[P.log_base + tile0 + w0 + row] + part;
-            if (P.ablate & EXP_NT) __builtin_nontemporal_store(v, dst);
+            if (TB_ABL(P, EXP_NT)) __builtin_nontemporal_store(v, dst);
             else *dst = v;
         }
     }

@@ -65,7 +65,7 @@ struct PassArgs {
     u64* pass_words;       // == sum_shards
     u64 log_base;          // transfer-log position of event 0 of the pass
     Tables T;
-    u32 ablate;            // timing-only ablation bits (TBGPU_ABLATE env, never in a parity run)
+    u32 ablate;            // timing-only ablation bits (TBGPU_TIMING_KNOBS builds only: TB_ABL)
     // Routed mode (tbgpu_commit_routed_async, a shard of a multi-GPU pass): the events are this
     // shard's share of the global pass, in global order, with no linked/post/void/balancing event.
     u32 routed;            // 1: each event carries its execute timestamp in its timestamp field
@@ -109,6 +109,14 @@ __device__ static inline u64 tb_event_ts(const PassArgs& P, u32 b, u64 boff, u32
     return P.routed ? *(const u64*)(P.events + (boff + i) * 128 + 120) : P.batch_ts[b] - L + 1 + i;
 }
 
+// Timing-only ablations (A/B experiments with tools/gpu/ab.sh) exist only in a build with
+// -DTBGPU_TIMING_KNOBS; in the product build every check folds to false, so no environment
+// variable can switch off a validation step.
+#ifdef TBGPU_TIMING_KNOBS
+#define TB_ABL(P, bits) ((((P).ablate) & (bits)) != 0)
+#else
+#define TB_ABL(P, bits) false
+#endif
 enum : u32 { ABL_DEDUP = 1, ABL_SPEC = 2, ABL_ACCTS = 4, ABL_XFIND = 8, ABL_STAGE = 16, ABL_RECORD = 32, ABL_CAS = 64, EXP_NT = 128,
              ABL_LEGS = 256, ABL_LEG_STORES = 512, ABL_LEG_WORK = 1024,  // ABL_LEG_*: timing only (wrong balances)
              ABL_FLOW = 2048 };  // sequential replay instead of the parallel flow path (exact either way)

@@ -34,6 +34,7 @@ class Options:
     pass_batches_max: int = 512
     device: int = 0
     profile: bool = False
+    sequential_fallback: bool = False  # ordered fallback on one lane (tb_replay) instead of tb_flow
     # Reference cache options are accepted for interface parity; the HBM tables hold every object.
     lsm_forest_node_count: int = 0
     cache_entries_accounts: int = 0
@@ -50,7 +51,8 @@ class Engine:
         self.lib = _lib.load()
         cfg = _lib.tbgpu_config(options.accounts_max, options.transfers_max, options.pass_events_max,
                                 options.pass_batches_max, options.device,
-                                _lib.CONFIG_PROFILE if options.profile else 0)
+                                (_lib.CONFIG_PROFILE if options.profile else 0)
+                                | (_lib.CONFIG_SEQUENTIAL_FALLBACK if options.sequential_fallback else 0))
         h = ctypes.c_void_p()
         _lib.check(self.lib.tbgpu_init(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
