@@ -141,9 +141,26 @@ typedef struct tbgpu_delta_counts {
     uint64_t transfers;
     uint64_t posted;
 } tbgpu_delta_counts;
-int tbgpu_checkpoint_delta(tbgpu_t* engine, void* accounts_out, uint64_t accounts_cap, void* transfers_out,
-                           uint64_t transfers_cap, uint64_t* posted_out, uint64_t posted_cap,
+int tbgpu_checkpoint_delta(tbgpu_t* engine, void* accounts_out, void* accounts_before_out, uint64_t accounts_cap,
+                           void* transfers_out, uint64_t transfers_cap, uint64_t* posted_out, uint64_t posted_cap,
                            tbgpu_delta_counts* counts);
+/* accounts_before_out (nullable, 64 B per account): {dp, dpost, cp, cpost} as of the previous
+ * write-back (zero for accounts created since) — the old object a groove upsert diffs the balance
+ * index trees against (src/lsm/groove.zig:925-963). */
+
+/* Replica restart (StateMachine.open, src/state_machine.zig:322-334, then WAL replay from the
+ * checkpoint): the HBM tables start empty while the forest holds the checkpointed objects.  The
+ * wrapper's prefetch (src/state_machine.zig:345-506) reads the objects a prepare needs from the
+ * forest and loads the ones the engine lacks: objects the engine already holds are newer and are
+ * left as they are.  posted_state per transfer: 0 = no posted entry, 1 = posted, 2 = voided. */
+int tbgpu_load_accounts(tbgpu_t* engine, const void* accounts, uint32_t n);
+int tbgpu_load_transfers(tbgpu_t* engine, const void* transfers, const uint8_t* posted_state, uint32_t n);
+
+/* The replica writes StateMachine.commit_timestamp itself: the header timestamp after every commit
+ * (src/vsr/replica.zig:3664-3665) and the checkpoint's value on open / state sync.  The wrapper
+ * pushes a changed value here before the next commit, so the engine asserts what the reference
+ * asserts (timestamp > commit_timestamp, src/state_machine.zig:519). */
+int tbgpu_set_commit_timestamp(tbgpu_t* engine, uint64_t timestamp);
 
 typedef struct tbgpu_stats {
     uint64_t passes;

@@ -119,7 +119,10 @@ SIGNATURES = [
     ("tbgpu_device_free", ctypes.c_int, [_P, _P]),
     ("tbgpu_copy_to_host", ctypes.c_int, [_P, _P, _P, _U64]),
     ("tbgpu_register_host", ctypes.c_int, [_P, _P, _U64]),
-    ("tbgpu_checkpoint_delta", ctypes.c_int, [_P, _P, _U64, _P, _U64, _P, _U64, _P]),
+    ("tbgpu_checkpoint_delta", ctypes.c_int, [_P, _P, _P, _U64, _P, _U64, _P, _U64, _P]),
+    ("tbgpu_load_accounts", ctypes.c_int, [_P, _P, _U32]),
+    ("tbgpu_load_transfers", ctypes.c_int, [_P, _P, _P, _U32]),
+    ("tbgpu_set_commit_timestamp", ctypes.c_int, [_P, _U64]),
     ("tbgpu_unregister_host", ctypes.c_int, [_P, _P]),
     ("tbgpu_copy_to_device", ctypes.c_int, [_P, _P, _P, _U64]),
     ("tbgpu_marker", ctypes.c_int, [_P, _U32]),

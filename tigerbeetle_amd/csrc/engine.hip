@@ -1095,9 +1095,9 @@ extern "C" int tbgpu_export_posted(tbgpu_t* E, uint64_t* out_pairs, uint64_t cap
 // its forest since the previous call (or since init / reset) — state_machine.zig:542-582 with the
 // groove semantics of src/lsm/groove.zig:902-963.  Accounts by id, transfers and posted pairs by
 // timestamp.  If a buffer is too small nothing advances: *counts holds the sizes needed.
-extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, uint64_t accounts_cap, void* transfers_out,
-                                      uint64_t transfers_cap, uint64_t* posted_out, uint64_t posted_cap,
-                                      tbgpu_delta_counts* counts) {
+extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, void* accounts_before_out, uint64_t accounts_cap,
+                                      void* transfers_out, uint64_t transfers_cap, uint64_t* posted_out,
+                                      uint64_t posted_cap, tbgpu_delta_counts* counts) {
     HIPCK(hipSetDevice(E->device));
     memset(counts, 0, sizeof(*counts));
     if (E->pending) {
@@ -1115,14 +1115,16 @@ extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, uint64_t a
         E->ckpt_ts = 0;
     }
     const u64 chunk = 1ULL << 20;
-    std::vector<u8> accts, xfers;
+    std::vector<u8> accts, xfers, before;
     std::vector<u64> posted;
     u8* d_out = nullptr;
+    u8* d_before = nullptr;
     u64* d_cnt = nullptr;
     u64* d_posted = nullptr;
     hipError_t err = hipMalloc(&d_out, chunk * 128);
     if (err == hipSuccess) err = hipMalloc(&d_cnt, 24);
     if (err == hipSuccess) err = hipMalloc(&d_posted, chunk * 16);
+    if (err == hipSuccess) err = hipMalloc(&d_before, chunk * sizeof(AccountBal));
     for (int pass = 0; pass < 2 && err == hipSuccess; pass++) {
         const u64 cap = pass == 0 ? E->account_cap : E->xidx_cap;
         for (u64 s = 0; s < cap && err == hipSuccess; s += chunk) {
@@ -1131,7 +1133,7 @@ extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, uint64_t a
             if (err != hipSuccess) break;
             if (pass == 0) {
                 hipLaunchKernelGGL(tb_delta_accounts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T,
-                                   E->ckpt_bal, E->ckpt_ts, s, s + n, d_out, chunk, d_cnt);
+                                   E->ckpt_bal, E->ckpt_ts, s, s + n, d_out, chunk, d_cnt, (AccountBal*)d_before);
             } else {
                 hipLaunchKernelGGL(tb_delta_transfers, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T,
                                    E->ckpt_posted, E->ckpt_pos, s, n, d_out, chunk, d_cnt, d_posted, chunk, d_cnt + 1);
@@ -1145,6 +1147,10 @@ extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, uint64_t a
                 const size_t at = recs.size();
                 recs.resize(at + cnt[0] * 128);
                 err = hipMemcpy(recs.data() + at, d_out, cnt[0] * 128, hipMemcpyDeviceToHost);
+                if (err == hipSuccess && pass == 0) {
+                    before.resize(before.size() + cnt[0] * sizeof(AccountBal));
+                    err = hipMemcpy(before.data() + at / 2, d_before, cnt[0] * sizeof(AccountBal), hipMemcpyDeviceToHost);
+                }
             }
             if (err == hipSuccess && cnt[1]) {
                 const size_t at = posted.size();
@@ -1156,6 +1162,7 @@ extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, uint64_t a
     (void)hipFree(d_out);
     (void)hipFree(d_cnt);
     (void)hipFree(d_posted);
+    (void)hipFree(d_before);
     if (err != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "checkpoint delta: %s", hipGetErrorString(err));
     const u64 na = accts.size() / 128, nt = xfers.size() / 128, np = posted.size() / 2;
     counts->accounts = na;
@@ -1170,6 +1177,9 @@ extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, uint64_t a
     for (u64 i = 0; i < na; i++) idx[i] = i;
     std::sort(idx.begin(), idx.end(), [&](u64 a, u64 b) { return id_less(&accts[a * 128], &accts[b * 128]); });
     for (u64 i = 0; i < na; i++) memcpy((u8*)accounts_out + i * 128, &accts[idx[i] * 128], 128);
+    if (accounts_before_out) {
+        for (u64 i = 0; i < na; i++) memcpy((u8*)accounts_before_out + i * 64, &before[idx[i] * 64], 64);
+    }
     idx.resize(nt);
     for (u64 i = 0; i < nt; i++) idx[i] = i;
     std::sort(idx.begin(), idx.end(), [&](u64 a, u64 b) { return ts_of(&xfers[a * 128]) < ts_of(&xfers[b * 128]); });
@@ -1593,9 +1603,12 @@ extern "C" int tbgpu_fetch_transfers(tbgpu_t* E, const uint64_t* ids, uint32_t n
     return TBGPU_STATUS_OK;
 }
 
-extern "C" int tbgpu_upsert_accounts(tbgpu_t* E, const void* records, uint32_t n) {
+static int upsert_accounts(tbgpu* E, const void* records, uint32_t n, bool if_absent) {
     HIPCK(hipSetDevice(E->device));
-    E->balances_set = true;  // balances loaded from elsewhere: the sequential replay stays exact
+    // Balances set from elsewhere: the sequential replay stays exact.  A load of absent accounts
+    // from a consistent forest snapshot keeps the flow path's invariants (pending balances cover
+    // the outstanding pending transfers).
+    if (!if_absent) E->balances_set = true;
     if (E->pending) {
         int st = engine_sync(E);
         if (st) return st;
@@ -1621,7 +1634,7 @@ extern "C" int tbgpu_upsert_accounts(tbgpu_t* E, const void* records, uint32_t n
         HIPCK(hipMemcpyAsync(E->lookup_out, (const u8*)records + (u64)c * 128, (u64)m * 128, hipMemcpyHostToDevice,
                              E->stream));
         hipLaunchKernelGGL(tb_upsert_accounts, dim3((m + 255) / 256), dim3(256), 0, E->stream, E->T, E->lookup_out, m,
-                           E->d_status);
+                           E->d_status, if_absent ? 1u : 0u);
         HIPCK(hipGetLastError());
         HIPCK(hipStreamSynchronize(E->stream));
     }
@@ -1632,7 +1645,15 @@ extern "C" int tbgpu_upsert_accounts(tbgpu_t* E, const void* records, uint32_t n
     return TBGPU_STATUS_OK;
 }
 
-extern "C" int tbgpu_upsert_transfers(tbgpu_t* E, const void* records, const uint8_t* state, uint32_t n) {
+extern "C" int tbgpu_upsert_accounts(tbgpu_t* E, const void* records, uint32_t n) {
+    return upsert_accounts(E, records, n, false);
+}
+
+extern "C" int tbgpu_load_accounts(tbgpu_t* E, const void* records, uint32_t n) {
+    return upsert_accounts(E, records, n, true);
+}
+
+static int upsert_transfers(tbgpu* E, const void* records, const uint8_t* state, uint32_t n, bool if_absent) {
     HIPCK(hipSetDevice(E->device));
     if (E->pending) {
         int st = engine_sync(E);
@@ -1646,7 +1667,7 @@ extern "C" int tbgpu_upsert_transfers(tbgpu_t* E, const void* records, const uin
         HIPCK(hipMemcpyAsync(E->lookup_found, state + c, m, hipMemcpyHostToDevice, E->stream));
         HIPCK(hipMemsetAsync(E->d_status + 1, 0, 4, E->stream));
         hipLaunchKernelGGL(tb_upsert_transfers, dim3((m + 255) / 256), dim3(256), 0, E->stream, E->T, E->lookup_out,
-                           E->lookup_found, m, E->log_next, E->d_status + 1, E->d_status);
+                           E->lookup_found, m, E->log_next, E->d_status + 1, E->d_status, if_absent ? 1u : 0u);
         HIPCK(hipGetLastError());
         u32 added = 0;
         HIPCK(hipMemcpyAsync(&added, E->d_status + 1, 4, hipMemcpyDeviceToHost, E->stream));
@@ -1656,5 +1677,34 @@ extern "C" int tbgpu_upsert_transfers(tbgpu_t* E, const void* records, const uin
     u32 status = 0;
     HIPCK(hipMemcpy(&status, E->d_status, 4, hipMemcpyDeviceToHost));
     if (status) return fail(TBGPU_STATUS_PANIC, "transfer log or index full");
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_upsert_transfers(tbgpu_t* E, const void* records, const uint8_t* state, uint32_t n) {
+    return upsert_transfers(E, records, state, n, false);
+}
+
+extern "C" int tbgpu_load_transfers(tbgpu_t* E, const void* records, const uint8_t* posted_state, uint32_t n) {
+    // posted_state is {0 none, 1 posted, 2 voided}; the upsert kernel takes 1 + that.
+    std::vector<u8> st(n);
+    for (u32 i = 0; i < n; i++) {
+        if (posted_state[i] > POSTED_VOIDED) return fail(TBGPU_STATUS_INVALID, "posted state %u", posted_state[i]);
+        st[i] = (u8)(posted_state[i] + 1);
+    }
+    return upsert_transfers(E, records, st.data(), n, true);
+}
+
+// The replica writes commit_timestamp after every commit (= the prepare header's timestamp,
+// src/vsr/replica.zig:3664-3665) and on state sync; the engine's commit asserts use that value.
+extern "C" int tbgpu_set_commit_timestamp(tbgpu_t* E, uint64_t timestamp) {
+    HIPCK(hipSetDevice(E->device));
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    E->commit_ts = timestamp;
+    E->last_batch_ts = timestamp;
+    HIPCK(hipMemcpyAsync(&E->g->commit_timestamp, &E->commit_ts, 8, hipMemcpyHostToDevice, E->stream));
+    HIPCK(hipStreamSynchronize(E->stream));
     return TBGPU_STATUS_OK;
 }

@@ -97,7 +97,7 @@ __global__ void tb_zero_balances(Tables T, u64 cap) {
 // dirty mark in every balance-writing kernel of the hot path.  Counts past `cap` are still counted
 // (the host retries with room).
 __global__ void tb_delta_accounts(Tables T, const AccountBal* snap, u64 ts0, u64 first, u64 last, u8* out, u64 cap,
-                                  u64* count) {
+                                  u64* count, AccountBal* before) {
     const u64 i = first + (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= last) return;
     const AccountHot& h = T.acct_hot[i];
@@ -107,7 +107,12 @@ __global__ void tb_delta_accounts(Tables T, const AccountBal* snap, u64 ts0, u64
                       b.credits_pending == s.credits_pending && b.credits_posted == s.credits_posted;
     if (h.timestamp <= ts0 && same) return;
     const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
-    if (k < cap) *(Account*)(out + k * 128) = tb_account_load(T, (u32)i);
+    if (k < cap) {
+        *(Account*)(out + k * 128) = tb_account_load(T, (u32)i);
+        // The balances the forest holds for it (zero for an account created since): what a groove
+        // upsert diffs the balance index trees against (src/lsm/groove.zig:925-963).
+        if (before) before[k] = h.timestamp <= ts0 ? s : AccountBal{0, 0, 0, 0};
+    }
 }
 
 __global__ void tb_delta_transfers(Tables T, const u8* snap_posted, u64 pos0, u64 first, u64 n, u8* out, u64 cap,

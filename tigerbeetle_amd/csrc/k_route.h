@@ -234,12 +234,15 @@ __global__ void tb_fetch_transfers(Tables T, const u64* ids, u32 n, u8* out, u8*
 
 // Insert accounts verbatim (metadata + balances + timestamp), or overwrite the balances of an
 // existing one.  Ids within one call are distinct.  status: bit0 table full.
-__global__ void tb_upsert_accounts(Tables T, const u8* recs, u32 n, u32* status) {
+// if_absent (tbgpu_load_accounts): only accounts the table does not hold are inserted; a resident
+// account is newer than any copy from the forest and stays as it is.
+__global__ void tb_upsert_accounts(Tables T, const u8* recs, u32 n, u32* status, u32 if_absent) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const Account a = *(const Account*)(recs + (u64)i * 128);
     u32 slot = tb_account_find(T, tb_lo(a.id), tb_hi(a.id));
     if (slot != TB_NOT_FOUND) {
+        if (if_absent) return;
         AccountBal b;
         b.debits_pending = a.debits_pending;
         b.debits_posted = a.debits_posted;
@@ -260,13 +263,14 @@ __global__ void tb_upsert_accounts(Tables T, const u8* recs, u32 n, u32* status)
 // Insert transfers verbatim at the end of the log (state = 1 + POSTED_*), or set the posted state
 // of an existing one (state != 0).  Ids within one call are distinct.
 __global__ void tb_upsert_transfers(Tables T, const u8* recs, const u8* state, u32 n, u64 log_base, u32* counter,
-                                    u32* status) {
+                                    u32* status, u32 if_absent) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const Transfer& t = *(const Transfer*)(recs + (u64)i * 128);
     const u32 pos = tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id));
     const u8 st = state[i];
     if (pos != TB_NOT_FOUND) {
+        if (if_absent) return;
         if (st) T.xposted[pos] = st - 1;
         return;
     }

@@ -133,11 +133,12 @@ Delta StateMachine::checkpoint_delta() {
     tbgpu_delta_counts counts{1024, 1024, 1024};
     for (;;) {
         d.accounts.resize(counts.accounts * 128);
+        d.accounts_before.resize(counts.accounts * 64);
         d.transfers.resize(counts.transfers * 128);
         d.posted.resize(counts.posted * 2);
         const uint64_t caps[3] = {counts.accounts, counts.transfers, counts.posted};
-        const int st = tbgpu_checkpoint_delta(engine_, d.accounts.data(), caps[0], d.transfers.data(), caps[1],
-                                              d.posted.data(), caps[2], &counts);
+        const int st = tbgpu_checkpoint_delta(engine_, d.accounts.data(), d.accounts_before.data(), caps[0],
+                                              d.transfers.data(), caps[1], d.posted.data(), caps[2], &counts);
         if (st == TBGPU_STATUS_INVALID &&
             (counts.accounts > caps[0] || counts.transfers > caps[1] || counts.posted > caps[2])) {
             counts.accounts = std::max(counts.accounts, caps[0]);
@@ -147,6 +148,7 @@ Delta StateMachine::checkpoint_delta() {
         }
         check(st, "checkpoint_delta");
         d.accounts.resize(counts.accounts * 128);
+        d.accounts_before.resize(counts.accounts * 64);
         d.transfers.resize(counts.transfers * 128);
         d.posted.resize(counts.posted * 2);
         return d;

@@ -145,6 +145,7 @@ struct DeviceError : std::runtime_error {
 // {pending timestamp, fulfillment} (by timestamp).
 struct Delta {
     std::vector<uint8_t> accounts;
+    std::vector<uint8_t> accounts_before;  // 64 B per account: balances as of the previous write-back
     std::vector<uint8_t> transfers;
     std::vector<uint64_t> posted;
 };

@@ -194,16 +194,17 @@ class Engine:
         caps = [1024, 1024, 1024]
         while True:
             a = np.zeros(caps[0], dtype=ACCOUNT_DTYPE)
+            before = np.zeros((caps[0], 8), dtype=np.uint64)
             t = np.zeros(caps[1], dtype=TRANSFER_DTYPE)
             p = np.zeros((caps[2], 2), dtype=np.uint64)
-            st = self.lib.tbgpu_checkpoint_delta(self.h, a.ctypes.data, caps[0], t.ctypes.data, caps[1], p.ctypes.data,
-                                                 caps[2], ctypes.byref(counts))
+            st = self.lib.tbgpu_checkpoint_delta(self.h, a.ctypes.data, before.ctypes.data, caps[0], t.ctypes.data,
+                                                 caps[1], p.ctypes.data, caps[2], ctypes.byref(counts))
             need = [counts.accounts, counts.transfers, counts.posted]
             if st == _lib.STATUS_INVALID and any(n > c for n, c in zip(need, caps)):
                 caps = [max(c, n) for c, n in zip(caps, need)]
                 continue
             _lib.check(st)
-            return Delta(a[:need[0]], t[:need[1]], p[:need[2]])
+            return Delta(a[:need[0]], t[:need[1]], p[:need[2]], before[:need[0]])
 
     def legs_min_events(self, events):
         """Passes of >= events transfers use the sorted balance legs (0: every pass)."""
@@ -241,6 +242,22 @@ class Engine:
         records = np.ascontiguousarray(records, dtype=ACCOUNT_DTYPE)
         if len(records):
             _lib.check(self.lib.tbgpu_upsert_accounts(self.h, records.ctypes.data, len(records)))
+
+    def load_accounts(self, records):
+        """Insert the accounts the engine lacks (replica restart warm-up, tbgpu_load_accounts)."""
+        records = np.ascontiguousarray(records, dtype=ACCOUNT_DTYPE)
+        if len(records):
+            _lib.check(self.lib.tbgpu_load_accounts(self.h, records.ctypes.data, len(records)))
+
+    def load_transfers(self, records, posted_state):
+        records = np.ascontiguousarray(records, dtype=TRANSFER_DTYPE)
+        posted_state = np.ascontiguousarray(posted_state, dtype=np.uint8)
+        if len(records):
+            _lib.check(self.lib.tbgpu_load_transfers(self.h, records.ctypes.data, posted_state.ctypes.data,
+                                                     len(records)))
+
+    def set_commit_timestamp(self, timestamp):
+        _lib.check(self.lib.tbgpu_set_commit_timestamp(self.h, int(timestamp)))
 
     def upsert_transfers(self, records, state):
         records = np.ascontiguousarray(records, dtype=TRANSFER_DTYPE)
@@ -299,6 +316,8 @@ class Delta:
     accounts: np.ndarray
     transfers: np.ndarray
     posted: np.ndarray
+    # [n, 8] u64: {dp, dpost, cp, cpost} (lo, hi) of each account as of the previous write-back
+    accounts_before: np.ndarray = None
 
 
 class StateMachine:
