@@ -140,6 +140,8 @@ typedef struct tbgpu_delta_counts {
     uint64_t accounts;
     uint64_t transfers;
     uint64_t posted;
+    uint64_t created_after;  /* accounts with a timestamp above this were created since the previous
+                                write-back (groove insert); the others changed (groove upsert) */
 } tbgpu_delta_counts;
 int tbgpu_checkpoint_delta(tbgpu_t* engine, void* accounts_out, void* accounts_before_out, uint64_t accounts_cap,
                            void* transfers_out, uint64_t transfers_cap, uint64_t* posted_out, uint64_t posted_cap,

@@ -153,3 +153,21 @@ def test_restart_from_forest(config, gpu_engine_factory):
     assert transfers == _rows(oracle.export_transfers())
     assert posted == _posted(oracle.export_posted())
     assert engine.commit_timestamp == oracle.commit_timestamp
+
+    # The restarted engine's next write-back: loaded objects are not new, re-balanced ones carry
+    # the forest's balances as `before`, and applying it (insert / upsert) rebuilds the oracle.
+    d = engine.checkpoint_delta()
+    for rec, before in zip(d.accounts.view(np.uint8).reshape(-1, 128), d.accounts_before):
+        key = bytes(rec[:16])
+        if int.from_bytes(bytes(rec[120:128]), "little") > d.created_after:
+            assert key not in forest_a and not before.any()  # groove insert
+        else:
+            assert np.array_equal(before, np.frombuffer(forest_a[key][16:80], dtype=np.uint64))  # upsert
+    new_t = _rows(d.transfers)
+    assert not set(new_t) & set(forest_t)  # every transfer in the delta is a groove insert
+    forest_a.update(_rows(d.accounts))
+    forest_t.update(new_t)
+    forest_p.update(_posted(d.posted))
+    assert forest_a == _rows(oracle.export_accounts())
+    assert forest_t == _rows(oracle.export_transfers())
+    assert forest_p == _posted(oracle.export_posted())

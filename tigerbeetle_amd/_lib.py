@@ -29,7 +29,8 @@ class tbgpu_config(ctypes.Structure):
 
 
 class tbgpu_delta_counts(ctypes.Structure):
-    _fields_ = [("accounts", ctypes.c_uint64), ("transfers", ctypes.c_uint64), ("posted", ctypes.c_uint64)]
+    _fields_ = [("accounts", ctypes.c_uint64), ("transfers", ctypes.c_uint64), ("posted", ctypes.c_uint64),
+                ("created_after", ctypes.c_uint64)]
 
 
 class tbgpu_stats(ctypes.Structure):

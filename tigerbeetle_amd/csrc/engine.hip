@@ -1095,15 +1095,8 @@ extern "C" int tbgpu_export_posted(tbgpu_t* E, uint64_t* out_pairs, uint64_t cap
 // its forest since the previous call (or since init / reset) — state_machine.zig:542-582 with the
 // groove semantics of src/lsm/groove.zig:902-963.  Accounts by id, transfers and posted pairs by
 // timestamp.  If a buffer is too small nothing advances: *counts holds the sizes needed.
-extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, void* accounts_before_out, uint64_t accounts_cap,
-                                      void* transfers_out, uint64_t transfers_cap, uint64_t* posted_out,
-                                      uint64_t posted_cap, tbgpu_delta_counts* counts) {
-    HIPCK(hipSetDevice(E->device));
-    memset(counts, 0, sizeof(*counts));
-    if (E->pending) {
-        int st = engine_sync(E);
-        if (st) return st;
-    }
+// The write-back snapshot exists and describes the previous write-back (the empty state if none).
+static int ckpt_snapshot_ready(tbgpu* E) {
     if (!E->ckpt_bal) {
         HIPCK(hipMalloc(&E->ckpt_bal, E->account_cap * sizeof(AccountBal)));
         HIPCK(hipMalloc(&E->ckpt_posted, E->xlog_cap));
@@ -1113,7 +1106,22 @@ extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, void* acco
         HIPCK(hipMemsetAsync(E->ckpt_posted, 0, E->xlog_cap, E->stream));
         E->ckpt_pos = 0;
         E->ckpt_ts = 0;
+        E->ckpt_valid = true;
     }
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, void* accounts_before_out, uint64_t accounts_cap,
+                                      void* transfers_out, uint64_t transfers_cap, uint64_t* posted_out,
+                                      uint64_t posted_cap, tbgpu_delta_counts* counts) {
+    HIPCK(hipSetDevice(E->device));
+    memset(counts, 0, sizeof(*counts));
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    int st0 = ckpt_snapshot_ready(E);
+    if (st0) return st0;
     const u64 chunk = 1ULL << 20;
     std::vector<u8> accts, xfers, before;
     std::vector<u64> posted;
@@ -1136,7 +1144,8 @@ extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, void* acco
                                    E->ckpt_bal, E->ckpt_ts, s, s + n, d_out, chunk, d_cnt, (AccountBal*)d_before);
             } else {
                 hipLaunchKernelGGL(tb_delta_transfers, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T,
-                                   E->ckpt_posted, E->ckpt_pos, s, n, d_out, chunk, d_cnt, d_posted, chunk, d_cnt + 1);
+                                   E->ckpt_posted, E->ckpt_pos, E->ckpt_ts, s, n, d_out, chunk, d_cnt, d_posted, chunk,
+                                   d_cnt + 1);
             }
             err = hipGetLastError();
             u64 cnt[2] = {0, 0};
@@ -1165,6 +1174,7 @@ extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, void* acco
     (void)hipFree(d_before);
     if (err != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "checkpoint delta: %s", hipGetErrorString(err));
     const u64 na = accts.size() / 128, nt = xfers.size() / 128, np = posted.size() / 2;
+    counts->created_after = E->ckpt_ts;
     counts->accounts = na;
     counts->transfers = nt;
     counts->posted = np;
@@ -1603,8 +1613,25 @@ extern "C" int tbgpu_fetch_transfers(tbgpu_t* E, const uint64_t* ids, uint32_t n
     return TBGPU_STATUS_OK;
 }
 
+// A load (if_absent) brings objects from the forest: they are already written back, so the
+// write-back snapshot takes their state too, and the "created since" timestamp covers them.
+static int load_snapshot(tbgpu* E, const void* records, uint32_t n) {
+    int st = ckpt_snapshot_ready(E);
+    if (st) return st;
+    for (u32 i = 0; i < n; i++) E->ckpt_ts = std::max(E->ckpt_ts, *(const u64*)((const u8*)records + (u64)i * 128 + 120));
+    return TBGPU_STATUS_OK;
+}
+
 static int upsert_accounts(tbgpu* E, const void* records, uint32_t n, bool if_absent) {
     HIPCK(hipSetDevice(E->device));
+    if (if_absent) {
+        if (E->pending) {
+            int st = engine_sync(E);
+            if (st) return st;
+        }
+        int st = load_snapshot(E, records, n);
+        if (st) return st;
+    }
     // Balances set from elsewhere: the sequential replay stays exact.  A load of absent accounts
     // from a consistent forest snapshot keeps the flow path's invariants (pending balances cover
     // the outstanding pending transfers).
@@ -1634,7 +1661,7 @@ static int upsert_accounts(tbgpu* E, const void* records, uint32_t n, bool if_ab
         HIPCK(hipMemcpyAsync(E->lookup_out, (const u8*)records + (u64)c * 128, (u64)m * 128, hipMemcpyHostToDevice,
                              E->stream));
         hipLaunchKernelGGL(tb_upsert_accounts, dim3((m + 255) / 256), dim3(256), 0, E->stream, E->T, E->lookup_out, m,
-                           E->d_status, if_absent ? 1u : 0u);
+                           E->d_status, if_absent ? 1u : 0u, if_absent ? E->ckpt_bal : nullptr);
         HIPCK(hipGetLastError());
         HIPCK(hipStreamSynchronize(E->stream));
     }
@@ -1655,6 +1682,14 @@ extern "C" int tbgpu_load_accounts(tbgpu_t* E, const void* records, uint32_t n) 
 
 static int upsert_transfers(tbgpu* E, const void* records, const uint8_t* state, uint32_t n, bool if_absent) {
     HIPCK(hipSetDevice(E->device));
+    if (if_absent) {
+        if (E->pending) {
+            int st = engine_sync(E);
+            if (st) return st;
+        }
+        int st = load_snapshot(E, records, n);
+        if (st) return st;
+    }
     if (E->pending) {
         int st = engine_sync(E);
         if (st) return st;
@@ -1667,7 +1702,8 @@ static int upsert_transfers(tbgpu* E, const void* records, const uint8_t* state,
         HIPCK(hipMemcpyAsync(E->lookup_found, state + c, m, hipMemcpyHostToDevice, E->stream));
         HIPCK(hipMemsetAsync(E->d_status + 1, 0, 4, E->stream));
         hipLaunchKernelGGL(tb_upsert_transfers, dim3((m + 255) / 256), dim3(256), 0, E->stream, E->T, E->lookup_out,
-                           E->lookup_found, m, E->log_next, E->d_status + 1, E->d_status, if_absent ? 1u : 0u);
+                           E->lookup_found, m, E->log_next, E->d_status + 1, E->d_status, if_absent ? 1u : 0u,
+                           if_absent ? E->ckpt_posted : nullptr);
         HIPCK(hipGetLastError());
         u32 added = 0;
         HIPCK(hipMemcpyAsync(&added, E->d_status + 1, 4, hipMemcpyDeviceToHost, E->stream));

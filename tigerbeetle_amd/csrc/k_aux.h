@@ -115,15 +115,18 @@ __global__ void tb_delta_accounts(Tables T, const AccountBal* snap, u64 ts0, u64
     }
 }
 
-__global__ void tb_delta_transfers(Tables T, const u8* snap_posted, u64 pos0, u64 first, u64 n, u8* out, u64 cap,
-                                   u64* count, u64* posted_out, u64 posted_cap, u64* posted_count) {
+// A transfer is new since the previous write-back if it sits past that write-back's log position
+// and is younger than its commit timestamp (positions past pos0 also hold objects loaded from the
+// forest after a restart, which are older).
+__global__ void tb_delta_transfers(Tables T, const u8* snap_posted, u64 pos0, u64 ts0, u64 first, u64 n, u8* out,
+                                   u64 cap, u64* count, u64* posted_out, u64 posted_cap, u64* posted_count) {
     const u64 i = first + (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= first + n) return;
     const u64 e = T.xidx[i];
     if (e == 0 || (e & XI_TOMB)) return;
     const u32 pos = tb_xi_pos(e);
     const Transfer& t = T.xlog[pos];
-    if (pos >= pos0) {
+    if (pos >= pos0 && t.timestamp > ts0) {
         const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
         if (k < cap) *(Transfer*)(out + k * 128) = t;
     }

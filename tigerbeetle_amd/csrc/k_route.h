@@ -236,7 +236,7 @@ __global__ void tb_fetch_transfers(Tables T, const u64* ids, u32 n, u8* out, u8*
 // existing one.  Ids within one call are distinct.  status: bit0 table full.
 // if_absent (tbgpu_load_accounts): only accounts the table does not hold are inserted; a resident
 // account is newer than any copy from the forest and stays as it is.
-__global__ void tb_upsert_accounts(Tables T, const u8* recs, u32 n, u32* status, u32 if_absent) {
+__global__ void tb_upsert_accounts(Tables T, const u8* recs, u32 n, u32* status, u32 if_absent, AccountBal* snap) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const Account a = *(const Account*)(recs + (u64)i * 128);
@@ -257,13 +257,14 @@ __global__ void tb_upsert_accounts(Tables T, const u8* recs, u32 n, u32* status,
         return;
     }
     tb_account_store_new(T, slot, a);
+    if (snap) snap[slot] = T.acct_bal[slot];  // loaded from the forest: written back already
     atomicAdd((unsigned long long*)&T.g->account_count, 1ULL);
 }
 
 // Insert transfers verbatim at the end of the log (state = 1 + POSTED_*), or set the posted state
 // of an existing one (state != 0).  Ids within one call are distinct.
 __global__ void tb_upsert_transfers(Tables T, const u8* recs, const u8* state, u32 n, u64 log_base, u32* counter,
-                                    u32* status, u32 if_absent) {
+                                    u32* status, u32 if_absent, u8* snap_posted) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const Transfer& t = *(const Transfer*)(recs + (u64)i * 128);
@@ -281,6 +282,7 @@ __global__ void tb_upsert_transfers(Tables T, const u8* recs, const u8* state, u
     }
     T.xlog[lp] = t;
     T.xposted[lp] = st ? st - 1 : POSTED_NONE;
+    if (snap_posted) snap_posted[lp] = T.xposted[lp];
     __threadfence();
     if (tb_transfer_claim_new(T, tb_lo(t.id), tb_hi(t.id), (u32)lp) == TB_NOT_FOUND) atomicOr(status, 1u);
     atomicAdd((unsigned long long*)&T.g->transfer_count, 1ULL);

@@ -130,7 +130,7 @@ void StateMachine::compact(const Callback& callback, uint64_t op) {
 
 Delta StateMachine::checkpoint_delta() {
     Delta d;
-    tbgpu_delta_counts counts{1024, 1024, 1024};
+    tbgpu_delta_counts counts{1024, 1024, 1024, 0};
     for (;;) {
         d.accounts.resize(counts.accounts * 128);
         d.accounts_before.resize(counts.accounts * 64);
@@ -151,6 +151,7 @@ Delta StateMachine::checkpoint_delta() {
         d.accounts_before.resize(counts.accounts * 64);
         d.transfers.resize(counts.transfers * 128);
         d.posted.resize(counts.posted * 2);
+        d.created_after = counts.created_after;
         return d;
     }
 }

@@ -146,6 +146,7 @@ struct DeviceError : std::runtime_error {
 struct Delta {
     std::vector<uint8_t> accounts;
     std::vector<uint8_t> accounts_before;  // 64 B per account: balances as of the previous write-back
+    uint64_t created_after = 0;            // accounts with a later timestamp are new (insert)
     std::vector<uint8_t> transfers;
     std::vector<uint64_t> posted;
 };

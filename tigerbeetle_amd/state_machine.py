@@ -204,7 +204,7 @@ class Engine:
                 caps = [max(c, n) for c, n in zip(caps, need)]
                 continue
             _lib.check(st)
-            return Delta(a[:need[0]], t[:need[1]], p[:need[2]], before[:need[0]])
+            return Delta(a[:need[0]], t[:need[1]], p[:need[2]], before[:need[0]], counts.created_after)
 
     def legs_min_events(self, events):
         """Passes of >= events transfers use the sorted balance legs (0: every pass)."""
@@ -318,6 +318,8 @@ class Delta:
     posted: np.ndarray
     # [n, 8] u64: {dp, dpost, cp, cpost} (lo, hi) of each account as of the previous write-back
     accounts_before: np.ndarray = None
+    # accounts with a timestamp above this were created since the previous write-back (insert)
+    created_after: int = 0
 
 
 class StateMachine:

@@ -1,83 +1,253 @@
-//! state_machine_gpu.zig — the reference-side binding a maintainer would add to route
-//! StateMachine.commit(create_accounts | create_transfers | lookup_*) to the MI355X engine.
+//! state_machine_gpu.zig — the reference-side binding a maintainer adds to run
+//! StateMachine.commit (create_accounts, create_transfers, lookup_accounts, lookup_transfers) on the
+//! MI355X engine (include/tbgpu.h), with the reference's LSM forest kept as the durable store.
 //!
-//! SOURCE ONLY: this image has no Zig toolchain, so this file is not compiled here.  It shows the
-//! wrapper shape against the reference's comptime duck-typed interface
-//! (src/state_machine.zig:28-1150, consumers src/vsr/replica.zig and src/testing/cluster.zig:49-55,
-//! SURVEY.md §8b).  Link with `-ltbgpu` and add `include/` to the C include path in build.zig.
+//! SOURCE ONLY: this image has no Zig toolchain (Zig 0.11, scripts/install_zig.sh needs network),
+//! so this file is checked by review against every member the reference's consumers use:
+//!   * the replica (src/vsr/replica.zig): init (:832), deinit, reset (:7763), open (:662, :7835),
+//!     prepare (:5137), prefetch (:3347), commit (:3654), compact (:3088), checkpoint (:3093), the
+//!     fields prepare_timestamp / commit_timestamp (:3621-3665, :5122-5131, :6854-6861) and forest
+//!     (state sync, :7903-7942), the decls Operation, Options, Forest;
+//!   * the cluster harness (src/testing/cluster.zig:49-55, :514, :534): Forest, forest, Options;
+//!   * clients / simulator / CLI: constants, Event, Result, Workload, PostedGrooveValue,
+//!     forest_options (src/tigerbeetle/cli.zig:278, src/lsm/forest_fuzz.zig:59).
+//! It is the reference StateMachine's shape (src/state_machine.zig:28-1150) with execute() replaced
+//! by the engine; the forest, its grooves and their persistence are the reference's own.
+//!
+//! Data flow:
+//!   commit      -> tbgpu_commit (the HBM tables are the state of record while the process lives);
+//!   compact     -> at the last op of every bar, the objects the engine changed during the bar go
+//!                  into the grooves (insert / upsert, src/lsm/groove.zig:902-963) before
+//!                  forest.compact, so each bar's table_mutable receives what the reference's own
+//!                  commits would have put there (bounded by the same value_count_max,
+//!                  src/state_machine.zig:100-178);
+//!   checkpoint  -> forest.checkpoint (the bar's write-back already happened in compact);
+//!   open        -> forest.open; if the forest already holds objects (a restart), prefetch runs
+//!                  the reference's groove prefetch and loads what a prepare reads and the engine
+//!                  lacks (tbgpu_load_*), before the replica commits it.
+//! Build: add include/ to the C include path and link tigerbeetle_amd/libtbgpu.so (INTEGRATION.md),
+//! then instantiate ReplicaType with this StateMachineType (src/tigerbeetle/main.zig:28-32).
 
 const std = @import("std");
 const assert = std.debug.assert;
+const mem = std.mem;
 
 const tbgpu = @cImport({
     @cInclude("tbgpu.h");
 });
 
+const global_constants = @import("constants.zig");
+const tb = @import("tigerbeetle.zig");
+const Account = tb.Account;
+const Transfer = tb.Transfer;
+const GridType = @import("vsr/grid.zig").GridType;
 const ReferenceStateMachineType = @import("state_machine.zig").StateMachineType;
 
-pub fn StateMachineType(comptime Storage: type, comptime config: @import("constants.zig").StateMachineConfig) type {
-    // Keep the reference type for everything the engine does not replace (Forest, Workload,
-    // prefetch plumbing, compaction and checkpoint of the LSM forest for durability).
+pub fn StateMachineType(
+    comptime Storage: type,
+    comptime config: global_constants.StateMachineConfig,
+) type {
+    // The reference type supplies the types (Forest and its grooves, Operation, Workload, ...);
+    // no instance of it exists.
     const Base = ReferenceStateMachineType(Storage, config);
 
     return struct {
         const StateMachine = @This();
+        const Grid = GridType(Storage);
+
         pub const Operation = Base.Operation;
-        pub const Options = Base.Options;
         pub const Forest = Base.Forest;
         pub const Workload = Base.Workload;
         pub const constants = Base.constants;
         pub const Event = Base.Event;
         pub const Result = Base.Result;
+        pub const PostedGrooveValue = Base.PostedGrooveValue;
 
-        base: Base,
+        const AccountsGroove = std.meta.FieldType(Forest.Grooves, .accounts);
+        const TransfersGroove = std.meta.FieldType(Forest.Grooves, .transfers);
+        const PostedGroove = std.meta.FieldType(Forest.Grooves, .posted);
+
+        /// The reference's options (src/state_machine.zig:216-221) plus the engine's HBM sizing.
+        /// The cache_entries_* knobs size the groove caches, not the number of objects, so the
+        /// engine has its own: every account and transfer the cluster will ever hold must fit the
+        /// device (DESIGN.md §2b: at most 2^31 of each; init fails if HBM is short).
+        pub const Options = struct {
+            lsm_forest_node_count: u32,
+            cache_entries_accounts: u32,
+            cache_entries_transfers: u32,
+            cache_entries_posted: u32,
+            engine_accounts_max: u64 = 1 << 26,
+            engine_transfers_max: u64 = 1 << 30,
+            engine_device: i32 = 0,
+
+            fn base(options: Options) Base.Options {
+                return .{
+                    .lsm_forest_node_count = options.lsm_forest_node_count,
+                    .cache_entries_accounts = options.cache_entries_accounts,
+                    .cache_entries_transfers = options.cache_entries_transfers,
+                    .cache_entries_posted = options.cache_entries_posted,
+                };
+            }
+        };
+
+        pub fn forest_options(options: Options) Forest.GroovesOptions {
+            return Base.forest_options(options.base());
+        }
+
+        // One bar of engine changes, the most the grooves accept per bar
+        // (value_count_max, src/state_machine.zig:100-178).
+        const bar_transfers_max = config.lsm_batch_multiple * constants.batch_max.create_transfers;
+        const bar_accounts_max = config.lsm_batch_multiple *
+            @max(constants.batch_max.create_accounts, 2 * constants.batch_max.create_transfers);
+        // Objects one prepare can read (the groove prefetch_entries_max, :1091-1146).
+        const prepare_accounts_max = @max(constants.batch_max.create_accounts, 2 * constants.batch_max.create_transfers);
+        const prepare_transfers_max = 2 * constants.batch_max.create_transfers;
+
+        const PrefetchContext = union(enum) {
+            accounts: AccountsGroove.PrefetchContext,
+            transfers: TransfersGroove.PrefetchContext,
+            posted: PostedGroove.PrefetchContext,
+        };
+
+        prepare_timestamp: u64,
+        commit_timestamp: u64,
+        forest: Forest,
+
         engine: *tbgpu.tbgpu_t,
+        /// commit_timestamp as the engine last saw it: the replica writes the field itself.
+        engine_commit_timestamp: u64 = 0,
+        /// The engine holds every object the forest holds (a freshly formatted cluster).  False
+        /// after open() finds objects in the forest, for the rest of the process.
+        engine_complete: bool = true,
 
-        // Mirrored fields the replica reads and writes (replica.zig:3621-3665, :5122-5131).
-        prepare_timestamp: u64 = 0,
-        commit_timestamp: u64 = 0,
+        prefetch_input: ?[]align(16) const u8 = null,
+        prefetch_operation: Operation = undefined,
+        prefetch_callback: ?*const fn (*StateMachine) void = null,
+        prefetch_context: PrefetchContext = undefined,
 
-        pub fn init(allocator: std.mem.Allocator, grid: anytype, options: Options) !StateMachine {
-            var base = try Base.init(allocator, grid, options);
-            errdefer base.deinit(allocator);
+        open_callback: ?*const fn (*StateMachine) void = null,
+        compact_callback: ?*const fn (*StateMachine) void = null,
+        checkpoint_callback: ?*const fn (*StateMachine) void = null,
+
+        // Static allocation (allocated in init, never resized).
+        writeback_accounts: []Account,
+        writeback_accounts_before: [][4]u128,
+        writeback_transfers: []Transfer,
+        writeback_posted: [][2]u64,
+        load_accounts: []Account,
+        load_transfers: []Transfer,
+        load_posted: []u8,
+
+        pub fn init(allocator: mem.Allocator, grid: *Grid, options: Options) !StateMachine {
+            var forest = try Forest.init(allocator, grid, options.lsm_forest_node_count, forest_options(options));
+            errdefer forest.deinit(allocator);
+
             const engine_config = tbgpu.tbgpu_config{
-                .accounts_max = options.cache_entries_accounts,
-                .transfers_max = options.cache_entries_transfers,
+                .accounts_max = options.engine_accounts_max,
+                .transfers_max = options.engine_transfers_max,
                 .pass_events_max = constants.batch_max.create_transfers,
                 .pass_batches_max = 1,
-                .device = 0,
+                .device = options.engine_device,
                 .flags = 0,
             };
             var engine: ?*tbgpu.tbgpu_t = null;
-            if (tbgpu.tbgpu_init(&engine_config, &engine) != tbgpu.TBGPU_STATUS_OK) return error.DeviceInit;
-            return .{ .base = base, .engine = engine.? };
+            if (tbgpu.tbgpu_init(&engine_config, &engine) != tbgpu.TBGPU_STATUS_OK) return error.EngineInit;
+            errdefer tbgpu.tbgpu_deinit(engine);
+
+            const writeback_accounts = try allocator.alloc(Account, bar_accounts_max);
+            errdefer allocator.free(writeback_accounts);
+            const writeback_accounts_before = try allocator.alloc([4]u128, bar_accounts_max);
+            errdefer allocator.free(writeback_accounts_before);
+            const writeback_transfers = try allocator.alloc(Transfer, bar_transfers_max);
+            errdefer allocator.free(writeback_transfers);
+            const writeback_posted = try allocator.alloc([2]u64, bar_transfers_max);
+            errdefer allocator.free(writeback_posted);
+            const load_accounts = try allocator.alloc(Account, prepare_accounts_max);
+            errdefer allocator.free(load_accounts);
+            const load_transfers = try allocator.alloc(Transfer, prepare_transfers_max);
+            errdefer allocator.free(load_transfers);
+            const load_posted = try allocator.alloc(u8, prepare_transfers_max);
+            errdefer allocator.free(load_posted);
+
+            return StateMachine{
+                .prepare_timestamp = 0,
+                .commit_timestamp = 0,
+                .forest = forest,
+                .engine = engine.?,
+                .writeback_accounts = writeback_accounts,
+                .writeback_accounts_before = writeback_accounts_before,
+                .writeback_transfers = writeback_transfers,
+                .writeback_posted = writeback_posted,
+                .load_accounts = load_accounts,
+                .load_transfers = load_transfers,
+                .load_posted = load_posted,
+            };
         }
 
-        pub fn deinit(self: *StateMachine, allocator: std.mem.Allocator) void {
+        pub fn deinit(self: *StateMachine, allocator: mem.Allocator) void {
+            allocator.free(self.load_posted);
+            allocator.free(self.load_transfers);
+            allocator.free(self.load_accounts);
+            allocator.free(self.writeback_posted);
+            allocator.free(self.writeback_transfers);
+            allocator.free(self.writeback_accounts_before);
+            allocator.free(self.writeback_accounts);
             tbgpu.tbgpu_deinit(self.engine);
-            self.base.deinit(allocator);
+            self.forest.deinit(allocator);
         }
 
         pub fn reset(self: *StateMachine) void {
-            self.base.reset();
-            if (tbgpu.tbgpu_reset(self.engine) != tbgpu.TBGPU_STATUS_OK) @panic("tbgpu_reset");
+            self.forest.reset();
+            check(tbgpu.tbgpu_reset(self.engine));
             self.prepare_timestamp = 0;
             self.commit_timestamp = 0;
+            self.engine_commit_timestamp = 0;
+            self.engine_complete = true;
+            self.prefetch_input = null;
+            self.prefetch_callback = null;
+            self.open_callback = null;
+            self.compact_callback = null;
+            self.checkpoint_callback = null;
+        }
+
+        fn check(status: c_int) void {
+            if (status != tbgpu.TBGPU_STATUS_OK) @panic(std.mem.span(tbgpu.tbgpu_last_error()));
         }
 
         pub fn open(self: *StateMachine, callback: *const fn (*StateMachine) void) void {
-            _ = self;
-            _ = callback;
-            @compileError("forward to Base.open with a callback adapter");
+            assert(self.open_callback == null);
+            self.open_callback = callback;
+            self.forest.open(forest_open_callback);
         }
 
+        fn forest_open_callback(forest: *Forest) void {
+            const self = @fieldParentPtr(StateMachine, "forest", forest);
+            const callback = self.open_callback.?;
+            self.open_callback = null;
+            // A forest with objects (a restart from a checkpoint): the engine starts empty and
+            // loads objects on demand in prefetch.
+            if (self.forest.grooves.accounts.objects.manifest.key_range() != null or
+                self.forest.grooves.transfers.objects.manifest.key_range() != null)
+            {
+                self.engine_complete = false;
+            }
+            callback(self);
+        }
+
+        /// src/state_machine.zig:336-343.
         pub fn prepare(self: *StateMachine, operation: Operation, input: []align(16) u8) void {
-            self.base.prepare_timestamp = self.prepare_timestamp;
-            self.base.prepare(operation, input);
-            self.prepare_timestamp = self.base.prepare_timestamp;
+            self.prepare_timestamp += switch (operation) {
+                .create_accounts => mem.bytesAsSlice(Account, input).len,
+                .create_transfers => mem.bytesAsSlice(Transfer, input).len,
+                .lookup_accounts => 0,
+                .lookup_transfers => 0,
+            };
         }
 
-        /// Objects are HBM-resident: complete synchronously (allowed, lsm/groove.zig:723-742).
+        /// With every object resident in HBM, prefetch completes synchronously (a callback inside
+        /// the call is allowed, src/lsm/groove.zig:723-742).  After a restart it runs the
+        /// reference's groove prefetch (src/state_machine.zig:345-506) and then loads into the
+        /// engine what the prepare reads.
         pub fn prefetch(
             self: *StateMachine,
             callback: *const fn (*StateMachine) void,
@@ -86,9 +256,145 @@ pub fn StateMachineType(comptime Storage: type, comptime config: @import("consta
             input: []align(16) const u8,
         ) void {
             _ = op;
-            _ = operation;
-            _ = input;
+            assert(self.prefetch_input == null);
+            assert(self.prefetch_callback == null);
+            if (self.engine_complete) return callback(self);
+
+            self.prefetch_input = input;
+            self.prefetch_operation = operation;
+            self.prefetch_callback = callback;
+            self.forest.grooves.accounts.prefetch_setup(null);
+            self.forest.grooves.transfers.prefetch_setup(null);
+            self.forest.grooves.posted.prefetch_setup(null);
+            switch (operation) {
+                .create_accounts => {
+                    for (mem.bytesAsSlice(Account, input)) |*a| self.forest.grooves.accounts.prefetch_enqueue(a.id);
+                    self.prefetch_context = .{ .accounts = undefined };
+                    self.forest.grooves.accounts.prefetch(prefetch_accounts_done, &self.prefetch_context.accounts);
+                },
+                .create_transfers => {
+                    for (mem.bytesAsSlice(Transfer, input)) |*t| {
+                        self.forest.grooves.transfers.prefetch_enqueue(t.id);
+                        if (t.flags.post_pending_transfer or t.flags.void_pending_transfer) {
+                            self.forest.grooves.transfers.prefetch_enqueue(t.pending_id);
+                        }
+                    }
+                    self.prefetch_context = .{ .transfers = undefined };
+                    self.forest.grooves.transfers.prefetch(prefetch_transfers_done, &self.prefetch_context.transfers);
+                },
+                // Lookups read the engine, which holds every object written since the restart;
+                // older ones are loaded the same way.
+                .lookup_accounts => {
+                    for (mem.bytesAsSlice(u128, input)) |id| self.forest.grooves.accounts.prefetch_enqueue(id);
+                    self.prefetch_context = .{ .accounts = undefined };
+                    self.forest.grooves.accounts.prefetch(prefetch_accounts_done, &self.prefetch_context.accounts);
+                },
+                .lookup_transfers => {
+                    for (mem.bytesAsSlice(u128, input)) |id| self.forest.grooves.transfers.prefetch_enqueue(id);
+                    self.prefetch_context = .{ .transfers = undefined };
+                    self.forest.grooves.transfers.prefetch(prefetch_transfers_done, &self.prefetch_context.transfers);
+                },
+            }
+        }
+
+        fn parent_of(comptime field: std.meta.FieldEnum(PrefetchContext), completion: anytype) *StateMachine {
+            const context = @fieldParentPtr(PrefetchContext, @tagName(field), completion);
+            return @fieldParentPtr(StateMachine, "prefetch_context", context);
+        }
+
+        fn prefetch_transfers_done(completion: *TransfersGroove.PrefetchContext) void {
+            const self = parent_of(.transfers, completion);
+            if (self.prefetch_operation == .lookup_transfers) return self.prefetch_finish();
+            // src/state_machine.zig:434-458: the pending transfer's posted entry and accounts.
+            for (mem.bytesAsSlice(Transfer, self.prefetch_input.?)) |*t| {
+                if (t.flags.post_pending_transfer or t.flags.void_pending_transfer) {
+                    if (self.forest.grooves.transfers.get(t.pending_id)) |p| {
+                        self.forest.grooves.posted.prefetch_enqueue(p.timestamp);
+                        self.forest.grooves.accounts.prefetch_enqueue(p.debit_account_id);
+                        self.forest.grooves.accounts.prefetch_enqueue(p.credit_account_id);
+                    }
+                } else {
+                    self.forest.grooves.accounts.prefetch_enqueue(t.debit_account_id);
+                    self.forest.grooves.accounts.prefetch_enqueue(t.credit_account_id);
+                }
+            }
+            self.prefetch_context = .{ .accounts = undefined };
+            self.forest.grooves.accounts.prefetch(prefetch_accounts_done, &self.prefetch_context.accounts);
+        }
+
+        fn prefetch_accounts_done(completion: *AccountsGroove.PrefetchContext) void {
+            const self = parent_of(.accounts, completion);
+            if (self.prefetch_operation != .create_transfers) return self.prefetch_finish();
+            self.prefetch_context = .{ .posted = undefined };
+            self.forest.grooves.posted.prefetch(prefetch_posted_done, &self.prefetch_context.posted);
+        }
+
+        fn prefetch_posted_done(completion: *PostedGroove.PrefetchContext) void {
+            parent_of(.posted, completion).prefetch_finish();
+        }
+
+        /// The prefetched objects are in the groove caches: hand the engine the ones it lacks
+        /// (tbgpu_load_* keeps every object the engine already holds — those are newer).
+        fn prefetch_finish(self: *StateMachine) void {
+            const input = self.prefetch_input.?;
+            var na: u32 = 0;
+            var nt: u32 = 0;
+            const grooves = &self.forest.grooves;
+            switch (self.prefetch_operation) {
+                .create_accounts => for (mem.bytesAsSlice(Account, input)) |*a| {
+                    if (grooves.accounts.get(a.id)) |found| self.push_account(&na, found);
+                },
+                .lookup_accounts => for (mem.bytesAsSlice(u128, input)) |id| {
+                    if (grooves.accounts.get(id)) |found| self.push_account(&na, found);
+                },
+                .lookup_transfers => for (mem.bytesAsSlice(u128, input)) |id| {
+                    if (grooves.transfers.get(id)) |found| self.push_transfer(&nt, found);
+                },
+                .create_transfers => for (mem.bytesAsSlice(Transfer, input)) |*t| {
+                    if (grooves.transfers.get(t.id)) |found| self.push_transfer(&nt, found);
+                    var dr = t.debit_account_id;
+                    var cr = t.credit_account_id;
+                    if (t.flags.post_pending_transfer or t.flags.void_pending_transfer) {
+                        if (grooves.transfers.get(t.pending_id)) |p| {
+                            self.push_transfer(&nt, p);
+                            dr = p.debit_account_id;
+                            cr = p.credit_account_id;
+                        }
+                    }
+                    if (grooves.accounts.get(dr)) |a| self.push_account(&na, a);
+                    if (grooves.accounts.get(cr)) |a| self.push_account(&na, a);
+                },
+            }
+            if (na > 0) check(tbgpu.tbgpu_load_accounts(self.engine, self.load_accounts.ptr, na));
+            if (nt > 0) {
+                check(tbgpu.tbgpu_load_transfers(self.engine, self.load_transfers.ptr, self.load_posted.ptr, nt));
+            }
+            const callback = self.prefetch_callback.?;
+            self.prefetch_input = null;
+            self.prefetch_callback = null;
+            self.prefetch_context = undefined;
             callback(self);
+        }
+
+        fn push_account(self: *StateMachine, n: *u32, a: *const Account) void {
+            // Duplicates are harmless (insert-if-absent); the buffer holds a prepare's worth.
+            if (n.* == self.load_accounts.len) return;
+            self.load_accounts[n.*] = a.*;
+            n.* += 1;
+        }
+
+        fn push_transfer(self: *StateMachine, n: *u32, t: *const Transfer) void {
+            if (n.* == self.load_transfers.len) return;
+            self.load_transfers[n.*] = t.*;
+            // Posted groove: {0 none, 1 posted, 2 voided} for tbgpu_load_transfers.
+            self.load_posted[n.*] = if (self.forest.grooves.posted.get(t.timestamp)) |posted|
+                @as(u8, switch (posted.fulfillment) {
+                    .posted => 1,
+                    .voided => 2,
+                })
+            else
+                0;
+            n.* += 1;
         }
 
         pub fn commit(
@@ -102,8 +408,15 @@ pub fn StateMachineType(comptime Storage: type, comptime config: @import("consta
         ) usize {
             _ = client;
             assert(op != 0);
+            assert(timestamp > self.commit_timestamp or global_constants.aof_recovery);
+            // The replica sets commit_timestamp to the header timestamp after every commit
+            // (replica.zig:3664-3665) and from the checkpoint on open / sync: the engine follows.
+            if (self.commit_timestamp != self.engine_commit_timestamp) {
+                check(tbgpu.tbgpu_set_commit_timestamp(self.engine, self.commit_timestamp));
+                self.engine_commit_timestamp = self.commit_timestamp;
+            }
             var out_len: u32 = 0;
-            const status = tbgpu.tbgpu_commit(
+            check(tbgpu.tbgpu_commit(
                 self.engine,
                 @intFromEnum(operation),
                 timestamp,
@@ -112,20 +425,87 @@ pub fn StateMachineType(comptime Storage: type, comptime config: @import("consta
                 output,
                 @intCast(output.len),
                 &out_len,
-            );
-            if (status != tbgpu.TBGPU_STATUS_OK) @panic(std.mem.span(tbgpu.tbgpu_last_error()));
+            ));
             self.commit_timestamp = tbgpu.tbgpu_commit_timestamp(self.engine);
+            self.engine_commit_timestamp = self.commit_timestamp;
             return out_len;
         }
 
-        /// Durability (write-back of dirty accounts / new transfers into the LSM forest) is the
-        /// next row of SURVEY.md §8f; until then compaction has nothing from the engine to persist.
         pub fn compact(self: *StateMachine, callback: *const fn (*StateMachine) void, op: u64) void {
-            _ = op;
+            assert(self.compact_callback == null);
+            assert(self.checkpoint_callback == null);
+            if ((op + 1) % config.lsm_batch_multiple == 0) self.write_back();
+            self.compact_callback = callback;
+            self.forest.compact(compact_finish, op);
+        }
+
+        fn compact_finish(forest: *Forest) void {
+            const self = @fieldParentPtr(StateMachine, "forest", forest);
+            const callback = self.compact_callback.?;
+            self.compact_callback = null;
             callback(self);
         }
 
+        /// The bar's changes into the grooves, as the reference's commits would have put them:
+        /// created objects by insert, re-balanced accounts by upsert against their previous version
+        /// (which the groove must hold to diff the balance index trees: the engine returns the
+        /// previous balances; the cache gets the old object first if it is not there).
+        fn write_back(self: *StateMachine) void {
+            var counts: tbgpu.tbgpu_delta_counts = undefined;
+            const status = tbgpu.tbgpu_checkpoint_delta(
+                self.engine,
+                self.writeback_accounts.ptr,
+                self.writeback_accounts_before.ptr,
+                self.writeback_accounts.len,
+                self.writeback_transfers.ptr,
+                self.writeback_transfers.len,
+                @ptrCast(self.writeback_posted.ptr),
+                self.writeback_posted.len,
+                &counts,
+            );
+            // The buffers hold one bar's worth, the most a bar can change: STATUS_INVALID with
+            // larger counts would mean the engine changed more objects than a bar's commits can
+            // (an invariant failure, like the reference's TableMemory.put assert), so it panics.
+            check(status);
+            const grooves = &self.forest.grooves;
+            for (self.writeback_accounts[0..counts.accounts], self.writeback_accounts_before[0..counts.accounts]) |*a, before| {
+                if (a.timestamp > counts.created_after) {
+                    grooves.accounts.insert(a); // created since the previous write-back
+                    continue;
+                }
+                if (grooves.accounts.get(a.id) == null) {
+                    // The groove diffs the balance index trees against the old object: give its
+                    // cache the version the forest holds (what a prefetch would have loaded).
+                    var old = a.*;
+                    old.debits_pending = before[0];
+                    old.debits_posted = before[1];
+                    old.credits_pending = before[2];
+                    old.credits_posted = before[3];
+                    grooves.accounts.objects_cache.upsert(&old);
+                }
+                grooves.accounts.upsert(a);
+            }
+            for (self.writeback_transfers[0..counts.transfers]) |*t| grooves.transfers.insert(t);
+            for (self.writeback_posted[0..counts.posted]) |pair| {
+                grooves.posted.insert(&PostedGrooveValue{
+                    .timestamp = pair[0],
+                    .fulfillment = if (pair[1] == 0) .posted else .voided,
+                    .padding = [_]u8{0} ** 7,
+                });
+            }
+        }
+
         pub fn checkpoint(self: *StateMachine, callback: *const fn (*StateMachine) void) void {
+            assert(self.compact_callback == null);
+            assert(self.checkpoint_callback == null);
+            self.checkpoint_callback = callback;
+            self.forest.checkpoint(checkpoint_finish);
+        }
+
+        fn checkpoint_finish(forest: *Forest) void {
+            const self = @fieldParentPtr(StateMachine, "forest", forest);
+            const callback = self.checkpoint_callback.?;
+            self.checkpoint_callback = null;
             callback(self);
         }
     };
