@@ -80,6 +80,21 @@ int tbgpu_route_plan_build(tbgpu_t* engine, uint32_t n_batches, const uint64_t* 
 int tbgpu_commit_routed_async(tbgpu_t* engine, uint64_t n, const void* events_dev, uint64_t ts_max,
                               uint32_t cert, uint8_t* codes_dev);
 
+/* Owner-partitioned balances: an account's balances live on owner(id) =
+ * tbgpu_home(id, world); every other rank holds zeros for it.  This is tbgpu_commit_routed_async
+ * for rank `self` of `world`, except that the home applies no balance itself: every committed
+ * transfer's two legs (state_machine.zig:870-880) are written to legs_dev, grouped by owner —
+ * owner o's legs at legs_dev + o * legs_cap * 40 B, {id lo, id hi, amount lo, amount hi, field
+ * (0 dp, 1 dpost, 2 cp, 3 cpost)} as u64 words — and leg_counts_dev[o] = their number.  legs_cap
+ * >= 2 n.  Enqueued. */
+int tbgpu_commit_routed_owner_async(tbgpu_t* engine, uint64_t n, const void* events_dev, uint64_t ts_max,
+                                    uint32_t cert, uint8_t* codes_dev, uint32_t world, uint32_t self,
+                                    void* legs_dev, uint64_t legs_cap, uint64_t* leg_counts_dev);
+
+/* Owner side: add n received legs (the layout above, back to back) to this rank's balances.  A leg
+ * for an account the table lacks is a PANIC (accounts are replicated).  Synchronous. */
+int tbgpu_apply_owner_legs_async(tbgpu_t* engine, const void* legs_dev, uint64_t n, uint32_t cert);
+
 /* Sparse per-prepare replies from the returned codes (codes_dev in send order): batch k's reply
  * at results_dev + 8*offset_k, its size in reply_bytes_dev[k]. Enqueued. */
 int tbgpu_route_replies_async(tbgpu_t* engine, uint32_t n_batches, const uint32_t* batch_lens,

@@ -16,6 +16,7 @@ from tigerbeetle_amd.types import TRANSFER_DTYPE, U128_MAX, AccountFlags
 
 from .oracle import OracleEngine
 
+U64_MASK = (1 << 64) - 1
 _LIMITS = int(AccountFlags.debits_must_not_exceed_credits | AccountFlags.credits_must_not_exceed_debits)
 
 
@@ -72,6 +73,46 @@ class OracleShard:
     def commit_routed(self, events, ts_max, cert):
         del ts_max, cert
         return torch.from_numpy(self.o.commit_routed(events.numpy()).copy())
+
+    def commit_routed_owner(self, events, ts_max, cert, rank):
+        """Routed commit with owner-partitioned balances (tbgpu_commit_routed_owner_async): the
+        oracle applies every committed transfer locally; each leg owned elsewhere is cancelled here
+        and sent to its owner (the GPU also sends self-owned legs of independent events to itself;
+        the final balances are the same)."""
+        codes = self.commit_routed(events, ts_max, cert)
+        ev = events.numpy().reshape(-1).view(TRANSFER_DTYPE)
+        ok = codes.numpy() == 0
+        per_owner = [[] for _ in range(self.world)]
+        for t in ev[ok]:
+            amount = (int(t["amount_hi"]) << 64) | int(t["amount_lo"])
+            pend = int(t["flags"]) & 2
+            for side, field in (("debit_account_id", 0 if pend else 1), ("credit_account_id", 2 if pend else 3)):
+                lo, hi = int(t[side + "_lo"]), int(t[side + "_hi"])
+                owner = int(homes_of(np.array([[lo, hi]], dtype=np.uint64), self.world)[0])
+                if owner == rank:
+                    continue
+                self._add_balance(lo, hi, field, (1 << 128) - amount)
+                per_owner[owner].append([lo, hi, amount & U64_MASK, amount >> 64, field])
+        counts = [len(p) for p in per_owner]
+        rows = [r for p in per_owner for r in p]
+        legs = np.array(rows, dtype=np.uint64).reshape(-1, 5).view(np.int64)
+        return codes, torch.from_numpy(legs.copy()), counts
+
+    def _add_balance(self, lo, hi, field, delta):
+        names = ("debits_pending", "debits_posted", "credits_pending", "credits_posted")
+        recs, found = self.o.fetch_accounts(np.array([[lo, hi]], dtype=np.uint64))
+        assert found[0], "leg for a missing account"
+        name = names[field]
+        v = ((int(recs[name + "_hi"][0]) << 64) | int(recs[name + "_lo"][0])) + delta
+        v &= (1 << 128) - 1
+        recs[name + "_lo"] = v & U64_MASK
+        recs[name + "_hi"] = v >> 64
+        self.o.upsert_accounts(recs)
+
+    def apply_owner_legs(self, legs, cert):
+        del cert
+        for w in legs.numpy().view(np.uint64).reshape(-1, 5):
+            self._add_balance(int(w[0]), int(w[1]), int(w[4]), (int(w[3]) << 64) | int(w[2]))
 
     def replies(self, lens, slots, codes_back):
         s = slots.numpy()

@@ -72,6 +72,13 @@ def run_rank(rank, world, port, kind, scenario_kw, max_prepares, result_path):
                 for p in parts:
                     replies.extend(p)
         sm.sync_commit_timestamp()
+        # Owner partition: a rank holds balances only for the accounts it owns.
+        local = backend.export_accounts()
+        not_mine = ~sm._owner_mask(local)
+        stray = sum(int(np.count_nonzero(local[f + w][not_mine])) for f in
+                    ("debits_pending", "debits_posted", "credits_pending", "credits_posted") for w in ("_lo", "_hi"))
+        stray_t = torch.tensor([stray], dtype=torch.int64)
+        dist.all_reduce(stray_t)
         accounts = sm.export_accounts()
         transfers = sm.export_transfers()
         posted = sm.export_posted()
@@ -93,6 +100,8 @@ def run_rank(rank, world, port, kind, scenario_kw, max_prepares, result_path):
                 problems.append("transfers differ (%d vs %d)" % (len(transfers), len(oracle.export_transfers())))
             if posted.tobytes() != oracle.export_posted().tobytes():
                 problems.append("posted differs")
+            if int(stray_t.item()):
+                problems.append("%d balance words held by a rank that does not own the account" % int(stray_t.item()))
             if sm.commit_timestamp != oracle.commit_timestamp:
                 problems.append("commit_timestamp %d != %d" % (sm.commit_timestamp, oracle.commit_timestamp))
             verdict = {"ok": not problems, "problems": problems, "clean": sm.passes_clean, "dirty": sm.passes_dirty,

@@ -494,7 +494,8 @@ static int engine_sync(tbgpu* E) {
 // result codes instead of sparse replies, cert_ext = the router's certificate.
 static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* events_dev, u32* results_dev,
                         u32* reply_bytes_dev, bool routed = false, u8* codes = nullptr, u32 cert_ext = 0,
-                        const u8* events_src = nullptr, const u64* d_meta = nullptr) {
+                        const u8* events_src = nullptr, const u64* d_meta = nullptr,
+                        const OwnerLegArgs* owner = nullptr) {
     const u64* d_off = d_meta ? d_meta : E->meta;
     const u64* d_ts = d_off + (nb + 1);
     u32 b0 = 0;
@@ -547,7 +548,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         // the resolve kernel (~20 G/s) only cost beyond ~LEGS_MIN_EVENTS events: the replica's
         // one-prepare commits take the atomics.
         P.legs = (op == OP_CREATE_TRANSFERS && E->legs_ok && b1 - b0 <= LEG_PREPARES_MAX && n >= E->legs_min &&
-                  !(E->ablate & ABL_LEGS)) ? 1 : 0;
+                  !(E->ablate & ABL_LEGS) && !owner) ? 1 : 0;
         P.apply_late = (op == OP_CREATE_TRANSFERS && !P.legs) ? 1 : 0;
         P.leg_shift = E->leg_shift;
         P.leg_buckets = E->leg_buckets;
@@ -606,7 +607,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
             if (P.legs) {
                 hipLaunchKernelGGL(tb_apply_legs, dim3(E->leg_buckets), dim3(APPLY_THREADS), (4u << E->leg_shift) * 8,
                                    E->stream, P);
-            } else if (n > 0) {
+            } else if (n > 0 && !owner) {  // owner-partitioned: the owners apply the legs instead
                 hipLaunchKernelGGL(tb_apply_events, dim3((u32)((n + 255) / 256)), dim3(256), 0, E->stream, P);
             }
             HIPCK(hipGetLastError());
@@ -628,6 +629,10 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         }
         HIPCK(hipGetLastError());
         if ((st = prof_end(E, &pp))) return st;
+        if (owner && n > 0) {  // every committed transfer's legs, grouped by owner (k_route.h)
+            hipLaunchKernelGGL(tb_owner_legs, dim3((u32)((n + 255) / 256)), dim3(256), 0, E->stream, P, *owner);
+            HIPCK(hipGetLastError());
+        }
         if ((st = prof_end(E, &pass_pp))) return st;
         E->passes++;
         E->events += n;
@@ -1550,6 +1555,59 @@ extern "C" int tbgpu_commit_routed_async(tbgpu_t* E, uint64_t n, const void* eve
     if (st) return st;
     E->last_batch_ts = std::max(E->last_batch_ts, ts_max);
     E->pending = true;
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_commit_routed_owner_async(tbgpu_t* E, uint64_t n, const void* events_dev, uint64_t ts_max,
+                                               uint32_t cert, uint8_t* codes_dev, uint32_t world, uint32_t self,
+                                               void* legs_dev, uint64_t legs_cap, uint64_t* leg_counts_dev) {
+    HIPCK(hipSetDevice(E->device));
+    if (cert != TBGPU_CERT_U128 && cert != TBGPU_CERT_U64) return fail(TBGPU_STATUS_INVALID, "routed commit needs a certificate");
+    if (world == 0 || world > ROUTE_WORLD_MAX || self >= world) return fail(TBGPU_STATUS_INVALID, "owner world / rank");
+    if (legs_cap < 2 * n) return fail(TBGPU_STATUS_INVALID, "owner leg regions need 2 legs per event");
+    HIPCK(hipMemsetAsync(leg_counts_dev, 0, (u64)world * 8, E->stream));
+    if (n == 0) return TBGPU_STATUS_OK;
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    const u64 per = BATCH_EVENTS_MAX - 1;
+    const u64 nb = (n + per - 1) / per;
+    if (nb > E->meta_cap) return fail(TBGPU_STATUS_INVALID, "routed call too large");
+    if (E->log_next + n > E->xlog_cap) {
+        return fail(TBGPU_STATUS_INVALID, "transfer log full (%llu + %llu events > capacity %llu)",
+                    (unsigned long long)E->log_next, (unsigned long long)n, (unsigned long long)E->xlog_cap);
+    }
+    u64* h_off = E->h_meta;
+    u64* h_ts = E->h_meta + nb + 1;
+    h_off[0] = 0;
+    for (u64 k = 0; k < nb; k++) {
+        h_off[k + 1] = std::min<u64>(n, h_off[k] + per);
+        h_ts[k] = ts_max;
+    }
+    HIPCK(hipMemcpyAsync(E->meta, E->h_meta, (2 * nb + 1) * 8, hipMemcpyHostToDevice, E->stream));
+    std::vector<u64> off(h_off, h_off + nb + 1);
+    OwnerLegArgs O{world, self, (u64*)legs_dev, legs_cap, leg_counts_dev};
+    int st = enqueue_call(E, OP_CREATE_TRANSFERS, (u32)nb, off.data(), (const u8*)events_dev, E->results,
+                          E->reply_bytes, true, codes_dev, cert, nullptr, nullptr, &O);
+    if (st) return st;
+    E->last_batch_ts = std::max(E->last_batch_ts, ts_max);
+    E->pending = true;
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_apply_owner_legs_async(tbgpu_t* E, const void* legs_dev, uint64_t n, uint32_t cert) {
+    HIPCK(hipSetDevice(E->device));
+    if (cert != TBGPU_CERT_U128 && cert != TBGPU_CERT_U64) return fail(TBGPU_STATUS_INVALID, "owner legs need a certificate");
+    if (n == 0) return TBGPU_STATUS_OK;
+    HIPCK(hipMemsetAsync(E->d_status, 0, 4, E->stream));
+    hipLaunchKernelGGL(tb_apply_owner_legs, dim3((u32)((n + 255) / 256)), dim3(256), 0, E->stream, E->T,
+                       (const u64*)legs_dev, n, cert == TBGPU_CERT_U64 ? 1u : 0u, E->d_status);
+    HIPCK(hipGetLastError());
+    u32 status = 0;
+    HIPCK(hipMemcpyAsync(&status, E->d_status, 4, hipMemcpyDeviceToHost, E->stream));
+    HIPCK(hipStreamSynchronize(E->stream));
+    if (status) return fail(TBGPU_STATUS_PANIC, "owner leg for an account this rank does not hold");
     return TBGPU_STATUS_OK;
 }
 

@@ -287,3 +287,98 @@ __global__ void tb_upsert_transfers(Tables T, const u8* recs, const u8* state, u
     if (tb_transfer_claim_new(T, tb_lo(t.id), tb_hi(t.id), (u32)lp) == TB_NOT_FOUND) atomicOr(status, 1u);
     atomicAdd((unsigned long long*)&T.g->transfer_count, 1ULL);
 }
+
+// ---- owner-partitioned balances ------------------------------------------------------------------
+// An account's balances live on owner(id) = tb_home(id, world) only (every other rank keeps zeros
+// there); the immutable account fields are replicated, so every home validates with local probes.
+// After a routed pass, every committed transfer's two balance deltas (state_machine.zig:870-880:
+// debits_{pending,posted} of the debit account, credits_{pending,posted} of the credit account)
+// become LEGS routed to the owners (all-to-all) and added there (tb_apply_owner_legs).
+//   * independent events were not applied here (the pass skips tb_apply_events), so each emits both
+//     legs, to whichever owner, itself included;
+//   * dependent events (id collisions replayed in order by tb_flow / tb_replay) were applied to the
+//     local table by the replay: a leg whose owner is another rank goes there and the local copy is
+//     cancelled (adds are mod 2^128; free balances feed no check in a clean pass, so the transient
+//     local value is never read).
+// Leg on the wire: {account id lo, hi, amount lo, hi, field (BAL_OFF / 16)}.
+#define OWNER_LEG_WORDS 5
+
+struct OwnerLegArgs {
+    u32 world;
+    u32 self;
+    u64* legs;      // [world][cap][OWNER_LEG_WORDS]: owner o's legs at legs + o * cap * OWNER_LEG_WORDS
+    u64 cap;        // legs per owner region
+    u64* counts;    // [world] legs written per owner (zeroed by the host before the call)
+};
+
+__global__ __launch_bounds__(256) void tb_owner_legs(PassArgs P, OwnerLegArgs O) {
+    __shared__ u32 s_cnt[ROUTE_WORLD_MAX];
+    __shared__ u64 s_base[ROUTE_WORLD_MAX];
+    if (threadIdx.x < O.world) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const u32 pe = blockIdx.x * 256 + threadIdx.x;
+    u32 owner[2] = {0, 0}, pos[2] = {0, 0};
+    bool emit[2] = {false, false};
+    Transfer t;
+    u32 field0 = 0;
+    if (pe < P.n && P.codes[P.e0 + pe] == R_OK) {
+        t = P.T.xlog[P.log_base + pe];
+        const bool dep = (P.info[pe] & HZ_DEP) != 0;
+        field0 = (t.flags & TF_PENDING) ? 0 : 1;  // debits_pending / debits_posted (+2: credits)
+#pragma unroll
+        for (u32 s = 0; s < 2; s++) {
+            const u128 id = s ? t.credit_account_id : t.debit_account_id;
+            owner[s] = tb_home(tb_lo(id), tb_hi(id), O.world);
+            emit[s] = !(dep && owner[s] == O.self);
+            if (emit[s]) pos[s] = atomicAdd(&s_cnt[owner[s]], 1u);
+            if (emit[s] && dep) {  // cancel the replay's local add: the owner applies it
+                const u32 slot = tb_account_find(P.T, tb_lo(id), tb_hi(id));
+                if (slot == TB_NOT_FOUND) {
+                    tb_panic(P.T.g, PANIC_ASSERT);
+                } else {
+                    u8* bal = (u8*)&P.T.acct_bal[slot];
+                    tb_atomic_add_u128(bal + 16 * (field0 + 2 * s), (u128)0 - t.amount);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < O.world) {
+        const u32 c = s_cnt[threadIdx.x];
+        s_base[threadIdx.x] = c ? atomicAdd((unsigned long long*)&O.counts[threadIdx.x], (unsigned long long)c) : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (u32 s = 0; s < 2; s++) {
+        if (!emit[s]) continue;
+        const u64 k = s_base[owner[s]] + pos[s];
+        if (k >= O.cap) {  // the host sized every region for the whole call
+            tb_panic(P.T.g, PANIC_ASSERT);
+            continue;
+        }
+        const u128 id = s ? t.credit_account_id : t.debit_account_id;
+        u64* w = O.legs + ((u64)owner[s] * O.cap + k) * OWNER_LEG_WORDS;
+        w[0] = tb_lo(id);
+        w[1] = tb_hi(id);
+        w[2] = tb_lo(t.amount);
+        w[3] = tb_hi(t.amount);
+        w[4] = field0 + 2 * s;
+    }
+}
+
+// Owner side: add every received leg to its account's balance field (the sums commute, so arrival
+// order does not matter).  cert64: the router's certificate bounds every balance below 2^64 this
+// pass, so the adds are low-word no-return atomics.
+__global__ __launch_bounds__(256) void tb_apply_owner_legs(Tables T, const u64* legs, u64 n, u32 cert64, u32* status) {
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const u64* w = legs + i * OWNER_LEG_WORDS;
+    const u32 slot = tb_account_find(T, w[0], w[1]);
+    if (slot == TB_NOT_FOUND || w[4] > 3) {
+        atomicOr(status, 1u);
+        return;
+    }
+    u8* f = (u8*)&T.acct_bal[slot] + 16 * w[4];
+    if (cert64) tb_atomic_add_lo_noret(f, w[2]);
+    else tb_atomic_add_u128(f, tb_u128(w[2], w[3]));
+}

@@ -4,8 +4,10 @@ One engine per GPU, one process per GPU, collectives over torch.distributed (bac
 RCCL over xGMI on an MI355X node; "gloo" for the CPU tests and for several ranks sharing one GPU).
 The partition and the pass protocol are documented in include/tbgpu_shard.h and DESIGN.md §6:
 
-* account records are replicated (every rank commits every create_accounts prepare);
-* account balances are per-rank partial sums (true balance = sum over ranks);
+* account records (their immutable fields) are replicated: every rank commits every
+  create_accounts prepare;
+* account balances are owner-partitioned: they live on owner(id) = tbgpu_home(id, world) only
+  (every other rank holds zeros), and the legs of committed transfers are routed to the owners;
 * a transfer lives on its home rank, tbgpu_home(id, world).
 
 Global order.  A collective pass takes every rank's prepares.  The global prepare order is rank 0's
@@ -13,7 +15,8 @@ prepares, then rank 1's, ..., and timestamps must increase in that order: the re
 those of one StateMachine committing the concatenation (src/state_machine.zig:508-540).
 
 A clean create_transfers pass is routed: one all-to-all of events (+ their execute timestamps) to
-their homes, a routed commit on every home, one all-to-all of result codes back.  A dirty pass
+their homes, a routed commit on every home, one all-to-all of the committed transfers' balance
+legs to the accounts' owners, one all-to-all of result codes back.  A dirty pass
 (linked / post / void / balancing event, limit-flag account, or no global overflow certificate)
 is committed by rank 0 on a scratch engine after prefetching the referenced transfers from their
 homes and the summed balances of the touched accounts (the reference's prefetch -> commit split,
@@ -132,6 +135,29 @@ class GpuShard:
                                                           codes.data_ptr()))
             self.engine.sync()
         return codes[:m]
+
+    def commit_routed_owner(self, events, ts_max, cert, rank):
+        """The home's routed commit with owner-partitioned balances: result codes, plus the legs of
+        every committed transfer grouped by owner (a [sum, 5] int64 tensor, owner by owner) and the
+        per-owner counts (host list)."""
+        m = events.shape[0]
+        codes = torch.empty(max(m, 1), dtype=torch.uint8, device=self.device)
+        cap = max(2 * m, 1)
+        legs = torch.empty((self.world * cap, 5), dtype=torch.int64, device=self.device)
+        counts = torch.zeros(self.world, dtype=torch.int64, device=self.device)
+        torch.cuda.synchronize(self.device)
+        _lib.check(self.lib.tbgpu_commit_routed_owner_async(self.engine.h, m, events.data_ptr(), ts_max, cert,
+                                                            codes.data_ptr(), self.world, rank, legs.data_ptr(), cap,
+                                                            counts.data_ptr()))
+        self.engine.sync()
+        c = [int(x) for x in counts.cpu().tolist()]
+        send = torch.cat([legs[o * cap:o * cap + c[o]] for o in range(self.world)])
+        return codes[:m], send, c
+
+    def apply_owner_legs(self, legs, cert):
+        if legs.shape[0]:
+            torch.cuda.synchronize(self.device)
+            _lib.check(self.lib.tbgpu_apply_owner_legs_async(self.engine.h, legs.data_ptr(), legs.shape[0], cert))
 
     def replies(self, lens, slots, codes_back):
         import ctypes
@@ -379,10 +405,20 @@ class ShardedStateMachine:
         return self.commit_timestamp
 
     def _commit_routed(self, plan, send_events, slots, lens, recv_counts, cert):
+        """Clean pass: events to their homes (all-to-all #1), the home commits them, the legs of the
+        committed transfers to the owners of their accounts (all-to-all #2, after a count exchange)
+        where the balances live, and the result codes back to the sources (all-to-all #3)."""
         recv_events = self._a2a(send_events, plan.counts, recv_counts)
-        codes = self.b.commit_routed(recv_events, self._pass_ts_max, cert)
+        codes, legs, leg_counts = self.b.commit_routed_owner(recv_events, self._pass_ts_max, cert, self.rank)
+        legs_in_counts = self._a2a(torch.tensor(leg_counts, dtype=torch.int64), [1] * self.world, [1] * self.world)
+        legs_in = self._a2a(legs, leg_counts, [int(x) for x in legs_in_counts.cpu().tolist()])
+        self.b.apply_owner_legs(legs_in, cert)
         codes_back = self._a2a(codes, recv_counts, plan.counts)
         return self.b.replies(lens, slots, codes_back)
+
+    def _owner_mask(self, records):
+        """True for the accounts this rank owns (their balances live here)."""
+        return self._homes(_ids(records["id_lo"], records["id_hi"])) == self.rank
 
     def _commit_replicated(self, operation, timestamps, lens, events):
         """create_accounts: every rank commits every prepare of the pass (records are replicated)."""
@@ -481,22 +517,21 @@ class ShardedStateMachine:
         else:
             local_ts = 0
 
-        # 4. write back: new transfers and posted states to their homes, balances collected on
-        #    rank 0 (every other rank's partial of a touched account becomes 0).
+        # 4. write back: new transfers and posted states to their homes, each touched account's
+        #    balances to its owner (every other rank holds zeros for it).
         wb_t = self._bcast_np(wb_t if root else None, TRANSFER_DTYPE)
         wb_s = self._bcast_np(wb_s if root else None, np.uint8)
         if len(wb_t):
             h = self._homes(_ids(wb_t["id_lo"], wb_t["id_hi"]))
             sel = h == self.rank
             self.b.upsert_transfers(wb_t[sel], wb_s[sel])
-        if root:
-            self.b.upsert_accounts(acc_after)
-        else:
-            zero = accts[afound].copy()
-            for name in _BAL_FIELDS:
-                zero[name + "_lo"] = 0
-                zero[name + "_hi"] = 0
-            self.b.upsert_accounts(zero)
+        acc_after = self._bcast_np(acc_after if root else None, ACCOUNT_DTYPE)
+        wb_a = acc_after.copy()
+        not_mine = ~self._owner_mask(wb_a)
+        for name in _BAL_FIELDS:
+            wb_a[name + "_lo"][not_mine] = 0
+            wb_a[name + "_hi"][not_mine] = 0
+        self.b.upsert_accounts(wb_a)
 
         # 5. replies back to their ranks.
         rlens = self._bcast_np(rlens if root else None, np.int64)
@@ -508,14 +543,15 @@ class ShardedStateMachine:
         return PassResult.from_bytes(mine_r, lens, self.b.device)
 
     def test_set_balances(self, account_id, dp, dpost, cp, cpost):
-        """Collective test-only `setup` action (state_machine.zig:1398-1407): rank 0's partial holds
-        the balances, every other rank's partial becomes 0."""
+        """Collective test-only `setup` action (state_machine.zig:1398-1407): the owner holds the
+        balances, every other rank zeros."""
         ids = np.array([[account_id & U64_MAX, account_id >> 64]], dtype=np.uint64)
         recs, found = self.b.fetch_accounts(ids)
         if not found[0]:
             raise _lib.EnginePanic(_lib.STATUS_PANIC, "setup of a missing account")
+        mine = bool(self._owner_mask(recs)[0])
         for name, v in zip(_BAL_FIELDS, (dp, dpost, cp, cpost)):
-            v = v if self.rank == 0 else 0
+            v = v if mine else 0
             recs[name + "_lo"] = v & U64_MAX
             recs[name + "_hi"] = v >> 64
         self.b.upsert_accounts(recs)
