@@ -53,8 +53,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--accounts", type=int, default=1_000_000)
-    p.add_argument("--transfers", type=int, default=100_000_000)
+    p.add_argument("--accounts", type=int, default=None, help="default: 1M (N=1, C2); 100M (N>1, C5)")
+    p.add_argument("--transfers", type=int, default=None,
+                   help="transfers per GPU; default: 100M (N=1, C2); 125M (N>1, C5: 1B over 8 GPUs)")
     p.add_argument("--batch", type=int, default=8190)
     p.add_argument("--pass-batches", type=int, default=512, help="prepares per device pass (device-resident leg)")
     p.add_argument("--chunk-prepares", type=int, default=64,
@@ -268,8 +269,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.accounts is None:
+        args.accounts = 100_000_000 if world > 1 else 1_000_000
+    if args.transfers is None:
+        args.transfers = 125_000_000 if world > 1 else 100_000_000
     if world > 1:
-        assert args.workload == "c2", "the multi-GPU bench runs the C2/C5 shape"
+        assert args.workload == "c2", "the multi-GPU bench runs the C5 shape (uniform, no flags)"
         if args.same_device:
             local_rank = 0
         torch.cuda.set_device(local_rank)
@@ -487,7 +492,12 @@ def main():
 
 
 def run_sharded(args, world, rank, local_rank):
-    """N>1: the routed multi-GPU commit (clean passes: all-to-all of events to their home GPU)."""
+    """N>1: BASELINE.json configs[4] ("C5"): 100M accounts hash-partitioned by owner, 1B transfers
+    on 8 GPUs — every rank submits 125M (weak scaling: at N=8 the node commits C5's 1B per step).
+    Each rank's prepares sit in its own pinned host memory (the replica's message pool); pass p+1
+    crosses PCIe on a side stream while pass p is routed and committed: events to their home GPU
+    (all-to-all over RCCL), the home's commit, the committed transfers' balance legs to the
+    accounts' owners (all-to-all), the result codes back (all-to-all), the replies to host."""
     import torch
     import torch.distributed as dist
 
@@ -501,32 +511,55 @@ def run_sharded(args, world, rank, local_rank):
     engine = Engine(Options(accounts_max=args.accounts, transfers_max=int(args.transfers * 1.05) + recv_max,
                             pass_events_max=recv_max, pass_batches_max=recv_max // 8190 + 2, device=local_rank,
                             profile=bool(args.profile)))
+    engine.profile_mask(engine.PROF_VALIDATE | engine.PROF_REPLAY)
     backend = GpuShard(engine, world, events_max=pass_events, device=dev)
     sm = ShardedStateMachine(backend)
 
-    # Accounts: replicated — every rank commits the same prepares (same seed).
+    # Accounts: every rank commits the same create_accounts prepares (the immutable fields are
+    # replicated; balances start at zero and live on their owners).
     acct_lens = batches(args.accounts, args.batch)
     acct_ts, t_end = timestamps(acct_lens, 1_000_000_000)
-    acct = torch.empty((args.accounts, 128), dtype=torch.uint8, device=dev)
-    engine.generate_accounts(acct.data_ptr(), 0, args.accounts, seed=args.seed)
-    res = torch.empty(args.accounts * 2, dtype=torch.int32, device=dev)
-    rb = torch.empty(len(acct_lens), dtype=torch.int32, device=dev)
-    engine.commit_device_async(128, acct_ts, acct_lens, acct.data_ptr(), res.data_ptr(), rb.data_ptr())
-    engine.sync()
-    assert int(rb.sum().item()) == 0, "account creation returned errors"
-    del acct, res, rb
+    chunk = 2048 * args.batch  # whole prepares per staging chunk (bounded staging for 100M accounts)
+    for a0 in range(0, args.accounts, chunk):
+        n_a = min(chunk, args.accounts - a0)
+        acct = torch.empty((n_a, 128), dtype=torch.uint8, device=dev)
+        engine.generate_accounts(acct.data_ptr(), a0, n_a, seed=args.seed)
+        lens_a = batches(n_a, args.batch)
+        k0 = a0 // args.batch
+        res = torch.empty(n_a * 2, dtype=torch.int32, device=dev)
+        rb = torch.empty(len(lens_a), dtype=torch.int32, device=dev)
+        engine.commit_device_async(128, acct_ts[k0:k0 + len(lens_a)], lens_a, acct.data_ptr(), res.data_ptr(),
+                                   rb.data_ptr())
+        engine.sync()
+        assert int(rb.sum().item()) == 0, "account creation returned errors"
+        del acct, res, rb
     sm.commit_timestamp = engine.commit_timestamp
 
-    # Transfers: this rank's share of the global sequence, resident in HBM.
-    events = torch.empty((args.transfers, 128), dtype=torch.uint8, device=dev)
-    engine.generate_transfers(events.data_ptr(), rank * args.transfers, args.transfers, args.accounts, seed=args.seed)
+    # Transfers: this rank's share of the global sequence, in pinned host memory.
+    gen = torch.empty((args.transfers, 128), dtype=torch.uint8, device=dev)
+    engine.generate_transfers(gen.data_ptr(), rank * args.transfers, args.transfers, args.accounts, seed=args.seed)
     engine.sync()
+    host = torch.empty((args.transfers, 128), dtype=torch.uint8, pin_memory=True)
+    host.copy_(gen)
+    del gen
+    torch.cuda.synchronize(dev)
     lens = batches(args.transfers, args.batch)
     passes = [lens[i:i + args.pass_batches] for i in range(0, len(lens), args.pass_batches)]
+    starts = np.concatenate([[0], np.cumsum([sum(p) for p in passes])]).astype(np.int64)
+    bufs = [torch.empty((pass_events, 128), dtype=torch.uint8, device=dev) for _ in range(2)]
+    copy_stream = torch.cuda.Stream(dev)
+    copied = [torch.cuda.Event() for _ in range(2)]
+
+    def h2d(p):
+        n = int(starts[p + 1] - starts[p])
+        with torch.cuda.stream(copy_stream):
+            copy_stream.wait_stream(torch.cuda.current_stream(dev))  # the buffer's previous pass is done
+            bufs[p % 2][:n].copy_(host[starts[p]:starts[p + 1]], non_blocking=True)
+            copied[p % 2].record(copy_stream)
 
     step_ms = []
     t_cursor = t_end
-    errors = torch.zeros(1, dtype=torch.int64, device=dev)
+    errors = 0
     for step in range(args.warmup + args.steps):
         timed = step >= args.warmup
         engine.reset_transfers()
@@ -534,20 +567,22 @@ def run_sharded(args, world, rank, local_rank):
             engine.reset_stats()
             sm.passes_clean = sm.passes_dirty = 0
         dist.barrier()
-        torch.cuda.synchronize()
+        torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        off = 0
-        for plens in passes:
+        h2d(0)
+        for p, plens in enumerate(passes):
             n = sum(plens)
             mine = None
             for r in range(world):  # rank-major global order of the pass
                 ts, t_cursor = timestamps(plens, t_cursor)
                 if r == rank:
                     mine = ts
-            out = sm.commit(129, mine, plens, events[off:off + n])
-            errors += out.reply_bytes.sum()
-            off += n
-        torch.cuda.synchronize()
+            torch.cuda.current_stream(dev).wait_event(copied[p % 2])
+            if p + 1 < len(passes):
+                h2d(p + 1)
+            out = sm.commit(129, mine, plens, bufs[p % 2][:n])
+            errors += int(out.reply_bytes.sum().item())  # the pass's reply sizes back on the host
+        torch.cuda.synchronize(dev)
         dist.barrier()
         dt = time.perf_counter() - t0
         if timed:
@@ -556,23 +591,31 @@ def run_sharded(args, world, rank, local_rank):
             step_ms.append(float(t.item()))
         t_cursor += 10
     stats = engine.stats()
-    pass_lat = engine.pass_latencies()
 
-    # Full-run properties: every reply empty, every transfer stored once somewhere, debits == credits.
-    tot = torch.tensor([int(errors.item()), stats["transfers"]], dtype=torch.int64, device=dev)
+    # Full-run properties: every reply empty, every transfer stored once somewhere, debits ==
+    # credits in total (summed over owners), no rank holding balances it does not own.
+    local = backend.export_accounts()
+    not_mine = ~sm._owner_mask(local)
+    stray = sum(int(np.count_nonzero(local[f + w][not_mine])) for f in
+                ("debits_pending", "debits_posted", "credits_pending", "credits_posted") for w in ("_lo", "_hi"))
+    dpost = sum(int(x) for x in local["debits_posted_lo"]) + (sum(int(x) for x in local["debits_posted_hi"]) << 64)
+    cpost = sum(int(x) for x in local["credits_posted_lo"]) + (sum(int(x) for x in local["credits_posted_hi"]) << 64)
+    tot = torch.tensor([errors, stats["transfers"], stray], dtype=torch.int64, device=dev)
     dist.all_reduce(tot)
-    accts = sm.export_accounts()
-    dpost = sum(int(x) for x in accts["debits_posted_lo"]) + (sum(int(x) for x in accts["debits_posted_hi"]) << 64)
-    cpost = sum(int(x) for x in accts["credits_posted_lo"]) + (sum(int(x) for x in accts["credits_posted_hi"]) << 64)
-    full_ok = bool(int(tot[0]) == 0 and int(tot[1]) == args.transfers * world and dpost == cpost and dpost > 0
-                   and sm.passes_dirty == 0)
+    sums = torch.tensor([[dpost & ((1 << 62) - 1), dpost >> 62], [cpost & ((1 << 62) - 1), cpost >> 62]],
+                        dtype=torch.int64, device=dev)
+    dist.all_reduce(sums)
+    s = sums.cpu().tolist()
+    d_all, c_all = s[0][0] + (s[0][1] << 62), s[1][0] + (s[1][1] << 62)
+    full_ok = bool(int(tot[0]) == 0 and int(tot[1]) == args.transfers * world and int(tot[2]) == 0
+                   and d_all == c_all and d_all > 0 and sm.passes_dirty == 0)
 
     total_ms = sum(step_ms)
     value = args.transfers * world * args.steps / (total_ms / 1e3)
     recv_per_launch = args.transfers / max(1, stats["launches_validate"] / max(1, args.steps))
     u_over_t = expected_unique(args.accounts, 2 * recv_per_launch) / recv_per_launch
     roof = roofline(stats, u_over_t, recv_per_launch, args, total_ms)
-    pass_lat = np.array(pass_lat) if len(pass_lat) else np.array([float("nan")])
+    pcie_gbs = args.transfers * 128 * args.steps / (total_ms / 1e3) / 1e9
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -585,14 +628,18 @@ def run_sharded(args, world, rank, local_rank):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u128",
-        "data": "synthetic (device-generated, reference benchmark shapes)",
-        "config": {"workload": "C2 per GPU, routed across GPUs (C5 shape): %d replicated accounts, %d uniform "
-                               "transfers submitted per GPU, home GPU = hash(id), prepares of %d"
-                               % (args.accounts, args.transfers, args.batch),
+        "data": "synthetic (generated on the GPU in the reference benchmark's shapes, copied to pinned host memory "
+                "before timing)",
+        "config": {"workload": "C5 (BASELINE.json configs[4]): %d accounts owner-partitioned by hash(id) over %d GPUs, "
+                               "%d uniform transfers submitted per GPU (%d in all), prepares of %d; transfer home = "
+                               "hash(id), legs to account owners, all-to-all over RCCL"
+                               % (args.accounts, world, args.transfers, args.transfers * world, args.batch),
                    "prepares_per_step": len(lens) * world, "pass_prepares_per_gpu": args.pass_batches,
-                   "parallelism": "route%d (all-to-all over RCCL)" % world},
-        "p99_batch_latency_ms": round(float(np.percentile(lat, 99)), 3),
-        "batch_latency_ms": {"definition": "device time of the home commit pass (rank 0); excludes the all-to-all"},
+                   "input": "prepare bodies in pinned host memory per rank; PCIe H2D inside the timed region, "
+                            "overlapped with the previous pass",
+                   "parallelism": "shard%d (events to home GPU, legs to owner GPU, RCCL all-to-all)" % world},
+        "pcie": {"achieved_per_gpu": round(pcie_gbs, 2), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(pcie_gbs / PCIE_PEAK_GBS, 4)},
         "passes": {"clean": sm.passes_clean, "dirty": sm.passes_dirty},
         "roofline": roof,
         "cpu_baseline": None,

@@ -78,6 +78,12 @@ class PassResult:
         return PassResult(torch.from_numpy(results.view(np.int32)).to(device), torch.from_numpy(rb).to(device), offsets)
 
 
+def _stream_sync(device):
+    """Wait for torch's current stream on `device` (its work, and the RCCL collectives it waits
+    on), not the whole device: a copy of the next pass on another stream keeps running."""
+    torch.cuda.current_stream(device).synchronize()
+
+
 def _events_np(events):
     return events.cpu().numpy().reshape(-1).view(TRANSFER_DTYPE)
 
@@ -119,7 +125,7 @@ class GpuShard:
         p = _lib.tbgpu_route_plan()
         ts = (ctypes.c_uint64 * max(nb, 1))(*[int(t) for t in timestamps])
         ls = (ctypes.c_uint32 * max(nb, 1))(*[int(x) for x in lens])
-        torch.cuda.synchronize(self.device)
+        _stream_sync(self.device)
         _lib.check(self.lib.tbgpu_route_plan_build(self.engine.h, nb, ts, ls, events.data_ptr(), send_events.data_ptr(),
                                                    slots.data_ptr(), ctypes.byref(p)))
         plan = RoutePlan([int(p.send_counts[i]) for i in range(self.world)], _u128(p.sum_lo, p.sum_hi),
@@ -130,7 +136,7 @@ class GpuShard:
         m = events.shape[0]
         codes = torch.empty(max(m, 1), dtype=torch.uint8, device=self.device)
         if m:
-            torch.cuda.synchronize(self.device)
+            _stream_sync(self.device)
             _lib.check(self.lib.tbgpu_commit_routed_async(self.engine.h, m, events.data_ptr(), ts_max, cert,
                                                           codes.data_ptr()))
             self.engine.sync()
@@ -145,7 +151,7 @@ class GpuShard:
         cap = max(2 * m, 1)
         legs = torch.empty((self.world * cap, 5), dtype=torch.int64, device=self.device)
         counts = torch.zeros(self.world, dtype=torch.int64, device=self.device)
-        torch.cuda.synchronize(self.device)
+        _stream_sync(self.device)
         _lib.check(self.lib.tbgpu_commit_routed_owner_async(self.engine.h, m, events.data_ptr(), ts_max, cert,
                                                             codes.data_ptr(), self.world, rank, legs.data_ptr(), cap,
                                                             counts.data_ptr()))
@@ -156,7 +162,7 @@ class GpuShard:
 
     def apply_owner_legs(self, legs, cert):
         if legs.shape[0]:
-            torch.cuda.synchronize(self.device)
+            _stream_sync(self.device)
             _lib.check(self.lib.tbgpu_apply_owner_legs_async(self.engine.h, legs.data_ptr(), legs.shape[0], cert))
 
     def replies(self, lens, slots, codes_back):
@@ -167,7 +173,7 @@ class GpuShard:
         reply_bytes = torch.zeros(max(nb, 1), dtype=torch.int32, device=self.device)
         if nb:
             ls = (ctypes.c_uint32 * nb)(*[int(x) for x in lens])
-            torch.cuda.synchronize(self.device)
+            _stream_sync(self.device)
             _lib.check(self.lib.tbgpu_route_replies_async(self.engine.h, nb, ls, slots.data_ptr(), codes_back.data_ptr(),
                                                           results.data_ptr(), reply_bytes.data_ptr()))
             self.engine.sync()
@@ -273,7 +279,7 @@ class ShardedStateMachine:
         out = torch.empty((int(sum(recv_counts)),) + shape, dtype=send.dtype, device=self.comm_device)
         src = send.to(self.comm_device)
         if self.comm_device.type == "cuda":
-            torch.cuda.synchronize(self.comm_device)
+            _stream_sync(self.comm_device)
         dist.all_to_all_single(out, src.contiguous(), [int(c) for c in recv_counts], [int(c) for c in send_counts],
                                group=self.group)
         return out.to(self.b.device)
