@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--chunk-prepares", type=int, default=64,
                    help="prepares per pipelined chunk of the headline (host memory -> PCIe -> commit -> reply)")
     p.add_argument("--device-steps", type=int, default=3, help="timed steps of the HBM-resident secondary leg")
+    p.add_argument("--secondary", type=int, default=10_000_000,
+                   help="transfers of the C3 / C4 secondary lines (0: skip)")
     p.add_argument("--cpu-sample", type=int, default=12_285_000, help="transfers in the CPU baseline / parity sample (0: skip)")
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"],
@@ -193,6 +195,83 @@ def run_cpu_baseline(engine, args, acct_lens, acct_ts, events_dev, sample_lens, 
         "seconds": dt,
         "c1": run_cpu_c1(engine, args),
     }, oracle, replies
+
+
+def run_secondary(args, kind, device):
+    """BASELINE.json configs[2] (C3) / configs[3] (C4) at 1M accounts and args.secondary transfers,
+    measured like the headline (prepares in registered host memory, pipelined chunks, PCIe
+    inclusive), with its own roofline; parity: the first 1M transfers committed on a fresh engine
+    and compared with the oracle byte for byte (replies, accounts, transfers, posted groove)."""
+    from tests.harness.configs import KINDS, SETTINGS, generate, split
+    from tests.harness.oracle import OracleEngine
+    from tigerbeetle_amd.state_machine import Engine, Options
+
+    wl = SETTINGS[kind]
+    n_acct, n_xfer = 1_000_000, args.secondary
+    eng = Engine(Options(accounts_max=n_acct, transfers_max=n_xfer, pass_events_max=args.chunk_prepares * args.batch,
+                         pass_batches_max=args.chunk_prepares, device=device, profile=True))
+    accts, xfers = generate(eng, kind, n_acct, n_xfer, seed=args.seed)
+    a_lens, x_lens = batches(n_acct, args.batch), batches(n_xfer, args.batch)
+    a_ts, t_end = timestamps(a_lens, 1_000_000_000)
+
+    def create_accounts(e):
+        rb, _, _ = e.commit_pipelined(128, a_ts, a_lens, accts, chunk_batches=args.chunk_prepares)
+        assert int(rb.sum()) == 0, "account creation returned errors"
+
+    create_accounts(eng)
+    eng.register_host(xfers)
+    replies = np.empty(n_xfer * 8, dtype=np.uint8)
+    step_ms, t_cursor = [], t_end
+    eng.profile_mask(eng.PROF_VALIDATE | eng.PROF_REPLAY)
+    for step in range(2):  # one warmup, one timed
+        eng.reset_transfers()
+        ts, t_cursor = timestamps(x_lens, t_cursor + 10, wl["gap_every"])
+        if step == 1:
+            eng.reset_stats()
+        t0 = time.perf_counter()
+        rb, _, _ = eng.commit_pipelined(129, ts, x_lens, xfers, chunk_batches=args.chunk_prepares, replies=replies)
+        if step == 1:
+            step_ms.append((time.perf_counter() - t0) * 1e3)
+    stats = eng.stats()
+    eng.unregister_host(xfers)
+    eng.close()
+    per_launch = n_xfer / max(1, stats["launches_validate"])
+    # The ordered fallback (tb_flow) has no byte roofline (it is bound by its dependency rounds):
+    # the roofline is the validate kernel's; tb_flow's time share is reported beside it.
+    roof = roofline(stats, expected_unique(n_acct, 2 * per_launch) / per_launch, per_launch,
+                    argparse.Namespace(transfers=n_xfer, steps=1), step_ms[0], None, kernel="tb_transfers_validate")
+    roof["flow_ms_share"] = round(stats["ms_replay"] / step_ms[0], 4)
+
+    # Parity: the first 1M transfers (the same prepares, same timestamps) on a fresh engine.
+    n_par = min(n_xfer, 1_000_000)
+    p_lens = batches(n_par, args.batch)
+    p_ts, _ = timestamps(p_lens, t_end + 10, wl["gap_every"])
+    oracle = OracleEngine(n_acct, n_par)
+    assert all(r == b"" for r in oracle.commit_many(128, a_ts, split(accts, a_lens)))
+    expected = oracle.commit_many(129, p_ts, split(xfers[:n_par * 128], p_lens))
+    eng = Engine(Options(accounts_max=n_acct, transfers_max=n_par, pass_events_max=args.chunk_prepares * args.batch,
+                         pass_batches_max=args.chunk_prepares, device=device))
+    create_accounts(eng)
+    rb, rep, _ = eng.commit_pipelined(129, p_ts, p_lens, np.ascontiguousarray(xfers[:n_par * 128]),
+                                      chunk_batches=args.chunk_prepares)
+    got, off = [], 0
+    for L, nb in zip(p_lens, rb):
+        got.append(bytes(rep[off * 8:off * 8 + int(nb)]))
+        off += L
+    parity = {"sample_transfers": n_par, "replies_equal": got == expected,
+              "accounts_equal": eng.export_accounts().tobytes() == oracle.export_accounts().tobytes(),
+              "transfers_equal": eng.export_transfers().tobytes() == oracle.export_transfers().tobytes(),
+              "posted_equal": bool(np.array_equal(eng.export_posted(), oracle.export_posted())),
+              "failed_events": sum(len(r) for r in expected) // 8}
+    eng.close()
+    return {"workload": WORKLOAD_TEXT[kind] % (n_acct, n_xfer, args.batch),
+            "value": round(n_xfer / (step_ms[0] / 1e3), 1), "unit": "transfers/s", "ms_per_step": round(step_ms[0], 3),
+            "input": "registered host memory, %d-prepare pipelined chunks, PCIe inclusive" % args.chunk_prepares,
+            "dependent_events": stats["dependent_events"],
+            "flow": {k: (round(stats[k], 3) if isinstance(stats[k], float) else stats[k])
+                     for k in ("flow_units", "flow_runs", "flow_plan_ms", "flow_run_ms", "bounds_passes", "bounds_units",
+                               "bounds_rounds", "bounds_skipped", "bounds_abandoned")},
+            "roofline": roof, "parity": parity}
 
 
 def run_cpu_c1(engine, args):
@@ -332,6 +411,7 @@ def main():
     engine.register_host(host_events)
     replies = np.empty(args.transfers * 8, dtype=np.uint8)
     step_ms, lat_all = [], []
+    rb_h = np.zeros(1, dtype=np.uint32)
     t_cursor = t_end
     breakdown = None
     if args.warmup:
@@ -360,7 +440,7 @@ def main():
     n_failed_host = int(rb_h.sum()) // 8
     engine.unregister_host(host_events)
     del host_events
-    lat = np.sort(np.concatenate(lat_all))
+    lat = np.sort(np.concatenate(lat_all)) if lat_all else np.array([float("nan")])
 
     # -- secondary: the same commits with the prepares already resident in HBM ----------------
     dev_ms = []
@@ -446,6 +526,11 @@ def main():
                        "accounts_equal": acc_equal, "transfers_equal": xfer_equal})
         cpu.pop("seconds")
 
+    secondary = {}
+    if rank == 0 and world == 1 and args.workload == "c2" and args.secondary:
+        for kind in ("c3", "c4"):
+            secondary[kind] = run_secondary(args, kind, local_rank)
+
     host = None
     if rank == 0 and world == 1 and args.host_prepares > 0:
         host, t_cursor = run_host_commits(engine, args, events_dev, t_cursor)
@@ -477,12 +562,14 @@ def main():
         "device_resident": device_resident,
         "dependent_events": stats["dependent_events"],
         "flow": {k: (round(stats[k], 3) if isinstance(stats[k], float) else stats[k])
-                 for k in ("flow_units", "flow_runs", "flow_run_units", "flow_plan_ms", "flow_run_ms")},
+                 for k in ("flow_units", "flow_runs", "flow_run_units", "flow_plan_ms", "flow_run_ms", "bounds_passes",
+                           "bounds_units", "bounds_rounds", "bounds_skipped", "bounds_abandoned")},
         "failed_events": n_failed,
         "roofline": roof,
         "cpu_baseline": cpu,
         "parity": parity,
         "host_commit": host,
+        "secondary": secondary or None,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -651,7 +738,7 @@ def run_sharded(args, world, rank, local_rank):
     dist.destroy_process_group()
 
 
-def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=None, steps=None):
+def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=None, steps=None, kernel=None):
     """The dominant kernel of the timed steps against the HBM peak; `kernels` = every kernel's mean
     launch time (from the warmup steps when given: the timed steps time only validate, replay/flow
     and whole passes)."""
@@ -666,7 +753,7 @@ def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=No
         }
 
     kernels = kernel_table(stats)
-    dom = max(kernels, key=lambda k: kernels[k][0])
+    dom = kernel or max(kernels, key=lambda k: kernels[k][0])
     ms_dom, n_dom = kernels[dom]
     # B = 296 + 256·U/T per transfer, split by where the work happens:
     # validate reads the event (128), probes + claims the id (32), writes the record (128) and reads

@@ -184,6 +184,11 @@ typedef struct tbgpu_stats {
     uint64_t flow_run_units;     /* units covered by runs */
     double flow_plan_ms;         /* tb_flow wall time planning the dependent events (workgroup 0) */
     double flow_run_ms;          /* tb_flow wall time executing them in order (workgroup 0) */
+    uint64_t bounds_passes;      /* passes whose limit checks were all decided by bounds scans (no ordered run) */
+    uint64_t bounds_units;       /* dependent events they decided */
+    uint64_t bounds_rounds;      /* scan rounds they took (and those of abandoned attempts) */
+    uint64_t bounds_skipped;     /* dependent passes with an event the bounds do not cover */
+    uint64_t bounds_abandoned;   /* passes whose bounds did not converge (ordered run instead) */
 } tbgpu_stats;
 
 int tbgpu_get_stats(tbgpu_t* engine, tbgpu_stats* stats);

@@ -56,6 +56,11 @@ class tbgpu_stats(ctypes.Structure):
         ("flow_run_units", ctypes.c_uint64),
         ("flow_plan_ms", ctypes.c_double),
         ("flow_run_ms", ctypes.c_double),
+        ("bounds_passes", ctypes.c_uint64),
+        ("bounds_units", ctypes.c_uint64),
+        ("bounds_rounds", ctypes.c_uint64),
+        ("bounds_skipped", ctypes.c_uint64),
+        ("bounds_abandoned", ctypes.c_uint64),
     ]
 
 

@@ -397,6 +397,13 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         INIT_CK(hipMalloc(&F.hist, (u64)F.grid * 256 * 4));
         INIT_CK(hipMalloc(&F.words, FW_WORDS * 4));
         INIT_CK(hipMalloc(&F.undo, pe * 4 * sizeof(UndoEntry)));
+        INIT_CK(hipMalloc(&F.b_st, pe * 4));
+        INIT_CK(hipMalloc(&F.b_vd, pe));
+        INIT_CK(hipMalloc(&F.b_vc, pe));
+        INIT_CK(hipMalloc(&F.b_amt, pe * 8 * FLOW_RMAX));
+        INIT_CK(hipMalloc(&F.b_meta, pe * 4 * FLOW_RMAX));
+        INIT_CK(hipMalloc(&F.b_blk, (u64)F.grid * 5 * 8));
+        F.bounds_rounds_max = FLOW_BOUNDS_ROUNDS_MAX;
     }
     INIT_CK(hipMalloc(&E->staging, pe * 128));
     INIT_CK(hipMalloc(&E->results, pe * 8));
@@ -446,7 +453,8 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->r_home,
                     E->r_block_counts, E->r_words, E->r_meta, E->leg_ev, E->leg_w, E->leg_off,
                     E->F.f_pe, E->F.f_batch, E->F.f_len, E->F.need, E->F.nsucc, E->F.queue, E->F.uflags, E->F.nacct, E->F.rpos, E->F.succ,
-                    E->F.run, E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo};
+                    E->F.run, E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo,
+                    E->F.b_st, E->F.b_vd, E->F.b_vc, E->F.b_amt, E->F.b_meta, E->F.b_blk};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int k = 0; k < PIPE_SLOTS; k++) {
         tbgpu::PipeSlot& S = E->pipe[k];
@@ -1247,6 +1255,11 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     s->flow_run_units = g.flow_run_units;
     s->flow_plan_ms = E->wall_khz ? (double)g.flow_plan_ticks / E->wall_khz : 0.0;
     s->flow_run_ms = E->wall_khz ? (double)g.flow_run_ticks / E->wall_khz : 0.0;
+    s->bounds_passes = g.bounds_passes;
+    s->bounds_units = g.bounds_units;
+    s->bounds_rounds = g.bounds_rounds;
+    s->bounds_skipped = g.bounds_skipped;
+    s->bounds_abandoned = g.bounds_abandoned;
     return TBGPU_STATUS_OK;
 }
 

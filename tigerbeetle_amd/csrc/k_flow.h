@@ -38,8 +38,11 @@
 #define FLOW_NB_MAX 4096        // prepares per pass the planner handles (LDS prefix)
 #define FLOW_SENT 0xFFFFFFFFu   // empty pair slot
 
-enum : u32 { FW_NUNITS = 0, FW_QTAIL = 1, FW_SEQ = 2, FW_WORDS = 8 };
-enum : u32 { UF_ID_SINGLE = 1 };  // the unit is the only dependent event of the pass naming its id
+enum : u32 { FW_NUNITS = 0, FW_QTAIL = 1, FW_SEQ = 2, FW_BNO = 3, FW_BUND = 4, FW_BDEC = 5, FW_WORDS = 8 };
+enum : u32 {
+    UF_ID_SINGLE = 1,  // the unit is the only dependent event of the pass whose id has its key
+    UF_ID_UNIQUE = 2,  // ... or the others sharing the key (a 31-bit hash) name different ids
+};
 
 // Everything a run needs of the unit at sorted position q, packed by the planner so the run walker
 // reads one level (the list entry) instead of three (list entry -> unit -> event).
@@ -69,6 +72,15 @@ struct FlowArgs {
     UndoEntry* undo;  // [4 * pass events] chain of head u: [4u, 4u + 4 * len)
     u32 grid;
     u64 stall_ticks;  // wall_clock64 ticks after which a wait is taken as an engine bug (PANIC_FLOW_STALL)
+    // Bounds certification of limit checks (fl_bounds): per unit head its state and the verdicts of
+    // its debit-side / credit-side limit check; per account-resource position its leg.
+    u32* b_st;      // [pass events] BS_*
+    u8* b_vd;       // [pass events] BV_* of the debit account's check
+    u8* b_vc;       // [pass events] BV_* of the credit account's check
+    u64* b_amt;     // [FLOW_RMAX * pass events] leg amount (< 2^64 under the certificate)
+    u32* b_meta;    // [FLOW_RMAX * pass events] unit << 3 | BT_* | BT_CR
+    u64* b_blk;     // [grid * 5] per workgroup: segment-start flag, then 4 sums
+    u32 bounds_rounds_max;
 };
 
 // Every wait of the kernel is bounded by wall time (s_memrealtime) since the wait began.
@@ -358,6 +370,299 @@ __device__ static inline void fl_finish(const PassArgs& P, u8* s_code, u32* s_wa
     }
 }
 
+// ---- bounds certification of the limit checks (north star (c)) ---------------------------------
+// A pass whose dependent events are all single plain create_transfers that kernel 1 validated
+// (their only open checks are the limits of their flagged accounts, tigerbeetle.zig:31-39,
+// state_machine.zig:863-864; the certificate rules out every overflow check and 64-bit sums
+// suffice) is decided without the ordered run.  Per limit account, its events in batch order form
+// a segment (the planner's sorted resource list).  For a debits_must_not_exceed_credits account
+// the check of a debit is  dp + dpost + (earlier ok debits) + amount <= cpost + (earlier ok posted
+// credits);  credits_must_not_exceed_debits is the mirror image.  Each ROUND takes a segmented
+// prefix scan (LDS + wave shuffles, grid-wide carries) of four sums per position: the earlier debits
+// counting only decided-ok units (min) or every unit not decided failing (max), and the same for the
+// credits.  A check certainly passes if it passes with max debits and min credits, certainly fails if
+// it fails with min debits and max credits.  A unit is decided once its checks decide its result in
+// the reference's order (exceeds_credits before exceeds_debits).  The first undecided event of every
+// segment sees only decided events before it, so each round decides at least one event per segment
+// and the rounds terminate; the bounds usually decide far more.  Decisions are
+// facts, not effects: nothing is applied until every unit is decided, then the ok units' balance
+// legs and index entries are applied in parallel (the sums commute).  A pass with any other kind of
+// dependent unit, or one that does not converge within bounds_rounds_max, takes the ordered run
+// with nothing changed.
+#define FLOW_BOUNDS_ROUNDS_MAX 4096
+enum : u8 { BS_UNK = 0, BS_OK = 1, BS_FAIL_CREDITS = 2, BS_FAIL_DEBITS = 3, BS_FAIL_STATIC = 4 };
+enum : u8 { BV_UNK = 0, BV_PASS = 1, BV_FAIL = 2 };
+enum : u32 { BT_NONE = 0, BT_X = 1, BT_Y = 2, BT_CR = 4 };  // X: checked side (any field); Y: other side, posted
+
+// Inclusive segmented scan of four u64 sums over the workgroup (one position per thread), on top of
+// `carry` (the running sums of the segment open at the chunk start).  f = 1 starts a segment.
+// Returns the inclusive sums in v; carry becomes the chunk's last inclusive sums.
+__device__ static inline void fl_seg_scan4(u64 (&v)[4], u32 f, u64 (&carry)[4], u64 (*s_wv)[4], u32* s_wf) {
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (u32 off = 1; off < 64; off <<= 1) {
+        u64 o[4];
+#pragma unroll
+        for (u32 k = 0; k < 4; k++) o[k] = __shfl_up((unsigned long long)v[k], off);
+        const u32 of = __shfl_up(f, off);
+        if (lane >= off) {
+            if (!f) {
+#pragma unroll
+                for (u32 k = 0; k < 4; k++) v[k] += o[k];
+            }
+            f |= of;
+        }
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (u32 k = 0; k < 4; k++) s_wv[wave][k] = v[k];
+        s_wf[wave] = f;
+    }
+    __syncthreads();
+    u64 pv[4] = {carry[0], carry[1], carry[2], carry[3]};
+    for (u32 w = 0; w < wave; w++) {
+        if (s_wf[w]) {
+#pragma unroll
+            for (u32 k = 0; k < 4; k++) pv[k] = s_wv[w][k];
+        } else {
+#pragma unroll
+            for (u32 k = 0; k < 4; k++) pv[k] += s_wv[w][k];
+        }
+    }
+    if (!f) {
+#pragma unroll
+        for (u32 k = 0; k < 4; k++) v[k] += pv[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == blockDim.x - 1) {
+#pragma unroll
+        for (u32 k = 0; k < 4; k++) s_wv[0][k] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (u32 k = 0; k < 4; k++) carry[k] = s_wv[0][k];
+    __syncthreads();
+}
+
+// Contribution of position q this round: {debits min, max, credits min, max} of the checked
+// account's sides (X = the checked side, Y = the other side's posted field).
+__device__ static inline void fl_bound_contrib(const FlowArgs& F, u32 q, u64 (&v)[4]) {
+    const u32 meta = F.b_meta[q];
+    const u64 a = F.b_amt[q];
+    const u32 st = F.b_st[meta >> 3];
+    const u64 mn = st == BS_OK ? a : 0, mx = (st == BS_OK || st == BS_UNK) ? a : 0;
+    const bool x = meta & BT_X, y = meta & BT_Y;
+    v[0] = x ? mn : 0;
+    v[1] = x ? mx : 0;
+    v[2] = y ? mn : 0;
+    v[3] = y ? mx : 0;
+}
+
+// Returns true when every unit was decided and applied (the ordered run is skipped).
+__device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u32 ndep, u32 N, bool cert64, u32& gen,
+                                        u64& tsmax, u64 (*s_wv)[4], u32* s_wf, u32* s_cnt) {
+    Globals* g = P.T.g;
+    const Tables& T = P.T;
+    const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid;
+    const u32* K = F.keys[0];
+    if (!cert64 || F.bounds_rounds_max == 0) return false;
+    // Account positions are the prefix of the sorted list (keys < 2^31).
+    u32 lo = 0, hi = N;
+    while (lo < hi) {
+        const u32 mid = (lo + hi) >> 1;
+        if (K[mid] < 0x80000000u) lo = mid + 1; else hi = mid;
+    }
+    const u32 NA = lo;
+
+    // S1: units — eligibility, static failures, no check yet.
+    for (u32 f = blockIdx.x * NT + tid; f < ndep; f += G * NT) {
+        if (!F.f_len[f]) continue;
+        const u32 pe = F.f_pe[f];
+        const u32 info = P.info[pe];
+        const u16 fl = P.eflags[pe];
+        const bool elig = F.f_len[f] == 1 && (F.uflags[f] & (UF_ID_SINGLE | UF_ID_UNIQUE)) && (info & HZ_SPEC) &&
+                          (info & HZ_ACCTS) &&
+                          !(fl & (TF_LINKED | TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT)) &&
+                          P.amt[2 * pe + 1] == 0;
+        if (!elig) {
+            atomicOr(&F.words[FW_BNO], 1u);
+            continue;
+        }
+        const bool ok = (info & 0xFF) == R_OK;
+        F.b_st[f] = ok ? BS_UNK : BS_FAIL_STATIC;
+        F.b_vd[f] = BV_PASS;
+        F.b_vc[f] = BV_PASS;
+        if (ok) atomicAdd(&F.words[FW_BUND], 1u);
+    }
+    fl_grid_sync(g, G, gen, F);
+    if (fl_stalled(g)) return false;
+    if (*(volatile u32*)&F.words[FW_BNO]) {
+        if (blockIdx.x == 0 && tid == 0) atomicAdd((unsigned long long*)&g->bounds_skipped, 1ULL);
+        return false;
+    }
+
+    // S2: positions — the leg each holds, and which checks are open.
+    for (u32 q = blockIdx.x * NT + tid; q < NA; q += G * NT) {
+        const RunEntry x = F.run[q];
+        const u32 r = K[q];
+        const u16 rf = T.acct_hot[r].flags;
+        const bool debit = x.dr == r, pend = x.flags & TF_PENDING;
+        u32 type = BT_NONE;
+        if (rf & AF_DEBITS_MUST_NOT_EXCEED_CREDITS) type = debit ? BT_X : (pend ? BT_NONE : BT_Y);
+        else if (rf & AF_CREDITS_MUST_NOT_EXCEED_DEBITS) type = debit ? (pend ? BT_NONE : BT_Y) : (BT_X | BT_CR);
+        F.b_meta[q] = (x.u << 3) | type;
+        F.b_amt[q] = x.amt_lo;
+        if ((type & BT_X) && F.b_st[x.u] == BS_UNK) {
+            if (type & BT_CR) F.b_vc[x.u] = BV_UNK;
+            else F.b_vd[x.u] = BV_UNK;
+        }
+    }
+    fl_grid_sync(g, G, gen, F);
+    if (fl_stalled(g)) return false;
+    // S3: units with no open check (a credit to a debits-limited account, ...) are ok.
+    for (u32 f = blockIdx.x * NT + tid; f < ndep; f += G * NT) {
+        if (F.f_len[f] && F.b_st[f] == BS_UNK && F.b_vd[f] == BV_PASS && F.b_vc[f] == BV_PASS) {
+            F.b_st[f] = BS_OK;
+            atomicSub(&F.words[FW_BUND], 1u);
+        }
+    }
+    fl_grid_sync(g, G, gen, F);
+    if (fl_stalled(g)) return false;
+
+    const u32 tile = ((NA + G - 1) / G + NT - 1) / NT * NT;
+    const u32 t0 = min(NA, blockIdx.x * tile), t1 = min(NA, t0 + tile);
+    bool converged = *(volatile u32*)&F.words[FW_BUND] == 0;
+    u32 rounds = 0;
+    for (; !converged && rounds < F.bounds_rounds_max; rounds++) {
+        u32* dec = &F.words[FW_BDEC + rounds % 3];
+        if (blockIdx.x == 0 && tid == 0) F.words[FW_BDEC + (rounds + 1) % 3] = 0;
+        // Phase A: this tile's aggregate (sums since its last segment start; start flag).
+        u64 carry[4] = {0, 0, 0, 0};
+        u32 any_start = 0;
+        for (u32 c0 = t0; c0 < t1; c0 += NT) {
+            const u32 q = c0 + tid;
+            u64 v[4] = {0, 0, 0, 0};
+            u32 f = 0;
+            if (q < t1) {
+                fl_bound_contrib(F, q, v);
+                f = q == 0 || K[q] != K[q - 1];
+            }
+            any_start |= __syncthreads_or(f);
+            fl_seg_scan4(v, f, carry, s_wv, s_wf);
+        }
+        if (tid == 0) {
+            F.b_blk[5 * blockIdx.x] = any_start;
+#pragma unroll
+            for (u32 k = 0; k < 4; k++) F.b_blk[5 * blockIdx.x + 1 + k] = carry[k];
+        }
+        fl_grid_sync(g, G, gen, F);
+        if (fl_stalled(g)) return false;
+        // Phase B: carry-in from the preceding tiles, then the scan again with the decisions.
+        u64 cin[4] = {0, 0, 0, 0};
+        for (int b = (int)blockIdx.x - 1; b >= 0; b--) {
+#pragma unroll
+            for (u32 k = 0; k < 4; k++) cin[k] += F.b_blk[5 * b + 1 + k];
+            if (F.b_blk[5 * b]) break;
+        }
+        if (tid == 0) *s_cnt = 0;
+        __syncthreads();
+        u32 mine = 0;
+        for (u32 c0 = t0; c0 < t1; c0 += NT) {
+            const u32 q = c0 + tid;
+            u64 v[4] = {0, 0, 0, 0}, own[4] = {0, 0, 0, 0};
+            u32 f = 0;
+            if (q < t1) {
+                fl_bound_contrib(F, q, v);
+                f = q == 0 || K[q] != K[q - 1];
+#pragma unroll
+                for (u32 k = 0; k < 4; k++) own[k] = v[k];
+            }
+            fl_seg_scan4(v, f, cin, s_wv, s_wf);
+            if (q >= t1) continue;
+            const u32 meta = F.b_meta[q];
+            const u32 u = meta >> 3;
+            if (!(meta & BT_X) || F.b_st[u] != BS_UNK) continue;
+            const bool cr_side = meta & BT_CR;
+            if ((cr_side ? F.b_vc[u] : F.b_vd[u]) == BV_UNK) {
+                // Exclusive sums: the decided / possible effects of the earlier events of the
+                // segment.  Statuses read in the middle of a round are facts, old or new, so any mix
+                // of them still bounds the truth.
+                const u64 xmin = v[0] - own[0], xmax = v[1] - own[1], ymin = v[2] - own[2], ymax = v[3] - own[3];
+                const AccountBal& B = T.acct_bal[K[q]];
+                const u64 xb = cr_side ? tb_lo(B.credits_pending) + tb_lo(B.credits_posted)
+                                       : tb_lo(B.debits_pending) + tb_lo(B.debits_posted);
+                const u64 yb = cr_side ? tb_lo(B.debits_posted) : tb_lo(B.credits_posted);
+                const u64 a = F.b_amt[q];
+                u8 verdict = BV_UNK;
+                if (xb + xmax + a <= yb + ymin) verdict = BV_PASS;
+                else if (xb + xmin + a > yb + ymax) verdict = BV_FAIL;
+                if (verdict == BV_UNK) continue;
+                if (cr_side) F.b_vc[u] = verdict;
+                else F.b_vd[u] = verdict;
+                __threadfence();
+            }
+            // Combine in the reference's order (:863-864: exceeds_credits first).  A unit whose two
+            // verdicts land in one round from two lanes is combined by either lane in a later round.
+            const u8 vd = *(volatile u8*)&F.b_vd[u], vc = *(volatile u8*)&F.b_vc[u];
+            u32 st = BS_UNK;
+            if (vd == BV_FAIL) st = BS_FAIL_CREDITS;
+            else if (vd == BV_PASS && vc == BV_FAIL) st = BS_FAIL_DEBITS;
+            else if (vd == BV_PASS && vc == BV_PASS) st = BS_OK;
+            if (st != BS_UNK && atomicCAS(&F.b_st[u], (u32)BS_UNK, st) == BS_UNK) mine++;
+        }
+        if (mine) atomicAdd(s_cnt, mine);
+        __syncthreads();
+        if (tid == 0 && *s_cnt) {
+            atomicAdd(dec, *s_cnt);
+            atomicSub(&F.words[FW_BUND], *s_cnt);
+        }
+        fl_grid_sync(g, G, gen, F);
+        if (fl_stalled(g)) return false;
+        converged = *(volatile u32*)&F.words[FW_BUND] == 0;
+        if (!converged && *(volatile u32*)dec == 0) break;  // no progress (not expected)
+    }
+    if (!converged) {
+        if (blockIdx.x == 0 && tid == 0) {
+            atomicAdd((unsigned long long*)&g->bounds_abandoned, 1ULL);
+            atomicAdd((unsigned long long*)&g->bounds_rounds, (unsigned long long)rounds);
+        }
+        return false;
+    }
+
+    // Apply: the ok units' legs (both accounts; sums commute), their index entries and counts; the
+    // failed ones' codes.  Kernel 1 already wrote every record at its log position.
+    u32 n_ok = 0;
+    u64 tsm = 0;
+    for (u32 f = blockIdx.x * NT + tid; f < ndep; f += G * NT) {
+        if (!F.f_len[f]) continue;
+        const u32 pe = F.f_pe[f];
+        const u8 st = F.b_st[f];
+        if (st == BS_OK) {
+            const u128 amount = tb_u128(P.amt[2 * pe], P.amt[2 * pe + 1]);
+            const bool pend = P.eflags[pe] & TF_PENDING;
+            u8* dr = (u8*)&T.acct_bal[P.dr[pe]];
+            u8* cr = (u8*)&T.acct_bal[P.cr[pe]];
+            tb_atomic_add_lo_noret(dr + (pend ? BAL_OFF_DEBITS_PENDING : BAL_OFF_DEBITS_POSTED), tb_lo(amount));
+            tb_atomic_add_lo_noret(cr + (pend ? BAL_OFF_CREDITS_PENDING : BAL_OFF_CREDITS_POSTED), tb_lo(amount));
+            __hip_atomic_fetch_and(&T.xidx[P.rs[pe]], ~(u64)XI_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            n_ok++;
+            const u32 b = F.f_batch[f];
+            const u64 boff = P.batch_off[b];
+            tsm = max(tsm, tb_event_ts(P, b, boff, (u32)(P.batch_off[b + 1] - boff), (u32)(P.e0 + pe - boff)));
+        } else if (st == BS_FAIL_CREDITS || st == BS_FAIL_DEBITS) {
+            P.info[pe] = (P.info[pe] & 0xFFFFFF00u) | (st == BS_FAIL_CREDITS ? CT_EXCEEDS_CREDITS : CT_EXCEEDS_DEBITS);
+        }
+    }
+    if (n_ok) atomicAdd((unsigned long long*)&g->transfer_count, (unsigned long long)n_ok);
+    tsmax = max(tsmax, tsm);
+    if (blockIdx.x == 0 && tid == 0) {
+        atomicAdd((unsigned long long*)&g->bounds_passes, 1ULL);
+        atomicAdd((unsigned long long*)&g->bounds_units, (unsigned long long)ndep);
+        atomicAdd((unsigned long long*)&g->bounds_rounds, (unsigned long long)rounds);
+    }
+    return true;
+}
+
 __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, UndoEntry* seq_undo, u32 seq_undo_cap) {
     __shared__ u32 s_dpre[FLOW_NB_MAX + 1];
     __shared__ u32 s_wave[FLOW_THREADS / 64];
@@ -528,6 +833,20 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
             const bool first = q == 0 || K[q - 1] != key;
             const u32 u = V[q];
             if (first && (key & 0x80000000u) && (q + 1 == N || K[q + 1] != key)) atomicOr(&F.uflags[u], UF_ID_SINGLE);
+            if ((key & 0x80000000u) && !(first && (q + 1 == N || K[q + 1] != key))) {
+                // A key shared by several units: a hash collision of different ids only orders them;
+                // the id is unique if no other unit of the run names the same one.
+                const Transfer* me = (const Transfer*)(P.events + (P.e0 + F.f_pe[u]) * 128);
+                bool unique = true;
+                u32 a = q;
+                while (a > 0 && K[a - 1] == key) a--;
+                for (u32 z = a; z < N && K[z] == key && unique; z++) {
+                    if (z == q || V[z] == u) continue;
+                    const Transfer* o = (const Transfer*)(P.events + (P.e0 + F.f_pe[V[z]]) * 128);
+                    unique = o->id != me->id && !((P.eflags[F.f_pe[V[z]]] & (TF_POST | TF_VOID)) && o->pending_id == me->id);
+                }
+                if (unique && (P.eflags[F.f_pe[u]] & (TF_POST | TF_VOID)) == 0) atomicOr(&F.uflags[u], UF_ID_UNIQUE);
+            }
             if (!first && V[q - 1] == u) continue;  // the same unit holds this resource twice
             if (!(key & 0x80000000u)) {
                 atomicAdd(&F.nacct[u], 1u);
@@ -572,8 +891,32 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
         fl_grid_sync(g, G, gen, F);
         if (fl_stalled(g)) return;
     }
+    const u64 ft1 = (blockIdx.x == 0 && tid == 0) ? fl_now() : 0;
+    if (!sequential) {
+        __shared__ u64 s_bwv[FLOW_THREADS / 64][4];
+        __shared__ u32 s_bwf[FLOW_THREADS / 64];
+        __shared__ u32 s_bcnt;
+        u64 tsb = 0;
+        if (fl_bounds(P, F, ndep, N, cert64, gen, tsb, s_bwv, s_bwf, &s_bcnt)) {
+            // Every unit decided and applied: replies and the pass close (workgroup 0) after all
+            // workgroups' writes.
+            if (tsb) atomicMax((unsigned long long*)&g->commit_timestamp, (unsigned long long)tsb);
+            fl_grid_sync(g, G, gen, F);
+            if (blockIdx.x != 0) return;
+            if (tid == 0) {
+                const u64 ft2 = fl_now();
+                atomicAdd((unsigned long long*)&g->flow_plan_ticks, (unsigned long long)(ft1 - ft0));
+                atomicAdd((unsigned long long*)&g->flow_run_ticks, (unsigned long long)(ft2 - ft1));
+                atomicAdd(&g->flow_passes, 1u);
+            }
+            fl_finish(P, s_code, s_wave, s_list, 0, true);
+            return;
+        }
+        // Not certifiable: nothing was applied; the ordered run decides every unit.
+        fl_grid_sync(g, G, gen, F);
+        if (fl_stalled(g)) return;
+    }
     if (blockIdx.x != 0) return;
-    const u64 ft1 = tid == 0 ? fl_now() : 0;
 
     // ---- run (workgroup 0) ---------------------------------------------------------------------
     u64 tsmax = 0;

@@ -193,6 +193,11 @@ struct Globals {
     u64 limit_accounts;       // accounts ever created with a limit flag (never decremented: an upper bound)
     u64 flow_plan_ticks;      // tb_flow wall-clock ticks (workgroup 0): planning, then the ordered run
     u64 flow_run_ticks;
+    u64 bounds_passes;        // passes whose dependent events were all decided by bounds (k_flow.h fl_bounds)
+    u64 bounds_units;         // units they decided
+    u64 bounds_rounds;        // scan rounds they took (and the rounds of abandoned attempts)
+    u64 bounds_skipped;       // dependent passes with an event the bounds do not cover (ordered run)
+    u64 bounds_abandoned;     // passes whose bounds did not converge in FLOW_BOUNDS_ROUNDS_MAX rounds
 };
 
 struct AccountHot {
