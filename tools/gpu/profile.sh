@@ -1,17 +1,26 @@
-# rocprofv3 evidence for the headline bench (MI355X_MICROARCH.md HBM recipe): one kernel-trace +
-# stats run of the default bench command, then FETCH_SIZE and WRITE_SIZE in separate --pmc passes
-# (they do not fit in one pass on gfx950) over a shorter run of the same configuration.
-# usage (on the GPU box): bash tools/gpu/profile.sh      -> gpurun_out/prof/
+# rocprofv3 evidence for the headline bench (MI355X_MICROARCH.md HBM recipe): a kernel-trace +
+# stats run of the headline leg of the default bench command (pipelined C2 commits from host
+# memory; the HBM-resident leg, the C3/C4 lines, the CPU sample and the one-prepare host leg are
+# switched off so every traced launch is a headline launch), and FETCH_SIZE / WRITE_SIZE in
+# separate --pmc passes (they do not fit in one pass on gfx950) over a shorter run of the same
+# configuration (same chunk size, so the same launch shape).  One mode per call:
+#   bash tools/gpu/profile.sh kt|fetch|write      -> gpurun_out/prof/<mode>/
+# (rocprofv3 has written its CSVs when the profiled python exits; a crash after that, in process
+# teardown, leaves them complete and is reported, not hidden.)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
+MODE=${1:-kt}
 OUT=$R/gpurun_out/prof
-rm -rf "$OUT"; mkdir -p "$OUT"
+mkdir -p "$OUT"; rm -rf "$OUT/$MODE"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 "$R/bench.py" --cpu-sample 0 --host-prepares 0 \
-    > "$OUT/bench_kt.log" 2>&1 || { echo KT_FAIL; tail -20 "$OUT/bench_kt.log"; exit 1; }
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 "$R/bench.py" --cpu-sample 0 --host-prepares 0 \
-    --steps 1 --warmup 0 --transfers 20000000 > "$OUT/fetch.log" 2>&1 || { echo FETCH_FAIL; tail -20 "$OUT/fetch.log"; exit 1; }
-timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 "$R/bench.py" --cpu-sample 0 --host-prepares 0 \
-    --steps 1 --warmup 0 --transfers 20000000 > "$OUT/write.log" 2>&1 || { echo WRITE_FAIL; tail -20 "$OUT/write.log"; exit 1; }
-find "$OUT" -name "*.csv" | sort
-tail -1 "$OUT/bench_kt.log" | cut -c1-300
+LEG="--cpu-sample 0 --host-prepares 0 --device-steps 0 --secondary 0"
+case $MODE in
+  kt) timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 "$R/bench.py" $LEG \
+        > "$OUT/bench_kt.log" 2>&1; rc=$? ;;
+  fetch|write) C=FETCH_SIZE; [ "$MODE" = write ] && C=WRITE_SIZE
+      timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/bench.py" $LEG \
+        --steps 1 --warmup 0 --transfers 20000000 > "$OUT/$MODE.log" 2>&1; rc=$? ;;
+esac
+echo "rc=$rc"
+find "$OUT/$MODE" -name "*.csv" | sort
+exit $rc
