@@ -71,8 +71,21 @@ typedef struct tbgpu_route_plan {
  * timestamp_must_be_zero, :643, before reading any state: answered here, never routed).
  * Synchronous (the plan is needed on the host for the collectives). */
 int tbgpu_route_plan_build(tbgpu_t* engine, uint32_t n_batches, const uint64_t* timestamps,
-                           const uint32_t* batch_lens, const void* events_dev, void* send_events_dev,
-                           uint32_t* slot_dev, tbgpu_route_plan* plan);
+                           const uint32_t* batch_lens, const void* events_dev, const uint8_t* skip_dev,
+                           void* send_events_dev, uint32_t* slot_dev, tbgpu_route_plan* plan);
+/* skip_dev (nullable, one byte per event): non-zero = a dependent event of a split dirty pass,
+ * committed by the pass's sequencer instead: not routed, slot 0xFFFFFFFE (its amount still counts
+ * in S). */
+
+/* Dependency classes of this rank's share of a dirty pass (dep_dev, one byte per event, synchronous):
+ * 1 linked-chain member, 2 post/void, 4 balancing, 8 touches an account with a limit flag, 16
+ * touches one of the n_marked accounts (host array of {lo, hi} ids sorted by hi then lo: the
+ * accounts the pass's balancing events touch, state_machine.zig:826-846). */
+/* home(id) of n {lo, hi} ids held in device memory (out_dev: one byte each).  Synchronous. */
+int tbgpu_route_homes(tbgpu_t* engine, const uint64_t* ids_dev, uint64_t n, uint32_t world, uint8_t* out_dev);
+
+int tbgpu_route_dependents(tbgpu_t* engine, uint32_t n_batches, const uint32_t* batch_lens, const void* events_dev,
+                           const uint64_t* marked_ids, uint32_t n_marked, uint8_t* dep_dev);
 
 /* Commit `n` routed events (this home's share of a clean pass, in global order, each carrying its
  * execute timestamp); codes_dev[i] = result code of event i.  `cert` = TBGPU_CERT_*.  `ts_max` =

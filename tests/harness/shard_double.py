@@ -35,7 +35,39 @@ class OracleShard:
         self.device = torch.device("cpu")
         self.o = OracleEngine(1 << 12, 1 << 14)
 
-    def plan(self, timestamps, lens, events):
+    def dependents(self, lens, events, marked):
+        """tb_route_dependents restated: 1 chain member, 2 post/void, 4 balancing, 8 limit-flag
+        account, 16 an account a balancing event of the pass touches."""
+        ev = events.numpy().reshape(-1).view(TRANSFER_DTYPE)
+        n = len(ev)
+        dep = np.zeros(n, dtype=np.uint8)
+        if n == 0:
+            return torch.from_numpy(dep)
+        fl = ev["flags"].astype(np.int64)
+        linked = (fl & 1) != 0
+        first = np.zeros(n, dtype=bool)
+        first[np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)] = True
+        prev_linked = np.zeros(n, dtype=bool)
+        prev_linked[1:] = linked[:-1]
+        prev_linked &= ~first
+        dep |= np.where(linked | prev_linked, 1, 0).astype(np.uint8)
+        dep |= np.where((fl & 12) != 0, 2, 0).astype(np.uint8)
+        dep |= np.where((fl & 48) != 0, 4, 0).astype(np.uint8)
+        mk = {(int(lo), int(hi)) for lo, hi in np.asarray(marked, dtype=np.uint64).reshape(-1, 2)}
+        for side in ("debit_account_id", "credit_account_id"):
+            ids = np.stack([ev[side + "_lo"], ev[side + "_hi"]], axis=1)
+            recs, found = self.o.fetch_accounts(ids)
+            lim = ((recs["flags"] & _LIMITS) != 0) & found.astype(bool)
+            dep |= np.where(lim, 8, 0).astype(np.uint8)
+            if mk:
+                hit = np.array([(int(a), int(b)) in mk for a, b in ids], dtype=bool)
+                dep |= np.where(hit, 16, 0).astype(np.uint8)
+        return torch.from_numpy(dep)
+
+    def homes(self, ids):
+        return torch.from_numpy(homes_of(ids.numpy().view(np.uint64).reshape(-1, 2), self.world).astype(np.uint8))
+
+    def plan(self, timestamps, lens, events, skip=None):
         ev = events.numpy().reshape(-1).view(TRANSFER_DTYPE)
         n = len(ev)
         homes = homes_of(np.stack([ev["id_lo"], ev["id_hi"]], axis=1), self.world)
@@ -54,15 +86,17 @@ class OracleShard:
         for t, L in zip(timestamps, lens):
             ts[o:o + L] = int(t) - L + 1 + np.arange(L, dtype=np.uint64)
             o += L
-        local = ev["timestamp"] != 0  # timestamp_must_be_zero: answered here, never routed
-        homes = np.where(local, self.world, homes)
+        skipped = skip.numpy().astype(bool) if skip is not None else np.zeros(n, dtype=bool)
+        local = (ev["timestamp"] != 0) & ~skipped  # timestamp_must_be_zero: answered here, never routed
+        homes = np.where(local | skipped, self.world, homes)
         order = np.argsort(homes, kind="stable")
         slots = np.empty(n, dtype=np.int64)
         slots[order] = np.arange(n)
         slots[local] = -1
+        slots[skipped] = -2  # SLOT_DEP: the sequencer commits it
         routed = ev.copy()
         routed["timestamp"] = ts
-        counts = np.bincount(homes[~local], minlength=self.world).tolist() if n else [0] * self.world
+        counts = np.bincount(homes[~(local | skipped)], minlength=self.world).tolist() if n else [0] * self.world
         S = 0
         for lo, hi in zip(ev["amount_lo"][~local], ev["amount_hi"][~local]):
             S = min(S + ((int(hi) << 64) | int(lo)), U128_MAX)

@@ -105,6 +105,7 @@ def run_rank(rank, world, port, kind, scenario_kw, max_prepares, result_path):
             if sm.commit_timestamp != oracle.commit_timestamp:
                 problems.append("commit_timestamp %d != %d" % (sm.commit_timestamp, oracle.commit_timestamp))
             verdict = {"ok": not problems, "problems": problems, "clean": sm.passes_clean, "dirty": sm.passes_dirty,
+                       "split": sm.passes_split, "demoted": int(torch.tensor([sm.demoted]).sum()),
                        "prepares": len(replies), "transfers": int(len(transfers))}
     except Exception:
         verdict = {"ok": False, "problems": [traceback.format_exc()]}

@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 def test_gpu_sharded_clean(tmp_path, seed):
     v = run_world(tmp_path, "gpu", 2, dict(seed=seed, n_accounts=64, n_transfer_batches=8, **CLEAN))
     assert v["ok"], v["problems"]
-    assert v["clean"] > 0 and v["dirty"] == 0
+    assert v["clean"] > 0 and v["dirty"] == 0 and v["split"] == 0
 
 
 def test_gpu_sharded_clean_large_batches(tmp_path):
@@ -28,7 +28,7 @@ def test_gpu_sharded_clean_large_batches(tmp_path):
 def test_gpu_sharded_mixed(tmp_path, seed):
     v = run_world(tmp_path, "gpu", 2, dict(seed=seed, n_accounts=64, n_transfer_batches=10))
     assert v["ok"], v["problems"]
-    assert v["dirty"] > 0
+    assert v["split"] > 0 and v["dirty"] == 0  # dependent subsequences sequenced, no whole-pass gather
 
 
 def test_gpu_sharded_interleaved(tmp_path):
@@ -36,9 +36,18 @@ def test_gpu_sharded_interleaved(tmp_path):
                                            p_pending=0.3, p_post_void=0.1, p_balancing=0.0, p_limit=0.0),
                   max_prepares=1)
     assert v["ok"], v["problems"]
-    assert v["clean"] > 0 and v["dirty"] > 0
+    assert v["clean"] > 0 and v["split"] > 0
 
 
 def test_gpu_sharded_three_ranks(tmp_path):
     v = run_world(tmp_path, "gpu", 3, dict(seed=12, n_accounts=64, n_transfer_batches=9, **CLEAN), max_prepares=3)
     assert v["ok"], v["problems"]
+
+
+def test_gpu_sharded_dependent_kinds(tmp_path):
+    # Split dirty passes with every dependency class and cross-rank duplicate ids (demotion), on the
+    # real kernels (tb_route_dependents, the skip-mask route plan, tb_route_homes).
+    v = run_world(tmp_path, "gpu", 2, dict(seed=31, n_accounts=24, n_transfer_batches=12, p_linked=0.25, p_limit=0.3,
+                                           p_balancing=0.1, p_pending=0.4, p_post_void=0.3, p_dup=0.15, id_space=400))
+    assert v["ok"], v["problems"]
+    assert v["split"] > 0 and v["demoted"] > 0

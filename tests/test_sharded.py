@@ -43,14 +43,14 @@ CLEAN = dict(p_limit=0.0, p_linked=0.0, p_pending=0.0, p_post_void=0.0, p_balanc
 def test_sharded_clean_passes(tmp_path, seed):
     v = run_world(tmp_path, "oracle", 2, dict(seed=seed, n_accounts=48, n_transfer_batches=8, **CLEAN))
     assert v["ok"], v["problems"]
-    assert v["clean"] > 0 and v["dirty"] == 0
+    assert v["clean"] > 0 and v["dirty"] == 0 and v["split"] == 0
 
 
 @pytest.mark.parametrize("seed", [3, 4])
 def test_sharded_mixed_passes(tmp_path, seed):
     v = run_world(tmp_path, "oracle", 2, dict(seed=seed, n_accounts=48, n_transfer_batches=10))
     assert v["ok"], v["problems"]
-    assert v["dirty"] > 0
+    assert v["split"] > 0 and v["dirty"] == 0  # dependent subsequences sequenced, no whole-pass gather
 
 
 def test_sharded_clean_then_dirty_interleaved(tmp_path):
@@ -60,7 +60,26 @@ def test_sharded_clean_then_dirty_interleaved(tmp_path):
                                               p_pending=0.3, p_post_void=0.1, p_balancing=0.0, p_limit=0.0),
                   max_prepares=1)
     assert v["ok"], v["problems"]
-    assert v["clean"] > 0 and v["dirty"] > 0
+    assert v["clean"] > 0 and v["split"] > 0
+
+
+@pytest.mark.parametrize("seed", [31, 32])
+def test_sharded_dependent_kinds(tmp_path, seed):
+    # Every dependency class in split passes: chains (with chain-breaking and open chains), limit
+    # accounts, balancing (its accounts marked pass-wide), two-phase in the same and later passes,
+    # duplicate ids across ranks (demoted to the sequencer), invalid events.
+    v = run_world(tmp_path, "oracle", 2, dict(seed=seed, n_accounts=24, n_transfer_batches=12, p_linked=0.25,
+                                              p_limit=0.3, p_balancing=0.1, p_pending=0.4, p_post_void=0.3,
+                                              p_dup=0.15, id_space=400))
+    assert v["ok"], v["problems"]
+    assert v["split"] > 0 and v["demoted"] > 0
+
+
+def test_sharded_three_ranks_split(tmp_path):
+    v = run_world(tmp_path, "oracle", 3, dict(seed=33, n_accounts=32, n_transfer_batches=9, p_linked=0.15,
+                                              p_post_void=0.2, p_pending=0.3), max_prepares=3)
+    assert v["ok"], v["problems"]
+    assert v["split"] > 0
 
 
 def test_sharded_near_overflow_balances(tmp_path):

@@ -137,8 +137,10 @@ SIGNATURES = [
     ("tbgpu_home", _U32, [_U64, _U64, _U32]),
     ("tbgpu_homes", None, [_P, _U64, _U32, _P]),
     ("tbgpu_route_init", ctypes.c_int, [_P, _U32, _U64]),
-    ("tbgpu_route_plan_build", ctypes.c_int, [_P, _U32, ctypes.POINTER(_U64), ctypes.POINTER(_U32), _P, _P, _P,
+    ("tbgpu_route_plan_build", ctypes.c_int, [_P, _U32, ctypes.POINTER(_U64), ctypes.POINTER(_U32), _P, _P, _P, _P,
                                               ctypes.POINTER(tbgpu_route_plan)]),
+    ("tbgpu_route_homes", ctypes.c_int, [_P, _P, _U64, _U32, _P]),
+    ("tbgpu_route_dependents", ctypes.c_int, [_P, _U32, ctypes.POINTER(_U32), _P, _P, _U32, _P]),
     ("tbgpu_commit_routed_async", ctypes.c_int, [_P, _U64, _P, _U64, _U32, _P]),
     ("tbgpu_commit_routed_owner_async", ctypes.c_int, [_P, _U64, _P, _U64, _U32, _P, _U32, _U32, _P, _U64, _P]),
     ("tbgpu_apply_owner_legs_async", ctypes.c_int, [_P, _P, _U64, _U32]),

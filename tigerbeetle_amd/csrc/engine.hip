@@ -1475,9 +1475,51 @@ static int route_meta(tbgpu* E, u32 nb, const u64* timestamps, const u32* lens, 
     return TBGPU_STATUS_OK;
 }
 
+extern "C" int tbgpu_route_homes(tbgpu_t* E, const uint64_t* ids_dev, uint64_t n, uint32_t world, uint8_t* out_dev) {
+    HIPCK(hipSetDevice(E->device));
+    if (world == 0 || world > ROUTE_WORLD_MAX) return fail(TBGPU_STATUS_INVALID, "world %u out of range", world);
+    if (n == 0) return TBGPU_STATUS_OK;
+    hipLaunchKernelGGL(tb_route_homes, dim3((u32)((n + 255) / 256)), dim3(256), 0, E->stream, ids_dev, n, world, out_dev);
+    HIPCK(hipGetLastError());
+    HIPCK(hipStreamSynchronize(E->stream));
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_route_dependents(tbgpu_t* E, uint32_t nb, const uint32_t* lens, const void* events_dev,
+                                      const uint64_t* marked_ids, uint32_t n_marked, uint8_t* dep_dev) {
+    HIPCK(hipSetDevice(E->device));
+    if (!E->r_home) return fail(TBGPU_STATUS_INVALID, "tbgpu_route_init was not called");
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    u64 n = 0;
+    int st = route_meta(E, nb, nullptr, lens, &n);
+    if (st) return st;
+    if (n == 0) return TBGPU_STATUS_OK;
+    u64* d_marked = nullptr;
+    if (n_marked) {
+        HIPCK(hipMalloc(&d_marked, (u64)n_marked * 16));
+        HIPCK(hipMemcpyAsync(d_marked, marked_ids, (u64)n_marked * 16, hipMemcpyHostToDevice, E->stream));
+    }
+    RouteArgs A{};
+    A.events = (const u8*)events_dev;
+    A.n = (u32)n;
+    A.nb = nb;
+    A.batch_off = E->r_meta;
+    A.T = E->T;
+    hipLaunchKernelGGL(tb_route_dependents, dim3((u32)((n + ROUTE_THREADS - 1) / ROUTE_THREADS)), dim3(ROUTE_THREADS), 0,
+                       E->stream, A, d_marked, n_marked, dep_dev);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(E->stream);
+    if (d_marked) (void)hipFree(d_marked);
+    if (e != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "route dependents: %s", hipGetErrorString(e));
+    return TBGPU_STATUS_OK;
+}
+
 extern "C" int tbgpu_route_plan_build(tbgpu_t* E, uint32_t nb, const uint64_t* timestamps, const uint32_t* lens,
-                                      const void* events_dev, void* send_events_dev, uint32_t* slot_dev,
-                                      tbgpu_route_plan* plan) {
+                                      const void* events_dev, const uint8_t* skip_dev, void* send_events_dev,
+                                      uint32_t* slot_dev, tbgpu_route_plan* plan) {
     HIPCK(hipSetDevice(E->device));
     if (!E->r_home) return fail(TBGPU_STATUS_INVALID, "tbgpu_route_init was not called");
     if (E->pending) {
@@ -1504,6 +1546,7 @@ extern "C" int tbgpu_route_plan_build(tbgpu_t* E, uint32_t nb, const uint64_t* t
     A.block_base = E->r_block_counts + E->r_block_cap;
     A.words = E->r_words;
     A.T = E->T;
+    A.skip = skip_dev;
     if (n > 0) {
         hipLaunchKernelGGL(tb_route_classify, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, E->stream, A);
         HIPCK(hipGetLastError());

@@ -23,6 +23,8 @@
 #define ROUTE_WORLD_MAX 64
 #define ROUTE_LOCAL 0xFF
 #define SLOT_LOCAL 0xFFFFFFFFu
+#define ROUTE_DEP 0xFE       // home of a skipped (dependent) event
+#define SLOT_DEP 0xFFFFFFFEu  // its slot
 
 enum : u32 { ROUTE_DIRTY_FLAGS = 1, ROUTE_DIRTY_LIMIT = 2 };
 
@@ -45,6 +47,7 @@ struct RouteArgs {
     u32* block_base;       // [nblocks][world] send-buffer position of those events
     u64* words;            // [2*SUM_SHARDS] S shards, [2*SUM_SHARDS] HUGE, [+1] dirty bits, [+2..] counts
     Tables T;
+    const u8* skip;        // [n] or null: non-zero = a dependent event the sequencer commits (not routed)
 };
 #define RW_HUGE (2 * SUM_SHARDS)
 #define RW_DIRTY (2 * SUM_SHARDS + 1)
@@ -67,7 +70,10 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_route_classify(RouteArgs A) 
         const u64* w = (const u64*)(A.events + e * 128);
         const u64 id_lo = w[0], id_hi = w[1];
         const u16 flags = *(const u16*)(A.events + e * 128 + 118);
-        if (w[15] != 0) {
+        if (A.skip && A.skip[e]) {
+            A.home[e] = ROUTE_DEP;  // committed in order by the pass's sequencer
+            amount = tb_u128(w[6], w[7]);
+        } else if (w[15] != 0) {
             A.home[e] = ROUTE_LOCAL;  // timestamp_must_be_zero, answered at the source
         } else {
             const u32 h = tb_home(id_lo, id_hi, A.world);
@@ -163,8 +169,8 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_route_scatter(RouteArgs A, u
     }
     __syncthreads();
     if (!live) return;
-    if (h == ROUTE_LOCAL) {
-        slot[e] = SLOT_LOCAL;
+    if (h == ROUTE_LOCAL || h == ROUTE_DEP) {
+        slot[e] = h == ROUTE_LOCAL ? SLOT_LOCAL : SLOT_DEP;
         return;
     }
     u32 pos = A.block_base[(u64)blockIdx.x * A.world + h] + before;
@@ -177,6 +183,54 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_route_scatter(RouteArgs A, u
     u32x4* dst = (u32x4*)(send_events + (u64)pos * 128);
 #pragma unroll
     for (u32 k = 0; k < 8; k++) dst[k] = *(const u32x4*)(stage + tb_stage_off(threadIdx.x, k));
+}
+
+// Dependency classes of every event of a dirty pass (its source's share), for the split commit
+// (tigerbeetle_amd/sharded.py): a dependent event is committed in global order by the pass's
+// sequencer, the others are routed to their homes as in a clean pass.  Bits: 1 member of a linked
+// chain (execute :628-692: an event is in a chain if it or its predecessor in the prepare is
+// linked), 2 post / void (:907-1014), 4 balancing (:826-846), 8 an account with a limit flag
+// (tigerbeetle.zig:31-39), 16 an account a balancing event of the pass touches (`marked`: sorted
+// {lo, hi} pairs, by hi then lo).
+__device__ static inline bool tb_route_marked(const u64* marked, u32 n, u64 lo, u64 hi) {
+    u32 a = 0, b = n;
+    while (a < b) {
+        const u32 m = (a + b) >> 1;
+        const u64 mh = marked[2 * m + 1], ml = marked[2 * m];
+        if (mh < hi || (mh == hi && ml < lo)) a = m + 1; else b = m;
+    }
+    return a < n && marked[2 * a] == lo && marked[2 * a + 1] == hi;
+}
+
+__global__ __launch_bounds__(ROUTE_THREADS) void tb_route_dependents(RouteArgs A, const u64* marked, u32 n_marked,
+                                                                    u8* dep) {
+    const u64 e = (u64)blockIdx.x * ROUTE_THREADS + threadIdx.x;
+    if (e >= A.n) return;
+    const u64* w = (const u64*)(A.events + e * 128);
+    const u16 flags = *(const u16*)(A.events + e * 128 + 118);
+    const u32 b = tb_batch_search(A.batch_off, 0, A.nb, e);
+    u8 d = 0;
+    if ((flags & TF_LINKED) || (e > A.batch_off[b] && (*(const u16*)(A.events + (e - 1) * 128 + 118) & TF_LINKED))) d |= 1;
+    if (flags & (TF_POST | TF_VOID)) d |= 2;
+    if (flags & (TF_BAL_DEBIT | TF_BAL_CREDIT)) d |= 4;
+    if (A.T.g->limit_accounts != 0) {
+        const u32 dr = tb_account_find(A.T, w[2], w[3]);
+        const u32 cr = tb_account_find(A.T, w[4], w[5]);
+        if ((dr != TB_NOT_FOUND && (A.T.acct_hot[dr].flags & AF_LIMITS)) ||
+            (cr != TB_NOT_FOUND && (A.T.acct_hot[cr].flags & AF_LIMITS))) {
+            d |= 8;
+        }
+    }
+    if (n_marked && (tb_route_marked(marked, n_marked, w[2], w[3]) || tb_route_marked(marked, n_marked, w[4], w[5]))) {
+        d |= 16;
+    }
+    dep[e] = d;
+}
+
+// home(id) of n {lo, hi} ids (device buffers): where a key a dependent event reads lives.
+__global__ void tb_route_homes(const u64* ids, u64 n, u32 world, u8* out) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (u8)tb_home(ids[2 * i], ids[2 * i + 1], world);
 }
 
 // Per-prepare sparse replies from the codes that came back (in send order): ascending index,

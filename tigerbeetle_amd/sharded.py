@@ -78,6 +78,15 @@ class PassResult:
         return PassResult(torch.from_numpy(results.view(np.int32)).to(device), torch.from_numpy(rb).to(device), offsets)
 
 
+DEMOTED = 0xFE  # a routed event its home did not commit: a dependent event reads its id
+
+
+def _key64(ids):
+    """A 64-bit key of {lo, hi} int64 pairs for set membership (a collision only demotes an extra
+    event to the sequencer, which is always exact)."""
+    return ids[:, 0] ^ (ids[:, 1] * -7046029254386353131)  # 0x9E3779B97F4A7C15 as int64
+
+
 def _stream_sync(device):
     """Wait for torch's current stream on `device` (its work, and the RCCL collectives it waits
     on), not the whole device: a copy of the next pass on another stream keeps running."""
@@ -116,7 +125,7 @@ class GpuShard:
         self._scratch = None
 
     # -- clean pass ------------------------------------------------------------------------
-    def plan(self, timestamps, lens, events):
+    def plan(self, timestamps, lens, events, skip=None):
         import ctypes
         n = events.shape[0]
         nb = len(lens)
@@ -126,8 +135,9 @@ class GpuShard:
         ts = (ctypes.c_uint64 * max(nb, 1))(*[int(t) for t in timestamps])
         ls = (ctypes.c_uint32 * max(nb, 1))(*[int(x) for x in lens])
         _stream_sync(self.device)
-        _lib.check(self.lib.tbgpu_route_plan_build(self.engine.h, nb, ts, ls, events.data_ptr(), send_events.data_ptr(),
-                                                   slots.data_ptr(), ctypes.byref(p)))
+        _lib.check(self.lib.tbgpu_route_plan_build(self.engine.h, nb, ts, ls, events.data_ptr(),
+                                                   skip.data_ptr() if skip is not None else None,
+                                                   send_events.data_ptr(), slots.data_ptr(), ctypes.byref(p)))
         plan = RoutePlan([int(p.send_counts[i]) for i in range(self.world)], _u128(p.sum_lo, p.sum_hi),
                          _u128(p.bound_lo, p.bound_hi), int(p.dirty))
         return plan, send_events[:sum(plan.counts)], slots[:n]
@@ -141,6 +151,29 @@ class GpuShard:
                                                           codes.data_ptr()))
             self.engine.sync()
         return codes[:m]
+
+    def dependents(self, lens, events, marked):
+        """Per-event dependency classes of a dirty pass (tbgpu_route_dependents): uint8 tensor."""
+        import ctypes
+        n, nb = events.shape[0], len(lens)
+        dep = torch.zeros(max(n, 1), dtype=torch.uint8, device=self.device)
+        if n:
+            ls = (ctypes.c_uint32 * nb)(*[int(x) for x in lens])
+            marked = np.ascontiguousarray(marked, dtype=np.uint64).reshape(-1, 2)
+            _stream_sync(self.device)
+            _lib.check(self.lib.tbgpu_route_dependents(self.engine.h, nb, ls, events.data_ptr(),
+                                                       marked.ctypes.data if len(marked) else None, len(marked),
+                                                       dep.data_ptr()))
+        return dep[:n]
+
+    def homes(self, ids):
+        """home(id) of an int64 [m, 2] {lo, hi} tensor on the device: uint8 tensor."""
+        out = torch.empty(max(ids.shape[0], 1), dtype=torch.uint8, device=self.device)
+        if ids.shape[0]:
+            ids = ids.contiguous()
+            _stream_sync(self.device)
+            _lib.check(self.lib.tbgpu_route_homes(self.engine.h, ids.data_ptr(), ids.shape[0], self.world, out.data_ptr()))
+        return out[:ids.shape[0]]
 
     def commit_routed_owner(self, events, ts_max, cert, rank):
         """The home's routed commit with owner-partitioned balances: result codes, plus the legs of
@@ -264,6 +297,8 @@ class ShardedStateMachine:
         self.commit_timestamp = 0
         self.passes_clean = 0
         self.passes_dirty = 0
+        self.passes_split = 0
+        self.demoted = 0  # routed events their homes demoted to the sequencer (split passes)
 
     # -- collectives helpers -----------------------------------------------------------------
     def _all_gather_i64(self, values):
@@ -375,9 +410,12 @@ class ShardedStateMachine:
         self._check_order(g[:, :4])
         dirty = int(np.bitwise_or.reduce(g[:, 4]))
         total = sum(int(g[r, 5 + k]) << (32 * (k % 4)) for r in range(self.world) for k in range(8))
-        if dirty or total >= U128 - 1:  # a saturated S (maxInt) is a lower bound: no certificate
+        if total >= U128 - 1:  # a saturated S (maxInt) is a lower bound: no certificate
             self.passes_dirty += 1
             return self._commit_dirty(operation, timestamps, lens, events)
+        if dirty:
+            self.passes_split += 1
+            return self._commit_split(timestamps, lens, events, _lib.CERT_U64 if total < U64 else _lib.CERT_U128)
         self.passes_clean += 1
         cert = _lib.CERT_U64 if total < U64 else _lib.CERT_U128
         return self._commit_routed(plan, send_events, slots, lens, g[:, 13 + self.rank], cert)
@@ -457,6 +495,185 @@ class ShardedStateMachine:
         pad[:len(arr)] = arr.view(np.int64)
         g = self._all_gather_i64(list(pad))
         return [g[r, :int(counts[r])].view(np.uint64) for r in range(self.world)]
+
+    # -- split dirty pass: clean events routed, the dependent subsequence sequenced --------------
+    def _commit_split(self, timestamps, lens, events, cert):
+        """A dirty pass under the global certificate.  Every rank classifies its events
+        (tbgpu_route_dependents: chain members, post/void, balancing, limit-flag accounts, accounts
+        a balancing event of the pass touches); the others are routed and committed by their homes
+        exactly as in a clean pass, except that a home DEMOTES a routed event whose id a dependent
+        event reads (its own id, or a post/void's pending id, sent to the home as probes), since its
+        existence must follow the global order.  The dependent and demoted events — the pass's
+        dependent subsequence — are committed by rank 0 in global order, runs of consecutive events
+        of a prepare as sub-prepares with their original execute timestamps (chains never leave a
+        run), with the referenced transfers and balances prefetched from their homes and owners
+        (state_machine.zig:345-506).  Nothing a dependent event reads is written by a routed one:
+        ids are demoted, constrained balances are only touched by dependent events, free balances
+        feed no check under the certificate."""
+        W, rank, dev = self.world, self.rank, self.b.device
+        n = events.shape[0]
+        # 1. accounts touched by balancing events anywhere in the pass (all-gather of their ids).
+        fl = events[:, 118].to(torch.int32) | (events[:, 119].to(torch.int32) << 8) if n else \
+            torch.zeros(0, dtype=torch.int32, device=dev)
+        bal = (fl & 48) != 0
+        mine = torch.cat([events[bal][:, 16:32], events[bal][:, 32:48]]).cpu().numpy().view(np.uint64).reshape(-1, 2) \
+            if n else np.zeros((0, 2), dtype=np.uint64)
+        sizes = self._all_gather_i64([len(mine)])[:, 0]
+        marked = np.concatenate(self._gather_all_np(mine.reshape(-1), sizes * 2)).reshape(-1, 2) if sizes.sum() else \
+            np.zeros((0, 2), dtype=np.uint64)
+        if len(marked):
+            marked = np.unique(marked, axis=0)
+            marked = marked[np.lexsort((marked[:, 0], marked[:, 1]))]
+        dep = self.b.dependents(lens, events, marked)
+        depm = dep != 0
+        # 2. the routed part: plan without the dependent events; counts for the all-to-alls.
+        plan, send_events, slots = self.b.plan(timestamps, lens, events, skip=dep)
+        counts = self._all_gather_i64(plan.counts)
+        recv_counts = counts[:, rank]
+        # 3. probes: the ids (and pending ids) dependent events read, to their homes.
+        dev_ev = events[depm]
+        pv = ((fl[depm] & 12) != 0) if n else fl
+        keys = torch.cat([dev_ev[:, 0:16], dev_ev[pv][:, 64:80]]).contiguous().view(torch.int64).reshape(-1, 2)
+        kh = self.b.homes(keys).to(torch.int64)
+        order = torch.argsort(kh, stable=True)
+        keys = keys[order]
+        kcount = torch.bincount(kh, minlength=W).cpu().tolist() if keys.shape[0] else [0] * W
+        kin = self._a2a(torch.tensor(kcount, dtype=torch.int64), [1] * W, [1] * W)
+        probe_keys = self._a2a(keys, kcount, [int(x) for x in kin.cpu().tolist()])
+        # 4. homes: demote, commit the rest, legs to the owners, codes back.
+        recv = self._a2a(send_events, plan.counts, recv_counts)
+        rid = recv[:, 0:16].contiguous().view(torch.int64).reshape(-1, 2)
+        demote = torch.isin(_key64(rid), _key64(probe_keys)) if (rid.shape[0] and probe_keys.shape[0]) else \
+            torch.zeros(rid.shape[0], dtype=torch.bool, device=dev)
+        keep = ~demote
+        codes_kept, legs, leg_counts = self.b.commit_routed_owner(recv[keep], self._pass_ts_max, cert, rank)
+        legs_in_counts = self._a2a(torch.tensor(leg_counts, dtype=torch.int64), [1] * W, [1] * W)
+        self.b.apply_owner_legs(self._a2a(legs, leg_counts, [int(x) for x in legs_in_counts.cpu().tolist()]), cert)
+        codes = torch.full((rid.shape[0],), DEMOTED, dtype=torch.uint8, device=dev)
+        codes[keep] = codes_kept.to(dev)
+        codes_back = self._a2a(codes, recv_counts, plan.counts)
+        # 5. dense codes at the source; the sequenced events: dependent ones and demoted ones.
+        sl = slots.to(torch.int64)
+        dense = torch.full((n,), 3, dtype=torch.uint8, device=dev)  # SLOT_LOCAL: timestamp_must_be_zero
+        routed = sl >= 0
+        dense[routed] = codes_back.to(dev)[sl[routed]] if codes_back.shape[0] else dense[routed]
+        demoted = routed & (dense == DEMOTED)
+        self.demoted += int(demoted.sum().item())
+        seq = depm | demoted
+        seq_idx = torch.nonzero(seq).reshape(-1)
+        # 6. the sequencer: every rank's sequenced events to rank 0, in global order.
+        seq_codes = self._sequence(timestamps, lens, events, seq_idx)
+        if seq_idx.shape[0]:
+            dense[seq_idx] = seq_codes.to(dev)
+        ident = torch.arange(max(n, 1), dtype=torch.int32, device=dev)[:n]
+        return self.b.replies(lens, ident, dense)
+
+    def _sequence(self, timestamps, lens, events, seq_idx):
+        """Commit the sequenced events of every rank on rank 0 (scratch engine, prefetch / write-back
+        as in _commit_dirty); returns this rank's codes for its seq_idx events."""
+        W, root = self.world, self.rank == 0
+        starts = np.concatenate([[0], np.cumsum(lens, dtype=np.int64)])
+        pos = seq_idx.cpu().numpy().astype(np.int64)
+        k = np.searchsorted(starts, pos, side="right") - 1  # prepare of each sequenced event
+        ts = np.asarray(timestamps, dtype=np.int64)
+        Ls = np.asarray(lens, dtype=np.int64)
+        ets = (ts[k] - Ls[k] + 1 + (pos - starts[k])) if len(pos) else np.zeros(0, dtype=np.int64)  # execute ts (:645)
+        # Runs of consecutive events of one prepare become sub-prepares (chains stay whole).
+        brk = np.ones(len(pos), dtype=bool)
+        if len(pos) > 1:
+            brk[1:] = (k[1:] != k[:-1]) | (pos[1:] != pos[:-1] + 1)
+        meta = np.stack([brk.astype(np.int64), ets], axis=1).reshape(-1)
+        recs = events[seq_idx].cpu().numpy() if len(pos) else np.zeros((0, 128), dtype=np.uint8)
+        meta_parts = self._gather_np(meta, np.int64)
+        rec_parts = self._gather_np(recs.reshape(-1), np.uint8)
+        counts = self._all_gather_i64([len(pos)])[:, 0]
+        if root:
+            allm = np.concatenate(meta_parts).reshape(-1, 2) if counts.sum() else np.zeros((0, 2), dtype=np.int64)
+            allr = np.concatenate(rec_parts).reshape(-1, 128) if counts.sum() else np.zeros((0, 128), dtype=np.uint8)
+            # A run also breaks between ranks (a rank's first event starts a sub-prepare).
+            firsts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+            for f, c in zip(firsts, counts):
+                if c:
+                    allm[f, 0] = 1
+            run_start = np.nonzero(allm[:, 0])[0] if len(allm) else np.zeros(0, dtype=np.int64)
+            run_end = np.concatenate([run_start[1:], [len(allm)]]) if len(run_start) else run_start
+            bodies = [allr[a:b].tobytes() for a, b in zip(run_start, run_end)]
+            stamps = [int(allm[b - 1, 1]) for b in run_end]
+            ev = allr.reshape(-1).view(TRANSFER_DTYPE) if len(allr) else np.zeros(0, dtype=TRANSFER_DTYPE)
+            codes = np.zeros(len(allm), dtype=np.uint8)
+        else:
+            ev, bodies, stamps = None, None, None
+        replies = self._scratch_commit(ev, bodies, stamps)
+        if root:
+            for (a, _b), r in zip(zip(run_start, run_end), replies):
+                p = np.frombuffer(r, dtype=np.uint32).reshape(-1, 2)
+                codes[a + p[:, 0].astype(np.int64)] = p[:, 1]
+        # Codes back to their ranks (rank r's events are rank r's slice, in order).
+        send_counts = [int(c) for c in counts] if root else [0] * W
+        out = self._a2a(torch.from_numpy(codes if root else np.zeros(0, dtype=np.uint8)), send_counts,
+                        [int(counts[self.rank]) if r == 0 else 0 for r in range(W)])
+        return out
+
+    def _scratch_commit(self, ev, bodies, stamps):
+        """Collective: rank 0 commits `bodies` (prepares at `stamps`) on a scratch engine loaded with
+        the transfers and accounts they read, then writes the effects back to their homes and
+        owners.  Returns the replies on rank 0 (None elsewhere)."""
+        W, root = self.world, self.rank == 0
+        if root:
+            pv = (ev["flags"] & (TransferFlags.post_pending_transfer | TransferFlags.void_pending_transfer)) != 0
+            tids = _unique_ids(np.concatenate([_ids(ev["id_lo"], ev["id_hi"]),
+                                               _ids(ev["pending_id_lo"][pv], ev["pending_id_hi"][pv])]))
+        tids = self._bcast_np(tids if root else None, np.uint64).reshape(-1, 2)
+        homes = self._homes(tids)
+        mine = np.nonzero(homes == self.rank)[0]
+        recs, state = self.b.fetch_transfers(tids[mine])
+        recs_parts = self._gather_np(recs, TRANSFER_DTYPE)
+        state_parts = self._gather_np(state, np.uint8)
+        if root:
+            fetched = np.zeros(len(tids), dtype=TRANSFER_DTYPE)
+            fstate = np.zeros(len(tids), dtype=np.uint8)
+            for r in range(W):
+                idx = np.nonzero(homes == r)[0]
+                fetched[idx] = recs_parts[r]
+                fstate[idx] = state_parts[r]
+            present = fstate != 0
+            aids = _unique_ids(np.concatenate([
+                _ids(ev["debit_account_id_lo"], ev["debit_account_id_hi"]),
+                _ids(ev["credit_account_id_lo"], ev["credit_account_id_hi"]),
+                _ids(fetched["debit_account_id_lo"][present], fetched["debit_account_id_hi"][present]),
+                _ids(fetched["credit_account_id_lo"][present], fetched["credit_account_id_hi"][present])]))
+        aids = self._bcast_np(aids if root else None, np.uint64).reshape(-1, 2)
+        accts, afound = self.b.fetch_accounts(aids)
+        accts = self._sum_balances(accts)
+        afound = afound.astype(bool)
+        replies = None
+        if root:
+            scratch = self.b.scratch(int(afound.sum()) + 1, int(present.sum()) + len(ev) + 1)
+            scratch.upsert_accounts(accts[afound])
+            scratch.upsert_transfers(fetched[present], fstate[present])
+            replies = scratch.commit_batches(int(Operation.create_transfers), stamps, bodies) if bodies else []
+            after, astate = scratch.fetch_transfers(tids)
+            changed = (astate != 0) & (astate != fstate)
+            wb_t, wb_s = after[changed], astate[changed]
+            acc_after, _ = scratch.fetch_accounts(aids[afound])
+            local_ts = scratch.commit_timestamp
+        else:
+            local_ts = 0
+        wb_t = self._bcast_np(wb_t if root else None, TRANSFER_DTYPE)
+        wb_s = self._bcast_np(wb_s if root else None, np.uint8)
+        if len(wb_t):
+            h = self._homes(_ids(wb_t["id_lo"], wb_t["id_hi"]))
+            sel = h == self.rank
+            self.b.upsert_transfers(wb_t[sel], wb_s[sel])
+        acc_after = self._bcast_np(acc_after if root else None, ACCOUNT_DTYPE)
+        wb_a = acc_after.copy()
+        not_mine = ~self._owner_mask(wb_a)
+        for name in _BAL_FIELDS:
+            wb_a[name + "_lo"][not_mine] = 0
+            wb_a[name + "_hi"][not_mine] = 0
+        self.b.upsert_accounts(wb_a)
+        self._finish(local_ts)
+        return replies
 
     # -- dirty pass: prefetch on rank 0, commit on a scratch engine, write back -----------------
     def _commit_dirty(self, operation, timestamps, lens, events):
