@@ -72,7 +72,10 @@ def parse():
     p.add_argument("--same-device", action="store_true", help="rehearsal: every rank on cuda:0")
     p.add_argument("--host-prepares", type=int, default=600,
                    help="prepares committed one per tbgpu_commit call from host memory (the replica's call; 0: skip)")
-    return p.parse_args()
+    args = p.parse_args()
+    if args.steps < 1:
+        p.error("--steps must be at least 1 (the headline is measured over the timed steps)")
+    return args
 
 
 def batches(total, batch):

@@ -38,7 +38,8 @@
 #define FLOW_NB_MAX 4096        // prepares per pass the planner handles (LDS prefix)
 #define FLOW_SENT 0xFFFFFFFFu   // empty pair slot
 
-enum : u32 { FW_NUNITS = 0, FW_QTAIL = 1, FW_SEQ = 2, FW_BNO = 3, FW_BUND = 4, FW_BDEC = 5, FW_WORDS = 8 };
+enum : u32 { FW_NUNITS = 0, FW_QTAIL = 1, FW_SEQ = 2, FW_BNO = 3, FW_BUND = 4, FW_BDEC = 5,  // 5, 6, 7
+             FW_QHEAD = 8, FW_DONE = 9, FW_WORDS = FLOW_WORDS };
 enum : u32 {
     UF_ID_SINGLE = 1,  // the unit is the only dependent event of the pass whose id has its key
     UF_ID_UNIQUE = 2,  // ... or the others sharing the key (a 31-bit hash) name different ids
@@ -319,7 +320,7 @@ __device__ static inline u32 fl_run_run(const PassArgs& P, const FlowArgs& F, co
         more = j == FLOW_RUN_STEP;
         q += FLOW_RUN_STEP;
     }
-    T.acct_bal[r] = B;
+    rp_store<true>(&T.acct_bal[r], B);
     if (n_ok) atomicAdd((unsigned long long*)&T.g->transfer_count, (unsigned long long)n_ok);
     if (last_ok_pe != TB_NOT_FOUND) {  // commit_timestamp: the run's last ok event is its latest
         u32 lo = P.b0, hi = P.b1;
@@ -671,7 +672,6 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     __shared__ u32 s_wcnt[FLOW_THREADS / 64][256];
     __shared__ u8 s_code[BATCH_LDS];
     __shared__ u32 s_list[FLOW_THREADS];
-    __shared__ u32 s_qhead, s_qtail, s_nunits, s_done;
     __shared__ u64 s_tsmax[FLOW_THREADS / 64];
 
     Globals* g = P.T.g;
@@ -916,11 +916,10 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
         fl_grid_sync(g, G, gen, F);
         if (fl_stalled(g)) return;
     }
-    if (blockIdx.x != 0) return;
-
-    // ---- run (workgroup 0) ---------------------------------------------------------------------
+    // ---- run --------------------------------------------------------------------------------------
     u64 tsmax = 0;
     if (sequential) {
+        if (blockIdx.x != 0) return;
         Replay R;
         R.T = P.T;
         R.undo = seq_undo;
@@ -938,14 +937,14 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
             }
         }
     } else {
-        if (tid == 0) {
-            s_qhead = 0;
-            s_qtail = F.words[FW_QTAIL];
-            s_nunits = F.words[FW_NUNITS];
-            s_done = 0;
-        }
-        __syncthreads();
-        const u32 nunits = s_nunits;
+        // Every lane of every workgroup (all co-resident: cooperative launch) takes tickets from one
+        // queue in global memory; the state units share is read with agent-scope loads and each
+        // unit's writes drain before its successors are released, so lanes on different CUs see
+        // exactly what lanes of one workgroup would.
+        const u32 nunits = *(volatile u32*)&F.words[FW_NUNITS];
+        u32* qhead = &F.words[FW_QHEAD];
+        u32* qtail = &F.words[FW_QTAIL];
+        u32* done = &F.words[FW_DONE];
         Replay R;
         R.T = P.T;
         R.failed = false;
@@ -967,18 +966,18 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
                 u = next;
                 next = FLOW_SENT;
             } else {
-                if (ticket == FLOW_SENT) ticket = atomicAdd(&s_qhead, 1u);
+                if (ticket == FLOW_SENT) ticket = atomicAdd(qhead, 1u);
                 const u32 item = ticket < nunits
                                      ? __hip_atomic_load(&F.queue[ticket], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                      : 0;
                 if (item == 0) {
-                    if (*(volatile u32*)&s_done >= nunits) break;
+                    if (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nunits) break;
                     if (spins++ == 0) w0 = fl_now();
                     if (spins % 256 == 0 && (fl_expired(F, w0) || fl_stalled(g))) {
                         tb_panic(g, PANIC_FLOW_STALL);
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(2);
                     continue;
                 }
                 spins = 0;
@@ -1015,21 +1014,30 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
                     if (next == FLOW_SENT) {
                         next = s;
                     } else {
-                        const u32 pos = atomicAdd(&s_qtail, 1u);
+                        const u32 pos = atomicAdd(qtail, 1u);
                         __hip_atomic_store(&F.queue[pos], s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                 }
             }
-            atomicAdd(&s_done, ran);
+            atomicAdd(done, ran);
         }
         if (runs) {
             atomicAdd((unsigned long long*)&g->flow_runs, (unsigned long long)runs);
             atomicAdd((unsigned long long*)&g->flow_run_units, (unsigned long long)run_units);
         }
-        if (tid == 0) {
+        if (blockIdx.x == 0 && tid == 0) {
             atomicAdd(&g->flow_passes, 1u);
             atomicAdd((unsigned long long*)&g->flow_units, (unsigned long long)nunits);
         }
+        // Every workgroup's commit timestamp, then workgroup 0 closes the pass after all writes.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        u64 m = tsmax;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) m = max(m, (u64)__shfl_xor((unsigned long long)m, off));
+        if ((tid & 63) == 0 && m) atomicMax((unsigned long long*)&g->commit_timestamp, (unsigned long long)m);
+        tsmax = 0;
+        fl_grid_sync(g, G, gen, F);
+        if (blockIdx.x != 0) return;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     u64 m = tsmax;

@@ -75,6 +75,33 @@ __device__ static inline u8 rp_load_posted(const Tables& T, u32 pos) {
     const u32 w = __hip_atomic_load((const u32*)(T.xposted + (pos & ~3u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return (u8)(w >> (8 * (pos & 3)));
 }
+// Flow-path stores: lanes of other workgroups (other XCDs, whose L2s are not coherent with this
+// one) read what a unit writes once its successors are released, so every word is stored
+// write-through at agent scope (sc1) and drained before the release (fl_run_unit).
+template <bool FLOW, typename R>
+__device__ static inline void rp_store(R* p, const R& v) {
+    static_assert(sizeof(R) % 8 == 0, "8-byte words");
+    if (!FLOW) {
+        *p = v;
+        return;
+    }
+    const u64* s = (const u64*)&v;
+#pragma unroll
+    for (u32 k = 0; k < sizeof(R) / 8; k++) {
+        __hip_atomic_store((u64*)p + k, s[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+template <bool FLOW>
+__device__ static inline void rp_store_posted(const Tables& T, u32 pos, u8 v) {
+    if (!FLOW) {
+        T.xposted[pos] = v;
+        return;
+    }
+    u32* w = (u32*)(T.xposted + (pos & ~3u));
+    const u32 sh = 8 * (pos & 3);
+    __hip_atomic_fetch_and(w, ~(0xFFu << sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v) __hip_atomic_fetch_or(w, (u32)v << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Flow path: is this account's balance an ordering resource (k_flow.h)?  Must agree with the
 // planner's choice.
@@ -144,7 +171,7 @@ __device__ static inline void rp_scope_close(Replay& R, bool persist) {
                 tb_account_tombstone(R.T, e.slot);
                 R.T.g->account_count--;
                 break;
-            case UNDO_BALANCE_UPDATE: R.T.acct_bal[e.slot] = e.before; break;
+            case UNDO_BALANCE_UPDATE: rp_store<FLOW>(&R.T.acct_bal[e.slot], e.before); break;
             case UNDO_FREE_DELTA: {
                 AccountBal neg;
                 neg.debits_pending = (u128)0 - e.before.debits_pending;
@@ -159,7 +186,7 @@ __device__ static inline void rp_scope_close(Replay& R, bool persist) {
                 if (FLOW) atomicAdd((unsigned long long*)&R.T.g->transfer_count, ~0ULL);
                 else R.T.g->transfer_count--;
                 break;
-            case UNDO_POSTED: R.T.xposted[e.slot] = POSTED_NONE; break;
+            case UNDO_POSTED: rp_store_posted<FLOW>(R.T, e.slot, POSTED_NONE); break;
             }
         }
     }
@@ -201,13 +228,13 @@ __device__ static inline void rp_balance_update(Replay& R, u32 slot, const Accou
         return;
     }
     rp_push(R, UNDO_BALANCE_UPDATE, slot, &before);
-    R.T.acct_bal[slot] = next;
+    rp_store<FLOW>(&R.T.acct_bal[slot], next);
 }
 
 // Insert a transfer record at the event's own log position (after an exact find said "absent").
 template <bool FLOW>
 __device__ static inline void rp_transfer_insert(Replay& R, const Transfer& t, u32 log_pos) {
-    R.T.xlog[log_pos] = t;
+    rp_store<FLOW>(&R.T.xlog[log_pos], t);
     if (FLOW) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record before its index entry
     const u32 entry = tb_transfer_claim_new(R.T, tb_lo(t.id), tb_hi(t.id), log_pos);
     if (entry == TB_NOT_FOUND) {
@@ -291,7 +318,7 @@ __device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t, u32 l
     if (R.failed) return R_OK;
 
     rp_push(R, UNDO_POSTED, pslot, nullptr);
-    T.xposted[pslot] = (f & TF_POST) ? POSTED_POSTED : POSTED_VOIDED;
+    rp_store_posted<FLOW>(T, pslot, (f & TF_POST) ? POSTED_POSTED : POSTED_VOIDED);
 
     bool dfree, cfree;
     const AccountBal dr0 = rp_balance_load<FLOW>(R, drs, &dfree);
@@ -406,7 +433,7 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u3
     Transfer t2 = t;
     t2.amount = amount;
     if (hint) {  // revive kernel 1's entry (a single event: no scope to undo)
-        R.T.xlog[log_pos] = t2;
+        rp_store<FLOW>(&R.T.xlog[log_pos], t2);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record before its index entry
         atomicAnd((unsigned long long*)&R.T.xidx[hint->entry], ~(unsigned long long)XI_TOMB);
         atomicAdd((unsigned long long*)&R.T.g->transfer_count, 1ULL);

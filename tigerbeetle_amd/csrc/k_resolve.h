@@ -248,7 +248,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         s_failed = 0;
         if (blockIdx.x == 0) {  // the replay kernel's per-pass counters (k_flow.h)
             T.g->flow_barrier = 0;
-            if (P.flow_words) for (u32 k = 0; k < 8; k++) P.flow_words[k] = 0;
+            if (P.flow_words) for (u32 k = 0; k < FLOW_WORDS; k++) P.flow_words[k] = 0;
         }
     }
     // a. classify.  Each thread owns events tid + k*RESOLVE_THREADS; their scratch words are loaded

@@ -28,6 +28,7 @@ enum : u32 {
 };
 
 #define SUM_SHARDS 64
+#define FLOW_WORDS 16  // tb_flow's per-pass counters (k_flow.h FW_*)
 #define VALIDATE_THREADS 256
 #define RESOLVE_THREADS 1024
 #define REPLAY_THREADS 256
@@ -82,7 +83,7 @@ struct PassArgs {
     u64* leg_w;            // [2 * pass events] the same leg words grouped by bucket per prepare
 
     u32* leg_off;          // [prepares of the pass][leg_buckets + 1] bucket starts in the prepare's legs
-    u32* flow_words;       // tb_flow's per-pass counters (k_flow.h), zeroed by tb_resolve (or null)
+    u32* flow_words;       // tb_flow's per-pass counters (k_flow.h, FLOW_WORDS), zeroed by tb_resolve (or null)
 };
 
 enum : u32 { CERT_EXT_U128 = 1, CERT_EXT_U64 = 2 };
