@@ -59,6 +59,11 @@ extern "C" {
 /* Ordered fallback on one lane in batch order (tb_replay) instead of the parallel flow path
  * (tb_flow); identical results, for cross-checking the two. */
 #define TBGPU_CONFIG_SEQUENTIAL_FALLBACK (1u << 1)
+/* Limit checks (tb_flow bounds): sweep whatever the first scan round leaves undecided in event
+ * order (TBGPU_CONFIG_SWEEP_EARLY), or never sweep (TBGPU_CONFIG_SWEEP_OFF: rounds until they
+ * converge, else the ordered run).  Identical results; for cross-checking the paths. */
+#define TBGPU_CONFIG_SWEEP_EARLY (1u << 2)
+#define TBGPU_CONFIG_SWEEP_OFF (1u << 3)
 
 typedef struct tbgpu_config {
     uint64_t accounts_max;      /* HBM account table capacity (the groove's object count) */
@@ -189,6 +194,10 @@ typedef struct tbgpu_stats {
     uint64_t bounds_rounds;      /* scan rounds they took (and those of abandoned attempts) */
     uint64_t bounds_skipped;     /* dependent passes with an event the bounds do not cover */
     uint64_t bounds_abandoned;   /* passes whose bounds did not converge (ordered run instead) */
+    uint64_t bounds_swept;       /* units decided by the in-order sweep after the rounds */
+    double sweep_ms;             /* tb_flow wall time of the sweeps (one wave) */
+    double sweep_loop_ms;        /* ... of it resolving windows in order */
+    double sweep_wait_ms;        /* ... of it waiting for memory between windows */
 } tbgpu_stats;
 
 int tbgpu_get_stats(tbgpu_t* engine, tbgpu_stats* stats);

@@ -19,11 +19,15 @@ pytestmark = pytest.mark.gpu
     ("c3", 2_000, 100_000, 16),   # hotter: long per-account segments, many exceeds_credits
     ("c4", 20_000, 200_000, 8),
     ("c4", 1_000, 100_000, 16),   # dense two-phase traffic per account
+    # BASELINE sizes of accounts, 2M transfers, the bench's 64-prepare passes (4 passes)
+    ("c3", 1_000_000, 2_000_000, 64),
+    ("c4", 1_000_000, 2_000_000, 64),
 ])
-def test_config_parity(config, n_accounts, n_transfers, pass_batches, gpu_engine_factory):
+def test_config_parity(config, n_accounts, n_transfers, pass_batches, gpu_engine_factory, bounds_sweep="auto"):
     batch = 8190
     engine = gpu_engine_factory(accounts_max=n_accounts, transfers_max=n_transfers,
-                                pass_events_max=pass_batches * batch, pass_batches_max=pass_batches)
+                                pass_events_max=pass_batches * batch, pass_batches_max=pass_batches,
+                                bounds_sweep=bounds_sweep)
     accts, xfers = generate(engine, config, n_accounts, n_transfers, seed=7)
     a_lens = batches(n_accounts, batch)
     a_ts, t = timestamps(a_lens, 10**12)
@@ -44,4 +48,18 @@ def test_config_parity(config, n_accounts, n_transfers, pass_batches, gpu_engine
         assert st["flow_units"] + st["bounds_units"] > 0
         assert sum(len(r) for r in expected) > 0
     if config == "c3":  # limit checks only: decided by the bounds scans (k_flow.h fl_bounds)
-        assert engine.stats()["bounds_passes"] > 0
+        st = engine.stats()
+        if bounds_sweep == "off":
+            assert st["bounds_swept"] == 0
+        else:  # every pass decided by rounds + sweep, never the ordered run
+            assert st["bounds_passes"] == st["flow_passes"] and st["bounds_abandoned"] == 0
+        if bounds_sweep == "early":
+            assert st["bounds_swept"] > 0
+
+
+@pytest.mark.parametrize("bounds_sweep", ["early", "off"])
+@pytest.mark.parametrize("n_accounts,n_transfers,pass_batches", [(20_000, 200_000, 8), (2_000, 100_000, 16)])
+def test_c3_sweep_modes(bounds_sweep, n_accounts, n_transfers, pass_batches, gpu_engine_factory):
+    """The limit checks decided by the in-order sweep right after the first scan round, and by
+    rounds alone (else the ordered run): the same bytes as the oracle either way."""
+    test_config_parity("c3", n_accounts, n_transfers, pass_batches, gpu_engine_factory, bounds_sweep)

@@ -15,6 +15,8 @@ STATUS_OK, STATUS_INVALID, STATUS_PANIC, STATUS_DEVICE = 0, 1, 2, 3
 
 CONFIG_PROFILE = 1
 CONFIG_SEQUENTIAL_FALLBACK = 2
+CONFIG_SWEEP_EARLY = 4
+CONFIG_SWEEP_OFF = 8
 
 
 class tbgpu_config(ctypes.Structure):
@@ -61,6 +63,10 @@ class tbgpu_stats(ctypes.Structure):
         ("bounds_rounds", ctypes.c_uint64),
         ("bounds_skipped", ctypes.c_uint64),
         ("bounds_abandoned", ctypes.c_uint64),
+        ("bounds_swept", ctypes.c_uint64),
+        ("sweep_ms", ctypes.c_double),
+        ("sweep_loop_ms", ctypes.c_double),
+        ("sweep_wait_ms", ctypes.c_double),
     ]
 
 

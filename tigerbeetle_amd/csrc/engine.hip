@@ -403,7 +403,16 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         INIT_CK(hipMalloc(&F.b_amt, pe * 8 * FLOW_RMAX));
         INIT_CK(hipMalloc(&F.b_meta, pe * 4 * FLOW_RMAX));
         INIT_CK(hipMalloc(&F.b_blk, (u64)F.grid * 5 * 8));
+        INIT_CK(hipMalloc(&F.b_qd, pe * 4));
+        INIT_CK(hipMalloc(&F.b_qc, pe * 4));
+        INIT_CK(hipMalloc(&F.b_head, pe * 4 * FLOW_RMAX));
+        INIT_CK(hipMalloc(&F.b_xy, pe * 16 * FLOW_RMAX));
+        INIT_CK(hipMalloc(&F.b_ex, pe * 16 * FLOW_RMAX));
+        INIT_CK(hipMalloc(&F.b_rec, pe * sizeof(SweepRec)));
         F.bounds_rounds_max = FLOW_BOUNDS_ROUNDS_MAX;
+        F.sweep_min = (config->flags & TBGPU_CONFIG_SWEEP_OFF) ? 0u
+                      : (config->flags & TBGPU_CONFIG_SWEEP_EARLY) ? 0xFFFFFFFFu
+                                                                   : FLOW_SWEEP_MIN;
     }
     INIT_CK(hipMalloc(&E->staging, pe * 128));
     INIT_CK(hipMalloc(&E->results, pe * 8));
@@ -454,7 +463,8 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->r_block_counts, E->r_words, E->r_meta, E->leg_ev, E->leg_w, E->leg_off,
                     E->F.f_pe, E->F.f_batch, E->F.f_len, E->F.need, E->F.nsucc, E->F.queue, E->F.uflags, E->F.nacct, E->F.rpos, E->F.succ,
                     E->F.run, E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo,
-                    E->F.b_st, E->F.b_vd, E->F.b_vc, E->F.b_amt, E->F.b_meta, E->F.b_blk};
+                    E->F.b_st, E->F.b_vd, E->F.b_vc, E->F.b_amt, E->F.b_meta, E->F.b_blk,
+                    E->F.b_qd, E->F.b_qc, E->F.b_head, E->F.b_xy, E->F.b_ex, E->F.b_rec};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int k = 0; k < PIPE_SLOTS; k++) {
         tbgpu::PipeSlot& S = E->pipe[k];
@@ -1260,6 +1270,10 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     s->bounds_rounds = g.bounds_rounds;
     s->bounds_skipped = g.bounds_skipped;
     s->bounds_abandoned = g.bounds_abandoned;
+    s->bounds_swept = g.bounds_swept;
+    s->sweep_ms = E->wall_khz ? (double)g.sweep_ticks[0] / E->wall_khz : 0.0;
+    s->sweep_loop_ms = E->wall_khz ? (double)g.sweep_ticks[1] / E->wall_khz : 0.0;
+    s->sweep_wait_ms = E->wall_khz ? (double)g.sweep_ticks[2] / E->wall_khz : 0.0;
     return TBGPU_STATUS_OK;
 }
 

@@ -82,6 +82,14 @@ struct FlowArgs {
     u32* b_meta;    // [FLOW_RMAX * pass events] unit << 3 | BT_* | BT_CR
     u64* b_blk;     // [grid * 5] per workgroup: segment-start flag, then 4 sums
     u32 bounds_rounds_max;
+    // The in-order sweep that decides what the rounds leave undecided (fl_sweep).
+    u32 sweep_min;  // rounds continue while one decides at least this many units
+    u32* b_qd;      // [pass events] per undecided unit: sorted position of its debit leg (or FLOW_SENT)
+    u32* b_qc;      // [pass events] ... of its credit leg
+    u32* b_head;    // [FLOW_RMAX * pass events] per position of an undecided unit: its segment's first
+    u64* b_xy;      // [2 * FLOW_RMAX * pass events] per such position: X, Y with the decided units before it
+    u64* b_ex;      // [2 * FLOW_RMAX * pass events] per segment head: X, Y added by swept ok units
+    struct SweepRec* b_rec;  // [pass events] per undecided unit in event order: what the sweep reads
 };
 
 // Every wait of the kernel is bounded by wall time (s_memrealtime) since the wait began.
@@ -391,6 +399,8 @@ __device__ static inline void fl_finish(const PassArgs& P, u8* s_code, u32* s_wa
 // dependent unit, or one that does not converge within bounds_rounds_max, takes the ordered run
 // with nothing changed.
 #define FLOW_BOUNDS_ROUNDS_MAX 4096
+// A scan round costs about as much as sweeping this many units in order (fl_sweep).
+#define FLOW_SWEEP_MIN 512
 enum : u8 { BS_UNK = 0, BS_OK = 1, BS_FAIL_CREDITS = 2, BS_FAIL_DEBITS = 3, BS_FAIL_STATIC = 4 };
 enum : u8 { BV_UNK = 0, BV_PASS = 1, BV_FAIL = 2 };
 enum : u32 { BT_NONE = 0, BT_X = 1, BT_Y = 2, BT_CR = 4 };  // X: checked side (any field); Y: other side, posted
@@ -457,6 +467,249 @@ __device__ static inline void fl_bound_contrib(const FlowArgs& F, u32 q, u64 (&v
     v[1] = x ? mx : 0;
     v[2] = y ? mn : 0;
     v[3] = y ? mx : 0;
+}
+
+// ---- the in-order sweep of what the rounds leave undecided --------------------------------------
+// When a round decides few units (a limit account whose balance hovers at its limit: every check
+// depends on the one before), the rest is decided exactly, in event order, by one wave:
+//  1. every workgroup: a last segmented scan over the positions with the decided units only records,
+//     per position of an undecided unit, X and Y of its account with every decided ok unit before it
+//     (the pre-pass balance plus the min sums) and its segment's first position (a segmented sum of
+//     q at the segment starts); then the undecided units are listed in event order;
+//  2. wave 0 of workgroup 0 walks the list 64 units at a time: a lane holds one unit's legs, adds
+//     what the swept ok units before its window added to its segments (b_ex, by segment head), and
+//     the window is resolved lane by lane in order, each verdict broadcast to the later lanes that
+//     share an account; the ok units' legs go to b_ex for the later windows.
+// X, Y are exact at every step: a position's earlier units are decided (in the min sums), or swept
+// (b_ex, and the window's broadcasts), or later in event order than the unit being swept.
+__device__ static inline void fl_record_contrib(const FlowArgs& F, const u32* K, u32 q, u64 (&v)[4], u32& f) {
+    const u32 meta = F.b_meta[q];
+    const u64 a = F.b_amt[q];
+    const bool ok = F.b_st[meta >> 3] == BS_OK;
+    f = q == 0 || K[q] != K[q - 1];
+    v[0] = ok && (meta & BT_X) ? a : 0;
+    v[1] = f ? q : 0;  // summed over a segment: its first position
+    v[2] = ok && (meta & BT_Y) ? a : 0;
+    v[3] = 0;
+}
+
+// Wave-uniform u64 read of lane j / write of lane j (j uniform).
+__device__ static inline u64 fl_rl64(u64 v, u32 j) {
+    return ((u64)(u32)__builtin_amdgcn_readlane((u32)(v >> 32), j) << 32) | (u32)__builtin_amdgcn_readlane((u32)v, j);
+}
+
+struct SweepRec {  // one undecided unit, in event order (fl_sweep)
+    u32 f, hd, hc;     // unit; segment heads of its debit / credit leg (FLOW_SENT: no leg)
+    u32 t;             // BT_* of the debit leg | ... of the credit leg << 4 | vd << 8 | vc << 12
+    u64 a;             // amount
+    u64 xd, yd, xc, yc;  // X, Y at each leg with the decided units before it
+    u64 pad;
+};
+
+__device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32 ndep, u32 NA, u32& gen,
+                                       u64 (*s_wv)[4], u32* s_wf, u32* s_cnt) {
+    Globals* g = P.T.g;
+    const Tables& T = P.T;
+    const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid;
+    const u32 lane = tid & 63, wave = tid >> 6;
+    const u32* K = F.keys[0];
+
+    // 1a. Units: no legs yet.
+    for (u32 f = blockIdx.x * NT + tid; f < ndep; f += G * NT) {
+        F.b_qd[f] = FLOW_SENT;
+        F.b_qc[f] = FLOW_SENT;
+    }
+    // 1b. The record scan (statuses are fixed from here to the sweep).
+    const u32 tile = ((NA + G - 1) / G + NT - 1) / NT * NT;
+    const u32 t0 = min(NA, blockIdx.x * tile), t1 = min(NA, t0 + tile);
+    u64 carry[4] = {0, 0, 0, 0};
+    u32 any_start = 0;
+    for (u32 c0 = t0; c0 < t1; c0 += NT) {
+        const u32 q = c0 + tid;
+        u64 v[4] = {0, 0, 0, 0};
+        u32 f = 0;
+        if (q < t1) fl_record_contrib(F, K, q, v, f);
+        any_start |= __syncthreads_or(f);
+        fl_seg_scan4(v, f, carry, s_wv, s_wf);
+    }
+    if (tid == 0) {
+        F.b_blk[5 * blockIdx.x] = any_start;
+#pragma unroll
+        for (u32 k = 0; k < 4; k++) F.b_blk[5 * blockIdx.x + 1 + k] = carry[k];
+    }
+    fl_grid_sync(g, G, gen, F);
+    if (fl_stalled(g)) return false;
+    u64 cin[4] = {0, 0, 0, 0};
+    for (int b = (int)blockIdx.x - 1; b >= 0; b--) {
+#pragma unroll
+        for (u32 k = 0; k < 4; k++) cin[k] += F.b_blk[5 * b + 1 + k];
+        if (F.b_blk[5 * b]) break;
+    }
+    for (u32 c0 = t0; c0 < t1; c0 += NT) {
+        const u32 q = c0 + tid;
+        u64 v[4] = {0, 0, 0, 0}, own[4] = {0, 0, 0, 0};
+        u32 f = 0;
+        if (q < t1) {
+            fl_record_contrib(F, K, q, v, f);
+#pragma unroll
+            for (u32 k = 0; k < 4; k++) own[k] = v[k];
+        }
+        fl_seg_scan4(v, f, cin, s_wv, s_wf);
+        if (q >= t1) continue;
+        const u32 meta = F.b_meta[q];
+        const u32 u = meta >> 3;
+        if (!(meta & (BT_X | BT_Y)) || F.b_st[u] != BS_UNK) continue;
+        const u32 r = K[q];
+        const AccountBal& B = T.acct_bal[r];
+        const bool dlim = T.acct_hot[r].flags & AF_DEBITS_MUST_NOT_EXCEED_CREDITS;
+        const u64 xb = dlim ? tb_lo(B.debits_pending) + tb_lo(B.debits_posted)
+                            : tb_lo(B.credits_pending) + tb_lo(B.credits_posted);
+        const u64 yb = dlim ? tb_lo(B.credits_posted) : tb_lo(B.debits_posted);
+        const u32 head = (u32)v[1];
+        F.b_xy[2 * q] = xb + v[0] - own[0];
+        F.b_xy[2 * q + 1] = yb + v[2] - own[2];
+        F.b_head[q] = head;
+        F.b_ex[2 * head] = 0;
+        F.b_ex[2 * head + 1] = 0;
+        if (F.run[q].dr == r) F.b_qd[u] = q;
+        else F.b_qc[u] = q;
+    }
+    // 1c. The undecided units in event order: per workgroup tile of units its count, then its offset.
+    const u32 ut = ((ndep + G - 1) / G + NT - 1) / NT * NT;
+    const u32 u0 = min(ndep, blockIdx.x * ut), u1 = min(ndep, u0 + ut);
+    u32 cnt = 0;
+    for (u32 c0 = u0; c0 < u1; c0 += NT) {
+        const u32 f = c0 + tid;
+        cnt += __syncthreads_count(f < u1 && F.f_len[f] && F.b_st[f] == BS_UNK);
+    }
+    if (tid == 0) F.b_blk[5 * blockIdx.x] = cnt;
+    fl_grid_sync(g, G, gen, F);
+    if (fl_stalled(g)) return false;
+    u32 off = 0, nu = 0;
+    for (u32 b = 0; b < G; b++) {
+        const u32 c = (u32)F.b_blk[5 * b];
+        off += b < blockIdx.x ? c : 0;
+        nu += c;
+    }
+    for (u32 c0 = u0; c0 < u1; c0 += NT) {
+        const u32 f = c0 + tid;
+        const bool pred = f < u1 && F.f_len[f] && F.b_st[f] == BS_UNK;
+        const u64 m = __ballot(pred);
+        if (lane == 0) s_wf[wave] = __popcll(m);
+        __syncthreads();
+        u32 before = 0, total = 0;
+        for (u32 w = 0; w < NT / 64; w++) {
+            before += w < wave ? s_wf[w] : 0;
+            total += s_wf[w];
+        }
+        if (pred) {  // the unit's sweep record (its legs with the decided units before them)
+            SweepRec x = {};
+            x.f = f;
+            x.hd = x.hc = FLOW_SENT;
+            const u32 qd = F.b_qd[f], qc = F.b_qc[f];
+            u32 td = BT_NONE, tc = BT_NONE;
+            if (qd != FLOW_SENT) {
+                x.hd = F.b_head[qd];
+                td = F.b_meta[qd] & (BT_X | BT_Y);
+                x.xd = F.b_xy[2 * qd];
+                x.yd = F.b_xy[2 * qd + 1];
+                x.a = F.b_amt[qd];
+            }
+            if (qc != FLOW_SENT) {
+                x.hc = F.b_head[qc];
+                tc = F.b_meta[qc] & (BT_X | BT_Y);
+                x.xc = F.b_xy[2 * qc];
+                x.yc = F.b_xy[2 * qc + 1];
+                x.a = F.b_amt[qc];
+            }
+            x.t = td | (tc << 4) | ((u32)F.b_vd[f] << 8) | ((u32)F.b_vc[f] << 12);
+            F.b_rec[off + before + __popcll(m & ((1ULL << lane) - 1))] = x;
+        }
+        off += total;
+        __syncthreads();
+    }
+    fl_grid_sync(g, G, gen, F);
+    if (fl_stalled(g)) return false;
+
+    // 2. The sweep: wave 0 of workgroup 0, 64 units a window; the next window's records load while
+    // this one is resolved.  A lane holds one unit: its legs' X, Y with the decided units and the
+    // swept ok units of earlier windows (b_ex); the window is resolved in lane order, each ok unit
+    // adding its legs to the later lanes that share an account (branch-free: one wave, so every
+    // instruction's latency is on the critical path).
+    if (blockIdx.x == 0 && wave == 0) {
+        SweepRec nx = {};
+        if (lane < nu) nx = F.b_rec[lane];
+        u64 t_all = fl_now(), t_wait = 0, t_loop = 0;
+        for (u32 w0 = 0; w0 < nu; w0 += 64) {
+            const SweepRec x = nx;
+            const u64 ta = fl_now();
+            const u32 nv = min(64u, nu - w0);
+            const bool valid = lane < nv;
+            u64 xd = x.xd, yd = x.yd, xc = x.xc, yc = x.yc;
+            if (valid && x.hd != FLOW_SENT) {
+                xd += fl_ld64(&F.b_ex[2 * x.hd]);
+                yd += fl_ld64(&F.b_ex[2 * x.hd + 1]);
+            }
+            if (valid && x.hc != FLOW_SENT) {
+                xc += fl_ld64(&F.b_ex[2 * x.hc]);
+                yc += fl_ld64(&F.b_ex[2 * x.hc + 1]);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const u64 tb = fl_now();
+            if (w0 + 64 + lane < nu) nx = F.b_rec[w0 + 64 + lane];
+            const u32 vd = (x.t >> 8) & 15, vc = (x.t >> 12) & 15;
+            const u64 a = x.a;
+            // Per lane: X, Y thresholds as "fails if X + a > Y": with the unknown sides' checks
+            // folded in once (a known verdict never changes), only the sums move.
+            const bool dknown = vd != BV_UNK, cknown = vc != BV_UNK;
+            const bool dfix = vd == BV_FAIL, cfix = vc == BV_FAIL;
+            for (u32 j = 0; j < nv; j++) {
+                const u32 jhd = __builtin_amdgcn_readlane(x.hd, j), jhc = __builtin_amdgcn_readlane(x.hc, j);
+                const u32 jt = __builtin_amdgcn_readlane(x.t, j);
+                const u64 ja = fl_rl64(a, j);
+                const bool dfail = dknown ? dfix : xd + a > yd;
+                const bool cfail = cknown ? cfix : xc + a > yc;
+                const u64 okj = __builtin_amdgcn_readlane((u32)(!dfail & !cfail), j);
+                const u64 m = lane > j && okj ? ja : 0;  // lane j's legs, if it is ok, for the later lanes
+                const u64 dxd = jt & BT_X ? m : 0, dyd = jt & BT_Y ? m : 0;
+                const u64 dxc = (jt >> 4) & BT_X ? m : 0, dyc = (jt >> 4) & BT_Y ? m : 0;
+                const bool dd = x.hd == jhd, dc = x.hd == jhc, cd = x.hc == jhd, cc = x.hc == jhc;
+                xd += (dd ? dxd : 0) + (dc ? dxc : 0);
+                yd += (dd ? dyd : 0) + (dc ? dyc : 0);
+                xc += (cd ? dxd : 0) + (cc ? dxc : 0);
+                yc += (cd ? dyd : 0) + (cc ? dyc : 0);
+            }
+            const u64 tc = fl_now();
+            t_loop += tc - tb;
+            if (valid) {
+                const bool dfail = dknown ? dfix : xd + a > yd;
+                const bool cfail = !dfail && (cknown ? cfix : xc + a > yc);
+                F.b_st[x.f] = dfail ? BS_FAIL_CREDITS : cfail ? BS_FAIL_DEBITS : BS_OK;
+                if (!dfail && !cfail) {
+                    const u32 td = x.t & 15, tc2 = (x.t >> 4) & 15;
+                    if (x.hd != FLOW_SENT) {
+                        if (td & BT_X) tb_atomic_add_lo_noret(&F.b_ex[2 * x.hd], a);
+                        if (td & BT_Y) tb_atomic_add_lo_noret(&F.b_ex[2 * x.hd + 1], a);
+                    }
+                    if (x.hc != FLOW_SENT) {
+                        if (tc2 & BT_X) tb_atomic_add_lo_noret(&F.b_ex[2 * x.hc], a);
+                        if (tc2 & BT_Y) tb_atomic_add_lo_noret(&F.b_ex[2 * x.hc + 1], a);
+                    }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next window reads b_ex
+            t_wait += (tb - ta) + (fl_now() - tc);
+        }
+        if (lane == 0) {
+            F.words[FW_BUND] = 0;
+            atomicAdd((unsigned long long*)&g->bounds_swept, (unsigned long long)nu);
+            atomicAdd((unsigned long long*)&g->sweep_ticks[0], (unsigned long long)(fl_now() - t_all));
+            atomicAdd((unsigned long long*)&g->sweep_ticks[1], (unsigned long long)t_loop);
+            atomicAdd((unsigned long long*)&g->sweep_ticks[2], (unsigned long long)t_wait);
+        }
+    }
+    fl_grid_sync(g, G, gen, F);
+    return !fl_stalled(g);
 }
 
 // Returns true when every unit was decided and applied (the ordered run is skipped).
@@ -620,7 +873,15 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
         fl_grid_sync(g, G, gen, F);
         if (fl_stalled(g)) return false;
         converged = *(volatile u32*)&F.words[FW_BUND] == 0;
-        if (!converged && *(volatile u32*)dec == 0) break;  // no progress (not expected)
+        // A round that decides few units costs more than sweeping them in order.
+        if (!converged && *(volatile u32*)dec < max(1u, F.sweep_min)) {
+            rounds++;
+            break;
+        }
+    }
+    if (!converged && F.sweep_min) {
+        converged = fl_sweep(P, F, ndep, NA, gen, s_wv, s_wf, s_cnt);
+        if (fl_stalled(g)) return false;
     }
     if (!converged) {
         if (blockIdx.x == 0 && tid == 0) {

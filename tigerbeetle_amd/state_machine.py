@@ -35,6 +35,9 @@ class Options:
     device: int = 0
     profile: bool = False
     sequential_fallback: bool = False  # ordered fallback on one lane (tb_replay) instead of tb_flow
+    # Limit checks: "auto" (scan rounds while they decide enough, then the in-order sweep), "early"
+    # (sweep after the first round) or "off" (rounds only, else the ordered run).  Identical results.
+    bounds_sweep: str = "auto"
     # Reference cache options are accepted for interface parity; the HBM tables hold every object.
     lsm_forest_node_count: int = 0
     cache_entries_accounts: int = 0
@@ -52,7 +55,9 @@ class Engine:
         cfg = _lib.tbgpu_config(options.accounts_max, options.transfers_max, options.pass_events_max,
                                 options.pass_batches_max, options.device,
                                 (_lib.CONFIG_PROFILE if options.profile else 0)
-                                | (_lib.CONFIG_SEQUENTIAL_FALLBACK if options.sequential_fallback else 0))
+                                | (_lib.CONFIG_SEQUENTIAL_FALLBACK if options.sequential_fallback else 0)
+                                | {"auto": 0, "early": _lib.CONFIG_SWEEP_EARLY,
+                                   "off": _lib.CONFIG_SWEEP_OFF}[options.bounds_sweep])
         h = ctypes.c_void_p()
         _lib.check(self.lib.tbgpu_init(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
