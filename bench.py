@@ -70,6 +70,8 @@ def parse():
     p.add_argument("--profile", type=int, default=1, help="time kernels with HIP events (roofline)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (rehearsal on one GPU)")
     p.add_argument("--same-device", action="store_true", help="rehearsal: every rank on cuda:0")
+    p.add_argument("--access-mix", type=int, default=1,
+                   help="time the validate kernel's access pattern without its logic (roofline.access_mix)")
     p.add_argument("--host-prepares", type=int, default=600,
                    help="prepares committed one per tbgpu_commit call from host memory (the replica's call; 0: skip)")
     args = p.parse_args()
@@ -314,8 +316,9 @@ def cpu_model():
     return "nproc %d" % os.cpu_count()
 
 
-def load_pmc(kernel):
-    """HBM traffic per launch of `kernel` from a committed rocprofv3 PMC summary, if any."""
+def load_pmc(kernel, transfers_per_launch=None):
+    """HBM traffic of `kernel` from the newest committed rocprofv3 PMC summary that has it, per
+    transfer and scaled to this run's launch size (the summary records its own)."""
     prof_dir = os.path.join(ROOT, "profiles")
     if not os.path.isdir(prof_dir):
         return None
@@ -326,10 +329,22 @@ def load_pmc(kernel):
             except (OSError, ValueError):
                 continue
             k = d.get("kernels", {}).get(kernel)
-            if k and "hbm_bytes_per_launch_raw" in k:
-                return {"bytes_per_launch": round(k["hbm_bytes_per_launch_raw"]), "source": "profiles/" + name,
-                        "counters": "FETCH_SIZE + WRITE_SIZE (raw; FETCH_SIZE may read up to 2x low on gfx950)",
-                        "bytes_per_launch_fetch_x2": round(k["hbm_bytes_per_launch"])}
+            if not (k and "hbm_bytes_per_launch_raw" in k):
+                continue
+            tpl = d.get("transfers_per_launch")
+            out = {"source": "profiles/" + name,
+                   "counters": "FETCH_SIZE + WRITE_SIZE (raw; FETCH_SIZE may read up to 2x low on gfx950)"}
+            if tpl:
+                raw, x2 = k["hbm_bytes_per_launch_raw"] / tpl, k["hbm_bytes_per_launch"] / tpl
+                out.update({"bytes_per_transfer": round(raw, 1), "bytes_per_transfer_fetch_x2": round(x2, 1),
+                            "profiled_transfers_per_launch": tpl})
+                if transfers_per_launch:
+                    out["bytes_per_launch"] = round(raw * transfers_per_launch)
+                    out["bytes_per_launch_fetch_x2"] = round(x2 * transfers_per_launch)
+            else:
+                out.update({"bytes_per_launch": round(k["hbm_bytes_per_launch_raw"]),
+                            "bytes_per_launch_fetch_x2": round(k["hbm_bytes_per_launch"])})
+            return out
     return None
 
 
@@ -488,7 +503,11 @@ def main():
     # -- roofline: the dominant kernel of the headline's timed steps ---------------------------
     per_launch_transfers = args.transfers / max(1, stats["launches_validate"] / max(1, args.steps))
     u_over_t = expected_unique(args.accounts, 2 * per_launch_transfers) / per_launch_transfers
-    roof = roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown)
+    # The ordered fallback (tb_flow) has no byte roofline (its dependency rounds bound it): the
+    # roofline is the validate kernel's, with tb_flow's share of the time beside it.
+    roof = roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown, kernel="tb_transfers_validate")
+    if roof is not None and args.workload != "c2":
+        roof["flow_ms_share"] = round(stats["ms_replay"] / total_ms, 4)
     pcie_gbs = args.transfers * 128 * args.steps / (total_ms / 1e3) / 1e9
     pcie = {"h2d_bytes_per_transfer": 128, "achieved": round(pcie_gbs, 2), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
             "frac": round(pcie_gbs / PCIE_PEAK_GBS, 4),
@@ -505,6 +524,13 @@ def main():
             "definition": "tbgpu_commit_device_async: the same prepares already resident in HBM (no PCIe)",
             "roofline": roofline(dev_stats, u_dev, per_launch_dev, args, dev_total, None, steps=args.device_steps),
         }
+
+    # -- the validate kernel against its own access pattern, measured live (rank 0, N=1) ------
+    if rank == 0 and world == 1 and args.access_mix and roof and roof["kernel"] == "tb_transfers_validate":
+        roof["access_mix"] = access_mix(engine, per_launch_transfers, roof["avg_launch_ms"])
+        if device_resident and device_resident["roofline"]:
+            dr = device_resident["roofline"]
+            dr["access_mix"] = access_mix(engine, per_launch_dev, dr["avg_launch_ms"])
 
     # -- CPU baseline + bit-exact sample parity (rank 0, N=1 only) ---------------------------
     cpu = None
@@ -741,6 +767,17 @@ def run_sharded(args, world, rank, local_rank):
     dist.destroy_process_group()
 
 
+def access_mix(engine, transfers, kernel_ms):
+    """tb_transfers_validate's memory accesses without its logic (tbgpu_bench_access_mix: stream the
+    event in and the record + per-event results out, two random account-row reads, one random CAS
+    into an index sized like the engine's), timed on this GPU for one launch's transfers: the
+    practical bound of the kernel's access pattern.  frac = that time / the kernel's launch time."""
+    parts = engine.access_mix(int(transfers))
+    return {"ms": round(parts["all"], 4), "kernel_ms": round(kernel_ms, 4), "frac": round(parts["all"] / kernel_ms, 3),
+            "parts_ms": {k: round(v, 4) for k, v in parts.items()}, "transfers": int(transfers),
+            "source": "tbgpu_bench_access_mix (k_workload.h tb_access_mix), measured in this run"}
+
+
 def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=None, steps=None, kernel=None):
     """The dominant kernel of the timed steps against the HBM peak; `kernels` = every kernel's mean
     launch time (from the warmup steps when given: the timed steps time only validate, replay/flow
@@ -776,7 +813,7 @@ def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=No
     src = kernel_table(breakdown) if breakdown else kernels
     per_kernel = {k: {"launches": int(n), "avg_launch_ms": round(ms / n, 4)} for k, (ms, n) in src.items() if n}
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc(dom), "kernel": dom,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc(dom, per_launch_transfers), "kernel": dom,
             "kernels": per_kernel, "kernels_timed_in": "warmup steps (every kernel)" if breakdown else "timed steps",
             "avg_launch_ms": round(ms_dom / n_dom, 4), "alg_bytes_per_transfer": round(alg_bytes / per_launch_transfers, 1),
             "path_bytes_per_transfer": round(296 + 256 * u_over_t, 1),

@@ -50,6 +50,12 @@ int tbgpu_bench_profile_mask(tbgpu_t* engine, uint32_t mask);
  * passes).  Exact either way. */
 int tbgpu_bench_legs_min_events(tbgpu_t* engine, uint32_t events);
 
+/* The memory-access mix of tb_transfers_validate without its logic, on scratch buffers sized like
+ * this engine's account table and transfer index, for `transfers` events (one pass): mean ms of
+ * {stream, probe, cas, stream+probe, stream+cas, probe+cas, all three} (k_workload.h).  The
+ * kernel's practical bound for its access pattern; allocates and frees its own buffers. */
+int tbgpu_bench_access_mix(tbgpu_t* engine, uint64_t transfers, double out_ms[7]);
+
 /* Device memory helpers for callers without a device allocator (ctypes users). */
 int tbgpu_device_alloc(tbgpu_t* engine, uint64_t bytes, void** out);
 int tbgpu_device_free(tbgpu_t* engine, void* ptr);

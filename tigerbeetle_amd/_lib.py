@@ -127,6 +127,7 @@ SIGNATURES = [
     ("tbgpu_bench_pass_latencies", ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
     ("tbgpu_bench_profile_mask", ctypes.c_int, [_P, _U32]),
     ("tbgpu_bench_legs_min_events", ctypes.c_int, [_P, _U32]),
+    ("tbgpu_bench_access_mix", ctypes.c_int, [_P, _U64, ctypes.POINTER(ctypes.c_double)]),
     ("tbgpu_device_alloc", ctypes.c_int, [_P, _U64, ctypes.POINTER(_P)]),
     ("tbgpu_device_free", ctypes.c_int, [_P, _P]),
     ("tbgpu_copy_to_host", ctypes.c_int, [_P, _P, _P, _U64]),

@@ -1342,6 +1342,65 @@ extern "C" int tbgpu_bench_legs_min_events(tbgpu_t* E, uint32_t events) {
     return TBGPU_STATUS_OK;
 }
 
+template <u32 M>
+static float access_mix_ms(tbgpu_t* E, const MixArgs& A, int reps) {
+    const dim3 grid((unsigned)((A.n + 255) / 256));
+    float total = 0;
+    for (int r = 0; r <= reps; r++) {  // the first launch warms up
+        if (hipMemsetAsync(A.index, 0, (A.index_mask + 1) * 8, E->stream) != hipSuccess) return -1;  // empty slots
+        if (hipEventRecord(E->markers[14], E->stream) != hipSuccess) return -1;
+        hipLaunchKernelGGL(tb_access_mix<M>, grid, dim3(256), 0, E->stream, A);
+        if (hipEventRecord(E->markers[15], E->stream) != hipSuccess) return -1;
+        if (hipEventSynchronize(E->markers[15]) != hipSuccess) return -1;
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, E->markers[14], E->markers[15]) != hipSuccess) return -1;
+        if (r > 0) total += ms;
+    }
+    return total / reps;
+}
+
+extern "C" int tbgpu_bench_access_mix(tbgpu_t* E, uint64_t transfers, double out_ms[7]) {
+    HIPCK(hipSetDevice(E->device));
+    HIPCK(hipStreamSynchronize(E->stream));
+    MixArgs A = {};
+    A.n = transfers;
+    const u64 rows = E->account_cap;
+    A.row_mask = rows - 1;
+    A.index_mask = E->xidx_cap - 1;
+    void *ev = nullptr, *rec = nullptr, *s4 = nullptr, *s2 = nullptr, *s8 = nullptr, *rw = nullptr, *ix = nullptr,
+         *sink = nullptr;
+    int st = TBGPU_STATUS_OK;
+    if (hipMalloc(&ev, transfers * 128) != hipSuccess || hipMalloc(&rec, transfers * 128) != hipSuccess ||
+        hipMalloc(&s4, transfers * 16) != hipSuccess || hipMalloc(&s2, transfers * 2) != hipSuccess ||
+        hipMalloc(&s8, transfers * 24) != hipSuccess || hipMalloc(&rw, rows * 32) != hipSuccess ||
+        hipMalloc(&ix, E->xidx_cap * 8) != hipSuccess || hipMalloc(&sink, 8) != hipSuccess ||
+        hipMemsetAsync(ev, 1, transfers * 128, E->stream) != hipSuccess ||
+        hipMemsetAsync(rw, 2, rows * 32, E->stream) != hipSuccess) {
+        st = fail(TBGPU_STATUS_DEVICE, "access mix: allocation failed");
+    } else {
+        A.events = (const uint4*)ev;
+        A.records = (uint4*)rec;
+        A.s4 = (u32*)s4;
+        A.s2 = (unsigned short*)s2;
+        A.s8 = (u64*)s8;
+        A.rows = (const uint4*)rw;
+        A.index = (u64*)ix;
+        A.sink = (u64*)sink;
+        const int reps = 5;
+        const float t[7] = {access_mix_ms<MIX_STREAM>(E, A, reps), access_mix_ms<MIX_PROBE>(E, A, reps),
+                            access_mix_ms<MIX_CAS>(E, A, reps), access_mix_ms<MIX_STREAM | MIX_PROBE>(E, A, reps),
+                            access_mix_ms<MIX_STREAM | MIX_CAS>(E, A, reps), access_mix_ms<MIX_PROBE | MIX_CAS>(E, A, reps),
+                            access_mix_ms<MIX_STREAM | MIX_PROBE | MIX_CAS>(E, A, reps)};
+        for (int k = 0; k < 7; k++) {
+            out_ms[k] = t[k];
+            if (t[k] < 0) st = fail(TBGPU_STATUS_DEVICE, "access mix: launch failed");
+        }
+    }
+    void* bufs[] = {ev, rec, s4, s2, s8, rw, ix, sink};
+    for (void* p : bufs) if (p) (void)hipFree(p);
+    return st;
+}
+
 extern "C" int tbgpu_bench_profile_mask(tbgpu_t* E, uint32_t mask) {
     E->prof_mask = mask;
     return TBGPU_STATUS_OK;

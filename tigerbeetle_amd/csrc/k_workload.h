@@ -191,3 +191,59 @@ __global__ void tb_gen_transfers(u8* out, u64 count, WorkloadParams W) {
     }
     *(Transfer*)(out + i * 128) = t;
 }
+
+// ---- the memory-access mix of tb_transfers_validate (bench only) ---------------------------------
+// tbgpu_bench_access_mix: the accesses kernel 1 makes per transfer, without its logic, on scratch
+// buffers sized like the engine's tables — what the hardware does for this pattern is the kernel's
+// practical bound.  STREAM: the 128-B event in, the 128-B record and 42 B of
+// per-event results out; PROBE: two random 32-B rows of an account-table-sized array; CAS: one
+// random 8-B CAS into an index-sized array.
+enum : u32 { MIX_STREAM = 1, MIX_PROBE = 2, MIX_CAS = 4 };
+struct MixArgs {
+    const uint4* events;
+    uint4* records;
+    u32* s4;             // 4 arrays of n u32 (info, dr, cr, rs)
+    unsigned short* s2;  // flags
+    u64* s8;             // 3 arrays of n u64 (amount lo, hi, key)
+    const uint4* rows;   // 32-B rows
+    u64 row_mask;
+    u64* index;
+    u64 index_mask;
+    u64 n;
+    u64* sink;
+};
+
+template <u32 M>
+__global__ __launch_bounds__(256) void tb_access_mix(MixArgs A) {
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= A.n) return;
+    u64 acc = 0;
+    uint4 ev[8];
+    const u64 h = tb_mix64(i * 0x9e3779b97f4a7c15ULL + 7);
+    if (M & MIX_STREAM) {
+#pragma unroll
+        for (int w = 0; w < 8; w++) ev[w] = A.events[8 * i + w];
+        acc ^= ev[0].x ^ ev[7].w;
+    }
+    if (M & MIX_PROBE) {
+        const u64 d = tb_mix64(h ^ 1) & A.row_mask, c = tb_mix64(h ^ 2) & A.row_mask;
+        const uint4 a0 = A.rows[2 * d], a1 = A.rows[2 * d + 1];
+        const uint4 b0 = A.rows[2 * c], b1 = A.rows[2 * c + 1];
+        acc ^= a0.x ^ a1.w ^ b0.y ^ b1.z ^ (d + c);
+    }
+    if (M & MIX_CAS) acc ^= atomicCAS((unsigned long long*)(A.index + (h & A.index_mask)), 0ULL, i + 1);
+    if (M & MIX_STREAM) {
+#pragma unroll
+        for (int w = 0; w < 8; w++) A.records[8 * i + w] = ev[w];
+        A.s4[i] = (u32)acc;
+        A.s4[A.n + i] = (u32)h;
+        A.s4[2 * A.n + i] = (u32)(h >> 8);
+        A.s4[3 * A.n + i] = (u32)(h >> 16);
+        A.s2[i] = (unsigned short)h;
+        A.s8[i] = h;
+        A.s8[A.n + i] = 0;
+        A.s8[2 * A.n + i] = acc;
+    } else if (acc == 0x123456789ULL) {
+        A.sink[0] = acc;
+    }
+}

@@ -215,6 +215,14 @@ class Engine:
         """Passes of >= events transfers use the sorted balance legs (0: every pass)."""
         _lib.check(self.lib.tbgpu_bench_legs_min_events(self.h, int(events)))
 
+    MIX_PARTS = ("stream", "probe", "cas", "stream+probe", "stream+cas", "probe+cas", "all")
+
+    def access_mix(self, transfers):
+        """Mean ms of kernel 1's memory-access mix without its logic, per part (tbgpu_bench.h)."""
+        out = (ctypes.c_double * 7)()
+        _lib.check(self.lib.tbgpu_bench_access_mix(self.h, int(transfers), out))
+        return dict(zip(self.MIX_PARTS, list(out)))
+
     def profile_mask(self, mask):
         """Kernels timed with HIP events when profiling (include/tbgpu_bench.h)."""
         _lib.check(self.lib.tbgpu_bench_profile_mask(self.h, mask))
