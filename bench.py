@@ -70,6 +70,8 @@ def parse():
     p.add_argument("--profile", type=int, default=1, help="time kernels with HIP events (roofline)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (rehearsal on one GPU)")
     p.add_argument("--same-device", action="store_true", help="rehearsal: every rank on cuda:0")
+    p.add_argument("--sharded", action="store_true",
+                   help="run the multi-GPU protocol even at one rank (rehearses the RCCL code path on one GPU)")
     p.add_argument("--access-mix", type=int, default=1,
                    help="time the validate kernel's access pattern without its logic (roofline.access_mix)")
     p.add_argument("--host-prepares", type=int, default=600,
@@ -370,7 +372,7 @@ def main():
         args.accounts = 100_000_000 if world > 1 else 1_000_000
     if args.transfers is None:
         args.transfers = 125_000_000 if world > 1 else 100_000_000
-    if world > 1:
+    if world > 1 or args.sharded:
         assert args.workload == "c2", "the multi-GPU bench runs the C5 shape (uniform, no flags)"
         if args.same_device:
             local_rank = 0

@@ -32,11 +32,15 @@ def _passes(sc, max_prepares):
     return out
 
 
-def run_rank(rank, world, port, kind, scenario_kw, max_prepares, result_path):
+def run_rank(rank, world, port, kind, scenario_kw, max_prepares, result_path, dist_backend="gloo"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if dist_backend == "nccl":  # RCCL: device tensors for every collective (one rank per GPU)
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     verdict = {"ok": False}
     try:
         from tigerbeetle_amd.sharded import ShardedStateMachine
@@ -77,7 +81,7 @@ def run_rank(rank, world, port, kind, scenario_kw, max_prepares, result_path):
         not_mine = ~sm._owner_mask(local)
         stray = sum(int(np.count_nonzero(local[f + w][not_mine])) for f in
                     ("debits_pending", "debits_posted", "credits_pending", "credits_posted") for w in ("_lo", "_hi"))
-        stray_t = torch.tensor([stray], dtype=torch.int64)
+        stray_t = torch.tensor([stray], dtype=torch.int64, device=sm.comm_device)
         dist.all_reduce(stray_t)
         accounts = sm.export_accounts()
         transfers = sm.export_transfers()

@@ -51,3 +51,12 @@ def test_gpu_sharded_dependent_kinds(tmp_path):
                                            p_balancing=0.1, p_pending=0.4, p_post_void=0.3, p_dup=0.15, id_space=400))
     assert v["ok"], v["problems"]
     assert v["split"] > 0 and v["demoted"] > 0
+
+
+def test_gpu_sharded_rccl_one_rank(tmp_path):
+    """The protocol over RCCL (backend "nccl"): device tensors for every collective, torch's current
+    stream synchronised before each.  One rank (the box has one GPU; RCCL refuses two ranks on one
+    device), every pass kind: clean and split passes through the real kernels and collectives."""
+    v = run_world(tmp_path, "gpu", 1, dict(seed=41, n_accounts=64, n_transfer_batches=10), dist_backend="nccl")
+    assert v["ok"], v["problems"]
+    assert v["clean"] + v["split"] + v["dirty"] > 0

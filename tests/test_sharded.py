@@ -18,12 +18,12 @@ def free_port():
         return s.getsockname()[1]
 
 
-def run_world(tmp_path, kind, world, scenario_kw, max_prepares=4, timeout=300):
+def run_world(tmp_path, kind, world, scenario_kw, max_prepares=4, timeout=300, dist_backend="gloo"):
     """Run the scenario on `world` ranks; a rank that dies or hangs fails the test (all ranks are
     killed at the deadline, never left waiting in a collective)."""
     out = tmp_path / "verdict.json"
-    ctx = mp.spawn(run_rank, args=(world, free_port(), kind, scenario_kw, max_prepares, str(out)), nprocs=world,
-                   join=False)
+    ctx = mp.spawn(run_rank, args=(world, free_port(), kind, scenario_kw, max_prepares, str(out), dist_backend),
+                   nprocs=world, join=False)
     deadline = time.monotonic() + timeout
     try:
         while not ctx.join(timeout=1.0):
