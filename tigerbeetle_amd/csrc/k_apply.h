@@ -73,22 +73,7 @@ __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
         }
 #pragma unroll
         for (u32 q = 0; q < 4; q++) {
-            // A hot account (Zipf traffic) fills most lanes with one slot, and LDS atomics on one
-            // address serialise: when many lanes share the first active lane's slot they are summed
-            // across the wave first (< 64 amounts < 2^52 each) and added once.
-            const u32 key = w[q] ? (u32)(w[q] >> LEG_AMT_BITS) : 0xFFFFFFFFu;
-            const u32 lead = __builtin_amdgcn_readfirstlane(key);
-            const bool same = w[q] && key == lead;
-            const u64 m = __ballot(same);
-            bool left = w[q] != 0;
-            if (__popcll(m) > 8) {
-                u64 part = same ? (w[q] & LEG_AMT_MASK) : 0;
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) part += __shfl_xor((unsigned long long)part, off);
-                if ((threadIdx.x & 63) == (u32)__builtin_ctzll(m)) atomicAdd((unsigned long long*)&s_acc[lead], (unsigned long long)part);
-                left = left && !same;
-            }
-            if (left) atomicAdd((unsigned long long*)&s_acc[key], (unsigned long long)(w[q] & LEG_AMT_MASK));
+            if (w[q]) atomicAdd((unsigned long long*)&s_acc[w[q] >> LEG_AMT_BITS], (unsigned long long)(w[q] & LEG_AMT_MASK));
         }
     }
     __syncthreads();
