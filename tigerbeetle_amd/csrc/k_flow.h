@@ -346,13 +346,15 @@ __device__ static inline u32 fl_run_run(const PassArgs& P, const FlowArgs& F, co
 
 // Replies of every prepare with dependent events (their final codes are in P.info), then close
 // the pass: bound += S, reset the dependent counter.  Workgroup 0, every thread.
+// Replies of the prepares with dependent events, those with k % parts == part (every workgroup of a
+// grid takes its share); the pass bookkeeping by the closing workgroup (`close`).
 __device__ static inline void fl_finish(const PassArgs& P, u8* s_code, u32* s_wave, u32* s_list, u64 tsmax_block,
-                                         bool any) {
+                                         bool any, u32 part = 0, u32 parts = 1, bool close = true) {
     Globals* g = P.T.g;
     const u32 nb = P.b1 - P.b0;
     for (u32 c = 0; any && c < nb; c += blockDim.x) {
         const u32 k = c + threadIdx.x;
-        const bool has = k < nb && P.dep_count[k] > 0;
+        const bool has = k < nb && k % parts == part && P.dep_count[k] > 0;
         u32 total;
         const u32 r = tb_block_rank(has, s_wave, total);
         if (has) s_list[r] = k;
@@ -368,7 +370,7 @@ __device__ static inline void fl_finish(const PassArgs& P, u8* s_code, u32* s_wa
             __syncthreads();
         }
     }
-    if (threadIdx.x == 0) {
+    if (close && threadIdx.x == 0) {
         if (tsmax_block > g->commit_timestamp) g->commit_timestamp = tsmax_block;
         const u128 S = tb_sum_total(P.sum_shards);
         const u128 nb2 = tb_sat_add(tb_u128(g->bound_lo, g->bound_hi), S);
@@ -1163,14 +1165,13 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
             // workgroups' writes.
             if (tsb) atomicMax((unsigned long long*)&g->commit_timestamp, (unsigned long long)tsb);
             fl_grid_sync(g, G, gen, F);
-            if (blockIdx.x != 0) return;
-            if (tid == 0) {
+            if (blockIdx.x == 0 && tid == 0) {
                 const u64 ft2 = fl_now();
                 atomicAdd((unsigned long long*)&g->flow_plan_ticks, (unsigned long long)(ft1 - ft0));
                 atomicAdd((unsigned long long*)&g->flow_run_ticks, (unsigned long long)(ft2 - ft1));
                 atomicAdd(&g->flow_passes, 1u);
             }
-            fl_finish(P, s_code, s_wave, s_list, 0, true);
+            fl_finish(P, s_code, s_wave, s_list, 0, true, blockIdx.x, G, blockIdx.x == 0);
             return;
         }
         // Not certifiable: nothing was applied; the ordered run decides every unit.
@@ -1298,7 +1299,6 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
         if ((tid & 63) == 0 && m) atomicMax((unsigned long long*)&g->commit_timestamp, (unsigned long long)m);
         tsmax = 0;
         fl_grid_sync(g, G, gen, F);
-        if (blockIdx.x != 0) return;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     u64 m = tsmax;
@@ -1308,10 +1308,13 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     __syncthreads();
     u64 mm = 0;
     for (u32 k = 0; k < NT / 64; k++) mm = max(mm, s_tsmax[k]);
-    if (tid == 0) {
+    if (blockIdx.x == 0 && tid == 0) {
         const u64 ft2 = fl_now();
         atomicAdd((unsigned long long*)&g->flow_plan_ticks, (unsigned long long)(ft1 - ft0));
         atomicAdd((unsigned long long*)&g->flow_run_ticks, (unsigned long long)(ft2 - ft1));
     }
-    fl_finish(P, s_code, s_wave, s_list, mm, true);
+    // The replies: every workgroup its share after the parallel run (all are still here), workgroup
+    // 0 alone after the sequential one (the others have left).
+    const u32 parts = sequential ? 1u : G;
+    fl_finish(P, s_code, s_wave, s_list, mm, true, blockIdx.x, parts, blockIdx.x == 0);
 }
