@@ -277,7 +277,8 @@ def run_secondary(args, kind, device):
             "dependent_events": stats["dependent_events"],
             "flow": {k: (round(stats[k], 3) if isinstance(stats[k], float) else stats[k])
                      for k in ("flow_units", "flow_runs", "flow_plan_ms", "flow_run_ms", "bounds_passes", "bounds_units",
-                               "bounds_rounds", "bounds_skipped", "bounds_abandoned")},
+                               "bounds_rounds", "bounds_skipped", "bounds_abandoned", "bounds_swept")},
+            "flow_phases_ms": flow_phases(stats),
             "roofline": roof, "parity": parity}
 
 
@@ -594,7 +595,8 @@ def main():
         "dependent_events": stats["dependent_events"],
         "flow": {k: (round(stats[k], 3) if isinstance(stats[k], float) else stats[k])
                  for k in ("flow_units", "flow_runs", "flow_run_units", "flow_plan_ms", "flow_run_ms", "bounds_passes",
-                           "bounds_units", "bounds_rounds", "bounds_skipped", "bounds_abandoned")},
+                           "bounds_units", "bounds_rounds", "bounds_skipped", "bounds_abandoned", "bounds_swept")},
+        "flow_phases_ms": flow_phases(stats),
         "failed_events": n_failed,
         "roofline": roof,
         "cpu_baseline": cpu,
@@ -767,6 +769,14 @@ def run_sharded(args, world, rank, local_rank):
         print(json.dumps(line), flush=True)
     engine.close()
     dist.destroy_process_group()
+
+
+FLOW_PHASES = ("plan", "sort", "link", "bounds_setup", "bounds_rounds", "sweep", "run_or_apply", "replies_wg0")
+
+
+def flow_phases(stats):
+    """tb_flow's wall time by phase (device clock, workgroup 0), ms over the measured steps."""
+    return {n: round(v, 3) for n, v in zip(FLOW_PHASES, stats["flow_phase_ms"])}
 
 
 def access_mix(engine, transfers, kernel_ms):

@@ -55,7 +55,11 @@ __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
     __syncthreads();
 
     // Gather: consecutive legs of a segment go to consecutive lanes (coalesced reads), four legs
-    // per thread in flight before their LDS adds.
+    // per thread in flight before their LDS adds.  A thread's legs j only grow, so the prepare
+    // holding j is found by walking forward from the last one (s_pref[nb] = total stops the walk):
+    // about one LDS read per leg, instead of a binary search whose dependent reads serialised the
+    // loads of a heavy (Zipf-hot) bucket.
+    u32 lo = 0;  // the last prepare whose segment starts at or before this thread's current leg
     for (u32 j0 = 0; j0 < total; j0 += 4 * APPLY_THREADS) {
         u64 w[4];
 #pragma unroll
@@ -63,11 +67,7 @@ __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
             const u32 j = j0 + q * APPLY_THREADS + threadIdx.x;
             w[q] = 0;
             if (j < total) {
-                u32 lo = 0, hi = nb;  // the last prepare whose segment starts at or before j
-                while (hi - lo > 1) {
-                    const u32 mid = (lo + hi) >> 1;
-                    if (s_pref[mid] <= j) lo = mid; else hi = mid;
-                }
+                while (s_pref[lo + 1] <= j) lo++;
                 w[q] = P.leg_w[(u64)s_start[lo] + (j - s_pref[lo])];
             }
         }

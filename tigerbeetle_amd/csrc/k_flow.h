@@ -98,6 +98,17 @@ __device__ static inline u64 fl_now() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     return t;
 }
+// Phase timer of tb_flow (workgroup 0, thread 0; device wall clock): adds the time since the last
+// mark to flow_phase_ticks[k].  Phases: FP_PLAN (flat list), FP_SORT, FP_LINK (links + packing),
+// FP_BSETUP, FP_BROUNDS, FP_SWEEP, FP_RUN (ordered run, or applying the bounds' decisions),
+// FP_REPLIES.
+enum : u32 { FP_PLAN = 0, FP_SORT, FP_LINK, FP_BSETUP, FP_BROUNDS, FP_SWEEP, FP_RUN, FP_REPLIES };
+__device__ static inline void fl_mark(Globals* g, u64& t, u32 k) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    const u64 now = (u64)wall_clock64();
+    atomicAdd((unsigned long long*)&g->flow_phase_ticks[k], (unsigned long long)(now - t));
+    t = now;
+}
 __device__ static inline bool fl_expired(const FlowArgs& F, u64 w0) {
     const u64 now = fl_now();
     return now > w0 && now - w0 > F.stall_ticks;
@@ -714,9 +725,33 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
     return !fl_stalled(g);
 }
 
+// No-return add of v to the low word at p (p == nullptr: nothing) for every lane of the wave; lanes
+// naming the word of one of the first two leaders add their sum with a single atomic.
+__device__ static inline void fl_add_lo(u64* p, u64 v) {
+    const u32 lane = threadIdx.x & 63;
+    bool left = p != nullptr;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const u64 live = __ballot(left);
+        if (!live) return;
+        const u32 l = (u32)__builtin_ctzll(live);
+        const u64 lead = ((u64)(u32)__builtin_amdgcn_readlane((u32)((uintptr_t)p >> 32), l) << 32) |
+                         (u32)__builtin_amdgcn_readlane((u32)(uintptr_t)p, l);
+        const bool mine = left && (u64)(uintptr_t)p == lead;
+        const u64 group = __ballot(mine);
+        if (__popcll(group) < 2) break;
+        u64 part = mine ? v : 0;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) part += __shfl_xor((unsigned long long)part, off);
+        if (lane == l) tb_atomic_add_lo_noret(p, part);
+        left = left && !mine;
+    }
+    if (left) tb_atomic_add_lo_noret(p, v);
+}
+
 // Returns true when every unit was decided and applied (the ordered run is skipped).
 __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u32 ndep, u32 N, bool cert64, u32& gen,
-                                        u64& tsmax, u64 (*s_wv)[4], u32* s_wf, u32* s_cnt) {
+                                        u64& tsmax, u64 (*s_wv)[4], u32* s_wf, u32* s_cnt, u64& tp) {
     Globals* g = P.T.g;
     const Tables& T = P.T;
     const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid;
@@ -785,6 +820,7 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
     fl_grid_sync(g, G, gen, F);
     if (fl_stalled(g)) return false;
 
+    fl_mark(g, tp, FP_BSETUP);
     const u32 tile = ((NA + G - 1) / G + NT - 1) / NT * NT;
     const u32 t0 = min(NA, blockIdx.x * tile), t1 = min(NA, t0 + tile);
     bool converged = *(volatile u32*)&F.words[FW_BUND] == 0;
@@ -881,9 +917,11 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
             break;
         }
     }
+    fl_mark(g, tp, FP_BROUNDS);
     if (!converged && F.sweep_min) {
         converged = fl_sweep(P, F, ndep, NA, gen, s_wv, s_wf, s_cnt);
         if (fl_stalled(g)) return false;
+        fl_mark(g, tp, FP_SWEEP);
     }
     if (!converged) {
         if (blockIdx.x == 0 && tid == 0) {
@@ -895,29 +933,43 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
 
     // Apply: the ok units' legs (both accounts; sums commute), their index entries and counts; the
     // failed ones' codes.  Kernel 1 already wrote every record at its log position.
+    // Zipf-hot accounts put one balance word in many lanes of a wave: atomics on one address
+    // serialise in L2, so the lanes sharing the first lane's word add their sum once (fl_add_lo).
     u32 n_ok = 0;
     u64 tsm = 0;
-    for (u32 f = blockIdx.x * NT + tid; f < ndep; f += G * NT) {
-        if (!F.f_len[f]) continue;
-        const u32 pe = F.f_pe[f];
-        const u8 st = F.b_st[f];
-        if (st == BS_OK) {
-            const u128 amount = tb_u128(P.amt[2 * pe], P.amt[2 * pe + 1]);
+    for (u32 f0 = blockIdx.x * NT; f0 < ndep; f0 += G * NT) {  // whole waves iterate together
+        const u32 f = f0 + tid;
+        bool ok = false;
+        u32 pe = 0;
+        if (f < ndep && F.f_len[f]) {
+            pe = F.f_pe[f];
+            const u8 st = F.b_st[f];
+            ok = st == BS_OK;
+            if (st == BS_FAIL_CREDITS || st == BS_FAIL_DEBITS) {
+                P.info[pe] = (P.info[pe] & 0xFFFFFF00u) | (st == BS_FAIL_CREDITS ? CT_EXCEEDS_CREDITS : CT_EXCEEDS_DEBITS);
+            }
+        }
+        u64* dw = nullptr;
+        u64* cw = nullptr;
+        u64 a = 0;
+        if (ok) {
+            a = P.amt[2 * pe];
             const bool pend = P.eflags[pe] & TF_PENDING;
-            u8* dr = (u8*)&T.acct_bal[P.dr[pe]];
-            u8* cr = (u8*)&T.acct_bal[P.cr[pe]];
-            tb_atomic_add_lo_noret(dr + (pend ? BAL_OFF_DEBITS_PENDING : BAL_OFF_DEBITS_POSTED), tb_lo(amount));
-            tb_atomic_add_lo_noret(cr + (pend ? BAL_OFF_CREDITS_PENDING : BAL_OFF_CREDITS_POSTED), tb_lo(amount));
+            dw = (u64*)((u8*)&T.acct_bal[P.dr[pe]] + (pend ? BAL_OFF_DEBITS_PENDING : BAL_OFF_DEBITS_POSTED));
+            cw = (u64*)((u8*)&T.acct_bal[P.cr[pe]] + (pend ? BAL_OFF_CREDITS_PENDING : BAL_OFF_CREDITS_POSTED));
             __hip_atomic_fetch_and(&T.xidx[P.rs[pe]], ~(u64)XI_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             n_ok++;
             const u32 b = F.f_batch[f];
             const u64 boff = P.batch_off[b];
             tsm = max(tsm, tb_event_ts(P, b, boff, (u32)(P.batch_off[b + 1] - boff), (u32)(P.e0 + pe - boff)));
-        } else if (st == BS_FAIL_CREDITS || st == BS_FAIL_DEBITS) {
-            P.info[pe] = (P.info[pe] & 0xFFFFFF00u) | (st == BS_FAIL_CREDITS ? CT_EXCEEDS_CREDITS : CT_EXCEEDS_DEBITS);
         }
+        fl_add_lo(dw, a);
+        fl_add_lo(cw, a);
     }
-    if (n_ok) atomicAdd((unsigned long long*)&g->transfer_count, (unsigned long long)n_ok);
+    u64 nw = n_ok;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nw += __shfl_xor((unsigned long long)nw, off);
+    if ((tid & 63) == 0 && nw) atomicAdd((unsigned long long*)&g->transfer_count, (unsigned long long)nw);
     tsmax = max(tsmax, tsm);
     if (blockIdx.x == 0 && tid == 0) {
         atomicAdd((unsigned long long*)&g->bounds_passes, 1ULL);
@@ -949,6 +1001,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     tb_pass_cert(P, S, cert_global, cert64);
     u32 gen = 0;
     const u64 ft0 = (blockIdx.x == 0 && tid == 0) ? fl_now() : 0;
+    u64 tp = ft0;
 
     // ---- plan 1: flat list of dependent events, units, resource pairs ------------------------
     for (u32 k = tid; k < nb; k += NT) s_dpre[k] = P.dep_count[k];
@@ -1015,6 +1068,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     fl_grid_sync(g, G, gen, F);
     if (fl_stalled(g)) return;
     const bool sequential = *(volatile u32*)&F.words[FW_SEQ] != 0;
+    fl_mark(g, tp, FP_PLAN);
 
     if (!sequential) {
         // ---- plan 2: stable LSD radix sort of the pairs by key (4 x 8 bits) ---------------------
@@ -1087,6 +1141,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
             if (fl_stalled(g)) return;
         }
 
+        fl_mark(g, tp, FP_SORT);
         // ---- plan 3: link each unit to its successor on every resource --------------------------
         const u32* K = F.keys[0];
         const u32* V = F.vals[0];
@@ -1155,12 +1210,13 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
         if (fl_stalled(g)) return;
     }
     const u64 ft1 = (blockIdx.x == 0 && tid == 0) ? fl_now() : 0;
+    fl_mark(g, tp, FP_LINK);
     if (!sequential) {
         __shared__ u64 s_bwv[FLOW_THREADS / 64][4];
         __shared__ u32 s_bwf[FLOW_THREADS / 64];
         __shared__ u32 s_bcnt;
         u64 tsb = 0;
-        if (fl_bounds(P, F, ndep, N, cert64, gen, tsb, s_bwv, s_bwf, &s_bcnt)) {
+        if (fl_bounds(P, F, ndep, N, cert64, gen, tsb, s_bwv, s_bwf, &s_bcnt, tp)) {
             // Every unit decided and applied: replies and the pass close (workgroup 0) after all
             // workgroups' writes.
             if (tsb) atomicMax((unsigned long long*)&g->commit_timestamp, (unsigned long long)tsb);
@@ -1171,7 +1227,9 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
                 atomicAdd((unsigned long long*)&g->flow_run_ticks, (unsigned long long)(ft2 - ft1));
                 atomicAdd(&g->flow_passes, 1u);
             }
+            fl_mark(g, tp, FP_RUN);
             fl_finish(P, s_code, s_wave, s_list, 0, true, blockIdx.x, G, blockIdx.x == 0);
+            fl_mark(g, tp, FP_REPLIES);  // workgroup 0's share
             return;
         }
         // Not certifiable: nothing was applied; the ordered run decides every unit.
@@ -1316,5 +1374,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     // The replies: every workgroup its share after the parallel run (all are still here), workgroup
     // 0 alone after the sequential one (the others have left).
     const u32 parts = sequential ? 1u : G;
+    fl_mark(g, tp, FP_RUN);
     fl_finish(P, s_code, s_wave, s_list, mm, true, blockIdx.x, parts, blockIdx.x == 0);
+    fl_mark(g, tp, FP_REPLIES);  // workgroup 0's share
 }

@@ -198,7 +198,8 @@ struct Globals {
     u64 bounds_rounds;        // scan rounds they took (and the rounds of abandoned attempts)
     u64 bounds_skipped;       // dependent passes with an event the bounds do not cover (ordered run)
     u64 bounds_swept;         // units the in-order sweep decided (fl_sweep)
-    u64 sweep_ticks[3];       // fl_sweep wall-clock ticks: the whole walk, its in-window loops, its memory waits
+    u64 sweep_ticks[3];
+    u64 flow_phase_ticks[8];  // tb_flow wall-clock ticks per phase (k_flow.h FP_*)       // fl_sweep wall-clock ticks: the whole walk, its in-window loops, its memory waits
     u64 bounds_abandoned;     // passes whose bounds did not converge in FLOW_BOUNDS_ROUNDS_MAX rounds
 };
 

@@ -185,7 +185,7 @@ class Engine:
     def stats(self):
         s = _lib.tbgpu_stats()
         _lib.check(self.lib.tbgpu_get_stats(self.h, ctypes.byref(s)))
-        return {f: getattr(s, f) for f, _ in s._fields_}
+        return {f: (list(getattr(s, f)) if f == "flow_phase_ms" else getattr(s, f)) for f, _ in s._fields_}
 
     def reset_stats(self):
         self.lib.tbgpu_reset_stats(self.h)

@@ -16,3 +16,5 @@ before = e.stats()
 e.commit_many(129, x_ts, split(xfers, x_lens))
 st = e.stats()
 print({k: st[k] - before.get(k, 0) if isinstance(st[k], int) else st[k] for k in st})
+names = ("plan", "sort", "link", "bounds_setup", "bounds_rounds", "sweep", "run_or_apply", "replies_wg0")
+print({n: round(a - b, 3) for n, a, b in zip(names, st["flow_phase_ms"], before["flow_phase_ms"])})
