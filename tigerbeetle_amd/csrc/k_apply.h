@@ -16,6 +16,36 @@
 
 #include "k_resolve.h"
 
+// Gather of one bucket's legs: consecutive legs of a segment go to consecutive lanes (coalesced
+// reads), Q legs per thread in flight before their LDS adds (a heavy, Zipf-hot bucket keeps more in
+// flight).  A thread's legs j only grow, so the prepare holding j is found by walking forward from
+// the last one (s_pref[nb] = total stops the walk): about one LDS read per leg, instead of a binary
+// search whose dependent reads serialised the loads.
+template <u32 Q>
+__device__ static inline void tb_gather_legs(const PassArgs& P, u32 total, const u32* s_start, const u32* s_pref,
+                                             u64* s_acc, u32 hot_key = 0xFFFFFFFFu, u64* hot = nullptr) {
+    u32 lo = 0;  // the last prepare whose segment starts at or before this thread's current leg
+    for (u32 j0 = 0; j0 < total; j0 += Q * APPLY_THREADS) {
+        u64 w[Q];
+#pragma unroll
+        for (u32 q = 0; q < Q; q++) {
+            const u32 j = j0 + q * APPLY_THREADS + threadIdx.x;
+            w[q] = 0;
+            if (j < total) {
+                while (s_pref[lo + 1] <= j) lo++;
+                w[q] = P.leg_w[(u64)s_start[lo] + (j - s_pref[lo])];
+            }
+        }
+#pragma unroll
+        for (u32 q = 0; q < Q; q++) {
+            if (!w[q]) continue;
+            const u32 key = (u32)(w[q] >> LEG_AMT_BITS);
+            if (hot && key == hot_key) *hot += w[q] & LEG_AMT_MASK;  // registers: LDS atomics on one word serialise
+            else atomicAdd((unsigned long long*)&s_acc[key], (unsigned long long)(w[q] & LEG_AMT_MASK));
+        }
+    }
+}
+
 __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
     extern __shared__ u64 s_acc[];                  // [4 << leg_shift] per (slot, field) sum (dynamic)
     __shared__ u32 s_start[LEG_PREPARES_MAX];       // the bucket's first leg in each prepare
@@ -54,29 +84,44 @@ __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
     if (threadIdx.x == 0) s_pref[nb] = total;
     __syncthreads();
 
-    // Gather: consecutive legs of a segment go to consecutive lanes (coalesced reads), four legs
-    // per thread in flight before their LDS adds.  A thread's legs j only grow, so the prepare
-    // holding j is found by walking forward from the last one (s_pref[nb] = total stops the walk):
-    // about one LDS read per leg, instead of a binary search whose dependent reads serialised the
-    // loads of a heavy (Zipf-hot) bucket.
-    u32 lo = 0;  // the last prepare whose segment starts at or before this thread's current leg
-    for (u32 j0 = 0; j0 < total; j0 += 4 * APPLY_THREADS) {
-        u64 w[4];
+    // Gather (tb_gather_legs).
+    if (total < 16 * 4 * APPLY_THREADS) {
+        tb_gather_legs<4>(P, total, s_start, s_pref, s_acc);
+        __syncthreads();
+    } else {
+        // A heavy bucket: its most frequent (slot, field) word among 256 legs spread over it (counted
+        // in s_acc, still zero) is summed in registers, then added once.
+        __shared__ u64 s_red[APPLY_THREADS / 64];
+        const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+        const u32 j = (u32)((u64)tid * total / APPLY_THREADS);
+        u32 p = 0;
+        while (s_pref[p + 1] <= j) p++;
+        const u32 key = (u32)(P.leg_w[(u64)s_start[p] + (j - s_pref[p])] >> LEG_AMT_BITS);
+        atomicAdd((unsigned long long*)&s_acc[key], 1ULL);
+        __syncthreads();
+        u64 best = (s_acc[key] << 32) | key;
 #pragma unroll
-        for (u32 q = 0; q < 4; q++) {
-            const u32 j = j0 + q * APPLY_THREADS + threadIdx.x;
-            w[q] = 0;
-            if (j < total) {
-                while (s_pref[lo + 1] <= j) lo++;
-                w[q] = P.leg_w[(u64)s_start[lo] + (j - s_pref[lo])];
-            }
-        }
+        for (int off = 32; off > 0; off >>= 1) best = max(best, (u64)__shfl_xor((unsigned long long)best, off));
+        if (lane == 0) s_red[wave] = best;
+        __syncthreads();
+        best = 0;
+        for (u32 k = 0; k < APPLY_THREADS / 64; k++) best = max(best, s_red[k]);
+        s_acc[key] = 0;
+        __syncthreads();
+        const u32 hot_key = (u32)best;
+        u64 hot = 0;
+        tb_gather_legs<16>(P, total, s_start, s_pref, s_acc, hot_key, &hot);
 #pragma unroll
-        for (u32 q = 0; q < 4; q++) {
-            if (w[q]) atomicAdd((unsigned long long*)&s_acc[w[q] >> LEG_AMT_BITS], (unsigned long long)(w[q] & LEG_AMT_MASK));
+        for (int off = 32; off > 0; off >>= 1) hot += __shfl_xor((unsigned long long)hot, off);
+        if (lane == 0) s_red[wave] = hot;
+        __syncthreads();
+        if (tid == 0) {
+            u64 v = 0;
+            for (u32 k = 0; k < APPLY_THREADS / 64; k++) v += s_red[k];
+            s_acc[hot_key] += v;
         }
+        __syncthreads();
     }
-    __syncthreads();
 
     // Write back: thread k -> (slot k/4, field k%4), consecutive threads on consecutive 16-B fields.
     u8* bal = (u8*)(P.T.acct_bal + (u64)g * W);
