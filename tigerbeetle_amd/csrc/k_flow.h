@@ -644,6 +644,13 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
     fl_grid_sync(g, G, gen, F);
     if (fl_stalled(g)) return false;
 
+    u128 S;
+    bool cert_global, cert64;
+    tb_pass_cert(P, S, cert_global, cert64);
+    u128 bs;
+    const bool slack = !P.cert_ext && cert_global && !tb_add_overflows(tb_u128(g->bound_lo, g->bound_hi), S, &bs) &&
+                       tb_hi(bs) == 0 && (tb_lo(bs) >> 63) == 0;
+
     // 2. The sweep: wave 0 of workgroup 0, 64 units a window; the next window's records load while
     // this one is resolved.  A lane holds one unit: its legs' X, Y with the decided units and the
     // swept ok units of earlier windows (b_ex); the window is resolved in lane order, each ok unit
@@ -672,33 +679,55 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
             if (w0 + 64 + lane < nu) nx = F.b_rec[w0 + 64 + lane];
             const u32 vd = (x.t >> 8) & 15, vc = (x.t >> 12) & 15;
             const u64 a = x.a;
-            // Per lane: X, Y thresholds as "fails if X + a > Y": with the unknown sides' checks
-            // folded in once (a known verdict never changes), only the sums move.
+            // A known verdict never changes; only the sums move.
             const bool dknown = vd != BV_UNK, cknown = vc != BV_UNK;
             const bool dfix = vd == BV_FAIL, cfix = vc == BV_FAIL;
-            for (u32 j = 0; j < nv; j++) {
-                const u32 jhd = __builtin_amdgcn_readlane(x.hd, j), jhc = __builtin_amdgcn_readlane(x.hc, j);
-                const u32 jt = __builtin_amdgcn_readlane(x.t, j);
-                const u64 ja = fl_rl64(a, j);
-                const bool dfail = dknown ? dfix : xd + a > yd;
-                const bool cfail = cknown ? cfix : xc + a > yc;
-                const u64 okj = __builtin_amdgcn_readlane((u32)(!dfail & !cfail), j);
-                const u64 m = lane > j && okj ? ja : 0;  // lane j's legs, if it is ok, for the later lanes
-                const u64 dxd = jt & BT_X ? m : 0, dyd = jt & BT_Y ? m : 0;
-                const u64 dxc = (jt >> 4) & BT_X ? m : 0, dyc = (jt >> 4) & BT_Y ? m : 0;
-                const bool dd = x.hd == jhd, dc = x.hd == jhc, cd = x.hc == jhd, cc = x.hc == jhc;
-                xd += (dd ? dxd : 0) + (dc ? dxc : 0);
-                yd += (dd ? dyd : 0) + (dc ? dyc : 0);
-                xc += (cd ? dxd : 0) + (cc ? dxc : 0);
-                yc += (cd ? dyd : 0) + (cc ? dyc : 0);
+            bool dfl, cfl;  // this lane's verdicts, final once every earlier lane has been told
+            if (slack) {
+                // Every balance, amount and sum below 2^63 (cert63): one signed slack Y - X per
+                // leg, "fails if slack < amount"; an ok unit moves each of its accounts' slack by
+                // one signed delta (an X leg: -a, a Y leg: +a) — half the work of X and Y apart.
+                i64 sd = (i64)(yd - xd), sc = (i64)(yc - xc);
+                const u32 td = x.t & 15, tc2 = (x.t >> 4) & 15;
+                const i64 dd_ = (td & BT_X) ? -(i64)a : (td & BT_Y) ? (i64)a : 0;
+                const i64 dc_ = (tc2 & BT_X) ? -(i64)a : (tc2 & BT_Y) ? (i64)a : 0;
+                for (u32 j = 0; j < nv; j++) {
+                    const u32 jhd = __builtin_amdgcn_readlane(x.hd, j), jhc = __builtin_amdgcn_readlane(x.hc, j);
+                    const i64 jdd = (i64)fl_rl64((u64)dd_, j), jdc = (i64)fl_rl64((u64)dc_, j);
+                    const bool dfail = dknown ? dfix : sd < (i64)a;
+                    const bool cfail = cknown ? cfix : sc < (i64)a;
+                    const bool okj = __builtin_amdgcn_readlane((u32)(!dfail & !cfail), j);
+                    const bool upd = okj && lane > j;
+                    sd += (upd && x.hd == jhd ? jdd : 0) + (upd && x.hd == jhc ? jdc : 0);
+                    sc += (upd && x.hc == jhd ? jdd : 0) + (upd && x.hc == jhc ? jdc : 0);
+                }
+                dfl = dknown ? dfix : sd < (i64)a;
+                cfl = !dfl && (cknown ? cfix : sc < (i64)a);
+            } else {
+                for (u32 j = 0; j < nv; j++) {
+                    const u32 jhd = __builtin_amdgcn_readlane(x.hd, j), jhc = __builtin_amdgcn_readlane(x.hc, j);
+                    const u32 jt = __builtin_amdgcn_readlane(x.t, j);
+                    const u64 ja = fl_rl64(a, j);
+                    const bool dfail = dknown ? dfix : xd + a > yd;
+                    const bool cfail = cknown ? cfix : xc + a > yc;
+                    const u64 okj = __builtin_amdgcn_readlane((u32)(!dfail & !cfail), j);
+                    const u64 m = lane > j && okj ? ja : 0;  // lane j's legs, if it is ok, for the later lanes
+                    const u64 dxd = jt & BT_X ? m : 0, dyd = jt & BT_Y ? m : 0;
+                    const u64 dxc = (jt >> 4) & BT_X ? m : 0, dyc = (jt >> 4) & BT_Y ? m : 0;
+                    const bool dd = x.hd == jhd, dc = x.hd == jhc, cd = x.hc == jhd, cc = x.hc == jhc;
+                    xd += (dd ? dxd : 0) + (dc ? dxc : 0);
+                    yd += (dd ? dyd : 0) + (dc ? dyc : 0);
+                    xc += (cd ? dxd : 0) + (cc ? dxc : 0);
+                    yc += (cd ? dyd : 0) + (cc ? dyc : 0);
+                }
+                dfl = dknown ? dfix : xd + a > yd;
+                cfl = !dfl && (cknown ? cfix : xc + a > yc);
             }
             const u64 tc = fl_now();
             t_loop += tc - tb;
             if (valid) {
-                const bool dfail = dknown ? dfix : xd + a > yd;
-                const bool cfail = !dfail && (cknown ? cfix : xc + a > yc);
-                F.b_st[x.f] = dfail ? BS_FAIL_CREDITS : cfail ? BS_FAIL_DEBITS : BS_OK;
-                if (!dfail && !cfail) {
+                F.b_st[x.f] = dfl ? BS_FAIL_CREDITS : cfl ? BS_FAIL_DEBITS : BS_OK;
+                if (!dfl && !cfl) {
                     const u32 td = x.t & 15, tc2 = (x.t >> 4) & 15;
                     if (x.hd != FLOW_SENT) {
                         if (td & BT_X) tb_atomic_add_lo_noret(&F.b_ex[2 * x.hd], a);

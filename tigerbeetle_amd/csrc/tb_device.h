@@ -9,6 +9,7 @@
 
 typedef unsigned __int128 u128;
 typedef uint64_t u64;
+typedef int64_t i64;
 typedef uint32_t u32;
 typedef uint16_t u16;
 typedef uint8_t u8;
