@@ -120,6 +120,12 @@ __device__ static inline u32 fl_key_id(u64 lo, u64 hi) {
     return 0x80000000u | (u32)(tb_mix64(lo ^ tb_mix64(hi ^ 0x9e3779b97f4a7c15ULL)) % 0x7FFFFFFFu);
 }
 
+// Grid barrier of the co-resident grid (cooperative launch).  Two levels, so arrivals do not all
+// serialise on one word: the workgroups of each of FL_BAR_GROUPS groups (blockIdx mod groups)
+// count on their group's word, the last of a group counts on the root word, and the last group
+// publishes the generation, which every workgroup polls.  Every counter only grows (generation gen
+// waits for gen * members); tb_resolve zeroes them each pass.  Each workgroup writes its L2 back
+// (release) before it arrives and invalidates (acquire) after it leaves.
 __device__ static inline void fl_grid_sync(Globals* g, u32 nblocks, u32& gen, const FlowArgs& F) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the barrier
     __syncthreads();
@@ -127,10 +133,21 @@ __device__ static inline void fl_grid_sync(Globals* g, u32 nblocks, u32& gen, co
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(&g->flow_barrier, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const u32 target = gen * nblocks;
+        const u32 groups = min(nblocks, (u32)FL_BAR_GROUPS), grp = blockIdx.x % groups;
+        const u32 members = (nblocks - grp + groups - 1) / groups;
+        u32* bar = g->flow_bar;
+        const u32 a = __hip_atomic_fetch_add(&bar[FL_BAR_STRIDE * grp], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a + 1 == gen * members) {
+            const u32 r = __hip_atomic_fetch_add(&bar[FL_BAR_STRIDE * FL_BAR_GROUPS], 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            if (r + 1 == gen * groups) {
+                __hip_atomic_store(&bar[FL_BAR_STRIDE * (FL_BAR_GROUPS + 1)], gen, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
         const u64 w0 = fl_now();
-        while (__hip_atomic_load(&g->flow_barrier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        while (__hip_atomic_load(&bar[FL_BAR_STRIDE * (FL_BAR_GROUPS + 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+               gen) {
             __builtin_amdgcn_s_sleep(2);
             if (fl_expired(F, w0)) {
                 tb_panic(g, PANIC_FLOW_STALL);
@@ -1117,12 +1134,34 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
             if (tid < 256) F.hist[blockIdx.x * 256 + tid] = s_hist[tid];
             fl_grid_sync(g, G, gen, F);
             if (fl_stalled(g)) return;
-            u32 tot = 0, before = 0;
+            // Digit totals over the grid and the counts of the workgroups before this one: every
+            // thread sums one digit over a quarter of the workgroups (G / 4 loads, eight in flight),
+            // then the quarters are combined.
+            {
+                const u32 d = tid & 255, qt = tid >> 8;  // FLOW_THREADS = 4 x 256
+                const u32 w0 = qt * G / 4, w1 = (qt + 1) * G / 4;
+                u32 tot = 0, before = 0;
+                for (u32 w = w0; w < w1; w += 8) {
+                    u32 c[8];
+#pragma unroll
+                    for (u32 k = 0; k < 8; k++) c[k] = w + k < w1 ? F.hist[(w + k) * 256 + d] : 0;
+#pragma unroll
+                    for (u32 k = 0; k < 8; k++) {
+                        tot += c[k];
+                        before += w + k < blockIdx.x ? c[k] : 0;
+                    }
+                }
+                s_wcnt[qt][d] = tot;
+                s_wcnt[4 + qt][d] = before;
+            }
+            __syncthreads();
+            u32 before = 0;
             if (tid < 256) {
-                for (u32 w = 0; w < G; w++) {
-                    const u32 c = F.hist[w * 256 + tid];
-                    tot += c;
-                    before += w < blockIdx.x ? c : 0;
+                u32 tot = 0;
+#pragma unroll
+                for (u32 qt = 0; qt < 4; qt++) {
+                    tot += s_wcnt[qt][tid];
+                    before += s_wcnt[4 + qt][tid];
                 }
                 s_hist[tid] = tot;
             }

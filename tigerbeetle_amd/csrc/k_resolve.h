@@ -247,7 +247,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         s_applied = 0;
         s_failed = 0;
         if (blockIdx.x == 0) {  // the replay kernel's per-pass counters (k_flow.h)
-            T.g->flow_barrier = 0;
+            for (u32 k = 0; k < FL_BAR_GROUPS + 2; k++) T.g->flow_bar[FL_BAR_STRIDE * k] = 0;
             if (P.flow_words) for (u32 k = 0; k < FLOW_WORDS; k++) P.flow_words[k] = 0;
         }
     }

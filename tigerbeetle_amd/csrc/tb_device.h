@@ -175,6 +175,8 @@ __device__ static inline u128 tb_sat_add(u128 a, u128 b) {
 // meets the claimed fingerprint on its probe path (or loses the CAS to it) — that is how same-pass
 // duplicate ids are detected, with no separate dedup set.
 // ------------------------------------------------------------------------------------------------
+#define FL_BAR_GROUPS 8
+#define FL_BAR_STRIDE 32  // u32 words: one 128-B line per counter
 struct Globals {
     u64 commit_timestamp;     // max timestamp of an event that returned ok when evaluated
     u64 panic;                // PANIC_* bits
@@ -186,7 +188,7 @@ struct Globals {
     u64 account_count;
     u64 transfer_count;
     u64 export_count;
-    u32 flow_barrier;         // tb_flow grid-barrier arrivals (reset by tb_resolve each pass)
+    u32 flow_barrier;         // (unused since the two-level barrier; kept for the layout)
     u32 flow_passes;          // passes whose dependent events ran on the parallel flow path
     u64 flow_units;           // cumulative units (chains / single events) the flow path executed
     u64 flow_runs;            // runs (k_flow.h) and the units they covered
@@ -202,6 +204,9 @@ struct Globals {
     u64 sweep_ticks[3];
     u64 flow_phase_ticks[8];  // tb_flow wall-clock ticks per phase (k_flow.h FP_*)       // fl_sweep wall-clock ticks: the whole walk, its in-window loops, its memory waits
     u64 bounds_abandoned;     // passes whose bounds did not converge in FLOW_BOUNDS_ROUNDS_MAX rounds
+    // tb_flow's two-level grid barrier (k_flow.h fl_grid_sync): FL_BAR_GROUPS group counters, the
+    // root counter, the published generation; one 128-B line each.  Zeroed by tb_resolve every pass.
+    u32 flow_bar[FL_BAR_STRIDE * (FL_BAR_GROUPS + 2)];
 };
 
 struct AccountHot {
