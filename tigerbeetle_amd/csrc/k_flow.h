@@ -1355,6 +1355,9 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
                 next = FLOW_SENT;
             } else {
                 if (ticket == FLOW_SENT) ticket = atomicAdd(qhead, 1u);
+                // At most nunits units are ever queued (each once), so a ticket past them is never
+                // filled: the lane leaves instead of polling `done` with the others.
+                if (ticket >= nunits) break;
                 const u32 item = ticket < nunits
                                      ? __hip_atomic_load(&F.queue[ticket], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                      : 0;
