@@ -290,7 +290,7 @@ __device__ static inline u64 fl_run_unit(const PassArgs& P, const FlowArgs& F, R
 // Runs the run headed by unit u (a run member); returns the last unit it ran (its successors are
 // released by the caller), *count = units run, *tsmax = max ok timestamp.
 // (q, r): the head's sorted position and its account resource, already read by the caller.
-__device__ static inline u32 fl_run_run(const PassArgs& P, const FlowArgs& F, const Replay& R, u32 u, u32 N,
+__device__ static inline u32 fl_run_run(const PassArgs& P, const FlowArgs& F, Replay& R, u32 u, u32 N,
                                         u32 q, u32 r, u32* count, u64* tsmax) {
     const Tables& T = P.T;
     const u32* K = F.keys[0];
@@ -357,7 +357,7 @@ __device__ static inline u32 fl_run_run(const PassArgs& P, const FlowArgs& F, co
         q += FLOW_RUN_STEP;
     }
     rp_store<true>(&T.acct_bal[r], B);
-    if (n_ok) atomicAdd((unsigned long long*)&T.g->transfer_count, (unsigned long long)n_ok);
+    R.xcount += n_ok;
     if (last_ok_pe != TB_NOT_FOUND) {  // commit_timestamp: the run's last ok event is its latest
         u32 lo = P.b0, hi = P.b1;
         const u64 e = P.e0 + last_ok_pe;
@@ -1412,6 +1412,10 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
             }
             atomicAdd(done, ran);
         }
+        u64 xc = R.xcount;  // the wave's transfers, one atomic
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) xc += __shfl_xor((unsigned long long)xc, off);
+        if ((tid & 63) == 0 && xc) atomicAdd((unsigned long long*)&g->transfer_count, (unsigned long long)xc);
         if (runs) {
             atomicAdd((unsigned long long*)&g->flow_runs, (unsigned long long)runs);
             atomicAdd((unsigned long long*)&g->flow_run_units, (unsigned long long)run_units);

@@ -41,6 +41,9 @@ struct Replay {
     u32 epoch;
     bool cert_global;
     bool cert64;  // no balance word can carry this pass: free-account deltas are low-word adds
+    // Flow path: this lane's change to transfer_count (mod 2^64), added once per wave when the run
+    // ends — one atomic per unit on that single word serialised the run.
+    u64 xcount = 0;
 };
 
 // Flow path, single-event unit whose lookups kernel 1 already did exactly (k_flow.h): the account
@@ -183,7 +186,7 @@ __device__ static inline void rp_scope_close(Replay& R, bool persist) {
             }
             case UNDO_TRANSFER_INSERT:
                 tb_xindex_tombstone(R.T, e.slot);
-                if (FLOW) atomicAdd((unsigned long long*)&R.T.g->transfer_count, ~0ULL);
+                if (FLOW) R.xcount--;
                 else R.T.g->transfer_count--;
                 break;
             case UNDO_POSTED: rp_store_posted<FLOW>(R.T, e.slot, POSTED_NONE); break;
@@ -241,7 +244,7 @@ __device__ static inline void rp_transfer_insert(Replay& R, const Transfer& t, u
         R.failed = true;
         return;
     }
-    if (FLOW) atomicAdd((unsigned long long*)&R.T.g->transfer_count, 1ULL);
+    if (FLOW) R.xcount++;
     else R.T.g->transfer_count++;
     rp_push(R, UNDO_TRANSFER_INSERT, entry, nullptr);
 }
@@ -436,7 +439,7 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u3
         rp_store<FLOW>(&R.T.xlog[log_pos], t2);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record before its index entry
         atomicAnd((unsigned long long*)&R.T.xidx[hint->entry], ~(unsigned long long)XI_TOMB);
-        atomicAdd((unsigned long long*)&R.T.g->transfer_count, 1ULL);
+        R.xcount++;  // only the flow path passes a hint
     } else {
         rp_transfer_insert<FLOW>(R, t2, log_pos);
     }
