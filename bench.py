@@ -595,7 +595,8 @@ def main():
         "dependent_events": stats["dependent_events"],
         "flow": {k: (round(stats[k], 3) if isinstance(stats[k], float) else stats[k])
                  for k in ("flow_units", "flow_runs", "flow_run_units", "flow_plan_ms", "flow_run_ms", "bounds_passes",
-                           "bounds_units", "bounds_rounds", "bounds_skipped", "bounds_abandoned", "bounds_swept")},
+                           "bounds_units", "bounds_rounds", "bounds_skipped", "bounds_abandoned", "bounds_swept",
+                           "flow_exec_ms")},
         "flow_phases_ms": flow_phases(stats),
         "failed_events": n_failed,
         "roofline": roof,

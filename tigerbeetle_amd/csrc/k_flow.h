@@ -1348,6 +1348,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
         u32 ticket = FLOW_SENT, spins = 0, next = FLOW_SENT;
         u64 w0 = 0;
         u32 runs = 0, run_units = 0;
+        u64 exec_ticks = 0;  // this lane's time executing units (stats: flow_exec_ms)
         while (true) {
             u32 u;
             if (next != FLOW_SENT) {
@@ -1376,6 +1377,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
                 u = item - 1;
             }
             u32 ran = 1;
+            const u64 te = (u64)wall_clock64();
             // Run head?  Two load levels through the packed entry (position, then entry + resource)
             // instead of the unit's and the event's words.
             const u32 rq = F.rpos[u];
@@ -1398,6 +1400,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
             }
             R.failed = false;  // a panic is recorded in g->panic; keep releasing successors
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this unit's writes land first
+            exec_ticks += (u64)wall_clock64() - te;
             const u32 ns = F.nsucc[u];
             for (u32 k = 0; k < ns; k++) {
                 const u32 s = F.succ[FLOW_RMAX * u + k];
@@ -1412,6 +1415,10 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
             }
             atomicAdd(done, ran);
         }
+        u64 et = exec_ticks;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) et += __shfl_xor((unsigned long long)et, off);
+        if ((tid & 63) == 0 && et) atomicAdd((unsigned long long*)&g->flow_exec_ticks, (unsigned long long)et);
         u64 xc = R.xcount;  // the wave's transfers, one atomic
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) xc += __shfl_xor((unsigned long long)xc, off);
