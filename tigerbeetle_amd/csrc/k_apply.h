@@ -18,11 +18,11 @@
 
 // Gather of one bucket's legs: consecutive legs of a segment go to consecutive lanes (coalesced
 // reads), Q legs per thread in flight before their LDS adds (a heavy, Zipf-hot bucket keeps more in
-// flight).  A thread's legs j only grow, so the prepare holding j is found by walking forward from
-// the last one (s_pref[nb] = total stops the walk): about one LDS read per leg, instead of a binary
-// search whose dependent reads serialised the loads.
+// flight).  A thread's legs j only grow, so the prepare holding j is searched for only past the
+// last one, and not at all while j stays in it (one LDS read: the common case in a heavy bucket,
+// whose binary searches per leg serialised the loads).
 template <u32 Q>
-__device__ static inline void tb_gather_legs(const PassArgs& P, u32 total, const u32* s_start, const u32* s_pref,
+__device__ static inline void tb_gather_legs(const PassArgs& P, u32 total, u32 nb_, const u32* s_start, const u32* s_pref,
                                              u64* s_acc, u32 hot_key = 0xFFFFFFFFu, u64* hot = nullptr) {
     u32 lo = 0;  // the last prepare whose segment starts at or before this thread's current leg
     for (u32 j0 = 0; j0 < total; j0 += Q * APPLY_THREADS) {
@@ -32,7 +32,14 @@ __device__ static inline void tb_gather_legs(const PassArgs& P, u32 total, const
             const u32 j = j0 + q * APPLY_THREADS + threadIdx.x;
             w[q] = 0;
             if (j < total) {
-                while (s_pref[lo + 1] <= j) lo++;
+                if (s_pref[lo + 1] <= j) {  // past this prepare: binary search in the ones after it
+                    u32 b = nb_;
+                    lo++;
+                    while (b - lo > 1) {
+                        const u32 mid = (lo + b) >> 1;
+                        if (s_pref[mid] <= j) lo = mid; else b = mid;
+                    }
+                }
                 w[q] = P.leg_w[(u64)s_start[lo] + (j - s_pref[lo])];
             }
         }
@@ -86,7 +93,7 @@ __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
 
     // Gather (tb_gather_legs).
     if (total < 16 * 4 * APPLY_THREADS) {
-        tb_gather_legs<4>(P, total, s_start, s_pref, s_acc);
+        tb_gather_legs<4>(P, total, nb, s_start, s_pref, s_acc);
         __syncthreads();
     } else {
         // A heavy bucket: its most frequent (slot, field) word among 256 legs spread over it (counted
@@ -110,7 +117,7 @@ __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
         __syncthreads();
         const u32 hot_key = (u32)best;
         u64 hot = 0;
-        tb_gather_legs<16>(P, total, s_start, s_pref, s_acc, hot_key, &hot);
+        tb_gather_legs<16>(P, total, nb, s_start, s_pref, s_acc, hot_key, &hot);
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) hot += __shfl_xor((unsigned long long)hot, off);
         if (lane == 0) s_red[wave] = hot;
