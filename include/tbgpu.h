@@ -198,6 +198,7 @@ typedef struct tbgpu_stats {
     double sweep_ms;             /* tb_flow wall time of the sweeps (one wave) */
     double sweep_loop_ms;        /* ... of it resolving windows in order */
     double sweep_wait_ms;        /* ... of it waiting for memory between windows */
+    uint64_t sweep_u64_passes;   /* sweeps in the u64 X/Y form (bound + S >= 2^63: no signed slack) */
     double flow_exec_ms;         /* tb_flow run: time lanes spent executing units, summed over lanes */
     double flow_phase_ms[8];     /* tb_flow wall time by phase: plan, sort, link, bounds setup, bounds
                                     rounds, sweep, run (or applying the bounds), replies */

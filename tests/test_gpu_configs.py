@@ -4,6 +4,7 @@ pending transfers with timeouts, post/void of earlier transfers across expiry ga
 Inputs come from the engine's device generator; both sides commit identical prepares, through
 multi-prepare device passes.  Bit-exact: replies, accounts, transfers, posted groove,
 commit_timestamp."""
+import numpy as np
 import pytest
 
 from tests.harness.configs import SETTINGS, batches, generate, split, timestamps
@@ -63,3 +64,29 @@ def test_c3_sweep_modes(bounds_sweep, n_accounts, n_transfers, pass_batches, gpu
     """The limit checks decided by the in-order sweep right after the first scan round, and by
     rounds alone (else the ordered run): the same bytes as the oracle either way."""
     test_config_parity("c3", n_accounts, n_transfers, pass_batches, gpu_engine_factory, bounds_sweep)
+
+
+def test_c3_sweep_u64_path(gpu_engine_factory):
+    """The sweep's u64 X/Y form: one transfer of 2^63 + 12345 in the first prepare pushes the
+    certificate's bound past 2^63 (no signed slack), while bound + S stays below 2^64 (the bounds
+    still apply); every later pass sweeps in the u64 form.  Same bytes as the oracle."""
+    n_accounts, n_transfers, pass_batches, batch = 20_000, 200_000, 8, 8190
+    engine = gpu_engine_factory(accounts_max=n_accounts, transfers_max=n_transfers,
+                                pass_events_max=pass_batches * batch, pass_batches_max=pass_batches,
+                                bounds_sweep="early")
+    accts, xfers = generate(engine, "c3", n_accounts, n_transfers, seed=13)
+    xfers = xfers.copy()
+    xfers[48:56] = np.frombuffer(np.uint64(2**63 + 12345).tobytes(), dtype=np.uint8)  # transfer 0's amount
+    xfers[56:64] = 0
+    a_lens, x_lens = batches(n_accounts, batch), batches(n_transfers, batch)
+    a_ts, t = timestamps(a_lens, 10**12)
+    x_ts, _ = timestamps(x_lens, t + 10)
+    oracle = OracleEngine(n_accounts, n_transfers)
+    for e in (oracle, engine):
+        assert all(r == b"" for r in e.commit_many(128, a_ts, split(accts, a_lens)))
+    expected = oracle.commit_many(129, x_ts, split(xfers, x_lens))
+    actual = engine.commit_many(129, x_ts, split(xfers, x_lens))
+    assert actual == expected
+    assert_same_state(oracle, engine)
+    st = engine.stats()
+    assert st["bounds_swept"] > 0 and st["bounds_passes"] > 0 and st["sweep_u64_passes"] > 0

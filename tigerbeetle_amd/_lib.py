@@ -67,6 +67,7 @@ class tbgpu_stats(ctypes.Structure):
         ("sweep_ms", ctypes.c_double),
         ("sweep_loop_ms", ctypes.c_double),
         ("sweep_wait_ms", ctypes.c_double),
+        ("sweep_u64_passes", ctypes.c_uint64),
         ("flow_exec_ms", ctypes.c_double),
         ("flow_phase_ms", ctypes.c_double * 8),
     ]

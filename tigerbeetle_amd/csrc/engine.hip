@@ -1274,6 +1274,7 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     s->sweep_ms = E->wall_khz ? (double)g.sweep_ticks[0] / E->wall_khz : 0.0;
     s->sweep_loop_ms = E->wall_khz ? (double)g.sweep_ticks[1] / E->wall_khz : 0.0;
     s->sweep_wait_ms = E->wall_khz ? (double)g.sweep_ticks[2] / E->wall_khz : 0.0;
+    s->sweep_u64_passes = g.sweep_u64_passes;
     s->flow_exec_ms = E->wall_khz ? (double)g.flow_exec_ticks / E->wall_khz : 0.0;
     for (int k = 0; k < 8; k++) s->flow_phase_ms[k] = E->wall_khz ? (double)g.flow_phase_ticks[k] / E->wall_khz : 0.0;
     return TBGPU_STATUS_OK;

@@ -762,6 +762,7 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
         if (lane == 0) {
             F.words[FW_BUND] = 0;
             atomicAdd((unsigned long long*)&g->bounds_swept, (unsigned long long)nu);
+            if (!slack) atomicAdd((unsigned long long*)&g->sweep_u64_passes, 1ULL);
             atomicAdd((unsigned long long*)&g->sweep_ticks[0], (unsigned long long)(fl_now() - t_all));
             atomicAdd((unsigned long long*)&g->sweep_ticks[1], (unsigned long long)t_loop);
             atomicAdd((unsigned long long*)&g->sweep_ticks[2], (unsigned long long)t_wait);
