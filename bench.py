@@ -46,6 +46,11 @@ sys.path.insert(0, ROOT)
 METRIC = "transfers/sec committed (whole node, bit-exact results) + p99 batch latency"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 PCIE_PEAK_GBS = 63.0   # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s spec
+# Prepares per pipelined chunk.  C2 and C3 at 64 (C3's in-order sweep grows with the chunk); C4 at
+# 128: its ordered run costs about (DAG depth x unit latency) per chunk whatever the chunk's size, so
+# larger chunks amortise it (10M C4 transfers: 282M/s at 64, 352M/s at 128, 351M/s at 256, with
+# p99 submit-to-reply 5.4 / 7.0 / 9.8 ms; tools/gpu/chunks.sh).
+CHUNK_PREPARES = {"c2": 64, "c3": 64, "c4": 128}
 
 
 def parse():
@@ -58,8 +63,9 @@ def parse():
                    help="transfers per GPU; default: 100M (N=1, C2); 125M (N>1, C5: 1B over 8 GPUs)")
     p.add_argument("--batch", type=int, default=8190)
     p.add_argument("--pass-batches", type=int, default=512, help="prepares per device pass (device-resident leg)")
-    p.add_argument("--chunk-prepares", type=int, default=64,
-                   help="prepares per pipelined chunk of the headline (host memory -> PCIe -> commit -> reply)")
+    p.add_argument("--chunk-prepares", type=int, default=None,
+                   help="prepares per pipelined chunk (host memory -> PCIe -> commit -> reply); default per "
+                        "workload: CHUNK_PREPARES")
     p.add_argument("--device-steps", type=int, default=3, help="timed steps of the HBM-resident secondary leg")
     p.add_argument("--secondary", type=int, default=10_000_000,
                    help="transfers of the C3 / C4 secondary lines (0: skip)")
@@ -214,6 +220,7 @@ def run_secondary(args, kind, device):
     from tigerbeetle_amd.state_machine import Engine, Options
 
     wl = SETTINGS[kind]
+    args = argparse.Namespace(**dict(vars(args), chunk_prepares=CHUNK_PREPARES[kind]))
     n_acct, n_xfer = 1_000_000, args.secondary
     eng = Engine(Options(accounts_max=n_acct, transfers_max=n_xfer, pass_events_max=args.chunk_prepares * args.batch,
                          pass_batches_max=args.chunk_prepares, device=device, profile=True))
@@ -277,7 +284,8 @@ def run_secondary(args, kind, device):
             "dependent_events": stats["dependent_events"],
             "flow": {k: (round(stats[k], 3) if isinstance(stats[k], float) else stats[k])
                      for k in ("flow_units", "flow_runs", "flow_plan_ms", "flow_run_ms", "bounds_passes", "bounds_units",
-                               "bounds_rounds", "bounds_skipped", "bounds_abandoned", "bounds_swept")},
+                               "bounds_rounds", "bounds_skipped", "bounds_abandoned", "bounds_swept", "sweep_ms",
+                               "sweep_loop_ms", "sweep_wait_ms")},
             "flow_phases_ms": flow_phases(stats),
             "roofline": roof, "parity": parity}
 
@@ -363,6 +371,8 @@ WORKLOAD_TEXT = {
 
 def main():
     args = parse()
+    if args.chunk_prepares is None:
+        args.chunk_prepares = CHUNK_PREPARES[args.workload]
     import torch
     import torch.distributed as dist
 
@@ -558,14 +568,20 @@ def main():
                        "accounts_equal": acc_equal, "transfers_equal": xfer_equal})
         cpu.pop("seconds")
 
+    host = None
+    if rank == 0 and world == 1 and args.host_prepares > 0:
+        host, t_cursor = run_host_commits(engine, args, events_dev, t_cursor)
+
+    # The C3/C4 lines run on an engine of their own: the headline engine (its 100M-transfer log and
+    # index, the resident prepares) is released first, so they run on the same memory a standalone
+    # `--workload c3|c4` run gets.
+    for ptr in (events_dev, res_dev, rb_dev):
+        engine.free(ptr)
+    engine.close()
     secondary = {}
     if rank == 0 and world == 1 and args.workload == "c2" and args.secondary:
         for kind in ("c3", "c4"):
             secondary[kind] = run_secondary(args, kind, local_rank)
-
-    host = None
-    if rank == 0 and world == 1 and args.host_prepares > 0:
-        host, t_cursor = run_host_commits(engine, args, events_dev, t_cursor)
 
     pass_lat = np.array(pass_lat) if len(pass_lat) else np.array([float("nan")])
     line = {
@@ -596,7 +612,7 @@ def main():
         "flow": {k: (round(stats[k], 3) if isinstance(stats[k], float) else stats[k])
                  for k in ("flow_units", "flow_runs", "flow_run_units", "flow_plan_ms", "flow_run_ms", "bounds_passes",
                            "bounds_units", "bounds_rounds", "bounds_skipped", "bounds_abandoned", "bounds_swept",
-                           "flow_exec_ms")},
+                           "sweep_ms", "sweep_loop_ms", "sweep_wait_ms", "flow_exec_ms")},
         "flow_phases_ms": flow_phases(stats),
         "failed_events": n_failed,
         "roofline": roof,

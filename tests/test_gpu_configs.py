@@ -23,6 +23,7 @@ pytestmark = pytest.mark.gpu
     # BASELINE sizes of accounts, 2M transfers, the bench's 64-prepare passes (4 passes)
     ("c3", 1_000_000, 2_000_000, 64),
     ("c4", 1_000_000, 2_000_000, 64),
+    ("c4", 1_000_000, 2_100_000, 128),  # the bench's C4 chunk (bench.py CHUNK_PREPARES)
 ])
 def test_config_parity(config, n_accounts, n_transfers, pass_batches, gpu_engine_factory, bounds_sweep="auto"):
     batch = 8190
