@@ -548,6 +548,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.ps = E->ps;
         P.rs = E->rs;
         P.amt = E->amt;
+        P.amt_hi = E->amt + E->pe_max;
         P.kid = E->kid;
         P.kpid = E->kpid;
         P.dep_list = E->dep_list;

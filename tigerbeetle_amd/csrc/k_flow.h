@@ -708,18 +708,27 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
                 const u32 td = x.t & 15, tc2 = (x.t >> 4) & 15;
                 const i64 dd_ = (td & BT_X) ? -(i64)a : (td & BT_Y) ? (i64)a : 0;
                 const i64 dc_ = (tc2 & BT_X) ? -(i64)a : (tc2 & BT_Y) ? (i64)a : 0;
+                // Verdicts as wave masks (scalar registers): step j compares every lane's slack
+                // (one vector compare per side), keeps lane j's bit, and only an ok lane j
+                // broadcasts its legs.  Lane j's verdict is final at step j (every earlier lane has
+                // been applied), so later steps may add to it freely: no lane > j guard.
+                const u64 nkd = ~__ballot(dknown), nkc = ~__ballot(cknown);
+                const u64 fxd = __ballot(dknown && dfix), fxc = __ballot(cknown && cfix);
+                u64 dflm = 0, cflm = 0;
                 for (u32 j = 0; j < nv; j++) {
+                    const u64 dfm = (__ballot(sd < (i64)a) & nkd) | fxd;
+                    const u64 cfm = (__ballot(sc < (i64)a) & nkc) | fxc;
+                    const u64 bit = 1ULL << j;
+                    dflm |= dfm & bit;
+                    cflm |= cfm & ~dfm & bit;
+                    if ((dfm | cfm) & bit) continue;  // lane j fails: nothing to broadcast
                     const u32 jhd = __builtin_amdgcn_readlane(x.hd, j), jhc = __builtin_amdgcn_readlane(x.hc, j);
                     const i64 jdd = (i64)fl_rl64((u64)dd_, j), jdc = (i64)fl_rl64((u64)dc_, j);
-                    const bool dfail = dknown ? dfix : sd < (i64)a;
-                    const bool cfail = cknown ? cfix : sc < (i64)a;
-                    const bool okj = __builtin_amdgcn_readlane((u32)(!dfail & !cfail), j);
-                    const bool upd = okj && lane > j;
-                    sd += (upd && x.hd == jhd ? jdd : 0) + (upd && x.hd == jhc ? jdc : 0);
-                    sc += (upd && x.hc == jhd ? jdd : 0) + (upd && x.hc == jhc ? jdc : 0);
+                    sd += (x.hd == jhd ? jdd : 0) + (x.hd == jhc ? jdc : 0);
+                    sc += (x.hc == jhd ? jdd : 0) + (x.hc == jhc ? jdc : 0);
                 }
-                dfl = dknown ? dfix : sd < (i64)a;
-                cfl = !dfl && (cknown ? cfix : sc < (i64)a);
+                dfl = (dflm >> lane) & 1;
+                cfl = (cflm >> lane) & 1;
             } else {
                 for (u32 j = 0; j < nv; j++) {
                     const u32 jhd = __builtin_amdgcn_readlane(x.hd, j), jhc = __builtin_amdgcn_readlane(x.hc, j);
@@ -821,7 +830,7 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
         const bool elig = F.f_len[f] == 1 && (F.uflags[f] & (UF_ID_SINGLE | UF_ID_UNIQUE)) && (info & HZ_SPEC) &&
                           (info & HZ_ACCTS) &&
                           !(fl & (TF_LINKED | TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT)) &&
-                          P.amt[2 * pe + 1] == 0;
+                          !(info & HZ_AMT_HI);
         if (!elig) {
             atomicOr(&F.words[FW_BNO], 1u);
             continue;
@@ -1000,7 +1009,7 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
         u64* cw = nullptr;
         u64 a = 0;
         if (ok) {
-            a = P.amt[2 * pe];
+            a = P.amt[pe];
             const bool pend = P.eflags[pe] & TF_PENDING;
             dw = (u64*)((u8*)&T.acct_bal[P.dr[pe]] + (pend ? BAL_OFF_DEBITS_PENDING : BAL_OFF_DEBITS_POSTED));
             cw = (u64*)((u8*)&T.acct_bal[P.cr[pe]] + (pend ? BAL_OFF_CREDITS_PENDING : BAL_OFF_CREDITS_POSTED));
@@ -1268,8 +1277,8 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
             x.dr = P.dr[pe];
             x.cr = P.cr[pe];
             x.rs = P.rs[pe];
-            x.amt_lo = P.amt[2 * pe];
-            x.amt_hi = P.amt[2 * pe + 1];
+            x.amt_lo = P.amt[pe];
+            x.amt_hi = (info & HZ_AMT_HI) ? P.amt_hi[pe] : 0ULL;
             const bool member = unit_ok && (info & HZ_SPEC) && (info & HZ_ACCTS) && (info & 0xFF) == R_OK &&
                                 !(fl & (TF_LINKED | TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT));
             x.flags = fl | (member ? RUN_MEMBER : 0u);

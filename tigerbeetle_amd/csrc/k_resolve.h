@@ -88,7 +88,7 @@ __device__ static inline void tb_apply_transfer(const PassArgs& P, u32 pe, u32 i
     const Tables& T = P.T;
     u8* dr = (u8*)&T.acct_bal[P.dr[pe]];
     u8* cr = (u8*)&T.acct_bal[P.cr[pe]];
-    const u128 amount = tb_u128(P.amt[2 * pe], P.amt[2 * pe + 1]);
+    const u128 amount = tb_u128(P.amt[pe], (info & HZ_AMT_HI) ? P.amt_hi[pe] : 0ULL);
     if (info & HZ_POSTVOID) {
         const u32 pslot = P.ps[pe];
         const u128 pamount = T.xlog[pslot].amount;
@@ -194,8 +194,13 @@ __device__ static inline bool tb_classify(const PassArgs& P, u32 pe, u32 info, u
     if (any_pv) {
         // Some post/void of this pass names a pending id: an event whose id is one of them, or a
         // post/void whose pending transfer was created in this pass, is dependent.
-        const u64 kid = P.kid[pe];
-        if (kid && tb_dedup_is_dup_or_present(P.dedup, P.dedup_mask, kid)) return true;
+        // The id's dedup key, for an event that reached the id check (kernel 1 set HZ_ACCTS or
+        // HZ_PV_KEY right before it), recomputed from the event.
+        if (info & (HZ_ACCTS | HZ_PV_KEY)) {
+            const Transfer* ev = (const Transfer*)(P.events + (P.e0 + pe) * 128);
+            const u64 kid = tb_dedup_key(tb_lo(ev->id), tb_hi(ev->id));
+            if (tb_dedup_is_dup_or_present(P.dedup, P.dedup_mask, kid)) return true;
+        }
         if (info & HZ_PV_KEY) {
             const Transfer* ev = (const Transfer*)(P.events + (P.e0 + pe) * 128);
             if (tb_transfer_claimed_in_pass(T, tb_lo(ev->pending_id), tb_hi(ev->pending_id), P.log_base)) return true;
@@ -325,8 +330,8 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         const u32 pe = pbase + i;
         r_dr[k] = want ? P.dr[pe] : 0u;
         r_cr[k] = want ? P.cr[pe] : 0u;
-        r_amt[k][0] = want ? P.amt[2 * pe] : 0ULL;
-        r_amt[k][1] = want ? P.amt[2 * pe + 1] : 0ULL;
+        r_amt[k][0] = want ? P.amt[pe] : 0ULL;
+        r_amt[k][1] = want && (r_info[k] & HZ_AMT_HI) ? P.amt_hi[pe] : 0ULL;
     }
     u64 tsmax = 0;
     u32 ndep = 0;

@@ -313,6 +313,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
             const u64 ts = P.routed ? routed_ts : P.batch_ts[b] - L + j + 1;  // :645
             code = tb_validate_transfer(P, t, ts, pe, s);
         }
+        if (tb_hi(s.amount)) s.hz |= HZ_AMT_HI;
         P.info[pe] = code | s.hz;
         P.eflags[pe] = t.flags;
         P.dr[pe] = s.dr;
@@ -324,9 +325,11 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
             P.kpid[pe] = s.kpid;
         }
         P.rs[pe] = s.rs;
-        P.amt[2 * pe] = tb_lo(s.amount);
-        P.amt[2 * pe + 1] = tb_hi(s.amount);
-        P.kid[pe] = s.kid;
+        // 26 B of scratch per event in the common case: the amount's high word only when it is
+        // non-zero, and no id key (tb_resolve recomputes it from the event when a post/void of
+        // the pass makes it matter).
+        P.amt[pe] = tb_lo(s.amount);
+        if (s.hz & HZ_AMT_HI) P.amt_hi[pe] = tb_hi(s.amount);
         if (code != R_OK) s.contrib = 0;
         // The record (create_transfer :870) is the event as staged, with its timestamp.
         if (s.rec_ts) *(u64*)(stage + tb_stage_off(threadIdx.x, 7) + 8) = s.rec_ts;  // timestamp @120

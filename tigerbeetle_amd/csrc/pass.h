@@ -25,6 +25,7 @@ enum : u32 {
     HZ_SPEC = 1u << 15,      // index entry rs[] claimed, record written at log_base + event
     HZ_SELFDEP = 1u << 16,   // kernel 1 already knows the event is dependent (id collision)
     HZ_PV_KEY = 1u << 17,    // post/void: pending id registered in the pass pending set
+    HZ_AMT_HI = 1u << 18,    // amt_hi[] holds the amount's high word (else it is zero, not written)
 };
 
 #define SUM_SHARDS 64
@@ -55,8 +56,9 @@ struct PassArgs {
     u32* cr;
     u32* ps;               // log position of the pending transfer (post/void)
     u32* rs;               // index entry claimed by the speculative insert
-    u64* amt;              // 2 words per event
-    u64* kid;
+    u64* amt;              // amount applied, low word
+    u64* amt_hi;           // high word, written only when non-zero (HZ_AMT_HI)
+    u64* kid;              // create_accounts: dedup key of the id (create_transfers: recomputed from the event)
     u64* kpid;
     u32* dep_list;         // pass-relative: batch k's dependent events at dep_list + (off[k]-e0)
     u32* dep_count;        // per batch (call-relative index - b0)

@@ -1,0 +1,100 @@
+// Host-to-device rates on MI355X for the headline's input path (prepare bodies in host memory):
+//   copy     hipMemcpyAsync from pinned host memory (the runtime's engine choice), one stream
+//   copy2    the same buffer split over two streams
+//   pull<W>  a kernel on W workgroups reading mapped host memory (16 B per lane per load, 8 loads in
+//            flight per lane) and storing to HBM
+// usage: microbench_h2d [MiB]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#define CK(x)                                                                      \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) {                                                    \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                               \
+        }                                                                          \
+    } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void pull(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n) {
+    const size_t stride = (size_t)gridDim.x * 256 * 8;
+    for (size_t base = (size_t)blockIdx.x * 256 * 8 + threadIdx.x; base < n; base += stride) {
+        u32x4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const size_t i = base + (size_t)k * 256;
+            v[k] = i < n ? __builtin_nontemporal_load(&src[i]) : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const size_t i = base + (size_t)k * 256;
+            if (i < n) dst[i] = v[k];
+        }
+    }
+}
+
+int main(int argc, char** argv) {
+    const size_t mib = argc > 1 ? (size_t)atol(argv[1]) : 1024;
+    const size_t bytes = mib << 20;
+    void* h = nullptr;
+    CK(hipHostMalloc(&h, bytes, hipHostMallocMapped));
+    memset(h, 1, bytes);
+    void* hd = nullptr;
+    CK(hipHostGetDevicePointer(&hd, h, 0));
+    void* d = nullptr;
+    CK(hipMalloc(&d, bytes));
+    hipStream_t s[2];
+    CK(hipStreamCreateWithFlags(&s[0], hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&s[1], hipStreamNonBlocking));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    const int reps = 5;
+    auto report = [&](const char* name) {
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        printf("%-10s %8.2f GB/s  (%zu MiB x %d in %.2f ms)\n", name, (double)bytes * reps / (ms * 1e-3) / 1e9, mib, reps,
+               ms);
+    };
+    for (int warm = 0; warm < 2; warm++) {
+        CK(hipEventRecord(a, s[0]));
+        for (int r = 0; r < reps; r++) CK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s[0]));
+        CK(hipEventRecord(b, s[0]));
+        CK(hipEventSynchronize(b));
+    }
+    report("copy");
+    CK(hipEventRecord(a, s[0]));
+    CK(hipStreamWaitEvent(s[1], a, 0));
+    for (int r = 0; r < reps; r++) {
+        CK(hipMemcpyAsync(d, h, bytes / 2, hipMemcpyHostToDevice, s[0]));
+        CK(hipMemcpyAsync((char*)d + bytes / 2, (char*)h + bytes / 2, bytes / 2, hipMemcpyHostToDevice, s[1]));
+    }
+    hipEvent_t c;
+    CK(hipEventCreate(&c));
+    CK(hipEventRecord(c, s[1]));
+    CK(hipStreamWaitEvent(s[0], c, 0));
+    CK(hipEventRecord(b, s[0]));
+    CK(hipEventSynchronize(b));
+    report("copy2");
+    const size_t n = bytes / 16;
+    for (int w : {16, 32, 64, 128, 256, 512}) {
+        for (int warm = 0; warm < 2; warm++) {
+            CK(hipEventRecord(a, s[0]));
+            for (int r = 0; r < reps; r++) hipLaunchKernelGGL(pull, dim3(w), dim3(256), 0, s[0], (const u32x4*)hd, (u32x4*)d, n);
+            CK(hipEventRecord(b, s[0]));
+            CK(hipEventSynchronize(b));
+        }
+        char name[32];
+        snprintf(name, sizeof name, "pull%d", w);
+        report(name);
+    }
+    unsigned char probe[16];
+    CK(hipMemcpy(probe, (char*)d + bytes - 16, 16, hipMemcpyDeviceToHost));
+    printf("check %s\n", probe[0] == 1 && probe[15] == 1 ? "ok" : "BAD");
+    return 0;
+}
