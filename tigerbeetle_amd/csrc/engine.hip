@@ -889,9 +889,9 @@ static int commit_pipelined(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, 
             h_off[k - C.k0 + 1] = h_off[k - C.k0] + lens[k];
             h_ts[k - C.k0] = timestamps[k];
         }
-        // Copy stream: metadata, then the bodies (runs of address-contiguous prepares as one DMA).
+        // Copy stream: the bodies only (runs of address-contiguous prepares as one DMA), back to back;
+        // the chunk's small metadata goes on the engine stream, which has time to spare.
         HIPCK(hipEventRecord(S.start, E->copy_stream));
-        HIPCK(hipMemcpyAsync(S.meta, S.h_meta, (2 * (u64)nb + 1) * 8, hipMemcpyHostToDevice, E->copy_stream));
         for (u32 k = C.k0; k < C.k1;) {
             u32 j = k + 1;
             const u8* base = (const u8*)inputs[k];
@@ -903,6 +903,7 @@ static int commit_pipelined(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, 
         }
         HIPCK(hipEventRecord(S.copied, E->copy_stream));
         // Engine stream: the chunk's passes, then its replies into the pinned arena.
+        HIPCK(hipMemcpyAsync(S.meta, S.h_meta, (2 * (u64)nb + 1) * 8, hipMemcpyHostToDevice, E->stream));
         HIPCK(hipStreamWaitEvent(E->stream, S.copied, 0));
         E->last_batch_ts = timestamps[C.k1 - 1];
         status = enqueue_call(E, op, nb, h_off, S.staging, E->results, E->reply_bytes, false, nullptr, 0, nullptr, S.meta);

@@ -5,6 +5,8 @@
 # separate --pmc passes (they do not fit in one pass on gfx950) over a shorter run of the same
 # configuration (same chunk size, so the same launch shape).  One mode per call:
 #   bash tools/gpu/profile.sh kt|fetch|write      -> gpurun_out/prof/<mode>/
+#   bash tools/gpu/profile.sh mc                  -> memory-copy + kernel trace of one headline step
+#     (the copy engine's timeline: body copies, their gaps, the per-chunk metadata copies)
 #   bash tools/gpu/profile.sh c3|c4               -> kernel trace of `bench.py --workload c3|c4`
 #     (1M accounts, 10M transfers, one timed step from host memory: tb_flow's bounds / sweep / run)
 # (rocprofv3 has written its CSVs when the profiled python exits; a crash after that, in process
@@ -19,6 +21,8 @@ LEG="--cpu-sample 0 --host-prepares 0 --device-steps 0 --secondary 0"
 case $MODE in
   kt) timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 "$R/bench.py" $LEG \
         > "$OUT/bench_kt.log" 2>&1; rc=$? ;;
+  mc) timeout -k 10 420 rocprofv3 --memory-copy-trace --kernel-trace --output-format csv -d "$OUT/mc" -o run -- \
+        python3 "$R/bench.py" $LEG --access-mix 0 --steps 1 --warmup 1 > "$OUT/bench_mc.log" 2>&1; rc=$? ;;
   fetch|write) C=FETCH_SIZE; [ "$MODE" = write ] && C=WRITE_SIZE
       timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/bench.py" $LEG \
         --steps 1 --warmup 0 --transfers 20000000 > "$OUT/$MODE.log" 2>&1; rc=$? ;;

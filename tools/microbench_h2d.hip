@@ -3,6 +3,9 @@
 //   copy2    the same buffer split over two streams
 //   pull<W>  a kernel on W workgroups reading mapped host memory (16 B per lane per load, 8 loads in
 //            flight per lane) and storing to HBM
+//   reg      hipMemcpyAsync from malloc'd memory registered with hipHostRegister (the engine's case)
+//   busy     `copy` while a kernel holding every CU spins on another stream: a copy engine (SDMA)
+//            keeps its rate, a blit kernel waits for CUs
 // usage: microbench_h2d [MiB]
 #include <hip/hip_runtime.h>
 
@@ -36,6 +39,13 @@ __global__ __launch_bounds__(256) void pull(const u32x4* __restrict__ src, u32x4
             if (i < n) dst[i] = v[k];
         }
     }
+}
+
+__global__ __launch_bounds__(256) void spin(unsigned long long cycles, unsigned* sink) {
+    const unsigned long long t0 = clock64();
+    unsigned x = threadIdx.x;
+    while (clock64() - t0 < cycles) x = x * 1664525u + 1013904223u;
+    if (x == 0x12345678u) *sink = x;
 }
 
 int main(int argc, char** argv) {
@@ -92,6 +102,32 @@ int main(int argc, char** argv) {
         char name[32];
         snprintf(name, sizeof name, "pull%d", w);
         report(name);
+    }
+    {
+        void* r = malloc(bytes);
+        memset(r, 1, bytes);
+        CK(hipHostRegister(r, bytes, hipHostRegisterDefault));
+        for (int warm = 0; warm < 2; warm++) {
+            CK(hipEventRecord(a, s[0]));
+            for (int r2 = 0; r2 < reps; r2++) CK(hipMemcpyAsync(d, r, bytes, hipMemcpyHostToDevice, s[0]));
+            CK(hipEventRecord(b, s[0]));
+            CK(hipEventSynchronize(b));
+        }
+        report("reg");
+        // busy: a spinning grid of 8 workgroups per CU on stream 1, the copy on stream 0
+        unsigned* sink = nullptr;
+        CK(hipMalloc(&sink, 4));
+        int cus = 0;
+        CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+        hipLaunchKernelGGL(spin, dim3(cus * 8), dim3(256), 0, s[1], 2000000000ULL, sink);  // ~1 s at 2 GHz
+        CK(hipEventRecord(a, s[0]));
+        for (int r2 = 0; r2 < reps; r2++) CK(hipMemcpyAsync(d, r, bytes, hipMemcpyHostToDevice, s[0]));
+        CK(hipEventRecord(b, s[0]));
+        CK(hipEventSynchronize(b));
+        report("busy");
+        CK(hipStreamSynchronize(s[1]));
+        CK(hipHostUnregister(r));
+        free(r);
     }
     unsigned char probe[16];
     CK(hipMemcpy(probe, (char*)d + bytes - 16, 16, hipMemcpyDeviceToHost));
