@@ -14,12 +14,13 @@ by a barrier + torch.cuda.synchronize(); value = transfers committed by all rank
 (max over ranks).  `device_resident` is the same commit with the prepares already in HBM (the
 engine's own rate, no PCIe); `pcie` is the host-link rate the headline reaches.
 
---gpus N (torchrun): one process per GPU over RCCL (tigerbeetle_amd.sharded).  The
-accounts are replicated (every rank commits the same create_accounts prepares); every rank
-submits its own 100M transfers (global transfer index r*100M + k), and every pass routes each
-transfer to its home GPU (tbgpu_home of its id) with an all-to-all over xGMI, commits it there and
-routes the result codes back.  The global prepare order of a pass is rank-major.  Per-GPU work is
-fixed as N grows: scaling is weak.
+--gpus N (torchrun): BASELINE.json configs[4] ("C5"), one process per GPU over RCCL
+(tigerbeetle_amd.sharded): 100M accounts, whose immutable fields every rank holds and
+whose balances live on their owner GPU (hash of the id); every rank submits its own 125M transfers
+(1B over 8 GPUs) from pinned host memory, and every pass routes each transfer to its home GPU with
+an all-to-all over xGMI, commits it there, sends its balance legs to the accounts' owners (all-to-all)
+and the result codes back to the source (all-to-all).  The global prepare order of a pass is
+rank-major.  Per-GPU work is fixed as N grows: scaling is weak.
 
 The JSON line also carries:
   roofline      the dominant kernel's algorithmic bytes per launch / its average launch time
