@@ -321,6 +321,33 @@ def run_cpu_c1(engine, args):
             "p99_batch_latency_ms": round(ref_percentile(lat, 99), 3)}
 
 
+def bind_local_numa(device):
+    """Run this process on the CPUs of its GPU's NUMA node (those it may use), before the prepare
+    bodies are allocated in host memory: their pages then sit on the socket whose PCIe root the GPU
+    hangs off, and with N ranks each rank's H2D reads its own socket's memory.  Returns the node, or
+    None when the topology is not visible (nothing changes)."""
+    import torch
+    try:
+        p = torch.cuda.get_device_properties(device)
+        bdf = "%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+        with open("/sys/bus/pci/devices/%s/numa_node" % bdf) as f:
+            node = int(f.read())
+        if node < 0:
+            return None
+        cpus = set()
+        with open("/sys/devices/system/node/node%d/cpulist" % node) as f:
+            for part in f.read().strip().split(","):
+                a, _, b = part.partition("-")
+                cpus.update(range(int(a), int(b or a) + 1))
+        allowed = os.sched_getaffinity(0) & cpus
+        if not allowed:
+            return None
+        os.sched_setaffinity(0, allowed)
+        return node
+    except (OSError, ValueError, RuntimeError, AttributeError):
+        return None
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -392,6 +419,7 @@ def main():
         if args.same_device:
             local_rank = 0
         torch.cuda.set_device(local_rank)
+        args.numa_node = bind_local_numa(local_rank)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
@@ -410,6 +438,7 @@ def main():
         return float(t.item())
 
     from tests.harness.configs import KINDS, SETTINGS
+    args.numa_node = bind_local_numa(local_rank)
     from tigerbeetle_amd.state_machine import Engine, Options
 
     wl = SETTINGS[args.workload]
@@ -605,7 +634,7 @@ def main():
         "config": {"workload": WORKLOAD_TEXT[args.workload] % (args.accounts, args.transfers, args.batch),
                    "prepares_per_step": len(xfer_lens), "chunk_prepares": args.chunk_prepares,
                    "input": "prepare bodies in registered host memory; PCIe H2D and reply D2H inside the timed region",
-                   "parallelism": "single"},
+                   "host_numa_node": args.numa_node, "parallelism": "single"},
         "p99_batch_latency_ms": round(ref_percentile(lat, 99), 3),
         "batch_latency_ms": dict(deciles(lat), definition=(
             "per prepare, submit to reply: from the start of its chunk's PCIe copy to its reply landing in host "
@@ -779,6 +808,7 @@ def run_sharded(args, world, rank, local_rank):
                    "prepares_per_step": len(lens) * world, "pass_prepares_per_gpu": args.pass_batches,
                    "input": "prepare bodies in pinned host memory per rank; PCIe H2D inside the timed region, "
                             "overlapped with the previous pass",
+                   "host_numa_node": args.numa_node,
                    "parallelism": "shard%d (events to home GPU, legs to owner GPU, RCCL all-to-all)" % world},
         "pcie": {"achieved_per_gpu": round(pcie_gbs, 2), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
                  "frac": round(pcie_gbs / PCIE_PEAK_GBS, 4), "measured_ceiling": PCIE_MEASURED_GBS,
