@@ -247,14 +247,17 @@ __device__ static inline u64 fl_run_unit(const PassArgs& P, const FlowArgs& F, R
             t.timestamp = ts;
             const u32 info = P.info[pe];
             FastHint hint;
-            const bool fast = m == 1 && (F.uflags[u] & UF_ID_SINGLE) && (info & HZ_SPEC) && (info & HZ_ACCTS) &&
+            // Kernel 1's account slots: a create's two accounts, or a post/void's pending transfer's
+            // (it reached HZ_ACCTS only with that pending from an earlier pass).
+            const bool slots = (info & HZ_ACCTS) != 0;
+            const bool fast = slots && m == 1 && (F.uflags[u] & UF_ID_SINGLE) && (info & HZ_SPEC) &&
                               !(flags & (TF_POST | TF_VOID));
-            if (fast) {
+            if (slots) {
                 hint.drs = P.dr[pe];
                 hint.crs = P.cr[pe];
-                hint.entry = P.rs[pe];
+                hint.entry = fast ? P.rs[pe] : TB_NOT_FOUND;
             }
-            result = rp_create_transfer<true>(R, t, (u32)(R.log_base + pe), fast ? &hint : nullptr);
+            result = rp_create_transfer<true>(R, t, (u32)(R.log_base + pe), slots ? &hint : nullptr);
             if (result == R_OK && !R.failed) tsmax = ts;
         }
         if (R.failed) break;

@@ -46,13 +46,14 @@ struct Replay {
     u64 xcount = 0;
 };
 
-// Flow path, single-event unit whose lookups kernel 1 already did exactly (k_flow.h): the account
-// slots (accounts never change in a create_transfers pass) and the id's absence (its speculative
-// claim was a new entry, and no other dependent event of the pass names this id).  The insert then
-// revives that entry instead of claiming a new one.
+// Flow path: lookups kernel 1 already did exactly (k_flow.h).  The account slots of an event it
+// validated through the account checks (HZ_ACCTS; accounts never change in a create_transfers
+// pass), and — for a single-event unit — the id's absence (its speculative claim was a new entry,
+// and no other dependent event of the pass names this id): the insert then revives that entry
+// instead of claiming a new one.  entry == TB_NOT_FOUND: the slots only (chain members).
 struct FastHint {
     u32 drs, crs;
-    u32 entry;  // index entry claimed by kernel 1 (tombstoned by kernel 2)
+    u32 entry;  // index entry claimed by kernel 1 (tombstoned by kernel 2), or TB_NOT_FOUND
 };
 
 __device__ static inline u64 fl_ld64(const void* p) {
@@ -250,7 +251,7 @@ __device__ static inline void rp_transfer_insert(Replay& R, const Transfer& t, u
 }
 
 template <bool FLOW>
-__device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t, u32 log_pos) {
+__device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t, u32 log_pos, const FastHint* hint = nullptr) {
     const Tables& T = R.T;
     const u16 f = t.flags;
     if ((f & TF_POST) && (f & TF_VOID)) return CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
@@ -266,8 +267,10 @@ __device__ static inline u32 rp_post_or_void(Replay& R, const Transfer& t, u32 l
     if (pslot == TB_NOT_FOUND) return CT_PENDING_TRANSFER_NOT_FOUND;
     const Transfer p = rp_load<FLOW>(&T.xlog[pslot]);
     if (!(p.flags & TF_PENDING)) return CT_PENDING_TRANSFER_NOT_PENDING;
-    const u32 drs = tb_account_find(T, tb_lo(p.debit_account_id), tb_hi(p.debit_account_id));
-    const u32 crs = tb_account_find(T, tb_lo(p.credit_account_id), tb_hi(p.credit_account_id));
+    // hint: the pending transfer's account slots, from kernel 1 (it found the same record: an
+    // earlier pass's, whose id no event of this pass can re-create).
+    const u32 drs = hint ? hint->drs : tb_account_find(T, tb_lo(p.debit_account_id), tb_hi(p.debit_account_id));
+    const u32 crs = hint ? hint->crs : tb_account_find(T, tb_lo(p.credit_account_id), tb_hi(p.credit_account_id));
     if (drs == TB_NOT_FOUND || crs == TB_NOT_FOUND) {
         rp_panic(R, PANIC_ASSERT);
         return R_OK;
@@ -353,7 +356,7 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u3
     if (f & TF_PADDING) return CT_RESERVED_FLAG;
     if (t.id == 0) return CT_ID_MUST_NOT_BE_ZERO;
     if (t.id == TB_U128_MAX) return CT_ID_MUST_NOT_BE_INT_MAX;
-    if (f & (TF_POST | TF_VOID)) return rp_post_or_void<FLOW>(R, t, log_pos);
+    if (f & (TF_POST | TF_VOID)) return rp_post_or_void<FLOW>(R, t, log_pos, hint);
 
     if (t.debit_account_id == 0) return CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
     if (t.debit_account_id == TB_U128_MAX) return CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
@@ -387,7 +390,8 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u3
     if (dh.ledger != ch.ledger) return CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
     if (t.ledger != dh.ledger) return CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
 
-    const u32 es = hint ? TB_NOT_FOUND : rp_transfer_find<FLOW>(T, tb_lo(t.id), tb_hi(t.id));
+    const bool revive = hint && hint->entry != TB_NOT_FOUND;
+    const u32 es = revive ? TB_NOT_FOUND : rp_transfer_find<FLOW>(T, tb_lo(t.id), tb_hi(t.id));
     if (es != TB_NOT_FOUND) return tb_transfer_exists(t, rp_load<FLOW>(&T.xlog[es]));
 
     u128 amount = t.amount;
@@ -435,7 +439,7 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u3
 
     Transfer t2 = t;
     t2.amount = amount;
-    if (hint) {  // revive kernel 1's entry (a single event: no scope to undo)
+    if (revive) {  // revive kernel 1's entry (a single event: no scope to undo)
         rp_store<FLOW>(&R.T.xlog[log_pos], t2);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record before its index entry
         atomicAnd((unsigned long long*)&R.T.xidx[hint->entry], ~(unsigned long long)XI_TOMB);
