@@ -1038,6 +1038,28 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
     return true;
 }
 
+// Exclusive prefix of v over the workgroup, in thread order; `total` = the workgroup's sum.
+__device__ static inline u32 fl_block_excl(u32 v, u32* s_wave, u32& total) {
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u32 x = v;
+#pragma unroll
+    for (u32 off = 1; off < 64; off <<= 1) {
+        const u32 y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) s_wave[wave] = x;
+    __syncthreads();
+    u32 before = 0;
+    total = 0;
+    for (u32 w = 0; w < blockDim.x / 64; w++) {
+        const u32 c = s_wave[w];
+        before += w < wave ? c : 0;
+        total += c;
+    }
+    __syncthreads();
+    return before + x - v;
+}
+
 __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, UndoEntry* seq_undo, u32 seq_undo_cap) {
     __shared__ u32 s_dpre[FLOW_NB_MAX + 1];
     __shared__ u32 s_wave[FLOW_THREADS / 64];
@@ -1067,8 +1089,15 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     __syncthreads();
     tb_block_scan_lds(s_dpre, nb, s_wave);
     const u32 ndep = s_dpre[nb];
-    const u32 N = FLOW_RMAX * ndep;
-    for (u32 f = blockIdx.x * NT + tid; f < ndep; f += G * NT) {
+    // Each workgroup plans a contiguous tile of the flat list; its resource pairs go to FLOW_RMAX
+    // slots per event in keys[1] / vals[1] first, and are compacted (in order) into keys[0] /
+    // vals[0] below, so the sort sees only real pairs (C4: ~1.3 of the 6 slots per event).
+    const u32 ftile = ((ndep + G - 1) / G + NT - 1) / NT * NT;
+    const u32 fa = min(ndep, blockIdx.x * ftile), fb = min(ndep, fa + ftile);
+    u32 my_pairs = 0;
+    for (u32 c0 = fa; c0 < fb; c0 += NT) {
+        const u32 f = c0 + tid;
+        if (f >= fb) break;
         u32 lo = 0, hi = nb;  // the batch k with s_dpre[k] <= f < s_dpre[k + 1]
         while (hi - lo > 1) {
             const u32 mid = (lo + hi) >> 1;
@@ -1119,14 +1148,53 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
         }
         if (!ok) atomicOr(&F.words[FW_SEQ], 1u);
 #pragma unroll
-        for (u32 k = 0; k < FLOW_RMAX; k++) {
-            F.keys[0][FLOW_RMAX * f + k] = k < nk ? keys[k] : FLOW_SENT;
-            F.vals[0][FLOW_RMAX * f + k] = unit;
-        }
+        for (u32 k = 0; k < FLOW_RMAX; k++) F.keys[1][FLOW_RMAX * f + k] = k < nk ? keys[k] : FLOW_SENT;
+        F.vals[1][FLOW_RMAX * f] = unit;
+        my_pairs += nk;
+    }
+    {
+        u32 total;
+        (void)fl_block_excl(my_pairs, s_wave, total);
+        if (tid == 0) F.b_blk[blockIdx.x] = total;
     }
     fl_grid_sync(g, G, gen, F);
     if (fl_stalled(g)) return;
     const bool sequential = *(volatile u32*)&F.words[FW_SEQ] != 0;
+    // Compaction: this workgroup's pairs start after those of the workgroups before it.
+    u32 N = 0, base = 0;
+    for (u32 w = 0; w < G; w++) {
+        const u32 c = (u32)F.b_blk[w];
+        base += w < blockIdx.x ? c : 0;
+        N += c;
+    }
+    if (!sequential) {
+        for (u32 c0 = fa; c0 < fb; c0 += NT) {
+            const u32 f = c0 + tid;
+            u32 kk[FLOW_RMAX], nk = 0;
+            if (f < fb) {
+#pragma unroll
+                for (u32 k = 0; k < FLOW_RMAX; k++) {
+                    kk[k] = F.keys[1][FLOW_RMAX * f + k];
+                    nk += kk[k] != FLOW_SENT ? 1u : 0u;
+                }
+            }
+            u32 total;
+            const u32 at = base + fl_block_excl(nk, s_wave, total);
+            if (nk) {
+                const u32 unit = F.vals[1][FLOW_RMAX * f];
+#pragma unroll
+                for (u32 k = 0; k < FLOW_RMAX; k++) {
+                    if (k < nk) {  // a slot's keys are packed at its front
+                        F.keys[0][at + k] = kk[k];
+                        F.vals[0][at + k] = unit;
+                    }
+                }
+            }
+            base += total;
+        }
+        fl_grid_sync(g, G, gen, F);
+        if (fl_stalled(g)) return;
+    }
     fl_mark(g, tp, FP_PLAN);
 
     if (!sequential) {
