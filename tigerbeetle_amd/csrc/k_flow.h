@@ -255,7 +255,9 @@ __device__ static inline u64 fl_run_unit(const PassArgs& P, const FlowArgs& F, R
             if (slots) {
                 hint.drs = P.dr[pe];
                 hint.crs = P.cr[pe];
-                hint.entry = fast ? P.rs[pe] : TB_NOT_FOUND;
+                hint.entry = (info & HZ_SPEC) ? P.rs[pe] : TB_NOT_FOUND;
+                hint.known_new = fast;
+                hint.rec = (info & HZ_REC) && !(flags & (TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT));
             }
             result = rp_create_transfer<true>(R, t, (u32)(R.log_base + pe), slots ? &hint : nullptr);
             if (result == R_OK && !R.failed) tsmax = ts;

@@ -51,9 +51,13 @@ struct Replay {
 // pass), and — for a single-event unit — the id's absence (its speculative claim was a new entry,
 // and no other dependent event of the pass names this id): the insert then revives that entry
 // instead of claiming a new one.  entry == TB_NOT_FOUND: the slots only (chain members).
+// rec: kernel 1 wrote this event's record at its log position under `entry` (HZ_REC; the record a
+// successful create writes, as it is not balancing): an insert revives `entry`, storing nothing.
 struct FastHint {
     u32 drs, crs;
     u32 entry;  // index entry claimed by kernel 1 (tombstoned by kernel 2), or TB_NOT_FOUND
+    bool known_new = false;  // the id is absent: skip the find, revive `entry`
+    bool rec = false;
 };
 
 __device__ static inline u64 fl_ld64(const void* p) {
@@ -390,7 +394,7 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u3
     if (dh.ledger != ch.ledger) return CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
     if (t.ledger != dh.ledger) return CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
 
-    const bool revive = hint && hint->entry != TB_NOT_FOUND;
+    const bool revive = hint && hint->known_new;
     const u32 es = revive ? TB_NOT_FOUND : rp_transfer_find<FLOW>(T, tb_lo(t.id), tb_hi(t.id));
     if (es != TB_NOT_FOUND) return tb_transfer_exists(t, rp_load<FLOW>(&T.xlog[es]));
 
@@ -439,7 +443,11 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u3
 
     Transfer t2 = t;
     t2.amount = amount;
-    if (revive) {  // revive kernel 1's entry (a single event: no scope to undo)
+    if (hint && hint->rec) {  // the record is in place: revive kernel 1's entry (undone by a tombstone)
+        atomicAnd((unsigned long long*)&R.T.xidx[hint->entry], ~(unsigned long long)XI_TOMB);
+        R.xcount++;  // only the flow path passes a hint
+        rp_push(R, UNDO_TRANSFER_INSERT, hint->entry, nullptr);
+    } else if (revive) {  // revive kernel 1's entry (a single event: no scope to undo)
         rp_store<FLOW>(&R.T.xlog[log_pos], t2);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record before its index entry
         atomicAnd((unsigned long long*)&R.T.xidx[hint->entry], ~(unsigned long long)XI_TOMB);

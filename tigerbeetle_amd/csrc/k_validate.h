@@ -272,7 +272,10 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     // then the timeout check (:862) is the next possible failure.
     const u64 timeout_ns = (u64)t.timeout * 1000000000ULL;
     if (ts + timeout_ns < ts) return CT_OVERFLOWS_TIMEOUT;  // entry withdrawn by kernel 2
-    if ((s.hz & HZ_SPEC) && !TB_ABL(P, ABL_RECORD)) s.rec_ts = ts;
+    if ((s.hz & HZ_SPEC) && !TB_ABL(P, ABL_RECORD)) {
+        s.rec_ts = ts;
+        s.hz |= HZ_REC;
+    }
     return R_OK;
 }
 

@@ -26,6 +26,8 @@ enum : u32 {
     HZ_SELFDEP = 1u << 16,   // kernel 1 already knows the event is dependent (id collision)
     HZ_PV_KEY = 1u << 17,    // post/void: pending id registered in the pass pending set
     HZ_AMT_HI = 1u << 18,    // amt_hi[] holds the amount's high word (else it is zero, not written)
+    HZ_REC = 1u << 19,       // kernel 1 wrote the event's record (timestamped, amount as given) at
+                             // log_base + event, under its claimed entry rs[]
 };
 
 #define SUM_SHARDS 64
