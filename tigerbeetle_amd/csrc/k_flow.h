@@ -43,6 +43,8 @@ enum : u32 { FW_NUNITS = 0, FW_QTAIL = 1, FW_SEQ = 2, FW_BNO = 3, FW_BUND = 4, F
 enum : u32 {
     UF_ID_SINGLE = 1,  // the unit is the only dependent event of the pass whose id has its key
     UF_ID_UNIQUE = 2,  // ... or the others sharing the key (a 31-bit hash) name different ids
+    UF_MEMBER_NEW = 4, // per flat entry f (any member of a unit): no other dependent event of the
+                       // pass has f's own id key (its id is new if kernel 1's claim was: HZ_SPEC)
 };
 
 // Everything a run needs of the unit at sorted position q, packed by the planner so the run walker
@@ -250,8 +252,8 @@ __device__ static inline u64 fl_run_unit(const PassArgs& P, const FlowArgs& F, R
             // Kernel 1's account slots: a create's two accounts, or a post/void's pending transfer's
             // (it reached HZ_ACCTS only with that pending from an earlier pass).
             const bool slots = (info & HZ_ACCTS) != 0;
-            const bool fast = slots && m == 1 && (F.uflags[u] & UF_ID_SINGLE) && (info & HZ_SPEC) &&
-                              !(flags & (TF_POST | TF_VOID));
+            const bool fast = slots && (info & HZ_SPEC) && !(flags & (TF_POST | TF_VOID)) &&
+                              ((m == 1 && (F.uflags[u] & UF_ID_SINGLE)) || (F.uflags[f] & UF_MEMBER_NEW));
             if (slots) {
                 hint.drs = P.dr[pe];
                 hint.crs = P.cr[pe];
@@ -1141,6 +1143,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
         const u16 fl = P.eflags[pe];
         const u32 info = P.info[pe];
         keys[nk++] = fl_key_id(tb_lo(ev->id), tb_hi(ev->id));
+        F.b_qd[f] = keys[0];  // own id key, for the link phase's UF_MEMBER_NEW (the sweep reuses b_qd)
         if (fl & (TF_POST | TF_VOID)) {
             keys[nk++] = fl_key_id(tb_lo(ev->pending_id), tb_hi(ev->pending_id));
             ok = ok && fl_pending_accounts(P, tb_lo(ev->pending_id), tb_hi(ev->pending_id), cert_global, keys, nk);
@@ -1301,7 +1304,15 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
             if (key == FLOW_SENT) continue;
             const bool first = q == 0 || K[q - 1] != key;
             const u32 u = V[q];
-            if (first && (key & 0x80000000u) && (q + 1 == N || K[q + 1] != key)) atomicOr(&F.uflags[u], UF_ID_SINGLE);
+            if (first && (key & 0x80000000u) && (q + 1 == N || K[q + 1] != key)) {
+                atomicOr(&F.uflags[u], UF_ID_SINGLE);
+                // Which member's own id is it (not a post/void's pending id)?  b_qd holds each
+                // entry's own id key until the sweep (plan 1).
+                const u32 m = F.f_len[u];
+                for (u32 j = 0; j < m; j++) {
+                    if (F.b_qd[u + j] == key) atomicOr(&F.uflags[u + j], UF_MEMBER_NEW);
+                }
+            }
             if ((key & 0x80000000u) && !(first && (q + 1 == N || K[q + 1] != key))) {
                 // A key shared by several units: a hash collision of different ids only orders them;
                 // the id is unique if no other unit of the run names the same one.

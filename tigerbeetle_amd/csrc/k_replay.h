@@ -447,11 +447,12 @@ __device__ static inline u32 rp_create_transfer(Replay& R, const Transfer& t, u3
         atomicAnd((unsigned long long*)&R.T.xidx[hint->entry], ~(unsigned long long)XI_TOMB);
         R.xcount++;  // only the flow path passes a hint
         rp_push(R, UNDO_TRANSFER_INSERT, hint->entry, nullptr);
-    } else if (revive) {  // revive kernel 1's entry (a single event: no scope to undo)
+    } else if (revive) {  // the id is new: store the record, revive kernel 1's entry
         rp_store<FLOW>(&R.T.xlog[log_pos], t2);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record before its index entry
         atomicAnd((unsigned long long*)&R.T.xidx[hint->entry], ~(unsigned long long)XI_TOMB);
         R.xcount++;  // only the flow path passes a hint
+        rp_push(R, UNDO_TRANSFER_INSERT, hint->entry, nullptr);
     } else {
         rp_transfer_insert<FLOW>(R, t2, log_pos);
     }
