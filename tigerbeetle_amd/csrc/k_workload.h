@@ -195,8 +195,8 @@ __global__ void tb_gen_transfers(u8* out, u64 count, WorkloadParams W) {
 // ---- the memory-access mix of tb_transfers_validate (bench only) ---------------------------------
 // tbgpu_bench_access_mix: the accesses kernel 1 makes per transfer, without its logic, on scratch
 // buffers sized like the engine's tables — what the hardware does for this pattern is the kernel's
-// practical bound.  STREAM: the 128-B event in, the 128-B record and 42 B of
-// per-event results out; PROBE: two random 32-B rows of an account-table-sized array; CAS: one
+// practical bound.  STREAM: the 128-B event in, the 128-B record and 26 B of
+// per-event results out (info, flags, dr, cr, rs, amount low word); PROBE: two random 32-B rows of an account-table-sized array; CAS: one
 // random 8-B CAS into an index-sized array.
 enum : u32 { MIX_STREAM = 1, MIX_PROBE = 2, MIX_CAS = 4 };
 struct MixArgs {
@@ -204,7 +204,7 @@ struct MixArgs {
     uint4* records;
     u32* s4;             // 4 arrays of n u32 (info, dr, cr, rs)
     unsigned short* s2;  // flags
-    u64* s8;             // 3 arrays of n u64 (amount lo, hi, key)
+    u64* s8;             // n u64 (amount low word)
     const uint4* rows;   // 32-B rows
     u64 row_mask;
     u64* index;
@@ -240,9 +240,7 @@ __global__ __launch_bounds__(256) void tb_access_mix(MixArgs A) {
         A.s4[2 * A.n + i] = (u32)(h >> 8);
         A.s4[3 * A.n + i] = (u32)(h >> 16);
         A.s2[i] = (unsigned short)h;
-        A.s8[i] = h;
-        A.s8[A.n + i] = 0;
-        A.s8[2 * A.n + i] = acc;
+        A.s8[i] = h ^ acc;
     } else if (acc == 0x123456789ULL) {
         A.sink[0] = acc;
     }
