@@ -220,16 +220,28 @@ __device__ static inline u64 fl_run_unit(const PassArgs& P, const FlowArgs& F, R
     R.scope = false;
     u64 tsmax = 0;
     bool in_chain = false, broken = false;
+    // A member's words are loaded together, one level after its flat-list entry, and the next
+    // member's entry is loaded with them (a chain's members then cost one round trip less each).
+    u32 pe_next = F.f_pe[u], b_next = F.f_batch[u];
     for (u32 j = 0; j < m && !R.failed; j++) {
         const u32 f = u + j;
-        const u32 pe = F.f_pe[f];
-        const u32 b = F.f_batch[f];
+        const u32 pe = pe_next;
+        const u32 b = b_next;
+        if (j + 1 < m) {
+            pe_next = F.f_pe[f + 1];
+            b_next = F.f_batch[f + 1];
+        }
+        const u8* ev = P.events + (P.e0 + pe) * 128;
         const u64 boff = P.batch_off[b];
-        const u32 L = (u32)(P.batch_off[b + 1] - boff);
-        const u32 i = (u32)(P.e0 + pe - boff);
-        const u8* ev = P.events + (boff + i) * 128;
+        const u64 bend = P.batch_off[b + 1];
         const u16 flags = P.eflags[pe];
-        const u64 evts = P.routed ? 0 : *(const u64*)(ev + 120);
+        const u32 info = P.info[pe];
+        const u32 w_dr = P.dr[pe], w_cr = P.cr[pe], w_rs = P.rs[pe];
+        const u32 uf = F.uflags[f];
+        Transfer t = *(const Transfer*)ev;
+        const u32 L = (u32)(bend - boff);
+        const u32 i = (u32)(P.e0 + pe - boff);
+        const u64 evts = P.routed ? 0 : t.timestamp;
         const bool linked = flags & TF_LINKED;
         u32 result;
         if (linked && !in_chain) {
@@ -245,19 +257,17 @@ __device__ static inline u64 fl_run_unit(const PassArgs& P, const FlowArgs& F, R
             result = R_TIMESTAMP_MUST_BE_ZERO;
         } else {
             const u64 ts = tb_event_ts(P, b, boff, L, i);
-            Transfer t = *(const Transfer*)ev;
             t.timestamp = ts;
-            const u32 info = P.info[pe];
             FastHint hint;
             // Kernel 1's account slots: a create's two accounts, or a post/void's pending transfer's
             // (it reached HZ_ACCTS only with that pending from an earlier pass).
             const bool slots = (info & HZ_ACCTS) != 0;
             const bool fast = slots && (info & HZ_SPEC) && !(flags & (TF_POST | TF_VOID)) &&
-                              ((m == 1 && (F.uflags[u] & UF_ID_SINGLE)) || (F.uflags[f] & UF_MEMBER_NEW));
+                              ((m == 1 && (uf & UF_ID_SINGLE)) || (uf & UF_MEMBER_NEW));
             if (slots) {
-                hint.drs = P.dr[pe];
-                hint.crs = P.cr[pe];
-                hint.entry = (info & HZ_SPEC) ? P.rs[pe] : TB_NOT_FOUND;
+                hint.drs = w_dr;
+                hint.crs = w_cr;
+                hint.entry = (info & HZ_SPEC) ? w_rs : TB_NOT_FOUND;
                 hint.known_new = fast;
                 hint.rec = (info & HZ_REC) && !(flags & (TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT));
             }
@@ -273,8 +283,7 @@ __device__ static inline u64 fl_run_unit(const PassArgs& P, const FlowArgs& F, R
                 *w = (*w & 0xFFFFFF00u) | R_LINKED_EVENT_FAILED;
             }
         }
-        u32* w = &P.info[pe];
-        *w = (*w & 0xFFFFFF00u) | result;
+        P.info[pe] = (info & 0xFFFFFF00u) | result;  // only this lane writes it from here
         if (in_chain && (!linked || result == R_LINKED_EVENT_CHAIN_OPEN)) {
             if (!broken) rp_scope_close<true>(R, true);
             in_chain = false;
