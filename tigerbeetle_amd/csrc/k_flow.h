@@ -37,6 +37,12 @@
 #define FLOW_CHAIN_MAX 64       // longer chains: sequential replay
 #define FLOW_NB_MAX 4096        // prepares per pass the planner handles (LDS prefix)
 #define FLOW_SENT 0xFFFFFFFFu   // empty pair slot
+#ifndef FLOW_POLL_SLEEP
+#define FLOW_POLL_SLEEP 16      // s_sleep units (64 cycles) between a waiting lane's polls
+#endif
+#ifndef FLOW_POLL_DONE
+#define FLOW_POLL_DONE 32       // a waiting lane reads the done counter every this many polls
+#endif
 
 enum : u32 { FW_NUNITS = 0, FW_QTAIL = 1, FW_SEQ = 2, FW_BNO = 3, FW_BUND = 4, FW_BDEC = 5,  // 5, 6, 7
              FW_QHEAD = 8, FW_DONE = 9, FW_WORDS = FLOW_WORDS };
@@ -1466,13 +1472,19 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
                                      ? __hip_atomic_load(&F.queue[ticket], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                      : 0;
                 if (item == 0) {
-                    if (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nunits) break;
+                    // A waiting lane polls its queue slot, and the done counter only every
+                    // FLOW_POLL_DONE-th time, sleeping between polls: the polls of idle waves
+                    // otherwise crowd the lines the running units' atomics need.
+                    if (spins % FLOW_POLL_DONE == 0 &&
+                        __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nunits) {
+                        break;
+                    }
                     if (spins++ == 0) w0 = fl_now();
                     if (spins % 256 == 0 && (fl_expired(F, w0) || fl_stalled(g))) {
                         tb_panic(g, PANIC_FLOW_STALL);
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(2);
+                    __builtin_amdgcn_s_sleep(FLOW_POLL_SLEEP);
                     continue;
                 }
                 spins = 0;
