@@ -452,7 +452,9 @@ __device__ static inline void fl_finish(const PassArgs& P, u8* s_code, u32* s_wa
 // with nothing changed.
 #define FLOW_BOUNDS_ROUNDS_MAX 4096
 // A scan round costs about as much as sweeping this many units in order (fl_sweep).
+#ifndef FLOW_SWEEP_MIN
 #define FLOW_SWEEP_MIN 512
+#endif
 enum : u8 { BS_UNK = 0, BS_OK = 1, BS_FAIL_CREDITS = 2, BS_FAIL_DEBITS = 3, BS_FAIL_STATIC = 4 };
 enum : u8 { BV_UNK = 0, BV_PASS = 1, BV_FAIL = 2 };
 enum : u32 { BT_NONE = 0, BT_X = 1, BT_Y = 2, BT_CR = 4 };  // X: checked side (any field); Y: other side, posted
