@@ -344,7 +344,7 @@ def bind_local_numa(device):
             return None
         os.sched_setaffinity(0, allowed)
         return node
-    except (OSError, ValueError, RuntimeError, AttributeError):
+    except (OSError, ValueError, RuntimeError, AttributeError, AssertionError):
         return None
 
 
