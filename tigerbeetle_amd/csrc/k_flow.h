@@ -17,13 +17,16 @@
 // :661-692) or a single event.  Two units that share a resource run in batch order; units that
 // share none commute.  The kernel:
 //   plan   every workgroup: list the pass's dependent events in order, emit (resource key, unit)
-//          pairs, radix-sort them by key (stable, so each key's units stay in batch order) and
-//          link every unit to its successor on each of its resources (need[] = predecessors);
-//   run    workgroup 0, 1024 lanes: a ticket queue of ready units; a lane executes its unit with
-//          the reference logic, then releases its successors, queueing those with no
-//          predecessor left.  The result equals the sequential replay's: every unit sees exactly
-//          the effects of the units before it on its resources, and nothing else it reads can
-//          differ.
+//          pairs, compact them in order, radix-sort them by key (stable, so each key's units stay
+//          in batch order) and link every unit to its successor on each of its resources
+//          (need[] = predecessors);
+//   bounds a pass whose dependent units are plain limit checks is decided by segmented-scan
+//          rounds and an in-order sweep instead of a run (fl_bounds, fl_sweep);
+//   run    every lane of every workgroup: one ticket queue of ready units in global memory; a
+//          lane executes its unit with the reference logic, then releases its successors,
+//          queueing those with no predecessor left.  The result equals the sequential replay's:
+//          every unit sees exactly the effects of the units before it on its resources, and
+//          nothing else it reads can differ.
 // Grid-wide phases are separated by a counter barrier (cooperative launch: every workgroup is
 // resident).  Cases the planner does not cover (a chain longer than FLOW_CHAIN_MAX, a pending id
 // whose creator in this pass is ambiguous) set a flag, and workgroup 0 runs the sequential replay

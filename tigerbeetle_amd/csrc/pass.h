@@ -6,9 +6,12 @@
 //      dedup-set inserts, balancing marks and the overflow-certificate sum S.
 //   2. tb_resolve<op>                     one workgroup per prepare: dependence classification,
 //      linked-chain resolution, in-place apply of independent ok events, sparse replies.
-//   3. tb_replay<op>                      one workgroup: the ordered fallback — replays the
-//      dependent events in batch order with the reference logic and an undo log, then writes
-//      the replies of the prepares that had dependent events.
+//   2b. tb_apply_legs                     one workgroup per account bucket: the legs of the
+//      independent ok transfers summed per account (k_apply.h).
+//   3. tb_flow (create_transfers)         the ordered fallback in parallel over the co-resident
+//      grid (k_flow.h); tb_replay<op> (one workgroup) replays create_accounts passes and engines
+//      whose balances were set directly.  Either writes the replies of the prepares that had
+//      dependent events.
 #pragma once
 
 #include "tb_device.h"
