@@ -809,12 +809,19 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
 }
 
 // No-return add of v to the low word at p (p == nullptr: nothing) for every lane of the wave; lanes
-// naming the word of one of the first two leaders add their sum with a single atomic.
+// naming the same word add their sum with a single atomic.
+#ifndef FL_ADD_ROUNDS
+#define FL_ADD_ROUNDS 16
+#endif
 __device__ static inline void fl_add_lo(u64* p, u64 v) {
     const u32 lane = threadIdx.x & 63;
     bool left = p != nullptr;
-#pragma unroll
-    for (int r = 0; r < 2; r++) {
+    // Leader by leader (the lowest lane still left), up to FL_ADD_ROUNDS of them: a lone lane adds
+    // its own value, a group its wave sum.  Stopping at the first lone leader (a cold account in
+    // lane 0 is the common case under Zipf) left the hot words' lanes to add one by one, and
+    // thousands of same-address atomics per pass serialise (C3's bounds apply: 0.15 ms per chunk).
+#pragma unroll 1
+    for (int r = 0; r < FL_ADD_ROUNDS; r++) {
         const u64 live = __ballot(left);
         if (!live) return;
         const u32 l = (u32)__builtin_ctzll(live);
@@ -822,10 +829,11 @@ __device__ static inline void fl_add_lo(u64* p, u64 v) {
                          (u32)__builtin_amdgcn_readlane((u32)(uintptr_t)p, l);
         const bool mine = left && (u64)(uintptr_t)p == lead;
         const u64 group = __ballot(mine);
-        if (__popcll(group) < 2) break;
         u64 part = mine ? v : 0;
+        if (__popcll(group) > 1) {
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) part += __shfl_xor((unsigned long long)part, off);
+            for (int off = 32; off > 0; off >>= 1) part += __shfl_xor((unsigned long long)part, off);
+        }
         if (lane == l) tb_atomic_add_lo_noret(p, part);
         left = left && !mine;
     }
