@@ -88,6 +88,7 @@ struct tbgpu {
     u64* leg_ev = nullptr;
     u64* leg_w = nullptr;
     u32* leg_off = nullptr;
+    u32* leg_tot = nullptr;  // [leg_buckets] legs per bucket of the current pass
     // Parallel ordered fallback (k_flow.h): create_transfers passes run tb_flow instead of
     // tb_replay while no balance was set directly (the post/void assert argument, k_replay.h).
     bool flow_ok = false;
@@ -376,6 +377,8 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         INIT_CK(hipMalloc(&E->leg_ev, pe * 2 * 8));
         INIT_CK(hipMalloc(&E->leg_w, pe * 2 * 8));
         INIT_CK(hipMalloc(&E->leg_off, (u64)std::min<u32>(E->pb_max, LEG_PREPARES_MAX) * (E->leg_buckets + 1) * 4));
+        INIT_CK(hipMalloc(&E->leg_tot, (u64)std::max<u32>(1, E->leg_buckets) * 4));
+        INIT_CK(hipMemset(E->leg_tot, 0, (u64)std::max<u32>(1, E->leg_buckets) * 4));
     }
     if (E->flow_ok) {
         FlowArgs& F = E->F;
@@ -460,7 +463,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->cr, E->ps, E->rs, E->dep_list, E->dep_count, E->amt, E->kid, E->kpid, E->dedup,
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
                     E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->r_home,
-                    E->r_block_counts, E->r_words, E->r_meta, E->leg_ev, E->leg_w, E->leg_off,
+                    E->r_block_counts, E->r_words, E->r_meta, E->leg_ev, E->leg_w, E->leg_off, E->leg_tot,
                     E->F.f_pe, E->F.f_batch, E->F.f_len, E->F.need, E->F.nsucc, E->F.queue, E->F.uflags, E->F.nacct, E->F.rpos, E->F.succ,
                     E->F.run, E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo,
                     E->F.b_st, E->F.b_vd, E->F.b_vc, E->F.b_amt, E->F.b_meta, E->F.b_blk,
@@ -574,6 +577,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.leg_ev = E->leg_ev;
         P.leg_w = E->leg_w;
         P.leg_off = E->leg_off;
+        P.leg_tot = E->leg_tot;
         const bool flow = op == OP_CREATE_TRANSFERS && E->flow_ok && !E->balances_set && !(E->ablate & ABL_FLOW) &&
                           b1 - b0 <= FLOW_NB_MAX;
         P.flow_words = E->flow_ok ? E->F.words : nullptr;
@@ -588,7 +592,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         const u64 clear_n = E->dedup_force ? E->dedup_cap : E->dedup_prev;
         const u32 clear_grid = (u32)std::min<u64>(1024, std::max<u64>(1, clear_n / 2048));
         hipLaunchKernelGGL(tb_pass_clear, dim3(clear_grid), dim3(256), 0, E->stream, E->dedup, E->dedup_cap, E->sum_shards,
-                           E->g, E->epoch, E->dedup_force ? 1u : 0u);
+                           E->g, E->epoch, E->dedup_force ? 1u : 0u, E->leg_tot, E->leg_buckets);
         HIPCK(hipGetLastError());
         E->dedup_force = false;
         E->dedup_prev = P.dedup_mask + 1;
@@ -624,7 +628,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         if (P.legs || P.apply_late) {
             if ((st = prof_begin(E, &pp, K_APPLY))) return st;
             if (P.legs) {
-                hipLaunchKernelGGL(tb_apply_legs, dim3(E->leg_buckets), dim3(APPLY_THREADS), (4u << E->leg_shift) * 8,
+                hipLaunchKernelGGL(tb_apply_legs, dim3(E->leg_buckets + APPLY_EXTRA), dim3(APPLY_THREADS), (4u << E->leg_shift) * 8,
                                    E->stream, P);
             } else if (n > 0 && !owner) {  // owner-partitioned: the owners apply the legs instead
                 hipLaunchKernelGGL(tb_apply_events, dim3((u32)((n + 255) / 256)), dim3(256), 0, E->stream, P);

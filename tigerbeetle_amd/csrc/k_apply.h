@@ -16,22 +16,27 @@
 
 #include "k_resolve.h"
 
+#define APPLY_HEAVY (16 * 4 * APPLY_THREADS)  // a range this long: 16 loads in flight, hot word in registers
+#define APPLY_PART 32768                      // legs per part of a split bucket
+#define APPLY_SPLIT_MIN (2 * APPLY_PART)      // buckets at least this heavy are split
+#define APPLY_EXTRA 64                        // extra workgroups of tb_apply_legs for the parts
+
 // Gather of one bucket's legs: consecutive legs of a segment go to consecutive lanes (coalesced
 // reads), Q legs per thread in flight before their LDS adds (a heavy, Zipf-hot bucket keeps more in
 // flight).  A thread's legs j only grow, so the prepare holding j is searched for only past the
 // last one, and not at all while j stays in it (one LDS read: the common case in a heavy bucket,
 // whose binary searches per leg serialised the loads).
 template <u32 Q>
-__device__ static inline void tb_gather_legs(const PassArgs& P, u32 total, u32 nb_, const u32* s_start, const u32* s_pref,
+__device__ static inline void tb_gather_legs(const PassArgs& P, u32 jb, u32 je, u32 nb_, const u32* s_start, const u32* s_pref,
                                              u64* s_acc, u32 hot_key = 0xFFFFFFFFu, u64* hot = nullptr) {
     u32 lo = 0;  // the last prepare whose segment starts at or before this thread's current leg
-    for (u32 j0 = 0; j0 < total; j0 += Q * APPLY_THREADS) {
+    for (u32 j0 = jb; j0 < je; j0 += Q * APPLY_THREADS) {
         u64 w[Q];
 #pragma unroll
         for (u32 q = 0; q < Q; q++) {
             const u32 j = j0 + q * APPLY_THREADS + threadIdx.x;
             w[q] = 0;
-            if (j < total) {
+            if (j < je) {
                 if (s_pref[lo + 1] <= j) {  // past this prepare: binary search in the ones after it
                     u32 b = nb_;
                     lo++;
@@ -53,24 +58,114 @@ __device__ static inline void tb_gather_legs(const PassArgs& P, u32 total, u32 n
     }
 }
 
+// Legs [jb, je) of the bucket into s_acc.  A heavy range's most frequent (slot, field) word among 256
+// legs spread over it (counted in s_acc, still zero) is summed in registers, then added once: LDS
+// atomics on one word serialise.
+__device__ static inline void tb_gather_range(const PassArgs& P, u32 jb, u32 je, u32 nb, const u32* s_start,
+                                              const u32* s_pref, u64* s_acc, u64* s_red) {
+    if (je - jb < APPLY_HEAVY) {
+        tb_gather_legs<4>(P, jb, je, nb, s_start, s_pref, s_acc);
+        __syncthreads();
+        return;
+    }
+    const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const u32 j = jb + (u32)((u64)tid * (je - jb) / APPLY_THREADS);
+    u32 p = 0;
+    while (s_pref[p + 1] <= j) p++;
+    const u32 key = (u32)(P.leg_w[(u64)s_start[p] + (j - s_pref[p])] >> LEG_AMT_BITS);
+    const u64 before = s_acc[key];  // an earlier range's sum (the counts are taken off again below)
+    __syncthreads();
+    atomicAdd((unsigned long long*)&s_acc[key], 1ULL);
+    __syncthreads();
+    u64 best = ((s_acc[key] - before) << 32) | key;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) best = max(best, (u64)__shfl_xor((unsigned long long)best, off));
+    if (lane == 0) s_red[wave] = best;
+    __syncthreads();
+    best = 0;
+    for (u32 k = 0; k < APPLY_THREADS / 64; k++) best = max(best, s_red[k]);
+    atomicAdd((unsigned long long*)&s_acc[key], ~0ULL);  // take this thread's count off again
+    __syncthreads();
+    const u32 hot_key = (u32)best;
+    u64 hot = 0;
+    tb_gather_legs<16>(P, jb, je, nb, s_start, s_pref, s_acc, hot_key, &hot);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) hot += __shfl_xor((unsigned long long)hot, off);
+    if (lane == 0) s_red[wave] = hot;
+    __syncthreads();
+    if (tid == 0) {
+        u64 v = 0;
+        for (u32 k = 0; k < APPLY_THREADS / 64; k++) v += s_red[k];
+        s_acc[hot_key] += v;
+    }
+    __syncthreads();
+}
+
+// Extra legs of a heavy bucket b (one of APPLY_PART legs beyond its first part), counted over the
+// buckets before it: the extra workgroups take them in this order.
+__device__ static inline u32 tb_bucket_extras(u32 total) {
+    return total >= APPLY_SPLIT_MIN ? (total - 1) / APPLY_PART : 0u;
+}
+
+// grid = leg_buckets + APPLY_EXTRA.  Workgroup g < leg_buckets owns bucket g.  A bucket with at least
+// APPLY_SPLIT_MIN legs (a Zipf-hot account's) is cut into parts of APPLY_PART legs: its owner takes
+// part 0, the extra workgroups take the others in bucket order (the owner also takes any the
+// extras cannot), and every workgroup of a split bucket adds its sums with atomics (no carry under
+// the certificate).  Every other bucket is summed by its owner alone and written back with plain
+// read-modify-writes.
 __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
     extern __shared__ u64 s_acc[];                  // [4 << leg_shift] per (slot, field) sum (dynamic)
     __shared__ u32 s_start[LEG_PREPARES_MAX];       // the bucket's first leg in each prepare
     __shared__ u32 s_pref[LEG_PREPARES_MAX + 1];    // exclusive prefix of the segment lengths
     __shared__ u32 s_wave[APPLY_THREADS / 64];
+    __shared__ u64 s_red[APPLY_THREADS / 64];
+    __shared__ u32 s_pick[3];                       // extra workgroup: bucket, part; owner: its first extra index
 
     u128 S;
     bool cert_global, cert64;
     tb_pass_cert(P, S, cert_global, cert64);
     if (!cert64 || TB_ABL(P, ABL_LEG_WORK)) return;  // the resolve kernel applied every leg with u128 atomics
 
-    const u32 g = blockIdx.x;
+    const u32 NBK = P.leg_buckets;
+    const bool owner = blockIdx.x < NBK;
+    u32 g = blockIdx.x, part = 0, first_extra = 0;
+    const u32 tot_g = owner ? P.leg_tot[g] : 0u;
+    if (!owner || tb_bucket_extras(tot_g)) {
+        // Extra-part numbering over the buckets in order: a block scan of each bucket's extras.
+        const u32 per = (NBK + APPLY_THREADS - 1) / APPLY_THREADS;
+        const u32 k0 = min(NBK, threadIdx.x * per), k1 = min(NBK, k0 + per);
+        u32 local = 0;
+        for (u32 k = k0; k < k1; k++) local += tb_bucket_extras(P.leg_tot[k]);
+        u32 all;
+        u32 run = tb_block_excl_sum(local, s_wave, &all);
+        const u32 e = blockIdx.x - NBK;  // this extra workgroup's part index (when !owner)
+        if (threadIdx.x == 0) s_pick[0] = 0xFFFFFFFFu;
+        __syncthreads();
+        for (u32 k = k0; k < k1; k++) {
+            const u32 x = tb_bucket_extras(P.leg_tot[k]);
+            if (owner && k == g) s_pick[2] = run;
+            if (!owner && e >= run && e < run + x) {
+                s_pick[0] = k;
+                s_pick[1] = e - run + 1;
+            }
+            run += x;
+        }
+        __syncthreads();
+        if (!owner) {
+            if (s_pick[0] == 0xFFFFFFFFu) return;  // more extra workgroups than extra parts
+            g = s_pick[0];
+            part = s_pick[1];
+        } else {
+            first_extra = s_pick[2];
+        }
+    }
+
     const u32 W = 1u << P.leg_shift;
     const u32 nb = P.b1 - P.b0;
-    const u32 stride = P.leg_buckets + 1;
+    const u32 stride = NBK + 1;
     for (u32 k = threadIdx.x; k < 4 * W; k += APPLY_THREADS) s_acc[k] = 0;
 
-    // Segment of this bucket in every prepare of the pass; each thread owns a run of prepares.
+    // Segment of bucket g in every prepare of the pass; each thread owns a run of prepares.
     const u32 per = (nb + APPLY_THREADS - 1) / APPLY_THREADS;
     const u32 p0 = min(nb, threadIdx.x * per), p1 = min(nb, p0 + per);
     u32 local = 0;
@@ -91,50 +186,27 @@ __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
     if (threadIdx.x == 0) s_pref[nb] = total;
     __syncthreads();
 
-    // Gather (tb_gather_legs).
-    if (total < 16 * 4 * APPLY_THREADS) {
-        tb_gather_legs<4>(P, total, nb, s_start, s_pref, s_acc);
-        __syncthreads();
-    } else {
-        // A heavy bucket: its most frequent (slot, field) word among 256 legs spread over it (counted
-        // in s_acc, still zero) is summed in registers, then added once.
-        __shared__ u64 s_red[APPLY_THREADS / 64];
-        const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-        const u32 j = (u32)((u64)tid * total / APPLY_THREADS);
-        u32 p = 0;
-        while (s_pref[p + 1] <= j) p++;
-        const u32 key = (u32)(P.leg_w[(u64)s_start[p] + (j - s_pref[p])] >> LEG_AMT_BITS);
-        atomicAdd((unsigned long long*)&s_acc[key], 1ULL);
-        __syncthreads();
-        u64 best = (s_acc[key] << 32) | key;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) best = max(best, (u64)__shfl_xor((unsigned long long)best, off));
-        if (lane == 0) s_red[wave] = best;
-        __syncthreads();
-        best = 0;
-        for (u32 k = 0; k < APPLY_THREADS / 64; k++) best = max(best, s_red[k]);
-        s_acc[key] = 0;
-        __syncthreads();
-        const u32 hot_key = (u32)best;
-        u64 hot = 0;
-        tb_gather_legs<16>(P, total, nb, s_start, s_pref, s_acc, hot_key, &hot);
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) hot += __shfl_xor((unsigned long long)hot, off);
-        if (lane == 0) s_red[wave] = hot;
-        __syncthreads();
-        if (tid == 0) {
-            u64 v = 0;
-            for (u32 k = 0; k < APPLY_THREADS / 64; k++) v += s_red[k];
-            s_acc[hot_key] += v;
+    const u32 extras = tb_bucket_extras(total);
+    if (!extras) {
+        tb_gather_range(P, 0, total, nb, s_start, s_pref, s_acc, s_red);
+        // Write back: thread k -> (slot k/4, field k%4), consecutive threads on consecutive 16-B fields.
+        u8* bal = (u8*)(P.T.acct_bal + (u64)g * W);
+        for (u32 k = threadIdx.x; k < 4 * W; k += APPLY_THREADS) {
+            const u64 v = s_acc[k];
+            if (v != 0) *(u64*)(bal + (u64)k * 16) += v;  // low word: no carry under the certificate
         }
-        __syncthreads();
+        return;
     }
-
-    // Write back: thread k -> (slot k/4, field k%4), consecutive threads on consecutive 16-B fields.
+    // A split bucket: this workgroup's parts, then atomic adds of its sums.
+    for (u32 q = 0; q <= extras; q++) {
+        const bool mine = owner ? (q == 0 || first_extra + q - 1 >= APPLY_EXTRA) : q == part;
+        if (!mine) continue;
+        tb_gather_range(P, q * APPLY_PART, min(total, (q + 1) * APPLY_PART), nb, s_start, s_pref, s_acc, s_red);
+    }
     u8* bal = (u8*)(P.T.acct_bal + (u64)g * W);
     for (u32 k = threadIdx.x; k < 4 * W; k += APPLY_THREADS) {
         const u64 v = s_acc[k];
-        if (v != 0) *(u64*)(bal + (u64)k * 16) += v;  // low word: no carry under the certificate
+        if (v != 0) tb_atomic_add_lo_noret(bal + (u64)k * 16, v);
     }
 }
 

@@ -139,7 +139,11 @@ __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 L, 
     const u16* h = (const u16*)s_hist;
     const u32 nlegs = h[P.leg_buckets];
     u32* row = P.leg_off + (u64)blockIdx.x * (P.leg_buckets + 1);
-    for (u32 k = threadIdx.x; k <= P.leg_buckets; k += blockDim.x) row[k] = h[k];
+    for (u32 k = threadIdx.x; k <= P.leg_buckets; k += blockDim.x) {
+        row[k] = h[k];
+        // The pass's legs per bucket: tb_apply_legs splits a Zipf-heavy bucket over workgroups.
+        if (k < P.leg_buckets && h[k + 1] != h[k]) atomicAdd(&P.leg_tot[k], (u32)(h[k + 1] - h[k]));
+    }
     __syncthreads();  // the row is read before the starts advance as cursors
 #pragma unroll
     for (u32 k = 0; k < RESOLVE_K; k++) {

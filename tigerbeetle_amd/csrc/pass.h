@@ -85,6 +85,7 @@ struct PassArgs {
     u32 legs;              // 1: the legs path is enabled for this pass (the host checked the sizes)
     u32 apply_late;        // 1: tb_apply_events applies the independent ok transfers (small passes)
     u32 leg_shift;         // bucket of an account slot = slot >> leg_shift (2^leg_shift slots each)
+    u32* leg_tot;          // [leg_buckets] legs per bucket in the pass (tb_emit_legs; zeroed by tb_pass_clear)
     u32 leg_buckets;       // account_cap >> leg_shift
     u64* leg_ev;           // [2 * pass events] leg word of event pe's side s at 2*pe+s (event order)
     u64* leg_w;            // [2 * pass events] the same leg words grouped by bucket per prepare
@@ -241,8 +242,11 @@ __device__ static inline void tb_dedup_mark(const PassArgs& P) {
 // Before kernel 1 of pass `epoch`: zero the S shards and pass words, and the dedup entries the
 // previous pass may have written (all `cap` entries when `force`).
 __global__ __launch_bounds__(256) void tb_pass_clear(u64* dedup, u64 cap, u64* sum_shards, const Globals* g, u32 epoch,
-                                                     u32 force) {
+                                                     u32 force, u32* leg_tot, u32 leg_buckets) {
     if (blockIdx.x == 0 && threadIdx.x < SUM_WORDS) sum_shards[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && leg_tot) {
+        for (u32 k = threadIdx.x; k < leg_buckets; k += 256) leg_tot[k] = 0;
+    }
     const u64 w = g->dedup_dirty;
     u64 n = 0;
     if (force) n = cap;
