@@ -390,6 +390,25 @@ def load_pmc(kernel, transfers_per_launch=None):
     return None
 
 
+def load_pmc_device(kernel, transfers_per_launch):
+    """HBM traffic of `kernel` in device-resident C2 passes (no host copy in flight), from the newest
+    committed profiles/*/device/pmc_device_c2.json (tools/gpu/device_pmc.py), per transfer and per
+    launch of this run."""
+    import glob
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "device", "pmc_device_c2.json")))
+    if not found:
+        return load_pmc(kernel, transfers_per_launch)
+    d = json.load(open(found[-1]))
+    k = d.get("kernels", {}).get(kernel)
+    if not k:
+        return None
+    return {"source": os.path.relpath(found[-1], ROOT),
+            "counters": "FETCH_SIZE + WRITE_SIZE (raw; FETCH_SIZE may read up to 2x low on gfx950)",
+            "bytes_per_transfer": k["raw_per_transfer"], "bytes_per_transfer_fetch_x2": k["fetch_x2_per_transfer"],
+            "bytes_per_launch": round(k["raw_per_transfer"] * transfers_per_launch),
+            "bytes_per_launch_fetch_x2": round(k["fetch_x2_per_transfer"] * transfers_per_launch)}
+
+
 WORKLOAD_TEXT = {
     "c2": "C2 (BASELINE.json configs[1]): %d accounts, %d uniform transfers/GPU, no flags, prepares of %d",
     "c3": "C3 (BASELINE.json configs[2]): %d accounts (10%% debits_must_not_exceed_credits, funded by a bank "
@@ -569,7 +588,8 @@ def main():
             "steps": args.device_steps, "ms_per_step": round(dev_total / args.device_steps, 3),
             "pass_prepares": args.pass_batches,
             "definition": "tbgpu_commit_device_async: the same prepares already resident in HBM (no PCIe)",
-            "roofline": roofline(dev_stats, u_dev, per_launch_dev, args, dev_total, None, steps=args.device_steps),
+            "roofline": roofline(dev_stats, u_dev, per_launch_dev, args, dev_total, None, steps=args.device_steps,
+                                 device=True),
         }
 
     # -- the validate kernel against its own access pattern, measured live (rank 0, N=1) ------
@@ -843,7 +863,8 @@ def access_mix(engine, transfers, kernel_ms):
             "source": "tbgpu_bench_access_mix (k_workload.h tb_access_mix), measured in this run"}
 
 
-def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=None, steps=None, kernel=None):
+def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=None, steps=None, kernel=None,
+             device=False):
     """The dominant kernel of the timed steps against the HBM peak; `kernels` = every kernel's mean
     launch time (from the warmup steps when given: the timed steps time only validate, replay/flow
     and whole passes)."""
@@ -878,7 +899,8 @@ def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=No
     src = kernel_table(breakdown) if breakdown else kernels
     per_kernel = {k: {"launches": int(n), "avg_launch_ms": round(ms / n, 4)} for k, (ms, n) in src.items() if n}
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc(dom, per_launch_transfers), "kernel": dom,
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": (load_pmc_device if device else load_pmc)(dom, per_launch_transfers), "kernel": dom,
             "kernels": per_kernel, "kernels_timed_in": "warmup steps (every kernel)" if breakdown else "timed steps",
             "avg_launch_ms": round(ms_dom / n_dom, 4), "alg_bytes_per_transfer": round(alg_bytes / per_launch_transfers, 1),
             "path_bytes_per_transfer": round(296 + 256 * u_over_t, 1),

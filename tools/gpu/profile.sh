@@ -5,6 +5,9 @@
 # separate --pmc passes (they do not fit in one pass on gfx950) over a shorter run of the same
 # configuration (same chunk size, so the same launch shape).  One mode per call:
 #   bash tools/gpu/profile.sh kt|fetch|write      -> gpurun_out/prof/<mode>/
+#   bash tools/gpu/profile.sh dfetch|dwrite       -> FETCH_SIZE / WRITE_SIZE of device-resident C2 passes
+#     (tools/gpu/device_pass.py: 512-prepare passes, no host copy in flight)
+#   bash tools/gpu/profile.sh dkt                 -> kernel trace + stats of the same run
 #   bash tools/gpu/profile.sh mc                  -> memory-copy + kernel trace of one headline step
 #     (the copy engine's timeline: body copies, their gaps, the per-chunk metadata copies)
 #   bash tools/gpu/profile.sh c3|c4               -> kernel trace of `bench.py --workload c3|c4`
@@ -23,6 +26,11 @@ case $MODE in
         > "$OUT/bench_kt.log" 2>&1; rc=$? ;;
   mc) timeout -k 10 420 rocprofv3 --memory-copy-trace --kernel-trace --output-format csv -d "$OUT/mc" -o run -- \
         python3 "$R/bench.py" $LEG --access-mix 0 --steps 1 --warmup 1 > "$OUT/bench_mc.log" 2>&1; rc=$? ;;
+  dfetch|dwrite) C=FETCH_SIZE; [ "$MODE" = dwrite ] && C=WRITE_SIZE
+      timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/tools/gpu/device_pass.py" \
+        > "$OUT/$MODE.log" 2>&1; rc=$? ;;
+  dkt) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/dkt" -o run -- \
+        python3 "$R/tools/gpu/device_pass.py" > "$OUT/dkt.log" 2>&1; rc=$? ;;
   fetch|write) C=FETCH_SIZE; [ "$MODE" = write ] && C=WRITE_SIZE
       timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/bench.py" $LEG \
         --steps 1 --warmup 0 --transfers 20000000 > "$OUT/$MODE.log" 2>&1; rc=$? ;;
