@@ -377,8 +377,8 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         INIT_CK(hipMalloc(&E->leg_ev, pe * 2 * 8));
         INIT_CK(hipMalloc(&E->leg_w, pe * 2 * 8));
         INIT_CK(hipMalloc(&E->leg_off, (u64)std::min<u32>(E->pb_max, LEG_PREPARES_MAX) * (E->leg_buckets + 1) * 4));
-        INIT_CK(hipMalloc(&E->leg_tot, (u64)std::max<u32>(1, E->leg_buckets) * 4));
-        INIT_CK(hipMemset(E->leg_tot, 0, (u64)std::max<u32>(1, E->leg_buckets) * 4));
+        INIT_CK(hipMalloc(&E->leg_tot, ((u64)E->leg_buckets + 1) * 4));
+        INIT_CK(hipMemset(E->leg_tot, 0, ((u64)E->leg_buckets + 1) * 4));
     }
     if (E->flow_ok) {
         FlowArgs& F = E->F;

@@ -18,7 +18,7 @@
 
 #define APPLY_HEAVY (16 * 4 * APPLY_THREADS)  // a range this long: 16 loads in flight, hot word in registers
 #define APPLY_PART 32768                      // legs per part of a split bucket
-#define APPLY_SPLIT_MIN (2 * APPLY_PART)      // buckets at least this heavy are split
+#define APPLY_SPLIT_MIN LEG_SPLIT_MIN         // buckets at least this heavy are split (2 parts)
 #define APPLY_EXTRA 64                        // extra workgroups of tb_apply_legs for the parts
 
 // Gather of one bucket's legs: consecutive legs of a segment go to consecutive lanes (coalesced
@@ -128,6 +128,7 @@ __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
 
     const u32 NBK = P.leg_buckets;
     const bool owner = blockIdx.x < NBK;
+    if (!owner && P.leg_tot[NBK] == 0) return;  // no bucket of this pass is split
     u32 g = blockIdx.x, part = 0, first_extra = 0;
     const u32 tot_g = owner ? P.leg_tot[g] : 0u;
     if (!owner || tb_bucket_extras(tot_g)) {

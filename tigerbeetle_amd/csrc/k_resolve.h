@@ -142,7 +142,11 @@ __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 L, 
     for (u32 k = threadIdx.x; k <= P.leg_buckets; k += blockDim.x) {
         row[k] = h[k];
         // The pass's legs per bucket: tb_apply_legs splits a Zipf-heavy bucket over workgroups.
-        if (k < P.leg_buckets && h[k + 1] != h[k]) atomicAdd(&P.leg_tot[k], (u32)(h[k + 1] - h[k]));
+        if (k < P.leg_buckets && h[k + 1] != h[k]) {
+            const u32 add = h[k + 1] - h[k];
+            const u32 was = atomicAdd(&P.leg_tot[k], add);
+            if (was < LEG_SPLIT_MIN && was + add >= LEG_SPLIT_MIN) atomicAdd(&P.leg_tot[P.leg_buckets], 1u);
+        }
     }
     __syncthreads();  // the row is read before the starts advance as cursors
 #pragma unroll

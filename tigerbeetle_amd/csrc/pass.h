@@ -85,7 +85,8 @@ struct PassArgs {
     u32 legs;              // 1: the legs path is enabled for this pass (the host checked the sizes)
     u32 apply_late;        // 1: tb_apply_events applies the independent ok transfers (small passes)
     u32 leg_shift;         // bucket of an account slot = slot >> leg_shift (2^leg_shift slots each)
-    u32* leg_tot;          // [leg_buckets] legs per bucket in the pass (tb_emit_legs; zeroed by tb_pass_clear)
+    u32* leg_tot;          // [leg_buckets + 1] legs per bucket in the pass (tb_emit_legs; zeroed by tb_pass_clear),
+                           // then the number of buckets that reached APPLY_SPLIT_MIN
     u32 leg_buckets;       // account_cap >> leg_shift
     u64* leg_ev;           // [2 * pass events] leg word of event pe's side s at 2*pe+s (event order)
     u64* leg_w;            // [2 * pass events] the same leg words grouped by bucket per prepare
@@ -103,6 +104,7 @@ enum : u32 { CERT_EXT_U128 = 1, CERT_EXT_U64 = 2 };
 #define LEG_BUCKETS_PREF 2048
 #define LEG_BUCKETS_MAX 4096  // u16 counters: 8 KB of tb_resolve's LDS (under 80 KB: two workgroups per CU)
 #define LEG_PREPARES_MAX 1024
+#define LEG_SPLIT_MIN 65536  // tb_apply_legs splits a bucket with at least this many legs in the pass
 #define LEGS_MIN_EVENTS (1u << 18)  // smaller passes apply balances with atomics (engine.hip)
 #define APPLY_THREADS 256
 // Leg word: ((slot within its bucket) << 2 | balance field (BAL_OFF / 16)) << LEG_AMT_BITS | amount.
@@ -245,7 +247,7 @@ __global__ __launch_bounds__(256) void tb_pass_clear(u64* dedup, u64 cap, u64* s
                                                      u32 force, u32* leg_tot, u32 leg_buckets) {
     if (blockIdx.x == 0 && threadIdx.x < SUM_WORDS) sum_shards[threadIdx.x] = 0;
     if (blockIdx.x == 0 && leg_tot) {
-        for (u32 k = threadIdx.x; k < leg_buckets; k += 256) leg_tot[k] = 0;
+        for (u32 k = threadIdx.x; k <= leg_buckets; k += 256) leg_tot[k] = 0;
     }
     const u64 w = g->dedup_dirty;
     u64 n = 0;
