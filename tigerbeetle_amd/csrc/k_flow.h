@@ -563,8 +563,30 @@ struct SweepRec {  // one undecided unit, in event order (fl_sweep)
     u64 pad;
 };
 
+// The sweep's LDS home for the swept sums of segment heads (b_ex in global memory otherwise): an
+// open-addressing table of SW_CAP heads in LDS the planner and the sort no longer use.  A head
+// claims a slot on first sight and keeps it; a head that finds its SW_PROBES slots taken stays in
+// global memory for the whole sweep (slots are never freed, so it never finds one later).
+#define SW_CAP 1024
+#define SW_PROBES 16
+#define SW_NONE 0xFFFFFFFFu
+__device__ static inline u32 fl_sw_slot(u32* s_hk, u32 head) {
+    if (head == FLOW_SENT) return SW_NONE;
+    u32 h = (head * 2654435761u) >> 22;  // 10 bits: SW_CAP
+    for (u32 n = 0; n < SW_PROBES; n++) {
+        const u32 k = s_hk[h];
+        if (k == head) return h;
+        if (k == FLOW_SENT) {
+            const u32 old = atomicCAS(&s_hk[h], FLOW_SENT, head);
+            if (old == FLOW_SENT || old == head) return h;
+        }
+        h = (h + 1) & (SW_CAP - 1);
+    }
+    return SW_NONE;
+}
+
 __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32 ndep, u32 NA, u32& gen,
-                                       u64 (*s_wv)[4], u32* s_wf, u32* s_cnt) {
+                                       u64 (*s_wv)[4], u32* s_wf, u32* s_cnt, u32* s_hk, u64* s_hx) {
     Globals* g = P.T.g;
     const Tables& T = P.T;
     const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid;
@@ -703,6 +725,11 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
     if (blockIdx.x == 0 && wave == 0) {
         SweepRec nx = {};
         if (lane < nu) nx = F.b_rec[lane];
+        for (u32 k = lane; k < SW_CAP; k += 64) {
+            s_hk[k] = FLOW_SENT;
+            s_hx[2 * k] = 0;
+            s_hx[2 * k + 1] = 0;
+        }
         u64 t_all = fl_now(), t_wait = 0, t_loop = 0;
         for (u32 w0 = 0; w0 < nu; w0 += 64) {
             const SweepRec x = nx;
@@ -710,15 +737,32 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
             const u32 nv = min(64u, nu - w0);
             const bool valid = lane < nv;
             u64 xd = x.xd, yd = x.yd, xc = x.xc, yc = x.yc;
+            // The swept sums of the lane's segments: LDS (one wave: its LDS operations complete in
+            // order), global memory for a head without a slot.
+            const u32 sld = valid ? fl_sw_slot(s_hk, x.hd) : SW_NONE;
+            const u32 slc = valid ? fl_sw_slot(s_hk, x.hc) : SW_NONE;
+            bool glob = false;
             if (valid && x.hd != FLOW_SENT) {
-                xd += fl_ld64(&F.b_ex[2 * x.hd]);
-                yd += fl_ld64(&F.b_ex[2 * x.hd + 1]);
+                if (sld != SW_NONE) {
+                    xd += s_hx[2 * sld];
+                    yd += s_hx[2 * sld + 1];
+                } else {
+                    xd += fl_ld64(&F.b_ex[2 * x.hd]);
+                    yd += fl_ld64(&F.b_ex[2 * x.hd + 1]);
+                    glob = true;
+                }
             }
             if (valid && x.hc != FLOW_SENT) {
-                xc += fl_ld64(&F.b_ex[2 * x.hc]);
-                yc += fl_ld64(&F.b_ex[2 * x.hc + 1]);
+                if (slc != SW_NONE) {
+                    xc += s_hx[2 * slc];
+                    yc += s_hx[2 * slc + 1];
+                } else {
+                    xc += fl_ld64(&F.b_ex[2 * x.hc]);
+                    yc += fl_ld64(&F.b_ex[2 * x.hc + 1]);
+                    glob = true;
+                }
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (__ballot(glob)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const u64 tb = fl_now();
             if (w0 + 64 + lane < nu) nx = F.b_rec[w0 + 64 + lane];
             const u32 vd = (x.t >> 8) & 15, vc = (x.t >> 12) & 15;
@@ -778,21 +822,34 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
             }
             const u64 tc = fl_now();
             t_loop += tc - tb;
+            bool gadd = false;
             if (valid) {
                 F.b_st[x.f] = dfl ? BS_FAIL_CREDITS : cfl ? BS_FAIL_DEBITS : BS_OK;
                 if (!dfl && !cfl) {
                     const u32 td = x.t & 15, tc2 = (x.t >> 4) & 15;
                     if (x.hd != FLOW_SENT) {
-                        if (td & BT_X) tb_atomic_add_lo_noret(&F.b_ex[2 * x.hd], a);
-                        if (td & BT_Y) tb_atomic_add_lo_noret(&F.b_ex[2 * x.hd + 1], a);
+                        if (sld != SW_NONE) {
+                            if (td & BT_X) atomicAdd((unsigned long long*)&s_hx[2 * sld], (unsigned long long)a);
+                            if (td & BT_Y) atomicAdd((unsigned long long*)&s_hx[2 * sld + 1], (unsigned long long)a);
+                        } else {
+                            if (td & BT_X) tb_atomic_add_lo_noret(&F.b_ex[2 * x.hd], a);
+                            if (td & BT_Y) tb_atomic_add_lo_noret(&F.b_ex[2 * x.hd + 1], a);
+                            gadd = true;
+                        }
                     }
                     if (x.hc != FLOW_SENT) {
-                        if (tc2 & BT_X) tb_atomic_add_lo_noret(&F.b_ex[2 * x.hc], a);
-                        if (tc2 & BT_Y) tb_atomic_add_lo_noret(&F.b_ex[2 * x.hc + 1], a);
+                        if (slc != SW_NONE) {
+                            if (tc2 & BT_X) atomicAdd((unsigned long long*)&s_hx[2 * slc], (unsigned long long)a);
+                            if (tc2 & BT_Y) atomicAdd((unsigned long long*)&s_hx[2 * slc + 1], (unsigned long long)a);
+                        } else {
+                            if (tc2 & BT_X) tb_atomic_add_lo_noret(&F.b_ex[2 * x.hc], a);
+                            if (tc2 & BT_Y) tb_atomic_add_lo_noret(&F.b_ex[2 * x.hc + 1], a);
+                            gadd = true;
+                        }
                     }
                 }
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next window reads b_ex
+            if (__ballot(gadd)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next window reads b_ex
             t_wait += (tb - ta) + (fl_now() - tc);
         }
         if (lane == 0) {
@@ -842,7 +899,8 @@ __device__ static inline void fl_add_lo(u64* p, u64 v) {
 
 // Returns true when every unit was decided and applied (the ordered run is skipped).
 __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u32 ndep, u32 N, bool cert64, u32& gen,
-                                        u64& tsmax, u64 (*s_wv)[4], u32* s_wf, u32* s_cnt, u64& tp) {
+                                        u64& tsmax, u64 (*s_wv)[4], u32* s_wf, u32* s_cnt, u64& tp, u32* s_hk,
+                                        u64* s_hx) {
     Globals* g = P.T.g;
     const Tables& T = P.T;
     const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid;
@@ -1010,7 +1068,7 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
     }
     fl_mark(g, tp, FP_BROUNDS);
     if (!converged && F.sweep_min) {
-        converged = fl_sweep(P, F, ndep, NA, gen, s_wv, s_wf, s_cnt);
+        converged = fl_sweep(P, F, ndep, NA, gen, s_wv, s_wf, s_cnt, s_hk, s_hx);
         if (fl_stalled(g)) return false;
         fl_mark(g, tp, FP_SWEEP);
     }
@@ -1097,7 +1155,9 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     __shared__ u32 s_wave[FLOW_THREADS / 64];
     __shared__ u32 s_hist[256];
     __shared__ u32 s_base[256];
-    __shared__ u32 s_wcnt[FLOW_THREADS / 64][256];
+    __shared__ __attribute__((aligned(16))) u32 s_wcnt[FLOW_THREADS / 64][256];
+    static_assert(SW_CAP <= FLOW_NB_MAX + 1 && 2 * SW_CAP * 8 <= sizeof(u32) * (FLOW_THREADS / 64) * 256,
+                  "the sweep's head table fits in s_dpre / s_wcnt");
     __shared__ u8 s_code[BATCH_LDS];
     __shared__ u32 s_list[FLOW_THREADS];
     __shared__ u64 s_tsmax[FLOW_THREADS / 64];
@@ -1406,7 +1466,8 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
         __shared__ u32 s_bwf[FLOW_THREADS / 64];
         __shared__ u32 s_bcnt;
         u64 tsb = 0;
-        if (fl_bounds(P, F, ndep, N, cert64, gen, tsb, s_bwv, s_bwf, &s_bcnt, tp)) {
+        // The sweep's head table lives in s_dpre / s_wcnt: plan 1 and the sort are done with them.
+        if (fl_bounds(P, F, ndep, N, cert64, gen, tsb, s_bwv, s_bwf, &s_bcnt, tp, s_dpre, (u64*)&s_wcnt[0][0])) {
             // Every unit decided and applied: replies and the pass close (workgroup 0) after all
             // workgroups' writes.
             if (tsb) atomicMax((unsigned long long*)&g->commit_timestamp, (unsigned long long)tsb);
