@@ -175,7 +175,9 @@ __device__ static inline u128 tb_sat_add(u128 a, u128 b) {
 // meets the claimed fingerprint on its probe path (or loses the CAS to it) — that is how same-pass
 // duplicate ids are detected, with no separate dedup set.
 // ------------------------------------------------------------------------------------------------
+#ifndef FL_BAR_GROUPS
 #define FL_BAR_GROUPS 8
+#endif
 #define FL_BAR_STRIDE 32  // u32 words: one 128-B line per counter
 struct Globals {
     u64 commit_timestamp;     // max timestamp of an event that returned ok when evaluated
