@@ -606,11 +606,15 @@ def main():
         sample_lens = batches(min(args.cpu_sample, args.transfers), args.batch)
         sample_ts, t_cursor = timestamps(sample_lens, t_cursor + 10, wl["gap_every"])
         cpu, oracle, expected = run_cpu_baseline(engine, args, acct_lens, acct_ts, events_dev, sample_lens, sample_ts)
+        # The sample goes through the headline's own timed path: tbgpu_commit_pipelined from
+        # registered host memory in chunks of chunk_prepares.
         engine.reset_transfers()
-        engine.commit_device_async(129, sample_ts, sample_lens, events_dev, res_dev, rb_dev)
-        engine.sync()
-        rb = engine.to_host(rb_dev, len(sample_lens) * 4).view(np.uint32)
-        results = engine.to_host(res_dev, sum(sample_lens) * 8)
+        sample_host = engine.to_host(events_dev, sum(sample_lens) * 128)
+        engine.register_host(sample_host)
+        rb, results, _ = engine.commit_pipelined(129, sample_ts, sample_lens, sample_host,
+                                                 chunk_batches=args.chunk_prepares)
+        engine.unregister_host(sample_host)
+        del sample_host
         got, off = [], 0
         for L, nb in zip(sample_lens, rb):  # sparse replies at the prepare's event offset
             got.append(bytes(results[off * 8:off * 8 + int(nb)]))
@@ -619,7 +623,9 @@ def main():
         acc_equal = engine.export_accounts().tobytes() == oracle.export_accounts().tobytes()
         xfer_equal = engine.export_transfers(cap=sum(sample_lens)).tobytes() == oracle.export_transfers().tobytes()
         parity.update({"sample_transfers": sum(sample_lens), "replies_equal": replies_equal,
-                       "accounts_equal": acc_equal, "transfers_equal": xfer_equal})
+                       "accounts_equal": acc_equal, "transfers_equal": xfer_equal,
+                       "sample_path": "tbgpu_commit_pipelined from registered host memory, %d-prepare chunks "
+                                      "(the timed path)" % args.chunk_prepares})
         cpu.pop("seconds")
 
     host = None

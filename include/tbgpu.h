@@ -65,13 +65,25 @@ extern "C" {
 #define TBGPU_CONFIG_SWEEP_EARLY (1u << 2)
 #define TBGPU_CONFIG_SWEEP_OFF (1u << 3)
 
+#define TBGPU_DEVICES_MAX 16u
+
 typedef struct tbgpu_config {
     uint64_t accounts_max;      /* HBM account table capacity (the groove's object count) */
-    uint64_t transfers_max;     /* HBM transfer store capacity */
-    uint32_t pass_events_max;   /* max events in one device pass (tbgpu_commit_many) */
-    uint32_t pass_batches_max;  /* max prepares in one device pass */
-    int32_t device;             /* HIP device ordinal */
+    uint64_t transfers_max;     /* HBM transfer store capacity (the whole ledger, over every device) */
+    uint32_t pass_events_max;   /* max events in one device pass (tbgpu_commit_many); on a node: per
+                                   source device and pass */
+    uint32_t pass_batches_max;  /* max prepares in one device pass; on a node: per source device */
+    int32_t device;             /* HIP device ordinal (device_count <= 1) */
     uint32_t flags;             /* TBGPU_CONFIG_* */
+    /* SURVEY.md §8b device_mask.  device_count >= 2: a NODE engine over devices[0 .. device_count),
+     * one shard per entry (an ordinal may repeat: logical shards sharing a GPU).  Every entry point
+     * of this header works on a node engine with the same semantics: accounts hash-partitioned (the
+     * records replicated, the balances on their owner shard), transfers on their home shard, each
+     * create_transfers pass routed across the shards by kernels reading their peers' HBM over xGMI
+     * (tigerbeetle_amd/csrc/node.h).  Not on a node: tbgpu_commit_device_async and the
+     * tbgpu_shard.h primitives (they take one device's engine). */
+    uint32_t device_count;
+    int32_t devices[TBGPU_DEVICES_MAX];
 } tbgpu_config;
 
 typedef struct tbgpu tbgpu_t;

@@ -1,0 +1,115 @@
+"""The node engine: one tbgpu handle over N shards (include/tbgpu.h tbgpu_config.devices, csrc/node.h)
+driven through the same C ABI as a single-device engine, against the oracle byte for byte.
+
+The box has one GPU, so the shards are LOGICAL shards sharing cuda:0 (devices = (0, 0) or
+(0, 0, 0)): the routing, the gathers from the sources' send buffers, the owner legs, the replies
+built from the homes' codes and the sequencer of dirty passes all run exactly as across GPUs; only
+the peer reads stay inside one HBM instead of crossing xGMI."""
+import numpy as np
+import pytest
+
+from tests.harness import known_answers, table
+from tests.harness.configs import batches, generate, split, timestamps
+from tests.harness.oracle import OracleEngine
+from tests.harness.workload import make_scenario
+from tests.test_gpu_differential import CONFIGS, _run, assert_same_state
+from tests.test_gpu_tables import TABLES
+from tigerbeetle_amd._lib import EngineError
+from tigerbeetle_amd.types import TRANSFER_DTYPE
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def node_factory():
+    from tigerbeetle_amd.state_machine import Engine, Options
+
+    made = []
+
+    def make(devices=(0, 0), **kw):
+        opts = dict(accounts_max=4096, transfers_max=1 << 17, pass_events_max=8192 * 4, pass_batches_max=64,
+                    devices=tuple(devices))
+        opts.update(kw)
+        e = Engine(Options(**opts))
+        made.append(e)
+        return e
+
+    yield make
+    for e in made:
+        e.close()
+
+
+@pytest.mark.parametrize("name,text", TABLES, ids=[n for n, _ in TABLES])
+def test_node_reproduces_reference_table(name, text, node_factory):
+    table.check(text, node_factory())
+
+
+@pytest.mark.parametrize("config", ["mixed", "chains", "two_phase", "limits", "hot_ids", "clean", "overflow",
+                                    "big_batches"])
+@pytest.mark.parametrize("many", [False, True], ids=["commit", "commit_many"])
+def test_node_differential(config, many, node_factory):
+    sc = make_scenario(5003 + sum(map(ord, config)), **CONFIGS[config])
+    _run(sc, OracleEngine(), node_factory(devices=(0, 0, 0) if many else (0, 0)), many)
+
+
+@pytest.mark.parametrize("scenario", known_answers.load(), ids=lambda s: s["name"])
+def test_node_client_answers(scenario, node_factory):
+    known_answers.run(scenario, node_factory())
+
+
+@pytest.mark.parametrize("shards", [2, 3, 4])
+def test_node_clean_passes_pipelined(shards, node_factory):
+    """C2-shaped passes from registered host memory (the headline's call), routed across the shards,
+    with the failures a clean pass can hold: duplicate ids inside a pass and across passes (exists,
+    exists_with_different_*), a non-zero timestamp field (answered at the source, never routed), a
+    missing account — every reply, account, transfer and the commit timestamp equal the oracle's."""
+    n_acc, n_xfer, batch, chunk = 6000, 300_000, 8190, 3
+    engine = node_factory(devices=(0,) * shards, accounts_max=n_acc, transfers_max=n_xfer,
+                          pass_events_max=chunk * batch, pass_batches_max=chunk)
+    accts, xfers = generate(engine, "c2", n_acc, n_xfer, seed=5 + shards)
+    x = xfers.view(TRANSFER_DTYPE).copy()
+    rng = np.random.default_rng(shards)
+    dup = rng.choice(np.arange(1000, n_xfer), 600, replace=False)
+    src = rng.integers(0, 900, 600)
+    x["id_lo"][dup] = x["id_lo"][src]
+    x["id_hi"][dup] = x["id_hi"][src]
+    x["amount_lo"][dup[:300]] += 1  # exists_with_different_amount for half of them
+    x["timestamp"][rng.choice(n_xfer, 200, replace=False)] = 7
+    x["debit_account_id_lo"][rng.choice(n_xfer, 200, replace=False)] ^= 0x5A5A
+    xfers = x.view(np.uint8).reshape(-1)
+    a_lens, x_lens = batches(n_acc, batch), batches(n_xfer, batch)
+    a_ts, t = timestamps(a_lens, 10**12)
+    x_ts, _ = timestamps(x_lens, t + 10)
+    oracle = OracleEngine(n_acc, n_xfer)
+    assert all(r == b"" for r in oracle.commit_many(128, a_ts, split(accts, a_lens)))
+    expected = oracle.commit_many(129, x_ts, split(xfers, x_lens))
+    rb, _, _ = engine.commit_pipelined(128, a_ts, a_lens, np.ascontiguousarray(accts), chunk_batches=chunk)
+    assert int(rb.sum()) == 0
+    host = np.ascontiguousarray(xfers)
+    engine.register_host(host)
+    try:
+        rb, rep, lat = engine.commit_pipelined(129, x_ts, x_lens, host, chunk_batches=chunk, latency=True)
+    finally:
+        engine.unregister_host(host)
+    got, off = [], 0
+    for L, nb in zip(x_lens, rb):
+        got.append(bytes(rep[off * 8:off * 8 + int(nb)]))
+        off += L
+    assert got == expected
+    assert sum(len(r) for r in expected) > 0
+    assert_same_state(oracle, engine)
+    st = engine.stats()
+    assert st["transfers"] == len(oracle.export_transfers())
+
+
+def test_node_checkpoint_and_lookups(node_factory):
+    """Write-back of a node equals the oracle's state diff (merged over the shards: each account's
+    owner copy, each transfer from its home), and lookups read each object where it lives."""
+    from tests.test_gpu_checkpoint import test_checkpoint_deltas
+    test_checkpoint_deltas("two_phase", lambda **kw: node_factory(devices=(0, 0, 0), **kw))
+
+
+def test_node_refuses_device_resident(node_factory):
+    engine = node_factory()
+    with pytest.raises(EngineError):
+        engine.commit_device_async(129, [10], [1], 0, 0, 0)

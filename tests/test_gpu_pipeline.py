@@ -122,3 +122,59 @@ def test_pipelined_rejects_bad_timestamps(gpu_engine_factory):
     body = np.zeros(128 * 2, dtype=np.uint8)
     with pytest.raises(EnginePanic):  # state_machine.zig:519: timestamp must exceed commit_timestamp
         engine.commit_pipelined(129, [100, 100], [1, 1], body)
+
+
+def test_pipelined_stops_at_device_panic(gpu_engine_factory):
+    """A device panic in an early chunk (the reference traps there: post of a pending transfer whose
+    pending balance was set below its amount, state_machine.zig:951-956 checked `-=`) ends the call
+    with PANIC; the chunks already enqueued behind it report no replies (out_lens stay 0)."""
+    import ctypes
+
+    from tigerbeetle_amd import _lib
+    from tigerbeetle_amd.types import ACCOUNT_DTYPE, TRANSFER_DTYPE, TransferFlags
+
+    engine = gpu_engine_factory()
+    acc = np.zeros(2, dtype=ACCOUNT_DTYPE)
+    acc["id_lo"] = [1, 2]
+    acc["ledger"] = 1
+    acc["code"] = 1
+    assert engine.commit(128, 10, acc.tobytes()) == b""
+    pend = np.zeros(1, dtype=TRANSFER_DTYPE)
+    pend["id_lo"] = 10
+    pend["debit_account_id_lo"] = 1
+    pend["credit_account_id_lo"] = 2
+    pend["amount_lo"] = 100
+    pend["ledger"] = 1
+    pend["code"] = 1
+    pend["flags"] = int(TransferFlags.pending)
+    assert engine.commit(129, 20, pend.tobytes()) == b""
+    engine.set_balances(1, 0, 0, 0, 0)  # debits_pending 100 -> 0: the post's `-=` traps
+
+    n = 6
+    x = np.zeros(n, dtype=TRANSFER_DTYPE)
+    x["id_lo"] = [11, 0, 21, 0, 31, 0]  # prepares 1, 3, 5 would reply id_must_not_be_zero
+    x["debit_account_id_lo"] = 1
+    x["credit_account_id_lo"] = 2
+    x["amount_lo"] = 1
+    x["ledger"] = 1
+    x["code"] = 1
+    x["pending_id_lo"][0] = 10
+    x["flags"][0] = int(TransferFlags.post_pending_transfer)
+    x["debit_account_id_lo"][0] = 0
+    x["credit_account_id_lo"][0] = 0
+    x["amount_lo"][0] = 0
+    body = np.frombuffer(x.tobytes(), dtype=np.uint8).copy()
+    replies = np.zeros(n * 8, dtype=np.uint8)
+    ts = np.arange(30, 30 + 10 * n, 10, dtype=np.uint64)
+    ins = (np.arange(n, dtype=np.uint64) * 128 + np.uint64(body.ctypes.data)).astype(np.uint64)
+    outs = (np.arange(n, dtype=np.uint64) * 8 + np.uint64(replies.ctypes.data)).astype(np.uint64)
+    in_lens = np.full(n, 128, dtype=np.uint32)
+    out_lens = np.full(n, 77, dtype=np.uint32)
+    P = ctypes.c_void_p
+    st = engine.lib.tbgpu_commit_pipelined(
+        engine.h, 129, n, ts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), ins.ctypes.data_as(ctypes.POINTER(P)),
+        in_lens.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), outs.ctypes.data_as(ctypes.POINTER(P)),
+        out_lens.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 1, None)
+    assert st == _lib.STATUS_PANIC
+    assert out_lens.tolist() == [0] * n  # nothing after the panicking chunk is reported
+    assert int(engine.lib.tbgpu_commit_timestamp(engine.h)) < int(ts[1])  # no later chunk advanced it

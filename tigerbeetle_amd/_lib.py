@@ -27,6 +27,8 @@ class tbgpu_config(ctypes.Structure):
         ("pass_batches_max", ctypes.c_uint32),
         ("device", ctypes.c_int32),
         ("flags", ctypes.c_uint32),
+        ("device_count", ctypes.c_uint32),
+        ("devices", ctypes.c_int32 * 16),  # TBGPU_DEVICES_MAX
     ]
 
 

@@ -98,11 +98,15 @@ def read_entries(path, validate_chain=True, validate_checksums=True):
     return out
 
 
-def read_prepares(path, validate_chain=True, validate_checksums=True):
+def read_prepares(path, validate_chain=True, validate_checksums=True, require_contiguous=True):
     """The committed prepares of an AOF in op order: `prepare` entries of state-machine operations
     (the replay skips VSR-reserved ones, src/aof.zig:349-350), one per op (duplicates — an AOF
-    can backtrack, :80-84 — must be identical).  The prepare ops, VSR-reserved ones included, must
-    form one contiguous range: a missing op would replay a different history."""
+    can backtrack, :80-84 — must be identical).
+
+    require_contiguous (default on) is a check BEYOND the reference's iterator, which validates
+    only the checksums and the parent chain (src/aof.zig:214-260): the prepare ops, VSR-reserved
+    ones included, must form one contiguous range, since a missing op would replay a different
+    history.  Pass False to read every file the reference's replay would read."""
     by_op, all_ops = {}, set()
     for command, p in read_entries(path, validate_chain, validate_checksums):
         if command != COMMAND_PREPARE:
@@ -114,9 +118,11 @@ def read_prepares(path, validate_chain=True, validate_checksums=True):
         if prev is not None and (prev.timestamp, prev.operation, prev.body) != (p.timestamp, p.operation, p.body):
             raise AofError("op %d logged twice with different contents" % p.op)
         by_op[p.op] = p
-    if all_ops and len(all_ops) != max(all_ops) - min(all_ops) + 1:
+    if require_contiguous and all_ops and len(all_ops) != max(all_ops) - min(all_ops) + 1:
         missing = sorted(set(range(min(all_ops), max(all_ops) + 1)) - all_ops)
-        raise AofError("op sequence has gaps (first missing op %d, %d missing)" % (missing[0], len(missing)))
+        raise AofError("op sequence has gaps (first missing op %d, %d missing; this check goes beyond the "
+                       "reference iterator: read_prepares(..., require_contiguous=False) skips it)"
+                       % (missing[0], len(missing)))
     return [by_op[k] for k in sorted(by_op)]
 
 

@@ -61,8 +61,11 @@ struct ProfilePair {
     hipEvent_t a, b;
 };
 
+struct TbNode;  // node.h: the multi-device engine (tbgpu_config.device_count > 1)
+
 struct tbgpu {
     tbgpu_config cfg{};
+    TbNode* node = nullptr;  // set: this handle is a node engine; every call goes to node.h
     int device = 0;
     hipStream_t stream = nullptr;
 
@@ -237,7 +240,33 @@ static int engine_clear(tbgpu* E) {
     return TBGPU_STATUS_OK;
 }
 
+// node.h entry points (defined at the end of this file).
+static int node_api_init(const tbgpu_config* config, tbgpu_t** out);
+static void node_free(TbNode* N);
+static int node_api_reset(TbNode* N);
+static int node_commit_pipelined(TbNode* N, u8 op, u32 n, const u64* ts, const void* const* inputs, const u32* input_lens,
+                                 void* const* outputs, u32* out_lens, u32 chunk, double* latency_ms);
+static int node_api_commit(TbNode* N, u8 op, u64 timestamp, const void* input, u32 input_len, void* output,
+                           u32 output_cap, u32* out_len);
+static int node_sync(TbNode* N);
+static u64 node_commit_ts(TbNode* N);
+static int node_api_set_balances(TbNode* N, u64 id_lo, u64 id_hi, const u64 b[8]);
+static int node_api_export(TbNode* N, int what, void* out, u64 cap, u64* count);
+static int node_api_checkpoint_delta(TbNode* N, void* accounts_out, void* accounts_before_out, u64 accounts_cap,
+                                     void* transfers_out, u64 transfers_cap, u64* posted_out, u64 posted_cap,
+                                     tbgpu_delta_counts* counts);
+static int node_api_get_stats(TbNode* N, tbgpu_stats* s);
+static u32 node_world(TbNode* N);
+static tbgpu* node_engine(TbNode* N, u32 d);
+static int node_api_register_host(TbNode* N, void* ptr, u64 bytes);
+static int node_api_unregister_host(TbNode* N, void* ptr);
+static int node_fetch(TbNode* N, bool accounts, const u64* ids, u32 n, u8* out, u8* found);
+static int node_api_accounts_in(TbNode* N, const void* records, u32 n, bool load);
+static int node_api_transfers_in(TbNode* N, const void* records, const u8* state, u32 n, bool load);
+static int node_api_set_commit_timestamp(TbNode* N, u64 timestamp);
+
 extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
+    if (config && config->device_count > 1) return node_api_init(config, out);
     *out = nullptr;
     if (!config || config->accounts_max == 0 || config->transfers_max == 0 || config->pass_events_max == 0 ||
         config->pass_batches_max == 0) {
@@ -455,6 +484,11 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
 }
 
 extern "C" void tbgpu_deinit(tbgpu_t* E) {
+    if (E && E->node) {
+        node_free(E->node);
+        delete E;
+        return;
+    }
     if (!E) return;
     (void)hipSetDevice(E->device);
     if (E->stream) (void)hipStreamSynchronize(E->stream);
@@ -490,6 +524,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
 }
 
 extern "C" int tbgpu_reset(tbgpu_t* E) {
+    if (E->node) return node_api_reset(E->node);
     HIPCK(hipSetDevice(E->device));
     E->ckpt_valid = false;
     return engine_clear(E);
@@ -853,9 +888,12 @@ static int commit_pipelined(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, 
     }
     int status = TBGPU_STATUS_OK;
     // Read chunk c's replies out of its slot (its done event has fired or is waited for here).
-    auto consume = [&](size_t c) -> int {
+    // After a failed chunk the later ones (already enqueued) are only waited for: the reference
+    // would have stopped at the panic, so their replies and timestamps are not taken.
+    auto consume = [&](size_t c, bool take) -> int {
         tbgpu::PipeSlot& S = E->pipe[c % PIPE_SLOTS];
         HIPCK(hipEventSynchronize(S.done));
+        if (!take) return TBGPU_STATUS_OK;
         const Chunk& C = chunks[c];
         const u32 nb = C.k1 - C.k0;
         const u64* head = (const u64*)S.h_reply;
@@ -880,7 +918,7 @@ static int commit_pipelined(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, 
     for (; issued < chunks.size() && status == TBGPU_STATUS_OK; issued++) {
         const size_t c = issued;
         if (c >= PIPE_SLOTS) {
-            status = consume(consumed++);
+            status = consume(consumed++, true);
             if (status) break;
         }
         tbgpu::PipeSlot& S = E->pipe[c % PIPE_SLOTS];
@@ -920,7 +958,7 @@ static int commit_pipelined(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, 
     // Drain what is in flight (also after a failure: every enqueued chunk has finished before the
     // call returns, as after any synchronous call).
     while (consumed < issued) {
-        const int st = consume(consumed++);
+        const int st = consume(consumed++, status == TBGPU_STATUS_OK);
         if (status == TBGPU_STATUS_OK) status = st;
     }
     HIPCK(hipStreamSynchronize(E->copy_stream));
@@ -931,6 +969,8 @@ static int commit_pipelined(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, 
 extern "C" int tbgpu_commit_pipelined(tbgpu_t* E, uint8_t operation, uint32_t n, const uint64_t* timestamps,
                                       const void* const* inputs, const uint32_t* input_lens, void* const* outputs,
                                       uint32_t* out_lens, uint32_t chunk_batches, double* latency_ms) {
+    if (E->node) return n ? node_commit_pipelined(E->node, operation, n, timestamps, inputs, input_lens, outputs, out_lens,
+                                                  chunk_batches, latency_ms) : TBGPU_STATUS_OK;
     HIPCK(hipSetDevice(E->device));
     if (n == 0) return TBGPU_STATUS_OK;
     return commit_pipelined(E, operation, n, timestamps, inputs, input_lens, outputs, out_lens, nullptr, chunk_batches,
@@ -939,6 +979,7 @@ extern "C" int tbgpu_commit_pipelined(tbgpu_t* E, uint8_t operation, uint32_t n,
 
 extern "C" int tbgpu_commit(tbgpu_t* E, uint8_t operation, uint64_t timestamp, const void* input,
                             uint32_t input_len, void* output, uint32_t output_cap, uint32_t* out_len) {
+    if (E->node) return node_api_commit(E->node, operation, timestamp, input, input_len, output, output_cap, out_len);
     *out_len = 0;
     HIPCK(hipSetDevice(E->device));
     if (operation < OP_CREATE_ACCOUNTS || operation > OP_LOOKUP_TRANSFERS) {
@@ -966,6 +1007,11 @@ extern "C" int tbgpu_commit(tbgpu_t* E, uint8_t operation, uint64_t timestamp, c
 extern "C" int tbgpu_commit_many(tbgpu_t* E, uint8_t operation, uint32_t n, const uint64_t* timestamps,
                                  const void* const* inputs, const uint32_t* input_lens, void* const* outputs,
                                  uint32_t* out_lens) {
+    if (E->node) {
+        for (u32 k = 0; k < n; k++) out_lens[k] = 0;
+        return n ? node_commit_pipelined(E->node, operation, n, timestamps, inputs, input_lens, outputs, out_lens, 0, nullptr)
+                 : TBGPU_STATUS_OK;
+    }
     HIPCK(hipSetDevice(E->device));
     for (u32 k = 0; k < n; k++) out_lens[k] = 0;
     if (n == 0) return TBGPU_STATUS_OK;
@@ -976,6 +1022,7 @@ extern "C" int tbgpu_commit_many(tbgpu_t* E, uint8_t operation, uint32_t n, cons
 extern "C" int tbgpu_commit_device_async(tbgpu_t* E, uint8_t operation, uint32_t n_batches,
                                          const uint64_t* timestamps, const uint32_t* batch_lens,
                                          const void* events_dev, void* results_dev, uint32_t* reply_bytes_dev) {
+    if (E->node) return fail(TBGPU_STATUS_INVALID, "device-resident commits need a single-device engine");
     HIPCK(hipSetDevice(E->device));
     const u64 floor_ts = std::max(E->commit_ts, E->pending ? E->last_batch_ts : 0);
     u64 total = 0;
@@ -989,16 +1036,19 @@ extern "C" int tbgpu_commit_device_async(tbgpu_t* E, uint8_t operation, uint32_t
 }
 
 extern "C" int tbgpu_sync(tbgpu_t* E) {
+    if (E->node) return node_sync(E->node);
     HIPCK(hipSetDevice(E->device));
     return engine_sync(E);
 }
 
 extern "C" uint64_t tbgpu_commit_timestamp(tbgpu_t* E) {
+    if (E->node) return node_commit_ts(E->node);
     if (E->pending) engine_sync(E);
     return E->commit_ts;
 }
 
 extern "C" int tbgpu_test_set_balances(tbgpu_t* E, uint64_t id_lo, uint64_t id_hi, const uint64_t b[8]) {
+    if (E->node) return node_api_set_balances(E->node, id_lo, id_hi, b);
     HIPCK(hipSetDevice(E->device));
     if (E->pending) {
         int st = engine_sync(E);
@@ -1080,6 +1130,7 @@ static int export_records(tbgpu* E, std::vector<u8>& recs, std::vector<u64>* pos
 }
 
 extern "C" int tbgpu_export_accounts(tbgpu_t* E, void* out, uint64_t cap, uint64_t* count) {
+    if (E->node) return node_api_export(E->node, 0, out, cap, count);
     HIPCK(hipSetDevice(E->device));
     std::vector<u8> recs;
     int st = export_records<true>(E, recs, nullptr);
@@ -1091,6 +1142,7 @@ extern "C" int tbgpu_export_accounts(tbgpu_t* E, void* out, uint64_t cap, uint64
 }
 
 extern "C" int tbgpu_export_transfers(tbgpu_t* E, void* out, uint64_t cap, uint64_t* count) {
+    if (E->node) return node_api_export(E->node, 1, out, cap, count);
     HIPCK(hipSetDevice(E->device));
     std::vector<u8> recs;
     int st = export_records<false>(E, recs, nullptr);
@@ -1102,6 +1154,7 @@ extern "C" int tbgpu_export_transfers(tbgpu_t* E, void* out, uint64_t cap, uint6
 }
 
 extern "C" int tbgpu_export_posted(tbgpu_t* E, uint64_t* out_pairs, uint64_t cap, uint64_t* count) {
+    if (E->node) return node_api_export(E->node, 2, out_pairs, cap, count);
     HIPCK(hipSetDevice(E->device));
     std::vector<u8> recs;
     std::vector<u64> posted;
@@ -1143,6 +1196,8 @@ static int ckpt_snapshot_ready(tbgpu* E) {
 extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, void* accounts_before_out, uint64_t accounts_cap,
                                       void* transfers_out, uint64_t transfers_cap, uint64_t* posted_out,
                                       uint64_t posted_cap, tbgpu_delta_counts* counts) {
+    if (E->node) return node_api_checkpoint_delta(E->node, accounts_out, accounts_before_out, accounts_cap, transfers_out,
+                                                  transfers_cap, posted_out, posted_cap, counts);
     HIPCK(hipSetDevice(E->device));
     memset(counts, 0, sizeof(*counts));
     if (E->pending) {
@@ -1242,6 +1297,7 @@ extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, void* acco
 }
 
 extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
+    if (E->node) return node_api_get_stats(E->node, s);
     HIPCK(hipSetDevice(E->device));
     if (E->pending) {
         int st = engine_sync(E);
@@ -1287,6 +1343,10 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
 }
 
 extern "C" void tbgpu_reset_stats(tbgpu_t* E) {
+    if (E->node) {
+        for (u32 d = 0; d < node_world(E->node); d++) tbgpu_reset_stats(node_engine(E->node, d));
+        return;
+    }
     for (int k = 0; k < K_COUNT; k++) {
         E->prof_ms[k] = 0;
         E->prof_n[k] = 0;
@@ -1327,6 +1387,7 @@ static WorkloadParams workload_params(const tbgpu_workload* w, u64 first) {
 
 extern "C" int tbgpu_bench_generate_accounts(tbgpu_t* E, void* out_dev, uint64_t first, uint64_t count,
                                              const tbgpu_workload* w) {
+    if (E->node) E = node_engine(E->node, 0);
     HIPCK(hipSetDevice(E->device));
     if (count == 0) return TBGPU_STATUS_OK;
     hipLaunchKernelGGL(tb_gen_accounts, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, E->stream,
@@ -1337,6 +1398,7 @@ extern "C" int tbgpu_bench_generate_accounts(tbgpu_t* E, void* out_dev, uint64_t
 
 extern "C" int tbgpu_bench_generate_transfers(tbgpu_t* E, void* out_dev, uint64_t first, uint64_t count,
                                               const tbgpu_workload* w) {
+    if (E->node) E = node_engine(E->node, 0);
     HIPCK(hipSetDevice(E->device));
     if (count == 0) return TBGPU_STATUS_OK;
     if (w->account_count < 2) return fail(TBGPU_STATUS_INVALID, "need at least two accounts");
@@ -1347,6 +1409,10 @@ extern "C" int tbgpu_bench_generate_transfers(tbgpu_t* E, void* out_dev, uint64_
 }
 
 extern "C" int tbgpu_bench_legs_min_events(tbgpu_t* E, uint32_t events) {
+    if (E->node) {
+        for (u32 d = 0; d < node_world(E->node); d++) tbgpu_bench_legs_min_events(node_engine(E->node, d), events);
+        return TBGPU_STATUS_OK;
+    }
     E->legs_min = events;
     return TBGPU_STATUS_OK;
 }
@@ -1369,6 +1435,7 @@ static float access_mix_ms(tbgpu_t* E, const MixArgs& A, int reps) {
 }
 
 extern "C" int tbgpu_bench_access_mix(tbgpu_t* E, uint64_t transfers, double out_ms[7]) {
+    if (E->node) E = node_engine(E->node, 0);
     HIPCK(hipSetDevice(E->device));
     HIPCK(hipStreamSynchronize(E->stream));
     MixArgs A = {};
@@ -1411,17 +1478,23 @@ extern "C" int tbgpu_bench_access_mix(tbgpu_t* E, uint64_t transfers, double out
 }
 
 extern "C" int tbgpu_bench_profile_mask(tbgpu_t* E, uint32_t mask) {
+    if (E->node) {
+        for (u32 d = 0; d < node_world(E->node); d++) tbgpu_bench_profile_mask(node_engine(E->node, d), mask);
+        return TBGPU_STATUS_OK;
+    }
     E->prof_mask = mask;
     return TBGPU_STATUS_OK;
 }
 
 extern "C" int tbgpu_device_alloc(tbgpu_t* E, uint64_t bytes, void** out) {
+    if (E->node) E = node_engine(E->node, 0);
     HIPCK(hipSetDevice(E->device));
     HIPCK(hipMalloc(out, bytes));
     return TBGPU_STATUS_OK;
 }
 
 extern "C" int tbgpu_device_free(tbgpu_t* E, void* ptr) {
+    if (E->node) E = node_engine(E->node, 0);
     HIPCK(hipSetDevice(E->device));
     HIPCK(hipFree(ptr));
     return TBGPU_STATUS_OK;
@@ -1430,6 +1503,7 @@ extern "C" int tbgpu_device_free(tbgpu_t* E, void* ptr) {
 // The replica's message pool is allocated once at init (static allocation); registering it lets
 // the prepare bodies go to HBM by DMA straight from the message, with no staging copy.
 extern "C" int tbgpu_register_host(tbgpu_t* E, void* ptr, uint64_t bytes) {
+    if (E->node) return node_api_register_host(E->node, ptr, bytes);
     HIPCK(hipSetDevice(E->device));
     HIPCK(hipHostRegister(ptr, bytes, hipHostRegisterMapped));
     void* dev = nullptr;
@@ -1439,6 +1513,7 @@ extern "C" int tbgpu_register_host(tbgpu_t* E, void* ptr, uint64_t bytes) {
 }
 
 extern "C" int tbgpu_unregister_host(tbgpu_t* E, void* ptr) {
+    if (E->node) return node_api_unregister_host(E->node, ptr);
     HIPCK(hipSetDevice(E->device));
     if (E->pending) {
         int st = engine_sync(E);
@@ -1456,6 +1531,7 @@ extern "C" int tbgpu_unregister_host(tbgpu_t* E, void* ptr) {
 }
 
 extern "C" int tbgpu_copy_to_host(tbgpu_t* E, void* dst, const void* src_dev, uint64_t bytes) {
+    if (E->node) E = node_engine(E->node, 0);
     HIPCK(hipSetDevice(E->device));
     HIPCK(hipStreamSynchronize(E->stream));
     HIPCK(hipMemcpy(dst, src_dev, bytes, hipMemcpyDeviceToHost));
@@ -1463,6 +1539,7 @@ extern "C" int tbgpu_copy_to_host(tbgpu_t* E, void* dst, const void* src_dev, ui
 }
 
 extern "C" int tbgpu_copy_to_device(tbgpu_t* E, void* dst_dev, const void* src, uint64_t bytes) {
+    if (E->node) E = node_engine(E->node, 0);
     HIPCK(hipSetDevice(E->device));
     HIPCK(hipStreamSynchronize(E->stream));
     HIPCK(hipMemcpy(dst_dev, src, bytes, hipMemcpyHostToDevice));
@@ -1470,6 +1547,13 @@ extern "C" int tbgpu_copy_to_device(tbgpu_t* E, void* dst_dev, const void* src, 
 }
 
 extern "C" int tbgpu_bench_reset_transfers(tbgpu_t* E) {
+    if (E->node) {
+        for (u32 d = 0; d < node_world(E->node); d++) {
+            const int st = tbgpu_bench_reset_transfers(node_engine(E->node, d));
+            if (st) return st;
+        }
+        return TBGPU_STATUS_OK;
+    }
     HIPCK(hipSetDevice(E->device));
     if (E->pending) {
         int st = engine_sync(E);
@@ -1488,6 +1572,7 @@ extern "C" int tbgpu_bench_reset_transfers(tbgpu_t* E) {
 }
 
 extern "C" int tbgpu_bench_pass_latencies(tbgpu_t* E, double* out_ms, uint64_t cap, uint64_t* count) {
+    if (E->node) E = node_engine(E->node, 0);
     if (E->pending) {
         int st = engine_sync(E);
         if (st) return st;
@@ -1499,12 +1584,14 @@ extern "C" int tbgpu_bench_pass_latencies(tbgpu_t* E, double* out_ms, uint64_t c
 }
 
 extern "C" int tbgpu_marker(tbgpu_t* E, uint32_t slot) {
+    if (E->node) E = node_engine(E->node, 0);
     if (slot >= 16) return fail(TBGPU_STATUS_INVALID, "marker slot");
     HIPCK(hipEventRecord(E->markers[slot], E->stream));
     return TBGPU_STATUS_OK;
 }
 
 extern "C" double tbgpu_marker_elapsed_ms(tbgpu_t* E, uint32_t a, uint32_t b) {
+    if (E->node) E = node_engine(E->node, 0);
     float ms = -1;
     if (a >= 16 || b >= 16) return -1;
     if (hipEventSynchronize(E->markers[b]) != hipSuccess) return -1;
@@ -1523,6 +1610,7 @@ extern "C" void tbgpu_homes(const uint64_t* ids, uint64_t n, uint32_t world, uin
 }
 
 extern "C" int tbgpu_route_init(tbgpu_t* E, uint32_t world, uint64_t events_max) {
+    if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (world == 0 || world > ROUTE_WORLD_MAX) return fail(TBGPU_STATUS_INVALID, "world %u out of range", world);
     if (E->r_home) return fail(TBGPU_STATUS_INVALID, "tbgpu_route_init called twice");
@@ -1558,6 +1646,7 @@ static int route_meta(tbgpu* E, u32 nb, const u64* timestamps, const u32* lens, 
 }
 
 extern "C" int tbgpu_route_homes(tbgpu_t* E, const uint64_t* ids_dev, uint64_t n, uint32_t world, uint8_t* out_dev) {
+    if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (world == 0 || world > ROUTE_WORLD_MAX) return fail(TBGPU_STATUS_INVALID, "world %u out of range", world);
     if (n == 0) return TBGPU_STATUS_OK;
@@ -1569,6 +1658,7 @@ extern "C" int tbgpu_route_homes(tbgpu_t* E, const uint64_t* ids_dev, uint64_t n
 
 extern "C" int tbgpu_route_dependents(tbgpu_t* E, uint32_t nb, const uint32_t* lens, const void* events_dev,
                                       const uint64_t* marked_ids, uint32_t n_marked, uint8_t* dep_dev) {
+    if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (!E->r_home) return fail(TBGPU_STATUS_INVALID, "tbgpu_route_init was not called");
     if (E->pending) {
@@ -1602,6 +1692,7 @@ extern "C" int tbgpu_route_dependents(tbgpu_t* E, uint32_t nb, const uint32_t* l
 extern "C" int tbgpu_route_plan_build(tbgpu_t* E, uint32_t nb, const uint64_t* timestamps, const uint32_t* lens,
                                       const void* events_dev, const uint8_t* skip_dev, void* send_events_dev,
                                       uint32_t* slot_dev, tbgpu_route_plan* plan) {
+    if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (!E->r_home) return fail(TBGPU_STATUS_INVALID, "tbgpu_route_init was not called");
     if (E->pending) {
@@ -1663,6 +1754,7 @@ extern "C" int tbgpu_route_plan_build(tbgpu_t* E, uint32_t nb, const uint64_t* t
 
 extern "C" int tbgpu_commit_routed_async(tbgpu_t* E, uint64_t n, const void* events_dev, uint64_t ts_max,
                                          uint32_t cert, uint8_t* codes_dev) {
+    if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (cert != TBGPU_CERT_U128 && cert != TBGPU_CERT_U64) return fail(TBGPU_STATUS_INVALID, "routed commit needs a certificate");
     if (n == 0) return TBGPU_STATUS_OK;
@@ -1699,6 +1791,7 @@ extern "C" int tbgpu_commit_routed_async(tbgpu_t* E, uint64_t n, const void* eve
 extern "C" int tbgpu_commit_routed_owner_async(tbgpu_t* E, uint64_t n, const void* events_dev, uint64_t ts_max,
                                                uint32_t cert, uint8_t* codes_dev, uint32_t world, uint32_t self,
                                                void* legs_dev, uint64_t legs_cap, uint64_t* leg_counts_dev) {
+    if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (cert != TBGPU_CERT_U128 && cert != TBGPU_CERT_U64) return fail(TBGPU_STATUS_INVALID, "routed commit needs a certificate");
     if (world == 0 || world > ROUTE_WORLD_MAX || self >= world) return fail(TBGPU_STATUS_INVALID, "owner world / rank");
@@ -1735,6 +1828,7 @@ extern "C" int tbgpu_commit_routed_owner_async(tbgpu_t* E, uint64_t n, const voi
 }
 
 extern "C" int tbgpu_apply_owner_legs_async(tbgpu_t* E, const void* legs_dev, uint64_t n, uint32_t cert) {
+    if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (cert != TBGPU_CERT_U128 && cert != TBGPU_CERT_U64) return fail(TBGPU_STATUS_INVALID, "owner legs need a certificate");
     if (n == 0) return TBGPU_STATUS_OK;
@@ -1751,6 +1845,7 @@ extern "C" int tbgpu_apply_owner_legs_async(tbgpu_t* E, const void* legs_dev, ui
 
 extern "C" int tbgpu_route_replies_async(tbgpu_t* E, uint32_t nb, const uint32_t* lens, const uint32_t* slot_dev,
                                          const uint8_t* codes_dev, void* results_dev, uint32_t* reply_bytes_dev) {
+    if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (!E->r_meta) return fail(TBGPU_STATUS_INVALID, "tbgpu_route_init was not called");
     if (nb == 0) return TBGPU_STATUS_OK;
@@ -1770,6 +1865,7 @@ extern "C" int tbgpu_route_replies_async(tbgpu_t* E, uint32_t nb, const uint32_t
 
 // Host <-> device staging through the lookup buffers, in chunks of lookup_cap.
 extern "C" int tbgpu_fetch_accounts(tbgpu_t* E, const uint64_t* ids, uint32_t n, void* out, uint8_t* found) {
+    if (E->node) return node_fetch(E->node, true, ids, n, (u8*)out, found);
     HIPCK(hipSetDevice(E->device));
     if (E->pending) {
         int st = engine_sync(E);
@@ -1790,6 +1886,7 @@ extern "C" int tbgpu_fetch_accounts(tbgpu_t* E, const uint64_t* ids, uint32_t n,
 }
 
 extern "C" int tbgpu_fetch_transfers(tbgpu_t* E, const uint64_t* ids, uint32_t n, void* out, uint8_t* state) {
+    if (E->node) return node_fetch(E->node, false, ids, n, (u8*)out, state);
     HIPCK(hipSetDevice(E->device));
     if (E->pending) {
         int st = engine_sync(E);
@@ -1818,7 +1915,7 @@ static int load_snapshot(tbgpu* E, const void* records, uint32_t n) {
     return TBGPU_STATUS_OK;
 }
 
-static int upsert_accounts(tbgpu* E, const void* records, uint32_t n, bool if_absent) {
+static int upsert_accounts(tbgpu* E, const void* records, uint32_t n, bool if_absent, bool keep_flow = false) {
     HIPCK(hipSetDevice(E->device));
     if (if_absent) {
         if (E->pending) {
@@ -1831,7 +1928,9 @@ static int upsert_accounts(tbgpu* E, const void* records, uint32_t n, bool if_ab
     // Balances set from elsewhere: the sequential replay stays exact.  A load of absent accounts
     // from a consistent forest snapshot keeps the flow path's invariants (pending balances cover
     // the outstanding pending transfers).
-    if (!if_absent) E->balances_set = true;
+    // keep_flow: balances a sequential commit from a consistent state produced (the node's
+    // sequencer write-back), so the invariants hold as well.
+    if (!if_absent && !keep_flow) E->balances_set = true;
     if (E->pending) {
         int st = engine_sync(E);
         if (st) return st;
@@ -1869,10 +1968,12 @@ static int upsert_accounts(tbgpu* E, const void* records, uint32_t n, bool if_ab
 }
 
 extern "C" int tbgpu_upsert_accounts(tbgpu_t* E, const void* records, uint32_t n) {
+    if (E->node) return node_api_accounts_in(E->node, records, n, false);
     return upsert_accounts(E, records, n, false);
 }
 
 extern "C" int tbgpu_load_accounts(tbgpu_t* E, const void* records, uint32_t n) {
+    if (E->node) return node_api_accounts_in(E->node, records, n, true);
     return upsert_accounts(E, records, n, true);
 }
 
@@ -1913,10 +2014,12 @@ static int upsert_transfers(tbgpu* E, const void* records, const uint8_t* state,
 }
 
 extern "C" int tbgpu_upsert_transfers(tbgpu_t* E, const void* records, const uint8_t* state, uint32_t n) {
+    if (E->node) return node_api_transfers_in(E->node, records, state, n, false);
     return upsert_transfers(E, records, state, n, false);
 }
 
 extern "C" int tbgpu_load_transfers(tbgpu_t* E, const void* records, const uint8_t* posted_state, uint32_t n) {
+    if (E->node) return node_api_transfers_in(E->node, records, posted_state, n, true);
     // posted_state is {0 none, 1 posted, 2 voided}; the upsert kernel takes 1 + that.
     std::vector<u8> st(n);
     for (u32 i = 0; i < n; i++) {
@@ -1929,6 +2032,7 @@ extern "C" int tbgpu_load_transfers(tbgpu_t* E, const void* records, const uint8
 // The replica writes commit_timestamp after every commit (= the prepare header's timestamp,
 // src/vsr/replica.zig:3664-3665) and on state sync; the engine's commit asserts use that value.
 extern "C" int tbgpu_set_commit_timestamp(tbgpu_t* E, uint64_t timestamp) {
+    if (E->node) return node_api_set_commit_timestamp(E->node, timestamp);
     HIPCK(hipSetDevice(E->device));
     if (E->pending) {
         int st = engine_sync(E);
@@ -1940,3 +2044,5 @@ extern "C" int tbgpu_set_commit_timestamp(tbgpu_t* E, uint64_t timestamp) {
     HIPCK(hipStreamSynchronize(E->stream));
     return TBGPU_STATUS_OK;
 }
+
+#include "node.h"

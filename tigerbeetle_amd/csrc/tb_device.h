@@ -203,10 +203,10 @@ struct Globals {
     u64 bounds_rounds;        // scan rounds they took (and the rounds of abandoned attempts)
     u64 bounds_skipped;       // dependent passes with an event the bounds do not cover (ordered run)
     u64 bounds_swept;         // units the in-order sweep decided (fl_sweep)
-    u64 sweep_ticks[3];
-    u64 flow_phase_ticks[8];
-    u64 flow_exec_ticks;
-    u64 sweep_u64_passes;     // sweeps that ran in the u64 X/Y form (bound + S >= 2^63)      // tb_flow run: lanes' time executing units, summed over lanes  // tb_flow wall-clock ticks per phase (k_flow.h FP_*)       // fl_sweep wall-clock ticks: the whole walk, its in-window loops, its memory waits
+    u64 sweep_ticks[3];       // fl_sweep wall-clock ticks: the whole walk, its in-window loops, its memory waits
+    u64 flow_phase_ticks[8];  // tb_flow wall-clock ticks per phase (k_flow.h FP_*)
+    u64 flow_exec_ticks;      // tb_flow run: lanes' time executing units, summed over lanes
+    u64 sweep_u64_passes;     // sweeps that ran in the u64 X/Y form (bound + S >= 2^63)
     u64 bounds_abandoned;     // passes whose bounds did not converge in FLOW_BOUNDS_ROUNDS_MAX rounds
     // tb_flow's two-level grid barrier (k_flow.h fl_grid_sync): FL_BAR_GROUPS group counters, the
     // root counter, the published generation; one 128-B line each.  Zeroed by tb_resolve every pass.

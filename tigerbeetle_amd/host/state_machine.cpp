@@ -58,6 +58,9 @@ StateMachine::StateMachine(const Options& o) {
     cfg.pass_batches_max = o.pass_batches_max;
     cfg.device = o.device;
     cfg.flags = o.profile ? TBGPU_CONFIG_PROFILE : 0;
+    if (o.devices.size() > TBGPU_DEVICES_MAX) throw std::invalid_argument("tbgpu_init: too many devices");
+    cfg.device_count = (uint32_t)o.devices.size();
+    for (size_t d = 0; d < o.devices.size(); d++) cfg.devices[d] = o.devices[d];
     const int st = tbgpu_init(&cfg, &engine_);
     if (st != TBGPU_STATUS_OK) {
         // init is the reference's only fallible call (`!StateMachine`).

@@ -130,6 +130,8 @@ struct Options {
     uint32_t pass_events_max = 8190 * 64;
     uint32_t pass_batches_max = 512;
     int32_t device = 0;
+    // Two or more entries: a node engine, one shard per listed device (tbgpu_config.devices).
+    std::vector<int32_t> devices;
     bool profile = false;
 };
 

@@ -33,6 +33,9 @@ class Options:
     pass_events_max: int = 8190 * 64
     pass_batches_max: int = 512
     device: int = 0
+    # Two or more HIP device ordinals: a node engine, one shard per entry (include/tbgpu.h
+    # tbgpu_config.devices; an ordinal may repeat: logical shards sharing one GPU).
+    devices: tuple = ()
     profile: bool = False
     sequential_fallback: bool = False  # ordered fallback on one lane (tb_replay) instead of tb_flow
     # Limit checks: "auto" (scan rounds while they decide enough, then the in-order sweep), "early"
@@ -46,7 +49,7 @@ class Options:
 
 
 class Engine:
-    """Thin ctypes handle over one tbgpu engine (one GPU)."""
+    """Thin ctypes handle over one tbgpu engine: one GPU, or a node of shards (Options.devices)."""
 
     def __init__(self, options=None, **kw):
         options = options or Options(**kw)
@@ -58,6 +61,12 @@ class Engine:
                                 | (_lib.CONFIG_SEQUENTIAL_FALLBACK if options.sequential_fallback else 0)
                                 | {"auto": 0, "early": _lib.CONFIG_SWEEP_EARLY,
                                    "off": _lib.CONFIG_SWEEP_OFF}[options.bounds_sweep])
+        devices = list(options.devices or ())
+        if len(devices) > len(cfg.devices):
+            raise ValueError("at most %d devices" % len(cfg.devices))
+        cfg.device_count = len(devices)
+        for i, d in enumerate(devices):
+            cfg.devices[i] = int(d)
         h = ctypes.c_void_p()
         _lib.check(self.lib.tbgpu_init(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
