@@ -33,6 +33,7 @@ The JSON line also carries:
                 every reply empty, no dependent event, debits == credits in total.
 """
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -44,6 +45,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+ctypes_u8 = ctypes.c_uint8
 METRIC = "transfers/sec committed (whole node, bit-exact results) + p99 batch latency"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 PCIE_PEAK_GBS = 63.0   # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s spec
@@ -86,6 +88,13 @@ def parse():
                    help="time the validate kernel's access pattern without its logic (roofline.access_mix)")
     p.add_argument("--host-prepares", type=int, default=600,
                    help="prepares committed one per tbgpu_commit call from host memory (the replica's call; 0: skip)")
+    p.add_argument("--engine", default="node", choices=["node", "ranks"],
+                   help="--gpus N > 1: 'node' = one tbgpu node engine over the N GPUs (include/tbgpu.h "
+                        "tbgpu_config.devices: what a replica binds), 'ranks' = one process per GPU over RCCL "
+                        "(tigerbeetle_amd/sharded.py)")
+    p.add_argument("--launch-check", action="store_true",
+                   help="launcher rehearsal (CPU): every rank reports its place in the process group and exits "
+                        "before touching a GPU")
     args = p.parse_args()
     if args.steps < 1:
         p.error("--steps must be at least 1 (the headline is measured over the timed steps)")
@@ -419,20 +428,61 @@ WORKLOAD_TEXT = {
 }
 
 
+def launch_ranks(n):
+    """`--gpus N` without a launcher around it: start N rank processes of this same command line
+    (torch.distributed.run, rendezvous on 127.0.0.1) before any GPU call, and exit with their code."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def launch_check(args, world, rank):
+    """Every rank joins the process group (gloo, CPU) and rank 0 prints who came: the launcher's
+    rehearsal, with no GPU call anywhere."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        got = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(got, torch.tensor([rank, world], dtype=torch.int64))
+        ranks = sorted(int(g[0]) for g in got)
+        worlds = sorted(set(int(g[1]) for g in got))
+        dist.destroy_process_group()
+    else:
+        ranks, worlds = [0], [1]
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "gpus": args.gpus, "engine": args.engine, "world": world,
+                          "ranks": ranks, "worlds": worlds}), flush=True)
+
+
 def main():
     args = parse()
     if args.chunk_prepares is None:
         args.chunk_prepares = CHUNK_PREPARES[args.workload]
-    import torch
-    import torch.distributed as dist
-
+    launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and args.engine == "ranks" and not launched:
+        sys.exit(launch_ranks(args.gpus))
+    if args.launch_check:
+        return launch_check(args, world, rank)
+    if launched and world > 1 and world != args.gpus:
+        raise SystemExit("bench.py: launched with %d ranks but --gpus %d" % (world, args.gpus))
+    import torch
+    import torch.distributed as dist
+
     if args.accounts is None:
-        args.accounts = 100_000_000 if world > 1 else 1_000_000
+        args.accounts = 100_000_000 if max(world, args.gpus) > 1 else 1_000_000
     if args.transfers is None:
-        args.transfers = 125_000_000 if world > 1 else 100_000_000
+        args.transfers = 125_000_000 if max(world, args.gpus) > 1 else 100_000_000
+    if args.gpus > 1 and args.engine == "node":
+        return run_node(args, world, rank)
     if world > 1 or args.sharded:
         assert args.workload == "c2", "the multi-GPU bench runs the C5 shape (uniform, no flags)"
         if args.same_device:
@@ -848,6 +898,207 @@ def run_sharded(args, world, rank, local_rank):
         print(json.dumps(line), flush=True)
     engine.close()
     dist.destroy_process_group()
+
+
+def numa_cpus(device):
+    """CPUs of the NUMA node a GPU hangs off (None when the topology is not visible)."""
+    import torch
+    try:
+        p = torch.cuda.get_device_properties(device)
+        bdf = "%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+        with open("/sys/bus/pci/devices/%s/numa_node" % bdf) as f:
+            node = int(f.read())
+        if node < 0:
+            return None, None
+        cpus = set()
+        with open("/sys/devices/system/node/node%d/cpulist" % node) as f:
+            for part in f.read().strip().split(","):
+                a, _, b = part.partition("-")
+                cpus.update(range(int(a), int(b or a) + 1))
+        cpus &= os.sched_getaffinity(0)
+        return node, cpus or None
+    except (OSError, ValueError, RuntimeError, AttributeError, AssertionError):
+        return None, None
+
+
+def run_node(args, procs, rank):
+    """--gpus N (engine "node"): BASELINE.json configs[4] ("C5") on ONE tbgpu node engine over the N
+    GPUs — the handle a replica binds (include/tbgpu.h tbgpu_config.devices, csrc/node.h): 100M
+    accounts (records replicated, balances on their owner GPU), 125M uniform transfers per GPU (1B
+    over 8), every pass of N x chunk prepares routed across the GPUs inside the library (each GPU pulls
+    its block of prepares over its own PCIe link, routes it, homes gather their transfers from the
+    sources' HBM over xGMI, owners pull their balance legs, sources pull their result codes).
+
+    Under torchrun (WORLD_SIZE = N, the driver's launch) rank 0 drives the node and the other ranks
+    only take part in the step barriers and the max-over-ranks timing (gloo: they touch no GPU)."""
+    import torch
+    import torch.distributed as dist
+
+    if procs > 1:
+        dist.init_process_group("gloo")
+    n_steps = args.warmup + args.steps
+
+    def barrier():
+        if procs > 1:
+            dist.barrier()
+
+    if rank != 0:  # followers: the barriers of every step, then the timing reduction
+        for _ in range(n_steps):
+            barrier()
+            barrier()
+        t = torch.zeros(args.steps, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.destroy_process_group()
+        return
+
+    from tigerbeetle_amd.state_machine import Engine, Options
+
+    N = args.gpus
+    devices = [0] * N if args.same_device else list(range(N))
+    chunk = args.chunk_prepares
+    T = args.transfers * N
+    engine = Engine(Options(accounts_max=args.accounts, transfers_max=T, pass_events_max=chunk * args.batch,
+                            pass_batches_max=chunk, devices=tuple(devices), profile=bool(args.profile)))
+    engine.profile_mask(engine.PROF_VALIDATE | engine.PROF_REPLAY)
+
+    # Accounts: generated on the first GPU in chunks, committed from host memory (every shard commits
+    # every create_accounts prepare: the records are replicated).
+    acct_lens = batches(args.accounts, args.batch)
+    acct_ts, t_end = timestamps(acct_lens, 1_000_000_000)
+    a_chunk = 2048 * args.batch
+    dev_buf = engine.alloc(a_chunk * 128)
+    for a0 in range(0, args.accounts, a_chunk):
+        n_a = min(a_chunk, args.accounts - a0)
+        engine.generate_accounts(dev_buf, a0, n_a, seed=args.seed)
+        host = engine.to_host(dev_buf, n_a * 128)
+        k0 = a0 // args.batch
+        lens_a = batches(n_a, args.batch)
+        rb, _, _ = engine.commit_pipelined(128, acct_ts[k0:k0 + len(lens_a)], lens_a, host, chunk_batches=chunk)
+        assert int(rb.sum()) == 0, "account creation returned errors"
+    engine.free(dev_buf)
+
+    # Transfers: prepare k of pass p = k // (N chunk) goes to source GPU d = (k mod N chunk) // chunk
+    # (tbgpu_config.devices: block d of a pass); each GPU's prepares sit in host memory on its own
+    # NUMA node, registered once (the replica's message pool).
+    lens = batches(T, args.batch)
+    n_prep = len(lens)
+    per_pass = N * chunk
+    src_of = (np.arange(n_prep) % per_pass) // chunk
+    starts = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    x_chunk = max(1, (1 << 24) // args.batch) * args.batch  # whole prepares per generation chunk
+    gen = engine.alloc(min(T, x_chunk) * 128)
+    buffers, ptrs = [], np.zeros(n_prep, dtype=np.uint64)
+    nodes = []
+    for d in range(N):
+        mine = np.nonzero(src_of == d)[0]
+        n_ev = int(sum(lens[k] for k in mine))
+        node, cpus = numa_cpus(devices[d])
+        nodes.append(node)
+        old_aff = os.sched_getaffinity(0)
+        if cpus:
+            os.sched_setaffinity(0, cpus)
+        buf = np.empty(max(n_ev, 1) * 128, dtype=np.uint8)
+        buf[::4096] = 0  # first touch from this GPU's NUMA node
+        if cpus:
+            os.sched_setaffinity(0, old_aff)
+        off = 0
+        for k in mine:
+            ptrs[k] = buf.ctypes.data + off * 128
+            off += lens[k]
+        buffers.append(buf)
+    # Fill: the global transfer sequence, generated in chunks, scattered prepare by prepare.
+    k_pos = 0
+    for x0 in range(0, T, x_chunk):
+        n_x = min(x_chunk, T - x0)
+        engine.generate_transfers(gen, x0, n_x, args.accounts, seed=args.seed)
+        host = engine.to_host(gen, n_x * 128)
+        while k_pos < n_prep and starts[k_pos + 1] <= x0 + n_x:
+            a, b = int(starts[k_pos]) - x0, int(starts[k_pos + 1]) - x0
+            dst = np.frombuffer((ctypes_u8 * ((b - a) * 128)).from_address(int(ptrs[k_pos])), dtype=np.uint8)
+            dst[:] = host[a * 128:b * 128]
+            k_pos += 1
+        assert k_pos == n_prep or starts[k_pos] >= x0 + n_x, "prepares straddle a generation chunk"
+    engine.free(gen)
+    for buf in buffers:
+        engine.register_host(buf)
+    replies = np.empty(T * 8, dtype=np.uint8)
+
+    step_ms, lat_all = [], []
+    t_cursor = t_end
+    rb = None
+    for step in range(n_steps):
+        timed = step >= args.warmup
+        engine.reset_transfers()
+        ts, t_cursor = timestamps(lens, t_cursor + 10)
+        if timed and step == args.warmup:
+            engine.reset_stats()
+        barrier()
+        t0 = time.perf_counter()
+        rb, lat = engine.commit_pipelined_ptrs(129, ts, lens, ptrs, replies, chunk_batches=chunk, latency=True)
+        dt = time.perf_counter() - t0
+        barrier()
+        if timed:
+            step_ms.append(dt * 1e3)
+            lat_all.append(lat)
+    stats = engine.stats()
+    t = torch.tensor(step_ms, dtype=torch.float64)
+    if procs > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    step_ms = [float(x) for x in t.tolist()]
+    summ = engine.ledger_summary()
+    for buf in buffers:
+        engine.unregister_host(buf)
+    n_failed = int(rb.sum()) // 8
+    full_ok = bool(n_failed == 0 and stats["transfers"] == T and summ["debits_posted"] == summ["credits_posted"]
+                   and summ["debits_posted"] > 0 and summ["debits_pending"] == summ["credits_pending"]
+                   and summ["stray"] == 0 and summ["accounts"] == args.accounts)
+    total_ms = sum(step_ms)
+    value = T * args.steps / (total_ms / 1e3)
+    lat = np.sort(np.concatenate(lat_all)) if lat_all else np.array([float("nan")])
+    per_launch = T / max(1, stats["launches_validate"] / max(1, args.steps))
+    u_over_t = expected_unique(args.accounts, 2 * per_launch) / per_launch
+    roof = roofline(stats, u_over_t, per_launch, argparse.Namespace(transfers=T, steps=args.steps), total_ms)
+    pcie_gbs = T * 128 * args.steps / (total_ms / 1e3) / 1e9
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "transfers/s",
+        "n_gpus": N,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(total_ms / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u128",
+        "data": "synthetic (generated on the GPU in the reference benchmark's shapes, copied to host memory before "
+                "timing)",
+        "config": {"workload": "C5 (BASELINE.json configs[4]): %d accounts, balances owner-partitioned by hash(id) over "
+                               "%d GPUs (records replicated), %d uniform transfers per GPU (%d in all), prepares of %d"
+                               % (args.accounts, N, args.transfers, T, args.batch),
+                   "prepares_per_step": n_prep, "chunk_prepares_per_gpu": chunk,
+                   "engine": "one tbgpu node engine (include/tbgpu.h tbgpu_config.devices = %s), driven by one "
+                             "process; %d process(es) launched" % (devices, procs),
+                   "input": "prepare bodies in registered host memory on each GPU's NUMA node (%s); PCIe H2D and "
+                            "replies inside the timed region" % nodes,
+                   "parallelism": "shard%d (transfer home = hash(id), balance legs to owner GPUs, peer reads over "
+                                  "xGMI inside the library)" % N},
+        "p99_batch_latency_ms": round(ref_percentile(lat, 99), 3),
+        "batch_latency_ms": dict(deciles(lat), definition=(
+            "per prepare, submit to reply: from the start of its block's PCIe copy to its reply landing in host "
+            "memory (device clock of its source GPU); percentiles by src/benchmark.zig:454-471")),
+        "pcie": {"achieved_per_gpu": round(pcie_gbs / N, 2), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(pcie_gbs / N / PCIE_PEAK_GBS, 4), "measured_ceiling": PCIE_MEASURED_GBS,
+                 "frac_of_measured": round(pcie_gbs / N / PCIE_MEASURED_GBS, 4)},
+        "failed_events": n_failed,
+        "roofline": roof,
+        "cpu_baseline": None,
+        "parity": {"full_run_properties": full_ok, "ledger": {k: str(v) for k, v in summ.items()}},
+    }
+    print(json.dumps(line), flush=True)
+    engine.close()
+    if procs > 1:
+        dist.destroy_process_group()
 
 
 FLOW_PHASES = ("plan", "sort", "link", "bounds_setup", "bounds_rounds", "sweep", "run_or_apply", "replies_wg0")

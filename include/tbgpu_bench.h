@@ -56,6 +56,17 @@ int tbgpu_bench_legs_min_events(tbgpu_t* engine, uint32_t events);
  * kernel's practical bound for its access pattern; allocates and frees its own buffers. */
 int tbgpu_bench_access_mix(tbgpu_t* engine, uint64_t transfers, double out_ms[7]);
 
+/* Size-independent properties of a full-size run without exporting the tables: the sums of the
+ * four balance fields over every account (u128, as {lo, hi} pairs: dp, dpost, cp, cpost), the live
+ * accounts, and — on a node engine — the accounts whose balances sit on a shard that is not their
+ * owner (must be 0).  On a node the sums are over every shard. */
+typedef struct tbgpu_ledger_summary {
+    uint64_t sums[8];
+    uint64_t accounts;
+    uint64_t stray;
+} tbgpu_ledger_summary;
+int tbgpu_bench_ledger_summary(tbgpu_t* engine, tbgpu_ledger_summary* out);
+
 /* Device memory helpers for callers without a device allocator (ctypes users). */
 int tbgpu_device_alloc(tbgpu_t* engine, uint64_t bytes, void** out);
 int tbgpu_device_free(tbgpu_t* engine, void* ptr);

@@ -85,6 +85,10 @@ class tbgpu_workload(ctypes.Structure):
     ]
 
 
+class tbgpu_ledger_summary(ctypes.Structure):
+    _fields_ = [("sums", ctypes.c_uint64 * 8), ("accounts", ctypes.c_uint64), ("stray", ctypes.c_uint64)]
+
+
 WORLD_MAX = 64
 DIRTY_FLAGS, DIRTY_LIMIT = 1, 2
 CERT_U128, CERT_U64 = 1, 2
@@ -133,6 +137,7 @@ SIGNATURES = [
     ("tbgpu_bench_profile_mask", ctypes.c_int, [_P, _U32]),
     ("tbgpu_bench_legs_min_events", ctypes.c_int, [_P, _U32]),
     ("tbgpu_bench_access_mix", ctypes.c_int, [_P, _U64, ctypes.POINTER(ctypes.c_double)]),
+    ("tbgpu_bench_ledger_summary", ctypes.c_int, [_P, ctypes.POINTER(tbgpu_ledger_summary)]),
     ("tbgpu_device_alloc", ctypes.c_int, [_P, _U64, ctypes.POINTER(_P)]),
     ("tbgpu_device_free", ctypes.c_int, [_P, _P]),
     ("tbgpu_copy_to_host", ctypes.c_int, [_P, _P, _P, _U64]),

@@ -23,6 +23,7 @@
 #include "k_aux.h"
 #include "k_replay.h"
 #include "k_route.h"
+#include "k_node.h"
 #include "k_workload.h"
 #include "checksum.h"
 
@@ -145,10 +146,13 @@ struct tbgpu {
     u64 wall_khz = 0;  // device wall clock (flow phase timing)
     // Groove write-back snapshot (tbgpu_checkpoint_delta), allocated on first use.
     AccountBal* ckpt_bal = nullptr;  // balances at the previous write-back
-    u8* ckpt_posted = nullptr;       // posted bytes at the previous write-back
+    u32* ckpt_mark = nullptr;        // per slot: the write-back epoch that last covered it
+    u32 ckpt_epoch = 0;
     u64 ckpt_pos = 0;                // log position of the first transfer not yet written back
     u64 ckpt_ts = 0;                 // commit timestamp at the previous write-back
     bool ckpt_valid = false;         // false: the snapshot is the empty state (zeroes)
+    bool ckpt_scan = false;          // accounts created that ckpt_ids lacks: diff the whole table next
+    std::vector<u64> ckpt_ids;       // ids (lo, hi) of create_accounts events / direct balance writes since
     u32 prof_mask = ~0u;  // kernels timed when profiling (1 << K_*; tbgpu_bench_profile_mask)
     u32 ablate = 0;  // TBGPU_TIMING_KNOBS builds only
     std::vector<hipEvent_t> event_pool;
@@ -171,6 +175,8 @@ struct tbgpu {
     u64* r_meta = nullptr;    // device [meta_cap + 1] offsets then [meta_cap] timestamps
     u64* h_rmeta = nullptr;   // pinned mirror
 };
+
+static void ckpt_note_ids(tbgpu* E, const u8* records, u64 n);
 
 // Pinned reply arena of one pipeline slot: head {panic, commit_ts}, reply bytes per prepare, then
 // the results of every event of the chunk (8 B each, the worst case).
@@ -492,7 +498,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
     if (!E) return;
     (void)hipSetDevice(E->device);
     if (E->stream) (void)hipStreamSynchronize(E->stream);
-    void* bufs[] = {E->ckpt_bal, E->ckpt_posted, E->T.acct_hot, E->T.acct_bal, E->T.acct_cold, E->T.account_mark, E->T.xidx, E->T.xdup, E->T.xlog,
+    void* bufs[] = {E->ckpt_bal, E->ckpt_mark, E->T.acct_hot, E->T.acct_bal, E->T.acct_cold, E->T.account_mark, E->T.xidx, E->T.xdup, E->T.xlog,
                     E->T.xposted, E->g, E->info, E->eflags, E->dr,
                     E->cr, E->ps, E->rs, E->dep_list, E->dep_count, E->amt, E->kid, E->kpid, E->dedup,
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
@@ -527,6 +533,8 @@ extern "C" int tbgpu_reset(tbgpu_t* E) {
     if (E->node) return node_api_reset(E->node);
     HIPCK(hipSetDevice(E->device));
     E->ckpt_valid = false;
+    E->ckpt_scan = false;
+    std::vector<u64>().swap(E->ckpt_ids);
     return engine_clear(E);
 }
 
@@ -601,6 +609,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.routed = routed ? 1 : 0;
         P.codes = codes;
         P.cert_ext = cert_ext;
+        P.seq_pv = E->balances_set ? 1u : 0u;
         // Legs pay a fixed ~30 us (one workgroup per bucket, LDS sums) that no-return atomics in
         // the resolve kernel (~20 G/s) only cost beyond ~LEGS_MIN_EVENTS events: the replica's
         // one-prepare commits take the atomics.
@@ -782,6 +791,9 @@ static int commit_host(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const
         lens[k] = input_lens[k] / 128;
         if (out_caps && (u64)out_caps[k] < (u64)lens[k] * 8) return fail(TBGPU_STATUS_INVALID, "output too small");
     }
+    if (op == OP_CREATE_ACCOUNTS) {  // the next write-back looks these ids up
+        for (u32 k = 0; k < n; k++) ckpt_note_ids(E, (const u8*)inputs[k], lens[k]);
+    }
     // Split into calls whose events fit the staging buffer.
     u32 k0 = 0;
     while (k0 < n) {
@@ -872,6 +884,9 @@ static int commit_pipelined(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, 
     if (op == OP_CREATE_TRANSFERS && E->log_next + total > E->xlog_cap) {
         return fail(TBGPU_STATUS_INVALID, "transfer log full (%llu + %llu events > capacity %llu)",
                     (unsigned long long)E->log_next, (unsigned long long)total, (unsigned long long)E->xlog_cap);
+    }
+    if (op == OP_CREATE_ACCOUNTS) {  // the next write-back looks these ids up
+        for (u32 k = 0; k < n; k++) ckpt_note_ids(E, (const u8*)inputs[k], lens[k]);
     }
     const u32 per_chunk = std::max<u32>(1, std::min<u32>(chunk_batches ? chunk_batches : E->pb_max, E->pb_max));
     struct Chunk {
@@ -1029,6 +1044,7 @@ extern "C" int tbgpu_commit_device_async(tbgpu_t* E, uint8_t operation, uint32_t
     int st = prepare_call(E, operation, n_batches, timestamps, batch_lens, floor_ts, &total);
     if (st) return st;
     std::vector<u64> h_off(E->h_meta, E->h_meta + n_batches + 1);
+    if (operation == OP_CREATE_ACCOUNTS) E->ckpt_scan = true;  // ids in device memory: diff the table next
     st = enqueue_call(E, operation, n_batches, h_off.data(), (const u8*)events_dev, (u32*)results_dev, reply_bytes_dev);
     if (st) return st;
     E->pending = true;
@@ -1055,6 +1071,12 @@ extern "C" int tbgpu_test_set_balances(tbgpu_t* E, uint64_t id_lo, uint64_t id_h
         if (st) return st;
     }
     E->balances_set = true;  // the flow path's post/void argument needs consistent pending balances
+    {
+        u8 rec[128] = {};
+        memcpy(rec, &id_lo, 8);
+        memcpy(rec + 8, &id_hi, 8);
+        ckpt_note_ids(E, rec, 1);
+    }
     hipLaunchKernelGGL(tb_set_balances, dim3(1), dim3(1), 0, E->stream, E->T, id_lo, id_hi, b[0], b[1], b[2], b[3],
                        b[4], b[5], b[6], b[7], E->d_status);
     HIPCK(hipGetLastError());
@@ -1177,20 +1199,216 @@ extern "C" int tbgpu_export_posted(tbgpu_t* E, uint64_t* out_pairs, uint64_t cap
 // its forest since the previous call (or since init / reset) — state_machine.zig:542-582 with the
 // groove semantics of src/lsm/groove.zig:902-963.  Accounts by id, transfers and posted pairs by
 // timestamp.  If a buffer is too small nothing advances: *counts holds the sizes needed.
+//
+// The cost is O(changes), not O(tables) (the reference's groove put / upsert per changed object):
+//   * transfers: the log positions written since the previous write-back, each checked live by one
+//     index probe (tb_delta_log);
+//   * posted-groove entries: one per new post / void record (the pending transfer's timestamp,
+//     posted or voided: state_machine.zig:988-990);
+//   * accounts: the debit and credit accounts of the new transfers, plus the ids of create_accounts
+//     events and of direct balance writes the engine listed since — each looked up once and emitted
+//     if created since or re-balanced (tb_delta_ids).  Only create_accounts committed from device
+//     memory (or more than CKPT_IDS_MAX listed ids) makes the next write-back diff the whole account
+//     table instead (tb_delta_accounts).
 // The write-back snapshot exists and describes the previous write-back (the empty state if none).
 static int ckpt_snapshot_ready(tbgpu* E) {
     if (!E->ckpt_bal) {
         HIPCK(hipMalloc(&E->ckpt_bal, E->account_cap * sizeof(AccountBal)));
-        HIPCK(hipMalloc(&E->ckpt_posted, E->xlog_cap));
+        HIPCK(hipMalloc(&E->ckpt_mark, E->account_cap * sizeof(u32)));
+        HIPCK(hipMemsetAsync(E->ckpt_mark, 0, E->account_cap * sizeof(u32), E->stream));
+        E->ckpt_epoch = 0;
     }
     if (!E->ckpt_valid) {  // the previous write-back is the empty state
         HIPCK(hipMemsetAsync(E->ckpt_bal, 0, E->account_cap * sizeof(AccountBal), E->stream));
-        HIPCK(hipMemsetAsync(E->ckpt_posted, 0, E->xlog_cap, E->stream));
         E->ckpt_pos = 0;
         E->ckpt_ts = 0;
         E->ckpt_valid = true;
     }
     return TBGPU_STATUS_OK;
+}
+
+// Listed since the previous write-back (host side): ids of create_accounts events and of direct
+// balance writes.  Past CKPT_IDS_MAX the list gives way to one whole-table diff.
+#define CKPT_IDS_MAX (1ULL << 24)
+static void ckpt_note_ids(tbgpu* E, const u8* records, u64 n) {
+    if (E->ckpt_scan) return;
+    if (E->ckpt_ids.size() / 2 + n > CKPT_IDS_MAX) {
+        E->ckpt_scan = true;
+        std::vector<u64>().swap(E->ckpt_ids);
+        return;
+    }
+    for (u64 i = 0; i < n; i++) {
+        E->ckpt_ids.push_back(*(const u64*)(records + i * 128));
+        E->ckpt_ids.push_back(*(const u64*)(records + i * 128 + 8));
+    }
+}
+
+// The live transfers written since the previous write-back (appended to `out`, unsorted).
+static int delta_transfers(tbgpu* E, std::vector<u8>& out) {
+    int st = ckpt_snapshot_ready(E);
+    if (st) return st;
+    const u64 chunk = 1ULL << 20;
+    u8* d_out = nullptr;
+    u64* d_cnt = nullptr;
+    hipError_t err = hipMalloc(&d_out, std::min<u64>(chunk, std::max<u64>(1, E->log_next - E->ckpt_pos)) * 128);
+    if (err == hipSuccess) err = hipMalloc(&d_cnt, 8);
+    for (u64 s = E->ckpt_pos; s < E->log_next && err == hipSuccess; s += chunk) {
+        const u64 n = std::min<u64>(chunk, E->log_next - s);
+        u64 cnt = 0;
+        err = hipMemsetAsync(d_cnt, 0, 8, E->stream);
+        if (err != hipSuccess) break;
+        hipLaunchKernelGGL(tb_delta_log, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T, s, n, E->ckpt_ts,
+                           d_out, d_cnt);
+        err = hipGetLastError();
+        if (err == hipSuccess) err = hipMemcpyAsync(&cnt, d_cnt, 8, hipMemcpyDeviceToHost, E->stream);
+        if (err == hipSuccess) err = hipStreamSynchronize(E->stream);
+        if (err == hipSuccess && cnt) {
+            const size_t at = out.size();
+            out.resize(at + cnt * 128);
+            err = hipMemcpy(out.data() + at, d_out, cnt * 128, hipMemcpyDeviceToHost);
+        }
+    }
+    if (d_out) (void)hipFree(d_out);
+    if (d_cnt) (void)hipFree(d_cnt);
+    if (err != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "checkpoint delta (transfers): %s", hipGetErrorString(err));
+    return TBGPU_STATUS_OK;
+}
+
+// The accounts among `ids` created or re-balanced since the previous write-back (records and the
+// balances the forest holds for them), or — after create_accounts the engine could not list — every
+// such account of the table.  `slots` / `scanned`: what delta_advance moves the snapshot over.
+static int delta_accounts(tbgpu* E, const std::vector<u64>& ids, std::vector<u8>& accts, std::vector<u8>& before,
+                          std::vector<u32>& slots, bool* scanned) {
+    int st = ckpt_snapshot_ready(E);
+    if (st) return st;
+    *scanned = E->ckpt_scan;
+    const u64 chunk = 1ULL << 20;
+    u8* d_out = nullptr;
+    u8* d_before = nullptr;
+    u64* d_cnt = nullptr;
+    u64* d_ids = nullptr;
+    u32* d_slots = nullptr;
+    hipError_t err = hipMalloc(&d_out, chunk * 128);
+    if (err == hipSuccess) err = hipMalloc(&d_before, chunk * sizeof(AccountBal));
+    if (err == hipSuccess) err = hipMalloc(&d_cnt, 16);
+    if (err == hipSuccess && !*scanned) err = hipMalloc(&d_ids, chunk * 16);
+    if (err == hipSuccess && !*scanned) err = hipMalloc(&d_slots, chunk * 4);
+    const u64 total = *scanned ? E->account_cap : ids.size() / 2;
+    if (!*scanned && ++E->ckpt_epoch == 0) {  // one epoch per call; wrapped: no stale mark may equal it
+        if (err == hipSuccess) err = hipMemsetAsync(E->ckpt_mark, 0, E->account_cap * sizeof(u32), E->stream);
+        E->ckpt_epoch = 1;
+    }
+    for (u64 s = 0; s < total && err == hipSuccess; s += chunk) {
+        const u64 n = std::min<u64>(chunk, total - s);
+        u64 cnt[2] = {0, 0};
+        err = hipMemsetAsync(d_cnt, 0, 16, E->stream);
+        if (err != hipSuccess) break;
+        if (*scanned) {
+            hipLaunchKernelGGL(tb_delta_accounts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T,
+                               E->ckpt_bal, E->ckpt_ts, s, s + n, d_out, chunk, d_cnt, (AccountBal*)d_before);
+        } else {
+            err = hipMemcpyAsync(d_ids, ids.data() + 2 * s, n * 16, hipMemcpyHostToDevice, E->stream);
+            if (err != hipSuccess) break;
+            hipLaunchKernelGGL(tb_delta_ids, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T, E->ckpt_bal,
+                               E->ckpt_ts, d_ids, n, E->ckpt_mark, E->ckpt_epoch, d_out, (AccountBal*)d_before, d_cnt, d_slots,
+                               d_cnt + 1);
+        }
+        err = hipGetLastError();
+        if (err == hipSuccess) err = hipMemcpyAsync(cnt, d_cnt, 16, hipMemcpyDeviceToHost, E->stream);
+        if (err == hipSuccess) err = hipStreamSynchronize(E->stream);
+        if (err == hipSuccess && cnt[0]) {  // one chunk holds at most `chunk` accounts
+            const size_t at = accts.size();
+            accts.resize(at + cnt[0] * 128);
+            before.resize(before.size() + cnt[0] * sizeof(AccountBal));
+            err = hipMemcpy(accts.data() + at, d_out, cnt[0] * 128, hipMemcpyDeviceToHost);
+            if (err == hipSuccess) err = hipMemcpy(before.data() + at / 2, d_before, cnt[0] * sizeof(AccountBal), hipMemcpyDeviceToHost);
+        }
+        if (err == hipSuccess && !*scanned && cnt[1]) {
+            const size_t at = slots.size();
+            slots.resize(at + cnt[1]);
+            err = hipMemcpy(slots.data() + at, d_slots, cnt[1] * 4, hipMemcpyDeviceToHost);
+        }
+    }
+    void* bufs[] = {d_out, d_before, d_cnt, d_ids, d_slots};
+    for (void* p : bufs) if (p) (void)hipFree(p);
+    if (err != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "checkpoint delta (accounts): %s", hipGetErrorString(err));
+    return TBGPU_STATUS_OK;
+}
+
+// The write-back happened: the snapshot takes the covered balances, the log and commit positions move.
+static int delta_advance(tbgpu* E, const std::vector<u32>& slots, bool scanned) {
+    if (scanned) {
+        HIPCK(hipMemcpyAsync(E->ckpt_bal, E->T.acct_bal, E->account_cap * sizeof(AccountBal), hipMemcpyDeviceToDevice,
+                             E->stream));
+    } else if (!slots.empty()) {
+        u32* d_slots = nullptr;
+        HIPCK(hipMalloc(&d_slots, slots.size() * 4));
+        hipError_t err = hipMemcpyAsync(d_slots, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, E->stream);
+        if (err == hipSuccess) {
+            hipLaunchKernelGGL(tb_delta_advance, dim3((unsigned)((slots.size() + 255) / 256)), dim3(256), 0, E->stream, E->T,
+                               E->ckpt_bal, d_slots, (u64)slots.size());
+            err = hipGetLastError();
+        }
+        if (err == hipSuccess) err = hipStreamSynchronize(E->stream);
+        (void)hipFree(d_slots);
+        if (err != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "checkpoint advance: %s", hipGetErrorString(err));
+    }
+    HIPCK(hipStreamSynchronize(E->stream));
+    E->ckpt_pos = E->log_next;
+    E->ckpt_ts = E->commit_ts;
+    E->ckpt_scan = false;
+    std::vector<u64>().swap(E->ckpt_ids);
+    return TBGPU_STATUS_OK;
+}
+
+// Ids of the accounts the new transfers moved (debit and credit of each).
+static void delta_transfer_accounts(const std::vector<u8>& xfers, std::vector<u64>& ids) {
+    const u64 n = xfers.size() / 128;
+    for (u64 i = 0; i < n; i++) {
+        const u64* w = (const u64*)&xfers[i * 128];
+        ids.push_back(w[2]);
+        ids.push_back(w[3]);
+        ids.push_back(w[4]);
+        ids.push_back(w[5]);
+    }
+}
+
+// The post / void records among the new transfers: their pending ids and the new posted state.
+static void delta_post_void(const std::vector<u8>& xfers, std::vector<u64>& pending_ids, std::vector<u8>& voided) {
+    const u64 n = xfers.size() / 128;
+    for (u64 i = 0; i < n; i++) {
+        const u8* r = &xfers[i * 128];
+        const u16 f = *(const u16*)(r + 118);
+        if (!(f & (TF_POST | TF_VOID))) continue;
+        pending_ids.push_back(*(const u64*)(r + 64));
+        pending_ids.push_back(*(const u64*)(r + 72));
+        voided.push_back((f & TF_POST) ? 0 : 1);
+    }
+}
+
+// Sorted outputs of a write-back.
+static void delta_emit(const std::vector<u8>& accts, const std::vector<u8>& before, const std::vector<u8>& xfers,
+                       const std::vector<std::pair<u64, u64>>& posted, void* accounts_out, void* accounts_before_out,
+                       void* transfers_out, u64* posted_out) {
+    const u64 na = accts.size() / 128, nt = xfers.size() / 128;
+    std::vector<u64> idx(na);
+    for (u64 i = 0; i < na; i++) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](u64 a, u64 b) { return id_less(&accts[a * 128], &accts[b * 128]); });
+    for (u64 i = 0; i < na; i++) memcpy((u8*)accounts_out + i * 128, &accts[idx[i] * 128], 128);
+    if (accounts_before_out) {
+        for (u64 i = 0; i < na; i++) memcpy((u8*)accounts_before_out + i * 64, &before[idx[i] * 64], 64);
+    }
+    auto ts_of = [&](u64 i) { return *(const u64*)&xfers[i * 128 + 120]; };
+    idx.resize(nt);
+    for (u64 i = 0; i < nt; i++) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](u64 a, u64 b) { return ts_of(a) < ts_of(b); });
+    for (u64 i = 0; i < nt; i++) memcpy((u8*)transfers_out + i * 128, &xfers[idx[i] * 128], 128);
+    std::vector<std::pair<u64, u64>> pairs(posted);
+    std::sort(pairs.begin(), pairs.end());
+    for (u64 i = 0; i < pairs.size(); i++) {
+        posted_out[2 * i] = pairs[i].first;
+        posted_out[2 * i + 1] = pairs[i].second;
+    }
 }
 
 extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, void* accounts_before_out, uint64_t accounts_cap,
@@ -1204,96 +1422,38 @@ extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, void* acco
         int st = engine_sync(E);
         if (st) return st;
     }
-    int st0 = ckpt_snapshot_ready(E);
-    if (st0) return st0;
-    const u64 chunk = 1ULL << 20;
-    std::vector<u8> accts, xfers, before;
-    std::vector<u64> posted;
-    u8* d_out = nullptr;
-    u8* d_before = nullptr;
-    u64* d_cnt = nullptr;
-    u64* d_posted = nullptr;
-    hipError_t err = hipMalloc(&d_out, chunk * 128);
-    if (err == hipSuccess) err = hipMalloc(&d_cnt, 24);
-    if (err == hipSuccess) err = hipMalloc(&d_posted, chunk * 16);
-    if (err == hipSuccess) err = hipMalloc(&d_before, chunk * sizeof(AccountBal));
-    for (int pass = 0; pass < 2 && err == hipSuccess; pass++) {
-        const u64 cap = pass == 0 ? E->account_cap : E->xidx_cap;
-        for (u64 s = 0; s < cap && err == hipSuccess; s += chunk) {
-            const u64 n = std::min<u64>(chunk, cap - s);
-            err = hipMemsetAsync(d_cnt, 0, 24, E->stream);
-            if (err != hipSuccess) break;
-            if (pass == 0) {
-                hipLaunchKernelGGL(tb_delta_accounts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T,
-                                   E->ckpt_bal, E->ckpt_ts, s, s + n, d_out, chunk, d_cnt, (AccountBal*)d_before);
-            } else {
-                hipLaunchKernelGGL(tb_delta_transfers, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T,
-                                   E->ckpt_posted, E->ckpt_pos, E->ckpt_ts, s, n, d_out, chunk, d_cnt, d_posted, chunk,
-                                   d_cnt + 1);
-            }
-            err = hipGetLastError();
-            u64 cnt[2] = {0, 0};
-            if (err == hipSuccess) err = hipMemcpyAsync(cnt, d_cnt, 16, hipMemcpyDeviceToHost, E->stream);
-            if (err == hipSuccess) err = hipStreamSynchronize(E->stream);
-            std::vector<u8>& recs = pass == 0 ? accts : xfers;
-            if (err == hipSuccess && cnt[0]) {  // one chunk of slots holds at most `chunk` objects
-                const size_t at = recs.size();
-                recs.resize(at + cnt[0] * 128);
-                err = hipMemcpy(recs.data() + at, d_out, cnt[0] * 128, hipMemcpyDeviceToHost);
-                if (err == hipSuccess && pass == 0) {
-                    before.resize(before.size() + cnt[0] * sizeof(AccountBal));
-                    err = hipMemcpy(before.data() + at / 2, d_before, cnt[0] * sizeof(AccountBal), hipMemcpyDeviceToHost);
-                }
-            }
-            if (err == hipSuccess && cnt[1]) {
-                const size_t at = posted.size();
-                posted.resize(at + cnt[1] * 2);
-                err = hipMemcpy(posted.data() + at, d_posted, cnt[1] * 16, hipMemcpyDeviceToHost);
-            }
+    std::vector<u8> xfers, accts, before;
+    int st = delta_transfers(E, xfers);
+    if (st) return st;
+    // Posted-groove entries: keyed by the pending transfer's timestamp.
+    std::vector<u64> pids;
+    std::vector<u8> voided;
+    delta_post_void(xfers, pids, voided);
+    std::vector<std::pair<u64, u64>> posted;
+    if (!voided.empty()) {
+        std::vector<u8> prec(voided.size() * 128), pst(voided.size());
+        if ((st = tbgpu_fetch_transfers(E, pids.data(), (u32)voided.size(), prec.data(), pst.data()))) return st;
+        for (size_t i = 0; i < voided.size(); i++) {
+            if (!pst[i]) return fail(TBGPU_STATUS_PANIC, "checkpoint delta: a posted pending transfer is missing");
+            posted.push_back({*(const u64*)&prec[i * 128 + 120], voided[i]});
         }
     }
-    (void)hipFree(d_out);
-    (void)hipFree(d_cnt);
-    (void)hipFree(d_posted);
-    (void)hipFree(d_before);
-    if (err != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "checkpoint delta: %s", hipGetErrorString(err));
-    const u64 na = accts.size() / 128, nt = xfers.size() / 128, np = posted.size() / 2;
+    std::vector<u64> ids(E->ckpt_ids);
+    delta_transfer_accounts(xfers, ids);
+    std::vector<u32> slots;
+    bool scanned = false;
+    if ((st = delta_accounts(E, ids, accts, before, slots, &scanned))) return st;
+    const u64 na = accts.size() / 128, nt = xfers.size() / 128, np = posted.size();
     counts->created_after = E->ckpt_ts;
     counts->accounts = na;
     counts->transfers = nt;
     counts->posted = np;
-    if (na > accounts_cap || nt > transfers_cap || np > posted_cap) {
+    if (na > accounts_cap || nt > transfers_cap || np > posted_cap) {  // nothing advanced; the marks are epoch'd
         return fail(TBGPU_STATUS_INVALID, "checkpoint delta: needs %llu accounts, %llu transfers, %llu posted",
                     (unsigned long long)na, (unsigned long long)nt, (unsigned long long)np);
     }
-    auto ts_of = [](const u8* r) { return *(const u64*)(r + 120); };
-    std::vector<u64> idx(na);
-    for (u64 i = 0; i < na; i++) idx[i] = i;
-    std::sort(idx.begin(), idx.end(), [&](u64 a, u64 b) { return id_less(&accts[a * 128], &accts[b * 128]); });
-    for (u64 i = 0; i < na; i++) memcpy((u8*)accounts_out + i * 128, &accts[idx[i] * 128], 128);
-    if (accounts_before_out) {
-        for (u64 i = 0; i < na; i++) memcpy((u8*)accounts_before_out + i * 64, &before[idx[i] * 64], 64);
-    }
-    idx.resize(nt);
-    for (u64 i = 0; i < nt; i++) idx[i] = i;
-    std::sort(idx.begin(), idx.end(), [&](u64 a, u64 b) { return ts_of(&xfers[a * 128]) < ts_of(&xfers[b * 128]); });
-    for (u64 i = 0; i < nt; i++) memcpy((u8*)transfers_out + i * 128, &xfers[idx[i] * 128], 128);
-    std::vector<std::pair<u64, u64>> pairs(np);
-    for (u64 i = 0; i < np; i++) pairs[i] = {posted[2 * i], posted[2 * i + 1]};
-    std::sort(pairs.begin(), pairs.end());
-    for (u64 i = 0; i < np; i++) {
-        posted_out[2 * i] = pairs[i].first;
-        posted_out[2 * i + 1] = pairs[i].second;
-    }
-    // Advance the snapshot.
-    HIPCK(hipMemcpyAsync(E->ckpt_bal, E->T.acct_bal, E->account_cap * sizeof(AccountBal), hipMemcpyDeviceToDevice,
-                         E->stream));
-    if (E->log_next) HIPCK(hipMemcpyAsync(E->ckpt_posted, E->T.xposted, E->log_next, hipMemcpyDeviceToDevice, E->stream));
-    HIPCK(hipStreamSynchronize(E->stream));
-    E->ckpt_pos = E->log_next;
-    E->ckpt_ts = E->commit_ts;
-    E->ckpt_valid = true;
-    return TBGPU_STATUS_OK;
+    delta_emit(accts, before, xfers, posted, accounts_out, accounts_before_out, transfers_out, posted_out);
+    return delta_advance(E, slots, scanned);
 }
 
 extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
@@ -1486,6 +1646,45 @@ extern "C" int tbgpu_bench_profile_mask(tbgpu_t* E, uint32_t mask) {
     return TBGPU_STATUS_OK;
 }
 
+static int ledger_summary(tbgpu* E, u32 world, u32 self, u64 out[10]) {
+    HIPCK(hipSetDevice(E->device));
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    u64* d = nullptr;
+    HIPCK(hipMalloc(&d, 80));
+    hipError_t e = hipMemsetAsync(d, 0, 80, E->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(tb_ledger_summary, dim3((unsigned)((E->account_cap + 255) / 256)), dim3(256), 0, E->stream, E->T,
+                           E->account_cap, world, self, d);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d, 80, hipMemcpyDeviceToHost, E->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(E->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "ledger summary: %s", hipGetErrorString(e));
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_bench_ledger_summary(tbgpu_t* E, tbgpu_ledger_summary* out) {
+    memset(out, 0, sizeof(*out));
+    const u32 W = E->node ? node_world(E->node) : 1;
+    for (u32 d = 0; d < W; d++) {
+        u64 v[10];
+        const int st = ledger_summary(E->node ? node_engine(E->node, d) : E, E->node ? W : 0, d, v);
+        if (st) return st;
+        for (int f = 0; f < 4; f++) {  // u128 adds (wrapping, as the reference's balances never wrap)
+            const u64 lo = out->sums[2 * f] + v[2 * f];
+            out->sums[2 * f + 1] += v[2 * f + 1] + (lo < out->sums[2 * f] ? 1 : 0);
+            out->sums[2 * f] = lo;
+        }
+        if (d == 0) out->accounts = v[8];  // replicated records
+        out->stray += v[9];
+    }
+    return TBGPU_STATUS_OK;
+}
+
 extern "C" int tbgpu_device_alloc(tbgpu_t* E, uint64_t bytes, void** out) {
     if (E->node) E = node_engine(E->node, 0);
     HIPCK(hipSetDevice(E->device));
@@ -1566,6 +1765,7 @@ extern "C" int tbgpu_bench_reset_transfers(tbgpu_t* E) {
                        E->account_cap);
     E->log_next = 0;
     E->ckpt_valid = false;
+    E->ckpt_scan = true;  // the accounts stay, created before the (empty) snapshot
     HIPCK(hipGetLastError());
     HIPCK(hipStreamSynchronize(E->stream));
     return TBGPU_STATUS_OK;
@@ -1931,6 +2131,7 @@ static int upsert_accounts(tbgpu* E, const void* records, uint32_t n, bool if_ab
     // keep_flow: balances a sequential commit from a consistent state produced (the node's
     // sequencer write-back), so the invariants hold as well.
     if (!if_absent && !keep_flow) E->balances_set = true;
+    if (!if_absent) ckpt_note_ids(E, (const u8*)records, n);
     if (E->pending) {
         int st = engine_sync(E);
         if (st) return st;
@@ -2000,7 +2201,7 @@ static int upsert_transfers(tbgpu* E, const void* records, const uint8_t* state,
         HIPCK(hipMemsetAsync(E->d_status + 1, 0, 4, E->stream));
         hipLaunchKernelGGL(tb_upsert_transfers, dim3((m + 255) / 256), dim3(256), 0, E->stream, E->T, E->lookup_out,
                            E->lookup_found, m, E->log_next, E->d_status + 1, E->d_status, if_absent ? 1u : 0u,
-                           if_absent ? E->ckpt_posted : nullptr);
+                           nullptr);
         HIPCK(hipGetLastError());
         u32 added = 0;
         HIPCK(hipMemcpyAsync(&added, E->d_status + 1, 4, hipMemcpyDeviceToHost, E->stream));

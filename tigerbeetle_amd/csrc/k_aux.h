@@ -92,10 +92,10 @@ __global__ void tb_zero_balances(Tables T, u64 cap) {
 // ---- groove write-back (StateMachine.checkpoint, state_machine.zig:542-582) --------------------
 // The objects a durable replica must insert / upsert into its forest since the previous write-back:
 // accounts created since (timestamp > ts0) or whose balances differ from the snapshot taken then,
-// transfers created since (log position >= pos0), and posted-groove entries whose state changed.
-// The snapshot is a copy of the balance array and of the posted bytes: a diff stream instead of a
-// dirty mark in every balance-writing kernel of the hot path.  Counts past `cap` are still counted
-// (the host retries with room).
+// transfers created since, and the posted-groove entries their post / void records created.
+// tb_delta_accounts is the whole-table diff, kept for the one case the host cannot name the changed
+// accounts (create_accounts committed from device memory, tbgpu_commit_device_async, or more of them
+// than the engine lists).  Counts past `cap` are still counted (the host retries with room).
 __global__ void tb_delta_accounts(Tables T, const AccountBal* snap, u64 ts0, u64 first, u64 last, u8* out, u64 cap,
                                   u64* count, AccountBal* before) {
     const u64 i = first + (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -115,29 +115,49 @@ __global__ void tb_delta_accounts(Tables T, const AccountBal* snap, u64 ts0, u64
     }
 }
 
-// A transfer is new since the previous write-back if it sits past that write-back's log position
-// and is younger than its commit timestamp (positions past pos0 also hold objects loaded from the
-// forest after a restart, which are older).
-__global__ void tb_delta_transfers(Tables T, const u8* snap_posted, u64 pos0, u64 ts0, u64 first, u64 n, u8* out,
-                                   u64 cap, u64* count, u64* posted_out, u64 posted_cap, u64* posted_count) {
-    const u64 i = first + (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= first + n) return;
-    const u64 e = T.xidx[i];
-    if (e == 0 || (e & XI_TOMB)) return;
-    const u32 pos = tb_xi_pos(e);
+// O(changes) write-back (tbgpu_checkpoint_delta): nothing scans a whole table.
+// Transfers: the log positions written since the previous write-back, [pos0, log_end).  A record is
+// new if the index holds it at that position (a withdrawn speculative record's entry is tombstoned;
+// a re-inserted id points elsewhere) and it is younger than the previous write-back (records loaded
+// from the forest after a restart are older).
+__global__ void tb_delta_log(Tables T, u64 pos0, u64 n, u64 ts0, u8* out, u64* count) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u64 pos = pos0 + i;
     const Transfer& t = T.xlog[pos];
-    if (pos >= pos0 && t.timestamp > ts0) {
-        const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
-        if (k < cap) *(Transfer*)(out + k * 128) = t;
-    }
-    const u8 st = T.xposted[pos];
-    if (st != snap_posted[pos]) {
-        const u64 q = atomicAdd((unsigned long long*)posted_count, 1ULL);
-        if (q < posted_cap) {
-            posted_out[2 * q] = t.timestamp;
-            posted_out[2 * q + 1] = st == POSTED_POSTED ? 0 : 1;
-        }
-    }
+    if (t.timestamp <= ts0) return;
+    if (tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id)) != (u32)pos) return;
+    const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
+    *(Transfer*)(out + k * 128) = t;
+}
+
+// Accounts: the ids the host names as possibly changed (the debit / credit accounts of the new
+// transfers, the ids of create_accounts events and of direct balance writes since the previous
+// write-back), each slot once (mark = this write-back's epoch).  Emitted when created since (timestamp
+// > ts0) or when its balances differ from the snapshot; `slots` lists every slot seen, for the
+// snapshot's advance.
+__global__ void tb_delta_ids(Tables T, const AccountBal* snap, u64 ts0, const u64* ids, u64 n, u32* mark, u32 epoch,
+                             u8* out, AccountBal* before, u64* count, u32* slots, u64* slot_count) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32 slot = tb_account_find(T, ids[2 * i], ids[2 * i + 1]);
+    if (slot == TB_NOT_FOUND) return;
+    if (atomicExch(&mark[slot], epoch) == epoch) return;  // another copy of the id took it
+    slots[atomicAdd((unsigned long long*)slot_count, 1ULL)] = slot;
+    const AccountHot& h = T.acct_hot[slot];
+    const AccountBal b = T.acct_bal[slot], s = snap[slot];
+    const bool same = b.debits_pending == s.debits_pending && b.debits_posted == s.debits_posted &&
+                      b.credits_pending == s.credits_pending && b.credits_posted == s.credits_posted;
+    if (h.timestamp <= ts0 && same) return;
+    const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
+    *(Account*)(out + k * 128) = tb_account_load(T, slot);
+    before[k] = h.timestamp <= ts0 ? s : AccountBal{0, 0, 0, 0};
+}
+
+// The snapshot follows the slots a write-back covered.
+__global__ void tb_delta_advance(Tables T, AccountBal* snap, const u32* slots, u64 n) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) snap[slots[i]] = T.acct_bal[slots[i]];
 }
 
 // ---- pipelined host commits (tbgpu_commit_pipelined) -------------------------------------------
@@ -162,3 +182,4 @@ __global__ __launch_bounds__(64) void tb_reply_out(const u64* batch_off, u32 nb,
     const u32* in = results + 2 * batch_off[k];
     for (u32 w = threadIdx.x; w < bytes / 4; w += 64) out[w] = in[w];
 }
+

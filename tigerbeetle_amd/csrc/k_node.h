@@ -113,3 +113,46 @@ __global__ __launch_bounds__(1024) void tb_node_replies(const u64* batch_off, co
     }
     if (threadIdx.x == 0) reply_bytes[b] = running * 8;
 }
+
+// Ledger summary (tbgpu_bench_ledger_summary): u128 sums of the balance fields over every live
+// slot (block-reduced, then one u128 atomic per field and block), live accounts, and slots whose
+// owner under `world` is not `self` but hold a non-zero balance (world 0: no owner check).
+__global__ __launch_bounds__(256) void tb_ledger_summary(Tables T, u64 cap, u32 world, u32 self, u64* out) {
+    __shared__ u64 s_red[4][2][256 / 64];
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    u128 v[4] = {0, 0, 0, 0};
+    u64 live = 0, stray = 0;
+    if (i < cap) {
+        const AccountHot& h = T.acct_hot[i];
+        if (h.timestamp != 0 && !tb_id_reserved(h.id_lo, h.id_hi)) {
+            const AccountBal b = T.acct_bal[i];
+            v[0] = b.debits_pending;
+            v[1] = b.debits_posted;
+            v[2] = b.credits_pending;
+            v[3] = b.credits_posted;
+            live = 1;
+            if (world && tb_home(h.id_lo, h.id_hi, world) != self && (v[0] | v[1] | v[2] | v[3]) != 0) stray = 1;
+        }
+    }
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int f = 0; f < 4; f++) {
+        const u128 w = tb_wave_sum_u128(v[f]);
+        if (lane == 0) {
+            s_red[f][0][wave] = tb_lo(w);
+            s_red[f][1][wave] = tb_hi(w);
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        live += __shfl_xor((unsigned long long)live, off);
+        stray += __shfl_xor((unsigned long long)stray, off);
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        u128 t = 0;
+        for (u32 w = 0; w < 256 / 64; w++) t += tb_u128(s_red[threadIdx.x][0][w], s_red[threadIdx.x][1][w]);
+        if (t != 0) tb_atomic_add_u128(out + 2 * threadIdx.x, t);
+    }
+    if (lane == 0 && live) atomicAdd((unsigned long long*)&out[8], (unsigned long long)live);
+    if (lane == 0 && stray) atomicAdd((unsigned long long*)&out[9], (unsigned long long)stray);
+}

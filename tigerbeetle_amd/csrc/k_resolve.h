@@ -195,6 +195,10 @@ __device__ static inline bool tb_classify(const PassArgs& P, u32 pe, u32 info, u
         return any_dup && (info & HZ_KEYS) && tb_dedup_is_dup(P.dedup, P.dedup_mask, P.kid[pe]);
     }
     if (info & HZ_SELFDEP) return true;
+    // The independent apply of a post / void trusts pending balances to cover its pending transfer
+    // (true of every state a commit sequence builds); after a direct balance write the ordered
+    // replay checks the reference's `-=` asserts instead (state_machine.zig:991-992).
+    if (P.seq_pv && (P.eflags[pe] & (TF_POST | TF_VOID))) return true;
     if (any_dup) {
         if ((info & HZ_SPEC) && T.xdup[P.rs[pe]]) return true;
         if ((info & HZ_PV_KEY) && tb_dedup_is_dup(P.dedup, P.dedup_mask, P.kpid[pe])) return true;

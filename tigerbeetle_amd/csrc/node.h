@@ -1030,58 +1030,68 @@ static int node_api_export(TbNode* N, int what, void* out, u64 cap, u64* count) 
     return TBGPU_STATUS_OK;
 }
 
-// Groove write-back of the node: every shard's delta, merged.  Accounts: created ones are listed by
-// every shard (replicated records), re-balanced ones by their owner; the owner's copy (its
-// balances, its previous balances) is the account's.  Transfers and posted pairs: each lives on one
-// home; concatenated and sorted by timestamp.
+// Groove write-back of the node, O(changes) like a single engine's (engine.hip delta_*): the new
+// transfers of every shard's log; the posted entries their post / void records make (the pending
+// transfer may live on another shard: its timestamp is fetched from its home); the accounts the new
+// transfers moved — wherever those transfers live — plus the listed creates and direct writes, each
+// looked up on its OWNER, whose copy holds its balances.  A created account is listed by every shard
+// (replicated records): the owner's copy wins the merge.
 static int node_api_checkpoint_delta(TbNode* N, void* accounts_out, void* accounts_before_out, u64 accounts_cap,
                                      void* transfers_out, u64 transfers_cap, u64* posted_out, u64 posted_cap,
                                      tbgpu_delta_counts* counts) {
     memset(counts, 0, sizeof(*counts));
     const u32 W = N->world;
-    // Sizes first (every shard, nothing advances), then the deltas.
-    std::vector<tbgpu_delta_counts> c(W);
+    int st = node_sync(N);
+    if (st) return st;
+    std::vector<u8> xfers;
     for (u32 d = 0; d < W; d++) {
-        const int st = tbgpu_checkpoint_delta(N->D[d].E, nullptr, nullptr, 0, nullptr, 0, nullptr, 0, &c[d]);
-        if (st && st != TBGPU_STATUS_INVALID) return st;
+        NCK(hipSetDevice(N->D[d].device));
+        if ((st = delta_transfers(N->D[d].E, xfers))) return st;
     }
-    // Upper bounds of the merged sizes: a caller whose buffers are smaller gets them back and
-    // nothing advances (the accounts' union is at most the sum).
-    u64 na = 0, nt = 0, np = 0;
-    for (u32 d = 0; d < W; d++) {
-        na += c[d].accounts;
-        nt += c[d].transfers;
-        np += c[d].posted;
+    std::vector<u64> pids;
+    std::vector<u8> voided;
+    delta_post_void(xfers, pids, voided);
+    std::vector<std::pair<u64, u64>> posted;
+    if (!voided.empty()) {
+        std::vector<u8> prec(voided.size() * 128), pst(voided.size());
+        if ((st = node_fetch(N, false, pids.data(), (u32)voided.size(), prec.data(), pst.data()))) return st;
+        for (size_t i = 0; i < voided.size(); i++) {
+            if (!pst[i]) return fail(TBGPU_STATUS_PANIC, "checkpoint delta: a posted pending transfer is missing");
+            posted.push_back({*(const u64*)&prec[i * 128 + 120], voided[i]});
+        }
     }
-    if (na > accounts_cap || nt > transfers_cap || np > posted_cap) {
-        counts->accounts = na;
-        counts->transfers = nt;
-        counts->posted = np;
-        counts->created_after = c[0].created_after;
-        return fail(TBGPU_STATUS_INVALID, "checkpoint delta: needs up to %llu accounts, %llu transfers, %llu posted",
-                    (unsigned long long)na, (unsigned long long)nt, (unsigned long long)np);
+    std::vector<u64> all;
+    delta_transfer_accounts(xfers, all);
+    for (u32 d = 0; d < W; d++) all.insert(all.end(), N->D[d].E->ckpt_ids.begin(), N->D[d].E->ckpt_ids.end());
+    std::vector<std::vector<u64>> ids(W);
+    for (size_t i = 0; i + 1 < all.size(); i += 2) {
+        const u32 o = tb_home(all[i], all[i + 1], W);
+        ids[o].push_back(all[i]);
+        ids[o].push_back(all[i + 1]);
     }
-    // Accounts of the union (created ones appear on every shard; owner-only changes on the owner).
     std::vector<std::vector<u8>> acc(W), bef(W);
-    std::vector<u8> xf;
-    std::vector<u64> ps;
+    std::vector<std::vector<u32>> slots(W);
+    std::vector<char> scanned(W, 0);
     for (u32 d = 0; d < W; d++) {
-        acc[d].resize(std::max<u64>(c[d].accounts, 1) * 128);
-        bef[d].resize(std::max<u64>(c[d].accounts, 1) * 64);
-        std::vector<u8> t(std::max<u64>(c[d].transfers, 1) * 128);
-        std::vector<u64> p(std::max<u64>(c[d].posted, 1) * 2);
-        tbgpu_delta_counts got{};
-        const int st = tbgpu_checkpoint_delta(N->D[d].E, acc[d].data(), bef[d].data(), c[d].accounts, t.data(), c[d].transfers,
-                                              p.data(), c[d].posted, &got);
-        if (st) return st;
-        acc[d].resize(got.accounts * 128);
-        bef[d].resize(got.accounts * 64);
-        xf.insert(xf.end(), t.begin(), t.begin() + got.transfers * 128);
-        ps.insert(ps.end(), p.begin(), p.begin() + got.posted * 2);
-        if (d == 0) counts->created_after = got.created_after;
+        NCK(hipSetDevice(N->D[d].device));
+        bool sc = false;
+        std::vector<u8> a, b;
+        if ((st = delta_accounts(N->D[d].E, ids[d], a, b, slots[d], &sc))) return st;
+        scanned[d] = sc;
+        // Sorted by id for the merge.
+        const u64 n = a.size() / 128;
+        std::vector<u64> idx(n);
+        for (u64 i = 0; i < n; i++) idx[i] = i;
+        std::sort(idx.begin(), idx.end(), [&](u64 x, u64 y) { return id_less(&a[x * 128], &a[y * 128]); });
+        acc[d].resize(n * 128);
+        bef[d].resize(n * 64);
+        for (u64 i = 0; i < n; i++) {
+            memcpy(&acc[d][i * 128], &a[idx[i] * 128], 128);
+            memcpy(&bef[d][i * 64], &b[idx[i] * 64], 64);
+        }
     }
     // Merge accounts by id: the owner's copy wins.
-    std::vector<std::pair<const u8*, const u8*>> merged;  // (record, before) sorted by id
+    std::vector<u8> accts, before;
     std::vector<size_t> pos(W, 0);
     while (true) {
         const u8* best = nullptr;
@@ -1094,41 +1104,36 @@ static int node_api_checkpoint_delta(TbNode* N, void* accounts_out, void* accoun
         if (!best) break;
         const u32 o = node_home(best, W);
         const u8* rec = nullptr;
-        const u8* before = nullptr;
+        const u8* bf = nullptr;
+        u8 key[16];
+        memcpy(key, best, 16);
         for (u32 d = 0; d < W; d++) {
-            if (pos[d] * 128 < acc[d].size() && memcmp(&acc[d][pos[d] * 128], best, 16) == 0) {
+            if (pos[d] * 128 < acc[d].size() && memcmp(&acc[d][pos[d] * 128], key, 16) == 0) {
                 if (!rec || d == o) {
                     rec = &acc[d][pos[d] * 128];
-                    before = &bef[d][pos[d] * 64];
+                    bf = &bef[d][pos[d] * 64];
                 }
             }
         }
-        for (u32 d = 0; d < W; d++) {  // advance every shard past this id
-            if (pos[d] * 128 < acc[d].size() && memcmp(&acc[d][pos[d] * 128], rec, 16) == 0) pos[d]++;
+        accts.insert(accts.end(), rec, rec + 128);
+        before.insert(before.end(), bf, bf + 64);
+        for (u32 d = 0; d < W; d++) {
+            if (pos[d] * 128 < acc[d].size() && memcmp(&acc[d][pos[d] * 128], key, 16) == 0) pos[d]++;
         }
-        merged.push_back({rec, before});
     }
-    na = merged.size();
-    nt = xf.size() / 128;
-    np = ps.size() / 2;
+    const u64 na = accts.size() / 128, nt = xfers.size() / 128, np = posted.size();
+    counts->created_after = N->D[0].E->ckpt_ts;
     counts->accounts = na;
     counts->transfers = nt;
     counts->posted = np;
-    for (u64 i = 0; i < na; i++) {
-        memcpy((u8*)accounts_out + i * 128, merged[i].first, 128);
-        if (accounts_before_out) memcpy((u8*)accounts_before_out + i * 64, merged[i].second, 64);
+    if (na > accounts_cap || nt > transfers_cap || np > posted_cap) {  // nothing advanced
+        return fail(TBGPU_STATUS_INVALID, "checkpoint delta: needs %llu accounts, %llu transfers, %llu posted",
+                    (unsigned long long)na, (unsigned long long)nt, (unsigned long long)np);
     }
-    std::vector<u64> idx(nt);
-    for (u64 i = 0; i < nt; i++) idx[i] = i;
-    auto ts_of = [&](u64 i) { return *(const u64*)&xf[i * 128 + 120]; };
-    std::sort(idx.begin(), idx.end(), [&](u64 a, u64 b) { return ts_of(a) < ts_of(b); });
-    for (u64 i = 0; i < nt; i++) memcpy((u8*)transfers_out + i * 128, &xf[idx[i] * 128], 128);
-    std::vector<std::pair<u64, u64>> pairs(np);
-    for (u64 i = 0; i < np; i++) pairs[i] = {ps[2 * i], ps[2 * i + 1]};
-    std::sort(pairs.begin(), pairs.end());
-    for (u64 i = 0; i < np; i++) {
-        posted_out[2 * i] = pairs[i].first;
-        posted_out[2 * i + 1] = pairs[i].second;
+    delta_emit(accts, before, xfers, posted, accounts_out, accounts_before_out, transfers_out, posted_out);
+    for (u32 d = 0; d < W; d++) {
+        NCK(hipSetDevice(N->D[d].device));
+        if ((st = delta_advance(N->D[d].E, slots[d], scanned[d]))) return st;
     }
     return TBGPU_STATUS_OK;
 }

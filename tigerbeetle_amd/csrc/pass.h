@@ -79,6 +79,8 @@ struct PassArgs {
     u32 routed;            // 1: each event carries its execute timestamp in its timestamp field
     u8* codes;             // call-relative dense result codes instead of sparse replies (or null)
     u32 cert_ext;          // 0: certificate from this engine's bound; CERT_EXT_*: given by the caller
+    u32 seq_pv;            // 1: balances were set directly (tbgpu_test_set_balances / upserts): every
+                           // post / void is dependent, so the replay checks its pending-balance `-=`
     // Balance legs (k_apply.h): with the 64-bit certificate, the balance deltas of independent ok
     // create_transfer events are written as legs, bucketed by account slot per prepare, and summed
     // per account by tb_apply_legs instead of being added with one global atomic per leg.

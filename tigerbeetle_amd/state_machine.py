@@ -143,6 +143,30 @@ class Engine:
             int(chunk_batches), lat.ctypes.data if lat is not None else None))
         return out_lens, replies, lat
 
+    def commit_pipelined_ptrs(self, operation, timestamps, lens, in_ptrs, replies, chunk_batches=0, latency=False):
+        """tbgpu_commit_pipelined over prepares at explicit host addresses (in_ptrs[k]: prepare k's
+        body, lens[k] events); replies: a uint8 host buffer, prepare k's reply at 8 * its first event
+        (prepares in order).  Returns (reply_bytes uint32[n], latency_ms float64[n] or None)."""
+        n = len(lens)
+        lens = np.asarray(lens, dtype=np.uint64)
+        first = np.zeros(n, dtype=np.uint64)
+        if n > 1:
+            first[1:] = np.cumsum(lens[:-1])
+        assert replies.dtype == np.uint8 and replies.nbytes >= int(lens.sum()) * 8
+        ts = np.ascontiguousarray(timestamps, dtype=np.uint64)
+        ins = np.ascontiguousarray(in_ptrs, dtype=np.uint64)
+        outs = (first * 8 + np.uint64(replies.ctypes.data)).astype(np.uint64)
+        in_lens = (lens * 128).astype(np.uint32)
+        out_lens = np.zeros(n, dtype=np.uint32)
+        lat = np.zeros(n, dtype=np.float64) if latency else None
+        P = ctypes.c_void_p
+        _lib.check(self.lib.tbgpu_commit_pipelined(
+            self.h, int(operation), n, ts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+            ins.ctypes.data_as(ctypes.POINTER(P)), in_lens.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+            outs.ctypes.data_as(ctypes.POINTER(P)), out_lens.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+            int(chunk_batches), lat.ctypes.data if lat is not None else None))
+        return out_lens, lat
+
     def register_host(self, array):
         """Pin a host array for DMA (the replica's message pool; tbgpu_register_host)."""
         _lib.check(self.lib.tbgpu_register_host(self.h, array.ctypes.data, array.nbytes))
@@ -219,6 +243,17 @@ class Engine:
                 continue
             _lib.check(st)
             return Delta(a[:need[0]], t[:need[1]], p[:need[2]], before[:need[0]], counts.created_after)
+
+    def ledger_summary(self):
+        """{"debits_pending", "debits_posted", "credits_pending", "credits_posted": u128 sums over every
+        account (every shard of a node), "accounts": live accounts, "stray": balances held by a shard
+        that is not the account's owner (node engines; must be 0)} — tbgpu_bench_ledger_summary."""
+        s = _lib.tbgpu_ledger_summary()
+        _lib.check(self.lib.tbgpu_bench_ledger_summary(self.h, ctypes.byref(s)))
+        names = ("debits_pending", "debits_posted", "credits_pending", "credits_posted")
+        out = {n: int(s.sums[2 * i]) | (int(s.sums[2 * i + 1]) << 64) for i, n in enumerate(names)}
+        out.update(accounts=int(s.accounts), stray=int(s.stray))
+        return out
 
     def legs_min_events(self, events):
         """Passes of >= events transfers use the sorted balance legs (0: every pass)."""
