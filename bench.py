@@ -1057,7 +1057,8 @@ def run_node(args, procs, rank):
     lat = np.sort(np.concatenate(lat_all)) if lat_all else np.array([float("nan")])
     per_launch = T / max(1, stats["launches_validate"] / max(1, args.steps))
     u_over_t = expected_unique(args.accounts, 2 * per_launch) / per_launch
-    roof = roofline(stats, u_over_t, per_launch, argparse.Namespace(transfers=T, steps=args.steps), total_ms)
+    roof = roofline(stats, u_over_t, per_launch, argparse.Namespace(transfers=T, steps=args.steps), total_ms,
+                    kernel="tb_transfers_validate")
     pcie_gbs = T * 128 * args.steps / (total_ms / 1e3) / 1e9
     line = {
         "metric": METRIC,

@@ -14,6 +14,8 @@
 #include <numeric>
 #include <string>
 #include <vector>
+#include <map>
+#include <mutex>
 
 #include "../../include/tbgpu.h"
 #include "../../include/tbgpu_bench.h"
@@ -97,6 +99,8 @@ struct tbgpu {
     // tb_replay while no balance was set directly (the post/void assert argument, k_replay.h).
     bool flow_ok = false;
     bool balances_set = false;
+    u64 flow_capacity = 0;     // tb_flow workgroups the device holds at once (occupancy x CUs)
+    bool dev_registered = false;
     FlowArgs F{};
 
     // Host-path staging.
@@ -246,6 +250,38 @@ static int engine_clear(tbgpu* E) {
     return TBGPU_STATUS_OK;
 }
 
+// tb_flow synchronises its workgroups with a software grid barrier, so every workgroup of a launch
+// must be resident at once.  The launch is an ordinary one (a cooperative launch makes the HIP
+// runtime keep a queue whose teardown at process exit faults inside libhsa-runtime when rocprofv3 is
+// loaded: tools/gpu/exit_probe.py), so residency is guaranteed here: the engines of
+// this process on one device split its capacity (occupancy x CUs) and each launches at most its
+// share — the persistent workgroups of every concurrent tb_flow then fit together, and every other
+// kernel they share the device with runs to completion without waiting on them.  Every barrier wait
+// is also bounded in wall time (PANIC_FLOW_STALL).
+static std::mutex g_dev_mu;
+static std::map<int, u32> g_dev_engines;
+
+static void dev_register(tbgpu* E, bool add) {
+    std::lock_guard<std::mutex> lock(g_dev_mu);
+    if (add && !E->dev_registered) {
+        g_dev_engines[E->device]++;
+        E->dev_registered = true;
+    } else if (!add && E->dev_registered) {
+        if (--g_dev_engines[E->device] == 0) g_dev_engines.erase(E->device);
+        E->dev_registered = false;
+    }
+}
+
+static u32 flow_grid(tbgpu* E) {
+    u32 engines = 1;
+    {
+        std::lock_guard<std::mutex> lock(g_dev_mu);
+        auto it = g_dev_engines.find(E->device);
+        if (it != g_dev_engines.end()) engines = std::max<u32>(1, it->second);
+    }
+    return (u32)std::max<u64>(1, std::min<u64>(E->F.grid, E->flow_capacity / engines));
+}
+
 // node.h entry points (defined at the end of this file).
 static int node_api_init(const tbgpu_config* config, tbgpu_t** out);
 static void node_free(TbNode* N);
@@ -307,6 +343,7 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     } while (0)
     INIT_CK(hipSetDevice(E->device));
     INIT_CK(hipStreamCreateWithFlags(&E->stream, hipStreamNonBlocking));
+    dev_register(E, true);
 
     // Account table slots per account (load factor <= 1/2).  4 slots shorten the probes (validate
     // -2..10 % at C2, box to box) but double the legs buckets (tb_apply_legs +40 %): a net loss.
@@ -356,23 +393,23 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     INIT_CK(hipMalloc(&E->T.xposted, E->xlog_cap));
     INIT_CK(hipMalloc(&E->g, sizeof(Globals)));
     {
-        // tb_flow: one 1024-thread workgroup per CU, all resident (cooperative launch).
+        // tb_flow: 1024-thread workgroups, all resident (see flow_grid).
         hipDeviceProp_t prop;
         int occ = 0;
         if (hipGetDeviceProperties(&prop, E->device) == hipSuccess &&
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&tb_flow), FLOW_THREADS, 0) ==
                 hipSuccess &&
-            occ >= 1 && prop.cooperativeLaunch) {
+            occ >= 1) {
             // A quarter of the CUs at most: co-residency of the grid then holds even with a few
             // engines (processes) sharing the device, each with a tb_flow in flight.
             E->F.grid = (u32)std::max(1, std::min(prop.multiProcessorCount / 4, 64));
 #ifdef TBGPU_TIMING_KNOBS
             if (const char* gs = getenv("TBGPU_FLOW_GRID")) E->F.grid = std::max(1u, std::min(E->F.grid, (u32)atoi(gs)));
 #endif
-            // tb_flow's grid barrier needs every workgroup resident: the launch is cooperative, so
-            // the runtime refuses it (an error status, never a spin) when the grid cannot be
-            // co-resident.  The grid is at most occupancy x CUs.
-            E->F.grid = (u32)std::min<u64>(E->F.grid, (u64)occ * prop.multiProcessorCount);
+            // tb_flow's grid barrier needs every workgroup resident: the grid is at most occupancy x
+            // CUs, shared among the engines of this process on the device (flow_grid).
+            E->flow_capacity = (u64)occ * prop.multiProcessorCount;
+            E->F.grid = (u32)std::min<u64>(E->F.grid, E->flow_capacity);
             int khz = 0;
             if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, E->device) != hipSuccess) khz = 0;
             khz = std::max(khz, 100000);  // s_memrealtime: 100 MHz on gfx9 parts; never trust a lower figure
@@ -497,6 +534,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
     }
     if (!E) return;
     (void)hipSetDevice(E->device);
+    dev_register(E, false);
     if (E->stream) (void)hipStreamSynchronize(E->stream);
     void* bufs[] = {E->ckpt_bal, E->ckpt_mark, E->T.acct_hot, E->T.acct_bal, E->T.acct_cold, E->T.account_mark, E->T.xidx, E->T.xdup, E->T.xlog,
                     E->T.xposted, E->g, E->info, E->eflags, E->dr,
@@ -684,9 +722,9 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         if (flow) {
             UndoEntry* seq_undo = E->undo;
             u32 seq_cap = E->undo_cap;
-            void* args[] = {&P, &E->F, &seq_undo, &seq_cap};
-            HIPCK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&tb_flow), dim3(E->F.grid), dim3(FLOW_THREADS),
-                                             args, 0, E->stream));
+            FlowArgs F = E->F;
+            F.grid = flow_grid(E);
+            hipLaunchKernelGGL(tb_flow, dim3(F.grid), dim3(FLOW_THREADS), 0, E->stream, P, F, seq_undo, seq_cap);
         } else if (op == OP_CREATE_TRANSFERS) {
             hipLaunchKernelGGL(tb_replay<OP_CREATE_TRANSFERS>, dim3(1), dim3(REPLAY_THREADS), 0, E->stream, P,
                                E->undo, E->undo_cap);
@@ -976,8 +1014,10 @@ static int commit_pipelined(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, 
         const int st = consume(consumed++, status == TBGPU_STATUS_OK);
         if (status == TBGPU_STATUS_OK) status = st;
     }
+    const u64 taken_ts = E->commit_ts;  // as of the last chunk whose replies were taken
     HIPCK(hipStreamSynchronize(E->copy_stream));
     const int st = engine_sync(E);
+    if (status) E->commit_ts = taken_ts;  // chunks queued behind a failure ran, but count for nothing
     return status ? status : st;
 }
 

@@ -27,8 +27,8 @@
 //          queueing those with no predecessor left.  The result equals the sequential replay's:
 //          every unit sees exactly the effects of the units before it on its resources, and
 //          nothing else it reads can differ.
-// Grid-wide phases are separated by a counter barrier (cooperative launch: every workgroup is
-// resident).  Cases the planner does not cover (a chain longer than FLOW_CHAIN_MAX, a pending id
+// Grid-wide phases are separated by a counter barrier (every workgroup is resident: the host
+// launches at most its device budget of workgroups, engine.hip flow_grid).  Cases the planner does not cover (a chain longer than FLOW_CHAIN_MAX, a pending id
 // whose creator in this pass is ambiguous) set a flag, and workgroup 0 runs the sequential replay
 // for the pass instead.  Every wait is bounded: a stall raises PANIC_FLOW_STALL, never a hang.
 #pragma once
@@ -131,7 +131,7 @@ __device__ static inline u32 fl_key_id(u64 lo, u64 hi) {
     return 0x80000000u | (u32)(tb_mix64(lo ^ tb_mix64(hi ^ 0x9e3779b97f4a7c15ULL)) % 0x7FFFFFFFu);
 }
 
-// Grid barrier of the co-resident grid (cooperative launch).  Two levels, so arrivals do not all
+// Grid barrier of the co-resident grid (engine.hip flow_grid).  Two levels, so arrivals do not all
 // serialise on one word: the workgroups of each of FL_BAR_GROUPS groups (blockIdx mod groups)
 // count on their group's word, the last of a group counts on the root word, and the last group
 // publishes the generation, which every workgroup polls.  Every counter only grows (generation gen
@@ -1508,7 +1508,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
             }
         }
     } else {
-        // Every lane of every workgroup (all co-resident: cooperative launch) takes tickets from one
+        // Every lane of every workgroup (all co-resident, engine.hip flow_grid) takes tickets from one
         // queue in global memory; the state units share is read with agent-scope loads and each
         // unit's writes drain before its successors are released, so lanes on different CUs see
         // exactly what lanes of one workgroup would.
