@@ -88,6 +88,8 @@ def parse():
                    help="time the validate kernel's access pattern without its logic (roofline.access_mix)")
     p.add_argument("--host-prepares", type=int, default=600,
                    help="prepares committed one per tbgpu_commit call from host memory (the replica's call; 0: skip)")
+    p.add_argument("--write-back", type=int, default=1,
+                   help="time the groove write-back per bar at the full stored count and near empty")
     p.add_argument("--engine", default="node", choices=["node", "ranks"],
                    help="--gpus N > 1: 'node' = one tbgpu node engine over the N GPUs (include/tbgpu.h "
                         "tbgpu_config.devices: what a replica binds), 'ranks' = one process per GPU over RCCL "
@@ -177,6 +179,37 @@ def run_host_commits(engine, args, events_dev, t_cursor):
                                                    ("flow", "replay"), ("pass_clear", "clear"))}
     _lib.check(lib.tbgpu_unregister_host(engine.h, body.ctypes.data))
     return res, t_cursor + 10
+
+
+def run_write_back(engine, args, t_cursor, bars=4):
+    """The durable replica's groove write-back per bar (tbgpu_checkpoint_delta after each bar of 64
+    prepares, as the Zig wrapper's compact does, src/state_machine.zig:542-582): the current state
+    is taken as written back (tbgpu_bench_checkpoint_mark), then each bar of fresh C2 transfers is
+    committed from host memory and its write-back timed (host clock: device work, the D2H of the
+    changed objects and their sort).  Its cost follows the bar's changes, not the stored objects:
+    compare the entries taken at different stored counts."""
+    L, bar = args.batch, 64
+    n = bar * L
+    dev = engine.alloc(n * 128)
+    out = []
+    engine.checkpoint_mark()
+    stored = engine.stats()["transfers"]
+    for k in range(bars):
+        engine.generate_transfers(dev, 10 * args.transfers + k * n, n, args.accounts, seed=args.seed + 7)
+        host = engine.to_host(dev, n * 128)
+        lens = batches(n, L)
+        ts, t_cursor = timestamps(lens, t_cursor + 10)
+        rb, _, _ = engine.commit_pipelined(129, ts, lens, host, chunk_batches=bar)
+        assert int(rb.sum()) == 0
+        t0 = time.perf_counter()
+        d = engine.checkpoint_delta(caps=(2 * n, n, n))
+        out.append({"ms": round((time.perf_counter() - t0) * 1e3, 3), "accounts": len(d.accounts),
+                    "transfers": len(d.transfers)})
+    engine.free(dev)
+    steady = out[1:] if len(out) > 1 else out  # the first call allocates and registers the buffers
+    return {"stored_transfers": int(stored), "bar_prepares": bar, "bars": out,
+            "ms_per_bar": round(float(np.mean([b["ms"] for b in steady])), 3),
+            "bytes_per_bar": int(np.mean([128 * b["transfers"] + 192 * b["accounts"] for b in steady]))}, t_cursor
 
 
 def run_cpu_baseline(engine, args, acct_lens, acct_ts, events_dev, sample_lens, sample_ts):
@@ -512,8 +545,9 @@ def main():
 
     wl = SETTINGS[args.workload]
     pass_events = args.pass_batches * args.batch
-    engine = Engine(Options(accounts_max=args.accounts, transfers_max=args.transfers, pass_events_max=pass_events,
-                            pass_batches_max=args.pass_batches, device=local_rank, profile=bool(args.profile)))
+    engine = Engine(Options(accounts_max=args.accounts, transfers_max=args.transfers + 6 * 64 * args.batch,
+                            pass_events_max=pass_events, pass_batches_max=args.pass_batches, device=local_rank,
+                            profile=bool(args.profile)))
     seed = args.seed + 1000003 * rank  # each rank: its own ledger shard
 
     # -- accounts (create_accounts through the engine) --------------------------------------
@@ -573,6 +607,15 @@ def main():
     n_failed_host = int(rb_h.sum()) // 8
     engine.unregister_host(host_events)
     del host_events
+    write_back = None
+    if rank == 0 and world == 1 and args.write_back:
+        at_full, t_cursor = run_write_back(engine, args, t_cursor)
+        engine.reset_transfers()
+        at_empty, t_cursor = run_write_back(engine, args, t_cursor)
+        write_back = {"definition": "tbgpu_checkpoint_delta per bar of 64 C2 prepares (524,160 transfers), host "
+                                    "clock: device work + D2H of the changed objects into registered buffers; "
+                                    "ms_per_bar over the bars after the first (which allocates the buffers)",
+                      "at_stored": [at_full, at_empty]}
     lat = np.sort(np.concatenate(lat_all)) if lat_all else np.array([float("nan")])
 
     # -- secondary: the same commits with the prepares already resident in HBM ----------------
@@ -729,6 +772,7 @@ def main():
         "cpu_baseline": cpu,
         "parity": parity,
         "host_commit": host,
+        "write_back": write_back,
         "secondary": secondary or None,
     }
     if rank == 0:

@@ -150,9 +150,11 @@ int tbgpu_export_posted(tbgpu_t* engine, uint64_t* out_pairs, uint64_t cap, uint
 /* Groove write-back for a durable replica (StateMachine.checkpoint / compact,
  * src/state_machine.zig:542-582; groove insert / upsert, src/lsm/groove.zig:902-963): the objects
  * changed since the previous call (or since init / reset) — accounts created or re-balanced (full
- * records, by id), transfers created (by timestamp), posted-groove entries created or changed
- * ({pending timestamp, fulfillment} pairs, by timestamp).  If a buffer is too small the call
- * returns TBGPU_STATUS_INVALID with the sizes needed in *counts and nothing advances. */
+ * records, in no particular order: the groove sorts its mutable table itself), transfers created
+ * (by timestamp), posted-groove entries created or changed ({pending timestamp, fulfillment} pairs,
+ * by timestamp).  The cost follows the changes, not the tables.  If a buffer is too small the call
+ * returns TBGPU_STATUS_INVALID with the sizes needed in *counts and nothing advances.  Buffers in
+ * registered host memory (tbgpu_register_host) are filled by DMA. */
 typedef struct tbgpu_delta_counts {
     uint64_t accounts;
     uint64_t transfers;

@@ -67,6 +67,11 @@ typedef struct tbgpu_ledger_summary {
 } tbgpu_ledger_summary;
 int tbgpu_bench_ledger_summary(tbgpu_t* engine, tbgpu_ledger_summary* out);
 
+/* Take the current state as written back (tbgpu_checkpoint_delta's snapshot and positions), so the
+ * next write-back covers only what is committed after this call: the bench times a bar's write-back
+ * at any number of stored objects without first writing them all back. */
+int tbgpu_bench_checkpoint_mark(tbgpu_t* engine);
+
 /* Device memory helpers for callers without a device allocator (ctypes users). */
 int tbgpu_device_alloc(tbgpu_t* engine, uint64_t bytes, void** out);
 int tbgpu_device_free(tbgpu_t* engine, void* ptr);

@@ -62,8 +62,8 @@ def test_checkpoint_deltas(config, gpu_engine_factory):
             old = old_rows.get(bytes(rec[:16]))
             want = np.frombuffer(old[16:80], dtype=np.uint64) if old else np.zeros(8, dtype=np.uint64)
             assert np.array_equal(before, want)
-        ids = [bytes(r[:16])[::-1] for r in d.accounts.view(np.uint8).reshape(-1, 128)]
-        assert ids == sorted(ids)
+        ids = [bytes(r[:16]) for r in d.accounts.view(np.uint8).reshape(-1, 128)]
+        assert len(ids) == len(set(ids))  # each account once (no particular order: the groove sorts)
         ts = d.transfers["timestamp"] if len(d.transfers) else np.array([], dtype=np.uint64)
         assert np.all(np.diff(ts.astype(np.int64)) > 0)
         # Replay into the host forest (insert / upsert).

@@ -15,6 +15,7 @@
 #include <string>
 #include <vector>
 #include <map>
+#include <functional>
 #include <mutex>
 
 #include "../../include/tbgpu.h"
@@ -1283,172 +1284,242 @@ static void ckpt_note_ids(tbgpu* E, const u8* records, u64 n) {
     }
 }
 
-// The live transfers written since the previous write-back (appended to `out`, unsorted).
-static int delta_transfers(tbgpu* E, std::vector<u8>& out) {
-    int st = ckpt_snapshot_ready(E);
-    if (st) return st;
-    const u64 chunk = 1ULL << 20;
-    u8* d_out = nullptr;
-    u64* d_cnt = nullptr;
-    hipError_t err = hipMalloc(&d_out, std::min<u64>(chunk, std::max<u64>(1, E->log_next - E->ckpt_pos)) * 128);
-    if (err == hipSuccess) err = hipMalloc(&d_cnt, 8);
-    for (u64 s = E->ckpt_pos; s < E->log_next && err == hipSuccess; s += chunk) {
-        const u64 n = std::min<u64>(chunk, E->log_next - s);
-        u64 cnt = 0;
-        err = hipMemsetAsync(d_cnt, 0, 8, E->stream);
-        if (err != hipSuccess) break;
-        hipLaunchKernelGGL(tb_delta_log, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T, s, n, E->ckpt_ts,
-                           d_out, d_cnt);
-        err = hipGetLastError();
-        if (err == hipSuccess) err = hipMemcpyAsync(&cnt, d_cnt, 8, hipMemcpyDeviceToHost, E->stream);
-        if (err == hipSuccess) err = hipStreamSynchronize(E->stream);
-        if (err == hipSuccess && cnt) {
-            const size_t at = out.size();
-            out.resize(at + cnt * 128);
-            err = hipMemcpy(out.data() + at, d_out, cnt * 128, hipMemcpyDeviceToHost);
-        }
-    }
-    if (d_out) (void)hipFree(d_out);
-    if (d_cnt) (void)hipFree(d_cnt);
-    if (err != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "checkpoint delta (transfers): %s", hipGetErrorString(err));
-    return TBGPU_STATUS_OK;
-}
+// One write-back of one engine, in steps the node engine can interleave across its shards:
+//   delta_begin      count the new transfers (ordered compaction, pass 1);
+//   delta_log_ids    their debit / credit account ids and post / void records (device lists);
+//   delta_accounts   the account delta for ids on the device (from the log) or on the host (the
+//                    listed creates and direct writes; a node routes ids to their owners), or the
+//                    whole-table diff when the engine could not list every create;
+//   delta_copy_*     into the caller's buffers, once the sizes are known to fit;
+//   delta_end        the snapshot advances (or, on failure, nothing does: the marks are epoch'd).
+struct DeltaCtx {
+    u64 pos0 = 0, range = 0, nblocks = 0, nt = 0;
+    u64* d_base = nullptr;      // [nblocks] exclusive prefix of live records per workgroup
+    u64* d_ids = nullptr;       // [nt][4] debit, credit account ids of the new transfers
+    u64* d_pv = nullptr;        // [nt][3] {pending id lo, hi, voided} of the post / void records
+    u64* d_cnt = nullptr;       // [0] accounts emitted, [1] slots seen, [2] post / void records
+    u64* d_hids = nullptr;      // host-listed ids, on the device
+    u64 hids_cap = 0;
+    u8* d_acc = nullptr;        // [acc_cap] emitted accounts
+    AccountBal* d_before = nullptr;
+    u32* d_slots = nullptr;     // [acc_cap] every slot covered (the snapshot's advance)
+    u64 acc_cap = 0;
+    bool scanned = false;
+};
 
-// The accounts among `ids` created or re-balanced since the previous write-back (records and the
-// balances the forest holds for them), or — after create_accounts the engine could not list — every
-// such account of the table.  `slots` / `scanned`: what delta_advance moves the snapshot over.
-static int delta_accounts(tbgpu* E, const std::vector<u64>& ids, std::vector<u8>& accts, std::vector<u8>& before,
-                          std::vector<u32>& slots, bool* scanned) {
-    int st = ckpt_snapshot_ready(E);
-    if (st) return st;
-    *scanned = E->ckpt_scan;
-    const u64 chunk = 1ULL << 20;
-    u8* d_out = nullptr;
-    u8* d_before = nullptr;
-    u64* d_cnt = nullptr;
-    u64* d_ids = nullptr;
-    u32* d_slots = nullptr;
-    hipError_t err = hipMalloc(&d_out, chunk * 128);
-    if (err == hipSuccess) err = hipMalloc(&d_before, chunk * sizeof(AccountBal));
-    if (err == hipSuccess) err = hipMalloc(&d_cnt, 16);
-    if (err == hipSuccess && !*scanned) err = hipMalloc(&d_ids, chunk * 16);
-    if (err == hipSuccess && !*scanned) err = hipMalloc(&d_slots, chunk * 4);
-    const u64 total = *scanned ? E->account_cap : ids.size() / 2;
-    if (!*scanned && ++E->ckpt_epoch == 0) {  // one epoch per call; wrapped: no stale mark may equal it
-        if (err == hipSuccess) err = hipMemsetAsync(E->ckpt_mark, 0, E->account_cap * sizeof(u32), E->stream);
-        E->ckpt_epoch = 1;
-    }
-    for (u64 s = 0; s < total && err == hipSuccess; s += chunk) {
-        const u64 n = std::min<u64>(chunk, total - s);
-        u64 cnt[2] = {0, 0};
-        err = hipMemsetAsync(d_cnt, 0, 16, E->stream);
-        if (err != hipSuccess) break;
-        if (*scanned) {
-            hipLaunchKernelGGL(tb_delta_accounts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T,
-                               E->ckpt_bal, E->ckpt_ts, s, s + n, d_out, chunk, d_cnt, (AccountBal*)d_before);
-        } else {
-            err = hipMemcpyAsync(d_ids, ids.data() + 2 * s, n * 16, hipMemcpyHostToDevice, E->stream);
-            if (err != hipSuccess) break;
-            hipLaunchKernelGGL(tb_delta_ids, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T, E->ckpt_bal,
-                               E->ckpt_ts, d_ids, n, E->ckpt_mark, E->ckpt_epoch, d_out, (AccountBal*)d_before, d_cnt, d_slots,
-                               d_cnt + 1);
-        }
-        err = hipGetLastError();
-        if (err == hipSuccess) err = hipMemcpyAsync(cnt, d_cnt, 16, hipMemcpyDeviceToHost, E->stream);
-        if (err == hipSuccess) err = hipStreamSynchronize(E->stream);
-        if (err == hipSuccess && cnt[0]) {  // one chunk holds at most `chunk` accounts
-            const size_t at = accts.size();
-            accts.resize(at + cnt[0] * 128);
-            before.resize(before.size() + cnt[0] * sizeof(AccountBal));
-            err = hipMemcpy(accts.data() + at, d_out, cnt[0] * 128, hipMemcpyDeviceToHost);
-            if (err == hipSuccess) err = hipMemcpy(before.data() + at / 2, d_before, cnt[0] * sizeof(AccountBal), hipMemcpyDeviceToHost);
-        }
-        if (err == hipSuccess && !*scanned && cnt[1]) {
-            const size_t at = slots.size();
-            slots.resize(at + cnt[1]);
-            err = hipMemcpy(slots.data() + at, d_slots, cnt[1] * 4, hipMemcpyDeviceToHost);
-        }
-    }
-    void* bufs[] = {d_out, d_before, d_cnt, d_ids, d_slots};
+static void delta_free(DeltaCtx& C) {
+    void* bufs[] = {C.d_base, C.d_ids, C.d_pv, C.d_cnt, C.d_hids, C.d_acc, C.d_before, C.d_slots};
     for (void* p : bufs) if (p) (void)hipFree(p);
-    if (err != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "checkpoint delta (accounts): %s", hipGetErrorString(err));
+    C = DeltaCtx{};
+}
+
+#define DCK(x)                                                                                     \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) {                                                                    \
+            delta_free(C);                                                                         \
+            return fail(TBGPU_STATUS_DEVICE, "checkpoint delta: %s: %s", #x, hipGetErrorString(e_)); \
+        }                                                                                          \
+    } while (0)
+
+// Pass 1 over the log range and the ordered bases.
+static int delta_begin(tbgpu* E, DeltaCtx& C) {
+    int st = ckpt_snapshot_ready(E);
+    if (st) return st;
+    C.pos0 = E->ckpt_pos;
+    C.range = E->log_next - E->ckpt_pos;
+    C.nblocks = (C.range + DELTA_THREADS - 1) / DELTA_THREADS;
+    C.scanned = E->ckpt_scan;
+    DCK(hipMalloc(&C.d_cnt, 32));
+    DCK(hipMemsetAsync(C.d_cnt, 0, 32, E->stream));
+    if (C.nblocks) {
+        u32* d_bc = nullptr;
+        DCK(hipMalloc(&d_bc, C.nblocks * 4));
+        hipLaunchKernelGGL(tb_delta_log_count, dim3((unsigned)C.nblocks), dim3(DELTA_THREADS), 0, E->stream, E->T, C.pos0,
+                           C.range, E->ckpt_ts, d_bc);
+        std::vector<u32> bc(C.nblocks);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(bc.data(), d_bc, C.nblocks * 4, hipMemcpyDeviceToHost, E->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(E->stream);
+        (void)hipFree(d_bc);
+        DCK(e);
+        std::vector<u64> base(C.nblocks);
+        for (u64 b = 0; b < C.nblocks; b++) {
+            base[b] = C.nt;
+            C.nt += bc[b];
+        }
+        DCK(hipMalloc(&C.d_base, C.nblocks * 8));
+        DCK(hipMemcpyAsync(C.d_base, base.data(), C.nblocks * 8, hipMemcpyHostToDevice, E->stream));
+        DCK(hipStreamSynchronize(E->stream));
+    }
     return TBGPU_STATUS_OK;
 }
 
-// The write-back happened: the snapshot takes the covered balances, the log and commit positions move.
-static int delta_advance(tbgpu* E, const std::vector<u32>& slots, bool scanned) {
-    if (scanned) {
-        HIPCK(hipMemcpyAsync(E->ckpt_bal, E->T.acct_bal, E->account_cap * sizeof(AccountBal), hipMemcpyDeviceToDevice,
-                             E->stream));
-    } else if (!slots.empty()) {
-        u32* d_slots = nullptr;
-        HIPCK(hipMalloc(&d_slots, slots.size() * 4));
-        hipError_t err = hipMemcpyAsync(d_slots, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, E->stream);
-        if (err == hipSuccess) {
-            hipLaunchKernelGGL(tb_delta_advance, dim3((unsigned)((slots.size() + 255) / 256)), dim3(256), 0, E->stream, E->T,
-                               E->ckpt_bal, d_slots, (u64)slots.size());
-            err = hipGetLastError();
+// Room for the emitted accounts: the accounts a write-back can name (the ids looked up: two per new
+// transfer plus the listed ones, at most every account); a whole-table diff, every account.
+static int delta_alloc_accounts(tbgpu* E, DeltaCtx& C, u64 host_ids) {
+    C.acc_cap = std::max<u64>(1, C.scanned ? E->account_cap : std::min<u64>(E->account_cap, 2 * C.nt + host_ids));
+    DCK(hipMalloc(&C.d_acc, C.acc_cap * 128));
+    DCK(hipMalloc(&C.d_before, C.acc_cap * sizeof(AccountBal)));
+    if (!C.scanned) {
+        DCK(hipMalloc(&C.d_slots, C.acc_cap * 4));
+        if (++E->ckpt_epoch == 0) {  // one epoch per write-back; wrapped: no stale mark may equal it
+            DCK(hipMemsetAsync(E->ckpt_mark, 0, E->account_cap * sizeof(u32), E->stream));
+            E->ckpt_epoch = 1;
         }
-        if (err == hipSuccess) err = hipStreamSynchronize(E->stream);
-        (void)hipFree(d_slots);
-        if (err != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "checkpoint advance: %s", hipGetErrorString(err));
     }
-    HIPCK(hipStreamSynchronize(E->stream));
+    return TBGPU_STATUS_OK;
+}
+
+// Pass 2: the new transfers' account ids and post / void records, on the device.  ids_host /
+// pv_host (optional): copies on the host (the node routes them).
+static int delta_log_ids(tbgpu* E, DeltaCtx& C, std::vector<u64>* ids_host, std::vector<u64>* pv_host) {
+    if (!C.nt) return TBGPU_STATUS_OK;
+    DCK(hipMalloc(&C.d_ids, C.nt * 32));
+    DCK(hipMalloc(&C.d_pv, C.nt * 24));
+    hipLaunchKernelGGL(tb_delta_log_scatter, dim3((unsigned)C.nblocks), dim3(DELTA_THREADS), 0, E->stream, E->T, C.pos0,
+                       C.range, E->ckpt_ts, C.d_base, (u8*)nullptr, C.d_ids, C.d_pv, C.d_cnt + 2);
+    DCK(hipGetLastError());
+    u64 npv = 0;
+    DCK(hipMemcpyAsync(&npv, C.d_cnt + 2, 8, hipMemcpyDeviceToHost, E->stream));
+    DCK(hipStreamSynchronize(E->stream));
+    if (pv_host) {
+        pv_host->resize(npv * 3);
+        if (npv) DCK(hipMemcpy(pv_host->data(), C.d_pv, npv * 24, hipMemcpyDeviceToHost));
+    }
+    if (ids_host) {
+        ids_host->resize(C.nt * 4);
+        DCK(hipMemcpy(ids_host->data(), C.d_ids, C.nt * 32, hipMemcpyDeviceToHost));
+    }
+    return TBGPU_STATUS_OK;
+}
+
+// The account delta of n ids in device memory (appended to the context's emitted accounts).
+static int delta_ids_dev(tbgpu* E, DeltaCtx& C, const u64* d_ids, u64 n) {
+    if (C.scanned || !n) return TBGPU_STATUS_OK;
+    hipLaunchKernelGGL(tb_delta_ids, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T, E->ckpt_bal,
+                       E->ckpt_ts, d_ids, n, E->ckpt_mark, E->ckpt_epoch, C.d_acc, C.d_before, C.d_cnt, C.d_slots,
+                       C.d_cnt + 1);
+    DCK(hipGetLastError());
+    return TBGPU_STATUS_OK;
+}
+
+static int delta_ids_host(tbgpu* E, DeltaCtx& C, const std::vector<u64>& ids) {
+    const u64 n = ids.size() / 2;
+    if (C.scanned || !n) return TBGPU_STATUS_OK;
+    if (n > C.hids_cap) {
+        if (C.d_hids) (void)hipFree(C.d_hids);
+        C.d_hids = nullptr;
+        DCK(hipMalloc(&C.d_hids, n * 16));
+        C.hids_cap = n;
+    }
+    DCK(hipMemcpyAsync(C.d_hids, ids.data(), n * 16, hipMemcpyHostToDevice, E->stream));
+    const int st = delta_ids_dev(E, C, C.d_hids, n);
+    if (st) return st;
+    DCK(hipStreamSynchronize(E->stream));  // the host buffer may go away
+    return TBGPU_STATUS_OK;
+}
+
+// The whole-table diff (after creates the engine could not list); on a node shard (world > 1) only
+// the accounts it owns.
+static int delta_scan(tbgpu* E, DeltaCtx& C, u32 world, u32 self) {
+    if (!C.scanned) return TBGPU_STATUS_OK;
+    hipLaunchKernelGGL(tb_delta_accounts, dim3((unsigned)((E->account_cap + 255) / 256)), dim3(256), 0, E->stream, E->T,
+                       E->ckpt_bal, E->ckpt_ts, (u64)0, E->account_cap, C.d_acc, C.acc_cap, C.d_cnt, C.d_before, world, self);
+    DCK(hipGetLastError());
+    return TBGPU_STATUS_OK;
+}
+
+static int delta_account_count(tbgpu* E, DeltaCtx& C, u64* na) {
+    u64 cnt[2] = {0, 0};
+    DCK(hipMemcpyAsync(cnt, C.d_cnt, 16, hipMemcpyDeviceToHost, E->stream));
+    DCK(hipStreamSynchronize(E->stream));
+    *na = cnt[0];
+    return TBGPU_STATUS_OK;
+}
+
+// The new transfers, in log (= timestamp) order, into host memory; in slices of a bounded device
+// buffer.
+static int delta_copy_transfers(tbgpu* E, DeltaCtx& C, u8* out) {
+    if (!C.nt) return TBGPU_STATUS_OK;
+    u8* d_out = nullptr;
+    DCK(hipMalloc(&d_out, C.nt * 128));
+    hipLaunchKernelGGL(tb_delta_log_scatter, dim3((unsigned)C.nblocks), dim3(DELTA_THREADS), 0, E->stream, E->T, C.pos0,
+                       C.range, E->ckpt_ts, C.d_base, d_out, (u64*)nullptr, (u64*)nullptr, (u64*)nullptr);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, C.nt * 128, hipMemcpyDeviceToHost, E->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(E->stream);
+    (void)hipFree(d_out);
+    DCK(e);
+    return TBGPU_STATUS_OK;
+}
+
+static int delta_copy_accounts(tbgpu* E, DeltaCtx& C, u64 na, u8* out, u8* before_out) {
+    if (!na) return TBGPU_STATUS_OK;
+    DCK(hipMemcpyAsync(out, C.d_acc, na * 128, hipMemcpyDeviceToHost, E->stream));
+    if (before_out) DCK(hipMemcpyAsync(before_out, C.d_before, na * sizeof(AccountBal), hipMemcpyDeviceToHost, E->stream));
+    DCK(hipStreamSynchronize(E->stream));
+    return TBGPU_STATUS_OK;
+}
+
+// The write-back happened: the snapshot takes the covered balances, the log and commit positions
+// move, the lists empty.
+static int delta_end(tbgpu* E, DeltaCtx& C) {
+    if (C.scanned) {
+        DCK(hipMemcpyAsync(E->ckpt_bal, E->T.acct_bal, E->account_cap * sizeof(AccountBal), hipMemcpyDeviceToDevice,
+                           E->stream));
+    } else {
+        u64 cnt[2] = {0, 0};
+        DCK(hipMemcpyAsync(cnt, C.d_cnt, 16, hipMemcpyDeviceToHost, E->stream));
+        DCK(hipStreamSynchronize(E->stream));
+        if (cnt[1]) {
+            hipLaunchKernelGGL(tb_delta_advance, dim3((unsigned)((cnt[1] + 255) / 256)), dim3(256), 0, E->stream, E->T,
+                               E->ckpt_bal, C.d_slots, cnt[1]);
+            DCK(hipGetLastError());
+        }
+    }
+    DCK(hipStreamSynchronize(E->stream));
     E->ckpt_pos = E->log_next;
     E->ckpt_ts = E->commit_ts;
     E->ckpt_scan = false;
     std::vector<u64>().swap(E->ckpt_ids);
+    delta_free(C);
     return TBGPU_STATUS_OK;
 }
 
-// Ids of the accounts the new transfers moved (debit and credit of each).
-static void delta_transfer_accounts(const std::vector<u8>& xfers, std::vector<u64>& ids) {
-    const u64 n = xfers.size() / 128;
-    for (u64 i = 0; i < n; i++) {
-        const u64* w = (const u64*)&xfers[i * 128];
-        ids.push_back(w[2]);
-        ids.push_back(w[3]);
-        ids.push_back(w[4]);
-        ids.push_back(w[5]);
-    }
+// Log order is timestamp order for everything a commit appends; records appended by an upsert or a
+// load (a node's sequencer write-back, a restart's warm-up) may sit out of order: sort those runs.
+static void delta_sort_by_timestamp(u8* recs, u64 n) {
+    auto ts = [&](u64 i) { return *(const u64*)(recs + i * 128 + 120); };
+    bool sorted = true;
+    for (u64 i = 1; i < n && sorted; i++) sorted = ts(i - 1) < ts(i);
+    if (sorted) return;
+    std::vector<std::pair<u64, u64>> key(n);
+    for (u64 i = 0; i < n; i++) key[i] = {ts(i), i};
+    std::sort(key.begin(), key.end());
+    std::vector<u8> tmp(recs, recs + n * 128);
+    for (u64 i = 0; i < n; i++) memcpy(recs + i * 128, &tmp[key[i].second * 128], 128);
 }
 
-// The post / void records among the new transfers: their pending ids and the new posted state.
-static void delta_post_void(const std::vector<u8>& xfers, std::vector<u64>& pending_ids, std::vector<u8>& voided) {
-    const u64 n = xfers.size() / 128;
+// The posted-groove pairs of the post / void records: {pending transfer's timestamp, voided}.
+static int delta_posted_pairs(const std::vector<u64>& pv, std::vector<std::pair<u64, u64>>& out,
+                              const std::function<int(const u64*, u32, u8*, u8*)>& fetch) {
+    const u64 n = pv.size() / 3;
+    if (!n) return TBGPU_STATUS_OK;
+    std::vector<u64> ids(2 * n);
     for (u64 i = 0; i < n; i++) {
-        const u8* r = &xfers[i * 128];
-        const u16 f = *(const u16*)(r + 118);
-        if (!(f & (TF_POST | TF_VOID))) continue;
-        pending_ids.push_back(*(const u64*)(r + 64));
-        pending_ids.push_back(*(const u64*)(r + 72));
-        voided.push_back((f & TF_POST) ? 0 : 1);
+        ids[2 * i] = pv[3 * i];
+        ids[2 * i + 1] = pv[3 * i + 1];
     }
-}
-
-// Sorted outputs of a write-back.
-static void delta_emit(const std::vector<u8>& accts, const std::vector<u8>& before, const std::vector<u8>& xfers,
-                       const std::vector<std::pair<u64, u64>>& posted, void* accounts_out, void* accounts_before_out,
-                       void* transfers_out, u64* posted_out) {
-    const u64 na = accts.size() / 128, nt = xfers.size() / 128;
-    std::vector<u64> idx(na);
-    for (u64 i = 0; i < na; i++) idx[i] = i;
-    std::sort(idx.begin(), idx.end(), [&](u64 a, u64 b) { return id_less(&accts[a * 128], &accts[b * 128]); });
-    for (u64 i = 0; i < na; i++) memcpy((u8*)accounts_out + i * 128, &accts[idx[i] * 128], 128);
-    if (accounts_before_out) {
-        for (u64 i = 0; i < na; i++) memcpy((u8*)accounts_before_out + i * 64, &before[idx[i] * 64], 64);
+    std::vector<u8> rec(n * 128), st(n);
+    const int s = fetch(ids.data(), (u32)n, rec.data(), st.data());
+    if (s) return s;
+    for (u64 i = 0; i < n; i++) {
+        if (!st[i]) return fail(TBGPU_STATUS_PANIC, "checkpoint delta: a posted pending transfer is missing");
+        out.push_back({*(const u64*)&rec[i * 128 + 120], pv[3 * i + 2]});
     }
-    auto ts_of = [&](u64 i) { return *(const u64*)&xfers[i * 128 + 120]; };
-    idx.resize(nt);
-    for (u64 i = 0; i < nt; i++) idx[i] = i;
-    std::sort(idx.begin(), idx.end(), [&](u64 a, u64 b) { return ts_of(a) < ts_of(b); });
-    for (u64 i = 0; i < nt; i++) memcpy((u8*)transfers_out + i * 128, &xfers[idx[i] * 128], 128);
-    std::vector<std::pair<u64, u64>> pairs(posted);
-    std::sort(pairs.begin(), pairs.end());
-    for (u64 i = 0; i < pairs.size(); i++) {
-        posted_out[2 * i] = pairs[i].first;
-        posted_out[2 * i + 1] = pairs[i].second;
-    }
+    std::sort(out.begin(), out.end());
+    return TBGPU_STATUS_OK;
 }
 
 extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, void* accounts_before_out, uint64_t accounts_cap,
@@ -1462,38 +1533,43 @@ extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, void* acco
         int st = engine_sync(E);
         if (st) return st;
     }
-    std::vector<u8> xfers, accts, before;
-    int st = delta_transfers(E, xfers);
-    if (st) return st;
-    // Posted-groove entries: keyed by the pending transfer's timestamp.
-    std::vector<u64> pids;
-    std::vector<u8> voided;
-    delta_post_void(xfers, pids, voided);
+    DeltaCtx C;
+    std::vector<u64> pv;
+    int st = delta_begin(E, C);
+    if (!st) st = delta_alloc_accounts(E, C, E->ckpt_ids.size() / 2);
+    if (!st) st = delta_log_ids(E, C, nullptr, &pv);
+    if (!st) st = delta_ids_dev(E, C, C.d_ids, 2 * C.nt);
+    if (!st) st = delta_ids_host(E, C, E->ckpt_ids);
+    if (!st) st = delta_scan(E, C, 0, 0);
+    u64 na = 0;
+    if (!st) st = delta_account_count(E, C, &na);
     std::vector<std::pair<u64, u64>> posted;
-    if (!voided.empty()) {
-        std::vector<u8> prec(voided.size() * 128), pst(voided.size());
-        if ((st = tbgpu_fetch_transfers(E, pids.data(), (u32)voided.size(), prec.data(), pst.data()))) return st;
-        for (size_t i = 0; i < voided.size(); i++) {
-            if (!pst[i]) return fail(TBGPU_STATUS_PANIC, "checkpoint delta: a posted pending transfer is missing");
-            posted.push_back({*(const u64*)&prec[i * 128 + 120], voided[i]});
-        }
+    if (!st) {
+        st = delta_posted_pairs(pv, posted, [&](const u64* ids, u32 n, u8* out, u8* state) {
+            return tbgpu_fetch_transfers(E, ids, n, out, state);
+        });
     }
-    std::vector<u64> ids(E->ckpt_ids);
-    delta_transfer_accounts(xfers, ids);
-    std::vector<u32> slots;
-    bool scanned = false;
-    if ((st = delta_accounts(E, ids, accts, before, slots, &scanned))) return st;
-    const u64 na = accts.size() / 128, nt = xfers.size() / 128, np = posted.size();
+    if (st) {
+        delta_free(C);
+        return st;
+    }
     counts->created_after = E->ckpt_ts;
     counts->accounts = na;
-    counts->transfers = nt;
-    counts->posted = np;
-    if (na > accounts_cap || nt > transfers_cap || np > posted_cap) {  // nothing advanced; the marks are epoch'd
+    counts->transfers = C.nt;
+    counts->posted = posted.size();
+    if (na > accounts_cap || C.nt > transfers_cap || posted.size() > posted_cap) {  // nothing advanced
+        delta_free(C);
         return fail(TBGPU_STATUS_INVALID, "checkpoint delta: needs %llu accounts, %llu transfers, %llu posted",
-                    (unsigned long long)na, (unsigned long long)nt, (unsigned long long)np);
+                    (unsigned long long)na, (unsigned long long)counts->transfers, (unsigned long long)counts->posted);
     }
-    delta_emit(accts, before, xfers, posted, accounts_out, accounts_before_out, transfers_out, posted_out);
-    return delta_advance(E, slots, scanned);
+    for (size_t i = 0; i < posted.size(); i++) {
+        posted_out[2 * i] = posted[i].first;
+        posted_out[2 * i + 1] = posted[i].second;
+    }
+    if ((st = delta_copy_transfers(E, C, (u8*)transfers_out))) return st;
+    delta_sort_by_timestamp((u8*)transfers_out, C.nt);
+    if ((st = delta_copy_accounts(E, C, na, (u8*)accounts_out, (u8*)accounts_before_out))) return st;
+    return delta_end(E, C);
 }
 
 extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
@@ -1809,6 +1885,28 @@ extern "C" int tbgpu_bench_reset_transfers(tbgpu_t* E) {
     HIPCK(hipGetLastError());
     HIPCK(hipStreamSynchronize(E->stream));
     return TBGPU_STATUS_OK;
+}
+
+// Bench: take the current state as written back (the snapshot, the log and commit positions), so
+// the next tbgpu_checkpoint_delta covers only what is committed after this call.
+extern "C" int tbgpu_bench_checkpoint_mark(tbgpu_t* E) {
+    if (E->node) {
+        for (u32 d = 0; d < node_world(E->node); d++) {
+            const int st = tbgpu_bench_checkpoint_mark(node_engine(E->node, d));
+            if (st) return st;
+        }
+        return TBGPU_STATUS_OK;
+    }
+    HIPCK(hipSetDevice(E->device));
+    if (E->pending) {
+        int st = engine_sync(E);
+        if (st) return st;
+    }
+    int st = ckpt_snapshot_ready(E);
+    if (st) return st;
+    DeltaCtx C;
+    C.scanned = true;
+    return delta_end(E, C);
 }
 
 extern "C" int tbgpu_bench_pass_latencies(tbgpu_t* E, double* out_ms, uint64_t cap, uint64_t* count) {

@@ -97,11 +97,12 @@ __global__ void tb_zero_balances(Tables T, u64 cap) {
 // accounts (create_accounts committed from device memory, tbgpu_commit_device_async, or more of them
 // than the engine lists).  Counts past `cap` are still counted (the host retries with room).
 __global__ void tb_delta_accounts(Tables T, const AccountBal* snap, u64 ts0, u64 first, u64 last, u8* out, u64 cap,
-                                  u64* count, AccountBal* before) {
+                                  u64* count, AccountBal* before, u32 world, u32 self) {
     const u64 i = first + (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= last) return;
     const AccountHot& h = T.acct_hot[i];
     if (h.timestamp == 0 || tb_id_reserved(h.id_lo, h.id_hi)) return;
+    if (world > 1 && tb_home(h.id_lo, h.id_hi, world) != self) return;  // a node shard: its owned accounts
     const AccountBal b = T.acct_bal[i], s = snap[i];
     const bool same = b.debits_pending == s.debits_pending && b.debits_posted == s.debits_posted &&
                       b.credits_pending == s.credits_pending && b.credits_posted == s.credits_posted;
@@ -119,16 +120,58 @@ __global__ void tb_delta_accounts(Tables T, const AccountBal* snap, u64 ts0, u64
 // Transfers: the log positions written since the previous write-back, [pos0, log_end).  A record is
 // new if the index holds it at that position (a withdrawn speculative record's entry is tombstoned;
 // a re-inserted id points elsewhere) and it is younger than the previous write-back (records loaded
-// from the forest after a restart are older).
-__global__ void tb_delta_log(Tables T, u64 pos0, u64 n, u64 ts0, u8* out, u64* count) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const u64 pos = pos0 + i;
+// from the forest after a restart are older).  Log order is timestamp order, and the compaction
+// keeps it: a count pass (live records per workgroup), the host's exclusive prefix over the
+// workgroups, then an ordered scatter.
+#define DELTA_THREADS 256
+
+__device__ static inline bool tb_delta_live(const Tables& T, u64 pos, u64 ts0) {
     const Transfer& t = T.xlog[pos];
-    if (t.timestamp <= ts0) return;
-    if (tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id)) != (u32)pos) return;
-    const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
-    *(Transfer*)(out + k * 128) = t;
+    return t.timestamp > ts0 && tb_transfer_find(T, tb_lo(t.id), tb_hi(t.id)) == (u32)pos;
+}
+
+__global__ __launch_bounds__(DELTA_THREADS) void tb_delta_log_count(Tables T, u64 pos0, u64 n, u64 ts0, u32* block_counts) {
+    __shared__ u32 s_wave[DELTA_THREADS / 64];
+    const u64 i = (u64)blockIdx.x * DELTA_THREADS + threadIdx.x;
+    const bool live = i < n && tb_delta_live(T, pos0 + i, ts0);
+    const u64 m = __ballot(live);
+    if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u32 c = 0;
+        for (u32 w = 0; w < DELTA_THREADS / 64; w++) c += s_wave[w];
+        block_counts[blockIdx.x] = c;
+    }
+}
+
+// The ordered scatter.  out (optional): the records; ids (optional): the debit and credit account
+// ids of each (4 words); pv: the post / void records' {pending id lo, hi, voided}, unordered.
+__global__ __launch_bounds__(DELTA_THREADS) void tb_delta_log_scatter(Tables T, u64 pos0, u64 n, u64 ts0, const u64* block_base,
+                                                                      u8* out, u64* ids, u64* pv, u64* pv_count) {
+    __shared__ u32 s_wave[DELTA_THREADS / 64];
+    const u64 i = (u64)blockIdx.x * DELTA_THREADS + threadIdx.x;
+    const bool live = i < n && tb_delta_live(T, pos0 + i, ts0);
+    const u64 m = __ballot(live);
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) s_wave[wave] = __popcll(m);
+    __syncthreads();
+    if (!live) return;
+    u64 k = block_base[blockIdx.x] + __popcll(m & ((1ULL << lane) - 1));
+    for (u32 w = 0; w < wave; w++) k += s_wave[w];
+    const Transfer& t = T.xlog[pos0 + i];
+    if (out) *(Transfer*)(out + k * 128) = t;
+    if (ids) {
+        ids[4 * k] = tb_lo(t.debit_account_id);
+        ids[4 * k + 1] = tb_hi(t.debit_account_id);
+        ids[4 * k + 2] = tb_lo(t.credit_account_id);
+        ids[4 * k + 3] = tb_hi(t.credit_account_id);
+    }
+    if (pv && (t.flags & (TF_POST | TF_VOID))) {
+        const u64 q = atomicAdd((unsigned long long*)pv_count, 1ULL);
+        pv[3 * q] = tb_lo(t.pending_id);
+        pv[3 * q + 1] = tb_hi(t.pending_id);
+        pv[3 * q + 2] = (t.flags & TF_POST) ? 0 : 1;
+    }
 }
 
 // Accounts: the ids the host names as possibly changed (the debit / credit accounts of the new

@@ -28,11 +28,7 @@
 
 enum : u32 { ROUTE_DIRTY_FLAGS = 1, ROUTE_DIRTY_LIMIT = 2 };
 
-// home(id): the top 32 bits of the id hash scaled to [0, world) — independent of the low hash bits
-// that pick the index position, so each home's index stays uniformly loaded.
-__host__ __device__ static inline u32 tb_home(u64 lo, u64 hi, u32 world) {
-    return (u32)(((tb_hash_id(lo, hi) >> 32) * (u64)world) >> 32);
-}
+// home(id) / owner(id): tb_home (tb_device.h).
 
 struct RouteArgs {
     const u8* events;      // this rank's events of the pass, back to back

@@ -1031,11 +1031,11 @@ static int node_api_export(TbNode* N, int what, void* out, u64 cap, u64* count) 
 }
 
 // Groove write-back of the node, O(changes) like a single engine's (engine.hip delta_*): the new
-// transfers of every shard's log; the posted entries their post / void records make (the pending
-// transfer may live on another shard: its timestamp is fetched from its home); the accounts the new
-// transfers moved — wherever those transfers live — plus the listed creates and direct writes, each
-// looked up on its OWNER, whose copy holds its balances.  A created account is listed by every shard
-// (replicated records): the owner's copy wins the merge.
+// transfers of every shard's log, merged by timestamp; the posted entries their post / void records
+// make (the pending transfer may live on another shard: its timestamp is fetched from its home); the
+// accounts the new transfers moved — wherever those transfers live — plus the listed creates and
+// direct writes, each looked up on its OWNER, whose copy holds its balances (a whole-table diff of
+// a shard keeps only the accounts it owns).
 static int node_api_checkpoint_delta(TbNode* N, void* accounts_out, void* accounts_before_out, u64 accounts_cap,
                                      void* transfers_out, u64 transfers_cap, u64* posted_out, u64 posted_cap,
                                      tbgpu_delta_counts* counts) {
@@ -1043,97 +1043,90 @@ static int node_api_checkpoint_delta(TbNode* N, void* accounts_out, void* accoun
     const u32 W = N->world;
     int st = node_sync(N);
     if (st) return st;
-    std::vector<u8> xfers;
+    std::vector<DeltaCtx> C(W);
+    auto abort_all = [&](int status) {
+        for (u32 d = 0; d < W; d++) delta_free(C[d]);
+        return status;
+    };
+    std::vector<u64> ids_all, pv_all;
+    u64 nt = 0;
     for (u32 d = 0; d < W; d++) {
         NCK(hipSetDevice(N->D[d].device));
-        if ((st = delta_transfers(N->D[d].E, xfers))) return st;
+        std::vector<u64> ids, pv;
+        if ((st = delta_begin(N->D[d].E, C[d]))) return abort_all(st);
+        if ((st = delta_log_ids(N->D[d].E, C[d], &ids, &pv))) return abort_all(st);
+        ids_all.insert(ids_all.end(), ids.begin(), ids.end());
+        pv_all.insert(pv_all.end(), pv.begin(), pv.end());
+        ids_all.insert(ids_all.end(), N->D[d].E->ckpt_ids.begin(), N->D[d].E->ckpt_ids.end());
+        nt += C[d].nt;
     }
-    std::vector<u64> pids;
-    std::vector<u8> voided;
-    delta_post_void(xfers, pids, voided);
+    std::vector<std::vector<u64>> owned(W);
+    for (size_t i = 0; i + 1 < ids_all.size(); i += 2) {
+        const u32 o = tb_home(ids_all[i], ids_all[i + 1], W);
+        owned[o].push_back(ids_all[i]);
+        owned[o].push_back(ids_all[i + 1]);
+    }
+    std::vector<u64> na(W, 0);
+    u64 na_total = 0;
+    for (u32 o = 0; o < W; o++) {
+        tbgpu* E = N->D[o].E;
+        NCK(hipSetDevice(N->D[o].device));
+        if ((st = delta_alloc_accounts(E, C[o], owned[o].size() / 2))) return abort_all(st);
+        if ((st = delta_ids_host(E, C[o], owned[o]))) return abort_all(st);
+        if ((st = delta_scan(E, C[o], W, o))) return abort_all(st);
+        if ((st = delta_account_count(E, C[o], &na[o]))) return abort_all(st);
+        na_total += na[o];
+    }
     std::vector<std::pair<u64, u64>> posted;
-    if (!voided.empty()) {
-        std::vector<u8> prec(voided.size() * 128), pst(voided.size());
-        if ((st = node_fetch(N, false, pids.data(), (u32)voided.size(), prec.data(), pst.data()))) return st;
-        for (size_t i = 0; i < voided.size(); i++) {
-            if (!pst[i]) return fail(TBGPU_STATUS_PANIC, "checkpoint delta: a posted pending transfer is missing");
-            posted.push_back({*(const u64*)&prec[i * 128 + 120], voided[i]});
-        }
-    }
-    std::vector<u64> all;
-    delta_transfer_accounts(xfers, all);
-    for (u32 d = 0; d < W; d++) all.insert(all.end(), N->D[d].E->ckpt_ids.begin(), N->D[d].E->ckpt_ids.end());
-    std::vector<std::vector<u64>> ids(W);
-    for (size_t i = 0; i + 1 < all.size(); i += 2) {
-        const u32 o = tb_home(all[i], all[i + 1], W);
-        ids[o].push_back(all[i]);
-        ids[o].push_back(all[i + 1]);
-    }
-    std::vector<std::vector<u8>> acc(W), bef(W);
-    std::vector<std::vector<u32>> slots(W);
-    std::vector<char> scanned(W, 0);
-    for (u32 d = 0; d < W; d++) {
-        NCK(hipSetDevice(N->D[d].device));
-        bool sc = false;
-        std::vector<u8> a, b;
-        if ((st = delta_accounts(N->D[d].E, ids[d], a, b, slots[d], &sc))) return st;
-        scanned[d] = sc;
-        // Sorted by id for the merge.
-        const u64 n = a.size() / 128;
-        std::vector<u64> idx(n);
-        for (u64 i = 0; i < n; i++) idx[i] = i;
-        std::sort(idx.begin(), idx.end(), [&](u64 x, u64 y) { return id_less(&a[x * 128], &a[y * 128]); });
-        acc[d].resize(n * 128);
-        bef[d].resize(n * 64);
-        for (u64 i = 0; i < n; i++) {
-            memcpy(&acc[d][i * 128], &a[idx[i] * 128], 128);
-            memcpy(&bef[d][i * 64], &b[idx[i] * 64], 64);
-        }
-    }
-    // Merge accounts by id: the owner's copy wins.
-    std::vector<u8> accts, before;
-    std::vector<size_t> pos(W, 0);
-    while (true) {
-        const u8* best = nullptr;
-        for (u32 d = 0; d < W; d++) {
-            if (pos[d] * 128 < acc[d].size()) {
-                const u8* r = &acc[d][pos[d] * 128];
-                if (!best || id_less(r, best)) best = r;
-            }
-        }
-        if (!best) break;
-        const u32 o = node_home(best, W);
-        const u8* rec = nullptr;
-        const u8* bf = nullptr;
-        u8 key[16];
-        memcpy(key, best, 16);
-        for (u32 d = 0; d < W; d++) {
-            if (pos[d] * 128 < acc[d].size() && memcmp(&acc[d][pos[d] * 128], key, 16) == 0) {
-                if (!rec || d == o) {
-                    rec = &acc[d][pos[d] * 128];
-                    bf = &bef[d][pos[d] * 64];
-                }
-            }
-        }
-        accts.insert(accts.end(), rec, rec + 128);
-        before.insert(before.end(), bf, bf + 64);
-        for (u32 d = 0; d < W; d++) {
-            if (pos[d] * 128 < acc[d].size() && memcmp(&acc[d][pos[d] * 128], key, 16) == 0) pos[d]++;
-        }
-    }
-    const u64 na = accts.size() / 128, nt = xfers.size() / 128, np = posted.size();
+    st = delta_posted_pairs(pv_all, posted, [&](const u64* ids, u32 n, u8* out, u8* state) {
+        return node_fetch(N, false, ids, n, out, state);
+    });
+    if (st) return abort_all(st);
     counts->created_after = N->D[0].E->ckpt_ts;
-    counts->accounts = na;
+    counts->accounts = na_total;
     counts->transfers = nt;
-    counts->posted = np;
-    if (na > accounts_cap || nt > transfers_cap || np > posted_cap) {  // nothing advanced
-        return fail(TBGPU_STATUS_INVALID, "checkpoint delta: needs %llu accounts, %llu transfers, %llu posted",
-                    (unsigned long long)na, (unsigned long long)nt, (unsigned long long)np);
+    counts->posted = posted.size();
+    if (na_total > accounts_cap || nt > transfers_cap || posted.size() > posted_cap) {  // nothing advanced
+        return abort_all(fail(TBGPU_STATUS_INVALID, "checkpoint delta: needs %llu accounts, %llu transfers, %llu posted",
+                              (unsigned long long)na_total, (unsigned long long)nt, (unsigned long long)posted.size()));
     }
-    delta_emit(accts, before, xfers, posted, accounts_out, accounts_before_out, transfers_out, posted_out);
+    for (size_t i = 0; i < posted.size(); i++) {
+        posted_out[2 * i] = posted[i].first;
+        posted_out[2 * i + 1] = posted[i].second;
+    }
+    // Transfers: each shard's in timestamp order, merged.
+    std::vector<std::vector<u8>> runs(W);
     for (u32 d = 0; d < W; d++) {
         NCK(hipSetDevice(N->D[d].device));
-        if ((st = delta_advance(N->D[d].E, slots[d], scanned[d]))) return st;
+        runs[d].resize(C[d].nt * 128);
+        if ((st = delta_copy_transfers(N->D[d].E, C[d], runs[d].data()))) return abort_all(st);
+        delta_sort_by_timestamp(runs[d].data(), C[d].nt);
+    }
+    {
+        std::vector<size_t> pos(W, 0);
+        auto ts_at = [&](u32 d) { return *(const u64*)&runs[d][pos[d] * 128 + 120]; };
+        for (u64 k = 0; k < nt; k++) {
+            u32 best = W;
+            for (u32 d = 0; d < W; d++) {
+                if (pos[d] < C[d].nt && (best == W || ts_at(d) < ts_at(best))) best = d;
+            }
+            memcpy((u8*)transfers_out + k * 128, &runs[best][pos[best] * 128], 128);
+            pos[best]++;
+        }
+    }
+    // Accounts: each owner's, one after the other.
+    u64 at = 0;
+    for (u32 o = 0; o < W; o++) {
+        NCK(hipSetDevice(N->D[o].device));
+        if ((st = delta_copy_accounts(N->D[o].E, C[o], na[o], (u8*)accounts_out + at * 128,
+                                      accounts_before_out ? (u8*)accounts_before_out + at * 64 : nullptr))) {
+            return abort_all(st);
+        }
+        at += na[o];
+    }
+    for (u32 d = 0; d < W; d++) {
+        NCK(hipSetDevice(N->D[d].device));
+        if ((st = delta_end(N->D[d].E, C[d]))) return abort_all(st);
     }
     return TBGPU_STATUS_OK;
 }

@@ -140,6 +140,13 @@ __host__ __device__ static inline u64 tb_hash_id(u64 lo, u64 hi) {
     return tb_mix64(lo ^ tb_mix64(hi ^ 0x243f6a8885a308d3ULL));
 }
 
+// home(id) of a transfer / owner(id) of an account among `world` shards: the top 32 bits of the id
+// hash scaled to [0, world) — independent of the low hash bits that pick the table position, so
+// each shard's tables stay uniformly loaded.
+__host__ __device__ static inline u32 tb_home(u64 lo, u64 hi, u32 world) {
+    return (u32)(((tb_hash_id(lo, hi) >> 32) * (u64)world) >> 32);
+}
+
 __host__ __device__ static inline u128 tb_u128(u64 lo, u64 hi) { return ((u128)hi << 64) | lo; }
 __host__ __device__ static inline u64 tb_lo(u128 v) { return (u64)v; }
 __host__ __device__ static inline u64 tb_hi(u128 v) { return (u64)(v >> 64); }

@@ -143,7 +143,7 @@ struct DeviceError : std::runtime_error {
 };
 
 // One groove write-back (tbgpu_checkpoint_delta): what checkpoint() hands to the durable
-// replica's forest — accounts (128-B records, by id), transfers (by timestamp), posted pairs
+// replica's forest — accounts (128-B records, in no particular order), transfers (by timestamp), posted pairs
 // {pending timestamp, fulfillment} (by timestamp).
 struct Delta {
     std::vector<uint8_t> accounts;

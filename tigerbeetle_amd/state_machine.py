@@ -73,6 +73,9 @@ class Engine:
 
     def close(self):
         if getattr(self, "h", None):
+            for arr in getattr(self, "_delta_bufs", (None, ()))[1]:
+                self.lib.tbgpu_unregister_host(self.h, arr.ctypes.data)
+            self._delta_bufs = None
             self.lib.tbgpu_deinit(self.h)
             self.h = None
 
@@ -225,16 +228,16 @@ class Engine:
 
     PROF_VALIDATE, PROF_RESOLVE, PROF_REPLAY, PROF_CLEAR, PROF_PASS, PROF_APPLY, PROF_ALL = 1, 2, 4, 8, 16, 32, 63
 
-    def checkpoint_delta(self):
-        """Objects changed since the previous call (groove write-back): a Delta of accounts (by
-        id), transfers (by timestamp) and posted pairs {pending timestamp, fulfillment}."""
+    def checkpoint_delta(self, caps=None):
+        """Objects changed since the previous call (groove write-back): a Delta of accounts (in no
+        particular order), transfers (by timestamp) and posted pairs {pending timestamp,
+        fulfillment}.  caps: initial buffer sizes (accounts, transfers, posted); grown and retried
+        when too small.  The arrays are views of buffers the engine keeps registered for DMA (the
+        wrapper's write-back buffers, allocated once): valid until the next call."""
         counts = _lib.tbgpu_delta_counts()
-        caps = [1024, 1024, 1024]
+        caps = list(caps) if caps else [1024, 1024, 1024]
         while True:
-            a = np.zeros(caps[0], dtype=ACCOUNT_DTYPE)
-            before = np.zeros((caps[0], 8), dtype=np.uint64)
-            t = np.zeros(caps[1], dtype=TRANSFER_DTYPE)
-            p = np.zeros((caps[2], 2), dtype=np.uint64)
+            a, before, t, p = self._delta_buffers(caps)
             st = self.lib.tbgpu_checkpoint_delta(self.h, a.ctypes.data, before.ctypes.data, caps[0], t.ctypes.data,
                                                  caps[1], p.ctypes.data, caps[2], ctypes.byref(counts))
             need = [counts.accounts, counts.transfers, counts.posted]
@@ -243,6 +246,22 @@ class Engine:
                 continue
             _lib.check(st)
             return Delta(a[:need[0]], t[:need[1]], p[:need[2]], before[:need[0]], counts.created_after)
+
+    def _delta_buffers(self, caps):
+        """Write-back buffers of at least `caps` entries, kept (and registered) across calls."""
+        have = getattr(self, "_delta_bufs", None)
+        if have is not None and all(h >= c for h, c in zip(have[0], caps)):
+            return have[1]
+        if have is not None:
+            for arr in have[1]:
+                _lib.check(self.lib.tbgpu_unregister_host(self.h, arr.ctypes.data))
+        caps = [max(c, 1) for c in caps]
+        bufs = (np.empty(caps[0], dtype=ACCOUNT_DTYPE), np.empty((caps[0], 8), dtype=np.uint64),
+                np.empty(caps[1], dtype=TRANSFER_DTYPE), np.empty((caps[2], 2), dtype=np.uint64))
+        for arr in bufs:
+            _lib.check(self.lib.tbgpu_register_host(self.h, arr.ctypes.data, arr.nbytes))
+        self._delta_bufs = (caps, bufs)
+        return bufs
 
     def ledger_summary(self):
         """{"debits_pending", "debits_posted", "credits_pending", "credits_posted": u128 sums over every
@@ -254,6 +273,10 @@ class Engine:
         out = {n: int(s.sums[2 * i]) | (int(s.sums[2 * i + 1]) << 64) for i, n in enumerate(names)}
         out.update(accounts=int(s.accounts), stray=int(s.stray))
         return out
+
+    def checkpoint_mark(self):
+        """Take the current state as written back (tbgpu_bench_checkpoint_mark)."""
+        _lib.check(self.lib.tbgpu_bench_checkpoint_mark(self.h))
 
     def legs_min_events(self, events):
         """Passes of >= events transfers use the sorted balance legs (0: every pass)."""
