@@ -88,6 +88,8 @@ def parse():
                    help="time the validate kernel's access pattern without its logic (roofline.access_mix)")
     p.add_argument("--host-prepares", type=int, default=600,
                    help="prepares committed one per tbgpu_commit call from host memory (the replica's call; 0: skip)")
+    p.add_argument("--replica-prepares", type=int, default=2000,
+                   help="ops of the replica call path through the C++ mirror (tb_replica_bench; 0: skip)")
     p.add_argument("--write-back", type=int, default=1,
                    help="time the groove write-back per bar at the full stored count and near empty")
     p.add_argument("--engine", default="node", choices=["node", "ranks"],
@@ -210,6 +212,25 @@ def run_write_back(engine, args, t_cursor, bars=4):
     return {"stored_transfers": int(stored), "bar_prepares": bar, "bars": out,
             "ms_per_bar": round(float(np.mean([b["ms"] for b in steady])), 3),
             "bytes_per_bar": int(np.mean([128 * b["transfers"] + 192 * b["accounts"] for b in steady]))}, t_cursor
+
+
+def run_replica_path(args, device):
+    """The replica's call path from C++ (tigerbeetle_amd/host/replica_bench.cpp, the tb::StateMachine
+    mirror): per op, prepare -> prefetch (the body's DMA from the registered message pool starts)
+    -> commit -> compact, serially, one C2 prepare of 8190 transfers each (src/vsr/replica.zig:
+    3045-3102); without and with the per-bar groove write-back in compact."""
+    import subprocess
+    exe = os.path.join(ROOT, "tigerbeetle_amd", "host", "tb_replica_bench")
+    out = {}
+    for name, opts in (("in_memory", []), ("in_memory_staged", ["--stage"]), ("with_write_back", ["--write-back"])):
+        cmd = [exe, "--accounts", str(args.accounts), "--prepares", str(args.replica_prepares),
+               "--device", str(device)] + opts
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            out[name] = {"error": (r.stdout + r.stderr)[-500:]}
+            continue
+        out[name] = json.loads(r.stdout.strip().splitlines()[-1])
+    return out
 
 
 def run_cpu_baseline(engine, args, acct_lens, acct_ts, events_dev, sample_lens, sample_ts):
@@ -731,6 +752,9 @@ def main():
     for ptr in (events_dev, res_dev, rb_dev):
         engine.free(ptr)
     engine.close()
+    replica_path = None
+    if rank == 0 and world == 1 and args.replica_prepares > 0:
+        replica_path = run_replica_path(args, local_rank)
     secondary = {}
     if rank == 0 and world == 1 and args.workload == "c2" and args.secondary:
         for kind in ("c3", "c4"):
@@ -772,6 +796,7 @@ def main():
         "cpu_baseline": cpu,
         "parity": parity,
         "host_commit": host,
+        "replica_path": replica_path,
         "write_back": write_back,
         "secondary": secondary or None,
     }

@@ -10,6 +10,7 @@
  *   StateMachine.init(allocator, grid, options)            tbgpu_init
  *     (src/state_machine.zig:264-278)
  *   StateMachine.deinit / reset (:280-299)                 tbgpu_deinit / tbgpu_reset
+ *   StateMachine.prefetch (:345-506)                       tbgpu_prefetch (stages the body by DMA)
  *   StateMachine.commit(client, op, timestamp, operation,  tbgpu_commit (one prepare) and
  *     input, output) -> usize (:508-540)                     tbgpu_commit_many (N prepares, one
  *                                                             device pass; same bytes as N commits)
@@ -99,6 +100,13 @@ int tbgpu_reset(tbgpu_t* engine);
  * Byte-identical to the reference for every operation. */
 int tbgpu_commit(tbgpu_t* engine, uint8_t operation, uint64_t timestamp, const void* input,
                  uint32_t input_len, void* output, uint32_t output_cap, uint32_t* out_len);
+
+/* StateMachine.prefetch (src/state_machine.zig:345-506) for the prepare about to be committed.  The
+ * objects are HBM-resident; what is staged is the body: a create body in registered host memory
+ * (tbgpu_register_host: the message pool) starts crossing PCIe by DMA at once, and the following
+ * tbgpu_commit of the same body (same pointer and length) only waits for the copy.  Completes
+ * immediately (the reference allows the callback inside the call, src/lsm/groove.zig:723-742). */
+int tbgpu_prefetch(tbgpu_t* engine, uint8_t operation, const void* input, uint32_t input_len);
 
 /* N consecutive prepares of the same create operation, pass_batches_max prepares per device pass
  * (tbgpu_commit_pipelined with chunk_batches = 0); identical results to N sequential tbgpu_commit

@@ -114,6 +114,7 @@ SIGNATURES = [
     ("tbgpu_deinit", None, [_P]),
     ("tbgpu_reset", ctypes.c_int, [_P]),
     ("tbgpu_commit", ctypes.c_int, [_P, _U8, _U64, _P, _U32, _P, _U32, ctypes.POINTER(_U32)]),
+    ("tbgpu_prefetch", ctypes.c_int, [_P, _U8, _P, _U32]),
     ("tbgpu_commit_many", ctypes.c_int, [_P, _U8, _U32, ctypes.POINTER(_U64), ctypes.POINTER(_P),
                                          ctypes.POINTER(_U32), ctypes.POINTER(_P), ctypes.POINTER(_U32)]),
     ("tbgpu_commit_pipelined", ctypes.c_int, [_P, _U8, _U32, ctypes.POINTER(_U64), ctypes.POINTER(_P),

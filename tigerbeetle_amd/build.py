@@ -66,9 +66,30 @@ def build_host(force=False, verbose=True):
     return RUNNER
 
 
+REPLICA_BENCH = os.path.join(HOST, "tb_replica_bench")
+
+
+def build_replica_bench(force=False, verbose=True):
+    """tb_replica_bench: the replica's call path (prepare -> prefetch -> commit -> compact) through the
+    C++ mirror, for bench.py's replica_path leg."""
+    srcs = [os.path.join(HOST, f) for f in ("state_machine.cpp", "replica_bench.cpp")]
+    deps = srcs + [os.path.join(HOST, "state_machine.hpp"), os.path.join(ROOT, "include", "tbgpu.h"),
+                   os.path.join(ROOT, "include", "tbgpu_bench.h"), LIB]
+    if not force and not _stale(REPLICA_BENCH, deps):
+        return REPLICA_BENCH
+    cmd = [CXX, "-O2", "-std=c++17", "-Wall", "-Wextra", "-o", REPLICA_BENCH + ".tmp"] + srcs + [
+        "-L" + PKG_DIR, "-ltbgpu", "-Wl,-rpath,$ORIGIN/.."]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(REPLICA_BENCH + ".tmp", REPLICA_BENCH)
+    return REPLICA_BENCH
+
+
 def build(force=False, verbose=True):
     lib = build_engine(force=force, verbose=verbose)
     build_host(force=force, verbose=verbose)
+    build_replica_bench(force=force, verbose=verbose)
     return lib
 
 

@@ -137,6 +137,12 @@ struct tbgpu {
     u8* lookup_out = nullptr;
     u8* lookup_found = nullptr;
     u32 lookup_cap = 0;
+    // tbgpu_prefetch: the body of the prepare about to be committed, staged in HBM by DMA.
+    u8* pf_staging = nullptr;     // BATCH_EVENTS_MAX events
+    hipEvent_t pf_done = nullptr; // on copy_stream: the staging copy landed
+    const void* pf_input = nullptr;
+    u32 pf_len = 0;
+    u8 pf_op = 0;
     u32* d_status = nullptr;
 
     u32 epoch = 0;
@@ -516,6 +522,8 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     INIT_CK(hipMalloc(&E->lookup_out, (u64)E->lookup_cap * 128));
     INIT_CK(hipMalloc(&E->lookup_found, E->lookup_cap));
     INIT_CK(hipMalloc(&E->d_status, 16));
+    INIT_CK(hipMalloc(&E->pf_staging, (u64)BATCH_EVENTS_MAX * 128));
+    INIT_CK(hipEventCreateWithFlags(&E->pf_done, hipEventDisableTiming));
     for (int i = 0; i < 16; i++) INIT_CK(hipEventCreate(&E->markers[i]));
 #undef INIT_CK
     st = engine_clear(E);
@@ -541,7 +549,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->T.xposted, E->g, E->info, E->eflags, E->dr,
                     E->cr, E->ps, E->rs, E->dep_list, E->dep_count, E->amt, E->kid, E->kpid, E->dedup,
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
-                    E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->r_home,
+                    E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->pf_staging, E->r_home,
                     E->r_block_counts, E->r_words, E->r_meta, E->leg_ev, E->leg_w, E->leg_off, E->leg_tot,
                     E->F.f_pe, E->F.f_batch, E->F.f_len, E->F.need, E->F.nsucc, E->F.queue, E->F.uflags, E->F.nacct, E->F.rpos, E->F.succ,
                     E->F.run, E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo,
@@ -563,6 +571,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
     if (E->h_results) (void)hipHostFree(E->h_results);
     if (E->h_rmeta) (void)hipHostFree(E->h_rmeta);
     for (hipEvent_t e : E->event_pool) (void)hipEventDestroy(e);
+    if (E->pf_done) (void)hipEventDestroy(E->pf_done);
     for (int i = 0; i < 16; i++) if (E->markers[i]) (void)hipEventDestroy(E->markers[i]);
     if (E->stream) (void)hipStreamDestroy(E->stream);
     delete E;
@@ -598,7 +607,7 @@ static int engine_sync(tbgpu* E) {
 static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* events_dev, u32* results_dev,
                         u32* reply_bytes_dev, bool routed = false, u8* codes = nullptr, u32 cert_ext = 0,
                         const u8* events_src = nullptr, const u64* d_meta = nullptr,
-                        const OwnerLegArgs* owner = nullptr) {
+                        const OwnerLegArgs* owner = nullptr, const u64* inline_meta = nullptr) {
     const u64* d_off = d_meta ? d_meta : E->meta;
     const u64* d_ts = d_off + (nb + 1);
     u32 b0 = 0;
@@ -674,8 +683,11 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         // thread per step), or the whole set when forced.
         const u64 clear_n = E->dedup_force ? E->dedup_cap : E->dedup_prev;
         const u32 clear_grid = (u32)std::min<u64>(1024, std::max<u64>(1, clear_n / 2048));
+        // inline_meta: a one-prepare call's metadata, written into E->meta by this first kernel.
+        u64* meta_dst = inline_meta && b0 == 0 ? (u64*)d_off : nullptr;
         hipLaunchKernelGGL(tb_pass_clear, dim3(clear_grid), dim3(256), 0, E->stream, E->dedup, E->dedup_cap, E->sum_shards,
-                           E->g, E->epoch, E->dedup_force ? 1u : 0u, E->leg_tot, E->leg_buckets);
+                           E->g, E->epoch, E->dedup_force ? 1u : 0u, E->leg_tot, E->leg_buckets, meta_dst,
+                           inline_meta ? inline_meta[0] : 0, inline_meta ? inline_meta[1] : 0, inline_meta ? inline_meta[2] : 0);
         HIPCK(hipGetLastError());
         E->dedup_force = false;
         E->dedup_prev = P.dedup_mask + 1;
@@ -725,6 +737,9 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
             u32 seq_cap = E->undo_cap;
             FlowArgs F = E->F;
             F.grid = flow_grid(E);
+            // A small pass (the replica's one-prepare commit) has at most n dependent events: a grid
+            // of one workgroup per 512 of them holds every unit and launches faster.
+            if (n <= 65536) F.grid = std::min<u32>(F.grid, std::max<u32>(4, (u32)((n + 511) / 512)));
             hipLaunchKernelGGL(tb_flow, dim3(F.grid), dim3(FLOW_THREADS), 0, E->stream, P, F, seq_undo, seq_cap);
         } else if (op == OP_CREATE_TRANSFERS) {
             hipLaunchKernelGGL(tb_replay<OP_CREATE_TRANSFERS>, dim3(1), dim3(REPLAY_THREADS), 0, E->stream, P,
@@ -751,7 +766,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
 // Host-side checks of the commit asserts (state_machine.zig:518-519, :645, :739, :780) and
 // upload of the call metadata.
 static int prepare_call(tbgpu* E, u8 op, u32 nb, const u64* timestamps, const u32* lens, u64 floor_ts,
-                        u64* total_events) {
+                        u64* total_events, bool upload = true) {
     if (op != OP_CREATE_ACCOUNTS && op != OP_CREATE_TRANSFERS) {
         return fail(TBGPU_STATUS_INVALID, "operation %u is not a create operation", op);
     }
@@ -784,7 +799,7 @@ static int prepare_call(tbgpu* E, u8 op, u32 nb, const u64* timestamps, const u3
         return fail(TBGPU_STATUS_INVALID, "transfer log full (%llu + %llu events > capacity %llu)",
                     (unsigned long long)E->log_next, (unsigned long long)h_off[nb], (unsigned long long)E->xlog_cap);
     }
-    HIPCK(hipMemcpyAsync(E->meta, E->h_meta, (2 * (u64)nb + 1) * 8, hipMemcpyHostToDevice, E->stream));
+    if (upload) HIPCK(hipMemcpyAsync(E->meta, E->h_meta, (2 * (u64)nb + 1) * 8, hipMemcpyHostToDevice, E->stream));
     E->last_batch_ts = prev;
     *total_events = h_off[nb];
     return TBGPU_STATUS_OK;
@@ -841,30 +856,59 @@ static int commit_host(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const
         while (k1 < n && k1 - k0 < E->meta_cap && ev + lens[k1] <= E->pe_max) ev += lens[k1++];
         if (k1 == k0) return fail(TBGPU_STATUS_INVALID, "batch larger than pass_events_max");
         u64 total = 0;
-        int st = prepare_call(E, op, k1 - k0, timestamps + k0, lens.data() + k0, E->commit_ts, &total);
+        const bool one = k1 - k0 == 1;
+        // One prepare (the replica's commit): its metadata rides on the first kernel's arguments
+        // and its reply comes back through the mapped reply arena — no copy on either side.
+        int st = prepare_call(E, op, k1 - k0, timestamps + k0, lens.data() + k0, E->commit_ts, &total, !one);
         if (st) return st;
-        // One prepare in registered memory (the replica's commit): kernel 1 reads it over PCIe and
-        // writes it through to staging — no copy ahead of the kernels.  Otherwise a DMA per input.
+        const u64 inline_meta[3] = {0, lens[k0], timestamps[k0]};
+        // Its body: staged by tbgpu_prefetch (in HBM once the copy lands), or read through by kernel
+        // 1 from registered memory (written through to staging), or copied here.
         const u8* src = nullptr;
-        if (k1 - k0 == 1 && lens[k0]) {
+        const u8* events = E->staging;
+        if (one && lens[k0] && E->pf_input == inputs[k0] && E->pf_len == lens[k0] * 128 && E->pf_op == op) {
+            if (hipEventQuery(E->pf_done) != hipSuccess) HIPCK(hipStreamWaitEvent(E->stream, E->pf_done, 0));
+            events = E->pf_staging;
+        } else if (one && lens[k0]) {
             const u8* in = (const u8*)inputs[k0];
             for (const auto& r : E->host_regions) {
                 if (in >= r.ptr && in + (u64)lens[k0] * 128 <= r.ptr + r.bytes) src = r.dev + (in - r.ptr);
             }
         }
+        E->pf_input = nullptr;
         u64 off = 0;
-        for (u32 k = k0; k < k1 && !src; k++) {
+        for (u32 k = k0; k < k1 && !src && events == E->staging; k++) {
             if (lens[k]) HIPCK(hipMemcpyAsync(E->staging + off * 128, inputs[k], (u64)lens[k] * 128,
                                               hipMemcpyHostToDevice, E->stream));
             off += lens[k];
         }
         std::vector<u64> h_off(E->h_meta, E->h_meta + (k1 - k0) + 1);
-        if ((st = enqueue_call(E, op, k1 - k0, h_off.data(), E->staging, E->results, E->reply_bytes, false, nullptr, 0,
-                               src))) {
+        if ((st = enqueue_call(E, op, k1 - k0, h_off.data(), events, E->results, E->reply_bytes, false, nullptr, 0,
+                               src, nullptr, nullptr, one ? inline_meta : nullptr))) {
             return st;
         }
-        // Reply sizes and (for calls of up to h_results_events events: every prepare the replica
-        // commits) the result slots come back on the stream with the globals: one round trip.
+        if (one) {
+            tbgpu::PipeSlot& S = E->pipe[0];
+            hipLaunchKernelGGL(tb_reply_out, dim3(1), dim3(64), 0, E->stream, E->meta, 1u, E->reply_bytes, E->results, E->g,
+                               S.d_reply);
+            HIPCK(hipGetLastError());
+            HIPCK(hipStreamSynchronize(E->stream));
+            E->pending = false;
+            if ((st = prof_collect(E))) return st;
+            const u64* head = (const u64*)S.h_reply;
+            const u32 bytes = *(const u32*)(S.h_reply + 16);
+            E->commit_ts = head[1];
+            if (head[0]) {
+                return fail(TBGPU_STATUS_PANIC, "device panic 0x%llx (the reference would have trapped)",
+                            (unsigned long long)head[0]);
+            }
+            if (bytes) memcpy(outputs[k0], S.h_reply + 16 + 4, bytes);
+            out_lens[k0] = bytes;
+            k0 = k1;
+            continue;
+        }
+        // Reply sizes and (for calls of up to h_results_events events) the result slots come back on
+        // the stream with the globals: one round trip.
         const u32* rb = E->h_rb;
         HIPCK(hipMemcpyAsync(E->h_rb, E->reply_bytes, (u64)(k1 - k0) * 4, hipMemcpyDeviceToHost, E->stream));
         const bool whole = total <= E->h_results_events;
@@ -1058,6 +1102,32 @@ extern "C" int tbgpu_commit(tbgpu_t* E, uint8_t operation, uint64_t timestamp, c
     const void* ins[1] = {input};
     void* outs[1] = {output};
     return commit_host(E, operation, 1, &timestamp, ins, &input_len, outs, out_len, &output_cap);
+}
+
+// StateMachine.prefetch (src/state_machine.zig:345-506): every object is HBM-resident, so what is
+// left to stage is the prepare body itself — a create body in registered host memory (the message
+// pool) starts crossing PCIe by DMA now, on the copy stream, and the commit of the same body only
+// waits for it.  Anything else needs no staging.
+extern "C" int tbgpu_prefetch(tbgpu_t* E, uint8_t operation, const void* input, uint32_t input_len) {
+    if (E->node) return TBGPU_STATUS_OK;
+    HIPCK(hipSetDevice(E->device));
+    E->pf_input = nullptr;
+    if ((operation != OP_CREATE_ACCOUNTS && operation != OP_CREATE_TRANSFERS) || input_len == 0 ||
+        input_len % 128 != 0 || input_len / 128 > BATCH_EVENTS_MAX) {
+        return TBGPU_STATUS_OK;
+    }
+    bool registered = false;
+    for (const auto& r : E->host_regions) {
+        if ((const u8*)input >= r.ptr && (const u8*)input + input_len <= r.ptr + r.bytes) registered = true;
+    }
+    if (!registered) return TBGPU_STATUS_OK;  // pageable: commit copies it (a DMA needs pinned pages)
+    // The staging slot's previous reader (the last commit) has finished: commits are synchronous.
+    HIPCK(hipMemcpyAsync(E->pf_staging, input, input_len, hipMemcpyHostToDevice, E->copy_stream));
+    HIPCK(hipEventRecord(E->pf_done, E->copy_stream));
+    E->pf_input = input;
+    E->pf_len = input_len;
+    E->pf_op = operation;
+    return TBGPU_STATUS_OK;
 }
 
 extern "C" int tbgpu_commit_many(tbgpu_t* E, uint8_t operation, uint32_t n, const uint64_t* timestamps,

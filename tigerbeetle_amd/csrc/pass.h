@@ -245,9 +245,17 @@ __device__ static inline void tb_dedup_mark(const PassArgs& P) {
 
 // Before kernel 1 of pass `epoch`: zero the S shards and pass words, and the dedup entries the
 // previous pass may have written (all `cap` entries when `force`).
+// meta (optional): a one-prepare call's metadata {offset 0, offset 1, timestamp}, carried here as
+// kernel arguments instead of a copy ahead of the pass (the replica's one-prepare commits).
 __global__ __launch_bounds__(256) void tb_pass_clear(u64* dedup, u64 cap, u64* sum_shards, const Globals* g, u32 epoch,
-                                                     u32 force, u32* leg_tot, u32 leg_buckets) {
+                                                     u32 force, u32* leg_tot, u32 leg_buckets, u64* meta, u64 m0, u64 m1,
+                                                     u64 m2) {
     if (blockIdx.x == 0 && threadIdx.x < SUM_WORDS) sum_shards[threadIdx.x] = 0;
+    if (meta && blockIdx.x == 0 && threadIdx.x == 0) {
+        meta[0] = m0;
+        meta[1] = m1;
+        meta[2] = m2;
+    }
     if (blockIdx.x == 0 && leg_tot) {
         for (u32 k = threadIdx.x; k <= leg_buckets; k += 256) leg_tot[k] = 0;
     }

@@ -68,7 +68,12 @@ StateMachine::StateMachine(const Options& o) {
     }
 }
 
-StateMachine::~StateMachine() { tbgpu_deinit(engine_); }
+StateMachine::~StateMachine() {
+    for (std::vector<uint8_t>* b : {&wb_accounts_, &wb_before_, &wb_transfers_, &wb_posted_}) {
+        if (!b->empty()) tbgpu_unregister_host(engine_, b->data());
+    }
+    tbgpu_deinit(engine_);
+}
 
 void StateMachine::reset() {
     check(tbgpu_reset(engine_), "reset");
@@ -88,11 +93,23 @@ void StateMachine::prepare(Operation operation, const void* input, size_t input_
 
 void StateMachine::prefetch(const Callback& callback, uint64_t op, Operation operation, const void* input,
                             size_t input_len) {
-    (void)operation, (void)input, (void)input_len;
     if (op == 0) throw Panic("prefetch: op == 0");
-    // Every object is HBM-resident: the prefetch completes at once (the reference allows the
-    // callback to fire inside the call, src/lsm/groove.zig:723-742).
+    // Every object is HBM-resident; the body starts crossing PCIe now (tbgpu_prefetch: a DMA from a
+    // registered message) and the prefetch completes at once (the reference allows the callback to
+    // fire inside the call, src/lsm/groove.zig:723-742).
+    if (stage_bodies) {
+        check(tbgpu_prefetch(engine_, static_cast<uint8_t>(operation), input, static_cast<uint32_t>(input_len)),
+              "prefetch");
+    }
     callback(*this);
+}
+
+void StateMachine::register_message_buffer(void* buffer, size_t bytes) {
+    check(tbgpu_register_host(engine_, buffer, bytes), "register_message_buffer");
+}
+
+void StateMachine::unregister_message_buffer(void* buffer) {
+    check(tbgpu_unregister_host(engine_, buffer), "unregister_message_buffer");
 }
 
 size_t StateMachine::commit(u128 client, uint64_t op, uint64_t timestamp, Operation operation, const void* input,
@@ -126,41 +143,54 @@ std::vector<size_t> StateMachine::commit_many(Operation operation, const std::ve
 }
 
 void StateMachine::compact(const Callback& callback, uint64_t op) {
-    (void)op;
-    // The HBM tables need no compaction; the forest write-back happens at checkpoint().
+    // The HBM tables need no compaction; the durable copy gets the bar's changes at its last op.
+    if (write_back && lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0) write_back(checkpoint_delta());
     callback(*this);
 }
 
-Delta StateMachine::checkpoint_delta() {
-    Delta d;
-    tbgpu_delta_counts counts{1024, 1024, 1024, 0};
+// The write-back buffers are the state machine's own, allocated and registered once (grown when a
+// delta needs more room: static allocation in the steady state), so the delta lands by DMA.
+static void grow_registered(tbgpu_t* engine, std::vector<uint8_t>& buf, size_t bytes) {
+    if (buf.size() >= bytes) return;
+    if (!buf.empty()) tbgpu_unregister_host(engine, buf.data());
+    std::vector<uint8_t>(bytes).swap(buf);
+    if (tbgpu_register_host(engine, buf.data(), buf.size()) != TBGPU_STATUS_OK) {
+        throw DeviceError(std::string("register write-back buffer: ") + tbgpu_last_error());
+    }
+}
+
+const Delta& StateMachine::checkpoint_delta() {
+    tbgpu_delta_counts counts{wb_caps_[0], wb_caps_[1], wb_caps_[2], 0};
     for (;;) {
-        d.accounts.resize(counts.accounts * 128);
-        d.accounts_before.resize(counts.accounts * 64);
-        d.transfers.resize(counts.transfers * 128);
-        d.posted.resize(counts.posted * 2);
-        const uint64_t caps[3] = {counts.accounts, counts.transfers, counts.posted};
-        const int st = tbgpu_checkpoint_delta(engine_, d.accounts.data(), d.accounts_before.data(), caps[0],
-                                              d.transfers.data(), caps[1], d.posted.data(), caps[2], &counts);
+        wb_caps_[0] = std::max<uint64_t>(wb_caps_[0], counts.accounts);
+        wb_caps_[1] = std::max<uint64_t>(wb_caps_[1], counts.transfers);
+        wb_caps_[2] = std::max<uint64_t>(wb_caps_[2], counts.posted);
+        grow_registered(engine_, wb_accounts_, wb_caps_[0] * 128);
+        grow_registered(engine_, wb_before_, wb_caps_[0] * 64);
+        grow_registered(engine_, wb_transfers_, wb_caps_[1] * 128);
+        grow_registered(engine_, wb_posted_, wb_caps_[2] * 16);
+        const int st = tbgpu_checkpoint_delta(engine_, wb_accounts_.data(), wb_before_.data(), wb_caps_[0],
+                                              wb_transfers_.data(), wb_caps_[1], (uint64_t*)wb_posted_.data(),
+                                              wb_caps_[2], &counts);
         if (st == TBGPU_STATUS_INVALID &&
-            (counts.accounts > caps[0] || counts.transfers > caps[1] || counts.posted > caps[2])) {
-            counts.accounts = std::max(counts.accounts, caps[0]);
-            counts.transfers = std::max(counts.transfers, caps[1]);
-            counts.posted = std::max(counts.posted, caps[2]);
+            (counts.accounts > wb_caps_[0] || counts.transfers > wb_caps_[1] || counts.posted > wb_caps_[2])) {
             continue;  // room for everything, then retry (nothing advanced)
         }
         check(st, "checkpoint_delta");
-        d.accounts.resize(counts.accounts * 128);
-        d.accounts_before.resize(counts.accounts * 64);
-        d.transfers.resize(counts.transfers * 128);
-        d.posted.resize(counts.posted * 2);
-        d.created_after = counts.created_after;
-        return d;
+        delta_.accounts = wb_accounts_.data();
+        delta_.accounts_before = wb_before_.data();
+        delta_.account_count = counts.accounts;
+        delta_.transfers = wb_transfers_.data();
+        delta_.transfer_count = counts.transfers;
+        delta_.posted = (const uint64_t*)wb_posted_.data();
+        delta_.posted_count = counts.posted;
+        delta_.created_after = counts.created_after;
+        return delta_;
     }
 }
 
 void StateMachine::checkpoint(const Callback& callback) {
-    const Delta d = checkpoint_delta();
+    const Delta& d = checkpoint_delta();
     if (write_back) write_back(d);
     callback(*this);
 }

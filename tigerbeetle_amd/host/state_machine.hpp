@@ -143,14 +143,19 @@ struct DeviceError : std::runtime_error {
 };
 
 // One groove write-back (tbgpu_checkpoint_delta): what checkpoint() hands to the durable
-// replica's forest — accounts (128-B records, in no particular order), transfers (by timestamp), posted pairs
-// {pending timestamp, fulfillment} (by timestamp).
+// replica's forest — accounts (128-B records, in no particular order, each with its 64-B balances as
+// of the previous write-back), transfers (128-B records, by timestamp), posted pairs {pending
+// timestamp, fulfillment} (by timestamp).  Views of the state machine's registered write-back
+// buffers: valid until the next write-back.
 struct Delta {
-    std::vector<uint8_t> accounts;
-    std::vector<uint8_t> accounts_before;  // 64 B per account: balances as of the previous write-back
-    uint64_t created_after = 0;            // accounts with a later timestamp are new (insert)
-    std::vector<uint8_t> transfers;
-    std::vector<uint64_t> posted;
+    const uint8_t* accounts = nullptr;
+    const uint8_t* accounts_before = nullptr;
+    uint64_t account_count = 0;
+    uint64_t created_after = 0;  // accounts with a later timestamp are new (insert)
+    const uint8_t* transfers = nullptr;
+    uint64_t transfer_count = 0;
+    const uint64_t* posted = nullptr;
+    uint64_t posted_count = 0;
 };
 
 class StateMachine {
@@ -175,11 +180,24 @@ public:
     std::vector<size_t> commit_many(Operation operation, const std::vector<uint64_t>& timestamps,
                                     const std::vector<const void*>& inputs, const std::vector<size_t>& input_lens,
                                     const std::vector<void*>& outputs);
+    // Writes the engine's changes back (checkpoint_delta -> write_back, when set) at the last op of
+    // every bar (config.zig:143 lsm_batch_multiple = 64), as the Zig wrapper does before
+    // forest.compact; then calls back.
     void compact(const Callback& callback, uint64_t op);
+    // The replica's message pool (MessagePool.init_capacity, src/message_pool.zig:98-120): buffers
+    // registered once, so prefetch stages a prepare body from its message by DMA.
+    void register_message_buffer(void* buffer, size_t bytes);
+    void unregister_message_buffer(void* buffer);
+    uint32_t lsm_batch_multiple = 64;
+    // prefetch stages a registered body by DMA (tbgpu_prefetch) — worth it when the replica has work
+    // between prefetch and commit (its client-replies stage, src/vsr/replica.zig:3060); off (the
+    // default): commit's first kernel reads the body straight from the registered message, which
+    // is faster when commit follows prefetch at once (tb_replica_bench: 0.092 vs 0.115 ms per op).
+    bool stage_bodies = false;
     // Hands the objects changed since the previous checkpoint to `write_back` (if set), then calls
     // back (state_machine.zig:565-582).
     void checkpoint(const Callback& callback);
-    Delta checkpoint_delta();
+    const Delta& checkpoint_delta();
     WriteBack write_back;
 
     // Test-only: the table harness `setup` action (state_machine.zig:1398-1407).
@@ -194,6 +212,9 @@ public:
 private:
     void check(int status, const char* what) const;
     tbgpu_t* engine_ = nullptr;
+    Delta delta_;
+    uint64_t wb_caps_[3] = {1024, 1024, 1024};
+    std::vector<uint8_t> wb_accounts_, wb_before_, wb_transfers_, wb_posted_;
 };
 
 }  // namespace tb
