@@ -41,6 +41,8 @@ const tb = @import("tigerbeetle.zig");
 const Account = tb.Account;
 const Transfer = tb.Transfer;
 const GridType = @import("vsr/grid.zig").GridType;
+const Header = @import("vsr.zig").Header;
+const messages_max_replica = @import("message_pool.zig").messages_max_replica;
 const ReferenceStateMachineType = @import("state_machine.zig").StateMachineType;
 
 pub fn StateMachineType(
@@ -79,6 +81,12 @@ pub fn StateMachineType(
             engine_accounts_max: u64 = 1 << 26,
             engine_transfers_max: u64 = 1 << 30,
             engine_device: i32 = 0,
+            /// Two or more devices: one node engine with a shard per device (tbgpu_config.devices).
+            engine_devices: []const i32 = &.{},
+            /// prefetch starts the prepare body's DMA (tbgpu_prefetch) — worth it when the replica
+            /// has work between prefetch and commit; otherwise commit's first kernel reads the body
+            /// straight from its registered message (DESIGN.md §5b).
+            engine_stage_bodies: bool = false,
 
             fn base(options: Options) Base.Options {
                 return .{
@@ -125,6 +133,11 @@ pub fn StateMachineType(
         prefetch_callback: ?*const fn (*StateMachine) void = null,
         prefetch_context: PrefetchContext = undefined,
 
+        engine_stage_bodies: bool,
+        /// Message buffers registered with the engine, keyed by address (at most the pool's
+        /// messages_max_replica, all allocated once by MessagePool.init_capacity).
+        registered_messages: std.AutoHashMapUnmanaged(usize, void),
+
         open_callback: ?*const fn (*StateMachine) void = null,
         compact_callback: ?*const fn (*StateMachine) void = null,
         checkpoint_callback: ?*const fn (*StateMachine) void = null,
@@ -142,14 +155,17 @@ pub fn StateMachineType(
             var forest = try Forest.init(allocator, grid, options.lsm_forest_node_count, forest_options(options));
             errdefer forest.deinit(allocator);
 
-            const engine_config = tbgpu.tbgpu_config{
-                .accounts_max = options.engine_accounts_max,
-                .transfers_max = options.engine_transfers_max,
-                .pass_events_max = constants.batch_max.create_transfers,
-                .pass_batches_max = 1,
-                .device = options.engine_device,
-                .flags = 0,
-            };
+            var engine_config = mem.zeroes(tbgpu.tbgpu_config);
+            engine_config.accounts_max = options.engine_accounts_max;
+            engine_config.transfers_max = options.engine_transfers_max;
+            engine_config.pass_events_max = constants.batch_max.create_transfers;
+            engine_config.pass_batches_max = 1;
+            engine_config.device = options.engine_device;
+            if (options.engine_devices.len >= 2) {
+                assert(options.engine_devices.len <= tbgpu.TBGPU_DEVICES_MAX);
+                engine_config.device_count = @intCast(options.engine_devices.len);
+                for (options.engine_devices, 0..) |d, i| engine_config.devices[i] = d;
+            }
             var engine: ?*tbgpu.tbgpu_t = null;
             if (tbgpu.tbgpu_init(&engine_config, &engine) != tbgpu.TBGPU_STATUS_OK) return error.EngineInit;
             errdefer tbgpu.tbgpu_deinit(engine);
@@ -168,6 +184,17 @@ pub fn StateMachineType(
             errdefer allocator.free(load_transfers);
             const load_posted = try allocator.alloc(u8, prepare_transfers_max);
             errdefer allocator.free(load_posted);
+            var registered_messages: std.AutoHashMapUnmanaged(usize, void) = .{};
+            try registered_messages.ensureTotalCapacity(allocator, messages_max_replica);
+            errdefer registered_messages.deinit(allocator);
+
+            // The write-back buffers receive each bar's delta by DMA (registered once).
+            inline for (.{ writeback_accounts, writeback_accounts_before, writeback_transfers, writeback_posted }) |buffer| {
+                const bytes = mem.sliceAsBytes(buffer);
+                if (tbgpu.tbgpu_register_host(engine.?, @constCast(bytes.ptr), bytes.len) != tbgpu.TBGPU_STATUS_OK) {
+                    return error.EngineInit;
+                }
+            }
 
             return StateMachine{
                 .prepare_timestamp = 0,
@@ -181,10 +208,18 @@ pub fn StateMachineType(
                 .load_accounts = load_accounts,
                 .load_transfers = load_transfers,
                 .load_posted = load_posted,
+                .engine_stage_bodies = options.engine_stage_bodies,
+                .registered_messages = registered_messages,
             };
         }
 
         pub fn deinit(self: *StateMachine, allocator: mem.Allocator) void {
+            var it = self.registered_messages.keyIterator();
+            while (it.next()) |address| check(tbgpu.tbgpu_unregister_host(self.engine, @ptrFromInt(address.*)));
+            self.registered_messages.deinit(allocator);
+            inline for (.{ self.writeback_accounts, self.writeback_accounts_before, self.writeback_transfers, self.writeback_posted }) |buffer| {
+                check(tbgpu.tbgpu_unregister_host(self.engine, mem.sliceAsBytes(buffer).ptr));
+            }
             allocator.free(self.load_posted);
             allocator.free(self.load_transfers);
             allocator.free(self.load_accounts);
@@ -258,7 +293,13 @@ pub fn StateMachineType(
             _ = op;
             assert(self.prefetch_input == null);
             assert(self.prefetch_callback == null);
-            if (self.engine_complete) return callback(self);
+            if (self.engine_complete) {
+                if (self.engine_stage_bodies and (operation == .create_accounts or operation == .create_transfers)) {
+                    self.register_message(input);
+                    check(tbgpu.tbgpu_prefetch(self.engine, @intFromEnum(operation), input.ptr, @intCast(input.len)));
+                }
+                return callback(self);
+            }
 
             self.prefetch_input = input;
             self.prefetch_operation = operation;
@@ -415,6 +456,7 @@ pub fn StateMachineType(
                 check(tbgpu.tbgpu_set_commit_timestamp(self.engine, self.commit_timestamp));
                 self.engine_commit_timestamp = self.commit_timestamp;
             }
+            self.register_message(input);
             var out_len: u32 = 0;
             check(tbgpu.tbgpu_commit(
                 self.engine,
@@ -429,6 +471,20 @@ pub fn StateMachineType(
             self.commit_timestamp = tbgpu.tbgpu_commit_timestamp(self.engine);
             self.engine_commit_timestamp = self.commit_timestamp;
             return out_len;
+        }
+
+        /// A prepare body lives in a message buffer of the replica's pool, right after its header
+        /// (MessagePool.init_capacity allocates each buffer once, sector-aligned, message_size_max
+        /// bytes: src/message_pool.zig:98-120).  The first commit from a buffer registers it with the
+        /// engine, so every later body from it reaches the GPU by direct read, with no staging copy.
+        /// A body elsewhere (not right after a sector-aligned header) is left pageable.
+        fn register_message(self: *StateMachine, input: []align(16) const u8) void {
+            const address = @intFromPtr(input.ptr) -| @sizeOf(Header);
+            if (address % global_constants.sector_size != 0) return;
+            if (self.registered_messages.contains(address)) return;
+            if (self.registered_messages.count() == messages_max_replica) return;
+            check(tbgpu.tbgpu_register_host(self.engine, @ptrFromInt(address), global_constants.message_size_max));
+            self.registered_messages.putAssumeCapacity(address, {});
         }
 
         pub fn compact(self: *StateMachine, callback: *const fn (*StateMachine) void, op: u64) void {
