@@ -56,7 +56,7 @@ PCIE_MEASURED_GBS = 57.3
 # 128: its ordered run costs about (DAG depth x unit latency) per chunk whatever the chunk's size, so
 # larger chunks amortise it (10M C4 transfers: 282M/s at 64, 352M/s at 128, 351M/s at 256, with
 # p99 submit-to-reply 5.4 / 7.0 / 9.8 ms; tools/gpu/chunks.sh).
-CHUNK_PREPARES = {"c2": 64, "c3": 64, "c4": 128}
+CHUNK_PREPARES = {"c2": 64, "c3": 64, "c3h": 64, "c4": 128}
 
 
 def parse():
@@ -77,7 +77,7 @@ def parse():
                    help="transfers of the C3 / C4 secondary lines (0: skip)")
     p.add_argument("--cpu-sample", type=int, default=12_285_000, help="transfers in the CPU baseline / parity sample (0: skip)")
     p.add_argument("--seed", type=int, default=42)
-    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"],
+    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c3h", "c4"],
                    help="BASELINE.json shape: c2 (headline, default), c3 Zipf + limit accounts, c4 chains + two-phase")
     p.add_argument("--profile", type=int, default=1, help="time kernels with HIP events (roofline)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (rehearsal on one GPU)")
@@ -240,7 +240,9 @@ def run_cpu_baseline(engine, args, acct_lens, acct_ts, events_dev, sample_lens, 
 
     n_acct = args.accounts
     acct_dev = engine.alloc(n_acct * 128)
-    engine.generate_accounts(acct_dev, 0, n_acct, seed=args.seed, limit_permille=SETTINGS[args.workload]["limit_permille"])
+    wl = SETTINGS[args.workload]
+    engine.generate_accounts(acct_dev, 0, n_acct, seed=args.seed, limit_permille=wl["limit_permille"],
+                             account_count=n_acct, hot_limited=wl.get("hot_limited", 0))
     acct_events = engine.to_host(acct_dev, n_acct * 128)
     engine.free(acct_dev)
     n_sample = sum(sample_lens)
@@ -352,7 +354,9 @@ def run_secondary(args, kind, device):
             "flow": {k: (round(stats[k], 3) if isinstance(stats[k], float) else stats[k])
                      for k in ("flow_units", "flow_runs", "flow_plan_ms", "flow_run_ms", "bounds_passes", "bounds_units",
                                "bounds_rounds", "bounds_skipped", "bounds_abandoned", "bounds_swept", "sweep_ms",
-                               "sweep_loop_ms", "sweep_wait_ms")},
+                               "sweep_loop_ms", "sweep_wait_ms", "walk_segments", "walk_heavy",
+                               "walk_heavy_positions", "walk_heavy_windows", "walk_heavy_stops", "walk_heavy_blocks",
+                               "walk_heavy_blocked_ms", "walk_longest")},
             "flow_phases_ms": flow_phases(stats),
             "roofline": roof, "parity": parity}
 
@@ -476,6 +480,9 @@ WORKLOAD_TEXT = {
     "c2": "C2 (BASELINE.json configs[1]): %d accounts, %d uniform transfers/GPU, no flags, prepares of %d",
     "c3": "C3 (BASELINE.json configs[2]): %d accounts (10%% debits_must_not_exceed_credits, funded by a bank "
           "account), %d transfers with Zipf(1.2) dr/cr, prepares of %d",
+    "c3h": "C3, adversarial (BASELINE.json configs[2] with the hottest Zipf rank limited too): %d accounts (10%% "
+           "debits_must_not_exceed_credits plus the hottest account, funded by a bank account), %d transfers with "
+           "Zipf(1.2) dr/cr, prepares of %d",
     "c4": "C4 (BASELINE.json configs[3]): %d accounts, %d transfers: ~20%% in linked chains (5%% chain-breaking), "
           "30%% pending with 0..10 s timeouts, 15%% post/void of earlier transfers, 0.5%% balancing, a 2 s "
           "timestamp gap every 64 prepares; prepares of %d",
@@ -575,7 +582,8 @@ def main():
     acct_lens = batches(args.accounts, args.batch)
     acct_ts, t_end = timestamps(acct_lens, 1_000_000_000)
     acct_dev = engine.alloc(args.accounts * 128)
-    engine.generate_accounts(acct_dev, 0, args.accounts, seed=seed, limit_permille=wl["limit_permille"])
+    engine.generate_accounts(acct_dev, 0, args.accounts, seed=seed, limit_permille=wl["limit_permille"],
+                             account_count=args.accounts, hot_limited=wl.get("hot_limited", 0))
     res_dev = engine.alloc(max(args.accounts, args.transfers) * 8)
     rb_dev = engine.alloc(max(len(acct_lens), args.transfers // args.batch + 2) * 4)
     engine.commit_device_async(128, acct_ts, acct_lens, acct_dev, res_dev, rb_dev)
@@ -588,7 +596,7 @@ def main():
     xfer_lens = batches(args.transfers, args.batch)
     events_dev = engine.alloc(args.transfers * 128)
     engine.generate_transfers(events_dev, 0, args.transfers, args.accounts, seed=seed, kind=KINDS[args.workload],
-                              limit_permille=wl["limit_permille"])
+                              limit_permille=wl["limit_permille"], hot_limited=wl.get("hot_limited", 0))
     engine.sync()
 
     # -- headline: the replica's batched commit from host memory (PCIe both ways) --------------
@@ -629,7 +637,7 @@ def main():
     engine.unregister_host(host_events)
     del host_events
     write_back = None
-    if rank == 0 and world == 1 and args.write_back:
+    if rank == 0 and world == 1 and args.write_back and args.workload == "c2":
         at_full, t_cursor = run_write_back(engine, args, t_cursor)
         engine.reset_transfers()
         at_empty, t_cursor = run_write_back(engine, args, t_cursor)
@@ -757,7 +765,7 @@ def main():
         replica_path = run_replica_path(args, local_rank)
     secondary = {}
     if rank == 0 and world == 1 and args.workload == "c2" and args.secondary:
-        for kind in ("c3", "c4"):
+        for kind in ("c3", "c3h", "c4"):
             secondary[kind] = run_secondary(args, kind, local_rank)
 
     pass_lat = np.array(pass_lat) if len(pass_lat) else np.array([float("nan")])
@@ -789,7 +797,9 @@ def main():
         "flow": {k: (round(stats[k], 3) if isinstance(stats[k], float) else stats[k])
                  for k in ("flow_units", "flow_runs", "flow_run_units", "flow_plan_ms", "flow_run_ms", "bounds_passes",
                            "bounds_units", "bounds_rounds", "bounds_skipped", "bounds_abandoned", "bounds_swept",
-                           "sweep_ms", "sweep_loop_ms", "sweep_wait_ms", "flow_exec_ms")},
+                           "sweep_ms", "sweep_loop_ms", "sweep_wait_ms", "flow_exec_ms", "walk_segments",
+                           "walk_heavy", "walk_heavy_positions", "walk_heavy_windows", "walk_heavy_stops",
+                           "walk_heavy_blocks", "walk_heavy_blocked_ms", "walk_longest")},
         "flow_phases_ms": flow_phases(stats),
         "failed_events": n_failed,
         "roofline": roof,

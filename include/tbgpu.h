@@ -65,6 +65,9 @@ extern "C" {
  * converge, else the ordered run).  Identical results; for cross-checking the paths. */
 #define TBGPU_CONFIG_SWEEP_EARLY (1u << 2)
 #define TBGPU_CONFIG_SWEEP_OFF (1u << 3)
+/* The sweep as one wave walking the undecided checks in event order, 64 a window (round 2's form),
+ * instead of one walker per limit account.  Identical results; for cross-checking the two. */
+#define TBGPU_CONFIG_SWEEP_WINDOW (1u << 4)
 
 #define TBGPU_DEVICES_MAX 16u
 
@@ -224,6 +227,13 @@ typedef struct tbgpu_stats {
     double flow_exec_ms;         /* tb_flow run: time lanes spent executing units, summed over lanes */
     double flow_phase_ms[8];     /* tb_flow wall time by phase: plan, sort, link, bounds setup, bounds
                                     rounds, sweep, run (or applying the bounds), replies */
+    /* The sweep's per-account walkers (k_flow.h fl_walk): segments walked, heavy segments (a wave
+     * each); over the heavy walkers: positions, windows, stops at a partner's open unit, blocked
+     * returns, blocked ms (summed over walkers), and the longest segment (positions). */
+    uint64_t walk_segments, walk_heavy, walk_heavy_positions, walk_heavy_windows, walk_heavy_stops,
+        walk_heavy_blocks;
+    double walk_heavy_blocked_ms;
+    uint64_t walk_longest;
 } tbgpu_stats;
 
 int tbgpu_get_stats(tbgpu_t* engine, tbgpu_stats* stats);

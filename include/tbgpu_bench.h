@@ -23,6 +23,10 @@ typedef struct tbgpu_workload {
                                      timeouts, post/void of earlier transfers, balancing (C4) */
     uint32_t limit_permille;   /* accounts with debits_must_not_exceed_credits, per mille */
     double zipf_s;             /* kind 1: Zipf exponent (BASELINE C3: 1.2) */
+    uint32_t hot_limited;      /* kind 1: the hottest Zipf ranks [0, hot_limited) also get
+                                  debits_must_not_exceed_credits (the adversarial C3: a limit
+                                  account on the hot path); account generation needs account_count */
+    uint32_t reserved;
 } tbgpu_workload;
 
 /* Write `count` Account events for account indices [first, first+count) into device memory. */

@@ -17,6 +17,7 @@ CONFIG_PROFILE = 1
 CONFIG_SEQUENTIAL_FALLBACK = 2
 CONFIG_SWEEP_EARLY = 4
 CONFIG_SWEEP_OFF = 8
+CONFIG_SWEEP_WINDOW = 16
 
 
 class tbgpu_config(ctypes.Structure):
@@ -72,6 +73,14 @@ class tbgpu_stats(ctypes.Structure):
         ("sweep_u64_passes", ctypes.c_uint64),
         ("flow_exec_ms", ctypes.c_double),
         ("flow_phase_ms", ctypes.c_double * 8),
+        ("walk_segments", ctypes.c_uint64),
+        ("walk_heavy", ctypes.c_uint64),
+        ("walk_heavy_positions", ctypes.c_uint64),
+        ("walk_heavy_windows", ctypes.c_uint64),
+        ("walk_heavy_stops", ctypes.c_uint64),
+        ("walk_heavy_blocks", ctypes.c_uint64),
+        ("walk_heavy_blocked_ms", ctypes.c_double),
+        ("walk_longest", ctypes.c_uint64),
     ]
 
 
@@ -82,6 +91,8 @@ class tbgpu_workload(ctypes.Structure):
         ("kind", ctypes.c_uint32),
         ("limit_permille", ctypes.c_uint32),
         ("zipf_s", ctypes.c_double),
+        ("hot_limited", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
     ]
 
 

@@ -491,6 +491,8 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         INIT_CK(hipMalloc(&F.b_xy, pe * 16 * FLOW_RMAX));
         INIT_CK(hipMalloc(&F.b_ex, pe * 16 * FLOW_RMAX));
         INIT_CK(hipMalloc(&F.b_rec, pe * sizeof(SweepRec)));
+        INIT_CK(hipMalloc(&F.b_vw, pe * 4));
+        F.walk = (config->flags & TBGPU_CONFIG_SWEEP_WINDOW) ? 0u : 1u;
         F.bounds_rounds_max = FLOW_BOUNDS_ROUNDS_MAX;
         F.sweep_min = (config->flags & TBGPU_CONFIG_SWEEP_OFF) ? 0u
                       : (config->flags & TBGPU_CONFIG_SWEEP_EARLY) ? 0xFFFFFFFFu
@@ -554,7 +556,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->F.f_pe, E->F.f_batch, E->F.f_len, E->F.need, E->F.nsucc, E->F.queue, E->F.uflags, E->F.nacct, E->F.rpos, E->F.succ,
                     E->F.run, E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo,
                     E->F.b_st, E->F.b_vd, E->F.b_vc, E->F.b_amt, E->F.b_meta, E->F.b_blk,
-                    E->F.b_qd, E->F.b_qc, E->F.b_head, E->F.b_xy, E->F.b_ex, E->F.b_rec};
+                    E->F.b_qd, E->F.b_qc, E->F.b_head, E->F.b_xy, E->F.b_ex, E->F.b_rec, E->F.b_vw};
     for (void* p : bufs) if (p) (void)hipFree(p);
     for (int k = 0; k < PIPE_SLOTS; k++) {
         tbgpu::PipeSlot& S = E->pipe[k];
@@ -1685,6 +1687,14 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     s->sweep_u64_passes = g.sweep_u64_passes;
     s->flow_exec_ms = E->wall_khz ? (double)g.flow_exec_ticks / E->wall_khz : 0.0;
     for (int k = 0; k < 8; k++) s->flow_phase_ms[k] = E->wall_khz ? (double)g.flow_phase_ticks[k] / E->wall_khz : 0.0;
+    s->walk_segments = g.walk[0];
+    s->walk_heavy = g.walk[1];
+    s->walk_heavy_positions = g.walk[2];
+    s->walk_heavy_windows = g.walk[3];
+    s->walk_heavy_stops = g.walk[4];
+    s->walk_heavy_blocks = g.walk[5];
+    s->walk_heavy_blocked_ms = E->wall_khz ? (double)g.walk[6] / E->wall_khz : 0.0;
+    s->walk_longest = g.walk[7];
     return TBGPU_STATUS_OK;
 }
 
@@ -1728,6 +1738,7 @@ static WorkloadParams workload_params(const tbgpu_workload* w, u64 first) {
     while (std::gcd(a, n) != 1) a = a + 1 == n ? 1 : a + 1;
     W.perm_a = a;
     W.perm_b = tb_splitmix(w->seed ^ 0x5bd1e995ULL) % n;
+    W.hot_limited = w->account_count >= 2 ? w->hot_limited : 0;
     return W;
 }
 

@@ -101,6 +101,10 @@ struct FlowArgs {
     u64* b_xy;      // [2 * FLOW_RMAX * pass events] per such position: X, Y with the decided units before it
     u64* b_ex;      // [2 * FLOW_RMAX * pass events] per segment head: X, Y added by swept ok units
     struct SweepRec* b_rec;  // [pass events] per undecided unit in event order: what the sweep reads
+    // Per-account walkers (fl_walk; the window sweep's replacement when every sum is below 2^62):
+    // their position records live in b_ex, their segment lists and cursors in b_rec.
+    u32* b_vw;      // [pass events] per undecided unit: its two checks' verdicts, vd | vc << 2 (atomicOr)
+    u32 walk;       // 1: per-account walkers; 0: the one-wave window sweep (TBGPU_CONFIG_SWEEP_WINDOW)
 };
 
 // Every wait of the kernel is bounded by wall time (s_memrealtime) since the wait began.
@@ -585,6 +589,408 @@ __device__ static inline u32 fl_sw_slot(u32* s_hk, u32 head) {
     return SW_NONE;
 }
 
+// ---- the sweep as per-account walkers (fl_walk) --------------------------------------------------
+// What the rounds leave undecided is a set of SEGMENTS: per limit account, its undecided positions in
+// event order.  A check at position q passes iff the account's slack there — Y − X with every
+// decided ok unit before q (b_xy) plus the swept ok units before q on the same account — is at
+// least the amount.  So one walker per segment decides its checks in order with a running sum d of
+// its own swept deltas (an ok X leg: −a, an ok Y leg: +a), and walkers meet only at units with legs
+// on two segments:
+//   * a Y leg (the other side's posted field) needs the unit's final status, which the walker of
+//     the unit's check publishes (b_st, agent scope);
+//   * a unit with two open checks (a debits-limited debit account and a credits-limited credit
+//     account) combines them in the reference's order (:863-864): each side ORs its verdict into
+//     b_vw, and whichever side completes the pair publishes the status.  A side that fails needs
+//     nothing more (its account takes no delta whatever the other side says).
+// Walkers wait only on units earlier in event order on their partner's account, so the walker at
+// the globally earliest waiting point is never blocked: no deadlock while every walker keeps
+// being visited.  A segment with at least WALK_HEAVY positions (a Zipf-hot limit account's) gets a
+// wave of its own; the others share the remaining waves, each wave cycling through its segments
+// and moving on from a blocked one.  A wave walks its segment 64 positions a window: the
+// records and the statuses its Y legs and paired checks need are loaded by the 64 lanes at once,
+// then the window is resolved in order on the scalar unit — one add, compare and select per
+// position — stopping at a position whose partner has not decided yet.
+struct WalkRec {
+    i64 base;  // Y − X of the account with every decided ok unit before this position (balances included)
+    i64 a;     // the leg's amount
+    u32 u;     // unit
+    u32 kind;  // BT_X | BT_Y | BT_CR of the leg; the unit's verdicts when listed: vd << 8 | vc << 12
+    u32 head;  // the segment's (account's) first sorted position
+    u32 pad;
+};
+#ifndef WALK_HEAVY
+#define WALK_HEAVY 256
+#endif
+#define WALK_BIG (1LL << 62)  // a position whose outcome is known: "always" (+) / "never" (−)
+
+__device__ static inline u32 fl_combine(u32 vd, u32 vc) {  // the unit's status from its two checks
+    if (vd == BV_FAIL) return BS_FAIL_CREDITS;
+    if (vd == BV_PASS && vc == BV_FAIL) return BS_FAIL_DEBITS;
+    if (vd == BV_PASS && vc == BV_PASS) return BS_OK;
+    return BS_UNK;
+}
+__device__ static inline u32 fl_ld32(const u32* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ static inline void fl_st32(u32* p, u32 v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Ordered compaction of [0, n) over the grid: emit(i, k) for the k-th i (in order) with pred(i).
+// Every workgroup gets the total.  Two grid barriers; false if the kernel stalled.
+template <class Pred, class Emit>
+__device__ static inline bool fl_compact(const FlowArgs& F, Globals* g, u32 n, u32& gen, u32* s_wf, u32& total,
+                                         Pred pred, Emit emit) {
+    const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid, lane = tid & 63, wave = tid >> 6;
+    const u32 ut = ((n + G - 1) / G + NT - 1) / NT * NT;
+    const u32 u0 = min(n, blockIdx.x * ut), u1 = min(n, u0 + ut);
+    u32 cnt = 0;
+    for (u32 c0 = u0; c0 < u1; c0 += NT) {
+        const u32 i = c0 + tid;
+        cnt += __syncthreads_count(i < u1 && pred(i));
+    }
+    if (tid == 0) F.b_blk[5 * blockIdx.x] = cnt;
+    fl_grid_sync(g, G, gen, F);
+    if (fl_stalled(g)) return false;
+    u32 off = 0;
+    total = 0;
+    for (u32 b = 0; b < G; b++) {
+        const u32 c = (u32)F.b_blk[5 * b];
+        off += b < blockIdx.x ? c : 0;
+        total += c;
+    }
+    for (u32 c0 = u0; c0 < u1; c0 += NT) {
+        const u32 i = c0 + tid;
+        const bool p = i < u1 && pred(i);
+        const u64 m = __ballot(p);
+        if (lane == 0) s_wf[wave] = __popcll(m);
+        __syncthreads();
+        u32 before = 0, tot = 0;
+        for (u32 w = 0; w < NT / 64; w++) {
+            before += w < wave ? s_wf[w] : 0;
+            tot += s_wf[w];
+        }
+        if (p) emit(i, off + before + __popcll(m & ((1ULL << lane) - 1)));
+        off += tot;
+        __syncthreads();
+    }
+    fl_grid_sync(g, G, gen, F);
+    return !fl_stalled(g);
+}
+
+// A window's inputs beyond its records: for a Y leg and for a check paired with another open one,
+// the unit's status; for the paired check, the other side's verdict so far (b_vw).
+__device__ static inline void fl_walk_status(const FlowArgs& F, const WalkRec& r, bool valid, u32& st, u32& vw) {
+    const bool isx = r.kind & BT_X, cr = r.kind & BT_CR;
+    const bool pair = valid && isx && (cr ? (r.kind >> 8) & 15 : (r.kind >> 12) & 15) == BV_UNK;
+    st = BS_UNK;
+    vw = 0;
+    if ((valid && !isx) || pair) st = fl_ld32(&F.b_st[r.u]);
+    if (pair) vw = fl_ld32(&F.b_vw[r.u]);
+}
+
+struct WalkStats {
+    u64 windows = 0, stops = 0, blocks = 0, loop_ticks = 0, block_ticks = 0;
+};
+
+// Resolves one window of n <= 64 positions (lane j: position j) in order from the running sum d
+// (wave-uniform), publishing the statuses its checks decide.  Returns the positions decided: n, or
+// the position of a partner that has not decided yet (the walk resumes there).
+__device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r, u32 st, u32 vw, u32 n, i64& d,
+                                            WalkStats& ws) {
+    const u32 lane = threadIdx.x & 63;
+    const bool valid = lane < n;
+    const bool isx = r.kind & BT_X, isy = valid && !isx, cr = r.kind & BT_CR;
+    const u32 vd = (r.kind >> 8) & 15, vc = (r.kind >> 12) & 15;
+    u32 oth = cr ? vd : vc;
+    if (valid && isx && oth == BV_UNK && st == BS_UNK) oth = cr ? (vw & 3) : ((vw >> 2) & 3);
+    // A position is SIMPLE when its outcome follows from d alone: a check whose partner side is
+    // known (v = slack − amount: ok iff v + d >= 0; its outcome is this side's verdict), or a leg
+    // whose unit is decided (v = ±BIG).  The others stop the scalar walk: a Y leg of an open unit, a
+    // check paired with an open one.
+    bool simple = true, check = false;
+    i64 v = 0, dl = 0;
+    if (!valid) {
+        simple = false;
+    } else if (st != BS_UNK) {
+        v = st == BS_OK ? WALK_BIG : -WALK_BIG;
+        dl = isx ? -r.a : r.a;
+    } else if (isy || oth == BV_UNK) {
+        simple = false;
+    } else {
+        check = true;
+        v = r.base - r.a;
+        dl = oth == BV_FAIL ? 0 : -r.a;  // the other side failed: no delta here either way
+    }
+    const u64 smask = __ballot(simple);
+    const u64 vmask = n == 64 ? ~0ULL : ((1ULL << n) - 1);
+    u64 okm = 0;  // lane j's outcome in the walk (a check's own verdict)
+    u32 j = 0, m = n;
+    const u64 ta = wall_clock64();
+    while (j < n) {
+        const u64 bar = ~smask & vmask & (~0ULL << j);
+        const u32 b = bar ? (u32)__builtin_ctzll(bar) : n;
+        for (; j < b; j++) {
+            const u64 vj = fl_rl64((u64)v, j), dj = fl_rl64((u64)dl, j);
+            // ok iff v + d >= 0: the sign of the sum (its true value fits in 64 bits)
+            const bool ok = (int)(u32)((vj + (u64)d) >> 32) >= 0;
+            d = (i64)((u64)d + (ok ? dj : 0));
+            okm |= ok ? 1ULL << j : 0;
+        }
+        if (b == n) break;
+        // Position b: its partner was open when the window loaded.
+        ws.stops++;
+        const u32 bu = __builtin_amdgcn_readlane(r.u, b), bk = __builtin_amdgcn_readlane(r.kind, b);
+        const i64 ba = (i64)fl_rl64((u64)r.a, b);
+        if (bk & BT_X) {
+            // A paired check: this side's verdict, ORed in; whoever completes the pair publishes.
+            const i64 bb = (i64)fl_rl64((u64)r.base, b);
+            const bool side_ok = (i64)((u64)bb + (u64)d) >= ba;
+            const u32 sh = (bk & BT_CR) ? 2 : 0, mine = (side_ok ? BV_PASS : BV_FAIL) << sh;
+            u32 old = 0;
+            if (lane == 0) old = __hip_atomic_fetch_or(&F.b_vw[bu], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const u32 both = __builtin_amdgcn_readfirstlane(old) | mine;
+            const u32 fin = fl_combine(both & 3, (both >> 2) & 3);
+            if (fin != BS_UNK) {
+                if (lane == 0) fl_st32(&F.b_st[bu], fin);
+                if (fin == BS_OK) d -= ba;
+            } else if (side_ok) {
+                m = b;  // blocked: the other side completes the pair
+                break;
+            }           // this side failed: no delta here whatever the other side says
+        } else {
+            u32 s2 = 0;
+            if (lane == 0) s2 = fl_ld32(&F.b_st[bu]);
+            s2 = __builtin_amdgcn_readfirstlane(s2);
+            if (s2 == BS_UNK) {
+                m = b;  // blocked: the unit's check has not been walked yet
+                break;
+            }
+            if (s2 == BS_OK) d += ba;
+        }
+        j = b + 1;
+    }
+    ws.loop_ticks += wall_clock64() - ta;
+    ws.windows++;
+    // Publish the checks walked in the scalar loop.
+    if (check && lane < m) {
+        const u32 mine = (okm >> lane) & 1 ? BV_PASS : BV_FAIL;
+        fl_st32(&F.b_st[r.u], cr ? fl_combine(oth, mine) : fl_combine(mine, oth));
+    }
+    return m;
+}
+
+// A light segment [s0, s0 + n_seg) from cursor c with running sum d (wave-uniform) until it is done
+// or blocked.  Returns the positions decided.
+__device__ static inline u32 fl_walk_segment(const FlowArgs& F, const WalkRec* R, u32 s0, u32 n_seg, u32& c, i64& d,
+                                             WalkStats& ws) {
+    const u32 lane = threadIdx.x & 63;
+    // Wave-uniform by construction; told to the compiler, so the walk runs on the scalar unit.
+    s0 = __builtin_amdgcn_readfirstlane(s0);
+    n_seg = __builtin_amdgcn_readfirstlane(n_seg);
+    c = __builtin_amdgcn_readfirstlane(c);
+    d = (i64)fl_rl64((u64)d, 0);
+    u32 done = 0;
+    while (c < n_seg) {
+        const u32 n = min(64u, n_seg - c);
+        WalkRec r = {};
+        if (lane < n) r = R[s0 + c + lane];
+        u32 st, vw;
+        fl_walk_status(F, r, lane < n, st, vw);
+        const u32 m = fl_walk_window(F, r, st, vw, n, d, ws);
+        c += m;
+        done += m;
+        if (m < n) break;
+    }
+    return done;
+}
+
+// A heavy segment, walked to its end by one wave with the next windows in flight: the records two
+// windows ahead and the statuses one window ahead (a status read early may be stale — still open —
+// which only stops the walk there, where it is read again).
+__device__ static inline bool fl_walk_heavy(const FlowArgs& F, Globals* g, const WalkRec* R, u32 s0, u32 n_seg,
+                                            WalkStats& ws) {
+    const u32 lane = threadIdx.x & 63;
+    s0 = __builtin_amdgcn_readfirstlane(s0);
+    n_seg = __builtin_amdgcn_readfirstlane(n_seg);
+    u32 c = 0;
+    i64 d = 0;
+    u64 wb = 0, tblock = 0;
+    while (c < n_seg) {
+        // (Re)start the pipeline at c.
+        WalkRec r0 = {}, r1 = {};
+        if (c + lane < n_seg) r0 = R[s0 + c + lane];
+        if (c + 64 + lane < n_seg) r1 = R[s0 + c + 64 + lane];
+        u32 st0, vw0;
+        fl_walk_status(F, r0, c + lane < n_seg, st0, vw0);
+        for (;;) {
+            const u32 n = min(64u, n_seg - c);
+            WalkRec r2 = {};
+            if (c + 128 + lane < n_seg) r2 = R[s0 + c + 128 + lane];
+            u32 st1, vw1;
+            fl_walk_status(F, r1, c + 64 + lane < n_seg, st1, vw1);
+            const u32 m = fl_walk_window(F, r0, st0, vw0, n, d, ws);
+            c += m;
+            if (m && tblock) {
+                ws.block_ticks += wall_clock64() - tblock;
+                tblock = 0;
+                wb = 0;
+            }
+            if (m < n) break;  // blocked: restart the pipeline at c
+            if (c >= n_seg) break;
+            r0 = r1;
+            r1 = r2;
+            st0 = st1;
+            vw0 = vw1;
+        }
+        if (c >= n_seg) break;
+        ws.blocks++;
+        const u64 now = fl_now();
+        if (!tblock) tblock = now;
+        if (!wb) wb = now;
+        if (now - wb > F.stall_ticks) {
+            if (lane == 0) tb_panic(g, PANIC_FLOW_STALL);
+            return false;
+        }
+        if (fl_stalled(g)) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if (tblock) ws.block_ticks += wall_clock64() - tblock;
+    return true;
+}
+
+__device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 ndep, u32 NA, u32& gen, u32* s_wf) {
+    Globals* g = P.T.g;
+    const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid;
+    const u32 lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    WalkRec* R = (WalkRec*)F.b_ex;                 // [2 * ndep] position records (sorted order)
+    const u32 segcap = 2 * ndep + 2;
+    u32* seg = (u32*)F.b_rec;                      // [NS + 1] segment first records
+    u32* hv = seg + segcap;                        // [NH] heavy segments
+    u32* cur = hv + segcap;                        // [NS] cursors (light segments)
+    i64* dsv = (i64*)(cur + segcap + (segcap & 1));  // [NS] running sums (light segments)
+
+    // W1. Units: the verdict words; the undecided count (stats).
+    u32 nu = 0;
+    for (u32 f = blockIdx.x * NT + tid; f < ndep; f += G * NT) {
+        if (F.f_len[f] && F.b_st[f] == BS_UNK) {
+            F.b_vw[f] = (u32)F.b_vd[f] | ((u32)F.b_vc[f] << 2);
+            nu++;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nu += __shfl_xor(nu, off);
+    if (lane == 0 && nu) atomicAdd((unsigned long long*)&g->bounds_swept, (unsigned long long)nu);
+    // W2. The undecided positions in sorted order (segments stay contiguous, in event order).
+    u32 M = 0;
+    if (!fl_compact(F, g, NA, gen, s_wf, M,
+                    [&](u32 q) {
+                        const u32 meta = F.b_meta[q];
+                        return (meta & (BT_X | BT_Y)) && F.b_st[meta >> 3] == BS_UNK;
+                    },
+                    [&](u32 q, u32 p) {
+                        const u32 meta = F.b_meta[q], u = meta >> 3;
+                        WalkRec r;
+                        r.base = (i64)(F.b_xy[2 * q + 1] - F.b_xy[2 * q]);
+                        r.a = (i64)F.b_amt[q];
+                        r.u = u;
+                        r.kind = (meta & (BT_X | BT_Y | BT_CR)) | ((u32)F.b_vd[u] << 8) | ((u32)F.b_vc[u] << 12);
+                        r.head = F.b_head[q];
+                        r.pad = 0;
+                        R[p] = r;
+                    }))
+        return false;
+    // W3. Segment starts.
+    u32 NS = 0;
+    if (!fl_compact(F, g, M, gen, s_wf, NS, [&](u32 p) { return p == 0 || R[p].head != R[p - 1].head; },
+                    [&](u32 p, u32 k) {
+                        seg[k] = p;
+                        if (k + 1 == NS) seg[NS] = M;  // NS is the total by now
+                        cur[k] = 0;
+                        dsv[k] = 0;
+                    }))
+        return false;
+    // W4. Heavy segments (a workgroup's first wave each).
+    u32 NH = 0;
+    if (!fl_compact(F, g, NS, gen, s_wf, NH,
+                    [&](u32 k) {
+                        const u32 len = seg[k + 1] - seg[k];
+                        if (len >= WALK_HEAVY) atomicMax((unsigned long long*)&g->walk[7], (unsigned long long)len);
+                        return len >= WALK_HEAVY;
+                    },
+                    [&](u32 k, u32 i) { hv[i] = k; }))
+        return false;
+    if (blockIdx.x == 0 && tid == 0) {
+        atomicAdd((unsigned long long*)&g->walk[0], (unsigned long long)NS);
+        atomicAdd((unsigned long long*)&g->walk[1], (unsigned long long)NH);
+    }
+
+    // W5. The walk.  Heavy segment i on the first wave of workgroup i (a CU whose other waves stay
+    // idle, so its scalar unit serves the walker alone) when at most half the workgroups are taken
+    // by them; the light segments spread over the waves of the other workgroups.
+    const bool split = NH > 0 && NH <= G / 2;
+    WalkStats ws;
+    const u64 w0 = fl_now();
+    bool heavy_walker = false;
+    if (split && blockIdx.x < NH) {
+        if (wave == 0) {
+            heavy_walker = true;
+            const u32 k = hv[blockIdx.x];
+            const u32 s0 = seg[k], len = seg[k + 1] - s0;
+            fl_walk_heavy(F, g, R, s0, len, ws);
+            if (lane == 0) atomicAdd((unsigned long long*)&g->walk[2], (unsigned long long)len);
+        }
+    } else {
+        const u32 W = split ? (G - NH) * (NT / 64) : G * (NT / 64);
+        const u32 first = (split ? blockIdx.x - NH : blockIdx.x) * (NT / 64) + wave;
+        u64 wb = 0;
+        for (;;) {
+            bool left = false, moved = false;
+            for (u32 k = first; k < NS; k += W) {
+                const u32 s0 = seg[k], n_seg = seg[k + 1] - s0;
+                if (split && n_seg >= WALK_HEAVY) continue;
+                u32 c = fl_ld32(&cur[k]);
+                if (c == n_seg) continue;
+                i64 d = (i64)fl_ld64(&dsv[k]);
+                if (fl_walk_segment(F, R, s0, n_seg, c, d, ws)) {
+                    moved = true;
+                    if (lane == 0) {
+                        cur[k] = c;
+                        dsv[k] = d;
+                    }
+                }
+                left |= c < n_seg;
+            }
+            if (!left) break;
+            const u64 now = fl_now();
+            if (moved) {
+                wb = 0;
+                continue;
+            }
+            if (!wb) wb = now;
+            if (now - wb > F.stall_ticks) {
+                if (lane == 0) tb_panic(g, PANIC_FLOW_STALL);
+                break;
+            }
+            if (fl_stalled(g)) break;
+            __builtin_amdgcn_s_sleep(8);
+        }
+    }
+    if (heavy_walker && lane == 0) {
+        const u64 t = fl_now() - w0;
+        atomicAdd((unsigned long long*)&g->walk[3], (unsigned long long)ws.windows);
+        atomicAdd((unsigned long long*)&g->walk[4], (unsigned long long)ws.stops);
+        atomicAdd((unsigned long long*)&g->walk[5], (unsigned long long)ws.blocks);
+        atomicAdd((unsigned long long*)&g->walk[6], (unsigned long long)ws.block_ticks);
+        if (blockIdx.x == 0) {
+            atomicAdd((unsigned long long*)&g->sweep_ticks[1], (unsigned long long)ws.loop_ticks);
+            atomicAdd((unsigned long long*)&g->sweep_ticks[2], (unsigned long long)(t - ws.loop_ticks));
+        }
+    }
+    fl_grid_sync(g, G, gen, F);
+    return !fl_stalled(g);
+}
+
 __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32 ndep, u32 NA, u32& gen,
                                        u64 (*s_wv)[4], u32* s_wf, u32* s_cnt, u32* s_hk, u64* s_hx) {
     Globals* g = P.T.g;
@@ -592,6 +998,18 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
     const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid;
     const u32 lane = tid & 63, wave = tid >> 6;
     const u32* K = F.keys[0];
+    const u64 t_all = (blockIdx.x == 0 && tid == 0) ? fl_now() : 0;
+
+    // Every balance, amount and sum below 2^63 (bound + S, the certificate's own numbers): the
+    // signed slack form; below 2^62: the per-account walkers (fl_walk), whose "always" / "never"
+    // sentinels (+-2^62) then cannot overflow.
+    u128 S;
+    bool cert_global, cert64;
+    tb_pass_cert(P, S, cert_global, cert64);
+    u128 bs;
+    const bool slack = !P.cert_ext && cert_global && !tb_add_overflows(tb_u128(g->bound_lo, g->bound_hi), S, &bs) &&
+                       tb_hi(bs) == 0 && (tb_lo(bs) >> 63) == 0;
+    const bool walk = F.walk && slack && (tb_lo(bs) >> 62) == 0;
 
     // 1a. Units: no legs yet.
     for (u32 f = blockIdx.x * NT + tid; f < ndep; f += G * NT) {
@@ -648,10 +1066,20 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
         F.b_xy[2 * q] = xb + v[0] - own[0];
         F.b_xy[2 * q + 1] = yb + v[2] - own[2];
         F.b_head[q] = head;
-        F.b_ex[2 * head] = 0;
-        F.b_ex[2 * head + 1] = 0;
+        if (!walk) {
+            F.b_ex[2 * head] = 0;
+            F.b_ex[2 * head + 1] = 0;
+        }
         if (F.run[q].dr == r) F.b_qd[u] = q;
         else F.b_qc[u] = q;
+    }
+    if (walk) {
+        fl_grid_sync(g, G, gen, F);
+        if (fl_stalled(g)) return false;
+        const bool done = fl_walk(P, F, ndep, NA, gen, s_wf);
+        if (blockIdx.x == 0 && tid == 0)
+            atomicAdd((unsigned long long*)&g->sweep_ticks[0], (unsigned long long)(fl_now() - t_all));
+        return done;
     }
     // 1c. The undecided units in event order: per workgroup tile of units its count, then its offset.
     const u32 ut = ((ndep + G - 1) / G + NT - 1) / NT * NT;
@@ -710,13 +1138,6 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
     fl_grid_sync(g, G, gen, F);
     if (fl_stalled(g)) return false;
 
-    u128 S;
-    bool cert_global, cert64;
-    tb_pass_cert(P, S, cert_global, cert64);
-    u128 bs;
-    const bool slack = !P.cert_ext && cert_global && !tb_add_overflows(tb_u128(g->bound_lo, g->bound_hi), S, &bs) &&
-                       tb_hi(bs) == 0 && (tb_lo(bs) >> 63) == 0;
-
     // 2. The sweep: wave 0 of workgroup 0, 64 units a window; the next window's records load while
     // this one is resolved.  A lane holds one unit: its legs' X, Y with the decided units and the
     // swept ok units of earlier windows (b_ex); the window is resolved in lane order, each ok unit
@@ -730,7 +1151,8 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
             s_hx[2 * k] = 0;
             s_hx[2 * k + 1] = 0;
         }
-        u64 t_all = fl_now(), t_wait = 0, t_loop = 0;
+        u64 t_wait = 0, t_loop = 0;
+        const u64 t_walk = fl_now();
         for (u32 w0 = 0; w0 < nu; w0 += 64) {
             const SweepRec x = nx;
             const u64 ta = fl_now();
@@ -856,7 +1278,7 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
             F.words[FW_BUND] = 0;
             atomicAdd((unsigned long long*)&g->bounds_swept, (unsigned long long)nu);
             if (!slack) atomicAdd((unsigned long long*)&g->sweep_u64_passes, 1ULL);
-            atomicAdd((unsigned long long*)&g->sweep_ticks[0], (unsigned long long)(fl_now() - t_all));
+            atomicAdd((unsigned long long*)&g->sweep_ticks[0], (unsigned long long)(fl_now() - t_walk));
             atomicAdd((unsigned long long*)&g->sweep_ticks[1], (unsigned long long)t_loop);
             atomicAdd((unsigned long long*)&g->sweep_ticks[2], (unsigned long long)t_wait);
         }

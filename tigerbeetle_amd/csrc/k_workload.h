@@ -31,6 +31,7 @@ struct WorkloadParams {
     u32 limit_permille;   // accounts with debits_must_not_exceed_credits, per mille (account 0 never)
     double zipf_s;        // C3: Zipf exponent over account ranks
     u64 perm_a, perm_b;   // C3: rank r -> account (perm_a * r + perm_b) mod account_count (gcd = 1)
+    u32 hot_limited;      // C3: ranks [0, hot_limited) are limit accounts too (account 0 never)
 };
 
 enum : u32 { WK_UNIFORM = 0, WK_ZIPF_LIMITS = 1, WK_TWO_PHASE = 2 };
@@ -48,7 +49,11 @@ __device__ static inline u128 tb_wk_account_id(u64 idx) { return TB_U128_MAX - (
 __device__ static inline u128 tb_wk_transfer_id(u64 k) { return TB_U128_MAX - (u128)(k + 1); }
 
 __device__ static inline bool tb_wk_limited(const WorkloadParams& W, u64 idx) {
-    return idx != 0 && W.limit_permille && tb_range(tb_rand(W.seed, idx, 17), 1000) < W.limit_permille;
+    if (idx == 0) return false;
+    for (u32 r = 0; r < W.hot_limited; r++) {
+        if ((u64)(((u128)W.perm_a * r + W.perm_b) % W.account_count) == idx) return true;
+    }
+    return W.limit_permille && tb_range(tb_rand(W.seed, idx, 17), 1000) < W.limit_permille;
 }
 
 // Exp(mean 10 000) +| 1 (benchmark.zig:309): u in (0, 1].

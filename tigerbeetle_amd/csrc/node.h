@@ -1170,6 +1170,14 @@ static int node_api_get_stats(TbNode* N, tbgpu_stats* s) {
         s->sweep_u64_passes += x.sweep_u64_passes;
         s->flow_exec_ms += x.flow_exec_ms;
         for (int k = 0; k < 8; k++) s->flow_phase_ms[k] += x.flow_phase_ms[k];
+        s->walk_segments += x.walk_segments;
+        s->walk_heavy += x.walk_heavy;
+        s->walk_heavy_positions += x.walk_heavy_positions;
+        s->walk_heavy_windows += x.walk_heavy_windows;
+        s->walk_heavy_stops += x.walk_heavy_stops;
+        s->walk_heavy_blocks += x.walk_heavy_blocks;
+        s->walk_heavy_blocked_ms += x.walk_heavy_blocked_ms;
+        s->walk_longest = std::max(s->walk_longest, x.walk_longest);
     }
     return TBGPU_STATUS_OK;
 }

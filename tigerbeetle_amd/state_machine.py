@@ -39,7 +39,9 @@ class Options:
     profile: bool = False
     sequential_fallback: bool = False  # ordered fallback on one lane (tb_replay) instead of tb_flow
     # Limit checks: "auto" (scan rounds while they decide enough, then the in-order sweep), "early"
-    # (sweep after the first round) or "off" (rounds only, else the ordered run).  Identical results.
+    # (sweep after the first round) or "off" (rounds only, else the ordered run); the sweep is one
+    # walker per limit account, or with "window" / "window-early" one wave walking the checks in
+    # event order (round 2's form).  Identical results.
     bounds_sweep: str = "auto"
     # Reference cache options are accepted for interface parity; the HBM tables hold every object.
     lsm_forest_node_count: int = 0
@@ -60,7 +62,9 @@ class Engine:
                                 (_lib.CONFIG_PROFILE if options.profile else 0)
                                 | (_lib.CONFIG_SEQUENTIAL_FALLBACK if options.sequential_fallback else 0)
                                 | {"auto": 0, "early": _lib.CONFIG_SWEEP_EARLY,
-                                   "off": _lib.CONFIG_SWEEP_OFF}[options.bounds_sweep])
+                                   "off": _lib.CONFIG_SWEEP_OFF, "window": _lib.CONFIG_SWEEP_WINDOW,
+                                   "window-early": _lib.CONFIG_SWEEP_WINDOW | _lib.CONFIG_SWEEP_EARLY,
+                                   }[options.bounds_sweep])
         devices = list(options.devices or ())
         if len(devices) > len(cfg.devices):
             raise ValueError("at most %d devices" % len(cfg.devices))
@@ -363,15 +367,16 @@ class Engine:
         array = np.ascontiguousarray(array)
         _lib.check(self.lib.tbgpu_copy_to_device(self.h, ptr, array.ctypes.data, array.nbytes))
 
-    def generate_accounts(self, out_dev, first, count, seed=42, limit_permille=0):
-        w = _lib.tbgpu_workload(seed, 0, 0, limit_permille, 0.0)
+    def generate_accounts(self, out_dev, first, count, seed=42, limit_permille=0, account_count=0, hot_limited=0):
+        """hot_limited > 0 (the hottest Zipf ranks get a limit flag too) needs account_count."""
+        w = _lib.tbgpu_workload(seed, account_count, 0, limit_permille, 0.0, hot_limited, 0)
         _lib.check(self.lib.tbgpu_bench_generate_accounts(self.h, out_dev, first, count, ctypes.byref(w)))
 
     def generate_transfers(self, out_dev, first, count, account_count, seed=42, kind=0, limit_permille=0,
-                           zipf_s=1.2):
+                           zipf_s=1.2, hot_limited=0):
         """kind 0: C2 uniform; 1: C3 Zipf + limit-account funding; 2: C4 chains / two-phase / balancing
         (include/tbgpu_bench.h).  limit_permille must match generate_accounts' for kind 1."""
-        w = _lib.tbgpu_workload(seed, account_count, kind, limit_permille, zipf_s)
+        w = _lib.tbgpu_workload(seed, account_count, kind, limit_permille, zipf_s, hot_limited, 0)
         _lib.check(self.lib.tbgpu_bench_generate_transfers(self.h, out_dev, first, count, ctypes.byref(w)))
 
     def reset_transfers(self):
