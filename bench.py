@@ -77,6 +77,9 @@ def parse():
                    help="transfers of the C3 / C4 secondary lines (0: skip)")
     p.add_argument("--cpu-sample", type=int, default=12_285_000, help="transfers in the CPU baseline / parity sample (0: skip)")
     p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--walk-merge", type=int, default=-1,
+                   help="heavy limit-account segments the sweep walks merged on one wave at most (-1: the engine's "
+                        "default; 0: a wave each)")
     p.add_argument("--workload", default="c2", choices=["c2", "c3", "c3h", "c4"],
                    help="BASELINE.json shape: c2 (headline, default), c3 Zipf + limit accounts, c4 chains + two-phase")
     p.add_argument("--profile", type=int, default=1, help="time kernels with HIP events (roofline)")
@@ -293,6 +296,8 @@ def run_secondary(args, kind, device):
     n_acct, n_xfer = 1_000_000, args.secondary
     eng = Engine(Options(accounts_max=n_acct, transfers_max=n_xfer, pass_events_max=args.chunk_prepares * args.batch,
                          pass_batches_max=args.chunk_prepares, device=device, profile=True))
+    if args.walk_merge >= 0:
+        eng.walk_merge_max(args.walk_merge)
     accts, xfers = generate(eng, kind, n_acct, n_xfer, seed=args.seed)
     a_lens, x_lens = batches(n_acct, args.batch), batches(n_xfer, args.batch)
     a_ts, t_end = timestamps(a_lens, 1_000_000_000)
@@ -356,7 +361,8 @@ def run_secondary(args, kind, device):
                                "bounds_rounds", "bounds_skipped", "bounds_abandoned", "bounds_swept", "sweep_ms",
                                "sweep_loop_ms", "sweep_wait_ms", "walk_segments", "walk_heavy",
                                "walk_heavy_positions", "walk_heavy_windows", "walk_heavy_stops", "walk_heavy_blocks",
-                               "walk_heavy_blocked_ms", "walk_longest")},
+                               "walk_heavy_blocked_ms", "walk_longest", "walk_crit_windows",
+                               "walk_crit_blocks", "walk_crit_loop_ms", "walk_crit_ms")},
             "flow_phases_ms": flow_phases(stats),
             "roofline": roof, "parity": parity}
 
@@ -576,6 +582,8 @@ def main():
     engine = Engine(Options(accounts_max=args.accounts, transfers_max=args.transfers + 6 * 64 * args.batch,
                             pass_events_max=pass_events, pass_batches_max=args.pass_batches, device=local_rank,
                             profile=bool(args.profile)))
+    if args.walk_merge >= 0:
+        engine.walk_merge_max(args.walk_merge)
     seed = args.seed + 1000003 * rank  # each rank: its own ledger shard
 
     # -- accounts (create_accounts through the engine) --------------------------------------
@@ -799,7 +807,8 @@ def main():
                            "bounds_units", "bounds_rounds", "bounds_skipped", "bounds_abandoned", "bounds_swept",
                            "sweep_ms", "sweep_loop_ms", "sweep_wait_ms", "flow_exec_ms", "walk_segments",
                            "walk_heavy", "walk_heavy_positions", "walk_heavy_windows", "walk_heavy_stops",
-                           "walk_heavy_blocks", "walk_heavy_blocked_ms", "walk_longest")},
+                           "walk_heavy_blocks", "walk_heavy_blocked_ms", "walk_longest", "walk_crit_windows",
+                               "walk_crit_blocks", "walk_crit_loop_ms", "walk_crit_ms")},
         "flow_phases_ms": flow_phases(stats),
         "failed_events": n_failed,
         "roofline": roof,

@@ -234,6 +234,11 @@ typedef struct tbgpu_stats {
         walk_heavy_blocks;
     double walk_heavy_blocked_ms;
     uint64_t walk_longest;
+    /* The critical walker (the longest segment's, a wave each): windows, blocked returns, ms in its
+     * windows' in-order loops, ms in all (summed over passes). */
+    uint64_t walk_crit_windows, walk_crit_blocks;
+    double walk_crit_loop_ms, walk_crit_ms;
+    uint64_t walk_dbg[4]; /* diagnostics: a stalled walker's kind | segment, unit, status, verdict bits */
 } tbgpu_stats;
 
 int tbgpu_get_stats(tbgpu_t* engine, tbgpu_stats* stats);

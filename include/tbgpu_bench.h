@@ -53,6 +53,9 @@ int tbgpu_bench_profile_mask(tbgpu_t* engine, uint32_t mask);
  * (k_apply.h), smaller ones with atomics (default 262144; tests set 0 to cover legs on small
  * passes).  Exact either way. */
 int tbgpu_bench_legs_min_events(tbgpu_t* engine, uint32_t events);
+/* The limit-check sweep's walkers (k_flow.h fl_walk): up to this many heavy segments are walked
+ * merged by one wave (default 63); 0: every heavy segment on a wave of its own. */
+int tbgpu_bench_walk_merge_max(tbgpu_t* engine, uint32_t segments);
 
 /* The memory-access mix of tb_transfers_validate without its logic, on scratch buffers sized like
  * this engine's account table and transfer index, for `transfers` events (one pass): mean ms of

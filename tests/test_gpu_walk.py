@@ -64,12 +64,15 @@ def commit_both(engine, accts, xfers, n_acc, n_xfer, gap_every=0):
     return expected
 
 
-@pytest.mark.parametrize("bounds_sweep", ["early", "auto", "window-early"])
+@pytest.mark.parametrize("bounds_sweep,walk_merge", [("early", 0), ("auto", 0), ("early", 63), ("auto", 63),
+                                                     ("window-early", 0)])
 @pytest.mark.parametrize("n_acc,n_xfer,pass_batches", [(64, 200_000, 8), (4096, 300_000, 16)])
-def test_mixed_limit_flags(bounds_sweep, n_acc, n_xfer, pass_batches, gpu_engine_factory):
+def test_mixed_limit_flags(bounds_sweep, walk_merge, n_acc, n_xfer, pass_batches, gpu_engine_factory):
+    """walk_merge 0: a wave per heavy segment (the default); 63: heavy segments walked merged."""
     accts, xfers = mixed_limits(n_acc, n_xfer, seed=n_acc)
     engine = gpu_engine_factory(accounts_max=n_acc, transfers_max=n_xfer, pass_events_max=pass_batches * 8190,
                                 pass_batches_max=pass_batches, bounds_sweep=bounds_sweep)
+    engine.walk_merge_max(walk_merge)
     expected = commit_both(engine, accts, xfers, n_acc, n_xfer)
     codes = np.frombuffer(b"".join(expected), dtype=np.uint32).reshape(-1, 2)[:, 1]
     assert (codes == CreateTransferResult.exceeds_credits).any() and (codes == CreateTransferResult.exceeds_debits).any()
@@ -79,11 +82,12 @@ def test_mixed_limit_flags(bounds_sweep, n_acc, n_xfer, pass_batches, gpu_engine
         assert st["bounds_swept"] > 0
 
 
-@pytest.mark.parametrize("bounds_sweep", ["auto", "window"])
-def test_c3_hot_limited(bounds_sweep, gpu_engine_factory):
+@pytest.mark.parametrize("bounds_sweep,walk_merge", [("auto", 0), ("auto", 63), ("window", 0)])
+def test_c3_hot_limited(bounds_sweep, walk_merge, gpu_engine_factory):
     n_acc, n_xfer, pb = 1_000_000, 2_000_000, 64
     engine = gpu_engine_factory(accounts_max=n_acc, transfers_max=n_xfer, pass_events_max=pb * 8190,
                                 pass_batches_max=pb, bounds_sweep=bounds_sweep)
+    engine.walk_merge_max(walk_merge)
     accts, xfers = generate(engine, "c3h", n_acc, n_xfer, seed=42)
     expected = commit_both(engine, accts, xfers, n_acc, n_xfer, SETTINGS["c3h"]["gap_every"])
     assert sum(len(r) for r in expected) > 0

@@ -81,6 +81,11 @@ class tbgpu_stats(ctypes.Structure):
         ("walk_heavy_blocks", ctypes.c_uint64),
         ("walk_heavy_blocked_ms", ctypes.c_double),
         ("walk_longest", ctypes.c_uint64),
+        ("walk_crit_windows", ctypes.c_uint64),
+        ("walk_crit_blocks", ctypes.c_uint64),
+        ("walk_crit_loop_ms", ctypes.c_double),
+        ("walk_crit_ms", ctypes.c_double),
+        ("walk_dbg", ctypes.c_uint64 * 4),
     ]
 
 
@@ -148,6 +153,7 @@ SIGNATURES = [
     ("tbgpu_bench_pass_latencies", ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
     ("tbgpu_bench_profile_mask", ctypes.c_int, [_P, _U32]),
     ("tbgpu_bench_legs_min_events", ctypes.c_int, [_P, _U32]),
+    ("tbgpu_bench_walk_merge_max", ctypes.c_int, [_P, _U32]),
     ("tbgpu_bench_access_mix", ctypes.c_int, [_P, _U64, ctypes.POINTER(ctypes.c_double)]),
     ("tbgpu_bench_ledger_summary", ctypes.c_int, [_P, ctypes.POINTER(tbgpu_ledger_summary)]),
     ("tbgpu_bench_checkpoint_mark", ctypes.c_int, [_P]),

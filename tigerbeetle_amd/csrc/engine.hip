@@ -421,6 +421,9 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
             if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, E->device) != hipSuccess) khz = 0;
             khz = std::max(khz, 100000);  // s_memrealtime: 100 MHz on gfx9 parts; never trust a lower figure
             E->F.stall_ticks = 60ULL * 1000ULL * (u64)khz;  // 60 s
+            if (const char* ms = getenv("TBGPU_STALL_MS")) {  // diagnostics: a shorter bound on every wait
+                E->F.stall_ticks = std::max<u64>(1, strtoull(ms, nullptr, 10)) * (u64)khz;
+            }
             E->wall_khz = (u64)khz;
             if (getenv("TBGPU_DEBUG")) {  // diagnostics only: changes no behaviour
                 fprintf(stderr, "tbgpu: flow grid %u, occupancy %d, wall clock %d kHz, stall ticks %llu\n", E->F.grid,
@@ -493,6 +496,7 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         INIT_CK(hipMalloc(&F.b_rec, pe * sizeof(SweepRec)));
         INIT_CK(hipMalloc(&F.b_vw, pe * 4));
         F.walk = (config->flags & TBGPU_CONFIG_SWEEP_WINDOW) ? 0u : 1u;
+        F.walk_merge = WALK_MERGE_DEFAULT;
         F.bounds_rounds_max = FLOW_BOUNDS_ROUNDS_MAX;
         F.sweep_min = (config->flags & TBGPU_CONFIG_SWEEP_OFF) ? 0u
                       : (config->flags & TBGPU_CONFIG_SWEEP_EARLY) ? 0xFFFFFFFFu
@@ -1695,6 +1699,11 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     s->walk_heavy_blocks = g.walk[5];
     s->walk_heavy_blocked_ms = E->wall_khz ? (double)g.walk[6] / E->wall_khz : 0.0;
     s->walk_longest = g.walk[7];
+    s->walk_crit_windows = g.walk[8];
+    s->walk_crit_blocks = g.walk[9];
+    s->walk_crit_loop_ms = E->wall_khz ? (double)g.walk[10] / E->wall_khz : 0.0;
+    s->walk_crit_ms = E->wall_khz ? (double)g.walk[11] / E->wall_khz : 0.0;
+    for (int k = 0; k < 4; k++) s->walk_dbg[k] = g.walk_dbg[k];
     return TBGPU_STATUS_OK;
 }
 
@@ -1762,6 +1771,15 @@ extern "C" int tbgpu_bench_generate_transfers(tbgpu_t* E, void* out_dev, uint64_
     hipLaunchKernelGGL(tb_gen_transfers, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, E->stream,
                        (u8*)out_dev, count, workload_params(w, first));
     HIPCK(hipGetLastError());
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_bench_walk_merge_max(tbgpu_t* E, uint32_t segments) {
+    if (E->node) {
+        for (u32 d = 0; d < node_world(E->node); d++) tbgpu_bench_walk_merge_max(node_engine(E->node, d), segments);
+        return TBGPU_STATUS_OK;
+    }
+    E->F.walk_merge = std::min<u32>(segments, WALK_MERGE_MAX);
     return TBGPU_STATUS_OK;
 }
 

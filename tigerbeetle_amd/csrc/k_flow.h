@@ -48,7 +48,7 @@
 #endif
 
 enum : u32 { FW_NUNITS = 0, FW_QTAIL = 1, FW_SEQ = 2, FW_BNO = 3, FW_BUND = 4, FW_BDEC = 5,  // 5, 6, 7
-             FW_QHEAD = 8, FW_DONE = 9, FW_WORDS = FLOW_WORDS };
+             FW_QHEAD = 8, FW_DONE = 9, FW_WMAX = 10, FW_WORDS = FLOW_WORDS };
 enum : u32 {
     UF_ID_SINGLE = 1,  // the unit is the only dependent event of the pass whose id has its key
     UF_ID_UNIQUE = 2,  // ... or the others sharing the key (a 31-bit hash) name different ids
@@ -105,6 +105,7 @@ struct FlowArgs {
     // their position records live in b_ex, their segment lists and cursors in b_rec.
     u32* b_vw;      // [pass events] per undecided unit: its two checks' verdicts, vd | vc << 2 (atomicOr)
     u32 walk;       // 1: per-account walkers; 0: the one-wave window sweep (TBGPU_CONFIG_SWEEP_WINDOW)
+    u32 walk_merge; // heavy segments walked merged by one wave at most (WALK_MERGE_MAX)
 };
 
 // Every wait of the kernel is bounded by wall time (s_memrealtime) since the wait began.
@@ -691,15 +692,79 @@ __device__ static inline void fl_walk_status(const FlowArgs& F, const WalkRec& r
 
 struct WalkStats {
     u64 windows = 0, stops = 0, blocks = 0, loop_ticks = 0, block_ticks = 0;
+    u64 runs = 0, run_cycles = 0, stop_cycles = 0, window_cycles = 0;
 };
+
+// hist lane j := x (wave-uniform x and j).  The lane select goes through m0: one SGPR operand per
+// VALU instruction on gfx950.
+__device__ static inline void fl_wl(int& hist, int x, u32 j) {
+    asm("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, m0" : "+v"(hist) : "s"(x), "s"(j) : "m0");
+}
+
+// The 32-bit chain over lanes [j, e) of one account: dc += d32 when v32 + dc >= 0; hist (lane i) :=
+// dc before lane i.  Four lanes a step: their inputs read ahead of the chain (a readlane's result
+// reaches the scalar unit late), the chain itself, then the sums before each lane recorded.
+__device__ static inline void fl_chain32(int v32, int d32, u32 j, u32 e, int& dc, int& hist) {
+    for (; j + 4 <= e; j += 4) {
+        const int v0 = __builtin_amdgcn_readlane(v32, j), v1 = __builtin_amdgcn_readlane(v32, j + 1);
+        const int v2 = __builtin_amdgcn_readlane(v32, j + 2), v3 = __builtin_amdgcn_readlane(v32, j + 3);
+        const int e0 = __builtin_amdgcn_readlane(d32, j), e1 = __builtin_amdgcn_readlane(d32, j + 1);
+        const int e2 = __builtin_amdgcn_readlane(d32, j + 2), e3 = __builtin_amdgcn_readlane(d32, j + 3);
+        __builtin_amdgcn_sched_barrier(0);  // every read issued before the chain starts
+        const int c0 = dc;
+        dc += v0 + dc >= 0 ? e0 : 0;
+        const int c1 = dc;
+        dc += v1 + dc >= 0 ? e1 : 0;
+        const int c2 = dc;
+        dc += v2 + dc >= 0 ? e2 : 0;
+        const int c3 = dc;
+        dc += v3 + dc >= 0 ? e3 : 0;
+        __builtin_amdgcn_sched_barrier(0);
+        fl_wl(hist, c0, j);
+        fl_wl(hist, c1, j + 1);
+        fl_wl(hist, c2, j + 2);
+        fl_wl(hist, c3, j + 3);
+    }
+    for (; j < e; j++) {
+        const int vj = __builtin_amdgcn_readlane(v32, j), dj = __builtin_amdgcn_readlane(d32, j);
+        fl_wl(hist, dc, j);
+        dc += vj + dc >= 0 ? dj : 0;
+    }
+}
+
+// The in-order walk of lanes [j, e) of one account from its running sum d: lane i is ok iff
+// v + d >= 0, and an ok lane adds dl to d; okm collects the outcomes.  When every |dl| of the run is
+// below 2^24 the run is walked in 32 bits, relative to d at its start (|sum of dl| < 2^30): each v + d0
+// is clamped to +-2^30, which keeps its sign against any partial sum, so every outcome is the same.
+__device__ static inline void fl_walk_run(i64 v, i64 dl, u32 j, u32 e, i64& d, u64& okm) {
+    const u32 lane = threadIdx.x & 63;
+    const bool in = lane >= j && lane < e;
+    if (!__ballot(in && (dl >= (1LL << 24) || dl <= -(1LL << 24)))) {
+        const i64 vv = (i64)((u64)v + (u64)d);  // the true value fits
+        const int v32 = (int)(vv > (1LL << 30) ? (1LL << 30) : vv < -(1LL << 30) ? -(1LL << 30) : vv);
+        const int d32 = (int)dl;
+        int dd = 0, hist = 0;  // hist (lane i): dd before lane i's step
+        fl_chain32(v32, d32, j, e, dd, hist);
+        okm |= __ballot(in && v32 + hist >= 0);
+        d += dd;
+        return;
+    }
+    for (; j < e; j++) {
+        const u64 vj = fl_rl64((u64)v, j), dj = fl_rl64((u64)dl, j);
+        // ok iff v + d >= 0: the sign of the sum (its true value fits in 64 bits)
+        const bool ok = (int)(u32)((vj + (u64)d) >> 32) >= 0;
+        d = (i64)((u64)d + (ok ? dj : 0));
+        okm |= ok ? 1ULL << j : 0;
+    }
+}
 
 // Resolves one window of n <= 64 positions (lane j: position j) in order from the running sum d
 // (wave-uniform), publishing the statuses its checks decide.  Returns the positions decided: n, or
 // the position of a partner that has not decided yet (the walk resumes there).
-__device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r, u32 st, u32 vw, u32 n, i64& d,
-                                            WalkStats& ws) {
+__device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r, u32 st, u32 vw, u32 s, u32 n,
+                                            i64& d, WalkStats& ws) {
     const u32 lane = threadIdx.x & 63;
-    const bool valid = lane < n;
+    const bool valid = lane >= s && lane < n;  // positions [s, n): the window from where it stopped
     const bool isx = r.kind & BT_X, isy = valid && !isx, cr = r.kind & BT_CR;
     const u32 vd = (r.kind >> 8) & 15, vc = (r.kind >> 12) & 15;
     u32 oth = cr ? vd : vc;
@@ -725,18 +790,13 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
     const u64 smask = __ballot(simple);
     const u64 vmask = n == 64 ? ~0ULL : ((1ULL << n) - 1);
     u64 okm = 0;  // lane j's outcome in the walk (a check's own verdict)
-    u32 j = 0, m = n;
+    u32 j = s, m = n;
     const u64 ta = wall_clock64();
     while (j < n) {
         const u64 bar = ~smask & vmask & (~0ULL << j);
         const u32 b = bar ? (u32)__builtin_ctzll(bar) : n;
-        for (; j < b; j++) {
-            const u64 vj = fl_rl64((u64)v, j), dj = fl_rl64((u64)dl, j);
-            // ok iff v + d >= 0: the sign of the sum (its true value fits in 64 bits)
-            const bool ok = (int)(u32)((vj + (u64)d) >> 32) >= 0;
-            d = (i64)((u64)d + (ok ? dj : 0));
-            okm |= ok ? 1ULL << j : 0;
-        }
+        fl_walk_run(v, dl, j, b, d, okm);
+        j = b;
         if (b == n) break;
         // Position b: its partner was open when the window loaded.
         ws.stops++;
@@ -747,10 +807,15 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
             const i64 bb = (i64)fl_rl64((u64)r.base, b);
             const bool side_ok = (i64)((u64)bb + (u64)d) >= ba;
             const u32 sh = (bk & BT_CR) ? 2 : 0, mine = (side_ok ? BV_PASS : BV_FAIL) << sh;
-            u32 old = 0;
-            if (lane == 0) old = __hip_atomic_fetch_or(&F.b_vw[bu], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // (a partner that walked its side as a plain check publishes the status, not its bit)
+            u32 old = 0, s2 = 0;
+            if (lane == 0) {
+                old = __hip_atomic_fetch_or(&F.b_vw[bu], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s2 = fl_ld32(&F.b_st[bu]);
+            }
             const u32 both = __builtin_amdgcn_readfirstlane(old) | mine;
-            const u32 fin = fl_combine(both & 3, (both >> 2) & 3);
+            u32 fin = fl_combine(both & 3, (both >> 2) & 3);
+            if (fin == BS_UNK) fin = __builtin_amdgcn_readfirstlane(s2);
             if (fin != BS_UNK) {
                 if (lane == 0) fl_st32(&F.b_st[bu], fin);
                 if (fin == BS_OK) d -= ba;
@@ -773,7 +838,7 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
     ws.loop_ticks += wall_clock64() - ta;
     ws.windows++;
     // Publish the checks walked in the scalar loop.
-    if (check && lane < m) {
+    if (check && valid && lane < m) {
         const u32 mine = (okm >> lane) & 1 ? BV_PASS : BV_FAIL;
         fl_st32(&F.b_st[r.u], cr ? fl_combine(oth, mine) : fl_combine(mine, oth));
     }
@@ -797,7 +862,7 @@ __device__ static inline u32 fl_walk_segment(const FlowArgs& F, const WalkRec* R
         if (lane < n) r = R[s0 + c + lane];
         u32 st, vw;
         fl_walk_status(F, r, lane < n, st, vw);
-        const u32 m = fl_walk_window(F, r, st, vw, n, d, ws);
+        const u32 m = fl_walk_window(F, r, st, vw, 0, n, d, ws);
         c += m;
         done += m;
         if (m < n) break;
@@ -807,59 +872,309 @@ __device__ static inline u32 fl_walk_segment(const FlowArgs& F, const WalkRec* R
 
 // A heavy segment, walked to its end by one wave with the next windows in flight: the records two
 // windows ahead and the statuses one window ahead (a status read early may be stale — still open —
-// which only stops the walk there, where it is read again).
+// which only stops the walk there; the stopped window is retried in place, the stopping position
+// re-reading its status).
 __device__ static inline bool fl_walk_heavy(const FlowArgs& F, Globals* g, const WalkRec* R, u32 s0, u32 n_seg,
                                             WalkStats& ws) {
     const u32 lane = threadIdx.x & 63;
     s0 = __builtin_amdgcn_readfirstlane(s0);
     n_seg = __builtin_amdgcn_readfirstlane(n_seg);
-    u32 c = 0;
     i64 d = 0;
     u64 wb = 0, tblock = 0;
-    while (c < n_seg) {
-        // (Re)start the pipeline at c.
-        WalkRec r0 = {}, r1 = {};
-        if (c + lane < n_seg) r0 = R[s0 + c + lane];
-        if (c + 64 + lane < n_seg) r1 = R[s0 + c + 64 + lane];
-        u32 st0, vw0;
-        fl_walk_status(F, r0, c + lane < n_seg, st0, vw0);
-        for (;;) {
-            const u32 n = min(64u, n_seg - c);
-            WalkRec r2 = {};
-            if (c + 128 + lane < n_seg) r2 = R[s0 + c + 128 + lane];
-            u32 st1, vw1;
-            fl_walk_status(F, r1, c + 64 + lane < n_seg, st1, vw1);
-            const u32 m = fl_walk_window(F, r0, st0, vw0, n, d, ws);
-            c += m;
-            if (m && tblock) {
+    WalkRec r0 = {}, r1 = {};
+    if (lane < n_seg) r0 = R[s0 + lane];
+    if (64 + lane < n_seg) r1 = R[s0 + 64 + lane];
+    u32 st0, vw0;
+    fl_walk_status(F, r0, lane < n_seg, st0, vw0);
+    for (u32 c = 0; c < n_seg; c += 64) {
+        const u32 n = min(64u, n_seg - c);
+        WalkRec r2 = {};
+        if (c + 128 + lane < n_seg) r2 = R[s0 + c + 128 + lane];
+        u32 st1, vw1;
+        fl_walk_status(F, r1, c + 64 + lane < n_seg, st1, vw1);
+        for (u32 s = 0;;) {
+            const u32 m = fl_walk_window(F, r0, st0, vw0, s, n, d, ws);
+            if (m > s && tblock) {
                 ws.block_ticks += wall_clock64() - tblock;
                 tblock = 0;
                 wb = 0;
             }
-            if (m < n) break;  // blocked: restart the pipeline at c
-            if (c >= n_seg) break;
-            r0 = r1;
-            r1 = r2;
-            st0 = st1;
-            vw0 = vw1;
+            s = m;
+            if (s >= n) break;
+            ws.blocks++;
+            const u64 now = fl_now();
+            if (!tblock) tblock = now;
+            if (!wb) wb = now;
+            if (now - wb > F.stall_ticks) {
+                const u32 bu = __builtin_amdgcn_readlane(r0.u, s), bk = __builtin_amdgcn_readlane(r0.kind, s);
+                if (lane == 0) {
+                    g->walk_dbg[0] = 1 | ((u64)bk << 8) | ((u64)c << 32);
+                    g->walk_dbg[1] = bu;
+                    g->walk_dbg[2] = fl_ld32(&F.b_st[bu]);
+                    g->walk_dbg[3] = fl_ld32(&F.b_vw[bu]);
+                    tb_panic(g, PANIC_FLOW_STALL);
+                }
+                return false;
+            }
+            if (fl_stalled(g)) return false;
+            __builtin_amdgcn_s_sleep(1);
         }
-        if (c >= n_seg) break;
-        ws.blocks++;
-        const u64 now = fl_now();
-        if (!tblock) tblock = now;
-        if (!wb) wb = now;
-        if (now - wb > F.stall_ticks) {
-            if (lane == 0) tb_panic(g, PANIC_FLOW_STALL);
-            return false;
-        }
-        if (fl_stalled(g)) return false;
-        __builtin_amdgcn_s_sleep(1);
+        r0 = r1;
+        r1 = r2;
+        st0 = st1;
+        vw0 = vw1;
     }
-    if (tblock) ws.block_ticks += wall_clock64() - tblock;
     return true;
 }
 
-__device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 ndep, u32 NA, u32& gen, u32* s_wf) {
+// ---- the merged heavy walk --------------------------------------------------------------------------
+// Heavy segments couple densely (the hottest limit accounts pay each other: thousands of units per
+// pass carry a leg on two of them), and a walker waiting on another through global memory loses
+// microseconds each time.  So up to WALK_MERGE_MAX heavy segments are walked TOGETHER by one wave,
+// in event order over the units that have a leg on any of them: lane i holds heavy segment i's
+// running sum, a run of consecutive units on one heavy account is walked with that sum on the scalar
+// unit, and a unit on two heavy accounts updates both.  Only units whose other check is on a light
+// segment still wait for that segment's walker.
+#define WALK_MERGE_MAX 63
+// Measured on the adversarial C3 (bench --workload c3h): a wave per heavy segment, 67.5 M
+// transfers/s, against 36 M/s merged — the single merged wave walks every heavy unit itself, while
+// separate walkers overlap and only stop at the units they share.  Merging stays for A/B runs.
+#ifndef WALK_MERGE_DEFAULT
+#define WALK_MERGE_DEFAULT 0
+#endif
+struct HotRec {  // an undecided unit with a leg on a heavy segment, in event order
+    i64 bd, bc;  // the debit / credit leg's base: Y − X with the decided units before it
+    i64 a;       // amount
+    u32 u;       // unit
+    u32 info;    // HI_*
+};
+enum : u32 {
+    HI_HD = 0x3Fu,        // bits 0-5: heavy index + 1 of the debit leg (0: light, or no leg)
+    HI_HC_SHIFT = 6,      // bits 6-11: the same for the credit leg
+    HI_DP = 1u << 12,     // the debit leg is a listed position (a limit account's)
+    HI_DX = 1u << 13,     // ... and carries the unit's debit-side check
+    HI_CP = 1u << 14,     // the credit leg is a listed position
+    HI_CX = 1u << 15,     // ... and carries the credit-side check (credits_must_not_exceed_debits)
+    HI_VD_SHIFT = 16,     // the unit's verdicts when listed (BV_*)
+    HI_VC_SHIFT = 20,
+};
+
+// The generic resolution of stream unit j (a unit on two heavy segments, or one whose other check is
+// on a light segment): its checks from the absolute running sums, the light side's verdict read
+// (or waited for), the status published when complete.  d(h) = dreg + rel of lane h - 1; an ok unit
+// moves rel.  Returns false when the unit waits on a light walker.
+template <typename T>  // int: rel in a 32-bit window; i64: a window with large amounts
+__device__ static inline bool fl_walk_hot_unit(const FlowArgs& F, const HotRec& r, u32 j, i64 dreg, T& rel,
+                                               WalkStats& ws) {
+    const u32 lane = threadIdx.x & 63;
+    ws.stops++;
+    const u32 u = __builtin_amdgcn_readlane(r.u, j), inf = __builtin_amdgcn_readlane(r.info, j);
+    const u32 jhd = inf & HI_HD, jhc = (inf >> HI_HC_SHIFT) & HI_HD;
+    const i64 a = (i64)fl_rl64((u64)r.a, j);
+    const i64 dd = jhd ? (i64)(fl_rl64((u64)dreg, jhd - 1) + fl_rl64((u64)(i64)rel, jhd - 1)) : 0;
+    const i64 dc = jhc ? (i64)(fl_rl64((u64)dreg, jhc - 1) + fl_rl64((u64)(i64)rel, jhc - 1)) : 0;
+    u32 vd = (inf >> HI_VD_SHIFT) & 15, vc = (inf >> HI_VC_SHIFT) & 15, mine = 0;
+    if ((inf & HI_DX) && jhd) {
+        vd = (i64)((u64)fl_rl64((u64)r.bd, j) + (u64)dd) >= a ? BV_PASS : BV_FAIL;
+        mine |= vd;
+    }
+    if ((inf & HI_CX) && jhc) {
+        vc = (i64)((u64)fl_rl64((u64)r.bc, j) + (u64)dc) >= a ? BV_PASS : BV_FAIL;
+        mine |= vc << 2;
+    }
+    u32 fin = fl_combine(vd, vc);
+    if (fin == BS_UNK) {
+        // A light side is open: ours go in (b_vw); whoever completes the pair publishes.
+        u32 old = 0, s2 = 0;
+        if (lane == 0) {
+            old = __hip_atomic_fetch_or(&F.b_vw[u], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s2 = fl_ld32(&F.b_st[u]);
+        }
+        const u32 both = __builtin_amdgcn_readfirstlane(old) | mine;
+        fin = fl_combine(both & 3, (both >> 2) & 3);
+        if (fin == BS_UNK) fin = __builtin_amdgcn_readfirstlane(s2);
+        if (fin == BS_UNK) {
+            // Heavy legs move only if the unit is ok: a failed side settles it for them.
+            return (both & 3) == BV_FAIL || ((both >> 2) & 3) == BV_FAIL;
+        }
+    }
+    if (lane == 0) fl_st32(&F.b_st[u], fin);
+    if (fin == BS_OK) {
+        if (jhd && lane == jhd - 1) rel += (inf & HI_DX) ? -(T)a : (T)a;
+        if (jhc && lane == jhc - 1) rel += (inf & HI_CX) ? -(T)a : (T)a;
+    }
+    return true;
+}
+
+// Resolves stream units [s, n) of a window (lane j: unit j) in event order.  dreg (lane i) is heavy
+// segment i's running sum.  Every amount of the window is below 2^24 (the caller checks), so the
+// window's moves stay below 2^30 per segment and the walk runs in 32 bits relative to dreg: rel
+// (lane i) is segment i's move so far in the window, dc the current segment's.  A unit with one heavy
+// leg whose outcome follows from its sum alone is SIMPLE (see fl_walk_window): one add, compare and
+// select on the scalar unit, switching segments where consecutive units change segment.  The others
+// go through fl_walk_hot_unit.  Returns the units decided (n, or the unit waiting on a light walker).
+__device__ static inline u32 fl_walk_hot_window(const FlowArgs& F, const HotRec& r, u32 s, u32 n, i64& dreg,
+                                                WalkStats& ws) {
+    const u32 lane = threadIdx.x & 63;
+    const bool valid = lane >= s && lane < n;
+    const u32 info = r.info;
+    const u32 hd = info & HI_HD, hc = (info >> HI_HC_SHIFT) & HI_HD;
+    const u32 vd0 = (info >> HI_VD_SHIFT) & 15, vc0 = (info >> HI_VC_SHIFT) & 15;
+    const bool one = (hd != 0) != (hc != 0);
+    const u32 h = hd ? hd : hc;
+    const bool hx = hd ? (info & HI_DX) : (info & HI_CX);  // the heavy leg is a check
+    const u32 oth = hd ? vc0 : vd0;                          // the other side's verdict as listed
+    // Simple: the heavy leg is a check whose other side is known (a light check that was still
+    // open when the unit was listed goes through fl_walk_hot_unit).
+    const bool check = valid && one && hx && oth != BV_UNK;
+    const i64 v = (hd ? r.bd : r.bc) - r.a, dl = oth == BV_FAIL ? 0 : -r.a;
+    const u32 hs = check ? h : 0;
+    // 32-bit walk: v + d at the window start, clamped to +-2^30 (keeps its sign against any move).
+    const i64 d0 = (i64)__shfl((unsigned long long)dreg, (int)(hs ? hs - 1 : 0));
+    const i64 vv = (i64)((u64)v + (u64)d0);
+    const int v32 = (int)(vv > (1LL << 30) ? (1LL << 30) : vv < -(1LL << 30) ? -(1LL << 30) : vv);
+    const int d32 = (int)dl;
+    // Where the segment changes (a simple unit after another segment's, or a unit on its own).
+    const u32 hprev = __shfl_up(hs, 1);
+    const u64 sw = __ballot(valid && (lane == s || hs != hprev || !hs));
+    int rel = 0, hist = 0;  // hist (lane j): the current segment's move before unit j
+    u32 m = n;
+    const u64 cw = clock64();
+    for (u32 j = s; j < n;) {
+        // j starts a stretch: units j .. e - 1 on one segment, or a unit on its own.
+        const u32 cur = __builtin_amdgcn_readlane(hs, j);
+        if (!cur) {
+            const u64 c1 = clock64();
+            const bool ok = fl_walk_hot_unit(F, r, j, dreg, rel, ws);
+            ws.stop_cycles += clock64() - c1;
+            if (!ok) {
+                m = j;  // waits on a light walker
+                break;
+            }
+            j++;
+            continue;
+        }
+        const u64 c0 = clock64();
+        ws.runs++;
+        const u64 next = sw & ~((2ULL << j) - 1);
+        const u32 e = next ? (u32)__builtin_ctzll(next) : n;
+        int dc = __builtin_amdgcn_readlane(rel, cur - 1);
+        fl_chain32(v32, d32, j, e, dc, hist);
+        j = e;
+        if (lane == cur - 1) rel = dc;
+        ws.run_cycles += clock64() - c0;
+    }
+    dreg += rel;
+    ws.window_cycles += clock64() - cw;
+    ws.windows++;
+    // Publish the checks walked in the scalar loop.
+    if (check && lane < m) {
+        const u32 mine = v32 + hist >= 0 ? BV_PASS : BV_FAIL;
+        fl_st32(&F.b_st[r.u], hd ? fl_combine(mine, oth) : fl_combine(oth, mine));
+    }
+    return m;
+}
+
+// The same for a window with an amount of 2^24 or more: 64-bit sums, every unit on its own.
+__device__ static inline u32 fl_walk_hot_window64(const FlowArgs& F, const HotRec& r, u32 s, u32 n, i64& dreg,
+                                                  WalkStats& ws) {
+    u32 m = n;
+    for (u32 j = s; j < n; j++) {
+        i64 rel = 0;
+        const bool ok = fl_walk_hot_unit(F, r, j, dreg, rel, ws);
+        dreg += rel;
+        if (!ok) {
+            m = j;
+            break;
+        }
+    }
+    return m;
+}
+
+// The merged walk over N stream units by wave 0 of workgroup 0, fed through an LDS ring by wave 1
+// (WALK_RING windows ahead), so the walker itself issues no global load: its only memory operations
+// are LDS reads of its windows and the fire-and-forget status stores (a load behind those would
+// wait for them).  ctl[0]: windows filled, ctl[1]: windows consumed (N windows: the walker quit).
+#define WALK_RING 8
+__device__ static inline void fl_walk_merged(const FlowArgs& F, Globals* g, const HotRec* H, u32 N, WalkStats& ws,
+                                             u32* ctl, HotRec* ring) {
+    const u32 lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    N = __builtin_amdgcn_readfirstlane(N);
+    const u32 nw = (N + 63) / 64;
+    if (wave == 1) {
+        // The prefetcher: windows w .. w + 3 loaded together, then written to their ring slots.
+        for (u32 w = 0; w < nw; w += 4) {
+            const u64 w0 = fl_now();
+            while (__hip_atomic_load(&ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) + WALK_RING < min(nw, w + 4)) {
+                __builtin_amdgcn_s_sleep(1);
+                if (fl_expired(F, w0) || fl_stalled(g)) return;
+            }
+            if (__hip_atomic_load(&ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= nw) return;  // quit
+            HotRec x[4];
+#pragma unroll
+            for (u32 k = 0; k < 4; k++) {
+                const u32 i = (w + k) * 64 + lane;
+                x[k] = i < N ? H[i] : HotRec{};
+            }
+#pragma unroll
+            for (u32 k = 0; k < 4; k++) {
+                // (a slot past the last window may still hold an unconsumed one: left alone)
+                if (w + k < nw) ring[((w + k) % WALK_RING) * 64 + lane] = x[k];
+            }
+            if (lane == 0) __hip_atomic_store(&ctl[0], min(nw, w + 4), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        return;
+    }
+    if (wave != 0) return;
+    i64 dreg = 0;
+    u64 wb = 0, tblock = 0;
+    const u64 ta = wall_clock64();
+    for (u32 w = 0; w < nw; w++) {
+        const u64 w0 = fl_now();
+        while (__hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= w) {
+            __builtin_amdgcn_s_sleep(1);
+            if (fl_expired(F, w0)) {
+                if (lane == 0) tb_panic(g, PANIC_FLOW_STALL);
+                w = nw;
+                break;
+            }
+        }
+        if (w >= nw) break;
+        const HotRec r = ring[(w % WALK_RING) * 64 + lane];
+        const u32 n = min(64u, N - w * 64);
+        const bool big = __ballot(lane < n && r.a >= (1LL << 24));
+        u32 s = 0;
+        for (;;) {
+            const u32 m = big ? fl_walk_hot_window64(F, r, s, n, dreg, ws) : fl_walk_hot_window(F, r, s, n, dreg, ws);
+            if (m > s && tblock) {
+                ws.block_ticks += wall_clock64() - tblock;
+                tblock = 0;
+                wb = 0;
+            }
+            s = m;
+            if (s >= n) break;
+            // Waiting on a light walker.
+            ws.blocks++;
+            const u64 now = fl_now();
+            if (!tblock) tblock = now;
+            if (!wb) wb = now;
+            if (now - wb > F.stall_ticks) {
+                if (lane == 0) tb_panic(g, PANIC_FLOW_STALL);
+                break;
+            }
+            if (fl_stalled(g)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (s < n) break;
+        if (lane == 0) __hip_atomic_store(&ctl[1], w + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (lane == 0) __hip_atomic_store(&ctl[1], nw, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);  // done or quit
+    if (tblock) ws.block_ticks += wall_clock64() - tblock;
+    ws.loop_ticks += wall_clock64() - ta;
+}
+
+__device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 ndep, u32 NA, u32& gen, u32* s_wf,
+                                       u32* s_ctl, HotRec* s_ring) {
     Globals* g = P.T.g;
     const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid;
     const u32 lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -898,6 +1213,7 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
                         r.head = F.b_head[q];
                         r.pad = 0;
                         R[p] = r;
+                        F.b_head[q] = p;  // from here on: position -> its record
                     }))
         return false;
     // W3. Segment starts.
@@ -915,7 +1231,10 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
     if (!fl_compact(F, g, NS, gen, s_wf, NH,
                     [&](u32 k) {
                         const u32 len = seg[k + 1] - seg[k];
-                        if (len >= WALK_HEAVY) atomicMax((unsigned long long*)&g->walk[7], (unsigned long long)len);
+                        if (len >= WALK_HEAVY) {
+                            atomicMax((unsigned long long*)&g->walk[7], (unsigned long long)len);
+                            atomicMax(&F.words[FW_WMAX], len);
+                        }
                         return len >= WALK_HEAVY;
                     },
                     [&](u32 k, u32 i) { hv[i] = k; }))
@@ -925,30 +1244,96 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
         atomicAdd((unsigned long long*)&g->walk[1], (unsigned long long)NH);
     }
 
-    // W5. The walk.  Heavy segment i on the first wave of workgroup i (a CU whose other waves stay
-    // idle, so its scalar unit serves the walker alone) when at most half the workgroups are taken
-    // by them; the light segments spread over the waves of the other workgroups.
-    const bool split = NH > 0 && NH <= G / 2;
+    // W5. The walk.  Up to WALK_MERGE_MAX heavy segments: merged, on the first wave of workgroup 0
+    // (a CU whose other waves stay idle, so its scalar unit serves the walk alone).  More: heavy
+    // segment i on the first wave of workgroup i when at most half the workgroups are taken by them.
+    // The light segments spread over the waves of the other workgroups.
+    const bool merged = NH > 0 && NH <= F.walk_merge;
+    const bool split = !merged && NH > 0 && NH <= G / 2;
+    HotRec* H = (HotRec*)F.b_xy;  // [ndep] the merged stream (b_xy is read by W2 only)
+    u32 NHU = 0;
+    if (merged) {
+        // Tag the heavy positions with their heavy index, then list the units with a heavy leg.
+        for (u32 i = 0; i < NH; i++) {
+            const u32 k = hv[i], s0 = seg[k], len = seg[k + 1] - s0;
+            for (u32 p = blockIdx.x * NT + tid; p < len; p += G * NT) R[s0 + p].pad = i + 1;
+        }
+        fl_grid_sync(g, G, gen, F);
+        if (fl_stalled(g)) return false;
+        auto heavy_leg = [&](u32 q) { return q != FLOW_SENT && R[F.b_head[q]].pad != 0; };
+        if (!fl_compact(F, g, ndep, gen, s_wf, NHU,
+                        [&](u32 f) {
+                            return F.f_len[f] && F.b_st[f] == BS_UNK && (heavy_leg(F.b_qd[f]) || heavy_leg(F.b_qc[f]));
+                        },
+                        [&](u32 f, u32 i) {
+                            HotRec h = {};
+                            h.u = f;
+                            u32 info = ((u32)F.b_vd[f] << HI_VD_SHIFT) | ((u32)F.b_vc[f] << HI_VC_SHIFT);
+                            const u32 qd = F.b_qd[f], qc = F.b_qc[f];
+                            if (qd != FLOW_SENT) {
+                                const WalkRec& x = R[F.b_head[qd]];
+                                h.bd = x.base;
+                                h.a = x.a;
+                                info |= HI_DP | ((x.kind & BT_X) ? HI_DX : 0) | x.pad;
+                            }
+                            if (qc != FLOW_SENT) {
+                                const WalkRec& x = R[F.b_head[qc]];
+                                h.bc = x.base;
+                                h.a = x.a;
+                                info |= HI_CP | ((x.kind & BT_X) ? HI_CX : 0) | (x.pad << HI_HC_SHIFT);
+                            }
+                            h.info = info;
+                            H[i] = h;
+                        }))
+            return false;
+    }
     WalkStats ws;
     const u64 w0 = fl_now();
-    bool heavy_walker = false;
-    if (split && blockIdx.x < NH) {
-        if (wave == 0) {
+    bool heavy_walker = false, light_wave = true;
+    u32 lw = blockIdx.x * (NT / 64) + wave, LW = G * (NT / 64);
+    if (merged) {
+        if (blockIdx.x == 0) {
+            // The walker (wave 0) and its feeder (wave 1); the ring lives in the planner's LDS.
+            if (tid == 0) {
+                s_ctl[0] = 0;
+                s_ctl[1] = 0;
+            }
+            __syncthreads();
+            heavy_walker = wave == 0;
+            fl_walk_merged(F, g, H, NHU, ws, s_ctl, s_ring);
+            if (heavy_walker && lane == 0) atomicAdd((unsigned long long*)&g->walk[2], (unsigned long long)NHU);
+        }
+        light_wave = G >= 2 ? blockIdx.x >= 1 : wave >= 2;  // (waves 0, 1 of workgroup 0: the walker, its feeder)
+        lw = G >= 2 ? (blockIdx.x - 1) * (NT / 64) + wave : wave - 2;
+        LW = G >= 2 ? (G - 1) * (NT / 64) : NT / 64 - 2;
+    } else if (split) {
+        if (blockIdx.x < NH && wave == 0) {
             heavy_walker = true;
             const u32 k = hv[blockIdx.x];
             const u32 s0 = seg[k], len = seg[k + 1] - s0;
             fl_walk_heavy(F, g, R, s0, len, ws);
-            if (lane == 0) atomicAdd((unsigned long long*)&g->walk[2], (unsigned long long)len);
+            if (lane == 0) {
+                atomicAdd((unsigned long long*)&g->walk[2], (unsigned long long)len);
+                if (len == *(volatile u32*)&F.words[FW_WMAX]) {  // the critical walker: the longest segment
+                    atomicAdd((unsigned long long*)&g->walk[8], (unsigned long long)ws.windows);
+                    atomicAdd((unsigned long long*)&g->walk[9], (unsigned long long)ws.blocks);
+                    atomicAdd((unsigned long long*)&g->walk[10], (unsigned long long)ws.loop_ticks);
+                    atomicAdd((unsigned long long*)&g->walk[11], (unsigned long long)(fl_now() - w0));
+                }
+            }
         }
-    } else {
-        const u32 W = split ? (G - NH) * (NT / 64) : G * (NT / 64);
-        const u32 first = (split ? blockIdx.x - NH : blockIdx.x) * (NT / 64) + wave;
+        light_wave = blockIdx.x >= NH;
+        lw = (blockIdx.x - NH) * (NT / 64) + wave;
+        LW = (G - NH) * (NT / 64);
+    }
+    if (light_wave) {
+        const bool skip_heavy = merged || split;
         u64 wb = 0;
         for (;;) {
             bool left = false, moved = false;
-            for (u32 k = first; k < NS; k += W) {
+            for (u32 k = lw; k < NS; k += LW) {
                 const u32 s0 = seg[k], n_seg = seg[k + 1] - s0;
-                if (split && n_seg >= WALK_HEAVY) continue;
+                if (skip_heavy && n_seg >= WALK_HEAVY) continue;
                 u32 c = fl_ld32(&cur[k]);
                 if (c == n_seg) continue;
                 i64 d = (i64)fl_ld64(&dsv[k]);
@@ -969,11 +1354,14 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
             }
             if (!wb) wb = now;
             if (now - wb > F.stall_ticks) {
-                if (lane == 0) tb_panic(g, PANIC_FLOW_STALL);
+                if (lane == 0) {
+                    g->walk_dbg[0] = 2 | ((u64)lw << 8) | ((u64)NS << 32);
+                    tb_panic(g, PANIC_FLOW_STALL);
+                }
                 break;
             }
             if (fl_stalled(g)) break;
-            __builtin_amdgcn_s_sleep(8);
+            __builtin_amdgcn_s_sleep(2);
         }
     }
     if (heavy_walker && lane == 0) {
@@ -982,6 +1370,7 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
         atomicAdd((unsigned long long*)&g->walk[4], (unsigned long long)ws.stops);
         atomicAdd((unsigned long long*)&g->walk[5], (unsigned long long)ws.blocks);
         atomicAdd((unsigned long long*)&g->walk[6], (unsigned long long)ws.block_ticks);
+
         if (blockIdx.x == 0) {
             atomicAdd((unsigned long long*)&g->sweep_ticks[1], (unsigned long long)ws.loop_ticks);
             atomicAdd((unsigned long long*)&g->sweep_ticks[2], (unsigned long long)(t - ws.loop_ticks));
@@ -1076,7 +1465,7 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
     if (walk) {
         fl_grid_sync(g, G, gen, F);
         if (fl_stalled(g)) return false;
-        const bool done = fl_walk(P, F, ndep, NA, gen, s_wf);
+        const bool done = fl_walk(P, F, ndep, NA, gen, s_wf, s_hk, (HotRec*)s_hx);
         if (blockIdx.x == 0 && tid == 0)
             atomicAdd((unsigned long long*)&g->sweep_ticks[0], (unsigned long long)(fl_now() - t_all));
         return done;

@@ -346,7 +346,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         r_amt[k][1] = want && (r_info[k] & HZ_AMT_HI) ? P.amt_hi[pe] : 0ULL;
     }
     u64 tsmax = 0;
-    u32 ndep = 0;
+    u32 ndep = 0, n_app = 0, n_fail = 0;  // per thread, summed per wave below (one LDS atomic per wave)
     u32 legmask = 0;  // bit k: this thread's event k contributes two legs
     u32* dep_out = P.dep_list + pbase;
 #pragma unroll
@@ -407,9 +407,9 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                     } else {
                         tb_apply_account(P, pe, ts);
                     }
-                    atomicAdd(&s_applied, 1u);
+                    n_app++;
                 } else {
-                    atomicAdd(&s_failed, 1u);
+                    n_fail++;
                 }
             } else {
                 P.info[pe] = info | HZ_DEP;
@@ -431,8 +431,16 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     // commit_timestamp: max over events that returned ok when evaluated (:763, :882, :1012).
     u64 m = tsmax;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) m = max(m, (u64)__shfl_xor((unsigned long long)m, off));
-    if ((threadIdx.x & 63) == 0) s_tsmax[threadIdx.x >> 6] = m;
+    for (int off = 32; off > 0; off >>= 1) {
+        m = max(m, (u64)__shfl_xor((unsigned long long)m, off));
+        n_app += __shfl_xor(n_app, off);
+        n_fail += __shfl_xor(n_fail, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_tsmax[threadIdx.x >> 6] = m;
+        if (n_app) atomicAdd(&s_applied, n_app);
+        if (n_fail) atomicAdd(&s_failed, n_fail);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         u64 mm = 0;

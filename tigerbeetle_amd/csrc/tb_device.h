@@ -213,8 +213,10 @@ struct Globals {
     u64 sweep_ticks[3];       // fl_sweep wall-clock ticks: the whole walk, its in-window loops, its memory waits
     u64 flow_phase_ticks[8];  // tb_flow wall-clock ticks per phase (k_flow.h FP_*)
     u64 flow_exec_ticks;      // tb_flow run: lanes' time executing units, summed over lanes
-    u64 walk[8];              // fl_walk: segments, heavy segments; over the heavy walkers: positions,
-                              // windows, partner stops, blocked returns, blocked ticks; the longest segment
+    u64 walk[12];             // fl_walk: segments, heavy segments; over the heavy walkers: positions,
+                              // windows, partner stops, blocked returns, blocked ticks; the longest segment;
+                              // the critical (longest-segment) walker's windows, blocks, loop and total ticks
+    u64 walk_dbg[4];          // fl_walk: what a walker that stalled was waiting on (diagnostics)
     u64 sweep_u64_passes;     // sweeps that ran in the u64 X/Y form (bound + S >= 2^63)
     u64 bounds_abandoned;     // passes whose bounds did not converge in FLOW_BOUNDS_ROUNDS_MAX rounds
     // tb_flow's two-level grid barrier (k_flow.h fl_grid_sync): FL_BAR_GROUPS group counters, the

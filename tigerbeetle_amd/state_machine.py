@@ -225,7 +225,7 @@ class Engine:
     def stats(self):
         s = _lib.tbgpu_stats()
         _lib.check(self.lib.tbgpu_get_stats(self.h, ctypes.byref(s)))
-        return {f: (list(getattr(s, f)) if f == "flow_phase_ms" else getattr(s, f)) for f, _ in s._fields_}
+        return {f: (list(getattr(s, f)) if f in ("flow_phase_ms", "walk_dbg") else getattr(s, f)) for f, _ in s._fields_}
 
     def reset_stats(self):
         self.lib.tbgpu_reset_stats(self.h)
@@ -281,6 +281,10 @@ class Engine:
     def checkpoint_mark(self):
         """Take the current state as written back (tbgpu_bench_checkpoint_mark)."""
         _lib.check(self.lib.tbgpu_bench_checkpoint_mark(self.h))
+
+    def walk_merge_max(self, segments):
+        """Heavy segments the limit-check sweep walks merged on one wave at most (0: a wave each)."""
+        _lib.check(self.lib.tbgpu_bench_walk_merge_max(self.h, int(segments)))
 
     def legs_min_events(self, events):
         """Passes of >= events transfers use the sorted balance legs (0: every pass)."""

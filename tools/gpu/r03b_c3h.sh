@@ -1,5 +1,5 @@
 #!/bin/bash
-# Walker parity (quick), then the adversarial C3 and C3 alone on the bench.
+# Walker parity (quick), then the adversarial C3 (merged heavy walk, and a wave per heavy segment) and C3.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r03b
@@ -8,17 +8,12 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 rc=$?
 echo "walk tests rc=$rc"; tail -3 gpurun_out/r03b/pytest_walk.log
 if [ $rc -ne 0 ]; then grep -E "^E |FAILED|Error" gpurun_out/r03b/pytest_walk.log | head -30; exit $rc; fi
-for w in c3h c3; do
-  timeout -k 10 300 python -u bench.py --workload $w --accounts 1000000 --transfers 10000000 --steps 1 --warmup 1 \
-    --cpu-sample 0 --host-prepares 0 --device-steps 0 --secondary 0 --replica-prepares 0 --access-mix 0 > gpurun_out/r03b/bench_$w.log 2>&1
+B="--accounts 1000000 --transfers 10000000 --steps 1 --warmup 1 --cpu-sample 0 --host-prepares 0 --device-steps 0 --secondary 0 --replica-prepares 0 --access-mix 0"
+for v in "c3h -1" "c3h 63" "c3 -1" "c3 63"; do
+  set -- $v
+  timeout -k 10 300 python -u bench.py --workload $1 --walk-merge $2 $B > gpurun_out/r03b/bench_$1_m$2.log 2>&1
   rc=$?
-  echo "$w bench rc=$rc"; tail -c 3000 gpurun_out/r03b/bench_$w.log | tr ',' '\n' | grep -E '"value"|sweep|walk|bounds_swept|"ms_per_step"|run_or_apply|rounds'
+  echo "$1 merge=$2 bench rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done
-# The replica call path's timeline (kernel trace of tb_replica_bench, 300 ops).
-cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/r03b/rp_trace -o run -- \
-  $GRAFT_REPO_ROOT/tigerbeetle_amd/host/tb_replica_bench --accounts 1000000 --prepares 300 --warmup 20 \
-  > $GRAFT_REPO_ROOT/gpurun_out/r03b/rp_trace.log 2>&1
-echo "replica trace rc=$?"
 exit 0
