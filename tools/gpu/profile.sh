@@ -10,7 +10,7 @@
 #   bash tools/gpu/profile.sh dkt                 -> kernel trace + stats of the same run
 #   bash tools/gpu/profile.sh mc                  -> memory-copy + kernel trace of one headline step
 #     (the copy engine's timeline: body copies, their gaps, the per-chunk metadata copies)
-#   bash tools/gpu/profile.sh c3|c4               -> kernel trace of `bench.py --workload c3|c4`
+#   bash tools/gpu/profile.sh c3|c3h|c4           -> kernel trace of `bench.py --workload c3|c3h|c4`
 #     (1M accounts, 10M transfers, one timed step from host memory: tb_flow's bounds / sweep / run)
 # (rocprofv3 has written its CSVs when the profiled python exits; a crash after that, in process
 # teardown, leaves them complete and is reported, not hidden.)
@@ -34,7 +34,7 @@ case $MODE in
   fetch|write) C=FETCH_SIZE; [ "$MODE" = write ] && C=WRITE_SIZE
       timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/bench.py" $LEG \
         --steps 1 --warmup 0 --transfers 20000000 > "$OUT/$MODE.log" 2>&1; rc=$? ;;
-  c3|c4) timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/bench.py" \
+  c3|c3h|c4) timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/bench.py" \
         --workload $MODE --accounts 1000000 --transfers 10000000 --steps 1 --warmup 0 $LEG --access-mix 0 \
         > "$OUT/bench_$MODE.log" 2>&1; rc=$? ;;
 esac
