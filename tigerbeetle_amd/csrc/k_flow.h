@@ -622,6 +622,7 @@ struct WalkRec {
 #ifndef WALK_HEAVY
 #define WALK_HEAVY 256
 #endif
+
 #define WALK_BIG (1LL << 62)  // a position whose outcome is known: "always" (+) / "never" (−)
 
 __device__ static inline u32 fl_combine(u32 vd, u32 vc) {  // the unit's status from its two checks
@@ -837,7 +838,9 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
     }
     ws.loop_ticks += wall_clock64() - ta;
     ws.windows++;
-    // Publish the checks walked in the scalar loop.
+    // Publish the checks walked in the scalar loop, once per window: a status poll issued after a
+    // store waits for it (vmcnt counts both), so publishing in smaller pieces ahead of the stops
+    // cost more than it saved partners (C3h 66.5 -> 54 M/s with 16-position pieces).
     if (check && valid && lane < m) {
         const u32 mine = (okm >> lane) & 1 ? BV_PASS : BV_FAIL;
         fl_st32(&F.b_st[r.u], cr ? fl_combine(oth, mine) : fl_combine(mine, oth));
