@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -151,6 +153,8 @@ struct tbgpu {
     u64 commit_ts = 0;       // exact after every synchronous call
     u64 last_batch_ts = 0;   // upper bound for async calls
     bool pending = false;    // an async call was enqueued and not yet synced
+    u32 reply_seq = 0;       // one-prepare commits: the done word tb_reply_out writes last
+
 
     bool profile = false;
     u32 legs_min = LEGS_MIN_EVENTS;
@@ -497,6 +501,7 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         INIT_CK(hipMalloc(&F.b_vw, pe * 4));
         F.walk = (config->flags & TBGPU_CONFIG_SWEEP_WINDOW) ? 0u : 1u;
         F.walk_merge = WALK_MERGE_DEFAULT;
+
         F.bounds_rounds_max = FLOW_BOUNDS_ROUNDS_MAX;
         F.sweep_min = (config->flags & TBGPU_CONFIG_SWEEP_OFF) ? 0u
                       : (config->flags & TBGPU_CONFIG_SWEEP_EARLY) ? 0xFFFFFFFFu
@@ -518,7 +523,8 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         else INIT_CK(hipMalloc(&S.staging, pe * 128));
         INIT_CK(hipMalloc(&S.meta, (2 * E->meta_cap + 1) * 8));
         INIT_CK(hipHostMalloc(&S.h_meta, (2 * E->meta_cap + 1) * 8, hipHostMallocDefault));
-        INIT_CK(hipHostMalloc(&S.h_reply, pipe_reply_bytes(E), hipHostMallocMapped));
+        INIT_CK(hipHostMalloc(&S.h_reply, pipe_reply_bytes(E) + 64, hipHostMallocMapped));  // + the done word
+        memset(S.h_reply + pipe_reply_bytes(E), 0, 64);
         INIT_CK(hipHostGetDevicePointer((void**)&S.d_reply, S.h_reply, 0));
         INIT_CK(hipEventCreate(&S.start));
         INIT_CK(hipEventCreate(&S.copied));
@@ -743,6 +749,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
             u32 seq_cap = E->undo_cap;
             FlowArgs F = E->F;
             F.grid = flow_grid(E);
+
             // A small pass (the replica's one-prepare commit) has at most n dependent events: a grid
             // of one workgroup per 512 of them holds every unit and launches faster.
             if (n <= 65536) F.grid = std::min<u32>(F.grid, std::max<u32>(4, (u32)((n + 511) / 512)));
@@ -895,10 +902,23 @@ static int commit_host(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const
         }
         if (one) {
             tbgpu::PipeSlot& S = E->pipe[0];
+            // The host spins on the arena's done word (system-scope store after the reply): the
+            // stream's completion signal reaches a waiting host thread later.
+            const u32 seq = ++E->reply_seq ? E->reply_seq : ++E->reply_seq;
+            volatile u32* done = (volatile u32*)(S.h_reply + pipe_reply_bytes(E));
             hipLaunchKernelGGL(tb_reply_out, dim3(1), dim3(64), 0, E->stream, E->meta, 1u, E->reply_bytes, E->results, E->g,
-                               S.d_reply);
+                               S.d_reply, (u32*)(S.d_reply + pipe_reply_bytes(E)), seq);
             HIPCK(hipGetLastError());
-            HIPCK(hipStreamSynchronize(E->stream));
+            if (!E->profile) {
+                const auto t0 = std::chrono::steady_clock::now();
+                for (u32 spin = 0; *done != seq; spin++) {
+                    // A kernel that faulted never writes it: after 2 s, wait for the stream (which
+                    // reports the fault) instead.
+                    if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+                }
+                std::atomic_thread_fence(std::memory_order_acquire);
+            }
+            if (E->profile || *done != seq) HIPCK(hipStreamSynchronize(E->stream));
             E->pending = false;
             if ((st = prof_collect(E))) return st;
             const u64* head = (const u64*)S.h_reply;

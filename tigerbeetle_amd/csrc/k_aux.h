@@ -208,8 +208,11 @@ __global__ void tb_delta_advance(Tables T, AccountBal* snap, const u32* slots, u
 // (mapped host memory): the panic word and commit timestamp, every prepare's reply size and the
 // non-empty replies.  Only bytes that exist cross PCIe (4 B per prepare for an all-ok chunk); the
 // host reads the arena once the chunk's `done` event fired.  One workgroup per prepare.
+// seq != 0 (a one-prepare call, one workgroup): after everything else, seq is written to the word
+// at `done` with system scope, so the host can spin on it instead of waiting for the stream.
 __global__ __launch_bounds__(64) void tb_reply_out(const u64* batch_off, u32 nb, const u32* reply_bytes,
-                                                   const u32* results, const Globals* g, u8* arena) {
+                                                   const u32* results, const Globals* g, u8* arena,
+                                                   u32* done = nullptr, u32 seq = 0) {
     u64* head = (u64*)arena;
     u32* rb = (u32*)(arena + 16);
     const u32 k = blockIdx.x;
@@ -217,12 +220,16 @@ __global__ __launch_bounds__(64) void tb_reply_out(const u64* batch_off, u32 nb,
         head[0] = g->panic;
         head[1] = g->commit_timestamp;
     }
-    if (k >= nb) return;
-    const u32 bytes = reply_bytes[k];
-    if (threadIdx.x == 0) rb[k] = bytes;
-    if (bytes == 0) return;
-    u32* out = (u32*)(arena + 16 + (u64)nb * 4 + 8 * batch_off[k]);  // 4-B aligned: nb words before
-    const u32* in = results + 2 * batch_off[k];
-    for (u32 w = threadIdx.x; w < bytes / 4; w += 64) out[w] = in[w];
+    if (k < nb) {
+        const u32 bytes = reply_bytes[k];
+        if (threadIdx.x == 0) rb[k] = bytes;
+        u32* out = (u32*)(arena + 16 + (u64)nb * 4 + 8 * batch_off[k]);  // 4-B aligned: nb words before
+        const u32* in = results + 2 * batch_off[k];
+        for (u32 w = threadIdx.x; w < bytes / 4; w += 64) out[w] = in[w];
+    }
+    if (seq) {  // one wave: its stores drain, then the flag
+        __threadfence_system();
+        if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 

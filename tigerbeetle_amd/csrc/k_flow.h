@@ -698,8 +698,12 @@ struct WalkStats {
 
 // hist lane j := x (wave-uniform x and j).  The lane select goes through m0: one SGPR operand per
 // VALU instruction on gfx950.
+// m0 is a reserved register the compiler may hold a value in: saved and restored around the write.
 __device__ static inline void fl_wl(int& hist, int x, u32 j) {
-    asm("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, m0" : "+v"(hist) : "s"(x), "s"(j) : "m0");
+    u32 keep;
+    asm("s_mov_b32 %1, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tv_writelane_b32 %0, %2, m0\n\ts_mov_b32 m0, %1"
+        : "+v"(hist), "=&s"(keep)
+        : "s"(x), "s"(j));
 }
 
 // The 32-bit chain over lanes [j, e) of one account: dc += d32 when v32 + dc >= 0; hist (lane i) :=
