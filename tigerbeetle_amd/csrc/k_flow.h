@@ -696,44 +696,45 @@ struct WalkStats {
     u64 runs = 0, run_cycles = 0, stop_cycles = 0, window_cycles = 0;
 };
 
-// hist lane j := x (wave-uniform x and j).  The lane select goes through m0: one SGPR operand per
-// VALU instruction on gfx950.
-// m0 is a reserved register the compiler may hold a value in: saved and restored around the write.
-__device__ static inline void fl_wl(int& hist, int x, u32 j) {
-    u32 keep;
-    asm("s_mov_b32 %1, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tv_writelane_b32 %0, %2, m0\n\ts_mov_b32 m0, %1"
-        : "+v"(hist), "=&s"(keep)
-        : "s"(x), "s"(j));
+// One step of the 32-bit chain on the scalar unit: t = v + dc; if t >= 0 { dc += e; okm |= bit }.
+// Written out so the compare's SCC feeds both selects (the compiler materialises the bool instead).
+__device__ static inline void fl_step32(int v, int e, u64 bit, int& dc, u64& okm) {
+    int t;
+    u64 y;
+    asm("s_add_i32 %2, %4, %0\n\t"
+        "s_cmp_ge_i32 %2, 0\n\t"
+        "s_cselect_b32 %2, %5, 0\n\t"
+        "s_cselect_b64 %3, %6, 0\n\t"
+        "s_add_i32 %0, %0, %2\n\t"
+        "s_or_b64 %1, %1, %3"
+        : "+s"(dc), "+s"(okm), "=&s"(t), "=&s"(y)
+        : "s"(v), "s"(e), "s"(bit)
+        : "scc");
 }
 
-// The 32-bit chain over lanes [j, e) of one account: dc += d32 when v32 + dc >= 0; hist (lane i) :=
-// dc before lane i.  Four lanes a step: their inputs read ahead of the chain (a readlane's result
-// reaches the scalar unit late), the chain itself, then the sums before each lane recorded.
-__device__ static inline void fl_chain32(int v32, int d32, u32 j, u32 e, int& dc, int& hist) {
+// The 32-bit chain over lanes [j, e) of one account: lane i is ok iff v32 + dc >= 0, and an ok lane
+// adds d32 to dc; okm collects the outcomes.  Four lanes a step: their inputs read ahead of the
+// chain (a readlane's result reaches the scalar unit late), then the chain itself.
+__device__ static inline void fl_chain32(int v32, int d32, u32 j, u32 e, int& dc, u64& okm) {
+    // Wave-uniform by construction; said so, or the compiler may keep them in vector registers.
+    j = __builtin_amdgcn_readfirstlane(j);
+    e = __builtin_amdgcn_readfirstlane(e);
+    dc = __builtin_amdgcn_readfirstlane(dc);
+    okm = fl_rl64(okm, 0);
     for (; j + 4 <= e; j += 4) {
         const int v0 = __builtin_amdgcn_readlane(v32, j), v1 = __builtin_amdgcn_readlane(v32, j + 1);
         const int v2 = __builtin_amdgcn_readlane(v32, j + 2), v3 = __builtin_amdgcn_readlane(v32, j + 3);
         const int e0 = __builtin_amdgcn_readlane(d32, j), e1 = __builtin_amdgcn_readlane(d32, j + 1);
         const int e2 = __builtin_amdgcn_readlane(d32, j + 2), e3 = __builtin_amdgcn_readlane(d32, j + 3);
+        const u64 bit = 1ULL << j;
         __builtin_amdgcn_sched_barrier(0);  // every read issued before the chain starts
-        const int c0 = dc;
-        dc += v0 + dc >= 0 ? e0 : 0;
-        const int c1 = dc;
-        dc += v1 + dc >= 0 ? e1 : 0;
-        const int c2 = dc;
-        dc += v2 + dc >= 0 ? e2 : 0;
-        const int c3 = dc;
-        dc += v3 + dc >= 0 ? e3 : 0;
-        __builtin_amdgcn_sched_barrier(0);
-        fl_wl(hist, c0, j);
-        fl_wl(hist, c1, j + 1);
-        fl_wl(hist, c2, j + 2);
-        fl_wl(hist, c3, j + 3);
+        fl_step32(v0, e0, bit, dc, okm);
+        fl_step32(v1, e1, bit << 1, dc, okm);
+        fl_step32(v2, e2, bit << 2, dc, okm);
+        fl_step32(v3, e3, bit << 3, dc, okm);
     }
     for (; j < e; j++) {
-        const int vj = __builtin_amdgcn_readlane(v32, j), dj = __builtin_amdgcn_readlane(d32, j);
-        fl_wl(hist, dc, j);
-        dc += vj + dc >= 0 ? dj : 0;
+        fl_step32(__builtin_amdgcn_readlane(v32, j), __builtin_amdgcn_readlane(d32, j), 1ULL << j, dc, okm);
     }
 }
 
@@ -748,9 +749,8 @@ __device__ static inline void fl_walk_run(i64 v, i64 dl, u32 j, u32 e, i64& d, u
         const i64 vv = (i64)((u64)v + (u64)d);  // the true value fits
         const int v32 = (int)(vv > (1LL << 30) ? (1LL << 30) : vv < -(1LL << 30) ? -(1LL << 30) : vv);
         const int d32 = (int)dl;
-        int dd = 0, hist = 0;  // hist (lane i): dd before lane i's step
-        fl_chain32(v32, d32, j, e, dd, hist);
-        okm |= __ballot(in && v32 + hist >= 0);
+        int dd = 0;
+        fl_chain32(v32, d32, j, e, dd, okm);
         d += dd;
         return;
     }
@@ -766,8 +766,10 @@ __device__ static inline void fl_walk_run(i64 v, i64 dl, u32 j, u32 e, i64& d, u
 // Resolves one window of n <= 64 positions (lane j: position j) in order from the running sum d
 // (wave-uniform), publishing the statuses its checks decide.  Returns the positions decided: n, or
 // the position of a partner that has not decided yet (the walk resumes there).
+// wait (a heavy walker: its wave walks this one segment) keeps a stopped window in place, polling the
+// partner's status, instead of returning; a light wave returns and visits its other segments.
 __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r, u32 st, u32 vw, u32 s, u32 n,
-                                            i64& d, WalkStats& ws) {
+                                            i64& d, WalkStats& ws, Globals* g = nullptr, bool wait = false) {
     const u32 lane = threadIdx.x & 63;
     const bool valid = lane >= s && lane < n;  // positions [s, n): the window from where it stopped
     const bool isx = r.kind & BT_X, isy = valid && !isx, cr = r.kind & BT_CR;
@@ -795,7 +797,7 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
     const u64 smask = __ballot(simple);
     const u64 vmask = n == 64 ? ~0ULL : ((1ULL << n) - 1);
     u64 okm = 0;  // lane j's outcome in the walk (a check's own verdict)
-    u32 j = s, m = n;
+    u32 j = s, m = n, pub = s;  // [s, pub): published while waiting in place
     const u64 ta = wall_clock64();
     while (j < n) {
         const u64 bar = ~smask & vmask & (~0ULL << j);
@@ -807,37 +809,55 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         ws.stops++;
         const u32 bu = __builtin_amdgcn_readlane(r.u, b), bk = __builtin_amdgcn_readlane(r.kind, b);
         const i64 ba = (i64)fl_rl64((u64)r.a, b);
-        if (bk & BT_X) {
-            // A paired check: this side's verdict, ORed in; whoever completes the pair publishes.
-            const i64 bb = (i64)fl_rl64((u64)r.base, b);
-            const bool side_ok = (i64)((u64)bb + (u64)d) >= ba;
-            const u32 sh = (bk & BT_CR) ? 2 : 0, mine = (side_ok ? BV_PASS : BV_FAIL) << sh;
-            // (a partner that walked its side as a plain check publishes the status, not its bit)
+        const i64 bb = (i64)fl_rl64((u64)r.base, b);
+        // The unit's status now: a paired check ORs this side's verdict in first (whoever completes
+        // the pair publishes; a partner that walked its side as a plain check publishes the status,
+        // not its bit).  BS_UNK: still open.
+        const bool side_ok = (bk & BT_X) && (i64)((u64)bb + (u64)d) >= ba;
+        auto poll = [&]() -> u32 {
             u32 old = 0, s2 = 0;
+            const u32 mine = (bk & BT_X) ? (side_ok ? BV_PASS : BV_FAIL) << ((bk & BT_CR) ? 2 : 0) : 0;
             if (lane == 0) {
-                old = __hip_atomic_fetch_or(&F.b_vw[bu], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (bk & BT_X) old = __hip_atomic_fetch_or(&F.b_vw[bu], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 s2 = fl_ld32(&F.b_st[bu]);
             }
             const u32 both = __builtin_amdgcn_readfirstlane(old) | mine;
-            u32 fin = fl_combine(both & 3, (both >> 2) & 3);
-            if (fin == BS_UNK) fin = __builtin_amdgcn_readfirstlane(s2);
+            const u32 fin = (bk & BT_X) ? fl_combine(both & 3, (both >> 2) & 3) : BS_UNK;
             if (fin != BS_UNK) {
                 if (lane == 0) fl_st32(&F.b_st[bu], fin);
-                if (fin == BS_OK) d -= ba;
-            } else if (side_ok) {
-                m = b;  // blocked: the other side completes the pair
-                break;
-            }           // this side failed: no delta here whatever the other side says
-        } else {
-            u32 s2 = 0;
-            if (lane == 0) s2 = fl_ld32(&F.b_st[bu]);
-            s2 = __builtin_amdgcn_readfirstlane(s2);
-            if (s2 == BS_UNK) {
-                m = b;  // blocked: the unit's check has not been walked yet
-                break;
+                return fin;
             }
-            if (s2 == BS_OK) d += ba;
+            return __builtin_amdgcn_readfirstlane(s2);
+        };
+        u32 fin = poll();
+        // A paired check whose own side failed moves nothing here, whatever the other side says.
+        const bool moot = (bk & BT_X) && !side_ok;
+        if (fin == BS_UNK && !moot && wait) {
+            // Publish what this window decided so far (the partner may be waiting on it), then wait.
+            if (check && valid && lane >= pub && lane < b) {
+                const u32 mine = (okm >> lane) & 1 ? BV_PASS : BV_FAIL;
+                fl_st32(&F.b_st[r.u], cr ? fl_combine(oth, mine) : fl_combine(mine, oth));
+            }
+            pub = b;
+            ws.blocks++;
+            const u64 w0 = fl_now();
+            while (fin == BS_UNK) {
+                __builtin_amdgcn_s_sleep(1);
+                fin = poll();
+                // (readfirstlane: an atomic load counts as divergent, which would make the walk's
+                // sums vector values)
+                if (__builtin_amdgcn_readfirstlane(fin == BS_UNK && (fl_expired(F, w0) || fl_stalled(g)))) {
+                    if (lane == 0) tb_panic(g, PANIC_FLOW_STALL);
+                    break;
+                }
+            }
+            ws.block_ticks += fl_now() - w0;
         }
+        if (fin == BS_UNK && !moot) {
+            m = b;  // blocked: the partner has not decided yet
+            break;
+        }
+        if (fin == BS_OK) d += (bk & BT_X) ? -ba : ba;
         j = b + 1;
     }
     ws.loop_ticks += wall_clock64() - ta;
@@ -845,7 +865,7 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
     // Publish the checks walked in the scalar loop, once per window: a status poll issued after a
     // store waits for it (vmcnt counts both), so publishing in smaller pieces ahead of the stops
     // cost more than it saved partners (C3h 66.5 -> 54 M/s with 16-position pieces).
-    if (check && valid && lane < m) {
+    if (check && valid && lane >= pub && lane < m) {
         const u32 mine = (okm >> lane) & 1 ? BV_PASS : BV_FAIL;
         fl_st32(&F.b_st[r.u], cr ? fl_combine(oth, mine) : fl_combine(mine, oth));
     }
@@ -900,7 +920,7 @@ __device__ static inline bool fl_walk_heavy(const FlowArgs& F, Globals* g, const
         u32 st1, vw1;
         fl_walk_status(F, r1, c + 64 + lane < n_seg, st1, vw1);
         for (u32 s = 0;;) {
-            const u32 m = fl_walk_window(F, r0, st0, vw0, s, n, d, ws);
+            const u32 m = fl_walk_window(F, r0, st0, vw0, s, n, d, ws, g, true);
             if (m > s && tblock) {
                 ws.block_ticks += wall_clock64() - tblock;
                 tblock = 0;
@@ -1044,7 +1064,8 @@ __device__ static inline u32 fl_walk_hot_window(const FlowArgs& F, const HotRec&
     // Where the segment changes (a simple unit after another segment's, or a unit on its own).
     const u32 hprev = __shfl_up(hs, 1);
     const u64 sw = __ballot(valid && (lane == s || hs != hprev || !hs));
-    int rel = 0, hist = 0;  // hist (lane j): the current segment's move before unit j
+    int rel = 0;
+    u64 okm = 0;  // the simple units' outcomes
     u32 m = n;
     const u64 cw = clock64();
     for (u32 j = s; j < n;) {
@@ -1066,7 +1087,7 @@ __device__ static inline u32 fl_walk_hot_window(const FlowArgs& F, const HotRec&
         const u64 next = sw & ~((2ULL << j) - 1);
         const u32 e = next ? (u32)__builtin_ctzll(next) : n;
         int dc = __builtin_amdgcn_readlane(rel, cur - 1);
-        fl_chain32(v32, d32, j, e, dc, hist);
+        fl_chain32(v32, d32, j, e, dc, okm);
         j = e;
         if (lane == cur - 1) rel = dc;
         ws.run_cycles += clock64() - c0;
@@ -1076,7 +1097,7 @@ __device__ static inline u32 fl_walk_hot_window(const FlowArgs& F, const HotRec&
     ws.windows++;
     // Publish the checks walked in the scalar loop.
     if (check && lane < m) {
-        const u32 mine = v32 + hist >= 0 ? BV_PASS : BV_FAIL;
+        const u32 mine = (okm >> lane) & 1 ? BV_PASS : BV_FAIL;
         fl_st32(&F.b_st[r.u], hd ? fl_combine(mine, oth) : fl_combine(oth, mine));
     }
     return m;
