@@ -362,7 +362,7 @@ def run_secondary(args, kind, device):
                                "sweep_loop_ms", "sweep_wait_ms", "walk_segments", "walk_heavy",
                                "walk_heavy_positions", "walk_heavy_windows", "walk_heavy_stops", "walk_heavy_blocks",
                                "walk_heavy_blocked_ms", "walk_longest", "walk_crit_windows",
-                               "walk_crit_blocks", "walk_crit_loop_ms", "walk_crit_ms")},
+                               "walk_crit_blocks", "walk_crit_wait_ms", "walk_crit_ms")},
             "flow_phases_ms": flow_phases(stats),
             "roofline": roof, "parity": parity}
 
@@ -808,7 +808,7 @@ def main():
                            "sweep_ms", "sweep_loop_ms", "sweep_wait_ms", "flow_exec_ms", "walk_segments",
                            "walk_heavy", "walk_heavy_positions", "walk_heavy_windows", "walk_heavy_stops",
                            "walk_heavy_blocks", "walk_heavy_blocked_ms", "walk_longest", "walk_crit_windows",
-                               "walk_crit_blocks", "walk_crit_loop_ms", "walk_crit_ms")},
+                               "walk_crit_blocks", "walk_crit_wait_ms", "walk_crit_ms")},
         "flow_phases_ms": flow_phases(stats),
         "failed_events": n_failed,
         "roofline": roof,

@@ -234,10 +234,10 @@ typedef struct tbgpu_stats {
         walk_heavy_blocks;
     double walk_heavy_blocked_ms;
     uint64_t walk_longest;
-    /* The critical walker (the longest segment's, a wave each): windows, blocked returns, ms in its
-     * windows' in-order loops, ms in all (summed over passes). */
+    /* The critical walker (the longest segment's, a wave each): windows, waits at a partner's open
+     * unit, ms spent waiting, ms in all (summed over passes). */
     uint64_t walk_crit_windows, walk_crit_blocks;
-    double walk_crit_loop_ms, walk_crit_ms;
+    double walk_crit_wait_ms, walk_crit_ms;
     uint64_t walk_dbg[4]; /* diagnostics: a stalled walker's kind | segment, unit, status, verdict bits */
 } tbgpu_stats;
 

@@ -83,7 +83,7 @@ class tbgpu_stats(ctypes.Structure):
         ("walk_longest", ctypes.c_uint64),
         ("walk_crit_windows", ctypes.c_uint64),
         ("walk_crit_blocks", ctypes.c_uint64),
-        ("walk_crit_loop_ms", ctypes.c_double),
+        ("walk_crit_wait_ms", ctypes.c_double),
         ("walk_crit_ms", ctypes.c_double),
         ("walk_dbg", ctypes.c_uint64 * 4),
     ]

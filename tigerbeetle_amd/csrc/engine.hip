@@ -1721,7 +1721,7 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     s->walk_longest = g.walk[7];
     s->walk_crit_windows = g.walk[8];
     s->walk_crit_blocks = g.walk[9];
-    s->walk_crit_loop_ms = E->wall_khz ? (double)g.walk[10] / E->wall_khz : 0.0;
+    s->walk_crit_wait_ms = E->wall_khz ? (double)g.walk[10] / E->wall_khz : 0.0;
     s->walk_crit_ms = E->wall_khz ? (double)g.walk[11] / E->wall_khz : 0.0;
     for (int k = 0; k < 4; k++) s->walk_dbg[k] = g.walk_dbg[k];
     return TBGPU_STATUS_OK;

@@ -622,6 +622,7 @@ struct WalkRec {
 #ifndef WALK_HEAVY
 #define WALK_HEAVY 256
 #endif
+#define WALK_RING 8  // windows a feeder wave keeps ahead of its walker in LDS
 
 #define WALK_BIG (1LL << 62)  // a position whose outcome is known: "always" (+) / "never" (−)
 
@@ -798,16 +799,77 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
     const u64 vmask = n == 64 ? ~0ULL : ((1ULL << n) - 1);
     u64 okm = 0;  // lane j's outcome in the walk (a check's own verdict)
     u32 j = s, m = n, pub = s;  // [s, pub): published while waiting in place
-    const u64 ta = wall_clock64();
+    // A waiting walker goes past a Y leg whose unit is still open: the leg is PENDING (pmask), its
+    // amount in dp, and d stays the sum without it.  A later check is decided if it decides the same
+    // way with and without every pending credit (d and d + dp); only a check that it would flip
+    // waits — for the pending units, not for the first of them.
+    u64 pmask = 0;
+    i64 dp = 0;
+    auto publish_to = [&](u32 upto) {  // this window's checks in [pub, upto)
+        if (check && valid && lane >= pub && lane < upto) {
+            const u32 mine = (okm >> lane) & 1 ? BV_PASS : BV_FAIL;
+            fl_st32(&F.b_st[r.u], cr ? fl_combine(oth, mine) : fl_combine(mine, oth));
+        }
+        pub = max(pub, upto);
+    };
+    auto settle = [&]() {  // the pending units decided by now: their amounts leave dp (and ok ones enter d)
+        u32 sx = BS_UNK;
+        if ((pmask >> lane) & 1) sx = fl_ld32(&F.b_st[r.u]);
+        const bool known = ((pmask >> lane) & 1) && sx != BS_UNK;
+        const u64 km = __ballot(known);
+        if (!km) return;
+        u64 okv = known && sx == BS_OK ? (u64)r.a : 0, allv = known ? (u64)r.a : 0;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            okv += __shfl_xor((unsigned long long)okv, off);
+            allv += __shfl_xor((unsigned long long)allv, off);
+        }
+        d += (i64)fl_rl64(okv, 0);
+        dp -= (i64)fl_rl64(allv, 0);
+        pmask &= ~km;
+    };
+    auto wait_until = [&](auto decided) {  // publish, then poll the pending units until decided()
+        publish_to(j);
+        ws.blocks++;
+        const u64 w0 = fl_now();
+        settle();
+        while (!decided()) {
+            __builtin_amdgcn_s_sleep(1);
+            settle();
+            if (__builtin_amdgcn_readfirstlane(!decided() && (fl_expired(F, w0) || fl_stalled(g)))) {
+                if (lane == 0) tb_panic(g, PANIC_FLOW_STALL);
+                pmask = 0;  // give up (the pass is lost to the panic)
+                dp = 0;
+                break;
+            }
+        }
+        ws.block_ticks += fl_now() - w0;
+    };
     while (j < n) {
         const u64 bar = ~smask & vmask & (~0ULL << j);
         const u32 b = bar ? (u32)__builtin_ctzll(bar) : n;
+        while (pmask && j < b) {  // bounded walk: d without the pending credits, d + dp with them
+            const i64 vj = (i64)fl_rl64((u64)v, j), dj = (i64)fl_rl64((u64)dl, j);
+            const bool lo = (i64)((u64)vj + (u64)d) >= 0, hi = (i64)((u64)vj + (u64)d + (u64)dp) >= 0;
+            if (lo != hi) {
+                wait_until([&]() {
+                    return !pmask || ((i64)((u64)vj + (u64)d) >= 0) == ((i64)((u64)vj + (u64)d + (u64)dp) >= 0);
+                });
+                continue;
+            }
+            if (lo) {
+                d += dj;
+                okm |= 1ULL << j;
+            }
+            j++;
+        }
         fl_walk_run(v, dl, j, b, d, okm);
         j = b;
         if (b == n) break;
         // Position b: its partner was open when the window loaded.
         ws.stops++;
         const u32 bu = __builtin_amdgcn_readlane(r.u, b), bk = __builtin_amdgcn_readlane(r.kind, b);
+        if ((bk & BT_X) && pmask) wait_until([&]() { return !pmask; });  // a paired check needs the exact d
         const i64 ba = (i64)fl_rl64((u64)r.a, b);
         const i64 bb = (i64)fl_rl64((u64)r.base, b);
         // The unit's status now: a paired check ORs this side's verdict in first (whoever completes
@@ -832,6 +894,12 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         u32 fin = poll();
         // A paired check whose own side failed moves nothing here, whatever the other side says.
         const bool moot = (bk & BT_X) && !side_ok;
+        if (fin == BS_UNK && !(bk & BT_X) && wait) {  // an open Y leg: pending (above)
+            pmask |= 1ULL << b;
+            dp += ba;
+            j = b + 1;
+            continue;
+        }
         if (fin == BS_UNK && !moot && wait) {
             // Publish what this window decided so far (the partner may be waiting on it), then wait.
             if (check && valid && lane >= pub && lane < b) {
@@ -860,7 +928,7 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         if (fin == BS_OK) d += (bk & BT_X) ? -ba : ba;
         j = b + 1;
     }
-    ws.loop_ticks += wall_clock64() - ta;
+    if (pmask) wait_until([&]() { return !pmask; });  // the window leaves with an exact d
     ws.windows++;
     // Publish the checks walked in the scalar loop, once per window: a status poll issued after a
     // store waits for it (vmcnt counts both), so publishing in smaller pieces ahead of the stops
@@ -1123,7 +1191,6 @@ __device__ static inline u32 fl_walk_hot_window64(const FlowArgs& F, const HotRe
 // (WALK_RING windows ahead), so the walker itself issues no global load: its only memory operations
 // are LDS reads of its windows and the fire-and-forget status stores (a load behind those would
 // wait for them).  ctl[0]: windows filled, ctl[1]: windows consumed (N windows: the walker quit).
-#define WALK_RING 8
 __device__ static inline void fl_walk_merged(const FlowArgs& F, Globals* g, const HotRec* H, u32 N, WalkStats& ws,
                                              u32* ctl, HotRec* ring) {
     const u32 lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1335,17 +1402,21 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
         lw = G >= 2 ? (blockIdx.x - 1) * (NT / 64) + wave : wave - 2;
         LW = G >= 2 ? (G - 1) * (NT / 64) : NT / 64 - 2;
     } else if (split) {
+        u32 len = 0;
         if (blockIdx.x < NH && wave == 0) {
             heavy_walker = true;
             const u32 k = hv[blockIdx.x];
-            const u32 s0 = seg[k], len = seg[k + 1] - s0;
+            const u32 s0 = seg[k];
+            len = seg[k + 1] - s0;
             fl_walk_heavy(F, g, R, s0, len, ws);
+        }
+        if (heavy_walker) {
             if (lane == 0) {
                 atomicAdd((unsigned long long*)&g->walk[2], (unsigned long long)len);
                 if (len == *(volatile u32*)&F.words[FW_WMAX]) {  // the critical walker: the longest segment
                     atomicAdd((unsigned long long*)&g->walk[8], (unsigned long long)ws.windows);
                     atomicAdd((unsigned long long*)&g->walk[9], (unsigned long long)ws.blocks);
-                    atomicAdd((unsigned long long*)&g->walk[10], (unsigned long long)ws.loop_ticks);
+                    atomicAdd((unsigned long long*)&g->walk[10], (unsigned long long)ws.block_ticks);
                     atomicAdd((unsigned long long*)&g->walk[11], (unsigned long long)(fl_now() - w0));
                 }
             }

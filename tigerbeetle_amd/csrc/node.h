@@ -1180,7 +1180,7 @@ static int node_api_get_stats(TbNode* N, tbgpu_stats* s) {
         s->walk_longest = std::max(s->walk_longest, x.walk_longest);
         s->walk_crit_windows += x.walk_crit_windows;
         s->walk_crit_blocks += x.walk_crit_blocks;
-        s->walk_crit_loop_ms += x.walk_crit_loop_ms;
+        s->walk_crit_wait_ms += x.walk_crit_wait_ms;
         s->walk_crit_ms += x.walk_crit_ms;
     }
     return TBGPU_STATUS_OK;

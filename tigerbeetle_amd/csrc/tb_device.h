@@ -215,7 +215,7 @@ struct Globals {
     u64 flow_exec_ticks;      // tb_flow run: lanes' time executing units, summed over lanes
     u64 walk[12];             // fl_walk: segments, heavy segments; over the heavy walkers: positions,
                               // windows, partner stops, blocked returns, blocked ticks; the longest segment;
-                              // the critical (longest-segment) walker's windows, blocks, loop and total ticks
+                              // the critical (longest-segment) walker's windows, waits, wait and total ticks
     u64 walk_dbg[4];          // fl_walk: what a walker that stalled was waiting on (diagnostics)
     u64 sweep_u64_passes;     // sweeps that ran in the u64 X/Y form (bound + S >= 2^63)
     u64 bounds_abandoned;     // passes whose bounds did not converge in FLOW_BOUNDS_ROUNDS_MAX rounds
