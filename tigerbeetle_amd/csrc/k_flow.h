@@ -848,6 +848,28 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
     while (j < n) {
         const u64 bar = ~smask & vmask & (~0ULL << j);
         const u32 b = bar ? (u32)__builtin_ctzll(bar) : n;
+        // Bounded walk while credits are pending: d without them, d + dp with them.  In 32 bits when
+        // the stretch's moves and the pending credits stay below 2^29 (amounts below 2^22): v + d
+        // clamped to +-2^29 keeps both signs.
+        if (pmask && j < b && dp < (1LL << 28) &&
+            !__ballot(lane >= j && lane < b && (dl >= (1LL << 22) || dl <= -(1LL << 22)))) {
+            const i64 vv = (i64)((u64)v + (u64)d);
+            const int v32 = (int)(vv > (1LL << 29) ? (1LL << 29) : vv < -(1LL << 29) ? -(1LL << 29) : vv);
+            const int d32 = (int)dl, p32 = (int)dp;
+            int dd = 0;
+            u32 i = j;
+            for (; i < b; i++) {
+                const int vi = __builtin_amdgcn_readlane(v32, i), di = __builtin_amdgcn_readlane(d32, i);
+                if (vi + dd >= 0) {
+                    dd += di;
+                    okm |= 1ULL << i;
+                } else if (vi + dd + p32 >= 0) {
+                    break;  // the pending credits could flip it
+                }
+            }
+            d += dd;
+            j = i;
+        }
         while (pmask && j < b) {  // bounded walk: d without the pending credits, d + dp with them
             const i64 vj = (i64)fl_rl64((u64)v, j), dj = (i64)fl_rl64((u64)dl, j);
             const bool lo = (i64)((u64)vj + (u64)d) >= 0, hi = (i64)((u64)vj + (u64)d + (u64)dp) >= 0;
