@@ -694,7 +694,6 @@ __device__ static inline void fl_walk_status(const FlowArgs& F, const WalkRec& r
 
 struct WalkStats {
     u64 windows = 0, stops = 0, blocks = 0, loop_ticks = 0, block_ticks = 0;
-    u64 runs = 0, run_cycles = 0, stop_cycles = 0, window_cycles = 0;
 };
 
 // One step of the 32-bit chain on the scalar unit: t = v + dc; if t >= 0 { dc += e; okm |= bit }.
@@ -1157,14 +1156,11 @@ __device__ static inline u32 fl_walk_hot_window(const FlowArgs& F, const HotRec&
     int rel = 0;
     u64 okm = 0;  // the simple units' outcomes
     u32 m = n;
-    const u64 cw = clock64();
     for (u32 j = s; j < n;) {
         // j starts a stretch: units j .. e - 1 on one segment, or a unit on its own.
         const u32 cur = __builtin_amdgcn_readlane(hs, j);
         if (!cur) {
-            const u64 c1 = clock64();
             const bool ok = fl_walk_hot_unit(F, r, j, dreg, rel, ws);
-            ws.stop_cycles += clock64() - c1;
             if (!ok) {
                 m = j;  // waits on a light walker
                 break;
@@ -1172,18 +1168,14 @@ __device__ static inline u32 fl_walk_hot_window(const FlowArgs& F, const HotRec&
             j++;
             continue;
         }
-        const u64 c0 = clock64();
-        ws.runs++;
         const u64 next = sw & ~((2ULL << j) - 1);
         const u32 e = next ? (u32)__builtin_ctzll(next) : n;
         int dc = __builtin_amdgcn_readlane(rel, cur - 1);
         fl_chain32(v32, d32, j, e, dc, okm);
         j = e;
         if (lane == cur - 1) rel = dc;
-        ws.run_cycles += clock64() - c0;
     }
     dreg += rel;
-    ws.window_cycles += clock64() - cw;
     ws.windows++;
     // Publish the checks walked in the scalar loop.
     if (check && lane < m) {
