@@ -216,11 +216,11 @@ __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
 // pass (the replica's commit) would issue all 16K atomics of its prepare from a single CU.
 __global__ __launch_bounds__(256) void tb_apply_events(PassArgs P) {
     const u32 pe = blockIdx.x * 256 + threadIdx.x;
+    u128 S;
+    bool cert_global, cert64;
+    tb_pass_cert(P, S, cert_global, cert64);  // every lane (a wave-wide sum)
     if (pe >= P.n) return;
     const u32 info = P.info[pe];
     if ((info & HZ_DEP) || (info & 0xFF) != R_OK || !(info & HZ_ACCTS)) return;
-    u128 S;
-    bool cert_global, cert64;
-    tb_pass_cert(P, S, cert_global, cert64);
     tb_apply_transfer(P, pe, info, P.eflags[pe], cert64);
 }

@@ -216,16 +216,29 @@ __global__ __launch_bounds__(64) void tb_reply_out(const u64* batch_off, u32 nb,
     u64* head = (u64*)arena;
     u32* rb = (u32*)(arena + 16);
     const u32 k = blockIdx.x;
+    // Loaded before the first store: a load issued after stores into the mapped arena would wait
+    // for their PCIe round trip (gfx950's vmcnt counts stores too).
+    const u32 bytes = k < nb ? reply_bytes[k] : 0;
+    const u64 boff = k < nb ? batch_off[k] : 0;
     if (k == 0 && threadIdx.x == 0) {
         head[0] = g->panic;
         head[1] = g->commit_timestamp;
     }
     if (k < nb) {
-        const u32 bytes = reply_bytes[k];
         if (threadIdx.x == 0) rb[k] = bytes;
-        u32* out = (u32*)(arena + 16 + (u64)nb * 4 + 8 * batch_off[k]);  // 4-B aligned: nb words before
-        const u32* in = results + 2 * batch_off[k];
-        for (u32 w = threadIdx.x; w < bytes / 4; w += 64) out[w] = in[w];
+        u32* out = (u32*)(arena + 16 + (u64)nb * 4 + 8 * boff);  // 4-B aligned: nb words before
+        const u32* in = results + 2 * boff;
+        // Eight loads in flight before their stores (each store into the arena is a PCIe write).
+        const u32 nw = bytes / 4;
+        for (u32 w0 = threadIdx.x; w0 < nw; w0 += 8 * 64) {
+            u32 v[8];
+#pragma unroll
+            for (u32 q = 0; q < 8; q++) v[q] = w0 + q * 64 < nw ? in[w0 + q * 64] : 0;
+#pragma unroll
+            for (u32 q = 0; q < 8; q++) {
+                if (w0 + q * 64 < nw) out[w0 + q * 64] = v[q];
+            }
+        }
     }
     if (seq) {  // one wave: its stores drain, then the flag
         __threadfence_system();

@@ -263,11 +263,11 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     if (threadIdx.x == 0) {
         s_applied = 0;
         s_failed = 0;
-        if (blockIdx.x == 0) {  // the replay kernel's per-pass counters (k_flow.h)
-            for (u32 k = 0; k < FL_BAR_GROUPS + 2; k++) T.g->flow_bar[FL_BAR_STRIDE * k] = 0;
-            if (P.flow_words) for (u32 k = 0; k < FLOW_WORDS; k++) P.flow_words[k] = 0;
-        }
     }
+    // The prepare's first timestamp, loaded before any global store of this kernel: on gfx950 a
+    // load waits for every earlier store of its wave to complete (vmcnt counts both), so a load
+    // left between the per-event stores below would serialise them.
+    const u64 ts0 = P.routed ? 0 : P.batch_ts[b] - L + 1;
     // a. classify.  Each thread owns events tid + k*RESOLVE_THREADS; their scratch words are loaded
     // for every k before any is used (one memory round trip instead of one per k).
     u32 r_info[RESOLVE_K];
@@ -386,7 +386,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                 if (fin == TB_CODE_PANIC) tb_panic(T.g, PANIC_ASSERT);
                 s_code[i] = (u8)fin;
                 P.info[pe] = (info & 0xFFFFFF00u) | fin | (eval_ok ? HZ_EVAL_OK : 0);
-                const u64 ts = tb_event_ts(P, b, boff, L, i);
+                const u64 ts = P.routed ? tb_event_ts(P, b, boff, L, i) : ts0 + i;
                 if (eval_ok) tsmax = ts;  // increasing in i
                 if (fin == R_OK) {
                     if (OP == OP_CREATE_TRANSFERS) {
@@ -443,6 +443,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+        if (blockIdx.x == 0) {  // the replay kernel's per-pass counters (k_flow.h), after every load
+            for (u32 k = 0; k < FL_BAR_GROUPS + 2; k++) T.g->flow_bar[FL_BAR_STRIDE * k] = 0;
+            if (P.flow_words) for (u32 k = 0; k < FLOW_WORDS; k++) P.flow_words[k] = 0;
+        }
         u64 mm = 0;
         for (u32 k = 0; k < RESOLVE_THREADS / 64; k++) mm = max(mm, s_tsmax[k]);
         if (mm) atomicMax((unsigned long long*)&T.g->commit_timestamp, (unsigned long long)mm);

@@ -250,6 +250,7 @@ __device__ static inline void tb_dedup_mark(const PassArgs& P) {
 __global__ __launch_bounds__(256) void tb_pass_clear(u64* dedup, u64 cap, u64* sum_shards, const Globals* g, u32 epoch,
                                                      u32 force, u32* leg_tot, u32 leg_buckets, u64* meta, u64 m0, u64 m1,
                                                      u64 m2) {
+    const u64 w = g->dedup_dirty;  // before the stores (a load after them waits for them)
     if (blockIdx.x == 0 && threadIdx.x < SUM_WORDS) sum_shards[threadIdx.x] = 0;
     if (meta && blockIdx.x == 0 && threadIdx.x == 0) {
         meta[0] = m0;
@@ -259,7 +260,6 @@ __global__ __launch_bounds__(256) void tb_pass_clear(u64* dedup, u64 cap, u64* s
     if (blockIdx.x == 0 && leg_tot) {
         for (u32 k = threadIdx.x; k <= leg_buckets; k += 256) leg_tot[k] = 0;
     }
-    const u64 w = g->dedup_dirty;
     u64 n = 0;
     if (force) n = cap;
     else if ((u32)(w >> 8) == epoch - 1 && w != 0) n = min(cap, 1ULL << (w & 255));
@@ -275,13 +275,42 @@ __device__ static inline u128 tb_sum_total(const u64* shards) {
     return s;
 }
 
+// The same sum over the lanes of a wave: lane l loads shard l and a butterfly of saturating adds
+// leaves the total in every lane.  Saturating addition of non-negative values is exact up to the
+// first carry out of 128 bits and sticky after it, so any order gives min(true sum, maxInt) as the
+// sequential loop does.  Every lane of the wave must call it (all 64 active).  It replaces 64
+// dependent u128 adds on the scalar unit per wave (one scalar unit serves all 16 waves of a
+// 1024-thread workgroup's CU).
+__device__ static inline u128 tb_sum_total_wave(const u64* shards) {
+    static_assert(SUM_SHARDS == 64, "one shard per lane");
+    if (shards[PW_HUGE]) return TB_U128_MAX;
+    const u32 lane = threadIdx.x & 63;
+    u64 lo = shards[2 * lane], hi = shards[2 * lane + 1];
+    u32 sat = 0;
+#pragma unroll
+    for (u32 off = 1; off < 64; off <<= 1) {
+        const u64 olo = __shfl_xor((unsigned long long)lo, off), ohi = __shfl_xor((unsigned long long)hi, off);
+        sat |= __shfl_xor(sat, off);
+        u128 r;
+        sat |= tb_add_overflows(tb_u128(lo, hi), tb_u128(olo, ohi), &r) ? 1u : 0u;
+        lo = tb_lo(r);
+        hi = tb_hi(r);
+    }
+    // Equal in every lane: take lane 0's words as wave-uniform (scalar) values.
+    const u32 l0 = __builtin_amdgcn_readfirstlane((u32)lo), l1 = __builtin_amdgcn_readfirstlane((u32)(lo >> 32));
+    const u32 h0 = __builtin_amdgcn_readfirstlane((u32)hi), h1 = __builtin_amdgcn_readfirstlane((u32)(hi >> 32));
+    if (__builtin_amdgcn_readfirstlane(sat)) return TB_U128_MAX;
+    return tb_u128(((u64)l1 << 32) | l0, ((u64)h1 << 32) | h0);
+}
+
 // The pass's overflow certificate (k_resolve.h header).  Every kernel of the pass between validate
 // and replay computes the same answer: S is final after validate and `bound` only moves at the end
 // of the replay kernel.
 //   cert_global: bound + S fits in u128 — no overflow check of create_transfer can fire;
 //   cert64:      bound + S < 2^64 — no balance word can carry this pass.
+// Every lane of the calling wave must call it (tb_sum_total_wave).
 __device__ static inline void tb_pass_cert(const PassArgs& P, u128& S, bool& cert_global, bool& cert64) {
-    S = tb_sum_total(P.sum_shards);
+    S = tb_sum_total_wave(P.sum_shards);
     u128 r;
     // S saturates at maxInt(u128) (and the HUGE word reads as maxInt): such an S is a lower bound
     // of the true sum, not an upper one, so it certifies nothing.

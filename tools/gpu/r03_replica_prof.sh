@@ -3,9 +3,9 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 R=$GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-mkdir -p gpurun_out/r03
+mkdir -p gpurun_out/r03c
 cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $R/gpurun_out/r03/rp_trace -o run -- \
-  $R/tigerbeetle_amd/host/tb_replica_bench --accounts 1000000 --prepares 300 --warmup 20 > $R/gpurun_out/r03/rp_trace.log 2>&1
-echo "rc=$?"; grep call_path $R/gpurun_out/r03/rp_trace.log
-find $R/gpurun_out/r03/rp_trace -name "*.csv" | head
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $R/gpurun_out/r03c/rp_trace -o run -- \
+  $R/tigerbeetle_amd/host/tb_replica_bench --accounts 1000000 --prepares 300 --warmup 20 > $R/gpurun_out/r03c/rp_trace.log 2>&1
+echo "rc=$?"; grep call_path $R/gpurun_out/r03c/rp_trace.log
+find $R/gpurun_out/r03c/rp_trace -name "*.csv" | head
