@@ -279,14 +279,21 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         r_fl[k] = i < L ? P.eflags[pbase + i] : (u16)0;
     }
     bool local_linked = false, local_dep = false;
+    // With every pass-wide condition of tb_classify off (uniform), what is left of it is a test of
+    // the event's own bits, computed without branches (a 1024-thread workgroup's divergent branches
+    // cost scalar instructions on its CU's one scalar unit).  Lanes past L hold info 0: not
+    // dependent, not linked, and their LDS words (i < BATCH_LDS) are never read.
+    const bool fast_cls = OP == OP_CREATE_TRANSFERS && !P.seq_pv && !any_dup && !any_pv && !any_bal && cert_global;
 #pragma unroll
     for (u32 k = 0; k < RESOLVE_K; k++) {
         const u32 i = k * RESOLVE_THREADS + threadIdx.x;
-        if (i >= L) continue;
+        if (!fast_cls && i >= L) continue;
         const u32 pe = pbase + i;
         const u32 info = r_info[k];
         const u32 code = info & 0xFF;
-        const bool dep = tb_classify<OP>(P, pe, info, code, S, cert_global, any_dup, any_bal, any_pv);
+        const bool dep = fast_cls ? ((info & HZ_SELFDEP) != 0) |
+                                        (((info & HZ_ACCTS) != 0) & (code == R_OK) & ((info & (HZ_BAL | HZ_LIMIT)) != 0))
+                                  : tb_classify<OP>(P, pe, info, code, S, cert_global, any_dup, any_bal, any_pv);
         const bool linked = r_fl[k] & 1;
         local_linked |= linked;
         local_dep |= dep;
@@ -349,6 +356,45 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     u32 ndep = 0, n_app = 0, n_fail = 0;  // per thread, summed per wave below (one LDS atomic per wave)
     u32 legmask = 0;  // bit k: this thread's event k contributes two legs
     u32* dep_out = P.dep_list + pbase;
+    // No chain and no dependent event (uniform): every final result is the intrinsic code, already
+    // in s_code; the loop below without its chain and dependent cases, branch-light.
+    if (OP == OP_CREATE_TRANSFERS && !any_linked && !any_dep) {
+        u32 panic = 0;
+#pragma unroll
+        for (u32 k = 0; k < RESOLVE_K; k++) {
+            const u32 i = k * RESOLVE_THREADS + threadIdx.x;
+            const bool valid = i < L;
+            const u32 pe = pbase + i;
+            const u32 info = r_info[k];
+            const u32 code = info & 0xFF;
+            const bool ok = valid & (code == R_OK);
+            panic |= code == TB_CODE_PANIC;
+            if (valid) P.info[pe] = info | (ok ? HZ_EVAL_OK : 0);
+            const u64 ts = P.routed ? (valid ? tb_event_ts(P, b, boff, L, i) : 0) : ts0 + i;
+            tsmax = ok ? ts : tsmax;
+            n_app += ok;
+            n_fail += valid & !ok;
+            if (ok) {
+                if (use_legs && !(info & HZ_POSTVOID) && r_amt[k][1] == 0 && r_amt[k][0] <= LEG_AMT_MASK) {
+                    const u32 drs = r_dr[k], crs = r_cr[k];
+                    const u64 pend = (r_fl[k] & TF_PENDING) ? 0 : 1;  // field: pending / posted
+                    const u32 mask = (1u << P.leg_shift) - 1;
+                    P.leg_ev[2 * (u64)pe] = ((((u64)(drs & mask) << 2) | pend) << LEG_AMT_BITS) | r_amt[k][0];
+                    P.leg_ev[2 * (u64)pe + 1] = ((((u64)(crs & mask) << 2) | 2 | pend) << LEG_AMT_BITS) | r_amt[k][0];
+                    if (!TB_ABL(P, ABL_LEG_WORK)) {
+                        tb_hist16_inc(s_hist, drs >> P.leg_shift);
+                        tb_hist16_inc(s_hist, crs >> P.leg_shift);
+                    }
+                    legmask |= 1u << k;
+                } else if (!P.apply_late) {
+                    tb_apply_transfer(P, pe, info, r_fl[k], cert64);
+                }
+            } else if (valid && (info & HZ_SPEC)) {
+                tb_xindex_tombstone(T, P.rs[pe]);  // a failed event's speculative record
+            }
+        }
+        if (panic) tb_panic(T.g, PANIC_ASSERT);
+    } else {
 #pragma unroll
     for (u32 k = 0; k < RESOLVE_K; k++) {
         const u32 i = k * RESOLVE_THREADS + threadIdx.x;
@@ -426,6 +472,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
             if (dep) dep_out[ndep + r] = i;
             ndep += total;
         }
+    }
     }
 
     // commit_timestamp: max over events that returned ok when evaluated (:763, :882, :1012).
