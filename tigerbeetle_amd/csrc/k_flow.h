@@ -428,14 +428,19 @@ __device__ static inline void fl_finish(const PassArgs& P, u8* s_code, u32* s_wa
             __syncthreads();
         }
     }
-    if (close && threadIdx.x == 0) {
-        if (tsmax_block > g->commit_timestamp) g->commit_timestamp = tsmax_block;
-        const u128 S = tb_sum_total(P.sum_shards);
-        const u128 nb2 = tb_sat_add(tb_u128(g->bound_lo, g->bound_hi), S);
-        g->bound_lo = tb_lo(nb2);
-        g->bound_hi = tb_hi(nb2);
-        g->dependent_all += g->dependent_total;
-        g->dependent_total = 0;
+    if (close && threadIdx.x < 64) {
+        const u128 S = tb_sum_total_wave(P.sum_shards);  // wave 0, every lane
+        if (threadIdx.x == 0) {
+            // Every load before the first store (a load after a store waits for it).
+            const u64 blo = g->bound_lo, bhi = g->bound_hi, da = g->dependent_all, dt = g->dependent_total;
+            // Other workgroups' atomicMax of their own maxima may still be in flight: max, not a store.
+            if (tsmax_block) atomicMax((unsigned long long*)&g->commit_timestamp, (unsigned long long)tsmax_block);
+            const u128 nb2 = tb_sat_add(tb_u128(blo, bhi), S);
+            g->bound_lo = tb_lo(nb2);
+            g->bound_hi = tb_hi(nb2);
+            g->dependent_all = da + dt;
+            g->dependent_total = 0;
+        }
     }
 }
 
