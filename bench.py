@@ -25,7 +25,8 @@ rank-major.  Per-GPU work is fixed as N grows: scaling is weak.
 The JSON line also carries:
   roofline      the dominant kernel's algorithmic bytes per launch / its average launch time
                 (HIP events on the engine stream, inside the timed steps) against 8 TB/s;
-                `traffic` comes from profiles/pmc_<round>.json (rocprofv3 PMC) when present.
+                `traffic` (HBM bytes per launch) comes from perf/pmc_r04.json (rocprofv3 PMC passes,
+                tools/gpu/r04_prof.sh), with rocprof's mean launch time of the same kernel beside it.
   cpu_baseline  the C oracle (reference semantics restated, single thread) timed on this host on
                 a bounded prefix of the same workload.
   parity        the same prefix committed on the GPU from a fresh state and compared with the
@@ -327,7 +328,8 @@ def run_secondary(args, kind, device):
     # The ordered fallback (tb_flow) has no byte roofline (it is bound by its dependency rounds):
     # the roofline is the validate kernel's; tb_flow's time share is reported beside it.
     roof = roofline(stats, expected_unique(n_acct, 2 * per_launch) / per_launch, per_launch,
-                    argparse.Namespace(transfers=n_xfer, steps=1), step_ms[0], None, kernel="tb_transfers_validate")
+                    argparse.Namespace(transfers=n_xfer, steps=1), step_ms[0], None, kernel="tb_transfers_validate",
+                    pmc=False)
     roof["flow_ms_share"] = round(stats["ms_replay"] / step_ms[0], 4)
 
     # Parity: the first 1M transfers (the same prepares, same timestamps) on a fresh engine.
@@ -431,55 +433,36 @@ def cpu_model():
     return "nproc %d" % os.cpu_count()
 
 
-def load_pmc(kernel, transfers_per_launch=None):
-    """HBM traffic of `kernel` from the newest committed rocprofv3 PMC summary that has it, per
-    transfer and scaled to this run's launch size (the summary records its own)."""
-    prof_dir = os.path.join(ROOT, "profiles")
-    if not os.path.isdir(prof_dir):
-        return None
-    for name in sorted(os.listdir(prof_dir), reverse=True):
-        if name.startswith("pmc_") and name.endswith(".json"):
-            try:
-                d = json.load(open(os.path.join(prof_dir, name)))
-            except (OSError, ValueError):
-                continue
-            k = d.get("kernels", {}).get(kernel)
-            if not (k and "hbm_bytes_per_launch_raw" in k):
-                continue
-            tpl = d.get("transfers_per_launch")
-            out = {"source": "profiles/" + name,
-                   "counters": "FETCH_SIZE + WRITE_SIZE (raw; FETCH_SIZE may read up to 2x low on gfx950)"}
-            if tpl:
-                raw, x2 = k["hbm_bytes_per_launch_raw"] / tpl, k["hbm_bytes_per_launch"] / tpl
-                out.update({"bytes_per_transfer": round(raw, 1), "bytes_per_transfer_fetch_x2": round(x2, 1),
-                            "profiled_transfers_per_launch": tpl})
-                if transfers_per_launch:
-                    out["bytes_per_launch"] = round(raw * transfers_per_launch)
-                    out["bytes_per_launch_fetch_x2"] = round(x2 * transfers_per_launch)
-            else:
-                out.update({"bytes_per_launch": round(k["hbm_bytes_per_launch_raw"]),
-                            "bytes_per_launch_fetch_x2": round(k["hbm_bytes_per_launch"])})
-            return out
-    return None
+# The rocprofv3 evidence behind `roofline.traffic` (tools/gpu/r04_prof.sh -> tools/perf_pmc.py): per
+# kernel, HBM bytes per committed transfer from FETCH_SIZE / WRITE_SIZE passes and rocprof's mean
+# launch time, for the headline leg (64-prepare chunks from host memory) and for device-resident
+# passes.  It lives outside profiles/ so it travels to the GPU box with the tree.
+PMC_FILE = os.path.join("perf", "pmc_r04.json")
 
 
-def load_pmc_device(kernel, transfers_per_launch):
-    """HBM traffic of `kernel` in device-resident C2 passes (no host copy in flight), from the newest
-    committed profiles/*/device/pmc_device_c2.json (tools/gpu/device_pmc.py), per transfer and per
-    launch of this run."""
-    import glob
-    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "device", "pmc_device_c2.json")))
-    if not found:
-        return load_pmc(kernel, transfers_per_launch)
-    d = json.load(open(found[-1]))
-    k = d.get("kernels", {}).get(kernel)
-    if not k:
-        return None
-    return {"source": os.path.relpath(found[-1], ROOT),
-            "counters": "FETCH_SIZE + WRITE_SIZE (raw; FETCH_SIZE may read up to 2x low on gfx950)",
-            "bytes_per_transfer": k["raw_per_transfer"], "bytes_per_transfer_fetch_x2": k["fetch_x2_per_transfer"],
-            "bytes_per_launch": round(k["raw_per_transfer"] * transfers_per_launch),
-            "bytes_per_launch_fetch_x2": round(k["fetch_x2_per_transfer"] * transfers_per_launch)}
+def load_pmc(leg, kernel, transfers_per_launch):
+    """`traffic` fields of the roofline from PMC_FILE: HBM bytes per launch of `kernel` (raw FETCH_SIZE +
+    WRITE_SIZE per transfer x this run's transfers per launch), the doubled-FETCH figure, and rocprof's
+    mean launch time of the profiled launches.  Missing file or kernel: says so loudly (stderr and the
+    `traffic_error` field) and leaves traffic null."""
+    path = os.path.join(ROOT, PMC_FILE)
+    try:
+        d = json.load(open(path))
+        k = d["legs"][leg]["kernels"][kernel]
+        lt = d["legs"][leg]["launch_transfers"]
+    except (OSError, ValueError, KeyError) as e:
+        msg = "bench.py: no PMC traffic for %s/%s in %s (%s: %s)" % (leg, kernel, PMC_FILE, type(e).__name__, e)
+        print(msg, file=sys.stderr, flush=True)
+        return {"traffic": None, "traffic_error": msg}
+    out = {"traffic": round(k["raw_per_transfer"] * transfers_per_launch),
+           "traffic_fetch_x2": round(k["fetch_x2_per_transfer"] * transfers_per_launch),
+           "traffic_per_transfer": k["raw_per_transfer"], "traffic_fetch_x2_per_transfer": k["fetch_x2_per_transfer"],
+           "traffic_source": "%s legs.%s (rocprofv3 FETCH_SIZE + WRITE_SIZE, separate passes; %s)" % (
+               PMC_FILE, leg, d.get("source", ""))}
+    if k.get("rocprof_avg_ms"):
+        out["rocprof_avg_launch_ms"] = k["rocprof_avg_ms"]
+        out["rocprof_launch_transfers"] = lt
+    return out
 
 
 WORKLOAD_TEXT = {
@@ -659,7 +642,7 @@ def main():
     dev_ms = []
     engine.profile_mask(engine.PROF_VALIDATE | engine.PROF_PASS | engine.PROF_REPLAY)
     dev_stats = None
-    for step in range(1 + args.device_steps):
+    for step in range(1 + args.device_steps if args.device_steps else 0):
         engine.reset_transfers()
         ts, t_cursor = timestamps(xfer_lens, t_cursor + 10, wl["gap_every"])
         if step == 1:
@@ -813,12 +796,20 @@ def main():
         "failed_events": n_failed,
         "roofline": roof,
         "cpu_baseline": cpu,
-        "parity": parity,
         "host_commit": host,
         "replica_path": replica_path,
         "write_back": write_back,
         "secondary": secondary or None,
     }
+    # Last, so the end of the line (what a log tail keeps) carries the verdicts.
+    for kind, sec in (secondary or {}).items():
+        sp = sec["parity"]
+        parity[kind + "_sample_equal"] = bool(sp["replies_equal"] and sp["accounts_equal"] and sp["transfers_equal"]
+                                              and sp["posted_equal"])
+    line["parity"] = parity
+    line["headline"] = {"value": line["value"], "unit": "transfers/s", "p99_batch_latency_ms": line["p99_batch_latency_ms"],
+                        "roofline_frac": roof["frac"] if roof else None,
+                        "roofline_traffic": roof.get("traffic") if roof else None}
     if rank == 0:
         print(json.dumps(line), flush=True)
     engine.close()
@@ -949,7 +940,7 @@ def run_sharded(args, world, rank, local_rank):
     value = args.transfers * world * args.steps / (total_ms / 1e3)
     recv_per_launch = args.transfers / max(1, stats["launches_validate"] / max(1, args.steps))
     u_over_t = expected_unique(args.accounts, 2 * recv_per_launch) / recv_per_launch
-    roof = roofline(stats, u_over_t, recv_per_launch, args, total_ms)
+    roof = roofline(stats, u_over_t, recv_per_launch, args, total_ms, pmc=False)
     pcie_gbs = args.transfers * 128 * args.steps / (total_ms / 1e3) / 1e9
     line = {
         "metric": METRIC,
@@ -1039,8 +1030,10 @@ def run_node(args, procs, rank):
         dist.destroy_process_group()
         return
 
+    from tests.harness.configs import KINDS, SETTINGS
     from tigerbeetle_amd.state_machine import Engine, Options
 
+    wl = SETTINGS[args.workload]
     N = args.gpus
     devices = [0] * N if args.same_device else list(range(N))
     chunk = args.chunk_prepares
@@ -1057,7 +1050,8 @@ def run_node(args, procs, rank):
     dev_buf = engine.alloc(a_chunk * 128)
     for a0 in range(0, args.accounts, a_chunk):
         n_a = min(a_chunk, args.accounts - a0)
-        engine.generate_accounts(dev_buf, a0, n_a, seed=args.seed)
+        engine.generate_accounts(dev_buf, a0, n_a, seed=args.seed, limit_permille=wl["limit_permille"],
+                                 account_count=args.accounts, hot_limited=wl.get("hot_limited", 0))
         host = engine.to_host(dev_buf, n_a * 128)
         k0 = a0 // args.batch
         lens_a = batches(n_a, args.batch)
@@ -1098,7 +1092,8 @@ def run_node(args, procs, rank):
     k_pos = 0
     for x0 in range(0, T, x_chunk):
         n_x = min(x_chunk, T - x0)
-        engine.generate_transfers(gen, x0, n_x, args.accounts, seed=args.seed)
+        engine.generate_transfers(gen, x0, n_x, args.accounts, seed=args.seed, kind=KINDS[args.workload],
+                                  limit_permille=wl["limit_permille"], hot_limited=wl.get("hot_limited", 0))
         host = engine.to_host(gen, n_x * 128)
         while k_pos < n_prep and starts[k_pos + 1] <= x0 + n_x:
             a, b = int(starts[k_pos]) - x0, int(starts[k_pos + 1]) - x0
@@ -1117,7 +1112,7 @@ def run_node(args, procs, rank):
     for step in range(n_steps):
         timed = step >= args.warmup
         engine.reset_transfers()
-        ts, t_cursor = timestamps(lens, t_cursor + 10)
+        ts, t_cursor = timestamps(lens, t_cursor + 10, wl["gap_every"])
         if timed and step == args.warmup:
             engine.reset_stats()
         barrier()
@@ -1137,16 +1132,17 @@ def run_node(args, procs, rank):
     for buf in buffers:
         engine.unregister_host(buf)
     n_failed = int(rb.sum()) // 8
-    full_ok = bool(n_failed == 0 and stats["transfers"] == T and summ["debits_posted"] == summ["credits_posted"]
-                   and summ["debits_posted"] > 0 and summ["debits_pending"] == summ["credits_pending"]
-                   and summ["stray"] == 0 and summ["accounts"] == args.accounts)
+    full_ok = bool((n_failed == 0 or args.workload != "c2") and stats["transfers"] == T - n_failed
+                   and summ["debits_posted"] == summ["credits_posted"] and summ["debits_posted"] > 0
+                   and summ["debits_pending"] == summ["credits_pending"] and summ["stray"] == 0
+                   and summ["accounts"] == args.accounts)
     total_ms = sum(step_ms)
     value = T * args.steps / (total_ms / 1e3)
     lat = np.sort(np.concatenate(lat_all)) if lat_all else np.array([float("nan")])
     per_launch = T / max(1, stats["launches_validate"] / max(1, args.steps))
     u_over_t = expected_unique(args.accounts, 2 * per_launch) / per_launch
     roof = roofline(stats, u_over_t, per_launch, argparse.Namespace(transfers=T, steps=args.steps), total_ms,
-                    kernel="tb_transfers_validate")
+                    kernel="tb_transfers_validate", pmc=False)
     pcie_gbs = T * 128 * args.steps / (total_ms / 1e3) / 1e9
     line = {
         "metric": METRIC,
@@ -1162,9 +1158,11 @@ def run_node(args, procs, rank):
         "dtype": "u128",
         "data": "synthetic (generated on the GPU in the reference benchmark's shapes, copied to host memory before "
                 "timing)",
-        "config": {"workload": "C5 (BASELINE.json configs[4]): %d accounts, balances owner-partitioned by hash(id) over "
-                               "%d GPUs (records replicated), %d uniform transfers per GPU (%d in all), prepares of %d"
-                               % (args.accounts, N, args.transfers, T, args.batch),
+        "config": {"workload": ("C5 (BASELINE.json configs[4]): %d accounts, balances owner-partitioned by hash(id) over "
+                                "%d GPUs (records replicated), %d uniform transfers per GPU (%d in all), prepares of %d"
+                                % (args.accounts, N, args.transfers, T, args.batch)) if args.workload == "c2" else
+                               ("%s on %d GPUs: " % (args.workload, N)) + WORKLOAD_TEXT[args.workload] % (
+                                   args.accounts, T, args.batch),
                    "prepares_per_step": n_prep, "chunk_prepares_per_gpu": chunk,
                    "engine": "one tbgpu node engine (include/tbgpu.h tbgpu_config.devices = %s), driven by one "
                              "process; %d process(es) launched" % (devices, procs),
@@ -1180,6 +1178,8 @@ def run_node(args, procs, rank):
                  "frac": round(pcie_gbs / N / PCIE_PEAK_GBS, 4), "measured_ceiling": PCIE_MEASURED_GBS,
                  "frac_of_measured": round(pcie_gbs / N / PCIE_MEASURED_GBS, 4)},
         "failed_events": n_failed,
+        "passes": {"clean": stats["node_passes_clean"], "split": stats["node_passes_split"],
+                   "whole": stats["node_passes_whole"], "sequenced_events": stats["node_sequenced_events"]},
         "roofline": roof,
         "cpu_baseline": None,
         "parity": {"full_run_properties": full_ok, "ledger": {k: str(v) for k, v in summ.items()}},
@@ -1210,7 +1210,7 @@ def access_mix(engine, transfers, kernel_ms):
 
 
 def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=None, steps=None, kernel=None,
-             device=False):
+             device=False, pmc=True):
     """The dominant kernel of the timed steps against the HBM peak; `kernels` = every kernel's mean
     launch time (from the warmup steps when given: the timed steps time only validate, replay/flow
     and whole passes)."""
@@ -1244,14 +1244,24 @@ def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=No
     achieved = alg_bytes / avg_s / 1e9
     src = kernel_table(breakdown) if breakdown else kernels
     per_kernel = {k: {"launches": int(n), "avg_launch_ms": round(ms / n, 4)} for k, (ms, n) in src.items() if n}
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": (load_pmc_device if device else load_pmc)(dom, per_launch_transfers), "kernel": dom,
-            "kernels": per_kernel, "kernels_timed_in": "warmup steps (every kernel)" if breakdown else "timed steps",
-            "avg_launch_ms": round(ms_dom / n_dom, 4), "alg_bytes_per_transfer": round(alg_bytes / per_launch_transfers, 1),
-            "path_bytes_per_transfer": round(296 + 256 * u_over_t, 1),
-            "path_achieved_GBs": round((296 + 256 * u_over_t) * args.transfers * (steps or args.steps) / (total_ms / 1e3) / 1e9, 1)}
-
+    out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel": dom,
+           "avg_launch_ms": round(ms_dom / n_dom, 4), "transfers_per_launch": round(per_launch_transfers, 1),
+           "alg_bytes_per_transfer": round(alg_bytes / per_launch_transfers, 1),
+           "timing": "HIP events on the engine stream around every launch of the kernel in the timed steps"}
+    if pmc:  # the C2 launches the PMC runs profiled (not the C3/C4 lines)
+        out.update(load_pmc("device" if device else "headline", dom, per_launch_transfers))
+    if out.get("rocprof_avg_launch_ms"):
+        # The same definition from the committed rocprof summary: algorithmic bytes per transfer x the
+        # profiled launches' mean transfers / rocprof's mean launch duration.
+        rp = out["rocprof_avg_launch_ms"] / 1e3
+        out["frac_rocprof"] = round(alg_bytes / per_launch_transfers * out["rocprof_launch_transfers"] / rp / 1e9
+                                    / HBM_PEAK_GBS, 4)
+    out.update({"kernels": per_kernel, "kernels_timed_in": "warmup steps (every kernel)" if breakdown else "timed steps",
+                "path_bytes_per_transfer": round(296 + 256 * u_over_t, 1),
+                "path_achieved_GBs": round((296 + 256 * u_over_t) * args.transfers * (steps or args.steps)
+                                           / (total_ms / 1e3) / 1e9, 1)})
+    return out
 
 if __name__ == "__main__":
     main()

@@ -31,7 +31,19 @@
  *     been called that way), TBGPU_STATUS_PANIC (the reference would have trapped: an overflow
  *     assert, a failed invariant, `timestamp <= commit_timestamp`), or TBGPU_STATUS_DEVICE
  *     (a HIP error).  The Zig wrapper turns PANIC/DEVICE into @panic.
- *   - No allocation after tbgpu_init.
+ *   - No allocation after tbgpu_init: every device buffer, pinned host buffer and HIP event is
+ *     made there (tbgpu_debug_allocations, tbgpu_bench.h, counts them; tests/test_gpu_alloc.py
+ *     holds the commit, prefetch and write-back entry points to zero).
+ *   - A device panic (the reference would have trapped mid-commit) leaves state the reference
+ *     never reaches, so the engine stops: every later call that changes state returns
+ *     TBGPU_STATUS_PANIC until tbgpu_reset (or tbgpu_deinit).  Reads (exports, stats) still work.
+ *   - Device exclusivity: the ordered fallback kernel (tb_flow) synchronises its workgroups with a
+ *     software grid barrier, so its grid (at most a quarter of the CUs, shared among this process's
+ *     engines on the device) must be resident at once.  tbgpu_init checks that once (a probe grid
+ *     of the same shape must become co-resident within 200 ms) and fails with TBGPU_STATUS_DEVICE
+ *     on a device other work holds; one engine process per device is the supported deployment.
+ *     A co-tenant that arrives later and starves the grid makes a pass end in PANIC (every wait is
+ *     bounded, PANIC_FLOW_STALL), never a hang.
  */
 #ifndef TBGPU_H
 #define TBGPU_H
@@ -108,7 +120,10 @@ int tbgpu_commit(tbgpu_t* engine, uint8_t operation, uint64_t timestamp, const v
  * objects are HBM-resident; what is staged is the body: a create body in registered host memory
  * (tbgpu_register_host: the message pool) starts crossing PCIe by DMA at once, and the following
  * tbgpu_commit of the same body (same pointer and length) only waits for the copy.  Completes
- * immediately (the reference allows the callback inside the call, src/lsm/groove.zig:723-742). */
+ * immediately (the reference allows the callback inside the call, src/lsm/groove.zig:723-742).
+ * The staged copy belongs to the very next call only, if that call is tbgpu_commit of this body
+ * (the replica's prefetch(op) -> commit(op)); any other call drops it.  The body must not change
+ * between the two (a prepare message is immutable while its op commits, as in the reference). */
 int tbgpu_prefetch(tbgpu_t* engine, uint8_t operation, const void* input, uint32_t input_len);
 
 /* N consecutive prepares of the same create operation, pass_batches_max prepares per device pass
@@ -178,7 +193,24 @@ int tbgpu_checkpoint_delta(tbgpu_t* engine, void* accounts_out, void* accounts_b
                            tbgpu_delta_counts* counts);
 /* accounts_before_out (nullable, 64 B per account): {dp, dpost, cp, cpost} as of the previous
  * write-back (zero for accounts created since) — the old object a groove upsert diffs the balance
- * index trees against (src/lsm/groove.zig:925-963). */
+ * index trees against (src/lsm/groove.zig:925-963).
+ * The buffers are checked before anything runs against what the write-back can emit at most
+ * (transfers and posted entries: the transfer-log positions written since; accounts: two per such
+ * position plus the listed creates, or every live account after creates the engine could not list):
+ * a refused call returns those sizes in *counts and changes nothing. */
+
+/* The same write-back without the wait (StateMachine.compact is asynchronous,
+ * src/state_machine.zig:542-567; the replica's compact stage, src/vsr/replica.zig:3088-3091): the
+ * delta is taken in stream order with the commits (the next commits follow it) and crosses PCIe
+ * into the caller's buffers beside them.  tbgpu_checkpoint_delta_wait returns the counts once the
+ * objects have landed (transfers and posted entries sorted as above); until then the buffers belong
+ * to the engine, and no other write-back may start.  Needs buffers registered with
+ * tbgpu_register_host and large enough for the bounds above; otherwise (or past one slice of the
+ * engine's write-back buffers) the call runs the synchronous write-back and the wait returns at
+ * once.  Single-device engines only. */
+int tbgpu_checkpoint_delta_async(tbgpu_t* engine, void* accounts_out, void* accounts_before_out, uint64_t accounts_cap,
+                                 void* transfers_out, uint64_t transfers_cap, uint64_t* posted_out, uint64_t posted_cap);
+int tbgpu_checkpoint_delta_wait(tbgpu_t* engine, tbgpu_delta_counts* counts);
 
 /* Replica restart (StateMachine.open, src/state_machine.zig:322-334, then WAL replay from the
  * checkpoint): the HBM tables start empty while the forest holds the checkpointed objects.  The
@@ -239,6 +271,15 @@ typedef struct tbgpu_stats {
     uint64_t walk_crit_windows, walk_crit_blocks;
     double walk_crit_wait_ms, walk_crit_ms;
     uint64_t walk_dbg[4]; /* diagnostics: a stalled walker's kind | segment, unit, status, verdict bits */
+    /* With TBGPU_CONFIG_PROFILE, the device clock of the launch itself (s_memrealtime): from the
+     * first workgroup's start to the last workgroup's end, summed over launches, for validate,
+     * resolve and apply (the HIP-event times above also hold the dispatch of each launch). */
+    double span_ms[3];
+    uint64_t span_launches[3];
+    /* Node engines: create_transfers passes routed whole (clean), split (the dependent subsequence
+     * committed by the sequencer, the rest routed), or sequenced whole (no overflow certificate);
+     * events the sequencer committed. */
+    uint64_t node_passes_clean, node_passes_split, node_passes_whole, node_sequenced_events;
 } tbgpu_stats;
 
 int tbgpu_get_stats(tbgpu_t* engine, tbgpu_stats* stats);

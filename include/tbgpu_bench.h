@@ -90,6 +90,11 @@ int tbgpu_copy_to_device(tbgpu_t* engine, void* dst_dev, const void* src, uint64
 int tbgpu_marker(tbgpu_t* engine, uint32_t slot);          /* slot < 16 */
 double tbgpu_marker_elapsed_ms(tbgpu_t* engine, uint32_t a, uint32_t b);
 
+/* Device allocations, pinned host allocations and HIP events the library has made so far (every
+ * engine of the process): a test reads it around commits to hold tbgpu.h's "no allocation after
+ * tbgpu_init". */
+uint64_t tbgpu_debug_allocations(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,236 @@
+"""The engine's conventions (include/tbgpu.h): no allocation after tbgpu_init on the commit,
+prefetch and write-back entry points; a prefetch-staged body belongs to the very next commit only;
+a device panic stops the engine until tbgpu_reset; kernel launch spans on the device clock; and the
+asynchronous write-back returns exactly what the synchronous one does, however many commits run
+while it is in flight."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from tests.harness.oracle import OracleEngine
+from tests.harness.workload import Scenario, make_scenario, run_many, run_oracle
+from tests.test_gpu_differential import CONFIGS
+from tigerbeetle_amd import _lib
+from tigerbeetle_amd._lib import EnginePanic
+from tigerbeetle_amd.types import ACCOUNT_DTYPE, TRANSFER_DTYPE, TransferFlags
+
+pytestmark = pytest.mark.gpu
+
+
+def allocations():
+    return int(_lib.load().tbgpu_debug_allocations())
+
+
+def _accounts(n, ledger=1):
+    a = np.zeros(n, dtype=ACCOUNT_DTYPE)
+    a["id_lo"] = np.arange(1, n + 1)
+    a["ledger"] = ledger
+    a["code"] = 1
+    return a
+
+
+def _transfers(n, first_id, n_accounts, amount=1):
+    t = np.zeros(n, dtype=TRANSFER_DTYPE)
+    t["id_lo"] = np.arange(first_id, first_id + n)
+    t["debit_account_id_lo"] = 1 + np.arange(n) % n_accounts
+    t["credit_account_id_lo"] = 1 + (np.arange(n) + 1) % n_accounts
+    t["amount_lo"] = amount
+    t["ledger"] = 1
+    t["code"] = 1
+    return t
+
+
+def _prefetch(engine, op, arr):
+    _lib.check(engine.lib.tbgpu_prefetch(engine.h, op, arr.ctypes.data, arr.nbytes))
+
+
+def _commit_raw(engine, op, ts, arr):
+    out = np.zeros(max(arr.nbytes // 128 * 8, 8), dtype=np.uint8)
+    n = ctypes.c_uint32(0)
+    _lib.check(engine.lib.tbgpu_commit(engine.h, op, ts, arr.ctypes.data, arr.nbytes, out.ctypes.data, out.nbytes,
+                                       ctypes.byref(n)))
+    return out[:n.value].tobytes()
+
+
+@pytest.mark.parametrize("profile", [False, True])
+def test_no_allocation_after_init(profile, gpu_engine_factory):
+    engine = gpu_engine_factory(accounts_max=1 << 12, transfers_max=1 << 18, pass_events_max=1 << 14,
+                                pass_batches_max=16, profile=profile)
+    body = np.zeros(4 * 8190 * 128, dtype=np.uint8)
+    engine.register_host(body)
+    before = allocations()
+    ts = 10**9
+    assert engine.commit(128, ts, _accounts(64).tobytes()) == b""
+    k = 1
+    for rnd in range(3):
+        t = _transfers(8190, k, 64)
+        k += 8190
+        ts += 10**4
+        assert engine.commit(129, ts, t.tobytes()) == b""                       # pageable, one prepare
+        body[:t.nbytes] = t.view(np.uint8)
+        ts += 10**4
+        assert _commit_raw(engine, 129, ts, body[:t.nbytes]) == b""             # registered: read through
+        t2 = _transfers(8190, k, 64)
+        k += 8190
+        body[:t2.nbytes] = t2.view(np.uint8)
+        _prefetch(engine, 129, body[:t2.nbytes])
+        ts += 10**4
+        assert _commit_raw(engine, 129, ts, body[:t2.nbytes]) == b""            # staged by prefetch
+        many = [_transfers(1000, k + 1000 * j, 64).tobytes() for j in range(3)]
+        k += 3000
+        assert engine.commit_many(129, [ts + 10**4 * (j + 1) for j in range(3)], many) == [b""] * 3
+        ts += 10**5
+        t3 = _transfers(3 * 8190, k, 64)
+        k += 3 * 8190
+        body[:t3.nbytes] = t3.view(np.uint8)
+        rb, _, _ = engine.commit_pipelined(129, [ts + 10**4 * (j + 1) for j in range(3)], [8190] * 3, body,
+                                           chunk_batches=1)
+        assert int(rb.sum()) == 0
+        ts += 10**5
+        ids = np.zeros((4, 2), dtype=np.uint64)
+        ids[:, 0] = [1, 2, 3, 999]
+        assert len(engine.commit(130, ts, ids.tobytes())) == 3 * 128              # lookup_accounts
+        ts += 10**4
+        d = engine.checkpoint_delta(caps=(1 << 16, 1 << 16, 1 << 16))          # synchronous write-back
+        assert len(d.transfers) > 0
+        ts += 10**4
+        assert engine.commit(129, ts, _transfers(100, k, 64).tobytes()) == b""
+        k += 100
+        engine.checkpoint_delta_async((1 << 16, 1 << 16, 1 << 16))             # asynchronous write-back
+        ts += 10**4
+        assert engine.commit(129, ts, _transfers(100, k, 64).tobytes()) == b""  # while it is in flight
+        k += 100
+        assert len(engine.checkpoint_delta_wait().transfers) == 100
+        engine.stats()
+        if rnd == 0:  # the write-back buffer sets of the mirror are registered by now
+            before = allocations()
+    assert allocations() == before, "an entry point allocated after tbgpu_init"
+    engine.unregister_host(body)
+
+
+def test_prefetch_staging_belongs_to_the_next_commit(gpu_engine_factory):
+    """A staged body is taken by the commit right after its prefetch only: any call in between drops
+    it, and a re-prefetch restages the current bytes."""
+    engine = gpu_engine_factory()
+    buf = np.zeros(64 * 128, dtype=np.uint8)
+    engine.register_host(buf)
+    assert engine.commit(128, 100, _accounts(8).tobytes()) == b""
+    good = _transfers(64, 1000, 8)
+    bad = good.copy()
+    bad["ledger"][::2] = 0  # every other event: ledger_must_not_be_zero (the same ids, never inserted)
+    ts = 1000
+
+    def expect_bad(reply):
+        r = np.frombuffer(reply, dtype=np.uint32).reshape(-1, 2)
+        assert r[:, 0].tolist() == list(range(0, 64, 2))
+
+    # 1. prefetch(good) -> another call -> buffer now holds `bad` -> commit sees `bad`.
+    buf[:] = good.view(np.uint8)
+    _prefetch(engine, 129, buf)
+    engine.stats()
+    buf[:] = bad.view(np.uint8)
+    ts += 100
+    expect_bad(_commit_raw(engine, 129, ts, buf))
+    # 2. prefetch(good) -> buffer changes -> prefetch again -> commit sees the new bytes.
+    good2 = _transfers(64, 5000, 8)
+    bad2 = good2.copy()
+    bad2["ledger"][::2] = 0
+    buf[:] = good2.view(np.uint8)
+    _prefetch(engine, 129, buf)
+    buf[:] = bad2.view(np.uint8)
+    _prefetch(engine, 129, buf)
+    ts += 100
+    expect_bad(_commit_raw(engine, 129, ts, buf))
+    # 3. a failed commit drops it too: prefetch(good) -> commit with a stale timestamp (PANIC, no
+    #    state change) -> buffer changes -> commit sees the new bytes.
+    good3 = _transfers(64, 9000, 8)
+    bad3 = good3.copy()
+    bad3["ledger"][::2] = 0
+    buf[:] = good3.view(np.uint8)
+    _prefetch(engine, 129, buf)
+    with pytest.raises(EnginePanic):
+        _commit_raw(engine, 129, 1, buf)
+    buf[:] = bad3.view(np.uint8)
+    ts += 100
+    expect_bad(_commit_raw(engine, 129, ts, buf))
+    # 4. the staged path itself: prefetch -> commit of the same bytes.
+    good4 = _transfers(64, 20000, 8)
+    buf[:] = good4.view(np.uint8)
+    _prefetch(engine, 129, buf)
+    ts += 100
+    assert _commit_raw(engine, 129, ts, buf) == b""
+    engine.unregister_host(buf)
+
+
+def test_device_panic_stops_the_engine_until_reset(gpu_engine_factory):
+    engine = gpu_engine_factory()
+    assert engine.commit(128, 10, _accounts(2).tobytes()) == b""
+    pend = _transfers(1, 10, 2, amount=100)
+    pend["flags"] = int(TransferFlags.pending)
+    assert engine.commit(129, 20, pend.tobytes()) == b""
+    engine.set_balances(1, 0, 0, 0, 0)  # debits_pending 100 -> 0: the post's checked `-=` traps
+    post = np.zeros(1, dtype=TRANSFER_DTYPE)
+    post["id_lo"] = 11
+    post["pending_id_lo"] = 10
+    post["flags"] = int(TransferFlags.post_pending_transfer)
+    with pytest.raises(EnginePanic):
+        engine.commit(129, 30, post.tobytes())
+    with pytest.raises(EnginePanic, match="stopped"):
+        engine.commit(129, 40, _transfers(1, 50, 2).tobytes())
+    engine.export_accounts()  # reads still work
+    engine.reset()
+    assert engine.commit(128, 10, _accounts(2).tobytes()) == b""
+    assert engine.commit(129, 20, _transfers(4, 1, 2).tobytes()) == b""
+
+
+def test_kernel_spans_on_the_device_clock(gpu_engine_factory):
+    engine = gpu_engine_factory(accounts_max=1 << 12, transfers_max=1 << 17, pass_events_max=1 << 15,
+                                pass_batches_max=8, profile=True)
+    assert engine.commit(128, 10**9, _accounts(256).tobytes()) == b""
+    engine.reset_stats()
+    bodies = [_transfers(8190, 1 + 8190 * j, 256).tobytes() for j in range(4)]
+    assert engine.commit_many(129, [10**10 + 10**5 * j for j in range(4)], bodies) == [b""] * 4
+    st = engine.stats()
+    n_val, n_res = st["span_launches"][0], st["span_launches"][1]
+    assert n_val == st["launches_validate"] > 0 and n_res == st["launches_resolve"]
+    for k, key in ((0, "ms_validate"), (1, "ms_resolve")):
+        assert 0 < st["span_ms"][k] <= st[key] * 1.05 + 0.01  # inside the HIP-event bracket
+
+
+@pytest.mark.parametrize("config", ["mixed", "two_phase", "chains"])
+def test_async_write_back_equals_sync(config, gpu_engine_factory):
+    """Each segment's write-back through tbgpu_checkpoint_delta_async, waited for only after the
+    next segment committed, equals the synchronous write-back of an engine committing the same."""
+    sc = make_scenario(707 + sum(map(ord, config)), **CONFIGS[config])
+    cut = np.linspace(0, len(sc.steps), 5).astype(int)
+    segs = []
+    for a, b in zip(cut[:-1], cut[1:]):
+        s = Scenario()
+        s.steps = sc.steps[a:b]
+        segs.append(s)
+    e_sync, e_async = gpu_engine_factory(), gpu_engine_factory()
+    caps = (1 << 14, 1 << 14, 1 << 14)
+
+    def rows(arr):
+        return sorted(bytes(r) for r in np.asarray(arr).view(np.uint8).reshape(len(arr), -1))
+
+    expected, got = [], []
+    for i, seg in enumerate(segs):
+        run_many(seg, e_sync)
+        expected.append(e_sync.checkpoint_delta(caps=caps))
+        run_many(seg, e_async)
+        if i:
+            got.append(e_async.checkpoint_delta_wait())  # the previous segment's, after this one committed
+        e_async.checkpoint_delta_async(caps)
+    got.append(e_async.checkpoint_delta_wait())
+    for d_s, d_a in zip(expected, got):
+        assert np.array_equal(d_s.transfers, d_a.transfers)  # by timestamp on both
+        assert np.array_equal(d_s.posted, d_a.posted)
+        assert d_s.created_after == d_a.created_after
+        assert rows(d_s.accounts) == rows(d_a.accounts)
+        assert sorted(zip(map(bytes, d_s.accounts.view(np.uint8).reshape(-1, 128)), map(bytes, d_s.accounts_before))) == \
+            sorted(zip(map(bytes, d_a.accounts.view(np.uint8).reshape(-1, 128)), map(bytes, d_a.accounts_before)))
+    oracle = OracleEngine()
+    run_oracle(sc, oracle)
+    assert e_async.export_accounts().tobytes() == oracle.export_accounts().tobytes()

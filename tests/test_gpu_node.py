@@ -113,3 +113,42 @@ def test_node_refuses_device_resident(node_factory):
     engine = node_factory()
     with pytest.raises(EngineError):
         engine.commit_device_async(129, [10], [1], 0, 0, 0)
+
+
+@pytest.mark.parametrize("config,shards", [("c3", 2), ("c3", 4), ("c4", 2), ("c4", 4)])
+def test_node_dirty_passes_split(config, shards, node_factory):
+    """BASELINE C3 / C4 shapes at 1M accounts and 2M transfers, through 2 and 4 shards in
+    64-prepare blocks: every dirty pass is SPLIT — the dependent subsequence committed in order by
+    the sequencer, the rest routed — never sequenced whole (no host code walks the events); every
+    reply, account, transfer and posted entry equals the oracle's."""
+    from tests.harness.configs import SETTINGS
+    n_acc, n_xfer, batch, chunk = 1_000_000, 2_000_000, 8190, 64
+    engine = node_factory(devices=(0,) * shards, accounts_max=n_acc, transfers_max=n_xfer,
+                          pass_events_max=chunk * batch, pass_batches_max=chunk)
+    accts, xfers = generate(engine, config, n_acc, n_xfer, seed=11 + shards)
+    a_lens, x_lens = batches(n_acc, batch), batches(n_xfer, batch)
+    a_ts, t = timestamps(a_lens, 10**12)
+    x_ts, _ = timestamps(x_lens, t + 10, gap_every=SETTINGS[config]["gap_every"])
+    oracle = OracleEngine(n_acc, n_xfer)
+    assert all(r == b"" for r in oracle.commit_many(128, a_ts, split(accts, a_lens)))
+    expected = oracle.commit_many(129, x_ts, split(xfers, x_lens))
+    rb, _, _ = engine.commit_pipelined(128, a_ts, a_lens, np.ascontiguousarray(accts), chunk_batches=chunk)
+    assert int(rb.sum()) == 0
+    engine.reset_stats()
+    host = np.ascontiguousarray(xfers)
+    engine.register_host(host)
+    try:
+        rb, rep, _ = engine.commit_pipelined(129, x_ts, x_lens, host, chunk_batches=chunk)
+    finally:
+        engine.unregister_host(host)
+    got, off = [], 0
+    for L, nb in zip(x_lens, rb):
+        got.append(bytes(rep[off * 8:off * 8 + int(nb)]))
+        off += L
+    for k, (e, a) in enumerate(zip(expected, got)):
+        assert e == a, "reply of prepare %d differs" % k
+    assert sum(len(r) for r in expected) > 0
+    assert_same_state(oracle, engine)
+    st = engine.stats()
+    assert st["node_passes_whole"] == 0 and st["node_passes_split"] > 0, st
+    assert 0 < st["node_sequenced_events"] < n_xfer, st  # only the dependent subsequence is sequenced

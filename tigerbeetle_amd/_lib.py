@@ -86,6 +86,12 @@ class tbgpu_stats(ctypes.Structure):
         ("walk_crit_wait_ms", ctypes.c_double),
         ("walk_crit_ms", ctypes.c_double),
         ("walk_dbg", ctypes.c_uint64 * 4),
+        ("span_ms", ctypes.c_double * 3),
+        ("span_launches", ctypes.c_uint64 * 3),
+        ("node_passes_clean", ctypes.c_uint64),
+        ("node_passes_split", ctypes.c_uint64),
+        ("node_passes_whole", ctypes.c_uint64),
+        ("node_sequenced_events", ctypes.c_uint64),
     ]
 
 
@@ -147,6 +153,7 @@ SIGNATURES = [
     ("tbgpu_reset_stats", None, [_P]),
     ("tbgpu_last_error", ctypes.c_char_p, []),
     ("tbgpu_checksum", None, [_P, _U64, _P]),
+    ("tbgpu_debug_allocations", _U64, []),
     ("tbgpu_bench_generate_accounts", ctypes.c_int, [_P, _P, _U64, _U64, ctypes.POINTER(tbgpu_workload)]),
     ("tbgpu_bench_generate_transfers", ctypes.c_int, [_P, _P, _U64, _U64, ctypes.POINTER(tbgpu_workload)]),
     ("tbgpu_bench_reset_transfers", ctypes.c_int, [_P]),
@@ -162,6 +169,8 @@ SIGNATURES = [
     ("tbgpu_copy_to_host", ctypes.c_int, [_P, _P, _P, _U64]),
     ("tbgpu_register_host", ctypes.c_int, [_P, _P, _U64]),
     ("tbgpu_checkpoint_delta", ctypes.c_int, [_P, _P, _P, _U64, _P, _U64, _P, _U64, _P]),
+    ("tbgpu_checkpoint_delta_async", ctypes.c_int, [_P, _P, _P, _U64, _P, _U64, _P, _U64]),
+    ("tbgpu_checkpoint_delta_wait", ctypes.c_int, [_P, _P]),
     ("tbgpu_load_accounts", ctypes.c_int, [_P, _P, _U32]),
     ("tbgpu_load_transfers", ctypes.c_int, [_P, _P, _P, _U32]),
     ("tbgpu_set_commit_timestamp", ctypes.c_int, [_P, _U64]),

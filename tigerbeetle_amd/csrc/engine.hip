@@ -34,6 +34,29 @@
 
 static thread_local std::string g_err;
 
+// Every device / pinned allocation and HIP event the library makes goes through these (counted):
+// tbgpu.h promises none after tbgpu_init on the commit path, and tests/test_gpu_alloc.py holds the
+// library to it with tbgpu_debug_allocations().
+static std::atomic<uint64_t> g_allocs{0};
+template <typename T>
+static hipError_t tbMalloc(T** p, size_t bytes) {
+    g_allocs++;
+    return hipMalloc((void**)p, bytes);
+}
+template <typename T>
+static hipError_t tbHostMalloc(T** p, size_t bytes, unsigned flags) {
+    g_allocs++;
+    return hipHostMalloc((void**)p, bytes, flags);
+}
+static hipError_t tbEventCreate(hipEvent_t* e) {
+    g_allocs++;
+    return hipEventCreate(e);
+}
+static hipError_t tbEventCreateWithFlags(hipEvent_t* e, unsigned flags) {
+    g_allocs++;
+    return hipEventCreateWithFlags(e, flags);
+}
+
 static int fail(int status, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 static int fail(int status, const char* fmt, ...) {
     char buf[512];
@@ -59,6 +82,7 @@ static u64 pow2_at_least(u64 v) {
 }
 
 #define PIPE_SLOTS 3
+#define KCLOCK_SLOTS 4096  // profiled passes between two collects (a full ring is collected early)
 
 enum { K_VALIDATE = 0, K_RESOLVE = 1, K_REPLAY = 2, K_CLEAR = 3, K_PASS = 4, K_APPLY = 5, K_COUNT = 6 };
 
@@ -68,6 +92,35 @@ struct ProfilePair {
 };
 
 struct TbNode;  // node.h: the multi-device engine (tbgpu_config.device_count > 1)
+
+// Groove write-back buffers (tbgpu_checkpoint_delta / _async), every one allocated at tbgpu_init.
+#define WB_IDS_MAX (1ULL << 20)  // listed ids (creates, direct balance writes) between write-backs
+#define WB_OUT_GRID 128          // workgroups of the asynchronous copy-out (a PCIe stream, not the CUs)
+enum { WB_ACCOUNTS = 0, WB_SLOTS = 1, WB_PV = 2, WB_RECORDS = 3, WB_STATUS = 4, WB_COUNT_WORDS = 8 };
+struct WbBufs {
+    u64 cap_t = 0;    // log positions per slice
+    u64 cap_ids = 0;  // listed ids per chunk
+    u64 cap_a = 0;    // accounts emitted per slice / chunk
+    u32* d_bc = nullptr;          // [cap_t / DELTA_THREADS] live records per workgroup
+    u64* d_base = nullptr;        // their exclusive prefix
+    u8* d_out = nullptr;          // [cap_t] records
+    u64* d_ids = nullptr;         // [cap_t][4] debit / credit account ids of the records
+    u64* d_pv = nullptr;          // [cap_t][3] post / void records: {pending id, voided}
+    u64* d_pairs = nullptr;       // [cap_t][2] posted pairs {pending timestamp, voided}
+    u64* d_hids = nullptr;        // [cap_ids][2] listed ids
+    u8* d_acc = nullptr;          // [cap_a] emitted accounts
+    AccountBal* d_before = nullptr;
+    u32* d_slots = nullptr;       // [account_cap] every slot one write-back covers
+    u64* d_cnt = nullptr;         // [WB_COUNT_WORDS] WB_* counters
+    u64* h_cnt = nullptr;         // pinned mirror
+    hipStream_t stream = nullptr; // the asynchronous copy-out
+    hipEvent_t gathered = nullptr, done = nullptr;
+    bool inflight = false;
+    tbgpu_delta_counts counts{};
+    u8* out_t = nullptr;          // the in-flight write-back's caller buffers (sorted by the wait)
+    u64* out_p = nullptr;
+    std::vector<u64> ids_inflight;
+};
 
 struct tbgpu {
     tbgpu_config cfg{};
@@ -142,10 +195,14 @@ struct tbgpu {
     // tbgpu_prefetch: the body of the prepare about to be committed, staged in HBM by DMA.
     u8* pf_staging = nullptr;     // BATCH_EVENTS_MAX events
     hipEvent_t pf_done = nullptr; // on copy_stream: the staging copy landed
-    const void* pf_input = nullptr;
+    const void* pf_input = nullptr;  // valid for the next entry point only, if it is tbgpu_commit
+    const void* pf_claim = nullptr;  // tbgpu_commit -> commit_host: the staged body it may take
     u32 pf_len = 0;
     u8 pf_op = 0;
     u32* d_status = nullptr;
+    // A device panic left state the reference never reaches (it traps there): every entry point that
+    // changes state refuses until tbgpu_reset.
+    bool poisoned = false;
 
     u32 epoch = 0;
     bool dedup_force = true;  // the next pass clears the whole dedup set (init, reset, epoch wrap)
@@ -159,7 +216,8 @@ struct tbgpu {
     bool profile = false;
     u32 legs_min = LEGS_MIN_EVENTS;
     u64 wall_khz = 0;  // device wall clock (flow phase timing)
-    // Groove write-back snapshot (tbgpu_checkpoint_delta), allocated on first use.
+    WbBufs wb;
+    // Groove write-back snapshot (tbgpu_checkpoint_delta).
     AccountBal* ckpt_bal = nullptr;  // balances at the previous write-back
     u32* ckpt_mark = nullptr;        // per slot: the write-back epoch that last covered it
     u32 ckpt_epoch = 0;
@@ -175,6 +233,13 @@ struct tbgpu {
     std::vector<ProfilePair> prof;
     double prof_ms[K_COUNT] = {};
     u64 prof_n[K_COUNT] = {};
+    // Launch spans on the device clock (tbgpu_stats.span_ms): a ring of KCLOCK_WORDS words per pass.
+    u64* kclock = nullptr;
+    u64* h_kclock = nullptr;        // pinned: the ring read back by prof_collect
+    u32 kclock_next = 0;            // next ring slot
+    std::vector<std::pair<u32, u32>> kclock_used;  // (slot, kernels launched: bit k) since the last collect
+    double span_ms[3] = {};
+    u64 span_n[3] = {};
     u64 passes = 0, events = 0;
     std::vector<double> pass_ms;  // device duration of every profiled pass (batch latency)
 
@@ -193,28 +258,37 @@ struct tbgpu {
 
 static void ckpt_note_ids(tbgpu* E, const u8* records, u64 n);
 
+// Every entry point but tbgpu_prefetch starts here.  A body staged by tbgpu_prefetch belongs to the
+// commit that comes next (src/vsr/replica.zig:3324-3662: prefetch(op) -> commit(op), nothing in
+// between): any other call first drops it, so a reused message buffer can never be committed from a
+// stale staging copy.  `mutates`: refused on a poisoned engine (a device panic, tbgpu.h).
+static int api_enter(tbgpu* E, bool mutates) {
+    E->pf_input = nullptr;
+    if (mutates && E->poisoned) {
+        return fail(TBGPU_STATUS_PANIC, "engine stopped by an earlier device panic (tbgpu_reset or tbgpu_deinit it)");
+    }
+    return TBGPU_STATUS_OK;
+}
+#define API_ENTER(E, mutates)                        \
+    do {                                             \
+        if (const int st_ = api_enter((E), (mutates))) return st_; \
+    } while (0)
+
 // Pinned reply arena of one pipeline slot: head {panic, commit_ts}, reply bytes per prepare, then
 // the results of every event of the chunk (8 B each, the worst case).
 static u64 pipe_reply_bytes(const tbgpu* E) { return 16 + E->meta_cap * 4 + (u64)E->pe_max * 8; }
 
-static int ev_get(tbgpu* E, hipEvent_t* out) {
-    if (E->event_next == E->event_pool.size()) {
-        hipEvent_t e;
-        HIPCK(hipEventCreate(&e));
-        E->event_pool.push_back(e);
-    }
-    *out = E->event_pool[E->event_next++];
-    return 0;
-}
+// HIP events of the profiling pairs: a pool created at init (TBGPU_CONFIG_PROFILE); a call that
+// would need more between two collects leaves the extra launches untimed rather than allocate.
+#define PROF_EVENTS 8192
 
 static int prof_begin(tbgpu* E, ProfilePair* p, int kind) {
     p->kind = -1;
     if (!E->profile || !(E->prof_mask & (1u << kind))) return 0;
+    if (E->event_next + 2 > E->event_pool.size()) return 0;
     p->kind = kind;
-    int st = ev_get(E, &p->a);
-    if (st) return st;
-    st = ev_get(E, &p->b);
-    if (st) return st;
+    p->a = E->event_pool[E->event_next++];
+    p->b = E->event_pool[E->event_next++];
     HIPCK(hipEventRecord(p->a, E->stream));
     return 0;
 }
@@ -227,6 +301,19 @@ static int prof_end(tbgpu* E, ProfilePair* p) {
 }
 
 static int prof_collect(tbgpu* E) {
+    if (!E->kclock_used.empty()) {  // the stream has drained: every stamped span is final
+        HIPCK(hipMemcpy(E->h_kclock, E->kclock, (u64)KCLOCK_SLOTS * KCLOCK_WORDS * 8, hipMemcpyDeviceToHost));
+        for (const auto& u : E->kclock_used) {
+            const u64* w = E->h_kclock + (u64)u.first * KCLOCK_WORDS;
+            for (u32 k = 0; k < 3; k++) {
+                if (!((u.second >> k) & 1) || w[2 * k + 1] < w[2 * k] || !E->wall_khz) continue;
+                E->span_ms[k] += (double)(w[2 * k + 1] - w[2 * k]) / E->wall_khz;
+                E->span_n[k] += 1;
+            }
+        }
+        E->kclock_used.clear();
+        E->kclock_next = 0;
+    }
     for (const ProfilePair& p : E->prof) {
         float ms = 0;
         HIPCK(hipEventElapsedTime(&ms, p.a, p.b));
@@ -283,6 +370,53 @@ static void dev_register(tbgpu* E, bool add) {
     }
 }
 
+// The co-residency tb_flow relies on, checked once at init (tbgpu.h "Device exclusivity"): a grid of
+// tb_flow's shape (workgroups, threads, LDS) whose workgroups each arrive at a counter and wait until
+// every one has arrived, for at most `deadline` ticks of the device clock.  A workgroup that gave up
+// sets *failed.  On a device this process has to itself every workgroup is resident at once and the
+// probe takes microseconds.
+__global__ __launch_bounds__(FLOW_THREADS) void tb_residency_probe(u32* counter, u32 total, u64 deadline, u32* failed) {
+    extern __shared__ u32 s_probe_lds[];  // sized like tb_flow's LDS: the same residency per CU
+    if (threadIdx.x != 0) return;
+    s_probe_lds[0] = 0;
+    atomicAdd(counter, 1u);
+    const u64 t0 = wall_clock64();
+    while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < total) {
+        if (wall_clock64() - t0 > deadline) {
+            atomicOr(failed, 1u);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+static int residency_probe(tbgpu* E, u32 grid) {
+    u32* d = nullptr;
+    HIPCK(tbMalloc(&d, 8));
+    hipFuncAttributes attr{};
+    size_t lds = 0;
+    if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&tb_flow)) == hipSuccess) lds = attr.sharedSizeBytes;
+    int st = TBGPU_STATUS_OK;
+    u32 h[2] = {0, 0};
+    hipError_t e = hipMemsetAsync(d, 0, 8, E->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(tb_residency_probe, dim3(grid), dim3(FLOW_THREADS), std::max<size_t>(lds, 4), E->stream, d, grid,
+                           (u64)200 * E->wall_khz, d + 1);  // 200 ms
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, E->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(E->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "tbgpu_init: residency probe: %s", hipGetErrorString(e));
+    if (h[1]) {
+        st = fail(TBGPU_STATUS_DEVICE,
+                  "tbgpu_init: device %d is not exclusive: %u workgroups of the ordered fallback's grid could not be "
+                  "resident together (another process or kernel holds its CUs; tbgpu.h \"Device exclusivity\")",
+                  E->device, grid);
+    }
+    return st;
+}
+
 static u32 flow_grid(tbgpu* E) {
     u32 engines = 1;
     {
@@ -309,6 +443,7 @@ static int node_api_checkpoint_delta(TbNode* N, void* accounts_out, void* accoun
                                      void* transfers_out, u64 transfers_cap, u64* posted_out, u64 posted_cap,
                                      tbgpu_delta_counts* counts);
 static int node_api_get_stats(TbNode* N, tbgpu_stats* s);
+static void node_reset_stats(TbNode* N);
 static u32 node_world(TbNode* N);
 static tbgpu* node_engine(TbNode* N, u32 d);
 static int node_api_register_host(TbNode* N, void* ptr, u64 bytes);
@@ -394,15 +529,15 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         return st;
     }
 
-    INIT_CK(hipMalloc(&E->T.acct_hot, E->account_cap * sizeof(AccountHot)));
-    INIT_CK(hipMalloc(&E->T.acct_bal, E->account_cap * sizeof(AccountBal)));
-    INIT_CK(hipMalloc(&E->T.acct_cold, E->account_cap * sizeof(AccountCold)));
-    INIT_CK(hipMalloc(&E->T.account_mark, E->account_cap * sizeof(u32)));
-    INIT_CK(hipMalloc(&E->T.xidx, E->xidx_cap * sizeof(u64)));
-    INIT_CK(hipMalloc(&E->T.xdup, E->xidx_cap));
-    INIT_CK(hipMalloc(&E->T.xlog, E->xlog_cap * sizeof(Transfer)));
-    INIT_CK(hipMalloc(&E->T.xposted, E->xlog_cap));
-    INIT_CK(hipMalloc(&E->g, sizeof(Globals)));
+    INIT_CK(tbMalloc(&E->T.acct_hot, E->account_cap * sizeof(AccountHot)));
+    INIT_CK(tbMalloc(&E->T.acct_bal, E->account_cap * sizeof(AccountBal)));
+    INIT_CK(tbMalloc(&E->T.acct_cold, E->account_cap * sizeof(AccountCold)));
+    INIT_CK(tbMalloc(&E->T.account_mark, E->account_cap * sizeof(u32)));
+    INIT_CK(tbMalloc(&E->T.xidx, E->xidx_cap * sizeof(u64)));
+    INIT_CK(tbMalloc(&E->T.xdup, E->xidx_cap));
+    INIT_CK(tbMalloc(&E->T.xlog, E->xlog_cap * sizeof(Transfer)));
+    INIT_CK(tbMalloc(&E->T.xposted, E->xlog_cap));
+    INIT_CK(tbMalloc(&E->g, sizeof(Globals)));
     {
         // tb_flow: 1024-thread workgroups, all resident (see flow_grid).
         hipDeviceProp_t prop;
@@ -445,60 +580,60 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     E->T.g = E->g;
 
     const u64 pe = E->pe_max;
-    INIT_CK(hipMalloc(&E->info, pe * 4));
-    INIT_CK(hipMalloc(&E->eflags, pe * 2));
-    INIT_CK(hipMalloc(&E->dr, pe * 4));
-    INIT_CK(hipMalloc(&E->cr, pe * 4));
-    INIT_CK(hipMalloc(&E->ps, pe * 4));
-    INIT_CK(hipMalloc(&E->rs, pe * 4));
-    INIT_CK(hipMalloc(&E->dep_list, pe * 4));
-    INIT_CK(hipMalloc(&E->dep_count, (u64)E->pb_max * 4));
-    INIT_CK(hipMalloc(&E->amt, pe * 16));
-    INIT_CK(hipMalloc(&E->kid, pe * 8));
-    INIT_CK(hipMalloc(&E->kpid, pe * 8));
-    INIT_CK(hipMalloc(&E->dedup, E->dedup_cap * 8));
-    INIT_CK(hipMalloc(&E->sum_shards, SUM_WORDS * 8));
-    INIT_CK(hipMalloc(&E->undo, (u64)E->undo_cap * sizeof(UndoEntry)));
+    INIT_CK(tbMalloc(&E->info, pe * 4));
+    INIT_CK(tbMalloc(&E->eflags, pe * 2));
+    INIT_CK(tbMalloc(&E->dr, pe * 4));
+    INIT_CK(tbMalloc(&E->cr, pe * 4));
+    INIT_CK(tbMalloc(&E->ps, pe * 4));
+    INIT_CK(tbMalloc(&E->rs, pe * 4));
+    INIT_CK(tbMalloc(&E->dep_list, pe * 4));
+    INIT_CK(tbMalloc(&E->dep_count, (u64)E->pb_max * 4));
+    INIT_CK(tbMalloc(&E->amt, pe * 16));
+    INIT_CK(tbMalloc(&E->kid, pe * 8));
+    INIT_CK(tbMalloc(&E->kpid, pe * 8));
+    INIT_CK(tbMalloc(&E->dedup, E->dedup_cap * 8));
+    INIT_CK(tbMalloc(&E->sum_shards, SUM_WORDS * 8));
+    INIT_CK(tbMalloc(&E->undo, (u64)E->undo_cap * sizeof(UndoEntry)));
     if (E->legs_ok) {
-        INIT_CK(hipMalloc(&E->leg_ev, pe * 2 * 8));
-        INIT_CK(hipMalloc(&E->leg_w, pe * 2 * 8));
-        INIT_CK(hipMalloc(&E->leg_off, (u64)std::min<u32>(E->pb_max, LEG_PREPARES_MAX) * (E->leg_buckets + 1) * 4));
-        INIT_CK(hipMalloc(&E->leg_tot, ((u64)E->leg_buckets + 1) * 4));
+        INIT_CK(tbMalloc(&E->leg_ev, pe * 2 * 8));
+        INIT_CK(tbMalloc(&E->leg_w, pe * 2 * 8));
+        INIT_CK(tbMalloc(&E->leg_off, (u64)std::min<u32>(E->pb_max, LEG_PREPARES_MAX) * (E->leg_buckets + 1) * 4));
+        INIT_CK(tbMalloc(&E->leg_tot, ((u64)E->leg_buckets + 1) * 4));
         INIT_CK(hipMemset(E->leg_tot, 0, ((u64)E->leg_buckets + 1) * 4));
     }
     if (E->flow_ok) {
         FlowArgs& F = E->F;
-        INIT_CK(hipMalloc(&F.f_pe, pe * 4));
-        INIT_CK(hipMalloc(&F.f_batch, pe * 4));
-        INIT_CK(hipMalloc(&F.f_len, pe * 4));
-        INIT_CK(hipMalloc(&F.need, pe * 4));
-        INIT_CK(hipMalloc(&F.nsucc, pe * 4));
-        INIT_CK(hipMalloc(&F.queue, pe * 4));
-        INIT_CK(hipMalloc(&F.uflags, pe * 4));
-        INIT_CK(hipMalloc(&F.nacct, pe * 4));
-        INIT_CK(hipMalloc(&F.rpos, pe * 4));
-        INIT_CK(hipMalloc(&F.succ, pe * 4 * FLOW_RMAX));
-        INIT_CK(hipMalloc(&F.run, pe * sizeof(RunEntry) * FLOW_RMAX));
+        INIT_CK(tbMalloc(&F.f_pe, pe * 4));
+        INIT_CK(tbMalloc(&F.f_batch, pe * 4));
+        INIT_CK(tbMalloc(&F.f_len, pe * 4));
+        INIT_CK(tbMalloc(&F.need, pe * 4));
+        INIT_CK(tbMalloc(&F.nsucc, pe * 4));
+        INIT_CK(tbMalloc(&F.queue, pe * 4));
+        INIT_CK(tbMalloc(&F.uflags, pe * 4));
+        INIT_CK(tbMalloc(&F.nacct, pe * 4));
+        INIT_CK(tbMalloc(&F.rpos, pe * 4));
+        INIT_CK(tbMalloc(&F.succ, pe * 4 * FLOW_RMAX));
+        INIT_CK(tbMalloc(&F.run, pe * sizeof(RunEntry) * FLOW_RMAX));
         for (int k = 0; k < 2; k++) {
-            INIT_CK(hipMalloc(&F.keys[k], pe * 4 * FLOW_RMAX));
-            INIT_CK(hipMalloc(&F.vals[k], pe * 4 * FLOW_RMAX));
+            INIT_CK(tbMalloc(&F.keys[k], pe * 4 * FLOW_RMAX));
+            INIT_CK(tbMalloc(&F.vals[k], pe * 4 * FLOW_RMAX));
         }
-        INIT_CK(hipMalloc(&F.hist, (u64)F.grid * 256 * 4));
-        INIT_CK(hipMalloc(&F.words, FW_WORDS * 4));
-        INIT_CK(hipMalloc(&F.undo, pe * 4 * sizeof(UndoEntry)));
-        INIT_CK(hipMalloc(&F.b_st, pe * 4));
-        INIT_CK(hipMalloc(&F.b_vd, pe));
-        INIT_CK(hipMalloc(&F.b_vc, pe));
-        INIT_CK(hipMalloc(&F.b_amt, pe * 8 * FLOW_RMAX));
-        INIT_CK(hipMalloc(&F.b_meta, pe * 4 * FLOW_RMAX));
-        INIT_CK(hipMalloc(&F.b_blk, (u64)F.grid * 5 * 8));
-        INIT_CK(hipMalloc(&F.b_qd, pe * 4));
-        INIT_CK(hipMalloc(&F.b_qc, pe * 4));
-        INIT_CK(hipMalloc(&F.b_head, pe * 4 * FLOW_RMAX));
-        INIT_CK(hipMalloc(&F.b_xy, pe * 16 * FLOW_RMAX));
-        INIT_CK(hipMalloc(&F.b_ex, pe * 16 * FLOW_RMAX));
-        INIT_CK(hipMalloc(&F.b_rec, pe * sizeof(SweepRec)));
-        INIT_CK(hipMalloc(&F.b_vw, pe * 4));
+        INIT_CK(tbMalloc(&F.hist, (u64)F.grid * 256 * 4));
+        INIT_CK(tbMalloc(&F.words, FW_WORDS * 4));
+        INIT_CK(tbMalloc(&F.undo, pe * 4 * sizeof(UndoEntry)));
+        INIT_CK(tbMalloc(&F.b_st, pe * 4));
+        INIT_CK(tbMalloc(&F.b_vd, pe));
+        INIT_CK(tbMalloc(&F.b_vc, pe));
+        INIT_CK(tbMalloc(&F.b_amt, pe * 8 * FLOW_RMAX));
+        INIT_CK(tbMalloc(&F.b_meta, pe * 4 * FLOW_RMAX));
+        INIT_CK(tbMalloc(&F.b_blk, (u64)F.grid * 5 * 8));
+        INIT_CK(tbMalloc(&F.b_qd, pe * 4));
+        INIT_CK(tbMalloc(&F.b_qc, pe * 4));
+        INIT_CK(tbMalloc(&F.b_head, pe * 4 * FLOW_RMAX));
+        INIT_CK(tbMalloc(&F.b_xy, pe * 16 * FLOW_RMAX));
+        INIT_CK(tbMalloc(&F.b_ex, pe * 16 * FLOW_RMAX));
+        INIT_CK(tbMalloc(&F.b_rec, pe * sizeof(SweepRec)));
+        INIT_CK(tbMalloc(&F.b_vw, pe * 4));
         F.walk = (config->flags & TBGPU_CONFIG_SWEEP_WINDOW) ? 0u : 1u;
         F.walk_merge = WALK_MERGE_DEFAULT;
 
@@ -507,38 +642,70 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
                       : (config->flags & TBGPU_CONFIG_SWEEP_EARLY) ? 0xFFFFFFFFu
                                                                    : FLOW_SWEEP_MIN;
     }
-    INIT_CK(hipMalloc(&E->staging, pe * 128));
-    INIT_CK(hipMalloc(&E->results, pe * 8));
-    INIT_CK(hipMalloc(&E->reply_bytes, E->meta_cap * 4));
-    INIT_CK(hipMalloc(&E->meta, (2 * E->meta_cap + 1) * 8));
-    INIT_CK(hipHostMalloc(&E->h_meta, (2 * E->meta_cap + 1) * 8, hipHostMallocDefault));
-    INIT_CK(hipHostMalloc(&E->h_globals, sizeof(Globals), hipHostMallocDefault));
-    INIT_CK(hipHostMalloc(&E->h_rb, E->meta_cap * 4, hipHostMallocDefault));
+    INIT_CK(tbMalloc(&E->staging, pe * 128));
+    INIT_CK(tbMalloc(&E->results, pe * 8));
+    INIT_CK(tbMalloc(&E->reply_bytes, E->meta_cap * 4));
+    INIT_CK(tbMalloc(&E->meta, (2 * E->meta_cap + 1) * 8));
+    INIT_CK(tbHostMalloc(&E->h_meta, (2 * E->meta_cap + 1) * 8, hipHostMallocDefault));
+    INIT_CK(tbHostMalloc(&E->h_globals, sizeof(Globals), hipHostMallocDefault));
+    INIT_CK(tbHostMalloc(&E->h_rb, E->meta_cap * 4, hipHostMallocDefault));
     E->h_results_events = std::min<u64>(E->pe_max, 1ULL << 16);
-    INIT_CK(hipHostMalloc(&E->h_results, E->h_results_events * 8, hipHostMallocDefault));
+    INIT_CK(tbHostMalloc(&E->h_results, E->h_results_events * 8, hipHostMallocDefault));
     INIT_CK(hipStreamCreateWithFlags(&E->copy_stream, hipStreamNonBlocking));
     for (int k = 0; k < PIPE_SLOTS; k++) {
         tbgpu::PipeSlot& S = E->pipe[k];
         if (k == 0) S.staging = E->staging;
-        else INIT_CK(hipMalloc(&S.staging, pe * 128));
-        INIT_CK(hipMalloc(&S.meta, (2 * E->meta_cap + 1) * 8));
-        INIT_CK(hipHostMalloc(&S.h_meta, (2 * E->meta_cap + 1) * 8, hipHostMallocDefault));
-        INIT_CK(hipHostMalloc(&S.h_reply, pipe_reply_bytes(E) + 64, hipHostMallocMapped));  // + the done word
+        else INIT_CK(tbMalloc(&S.staging, pe * 128));
+        INIT_CK(tbMalloc(&S.meta, (2 * E->meta_cap + 1) * 8));
+        INIT_CK(tbHostMalloc(&S.h_meta, (2 * E->meta_cap + 1) * 8, hipHostMallocDefault));
+        INIT_CK(tbHostMalloc(&S.h_reply, pipe_reply_bytes(E) + 64, hipHostMallocMapped));  // + the done word
         memset(S.h_reply + pipe_reply_bytes(E), 0, 64);
         INIT_CK(hipHostGetDevicePointer((void**)&S.d_reply, S.h_reply, 0));
-        INIT_CK(hipEventCreate(&S.start));
-        INIT_CK(hipEventCreate(&S.copied));
-        INIT_CK(hipEventCreate(&S.done));
+        INIT_CK(tbEventCreate(&S.start));
+        INIT_CK(tbEventCreate(&S.copied));
+        INIT_CK(tbEventCreate(&S.done));
     }
-    INIT_CK(hipMalloc(&E->lookup_ids, (u64)E->lookup_cap * 16));
-    INIT_CK(hipMalloc(&E->lookup_out, (u64)E->lookup_cap * 128));
-    INIT_CK(hipMalloc(&E->lookup_found, E->lookup_cap));
-    INIT_CK(hipMalloc(&E->d_status, 16));
-    INIT_CK(hipMalloc(&E->pf_staging, (u64)BATCH_EVENTS_MAX * 128));
-    INIT_CK(hipEventCreateWithFlags(&E->pf_done, hipEventDisableTiming));
-    for (int i = 0; i < 16; i++) INIT_CK(hipEventCreate(&E->markers[i]));
+    INIT_CK(tbMalloc(&E->lookup_ids, (u64)E->lookup_cap * 16));
+    INIT_CK(tbMalloc(&E->lookup_out, (u64)E->lookup_cap * 128));
+    INIT_CK(tbMalloc(&E->lookup_found, E->lookup_cap));
+    INIT_CK(tbMalloc(&E->d_status, 16));
+    INIT_CK(tbMalloc(&E->pf_staging, (u64)BATCH_EVENTS_MAX * 128));
+    INIT_CK(tbEventCreateWithFlags(&E->pf_done, hipEventDisableTiming));
+    {  // groove write-back (tbgpu_checkpoint_delta*): snapshot, marks and one slice of buffers
+        WbBufs& W = E->wb;
+        W.cap_t = std::max<u64>(1, std::min<u64>(E->xlog_cap, std::max<u64>(pe, 64ULL * BATCH_EVENTS_MAX)));
+        W.cap_ids = WB_IDS_MAX;
+        W.cap_a = std::min<u64>(E->account_cap, std::max<u64>(2 * W.cap_t, W.cap_ids));
+        const u64 nb = (W.cap_t + DELTA_THREADS - 1) / DELTA_THREADS;
+        INIT_CK(tbMalloc(&E->ckpt_bal, E->account_cap * sizeof(AccountBal)));
+        INIT_CK(tbMalloc(&E->ckpt_mark, E->account_cap * sizeof(u32)));
+        INIT_CK(hipMemset(E->ckpt_mark, 0, E->account_cap * sizeof(u32)));
+        INIT_CK(tbMalloc(&W.d_bc, nb * 4));
+        INIT_CK(tbMalloc(&W.d_base, nb * 8));
+        INIT_CK(tbMalloc(&W.d_out, W.cap_t * 128));
+        INIT_CK(tbMalloc(&W.d_ids, W.cap_t * 32));
+        INIT_CK(tbMalloc(&W.d_pv, W.cap_t * 24));
+        INIT_CK(tbMalloc(&W.d_pairs, W.cap_t * 16));
+        INIT_CK(tbMalloc(&W.d_hids, W.cap_ids * 16));
+        INIT_CK(tbMalloc(&W.d_acc, W.cap_a * 128));
+        INIT_CK(tbMalloc(&W.d_before, W.cap_a * sizeof(AccountBal)));
+        INIT_CK(tbMalloc(&W.d_slots, E->account_cap * 4));
+        INIT_CK(tbMalloc(&W.d_cnt, WB_COUNT_WORDS * 8));
+        INIT_CK(tbHostMalloc(&W.h_cnt, WB_COUNT_WORDS * 8, hipHostMallocDefault));
+        INIT_CK(hipStreamCreateWithFlags(&W.stream, hipStreamNonBlocking));
+        INIT_CK(tbEventCreateWithFlags(&W.gathered, hipEventDisableTiming));
+        INIT_CK(tbEventCreateWithFlags(&W.done, hipEventDisableTiming));
+    }
+    INIT_CK(tbMalloc(&E->kclock, (u64)KCLOCK_SLOTS * KCLOCK_WORDS * 8));
+    INIT_CK(tbHostMalloc(&E->h_kclock, (u64)KCLOCK_SLOTS * KCLOCK_WORDS * 8, hipHostMallocDefault));
+    for (int i = 0; i < 16; i++) INIT_CK(tbEventCreate(&E->markers[i]));
+    if (E->profile) {
+        E->event_pool.resize(PROF_EVENTS);
+        for (auto& ev : E->event_pool) INIT_CK(tbEventCreate(&ev));
+    }
 #undef INIT_CK
     st = engine_clear(E);
+    if (st == TBGPU_STATUS_OK && E->flow_ok) st = residency_probe(E, flow_grid(E));
     if (st) {
         tbgpu_deinit(E);
         return st;
@@ -561,7 +728,9 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->T.xposted, E->g, E->info, E->eflags, E->dr,
                     E->cr, E->ps, E->rs, E->dep_list, E->dep_count, E->amt, E->kid, E->kpid, E->dedup,
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
-                    E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->pf_staging, E->r_home,
+                    E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->pf_staging, E->kclock, E->r_home,
+                    E->wb.d_bc, E->wb.d_base, E->wb.d_out, E->wb.d_ids, E->wb.d_pv, E->wb.d_pairs, E->wb.d_hids,
+                    E->wb.d_acc, E->wb.d_before, E->wb.d_slots, E->wb.d_cnt,
                     E->r_block_counts, E->r_words, E->r_meta, E->leg_ev, E->leg_w, E->leg_off, E->leg_tot,
                     E->F.f_pe, E->F.f_batch, E->F.f_len, E->F.need, E->F.nsucc, E->F.queue, E->F.uflags, E->F.nacct, E->F.rpos, E->F.succ,
                     E->F.run, E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo,
@@ -582,6 +751,14 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
     if (E->h_rb) (void)hipHostFree(E->h_rb);
     if (E->h_results) (void)hipHostFree(E->h_results);
     if (E->h_rmeta) (void)hipHostFree(E->h_rmeta);
+    if (E->h_kclock) (void)hipHostFree(E->h_kclock);
+    if (E->wb.h_cnt) (void)hipHostFree(E->wb.h_cnt);
+    if (E->wb.stream) {
+        (void)hipStreamSynchronize(E->wb.stream);
+        (void)hipStreamDestroy(E->wb.stream);
+    }
+    if (E->wb.gathered) (void)hipEventDestroy(E->wb.gathered);
+    if (E->wb.done) (void)hipEventDestroy(E->wb.done);
     for (hipEvent_t e : E->event_pool) (void)hipEventDestroy(e);
     if (E->pf_done) (void)hipEventDestroy(E->pf_done);
     for (int i = 0; i < 16; i++) if (E->markers[i]) (void)hipEventDestroy(E->markers[i]);
@@ -591,7 +768,13 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
 
 extern "C" int tbgpu_reset(tbgpu_t* E) {
     if (E->node) return node_api_reset(E->node);
+    E->pf_input = E->pf_claim = nullptr;
+    E->poisoned = false;
     HIPCK(hipSetDevice(E->device));
+    if (E->wb.inflight) {  // its copy-out finishes; its results are dropped with the state
+        HIPCK(hipStreamSynchronize(E->wb.stream));
+        E->wb.inflight = false;
+    }
     E->ckpt_valid = false;
     E->ckpt_scan = false;
     std::vector<u64>().swap(E->ckpt_ids);
@@ -608,8 +791,10 @@ static int engine_sync(tbgpu* E) {
     E->pending = false;
     int st = prof_collect(E);
     if (st) return st;
-    if (g.panic) return fail(TBGPU_STATUS_PANIC, "device panic 0x%llx (the reference would have trapped)",
-                             (unsigned long long)g.panic);
+    if (g.panic) {
+        E->poisoned = true;
+        return fail(TBGPU_STATUS_PANIC, "device panic 0x%llx (the reference would have trapped)", (unsigned long long)g.panic);
+    }
     return TBGPU_STATUS_OK;
 }
 
@@ -686,6 +871,15 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
                           b1 - b0 <= FLOW_NB_MAX;
         P.flow_words = E->flow_ok ? E->F.words : nullptr;
 
+        // Launch spans of this pass's kernels on the device clock (profiling only).
+        P.kclock = nullptr;
+        if (E->profile && (E->prof_mask & ((1u << K_VALIDATE) | (1u << K_RESOLVE) | (1u << K_APPLY))) &&
+            E->kclock_next < KCLOCK_SLOTS) {
+            const u32 slot = E->kclock_next++;
+            P.kclock = E->kclock + (u64)slot * KCLOCK_WORDS;
+            E->kclock_used.push_back({slot, (n > 0 ? 1u : 0u) | 2u | (P.legs ? 4u : 0u)});
+        }
+
         ProfilePair pass_pp;
         int st = prof_begin(E, &pass_pp, K_PASS);
         if (st) return st;
@@ -699,7 +893,8 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         u64* meta_dst = inline_meta && b0 == 0 ? (u64*)d_off : nullptr;
         hipLaunchKernelGGL(tb_pass_clear, dim3(clear_grid), dim3(256), 0, E->stream, E->dedup, E->dedup_cap, E->sum_shards,
                            E->g, E->epoch, E->dedup_force ? 1u : 0u, E->leg_tot, E->leg_buckets, meta_dst,
-                           inline_meta ? inline_meta[0] : 0, inline_meta ? inline_meta[1] : 0, inline_meta ? inline_meta[2] : 0);
+                           inline_meta ? inline_meta[0] : 0, inline_meta ? inline_meta[1] : 0, inline_meta ? inline_meta[2] : 0,
+                           P.kclock);
         HIPCK(hipGetLastError());
         E->dedup_force = false;
         E->dedup_prev = P.dedup_mask + 1;
@@ -852,6 +1047,8 @@ static int commit_lookup(tbgpu* E, bool accounts, const void* input, uint32_t in
 
 static int commit_host(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const void* const* inputs,
                        const uint32_t* input_lens, void* const* outputs, uint32_t* out_lens, const uint32_t* out_caps) {
+    const void* claim = E->pf_claim;  // the staged body tbgpu_commit handed over (or null), taken once
+    E->pf_claim = nullptr;
     std::vector<u32> lens(n);
     for (u32 k = 0; k < n; k++) {
         if (input_lens[k] % 128 != 0) return fail(TBGPU_STATUS_INVALID, "create body not a multiple of 128");
@@ -879,7 +1076,7 @@ static int commit_host(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const
         // 1 from registered memory (written through to staging), or copied here.
         const u8* src = nullptr;
         const u8* events = E->staging;
-        if (one && lens[k0] && E->pf_input == inputs[k0] && E->pf_len == lens[k0] * 128 && E->pf_op == op) {
+        if (one && lens[k0] && claim == inputs[k0] && E->pf_len == lens[k0] * 128 && E->pf_op == op) {
             if (hipEventQuery(E->pf_done) != hipSuccess) HIPCK(hipStreamWaitEvent(E->stream, E->pf_done, 0));
             events = E->pf_staging;
         } else if (one && lens[k0]) {
@@ -888,7 +1085,7 @@ static int commit_host(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const
                 if (in >= r.ptr && in + (u64)lens[k0] * 128 <= r.ptr + r.bytes) src = r.dev + (in - r.ptr);
             }
         }
-        E->pf_input = nullptr;
+        claim = nullptr;
         u64 off = 0;
         for (u32 k = k0; k < k1 && !src && events == E->staging; k++) {
             if (lens[k]) HIPCK(hipMemcpyAsync(E->staging + off * 128, inputs[k], (u64)lens[k] * 128,
@@ -925,6 +1122,7 @@ static int commit_host(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const
             const u32 bytes = *(const u32*)(S.h_reply + 16);
             E->commit_ts = head[1];
             if (head[0]) {
+                E->poisoned = true;
                 return fail(TBGPU_STATUS_PANIC, "device panic 0x%llx (the reference would have trapped)",
                             (unsigned long long)head[0]);
             }
@@ -1033,6 +1231,7 @@ static int commit_pipelined(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, 
         }
         E->commit_ts = std::max(E->commit_ts, head[1]);
         if (head[0]) {
+            E->poisoned = true;
             return fail(TBGPU_STATUS_PANIC, "device panic 0x%llx (the reference would have trapped)",
                         (unsigned long long)head[0]);
         }
@@ -1095,6 +1294,7 @@ static int commit_pipelined(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, 
 extern "C" int tbgpu_commit_pipelined(tbgpu_t* E, uint8_t operation, uint32_t n, const uint64_t* timestamps,
                                       const void* const* inputs, const uint32_t* input_lens, void* const* outputs,
                                       uint32_t* out_lens, uint32_t chunk_batches, double* latency_ms) {
+    API_ENTER(E, true);
     if (E->node) return n ? node_commit_pipelined(E->node, operation, n, timestamps, inputs, input_lens, outputs, out_lens,
                                                   chunk_batches, latency_ms) : TBGPU_STATUS_OK;
     HIPCK(hipSetDevice(E->device));
@@ -1107,6 +1307,10 @@ extern "C" int tbgpu_commit(tbgpu_t* E, uint8_t operation, uint64_t timestamp, c
                             uint32_t input_len, void* output, uint32_t output_cap, uint32_t* out_len) {
     if (E->node) return node_api_commit(E->node, operation, timestamp, input, input_len, output, output_cap, out_len);
     *out_len = 0;
+    // The body tbgpu_prefetch staged (if any) may be taken by this commit only: hand it to
+    // commit_host and drop it from the engine whatever happens next.
+    const void* staged = E->pf_input;
+    API_ENTER(E, true);
     HIPCK(hipSetDevice(E->device));
     if (operation < OP_CREATE_ACCOUNTS || operation > OP_LOOKUP_TRANSFERS) {
         return fail(TBGPU_STATUS_INVALID, "unknown operation %u", operation);
@@ -1127,6 +1331,7 @@ extern "C" int tbgpu_commit(tbgpu_t* E, uint8_t operation, uint64_t timestamp, c
     }
     const void* ins[1] = {input};
     void* outs[1] = {output};
+    E->pf_claim = staged;
     return commit_host(E, operation, 1, &timestamp, ins, &input_len, outs, out_len, &output_cap);
 }
 
@@ -1159,6 +1364,7 @@ extern "C" int tbgpu_prefetch(tbgpu_t* E, uint8_t operation, const void* input, 
 extern "C" int tbgpu_commit_many(tbgpu_t* E, uint8_t operation, uint32_t n, const uint64_t* timestamps,
                                  const void* const* inputs, const uint32_t* input_lens, void* const* outputs,
                                  uint32_t* out_lens) {
+    API_ENTER(E, true);
     if (E->node) {
         for (u32 k = 0; k < n; k++) out_lens[k] = 0;
         return n ? node_commit_pipelined(E->node, operation, n, timestamps, inputs, input_lens, outputs, out_lens, 0, nullptr)
@@ -1174,6 +1380,7 @@ extern "C" int tbgpu_commit_many(tbgpu_t* E, uint8_t operation, uint32_t n, cons
 extern "C" int tbgpu_commit_device_async(tbgpu_t* E, uint8_t operation, uint32_t n_batches,
                                          const uint64_t* timestamps, const uint32_t* batch_lens,
                                          const void* events_dev, void* results_dev, uint32_t* reply_bytes_dev) {
+    API_ENTER(E, true);
     if (E->node) return fail(TBGPU_STATUS_INVALID, "device-resident commits need a single-device engine");
     HIPCK(hipSetDevice(E->device));
     const u64 floor_ts = std::max(E->commit_ts, E->pending ? E->last_batch_ts : 0);
@@ -1189,6 +1396,7 @@ extern "C" int tbgpu_commit_device_async(tbgpu_t* E, uint8_t operation, uint32_t
 }
 
 extern "C" int tbgpu_sync(tbgpu_t* E) {
+    API_ENTER(E, false);
     if (E->node) return node_sync(E->node);
     HIPCK(hipSetDevice(E->device));
     return engine_sync(E);
@@ -1201,6 +1409,7 @@ extern "C" uint64_t tbgpu_commit_timestamp(tbgpu_t* E) {
 }
 
 extern "C" int tbgpu_test_set_balances(tbgpu_t* E, uint64_t id_lo, uint64_t id_hi, const uint64_t b[8]) {
+    API_ENTER(E, true);
     if (E->node) return node_api_set_balances(E->node, id_lo, id_hi, b);
     HIPCK(hipSetDevice(E->device));
     if (E->pending) {
@@ -1242,9 +1451,9 @@ static int export_records(tbgpu* E, std::vector<u8>& recs, std::vector<u64>* pos
     u8* d_out = nullptr;
     u64* d_cnt = nullptr;
     u64* d_posted = nullptr;
-    HIPCK(hipMalloc(&d_out, chunk * 128));
-    HIPCK(hipMalloc(&d_cnt, 16));
-    HIPCK(hipMalloc(&d_posted, chunk * 16));
+    HIPCK(tbMalloc(&d_out, chunk * 128));
+    HIPCK(tbMalloc(&d_cnt, 16));
+    HIPCK(tbMalloc(&d_posted, chunk * 16));
     int st = TBGPU_STATUS_OK;
     for (u64 s = 0; s < cap && st == TBGPU_STATUS_OK; s += chunk) {
         const u64 n = std::min<u64>(chunk, cap - s);
@@ -1289,6 +1498,7 @@ static int export_records(tbgpu* E, std::vector<u8>& recs, std::vector<u64>* pos
 }
 
 extern "C" int tbgpu_export_accounts(tbgpu_t* E, void* out, uint64_t cap, uint64_t* count) {
+    API_ENTER(E, false);
     if (E->node) return node_api_export(E->node, 0, out, cap, count);
     HIPCK(hipSetDevice(E->device));
     std::vector<u8> recs;
@@ -1301,6 +1511,7 @@ extern "C" int tbgpu_export_accounts(tbgpu_t* E, void* out, uint64_t cap, uint64
 }
 
 extern "C" int tbgpu_export_transfers(tbgpu_t* E, void* out, uint64_t cap, uint64_t* count) {
+    API_ENTER(E, false);
     if (E->node) return node_api_export(E->node, 1, out, cap, count);
     HIPCK(hipSetDevice(E->device));
     std::vector<u8> recs;
@@ -1313,6 +1524,7 @@ extern "C" int tbgpu_export_transfers(tbgpu_t* E, void* out, uint64_t cap, uint6
 }
 
 extern "C" int tbgpu_export_posted(tbgpu_t* E, uint64_t* out_pairs, uint64_t cap, uint64_t* count) {
+    API_ENTER(E, false);
     if (E->node) return node_api_export(E->node, 2, out_pairs, cap, count);
     HIPCK(hipSetDevice(E->device));
     std::vector<u8> recs;
@@ -1335,26 +1547,25 @@ extern "C" int tbgpu_export_posted(tbgpu_t* E, uint64_t* out_pairs, uint64_t cap
 // Groove write-back: everything a durable replica's checkpoint / compact must insert or upsert into
 // its forest since the previous call (or since init / reset) — state_machine.zig:542-582 with the
 // groove semantics of src/lsm/groove.zig:902-963.  Accounts by id, transfers and posted pairs by
-// timestamp.  If a buffer is too small nothing advances: *counts holds the sizes needed.
+// timestamp.
 //
 // The cost is O(changes), not O(tables) (the reference's groove put / upsert per changed object):
 //   * transfers: the log positions written since the previous write-back, each checked live by one
-//     index probe (tb_delta_log);
+//     index probe (tb_delta_log_*), compacted in log (= timestamp) order on the device;
 //   * posted-groove entries: one per new post / void record (the pending transfer's timestamp,
-//     posted or voided: state_machine.zig:988-990);
+//     posted or voided: state_machine.zig:988-990), looked up on the device (tb_delta_posted);
 //   * accounts: the debit and credit accounts of the new transfers, plus the ids of create_accounts
 //     events and of direct balance writes the engine listed since — each looked up once and emitted
 //     if created since or re-balanced (tb_delta_ids).  Only create_accounts committed from device
-//     memory (or more than CKPT_IDS_MAX listed ids) makes the next write-back diff the whole account
+//     memory (or more listed ids than WB_IDS_MAX) makes the next write-back diff the whole account
 //     table instead (tb_delta_accounts).
-// The write-back snapshot exists and describes the previous write-back (the empty state if none).
+// Every device buffer is allocated at tbgpu_init (WbBufs): a write-back walks the log in slices of
+// the buffers' size.  The caller's buffers are checked up front against what the write-back can
+// emit at most (every log position since, twice as many accounts plus the listed ids), so a write-
+// back that runs always fits and a refused one changes nothing.
+//
+// The snapshot exists and describes the previous write-back (the empty state if none).
 static int ckpt_snapshot_ready(tbgpu* E) {
-    if (!E->ckpt_bal) {
-        HIPCK(hipMalloc(&E->ckpt_bal, E->account_cap * sizeof(AccountBal)));
-        HIPCK(hipMalloc(&E->ckpt_mark, E->account_cap * sizeof(u32)));
-        HIPCK(hipMemsetAsync(E->ckpt_mark, 0, E->account_cap * sizeof(u32), E->stream));
-        E->ckpt_epoch = 0;
-    }
     if (!E->ckpt_valid) {  // the previous write-back is the empty state
         HIPCK(hipMemsetAsync(E->ckpt_bal, 0, E->account_cap * sizeof(AccountBal), E->stream));
         E->ckpt_pos = 0;
@@ -1365,11 +1576,10 @@ static int ckpt_snapshot_ready(tbgpu* E) {
 }
 
 // Listed since the previous write-back (host side): ids of create_accounts events and of direct
-// balance writes.  Past CKPT_IDS_MAX the list gives way to one whole-table diff.
-#define CKPT_IDS_MAX (1ULL << 24)
+// balance writes.  Past WB_IDS_MAX the list gives way to one whole-table diff.
 static void ckpt_note_ids(tbgpu* E, const u8* records, u64 n) {
     if (E->ckpt_scan) return;
-    if (E->ckpt_ids.size() / 2 + n > CKPT_IDS_MAX) {
+    if (E->ckpt_ids.size() / 2 + n > WB_IDS_MAX) {
         E->ckpt_scan = true;
         std::vector<u64>().swap(E->ckpt_ids);
         return;
@@ -1380,206 +1590,134 @@ static void ckpt_note_ids(tbgpu* E, const u8* records, u64 n) {
     }
 }
 
-// One write-back of one engine, in steps the node engine can interleave across its shards:
-//   delta_begin      count the new transfers (ordered compaction, pass 1);
-//   delta_log_ids    their debit / credit account ids and post / void records (device lists);
-//   delta_accounts   the account delta for ids on the device (from the log) or on the host (the
-//                    listed creates and direct writes; a node routes ids to their owners), or the
-//                    whole-table diff when the engine could not list every create;
-//   delta_copy_*     into the caller's buffers, once the sizes are known to fit;
-//   delta_end        the snapshot advances (or, on failure, nothing does: the marks are epoch'd).
-struct DeltaCtx {
-    u64 pos0 = 0, range = 0, nblocks = 0, nt = 0;
-    u64* d_base = nullptr;      // [nblocks] exclusive prefix of live records per workgroup
-    u64* d_ids = nullptr;       // [nt][4] debit, credit account ids of the new transfers
-    u64* d_pv = nullptr;        // [nt][3] {pending id lo, hi, voided} of the post / void records
-    u64* d_cnt = nullptr;       // [0] accounts emitted, [1] slots seen, [2] post / void records
-    u64* d_hids = nullptr;      // host-listed ids, on the device
-    u64 hids_cap = 0;
-    u8* d_acc = nullptr;        // [acc_cap] emitted accounts
-    AccountBal* d_before = nullptr;
-    u32* d_slots = nullptr;     // [acc_cap] every slot covered (the snapshot's advance)
-    u64 acc_cap = 0;
-    bool scanned = false;
+// This write-back's epoch: every slot it covers is marked once (tb_delta_ids); wrapped, the marks
+// are cleared so no stale one can equal it.
+static int wb_next_epoch(tbgpu* E) {
+    if (++E->ckpt_epoch == 0) {
+        HIPCK(hipMemsetAsync(E->ckpt_mark, 0, E->account_cap * sizeof(u32), E->stream));
+        E->ckpt_epoch = 1;
+    }
+    return TBGPU_STATUS_OK;
+}
+
+// What a write-back of this engine can emit at most: transfers and posted entries <= the log
+// positions written since; accounts <= two per new transfer plus the listed ids (or, after an
+// unlisted create, every live account).
+struct WbBounds {
+    u64 transfers, posted, accounts;
 };
-
-static void delta_free(DeltaCtx& C) {
-    void* bufs[] = {C.d_base, C.d_ids, C.d_pv, C.d_cnt, C.d_hids, C.d_acc, C.d_before, C.d_slots};
-    for (void* p : bufs) if (p) (void)hipFree(p);
-    C = DeltaCtx{};
+static WbBounds wb_bounds(tbgpu* E, u64 live_accounts) {
+    const u64 range = E->log_next - (E->ckpt_valid ? E->ckpt_pos : 0);
+    WbBounds b;
+    b.transfers = b.posted = range;
+    b.accounts = E->ckpt_scan ? live_accounts : std::min<u64>(E->account_cap, 2 * range + E->ckpt_ids.size() / 2);
+    return b;
 }
 
-#define DCK(x)                                                                                     \
-    do {                                                                                           \
-        hipError_t e_ = (x);                                                                       \
-        if (e_ != hipSuccess) {                                                                    \
-            delta_free(C);                                                                         \
-            return fail(TBGPU_STATUS_DEVICE, "checkpoint delta: %s: %s", #x, hipGetErrorString(e_)); \
-        }                                                                                          \
-    } while (0)
+// Slice [a, b) of the log range: gather its new transfers (records, their account ids, their post /
+// void records and posted pairs) into the write-back buffers and look their accounts up.  Enqueued
+// only; the slice's counts land in d_cnt (records, post / void records, accounts emitted).
+static int wb_gather_slice(tbgpu* E, u64 a, u64 b, bool want_records, bool posted = true) {
+    WbBufs& W = E->wb;
+    const u64 n = b - a, nblocks = (n + DELTA_THREADS - 1) / DELTA_THREADS;
+    HIPCK(hipMemsetAsync(W.d_cnt + WB_ACCOUNTS, 0, 8, E->stream));
+    HIPCK(hipMemsetAsync(W.d_cnt + WB_PV, 0, 16, E->stream));  // WB_PV, WB_RECORDS
+    if (!n) return TBGPU_STATUS_OK;
+    hipLaunchKernelGGL(tb_delta_log_count, dim3((unsigned)nblocks), dim3(DELTA_THREADS), 0, E->stream, E->T, a, n, E->ckpt_ts,
+                       W.d_bc);
+    hipLaunchKernelGGL(tb_delta_scan_blocks, dim3(1), dim3(1024), 0, E->stream, W.d_bc, nblocks, W.d_base,
+                       W.d_cnt + WB_RECORDS);
+    hipLaunchKernelGGL(tb_delta_log_scatter, dim3((unsigned)nblocks), dim3(DELTA_THREADS), 0, E->stream, E->T, a, n,
+                       E->ckpt_ts, W.d_base, want_records ? W.d_out : (u8*)nullptr, W.d_ids, W.d_pv, W.d_cnt + WB_PV);
+    if (posted) {  // a node's pending transfer may live on another shard: the node looks it up
+        hipLaunchKernelGGL(tb_delta_posted, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T, W.d_pv,
+                           W.d_cnt + WB_PV, W.d_pairs, W.d_cnt + WB_STATUS);
+    }
+    HIPCK(hipGetLastError());
+    return TBGPU_STATUS_OK;
+}
 
-// Pass 1 over the log range and the ordered bases.
-static int delta_begin(tbgpu* E, DeltaCtx& C) {
-    int st = ckpt_snapshot_ready(E);
-    if (st) return st;
-    C.pos0 = E->ckpt_pos;
-    C.range = E->log_next - E->ckpt_pos;
-    C.nblocks = (C.range + DELTA_THREADS - 1) / DELTA_THREADS;
-    C.scanned = E->ckpt_scan;
-    DCK(hipMalloc(&C.d_cnt, 32));
-    DCK(hipMemsetAsync(C.d_cnt, 0, 32, E->stream));
-    if (C.nblocks) {
-        u32* d_bc = nullptr;
-        DCK(hipMalloc(&d_bc, C.nblocks * 4));
-        hipLaunchKernelGGL(tb_delta_log_count, dim3((unsigned)C.nblocks), dim3(DELTA_THREADS), 0, E->stream, E->T, C.pos0,
-                           C.range, E->ckpt_ts, d_bc);
-        std::vector<u32> bc(C.nblocks);
-        hipError_t e = hipGetLastError();
-        if (e == hipSuccess) e = hipMemcpyAsync(bc.data(), d_bc, C.nblocks * 4, hipMemcpyDeviceToHost, E->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(E->stream);
-        (void)hipFree(d_bc);
-        DCK(e);
-        std::vector<u64> base(C.nblocks);
-        for (u64 b = 0; b < C.nblocks; b++) {
-            base[b] = C.nt;
-            C.nt += bc[b];
+// The account delta of ids on the device (2 x *n_dev of them when n_dev is given, else n).
+static int wb_ids(tbgpu* E, const u64* d_ids, u64 n, const u64* n_dev) {
+    if (E->ckpt_scan || !n) return TBGPU_STATUS_OK;
+    WbBufs& W = E->wb;
+    hipLaunchKernelGGL(tb_delta_ids, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T, E->ckpt_bal, E->ckpt_ts,
+                       d_ids, n, E->ckpt_mark, E->ckpt_epoch, W.d_acc, W.d_before, W.d_cnt + WB_ACCOUNTS, W.d_slots,
+                       W.d_cnt + WB_SLOTS, n_dev);
+    HIPCK(hipGetLastError());
+    return TBGPU_STATUS_OK;
+}
+
+static int wb_read_counts(tbgpu* E) {
+    HIPCK(hipMemcpyAsync(E->wb.h_cnt, E->wb.d_cnt, WB_COUNT_WORDS * 8, hipMemcpyDeviceToHost, E->stream));
+    HIPCK(hipStreamSynchronize(E->stream));
+    if (E->wb.h_cnt[WB_STATUS]) return fail(TBGPU_STATUS_PANIC, "checkpoint delta: a posted pending transfer is missing");
+    return TBGPU_STATUS_OK;
+}
+
+// The emitted accounts of the current slice / chunk into the caller's buffers at *na.
+static int wb_take_accounts(tbgpu* E, u8* out, u8* before_out, u64* na) {
+    const u64 k = E->wb.h_cnt[WB_ACCOUNTS];
+    if (k) {
+        HIPCK(hipMemcpyAsync(out + *na * 128, E->wb.d_acc, k * 128, hipMemcpyDeviceToHost, E->stream));
+        if (before_out) {
+            HIPCK(hipMemcpyAsync(before_out + *na * sizeof(AccountBal), E->wb.d_before, k * sizeof(AccountBal),
+                                 hipMemcpyDeviceToHost, E->stream));
         }
-        DCK(hipMalloc(&C.d_base, C.nblocks * 8));
-        DCK(hipMemcpyAsync(C.d_base, base.data(), C.nblocks * 8, hipMemcpyHostToDevice, E->stream));
-        DCK(hipStreamSynchronize(E->stream));
+        HIPCK(hipStreamSynchronize(E->stream));
     }
+    *na += k;
+    HIPCK(hipMemsetAsync(E->wb.d_cnt + WB_ACCOUNTS, 0, 8, E->stream));
     return TBGPU_STATUS_OK;
 }
 
-// Room for the emitted accounts: the accounts a write-back can name (the ids looked up: two per new
-// transfer plus the listed ones, at most every account); a whole-table diff, every account.
-static int delta_alloc_accounts(tbgpu* E, DeltaCtx& C, u64 host_ids) {
-    C.acc_cap = std::max<u64>(1, C.scanned ? E->account_cap : std::min<u64>(E->account_cap, 2 * C.nt + host_ids));
-    DCK(hipMalloc(&C.d_acc, C.acc_cap * 128));
-    DCK(hipMalloc(&C.d_before, C.acc_cap * sizeof(AccountBal)));
-    if (!C.scanned) {
-        DCK(hipMalloc(&C.d_slots, C.acc_cap * 4));
-        if (++E->ckpt_epoch == 0) {  // one epoch per write-back; wrapped: no stale mark may equal it
-            DCK(hipMemsetAsync(E->ckpt_mark, 0, E->account_cap * sizeof(u32), E->stream));
-            E->ckpt_epoch = 1;
-        }
-    }
-    return TBGPU_STATUS_OK;
-}
-
-// Pass 2: the new transfers' account ids and post / void records, on the device.  ids_host /
-// pv_host (optional): copies on the host (the node routes them).
-static int delta_log_ids(tbgpu* E, DeltaCtx& C, std::vector<u64>* ids_host, std::vector<u64>* pv_host) {
-    if (!C.nt) return TBGPU_STATUS_OK;
-    DCK(hipMalloc(&C.d_ids, C.nt * 32));
-    DCK(hipMalloc(&C.d_pv, C.nt * 24));
-    hipLaunchKernelGGL(tb_delta_log_scatter, dim3((unsigned)C.nblocks), dim3(DELTA_THREADS), 0, E->stream, E->T, C.pos0,
-                       C.range, E->ckpt_ts, C.d_base, (u8*)nullptr, C.d_ids, C.d_pv, C.d_cnt + 2);
-    DCK(hipGetLastError());
-    u64 npv = 0;
-    DCK(hipMemcpyAsync(&npv, C.d_cnt + 2, 8, hipMemcpyDeviceToHost, E->stream));
-    DCK(hipStreamSynchronize(E->stream));
-    if (pv_host) {
-        pv_host->resize(npv * 3);
-        if (npv) DCK(hipMemcpy(pv_host->data(), C.d_pv, npv * 24, hipMemcpyDeviceToHost));
-    }
-    if (ids_host) {
-        ids_host->resize(C.nt * 4);
-        DCK(hipMemcpy(ids_host->data(), C.d_ids, C.nt * 32, hipMemcpyDeviceToHost));
-    }
-    return TBGPU_STATUS_OK;
-}
-
-// The account delta of n ids in device memory (appended to the context's emitted accounts).
-static int delta_ids_dev(tbgpu* E, DeltaCtx& C, const u64* d_ids, u64 n) {
-    if (C.scanned || !n) return TBGPU_STATUS_OK;
-    hipLaunchKernelGGL(tb_delta_ids, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T, E->ckpt_bal,
-                       E->ckpt_ts, d_ids, n, E->ckpt_mark, E->ckpt_epoch, C.d_acc, C.d_before, C.d_cnt, C.d_slots,
-                       C.d_cnt + 1);
-    DCK(hipGetLastError());
-    return TBGPU_STATUS_OK;
-}
-
-static int delta_ids_host(tbgpu* E, DeltaCtx& C, const std::vector<u64>& ids) {
+// Listed ids (host) in chunks of the ids buffer, each chunk's accounts taken as it completes.
+static int wb_listed_ids(tbgpu* E, const std::vector<u64>& ids, u8* out, u8* before_out, u64* na) {
     const u64 n = ids.size() / 2;
-    if (C.scanned || !n) return TBGPU_STATUS_OK;
-    if (n > C.hids_cap) {
-        if (C.d_hids) (void)hipFree(C.d_hids);
-        C.d_hids = nullptr;
-        DCK(hipMalloc(&C.d_hids, n * 16));
-        C.hids_cap = n;
+    for (u64 c = 0; c < n && !E->ckpt_scan; c += E->wb.cap_ids) {
+        const u64 m = std::min<u64>(E->wb.cap_ids, n - c);
+        HIPCK(hipMemcpyAsync(E->wb.d_hids, ids.data() + 2 * c, m * 16, hipMemcpyHostToDevice, E->stream));
+        int st = wb_ids(E, E->wb.d_hids, m, nullptr);
+        if (!st) st = wb_read_counts(E);  // also: the host list may change once this returns
+        if (!st) st = wb_take_accounts(E, out, before_out, na);
+        if (st) return st;
     }
-    DCK(hipMemcpyAsync(C.d_hids, ids.data(), n * 16, hipMemcpyHostToDevice, E->stream));
-    const int st = delta_ids_dev(E, C, C.d_hids, n);
-    if (st) return st;
-    DCK(hipStreamSynchronize(E->stream));  // the host buffer may go away
     return TBGPU_STATUS_OK;
 }
 
-// The whole-table diff (after creates the engine could not list); on a node shard (world > 1) only
-// the accounts it owns.
-static int delta_scan(tbgpu* E, DeltaCtx& C, u32 world, u32 self) {
-    if (!C.scanned) return TBGPU_STATUS_OK;
-    hipLaunchKernelGGL(tb_delta_accounts, dim3((unsigned)((E->account_cap + 255) / 256)), dim3(256), 0, E->stream, E->T,
-                       E->ckpt_bal, E->ckpt_ts, (u64)0, E->account_cap, C.d_acc, C.acc_cap, C.d_cnt, C.d_before, world, self);
-    DCK(hipGetLastError());
+// The whole-table diff, in slot ranges of the accounts buffer; on a node shard (world > 1) only the
+// accounts it owns.
+static int wb_scan(tbgpu* E, u32 world, u32 self, u8* out, u8* before_out, u64* na) {
+    if (!E->ckpt_scan) return TBGPU_STATUS_OK;
+    for (u64 s0 = 0; s0 < E->account_cap; s0 += E->wb.cap_a) {
+        const u64 s1 = std::min<u64>(E->account_cap, s0 + E->wb.cap_a);
+        hipLaunchKernelGGL(tb_delta_accounts, dim3((unsigned)((s1 - s0 + 255) / 256)), dim3(256), 0, E->stream, E->T,
+                           E->ckpt_bal, E->ckpt_ts, s0, s1, E->wb.d_acc, E->wb.cap_a, E->wb.d_cnt + WB_ACCOUNTS,
+                           E->wb.d_before, world, self);
+        HIPCK(hipGetLastError());
+        int st = wb_read_counts(E);
+        if (!st) st = wb_take_accounts(E, out, before_out, na);
+        if (st) return st;
+    }
     return TBGPU_STATUS_OK;
 }
 
-static int delta_account_count(tbgpu* E, DeltaCtx& C, u64* na) {
-    u64 cnt[2] = {0, 0};
-    DCK(hipMemcpyAsync(cnt, C.d_cnt, 16, hipMemcpyDeviceToHost, E->stream));
-    DCK(hipStreamSynchronize(E->stream));
-    *na = cnt[0];
-    return TBGPU_STATUS_OK;
-}
-
-// The new transfers, in log (= timestamp) order, into host memory; in slices of a bounded device
-// buffer.
-static int delta_copy_transfers(tbgpu* E, DeltaCtx& C, u8* out) {
-    if (!C.nt) return TBGPU_STATUS_OK;
-    u8* d_out = nullptr;
-    DCK(hipMalloc(&d_out, C.nt * 128));
-    hipLaunchKernelGGL(tb_delta_log_scatter, dim3((unsigned)C.nblocks), dim3(DELTA_THREADS), 0, E->stream, E->T, C.pos0,
-                       C.range, E->ckpt_ts, C.d_base, d_out, (u64*)nullptr, (u64*)nullptr, (u64*)nullptr);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, C.nt * 128, hipMemcpyDeviceToHost, E->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(E->stream);
-    (void)hipFree(d_out);
-    DCK(e);
-    return TBGPU_STATUS_OK;
-}
-
-static int delta_copy_accounts(tbgpu* E, DeltaCtx& C, u64 na, u8* out, u8* before_out) {
-    if (!na) return TBGPU_STATUS_OK;
-    DCK(hipMemcpyAsync(out, C.d_acc, na * 128, hipMemcpyDeviceToHost, E->stream));
-    if (before_out) DCK(hipMemcpyAsync(before_out, C.d_before, na * sizeof(AccountBal), hipMemcpyDeviceToHost, E->stream));
-    DCK(hipStreamSynchronize(E->stream));
-    return TBGPU_STATUS_OK;
-}
-
-// The write-back happened: the snapshot takes the covered balances, the log and commit positions
-// move, the lists empty.
-static int delta_end(tbgpu* E, DeltaCtx& C) {
-    if (C.scanned) {
-        DCK(hipMemcpyAsync(E->ckpt_bal, E->T.acct_bal, E->account_cap * sizeof(AccountBal), hipMemcpyDeviceToDevice,
-                           E->stream));
+// The write-back happened: the snapshot takes the covered balances (enqueued), the log and commit
+// positions move, the lists empty.
+static int wb_advance(tbgpu* E) {
+    if (E->ckpt_scan) {
+        HIPCK(hipMemcpyAsync(E->ckpt_bal, E->T.acct_bal, E->account_cap * sizeof(AccountBal), hipMemcpyDeviceToDevice,
+                             E->stream));
     } else {
-        u64 cnt[2] = {0, 0};
-        DCK(hipMemcpyAsync(cnt, C.d_cnt, 16, hipMemcpyDeviceToHost, E->stream));
-        DCK(hipStreamSynchronize(E->stream));
-        if (cnt[1]) {
-            hipLaunchKernelGGL(tb_delta_advance, dim3((unsigned)((cnt[1] + 255) / 256)), dim3(256), 0, E->stream, E->T,
-                               E->ckpt_bal, C.d_slots, cnt[1]);
-            DCK(hipGetLastError());
-        }
+        const u32 grid = (u32)std::max<u64>(1, std::min<u64>(2048, (E->account_cap + 255) / 256));
+        hipLaunchKernelGGL(tb_delta_advance, dim3(grid), dim3(256), 0, E->stream, E->T, E->ckpt_bal, E->wb.d_slots,
+                           E->wb.d_cnt + WB_SLOTS);
+        HIPCK(hipGetLastError());
     }
-    DCK(hipStreamSynchronize(E->stream));
     E->ckpt_pos = E->log_next;
     E->ckpt_ts = E->commit_ts;
     E->ckpt_scan = false;
     std::vector<u64>().swap(E->ckpt_ids);
-    delta_free(C);
     return TBGPU_STATUS_OK;
 }
 
@@ -1597,78 +1735,188 @@ static void delta_sort_by_timestamp(u8* recs, u64 n) {
     for (u64 i = 0; i < n; i++) memcpy(recs + i * 128, &tmp[key[i].second * 128], 128);
 }
 
-// The posted-groove pairs of the post / void records: {pending transfer's timestamp, voided}.
-static int delta_posted_pairs(const std::vector<u64>& pv, std::vector<std::pair<u64, u64>>& out,
-                              const std::function<int(const u64*, u32, u8*, u8*)>& fetch) {
-    const u64 n = pv.size() / 3;
-    if (!n) return TBGPU_STATUS_OK;
-    std::vector<u64> ids(2 * n);
-    for (u64 i = 0; i < n; i++) {
-        ids[2 * i] = pv[3 * i];
-        ids[2 * i + 1] = pv[3 * i + 1];
+static void delta_sort_pairs(u64* pairs, u64 n) {
+    std::sort((std::pair<u64, u64>*)pairs, (std::pair<u64, u64>*)pairs + n);
+}
+
+// The asynchronous write-back in flight (if any) has landed: its counts, sorted outputs.
+static int wb_wait(tbgpu* E, tbgpu_delta_counts* counts) {
+    WbBufs& W = E->wb;
+    if (!W.inflight) return fail(TBGPU_STATUS_INVALID, "no asynchronous write-back in flight");
+    W.inflight = false;
+    HIPCK(hipEventSynchronize(W.done));
+    *counts = W.counts;
+    counts->transfers = W.h_cnt[WB_RECORDS];
+    counts->posted = W.h_cnt[WB_PV];
+    counts->accounts = W.h_cnt[WB_ACCOUNTS];
+    if (W.h_cnt[WB_STATUS]) {
+        E->poisoned = true;
+        return fail(TBGPU_STATUS_PANIC, "checkpoint delta: a posted pending transfer is missing");
     }
-    std::vector<u8> rec(n * 128), st(n);
-    const int s = fetch(ids.data(), (u32)n, rec.data(), st.data());
-    if (s) return s;
-    for (u64 i = 0; i < n; i++) {
-        if (!st[i]) return fail(TBGPU_STATUS_PANIC, "checkpoint delta: a posted pending transfer is missing");
-        out.push_back({*(const u64*)&rec[i * 128 + 120], pv[3 * i + 2]});
+    delta_sort_by_timestamp(W.out_t, counts->transfers);
+    delta_sort_pairs(W.out_p, counts->posted);
+    return TBGPU_STATUS_OK;
+}
+
+static int wb_checkpoint_sync(tbgpu* E, u8* accounts_out, u8* before_out, u64 accounts_cap, u8* transfers_out,
+                              u64 transfers_cap, u64* posted_out, u64 posted_cap, tbgpu_delta_counts* counts) {
+    memset(counts, 0, sizeof(*counts));
+    int st = ckpt_snapshot_ready(E);
+    if (st) return st;
+    const WbBounds bd = wb_bounds(E, E->h_globals->account_count);
+    counts->created_after = E->ckpt_ts;
+    if (bd.accounts > accounts_cap || bd.transfers > transfers_cap || bd.posted > posted_cap) {  // nothing moved
+        counts->accounts = bd.accounts;
+        counts->transfers = bd.transfers;
+        counts->posted = bd.posted;
+        return fail(TBGPU_STATUS_INVALID, "checkpoint delta: buffers must hold %llu accounts, %llu transfers, %llu posted",
+                    (unsigned long long)bd.accounts, (unsigned long long)bd.transfers, (unsigned long long)bd.posted);
     }
-    std::sort(out.begin(), out.end());
+    if ((st = wb_next_epoch(E))) return st;
+    HIPCK(hipMemsetAsync(E->wb.d_cnt, 0, WB_COUNT_WORDS * 8, E->stream));
+    u64 nt = 0, npv = 0, na = 0;
+    for (u64 a = E->ckpt_pos; a < E->log_next; a += E->wb.cap_t) {
+        const u64 b = std::min<u64>(E->log_next, a + E->wb.cap_t);
+        if ((st = wb_gather_slice(E, a, b, true))) return st;
+        if ((st = wb_ids(E, E->wb.d_ids, 2 * (b - a), E->wb.d_cnt + WB_RECORDS))) return st;
+        if ((st = wb_read_counts(E))) return st;
+        const u64* c = E->wb.h_cnt;
+        if (c[WB_RECORDS]) HIPCK(hipMemcpyAsync(transfers_out + nt * 128, E->wb.d_out, c[WB_RECORDS] * 128,
+                                                hipMemcpyDeviceToHost, E->stream));
+        if (c[WB_PV]) HIPCK(hipMemcpyAsync(posted_out + 2 * npv, E->wb.d_pairs, c[WB_PV] * 16, hipMemcpyDeviceToHost,
+                                           E->stream));
+        nt += c[WB_RECORDS];
+        npv += c[WB_PV];
+        if ((st = wb_take_accounts(E, accounts_out, before_out, &na))) return st;  // syncs the copies above too
+    }
+    if ((st = wb_listed_ids(E, E->ckpt_ids, accounts_out, before_out, &na))) return st;
+    if ((st = wb_scan(E, 0, 0, accounts_out, before_out, &na))) return st;
+    if ((st = wb_advance(E))) return st;
+    HIPCK(hipStreamSynchronize(E->stream));
+    delta_sort_by_timestamp(transfers_out, nt);
+    delta_sort_pairs(posted_out, npv);
+    counts->accounts = na;
+    counts->transfers = nt;
+    counts->posted = npv;
     return TBGPU_STATUS_OK;
 }
 
 extern "C" int tbgpu_checkpoint_delta(tbgpu_t* E, void* accounts_out, void* accounts_before_out, uint64_t accounts_cap,
                                       void* transfers_out, uint64_t transfers_cap, uint64_t* posted_out,
                                       uint64_t posted_cap, tbgpu_delta_counts* counts) {
+    API_ENTER(E, true);
     if (E->node) return node_api_checkpoint_delta(E->node, accounts_out, accounts_before_out, accounts_cap, transfers_out,
                                                   transfers_cap, posted_out, posted_cap, counts);
     HIPCK(hipSetDevice(E->device));
-    memset(counts, 0, sizeof(*counts));
+    if (E->wb.inflight) return fail(TBGPU_STATUS_INVALID, "an asynchronous write-back is in flight (tbgpu_checkpoint_delta_wait)");
+    int st = engine_sync(E);  // the globals (live accounts) and every enqueued commit
+    if (st) return st;
+    return wb_checkpoint_sync(E, (u8*)accounts_out, (u8*)accounts_before_out, accounts_cap, (u8*)transfers_out,
+                              transfers_cap, posted_out, posted_cap, counts);
+}
+
+// The durable replica's compact without the wait (tbgpu.h): the bar's delta is gathered on the
+// engine stream in stream order (so the next commits follow it), the snapshot advances there, and
+// the objects cross PCIe on the write-back stream beside the next commits, straight into the
+// caller's registered buffers (tb_delta_out).  When a precondition does not hold, the write-back runs
+// synchronously instead and tbgpu_checkpoint_delta_wait returns at once.
+extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void* accounts_before_out,
+                                            uint64_t accounts_cap, void* transfers_out, uint64_t transfers_cap,
+                                            uint64_t* posted_out, uint64_t posted_cap) {
+    API_ENTER(E, true);
+    if (E->node) return fail(TBGPU_STATUS_INVALID, "asynchronous write-back needs a single-device engine");
+    HIPCK(hipSetDevice(E->device));
+    WbBufs& W = E->wb;
+    if (W.inflight) return fail(TBGPU_STATUS_INVALID, "an asynchronous write-back is in flight (tbgpu_checkpoint_delta_wait)");
     if (E->pending) {
-        int st = engine_sync(E);
+        const int st = engine_sync(E);
         if (st) return st;
     }
-    DeltaCtx C;
-    std::vector<u64> pv;
-    int st = delta_begin(E, C);
-    if (!st) st = delta_alloc_accounts(E, C, E->ckpt_ids.size() / 2);
-    if (!st) st = delta_log_ids(E, C, nullptr, &pv);
-    if (!st) st = delta_ids_dev(E, C, C.d_ids, 2 * C.nt);
-    if (!st) st = delta_ids_host(E, C, E->ckpt_ids);
-    if (!st) st = delta_scan(E, C, 0, 0);
-    u64 na = 0;
-    if (!st) st = delta_account_count(E, C, &na);
-    std::vector<std::pair<u64, u64>> posted;
-    if (!st) {
-        st = delta_posted_pairs(pv, posted, [&](const u64* ids, u32 n, u8* out, u8* state) {
-            return tbgpu_fetch_transfers(E, ids, n, out, state);
-        });
+    int st = ckpt_snapshot_ready(E);
+    if (st) return st;
+    const u64 range = E->log_next - E->ckpt_pos;
+    const WbBounds bd = wb_bounds(E, ~0ULL);
+    // The caller's buffers, device-mapped (registered memory).
+    auto mapped = [&](const void* p, u64 bytes) -> u8* {
+        for (const auto& r : E->host_regions) {
+            if ((const u8*)p >= r.ptr && (const u8*)p + bytes <= r.ptr + r.bytes) return (u8*)r.dev + ((const u8*)p - r.ptr);
+        }
+        return nullptr;
+    };
+    u8* m_acc = mapped(accounts_out, bd.accounts * 128);
+    u8* m_before = accounts_before_out ? mapped(accounts_before_out, bd.accounts * sizeof(AccountBal)) : nullptr;
+    u8* m_t = mapped(transfers_out, bd.transfers * 128);
+    u8* m_p = mapped(posted_out, bd.posted * 16);
+    const bool fits = !E->ckpt_scan && range <= W.cap_t && E->ckpt_ids.size() / 2 <= W.cap_ids &&
+                      bd.accounts <= W.cap_a && bd.accounts <= accounts_cap && bd.transfers <= transfers_cap &&
+                      bd.posted <= posted_cap && m_acc && m_t && m_p && (m_before || !accounts_before_out);
+    W.out_t = (u8*)transfers_out;
+    W.out_p = posted_out;
+    if (!fits) {  // the synchronous write-back, its result kept for the wait
+        st = engine_sync(E);
+        if (!st) st = wb_checkpoint_sync(E, (u8*)accounts_out, (u8*)accounts_before_out, accounts_cap, (u8*)transfers_out,
+                                         transfers_cap, posted_out, posted_cap, &W.counts);
+        if (st) return st;
+        W.h_cnt[WB_RECORDS] = W.counts.transfers;
+        W.h_cnt[WB_PV] = W.counts.posted;
+        W.h_cnt[WB_ACCOUNTS] = W.counts.accounts;
+        W.h_cnt[WB_STATUS] = 0;
+        W.out_t = nullptr;  // already sorted
+        W.out_p = nullptr;
+        HIPCK(hipEventRecord(W.done, E->stream));
+        W.inflight = true;
+        return TBGPU_STATUS_OK;
     }
-    if (st) {
-        delta_free(C);
-        return st;
+    memset(&W.counts, 0, sizeof(W.counts));
+    W.counts.created_after = E->ckpt_ts;
+    if ((st = wb_next_epoch(E))) return st;
+    HIPCK(hipMemsetAsync(W.d_cnt, 0, WB_COUNT_WORDS * 8, E->stream));
+    if ((st = wb_gather_slice(E, E->ckpt_pos, E->log_next, true))) return st;
+    if ((st = wb_ids(E, W.d_ids, 2 * range, W.d_cnt + WB_RECORDS))) return st;
+    const u64 nl = E->ckpt_ids.size() / 2;
+    if (nl) {  // the listed ids cross in the same stream order (their host copy lives until then)
+        W.ids_inflight.swap(E->ckpt_ids);
+        HIPCK(hipMemcpyAsync(W.d_hids, W.ids_inflight.data(), nl * 16, hipMemcpyHostToDevice, E->stream));
+        if ((st = wb_ids(E, W.d_hids, nl, nullptr))) return st;
     }
-    counts->created_after = E->ckpt_ts;
-    counts->accounts = na;
-    counts->transfers = C.nt;
-    counts->posted = posted.size();
-    if (na > accounts_cap || C.nt > transfers_cap || posted.size() > posted_cap) {  // nothing advanced
-        delta_free(C);
-        return fail(TBGPU_STATUS_INVALID, "checkpoint delta: needs %llu accounts, %llu transfers, %llu posted",
-                    (unsigned long long)na, (unsigned long long)counts->transfers, (unsigned long long)counts->posted);
-    }
-    for (size_t i = 0; i < posted.size(); i++) {
-        posted_out[2 * i] = posted[i].first;
-        posted_out[2 * i + 1] = posted[i].second;
-    }
-    if ((st = delta_copy_transfers(E, C, (u8*)transfers_out))) return st;
-    delta_sort_by_timestamp((u8*)transfers_out, C.nt);
-    if ((st = delta_copy_accounts(E, C, na, (u8*)accounts_out, (u8*)accounts_before_out))) return st;
-    return delta_end(E, C);
+    if ((st = wb_advance(E))) return st;
+    HIPCK(hipMemcpyAsync(W.h_cnt, W.d_cnt, WB_COUNT_WORDS * 8, hipMemcpyDeviceToHost, E->stream));
+    HIPCK(hipEventRecord(W.gathered, E->stream));
+    HIPCK(hipStreamWaitEvent(W.stream, W.gathered, 0));
+    DeltaOut O{};
+    O.src[0] = W.d_out;
+    O.dst[0] = m_t;
+    O.count[0] = W.d_cnt + WB_RECORDS;
+    O.elem[0] = 128;
+    O.src[1] = W.d_acc;
+    O.dst[1] = m_acc;
+    O.count[1] = W.d_cnt + WB_ACCOUNTS;
+    O.elem[1] = 128;
+    O.src[2] = m_before ? (const u8*)W.d_before : nullptr;
+    O.dst[2] = m_before;
+    O.count[2] = W.d_cnt + WB_ACCOUNTS;
+    O.elem[2] = sizeof(AccountBal);
+    O.src[3] = (const u8*)W.d_pairs;
+    O.dst[3] = m_p;
+    O.count[3] = W.d_cnt + WB_PV;
+    O.elem[3] = 16;
+    hipLaunchKernelGGL(tb_delta_out, dim3(WB_OUT_GRID), dim3(256), 0, W.stream, O);
+    HIPCK(hipGetLastError());
+    HIPCK(hipEventRecord(W.done, W.stream));
+    W.inflight = true;
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_checkpoint_delta_wait(tbgpu_t* E, tbgpu_delta_counts* counts) {
+    API_ENTER(E, false);
+    memset(counts, 0, sizeof(*counts));
+    if (E->node) return fail(TBGPU_STATUS_INVALID, "asynchronous write-back needs a single-device engine");
+    HIPCK(hipSetDevice(E->device));
+    return wb_wait(E, counts);
 }
 
 extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
+    API_ENTER(E, false);
     if (E->node) return node_api_get_stats(E->node, s);
     HIPCK(hipSetDevice(E->device));
     if (E->pending) {
@@ -1693,6 +1941,10 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     s->launches_clear = E->prof_n[K_CLEAR];
     s->ms_apply = E->prof_ms[K_APPLY];
     s->launches_apply = E->prof_n[K_APPLY];
+    for (u32 k = 0; k < 3; k++) {
+        s->span_ms[k] = E->span_ms[k];
+        s->span_launches[k] = E->span_n[k];
+    }
     s->flow_passes = g.flow_passes;
     s->flow_units = g.flow_units;
     s->flow_runs = g.flow_runs;
@@ -1730,11 +1982,16 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
 extern "C" void tbgpu_reset_stats(tbgpu_t* E) {
     if (E->node) {
         for (u32 d = 0; d < node_world(E->node); d++) tbgpu_reset_stats(node_engine(E->node, d));
+        node_reset_stats(E->node);
         return;
     }
     for (int k = 0; k < K_COUNT; k++) {
         E->prof_ms[k] = 0;
         E->prof_n[k] = 0;
+    }
+    for (int k = 0; k < 3; k++) {
+        E->span_ms[k] = 0;
+        E->span_n[k] = 0;
     }
     E->passes = 0;
     E->events = 0;
@@ -1742,6 +1999,8 @@ extern "C" void tbgpu_reset_stats(tbgpu_t* E) {
 }
 
 extern "C" const char* tbgpu_last_error(void) { return g_err.c_str(); }
+
+extern "C" uint64_t tbgpu_debug_allocations(void) { return g_allocs.load(); }
 
 // vsr.checksum (src/vsr/checksum.zig:50): host only, no device or engine needed.
 extern "C" void tbgpu_checksum(const void* data, uint64_t len, uint8_t out[16]) {
@@ -1773,6 +2032,7 @@ static WorkloadParams workload_params(const tbgpu_workload* w, u64 first) {
 
 extern "C" int tbgpu_bench_generate_accounts(tbgpu_t* E, void* out_dev, uint64_t first, uint64_t count,
                                              const tbgpu_workload* w) {
+    API_ENTER(E, false);
     if (E->node) E = node_engine(E->node, 0);
     HIPCK(hipSetDevice(E->device));
     if (count == 0) return TBGPU_STATUS_OK;
@@ -1784,6 +2044,7 @@ extern "C" int tbgpu_bench_generate_accounts(tbgpu_t* E, void* out_dev, uint64_t
 
 extern "C" int tbgpu_bench_generate_transfers(tbgpu_t* E, void* out_dev, uint64_t first, uint64_t count,
                                               const tbgpu_workload* w) {
+    API_ENTER(E, false);
     if (E->node) E = node_engine(E->node, 0);
     HIPCK(hipSetDevice(E->device));
     if (count == 0) return TBGPU_STATUS_OK;
@@ -1795,6 +2056,7 @@ extern "C" int tbgpu_bench_generate_transfers(tbgpu_t* E, void* out_dev, uint64_
 }
 
 extern "C" int tbgpu_bench_walk_merge_max(tbgpu_t* E, uint32_t segments) {
+    API_ENTER(E, false);
     if (E->node) {
         for (u32 d = 0; d < node_world(E->node); d++) tbgpu_bench_walk_merge_max(node_engine(E->node, d), segments);
         return TBGPU_STATUS_OK;
@@ -1804,6 +2066,7 @@ extern "C" int tbgpu_bench_walk_merge_max(tbgpu_t* E, uint32_t segments) {
 }
 
 extern "C" int tbgpu_bench_legs_min_events(tbgpu_t* E, uint32_t events) {
+    API_ENTER(E, false);
     if (E->node) {
         for (u32 d = 0; d < node_world(E->node); d++) tbgpu_bench_legs_min_events(node_engine(E->node, d), events);
         return TBGPU_STATUS_OK;
@@ -1830,6 +2093,7 @@ static float access_mix_ms(tbgpu_t* E, const MixArgs& A, int reps) {
 }
 
 extern "C" int tbgpu_bench_access_mix(tbgpu_t* E, uint64_t transfers, double out_ms[7]) {
+    API_ENTER(E, false);
     if (E->node) E = node_engine(E->node, 0);
     HIPCK(hipSetDevice(E->device));
     HIPCK(hipStreamSynchronize(E->stream));
@@ -1841,10 +2105,10 @@ extern "C" int tbgpu_bench_access_mix(tbgpu_t* E, uint64_t transfers, double out
     void *ev = nullptr, *rec = nullptr, *s4 = nullptr, *s2 = nullptr, *s8 = nullptr, *rw = nullptr, *ix = nullptr,
          *sink = nullptr;
     int st = TBGPU_STATUS_OK;
-    if (hipMalloc(&ev, transfers * 128) != hipSuccess || hipMalloc(&rec, transfers * 128) != hipSuccess ||
-        hipMalloc(&s4, transfers * 16) != hipSuccess || hipMalloc(&s2, transfers * 2) != hipSuccess ||
-        hipMalloc(&s8, transfers * 24) != hipSuccess || hipMalloc(&rw, rows * 32) != hipSuccess ||
-        hipMalloc(&ix, E->xidx_cap * 8) != hipSuccess || hipMalloc(&sink, 8) != hipSuccess ||
+    if (tbMalloc(&ev, transfers * 128) != hipSuccess || tbMalloc(&rec, transfers * 128) != hipSuccess ||
+        tbMalloc(&s4, transfers * 16) != hipSuccess || tbMalloc(&s2, transfers * 2) != hipSuccess ||
+        tbMalloc(&s8, transfers * 24) != hipSuccess || tbMalloc(&rw, rows * 32) != hipSuccess ||
+        tbMalloc(&ix, E->xidx_cap * 8) != hipSuccess || tbMalloc(&sink, 8) != hipSuccess ||
         hipMemsetAsync(ev, 1, transfers * 128, E->stream) != hipSuccess ||
         hipMemsetAsync(rw, 2, rows * 32, E->stream) != hipSuccess) {
         st = fail(TBGPU_STATUS_DEVICE, "access mix: allocation failed");
@@ -1873,6 +2137,7 @@ extern "C" int tbgpu_bench_access_mix(tbgpu_t* E, uint64_t transfers, double out
 }
 
 extern "C" int tbgpu_bench_profile_mask(tbgpu_t* E, uint32_t mask) {
+    API_ENTER(E, false);
     if (E->node) {
         for (u32 d = 0; d < node_world(E->node); d++) tbgpu_bench_profile_mask(node_engine(E->node, d), mask);
         return TBGPU_STATUS_OK;
@@ -1888,7 +2153,7 @@ static int ledger_summary(tbgpu* E, u32 world, u32 self, u64 out[10]) {
         if (st) return st;
     }
     u64* d = nullptr;
-    HIPCK(hipMalloc(&d, 80));
+    HIPCK(tbMalloc(&d, 80));
     hipError_t e = hipMemsetAsync(d, 0, 80, E->stream);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(tb_ledger_summary, dim3((unsigned)((E->account_cap + 255) / 256)), dim3(256), 0, E->stream, E->T,
@@ -1903,6 +2168,7 @@ static int ledger_summary(tbgpu* E, u32 world, u32 self, u64 out[10]) {
 }
 
 extern "C" int tbgpu_bench_ledger_summary(tbgpu_t* E, tbgpu_ledger_summary* out) {
+    API_ENTER(E, false);
     memset(out, 0, sizeof(*out));
     const u32 W = E->node ? node_world(E->node) : 1;
     for (u32 d = 0; d < W; d++) {
@@ -1921,13 +2187,15 @@ extern "C" int tbgpu_bench_ledger_summary(tbgpu_t* E, tbgpu_ledger_summary* out)
 }
 
 extern "C" int tbgpu_device_alloc(tbgpu_t* E, uint64_t bytes, void** out) {
+    API_ENTER(E, false);
     if (E->node) E = node_engine(E->node, 0);
     HIPCK(hipSetDevice(E->device));
-    HIPCK(hipMalloc(out, bytes));
+    HIPCK(tbMalloc(out, bytes));
     return TBGPU_STATUS_OK;
 }
 
 extern "C" int tbgpu_device_free(tbgpu_t* E, void* ptr) {
+    API_ENTER(E, false);
     if (E->node) E = node_engine(E->node, 0);
     HIPCK(hipSetDevice(E->device));
     HIPCK(hipFree(ptr));
@@ -1937,6 +2205,7 @@ extern "C" int tbgpu_device_free(tbgpu_t* E, void* ptr) {
 // The replica's message pool is allocated once at init (static allocation); registering it lets
 // the prepare bodies go to HBM by DMA straight from the message, with no staging copy.
 extern "C" int tbgpu_register_host(tbgpu_t* E, void* ptr, uint64_t bytes) {
+    API_ENTER(E, false);
     if (E->node) return node_api_register_host(E->node, ptr, bytes);
     HIPCK(hipSetDevice(E->device));
     HIPCK(hipHostRegister(ptr, bytes, hipHostRegisterMapped));
@@ -1947,6 +2216,7 @@ extern "C" int tbgpu_register_host(tbgpu_t* E, void* ptr, uint64_t bytes) {
 }
 
 extern "C" int tbgpu_unregister_host(tbgpu_t* E, void* ptr) {
+    API_ENTER(E, false);
     if (E->node) return node_api_unregister_host(E->node, ptr);
     HIPCK(hipSetDevice(E->device));
     if (E->pending) {
@@ -1965,6 +2235,7 @@ extern "C" int tbgpu_unregister_host(tbgpu_t* E, void* ptr) {
 }
 
 extern "C" int tbgpu_copy_to_host(tbgpu_t* E, void* dst, const void* src_dev, uint64_t bytes) {
+    API_ENTER(E, false);
     if (E->node) E = node_engine(E->node, 0);
     HIPCK(hipSetDevice(E->device));
     HIPCK(hipStreamSynchronize(E->stream));
@@ -1973,6 +2244,7 @@ extern "C" int tbgpu_copy_to_host(tbgpu_t* E, void* dst, const void* src_dev, ui
 }
 
 extern "C" int tbgpu_copy_to_device(tbgpu_t* E, void* dst_dev, const void* src, uint64_t bytes) {
+    API_ENTER(E, false);
     if (E->node) E = node_engine(E->node, 0);
     HIPCK(hipSetDevice(E->device));
     HIPCK(hipStreamSynchronize(E->stream));
@@ -1981,6 +2253,7 @@ extern "C" int tbgpu_copy_to_device(tbgpu_t* E, void* dst_dev, const void* src, 
 }
 
 extern "C" int tbgpu_bench_reset_transfers(tbgpu_t* E) {
+    API_ENTER(E, true);
     if (E->node) {
         for (u32 d = 0; d < node_world(E->node); d++) {
             const int st = tbgpu_bench_reset_transfers(node_engine(E->node, d));
@@ -2009,6 +2282,7 @@ extern "C" int tbgpu_bench_reset_transfers(tbgpu_t* E) {
 // Bench: take the current state as written back (the snapshot, the log and commit positions), so
 // the next tbgpu_checkpoint_delta covers only what is committed after this call.
 extern "C" int tbgpu_bench_checkpoint_mark(tbgpu_t* E) {
+    API_ENTER(E, true);
     if (E->node) {
         for (u32 d = 0; d < node_world(E->node); d++) {
             const int st = tbgpu_bench_checkpoint_mark(node_engine(E->node, d));
@@ -2021,14 +2295,17 @@ extern "C" int tbgpu_bench_checkpoint_mark(tbgpu_t* E) {
         int st = engine_sync(E);
         if (st) return st;
     }
+    if (E->wb.inflight) return fail(TBGPU_STATUS_INVALID, "an asynchronous write-back is in flight");
     int st = ckpt_snapshot_ready(E);
     if (st) return st;
-    DeltaCtx C;
-    C.scanned = true;
-    return delta_end(E, C);
+    E->ckpt_scan = true;  // the whole table is taken as written back
+    if ((st = wb_advance(E))) return st;
+    HIPCK(hipStreamSynchronize(E->stream));
+    return TBGPU_STATUS_OK;
 }
 
 extern "C" int tbgpu_bench_pass_latencies(tbgpu_t* E, double* out_ms, uint64_t cap, uint64_t* count) {
+    API_ENTER(E, false);
     if (E->node) E = node_engine(E->node, 0);
     if (E->pending) {
         int st = engine_sync(E);
@@ -2041,6 +2318,7 @@ extern "C" int tbgpu_bench_pass_latencies(tbgpu_t* E, double* out_ms, uint64_t c
 }
 
 extern "C" int tbgpu_marker(tbgpu_t* E, uint32_t slot) {
+    API_ENTER(E, false);
     if (E->node) E = node_engine(E->node, 0);
     if (slot >= 16) return fail(TBGPU_STATUS_INVALID, "marker slot");
     HIPCK(hipEventRecord(E->markers[slot], E->stream));
@@ -2067,6 +2345,7 @@ extern "C" void tbgpu_homes(const uint64_t* ids, uint64_t n, uint32_t world, uin
 }
 
 extern "C" int tbgpu_route_init(tbgpu_t* E, uint32_t world, uint64_t events_max) {
+    API_ENTER(E, false);
     if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (world == 0 || world > ROUTE_WORLD_MAX) return fail(TBGPU_STATUS_INVALID, "world %u out of range", world);
@@ -2075,12 +2354,12 @@ extern "C" int tbgpu_route_init(tbgpu_t* E, uint32_t world, uint64_t events_max)
     E->route_world = world;
     E->route_events_max = events_max;
     const u64 nblocks = (events_max + ROUTE_THREADS - 1) / ROUTE_THREADS;
-    HIPCK(hipMalloc(&E->r_home, events_max));
-    HIPCK(hipMalloc(&E->r_block_counts, 2 * nblocks * world * 4));  // counts, then bases
+    HIPCK(tbMalloc(&E->r_home, events_max));
+    HIPCK(tbMalloc(&E->r_block_counts, 2 * nblocks * world * 4));  // counts, then bases
     E->r_block_cap = nblocks * world;
-    HIPCK(hipMalloc(&E->r_words, ROUTE_WORDS * 8));
-    HIPCK(hipMalloc(&E->r_meta, (2 * E->meta_cap + 1) * 8));
-    HIPCK(hipHostMalloc(&E->h_rmeta, (2 * E->meta_cap + 1) * 8, hipHostMallocDefault));
+    HIPCK(tbMalloc(&E->r_words, ROUTE_WORDS * 8));
+    HIPCK(tbMalloc(&E->r_meta, (2 * E->meta_cap + 1) * 8));
+    HIPCK(tbHostMalloc(&E->h_rmeta, (2 * E->meta_cap + 1) * 8, hipHostMallocDefault));
     return TBGPU_STATUS_OK;
 }
 
@@ -2103,6 +2382,7 @@ static int route_meta(tbgpu* E, u32 nb, const u64* timestamps, const u32* lens, 
 }
 
 extern "C" int tbgpu_route_homes(tbgpu_t* E, const uint64_t* ids_dev, uint64_t n, uint32_t world, uint8_t* out_dev) {
+    API_ENTER(E, false);
     if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (world == 0 || world > ROUTE_WORLD_MAX) return fail(TBGPU_STATUS_INVALID, "world %u out of range", world);
@@ -2115,6 +2395,7 @@ extern "C" int tbgpu_route_homes(tbgpu_t* E, const uint64_t* ids_dev, uint64_t n
 
 extern "C" int tbgpu_route_dependents(tbgpu_t* E, uint32_t nb, const uint32_t* lens, const void* events_dev,
                                       const uint64_t* marked_ids, uint32_t n_marked, uint8_t* dep_dev) {
+    API_ENTER(E, false);
     if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (!E->r_home) return fail(TBGPU_STATUS_INVALID, "tbgpu_route_init was not called");
@@ -2128,7 +2409,7 @@ extern "C" int tbgpu_route_dependents(tbgpu_t* E, uint32_t nb, const uint32_t* l
     if (n == 0) return TBGPU_STATUS_OK;
     u64* d_marked = nullptr;
     if (n_marked) {
-        HIPCK(hipMalloc(&d_marked, (u64)n_marked * 16));
+        HIPCK(tbMalloc(&d_marked, (u64)n_marked * 16));
         HIPCK(hipMemcpyAsync(d_marked, marked_ids, (u64)n_marked * 16, hipMemcpyHostToDevice, E->stream));
     }
     RouteArgs A{};
@@ -2149,6 +2430,7 @@ extern "C" int tbgpu_route_dependents(tbgpu_t* E, uint32_t nb, const uint32_t* l
 extern "C" int tbgpu_route_plan_build(tbgpu_t* E, uint32_t nb, const uint64_t* timestamps, const uint32_t* lens,
                                       const void* events_dev, const uint8_t* skip_dev, void* send_events_dev,
                                       uint32_t* slot_dev, tbgpu_route_plan* plan) {
+    API_ENTER(E, false);
     if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (!E->r_home) return fail(TBGPU_STATUS_INVALID, "tbgpu_route_init was not called");
@@ -2211,6 +2493,7 @@ extern "C" int tbgpu_route_plan_build(tbgpu_t* E, uint32_t nb, const uint64_t* t
 
 extern "C" int tbgpu_commit_routed_async(tbgpu_t* E, uint64_t n, const void* events_dev, uint64_t ts_max,
                                          uint32_t cert, uint8_t* codes_dev) {
+    API_ENTER(E, true);
     if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (cert != TBGPU_CERT_U128 && cert != TBGPU_CERT_U64) return fail(TBGPU_STATUS_INVALID, "routed commit needs a certificate");
@@ -2248,6 +2531,7 @@ extern "C" int tbgpu_commit_routed_async(tbgpu_t* E, uint64_t n, const void* eve
 extern "C" int tbgpu_commit_routed_owner_async(tbgpu_t* E, uint64_t n, const void* events_dev, uint64_t ts_max,
                                                uint32_t cert, uint8_t* codes_dev, uint32_t world, uint32_t self,
                                                void* legs_dev, uint64_t legs_cap, uint64_t* leg_counts_dev) {
+    API_ENTER(E, true);
     if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (cert != TBGPU_CERT_U128 && cert != TBGPU_CERT_U64) return fail(TBGPU_STATUS_INVALID, "routed commit needs a certificate");
@@ -2285,6 +2569,7 @@ extern "C" int tbgpu_commit_routed_owner_async(tbgpu_t* E, uint64_t n, const voi
 }
 
 extern "C" int tbgpu_apply_owner_legs_async(tbgpu_t* E, const void* legs_dev, uint64_t n, uint32_t cert) {
+    API_ENTER(E, true);
     if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (cert != TBGPU_CERT_U128 && cert != TBGPU_CERT_U64) return fail(TBGPU_STATUS_INVALID, "owner legs need a certificate");
@@ -2302,6 +2587,7 @@ extern "C" int tbgpu_apply_owner_legs_async(tbgpu_t* E, const void* legs_dev, ui
 
 extern "C" int tbgpu_route_replies_async(tbgpu_t* E, uint32_t nb, const uint32_t* lens, const uint32_t* slot_dev,
                                          const uint8_t* codes_dev, void* results_dev, uint32_t* reply_bytes_dev) {
+    API_ENTER(E, false);
     if (E->node) return fail(TBGPU_STATUS_INVALID, "tbgpu_shard.h primitives take a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (!E->r_meta) return fail(TBGPU_STATUS_INVALID, "tbgpu_route_init was not called");
@@ -2322,6 +2608,7 @@ extern "C" int tbgpu_route_replies_async(tbgpu_t* E, uint32_t nb, const uint32_t
 
 // Host <-> device staging through the lookup buffers, in chunks of lookup_cap.
 extern "C" int tbgpu_fetch_accounts(tbgpu_t* E, const uint64_t* ids, uint32_t n, void* out, uint8_t* found) {
+    API_ENTER(E, false);
     if (E->node) return node_fetch(E->node, true, ids, n, (u8*)out, found);
     HIPCK(hipSetDevice(E->device));
     if (E->pending) {
@@ -2343,6 +2630,7 @@ extern "C" int tbgpu_fetch_accounts(tbgpu_t* E, const uint64_t* ids, uint32_t n,
 }
 
 extern "C" int tbgpu_fetch_transfers(tbgpu_t* E, const uint64_t* ids, uint32_t n, void* out, uint8_t* state) {
+    API_ENTER(E, false);
     if (E->node) return node_fetch(E->node, false, ids, n, (u8*)out, state);
     HIPCK(hipSetDevice(E->device));
     if (E->pending) {
@@ -2426,11 +2714,13 @@ static int upsert_accounts(tbgpu* E, const void* records, uint32_t n, bool if_ab
 }
 
 extern "C" int tbgpu_upsert_accounts(tbgpu_t* E, const void* records, uint32_t n) {
+    API_ENTER(E, true);
     if (E->node) return node_api_accounts_in(E->node, records, n, false);
     return upsert_accounts(E, records, n, false);
 }
 
 extern "C" int tbgpu_load_accounts(tbgpu_t* E, const void* records, uint32_t n) {
+    API_ENTER(E, true);
     if (E->node) return node_api_accounts_in(E->node, records, n, true);
     return upsert_accounts(E, records, n, true);
 }
@@ -2472,11 +2762,13 @@ static int upsert_transfers(tbgpu* E, const void* records, const uint8_t* state,
 }
 
 extern "C" int tbgpu_upsert_transfers(tbgpu_t* E, const void* records, const uint8_t* state, uint32_t n) {
+    API_ENTER(E, true);
     if (E->node) return node_api_transfers_in(E->node, records, state, n, false);
     return upsert_transfers(E, records, state, n, false);
 }
 
 extern "C" int tbgpu_load_transfers(tbgpu_t* E, const void* records, const uint8_t* posted_state, uint32_t n) {
+    API_ENTER(E, true);
     if (E->node) return node_api_transfers_in(E->node, records, posted_state, n, true);
     // posted_state is {0 none, 1 posted, 2 voided}; the upsert kernel takes 1 + that.
     std::vector<u8> st(n);
@@ -2490,6 +2782,7 @@ extern "C" int tbgpu_load_transfers(tbgpu_t* E, const void* records, const uint8
 // The replica writes commit_timestamp after every commit (= the prepare header's timestamp,
 // src/vsr/replica.zig:3664-3665) and on state sync; the engine's commit asserts use that value.
 extern "C" int tbgpu_set_commit_timestamp(tbgpu_t* E, uint64_t timestamp) {
+    API_ENTER(E, true);
     if (E->node) return node_api_set_commit_timestamp(E->node, timestamp);
     HIPCK(hipSetDevice(E->device));
     if (E->pending) {

@@ -113,8 +113,16 @@ __device__ static inline u32 tb_bucket_extras(u32 total) {
 // extras cannot), and every workgroup of a split bucket adds its sums with atomics (no carry under
 // the certificate).  Every other bucket is summed by its owner alone and written back with plain
 // read-modify-writes.
+__device__ static inline void tb_apply_legs_body(const PassArgs& P, u64* s_acc);
+
 __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
     extern __shared__ u64 s_acc[];                  // [4 << leg_shift] per (slot, field) sum (dynamic)
+    tb_kclock_start(P, 2);
+    tb_apply_legs_body(P, s_acc);
+    tb_kclock_end(P, 2);
+}
+
+__device__ static inline void tb_apply_legs_body(const PassArgs& P, u64* s_acc) {
     __shared__ u32 s_start[LEG_PREPARES_MAX];       // the bucket's first leg in each prepare
     __shared__ u32 s_pref[LEG_PREPARES_MAX + 1];    // exclusive prefix of the segment lengths
     __shared__ u32 s_wave[APPLY_THREADS / 64];

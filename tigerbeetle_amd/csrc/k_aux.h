@@ -2,7 +2,7 @@
 // export, and the table-test `setup` action (state_machine.zig:1398-1407).
 #pragma once
 
-#include "tb_device.h"
+#include "pass.h"
 
 // One id per lane; found records are written at out[i] and found[i] = 1.  The host keeps input
 // order and skips not-found ids, exactly like the reference.
@@ -174,15 +174,49 @@ __global__ __launch_bounds__(DELTA_THREADS) void tb_delta_log_scatter(Tables T, 
     }
 }
 
+// The ordered bases on the device (no host round trip): exclusive prefix of the per-workgroup
+// counts of tb_delta_log_count, and the total.  One workgroup; each thread owns a run of counts.
+__global__ __launch_bounds__(1024) void tb_delta_scan_blocks(const u32* counts, u64 nblocks, u64* base, u64* total) {
+    __shared__ u32 s_wave[1024 / 64];
+    const u64 per = (nblocks + 1023) / 1024;
+    const u64 k0 = min(nblocks, (u64)threadIdx.x * per), k1 = min(nblocks, k0 + per);
+    u32 local = 0;
+    for (u64 k = k0; k < k1; k++) local += counts[k];
+    u32 all;
+    u64 run = tb_block_excl_sum(local, s_wave, &all);
+    for (u64 k = k0; k < k1; k++) {
+        base[k] = run;
+        run += counts[k];
+    }
+    if (threadIdx.x == 0) *total = all;
+}
+
+// The posted-groove entry each new post / void record makes (state_machine.zig:987-995): {the
+// pending transfer's timestamp, voided}.  A pending transfer that is missing is an invariant failure
+// (status bit 0).
+__global__ void tb_delta_posted(Tables T, const u64* pv, const u64* npv, u64* pairs, u64* status) {
+    const u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= *npv) return;
+    const u32 pos = tb_transfer_find(T, pv[3 * q], pv[3 * q + 1]);
+    if (pos == TB_NOT_FOUND) {
+        atomicOr((unsigned long long*)status, 1ULL);
+        return;
+    }
+    pairs[2 * q] = T.xlog[pos].timestamp;
+    pairs[2 * q + 1] = pv[3 * q + 2];
+}
+
 // Accounts: the ids the host names as possibly changed (the debit / credit accounts of the new
 // transfers, the ids of create_accounts events and of direct balance writes since the previous
 // write-back), each slot once (mark = this write-back's epoch).  Emitted when created since (timestamp
 // > ts0) or when its balances differ from the snapshot; `slots` lists every slot seen, for the
-// snapshot's advance.
+// snapshot's advance.  n_dev (optional): the id count is 2 x *n_dev (the new transfers' two accounts,
+// counted on the device), n is then only the grid's bound.
 __global__ void tb_delta_ids(Tables T, const AccountBal* snap, u64 ts0, const u64* ids, u64 n, u32* mark, u32 epoch,
-                             u8* out, AccountBal* before, u64* count, u32* slots, u64* slot_count) {
+                             u8* out, AccountBal* before, u64* count, u32* slots, u64* slot_count,
+                             const u64* n_dev = nullptr) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    if (i >= n || (n_dev && i >= 2 * *n_dev)) return;
     const u32 slot = tb_account_find(T, ids[2 * i], ids[2 * i + 1]);
     if (slot == TB_NOT_FOUND) return;
     if (atomicExch(&mark[slot], epoch) == epoch) return;  // another copy of the id took it
@@ -197,10 +231,34 @@ __global__ void tb_delta_ids(Tables T, const AccountBal* snap, u64 ts0, const u6
     before[k] = h.timestamp <= ts0 ? s : AccountBal{0, 0, 0, 0};
 }
 
-// The snapshot follows the slots a write-back covered.
-__global__ void tb_delta_advance(Tables T, AccountBal* snap, const u32* slots, u64 n) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) snap[slots[i]] = T.acct_bal[slots[i]];
+// The snapshot follows the slots a write-back covered (*n of them), grid-stride.
+__global__ void tb_delta_advance(Tables T, AccountBal* snap, const u32* slots, const u64* n) {
+    const u64 m = *n;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (u64)gridDim.x * blockDim.x) {
+        snap[slots[i]] = T.acct_bal[slots[i]];
+    }
+}
+
+// The asynchronous write-back's copy-out (tbgpu_checkpoint_delta_async): the gathered objects, from
+// HBM into the caller's registered host buffers (their device mappings), each region as long as its
+// device-side count says — so no host round trip has to learn the sizes first.  Runs on its own
+// stream, beside the next commits; 16-B stores, consecutive lanes on consecutive chunks.
+struct DeltaOut {
+    const u8* src[4];
+    u8* dst[4];
+    const u64* count[4];  // elements of each region
+    u32 elem[4];          // bytes per element
+};
+__global__ __launch_bounds__(256) void tb_delta_out(DeltaOut A) {
+    const u64 stride = (u64)gridDim.x * 256;
+#pragma unroll
+    for (u32 r = 0; r < 4; r++) {
+        if (!A.src[r]) continue;
+        const u64 chunks = *A.count[r] * A.elem[r] / 16;
+        const u32x4* in = (const u32x4*)A.src[r];
+        u32x4* out = (u32x4*)A.dst[r];
+        for (u64 c = (u64)blockIdx.x * 256 + threadIdx.x; c < chunks; c += stride) out[c] = in[c];
+    }
 }
 
 // ---- pipelined host commits (tbgpu_commit_pipelined) -------------------------------------------

@@ -74,6 +74,7 @@ __global__ __launch_bounds__(256) void tb_node_apply_legs(Tables T, NodeLegArgs 
 struct NodeReplyArgs {
     const u8* codes[NODE_WORLD_MAX];  // home h's result codes (one byte per received event)
     i64 delta[NODE_WORLD_MAX];        // code of an event sent to h at send slot q: codes[h][q + delta[h]]
+    const u8* seq;                    // split pass: the sequencer's code of this block's event e at seq[e]
 };
 
 // Per-prepare sparse replies of a source's block (tb_route_replies with the codes read from their
@@ -92,7 +93,8 @@ __global__ __launch_bounds__(1024) void tb_node_replies(const u64* batch_off, co
         if (i < L) {
             const u32 h = home[boff + i];
             code = h == ROUTE_LOCAL ? (u32)R_TIMESTAMP_MUST_BE_ZERO
-                                    : (u32)A.codes[h][(i64)slot[boff + i] + A.delta[h]];
+                   : h == ROUTE_DEP   ? (u32)A.seq[boff + i]
+                                      : (u32)A.codes[h][(i64)slot[boff + i] + A.delta[h]];
         }
         const u64 m = __ballot(code != R_OK);
         const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -155,4 +157,322 @@ __global__ __launch_bounds__(256) void tb_ledger_summary(Tables T, u64 cap, u32 
     }
     if (lane == 0 && live) atomicAdd((unsigned long long*)&out[8], (unsigned long long)live);
     if (lane == 0 && stray) atomicAdd((unsigned long long*)&out[9], (unsigned long long)stray);
+}
+
+// ---- dirty passes: the dependent subsequence, sequenced on the devices ----------------------------
+// A pass with linked / post / void / balancing events or limit accounts is SPLIT (node.h
+// node_split_pass): every source classifies its events; the independent ones are routed and committed
+// by their homes exactly as in a clean pass; the dependent ones (and every event whose id a dependent
+// event reads) are committed in order by the SEQUENCER, a scratch engine on the first device that
+// holds exactly the state they read (the reference's prefetch -> commit split,
+// src/state_machine.zig:345-506), and what they changed is written back to homes and owners.
+//
+// Dependence (the per-process protocol's rule, tigerbeetle_amd/sharded.py, and DESIGN.md §5b): a
+// member of a linked chain (it or its predecessor in the prepare is linked, execute :628-692), a
+// post / void (:907-1014), a balancing event (:826-846), an event on a limit-flag account
+// (tigerbeetle.zig:31-39) or on an account a balancing event of the pass touches, and — so that no
+// routed event creates an id a dependent event reads — every event whose id is the id or pending id
+// of a dependent event.
+
+struct NodeDepArgs {
+    u8* dep1;          // [n] primary classes (0: none)
+    u8* dep;           // [n] final: 1 = sequenced (the route plan's skip mask)
+    u64* keys;         // [2n][2] ids and pending ids of primary-dependent events
+    u64* bal;          // [2n][2] accounts of balancing events
+    u64* counts;       // [0] keys, [1] balancing accounts, [2] sequenced events
+    u32 all;           // 1: every event is sequenced (no global certificate)
+};
+
+__global__ __launch_bounds__(ROUTE_THREADS) void tb_node_classify1(RouteArgs A, NodeDepArgs D) {
+    const u64 e = (u64)blockIdx.x * ROUTE_THREADS + threadIdx.x;
+    if (e >= A.n) return;
+    const u64* w = (const u64*)(A.events + e * 128);
+    const u16 flags = *(const u16*)(A.events + e * 128 + 118);
+    const u32 b = tb_batch_search(A.batch_off, 0, A.nb, e);
+    u8 d = D.all ? 32 : 0;
+    if ((flags & TF_LINKED) || (e > A.batch_off[b] && (*(const u16*)(A.events + (e - 1) * 128 + 118) & TF_LINKED))) d |= 1;
+    if (flags & (TF_POST | TF_VOID)) d |= 2;
+    if (flags & (TF_BAL_DEBIT | TF_BAL_CREDIT)) d |= 4;
+    if (A.T.g->limit_accounts != 0) {
+        const u32 dr = tb_account_find(A.T, w[2], w[3]);
+        const u32 cr = tb_account_find(A.T, w[4], w[5]);
+        if ((dr != TB_NOT_FOUND && (A.T.acct_hot[dr].flags & AF_LIMITS)) ||
+            (cr != TB_NOT_FOUND && (A.T.acct_hot[cr].flags & AF_LIMITS))) {
+            d |= 8;
+        }
+    }
+    D.dep1[e] = d;
+    if (d) {  // the ids it reads: its own, and its pending transfer's
+        const bool pv = (flags & (TF_POST | TF_VOID)) != 0;
+        const u64 k = atomicAdd((unsigned long long*)&D.counts[0], pv ? 2ULL : 1ULL);
+        D.keys[2 * k] = w[0];
+        D.keys[2 * k + 1] = w[1];
+        if (pv) {
+            D.keys[2 * k + 2] = w[8];
+            D.keys[2 * k + 3] = w[9];
+        }
+    }
+    if (flags & (TF_BAL_DEBIT | TF_BAL_CREDIT)) {
+        const u64 k = atomicAdd((unsigned long long*)&D.counts[1], 2ULL);
+        D.bal[2 * k] = w[2];
+        D.bal[2 * k + 1] = w[3];
+        D.bal[2 * k + 2] = w[4];
+        D.bal[2 * k + 3] = w[5];
+    }
+}
+
+// Every source's keys and balancing accounts into this device's two 64-bit key sets (a false match
+// only makes one more event sequenced, which is always exact).  Grid-stride over the lists' lengths,
+// read from the sources' count words (peer reads: no host round trip).
+struct NodeSetArgs {
+    const u64* keys[NODE_WORLD_MAX];
+    const u64* bal[NODE_WORLD_MAX];
+    const u64* counts[NODE_WORLD_MAX];
+    u32 world;
+    u64* keyset;
+    u64 keyset_mask;
+    u64* markset;
+    u64 markset_mask;
+};
+
+__global__ __launch_bounds__(256) void tb_node_sets(NodeSetArgs S) {
+    const u64 stride = (u64)gridDim.x * 256;
+    for (u32 s = 0; s < S.world; s++) {
+        const u64 nk = S.counts[s][0], nb = S.counts[s][1];
+        for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < nk; i += stride) {
+            (void)tb_dedup_insert(S.keyset, S.keyset_mask, tb_dedup_key(S.keys[s][2 * i], S.keys[s][2 * i + 1]));
+        }
+        for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < nb; i += stride) {
+            (void)tb_dedup_insert(S.markset, S.markset_mask, tb_dedup_key(S.bal[s][2 * i], S.bal[s][2 * i + 1]));
+        }
+    }
+}
+
+__global__ __launch_bounds__(ROUTE_THREADS) void tb_node_classify2(RouteArgs A, NodeDepArgs D, const u64* keyset, u64 keyset_mask,
+                                                                   const u64* markset, u64 markset_mask) {
+    const u64 e = (u64)blockIdx.x * ROUTE_THREADS + threadIdx.x;
+    bool seq = false;
+    if (e < A.n) {
+        const u64* w = (const u64*)(A.events + e * 128);
+        seq = D.dep1[e] != 0 || tb_dedup_is_dup_or_present(keyset, keyset_mask, tb_dedup_key(w[0], w[1])) ||
+              tb_dedup_is_dup_or_present(markset, markset_mask, tb_dedup_key(w[2], w[3])) ||
+              tb_dedup_is_dup_or_present(markset, markset_mask, tb_dedup_key(w[4], w[5]));
+        D.dep[e] = seq ? 1 : 0;
+    }
+    const u64 m = __ballot(seq);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd((unsigned long long*)&D.counts[2], (unsigned long long)__popcll(m));
+}
+
+// The sequencer's prefetch sets: 64-bit fingerprints of 128-bit ids with the id stored by the thread
+// that claimed the entry.  A thread that finds its fingerprint already claimed does not wait for the
+// id (two lanes of one wave must never spin on each other): it files itself on the `dups` list, and
+// tb_seq_verify compares the ids once every claim is published — distinct ids with one 64-bit
+// fingerprint (never seen; about 2^-64 per pair) stop the pass with PANIC_ASSERT rather than drop an
+// object.
+struct SeqEntry {
+    u64 tag;       // fingerprint, 0 = empty
+    u64 lo, hi;
+    u32 x;         // its slot / log position in the sequencer (TB_NOT_FOUND: absent everywhere)
+    u32 home;      // its slot / log position on its owner / home shard
+};
+
+struct SeqSet {
+    SeqEntry* e;
+    u64 mask;
+    u32* list;     // claimed entries, in claim order
+    u64* count;    // [0] claimed, [1] dups
+    u64* dups;     // [cap][3] {entry, lo, hi} of the threads that found their fingerprint claimed
+};
+
+__device__ static inline void tb_seq_insert(const SeqSet& S, u64 lo, u64 hi) {
+    if (tb_id_reserved(lo, hi)) return;
+    const u64 tag = tb_fingerprint(lo, hi);
+    u64 pos = tb_mix64(tag) & S.mask;
+    for (u64 n = 0; n <= S.mask; n++) {
+        SeqEntry* q = &S.e[pos];
+        u64 cur = __hip_atomic_load(&q->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == 0) cur = atomicCAS((unsigned long long*)&q->tag, 0ULL, (unsigned long long)tag);
+        if (cur == 0) {
+            q->lo = lo;
+            q->hi = hi;
+            q->x = TB_NOT_FOUND;
+            q->home = TB_NOT_FOUND;
+            S.list[atomicAdd((unsigned long long*)&S.count[0], 1ULL)] = (u32)pos;
+            return;
+        }
+        if (cur == tag) {
+            const u64 k = atomicAdd((unsigned long long*)&S.count[1], 1ULL);
+            S.dups[3 * k] = pos;
+            S.dups[3 * k + 1] = lo;
+            S.dups[3 * k + 2] = hi;
+            return;
+        }
+        pos = (pos + 1) & S.mask;
+    }
+}
+
+__global__ void tb_seq_verify(SeqSet S, u64* panic) {
+    const u64 n = S.count[1];
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        const SeqEntry& q = S.e[S.dups[3 * i]];
+        if (q.lo != S.dups[3 * i + 1] || q.hi != S.dups[3 * i + 2]) atomicOr((unsigned long long*)panic, PANIC_ASSERT);
+    }
+}
+
+// The pass as the sequencer commits it: every event of the pass at its place (block-major, the
+// pass's global order), the sequenced ones verbatim from their source (a peer read), every other one a
+// placeholder that fails its first check without reading any state (a reserved flag bit; never
+// linked, so no chain crosses it, and every chain member is sequenced).  Positions and prepares keep
+// their original layout, so every execute timestamp (:645) and chain boundary is the original one.
+// The ids the sequenced events read go to the transfer set.
+struct SeqGatherArgs {
+    const u8* src[NODE_WORLD_MAX];   // source s's block of the pass (its staging buffer)
+    const u8* dep[NODE_WORLD_MAX];   // its sequenced mask
+    u64 start[NODE_WORLD_MAX + 1];   // block starts in the pass
+    u32 world;
+    u8* out;                         // the sequencer's staging
+};
+
+__global__ __launch_bounds__(256) void tb_seq_gather(SeqGatherArgs A, SeqSet tset) {
+    const u64 n = A.start[A.world];
+    const u64 g = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (g >= n) return;
+    u32 s = 0;
+    while (s + 1 < A.world && A.start[s + 1] <= g) s++;
+    const u64 e = g - A.start[s];
+    u32x4* dst = (u32x4*)(A.out + g * 128);
+    if (!A.dep[s][e]) {
+        const u32x4 z = {0, 0, 0, 0};
+#pragma unroll
+        for (u32 k = 0; k < 8; k++) dst[k] = z;
+        ((u16*)(A.out + g * 128))[59] = (u16)0x8000;  // flags @118: a reserved bit
+        return;
+    }
+    const u32x4* in = (const u32x4*)(A.src[s] + e * 128);
+    u32x4 v[8];
+#pragma unroll
+    for (u32 k = 0; k < 8; k++) v[k] = in[k];
+#pragma unroll
+    for (u32 k = 0; k < 8; k++) dst[k] = v[k];
+    const u64* w = (const u64*)v;
+    tb_seq_insert(tset, w[0], w[1]);
+    if (((const u16*)v)[59] & (TF_POST | TF_VOID)) tb_seq_insert(tset, w[8], w[9]);
+}
+
+struct NodeTablesArgs {
+    Tables T[NODE_WORLD_MAX];  // every shard's tables (device pointers; peers read over xGMI)
+    u32 world;
+};
+
+// The transfers the sequenced events read, from their homes: record, posted state, into the
+// sequencer's log at [0, loaded) and its index.  Their accounts go to the account set (a post / void
+// reads its pending transfer's accounts).
+__global__ void tb_seq_load_transfers(NodeTablesArgs N, SeqSet tset, Tables X, u64* loaded, SeqSet aset) {
+    const u64 n = tset.count[0];
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        SeqEntry& q = tset.e[tset.list[i]];
+        const Tables& H = N.T[tb_home(q.lo, q.hi, N.world)];
+        const u32 pos = tb_transfer_find(H, q.lo, q.hi);
+        if (pos == TB_NOT_FOUND) continue;
+        const Transfer t = H.xlog[pos];
+        const u32 xp = (u32)atomicAdd((unsigned long long*)loaded, 1ULL);
+        X.xlog[xp] = t;
+        X.xposted[xp] = H.xposted[pos];
+        q.x = xp;
+        q.home = pos;
+        __threadfence();
+        if (tb_transfer_claim_new(X, q.lo, q.hi, xp) == TB_NOT_FOUND) continue;  // PANIC_TABLE_FULL set
+        tb_seq_insert(aset, tb_lo(t.debit_account_id), tb_hi(t.debit_account_id));
+        tb_seq_insert(aset, tb_lo(t.credit_account_id), tb_hi(t.credit_account_id));
+    }
+}
+
+// The accounts every sequenced event names, to the account set.
+__global__ __launch_bounds__(256) void tb_seq_event_accounts(const u8* events, u64 n, SeqSet aset) {
+    const u64 g = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (g >= n) return;
+    const u64* w = (const u64*)(events + g * 128);
+    if (((const u16*)(events + g * 128))[59] & 0x8000) return;  // a placeholder (or a reserved-flag event: no state read)
+    tb_seq_insert(aset, w[2], w[3]);
+    tb_seq_insert(aset, w[4], w[5]);
+}
+
+// The accounts, into the sequencer: the record from the first shard's copy (records are replicated),
+// the balances from the owner's (the only true ones).
+__global__ void tb_seq_load_accounts(NodeTablesArgs N, SeqSet aset, Tables X) {
+    const u64 n = aset.count[0];
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        SeqEntry& q = aset.e[aset.list[i]];
+        const u32 local = tb_account_find(N.T[0], q.lo, q.hi);
+        if (local == TB_NOT_FOUND) continue;
+        const Tables& O = N.T[tb_home(q.lo, q.hi, N.world)];
+        const u32 os = tb_account_find(O, q.lo, q.hi);
+        if (os == TB_NOT_FOUND) {
+            tb_panic(X.g, PANIC_ASSERT);  // records are replicated on every shard
+            continue;
+        }
+        Account a = tb_account_load(N.T[0], local);
+        const AccountBal b = O.acct_bal[os];
+        a.debits_pending = b.debits_pending;
+        a.debits_posted = b.debits_posted;
+        a.credits_pending = b.credits_pending;
+        a.credits_posted = b.credits_posted;
+        const u32 xs = tb_account_claim(X, q.lo, q.hi, a.timestamp);
+        if (xs == TB_NOT_FOUND) continue;  // PANIC_TABLE_FULL set
+        tb_account_store_new(X, xs, a);
+        q.x = xs;
+        q.home = os;
+    }
+}
+
+// Write-back, on home h: the transfers the sequencer created (its log at [base, base + n), live in its
+// index) whose home is h, appended to h's log at h_base + (a per-home counter); and the posted state of
+// every loaded transfer of h that the pass posted or voided.
+__global__ void tb_seq_writeback_transfers(Tables X, u64 base, u64 n, SeqSet tset, Tables H, u32 self, u32 world,
+                                           u64 h_base, u64* h_count) {
+    const u64 stride = (u64)gridDim.x * blockDim.x;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const Transfer& t = X.xlog[base + i];
+        if (t.timestamp == 0 || tb_home(tb_lo(t.id), tb_hi(t.id), world) != self) continue;
+        if (tb_transfer_find(X, tb_lo(t.id), tb_hi(t.id)) != (u32)(base + i)) continue;  // withdrawn
+        const u64 lp = h_base + atomicAdd((unsigned long long*)h_count, 1ULL);
+        if (lp >= H.xlog_cap) {
+            tb_panic(H.g, PANIC_TABLE_FULL);
+            continue;
+        }
+        H.xlog[lp] = t;
+        H.xposted[lp] = X.xposted[base + i];
+        __threadfence();
+        if (tb_transfer_claim_new(H, tb_lo(t.id), tb_hi(t.id), (u32)lp) == TB_NOT_FOUND) continue;
+        atomicAdd((unsigned long long*)&H.g->transfer_count, 1ULL);
+    }
+    const u64 m = tset.count[0];
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+        const SeqEntry& q = tset.e[tset.list[i]];
+        if (q.x == TB_NOT_FOUND || tb_home(q.lo, q.hi, world) != self) continue;
+        const u8 st = X.xposted[q.x];
+        if (H.xposted[q.home] != st) H.xposted[q.home] = st;
+    }
+}
+
+// Write-back, on owner o: the balances of every account the sequencer held that o owns.
+__global__ void tb_seq_writeback_accounts(Tables X, SeqSet aset, Tables O, u32 self, u32 world) {
+    const u64 n = aset.count[0];
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        const SeqEntry& q = aset.e[aset.list[i]];
+        if (q.x == TB_NOT_FOUND || tb_home(q.lo, q.hi, world) != self) continue;
+        O.acct_bal[q.home] = X.acct_bal[q.x];
+    }
+}
+
+// Empties what the pass put in the sequencer's account table and both sets (by their lists).
+__global__ void tb_seq_clear(SeqSet tset, SeqSet aset, Tables X) {
+    const u64 stride = (u64)gridDim.x * blockDim.x;
+    const u64 na = aset.count[0], nt = tset.count[0];
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) {
+        SeqEntry& q = aset.e[aset.list[i]];
+        if (q.x != TB_NOT_FOUND) X.acct_hot[q.x] = AccountHot{};
+        q.tag = 0;
+    }
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nt; i += stride) tset.e[tset.list[i]].tag = 0;
 }

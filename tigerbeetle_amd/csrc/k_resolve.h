@@ -248,6 +248,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     const u64 boff = P.batch_off[b];
     const u32 L = (u32)(P.batch_off[b + 1] - boff);
     const u32 pbase = (u32)(boff - P.e0);
+    tb_kclock_start(P, 1);
 
     u128 S = 0;
     bool cert_global = true, cert64 = true;
@@ -506,4 +507,5 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     }
     if (use_legs) tb_emit_legs(P, pbase, L, legmask, r_dr, r_cr, s_hist, (u16*)s_key, s_wave);  // s_key is dead here
     if (ndep == 0) tb_write_replies(P, b, L, s_code, s_wave, s_failed);
+    tb_kclock_end(P, 1);
 }

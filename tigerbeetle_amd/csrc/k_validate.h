@@ -238,11 +238,22 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     } else {
         tb_account_find2(T, dlo, dhi, dpos, d0, clo, chi, cpos, c0, &drs, &crs, &dr, &cr);
     }
-    if (drs == TB_NOT_FOUND) return CT_DEBIT_ACCOUNT_NOT_FOUND;
-    if (crs == TB_NOT_FOUND) return CT_CREDIT_ACCOUNT_NOT_FOUND;
-    if (!(ts > dr.timestamp) || !(ts > cr.timestamp)) return TB_CODE_PANIC;  // :817-818
-    if (dr.ledger != cr.ledger) return CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
-    if (t.ledger != dr.ledger) return CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+    u32 early = R_OK;
+    if (drs == TB_NOT_FOUND) early = CT_DEBIT_ACCOUNT_NOT_FOUND;
+    else if (crs == TB_NOT_FOUND) early = CT_CREDIT_ACCOUNT_NOT_FOUND;
+    else if (!(ts > dr.timestamp) || !(ts > cr.timestamp)) early = TB_CODE_PANIC;  // :817-818
+    else if (dr.ledger != cr.ledger) early = CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+    else if (t.ledger != dr.ledger) early = CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+    if (early != R_OK) {
+        // Every event past the stateless checks claims its id, whether or not its home entry was
+        // free: which same-pass events collide (and so which are dependent) is then a function of
+        // the input, not of the order the claims landed in (tests/harness/dependence.py).
+        if (x0 != 0 && x0 != ~0ULL) {
+            u32 es = TB_NOT_FOUND;
+            (void)tb_claim_id(P, t, pe, s, &es, x0);
+        }
+        return early;
+    }
 
     // From here the event may end up ok: account for it in S and mark balancing accounts before
     // the id check, so that a dependent (colliding) event is covered too.
@@ -289,6 +300,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
 
     const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
     const u32 count = min((u32)VALIDATE_THREADS, P.n - tile0);
+    tb_kclock_start(P, 0);
     tb_stage_tile<SRC>(P, tile0, count, stage, TB_ABL(P, EXP_NT));
 
     const u32 pe = tile0 + threadIdx.x;  // pass-relative event
@@ -373,6 +385,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
             total = tb_sat_add(total, tb_u128(*(const u64*)q, *(const u64*)(q + 8)));
         }
         tb_sum_publish(P, total);
+        if (P.kclock) atomicMax((unsigned long long*)&P.kclock[1], (unsigned long long)wall_clock64());
     }
 }
 

@@ -22,10 +22,14 @@
 //
 // A pass is CLEAN when no event is linked / post / void / balancing, no account it touches carries
 // a limit flag, and (sum of the shards' bounds) + S < 2^128 (host-tracked, conservative).  A
-// dirty pass is sequenced (node_sequence_pass): every in-flight pass drains, the transfers and
-// accounts the pass reads are fetched from their homes / owners into a scratch engine on the first
-// device, the pass commits there in order (the reference's prefetch -> commit split,
-// src/state_machine.zig:345-506), and what changed is written back to homes and owners.
+// dirty pass is SPLIT (node_split_pass, k_node.h): every source classifies its events on the device,
+// the independent ones are routed and committed by their homes as in a clean pass, and the
+// dependent subsequence is committed in order by the sequencer — an engine on the first device,
+// allocated at init, that the pass loads with exactly the transfers and accounts those events read
+// (peer reads from their homes and owners: the reference's prefetch -> commit split,
+// src/state_machine.zig:345-506) — whose changes are written back to homes and owners by kernels
+// on those devices.  No host code walks the events.  Without the overflow certificate every event of
+// the pass is sequenced.
 #pragma once
 
 #include <thread>
@@ -60,6 +64,18 @@ struct NodeDev {
     u8* d_arena[3] = {};
     hipEvent_t ev_start[3] = {}, ev_done[3] = {}, ev_planned[2] = {}, ev_copied = nullptr;
     hipEvent_t ev_gathered = nullptr, ev_committed = nullptr, ev_applied = nullptr, ev_replied = nullptr;
+    // Dirty passes (k_node.h): the block's classification and this device's key sets.
+    u8* dep1 = nullptr;
+    u8* dep = nullptr;
+    u64* dkeys = nullptr;        // [2 pe_src][2]
+    u64* dbal = nullptr;         // [2 pe_src][2]
+    u64* dcounts = nullptr;      // [4]
+    u64* h_dcounts = nullptr;    // pinned
+    u64* keyset = nullptr;
+    u64* markset = nullptr;
+    u64 set_mask = 0;
+    u64* wb_count = nullptr;     // sequencer write-back: records appended here
+    hipEvent_t ev_cls = nullptr;
 };
 
 struct NodeBlock {
@@ -81,9 +97,21 @@ struct TbNode {
     u32 pb_src = 0;        // source prepares per pass per shard
     u64 recv_cap = 0;      // events a home can receive in one pass (world * pe_src)
     u64 commit_ts = 0;
-    tbgpu* scratch = nullptr;  // the sequencer's engine (device of shard 0), grown on demand
-    tbgpu_config scratch_cfg{};
-    u64 passes_clean = 0, passes_sequenced = 0;
+    // The sequencer (first device), sized at init for a whole pass: its log holds the loaded
+    // transfers at [0, seq_tcap) and the pass at [seq_tcap, ...).
+    tbgpu* X = nullptr;
+    u64 seq_tcap = 0;
+    SeqEntry* tset_e = nullptr;
+    SeqEntry* aset_e = nullptr;
+    u64 tset_mask = 0, aset_mask = 0;
+    u32* tset_list = nullptr;
+    u32* aset_list = nullptr;
+    u64* seq_counts = nullptr;   // [0..1] tset, [2..3] aset, [4] loaded transfers
+    u64* tset_dups = nullptr;
+    u64* aset_dups = nullptr;
+    u8* seq_codes = nullptr;     // [world * pe_src] the pass's dense codes from the sequencer
+    u64* h_seq = nullptr;        // pinned scratch words
+    u64 passes_clean = 0, passes_split = 0, passes_whole = 0, seq_events = 0;
 };
 
 static int node_fail_dev(const char* what, hipError_t e) {
@@ -111,19 +139,27 @@ static void node_free(TbNode* N) {
         }
         void* dev[] = {D.stage[0], D.stage[1], D.send[0], D.send[1], D.slot[0], D.slot[1], D.home[0], D.home[1],
                        D.words[0], D.words[1], D.meta[0], D.meta[1], D.block_counts, D.results, D.reply_bytes,
-                       D.recv, D.codes, D.legs, D.leg_counts, D.hmeta_dev[0], D.hmeta_dev[1], D.hmeta_dev[2]};
+                       D.recv, D.codes, D.legs, D.leg_counts, D.hmeta_dev[0], D.hmeta_dev[1], D.hmeta_dev[2],
+                       D.dep1, D.dep, D.dkeys, D.dbal, D.dcounts, D.keyset, D.markset, D.wb_count};
         for (void* p : dev) if (p) (void)hipFree(p);
         void* host[] = {D.h_words[0], D.h_words[1], D.h_meta[0], D.h_meta[1], D.hmeta_host[0], D.hmeta_host[1],
-                        D.hmeta_host[2], D.h_arena[0], D.h_arena[1], D.h_arena[2]};
+                        D.hmeta_host[2], D.h_arena[0], D.h_arena[1], D.h_arena[2], D.h_dcounts};
         for (void* p : host) if (p) (void)hipHostFree(p);
         hipEvent_t evs[] = {D.ev_start[0], D.ev_start[1], D.ev_start[2], D.ev_done[0], D.ev_done[1], D.ev_done[2],
                             D.ev_planned[0], D.ev_planned[1], D.ev_copied, D.ev_gathered, D.ev_committed,
-                            D.ev_applied, D.ev_replied};
+                            D.ev_applied, D.ev_replied, D.ev_cls};
         for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
         if (D.rs) (void)hipStreamDestroy(D.rs);
         if (D.E) tbgpu_deinit(D.E);
     }
-    if (N->scratch) tbgpu_deinit(N->scratch);
+    if (N->X) {
+        (void)hipSetDevice(N->D[0].device);
+        void* dev[] = {N->tset_e, N->aset_e, N->tset_list, N->aset_list, N->seq_counts, N->tset_dups, N->aset_dups,
+                       N->seq_codes};
+        for (void* p : dev) if (p) (void)hipFree(p);
+        if (N->h_seq) (void)hipHostFree(N->h_seq);
+        tbgpu_deinit(N->X);
+    }
     delete N;
 }
 
@@ -194,49 +230,99 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
         NALLOC(hipSetDevice(D.device));
         NALLOC(hipStreamCreateWithFlags(&D.rs, hipStreamNonBlocking));
         for (int k = 0; k < 2; k++) {
-            NALLOC(hipMalloc(&D.stage[k], pe * 128));
-            NALLOC(hipMalloc(&D.send[k], pe * 128));
-            NALLOC(hipMalloc(&D.slot[k], pe * 4));
-            NALLOC(hipMalloc(&D.home[k], pe));
-            NALLOC(hipMalloc(&D.words[k], ROUTE_WORDS * 8));
-            NALLOC(hipHostMalloc(&D.h_words[k], ROUTE_WORDS * 8, hipHostMallocDefault));
-            NALLOC(hipMalloc(&D.meta[k], (2 * (u64)N->pb_src + 1) * 8));
-            NALLOC(hipHostMalloc(&D.h_meta[k], (2 * (u64)N->pb_src + 1) * 8, hipHostMallocDefault));
-            NALLOC(hipEventCreateWithFlags(&D.ev_planned[k], hipEventDisableTiming));
+            NALLOC(tbMalloc(&D.stage[k], pe * 128));
+            NALLOC(tbMalloc(&D.send[k], pe * 128));
+            NALLOC(tbMalloc(&D.slot[k], pe * 4));
+            NALLOC(tbMalloc(&D.home[k], pe));
+            NALLOC(tbMalloc(&D.words[k], ROUTE_WORDS * 8));
+            NALLOC(tbHostMalloc(&D.h_words[k], ROUTE_WORDS * 8, hipHostMallocDefault));
+            NALLOC(tbMalloc(&D.meta[k], (2 * (u64)N->pb_src + 1) * 8));
+            NALLOC(tbHostMalloc(&D.h_meta[k], (2 * (u64)N->pb_src + 1) * 8, hipHostMallocDefault));
+            NALLOC(tbEventCreateWithFlags(&D.ev_planned[k], hipEventDisableTiming));
         }
-        NALLOC(hipMalloc(&D.block_counts, 2 * nblocks * W * 4));
-        NALLOC(hipMalloc(&D.results, pe * 8));
-        NALLOC(hipMalloc(&D.reply_bytes, (u64)N->pb_src * 4));
-        NALLOC(hipMalloc(&D.recv, N->recv_cap * 128));
-        NALLOC(hipMalloc(&D.codes, N->recv_cap));
-        NALLOC(hipMalloc(&D.legs, legs_cap_total * OWNER_LEG_WORDS * 8));
-        NALLOC(hipMalloc(&D.leg_counts, (u64)W * 8));
+        NALLOC(tbMalloc(&D.block_counts, 2 * nblocks * W * 4));
+        NALLOC(tbMalloc(&D.results, pe * 8));
+        NALLOC(tbMalloc(&D.reply_bytes, (u64)N->pb_src * 4));
+        NALLOC(tbMalloc(&D.recv, N->recv_cap * 128));
+        NALLOC(tbMalloc(&D.codes, N->recv_cap));
+        NALLOC(tbMalloc(&D.legs, legs_cap_total * OWNER_LEG_WORDS * 8));
+        NALLOC(tbMalloc(&D.leg_counts, (u64)W * 8));
         const u64 hm = 2 * ((N->recv_cap + BATCH_EVENTS_MAX - 2) / (BATCH_EVENTS_MAX - 1) + 2) + 1;
         for (int k = 0; k < 3; k++) {
-            NALLOC(hipMalloc(&D.hmeta_dev[k], hm * 8));
-            NALLOC(hipHostMalloc(&D.hmeta_host[k], hm * 8, hipHostMallocDefault));
-            NALLOC(hipHostMalloc(&D.h_arena[k], node_arena_bytes(N), hipHostMallocMapped));
+            NALLOC(tbMalloc(&D.hmeta_dev[k], hm * 8));
+            NALLOC(tbHostMalloc(&D.hmeta_host[k], hm * 8, hipHostMallocDefault));
+            NALLOC(tbHostMalloc(&D.h_arena[k], node_arena_bytes(N), hipHostMallocMapped));
             if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&D.d_arena[k], D.h_arena[k], 0);
-            NALLOC(hipEventCreate(&D.ev_start[k]));
-            NALLOC(hipEventCreate(&D.ev_done[k]));
+            NALLOC(tbEventCreate(&D.ev_start[k]));
+            NALLOC(tbEventCreate(&D.ev_done[k]));
         }
-        NALLOC(hipEventCreateWithFlags(&D.ev_copied, hipEventDisableTiming));
-        NALLOC(hipEventCreateWithFlags(&D.ev_gathered, hipEventDisableTiming));
-        NALLOC(hipEventCreateWithFlags(&D.ev_committed, hipEventDisableTiming));
-        NALLOC(hipEventCreateWithFlags(&D.ev_applied, hipEventDisableTiming));
-        NALLOC(hipEventCreateWithFlags(&D.ev_replied, hipEventDisableTiming));
+        NALLOC(tbEventCreateWithFlags(&D.ev_copied, hipEventDisableTiming));
+        NALLOC(tbEventCreateWithFlags(&D.ev_gathered, hipEventDisableTiming));
+        NALLOC(tbEventCreateWithFlags(&D.ev_committed, hipEventDisableTiming));
+        NALLOC(tbEventCreateWithFlags(&D.ev_applied, hipEventDisableTiming));
+        NALLOC(tbEventCreateWithFlags(&D.ev_replied, hipEventDisableTiming));
         // The events of "the previous pass" exist before the first pass: record them once.
         NALLOC(hipEventRecord(D.ev_gathered, D.E->stream));
         NALLOC(hipEventRecord(D.ev_applied, D.E->stream));
         NALLOC(hipEventRecord(D.ev_replied, D.E->stream));
+        // Dirty passes: the block's classification, the key sets (every source's keys), the
+        // sequencer write-back counter.
+        D.set_mask = pow2_at_least(std::max<u64>(1024, 4 * (u64)W * pe)) - 1;
+        NALLOC(tbMalloc(&D.dep1, pe));
+        NALLOC(tbMalloc(&D.dep, pe));
+        NALLOC(tbMalloc(&D.dkeys, 2 * pe * 16));
+        NALLOC(tbMalloc(&D.dbal, 2 * pe * 16));
+        NALLOC(tbMalloc(&D.dcounts, 4 * 8));
+        NALLOC(tbHostMalloc(&D.h_dcounts, 4 * 8, hipHostMallocDefault));
+        NALLOC(tbMalloc(&D.keyset, (D.set_mask + 1) * 8));
+        NALLOC(tbMalloc(&D.markset, (D.set_mask + 1) * 8));
+        NALLOC(tbMalloc(&D.wb_count, 8));
+        NALLOC(tbEventCreateWithFlags(&D.ev_cls, hipEventDisableTiming));
     }
 #undef NALLOC
     if (e != hipSuccess) {
         node_free(N);
         return node_fail_dev("tbgpu_init (node buffers)", e);
     }
-    N->scratch_cfg = sc;
-    N->scratch_cfg.device = N->D[0].device;
+    // The sequencer: one whole pass (every source's block) with the objects it can read — two
+    // transfers (id, pending id) and up to four accounts per event.
+    {
+        const u64 pass = (u64)W * pe;
+        tbgpu_config xc = sc;
+        xc.device = N->D[0].device;
+        xc.flags &= ~(u32)TBGPU_CONFIG_PROFILE;
+        xc.accounts_max = std::max<u64>(1024, std::min<u64>(config->accounts_max, 4 * pass));
+        N->seq_tcap = 2 * pass;
+        xc.transfers_max = N->seq_tcap + pass;
+        xc.pass_events_max = (u32)std::min<u64>(pass, 0xFFFFFFFFull);
+        xc.pass_batches_max = W * N->pb_src;
+        int st2 = tbgpu_init(&xc, &N->X);
+        if (st2) {
+            node_free(N);
+            return st2;
+        }
+        (void)hipSetDevice(N->D[0].device);
+        N->tset_mask = pow2_at_least(4 * pass) - 1;
+        N->aset_mask = pow2_at_least(2 * (xc.accounts_max + 2 * pass)) - 1;
+#define XALLOC(x) \
+    if (e == hipSuccess) e = (x)
+        XALLOC(tbMalloc(&N->tset_e, (N->tset_mask + 1) * sizeof(SeqEntry)));
+        XALLOC(tbMalloc(&N->aset_e, (N->aset_mask + 1) * sizeof(SeqEntry)));
+        XALLOC(tbMalloc(&N->tset_list, 2 * pass * 4));
+        XALLOC(tbMalloc(&N->aset_list, 6 * pass * 4));
+        XALLOC(tbMalloc(&N->seq_counts, 8 * 8));
+        XALLOC(tbMalloc(&N->tset_dups, 2 * pass * 24));
+        XALLOC(tbMalloc(&N->aset_dups, 6 * pass * 24));
+        XALLOC(tbMalloc(&N->seq_codes, pass));
+        XALLOC(tbHostMalloc(&N->h_seq, 16 * 8, hipHostMallocDefault));
+        XALLOC(hipMemset(N->tset_e, 0, (N->tset_mask + 1) * sizeof(SeqEntry)));
+        XALLOC(hipMemset(N->aset_e, 0, (N->aset_mask + 1) * sizeof(SeqEntry)));
+#undef XALLOC
+        if (e != hipSuccess) {
+            node_free(N);
+            return node_fail_dev("tbgpu_init (node sequencer)", e);
+        }
+    }
     *out = N;
     return TBGPU_STATUS_OK;
 }
@@ -431,27 +517,44 @@ static int node_read_plan(TbNode* N, const NodePass& P, u32 p, NodePlan* out) {
     return TBGPU_STATUS_OK;
 }
 
-// Gather, routed commit with owner legs, legs to owners, replies to sources — every device, enqueued.
-static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, u32 cert, u64 ts_max) {
-    const u32 W = N->world, par = p & 1, tri = p % 3;
+// Where each source's run for each home sits, on both sides of the exchange.
+struct NodeRoute {
     u64 R[NODE_WORLD_MAX][NODE_WORLD_MAX];    // R[h][s]: where source s's run starts in home h's receipt
     u64 off[NODE_WORLD_MAX][NODE_WORLD_MAX];  // off[s][h]: where home h's run starts in source s's send buffer
     u64 nh[NODE_WORLD_MAX];
+};
+
+static void node_route(const TbNode* N, const NodePlan& PL, NodeRoute& X) {
+    const u32 W = N->world;
     for (u32 h = 0; h < W; h++) {
         u64 r = 0;
         for (u32 s = 0; s < W; s++) {
-            R[h][s] = r;
+            X.R[h][s] = r;
             r += PL.C[s][h];
         }
-        nh[h] = r;
+        X.nh[h] = r;
     }
     for (u32 s = 0; s < W; s++) {
         u64 o = 0;
         for (u32 h = 0; h < W; h++) {
-            off[s][h] = o;
+            X.off[s][h] = o;
             o += PL.C[s][h];
         }
     }
+}
+
+static int node_issue_replies(TbNode* N, NodePass& P, u32 p, const NodeRoute& X, const u8* seq_codes);
+
+// Gather, routed commit with owner legs, legs to owners, replies to sources — every device, enqueued.
+// replies = false (a split pass): the sources' replies wait for the sequencer (node_issue_replies).
+static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, u32 cert, u64 ts_max,
+                             bool replies = true) {
+    const u32 W = N->world, par = p & 1, tri = p % 3;
+    NodeRoute RT;
+    node_route(N, PL, RT);
+    const auto& R = RT.R;
+    const auto& off = RT.off;
+    const auto& nh = RT.nh;
     for (u32 h = 0; h < W; h++) {
         if (nh[h] > N->recv_cap) return fail(TBGPU_STATUS_INVALID, "node: home %u receives %llu events > %llu", h,
                                              (unsigned long long)nh[h], (unsigned long long)N->recv_cap);
@@ -527,7 +630,15 @@ static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, 
         }
         NCK(hipEventRecord(D.ev_applied, E->stream));
     }
-    // 3. Sources: replies from the codes their homes wrote, into the reply arena.
+    P.issued = true;
+    return replies ? node_issue_replies(N, P, p, RT, nullptr) : TBGPU_STATUS_OK;
+}
+
+// 3. Sources: replies from the codes their homes wrote (and, for a split pass, the sequencer's codes
+// of the events it committed: seq_codes, the whole pass block-major), into the reply arena.
+static int node_issue_replies(TbNode* N, NodePass& P, u32 p, const NodeRoute& RT, const u8* seq_codes) {
+    const u32 W = N->world, par = p & 1, tri = p % 3;
+    u64 base = 0;
     for (u32 s = 0; s < W; s++) {
         NodeDev& D = N->D[s];
         tbgpu* E = D.E;
@@ -537,12 +648,14 @@ static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, 
             NodeReplyArgs A{};
             for (u32 h = 0; h < W; h++) {
                 A.codes[h] = N->D[h].codes;
-                A.delta[h] = (i64)R[h][s] - (i64)off[s][h];
+                A.delta[h] = (i64)RT.R[h][s] - (i64)RT.off[s][h];
             }
+            A.seq = seq_codes ? seq_codes + base : nullptr;
             hipLaunchKernelGGL(tb_node_replies, dim3(nb), dim3(1024), 0, E->stream, D.meta[par], D.home[par], D.slot[par], A,
                                D.results, D.reply_bytes);
             NCK(hipGetLastError());
         }
+        base += P.blk[s].events;
         NCK(hipEventRecord(D.ev_replied, E->stream));
         if (nb) {
             hipLaunchKernelGGL(tb_reply_out, dim3(nb), dim3(64), 0, E->stream, D.meta[par], nb, D.reply_bytes, D.results,
@@ -579,6 +692,7 @@ static int node_consume(TbNode* N, NodePass& P, u32 p, void* const* outputs, u32
             if (latency_ms) latency_ms[k] = ms;
         }
         N->commit_ts = std::max(N->commit_ts, head[1]);
+        if (head[0]) D.E->poisoned = true;
         if (head[0]) status = fail(TBGPU_STATUS_PANIC, "device panic 0x%llx on shard %u (the reference would have trapped)",
                                    (unsigned long long)head[0], s);
     }
@@ -586,182 +700,212 @@ static int node_consume(TbNode* N, NodePass& P, u32 p, void* const* outputs, u32
     return status;
 }
 
-static int node_upsert_accounts_keep_flow(tbgpu* E, const void* records, uint32_t n);
-
-// A dirty pass, committed in order on the scratch engine after fetching what it reads, then
-// written back (synchronous; every earlier pass has drained).
-static int node_sequence_pass(TbNode* N, const NodePass& P, const u64* ts, const void* const* inputs, const u32* lens,
-                              void* const* outputs, u32* out_lens) {
+// A dirty pass, SPLIT (k_node.h): the dependent subsequence is committed in order by the sequencer,
+// every other event is routed to its home as in a clean pass.  Synchronous (every earlier pass has
+// drained); the pass's bodies are in the sources' staging buffers (its plan was issued).  all: no
+// overflow certificate — every event goes to the sequencer.  One host round trip for the plan (the
+// routed part's counts, as in a clean pass) and one to learn how many records each home received.
+static int node_split_pass(TbNode* N, NodePass& P, u32 p, const u64* ts, u64 bound_lo, u64 bound_hi, bool all) {
+    const u32 W = N->world, par = p & 1;
+    tbgpu* X = N->X;
+    // -- 1. classification on every source: primary classes, then the key sets, then the final mask
+    //       and the route plan of the rest.
+    for (u32 d = 0; d < W; d++) {
+        NodeDev& D = N->D[d];
+        const NodeBlock& B = P.blk[d];
+        NCK(hipSetDevice(D.device));
+        NCK(hipMemsetAsync(D.dcounts, 0, 4 * 8, D.rs));
+        if (B.events) {
+            RouteArgs A{};
+            A.events = D.stage[par];
+            A.n = (u32)B.events;
+            A.nb = B.k1 - B.k0;
+            A.batch_off = D.meta[par];
+            A.batch_ts = D.meta[par] + A.nb + 1;
+            A.world = W;
+            A.T = D.E->T;
+            NodeDepArgs Dp{D.dep1, D.dep, D.dkeys, D.dbal, D.dcounts, all ? 1u : 0u};
+            hipLaunchKernelGGL(tb_node_classify1, dim3((unsigned)((B.events + ROUTE_THREADS - 1) / ROUTE_THREADS)),
+                               dim3(ROUTE_THREADS), 0, D.rs, A, Dp);
+            NCK(hipGetLastError());
+        }
+        NCK(hipEventRecord(D.ev_cls, D.rs));
+    }
+    NodeSetArgs S{};
+    S.world = W;
+    for (u32 d = 0; d < W; d++) {
+        S.keys[d] = N->D[d].dkeys;
+        S.bal[d] = N->D[d].dbal;
+        S.counts[d] = N->D[d].dcounts;
+    }
+    for (u32 d = 0; d < W; d++) {
+        NodeDev& D = N->D[d];
+        const NodeBlock& B = P.blk[d];
+        NCK(hipSetDevice(D.device));
+        for (u32 s = 0; s < W; s++) NCK(hipStreamWaitEvent(D.rs, N->D[s].ev_cls, 0));
+        NCK(hipMemsetAsync(D.keyset, 0, (D.set_mask + 1) * 8, D.rs));
+        NCK(hipMemsetAsync(D.markset, 0, (D.set_mask + 1) * 8, D.rs));
+        NodeSetArgs Sd = S;
+        Sd.keyset = D.keyset;
+        Sd.markset = D.markset;
+        Sd.keyset_mask = Sd.markset_mask = D.set_mask;
+        hipLaunchKernelGGL(tb_node_sets, dim3(512), dim3(256), 0, D.rs, Sd);
+        NCK(hipGetLastError());
+        NCK(hipMemsetAsync(D.words[par], 0, ROUTE_WORDS * 8, D.rs));
+        if (B.events) {
+            RouteArgs A{};
+            A.events = D.stage[par];
+            A.n = (u32)B.events;
+            A.nb = B.k1 - B.k0;
+            A.batch_off = D.meta[par];
+            A.batch_ts = D.meta[par] + A.nb + 1;
+            A.world = W;
+            A.nblocks = (u32)((B.events + ROUTE_THREADS - 1) / ROUTE_THREADS);
+            A.home = D.home[par];
+            A.block_counts = D.block_counts;
+            A.block_base = D.block_counts + (u64)A.nblocks * W;
+            A.words = D.words[par];
+            A.T = D.E->T;
+            NodeDepArgs Dp{D.dep1, D.dep, D.dkeys, D.dbal, D.dcounts, all ? 1u : 0u};
+            hipLaunchKernelGGL(tb_node_classify2, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, D.rs, A, Dp, D.keyset, D.set_mask,
+                               D.markset, D.set_mask);
+            A.skip = D.dep;
+            hipLaunchKernelGGL(tb_route_classify, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, D.rs, A);
+            hipLaunchKernelGGL(tb_route_offsets, dim3(A.world), dim3(1024), 0, D.rs, A);
+            hipLaunchKernelGGL(tb_route_scatter, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, D.rs, A, D.send[par], D.slot[par]);
+            NCK(hipGetLastError());
+        }
+        NCK(hipMemcpyAsync(D.h_words[par], D.words[par], ROUTE_WORDS * 8, hipMemcpyDeviceToHost, D.rs));
+        NCK(hipMemcpyAsync(D.h_dcounts, D.dcounts, 4 * 8, hipMemcpyDeviceToHost, D.rs));
+        NCK(hipEventRecord(D.ev_planned[par], D.rs));
+    }
+    NodePlan PL;
+    int st = node_read_plan(N, P, p, &PL);
+    if (st) return st;
+    u64 n_seq = 0, n_pass = 0;
+    for (u32 d = 0; d < W; d++) {
+        n_seq += N->D[d].h_dcounts[2];
+        n_pass += P.blk[d].events;
+    }
+    // -- 2. the routed part, committed by the homes (legs to the owners); its certificate covers the
+    //       whole pass's amounts.
     typedef unsigned __int128 h128;
-    const u32 W = N->world;
-    auto key = [](const u8* p) { return *(const h128*)p; };
-    const h128 MAXID = ~(h128)0;
-    // 1. The transfers the pass reads: every event id, the pending id of post / void events.
-    std::vector<h128> tids;
-    for (u32 k = P.k0; k < P.k1; k++) {
-        const u8* body = (const u8*)inputs[k];
-        for (u32 i = 0; i < lens[k]; i++) {
-            const u8* ev = body + (u64)i * 128;
-            tids.push_back(key(ev));
-            const u16 fl = *(const u16*)(ev + 118);
-            if (fl & (TF_POST | TF_VOID)) tids.push_back(key(ev + 64));
-        }
-    }
-    auto uniq = [&](std::vector<h128>& v) {
-        std::sort(v.begin(), v.end());
-        v.erase(std::unique(v.begin(), v.end()), v.end());
-        v.erase(std::remove_if(v.begin(), v.end(), [&](h128 x) { return x == 0 || x == MAXID; }), v.end());
-    };
-    uniq(tids);
-    const u64 nt = tids.size();
-    std::vector<u8> trec(nt * 128), tstate(nt);
+    const h128 bound = ((h128)bound_hi << 64) | bound_lo;
+    const h128 total = bound + PL.S < bound ? ~(h128)0 : bound + PL.S;
+    const u32 cert = (total >> 64) == 0 ? TBGPU_CERT_U64 : TBGPU_CERT_U128;
+    if (!all && (st = node_issue_commit(N, P, p, PL, cert, ts[P.k1 - 1], false))) return st;
+    if ((st = node_sync(N))) return st;
+    // -- 3. the sequencer: the pass at its place (the dependent events verbatim, placeholders
+    //       elsewhere), loaded with what they read, committed in order.
+    const int dev0 = N->D[0].device;
+    NCK(hipSetDevice(dev0));
+    hipStream_t xs = X->stream;
+    NCK(hipMemsetAsync(X->T.xidx, 0, X->xidx_cap * 8, xs));
+    NCK(hipMemsetAsync(X->T.xdup, 0, X->xidx_cap, xs));
+    NCK(hipMemsetAsync(X->T.xposted, 0, X->xlog_cap, xs));
+    NCK(hipMemsetAsync(N->seq_counts, 0, 8 * 8, xs));
+    SeqSet tset{N->tset_e, N->tset_mask, N->tset_list, N->seq_counts, N->tset_dups};
+    SeqSet aset{N->aset_e, N->aset_mask, N->aset_list, N->seq_counts + 2, N->aset_dups};
+    SeqGatherArgs G{};
+    G.world = W;
+    G.out = X->staging;
     {
-        std::vector<std::vector<u64>> ids(W);
-        std::vector<std::vector<u64>> where(W);
-        for (u64 i = 0; i < nt; i++) {
-            const u32 h = node_home((const u8*)&tids[i], W);
-            ids[h].push_back((u64)tids[i]);
-            ids[h].push_back((u64)(tids[i] >> 64));
-            where[h].push_back(i);
+        u64 at = 0;
+        for (u32 d = 0; d < W; d++) {
+            G.src[d] = N->D[d].stage[par];
+            G.dep[d] = N->D[d].dep;
+            G.start[d] = at;
+            at += P.blk[d].events;
         }
-        for (u32 h = 0; h < W; h++) {
-            const u64 m = where[h].size();
-            if (!m) continue;
-            std::vector<u8> rec(m * 128), st(m);
-            const int s = tbgpu_fetch_transfers(N->D[h].E, ids[h].data(), (u32)m, rec.data(), st.data());
-            if (s) return s;
-            for (u64 j = 0; j < m; j++) {
-                memcpy(&trec[where[h][j] * 128], &rec[j * 128], 128);
-                tstate[where[h][j]] = st[j];
-            }
-        }
+        G.start[W] = at;
     }
-    // 2. The accounts: of every event, and of every pending transfer a post / void reads.
-    std::vector<h128> aids;
-    for (u32 k = P.k0; k < P.k1; k++) {
-        const u8* body = (const u8*)inputs[k];
-        for (u32 i = 0; i < lens[k]; i++) {
-            aids.push_back(key(body + (u64)i * 128 + 16));
-            aids.push_back(key(body + (u64)i * 128 + 32));
-        }
+    NodeTablesArgs NT{};
+    NT.world = W;
+    for (u32 d = 0; d < W; d++) NT.T[d] = N->D[d].E->T;
+    if (n_pass) {
+        hipLaunchKernelGGL(tb_seq_gather, dim3((unsigned)((n_pass + 255) / 256)), dim3(256), 0, xs, G, tset);
+        hipLaunchKernelGGL(tb_seq_load_transfers, dim3(1024), dim3(256), 0, xs, NT, tset, X->T, N->seq_counts + 4, aset);
+        hipLaunchKernelGGL(tb_seq_event_accounts, dim3((unsigned)((n_pass + 255) / 256)), dim3(256), 0, xs, X->staging,
+                           n_pass, aset);
+        hipLaunchKernelGGL(tb_seq_verify, dim3(256), dim3(256), 0, xs, tset, (u64*)&X->g->panic);
+        hipLaunchKernelGGL(tb_seq_verify, dim3(256), dim3(256), 0, xs, aset, (u64*)&X->g->panic);
+        hipLaunchKernelGGL(tb_seq_load_accounts, dim3(1024), dim3(256), 0, xs, NT, aset, X->T);
+        NCK(hipGetLastError());
     }
-    for (u64 i = 0; i < nt; i++) {
-        if (!tstate[i]) continue;
-        aids.push_back(key(&trec[i * 128 + 16]));
-        aids.push_back(key(&trec[i * 128 + 32]));
-    }
-    uniq(aids);
-    const u64 na = aids.size();
-    std::vector<u8> arec(na * 128), afound(na);
+    // Its commit timestamp and balance bound: the node's.
+    N->h_seq[0] = N->commit_ts;
+    N->h_seq[1] = bound_lo;
+    N->h_seq[2] = bound_hi;
+    NCK(hipMemcpyAsync(&X->g->commit_timestamp, N->h_seq, 8, hipMemcpyHostToDevice, xs));
+    NCK(hipMemcpyAsync(&X->g->bound_lo, N->h_seq + 1, 16, hipMemcpyHostToDevice, xs));
+    X->commit_ts = N->commit_ts;
+    X->last_batch_ts = N->commit_ts;
+    X->log_next = N->seq_tcap;
+    // The pass's prepares: every block's, in order (their offsets in the pass and timestamps).
+    const u32 nb = P.k1 - P.k0;
+    u64* h_off = X->h_meta;
+    u64* h_ts = X->h_meta + nb + 1;
     {
-        std::vector<std::vector<u64>> ids(W);
-        std::vector<std::vector<u64>> where(W);
-        for (u64 i = 0; i < na; i++) {
-            const u32 o = node_home((const u8*)&aids[i], W);
-            ids[o].push_back((u64)aids[i]);
-            ids[o].push_back((u64)(aids[i] >> 64));
-            where[o].push_back(i);
-        }
-        for (u32 o = 0; o < W; o++) {
-            const u64 m = where[o].size();
-            if (!m) continue;
-            std::vector<u8> rec(m * 128), fd(m);
-            const int s = tbgpu_fetch_accounts(N->D[o].E, ids[o].data(), (u32)m, rec.data(), fd.data());
-            if (s) return s;
-            for (u64 j = 0; j < m; j++) {
-                memcpy(&arec[where[o][j] * 128], &rec[j * 128], 128);
-                afound[where[o][j]] = fd[j];
+        u64 at = 0;
+        u32 k = 0;
+        h_off[0] = 0;
+        for (u32 d = 0; d < W; d++) {
+            for (u32 j = 0; j < P.blk[d].k1 - P.blk[d].k0; j++, k++) {
+                h_off[k + 1] = at + P.off[d][j + 1];
+                h_ts[k] = ts[P.blk[d].k0 + j];
             }
+            at += P.blk[d].events;
         }
     }
-    // 3. The scratch engine, holding exactly what the pass reads.
-    u64 events = 0;
-    for (u32 k = P.k0; k < P.k1; k++) events += lens[k];
-    const u64 need_a = std::max<u64>(1024, na + 1), need_t = std::max<u64>(1024, nt + events + 1);
-    if (N->scratch && (N->scratch->cfg.accounts_max < need_a || N->scratch->cfg.transfers_max < need_t)) {
-        tbgpu_deinit(N->scratch);
-        N->scratch = nullptr;
+    NCK(hipMemcpyAsync(X->meta, X->h_meta, (2 * (u64)nb + 1) * 8, hipMemcpyHostToDevice, xs));
+    if (n_pass && (st = enqueue_call(X, OP_CREATE_TRANSFERS, nb, h_off, X->staging, X->results, X->reply_bytes, false,
+                                     N->seq_codes, 0, nullptr, X->meta))) {
+        return st;
     }
-    if (!N->scratch) {
-        tbgpu_config c = N->scratch_cfg;
-        c.accounts_max = std::max<u64>(need_a, 1 << 16);
-        c.transfers_max = std::max<u64>(need_t, 1 << 20);
-        c.pass_events_max = (u32)std::max<u64>(N->pe_src, BATCH_EVENTS_MAX);
-        c.pass_batches_max = std::max<u32>(1, std::min<u32>(N->pb_src, FLOW_NB_MAX));
-        c.flags &= ~(u32)TBGPU_CONFIG_PROFILE;
-        const int s = tbgpu_init(&c, &N->scratch);
-        if (s) return s;
+    if ((st = engine_sync(X))) return st;
+    const h128 xbound = ((h128)X->h_globals->bound_hi << 64) | X->h_globals->bound_lo;
+    // -- 4. write-back: the new transfers and posted states to their homes, the balances to their
+    //       owners (kernels on those devices, reading the sequencer over xGMI).
+    for (u32 d = 0; d < W; d++) {
+        NodeDev& D = N->D[d];
+        NCK(hipSetDevice(D.device));
+        NCK(hipMemsetAsync(D.wb_count, 0, 8, D.E->stream));
+        hipLaunchKernelGGL(tb_seq_writeback_transfers, dim3(1024), dim3(256), 0, D.E->stream, X->T, N->seq_tcap, n_pass,
+                           tset, D.E->T, d, W, D.E->log_next, D.wb_count);
+        hipLaunchKernelGGL(tb_seq_writeback_accounts, dim3(1024), dim3(256), 0, D.E->stream, X->T, aset, D.E->T, d, W);
+        NCK(hipGetLastError());
+        NCK(hipMemcpyAsync(D.h_dcounts + 3, D.wb_count, 8, hipMemcpyDeviceToHost, D.E->stream));
     }
-    tbgpu* X = N->scratch;
-    int s = tbgpu_reset(X);
-    if (s) return s;
-    if ((s = tbgpu_set_commit_timestamp(X, N->commit_ts))) return s;
-    {
-        std::vector<u8> found_recs;
-        for (u64 i = 0; i < na; i++) {
-            if (afound[i]) found_recs.insert(found_recs.end(), &arec[i * 128], &arec[i * 128] + 128);
-        }
-        if (!found_recs.empty() && (s = tbgpu_load_accounts(X, found_recs.data(), (u32)(found_recs.size() / 128)))) return s;
-        std::vector<u8> present, pstate;
-        for (u64 i = 0; i < nt; i++) {
-            if (!tstate[i]) continue;
-            present.insert(present.end(), &trec[i * 128], &trec[i * 128] + 128);
-            pstate.push_back((u8)(tstate[i] - 1));
-        }
-        if (!pstate.empty() && (s = tbgpu_load_transfers(X, present.data(), pstate.data(), (u32)pstate.size()))) return s;
+    // The sequenced part's balance growth goes to the first shard's bound (the node's bound is the
+    // shards' sum): read back below, written after the sync.
+    for (u32 d = 0; d < W; d++) {
+        NCK(hipSetDevice(N->D[d].device));
+        NCK(hipStreamSynchronize(N->D[d].E->stream));
+        N->D[d].E->log_next += N->D[d].h_dcounts[3];
     }
-    // 4. The pass, in order.
-    const u32 nk = P.k1 - P.k0;
-    std::vector<u32> in_lens(nk);
-    for (u32 k = 0; k < nk; k++) in_lens[k] = lens[P.k0 + k] * 128;
-    if ((s = commit_pipelined(X, OP_CREATE_TRANSFERS, nk, ts + P.k0, inputs + P.k0, in_lens.data(), outputs + P.k0,
-                              out_lens + P.k0, nullptr, std::min<u32>(nk, X->pb_max), nullptr))) {
-        return s;
-    }
-    // 5. Write back: new transfers and changed posted states to their homes, the touched accounts'
-    //    balances to their owners.
-    {
-        std::vector<u64> ids(2 * nt);
-        for (u64 i = 0; i < nt; i++) {
-            ids[2 * i] = (u64)tids[i];
-            ids[2 * i + 1] = (u64)(tids[i] >> 64);
-        }
-        std::vector<u8> after(nt * 128), ast(nt);
-        if (nt && (s = tbgpu_fetch_transfers(X, ids.data(), (u32)nt, after.data(), ast.data()))) return s;
-        std::vector<std::vector<u8>> recs(W), sts(W);
-        for (u64 i = 0; i < nt; i++) {
-            if (ast[i] == 0 || ast[i] == tstate[i]) continue;
-            const u32 h = node_home(&after[i * 128], W);
-            recs[h].insert(recs[h].end(), &after[i * 128], &after[i * 128] + 128);
-            sts[h].push_back(ast[i]);
-        }
-        for (u32 h = 0; h < W; h++) {
-            if (!sts[h].empty() && (s = tbgpu_upsert_transfers(N->D[h].E, recs[h].data(), sts[h].data(), (u32)sts[h].size()))) {
-                return s;
-            }
-        }
-        std::vector<u64> aid2;
-        for (u64 i = 0; i < na; i++) {
-            if (!afound[i]) continue;
-            aid2.push_back((u64)aids[i]);
-            aid2.push_back((u64)(aids[i] >> 64));
-        }
-        const u64 nf = aid2.size() / 2;
-        std::vector<u8> aafter(nf * 128), afd(nf);
-        if (nf && (s = tbgpu_fetch_accounts(X, aid2.data(), (u32)nf, aafter.data(), afd.data()))) return s;
-        std::vector<std::vector<u8>> arecs(W);
-        for (u64 i = 0; i < nf; i++) {
-            const u32 o = node_home(&aafter[i * 128], W);
-            arecs[o].insert(arecs[o].end(), &aafter[i * 128], &aafter[i * 128] + 128);
-        }
-        for (u32 o = 0; o < W; o++) {
-            if (!arecs[o].empty() && (s = node_upsert_accounts_keep_flow(N->D[o].E, arecs[o].data(), (u32)(arecs[o].size() / 128)))) {
-                return s;
-            }
-        }
+    if ((st = node_sync(N))) return st;
+    if (xbound > bound) {
+        tbgpu* E0 = N->D[0].E;
+        const h128 b0 = (((h128)E0->h_globals->bound_hi << 64) | E0->h_globals->bound_lo);
+        const h128 nb0 = b0 + (xbound - bound) < b0 ? ~(h128)0 : b0 + (xbound - bound);
+        N->h_seq[3] = (u64)nb0;
+        N->h_seq[4] = (u64)(nb0 >> 64);
+        NCK(hipSetDevice(N->D[0].device));
+        NCK(hipMemcpyAsync(&E0->g->bound_lo, N->h_seq + 3, 16, hipMemcpyHostToDevice, E0->stream));
+        NCK(hipStreamSynchronize(E0->stream));
     }
     N->commit_ts = std::max(N->commit_ts, X->commit_ts);
-    N->passes_sequenced++;
+    // -- 5. replies (the homes' codes and the sequencer's), then the sequencer's tables empty.
+    NodeRoute RT;
+    node_route(N, PL, RT);
+    if ((st = node_issue_replies(N, P, p, RT, N->seq_codes))) return st;
+    NCK(hipSetDevice(dev0));
+    hipLaunchKernelGGL(tb_seq_clear, dim3(1024), dim3(256), 0, xs, tset, aset, X->T);
+    NCK(hipGetLastError());
+    NCK(hipStreamSynchronize(xs));
+    if (all) N->passes_whole++;
+    else N->passes_split++;
+    N->seq_events += n_seq;
     return TBGPU_STATUS_OK;
 }
 
@@ -818,9 +962,13 @@ static int node_commit_transfers(TbNode* N, u32 n, const u64* ts, const void* co
             consume_upto(p);
             if (status) break;
             if ((status = node_sync(N))) break;
-            if ((status = node_sequence_pass(N, passes[p], ts, inputs, lens, outputs, out_lens))) break;
-            if (latency_ms) for (u32 k = passes[p].k0; k < passes[p].k1; k++) latency_ms[k] = 0;
-            passes[p].consumed = true;
+            bound = node_bound(N);
+            if ((status = node_split_pass(N, passes[p], p, ts, (u64)bound, (u64)(bound >> 64),
+                                          PL.huge || total == ~(h128)0))) {
+                break;
+            }
+            consume_upto(p + 1);
+            if (status) break;
             if ((status = node_sync(N))) break;
             bound = node_bound(N);
             continue;
@@ -837,8 +985,19 @@ static int node_commit_transfers(TbNode* N, u32 n, const u64* ts, const void* co
     return status ? status : s3;
 }
 
+// A device panic on any shard stops the node (tbgpu.h: until tbgpu_reset).
+static int node_poisoned(TbNode* N) {
+    for (u32 d = 0; d < N->world; d++) {
+        if (N->D[d].E->poisoned) {
+            return fail(TBGPU_STATUS_PANIC, "node stopped by an earlier device panic on shard %u (tbgpu_reset or tbgpu_deinit it)", d);
+        }
+    }
+    return TBGPU_STATUS_OK;
+}
+
 static int node_commit_pipelined(TbNode* N, u8 op, u32 n, const u64* ts, const void* const* inputs, const u32* input_lens,
                                  void* const* outputs, u32* out_lens, u32 chunk, double* latency_ms) {
+    if (const int st = node_poisoned(N)) return st;
     if (op != OP_CREATE_ACCOUNTS && op != OP_CREATE_TRANSFERS) {
         return fail(TBGPU_STATUS_INVALID, "operation %u is not a create operation", op);
     }
@@ -977,6 +1136,7 @@ static int node_api_reset(TbNode* N) {
 static int node_api_commit(TbNode* N, u8 op, u64 timestamp, const void* input, u32 input_len, void* output,
                            u32 output_cap, u32* out_len) {
     *out_len = 0;
+    if (const int st = node_poisoned(N)) return st;
     if (op < OP_CREATE_ACCOUNTS || op > OP_LOOKUP_TRANSFERS) return fail(TBGPU_STATUS_INVALID, "unknown operation %u", op);
     if (!(timestamp > N->commit_ts)) {  // state_machine.zig:519
         return fail(TBGPU_STATUS_PANIC, "timestamp %llu <= commit timestamp %llu", (unsigned long long)timestamp,
@@ -1030,12 +1190,13 @@ static int node_api_export(TbNode* N, int what, void* out, u64 cap, u64* count) 
     return TBGPU_STATUS_OK;
 }
 
-// Groove write-back of the node, O(changes) like a single engine's (engine.hip delta_*): the new
-// transfers of every shard's log, merged by timestamp; the posted entries their post / void records
-// make (the pending transfer may live on another shard: its timestamp is fetched from its home); the
-// accounts the new transfers moved — wherever those transfers live — plus the listed creates and
-// direct writes, each looked up on its OWNER, whose copy holds its balances (a whole-table diff of
-// a shard keeps only the accounts it owns).
+// Groove write-back of the node, O(changes) like a single engine's (engine.hip wb_*, the same
+// preallocated buffers on every shard): the new transfers of every shard's log, merged by timestamp;
+// the posted entries their post / void records make (the pending transfer may live on another
+// shard: its timestamp is fetched from its home); the accounts the new transfers moved — wherever
+// those transfers live — plus the listed creates and direct writes, each looked up on its OWNER,
+// whose copy holds its balances (a whole-table diff of a shard keeps only the accounts it owns).
+// The caller's buffers are checked up front against the most the write-back can emit.
 static int node_api_checkpoint_delta(TbNode* N, void* accounts_out, void* accounts_before_out, u64 accounts_cap,
                                      void* transfers_out, u64 transfers_cap, u64* posted_out, u64 posted_cap,
                                      tbgpu_delta_counts* counts) {
@@ -1043,105 +1204,135 @@ static int node_api_checkpoint_delta(TbNode* N, void* accounts_out, void* accoun
     const u32 W = N->world;
     int st = node_sync(N);
     if (st) return st;
-    std::vector<DeltaCtx> C(W);
-    auto abort_all = [&](int status) {
-        for (u32 d = 0; d < W; d++) delta_free(C[d]);
-        return status;
-    };
+    WbBounds bd{0, 0, 0};
+    u64 listed = 0;
+    bool scan = false;
+    for (u32 d = 0; d < W; d++) {
+        tbgpu* E = N->D[d].E;
+        NCK(hipSetDevice(N->D[d].device));
+        if (E->wb.inflight) return fail(TBGPU_STATUS_INVALID, "an asynchronous write-back is in flight");
+        if ((st = ckpt_snapshot_ready(E))) return st;
+        const WbBounds b = wb_bounds(E, E->h_globals->account_count);
+        bd.transfers += b.transfers;
+        bd.posted += b.posted;
+        listed += E->ckpt_ids.size() / 2;
+        scan |= E->ckpt_scan;
+    }
+    bd.accounts = std::min<u64>(N->D[0].E->h_globals->account_count, scan ? ~0ULL : 2 * bd.transfers + listed);
+    counts->created_after = N->D[0].E->ckpt_ts;
+    if (bd.accounts > accounts_cap || bd.transfers > transfers_cap || bd.posted > posted_cap) {  // nothing moved
+        counts->accounts = bd.accounts;
+        counts->transfers = bd.transfers;
+        counts->posted = bd.posted;
+        return fail(TBGPU_STATUS_INVALID, "checkpoint delta: buffers must hold %llu accounts, %llu transfers, %llu posted",
+                    (unsigned long long)bd.accounts, (unsigned long long)bd.transfers, (unsigned long long)bd.posted);
+    }
+    // 1. Every shard's new transfers (records, their account ids, post / void records), slice by slice.
+    std::vector<std::vector<u8>> runs(W);
     std::vector<u64> ids_all, pv_all;
     u64 nt = 0;
     for (u32 d = 0; d < W; d++) {
+        tbgpu* E = N->D[d].E;
         NCK(hipSetDevice(N->D[d].device));
-        std::vector<u64> ids, pv;
-        if ((st = delta_begin(N->D[d].E, C[d]))) return abort_all(st);
-        if ((st = delta_log_ids(N->D[d].E, C[d], &ids, &pv))) return abort_all(st);
-        ids_all.insert(ids_all.end(), ids.begin(), ids.end());
-        pv_all.insert(pv_all.end(), pv.begin(), pv.end());
-        ids_all.insert(ids_all.end(), N->D[d].E->ckpt_ids.begin(), N->D[d].E->ckpt_ids.end());
-        nt += C[d].nt;
+        if ((st = wb_next_epoch(E))) return st;
+        NCK(hipMemsetAsync(E->wb.d_cnt, 0, WB_COUNT_WORDS * 8, E->stream));
+        for (u64 a = E->ckpt_pos; a < E->log_next; a += E->wb.cap_t) {
+            const u64 b = std::min<u64>(E->log_next, a + E->wb.cap_t);
+            if ((st = wb_gather_slice(E, a, b, true, false))) return st;
+            if ((st = wb_read_counts(E))) return st;
+            const u64 k = E->wb.h_cnt[WB_RECORDS], q = E->wb.h_cnt[WB_PV];
+            const size_t r0 = runs[d].size(), i0 = ids_all.size(), p0 = pv_all.size();
+            runs[d].resize(r0 + k * 128);
+            ids_all.resize(i0 + k * 4);
+            pv_all.resize(p0 + q * 3);
+            if (k) NCK(hipMemcpyAsync(runs[d].data() + r0, E->wb.d_out, k * 128, hipMemcpyDeviceToHost, E->stream));
+            if (k) NCK(hipMemcpyAsync(ids_all.data() + i0, E->wb.d_ids, k * 32, hipMemcpyDeviceToHost, E->stream));
+            if (q) NCK(hipMemcpyAsync(pv_all.data() + p0, E->wb.d_pv, q * 24, hipMemcpyDeviceToHost, E->stream));
+            NCK(hipStreamSynchronize(E->stream));
+        }
+        delta_sort_by_timestamp(runs[d].data(), runs[d].size() / 128);
+        nt += runs[d].size() / 128;
+        ids_all.insert(ids_all.end(), E->ckpt_ids.begin(), E->ckpt_ids.end());
     }
+    // 2. The accounts, on their owners: the ids routed there, or the owner's whole-table diff.
     std::vector<std::vector<u64>> owned(W);
     for (size_t i = 0; i + 1 < ids_all.size(); i += 2) {
         const u32 o = tb_home(ids_all[i], ids_all[i + 1], W);
         owned[o].push_back(ids_all[i]);
         owned[o].push_back(ids_all[i + 1]);
     }
-    std::vector<u64> na(W, 0);
-    u64 na_total = 0;
+    u64 na = 0;
     for (u32 o = 0; o < W; o++) {
         tbgpu* E = N->D[o].E;
         NCK(hipSetDevice(N->D[o].device));
-        if ((st = delta_alloc_accounts(E, C[o], owned[o].size() / 2))) return abort_all(st);
-        if ((st = delta_ids_host(E, C[o], owned[o]))) return abort_all(st);
-        if ((st = delta_scan(E, C[o], W, o))) return abort_all(st);
-        if ((st = delta_account_count(E, C[o], &na[o]))) return abort_all(st);
-        na_total += na[o];
+        if ((st = wb_listed_ids(E, owned[o], (u8*)accounts_out, (u8*)accounts_before_out, &na))) return st;
+        if ((st = wb_scan(E, W, o, (u8*)accounts_out, (u8*)accounts_before_out, &na))) return st;
     }
-    std::vector<std::pair<u64, u64>> posted;
-    st = delta_posted_pairs(pv_all, posted, [&](const u64* ids, u32 n, u8* out, u8* state) {
-        return node_fetch(N, false, ids, n, out, state);
-    });
-    if (st) return abort_all(st);
-    counts->created_after = N->D[0].E->ckpt_ts;
-    counts->accounts = na_total;
-    counts->transfers = nt;
-    counts->posted = posted.size();
-    if (na_total > accounts_cap || nt > transfers_cap || posted.size() > posted_cap) {  // nothing advanced
-        return abort_all(fail(TBGPU_STATUS_INVALID, "checkpoint delta: needs %llu accounts, %llu transfers, %llu posted",
-                              (unsigned long long)na_total, (unsigned long long)nt, (unsigned long long)posted.size()));
+    // 3. The posted pairs: each post / void record's pending transfer, from its home.
+    const u64 npv = pv_all.size() / 3;
+    if (npv) {
+        std::vector<u64> ids(2 * npv);
+        for (u64 i = 0; i < npv; i++) {
+            ids[2 * i] = pv_all[3 * i];
+            ids[2 * i + 1] = pv_all[3 * i + 1];
+        }
+        std::vector<u8> rec(npv * 128), found(npv);
+        if ((st = node_fetch(N, false, ids.data(), (u32)npv, rec.data(), found.data()))) return st;
+        for (u64 i = 0; i < npv; i++) {
+            if (!found[i]) return fail(TBGPU_STATUS_PANIC, "checkpoint delta: a posted pending transfer is missing");
+            posted_out[2 * i] = *(const u64*)&rec[i * 128 + 120];
+            posted_out[2 * i + 1] = pv_all[3 * i + 2];
+        }
+        delta_sort_pairs(posted_out, npv);
     }
-    for (size_t i = 0; i < posted.size(); i++) {
-        posted_out[2 * i] = posted[i].first;
-        posted_out[2 * i + 1] = posted[i].second;
-    }
-    // Transfers: each shard's in timestamp order, merged.
-    std::vector<std::vector<u8>> runs(W);
-    for (u32 d = 0; d < W; d++) {
-        NCK(hipSetDevice(N->D[d].device));
-        runs[d].resize(C[d].nt * 128);
-        if ((st = delta_copy_transfers(N->D[d].E, C[d], runs[d].data()))) return abort_all(st);
-        delta_sort_by_timestamp(runs[d].data(), C[d].nt);
-    }
+    // 4. Transfers: each shard's in timestamp order, merged.
     {
         std::vector<size_t> pos(W, 0);
         auto ts_at = [&](u32 d) { return *(const u64*)&runs[d][pos[d] * 128 + 120]; };
         for (u64 k = 0; k < nt; k++) {
             u32 best = W;
             for (u32 d = 0; d < W; d++) {
-                if (pos[d] < C[d].nt && (best == W || ts_at(d) < ts_at(best))) best = d;
+                if (pos[d] < runs[d].size() / 128 && (best == W || ts_at(d) < ts_at(best))) best = d;
             }
             memcpy((u8*)transfers_out + k * 128, &runs[best][pos[best] * 128], 128);
             pos[best]++;
         }
     }
-    // Accounts: each owner's, one after the other.
-    u64 at = 0;
-    for (u32 o = 0; o < W; o++) {
-        NCK(hipSetDevice(N->D[o].device));
-        if ((st = delta_copy_accounts(N->D[o].E, C[o], na[o], (u8*)accounts_out + at * 128,
-                                      accounts_before_out ? (u8*)accounts_before_out + at * 64 : nullptr))) {
-            return abort_all(st);
-        }
-        at += na[o];
-    }
+    // 5. Every shard's snapshot advances.
     for (u32 d = 0; d < W; d++) {
         NCK(hipSetDevice(N->D[d].device));
-        if ((st = delta_end(N->D[d].E, C[d]))) return abort_all(st);
+        if ((st = wb_advance(N->D[d].E))) return st;
+        NCK(hipStreamSynchronize(N->D[d].E->stream));
     }
+    counts->accounts = na;
+    counts->transfers = nt;
+    counts->posted = npv;
     return TBGPU_STATUS_OK;
+}
+
+static void node_reset_stats(TbNode* N) {
+    tbgpu_reset_stats(N->X);
+    N->passes_clean = N->passes_split = N->passes_whole = N->seq_events = 0;
 }
 
 static int node_api_get_stats(TbNode* N, tbgpu_stats* s) {
     memset(s, 0, sizeof(*s));
-    for (u32 d = 0; d < N->world; d++) {
+    s->node_passes_clean = N->passes_clean;
+    s->node_passes_split = N->passes_split;
+    s->node_passes_whole = N->passes_whole;
+    s->node_sequenced_events = N->seq_events;
+    for (u32 d = 0; d <= N->world; d++) {  // every shard, then the sequencer (its ordered-path work)
+        const bool seq = d == N->world;
         tbgpu_stats x;
-        const int st = tbgpu_get_stats(N->D[d].E, &x);
+        const int st = tbgpu_get_stats(seq ? N->X : N->D[d].E, &x);
         if (st) return st;
-        s->passes += x.passes;
-        s->events += x.events;
         s->dependent_events += x.dependent_events;
-        if (d == 0) s->accounts = x.accounts;  // replicated records
-        s->transfers += x.transfers;
+        if (!seq) {
+            s->passes += x.passes;
+            s->events += x.events;
+            if (d == 0) s->accounts = x.accounts;  // replicated records
+            s->transfers += x.transfers;
+        }
         s->ms_validate += x.ms_validate;
         s->ms_resolve += x.ms_resolve;
         s->ms_replay += x.ms_replay;
@@ -1238,9 +1429,6 @@ static int node_api_transfers_in(TbNode* N, const void* records, const u8* state
     return TBGPU_STATUS_OK;
 }
 
-static int node_upsert_accounts_keep_flow(tbgpu* E, const void* records, uint32_t n) {
-    return upsert_accounts(E, records, n, false, true);
-}
 
 static u64 node_commit_ts(TbNode* N) { return N->commit_ts; }
 static u32 node_world(TbNode* N) { return N->world; }

@@ -95,7 +95,22 @@ struct PassArgs {
 
     u32* leg_off;          // [prepares of the pass][leg_buckets + 1] bucket starts in the prepare's legs
     u32* flow_words;       // tb_flow's per-pass counters (k_flow.h, FLOW_WORDS), zeroed by tb_resolve (or null)
+    u64* kclock;           // profiling (or null): this pass's launch spans, {first start, last end} of
+                           // validate, resolve and apply (device wall clock), set up by tb_pass_clear
 };
+
+// Launch span of a profiled kernel (tbgpu_stats.span_ms): every workgroup lowers the start word to
+// its own start and raises the end word to its own end; the host reads them after the pass.
+#define KCLOCK_WORDS 6  // per pass: [2k] start, [2k + 1] end of kernel k (0 validate, 1 resolve, 2 apply)
+__device__ static inline void tb_kclock_start(const PassArgs& P, u32 k) {
+    if (P.kclock && threadIdx.x == 0) atomicMin((unsigned long long*)&P.kclock[2 * k], (unsigned long long)wall_clock64());
+}
+// Every thread of the workgroup calls it (a barrier, then thread 0 stamps).
+__device__ static inline void tb_kclock_end(const PassArgs& P, u32 k) {
+    if (!P.kclock) return;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax((unsigned long long*)&P.kclock[2 * k + 1], (unsigned long long)wall_clock64());
+}
 
 enum : u32 { CERT_EXT_U128 = 1, CERT_EXT_U64 = 2 };
 
@@ -249,9 +264,10 @@ __device__ static inline void tb_dedup_mark(const PassArgs& P) {
 // kernel arguments instead of a copy ahead of the pass (the replica's one-prepare commits).
 __global__ __launch_bounds__(256) void tb_pass_clear(u64* dedup, u64 cap, u64* sum_shards, const Globals* g, u32 epoch,
                                                      u32 force, u32* leg_tot, u32 leg_buckets, u64* meta, u64 m0, u64 m1,
-                                                     u64 m2) {
+                                                     u64 m2, u64* kclock) {
     const u64 w = g->dedup_dirty;  // before the stores (a load after them waits for them)
     if (blockIdx.x == 0 && threadIdx.x < SUM_WORDS) sum_shards[threadIdx.x] = 0;
+    if (kclock && blockIdx.x == 0 && threadIdx.x < KCLOCK_WORDS) kclock[threadIdx.x] = (threadIdx.x & 1) ? 0 : ~0ULL;
     if (meta && blockIdx.x == 0 && threadIdx.x == 0) {
         meta[0] = m0;
         meta[1] = m1;

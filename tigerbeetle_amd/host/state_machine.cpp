@@ -69,13 +69,20 @@ StateMachine::StateMachine(const Options& o) {
 }
 
 StateMachine::~StateMachine() {
-    for (std::vector<uint8_t>* b : {&wb_accounts_, &wb_before_, &wb_transfers_, &wb_posted_}) {
-        if (!b->empty()) tbgpu_unregister_host(engine_, b->data());
+    if (wb_inflight_ >= 0) {
+        tbgpu_delta_counts c;
+        (void)tbgpu_checkpoint_delta_wait(engine_, &c);  // its buffers go away with this object
+    }
+    for (WbSet& w : wb_) {
+        for (std::vector<uint8_t>* b : {&w.accounts, &w.before, &w.transfers, &w.posted}) {
+            if (!b->empty()) tbgpu_unregister_host(engine_, b->data());
+        }
     }
     tbgpu_deinit(engine_);
 }
 
 void StateMachine::reset() {
+    wb_inflight_ = -1;  // the engine drops a write-back in flight with its state
     check(tbgpu_reset(engine_), "reset");
     prepare_timestamp = 0;
     commit_timestamp = 0;
@@ -143,13 +150,22 @@ std::vector<size_t> StateMachine::commit_many(Operation operation, const std::ve
 }
 
 void StateMachine::compact(const Callback& callback, uint64_t op) {
-    // The HBM tables need no compaction; the durable copy gets the bar's changes at its last op.
-    if (write_back && lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0) write_back(checkpoint_delta());
+    // The HBM tables need no compaction; the durable copy gets each bar's changes, one bar behind.
+    if (write_back && lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0) {
+        wb_deliver_inflight();  // the previous bar's objects: landed while this bar committed
+        reserve_write_back();
+        WbSet& w = wb_[wb_bar_];
+        check(tbgpu_checkpoint_delta_async(engine_, w.accounts.data(), w.before.data(), w.caps[0], w.transfers.data(),
+                                           w.caps[1], (uint64_t*)w.posted.data(), w.caps[2]),
+              "checkpoint_delta_async");
+        wb_inflight_ = wb_bar_;
+        wb_bar_ ^= 1;
+    }
     callback(*this);
 }
 
-// The write-back buffers are the state machine's own, allocated and registered once (grown when a
-// delta needs more room: static allocation in the steady state), so the delta lands by DMA.
+// The write-back buffers are the state machine's own, registered once (grown only when a delta
+// needs more room), so the objects land by DMA.
 static void grow_registered(tbgpu_t* engine, std::vector<uint8_t>& buf, size_t bytes) {
     if (buf.size() >= bytes) return;
     if (!buf.empty()) tbgpu_unregister_host(engine, buf.data());
@@ -159,37 +175,67 @@ static void grow_registered(tbgpu_t* engine, std::vector<uint8_t>& buf, size_t b
     }
 }
 
+void StateMachine::reserve_write_back() {
+    // Room for a whole bar (what a bar of prepares can change at most, tbgpu.h), registered once.
+    const uint64_t ev = (uint64_t)lsm_batch_multiple * TBGPU_BATCH_EVENTS_MAX;
+    const uint64_t caps[3] = {2 * ev, ev, ev};
+    for (WbSet& w : wb_) wb_reserve(w, caps);
+}
+
+void StateMachine::wb_reserve(WbSet& w, const uint64_t caps[3]) {
+    for (int k = 0; k < 3; k++) w.caps[k] = std::max(w.caps[k], std::max<uint64_t>(caps[k], 1));
+    grow_registered(engine_, w.accounts, w.caps[0] * 128);
+    grow_registered(engine_, w.before, w.caps[0] * 64);
+    grow_registered(engine_, w.transfers, w.caps[1] * 128);
+    grow_registered(engine_, w.posted, w.caps[2] * 16);
+}
+
+const Delta& StateMachine::wb_view(const WbSet& w, const tbgpu_delta_counts& c) {
+    delta_.accounts = w.accounts.data();
+    delta_.accounts_before = w.before.data();
+    delta_.account_count = c.accounts;
+    delta_.transfers = w.transfers.data();
+    delta_.transfer_count = c.transfers;
+    delta_.posted = (const uint64_t*)w.posted.data();
+    delta_.posted_count = c.posted;
+    delta_.created_after = c.created_after;
+    return delta_;
+}
+
+void StateMachine::wb_deliver_inflight() {
+    if (wb_inflight_ < 0) return;
+    tbgpu_delta_counts c{};
+    const int set = wb_inflight_;
+    wb_inflight_ = -1;
+    check(tbgpu_checkpoint_delta_wait(engine_, &c), "checkpoint_delta_wait");
+    const Delta& d = wb_view(wb_[set], c);
+    if (write_back) write_back(d);
+}
+
 const Delta& StateMachine::checkpoint_delta() {
-    tbgpu_delta_counts counts{wb_caps_[0], wb_caps_[1], wb_caps_[2], 0};
+    wb_deliver_inflight();
+    WbSet& w = wb_[0];
+    if (!w.caps[0]) {
+        const uint64_t first[3] = {1024, 1024, 1024};
+        wb_reserve(w, first);
+    }
+    tbgpu_delta_counts counts{};
     for (;;) {
-        wb_caps_[0] = std::max<uint64_t>(wb_caps_[0], counts.accounts);
-        wb_caps_[1] = std::max<uint64_t>(wb_caps_[1], counts.transfers);
-        wb_caps_[2] = std::max<uint64_t>(wb_caps_[2], counts.posted);
-        grow_registered(engine_, wb_accounts_, wb_caps_[0] * 128);
-        grow_registered(engine_, wb_before_, wb_caps_[0] * 64);
-        grow_registered(engine_, wb_transfers_, wb_caps_[1] * 128);
-        grow_registered(engine_, wb_posted_, wb_caps_[2] * 16);
-        const int st = tbgpu_checkpoint_delta(engine_, wb_accounts_.data(), wb_before_.data(), wb_caps_[0],
-                                              wb_transfers_.data(), wb_caps_[1], (uint64_t*)wb_posted_.data(),
-                                              wb_caps_[2], &counts);
+        const int st = tbgpu_checkpoint_delta(engine_, w.accounts.data(), w.before.data(), w.caps[0], w.transfers.data(),
+                                              w.caps[1], (uint64_t*)w.posted.data(), w.caps[2], &counts);
         if (st == TBGPU_STATUS_INVALID &&
-            (counts.accounts > wb_caps_[0] || counts.transfers > wb_caps_[1] || counts.posted > wb_caps_[2])) {
-            continue;  // room for everything, then retry (nothing advanced)
+            (counts.accounts > w.caps[0] || counts.transfers > w.caps[1] || counts.posted > w.caps[2])) {
+            const uint64_t need[3] = {counts.accounts, counts.transfers, counts.posted};
+            wb_reserve(w, need);  // room for everything, then retry (nothing advanced)
+            continue;
         }
         check(st, "checkpoint_delta");
-        delta_.accounts = wb_accounts_.data();
-        delta_.accounts_before = wb_before_.data();
-        delta_.account_count = counts.accounts;
-        delta_.transfers = wb_transfers_.data();
-        delta_.transfer_count = counts.transfers;
-        delta_.posted = (const uint64_t*)wb_posted_.data();
-        delta_.posted_count = counts.posted;
-        delta_.created_after = counts.created_after;
-        return delta_;
+        return wb_view(w, counts);
     }
 }
 
 void StateMachine::checkpoint(const Callback& callback) {
+    wb_deliver_inflight();
     const Delta& d = checkpoint_delta();
     if (write_back) write_back(d);
     callback(*this);

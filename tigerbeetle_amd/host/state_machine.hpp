@@ -180,9 +180,11 @@ public:
     std::vector<size_t> commit_many(Operation operation, const std::vector<uint64_t>& timestamps,
                                     const std::vector<const void*>& inputs, const std::vector<size_t>& input_lens,
                                     const std::vector<void*>& outputs);
-    // Writes the engine's changes back (checkpoint_delta -> write_back, when set) at the last op of
-    // every bar (config.zig:143 lsm_batch_multiple = 64), as the Zig wrapper does before
-    // forest.compact; then calls back.
+    // At the last op of every bar (config.zig:143 lsm_batch_multiple = 64) with `write_back` set:
+    // hands the PREVIOUS bar's changes to write_back (they crossed PCIe while this bar committed)
+    // and starts this bar's without waiting (tbgpu_checkpoint_delta_async: the reference's compact
+    // is asynchronous, src/state_machine.zig:542-567); then calls back.  The forest so trails the
+    // engine by at most one bar, and checkpoint() closes the gap.
     void compact(const Callback& callback, uint64_t op);
     // The replica's message pool (MessagePool.init_capacity, src/message_pool.zig:98-120): buffers
     // registered once, so prefetch stages a prepare body from its message by DMA.
@@ -194,11 +196,15 @@ public:
     // default): commit's first kernel reads the body straight from the registered message, which
     // is faster when commit follows prefetch at once (tb_replica_bench: 0.092 vs 0.115 ms per op).
     bool stage_bodies = false;
-    // Hands the objects changed since the previous checkpoint to `write_back` (if set), then calls
-    // back (state_machine.zig:565-582).
+    // Hands every object changed since the previous write-back to `write_back` (if set) — the bar
+    // still in flight, then the rest — then calls back (state_machine.zig:565-582).
     void checkpoint(const Callback& callback);
+    // The synchronous write-back (a bar in flight is handed to write_back first).
     const Delta& checkpoint_delta();
     WriteBack write_back;
+    // Allocates and registers both bar-sized write-back buffer sets now (the Zig wrapper does it in
+    // init): otherwise the first bar's compact does.
+    void reserve_write_back();
 
     // Test-only: the table harness `setup` action (state_machine.zig:1398-1407).
     void test_set_balances(u128 account_id, u128 debits_pending, u128 debits_posted, u128 credits_pending,
@@ -211,10 +217,18 @@ public:
 
 private:
     void check(int status, const char* what) const;
+    struct WbSet {  // one set of registered write-back buffers
+        uint64_t caps[3] = {0, 0, 0};  // accounts, transfers, posted
+        std::vector<uint8_t> accounts, before, transfers, posted;
+    };
+    void wb_reserve(WbSet& w, const uint64_t caps[3]);
+    const Delta& wb_view(const WbSet& w, const tbgpu_delta_counts& c);
+    void wb_deliver_inflight();
     tbgpu_t* engine_ = nullptr;
     Delta delta_;
-    uint64_t wb_caps_[3] = {1024, 1024, 1024};
-    std::vector<uint8_t> wb_accounts_, wb_before_, wb_transfers_, wb_posted_;
+    WbSet wb_[2];          // [0]: synchronous write-backs and even bars, [1]: odd bars
+    int wb_bar_ = 0;       // the set the next bar's asynchronous write-back uses
+    int wb_inflight_ = -1; // the set of the write-back in flight, or -1
 };
 
 }  // namespace tb

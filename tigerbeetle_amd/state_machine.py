@@ -77,8 +77,9 @@ class Engine:
 
     def close(self):
         if getattr(self, "h", None):
-            for arr in getattr(self, "_delta_bufs", (None, ()))[1]:
-                self.lib.tbgpu_unregister_host(self.h, arr.ctypes.data)
+            for _caps, bufs in (getattr(self, "_delta_bufs", None) or {}).values():
+                for arr in bufs:
+                    self.lib.tbgpu_unregister_host(self.h, arr.ctypes.data)
             self._delta_bufs = None
             self.lib.tbgpu_deinit(self.h)
             self.h = None
@@ -225,23 +226,23 @@ class Engine:
     def stats(self):
         s = _lib.tbgpu_stats()
         _lib.check(self.lib.tbgpu_get_stats(self.h, ctypes.byref(s)))
-        return {f: (list(getattr(s, f)) if f in ("flow_phase_ms", "walk_dbg") else getattr(s, f)) for f, _ in s._fields_}
+        return {f: (list(getattr(s, f)) if f in ("flow_phase_ms", "walk_dbg", "span_ms", "span_launches") else getattr(s, f)) for f, _ in s._fields_}
 
     def reset_stats(self):
         self.lib.tbgpu_reset_stats(self.h)
 
     PROF_VALIDATE, PROF_RESOLVE, PROF_REPLAY, PROF_CLEAR, PROF_PASS, PROF_APPLY, PROF_ALL = 1, 2, 4, 8, 16, 32, 63
 
-    def checkpoint_delta(self, caps=None):
+    def checkpoint_delta(self, caps=None, copy=True):
         """Objects changed since the previous call (groove write-back): a Delta of accounts (in no
         particular order), transfers (by timestamp) and posted pairs {pending timestamp,
         fulfillment}.  caps: initial buffer sizes (accounts, transfers, posted); grown and retried
-        when too small.  The arrays are views of buffers the engine keeps registered for DMA (the
-        wrapper's write-back buffers, allocated once): valid until the next call."""
+        when too small (the engine says what suffices).  copy=False returns views of the buffers the
+        engine keeps registered for DMA: valid only until the next write-back."""
         counts = _lib.tbgpu_delta_counts()
         caps = list(caps) if caps else [1024, 1024, 1024]
         while True:
-            a, before, t, p = self._delta_buffers(caps)
+            a, before, t, p = self._delta_buffers(caps, 0)
             st = self.lib.tbgpu_checkpoint_delta(self.h, a.ctypes.data, before.ctypes.data, caps[0], t.ctypes.data,
                                                  caps[1], p.ctypes.data, caps[2], ctypes.byref(counts))
             need = [counts.accounts, counts.transfers, counts.posted]
@@ -249,11 +250,38 @@ class Engine:
                 caps = [max(c, n) for c, n in zip(caps, need)]
                 continue
             _lib.check(st)
-            return Delta(a[:need[0]], t[:need[1]], p[:need[2]], before[:need[0]], counts.created_after)
+            return self._delta(a, before, t, p, counts, copy)
 
-    def _delta_buffers(self, caps):
-        """Write-back buffers of at least `caps` entries, kept (and registered) across calls."""
-        have = getattr(self, "_delta_bufs", None)
+    def checkpoint_delta_async(self, caps):
+        """tbgpu_checkpoint_delta_async into one of two registered buffer sets of at least `caps`
+        (accounts, transfers, posted) entries — size them for a bar, as the Zig wrapper does; the
+        objects land while later commits run.  checkpoint_delta_wait() returns the Delta."""
+        self._wb_set = 1 - getattr(self, "_wb_set", 1)
+        a, before, t, p = self._delta_buffers(list(caps), self._wb_set)
+        _lib.check(self.lib.tbgpu_checkpoint_delta_async(self.h, a.ctypes.data, before.ctypes.data, caps[0],
+                                                         t.ctypes.data, caps[1], p.ctypes.data, caps[2]))
+        self._wb_inflight = (a, before, t, p)
+
+    def checkpoint_delta_wait(self, copy=True):
+        counts = _lib.tbgpu_delta_counts()
+        _lib.check(self.lib.tbgpu_checkpoint_delta_wait(self.h, ctypes.byref(counts)))
+        a, before, t, p = self._wb_inflight
+        self._wb_inflight = None
+        return self._delta(a, before, t, p, counts, copy)
+
+    @staticmethod
+    def _delta(a, before, t, p, counts, copy):
+        need = [counts.accounts, counts.transfers, counts.posted]
+        parts = (a[:need[0]], t[:need[1]], p[:need[2]], before[:need[0]])
+        if copy:
+            parts = tuple(x.copy() for x in parts)
+        return Delta(*parts, counts.created_after)
+
+    def _delta_buffers(self, caps, which):
+        """Write-back buffer set `which` (0 / 1) of at least `caps` entries, kept (and registered)
+        across calls."""
+        sets = getattr(self, "_delta_bufs", None) or {}
+        have = sets.get(which)
         if have is not None and all(h >= c for h, c in zip(have[0], caps)):
             return have[1]
         if have is not None:
@@ -264,7 +292,8 @@ class Engine:
                 np.empty(caps[1], dtype=TRANSFER_DTYPE), np.empty((caps[2], 2), dtype=np.uint64))
         for arr in bufs:
             _lib.check(self.lib.tbgpu_register_host(self.h, arr.ctypes.data, arr.nbytes))
-        self._delta_bufs = (caps, bufs)
+        sets[which] = (caps, bufs)
+        self._delta_bufs = sets
         return bufs
 
     def ledger_summary(self):

@@ -20,7 +20,7 @@ MODE=${1:-kt}
 OUT=$R/gpurun_out/prof
 mkdir -p "$OUT"; rm -rf "$OUT/$MODE"
 cd /tmp && export TMPDIR=/tmp
-LEG="--cpu-sample 0 --host-prepares 0 --device-steps 0 --secondary 0"
+LEG="--cpu-sample 0 --host-prepares 0 --device-steps 0 --secondary 0 --write-back 0 --replica-prepares 0"
 case $MODE in
   kt) timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 "$R/bench.py" $LEG \
         > "$OUT/bench_kt.log" 2>&1; rc=$? ;;
@@ -33,7 +33,7 @@ case $MODE in
         python3 "$R/tools/gpu/device_pass.py" > "$OUT/dkt.log" 2>&1; rc=$? ;;
   fetch|write) C=FETCH_SIZE; [ "$MODE" = write ] && C=WRITE_SIZE
       timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/bench.py" $LEG \
-        --steps 1 --warmup 0 --transfers 20000000 > "$OUT/$MODE.log" 2>&1; rc=$? ;;
+        --steps 1 --warmup 0 > "$OUT/$MODE.log" 2>&1; rc=$? ;;
   c3|c3h|c4) timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/bench.py" \
         --workload $MODE --accounts 1000000 --transfers 10000000 --steps 1 --warmup 0 $LEG --access-mix 0 \
         > "$OUT/bench_$MODE.log" 2>&1; rc=$? ;;

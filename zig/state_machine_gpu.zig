@@ -31,6 +31,7 @@
 const std = @import("std");
 const assert = std.debug.assert;
 const mem = std.mem;
+const log = std.log.scoped(.state_machine_gpu);
 
 const tbgpu = @cImport({
     @cInclude("tbgpu.h");
@@ -87,6 +88,12 @@ pub fn StateMachineType(
             /// has work between prefetch and commit; otherwise commit's first kernel reads the body
             /// straight from its registered message (DESIGN.md §5b).
             engine_stage_bodies: bool = false,
+            /// The caller guarantees every prepare body it passes lives in a MessagePool buffer, right
+            /// after its sector-aligned header (src/message_pool.zig:98-120): the engine may then pin
+            /// those buffers (tbgpu_register_host) for direct reads.  Off: bodies are copied from
+            /// pageable memory, and the engine pins nothing it does not own (test / fuzzer / replay
+            /// buffers from any allocator stay safe).
+            engine_register_messages: bool = false,
 
             fn base(options: Options) Base.Options {
                 return .{
@@ -134,6 +141,7 @@ pub fn StateMachineType(
         prefetch_context: PrefetchContext = undefined,
 
         engine_stage_bodies: bool,
+        engine_register_messages: bool,
         /// Message buffers registered with the engine, keyed by address (at most the pool's
         /// messages_max_replica, all allocated once by MessagePool.init_capacity).
         registered_messages: std.AutoHashMapUnmanaged(usize, void),
@@ -209,6 +217,7 @@ pub fn StateMachineType(
                 .load_transfers = load_transfers,
                 .load_posted = load_posted,
                 .engine_stage_bodies = options.engine_stage_bodies,
+                .engine_register_messages = options.engine_register_messages,
                 .registered_messages = registered_messages,
             };
         }
@@ -473,17 +482,27 @@ pub fn StateMachineType(
             return out_len;
         }
 
-        /// A prepare body lives in a message buffer of the replica's pool, right after its header
-        /// (MessagePool.init_capacity allocates each buffer once, sector-aligned, message_size_max
-        /// bytes: src/message_pool.zig:98-120).  The first commit from a buffer registers it with the
-        /// engine, so every later body from it reaches the GPU by direct read, with no staging copy.
-        /// A body elsewhere (not right after a sector-aligned header) is left pageable.
+        /// With engine_register_messages (the caller's promise that bodies come from the replica's
+        /// MessagePool: each buffer allocated once, sector-aligned, message_size_max bytes, the body
+        /// right after its header, src/message_pool.zig:98-120), the first commit from a buffer
+        /// registers it with the engine, so every later body from it reaches the GPU by direct read.
+        /// A body elsewhere, or a registration the runtime refuses, is simply left pageable: the
+        /// commit copies it (the reference never panics on commit over where a body lives).
         fn register_message(self: *StateMachine, input: []align(16) const u8) void {
+            if (!self.engine_register_messages) return;
             const address = @intFromPtr(input.ptr) -| @sizeOf(Header);
             if (address % global_constants.sector_size != 0) return;
             if (self.registered_messages.contains(address)) return;
             if (self.registered_messages.count() == messages_max_replica) return;
-            check(tbgpu.tbgpu_register_host(self.engine, @ptrFromInt(address), global_constants.message_size_max));
+            if (tbgpu.tbgpu_register_host(self.engine, @ptrFromInt(address), global_constants.message_size_max) !=
+                tbgpu.TBGPU_STATUS_OK)
+            {
+                log.warn("message buffer 0x{x} not registered ({s}); its bodies are copied", .{
+                    address,
+                    std.mem.span(tbgpu.tbgpu_last_error()),
+                });
+                return;
+            }
             self.registered_messages.putAssumeCapacity(address, {});
         }
 
