@@ -306,8 +306,11 @@ static int prof_collect(tbgpu* E) {
         for (const auto& u : E->kclock_used) {
             const u64* w = E->h_kclock + (u64)u.first * KCLOCK_WORDS;
             for (u32 k = 0; k < 3; k++) {
-                if (!((u.second >> k) & 1) || w[2 * k + 1] < w[2 * k] || !E->wall_khz) continue;
-                E->span_ms[k] += (double)(w[2 * k + 1] - w[2 * k]) / E->wall_khz;
+                const u64* kw = w + k * KCLOCK_STRIDE;
+                u64 end = 0;
+                for (u32 q = 1; q <= KCLOCK_ENDS; q++) end = std::max(end, kw[q]);
+                if (!((u.second >> k) & 1) || end < kw[0] || !E->wall_khz) continue;
+                E->span_ms[k] += (double)(end - kw[0]) / E->wall_khz;
                 E->span_n[k] += 1;
             }
         }
@@ -930,6 +933,8 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         if (P.legs || P.apply_late) {
             if ((st = prof_begin(E, &pp, K_APPLY))) return st;
             if (P.legs) {
+                hipLaunchKernelGGL(tb_leg_totals, dim3((b1 - b0 + TOTALS_PREPARES - 1) / TOTALS_PREPARES), dim3(256), 0,
+                                   E->stream, P);
                 hipLaunchKernelGGL(tb_apply_legs, dim3(E->leg_buckets + APPLY_EXTRA), dim3(APPLY_THREADS), (4u << E->leg_shift) * 8,
                                    E->stream, P);
             } else if (n > 0 && !owner) {  // owner-partitioned: the owners apply the legs instead

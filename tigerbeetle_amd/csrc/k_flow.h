@@ -780,26 +780,33 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
     const bool isx = r.kind & BT_X, isy = valid && !isx, cr = r.kind & BT_CR;
     const u32 vd = (r.kind >> 8) & 15, vc = (r.kind >> 12) & 15;
     u32 oth = cr ? vd : vc;
-    if (valid && isx && oth == BV_UNK && st == BS_UNK) oth = cr ? (vw & 3) : ((vw >> 2) & 3);
     // A position is SIMPLE when its outcome follows from d alone: a check whose partner side is
     // known (v = slack − amount: ok iff v + d >= 0; its outcome is this side's verdict), or a leg
     // whose unit is decided (v = ±BIG).  The others stop the scalar walk: a Y leg of an open unit, a
     // check paired with an open one.
     bool simple = true, check = false;
     i64 v = 0, dl = 0;
-    if (!valid) {
-        simple = false;
-    } else if (st != BS_UNK) {
-        v = st == BS_OK ? WALK_BIG : -WALK_BIG;
-        dl = isx ? -r.a : r.a;
-    } else if (isy || oth == BV_UNK) {
-        simple = false;
-    } else {
-        check = true;
-        v = r.base - r.a;
-        dl = oth == BV_FAIL ? 0 : -r.a;  // the other side failed: no delta here either way
-    }
-    const u64 smask = __ballot(simple);
+    auto classify = [&]() {
+        if (valid && isx && oth == BV_UNK && st == BS_UNK) oth = cr ? (vw & 3) : ((vw >> 2) & 3);
+        simple = true;
+        check = false;
+        v = 0;
+        dl = 0;
+        if (!valid) {
+            simple = false;
+        } else if (st != BS_UNK) {
+            v = st == BS_OK ? WALK_BIG : -WALK_BIG;
+            dl = isx ? -r.a : r.a;
+        } else if (isy || oth == BV_UNK) {
+            simple = false;
+        } else {
+            check = true;
+            v = r.base - r.a;
+            dl = oth == BV_FAIL ? 0 : -r.a;  // the other side failed: no delta here either way
+        }
+    };
+    classify();
+    u64 smask = __ballot(simple);
     const u64 vmask = n == 64 ? ~0ULL : ((1ULL << n) - 1);
     u64 okm = 0;  // lane j's outcome in the walk (a check's own verdict)
     u32 j = s, m = n, pub = s;  // [s, pub): published while waiting in place
@@ -892,8 +899,16 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         fl_walk_run(v, dl, j, b, d, okm);
         j = b;
         if (b == n) break;
-        // Position b: its partner was open when the window loaded.
+        // Position b: its partner was open when the window loaded.  The window's other open
+        // positions after b re-read their statuses in the same round trip as b's poll (they were
+        // loaded a window ahead; a partner walker has usually decided them since): each one decided
+        // by now walks as a simple position instead of stopping the walk again.
         ws.stops++;
+        const bool refresh = valid && lane > b && !simple;
+        if (refresh) {
+            st = fl_ld32(&F.b_st[r.u]);
+            if (isx) vw = fl_ld32(&F.b_vw[r.u]);
+        }
         const u32 bu = __builtin_amdgcn_readlane(r.u, b), bk = __builtin_amdgcn_readlane(r.kind, b);
         if ((bk & BT_X) && pmask) wait_until([&]() { return !pmask; });  // a paired check needs the exact d
         const i64 ba = (i64)fl_rl64((u64)r.a, b);
@@ -918,6 +933,10 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
             return __builtin_amdgcn_readfirstlane(s2);
         };
         u32 fin = poll();
+        if (__ballot(refresh)) {  // the refreshed positions after b, classified again
+            if (refresh) classify();
+            smask = __ballot(simple);
+        }
         // A paired check whose own side failed moves nothing here, whatever the other side says.
         const bool moot = (bk & BT_X) && !side_ok;
         if (fin == BS_UNK && !(bk & BT_X) && wait) {  // an open Y leg: pending (above)

@@ -385,7 +385,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
             total = tb_sat_add(total, tb_u128(*(const u64*)q, *(const u64*)(q + 8)));
         }
         tb_sum_publish(P, total);
-        if (P.kclock) atomicMax((unsigned long long*)&P.kclock[1], (unsigned long long)wall_clock64());
+        if (P.kclock) tb_kclock_stamp_end(P.kclock + 1 + (blockIdx.x % KCLOCK_ENDS));
     }
 }
 
