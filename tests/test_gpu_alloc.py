@@ -68,6 +68,8 @@ def test_no_allocation_after_init(profile, gpu_engine_factory):
         k += 8190
         ts += 10**4
         assert engine.commit(129, ts, t.tobytes()) == b""                       # pageable, one prepare
+        t = _transfers(8190, k, 64)
+        k += 8190
         body[:t.nbytes] = t.view(np.uint8)
         ts += 10**4
         assert _commit_raw(engine, 129, ts, body[:t.nbytes]) == b""             # registered: read through

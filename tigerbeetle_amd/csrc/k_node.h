@@ -221,24 +221,24 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_node_classify1(RouteArgs A, 
     }
 }
 
-// Every source's keys and balancing accounts into this device's two 64-bit key sets (a false match
-// only makes one more event sequenced, which is always exact).  Grid-stride over the lists' lengths,
-// read from the sources' count words (peer reads: no host round trip).
+// Every source's keys or balancing accounts (whichever set is given) into this device's 64-bit key set
+// (a false match only makes one more event sequenced, which is always exact).  Grid-stride over the
+// lists' lengths, read from the sources' count words (peer reads: no host round trip).
 struct NodeSetArgs {
     const u64* keys[NODE_WORLD_MAX];
     const u64* bal[NODE_WORLD_MAX];
     const u64* counts[NODE_WORLD_MAX];
     u32 world;
-    u64* keyset;
+    u64* keyset;      // null: skip the keys
     u64 keyset_mask;
-    u64* markset;
+    u64* markset;     // null: skip the balancing accounts
     u64 markset_mask;
 };
 
 __global__ __launch_bounds__(256) void tb_node_sets(NodeSetArgs S) {
     const u64 stride = (u64)gridDim.x * 256;
     for (u32 s = 0; s < S.world; s++) {
-        const u64 nk = S.counts[s][0], nb = S.counts[s][1];
+        const u64 nk = S.keyset ? S.counts[s][0] : 0, nb = S.markset ? S.counts[s][1] : 0;
         for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < nk; i += stride) {
             (void)tb_dedup_insert(S.keyset, S.keyset_mask, tb_dedup_key(S.keys[s][2 * i], S.keys[s][2 * i + 1]));
         }
@@ -248,15 +248,29 @@ __global__ __launch_bounds__(256) void tb_node_sets(NodeSetArgs S) {
     }
 }
 
-__global__ __launch_bounds__(ROUTE_THREADS) void tb_node_classify2(RouteArgs A, NodeDepArgs D, const u64* keyset, u64 keyset_mask,
-                                                                   const u64* markset, u64 markset_mask) {
+// An event on an account some balancing event of the pass touches is primary-dependent too, and its
+// id joins the keys (before the key set is built): every sequenced event's id is then a key.
+__global__ __launch_bounds__(ROUTE_THREADS) void tb_node_classify_marked(RouteArgs A, NodeDepArgs D, const u64* markset,
+                                                                         u64 markset_mask) {
+    const u64 e = (u64)blockIdx.x * ROUTE_THREADS + threadIdx.x;
+    if (e >= A.n || D.dep1[e] != 0) return;
+    const u64* w = (const u64*)(A.events + e * 128);
+    if (tb_dedup_is_dup_or_present(markset, markset_mask, tb_dedup_key(w[2], w[3])) ||
+        tb_dedup_is_dup_or_present(markset, markset_mask, tb_dedup_key(w[4], w[5]))) {
+        D.dep1[e] = 16;
+        const u64 k = atomicAdd((unsigned long long*)&D.counts[0], 1ULL);
+        D.keys[2 * k] = w[0];
+        D.keys[2 * k + 1] = w[1];
+    }
+}
+
+// Final: sequenced = primary-dependent, or its id is a key (the id or pending id of a primary one).
+__global__ __launch_bounds__(ROUTE_THREADS) void tb_node_classify2(RouteArgs A, NodeDepArgs D, const u64* keyset, u64 keyset_mask) {
     const u64 e = (u64)blockIdx.x * ROUTE_THREADS + threadIdx.x;
     bool seq = false;
     if (e < A.n) {
         const u64* w = (const u64*)(A.events + e * 128);
-        seq = D.dep1[e] != 0 || tb_dedup_is_dup_or_present(keyset, keyset_mask, tb_dedup_key(w[0], w[1])) ||
-              tb_dedup_is_dup_or_present(markset, markset_mask, tb_dedup_key(w[2], w[3])) ||
-              tb_dedup_is_dup_or_present(markset, markset_mask, tb_dedup_key(w[4], w[5]));
+        seq = D.dep1[e] != 0 || tb_dedup_is_dup_or_present(keyset, keyset_mask, tb_dedup_key(w[0], w[1]));
         D.dep[e] = seq ? 1 : 0;
     }
     const u64 m = __ballot(seq);

@@ -75,7 +75,7 @@ struct NodeDev {
     u64* markset = nullptr;
     u64 set_mask = 0;
     u64* wb_count = nullptr;     // sequencer write-back: records appended here
-    hipEvent_t ev_cls = nullptr;
+    hipEvent_t ev_cls = nullptr, ev_marked = nullptr;
 };
 
 struct NodeBlock {
@@ -147,7 +147,7 @@ static void node_free(TbNode* N) {
         for (void* p : host) if (p) (void)hipHostFree(p);
         hipEvent_t evs[] = {D.ev_start[0], D.ev_start[1], D.ev_start[2], D.ev_done[0], D.ev_done[1], D.ev_done[2],
                             D.ev_planned[0], D.ev_planned[1], D.ev_copied, D.ev_gathered, D.ev_committed,
-                            D.ev_applied, D.ev_replied, D.ev_cls};
+                            D.ev_applied, D.ev_replied, D.ev_cls, D.ev_marked};
         for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
         if (D.rs) (void)hipStreamDestroy(D.rs);
         if (D.E) tbgpu_deinit(D.E);
@@ -278,6 +278,7 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
         NALLOC(tbMalloc(&D.markset, (D.set_mask + 1) * 8));
         NALLOC(tbMalloc(&D.wb_count, 8));
         NALLOC(tbEventCreateWithFlags(&D.ev_cls, hipEventDisableTiming));
+        NALLOC(tbEventCreateWithFlags(&D.ev_marked, hipEventDisableTiming));
     }
 #undef NALLOC
     if (e != hipSuccess) {
@@ -708,22 +709,26 @@ static int node_consume(TbNode* N, NodePass& P, u32 p, void* const* outputs, u32
 static int node_split_pass(TbNode* N, NodePass& P, u32 p, const u64* ts, u64 bound_lo, u64 bound_hi, bool all) {
     const u32 W = N->world, par = p & 1;
     tbgpu* X = N->X;
-    // -- 1. classification on every source: primary classes, then the key sets, then the final mask
-    //       and the route plan of the rest.
+    auto route_args = [&](NodeDev& D, const NodeBlock& B) {
+        RouteArgs A{};
+        A.events = D.stage[par];
+        A.n = (u32)B.events;
+        A.nb = B.k1 - B.k0;
+        A.batch_off = D.meta[par];
+        A.batch_ts = D.meta[par] + A.nb + 1;
+        A.world = W;
+        A.T = D.E->T;
+        return A;
+    };
+    // -- 1. classification on every source: primary classes, then the events on balancing-marked
+    //       accounts, then the key set, the final mask and the route plan of the rest.
     for (u32 d = 0; d < W; d++) {
         NodeDev& D = N->D[d];
         const NodeBlock& B = P.blk[d];
         NCK(hipSetDevice(D.device));
         NCK(hipMemsetAsync(D.dcounts, 0, 4 * 8, D.rs));
         if (B.events) {
-            RouteArgs A{};
-            A.events = D.stage[par];
-            A.n = (u32)B.events;
-            A.nb = B.k1 - B.k0;
-            A.batch_off = D.meta[par];
-            A.batch_ts = D.meta[par] + A.nb + 1;
-            A.world = W;
-            A.T = D.E->T;
+            const RouteArgs A = route_args(D, B);
             NodeDepArgs Dp{D.dep1, D.dep, D.dkeys, D.dbal, D.dcounts, all ? 1u : 0u};
             hipLaunchKernelGGL(tb_node_classify1, dim3((unsigned)((B.events + ROUTE_THREADS - 1) / ROUTE_THREADS)),
                                dim3(ROUTE_THREADS), 0, D.rs, A, Dp);
@@ -738,37 +743,49 @@ static int node_split_pass(TbNode* N, NodePass& P, u32 p, const u64* ts, u64 bou
         S.bal[d] = N->D[d].dbal;
         S.counts[d] = N->D[d].dcounts;
     }
+    // Events on a balancing-marked account become primary-dependent (their ids join the key lists),
+    // once every source's balancing accounts are known: every sequenced event's id is then a key, so
+    // no routed event creates an id a sequenced event reads.
     for (u32 d = 0; d < W; d++) {
         NodeDev& D = N->D[d];
         const NodeBlock& B = P.blk[d];
         NCK(hipSetDevice(D.device));
         for (u32 s = 0; s < W; s++) NCK(hipStreamWaitEvent(D.rs, N->D[s].ev_cls, 0));
-        NCK(hipMemsetAsync(D.keyset, 0, (D.set_mask + 1) * 8, D.rs));
         NCK(hipMemsetAsync(D.markset, 0, (D.set_mask + 1) * 8, D.rs));
         NodeSetArgs Sd = S;
-        Sd.keyset = D.keyset;
         Sd.markset = D.markset;
-        Sd.keyset_mask = Sd.markset_mask = D.set_mask;
+        Sd.markset_mask = D.set_mask;
+        hipLaunchKernelGGL(tb_node_sets, dim3(512), dim3(256), 0, D.rs, Sd);
+        if (B.events) {
+            const RouteArgs A = route_args(D, B);
+            NodeDepArgs Dp{D.dep1, D.dep, D.dkeys, D.dbal, D.dcounts, all ? 1u : 0u};
+            hipLaunchKernelGGL(tb_node_classify_marked, dim3((unsigned)((B.events + ROUTE_THREADS - 1) / ROUTE_THREADS)),
+                               dim3(ROUTE_THREADS), 0, D.rs, A, Dp, D.markset, D.set_mask);
+        }
+        NCK(hipGetLastError());
+        NCK(hipEventRecord(D.ev_marked, D.rs));
+    }
+    for (u32 d = 0; d < W; d++) {
+        NodeDev& D = N->D[d];
+        const NodeBlock& B = P.blk[d];
+        NCK(hipSetDevice(D.device));
+        for (u32 s = 0; s < W; s++) NCK(hipStreamWaitEvent(D.rs, N->D[s].ev_marked, 0));
+        NCK(hipMemsetAsync(D.keyset, 0, (D.set_mask + 1) * 8, D.rs));
+        NodeSetArgs Sd = S;
+        Sd.keyset = D.keyset;
+        Sd.keyset_mask = D.set_mask;
         hipLaunchKernelGGL(tb_node_sets, dim3(512), dim3(256), 0, D.rs, Sd);
         NCK(hipGetLastError());
         NCK(hipMemsetAsync(D.words[par], 0, ROUTE_WORDS * 8, D.rs));
         if (B.events) {
-            RouteArgs A{};
-            A.events = D.stage[par];
-            A.n = (u32)B.events;
-            A.nb = B.k1 - B.k0;
-            A.batch_off = D.meta[par];
-            A.batch_ts = D.meta[par] + A.nb + 1;
-            A.world = W;
+            RouteArgs A = route_args(D, B);
             A.nblocks = (u32)((B.events + ROUTE_THREADS - 1) / ROUTE_THREADS);
             A.home = D.home[par];
             A.block_counts = D.block_counts;
             A.block_base = D.block_counts + (u64)A.nblocks * W;
             A.words = D.words[par];
-            A.T = D.E->T;
             NodeDepArgs Dp{D.dep1, D.dep, D.dkeys, D.dbal, D.dcounts, all ? 1u : 0u};
-            hipLaunchKernelGGL(tb_node_classify2, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, D.rs, A, Dp, D.keyset, D.set_mask,
-                               D.markset, D.set_mask);
+            hipLaunchKernelGGL(tb_node_classify2, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, D.rs, A, Dp, D.keyset, D.set_mask);
             A.skip = D.dep;
             hipLaunchKernelGGL(tb_route_classify, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, D.rs, A);
             hipLaunchKernelGGL(tb_route_offsets, dim3(A.world), dim3(1024), 0, D.rs, A);

@@ -8,10 +8,10 @@ export TMPDIR=/tmp
 O=gpurun_out/r04
 mkdir -p $O
 run() { echo "== $*"; }
-timeout -k 10 600 python -u -m pytest -x -v --timeout 240 --timeout-method thread -m gpu \
+timeout -k 10 600 python -u -m pytest -v --timeout 240 --timeout-method thread -m gpu \
   tests/test_gpu_alloc.py tests/test_gpu_determinism.py tests/test_gpu_checkpoint.py tests/test_gpu_node.py > $O/new.log 2>&1
 rc=$?; echo "new tests rc=$rc"; grep -E "PASSED|FAILED|ERROR" $O/new.log | tail -40
-[ $rc -ne 0 ] && { grep -E "^E " $O/new.log | head -40; exit $rc; }
+[ $rc -ne 0 ] && { grep -E "^E " $O/new.log | head -60; exit $rc; }
 [ "$1" = quick ] && exit 0
 timeout -k 10 900 python -u -m pytest -q -x --timeout 300 --timeout-method thread -m gpu tests > $O/suite.log 2>&1
 rc=$?; echo "suite rc=$rc"; tail -3 $O/suite.log
