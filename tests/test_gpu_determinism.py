@@ -47,3 +47,22 @@ def test_dependent_events_equal_the_model(seed, knobs, gpu_engine_factory):
         counts.append(engine.stats()["dependent_events"] - before)
         engine.close()
     assert counts == [expected] * 3, (counts, expected)
+
+
+@pytest.mark.parametrize("config", ["overflow", "mixed"])
+def test_dependent_events_repeat_without_the_global_certificate(config, gpu_engine_factory):
+    """Near-overflow balances (set directly) defeat the global certificate, so every account-touching
+    event is checked against its own accounts' pre-pass balances: the count must not depend on which
+    workgroups ran first (nothing applies balances while the resolve kernel classifies)."""
+    knobs = dict(CONFIGS[config])
+    knobs["near_overflow"] = True
+    counts, replies = [], []
+    for _ in range(3):
+        engine = gpu_engine_factory()
+        replies.append(run_many(make_scenario(4244, **knobs), engine))
+        counts.append(engine.stats()["dependent_events"])
+        engine.close()
+    assert counts[0] > 0 and counts == [counts[0]] * 3, counts
+    assert replies[0] == replies[1] == replies[2]
+    oracle = OracleEngine()
+    assert run_oracle(make_scenario(4244, **knobs), oracle) == replies[0]

@@ -96,7 +96,7 @@ struct TbNode;  // node.h: the multi-device engine (tbgpu_config.device_count > 
 // Groove write-back buffers (tbgpu_checkpoint_delta / _async), every one allocated at tbgpu_init.
 #define WB_IDS_MAX (1ULL << 20)  // listed ids (creates, direct balance writes) between write-backs
 #define WB_OUT_GRID 128          // workgroups of the asynchronous copy-out (a PCIe stream, not the CUs)
-enum { WB_ACCOUNTS = 0, WB_SLOTS = 1, WB_PV = 2, WB_RECORDS = 3, WB_STATUS = 4, WB_COUNT_WORDS = 8 };
+enum { WB_ACCOUNTS = 0, WB_SLOTS = 1, WB_PV = 2, WB_RECORDS = 3, WB_STATUS = 4, WB_ORDER = 5, WB_COUNT_WORDS = 8 };
 struct WbBufs {
     u64 cap_t = 0;    // log positions per slice
     u64 cap_ids = 0;  // listed ids per chunk
@@ -937,8 +937,10 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
                                    E->stream, P);
                 hipLaunchKernelGGL(tb_apply_legs, dim3(E->leg_buckets + APPLY_EXTRA), dim3(APPLY_THREADS), (4u << E->leg_shift) * 8,
                                    E->stream, P);
-            } else if (n > 0 && !owner) {  // owner-partitioned: the owners apply the legs instead
-                hipLaunchKernelGGL(tb_apply_events, dim3((u32)((n + 255) / 256)), dim3(256), 0, E->stream, P);
+            }
+            if (n > 0 && !owner) {  // owner-partitioned: the owners apply the legs instead
+                const u32 grid = (u32)std::min<u64>((n + 255) / 256, P.legs ? 2048 : 1u << 20);
+                hipLaunchKernelGGL(tb_apply_events, dim3(grid), dim3(256), 0, E->stream, P);
             }
             HIPCK(hipGetLastError());
             if ((st = prof_end(E, &pp))) return st;
@@ -1758,8 +1760,9 @@ static int wb_wait(tbgpu* E, tbgpu_delta_counts* counts) {
         E->poisoned = true;
         return fail(TBGPU_STATUS_PANIC, "checkpoint delta: a posted pending transfer is missing");
     }
-    delta_sort_by_timestamp(W.out_t, counts->transfers);
-    delta_sort_pairs(W.out_p, counts->posted);
+    // Only when tb_delta_out saw them out of order (the synchronous path's outputs are sorted).
+    if (W.out_t && (W.h_cnt[WB_ORDER] & 1)) delta_sort_by_timestamp(W.out_t, counts->transfers);
+    if (W.out_p && (W.h_cnt[WB_ORDER] & 2)) delta_sort_pairs(W.out_p, counts->posted);
     return TBGPU_STATUS_OK;
 }
 
@@ -1905,8 +1908,10 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
     O.dst[3] = m_p;
     O.count[3] = W.d_cnt + WB_PV;
     O.elem[3] = 16;
+    O.order = W.d_cnt + WB_ORDER;
     hipLaunchKernelGGL(tb_delta_out, dim3(WB_OUT_GRID), dim3(256), 0, W.stream, O);
     HIPCK(hipGetLastError());
+    HIPCK(hipMemcpyAsync(W.h_cnt + WB_ORDER, W.d_cnt + WB_ORDER, 8, hipMemcpyDeviceToHost, W.stream));
     HIPCK(hipEventRecord(W.done, W.stream));
     W.inflight = true;
     return TBGPU_STATUS_OK;

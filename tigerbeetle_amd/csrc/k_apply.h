@@ -275,16 +275,22 @@ __device__ static inline void tb_apply_legs_body(const PassArgs& P, u64* s_acc) 
     }
 }
 
-// Kernel 2b of a small pass (no legs): the balance effects of every independent ok transfer, one
-// event per lane.  The resolve kernel has one workgroup per prepare; left there, a one-prepare
-// pass (the replica's commit) would issue all 16K atomics of its prepare from a single CU.
+// Kernel 2b: the balance effects of every independent ok transfer that is not a leg, grid-stride,
+// one event per lane — every one in a small pass (no legs: the resolve kernel has one workgroup per
+// prepare, and a one-prepare pass, the replica's commit, would issue all 16K atomics of its prepare
+// from a single CU), the post / voids and the wide amounts in a legs pass (none at all when the pass
+// word says so: the launch exits at once).  The resolve kernel applies nothing itself, so its
+// classification reads the pre-pass balances.
 __global__ __launch_bounds__(256) void tb_apply_events(PassArgs P) {
-    const u32 pe = blockIdx.x * 256 + threadIdx.x;
+    if (P.legs && !P.pass_words[PW_LATE]) return;
     u128 S;
     bool cert_global, cert64;
     tb_pass_cert(P, S, cert_global, cert64);  // every lane (a wave-wide sum)
-    if (pe >= P.n) return;
-    const u32 info = P.info[pe];
-    if ((info & HZ_DEP) || (info & 0xFF) != R_OK || !(info & HZ_ACCTS)) return;
-    tb_apply_transfer(P, pe, info, P.eflags[pe], cert64);
+    for (u32 pe = blockIdx.x * 256 + threadIdx.x; pe < P.n; pe += gridDim.x * 256) {
+        const u32 info = P.info[pe];
+        if ((info & HZ_DEP) || (info & 0xFF) != R_OK || !(info & HZ_ACCTS)) continue;
+        // The resolve kernel's leg condition: those went to tb_apply_legs.
+        if (P.legs && cert64 && !(info & (HZ_POSTVOID | HZ_AMT_HI)) && P.amt[pe] <= LEG_AMT_MASK) continue;
+        tb_apply_transfer(P, pe, info, P.eflags[pe], cert64);
+    }
 }

@@ -243,11 +243,16 @@ __global__ void tb_delta_advance(Tables T, AccountBal* snap, const u32* slots, c
 // HBM into the caller's registered host buffers (their device mappings), each region as long as its
 // device-side count says — so no host round trip has to learn the sizes first.  Runs on its own
 // stream, beside the next commits; 16-B stores, consecutive lanes on consecutive chunks.
+// Regions 0 (transfer records) and 3 (posted pairs) are also checked for order on the way: `order`
+// gets bit 0 when a record's timestamp does not exceed its predecessor's (records appended by an
+// upsert or a load), bit 1 when a pair is below its predecessor — the host sorts only then, instead
+// of reading every record back to find out.
 struct DeltaOut {
     const u8* src[4];
     u8* dst[4];
     const u64* count[4];  // elements of each region
     u32 elem[4];          // bytes per element
+    u64* order;
 };
 __global__ __launch_bounds__(256) void tb_delta_out(DeltaOut A) {
     const u64 stride = (u64)gridDim.x * 256;
@@ -259,6 +264,18 @@ __global__ __launch_bounds__(256) void tb_delta_out(DeltaOut A) {
         u32x4* out = (u32x4*)A.dst[r];
         for (u64 c = (u64)blockIdx.x * 256 + threadIdx.x; c < chunks; c += stride) out[c] = in[c];
     }
+    bool unsorted_t = false, unsorted_p = false;
+    const u64 nt = *A.count[0], np = *A.count[3];
+    for (u64 i = 1 + (u64)blockIdx.x * 256 + threadIdx.x; i < nt; i += stride) {
+        const u64* t = (const u64*)(A.src[0] + i * 128 + 120);
+        unsorted_t |= t[-16] >= t[0];  // the previous record's timestamp
+    }
+    for (u64 i = 1 + (u64)blockIdx.x * 256 + threadIdx.x; i < np; i += stride) {
+        const u64* q = (const u64*)A.src[3] + 2 * i;
+        unsorted_p |= q[-2] > q[0] || (q[-2] == q[0] && q[-1] > q[1]);
+    }
+    const u64 flags = (__ballot(unsorted_t) ? 1 : 0) | (__ballot(unsorted_p) ? 2 : 0);
+    if ((threadIdx.x & 63) == 0 && flags) atomicOr((unsigned long long*)A.order, (unsigned long long)flags);
 }
 
 // ---- pipelined host commits (tbgpu_commit_pipelined) -------------------------------------------

@@ -351,6 +351,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     u64 tsmax = 0;
     u32 ndep = 0, n_app = 0, n_fail = 0;  // per thread, summed per wave below (one LDS atomic per wave)
     u32 legmask = 0;  // bit k: this thread's event k contributes two legs
+    // An independent ok transfer that is not a leg is applied by tb_apply_events after this kernel:
+    // no balance changes while any workgroup classifies, so the per-account certificate checks read
+    // the pre-pass balances and the classification is a function of the input alone.
+    bool late = false;
     u32* dep_out = P.dep_list + pbase;
     // No chain and no dependent event (uniform): every final result is the intrinsic code, already
     // in s_code; the loop below without its chain and dependent cases, branch-light.
@@ -382,8 +386,8 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                         tb_hist16_inc(s_hist, crs >> P.leg_shift);
                     }
                     legmask |= 1u << k;
-                } else if (!P.apply_late) {
-                    tb_apply_transfer(P, pe, info, r_fl[k], cert64);
+                } else {
+                    late = true;
                 }
             } else if (valid && (info & HZ_SPEC)) {
                 tb_xindex_tombstone(T, P.rs[pe]);  // a failed event's speculative record
@@ -443,8 +447,8 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                                 tb_hist16_inc(s_hist, crs >> P.leg_shift);
                             }
                             legmask |= 1u << k;
-                        } else if (!P.apply_late) {
-                            tb_apply_transfer(P, pe, info, r_fl[k], cert64);
+                        } else {
+                            late = true;
                         }
                     } else {
                         tb_apply_account(P, pe, ts);
@@ -471,6 +475,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     }
     }
 
+    if (P.legs && __ballot(late) && (threadIdx.x & 63) == 0) P.pass_words[PW_LATE] = 1;
     // commit_timestamp: max over events that returned ok when evaluated (:763, :882, :1012).
     u64 m = tsmax;
 #pragma unroll

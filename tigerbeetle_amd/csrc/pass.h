@@ -85,7 +85,7 @@ struct PassArgs {
     // create_transfer events are written as legs, bucketed by account slot per prepare, and summed
     // per account by tb_apply_legs instead of being added with one global atomic per leg.
     u32 legs;              // 1: the legs path is enabled for this pass (the host checked the sizes)
-    u32 apply_late;        // 1: tb_apply_events applies the independent ok transfers (small passes)
+    u32 apply_late;        // 1: no legs; tb_apply_events applies the independent ok transfers (small passes)
     u32 leg_shift;         // bucket of an account slot = slot >> leg_shift (2^leg_shift slots each)
     u32* leg_tot;          // [leg_buckets + 1] legs per bucket in the pass (tb_leg_totals; zeroed by tb_pass_clear),
                            // then the number of buckets that reached APPLY_SPLIT_MIN
@@ -249,12 +249,14 @@ __device__ static inline u128 tb_wave_sum_u128(u128 v) {
 // blocks per pass) so the mod-2^128 shard atomics never wrap.
 // Pass words after the shards: HUGE (S >= 2^100 somewhere), DUP (an id or pending-id collision
 // happened), BAL (a tentatively-ok balancing event exists), PV (a post/void event registered its
-// pending id).  Written with idempotent stores.
+// pending id), LATE (an independent ok transfer of a legs pass is not a leg: tb_apply_events applies
+// it).  Written with idempotent stores.
 #define PW_HUGE (2 * SUM_SHARDS)
 #define PW_DUP (2 * SUM_SHARDS + 1)
 #define PW_BAL (2 * SUM_SHARDS + 2)
 #define PW_PV (2 * SUM_SHARDS + 3)
-#define SUM_WORDS (2 * SUM_SHARDS + 4)
+#define PW_LATE (2 * SUM_SHARDS + 4)
+#define SUM_WORDS (2 * SUM_SHARDS + 5)
 __device__ static inline void tb_sum_publish(const PassArgs& P, u128 block_sum) {
     if (block_sum == 0) return;
     if (tb_hi(block_sum) >> 36) {

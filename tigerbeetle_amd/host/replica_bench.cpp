@@ -127,6 +127,7 @@ int main(int argc, char** argv) {
     std::vector<double> lat;
     lat.reserve(prepares);
     uint64_t failed = 0;
+    double compact_ms = 0, compact_max = 0;  // inside compact (the write-back's host side)
     const auto run0 = std::chrono::steady_clock::now();
     auto t_timed = run0;
     for (uint64_t op = 1; op <= total_ops; op++) {
@@ -137,8 +138,14 @@ int main(int argc, char** argv) {
         sm.prepare(tb::Operation::create_transfers, body, len);
         sm.prefetch([](tb::StateMachine&) {}, op, tb::Operation::create_transfers, body, len);
         const size_t n = sm.commit(0, op, sm.prepare_timestamp, tb::Operation::create_transfers, body, len, reply.data());
+        const auto tc = std::chrono::steady_clock::now();
         sm.compact([](tb::StateMachine&) {}, op);
         const auto t1 = std::chrono::steady_clock::now();
+        if (op > warmup) {
+            const double c = std::chrono::duration<double, std::milli>(t1 - tc).count();
+            compact_ms += c;
+            compact_max = std::max(compact_max, c);
+        }
         failed += n / 8;
         sm.prepare_timestamp += 1;
         if (op > warmup) lat.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
@@ -151,10 +158,10 @@ int main(int argc, char** argv) {
     printf("{\"call_path\": \"prepare -> prefetch -> commit -> compact per op (tb::StateMachine, C++)\", "
            "\"ops\": %llu, \"events_per_op\": %u, \"write_back\": %s, \"prefetch_stages_body\": %s, \"transfers_per_s\": %.1f, "
            "\"ms_per_op\": %.4f, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"p100_ms\": %.4f, \"failed_events\": %llu, "
-           "\"written_back_objects\": %llu}\n",
+           "\"written_back_objects\": %llu, \"compact_ms_per_op\": %.4f, \"compact_ms_max\": %.4f}\n",
            (unsigned long long)prepares, batch, write_back ? "true" : "false", stage ? "true" : "false",
            prepares * batch / (total_ms / 1e3),
            total_ms / prepares, pick(sorted, 50), pick(sorted, 99), pick(sorted, 100), (unsigned long long)failed,
-           (unsigned long long)wb_objects);
+           (unsigned long long)wb_objects, compact_ms / prepares, compact_max);
     return failed ? 1 : 0;
 }
