@@ -82,7 +82,7 @@ static u64 pow2_at_least(u64 v) {
 }
 
 #define PIPE_SLOTS 3
-#define KCLOCK_SLOTS 4096  // profiled passes between two collects (a full ring is collected early)
+#define KCLOCK_SLOTS 2048  // profiled passes between two collects (a full ring is collected early)
 
 enum { K_VALIDATE = 0, K_RESOLVE = 1, K_REPLAY = 2, K_CLEAR = 3, K_PASS = 4, K_APPLY = 5, K_COUNT = 6 };
 
@@ -214,6 +214,7 @@ struct tbgpu {
 
 
     bool profile = false;
+    bool kclock_off = false;
     u32 legs_min = LEGS_MIN_EVENTS;
     u64 wall_khz = 0;  // device wall clock (flow phase timing)
     WbBufs wb;
@@ -302,13 +303,13 @@ static int prof_end(tbgpu* E, ProfilePair* p) {
 
 static int prof_collect(tbgpu* E) {
     if (!E->kclock_used.empty()) {  // the stream has drained: every stamped span is final
-        HIPCK(hipMemcpy(E->h_kclock, E->kclock, (u64)KCLOCK_SLOTS * KCLOCK_WORDS * 8, hipMemcpyDeviceToHost));
+        HIPCK(hipMemcpy(E->h_kclock, E->kclock, (u64)E->kclock_next * KCLOCK_WORDS * 8, hipMemcpyDeviceToHost));
         for (const auto& u : E->kclock_used) {
             const u64* w = E->h_kclock + (u64)u.first * KCLOCK_WORDS;
             for (u32 k = 0; k < 3; k++) {
                 const u64* kw = w + k * KCLOCK_STRIDE;
                 u64 end = 0;
-                for (u32 q = 1; q <= KCLOCK_ENDS; q++) end = std::max(end, kw[q]);
+                for (u32 q = 1; q <= KCLOCK_ENDS; q++) end = std::max(end, kw[q * KCLOCK_LINE]);
                 if (!((u.second >> k) & 1) || end < kw[0] || !E->wall_khz) continue;
                 E->span_ms[k] += (double)(end - kw[0]) / E->wall_khz;
                 E->span_n[k] += 1;
@@ -479,6 +480,7 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     E->profile = (config->flags & TBGPU_CONFIG_PROFILE) != 0;
 #ifdef TBGPU_TIMING_KNOBS
     if (const char* ab = getenv("TBGPU_ABLATE")) E->ablate = (u32)strtoul(ab, nullptr, 0);  // timing experiments only
+    E->kclock_off = getenv("TBGPU_NO_KCLOCK") != nullptr;  // timing experiments: no launch-span stamps
 #endif
     int st = TBGPU_STATUS_OK;
 #define INIT_CK(x)                                                                                 \
@@ -876,7 +878,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
 
         // Launch spans of this pass's kernels on the device clock (profiling only).
         P.kclock = nullptr;
-        if (E->profile && (E->prof_mask & ((1u << K_VALIDATE) | (1u << K_RESOLVE) | (1u << K_APPLY))) &&
+        if (E->profile && !E->kclock_off && (E->prof_mask & ((1u << K_VALIDATE) | (1u << K_RESOLVE) | (1u << K_APPLY))) &&
             E->kclock_next < KCLOCK_SLOTS) {
             const u32 slot = E->kclock_next++;
             P.kclock = E->kclock + (u64)slot * KCLOCK_WORDS;
@@ -933,8 +935,6 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         if (P.legs || P.apply_late) {
             if ((st = prof_begin(E, &pp, K_APPLY))) return st;
             if (P.legs) {
-                hipLaunchKernelGGL(tb_leg_totals, dim3((b1 - b0 + TOTALS_PREPARES - 1) / TOTALS_PREPARES), dim3(256), 0,
-                                   E->stream, P);
                 hipLaunchKernelGGL(tb_apply_legs, dim3(E->leg_buckets + APPLY_EXTRA), dim3(APPLY_THREADS), (4u << E->leg_shift) * 8,
                                    E->stream, P);
             }

@@ -21,37 +21,6 @@
 #define APPLY_SPLIT_MIN LEG_SPLIT_MIN         // buckets at least this heavy are split (2 parts)
 #define APPLY_EXTRA 64                        // extra workgroups of tb_apply_legs for the parts
 
-// The pass's legs per bucket (leg_tot; zeroed by tb_pass_clear) from the prepares' bucket-start rows:
-// each workgroup sums a run of prepares' rows column-wise (coalesced row reads, eight buckets a
-// thread in registers) and adds its sums once per bucket; leg_tot[NBK] counts the buckets that
-// reached LEG_SPLIT_MIN.  Between tb_resolve and tb_apply_legs.
-#define TOTALS_PREPARES 16  // prepares a workgroup sums
-__global__ __launch_bounds__(256) void tb_leg_totals(PassArgs P) {
-    u128 S;
-    bool cert_global, cert64;
-    tb_pass_cert(P, S, cert_global, cert64);
-    if (!cert64) return;  // no legs were emitted this pass
-    const u32 NBK = P.leg_buckets, nb = P.b1 - P.b0, stride = NBK + 1;
-    const u32 p0 = blockIdx.x * TOTALS_PREPARES, p1 = min(nb, p0 + TOTALS_PREPARES);
-    for (u32 k0 = threadIdx.x * 8; k0 < NBK; k0 += 256 * 8) {
-        u32 sum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (u32 p = p0; p < p1; p++) {
-            const u32* row = P.leg_off + (u64)p * stride + k0;
-            u32 w[9];
-#pragma unroll
-            for (u32 q = 0; q < 9; q++) w[q] = k0 + q <= NBK ? row[q] : 0;
-#pragma unroll
-            for (u32 q = 0; q < 8; q++) sum[q] += k0 + q < NBK ? w[q + 1] - w[q] : 0;
-        }
-#pragma unroll
-        for (u32 q = 0; q < 8; q++) {
-            if (!sum[q]) continue;
-            const u32 was = atomicAdd(&P.leg_tot[k0 + q], sum[q]);
-            if (was < LEG_SPLIT_MIN && was + sum[q] >= LEG_SPLIT_MIN) atomicAdd(&P.leg_tot[NBK], 1u);
-        }
-    }
-}
-
 // Gather of one bucket's legs: consecutive legs of a segment go to consecutive lanes (coalesced
 // reads), Q legs per thread in flight before their LDS adds (a heavy, Zipf-hot bucket keeps more in
 // flight).  A thread's legs j only grow, so the prepare holding j is searched for only past the
@@ -95,7 +64,7 @@ __device__ static inline void tb_gather_legs(const PassArgs& P, u32 jb, u32 je, 
 __device__ static inline void tb_gather_range(const PassArgs& P, u32 jb, u32 je, u32 nb, const u32* s_start,
                                               const u32* s_pref, u64* s_acc, u64* s_red) {
     if (je - jb < APPLY_HEAVY) {
-        tb_gather_legs<8>(P, jb, je, nb, s_start, s_pref, s_acc);
+        tb_gather_legs<4>(P, jb, je, nb, s_start, s_pref, s_acc);
         __syncthreads();
         return;
     }
@@ -209,25 +178,12 @@ __device__ static inline void tb_apply_legs_body(const PassArgs& P, u64* s_acc) 
     const u32 per = (nb + APPLY_THREADS - 1) / APPLY_THREADS;
     const u32 p0 = min(nb, threadIdx.x * per), p1 = min(nb, p0 + per);
     u32 local = 0;
-    for (u32 pq = p0; pq < p1; pq += 4) {  // four prepares' loads in flight together
-        u32 a[4], z[4];
-        u64 o[4];
-#pragma unroll
-        for (u32 q = 0; q < 4; q++) {
-            const u32 p = pq + q;
-            const u32* row = P.leg_off + (u64)min(p, p1 - 1) * stride;
-            a[q] = row[g];
-            z[q] = row[g + 1];
-            o[q] = P.batch_off[P.b0 + min(p, p1 - 1)];
-        }
-#pragma unroll
-        for (u32 q = 0; q < 4; q++) {
-            const u32 p = pq + q;
-            if (p >= p1) break;
-            s_start[p] = (u32)(2 * (o[q] - P.e0)) + a[q];
-            s_pref[p] = z[q] - a[q];
-            local += z[q] - a[q];
-        }
+    for (u32 p = p0; p < p1; p++) {
+        const u32* row = P.leg_off + (u64)p * stride;
+        const u32 a = row[g], len = row[g + 1] - a;
+        s_start[p] = (u32)(2 * (P.batch_off[P.b0 + p] - P.e0)) + a;
+        s_pref[p] = len;
+        local += len;
     }
     u32 total;
     u32 run = tb_block_excl_sum(local, s_wave, &total);
@@ -243,22 +199,10 @@ __device__ static inline void tb_apply_legs_body(const PassArgs& P, u64* s_acc) 
     if (!extras) {
         tb_gather_range(P, 0, total, nb, s_start, s_pref, s_acc, s_red);
         // Write back: thread k -> (slot k/4, field k%4), consecutive threads on consecutive 16-B fields.
-        // Eight fields a thread at a time: their loads are in flight together before any store (one
-        // memory round trip per eight read-modify-writes instead of one each).
-        u64* __restrict__ bal = (u64*)(P.T.acct_bal + (u64)g * W);
-        for (u32 k0 = threadIdx.x; k0 < 4 * W; k0 += 8 * APPLY_THREADS) {
-            u64 v[8], old[8];
-#pragma unroll
-            for (u32 q = 0; q < 8; q++) {
-                const u32 k = k0 + q * APPLY_THREADS;
-                v[q] = k < 4 * W ? s_acc[k] : 0;
-                old[q] = v[q] ? bal[2 * (u64)k] : 0;
-            }
-#pragma unroll
-            for (u32 q = 0; q < 8; q++) {
-                const u32 k = k0 + q * APPLY_THREADS;
-                if (v[q]) bal[2 * (u64)k] = old[q] + v[q];  // low word: no carry under the certificate
-            }
+        u8* bal = (u8*)(P.T.acct_bal + (u64)g * W);
+        for (u32 k = threadIdx.x; k < 4 * W; k += APPLY_THREADS) {
+            const u64 v = s_acc[k];
+            if (v != 0) *(u64*)(bal + (u64)k * 16) += v;  // low word: no carry under the certificate
         }
         return;
     }

@@ -139,10 +139,15 @@ __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 L, 
     const u16* h = (const u16*)s_hist;
     const u32 nlegs = h[P.leg_buckets];
     u32* row = P.leg_off + (u64)blockIdx.x * (P.leg_buckets + 1);
-    // (The pass's legs per bucket, which tb_apply_legs needs to split a Zipf-heavy bucket, are summed
-    // over these rows by tb_leg_totals: one atomic per bucket from every prepare here contended on
-    // the same 2K words.)
-    for (u32 k = threadIdx.x; k <= P.leg_buckets; k += blockDim.x) row[k] = h[k];
+    for (u32 k = threadIdx.x; k <= P.leg_buckets; k += blockDim.x) {
+        row[k] = h[k];
+        // The pass's legs per bucket: tb_apply_legs splits a Zipf-heavy bucket over workgroups.
+        if (k < P.leg_buckets && h[k + 1] != h[k]) {
+            const u32 add = h[k + 1] - h[k];
+            const u32 was = atomicAdd(&P.leg_tot[k], add);
+            if (was < LEG_SPLIT_MIN && was + add >= LEG_SPLIT_MIN) atomicAdd(&P.leg_tot[P.leg_buckets], 1u);
+        }
+    }
     __syncthreads();  // the row is read before the starts advance as cursors
 #pragma unroll
     for (u32 k = 0; k < RESOLVE_K; k++) {

@@ -244,37 +244,31 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     else if (!(ts > dr.timestamp) || !(ts > cr.timestamp)) early = TB_CODE_PANIC;  // :817-818
     else if (dr.ledger != cr.ledger) early = CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
     else if (t.ledger != dr.ledger) early = CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
-    if (early != R_OK) {
-        // Every event past the stateless checks claims its id, whether or not its home entry was
-        // free: which same-pass events collide (and so which are dependent) is then a function of
-        // the input, not of the order the claims landed in (tests/harness/dependence.py).
-        if (x0 != 0 && x0 != ~0ULL) {
-            u32 es = TB_NOT_FOUND;
-            (void)tb_claim_id(P, t, pe, s, &es, x0);
-        }
-        return early;
-    }
-
-    // From here the event may end up ok: account for it in S and mark balancing accounts before
-    // the id check, so that a dependent (colliding) event is covered too.
     const bool balancing = (f & (TF_BAL_DEBIT | TF_BAL_CREDIT)) != 0;
-    s.contrib = balancing && t.amount == 0 ? (u128)UINT64_MAX : t.amount;
-    s.dr = drs;
-    s.cr = crs;
-    s.hz |= HZ_ACCTS;
-    if ((dr.flags | cr.flags) & AF_LIMITS) s.hz |= HZ_LIMIT;
-    if (balancing) {
-        // The amount depends on the running balance (:826-846): dependent, and so is every event
-        // touching the balanced account in this pass.
-        s.hz |= HZ_BAL;
-        if (f & TF_BAL_DEBIT) P.T.account_mark[drs] = P.epoch;
-        if (f & TF_BAL_CREDIT) P.T.account_mark[crs] = P.epoch;
-        P.pass_words[PW_BAL] = 1;
+    if (early == R_OK) {
+        // From here the event may end up ok: account for it in S and mark balancing accounts before
+        // the id check, so that a dependent (colliding) event is covered too.
+        s.contrib = balancing && t.amount == 0 ? (u128)UINT64_MAX : t.amount;
+        s.dr = drs;
+        s.cr = crs;
+        s.hz |= HZ_ACCTS;
+        if ((dr.flags | cr.flags) & AF_LIMITS) s.hz |= HZ_LIMIT;
+        if (balancing) {
+            // The amount depends on the running balance (:826-846): dependent, and so is every event
+            // touching the balanced account in this pass.
+            s.hz |= HZ_BAL;
+            if (f & TF_BAL_DEBIT) P.T.account_mark[drs] = P.epoch;
+            if (f & TF_BAL_CREDIT) P.T.account_mark[crs] = P.epoch;
+            P.pass_words[PW_BAL] = 1;
+        }
     }
-
-    // The existence check of `id` (:824) fused with the speculative claim of its index entry.
+    // The existence check of `id` (:824) fused with the speculative claim of its index entry.  An
+    // event that failed the account checks claims too (its home entry was claimed with the probes
+    // anyway): which same-pass events collide, and so which are dependent, is then a function of the
+    // input, not of the order the claims landed in (tests/harness/dependence.py).
     u32 es = TB_NOT_FOUND;
     const u32 claim = tb_claim_id(P, t, pe, s, &es, x0);
+    if (early != R_OK) return early;
     if (claim == CLAIM_EXISTS) return tb_transfer_exists(t, T.xlog[es]);
     if (claim == CLAIM_COLLIDED || balancing) return R_OK;  // dependent: the replay decides
 
@@ -300,7 +294,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
 
     const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
     const u32 count = min((u32)VALIDATE_THREADS, P.n - tile0);
-    tb_kclock_start(P, 0);
+    const u64 t_start = wall_clock64();  // the launch span's start (stamped at the end: no entry branch)
     tb_stage_tile<SRC>(P, tile0, count, stage, TB_ABL(P, EXP_NT));
 
     const u32 pe = tile0 + threadIdx.x;  // pass-relative event
@@ -385,7 +379,10 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
             total = tb_sat_add(total, tb_u128(*(const u64*)q, *(const u64*)(q + 8)));
         }
         tb_sum_publish(P, total);
-        if (P.kclock) tb_kclock_stamp_end(P.kclock + 1 + (blockIdx.x % KCLOCK_ENDS));
+        if (P.kclock) {
+            if (blockIdx.x < 8) atomicMin((unsigned long long*)P.kclock, (unsigned long long)t_start);
+            tb_kclock_stamp_end(P.kclock);
+        }
     }
 }
 

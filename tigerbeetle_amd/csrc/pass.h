@@ -87,7 +87,7 @@ struct PassArgs {
     u32 legs;              // 1: the legs path is enabled for this pass (the host checked the sizes)
     u32 apply_late;        // 1: no legs; tb_apply_events applies the independent ok transfers (small passes)
     u32 leg_shift;         // bucket of an account slot = slot >> leg_shift (2^leg_shift slots each)
-    u32* leg_tot;          // [leg_buckets + 1] legs per bucket in the pass (tb_leg_totals; zeroed by tb_pass_clear),
+    u32* leg_tot;          // [leg_buckets + 1] legs per bucket in the pass (tb_emit_legs; zeroed by tb_pass_clear),
                            // then the number of buckets that reached APPLY_SPLIT_MIN
     u32 leg_buckets;       // account_cap >> leg_shift
     u64* leg_ev;           // [2 * pass events] leg word of event pe's side s at 2*pe+s (event order)
@@ -99,30 +99,30 @@ struct PassArgs {
                            // validate, resolve and apply (device wall clock), set up by tb_pass_clear
 };
 
-// Launch span of a profiled kernel (tbgpu_stats.span_ms): every workgroup lowers the start word to
-// its own start and raises an end word to its own end; the host reads them after the pass.  The end
-// is sharded over KCLOCK_ENDS words (by workgroup) and both updates are skipped when they would not
-// change the word: the stamps cost a few atomics per launch, not one same-address atomic per
-// workgroup.
-#define KCLOCK_ENDS 32
-#define KCLOCK_STRIDE 64                  // per kernel: [0] start, [1 .. KCLOCK_ENDS] end shards
-#define KCLOCK_WORDS (3 * KCLOCK_STRIDE)  // per pass: kernel 0 validate, 1 resolve, 2 apply
-__device__ static inline void tb_kclock_stamp_start(u64* w) {
-    const u64 t = wall_clock64();
-    if (t < __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin((unsigned long long*)w, (unsigned long long)t);
-}
-__device__ static inline void tb_kclock_stamp_end(u64* w) {
-    const u64 t = wall_clock64();
-    if (t > __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax((unsigned long long*)w, (unsigned long long)t);
+// Launch span of a profiled kernel (tbgpu_stats.span_ms): the first workgroup of each XCD lowers the
+// start word to its start, and every workgroup raises one of KCLOCK_ENDS end words (one 128-B line
+// each, by workgroup) to its end; the host takes the maximum after the pass.  Both are no-return
+// atomics, so no wave waits on them, and no line takes more than a few hundred per launch (one
+// same-address atomic per workgroup, or a load that must return before the workgroup starts, slowed
+// validate by 13-40 %).
+#define KCLOCK_ENDS 16
+#define KCLOCK_LINE 16                                   // u64 words per 128-B line
+#define KCLOCK_STRIDE (KCLOCK_LINE * (1 + KCLOCK_ENDS))  // per kernel: [0] start, [(1 + q) * KCLOCK_LINE] end q
+#define KCLOCK_WORDS (3 * KCLOCK_STRIDE)                 // per pass: kernel 0 validate, 1 resolve, 2 apply
+__device__ static inline void tb_kclock_stamp_end(u64* kernel_words) {
+    atomicMax((unsigned long long*)(kernel_words + (1 + blockIdx.x % KCLOCK_ENDS) * KCLOCK_LINE),
+              (unsigned long long)wall_clock64());
 }
 __device__ static inline void tb_kclock_start(const PassArgs& P, u32 k) {
-    if (P.kclock && threadIdx.x == 0) tb_kclock_stamp_start(P.kclock + k * KCLOCK_STRIDE);
+    if (P.kclock && blockIdx.x < 8 && threadIdx.x == 0) {
+        atomicMin((unsigned long long*)(P.kclock + k * KCLOCK_STRIDE), (unsigned long long)wall_clock64());
+    }
 }
 // Every thread of the workgroup calls it (a barrier, then thread 0 stamps).
 __device__ static inline void tb_kclock_end(const PassArgs& P, u32 k) {
     if (!P.kclock) return;
     __syncthreads();
-    if (threadIdx.x == 0) tb_kclock_stamp_end(P.kclock + k * KCLOCK_STRIDE + 1 + (blockIdx.x % KCLOCK_ENDS));
+    if (threadIdx.x == 0) tb_kclock_stamp_end(P.kclock + k * KCLOCK_STRIDE);
 }
 
 enum : u32 { CERT_EXT_U128 = 1, CERT_EXT_U64 = 2 };
@@ -282,7 +282,9 @@ __global__ __launch_bounds__(256) void tb_pass_clear(u64* dedup, u64 cap, u64* s
                                                      u64 m2, u64* kclock) {
     const u64 w = g->dedup_dirty;  // before the stores (a load after them waits for them)
     if (blockIdx.x == 0 && threadIdx.x < SUM_WORDS) sum_shards[threadIdx.x] = 0;
-    if (kclock && blockIdx.x == 0 && threadIdx.x < KCLOCK_WORDS) kclock[threadIdx.x] = threadIdx.x % KCLOCK_STRIDE ? 0 : ~0ULL;
+    if (kclock && blockIdx.x == 0) {
+        for (u32 k = threadIdx.x; k < KCLOCK_WORDS; k += 256) kclock[k] = k % KCLOCK_STRIDE ? 0 : ~0ULL;
+    }
     if (meta && blockIdx.x == 0 && threadIdx.x == 0) {
         meta[0] = m0;
         meta[1] = m1;
