@@ -95,7 +95,7 @@ struct TbNode;  // node.h: the multi-device engine (tbgpu_config.device_count > 
 
 // Groove write-back buffers (tbgpu_checkpoint_delta / _async), every one allocated at tbgpu_init.
 #define WB_IDS_MAX (1ULL << 20)  // listed ids (creates, direct balance writes) between write-backs
-#define WB_OUT_GRID 128          // workgroups of the asynchronous copy-out (a PCIe stream, not the CUs)
+#define WB_OUT_GRID 64           // workgroups of the asynchronous copy-out (4 KB a step each: tb_delta_out)
 enum { WB_ACCOUNTS = 0, WB_SLOTS = 1, WB_PV = 2, WB_RECORDS = 3, WB_STATUS = 4, WB_ORDER = 5, WB_COUNT_WORDS = 8 };
 struct WbBufs {
     u64 cap_t = 0;    // log positions per slice
@@ -112,6 +112,7 @@ struct WbBufs {
     AccountBal* d_before = nullptr;
     u32* d_slots = nullptr;       // [account_cap] every slot one write-back covers
     u64* d_cnt = nullptr;         // [WB_COUNT_WORDS] WB_* counters
+    u32* d_gate = nullptr;        // PassArgs.pcie_gate while a copy-out is in flight
     u64* h_cnt = nullptr;         // pinned mirror
     hipStream_t stream = nullptr; // the asynchronous copy-out
     hipEvent_t gathered = nullptr, done = nullptr;
@@ -696,6 +697,8 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         INIT_CK(tbMalloc(&W.d_before, W.cap_a * sizeof(AccountBal)));
         INIT_CK(tbMalloc(&W.d_slots, E->account_cap * 4));
         INIT_CK(tbMalloc(&W.d_cnt, WB_COUNT_WORDS * 8));
+        INIT_CK(tbMalloc(&W.d_gate, 4));
+        INIT_CK(hipMemset(W.d_gate, 0, 4));
         INIT_CK(tbHostMalloc(&W.h_cnt, WB_COUNT_WORDS * 8, hipHostMallocDefault));
         INIT_CK(hipStreamCreateWithFlags(&W.stream, hipStreamNonBlocking));
         INIT_CK(tbEventCreateWithFlags(&W.gathered, hipEventDisableTiming));
@@ -735,7 +738,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
                     E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->pf_staging, E->kclock, E->r_home,
                     E->wb.d_bc, E->wb.d_base, E->wb.d_out, E->wb.d_ids, E->wb.d_pv, E->wb.d_pairs, E->wb.d_hids,
-                    E->wb.d_acc, E->wb.d_before, E->wb.d_slots, E->wb.d_cnt,
+                    E->wb.d_acc, E->wb.d_before, E->wb.d_slots, E->wb.d_cnt, E->wb.d_gate,
                     E->r_block_counts, E->r_words, E->r_meta, E->leg_ev, E->leg_w, E->leg_off, E->leg_tot,
                     E->F.f_pe, E->F.f_batch, E->F.f_len, E->F.need, E->F.nsucc, E->F.queue, E->F.uflags, E->F.nacct, E->F.rpos, E->F.succ,
                     E->F.run, E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo,
@@ -780,6 +783,7 @@ extern "C" int tbgpu_reset(tbgpu_t* E) {
         HIPCK(hipStreamSynchronize(E->wb.stream));
         E->wb.inflight = false;
     }
+    if (E->wb.d_gate) HIPCK(hipMemset(E->wb.d_gate, 0, 4));
     E->ckpt_valid = false;
     E->ckpt_scan = false;
     std::vector<u64>().swap(E->ckpt_ids);
@@ -877,6 +881,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.flow_words = E->flow_ok ? E->F.words : nullptr;
 
         // Launch spans of this pass's kernels on the device clock (profiling only).
+        P.pcie_gate = E->wb.inflight ? E->wb.d_gate : nullptr;  // a copy-out may be streaming to the host
         P.kclock = nullptr;
         if (E->profile && !E->kclock_off && (E->prof_mask & ((1u << K_VALIDATE) | (1u << K_RESOLVE) | (1u << K_APPLY))) &&
             E->kclock_next < KCLOCK_SLOTS) {
@@ -899,7 +904,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         hipLaunchKernelGGL(tb_pass_clear, dim3(clear_grid), dim3(256), 0, E->stream, E->dedup, E->dedup_cap, E->sum_shards,
                            E->g, E->epoch, E->dedup_force ? 1u : 0u, E->leg_tot, E->leg_buckets, meta_dst,
                            inline_meta ? inline_meta[0] : 0, inline_meta ? inline_meta[1] : 0, inline_meta ? inline_meta[2] : 0,
-                           P.kclock);
+                           P.kclock, P.pcie_gate);
         HIPCK(hipGetLastError());
         E->dedup_force = false;
         E->dedup_prev = P.dedup_mask + 1;
@@ -1783,10 +1788,14 @@ static int wb_checkpoint_sync(tbgpu* E, u8* accounts_out, u8* before_out, u64 ac
     if ((st = wb_next_epoch(E))) return st;
     HIPCK(hipMemsetAsync(E->wb.d_cnt, 0, WB_COUNT_WORDS * 8, E->stream));
     u64 nt = 0, npv = 0, na = 0;
-    for (u64 a = E->ckpt_pos; a < E->log_next; a += E->wb.cap_t) {
+    u32 slices = 0;
+    for (u64 a = E->ckpt_pos; a < E->log_next; a += E->wb.cap_t, slices++) {
         const u64 b = std::min<u64>(E->log_next, a + E->wb.cap_t);
         if ((st = wb_gather_slice(E, a, b, true))) return st;
         if ((st = wb_ids(E, E->wb.d_ids, 2 * (b - a), E->wb.d_cnt + WB_RECORDS))) return st;
+        hipLaunchKernelGGL(tb_delta_order, dim3(256), dim3(256), 0, E->stream, E->wb.d_out, E->wb.d_cnt + WB_RECORDS,
+                           E->wb.d_pairs, E->wb.d_cnt + WB_PV, E->wb.d_cnt + WB_ORDER);
+        HIPCK(hipGetLastError());
         if ((st = wb_read_counts(E))) return st;
         const u64* c = E->wb.h_cnt;
         if (c[WB_RECORDS]) HIPCK(hipMemcpyAsync(transfers_out + nt * 128, E->wb.d_out, c[WB_RECORDS] * 128,
@@ -1801,8 +1810,10 @@ static int wb_checkpoint_sync(tbgpu* E, u8* accounts_out, u8* before_out, u64 ac
     if ((st = wb_scan(E, 0, 0, accounts_out, before_out, &na))) return st;
     if ((st = wb_advance(E))) return st;
     HIPCK(hipStreamSynchronize(E->stream));
-    delta_sort_by_timestamp(transfers_out, nt);
-    delta_sort_pairs(posted_out, npv);
+    // Sorted on the device's word (tb_delta_order: within each slice; across slices the host looks).
+    const u64 order = E->wb.h_cnt[WB_ORDER];
+    if ((order & 1) || slices > 1) delta_sort_by_timestamp(transfers_out, nt);
+    if ((order & 2) || slices > 1) delta_sort_pairs(posted_out, npv);
     counts->accounts = na;
     counts->transfers = nt;
     counts->posted = npv;
@@ -1909,6 +1920,8 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
     O.count[3] = W.d_cnt + WB_PV;
     O.elem[3] = 16;
     O.order = W.d_cnt + WB_ORDER;
+    O.gate = W.d_gate;
+    O.gate_wait_max = 2 * E->wall_khz;  // 2 ms
     hipLaunchKernelGGL(tb_delta_out, dim3(WB_OUT_GRID), dim3(256), 0, W.stream, O);
     HIPCK(hipGetLastError());
     HIPCK(hipMemcpyAsync(W.h_cnt + WB_ORDER, W.d_cnt + WB_ORDER, 8, hipMemcpyDeviceToHost, W.stream));

@@ -212,23 +212,46 @@ __global__ void tb_delta_posted(Tables T, const u64* pv, const u64* npv, u64* pa
 // > ts0) or when its balances differ from the snapshot; `slots` lists every slot seen, for the
 // snapshot's advance.  n_dev (optional): the id count is 2 x *n_dev (the new transfers' two accounts,
 // counted on the device), n is then only the grid's bound.
+// A wave's lanes with `take` set get consecutive positions from one atomic on *count (one per wave,
+// not one per lane: every lane of the write-back otherwise adds to the same two words).
+__device__ static inline u64 tb_wave_claim(bool take, u64* count) {
+    const u64 m = __ballot(take);
+    if (!m) return 0;
+    const u32 lane = threadIdx.x & 63;
+    const u32 leader = __ffsll((long long)m) - 1;
+    u64 base = 0;
+    if (lane == leader) base = atomicAdd((unsigned long long*)count, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader);
+    return base + __popcll(m & ((1ULL << lane) - 1));
+}
+
 __global__ void tb_delta_ids(Tables T, const AccountBal* snap, u64 ts0, const u64* ids, u64 n, u32* mark, u32 epoch,
                              u8* out, AccountBal* before, u64* count, u32* slots, u64* slot_count,
                              const u64* n_dev = nullptr) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || (n_dev && i >= 2 * *n_dev)) return;
-    const u32 slot = tb_account_find(T, ids[2 * i], ids[2 * i + 1]);
-    if (slot == TB_NOT_FOUND) return;
-    if (atomicExch(&mark[slot], epoch) == epoch) return;  // another copy of the id took it
-    slots[atomicAdd((unsigned long long*)slot_count, 1ULL)] = slot;
-    const AccountHot& h = T.acct_hot[slot];
-    const AccountBal b = T.acct_bal[slot], s = snap[slot];
-    const bool same = b.debits_pending == s.debits_pending && b.debits_posted == s.debits_posted &&
-                      b.credits_pending == s.credits_pending && b.credits_posted == s.credits_posted;
-    if (h.timestamp <= ts0 && same) return;
-    const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
-    *(Account*)(out + k * 128) = tb_account_load(T, slot);
-    before[k] = h.timestamp <= ts0 ? s : AccountBal{0, 0, 0, 0};
+    const bool live = i < n && !(n_dev && i >= 2 * *n_dev);
+    u32 slot = TB_NOT_FOUND;
+    if (live) slot = tb_account_find(T, ids[2 * i], ids[2 * i + 1]);
+    // The first copy of an id takes its slot (a later one finds this write-back's epoch there).
+    const bool first = slot != TB_NOT_FOUND && atomicExch(&mark[slot], epoch) != epoch;
+    bool emit = false;
+    AccountBal s{};
+    u64 hts = 0;
+    if (first) {
+        hts = T.acct_hot[slot].timestamp;
+        const AccountBal b = T.acct_bal[slot];
+        s = snap[slot];
+        const bool same = b.debits_pending == s.debits_pending && b.debits_posted == s.debits_posted &&
+                          b.credits_pending == s.credits_pending && b.credits_posted == s.credits_posted;
+        emit = hts > ts0 || !same;
+    }
+    const u64 si = tb_wave_claim(first, slot_count);
+    if (first) slots[si] = slot;
+    const u64 k = tb_wave_claim(emit, count);
+    if (emit) {
+        *(Account*)(out + k * 128) = tb_account_load(T, slot);
+        before[k] = hts <= ts0 ? s : AccountBal{0, 0, 0, 0};
+    }
 }
 
 // The snapshot follows the slots a write-back covered (*n of them), grid-stride.
@@ -247,35 +270,67 @@ __global__ void tb_delta_advance(Tables T, AccountBal* snap, const u32* slots, c
 // gets bit 0 when a record's timestamp does not exceed its predecessor's (records appended by an
 // upsert or a load), bit 1 when a pair is below its predecessor — the host sorts only then, instead
 // of reading every record back to find out.
+// Order of the gathered records (bit 0 of *order: a timestamp not above its predecessor's) and
+// posted pairs (bit 1: a pair below its predecessor), grid-stride; the host sorts only when set.
+__device__ static inline void tb_delta_order_check(const u8* recs, u64 nt, const u64* pairs, u64 np, u64* order) {
+    const u64 stride = (u64)gridDim.x * blockDim.x;
+    bool unsorted_t = false, unsorted_p = false;
+    for (u64 i = 1 + (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nt; i += stride) {
+        const u64* t = (const u64*)(recs + i * 128 + 120);
+        unsorted_t |= t[-16] >= t[0];  // the previous record's timestamp
+    }
+    for (u64 i = 1 + (u64)blockIdx.x * blockDim.x + threadIdx.x; pairs && i < np; i += stride) {
+        const u64* q = pairs + 2 * i;
+        unsorted_p |= q[-2] > q[0] || (q[-2] == q[0] && q[-1] > q[1]);
+    }
+    const u64 flags = (__ballot(unsorted_t) ? 1 : 0) | (__ballot(unsorted_p) ? 2 : 0);
+    if ((threadIdx.x & 63) == 0 && flags) atomicOr((unsigned long long*)order, (unsigned long long)flags);
+}
+
 struct DeltaOut {
     const u8* src[4];
     u8* dst[4];
     const u64* count[4];  // elements of each region
     u32 elem[4];          // bytes per element
     u64* order;
+    const u32* gate;      // set while a commit reads its body over PCIe (PassArgs.pcie_gate)
+    u64 gate_wait_max;    // device-clock ticks a workgroup waits on the gate at most (then goes on)
 };
+// Posted writes to host memory and the device's read requests share the link's device-to-host
+// direction, and a read may not pass the writes queued before it: a copy-out streaming 100+ MB
+// beside a one-prepare commit held that commit's read-through for milliseconds.  So the copy-out is
+// 4 KB per workgroup step (a few hundred KB in flight across the grid, microseconds to drain) and
+// waits, between steps, while a commit holds the gate.  The gate only orders traffic: past
+// gate_wait_max a workgroup goes on regardless.
 __global__ __launch_bounds__(256) void tb_delta_out(DeltaOut A) {
     const u64 stride = (u64)gridDim.x * 256;
-#pragma unroll
     for (u32 r = 0; r < 4; r++) {
         if (!A.src[r]) continue;
         const u64 chunks = *A.count[r] * A.elem[r] / 16;
         const u32x4* in = (const u32x4*)A.src[r];
         u32x4* out = (u32x4*)A.dst[r];
-        for (u64 c = (u64)blockIdx.x * 256 + threadIdx.x; c < chunks; c += stride) out[c] = in[c];
+        for (u64 c0 = (u64)blockIdx.x * 256; c0 < chunks; c0 += stride) {
+            if (A.gate) {
+                if (threadIdx.x == 0) {
+                    const u64 t0 = wall_clock64();
+                    while (__hip_atomic_load(A.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
+                           wall_clock64() - t0 < A.gate_wait_max) {
+                        __builtin_amdgcn_s_sleep(4);
+                    }
+                }
+                __syncthreads();  // the workgroup's step waits for thread 0's poll
+            }
+            const u64 c = c0 + threadIdx.x;
+            if (c < chunks) out[c] = in[c];
+        }
     }
-    bool unsorted_t = false, unsorted_p = false;
-    const u64 nt = *A.count[0], np = *A.count[3];
-    for (u64 i = 1 + (u64)blockIdx.x * 256 + threadIdx.x; i < nt; i += stride) {
-        const u64* t = (const u64*)(A.src[0] + i * 128 + 120);
-        unsorted_t |= t[-16] >= t[0];  // the previous record's timestamp
-    }
-    for (u64 i = 1 + (u64)blockIdx.x * 256 + threadIdx.x; i < np; i += stride) {
-        const u64* q = (const u64*)A.src[3] + 2 * i;
-        unsorted_p |= q[-2] > q[0] || (q[-2] == q[0] && q[-1] > q[1]);
-    }
-    const u64 flags = (__ballot(unsorted_t) ? 1 : 0) | (__ballot(unsorted_p) ? 2 : 0);
-    if ((threadIdx.x & 63) == 0 && flags) atomicOr((unsigned long long*)A.order, (unsigned long long)flags);
+    tb_delta_order_check(A.src[0], *A.count[0], (const u64*)A.src[3], *A.count[3], A.order);
+}
+
+// The same order check for the synchronous write-back (on one slice's gathered records and pairs).
+__global__ __launch_bounds__(256) void tb_delta_order(const u8* recs, const u64* nt, const u64* pairs, const u64* np,
+                                                      u64* order) {
+    tb_delta_order_check(recs, *nt, pairs, *np, order);
 }
 
 // ---- pipelined host commits (tbgpu_commit_pipelined) -------------------------------------------
