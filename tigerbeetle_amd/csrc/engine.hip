@@ -95,7 +95,6 @@ struct TbNode;  // node.h: the multi-device engine (tbgpu_config.device_count > 
 
 // Groove write-back buffers (tbgpu_checkpoint_delta / _async), every one allocated at tbgpu_init.
 #define WB_IDS_MAX (1ULL << 20)  // listed ids (creates, direct balance writes) between write-backs
-#define WB_OUT_GRID 64           // workgroups of the asynchronous copy-out (4 KB a step each: tb_delta_out)
 enum { WB_ACCOUNTS = 0, WB_SLOTS = 1, WB_PV = 2, WB_RECORDS = 3, WB_STATUS = 4, WB_ORDER = 5, WB_COUNT_WORDS = 8 };
 struct WbBufs {
     u64 cap_t = 0;    // log positions per slice
@@ -112,11 +111,18 @@ struct WbBufs {
     AccountBal* d_before = nullptr;
     u32* d_slots = nullptr;       // [account_cap] every slot one write-back covers
     u64* d_cnt = nullptr;         // [WB_COUNT_WORDS] WB_* counters
-    u32* d_gate = nullptr;        // PassArgs.pcie_gate while a copy-out is in flight
     u64* h_cnt = nullptr;         // pinned mirror
-    hipStream_t stream = nullptr; // the asynchronous copy-out
+    hipStream_t stream = nullptr; // the asynchronous copy-out (DMA engine)
     hipEvent_t gathered = nullptr, done = nullptr;
+    hipEvent_t read_done = nullptr;  // on the engine stream after a commit's validate (its PCIe reads)
     bool inflight = false;
+    // The copy-out in flight: regions (records, accounts, before, pairs) from HBM to the caller's
+    // registered buffers, sent a slice per commit (wb_pump) once the gather's counts are known.
+    bool copying = false, counts_known = false;
+    const u8* src[4] = {};
+    u8* dst[4] = {};
+    u64 len[4] = {}, at[4] = {};
+    u64 slice = 0;
     tbgpu_delta_counts counts{};
     u8* out_t = nullptr;          // the in-flight write-back's caller buffers (sorted by the wait)
     u64* out_p = nullptr;
@@ -697,12 +703,11 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         INIT_CK(tbMalloc(&W.d_before, W.cap_a * sizeof(AccountBal)));
         INIT_CK(tbMalloc(&W.d_slots, E->account_cap * 4));
         INIT_CK(tbMalloc(&W.d_cnt, WB_COUNT_WORDS * 8));
-        INIT_CK(tbMalloc(&W.d_gate, 4));
-        INIT_CK(hipMemset(W.d_gate, 0, 4));
         INIT_CK(tbHostMalloc(&W.h_cnt, WB_COUNT_WORDS * 8, hipHostMallocDefault));
         INIT_CK(hipStreamCreateWithFlags(&W.stream, hipStreamNonBlocking));
         INIT_CK(tbEventCreateWithFlags(&W.gathered, hipEventDisableTiming));
         INIT_CK(tbEventCreateWithFlags(&W.done, hipEventDisableTiming));
+        INIT_CK(tbEventCreateWithFlags(&W.read_done, hipEventDisableTiming));
     }
     INIT_CK(tbMalloc(&E->kclock, (u64)KCLOCK_SLOTS * KCLOCK_WORDS * 8));
     INIT_CK(tbHostMalloc(&E->h_kclock, (u64)KCLOCK_SLOTS * KCLOCK_WORDS * 8, hipHostMallocDefault));
@@ -738,7 +743,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
                     E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->pf_staging, E->kclock, E->r_home,
                     E->wb.d_bc, E->wb.d_base, E->wb.d_out, E->wb.d_ids, E->wb.d_pv, E->wb.d_pairs, E->wb.d_hids,
-                    E->wb.d_acc, E->wb.d_before, E->wb.d_slots, E->wb.d_cnt, E->wb.d_gate,
+                    E->wb.d_acc, E->wb.d_before, E->wb.d_slots, E->wb.d_cnt,
                     E->r_block_counts, E->r_words, E->r_meta, E->leg_ev, E->leg_w, E->leg_off, E->leg_tot,
                     E->F.f_pe, E->F.f_batch, E->F.f_len, E->F.need, E->F.nsucc, E->F.queue, E->F.uflags, E->F.nacct, E->F.rpos, E->F.succ,
                     E->F.run, E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo,
@@ -767,6 +772,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
     }
     if (E->wb.gathered) (void)hipEventDestroy(E->wb.gathered);
     if (E->wb.done) (void)hipEventDestroy(E->wb.done);
+    if (E->wb.read_done) (void)hipEventDestroy(E->wb.read_done);
     for (hipEvent_t e : E->event_pool) (void)hipEventDestroy(e);
     if (E->pf_done) (void)hipEventDestroy(E->pf_done);
     for (int i = 0; i < 16; i++) if (E->markers[i]) (void)hipEventDestroy(E->markers[i]);
@@ -780,10 +786,10 @@ extern "C" int tbgpu_reset(tbgpu_t* E) {
     E->poisoned = false;
     HIPCK(hipSetDevice(E->device));
     if (E->wb.inflight) {  // its copy-out finishes; its results are dropped with the state
+        HIPCK(hipStreamSynchronize(E->stream));  // its gather
         HIPCK(hipStreamSynchronize(E->wb.stream));
-        E->wb.inflight = false;
+        E->wb.inflight = E->wb.copying = E->wb.counts_known = false;
     }
-    if (E->wb.d_gate) HIPCK(hipMemset(E->wb.d_gate, 0, 4));
     E->ckpt_valid = false;
     E->ckpt_scan = false;
     std::vector<u64>().swap(E->ckpt_ids);
@@ -881,7 +887,6 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.flow_words = E->flow_ok ? E->F.words : nullptr;
 
         // Launch spans of this pass's kernels on the device clock (profiling only).
-        P.pcie_gate = E->wb.inflight ? E->wb.d_gate : nullptr;  // a copy-out may be streaming to the host
         P.kclock = nullptr;
         if (E->profile && !E->kclock_off && (E->prof_mask & ((1u << K_VALIDATE) | (1u << K_RESOLVE) | (1u << K_APPLY))) &&
             E->kclock_next < KCLOCK_SLOTS) {
@@ -904,7 +909,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         hipLaunchKernelGGL(tb_pass_clear, dim3(clear_grid), dim3(256), 0, E->stream, E->dedup, E->dedup_cap, E->sum_shards,
                            E->g, E->epoch, E->dedup_force ? 1u : 0u, E->leg_tot, E->leg_buckets, meta_dst,
                            inline_meta ? inline_meta[0] : 0, inline_meta ? inline_meta[1] : 0, inline_meta ? inline_meta[2] : 0,
-                           P.kclock, P.pcie_gate);
+                           P.kclock);
         HIPCK(hipGetLastError());
         E->dedup_force = false;
         E->dedup_prev = P.dedup_mask + 1;
@@ -927,6 +932,8 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
                 }
             }
             HIPCK(hipGetLastError());
+            // A write-back's copy-out slice may follow this pass's PCIe reads (wb_pump).
+            if (E->wb.copying) HIPCK(hipEventRecord(E->wb.read_done, E->stream));
             if ((st = prof_end(E, &pp))) return st;
         }
         if ((st = prof_begin(E, &pp, K_RESOLVE))) return st;
@@ -1057,6 +1064,8 @@ static int commit_lookup(tbgpu* E, bool accounts, const void* input, uint32_t in
     return TBGPU_STATUS_OK;
 }
 
+static int wb_pump(tbgpu* E, u64 budget, hipEvent_t after);  // the write-back's copy-out (below)
+
 static int commit_host(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const void* const* inputs,
                        const uint32_t* input_lens, void* const* outputs, uint32_t* out_lens, const uint32_t* out_caps) {
     const void* claim = E->pf_claim;  // the staged body tbgpu_commit handed over (or null), taken once
@@ -1118,6 +1127,7 @@ static int commit_host(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const
             hipLaunchKernelGGL(tb_reply_out, dim3(1), dim3(64), 0, E->stream, E->meta, 1u, E->reply_bytes, E->results, E->g,
                                S.d_reply, (u32*)(S.d_reply + pipe_reply_bytes(E)), seq);
             HIPCK(hipGetLastError());
+            if ((st = wb_pump(E, 0, E->wb.read_done))) return st;  // one slice of a write-back in flight
             if (!E->profile) {
                 const auto t0 = std::chrono::steady_clock::now();
                 for (u32 spin = 0; *done != seq; spin++) {
@@ -1755,6 +1765,10 @@ static void delta_sort_pairs(u64* pairs, u64 n) {
 static int wb_wait(tbgpu* E, tbgpu_delta_counts* counts) {
     WbBufs& W = E->wb;
     if (!W.inflight) return fail(TBGPU_STATUS_INVALID, "no asynchronous write-back in flight");
+    if (W.copying) {  // what the commits since did not send yet
+        const int st = wb_pump(E, ~0ULL, nullptr);
+        if (st) return st;
+    }
     W.inflight = false;
     HIPCK(hipEventSynchronize(W.done));
     *counts = W.counts;
@@ -1765,7 +1779,7 @@ static int wb_wait(tbgpu* E, tbgpu_delta_counts* counts) {
         E->poisoned = true;
         return fail(TBGPU_STATUS_PANIC, "checkpoint delta: a posted pending transfer is missing");
     }
-    // Only when tb_delta_out saw them out of order (the synchronous path's outputs are sorted).
+    // Only when tb_delta_order saw them out of order (the synchronous path's outputs are sorted).
     if (W.out_t && (W.h_cnt[WB_ORDER] & 1)) delta_sort_by_timestamp(W.out_t, counts->transfers);
     if (W.out_p && (W.h_cnt[WB_ORDER] & 2)) delta_sort_pairs(W.out_p, counts->posted);
     return TBGPU_STATUS_OK;
@@ -1899,34 +1913,68 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
         if ((st = wb_ids(E, W.d_hids, nl, nullptr))) return st;
     }
     if ((st = wb_advance(E))) return st;
+    hipLaunchKernelGGL(tb_delta_order, dim3(256), dim3(256), 0, E->stream, W.d_out, W.d_cnt + WB_RECORDS, W.d_pairs,
+                       W.d_cnt + WB_PV, W.d_cnt + WB_ORDER);
+    HIPCK(hipGetLastError());
     HIPCK(hipMemcpyAsync(W.h_cnt, W.d_cnt, WB_COUNT_WORDS * 8, hipMemcpyDeviceToHost, E->stream));
     HIPCK(hipEventRecord(W.gathered, E->stream));
-    HIPCK(hipStreamWaitEvent(W.stream, W.gathered, 0));
-    DeltaOut O{};
-    O.src[0] = W.d_out;
-    O.dst[0] = m_t;
-    O.count[0] = W.d_cnt + WB_RECORDS;
-    O.elem[0] = 128;
-    O.src[1] = W.d_acc;
-    O.dst[1] = m_acc;
-    O.count[1] = W.d_cnt + WB_ACCOUNTS;
-    O.elem[1] = 128;
-    O.src[2] = m_before ? (const u8*)W.d_before : nullptr;
-    O.dst[2] = m_before;
-    O.count[2] = W.d_cnt + WB_ACCOUNTS;
-    O.elem[2] = sizeof(AccountBal);
-    O.src[3] = (const u8*)W.d_pairs;
-    O.dst[3] = m_p;
-    O.count[3] = W.d_cnt + WB_PV;
-    O.elem[3] = 16;
-    O.order = W.d_cnt + WB_ORDER;
-    O.gate = W.d_gate;
-    O.gate_wait_max = 2 * E->wall_khz;  // 2 ms
-    hipLaunchKernelGGL(tb_delta_out, dim3(WB_OUT_GRID), dim3(256), 0, W.stream, O);
-    HIPCK(hipGetLastError());
-    HIPCK(hipMemcpyAsync(W.h_cnt + WB_ORDER, W.d_cnt + WB_ORDER, 8, hipMemcpyDeviceToHost, W.stream));
-    HIPCK(hipEventRecord(W.done, W.stream));
+    W.src[0] = W.d_out;
+    W.dst[0] = (u8*)transfers_out;
+    W.src[1] = W.d_acc;
+    W.dst[1] = (u8*)accounts_out;
+    W.src[2] = accounts_before_out ? (const u8*)W.d_before : nullptr;
+    W.dst[2] = (u8*)accounts_before_out;
+    W.src[3] = (const u8*)W.d_pairs;
+    W.dst[3] = (u8*)posted_out;
+    W.copying = true;
+    W.counts_known = false;
     W.inflight = true;
+    return TBGPU_STATUS_OK;
+}
+
+// The copy-out of an asynchronous write-back, a slice at a time (up to `budget` bytes; ~0: all of
+// it), by the DMA engine on the write-back stream — after `after` (when given) on the engine stream.
+// A device-initiated read from host memory may not pass the posted writes queued before it on the
+// link, so a copy-out streaming 100+ MB beside a one-prepare commit held that commit's body read for
+// milliseconds, and a copy kernel's host writes also crowded the L2 every other kernel shares.  So
+// each commit sends one slice after its validate has read the body (the slice then overlaps its
+// resolve, apply, flow and reply and the host's turn), sized to spread the bar's objects over about
+// WB_SLICE_CALLS commits.  The sizes come from the gather's counts, known once it completed.
+#define WB_SLICE_CALLS 56
+static int wb_pump(tbgpu* E, u64 budget, hipEvent_t after) {
+    WbBufs& W = E->wb;
+    if (!W.copying) return TBGPU_STATUS_OK;
+    if (!W.counts_known) {
+        if (budget != ~0ULL && hipEventQuery(W.gathered) != hipSuccess) return TBGPU_STATUS_OK;  // next call
+        HIPCK(hipEventSynchronize(W.gathered));
+        const u64 na = W.h_cnt[WB_ACCOUNTS];
+        W.len[0] = W.h_cnt[WB_RECORDS] * 128;
+        W.len[1] = na * 128;
+        W.len[2] = W.src[2] ? na * sizeof(AccountBal) : 0;
+        W.len[3] = W.h_cnt[WB_PV] * 16;
+        u64 total = 0;
+        for (u32 r = 0; r < 4; r++) {
+            W.at[r] = 0;
+            total += W.len[r];
+        }
+        W.slice = std::max<u64>(512 << 10, (total / WB_SLICE_CALLS + 65535) & ~65535ULL);
+        W.counts_known = true;
+    }
+    if (budget != ~0ULL) budget = W.slice;
+    if (after) HIPCK(hipStreamWaitEvent(W.stream, after, 0));
+    for (u32 r = 0; r < 4 && budget; r++) {
+        const u64 n = std::min<u64>(budget, W.len[r] - W.at[r]);
+        if (!n) continue;
+        HIPCK(hipMemcpyAsync(W.dst[r] + W.at[r], W.src[r] + W.at[r], n, hipMemcpyDeviceToHost, W.stream));
+        W.at[r] += n;
+        budget -= n;
+    }
+    bool left = false;
+    for (u32 r = 0; r < 4; r++) left |= W.at[r] < W.len[r];
+    if (!left) {
+        HIPCK(hipEventRecord(W.done, W.stream));
+        W.copying = false;
+    }
     return TBGPU_STATUS_OK;
 }
 

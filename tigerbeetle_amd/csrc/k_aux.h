@@ -262,16 +262,10 @@ __global__ void tb_delta_advance(Tables T, AccountBal* snap, const u32* slots, c
     }
 }
 
-// The asynchronous write-back's copy-out (tbgpu_checkpoint_delta_async): the gathered objects, from
-// HBM into the caller's registered host buffers (their device mappings), each region as long as its
-// device-side count says — so no host round trip has to learn the sizes first.  Runs on its own
-// stream, beside the next commits; 16-B stores, consecutive lanes on consecutive chunks.
-// Regions 0 (transfer records) and 3 (posted pairs) are also checked for order on the way: `order`
-// gets bit 0 when a record's timestamp does not exceed its predecessor's (records appended by an
-// upsert or a load), bit 1 when a pair is below its predecessor — the host sorts only then, instead
-// of reading every record back to find out.
 // Order of the gathered records (bit 0 of *order: a timestamp not above its predecessor's) and
-// posted pairs (bit 1: a pair below its predecessor), grid-stride; the host sorts only when set.
+// posted pairs (bit 1: a pair below its predecessor), grid-stride; the host sorts only when set,
+// instead of reading every record back to find out (records appended by an upsert or a load may
+// sit out of timestamp order in the log).
 __device__ static inline void tb_delta_order_check(const u8* recs, u64 nt, const u64* pairs, u64 np, u64* order) {
     const u64 stride = (u64)gridDim.x * blockDim.x;
     bool unsorted_t = false, unsorted_p = false;
@@ -287,47 +281,8 @@ __device__ static inline void tb_delta_order_check(const u8* recs, u64 nt, const
     if ((threadIdx.x & 63) == 0 && flags) atomicOr((unsigned long long*)order, (unsigned long long)flags);
 }
 
-struct DeltaOut {
-    const u8* src[4];
-    u8* dst[4];
-    const u64* count[4];  // elements of each region
-    u32 elem[4];          // bytes per element
-    u64* order;
-    const u32* gate;      // set while a commit reads its body over PCIe (PassArgs.pcie_gate)
-    u64 gate_wait_max;    // device-clock ticks a workgroup waits on the gate at most (then goes on)
-};
-// Posted writes to host memory and the device's read requests share the link's device-to-host
-// direction, and a read may not pass the writes queued before it: a copy-out streaming 100+ MB
-// beside a one-prepare commit held that commit's read-through for milliseconds.  So the copy-out is
-// 4 KB per workgroup step (a few hundred KB in flight across the grid, microseconds to drain) and
-// waits, between steps, while a commit holds the gate.  The gate only orders traffic: past
-// gate_wait_max a workgroup goes on regardless.
-__global__ __launch_bounds__(256) void tb_delta_out(DeltaOut A) {
-    const u64 stride = (u64)gridDim.x * 256;
-    for (u32 r = 0; r < 4; r++) {
-        if (!A.src[r]) continue;
-        const u64 chunks = *A.count[r] * A.elem[r] / 16;
-        const u32x4* in = (const u32x4*)A.src[r];
-        u32x4* out = (u32x4*)A.dst[r];
-        for (u64 c0 = (u64)blockIdx.x * 256; c0 < chunks; c0 += stride) {
-            if (A.gate) {
-                if (threadIdx.x == 0) {
-                    const u64 t0 = wall_clock64();
-                    while (__hip_atomic_load(A.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
-                           wall_clock64() - t0 < A.gate_wait_max) {
-                        __builtin_amdgcn_s_sleep(4);
-                    }
-                }
-                __syncthreads();  // the workgroup's step waits for thread 0's poll
-            }
-            const u64 c = c0 + threadIdx.x;
-            if (c < chunks) out[c] = in[c];
-        }
-    }
-    tb_delta_order_check(A.src[0], *A.count[0], (const u64*)A.src[3], *A.count[3], A.order);
-}
-
-// The same order check for the synchronous write-back (on one slice's gathered records and pairs).
+// The order check of a write-back's gathered records and pairs (one slice of them), on the engine
+// stream after the gather.
 __global__ __launch_bounds__(256) void tb_delta_order(const u8* recs, const u64* nt, const u64* pairs, const u64* np,
                                                       u64* order) {
     tb_delta_order_check(recs, *nt, pairs, *np, order);

@@ -249,9 +249,6 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     const u32 L = (u32)(P.batch_off[b + 1] - boff);
     const u32 pbase = (u32)(boff - P.e0);
     tb_kclock_start(P, 1);
-    // The pass's PCIe reads (the body's read-through in validate) are done: the write-back's copy-out
-    // may go on.
-    if (P.pcie_gate && blockIdx.x == 0 && threadIdx.x == 0) *P.pcie_gate = 0;
 
     u128 S = 0;
     bool cert_global = true, cert64 = true;

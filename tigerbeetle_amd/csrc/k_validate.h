@@ -294,7 +294,9 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
 
     const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
     const u32 count = min((u32)VALIDATE_THREADS, P.n - tile0);
-    const u64 t_start = wall_clock64();  // the launch span's start (stamped at the end: no entry branch)
+    // The launch span's start: the first workgroup's clock (dispatch is in workgroup order), read on
+    // the scalar unit and stamped at the end — no vector work at entry.
+    const u64 t_start = blockIdx.x == 0 && P.kclock ? wall_clock64() : 0;
     tb_stage_tile<SRC>(P, tile0, count, stage, TB_ABL(P, EXP_NT));
 
     const u32 pe = tile0 + threadIdx.x;  // pass-relative event
@@ -380,7 +382,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
         }
         tb_sum_publish(P, total);
         if (P.kclock) {
-            if (blockIdx.x < 8) atomicMin((unsigned long long*)P.kclock, (unsigned long long)t_start);
+            if (blockIdx.x == 0) atomicMin((unsigned long long*)P.kclock, (unsigned long long)t_start);
             tb_kclock_stamp_end(P.kclock);
         }
     }

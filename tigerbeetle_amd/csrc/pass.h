@@ -95,8 +95,6 @@ struct PassArgs {
 
     u32* leg_off;          // [prepares of the pass][leg_buckets + 1] bucket starts in the prepare's legs
     u32* flow_words;       // tb_flow's per-pass counters (k_flow.h, FLOW_WORDS), zeroed by tb_resolve (or null)
-    u32* pcie_gate;        // (or null) set by tb_pass_clear, cleared by tb_resolve: while set, the asynchronous
-                           // write-back's copy-out (tb_delta_out) holds its PCIe writes (engine.hip)
     u64* kclock;           // profiling (or null): this pass's launch spans, {first start, last end} of
                            // validate, resolve and apply (device wall clock), set up by tb_pass_clear
 };
@@ -281,13 +279,12 @@ __device__ static inline void tb_dedup_mark(const PassArgs& P) {
 // kernel arguments instead of a copy ahead of the pass (the replica's one-prepare commits).
 __global__ __launch_bounds__(256) void tb_pass_clear(u64* dedup, u64 cap, u64* sum_shards, const Globals* g, u32 epoch,
                                                      u32 force, u32* leg_tot, u32 leg_buckets, u64* meta, u64 m0, u64 m1,
-                                                     u64 m2, u64* kclock, u32* pcie_gate) {
+                                                     u64 m2, u64* kclock) {
     const u64 w = g->dedup_dirty;  // before the stores (a load after them waits for them)
     if (blockIdx.x == 0 && threadIdx.x < SUM_WORDS) sum_shards[threadIdx.x] = 0;
     if (kclock && blockIdx.x == 0) {
         for (u32 k = threadIdx.x; k < KCLOCK_WORDS; k += 256) kclock[k] = k % KCLOCK_STRIDE ? 0 : ~0ULL;
     }
-    if (pcie_gate && blockIdx.x == 0 && threadIdx.x == 0) *pcie_gate = 1;
     if (meta && blockIdx.x == 0 && threadIdx.x == 0) {
         meta[0] = m0;
         meta[1] = m1;

@@ -27,10 +27,10 @@ case $MODE in
   mc) timeout -k 10 420 rocprofv3 --memory-copy-trace --kernel-trace --output-format csv -d "$OUT/mc" -o run -- \
         python3 "$R/bench.py" $LEG --access-mix 0 --steps 1 --warmup 1 > "$OUT/bench_mc.log" 2>&1; rc=$? ;;
   dfetch|dwrite) C=FETCH_SIZE; [ "$MODE" = dwrite ] && C=WRITE_SIZE
-      timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/tools/gpu/device_pass.py" \
+      timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/tools/gpu/device_pass.py" 100000000 \
         > "$OUT/$MODE.log" 2>&1; rc=$? ;;
   dkt) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/dkt" -o run -- \
-        python3 "$R/tools/gpu/device_pass.py" > "$OUT/dkt.log" 2>&1; rc=$? ;;
+        python3 "$R/tools/gpu/device_pass.py" 100000000 > "$OUT/dkt.log" 2>&1; rc=$? ;;
   fetch|write) C=FETCH_SIZE; [ "$MODE" = write ] && C=WRITE_SIZE
       timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/bench.py" $LEG \
         --steps 1 --warmup 0 > "$OUT/$MODE.log" 2>&1; rc=$? ;;

@@ -22,4 +22,4 @@ python3 "$R/tools/perf_pmc.py" "$P/pmc_r04.json" r04 \
   headline "$(f kt '*kernel_stats.csv')" "$(f fetch '*counter_collection.csv')" "$(f write '*counter_collection.csv')" \
            100000000 523560 \
   device "$(f dkt '*kernel_stats.csv')" "$(f dfetch '*counter_collection.csv')" "$(f dwrite '*counter_collection.csv')" \
-           20971200 4193280
+           100000000 4166667

@@ -4,9 +4,10 @@
 Two legs, each from three runs of one command (kernel trace + stats; FETCH_SIZE alone; WRITE_SIZE
 alone — they do not fit in one pass on gfx950, MI355X_MICROARCH.md §HBM):
   headline  bench.py's headline leg (pipelined C2 commits from registered host memory, 64-prepare
-            chunks of 523,560 transfers; counters from a 20M-transfer run of the same chunks)
-  device    tools/gpu/device_pass.py (the same prepares already in HBM, 512-prepare passes of
-            4,193,280 transfers: no host copy in flight while the pass kernels run)
+            chunks of 523,560 transfers; counters from one 100M-transfer step of the same chunks)
+  device    tools/gpu/device_pass.py 100000000 (the bench's device-resident leg: the same 100M
+            prepares already in HBM, 512-prepare passes: no host copy in flight while the pass
+            kernels run)
 
 Per kernel: rocprof calls and mean duration, and the counters summed over every dispatch divided by
 the transfers those dispatches committed (FETCH_SIZE / WRITE_SIZE are KB).  `raw` = FETCH + WRITE;
