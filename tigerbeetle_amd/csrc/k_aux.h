@@ -225,32 +225,50 @@ __device__ static inline u64 tb_wave_claim(bool take, u64* count) {
     return base + __popcll(m & ((1ULL << lane) - 1));
 }
 
-__global__ void tb_delta_ids(Tables T, const AccountBal* snap, u64 ts0, const u64* ids, u64 n, u32* mark, u32 epoch,
-                             u8* out, AccountBal* before, u64* count, u32* slots, u64* slot_count,
-                             const u64* n_dev = nullptr) {
+__global__ __launch_bounds__(256) void tb_delta_ids(Tables T, const AccountBal* snap, u64 ts0, const u64* ids, u64 n,
+                                                    u32* mark, u32 epoch, u8* out, AccountBal* before, u64* count,
+                                                    u32* slots, u64* slot_count, const u64* n_dev = nullptr) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = i < n && !(n_dev && i >= 2 * *n_dev);
     u32 slot = TB_NOT_FOUND;
     if (live) slot = tb_account_find(T, ids[2 * i], ids[2 * i + 1]);
-    // The first copy of an id takes its slot (a later one finds this write-back's epoch there).
-    const bool first = slot != TB_NOT_FOUND && atomicExch(&mark[slot], epoch) != epoch;
-    bool emit = false;
-    AccountBal s{};
-    u64 hts = 0;
-    if (first) {
-        hts = T.acct_hot[slot].timestamp;
-        const AccountBal b = T.acct_bal[slot];
-        s = snap[slot];
-        const bool same = b.debits_pending == s.debits_pending && b.debits_posted == s.debits_posted &&
-                          b.credits_pending == s.credits_pending && b.credits_posted == s.credits_posted;
-        emit = hts > ts0 || !same;
+    // The slot's words are read together with the epoch exchange (one round trip, not three: the
+    // exchange decides only whether this copy of the id is the one that emits).
+    u32 was = epoch;
+    AccountHot h{};
+    AccountBal b{}, sn{};
+    AccountCold c{};
+    if (slot != TB_NOT_FOUND) {
+        was = atomicExch(&mark[slot], epoch);
+        h = T.acct_hot[slot];
+        b = T.acct_bal[slot];
+        sn = snap[slot];
+        c = T.acct_cold[slot];
     }
+    const bool first = was != epoch;  // the first copy of the id takes its slot
+    const bool same = b.debits_pending == sn.debits_pending && b.debits_posted == sn.debits_posted &&
+                      b.credits_pending == sn.credits_pending && b.credits_posted == sn.credits_posted;
+    const bool emit = first && (h.timestamp > ts0 || !same);
     const u64 si = tb_wave_claim(first, slot_count);
     if (first) slots[si] = slot;
     const u64 k = tb_wave_claim(emit, count);
     if (emit) {
-        *(Account*)(out + k * 128) = tb_account_load(T, slot);
-        before[k] = hts <= ts0 ? s : AccountBal{0, 0, 0, 0};
+        Account a;
+        a.id = tb_u128(h.id_lo, h.id_hi);
+        a.debits_pending = b.debits_pending;
+        a.debits_posted = b.debits_posted;
+        a.credits_pending = b.credits_pending;
+        a.credits_posted = b.credits_posted;
+        a.user_data_128 = c.user_data_128;
+        a.user_data_64 = c.user_data_64;
+        a.user_data_32 = c.user_data_32;
+        a.reserved = c.reserved;
+        a.ledger = h.ledger;
+        a.code = h.code;
+        a.flags = h.flags;
+        a.timestamp = h.timestamp;
+        *(Account*)(out + k * 128) = a;
+        before[k] = h.timestamp <= ts0 ? sn : AccountBal{0, 0, 0, 0};
     }
 }
 

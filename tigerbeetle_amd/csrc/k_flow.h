@@ -628,6 +628,9 @@ struct WalkRec {
 #define WALK_HEAVY 256
 #endif
 #define WALK_RING 8  // windows a feeder wave keeps ahead of its walker in LDS
+#ifndef WALK_REFRESH
+#define WALK_REFRESH 1  // a heavy walker re-reads a window's open partner statuses before walking it
+#endif
 
 #define WALK_BIG (1LL << 62)  // a position whose outcome is known: "always" (+) / "never" (−)
 
@@ -1032,6 +1035,19 @@ __device__ static inline bool fl_walk_heavy(const FlowArgs& F, Globals* g, const
         if (c + 128 + lane < n_seg) r2 = R[s0 + c + 128 + lane];
         u32 st1, vw1;
         fl_walk_status(F, r1, c + 64 + lane < n_seg, st1, vw1);
+#if WALK_REFRESH
+        {   // The window's still-open partner statuses, read again right before it is walked (they were
+            // read a window ago; a partner walker has often decided them since): one round trip here
+            // instead of a stop at each of them in the walk.
+            const bool open = lane < n && st0 == BS_UNK;
+            u32 st2 = BS_UNK, vw2 = 0;
+            if (__ballot(open)) fl_walk_status(F, r0, open, st2, vw2);
+            if (open) {
+                st0 = st2;
+                vw0 = vw2 ? vw2 : vw0;
+            }
+        }
+#endif
         for (u32 s = 0;;) {
             const u32 m = fl_walk_window(F, r0, st0, vw0, s, n, d, ws, g, true);
             if (m > s && tblock) {
