@@ -317,6 +317,7 @@ static int prof_collect(tbgpu* E) {
                 const u64* kw = w + k * KCLOCK_STRIDE;
                 u64 end = 0;
                 for (u32 q = 1; q <= KCLOCK_ENDS; q++) end = std::max(end, kw[q * KCLOCK_LINE]);
+                if (k == 0) end = w[KCLOCK_STRIDE];  // validate: until resolve's start (pass.h)
                 if (!((u.second >> k) & 1) || end < kw[0] || !E->wall_khz) continue;
                 E->span_ms[k] += (double)(end - kw[0]) / E->wall_khz;
                 E->span_n[k] += 1;

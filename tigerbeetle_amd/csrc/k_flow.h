@@ -629,7 +629,7 @@ struct WalkRec {
 #endif
 #define WALK_RING 8  // windows a feeder wave keeps ahead of its walker in LDS
 #ifndef WALK_REFRESH
-#define WALK_REFRESH 1  // a heavy walker re-reads a window's open partner statuses before walking it
+#define WALK_REFRESH 0  // 1: a heavy walker re-reads a window's open partner statuses before walking it (C3h: no gain, stops -5 %)
 #endif
 
 #define WALK_BIG (1LL << 62)  // a position whose outcome is known: "always" (+) / "never" (−)

@@ -294,9 +294,6 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
 
     const u32 tile0 = blockIdx.x * VALIDATE_THREADS;
     const u32 count = min((u32)VALIDATE_THREADS, P.n - tile0);
-    // The launch span's start: the first workgroup's clock (dispatch is in workgroup order), one plain
-    // store by that workgroup (nothing kept live across the kernel: its SGPRs already spill).
-    if (blockIdx.x == 0 && threadIdx.x == 0 && P.kclock) P.kclock[0] = wall_clock64();
     tb_stage_tile<SRC>(P, tile0, count, stage, TB_ABL(P, EXP_NT));
 
     const u32 pe = tile0 + threadIdx.x;  // pass-relative event
@@ -381,7 +378,6 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
             total = tb_sat_add(total, tb_u128(*(const u64*)q, *(const u64*)(q + 8)));
         }
         tb_sum_publish(P, total);
-        if (P.kclock) tb_kclock_stamp_end(P.kclock);
     }
 }
 

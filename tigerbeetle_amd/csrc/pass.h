@@ -99,12 +99,15 @@ struct PassArgs {
                            // validate, resolve and apply (device wall clock), set up by tb_pass_clear
 };
 
-// Launch span of a profiled kernel (tbgpu_stats.span_ms): the first workgroup of each XCD lowers the
-// start word to its start, and every workgroup raises one of KCLOCK_ENDS end words (one 128-B line
-// each, by workgroup) to its end; the host takes the maximum after the pass.  Both are no-return
-// atomics, so no wave waits on them, and no line takes more than a few hundred per launch (one
-// same-address atomic per workgroup, or a load that must return before the workgroup starts, slowed
-// validate by 13-40 %).
+// Launch span of a profiled kernel (tbgpu_stats.span_ms).  Resolve and apply: the first workgroup of
+// each XCD lowers the start word to its start, and every workgroup raises one of KCLOCK_ENDS end
+// words (one 128-B line each, by workgroup) to its end; the host takes the maximum after the pass.
+// Both are no-return atomics, so no wave waits on them.  Validate carries no stamp at all: any
+// stamping code in it — even one store by one workgroup — measured 10 % slower in same-box A/B runs
+// (its SGPRs already spill); its span is from the end of tb_pass_clear (the kernel before it on the
+// stream, stamped by its workgroup 0 into validate's start word) to the start of tb_resolve (the one
+// after it, kernel 1's start word): the two launch gaps inside were below the kernel trace's
+// resolution (profiles/r04).
 #define KCLOCK_ENDS 16
 #define KCLOCK_LINE 16                                   // u64 words per 128-B line
 #define KCLOCK_STRIDE (KCLOCK_LINE * (1 + KCLOCK_ENDS))  // per kernel: [0] start, [(1 + q) * KCLOCK_LINE] end q
@@ -299,6 +302,10 @@ __global__ __launch_bounds__(256) void tb_pass_clear(u64* dedup, u64 cap, u64* s
     typedef unsigned int v4 __attribute__((ext_vector_type(4)));
     const v4 z = {0, 0, 0, 0};
     for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; 2 * i < n; i += (u64)gridDim.x * 256) ((v4*)dedup)[i] = z;
+    if (kclock && blockIdx.x == 0) {  // validate's span starts where this kernel ends (see KCLOCK_STRIDE)
+        __syncthreads();
+        if (threadIdx.x == 0) kclock[0] = wall_clock64();
+    }
 }
 
 __device__ static inline u128 tb_sum_total(const u64* shards) {
