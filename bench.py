@@ -311,7 +311,7 @@ def run_secondary(args, kind, device):
     eng.register_host(xfers)
     replies = np.empty(n_xfer * 8, dtype=np.uint8)
     step_ms, t_cursor = [], t_end
-    eng.profile_mask(eng.PROF_VALIDATE | eng.PROF_REPLAY)
+    eng.profile_mask(eng.PROF_APPLY | eng.PROF_REPLAY)  # validate on the device clock (no event pair inside its span)
     for step in range(2):  # one warmup, one timed
         eng.reset_transfers()
         ts, t_cursor = timestamps(x_lens, t_cursor + 10, wl["gap_every"])
@@ -324,7 +324,7 @@ def run_secondary(args, kind, device):
     stats = eng.stats()
     eng.unregister_host(xfers)
     eng.close()
-    per_launch = n_xfer / max(1, stats["launches_validate"])
+    per_launch = n_xfer / max(1, stats["span_launches"][0] or stats["launches_validate"])
     # The ordered fallback (tb_flow) has no byte roofline (it is bound by its dependency rounds):
     # the roofline is the validate kernel's; tb_flow's time share is reported beside it.
     roof = roofline(stats, expected_unique(n_acct, 2 * per_launch) / per_launch, per_launch,
@@ -611,7 +611,7 @@ def main():
             if args.warmup:
                 breakdown = engine.stats()
             engine.reset_stats()
-            engine.profile_mask(engine.PROF_VALIDATE | engine.PROF_REPLAY)
+            engine.profile_mask(engine.PROF_APPLY | engine.PROF_REPLAY)  # validate on the device clock only
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -640,13 +640,15 @@ def main():
 
     # -- secondary: the same commits with the prepares already resident in HBM ----------------
     dev_ms = []
-    engine.profile_mask(engine.PROF_VALIDATE | engine.PROF_PASS | engine.PROF_REPLAY)
-    dev_stats = None
+    engine.profile_mask(engine.PROF_ALL)  # first (untimed) step: every kernel's HIP-event time
+    dev_stats = dev_breakdown = None
     for step in range(1 + args.device_steps if args.device_steps else 0):
         engine.reset_transfers()
         ts, t_cursor = timestamps(xfer_lens, t_cursor + 10, wl["gap_every"])
         if step == 1:
+            dev_breakdown = engine.stats()
             engine.reset_stats()
+            engine.profile_mask(engine.PROF_APPLY | engine.PROF_PASS | engine.PROF_REPLAY)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         engine.commit_device_async(129, ts, xfer_lens, events_dev, res_dev, rb_dev)
@@ -679,7 +681,8 @@ def main():
     full_ok = full_ok and n_failed_host == n_failed
 
     # -- roofline: the dominant kernel of the headline's timed steps ---------------------------
-    per_launch_transfers = args.transfers / max(1, stats["launches_validate"] / max(1, args.steps))
+    n_val = (stats.get("span_launches") or [0])[0] or stats["launches_validate"]  # validate launches, timed steps
+    per_launch_transfers = args.transfers / max(1, n_val / max(1, args.steps))
     u_over_t = expected_unique(args.accounts, 2 * per_launch_transfers) / per_launch_transfers
     # The ordered fallback (tb_flow) has no byte roofline (its dependency rounds bound it): the
     # roofline is the validate kernel's, with tb_flow's share of the time beside it.
@@ -694,15 +697,17 @@ def main():
     device_resident = None
     if dev_ms:
         dev_total = sum(dev_ms)
-        per_launch_dev = args.transfers / max(1, dev_stats["launches_validate"] / max(1, args.device_steps))
+        # validate launches of one step (its device-clock spans: no HIP events around it when timed)
+        n_val = dev_stats["span_launches"][0] or dev_stats["launches_validate"]
+        per_launch_dev = args.transfers / max(1, n_val / max(1, args.device_steps))
         u_dev = expected_unique(args.accounts, 2 * per_launch_dev) / per_launch_dev
         device_resident = {
             "value": round(args.transfers * args.device_steps / (dev_total / 1e3), 1), "unit": "transfers/s",
             "steps": args.device_steps, "ms_per_step": round(dev_total / args.device_steps, 3),
             "pass_prepares": args.pass_batches,
             "definition": "tbgpu_commit_device_async: the same prepares already resident in HBM (no PCIe)",
-            "roofline": roofline(dev_stats, u_dev, per_launch_dev, args, dev_total, None, steps=args.device_steps,
-                                 device=True),
+            "roofline": roofline(dev_stats, u_dev, per_launch_dev, args, dev_total, dev_breakdown, steps=args.device_steps,
+                                 kernel="tb_transfers_validate", device=True),
         }
 
     # -- the validate kernel against its own access pattern, measured live (rank 0, N=1) ------
@@ -1227,6 +1232,12 @@ def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=No
     kernels = kernel_table(stats)
     dom = kernel or max(kernels, key=lambda k: kernels[k][0])
     ms_dom, n_dom = kernels[dom]
+    # The launch's own duration on the device clock (tbgpu_stats.span_ms; validate: from the end of
+    # the kernel before it to the start of the one after it, pass.h), what rocprofv3's kernel trace
+    # measures too.  The timed steps put no HIP event pair around validate (an event record between
+    # the kernels would sit inside its span): its HIP-event mean comes from the warmup steps.
+    span_idx = {"tb_transfers_validate": 0, "tb_resolve<129>": 1, "tb_apply_legs": 2}.get(dom)
+    has_span = bool(span_idx is not None and stats.get("span_launches") and stats["span_launches"][span_idx])
     # B = 296 + 256·U/T per transfer, split by where the work happens:
     # validate reads the event (128), probes + claims the id (32), writes the record (128) and reads
     # each touched account once (128·U/T); resolve writes the result slot (8) and each touched
@@ -1238,25 +1249,23 @@ def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=No
     alg_bytes = {"tb_transfers_validate": b_validate, "tb_resolve<129>": b_resolve, "tb_flow": 0.0,
                  "tb_pass_clear": 0.0,
                  "tb_apply_legs": b_apply}[dom] * per_launch_transfers
-    if not n_dom:
+    if not n_dom and not has_span:
         return None
-    # The launch's own duration on the device clock (first workgroup's start to last workgroup's end,
-    # s_memrealtime; tbgpu_stats.span_ms), what rocprofv3's kernel trace measures too; the HIP-event
-    # pair around the launch also holds its dispatch.
-    span_idx = {"tb_transfers_validate": 0, "tb_resolve<129>": 1, "tb_apply_legs": 2}.get(dom)
-    hip_avg = ms_dom / n_dom
+    hms, hn = (kernels if n_dom else kernel_table(breakdown) if breakdown else kernels)[dom]
+    hip_avg = hms / hn if hn else None
     avg_ms, timing = hip_avg, "HIP events on the engine stream around every launch of the kernel in the timed steps"
-    if span_idx is not None and stats.get("span_launches") and stats["span_launches"][span_idx]:
+    if has_span:
         avg_ms = stats["span_ms"][span_idx] / stats["span_launches"][span_idx]
-        timing = ("device clock (s_memrealtime) from the first workgroup's start to the last one's end, every launch "
-                  "of the kernel in the timed steps")
+        timing = ("device clock (s_memrealtime), every launch of the kernel in the timed steps: validate from the end of "
+                  "tb_pass_clear to the start of tb_resolve, the others from the first workgroup's start to the last "
+                  "one's end")
     avg_s = avg_ms / 1e3
     achieved = alg_bytes / avg_s / 1e9
     src = kernel_table(breakdown) if breakdown else kernels
     per_kernel = {k: {"launches": int(n), "avg_launch_ms": round(ms / n, 4)} for k, (ms, n) in src.items() if n}
     out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel": dom,
-           "avg_launch_ms": round(avg_ms, 4), "avg_launch_ms_hip_events": round(hip_avg, 4),
+           "avg_launch_ms": round(avg_ms, 4), "avg_launch_ms_hip_events": round(hip_avg, 4) if hip_avg else None,
            "transfers_per_launch": round(per_launch_transfers, 1),
            "alg_bytes_per_transfer": round(alg_bytes / per_launch_transfers, 1), "timing": timing}
     if pmc:  # the C2 launches the PMC runs profiled (not the C3/C4 lines)

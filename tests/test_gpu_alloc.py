@@ -187,17 +187,27 @@ def test_device_panic_stops_the_engine_until_reset(gpu_engine_factory):
 
 
 def test_kernel_spans_on_the_device_clock(gpu_engine_factory):
-    engine = gpu_engine_factory(accounts_max=1 << 12, transfers_max=1 << 17, pass_events_max=1 << 15,
+    """Launch spans on the device clock: one per pass for validate and resolve, each no longer than the
+    HIP-event pair around the same launch (which also holds its dispatch) — validate's span measured
+    with no event pair inside it (between tb_pass_clear and tb_resolve, pass.h)."""
+    engine = gpu_engine_factory(accounts_max=1 << 12, transfers_max=1 << 18, pass_events_max=1 << 15,
                                 pass_batches_max=8, profile=True)
     assert engine.commit(128, 10**9, _accounts(256).tobytes()) == b""
-    engine.reset_stats()
-    bodies = [_transfers(8190, 1 + 8190 * j, 256).tobytes() for j in range(4)]
-    assert engine.commit_many(129, [10**10 + 10**5 * j for j in range(4)], bodies) == [b""] * 4
-    st = engine.stats()
-    n_val, n_res = st["span_launches"][0], st["span_launches"][1]
-    assert n_val == st["launches_validate"] > 0 and n_res == st["launches_resolve"]
-    for k, key in ((0, "ms_validate"), (1, "ms_resolve")):
-        assert 0 < st["span_ms"][k] <= st[key] * 1.05 + 0.01  # inside the HIP-event bracket
+
+    def run(first, mask):
+        engine.reset_stats()
+        engine.profile_mask(mask)
+        bodies = [_transfers(8190, first + 8190 * j, 256).tobytes() for j in range(4)]
+        assert engine.commit_many(129, [10**10 * first + 10**5 * j for j in range(4)], bodies) == [b""] * 4
+        return engine.stats()
+
+    hip = run(1, engine.PROF_ALL)
+    st = run(1 + 4 * 8190, engine.PROF_APPLY)
+    assert st["span_launches"][0] == st["passes"] > 0 and st["span_launches"][1] == st["passes"]
+    for k, key, launches in ((0, "ms_validate", "launches_validate"), (1, "ms_resolve", "launches_resolve")):
+        per_span = st["span_ms"][k] / st["span_launches"][k]
+        per_hip = hip[key] / hip[launches]
+        assert 0 < per_span <= per_hip * 1.25 + 0.005, (k, per_span, per_hip)
 
 
 @pytest.mark.parametrize("config", ["mixed", "two_phase", "chains"])
