@@ -110,11 +110,13 @@ struct WbBufs {
     u8* d_acc = nullptr;          // [cap_a] emitted accounts
     AccountBal* d_before = nullptr;
     u32* d_slots = nullptr;       // [account_cap] every slot one write-back covers
+    AccountBal* d_cap = nullptr;  // [cap_a] asynchronous write-back: the balances captured at the bar
     u64* d_cnt = nullptr;         // [WB_COUNT_WORDS] WB_* counters
     u64* h_cnt = nullptr;         // pinned mirror
     hipStream_t stream = nullptr; // the asynchronous copy-out (DMA engine)
     hipEvent_t gathered = nullptr, done = nullptr;
     hipEvent_t read_done = nullptr;  // on the engine stream after a commit's validate (its PCIe reads)
+    hipEvent_t captured = nullptr;   // on the engine stream after the bar's capture (the rest follows beside)
     bool inflight = false;
     // The copy-out in flight: regions (records, accounts, before, pairs) from HBM to the caller's
     // registered buffers, sent a slice per commit (wb_pump) once the gather's counts are known.
@@ -703,12 +705,14 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         INIT_CK(tbMalloc(&W.d_acc, W.cap_a * 128));
         INIT_CK(tbMalloc(&W.d_before, W.cap_a * sizeof(AccountBal)));
         INIT_CK(tbMalloc(&W.d_slots, E->account_cap * 4));
+        INIT_CK(tbMalloc(&W.d_cap, W.cap_a * sizeof(AccountBal)));
         INIT_CK(tbMalloc(&W.d_cnt, WB_COUNT_WORDS * 8));
         INIT_CK(tbHostMalloc(&W.h_cnt, WB_COUNT_WORDS * 8, hipHostMallocDefault));
         INIT_CK(hipStreamCreateWithFlags(&W.stream, hipStreamNonBlocking));
         INIT_CK(tbEventCreateWithFlags(&W.gathered, hipEventDisableTiming));
         INIT_CK(tbEventCreateWithFlags(&W.done, hipEventDisableTiming));
         INIT_CK(tbEventCreateWithFlags(&W.read_done, hipEventDisableTiming));
+        INIT_CK(tbEventCreateWithFlags(&W.captured, hipEventDisableTiming));
     }
     INIT_CK(tbMalloc(&E->kclock, (u64)KCLOCK_SLOTS * KCLOCK_WORDS * 8));
     INIT_CK(tbHostMalloc(&E->h_kclock, (u64)KCLOCK_SLOTS * KCLOCK_WORDS * 8, hipHostMallocDefault));
@@ -744,7 +748,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
                     E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->pf_staging, E->kclock, E->r_home,
                     E->wb.d_bc, E->wb.d_base, E->wb.d_out, E->wb.d_ids, E->wb.d_pv, E->wb.d_pairs, E->wb.d_hids,
-                    E->wb.d_acc, E->wb.d_before, E->wb.d_slots, E->wb.d_cnt,
+                    E->wb.d_acc, E->wb.d_before, E->wb.d_slots, E->wb.d_cap, E->wb.d_cnt,
                     E->r_block_counts, E->r_words, E->r_meta, E->leg_ev, E->leg_w, E->leg_off, E->leg_tot,
                     E->F.f_pe, E->F.f_batch, E->F.f_len, E->F.need, E->F.nsucc, E->F.queue, E->F.uflags, E->F.nacct, E->F.rpos, E->F.succ,
                     E->F.run, E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo,
@@ -774,6 +778,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
     if (E->wb.gathered) (void)hipEventDestroy(E->wb.gathered);
     if (E->wb.done) (void)hipEventDestroy(E->wb.done);
     if (E->wb.read_done) (void)hipEventDestroy(E->wb.read_done);
+    if (E->wb.captured) (void)hipEventDestroy(E->wb.captured);
     for (hipEvent_t e : E->event_pool) (void)hipEventDestroy(e);
     if (E->pf_done) (void)hipEventDestroy(E->pf_done);
     for (int i = 0; i < 16; i++) if (E->markers[i]) (void)hipEventDestroy(E->markers[i]);
@@ -1905,20 +1910,40 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
     W.counts.created_after = E->ckpt_ts;
     if ((st = wb_next_epoch(E))) return st;
     HIPCK(hipMemsetAsync(W.d_cnt, 0, WB_COUNT_WORDS * 8, E->stream));
+    // In stream order (the next commits follow): the log range's records and account ids, and each
+    // account's slot and balances as of the bar (tb_delta_capture).
     if ((st = wb_gather_slice(E, E->ckpt_pos, E->log_next, true))) return st;
-    if ((st = wb_ids(E, W.d_ids, 2 * range, W.d_cnt + WB_RECORDS))) return st;
+    const u64 n_ids = 2 * range;
+    if (n_ids) {
+        hipLaunchKernelGGL(tb_delta_capture, dim3((unsigned)((n_ids + 255) / 256)), dim3(256), 0, E->stream, E->T, W.d_ids,
+                           n_ids, E->ckpt_mark, E->ckpt_epoch, W.d_slots, W.d_cap, W.d_cnt + WB_SLOTS,
+                           W.d_cnt + WB_RECORDS);
+    }
     const u64 nl = E->ckpt_ids.size() / 2;
     if (nl) {  // the listed ids cross in the same stream order (their host copy lives until then)
         W.ids_inflight.swap(E->ckpt_ids);
         HIPCK(hipMemcpyAsync(W.d_hids, W.ids_inflight.data(), nl * 16, hipMemcpyHostToDevice, E->stream));
-        if ((st = wb_ids(E, W.d_hids, nl, nullptr))) return st;
+        hipLaunchKernelGGL(tb_delta_capture, dim3((unsigned)((nl + 255) / 256)), dim3(256), 0, E->stream, E->T, W.d_hids, nl,
+                           E->ckpt_mark, E->ckpt_epoch, W.d_slots, W.d_cap, W.d_cnt + WB_SLOTS, nullptr);
     }
-    if ((st = wb_advance(E))) return st;
-    hipLaunchKernelGGL(tb_delta_order, dim3(256), dim3(256), 0, E->stream, W.d_out, W.d_cnt + WB_RECORDS, W.d_pairs,
+    HIPCK(hipGetLastError());
+    HIPCK(hipEventRecord(W.captured, E->stream));
+    // Beside the next commits, on the write-back stream: the records, the emission, the snapshot.
+    const u64 ts0 = E->ckpt_ts;
+    HIPCK(hipStreamWaitEvent(W.stream, W.captured, 0));
+    hipLaunchKernelGGL(tb_delta_emit, dim3(1024), dim3(256), 0, W.stream, E->T, E->ckpt_bal, ts0, W.d_slots, W.d_cap,
+                       W.d_cnt + WB_SLOTS, W.d_acc, W.d_before, W.d_cnt + WB_ACCOUNTS);
+    hipLaunchKernelGGL(tb_delta_advance_from, dim3(1024), dim3(256), 0, W.stream, E->ckpt_bal, W.d_slots, W.d_cap,
+                       W.d_cnt + WB_SLOTS);
+    hipLaunchKernelGGL(tb_delta_order, dim3(256), dim3(256), 0, W.stream, W.d_out, W.d_cnt + WB_RECORDS, W.d_pairs,
                        W.d_cnt + WB_PV, W.d_cnt + WB_ORDER);
     HIPCK(hipGetLastError());
-    HIPCK(hipMemcpyAsync(W.h_cnt, W.d_cnt, WB_COUNT_WORDS * 8, hipMemcpyDeviceToHost, E->stream));
-    HIPCK(hipEventRecord(W.gathered, E->stream));
+    HIPCK(hipMemcpyAsync(W.h_cnt, W.d_cnt, WB_COUNT_WORDS * 8, hipMemcpyDeviceToHost, W.stream));
+    HIPCK(hipEventRecord(W.gathered, W.stream));
+    E->ckpt_pos = E->log_next;  // wb_advance's host part (the snapshot advances on the write-back stream)
+    E->ckpt_ts = E->commit_ts;
+    E->ckpt_scan = false;
+    E->ckpt_ids.clear();  // (holds the previous write-back's list after the swap above)
     W.src[0] = W.d_out;
     W.dst[0] = (u8*)transfers_out;
     W.src[1] = W.d_acc;

@@ -272,6 +272,81 @@ __global__ __launch_bounds__(256) void tb_delta_ids(Tables T, const AccountBal* 
     }
 }
 
+// The asynchronous write-back splits tb_delta_ids in two.  In stream order, right after the bar
+// (tb_delta_capture): each id's slot, deduplicated by the epoch mark, and its balances as they are
+// now — the only part of an account the next commits change.  Beside those commits, on the
+// write-back stream (tb_delta_emit): the records (the hot and cold words of an existing account
+// never change; a create of another account only fills an empty slot, off every existing probe
+// chain), the snapshot comparison, the emission, then the snapshot's advance from the captured
+// balances (tb_delta_advance_from).
+__global__ __launch_bounds__(256) void tb_delta_capture(Tables T, const u64* ids, u64 n, u32* mark, u32 epoch,
+                                                        u32* slots, AccountBal* cap, u64* slot_count,
+                                                        const u64* n_dev = nullptr) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = i < n && !(n_dev && i >= 2 * *n_dev);
+    u32 slot = TB_NOT_FOUND;
+    if (live) slot = tb_account_find(T, ids[2 * i], ids[2 * i + 1]);
+    u32 was = epoch;
+    AccountBal b{};
+    if (slot != TB_NOT_FOUND) {
+        was = atomicExch(&mark[slot], epoch);
+        b = T.acct_bal[slot];
+    }
+    const bool first = was != epoch;
+    const u64 si = tb_wave_claim(first, slot_count);
+    if (first) {
+        slots[si] = slot;
+        cap[si] = b;
+    }
+}
+
+__global__ __launch_bounds__(256) void tb_delta_emit(Tables T, const AccountBal* snap, u64 ts0, const u32* slots,
+                                                     const AccountBal* cap, const u64* slot_count, u8* out,
+                                                     AccountBal* before, u64* count) {
+    const u64 m = *slot_count;
+    for (u64 i0 = (u64)blockIdx.x * blockDim.x; i0 < m; i0 += (u64)gridDim.x * blockDim.x) {
+        const u64 i = i0 + threadIdx.x;
+        const bool live = i < m;
+        AccountHot h{};
+        AccountCold c{};
+        AccountBal b{}, sn{};
+        if (live) {
+            const u32 slot = slots[i];
+            h = T.acct_hot[slot];
+            c = T.acct_cold[slot];
+            sn = snap[slot];
+            b = cap[i];
+        }
+        const bool same = b.debits_pending == sn.debits_pending && b.debits_posted == sn.debits_posted &&
+                          b.credits_pending == sn.credits_pending && b.credits_posted == sn.credits_posted;
+        const bool emit = live && (h.timestamp > ts0 || !same);
+        const u64 k = tb_wave_claim(emit, count);
+        if (emit) {
+            Account a;
+            a.id = tb_u128(h.id_lo, h.id_hi);
+            a.debits_pending = b.debits_pending;
+            a.debits_posted = b.debits_posted;
+            a.credits_pending = b.credits_pending;
+            a.credits_posted = b.credits_posted;
+            a.user_data_128 = c.user_data_128;
+            a.user_data_64 = c.user_data_64;
+            a.user_data_32 = c.user_data_32;
+            a.reserved = c.reserved;
+            a.ledger = h.ledger;
+            a.code = h.code;
+            a.flags = h.flags;
+            a.timestamp = h.timestamp;
+            *(Account*)(out + k * 128) = a;
+            before[k] = h.timestamp <= ts0 ? sn : AccountBal{0, 0, 0, 0};
+        }
+    }
+}
+
+__global__ void tb_delta_advance_from(AccountBal* snap, const u32* slots, const AccountBal* cap, const u64* n) {
+    const u64 m = *n;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (u64)gridDim.x * blockDim.x) snap[slots[i]] = cap[i];
+}
+
 // The snapshot follows the slots a write-back covered (*n of them), grid-stride.
 __global__ void tb_delta_advance(Tables T, AccountBal* snap, const u32* slots, const u64* n) {
     const u64 m = *n;
