@@ -1645,20 +1645,21 @@ static WbBounds wb_bounds(tbgpu* E, u64 live_accounts) {
 // Slice [a, b) of the log range: gather its new transfers (records, their account ids, their post /
 // void records and posted pairs) into the write-back buffers and look their accounts up.  Enqueued
 // only; the slice's counts land in d_cnt (records, post / void records, accounts emitted).
-static int wb_gather_slice(tbgpu* E, u64 a, u64 b, bool want_records, bool posted = true) {
+static int wb_gather_slice(tbgpu* E, u64 a, u64 b, bool want_records, bool posted = true, hipStream_t stream = nullptr) {
     WbBufs& W = E->wb;
+    if (!stream) stream = E->stream;
     const u64 n = b - a, nblocks = (n + DELTA_THREADS - 1) / DELTA_THREADS;
-    HIPCK(hipMemsetAsync(W.d_cnt + WB_ACCOUNTS, 0, 8, E->stream));
-    HIPCK(hipMemsetAsync(W.d_cnt + WB_PV, 0, 16, E->stream));  // WB_PV, WB_RECORDS
+    HIPCK(hipMemsetAsync(W.d_cnt + WB_ACCOUNTS, 0, 8, stream));
+    HIPCK(hipMemsetAsync(W.d_cnt + WB_PV, 0, 16, stream));  // WB_PV, WB_RECORDS
     if (!n) return TBGPU_STATUS_OK;
-    hipLaunchKernelGGL(tb_delta_log_count, dim3((unsigned)nblocks), dim3(DELTA_THREADS), 0, E->stream, E->T, a, n, E->ckpt_ts,
+    hipLaunchKernelGGL(tb_delta_log_count, dim3((unsigned)nblocks), dim3(DELTA_THREADS), 0, stream, E->T, a, n, E->ckpt_ts,
                        W.d_bc);
-    hipLaunchKernelGGL(tb_delta_scan_blocks, dim3(1), dim3(1024), 0, E->stream, W.d_bc, nblocks, W.d_base,
+    hipLaunchKernelGGL(tb_delta_scan_blocks, dim3(1), dim3(1024), 0, stream, W.d_bc, nblocks, W.d_base,
                        W.d_cnt + WB_RECORDS);
-    hipLaunchKernelGGL(tb_delta_log_scatter, dim3((unsigned)nblocks), dim3(DELTA_THREADS), 0, E->stream, E->T, a, n,
+    hipLaunchKernelGGL(tb_delta_log_scatter, dim3((unsigned)nblocks), dim3(DELTA_THREADS), 0, stream, E->T, a, n,
                        E->ckpt_ts, W.d_base, want_records ? W.d_out : (u8*)nullptr, W.d_ids, W.d_pv, W.d_cnt + WB_PV);
     if (posted) {  // a node's pending transfer may live on another shard: the node looks it up
-        hipLaunchKernelGGL(tb_delta_posted, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T, W.d_pv,
+        hipLaunchKernelGGL(tb_delta_posted, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, E->T, W.d_pv,
                            W.d_cnt + WB_PV, W.d_pairs, W.d_cnt + WB_STATUS);
     }
     HIPCK(hipGetLastError());
@@ -1910,14 +1911,11 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
     W.counts.created_after = E->ckpt_ts;
     if ((st = wb_next_epoch(E))) return st;
     HIPCK(hipMemsetAsync(W.d_cnt, 0, WB_COUNT_WORDS * 8, E->stream));
-    // In stream order (the next commits follow): the log range's records and account ids, and each
-    // account's slot and balances as of the bar (tb_delta_capture).
-    if ((st = wb_gather_slice(E, E->ckpt_pos, E->log_next, true))) return st;
-    const u64 n_ids = 2 * range;
-    if (n_ids) {
-        hipLaunchKernelGGL(tb_delta_capture, dim3((unsigned)((n_ids + 255) / 256)), dim3(256), 0, E->stream, E->T, W.d_ids,
-                           n_ids, E->ckpt_mark, E->ckpt_epoch, W.d_slots, W.d_cap, W.d_cnt + WB_SLOTS,
-                           W.d_cnt + WB_RECORDS);
+    // In stream order (the next commits follow): each account the bar's log range names, its slot and
+    // its balances as of the bar (tb_delta_capture_log).
+    if (range) {
+        hipLaunchKernelGGL(tb_delta_capture_log, dim3((unsigned)((2 * range + 255) / 256)), dim3(256), 0, E->stream, E->T,
+                           E->ckpt_pos, range, E->ckpt_mark, E->ckpt_epoch, W.d_slots, W.d_cap, W.d_cnt + WB_SLOTS);
     }
     const u64 nl = E->ckpt_ids.size() / 2;
     if (nl) {  // the listed ids cross in the same stream order (their host copy lives until then)
@@ -1928,9 +1926,11 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
     }
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(W.captured, E->stream));
-    // Beside the next commits, on the write-back stream: the records, the emission, the snapshot.
+    // Beside the next commits, on the write-back stream: the records (the log range is immutable
+    // now), the emission, the snapshot.
     const u64 ts0 = E->ckpt_ts;
     HIPCK(hipStreamWaitEvent(W.stream, W.captured, 0));
+    if ((st = wb_gather_slice(E, E->ckpt_pos, E->log_next, true, true, W.stream))) return st;
     hipLaunchKernelGGL(tb_delta_emit, dim3(1024), dim3(256), 0, W.stream, E->T, E->ckpt_bal, ts0, W.d_slots, W.d_cap,
                        W.d_cnt + WB_SLOTS, W.d_acc, W.d_before, W.d_cnt + WB_ACCOUNTS);
     hipLaunchKernelGGL(tb_delta_advance_from, dim3(1024), dim3(256), 0, W.stream, E->ckpt_bal, W.d_slots, W.d_cap,

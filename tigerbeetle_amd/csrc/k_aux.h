@@ -300,6 +300,33 @@ __global__ __launch_bounds__(256) void tb_delta_capture(Tables T, const u64* ids
     }
 }
 
+// The same capture from the log range itself, without the gather's liveness check (so it needs
+// nothing the gather computes): the debit and credit account of every record at [pos0, pos0 + n).  A
+// record that did not commit (a failed or withdrawn event's position) only adds accounts whose
+// balances did not change, which the emission drops (unless created since, which is listed anyway).
+__global__ __launch_bounds__(256) void tb_delta_capture_log(Tables T, u64 pos0, u64 n, u32* mark, u32 epoch, u32* slots,
+                                                            AccountBal* cap, u64* slot_count) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // record i / 2, side i % 2
+    u32 slot = TB_NOT_FOUND;
+    if (i < 2 * n) {
+        const u64* w = (const u64*)&T.xlog[pos0 + (i >> 1)] + 2 + 2 * (i & 1);  // debit @16, credit @32
+        const u64 lo = w[0], hi = w[1];
+        if (!tb_id_reserved(lo, hi)) slot = tb_account_find(T, lo, hi);
+    }
+    u32 was = epoch;
+    AccountBal b{};
+    if (slot != TB_NOT_FOUND) {
+        was = atomicExch(&mark[slot], epoch);
+        b = T.acct_bal[slot];
+    }
+    const bool first = was != epoch;
+    const u64 si = tb_wave_claim(first, slot_count);
+    if (first) {
+        slots[si] = slot;
+        cap[si] = b;
+    }
+}
+
 __global__ __launch_bounds__(256) void tb_delta_emit(Tables T, const AccountBal* snap, u64 ts0, const u32* slots,
                                                      const AccountBal* cap, const u64* slot_count, u8* out,
                                                      AccountBal* before, u64* count) {
