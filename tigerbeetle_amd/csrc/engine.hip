@@ -708,7 +708,12 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         INIT_CK(tbMalloc(&W.d_cap, W.cap_a * sizeof(AccountBal)));
         INIT_CK(tbMalloc(&W.d_cnt, WB_COUNT_WORDS * 8));
         INIT_CK(tbHostMalloc(&W.h_cnt, WB_COUNT_WORDS * 8, hipHostMallocDefault));
-        INIT_CK(hipStreamCreateWithFlags(&W.stream, hipStreamNonBlocking));
+        {   // the copy-out and the work beside the commits: the lowest priority, so the commits' kernels
+            // are dispatched first
+            int least = 0, greatest = 0;
+            INIT_CK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            INIT_CK(hipStreamCreateWithPriority(&W.stream, hipStreamNonBlocking, least));
+        }
         INIT_CK(tbEventCreateWithFlags(&W.gathered, hipEventDisableTiming));
         INIT_CK(tbEventCreateWithFlags(&W.done, hipEventDisableTiming));
         INIT_CK(tbEventCreateWithFlags(&W.read_done, hipEventDisableTiming));
@@ -1914,7 +1919,7 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
     // In stream order (the next commits follow): each account the bar's log range names, its slot and
     // its balances as of the bar (tb_delta_capture_log).
     if (range) {
-        hipLaunchKernelGGL(tb_delta_capture_log, dim3((unsigned)((2 * range + 255) / 256)), dim3(256), 0, E->stream, E->T,
+        hipLaunchKernelGGL(tb_delta_capture_log, dim3((unsigned)((range + 255) / 256)), dim3(256), 0, E->stream, E->T,
                            E->ckpt_pos, range, E->ckpt_mark, E->ckpt_epoch, W.d_slots, W.d_cap, W.d_cnt + WB_SLOTS);
     }
     const u64 nl = E->ckpt_ids.size() / 2;

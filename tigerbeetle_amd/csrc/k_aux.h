@@ -306,24 +306,42 @@ __global__ __launch_bounds__(256) void tb_delta_capture(Tables T, const u64* ids
 // balances did not change, which the emission drops (unless created since, which is listed anyway).
 __global__ __launch_bounds__(256) void tb_delta_capture_log(Tables T, u64 pos0, u64 n, u32* mark, u32 epoch, u32* slots,
                                                             AccountBal* cap, u64* slot_count) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // record i / 2, side i % 2
-    u32 slot = TB_NOT_FOUND;
-    if (i < 2 * n) {
-        const u64* w = (const u64*)&T.xlog[pos0 + (i >> 1)] + 2 + 2 * (i & 1);  // debit @16, credit @32
-        const u64 lo = w[0], hi = w[1];
-        if (!tb_id_reserved(lo, hi)) slot = tb_account_find(T, lo, hi);
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // one record: both accounts' chains together
+    u32 ds = TB_NOT_FOUND, cs = TB_NOT_FOUND;
+    if (i < n) {
+        const u64* w = (const u64*)&T.xlog[pos0 + i];
+        const u64 dlo = w[2], dhi = w[3], clo = w[4], chi = w[5];  // debit @16, credit @32
+        if (!tb_id_reserved(dlo, dhi) && !tb_id_reserved(clo, chi)) {
+            const u64 dpos = tb_hash_id(dlo, dhi) & T.account_mask, cpos = tb_hash_id(clo, chi) & T.account_mask;
+            const AccountHot d0 = T.acct_hot[dpos], c0 = T.acct_hot[cpos];
+            AccountHot dh, ch;
+            tb_account_find2(T, dlo, dhi, dpos, d0, clo, chi, cpos, c0, &ds, &cs, &dh, &ch);
+        } else {
+            if (!tb_id_reserved(dlo, dhi)) ds = tb_account_find(T, dlo, dhi);
+            if (!tb_id_reserved(clo, chi)) cs = tb_account_find(T, clo, chi);
+        }
+        if (cs == ds) cs = TB_NOT_FOUND;  // a garbage record naming one account twice
     }
-    u32 was = epoch;
-    AccountBal b{};
-    if (slot != TB_NOT_FOUND) {
-        was = atomicExch(&mark[slot], epoch);
-        b = T.acct_bal[slot];
+    u32 dw = epoch, cw = epoch;
+    AccountBal db{}, cb{};
+    if (ds != TB_NOT_FOUND) {
+        dw = atomicExch(&mark[ds], epoch);
+        db = T.acct_bal[ds];
     }
-    const bool first = was != epoch;
-    const u64 si = tb_wave_claim(first, slot_count);
-    if (first) {
-        slots[si] = slot;
-        cap[si] = b;
+    if (cs != TB_NOT_FOUND) {
+        cw = atomicExch(&mark[cs], epoch);
+        cb = T.acct_bal[cs];
+    }
+    const bool df = dw != epoch, cf = cw != epoch;
+    const u64 dsi = tb_wave_claim(df, slot_count);
+    if (df) {
+        slots[dsi] = ds;
+        cap[dsi] = db;
+    }
+    const u64 csi = tb_wave_claim(cf, slot_count);
+    if (cf) {
+        slots[csi] = cs;
+        cap[csi] = cb;
     }
 }
 
