@@ -121,6 +121,8 @@ struct WbBufs {
     // The copy-out in flight: regions (records, accounts, before, pairs) from HBM to the caller's
     // registered buffers, sent a slice per commit (wb_pump) once the gather's counts are known.
     bool copying = false, counts_known = false;
+    bool tail = false;            // the gather's work beside the commits is not enqueued yet (wb_tail)
+    u64 tail_pos0 = 0, tail_pos1 = 0, tail_ts0 = 0;
     const u8* src[4] = {};
     u8* dst[4] = {};
     u64 len[4] = {}, at[4] = {};
@@ -799,7 +801,7 @@ extern "C" int tbgpu_reset(tbgpu_t* E) {
     if (E->wb.inflight) {  // its copy-out finishes; its results are dropped with the state
         HIPCK(hipStreamSynchronize(E->stream));  // its gather
         HIPCK(hipStreamSynchronize(E->wb.stream));
-        E->wb.inflight = E->wb.copying = E->wb.counts_known = false;
+        E->wb.inflight = E->wb.copying = E->wb.counts_known = E->wb.tail = false;
     }
     E->ckpt_valid = false;
     E->ckpt_scan = false;
@@ -1931,20 +1933,12 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
     }
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(W.captured, E->stream));
-    // Beside the next commits, on the write-back stream: the records (the log range is immutable
-    // now), the emission, the snapshot.
-    const u64 ts0 = E->ckpt_ts;
-    HIPCK(hipStreamWaitEvent(W.stream, W.captured, 0));
-    if ((st = wb_gather_slice(E, E->ckpt_pos, E->log_next, true, true, W.stream))) return st;
-    hipLaunchKernelGGL(tb_delta_emit, dim3(1024), dim3(256), 0, W.stream, E->T, E->ckpt_bal, ts0, W.d_slots, W.d_cap,
-                       W.d_cnt + WB_SLOTS, W.d_acc, W.d_before, W.d_cnt + WB_ACCOUNTS);
-    hipLaunchKernelGGL(tb_delta_advance_from, dim3(1024), dim3(256), 0, W.stream, E->ckpt_bal, W.d_slots, W.d_cap,
-                       W.d_cnt + WB_SLOTS);
-    hipLaunchKernelGGL(tb_delta_order, dim3(256), dim3(256), 0, W.stream, W.d_out, W.d_cnt + WB_RECORDS, W.d_pairs,
-                       W.d_cnt + WB_PV, W.d_cnt + WB_ORDER);
-    HIPCK(hipGetLastError());
-    HIPCK(hipMemcpyAsync(W.h_cnt, W.d_cnt, WB_COUNT_WORDS * 8, hipMemcpyDeviceToHost, W.stream));
-    HIPCK(hipEventRecord(W.gathered, W.stream));
+    // The rest runs on the write-back stream beside the commits, enqueued by the next commit (wb_tail)
+    // so that it overlaps that commit's later kernels rather than the first one after the bar.
+    W.tail = true;
+    W.tail_pos0 = E->ckpt_pos;
+    W.tail_pos1 = E->log_next;
+    W.tail_ts0 = E->ckpt_ts;
     E->ckpt_pos = E->log_next;  // wb_advance's host part (the snapshot advances on the write-back stream)
     E->ckpt_ts = E->commit_ts;
     E->ckpt_scan = false;
@@ -1972,9 +1966,38 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
 // resolve, apply, flow and reply and the host's turn), sized to spread the bar's objects over about
 // WB_SLICE_CALLS commits.  The sizes come from the gather's counts, known once it completed.
 #define WB_SLICE_CALLS 56
+// The asynchronous write-back's work beside the commits, after the in-order capture (and `after`):
+// the records of the log range (immutable now), the emission, the snapshot's advance, the order
+// check, the counts back to the host.
+static int wb_tail(tbgpu* E, hipEvent_t after) {
+    WbBufs& W = E->wb;
+    W.tail = false;
+    HIPCK(hipStreamWaitEvent(W.stream, W.captured, 0));
+    if (after) HIPCK(hipStreamWaitEvent(W.stream, after, 0));
+    const u64 ts = E->ckpt_ts;  // wb_gather_slice reads the previous write-back's timestamp
+    E->ckpt_ts = W.tail_ts0;
+    const int st = wb_gather_slice(E, W.tail_pos0, W.tail_pos1, true, true, W.stream);
+    E->ckpt_ts = ts;
+    if (st) return st;
+    hipLaunchKernelGGL(tb_delta_emit, dim3(1024), dim3(256), 0, W.stream, E->T, E->ckpt_bal, W.tail_ts0, W.d_slots, W.d_cap,
+                       W.d_cnt + WB_SLOTS, W.d_acc, W.d_before, W.d_cnt + WB_ACCOUNTS);
+    hipLaunchKernelGGL(tb_delta_advance_from, dim3(1024), dim3(256), 0, W.stream, E->ckpt_bal, W.d_slots, W.d_cap,
+                       W.d_cnt + WB_SLOTS);
+    hipLaunchKernelGGL(tb_delta_order, dim3(256), dim3(256), 0, W.stream, W.d_out, W.d_cnt + WB_RECORDS, W.d_pairs,
+                       W.d_cnt + WB_PV, W.d_cnt + WB_ORDER);
+    HIPCK(hipGetLastError());
+    HIPCK(hipMemcpyAsync(W.h_cnt, W.d_cnt, WB_COUNT_WORDS * 8, hipMemcpyDeviceToHost, W.stream));
+    HIPCK(hipEventRecord(W.gathered, W.stream));
+    return TBGPU_STATUS_OK;
+}
+
 static int wb_pump(tbgpu* E, u64 budget, hipEvent_t after) {
     WbBufs& W = E->wb;
     if (!W.copying) return TBGPU_STATUS_OK;
+    if (W.tail) {
+        const int st = wb_tail(E, after);
+        if (st || budget != ~0ULL) return st;  // its counts come back by the next commit
+    }
     if (!W.counts_known) {
         if (budget != ~0ULL && hipEventQuery(W.gathered) != hipSuccess) return TBGPU_STATUS_OK;  // next call
         HIPCK(hipEventSynchronize(W.gathered));
