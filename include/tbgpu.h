@@ -201,8 +201,11 @@ int tbgpu_checkpoint_delta(tbgpu_t* engine, void* accounts_out, void* accounts_b
 
 /* The same write-back without the wait (StateMachine.compact is asynchronous,
  * src/state_machine.zig:542-567; the replica's compact stage, src/vsr/replica.zig:3088-3091): the
- * delta is taken in stream order with the commits (the next commits follow it) and crosses PCIe
- * into the caller's buffers beside them.  tbgpu_checkpoint_delta_wait returns the counts once the
+ * state it describes is captured in stream order with the commits (the accounts the bar's transfers
+ * name, with their balances; the next commits follow the capture), the rest is gathered on a
+ * low-priority stream beside them, and the objects cross PCIe into the caller's buffers by DMA,
+ * one slice after each one-prepare tbgpu_commit's body read (or all at the wait).
+ * tbgpu_checkpoint_delta_wait returns the counts once the
  * objects have landed (transfers and posted entries sorted as above); until then the buffers belong
  * to the engine, and no other write-back may start.  Needs buffers registered with
  * tbgpu_register_host and large enough for the bounds above; otherwise (or past one slice of the
