@@ -226,6 +226,8 @@ struct tbgpu {
 
     bool profile = false;
     bool kclock_off = false;
+    u64 api_calls = 0;        // entry points called on this handle (a node skips redundant drains by it)
+    u64* h_pub = nullptr;     // pinned staging word of a node's commit-timestamp push to this shard
     u32 legs_min = LEGS_MIN_EVENTS;
     u64 wall_khz = 0;  // device wall clock (flow phase timing)
     WbBufs wb;
@@ -276,6 +278,7 @@ static void ckpt_note_ids(tbgpu* E, const u8* records, u64 n);
 // stale staging copy.  `mutates`: refused on a poisoned engine (a device panic, tbgpu.h).
 static int api_enter(tbgpu* E, bool mutates) {
     E->pf_input = nullptr;
+    E->api_calls++;
     if (mutates && E->poisoned) {
         return fail(TBGPU_STATUS_PANIC, "engine stopped by an earlier device panic (tbgpu_reset or tbgpu_deinit it)");
     }
@@ -721,6 +724,7 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
         INIT_CK(tbEventCreateWithFlags(&W.read_done, hipEventDisableTiming));
         INIT_CK(tbEventCreateWithFlags(&W.captured, hipEventDisableTiming));
     }
+    INIT_CK(tbHostMalloc(&E->h_pub, 8, hipHostMallocDefault));
     INIT_CK(tbMalloc(&E->kclock, (u64)KCLOCK_SLOTS * KCLOCK_WORDS * 8));
     INIT_CK(tbHostMalloc(&E->h_kclock, (u64)KCLOCK_SLOTS * KCLOCK_WORDS * 8, hipHostMallocDefault));
     for (int i = 0; i < 16; i++) INIT_CK(tbEventCreate(&E->markers[i]));
@@ -777,6 +781,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
     if (E->h_results) (void)hipHostFree(E->h_results);
     if (E->h_rmeta) (void)hipHostFree(E->h_rmeta);
     if (E->h_kclock) (void)hipHostFree(E->h_kclock);
+    if (E->h_pub) (void)hipHostFree(E->h_pub);
     if (E->wb.h_cnt) (void)hipHostFree(E->wb.h_cnt);
     if (E->wb.stream) {
         (void)hipStreamSynchronize(E->wb.stream);

@@ -112,6 +112,8 @@ struct TbNode {
     u8* seq_codes = nullptr;     // [world * pe_src] the pass's dense codes from the sequencer
     u64* h_seq = nullptr;        // pinned scratch words
     u64 passes_clean = 0, passes_split = 0, passes_whole = 0, seq_events = 0;
+    const u64* api_calls = nullptr;  // the node handle's entry-point count (tbgpu::api_calls)
+    u64 drained_at = ~0ULL;          // its value when a create_transfers call last ended drained
 };
 
 static int node_fail_dev(const char* what, hipError_t e) {
@@ -362,9 +364,10 @@ static int node_publish_commit_ts(TbNode* N) {
         NCK(hipSetDevice(N->D[d].device));
         E->commit_ts = N->commit_ts;
         E->last_batch_ts = N->commit_ts;
-        E->h_meta[0] = N->commit_ts;  // staging word for the async copy (the stream is drained)
-        NCK(hipMemcpyAsync(&E->g->commit_timestamp, E->h_meta, 8, hipMemcpyHostToDevice, E->stream));
-        NCK(hipStreamSynchronize(E->stream));
+        // Not waited for: the shard's next work follows it on the stream, and a later push that
+        // overwrites the staging word before this copy runs only carries a newer timestamp.
+        *E->h_pub = N->commit_ts;
+        NCK(hipMemcpyAsync(&E->g->commit_timestamp, E->h_pub, 8, hipMemcpyHostToDevice, E->stream));
     }
     return TBGPU_STATUS_OK;
 }
@@ -952,8 +955,13 @@ static int node_commit_transfers(TbNode* N, u32 n, const u64* ts, const void* co
         P.k1 = k;
         passes.push_back(std::move(P));
     }
-    int st = node_sync(N);
-    if (st) return st;
+    // Drain the shards and read their bounds back — unless the previous call on this handle was a
+    // create_transfers call that ended drained (nothing ran since: its read-back still holds).
+    const bool drained = N->api_calls && *N->api_calls == N->drained_at + 1;
+    if (!drained) {
+        const int st0 = node_sync(N);
+        if (st0) return st0;
+    }
     h128 bound = node_bound(N);
     int status = TBGPU_STATUS_OK;
     const u32 NP = (u32)passes.size();
@@ -999,6 +1007,7 @@ static int node_commit_transfers(TbNode* N, u32 n, const u64* ts, const void* co
     const int s2 = node_sync(N);
     if (status == TBGPU_STATUS_OK) status = s2;
     const int s3 = node_publish_commit_ts(N);
+    if (status == TBGPU_STATUS_OK && s3 == TBGPU_STATUS_OK && N->api_calls) N->drained_at = *N->api_calls;
     return status ? status : s3;
 }
 
@@ -1136,6 +1145,7 @@ static int node_api_init(const tbgpu_config* config, tbgpu_t** out) {
     tbgpu* E = new tbgpu();
     E->cfg = *config;
     E->node = N;
+    N->api_calls = &E->api_calls;
     E->device = N->D[0].device;
     *out = E;
     return TBGPU_STATUS_OK;
