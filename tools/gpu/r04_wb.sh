@@ -14,4 +14,4 @@ done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/$O/replica_wb2 -o run --output-format csv -- \
   $R/tigerbeetle_amd/host/tb_replica_bench --accounts 1000000 --prepares 400 --write-back > /dev/null 2>&1 || exit 1
-cd $R && AB_VARIANTS="${AB:-r3val cur}" bash tools/gpu/r04_ab.sh
+cd $R && AB_VARIANTS="${AB:-cur}" bash tools/gpu/r04_ab.sh
