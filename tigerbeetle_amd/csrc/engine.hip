@@ -965,8 +965,8 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         if (P.legs || P.apply_late) {
             if ((st = prof_begin(E, &pp, K_APPLY))) return st;
             if (P.legs) {
-                hipLaunchKernelGGL(tb_apply_legs, dim3(E->leg_buckets + APPLY_EXTRA), dim3(APPLY_THREADS), (4u << E->leg_shift) * 8,
-                                   E->stream, P);
+                hipLaunchKernelGGL(tb_apply_legs, dim3(E->leg_buckets + APPLY_EXTRA), dim3(APPLY_THREADS),
+                                   tb_apply_lds_bytes(E->leg_shift, b1 - b0), E->stream, P);
             }
             if (n > 0 && !owner) {  // owner-partitioned: the owners apply the legs instead
                 const u32 grid = (u32)std::min<u64>((n + 255) / 256, P.legs ? 2048 : 1u << 20);

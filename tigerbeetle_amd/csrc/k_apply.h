@@ -115,16 +115,25 @@ __device__ static inline u32 tb_bucket_extras(u32 total) {
 // read-modify-writes.
 __device__ static inline void tb_apply_legs_body(const PassArgs& P, u64* s_acc);
 
+// Dynamic LDS: [4 << leg_shift] per (slot, field) sums, then the bucket's first leg in each prepare of
+// the pass and the exclusive prefix of the segment lengths (sized by the pass's prepares, not
+// LEG_PREPARES_MAX: at 2048 buckets of 1024 slots that keeps a workgroup under 40 KB, four per CU).
+__host__ __device__ static inline u32 tb_apply_lds_bytes(u32 leg_shift, u32 nb) {
+    return (4u << leg_shift) * 8 + (2 * nb + 1) * 4;
+}
+
 __global__ __launch_bounds__(APPLY_THREADS) void tb_apply_legs(PassArgs P) {
-    extern __shared__ u64 s_acc[];                  // [4 << leg_shift] per (slot, field) sum (dynamic)
+    extern __shared__ u64 s_acc[];
     tb_kclock_start(P, 2);
     tb_apply_legs_body(P, s_acc);
     tb_kclock_end(P, 2);
 }
 
 __device__ static inline void tb_apply_legs_body(const PassArgs& P, u64* s_acc) {
-    __shared__ u32 s_start[LEG_PREPARES_MAX];       // the bucket's first leg in each prepare
-    __shared__ u32 s_pref[LEG_PREPARES_MAX + 1];    // exclusive prefix of the segment lengths
+    const u32 W = 1u << P.leg_shift;
+    const u32 nb = P.b1 - P.b0;
+    u32* s_start = (u32*)(s_acc + 4 * W);           // [nb] the bucket's first leg in each prepare
+    u32* s_pref = s_start + nb;                     // [nb + 1] exclusive prefix of the segment lengths
     __shared__ u32 s_wave[APPLY_THREADS / 64];
     __shared__ u64 s_red[APPLY_THREADS / 64];
     __shared__ u32 s_pick[3];                       // extra workgroup: bucket, part; owner: its first extra index
@@ -169,8 +178,6 @@ __device__ static inline void tb_apply_legs_body(const PassArgs& P, u64* s_acc) 
         }
     }
 
-    const u32 W = 1u << P.leg_shift;
-    const u32 nb = P.b1 - P.b0;
     const u32 stride = NBK + 1;
     for (u32 k = threadIdx.x; k < 4 * W; k += APPLY_THREADS) s_acc[k] = 0;
 

@@ -22,6 +22,7 @@ k = r["kernels"]; dk = dr.get("kernels", {})
 print(sys.argv[2], "value %.1f" % (d["value"] / 1e6), "head validate %.4f resolve %.4f apply %.4f" % (
     k["tb_transfers_validate"]["avg_launch_ms"], k.get("tb_resolve<129>", {}).get("avg_launch_ms", 0),
     k.get("tb_apply_legs", {}).get("avg_launch_ms", 0)), "dev validate", dk.get("tb_transfers_validate"),
+    "dev resolve/apply", dk.get("tb_resolve<129>"), dk.get("tb_apply_legs"),
     "dev value %.2f G/s" % (d.get("device_resident", {}).get("value", 0) / 1e9))
 PY
 done
