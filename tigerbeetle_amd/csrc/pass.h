@@ -139,7 +139,9 @@ enum : u32 { CERT_EXT_U128 = 1, CERT_EXT_U64 = 2 };
 #define LEG_PREPARES_MAX 1024
 #define LEG_SPLIT_MIN 65536  // tb_apply_legs splits a bucket with at least this many legs in the pass
 #define LEGS_MIN_EVENTS (1u << 18)  // smaller passes apply balances with atomics (engine.hip)
+#ifndef APPLY_THREADS  // -DAPPLY_THREADS=... builds an A/B variant (tools/gpu/r04_ab.sh)
 #define APPLY_THREADS 256
+#endif
 // Leg word: ((slot within its bucket) << 2 | balance field (BAL_OFF / 16)) << LEG_AMT_BITS | amount.
 // An amount of 2^LEG_AMT_BITS or more is applied by the resolve kernel with an atomic instead.
 #define LEG_AMT_BITS 52  // leaves 12 bits: slot-in-bucket (<= 10, LEG_SLOTS_MAX) + field (2)
