@@ -4,34 +4,31 @@ Workload (BASELINE.json configs[1], "C2"): 1M accounts, 100M uniform-random tran
 no flags), prepares of 8190 events, synthetic data generated on the GPU (tigerbeetle_amd
 k_workload.h, shapes of the reference benchmark client src/benchmark.zig:223-327).
 
-A step = committing all 100M transfers (12,211 prepares) from the post-account-creation state, as
-the metric defines it: from the first H2D to the last reply D2H.  The prepare
-bodies sit in host memory registered once (the replica's message pool); tbgpu_commit_pipelined
-moves chunk c+1 (64 prepares) over PCIe while chunk c commits, and each chunk's replies land in
-host memory as soon as it is committed.  Between steps the transfer store and balances are
-restored (untimed), so every step commits the same 100M transfers.  Each timed step is bracketed
-by a barrier + torch.cuda.synchronize(); value = transfers committed by all ranks / Σ step time
-(max over ranks).  `device_resident` is the same commit with the prepares already in HBM (the
-engine's own rate, no PCIe); `pcie` is the host-link rate the headline reaches.
+A step = committing all 100M transfers (12,211 prepares) from the post-account-creation state.
+`value` is measured with the prepare bodies already resident in HBM when the timed region starts
+(tbgpu_commit_device_async, passes of --pass-batches prepares; replies written to HBM): the engine's
+own rate.  Between steps the transfer store and balances are restored (untimed), so every step
+commits the same 100M transfers.  Each timed step is bracketed by a barrier + torch.cuda.synchronize();
+value = transfers committed by all ranks / sum of step times (max over ranks).  `host_path` is the
+same commit from registered host memory (tbgpu_commit_pipelined: chunk c+1 crosses PCIe while chunk c
+commits, replies back in host memory): the replica's batched call, PCIe both ways inside its timing.
 
---gpus N (torchrun): BASELINE.json configs[4] ("C5"), one process per GPU over RCCL
-(tigerbeetle_amd.sharded): 100M accounts, whose immutable fields every rank holds and
-whose balances live on their owner GPU (hash of the id); every rank submits its own 125M transfers
-(1B over 8 GPUs) from pinned host memory, and every pass routes each transfer to its home GPU with
-an all-to-all over xGMI, commits it there, sends its balance legs to the accounts' owners (all-to-all)
-and the result codes back to the source (all-to-all).  The global prepare order of a pass is
-rank-major.  Per-GPU work is fixed as N grows: scaling is weak.
+--gpus N: BASELINE.json configs[4] ("C5") on one tbgpu node engine over the N GPUs (run_node): 100M
+accounts hash-partitioned by owner, 125M uniform transfers per GPU (1B over 8), the prepares resident
+in their source GPU's HBM for `value` (host memory for `host_path`).  Per-GPU work is fixed as N
+grows: scaling is weak.
 
 The JSON line also carries:
   roofline      the dominant kernel's algorithmic bytes per launch / its average launch time
-                (HIP events on the engine stream, inside the timed steps) against 8 TB/s;
-                `traffic` (HBM bytes per launch) comes from perf/pmc_r04.json (rocprofv3 PMC passes,
-                tools/gpu/r04_prof.sh), with rocprof's mean launch time of the same kernel beside it.
+                (device clock, inside the timed steps) against 8 TB/s; `traffic` (HBM bytes per
+                launch) comes from the PMC_FILE (rocprofv3 PMC passes), with rocprof's mean launch
+                time of the same kernel beside it.
   cpu_baseline  the C oracle (reference semantics restated, single thread) timed on this host on
                 a bounded prefix of the same workload.
-  parity        the same prefix committed on the GPU from a fresh state and compared with the
-                oracle byte for byte (replies, every account, every transfer); for the full run,
-                every reply empty, no dependent event, debits == credits in total.
+  parity        the same prefix committed on the GPU from a fresh state through the timed path (and
+                through the host path) and compared with the oracle byte for byte (replies, every
+                account, every transfer); for the full run, every reply empty, no dependent event,
+                debits == credits in total.
 """
 import argparse
 import ctypes
@@ -47,6 +44,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 ctypes_u8 = ctypes.c_uint8
+U64_ALL = np.uint64(0xFFFFFFFFFFFFFFFF)
 METRIC = "transfers/sec committed (whole node, bit-exact results) + p99 batch latency"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 PCIE_PEAK_GBS = 63.0   # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s spec
@@ -73,7 +71,8 @@ def parse():
     p.add_argument("--chunk-prepares", type=int, default=None,
                    help="prepares per pipelined chunk (host memory -> PCIe -> commit -> reply); default per "
                         "workload: CHUNK_PREPARES")
-    p.add_argument("--device-steps", type=int, default=3, help="timed steps of the HBM-resident secondary leg")
+    p.add_argument("--host-steps", type=int, default=3,
+                   help="timed steps of the host path (prepares in registered host memory, PCIe inclusive; 0: skip)")
     p.add_argument("--secondary", type=int, default=10_000_000,
                    help="transfers of the C3 / C4 secondary lines (0: skip)")
     p.add_argument("--cpu-sample", type=int, default=12_285_000, help="transfers in the CPU baseline / parity sample (0: skip)")
@@ -328,8 +327,7 @@ def run_secondary(args, kind, device):
     # The ordered fallback (tb_flow) has no byte roofline (it is bound by its dependency rounds):
     # the roofline is the validate kernel's; tb_flow's time share is reported beside it.
     roof = roofline(stats, expected_unique(n_acct, 2 * per_launch) / per_launch, per_launch,
-                    argparse.Namespace(transfers=n_xfer, steps=1), step_ms[0], None, kernel="tb_transfers_validate",
-                    pmc=False)
+                    argparse.Namespace(transfers=n_xfer, steps=1), step_ms[0], None, kernel="tb_transfers_validate")
     roof["flow_ms_share"] = round(stats["ms_replay"] / step_ms[0], 4)
 
     # Parity: the first 1M transfers (the same prepares, same timestamps) on a fresh engine.
@@ -590,19 +588,13 @@ def main():
                               limit_permille=wl["limit_permille"], hot_limited=wl.get("hot_limited", 0))
     engine.sync()
 
-    # -- headline: the replica's batched commit from host memory (PCIe both ways) --------------
-    # throughput = transfers / wall time from the first H2D to the last reply D2H.
-    # The prepares sit in host memory registered once (the replica's message pool), and
-    # tbgpu_commit_pipelined moves chunk c+1 over PCIe while chunk c commits.
-    host_events = engine.to_host(events_dev, args.transfers * 128)
-    engine.register_host(host_events)
-    replies = np.empty(args.transfers * 8, dtype=np.uint8)
-    step_ms, lat_all = [], []
-    rb_h = np.zeros(1, dtype=np.uint32)
+    # -- headline: the prepares already resident in HBM (the measurement rule: inputs in HBM when
+    # the timed region starts), tbgpu_commit_device_async in passes of pass_batches prepares.  Each
+    # step commits all of them from the post-account-creation state; bracketed by barrier + sync.
+    step_ms = []
     t_cursor = t_end
+    engine.profile_mask(engine.PROF_ALL)  # warmup: every kernel's HIP-event time (the breakdown)
     breakdown = None
-    if args.warmup:
-        engine.profile_mask(engine.PROF_ALL)
     for step in range(args.warmup + args.steps):
         timed = step >= args.warmup
         engine.reset_transfers()
@@ -611,22 +603,79 @@ def main():
             if args.warmup:
                 breakdown = engine.stats()
             engine.reset_stats()
-            engine.profile_mask(engine.PROF_APPLY | engine.PROF_REPLAY)  # validate on the device clock only
+            # validate on the device clock only (no HIP event pair inside its span); whole passes
+            # timed for the batch latency
+            engine.profile_mask(engine.PROF_APPLY | engine.PROF_PASS | engine.PROF_REPLAY)
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        rb_h, _, lat = engine.commit_pipelined(129, ts, xfer_lens, host_events, chunk_batches=args.chunk_prepares,
-                                               latency=True, replies=replies)
+        engine.commit_device_async(129, ts, xfer_lens, events_dev, res_dev, rb_dev)
+        engine.sync()
         torch.cuda.synchronize()
         barrier()
         dt = time.perf_counter() - t0
         if timed:
             step_ms.append(allmax(dt * 1e3))
-            lat_all.append(lat)
     stats = engine.stats()
-    n_failed_host = int(rb_h.sum()) // 8
-    engine.unregister_host(host_events)
-    del host_events
+    pass_lat = engine.pass_latencies()
+    rb = engine.to_host(rb_dev, len(xfer_lens) * 4).view(np.uint32)
+    n_failed = int(rb.sum()) // 8
+
+    # -- the host path: the same prepares from registered host memory, PCIe both ways (the replica's
+    # batched call, tbgpu_commit_pipelined: chunk c+1 crosses PCIe while chunk c commits) ---------
+    host_path = None
+    n_failed_host = n_failed
+    if args.host_steps:
+        host_events = engine.to_host(events_dev, args.transfers * 128)
+        engine.register_host(host_events)
+        replies = np.empty(args.transfers * 8, dtype=np.uint8)
+        h_ms, lat_all = [], []
+        engine.profile_mask(engine.PROF_ALL)
+        h_breakdown = None
+        for step in range(1 + args.host_steps):
+            engine.reset_transfers()
+            ts, t_cursor = timestamps(xfer_lens, t_cursor + 10, wl["gap_every"])
+            if step == 1:
+                h_breakdown = engine.stats()
+                engine.reset_stats()
+                engine.profile_mask(engine.PROF_APPLY | engine.PROF_REPLAY)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rb_h, _, lat = engine.commit_pipelined(129, ts, xfer_lens, host_events, chunk_batches=args.chunk_prepares,
+                                                   latency=True, replies=replies)
+            torch.cuda.synchronize()
+            if step >= 1:
+                h_ms.append((time.perf_counter() - t0) * 1e3)
+                lat_all.append(lat)
+        h_stats = engine.stats()
+        n_failed_host = int(rb_h.sum()) // 8
+        engine.unregister_host(host_events)
+        del host_events
+        h_total = sum(h_ms)
+        h_lat = np.sort(np.concatenate(lat_all))
+        n_val = (h_stats.get("span_launches") or [0])[0] or h_stats["launches_validate"]
+        per_launch_h = args.transfers / max(1, n_val / args.host_steps)
+        u_h = expected_unique(args.accounts, 2 * per_launch_h) / per_launch_h
+        pcie_gbs = args.transfers * 128 * args.host_steps / (h_total / 1e3) / 1e9
+        host_path = {
+            "value": round(args.transfers * args.host_steps / (h_total / 1e3), 1), "unit": "transfers/s",
+            "steps": args.host_steps, "warmup": 1, "ms_per_step": round(h_total / args.host_steps, 3),
+            "chunk_prepares": args.chunk_prepares,
+            "definition": "tbgpu_commit_pipelined from registered host memory (the replica's message pool): PCIe "
+                          "H2D of the bodies and the reply D2H inside the timed region, %d-prepare chunks, 3 in flight"
+                          % args.chunk_prepares,
+            "p99_batch_latency_ms": round(ref_percentile(h_lat, 99), 3),
+            "batch_latency_ms": dict(deciles(h_lat), definition=(
+                "per prepare, submit to reply: from the start of its chunk's PCIe copy to its reply landing in host "
+                "memory (device clock); percentiles by src/benchmark.zig:454-471")),
+            "pcie": {"h2d_bytes_per_transfer": 128, "achieved": round(pcie_gbs, 2), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(pcie_gbs / PCIE_PEAK_GBS, 4), "measured_ceiling": PCIE_MEASURED_GBS,
+                     "frac_of_measured": round(pcie_gbs / PCIE_MEASURED_GBS, 4),
+                     "note": "host link (PCIe Gen5 x16, MI355X_MICROARCH.md): the bound of this path"},
+            "roofline": roofline(h_stats, u_h, per_launch_h, argparse.Namespace(transfers=args.transfers,
+                                                                                steps=args.host_steps),
+                                 h_total, h_breakdown, kernel="tb_transfers_validate", pmc_leg="headline"),
+        }
     write_back = None
     if rank == 0 and world == 1 and args.write_back and args.workload == "c2":
         at_full, t_cursor = run_write_back(engine, args, t_cursor)
@@ -636,86 +685,49 @@ def main():
                                     "clock: device work + D2H of the changed objects into registered buffers; "
                                     "ms_per_bar over the bars after the first (which allocates the buffers)",
                       "at_stored": [at_full, at_empty]}
-    lat = np.sort(np.concatenate(lat_all)) if lat_all else np.array([float("nan")])
 
-    # -- secondary: the same commits with the prepares already resident in HBM ----------------
-    dev_ms = []
-    engine.profile_mask(engine.PROF_ALL)  # first (untimed) step: every kernel's HIP-event time
-    dev_stats = dev_breakdown = None
-    for step in range(1 + args.device_steps if args.device_steps else 0):
-        engine.reset_transfers()
-        ts, t_cursor = timestamps(xfer_lens, t_cursor + 10, wl["gap_every"])
-        if step == 1:
-            dev_breakdown = engine.stats()
-            engine.reset_stats()
-            engine.profile_mask(engine.PROF_APPLY | engine.PROF_PASS | engine.PROF_REPLAY)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        engine.commit_device_async(129, ts, xfer_lens, events_dev, res_dev, rb_dev)
-        engine.sync()
-        torch.cuda.synchronize()
-        if step >= 1:
-            dev_ms.append((time.perf_counter() - t0) * 1e3)
-    if args.device_steps:
-        dev_stats = engine.stats()
-    pass_lat = engine.pass_latencies()
-
-    # -- full-run checks (size-independent properties) ---------------------------------------
+    # -- full-run checks (size-independent properties) of the last timed step ---------------------
+    # (the write-back leg committed other transfers since: re-run one untimed step to check them)
+    engine.reset_transfers()
+    ts, t_cursor = timestamps(xfer_lens, t_cursor + 10, wl["gap_every"])
+    engine.commit_device_async(129, ts, xfer_lens, events_dev, res_dev, rb_dev)
+    engine.sync()
     rb = engine.to_host(rb_dev, len(xfer_lens) * 4).view(np.uint32)
     accts = engine.export_accounts()
+    check_stats = engine.stats()
 
     def total(field):
         return sum(int(x) for x in accts[field + "_lo"]) + (sum(int(x) for x in accts[field + "_hi"]) << 64)
 
     dpost, cpost = total("debits_posted"), total("credits_posted")
-    n_failed = int(rb.sum()) // 8 if dev_ms else n_failed_host
     # C2: every transfer commits.  Every config: each committed transfer is one record; debits equal
     # credits in total, posted and pending.
-    full_ok = bool(stats["transfers"] == args.transfers - n_failed and dpost == cpost and dpost > 0
+    full_ok = bool(check_stats["transfers"] == args.transfers - n_failed and dpost == cpost and dpost > 0
                    and total("debits_pending") == total("credits_pending") and len(accts) == args.accounts
-                   and (n_failed == 0 or args.workload != "c2"))
+                   and (n_failed == 0 or args.workload != "c2") and int(rb.sum()) // 8 == n_failed
+                   and n_failed_host == n_failed)
 
     total_ms = sum(step_ms)
     n_total = args.transfers * world * args.steps
     value = n_total / (total_ms / 1e3)
-    full_ok = full_ok and n_failed_host == n_failed
 
-    # -- roofline: the dominant kernel of the headline's timed steps ---------------------------
-    n_val = (stats.get("span_launches") or [0])[0] or stats["launches_validate"]  # validate launches, timed steps
+    # -- roofline: the dominant kernel of the timed steps (validate, device clock) ----------------
+    n_val = (stats.get("span_launches") or [0])[0] or stats["launches_validate"]
     per_launch_transfers = args.transfers / max(1, n_val / max(1, args.steps))
     u_over_t = expected_unique(args.accounts, 2 * per_launch_transfers) / per_launch_transfers
     # The ordered fallback (tb_flow) has no byte roofline (its dependency rounds bound it): the
     # roofline is the validate kernel's, with tb_flow's share of the time beside it.
-    roof = roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown, kernel="tb_transfers_validate")
+    roof = roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown, kernel="tb_transfers_validate",
+                    pmc_leg="device")
     if roof is not None and args.workload != "c2":
         roof["flow_ms_share"] = round(stats["ms_replay"] / total_ms, 4)
-    pcie_gbs = args.transfers * 128 * args.steps / (total_ms / 1e3) / 1e9
-    pcie = {"h2d_bytes_per_transfer": 128, "achieved": round(pcie_gbs, 2), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
-            "frac": round(pcie_gbs / PCIE_PEAK_GBS, 4),
-            "measured_ceiling": PCIE_MEASURED_GBS, "frac_of_measured": round(pcie_gbs / PCIE_MEASURED_GBS, 4),
-            "note": "host link (PCIe Gen5 x16, MI355X_MICROARCH.md); the bound of the PCIe-inclusive value"}
-    device_resident = None
-    if dev_ms:
-        dev_total = sum(dev_ms)
-        # validate launches of one step (its device-clock spans: no HIP events around it when timed)
-        n_val = dev_stats["span_launches"][0] or dev_stats["launches_validate"]
-        per_launch_dev = args.transfers / max(1, n_val / max(1, args.device_steps))
-        u_dev = expected_unique(args.accounts, 2 * per_launch_dev) / per_launch_dev
-        device_resident = {
-            "value": round(args.transfers * args.device_steps / (dev_total / 1e3), 1), "unit": "transfers/s",
-            "steps": args.device_steps, "ms_per_step": round(dev_total / args.device_steps, 3),
-            "pass_prepares": args.pass_batches,
-            "definition": "tbgpu_commit_device_async: the same prepares already resident in HBM (no PCIe)",
-            "roofline": roofline(dev_stats, u_dev, per_launch_dev, args, dev_total, dev_breakdown, steps=args.device_steps,
-                                 kernel="tb_transfers_validate", device=True),
-        }
 
     # -- the validate kernel against its own access pattern, measured live (rank 0, N=1) ------
     if rank == 0 and world == 1 and args.access_mix and roof and roof["kernel"] == "tb_transfers_validate":
         roof["access_mix"] = access_mix(engine, per_launch_transfers, roof["avg_launch_ms"])
-        if device_resident and device_resident["roofline"]:
-            dr = device_resident["roofline"]
-            dr["access_mix"] = access_mix(engine, per_launch_dev, dr["avg_launch_ms"])
+        if host_path and host_path["roofline"]:
+            hr = host_path["roofline"]
+            hr["access_mix"] = access_mix(engine, hr["transfers_per_launch"], hr["avg_launch_ms"])
 
     # -- CPU baseline + bit-exact sample parity (rank 0, N=1 only) ---------------------------
     cpu = None
@@ -724,26 +736,38 @@ def main():
         sample_lens = batches(min(args.cpu_sample, args.transfers), args.batch)
         sample_ts, t_cursor = timestamps(sample_lens, t_cursor + 10, wl["gap_every"])
         cpu, oracle, expected = run_cpu_baseline(engine, args, acct_lens, acct_ts, events_dev, sample_lens, sample_ts)
-        # The sample goes through the headline's own timed path: tbgpu_commit_pipelined from
-        # registered host memory in chunks of chunk_prepares.
+        n_sample = sum(sample_lens)
+
+        def got_replies(rb, results):
+            got, off = [], 0
+            for L, nb in zip(sample_lens, rb):  # sparse replies at the prepare's event offset
+                got.append(bytes(results[off * 8:off * 8 + int(nb)]))
+                off += L
+            return got
+
+        # 1. The headline's own timed path: the sample resident in HBM, tbgpu_commit_device_async.
         engine.reset_transfers()
-        sample_host = engine.to_host(events_dev, sum(sample_lens) * 128)
+        engine.commit_device_async(129, sample_ts, sample_lens, events_dev, res_dev, rb_dev)
+        engine.sync()
+        rb = engine.to_host(rb_dev, len(sample_lens) * 4).view(np.uint32)
+        results = engine.to_host(res_dev, n_sample * 8)
+        acc_equal = engine.export_accounts().tobytes() == oracle.export_accounts().tobytes()
+        xfer_equal = engine.export_transfers(cap=n_sample).tobytes() == oracle.export_transfers().tobytes()
+        parity.update({"sample_transfers": n_sample, "replies_equal": got_replies(rb, results) == expected,
+                       "accounts_equal": acc_equal, "transfers_equal": xfer_equal,
+                       "sample_path": "tbgpu_commit_device_async, %d-prepare passes (the timed path)" % args.pass_batches})
+        # 2. The host path: tbgpu_commit_pipelined from registered host memory.
+        engine.reset_transfers()
+        sample_host = engine.to_host(events_dev, n_sample * 128)
         engine.register_host(sample_host)
         rb, results, _ = engine.commit_pipelined(129, sample_ts, sample_lens, sample_host,
                                                  chunk_batches=args.chunk_prepares)
         engine.unregister_host(sample_host)
         del sample_host
-        got, off = [], 0
-        for L, nb in zip(sample_lens, rb):  # sparse replies at the prepare's event offset
-            got.append(bytes(results[off * 8:off * 8 + int(nb)]))
-            off += L
-        replies_equal = got == expected
-        acc_equal = engine.export_accounts().tobytes() == oracle.export_accounts().tobytes()
-        xfer_equal = engine.export_transfers(cap=sum(sample_lens)).tobytes() == oracle.export_transfers().tobytes()
-        parity.update({"sample_transfers": sum(sample_lens), "replies_equal": replies_equal,
-                       "accounts_equal": acc_equal, "transfers_equal": xfer_equal,
-                       "sample_path": "tbgpu_commit_pipelined from registered host memory, %d-prepare chunks "
-                                      "(the timed path)" % args.chunk_prepares})
+        parity["host_path_sample_equal"] = bool(
+            got_replies(rb, results) == expected
+            and engine.export_accounts().tobytes() == oracle.export_accounts().tobytes()
+            and engine.export_transfers(cap=n_sample).tobytes() == oracle.export_transfers().tobytes())
         cpu.pop("seconds")
 
     host = None
@@ -764,7 +788,7 @@ def main():
         for kind in ("c3", "c3h", "c4"):
             secondary[kind] = run_secondary(args, kind, local_rank)
 
-    pass_lat = np.array(pass_lat) if len(pass_lat) else np.array([float("nan")])
+    pass_lat = np.sort(np.array(pass_lat)) if len(pass_lat) else np.array([float("nan")])
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -777,18 +801,18 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u128",
-        "data": "synthetic (generated on the GPU in the reference benchmark's shapes, copied to host memory before timing)",
+        "data": "synthetic (generated on the GPU in the reference benchmark's shapes, resident in HBM before timing)",
         "config": {"workload": WORKLOAD_TEXT[args.workload] % (args.accounts, args.transfers, args.batch),
-                   "prepares_per_step": len(xfer_lens), "chunk_prepares": args.chunk_prepares,
-                   "input": "prepare bodies in registered host memory; PCIe H2D and reply D2H inside the timed region",
+                   "prepares_per_step": len(xfer_lens), "pass_prepares": args.pass_batches,
+                   "input": "prepare bodies resident in HBM when the timed region starts (tbgpu_commit_device_async); "
+                            "replies written to HBM; the PCIe-inclusive rate is `host_path`",
                    "host_numa_node": args.numa_node, "parallelism": "single"},
-        "p99_batch_latency_ms": round(ref_percentile(lat, 99), 3),
-        "batch_latency_ms": dict(deciles(lat), definition=(
-            "per prepare, submit to reply: from the start of its chunk's PCIe copy to its reply landing in host "
-            "memory (device clock; %d-prepare chunks, 3 in flight); percentiles by src/benchmark.zig:454-471"
-            % args.chunk_prepares)),
-        "pcie": pcie,
-        "device_resident": device_resident,
+        "p99_batch_latency_ms": round(ref_percentile(pass_lat, 99), 3),
+        "batch_latency_ms": dict(deciles(pass_lat), definition=(
+            "per prepare, commit to reply: its device pass's duration (a prepare's reply is complete when its "
+            "%d-prepare pass is; device clock, HIP events around each pass); percentiles by "
+            "src/benchmark.zig:454-471" % args.pass_batches)),
+        "host_path": host_path,
         "dependent_events": stats["dependent_events"],
         "flow": {k: (round(stats[k], 3) if isinstance(stats[k], float) else stats[k])
                  for k in ("flow_units", "flow_runs", "flow_run_units", "flow_plan_ms", "flow_run_ms", "bounds_passes",
@@ -796,7 +820,7 @@ def main():
                            "sweep_ms", "sweep_loop_ms", "sweep_wait_ms", "flow_exec_ms", "walk_segments",
                            "walk_heavy", "walk_heavy_positions", "walk_heavy_windows", "walk_heavy_stops",
                            "walk_heavy_blocks", "walk_heavy_blocked_ms", "walk_longest", "walk_crit_windows",
-                               "walk_crit_blocks", "walk_crit_wait_ms", "walk_crit_ms")},
+                           "walk_crit_blocks", "walk_crit_wait_ms", "walk_crit_ms")},
         "flow_phases_ms": flow_phases(stats),
         "failed_events": n_failed,
         "roofline": roof,
@@ -814,7 +838,8 @@ def main():
     line["parity"] = parity
     line["headline"] = {"value": line["value"], "unit": "transfers/s", "p99_batch_latency_ms": line["p99_batch_latency_ms"],
                         "roofline_frac": roof["frac"] if roof else None,
-                        "roofline_traffic": roof.get("traffic") if roof else None}
+                        "roofline_traffic": roof.get("traffic") if roof else None,
+                        "host_path_value": host_path["value"] if host_path else None}
     if rank == 0:
         print(json.dumps(line), flush=True)
     engine.close()
@@ -945,7 +970,7 @@ def run_sharded(args, world, rank, local_rank):
     value = args.transfers * world * args.steps / (total_ms / 1e3)
     recv_per_launch = args.transfers / max(1, stats["launches_validate"] / max(1, args.steps))
     u_over_t = expected_unique(args.accounts, 2 * recv_per_launch) / recv_per_launch
-    roof = roofline(stats, u_over_t, recv_per_launch, args, total_ms, pmc=False)
+    roof = roofline(stats, u_over_t, recv_per_launch, args, total_ms)
     pcie_gbs = args.transfers * 128 * args.steps / (total_ms / 1e3) / 1e9
     line = {
         "metric": METRIC,
@@ -1008,10 +1033,16 @@ def numa_cpus(device):
 def run_node(args, procs, rank):
     """--gpus N (engine "node"): BASELINE.json configs[4] ("C5") on ONE tbgpu node engine over the N
     GPUs — the handle a replica binds (include/tbgpu.h tbgpu_config.devices, csrc/node.h): 100M
-    accounts (records replicated, balances on their owner GPU), 125M uniform transfers per GPU (1B
-    over 8), every pass of N x chunk prepares routed across the GPUs inside the library (each GPU pulls
-    its block of prepares over its own PCIe link, routes it, homes gather their transfers from the
-    sources' HBM over xGMI, owners pull their balance legs, sources pull their result codes).
+    accounts hash-partitioned by owner, 125M uniform transfers per GPU (1B over 8), every pass of N x
+    chunk prepares routed across the GPUs inside the library (homes gather their transfers from the
+    sources over xGMI, owners pull their balance legs, sources pull their result codes).
+
+    `value`: the prepares resident in their source GPU's HBM when the timing starts (block d of every
+    pass generated on GPU d, read in place by its route kernels), replies back in host memory.
+    `host_path`: the same prepares from registered host memory on each GPU's NUMA node, PCIe inside.
+    `parity`: one full pass (N x chunk prepares) committed from a fresh state through the timed path
+    and compared byte for byte with the oracle, which holds exactly the accounts the sample touches
+    (generator records with their create timestamps); then the full-run properties.
 
     Under torchrun (WORLD_SIZE = N, the driver's launch) rank 0 drives the node and the other ranks
     only take part in the step barriers and the max-over-ranks timing (gloo: they touch no GPU)."""
@@ -1035,8 +1066,11 @@ def run_node(args, procs, rank):
         dist.destroy_process_group()
         return
 
-    from tests.harness.configs import KINDS, SETTINGS
+    from tests.harness.configs import KINDS, SETTINGS, split
+    from tests.harness.oracle import OracleEngine
+    from tigerbeetle_amd import _lib
     from tigerbeetle_amd.state_machine import Engine, Options
+    from tigerbeetle_amd.types import ACCOUNT_DTYPE, TRANSFER_DTYPE
 
     wl = SETTINGS[args.workload]
     N = args.gpus
@@ -1045,14 +1079,41 @@ def run_node(args, procs, rank):
     T = args.transfers * N
     engine = Engine(Options(accounts_max=args.accounts, transfers_max=T, pass_events_max=chunk * args.batch,
                             pass_batches_max=chunk, devices=tuple(devices), profile=bool(args.profile)))
-    engine.profile_mask(engine.PROF_VALIDATE | engine.PROF_REPLAY)
+    shards = [engine.shard(d) for d in range(N)]
+    gen_kw = dict(seed=args.seed, kind=KINDS[args.workload], limit_permille=wl["limit_permille"],
+                  hot_limited=wl.get("hot_limited", 0))
 
-    # Accounts: generated on the first GPU in chunks, committed from host memory (every shard commits
-    # every create_accounts prepare: the records are replicated).
+    # Prepare k of pass p = k // (N chunk) belongs to source GPU d = (k mod N chunk) // chunk.
+    lens = batches(T, args.batch)
+    n_prep = len(lens)
+    per_pass = N * chunk
+    src_of = (np.arange(n_prep) % per_pass) // chunk
+    starts = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+
+    # The parity sample: the first pass, its transfers generated once on the host side.
+    n_sample_prep = min(n_prep, per_pass) if args.cpu_sample > 0 else 0
+    n_sample = int(starts[n_sample_prep])
+    sample_x = None
+    sample_idx = np.zeros(0, dtype=np.uint64)
+    if n_sample:
+        gen = engine.alloc(n_sample * 128)
+        engine.generate_transfers(gen, 0, n_sample, args.accounts, **gen_kw)
+        sample_x = engine.to_host(gen, n_sample * 128)
+        engine.free(gen)
+        x = sample_x.view(TRANSFER_DTYPE)
+        # account ids are IdPermutation.inversion: maxInt(u128) - (index + 1), one high word
+        assert (x["debit_account_id_hi"] == U64_ALL).all() and (x["credit_account_id_hi"] == U64_ALL).all()
+        lo = np.unique(np.concatenate([x["debit_account_id_lo"], x["credit_account_id_lo"]]))
+        sample_idx = np.uint64(U64_ALL - 1) - lo
+
+    # Accounts: generated on the first GPU in chunks, committed from host memory; the oracle gets the
+    # sample's accounts as created (generator record + create timestamp).
     acct_lens = batches(args.accounts, args.batch)
     acct_ts, t_end = timestamps(acct_lens, 1_000_000_000)
+    a_lens_arr, a_ts_arr = np.asarray(acct_lens, dtype=np.uint64), np.asarray(acct_ts, dtype=np.uint64)
     a_chunk = 2048 * args.batch
     dev_buf = engine.alloc(a_chunk * 128)
+    oracle_accts = []
     for a0 in range(0, args.accounts, a_chunk):
         n_a = min(a_chunk, args.accounts - a0)
         engine.generate_accounts(dev_buf, a0, n_a, seed=args.seed, limit_permille=wl["limit_permille"],
@@ -1062,93 +1123,154 @@ def run_node(args, procs, rank):
         lens_a = batches(n_a, args.batch)
         rb, _, _ = engine.commit_pipelined(128, acct_ts[k0:k0 + len(lens_a)], lens_a, host, chunk_batches=chunk)
         assert int(rb.sum()) == 0, "account creation returned errors"
+        sel = sample_idx[(sample_idx >= a0) & (sample_idx < a0 + n_a)]
+        if len(sel):
+            recs = host.view(ACCOUNT_DTYPE)[(sel - np.uint64(a0)).astype(np.int64)].copy()
+            k = (sel // np.uint64(args.batch)).astype(np.int64)
+            recs["timestamp"] = a_ts_arr[k] - a_lens_arr[k] + np.uint64(1) + sel % np.uint64(args.batch)
+            oracle_accts.append(recs)
     engine.free(dev_buf)
 
-    # Transfers: prepare k of pass p = k // (N chunk) goes to source GPU d = (k mod N chunk) // chunk
-    # (tbgpu_config.devices: block d of a pass); each GPU's prepares sit in host memory on its own
-    # NUMA node, registered once (the replica's message pool).
-    lens = batches(T, args.batch)
-    n_prep = len(lens)
-    per_pass = N * chunk
-    src_of = (np.arange(n_prep) % per_pass) // chunk
-    starts = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
-    x_chunk = max(1, (1 << 24) // args.batch) * args.batch  # whole prepares per generation chunk
-    gen = engine.alloc(min(T, x_chunk) * 128)
-    buffers, ptrs = [], np.zeros(n_prep, dtype=np.uint64)
-    nodes = []
+    # Transfers: source d's prepares back to back in d's HBM (every pass's block d in turn), generated
+    # there; the host path's copy on d's NUMA node, registered once (the replica's message pool).
+    dptrs, hptrs = np.zeros(n_prep, dtype=np.uint64), np.zeros(n_prep, dtype=np.uint64)
+    dbufs, hbufs, nodes = [], [], []
     for d in range(N):
         mine = np.nonzero(src_of == d)[0]
         n_ev = int(sum(lens[k] for k in mine))
-        node, cpus = numa_cpus(devices[d])
-        nodes.append(node)
-        old_aff = os.sched_getaffinity(0)
-        if cpus:
-            os.sched_setaffinity(0, cpus)
-        buf = np.empty(max(n_ev, 1) * 128, dtype=np.uint8)
-        buf[::4096] = 0  # first touch from this GPU's NUMA node
-        if cpus:
-            os.sched_setaffinity(0, old_aff)
-        off = 0
-        for k in mine:
-            ptrs[k] = buf.ctypes.data + off * 128
-            off += lens[k]
-        buffers.append(buf)
-    # Fill: the global transfer sequence, generated in chunks, scattered prepare by prepare.
-    k_pos = 0
-    for x0 in range(0, T, x_chunk):
-        n_x = min(x_chunk, T - x0)
-        engine.generate_transfers(gen, x0, n_x, args.accounts, seed=args.seed, kind=KINDS[args.workload],
-                                  limit_permille=wl["limit_permille"], hot_limited=wl.get("hot_limited", 0))
-        host = engine.to_host(gen, n_x * 128)
-        while k_pos < n_prep and starts[k_pos + 1] <= x0 + n_x:
-            a, b = int(starts[k_pos]) - x0, int(starts[k_pos + 1]) - x0
-            dst = np.frombuffer((ctypes_u8 * ((b - a) * 128)).from_address(int(ptrs[k_pos])), dtype=np.uint8)
-            dst[:] = host[a * 128:b * 128]
-            k_pos += 1
-        assert k_pos == n_prep or starts[k_pos] >= x0 + n_x, "prepares straddle a generation chunk"
-    engine.free(gen)
-    for buf in buffers:
-        engine.register_host(buf)
+        dbuf = shards[d].alloc(max(n_ev, 1) * 128)
+        dbufs.append(dbuf)
+        off, i = 0, 0
+        while i < len(mine):  # runs of consecutive prepares (one block of a pass) in one launch
+            j = i + 1
+            while j < len(mine) and mine[j] == mine[j - 1] + 1:
+                j += 1
+            k0, k1 = int(mine[i]), int(mine[j - 1]) + 1
+            for k in range(k0, k1):
+                dptrs[k] = dbuf + (off + int(starts[k] - starts[k0])) * 128
+            shards[d].generate_transfers(dbuf + off * 128, int(starts[k0]), int(starts[k1] - starts[k0]), args.accounts,
+                                         **gen_kw)
+            off += int(starts[k1] - starts[k0])
+            i = j
+        if args.host_steps:
+            node, cpus = numa_cpus(devices[d])
+            nodes.append(node)
+            old_aff = os.sched_getaffinity(0)
+            if cpus:
+                os.sched_setaffinity(0, cpus)
+            buf = np.empty(max(n_ev, 1) * 128, dtype=np.uint8)
+            buf[::4096] = 0  # first touch from this GPU's NUMA node
+            if cpus:
+                os.sched_setaffinity(0, old_aff)
+            _lib.check(engine.lib.tbgpu_copy_to_host(shards[d].h, buf.ctypes.data, ctypes.c_void_p(dbuf), n_ev * 128))
+            hbufs.append(buf)
+            hptrs[np.nonzero(src_of == d)[0]] = dptrs[src_of == d] - np.uint64(dbuf) + np.uint64(buf.ctypes.data)
     replies = np.empty(T * 8, dtype=np.uint8)
 
-    step_ms, lat_all = [], []
-    t_cursor = t_end
-    rb = None
-    for step in range(n_steps):
-        timed = step >= args.warmup
-        engine.reset_transfers()
-        ts, t_cursor = timestamps(lens, t_cursor + 10, wl["gap_every"])
-        if timed and step == args.warmup:
-            engine.reset_stats()
-        barrier()
-        t0 = time.perf_counter()
-        rb, lat = engine.commit_pipelined_ptrs(129, ts, lens, ptrs, replies, chunk_batches=chunk, latency=True)
-        dt = time.perf_counter() - t0
-        barrier()
-        if timed:
-            step_ms.append(dt * 1e3)
-            lat_all.append(lat)
+    def run_steps(ptrs, warmup, steps, t_cursor):
+        ms, lat_all, rb = [], [], None
+        for step in range(warmup + steps):
+            timed = step >= warmup
+            engine.reset_transfers()
+            ts, t_cursor = timestamps(lens, t_cursor + 10, wl["gap_every"])
+            if step == 0:
+                engine.profile_mask(engine.PROF_ALL)
+            if timed and step == warmup:
+                engine.reset_stats()
+                engine.profile_mask(engine.PROF_APPLY | engine.PROF_REPLAY)  # validate on the device clock
+            barrier()
+            t0 = time.perf_counter()
+            rb, lat = engine.commit_pipelined_ptrs(129, ts, lens, ptrs, replies, chunk_batches=chunk, latency=True)
+            dt = time.perf_counter() - t0
+            barrier()
+            if timed:
+                ms.append(dt * 1e3)
+                lat_all.append(lat)
+        return ms, np.sort(np.concatenate(lat_all)) if lat_all else np.array([float("nan")]), rb, t_cursor
+
+    # -- value: device-resident prepares --------------------------------------------------------
+    step_ms, lat, rb, t_cursor = run_steps(dptrs, args.warmup, args.steps, t_end)
     stats = engine.stats()
     t = torch.tensor(step_ms, dtype=torch.float64)
     if procs > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    step_ms = [float(x) for x in t.tolist()]
-    summ = engine.ledger_summary()
-    for buf in buffers:
-        engine.unregister_host(buf)
+    step_ms = [float(v) for v in t.tolist()]
     n_failed = int(rb.sum()) // 8
+    summ = engine.ledger_summary()
     full_ok = bool((n_failed == 0 or args.workload != "c2") and stats["transfers"] == T - n_failed
                    and summ["debits_posted"] == summ["credits_posted"] and summ["debits_posted"] > 0
                    and summ["debits_pending"] == summ["credits_pending"] and summ["stray"] == 0
                    and summ["accounts"] == args.accounts)
     total_ms = sum(step_ms)
     value = T * args.steps / (total_ms / 1e3)
-    lat = np.sort(np.concatenate(lat_all)) if lat_all else np.array([float("nan")])
-    per_launch = T / max(1, stats["launches_validate"] / max(1, args.steps))
+    n_val = (stats.get("span_launches") or [0])[0] or stats["launches_validate"]
+    per_launch = T / max(1, n_val / max(1, args.steps))
     u_over_t = expected_unique(args.accounts, 2 * per_launch) / per_launch
     roof = roofline(stats, u_over_t, per_launch, argparse.Namespace(transfers=T, steps=args.steps), total_ms,
-                    kernel="tb_transfers_validate", pmc=False)
-    pcie_gbs = T * 128 * args.steps / (total_ms / 1e3) / 1e9
+                    kernel="tb_transfers_validate")
+    passes = {"clean": stats["node_passes_clean"], "split": stats["node_passes_split"],
+              "whole": stats["node_passes_whole"], "sequenced_events": stats["node_sequenced_events"]}
+
+    # -- host path: the same prepares from registered host memory -------------------------------
+    host_path = None
+    if args.host_steps:
+        for buf in hbufs:
+            engine.register_host(buf)
+        h_ms, h_lat, h_rb, t_cursor = run_steps(hptrs, 1, args.host_steps, t_cursor)
+        h_stats = engine.stats()
+        for buf in hbufs:
+            engine.unregister_host(buf)
+        h_summ = engine.ledger_summary()
+        full_ok = full_ok and int(h_rb.sum()) == int(rb.sum()) and h_summ == summ
+        h_total = sum(h_ms)
+        pcie_gbs = T * 128 * args.host_steps / (h_total / 1e3) / 1e9
+        n_hv = (h_stats.get("span_launches") or [0])[0] or h_stats["launches_validate"]
+        per_launch_h = T / max(1, n_hv / args.host_steps)
+        host_path = {
+            "value": round(T * args.host_steps / (h_total / 1e3), 1), "unit": "transfers/s", "steps": args.host_steps,
+            "warmup": 1, "ms_per_step": round(h_total / args.host_steps, 3),
+            "definition": "the same prepares in registered host memory on each GPU's NUMA node (%s), PCIe H2D and "
+                          "replies inside the timed region" % nodes,
+            "p99_batch_latency_ms": round(ref_percentile(h_lat, 99), 3),
+            "pcie": {"achieved_per_gpu": round(pcie_gbs / N, 2), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(pcie_gbs / N / PCIE_PEAK_GBS, 4), "measured_ceiling": PCIE_MEASURED_GBS,
+                     "frac_of_measured": round(pcie_gbs / N / PCIE_MEASURED_GBS, 4)},
+            "roofline": roofline(h_stats, expected_unique(args.accounts, 2 * per_launch_h) / per_launch_h, per_launch_h,
+                                 argparse.Namespace(transfers=T, steps=args.host_steps), h_total,
+                                 kernel="tb_transfers_validate"),
+        }
+
+    # -- parity: one full pass through the timed path against the oracle --------------------------
+    parity = {"full_run_properties": full_ok, "ledger": {k: str(v) for k, v in summ.items()}}
+    if n_sample:
+        oracle_accts = np.concatenate(oracle_accts)
+        assert len(oracle_accts) == len(sample_idx)
+        s_lens = lens[:n_sample_prep]
+        s_ts, t_cursor = timestamps(s_lens, t_cursor + 10, wl["gap_every"])
+        oracle = OracleEngine(len(oracle_accts) + 16, n_sample)
+        oracle.upsert_accounts(oracle_accts)
+        expected = oracle.commit_many(129, s_ts, split(sample_x, s_lens))
+        engine.reset_transfers()
+        rb_s, _ = engine.commit_pipelined_ptrs(129, s_ts, s_lens, dptrs[:n_sample_prep], replies, chunk_batches=chunk)
+        got, off = [], 0
+        for L, nb in zip(s_lens, rb_s):
+            got.append(bytes(replies[off * 8:off * 8 + int(nb)]))
+            off += L
+        ids = np.stack([oracle_accts["id_lo"], oracle_accts["id_hi"]], axis=1)
+        mine, found = engine.fetch_accounts(ids)
+        theirs, _ = oracle.fetch_accounts(ids)
+        parity.update({
+            "sample_transfers": n_sample, "sample_prepares": n_sample_prep,
+            "sample_path": "one full pass (%d sources x %d prepares) from device-resident prepares (the timed path)"
+                           % (N, chunk),
+            "replies_equal": got == expected,
+            "accounts_equal": bool(found.all()) and mine.tobytes() == theirs.tobytes(),
+            "transfers_equal": engine.export_transfers(cap=n_sample).tobytes() == oracle.export_transfers().tobytes(),
+            "sample_failed_events": sum(len(r) for r in expected) // 8,
+        })
+    for dbuf, sh in zip(dbufs, shards):
+        sh.free(dbuf)
+
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -1161,34 +1283,34 @@ def run_node(args, procs, rank):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u128",
-        "data": "synthetic (generated on the GPU in the reference benchmark's shapes, copied to host memory before "
-                "timing)",
-        "config": {"workload": ("C5 (BASELINE.json configs[4]): %d accounts, balances owner-partitioned by hash(id) over "
-                                "%d GPUs (records replicated), %d uniform transfers per GPU (%d in all), prepares of %d"
+        "data": "synthetic (generated on the GPUs in the reference benchmark's shapes, resident in each source GPU's "
+                "HBM before timing)",
+        "config": {"workload": ("C5 (BASELINE.json configs[4]): %d accounts hash-partitioned by owner over %d GPUs, %d "
+                                "uniform transfers per GPU (%d in all), prepares of %d"
                                 % (args.accounts, N, args.transfers, T, args.batch)) if args.workload == "c2" else
                                ("%s on %d GPUs: " % (args.workload, N)) + WORKLOAD_TEXT[args.workload] % (
                                    args.accounts, T, args.batch),
                    "prepares_per_step": n_prep, "chunk_prepares_per_gpu": chunk,
                    "engine": "one tbgpu node engine (include/tbgpu.h tbgpu_config.devices = %s), driven by one "
                              "process; %d process(es) launched" % (devices, procs),
-                   "input": "prepare bodies in registered host memory on each GPU's NUMA node (%s); PCIe H2D and "
-                            "replies inside the timed region" % nodes,
+                   "input": "prepare bodies resident in their source GPU's HBM (block d of every pass on GPU d); "
+                            "replies into host memory; the PCIe-inclusive rate is `host_path`",
                    "parallelism": "shard%d (transfer home = hash(id), balance legs to owner GPUs, peer reads over "
                                   "xGMI inside the library)" % N},
         "p99_batch_latency_ms": round(ref_percentile(lat, 99), 3),
         "batch_latency_ms": dict(deciles(lat), definition=(
-            "per prepare, submit to reply: from the start of its block's PCIe copy to its reply landing in host "
+            "per prepare, submit to reply: from the start of its pass on its source GPU to its reply landing in host "
             "memory (device clock of its source GPU); percentiles by src/benchmark.zig:454-471")),
-        "pcie": {"achieved_per_gpu": round(pcie_gbs / N, 2), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
-                 "frac": round(pcie_gbs / N / PCIE_PEAK_GBS, 4), "measured_ceiling": PCIE_MEASURED_GBS,
-                 "frac_of_measured": round(pcie_gbs / N / PCIE_MEASURED_GBS, 4)},
         "failed_events": n_failed,
-        "passes": {"clean": stats["node_passes_clean"], "split": stats["node_passes_split"],
-                   "whole": stats["node_passes_whole"], "sequenced_events": stats["node_sequenced_events"]},
+        "passes": passes,
         "roofline": roof,
+        "host_path": host_path,
         "cpu_baseline": None,
-        "parity": {"full_run_properties": full_ok, "ledger": {k: str(v) for k, v in summ.items()}},
+        "parity": parity,
     }
+    line["headline"] = {"value": line["value"], "unit": "transfers/s", "p99_batch_latency_ms": line["p99_batch_latency_ms"],
+                        "roofline_frac": roof["frac"] if roof else None,
+                        "host_path_value": host_path["value"] if host_path else None}
     print(json.dumps(line), flush=True)
     engine.close()
     if procs > 1:
@@ -1215,7 +1337,7 @@ def access_mix(engine, transfers, kernel_ms):
 
 
 def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=None, steps=None, kernel=None,
-             device=False, pmc=True):
+             pmc_leg=None):
     """The dominant kernel of the timed steps against the HBM peak; `kernels` = every kernel's mean
     launch time (from the warmup steps when given: the timed steps time only validate, replay/flow
     and whole passes)."""
@@ -1268,8 +1390,8 @@ def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=No
            "avg_launch_ms": round(avg_ms, 4), "avg_launch_ms_hip_events": round(hip_avg, 4) if hip_avg else None,
            "transfers_per_launch": round(per_launch_transfers, 1),
            "alg_bytes_per_transfer": round(alg_bytes / per_launch_transfers, 1), "timing": timing}
-    if pmc:  # the C2 launches the PMC runs profiled (not the C3/C4 lines)
-        out.update(load_pmc("device" if device else "headline", dom, per_launch_transfers))
+    if pmc_leg:  # the C2 launches the PMC runs profiled (not the C3/C4 lines)
+        out.update(load_pmc(pmc_leg, dom, per_launch_transfers))
     if out.get("rocprof_avg_launch_ms"):
         # The same definition from the committed rocprof summary: algorithmic bytes per transfer x the
         # profiled launches' mean transfers / rocprof's mean launch duration.

@@ -140,7 +140,11 @@ int tbgpu_commit_many(tbgpu_t* engine, uint8_t operation, uint32_t n, const uint
  * committed.  Bodies in memory registered with tbgpu_register_host (or otherwise pinned) move by
  * DMA; runs of address-contiguous prepares move as one copy.  Results are identical to N sequential
  * tbgpu_commit calls.  latency_ms (optional, N entries): per-prepare submit-to-reply time, from the
- * start of its chunk's PCIe copy to its reply landing in host memory (device clock). */
+ * start of its chunk's PCIe copy to its reply landing in host memory (device clock).
+ * On a node engine the bodies may also be in device memory (UVA pointers): a source shard's block of a
+ * pass whose prepares sit back to back in that shard's own HBM is read in place (the node's
+ * device-resident commit: prepares received or generated on each GPU), anything else is copied to it
+ * (from another GPU over xGMI).  Replies still land in the host `outputs`. */
 int tbgpu_commit_pipelined(tbgpu_t* engine, uint8_t operation, uint32_t n, const uint64_t* timestamps,
                            const void* const* inputs, const uint32_t* input_lens, void* const* outputs,
                            uint32_t* out_lens, uint32_t chunk_batches, double* latency_ms);

@@ -79,6 +79,12 @@ int tbgpu_bench_ledger_summary(tbgpu_t* engine, tbgpu_ledger_summary* out);
  * at any number of stored objects without first writing them all back. */
 int tbgpu_bench_checkpoint_mark(tbgpu_t* engine);
 
+/* A node engine's shard d (tbgpu_config.devices[d]) as an engine handle of its own, for the bench's
+ * per-GPU buffers: tbgpu_device_alloc / _free, tbgpu_copy_* and the generators on that handle work on
+ * shard d's device (the prepares of a device-resident node commit are generated in their source
+ * GPU's HBM).  Owned by the node: never tbgpu_deinit it, and commit only through the node. */
+int tbgpu_bench_node_shard(tbgpu_t* engine, uint32_t shard, tbgpu_t** out);
+
 /* Device memory helpers for callers without a device allocator (ctypes users). */
 int tbgpu_device_alloc(tbgpu_t* engine, uint64_t bytes, void** out);
 int tbgpu_device_free(tbgpu_t* engine, void* ptr);

@@ -152,3 +152,72 @@ def test_node_dirty_passes_split(config, shards, node_factory):
     st = engine.stats()
     assert st["node_passes_whole"] == 0 and st["node_passes_split"] > 0, st
     assert 0 < st["node_sequenced_events"] < n_xfer, st  # only the dependent subsequence is sequenced
+
+
+@pytest.mark.parametrize("shards", [2, 3])
+def test_node_device_resident_blocks(shards, node_factory):
+    """The node's device-resident commit (bench.py's `value` at N > 1): every source's prepares sit
+    back to back in its own HBM in pass-block order and its route kernels read them in place; the
+    same prepares from host memory, and from device memory in another block layout (copied), give the
+    oracle's bytes too."""
+    n_acc, n_xfer, batch, chunk = 5000, 200_000, 8190, 2
+    engine = node_factory(devices=(0,) * shards, accounts_max=n_acc, transfers_max=n_xfer,
+                          pass_events_max=chunk * batch, pass_batches_max=chunk)
+    accts, xfers = generate(engine, "c2", n_acc, n_xfer, seed=17 + shards)
+    x = xfers.view(TRANSFER_DTYPE).copy()
+    rng = np.random.default_rng(shards)
+    dup = rng.choice(np.arange(1000, n_xfer), 300, replace=False)
+    x["id_lo"][dup] = x["id_lo"][rng.integers(0, 900, 300)]
+    x["id_hi"][dup] = x["id_hi"][0]
+    xfers = x.view(np.uint8).reshape(-1)
+    a_lens, x_lens = batches(n_acc, batch), batches(n_xfer, batch)
+    a_ts, t = timestamps(a_lens, 10**12)
+    oracle = OracleEngine(n_acc, n_xfer)
+    assert all(r == b"" for r in oracle.commit_many(128, a_ts, split(accts, a_lens)))
+    rb, _, _ = engine.commit_pipelined(128, a_ts, a_lens, np.ascontiguousarray(accts), chunk_batches=chunk)
+    assert int(rb.sum()) == 0
+    n_prep = len(x_lens)
+    starts = np.concatenate([[0], np.cumsum(x_lens)]).astype(np.int64)
+    src_of = (np.arange(n_prep) % (shards * chunk)) // chunk
+    ptrs = np.zeros(n_prep, dtype=np.uint64)
+    bufs = []
+    for d in range(shards):
+        sh = engine.shard(d)
+        mine = np.nonzero(src_of == d)[0]
+        body = np.concatenate([xfers[starts[k] * 128:starts[k + 1] * 128] for k in mine]) if len(mine) else np.zeros(128, np.uint8)
+        dev = sh.alloc(body.nbytes)
+        sh.to_device(dev, body)
+        bufs.append((sh, dev))
+        off = 0
+        for k in mine:
+            ptrs[k] = dev + off * 128
+            off += x_lens[k]
+    replies = np.empty(n_xfer * 8, dtype=np.uint8)
+
+    def run(ptr_list, chunk_batches, t0):
+        engine.reset_transfers()
+        ts, _ = timestamps(x_lens, t0)
+        rb, _ = engine.commit_pipelined_ptrs(129, ts, x_lens, ptr_list, replies, chunk_batches=chunk_batches)
+        got, off = [], 0
+        for L, nb in zip(x_lens, rb):
+            got.append(bytes(replies[off * 8:off * 8 + int(nb)]))
+            off += L
+        return ts, got
+
+    try:
+        t0 = t + 10
+        ts, got = run(ptrs, chunk, t0)  # resident: every block read in place
+        o2 = OracleEngine(n_acc, n_xfer)
+        assert all(r == b"" for r in o2.commit_many(128, a_ts, split(accts, a_lens)))
+        expected = o2.commit_many(129, ts, split(xfers, x_lens))
+        assert got == expected and sum(len(r) for r in expected) > 0
+        assert_same_state(o2, engine)
+        t0 = ts[-1] + 10
+        ts, got = run(ptrs, chunk + 1, t0)  # other blocks: device bodies copied to the sources
+        o3 = OracleEngine(n_acc, n_xfer)
+        assert all(r == b"" for r in o3.commit_many(128, a_ts, split(accts, a_lens)))
+        assert got == o3.commit_many(129, ts, split(xfers, x_lens))
+        assert_same_state(o3, engine)
+    finally:
+        for sh, dev in bufs:
+            sh.free(dev)

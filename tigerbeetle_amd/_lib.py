@@ -164,6 +164,7 @@ SIGNATURES = [
     ("tbgpu_bench_access_mix", ctypes.c_int, [_P, _U64, ctypes.POINTER(ctypes.c_double)]),
     ("tbgpu_bench_ledger_summary", ctypes.c_int, [_P, ctypes.POINTER(tbgpu_ledger_summary)]),
     ("tbgpu_bench_checkpoint_mark", ctypes.c_int, [_P]),
+    ("tbgpu_bench_node_shard", ctypes.c_int, [_P, _U32, ctypes.POINTER(_P)]),
     ("tbgpu_device_alloc", ctypes.c_int, [_P, _U64, ctypes.POINTER(_P)]),
     ("tbgpu_device_free", ctypes.c_int, [_P, _P]),
     ("tbgpu_copy_to_host", ctypes.c_int, [_P, _P, _P, _U64]),

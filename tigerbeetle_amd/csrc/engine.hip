@@ -167,6 +167,7 @@ struct tbgpu {
     bool flow_ok = false;
     bool balances_set = false;
     u64 flow_capacity = 0;     // tb_flow workgroups the device holds at once (occupancy x CUs)
+    u32 flow_occ = 0;          // tb_flow workgroups per CU (its registers and LDS)
     bool dev_registered = false;
     FlowArgs F{};
 
@@ -415,6 +416,18 @@ static int residency_probe(tbgpu* E, u32 grid) {
     hipFuncAttributes attr{};
     size_t lds = 0;
     if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&tb_flow)) == hipSuccess) lds = attr.sharedSizeBytes;
+    // The probe uses almost no registers, so more of its workgroups than tb_flow's can share a CU.  The
+    // property to prove is that the CUs tb_flow's grid needs (grid / tb_flow's occupancy) are free: so
+    // the probe launches that many CUs' worth of ITS workgroups (grid x its occupancy / tb_flow's), all
+    // of which must become resident together.
+    lds = std::max<size_t>(lds, 4);
+    int probe_occ = 0;
+    if (E->flow_occ &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&probe_occ, reinterpret_cast<const void*>(&tb_residency_probe),
+                                                     FLOW_THREADS, lds) == hipSuccess &&
+        probe_occ > (int)E->flow_occ) {
+        grid = (u32)(((u64)grid * (u64)probe_occ + E->flow_occ - 1) / E->flow_occ);
+    }
     int st = TBGPU_STATUS_OK;
     u32 h[2] = {0, 0};
     hipError_t e = hipMemsetAsync(d, 0, 8, E->stream);
@@ -575,6 +588,7 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
             // tb_flow's grid barrier needs every workgroup resident: the grid is at most occupancy x
             // CUs, shared among the engines of this process on the device (flow_grid).
             E->flow_capacity = (u64)occ * prop.multiProcessorCount;
+            E->flow_occ = (u32)occ;
             E->F.grid = (u32)std::min<u64>(E->F.grid, E->flow_capacity);
             int khz = 0;
             if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, E->device) != hipSuccess) khz = 0;
@@ -799,6 +813,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
 }
 
 extern "C" int tbgpu_reset(tbgpu_t* E) {
+    API_ENTER(E, false);
     if (E->node) return node_api_reset(E->node);
     E->pf_input = E->pf_claim = nullptr;
     E->poisoned = false;
@@ -1345,12 +1360,12 @@ extern "C" int tbgpu_commit_pipelined(tbgpu_t* E, uint8_t operation, uint32_t n,
 
 extern "C" int tbgpu_commit(tbgpu_t* E, uint8_t operation, uint64_t timestamp, const void* input,
                             uint32_t input_len, void* output, uint32_t output_cap, uint32_t* out_len) {
-    if (E->node) return node_api_commit(E->node, operation, timestamp, input, input_len, output, output_cap, out_len);
     *out_len = 0;
     // The body tbgpu_prefetch staged (if any) may be taken by this commit only: hand it to
     // commit_host and drop it from the engine whatever happens next.
     const void* staged = E->pf_input;
-    API_ENTER(E, true);
+    API_ENTER(E, true);  // before the node hand-off too: a node keys its drain skipping on the count
+    if (E->node) return node_api_commit(E->node, operation, timestamp, input, input_len, output, output_cap, out_len);
     HIPCK(hipSetDevice(E->device));
     if (operation < OP_CREATE_ACCOUNTS || operation > OP_LOOKUP_TRANSFERS) {
         return fail(TBGPU_STATUS_INVALID, "unknown operation %u", operation);
@@ -1915,6 +1930,7 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
         W.h_cnt[WB_STATUS] = 0;
         W.out_t = nullptr;  // already sorted
         W.out_p = nullptr;
+        for (u32 r = 0; r < 4; r++) W.dst[r] = nullptr;  // nothing is copied into the caller's buffers later
         HIPCK(hipEventRecord(W.done, E->stream));
         W.inflight = true;
         return TBGPU_STATUS_OK;
@@ -2185,6 +2201,14 @@ extern "C" int tbgpu_bench_generate_transfers(tbgpu_t* E, void* out_dev, uint64_
     return TBGPU_STATUS_OK;
 }
 
+extern "C" int tbgpu_bench_node_shard(tbgpu_t* E, uint32_t shard, tbgpu_t** out) {
+    API_ENTER(E, false);
+    *out = nullptr;
+    if (!E->node || shard >= node_world(E->node)) return fail(TBGPU_STATUS_INVALID, "not a node shard");
+    *out = node_engine(E->node, shard);
+    return TBGPU_STATUS_OK;
+}
+
 extern "C" int tbgpu_bench_walk_merge_max(tbgpu_t* E, uint32_t segments) {
     API_ENTER(E, false);
     if (E->node) {
@@ -2349,11 +2373,25 @@ extern "C" int tbgpu_unregister_host(tbgpu_t* E, void* ptr) {
     API_ENTER(E, false);
     if (E->node) return node_api_unregister_host(E->node, ptr);
     HIPCK(hipSetDevice(E->device));
+    // A region an asynchronous write-back is still copying into belongs to the engine until
+    // tbgpu_checkpoint_delta_wait (tbgpu.h): refuse it rather than unpin pages under the DMA.
+    if (E->wb.inflight) {
+        for (const auto& r : E->host_regions) {
+            if (r.ptr != (const u8*)ptr) continue;
+            for (u32 k = 0; k < 4; k++) {
+                if (E->wb.dst[k] && E->wb.dst[k] >= r.ptr && E->wb.dst[k] < r.ptr + r.bytes) {
+                    return fail(TBGPU_STATUS_INVALID, "unregister: an asynchronous write-back is copying into this "
+                                                      "region (tbgpu_checkpoint_delta_wait first)");
+                }
+            }
+        }
+    }
     if (E->pending) {
         int st = engine_sync(E);
         if (st) return st;
     }
     HIPCK(hipStreamSynchronize(E->stream));
+    HIPCK(hipStreamSynchronize(E->wb.stream));  // no copy-out slice still in flight
     for (size_t i = 0; i < E->host_regions.size(); i++) {
         if (E->host_regions[i].ptr == (const u8*)ptr) {
             E->host_regions.erase(E->host_regions.begin() + i);

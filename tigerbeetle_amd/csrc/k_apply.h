@@ -141,7 +141,9 @@ __device__ static inline void tb_apply_legs_body(const PassArgs& P, u64* s_acc) 
     u128 S;
     bool cert_global, cert64;
     tb_pass_cert(P, S, cert_global, cert64);
-    if (!cert64 || TB_ABL(P, ABL_LEG_WORK)) return;  // the resolve kernel applied every leg with u128 atomics
+    // Without the 64-bit certificate the resolve kernel emitted no leg: every independent ok event is
+    // HZ_LATE and tb_apply_events adds it with u128 atomics.
+    if (!cert64 || TB_ABL(P, ABL_LEG_WORK)) return;
 
     const u32 NBK = P.leg_buckets;
     const bool owner = blockIdx.x < NBK;
@@ -251,9 +253,9 @@ __global__ __launch_bounds__(256) void tb_apply_events(PassArgs P) {
     tb_pass_cert(P, S, cert_global, cert64);  // every lane (a wave-wide sum)
     for (u32 pe = blockIdx.x * 256 + threadIdx.x; pe < P.n; pe += gridDim.x * 256) {
         const u32 info = P.info[pe];
-        if ((info & HZ_DEP) || (info & 0xFF) != R_OK || !(info & HZ_ACCTS)) continue;
-        // The resolve kernel's leg condition: those went to tb_apply_legs.
-        if (P.legs && cert64 && !(info & (HZ_POSTVOID | HZ_AMT_HI)) && P.amt[pe] <= LEG_AMT_MASK) continue;
+        // Exactly the events the resolve kernel marked: independent, ok, and not a balance leg (the
+        // legs went to tb_apply_legs) — one decision, made once, so no event is applied twice or never.
+        if (!(info & HZ_LATE) || (info & HZ_DEP) || (info & 0xFF) != R_OK || !(info & HZ_ACCTS)) continue;
         tb_apply_transfer(P, pe, info, P.eflags[pe], cert64);
     }
 }

@@ -374,13 +374,14 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
             const u32 code = info & 0xFF;
             const bool ok = valid & (code == R_OK);
             panic |= code == TB_CODE_PANIC;
-            if (valid) P.info[pe] = info | (ok ? HZ_EVAL_OK : 0);
+            const bool leg = use_legs && !(info & HZ_POSTVOID) && r_amt[k][1] == 0 && r_amt[k][0] <= LEG_AMT_MASK;
+            if (valid) P.info[pe] = info | (ok ? HZ_EVAL_OK : 0) | (ok && !leg ? HZ_LATE : 0);
             const u64 ts = P.routed ? (valid ? tb_event_ts(P, b, boff, L, i) : 0) : ts0 + i;
             tsmax = ok ? ts : tsmax;
             n_app += ok;
             n_fail += valid & !ok;
             if (ok) {
-                if (use_legs && !(info & HZ_POSTVOID) && r_amt[k][1] == 0 && r_amt[k][0] <= LEG_AMT_MASK) {
+                if (leg) {
                     const u32 drs = r_dr[k], crs = r_cr[k];
                     const u64 pend = (r_fl[k] & TF_PENDING) ? 0 : 1;  // field: pending / posted
                     const u32 mask = (1u << P.leg_shift) - 1;
@@ -436,12 +437,15 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
             if (!dep) {
                 if (fin == TB_CODE_PANIC) tb_panic(T.g, PANIC_ASSERT);
                 s_code[i] = (u8)fin;
-                P.info[pe] = (info & 0xFFFFFF00u) | fin | (eval_ok ? HZ_EVAL_OK : 0);
+                const bool leg = OP == OP_CREATE_TRANSFERS && use_legs && !(info & HZ_POSTVOID) && r_amt[k][1] == 0 &&
+                                 r_amt[k][0] <= LEG_AMT_MASK;
+                const bool late_ev = OP == OP_CREATE_TRANSFERS && fin == R_OK && !leg;
+                P.info[pe] = (info & 0xFFFFFF00u) | fin | (eval_ok ? HZ_EVAL_OK : 0) | (late_ev ? HZ_LATE : 0);
                 const u64 ts = P.routed ? tb_event_ts(P, b, boff, L, i) : ts0 + i;
                 if (eval_ok) tsmax = ts;  // increasing in i
                 if (fin == R_OK) {
                     if (OP == OP_CREATE_TRANSFERS) {
-                        if (use_legs && !(info & HZ_POSTVOID) && r_amt[k][1] == 0 && r_amt[k][0] <= LEG_AMT_MASK) {
+                        if (leg) {
                             const u32 drs = r_dr[k], crs = r_cr[k];
                             const u64 pend = (r_fl[k] & TF_PENDING) ? 0 : 1;  // field: pending / posted
                             const u32 mask = (1u << P.leg_shift) - 1;

@@ -42,6 +42,7 @@ struct NodeDev {
     hipStream_t rs = nullptr;   // route stream (plans); E->copy_stream: H2D; E->stream: the pass
     // Source side, by pass parity.
     u8* stage[2] = {};
+    const u8* ev[2] = {};        // the block's events this pass parity: stage[], or the caller's HBM
     u8* send[2] = {};
     u32* slot[2] = {};
     u8* home[2] = {};
@@ -114,6 +115,7 @@ struct TbNode {
     u64 passes_clean = 0, passes_split = 0, passes_whole = 0, seq_events = 0;
     const u64* api_calls = nullptr;  // the node handle's entry-point count (tbgpu::api_calls)
     u64 drained_at = ~0ULL;          // its value when a create_transfers call last ended drained
+    unsigned __int128 bound_carry = 0;  // the node's balance bound at that point (host-tracked)
 };
 
 static int node_fail_dev(const char* what, hipError_t e) {
@@ -422,6 +424,25 @@ static int node_commit_replicated(TbNode* N, u8 op, u32 n, const u64* ts, const 
 
 // -- create_transfers ----------------------------------------------------------------------------
 
+// Is source d's block of the pass already in d's HBM, its prepares back to back?  (Then the route
+// kernels read it in place: the node's device-resident commit, the prepares generated or received
+// on each GPU.)
+static bool node_block_resident(const NodeDev& D, const NodePass& P, u32 d, const void* const* inputs, const u32* lens) {
+    const NodeBlock& B = P.blk[d];
+    if (B.k1 == B.k0 || B.events == 0) return false;
+    const u8* base = (const u8*)inputs[B.k0];
+    for (u32 k = B.k0; k < B.k1; k++) {
+        if ((const u8*)inputs[k] != base + P.off[d][k - B.k0] * 128) return false;
+    }
+    hipPointerAttribute_t attr{};
+    if (hipPointerGetAttributes(&attr, base) != hipSuccess) {
+        (void)hipGetLastError();  // pageable host memory: not a HIP allocation
+        return false;
+    }
+    (void)lens;
+    return attr.type == hipMemoryTypeDevice && attr.device == D.device;
+}
+
 // H2D of source d's block of pass p and its route plan (enqueued; ev_planned[p & 1] fires when the
 // plan's words are in pinned host memory).
 static int node_issue_plan(TbNode* N, NodePass& P, u32 p, const u64* ts, const void* const* inputs, const u32* lens) {
@@ -437,16 +458,24 @@ static int node_issue_plan(TbNode* N, NodePass& P, u32 p, const u64* ts, const v
         u64* h_ts = h_off + nb + 1;
         for (u32 k = 0; k <= nb; k++) h_off[k] = P.off[d][k];
         for (u32 k = 0; k < nb; k++) h_ts[k] = ts[B.k0 + k];
-        // Copy stream: the bodies (runs of address-contiguous prepares as one DMA).
+        // The block's bodies.  Already in this device's HBM, back to back (a device-resident call):
+        // read where they are.  Otherwise the copy stream moves them (runs of address-contiguous
+        // prepares as one DMA; host memory over the device's own PCIe link, another device's HBM
+        // over xGMI).
         NCK(hipEventRecord(D.ev_start[p % 3], E->copy_stream));
-        for (u32 k = B.k0; k < B.k1;) {
-            u32 j = k + 1;
-            const u8* base = (const u8*)inputs[k];
-            u64 bytes = (u64)lens[k] * 128;
-            while (j < B.k1 && (const u8*)inputs[j] == base + bytes) bytes += (u64)lens[j++] * 128;
-            if (bytes) NCK(hipMemcpyAsync(D.stage[par] + P.off[d][k - B.k0] * 128, base, bytes, hipMemcpyHostToDevice,
-                                          E->copy_stream));
-            k = j;
+        D.ev[par] = D.stage[par];
+        if (node_block_resident(D, P, d, inputs, lens)) {
+            D.ev[par] = (const u8*)inputs[B.k0];
+        } else {
+            for (u32 k = B.k0; k < B.k1;) {
+                u32 j = k + 1;
+                const u8* base = (const u8*)inputs[k];
+                u64 bytes = (u64)lens[k] * 128;
+                while (j < B.k1 && (const u8*)inputs[j] == base + bytes) bytes += (u64)lens[j++] * 128;
+                if (bytes) NCK(hipMemcpyAsync(D.stage[par] + P.off[d][k - B.k0] * 128, base, bytes, hipMemcpyDefault,
+                                              E->copy_stream));
+                k = j;
+            }
         }
         NCK(hipEventRecord(D.ev_copied, E->copy_stream));
         // Route stream: wait for the buffers' previous users (pass p-2's gathers on every home and
@@ -460,7 +489,7 @@ static int node_issue_plan(TbNode* N, NodePass& P, u32 p, const u64* ts, const v
         NCK(hipMemcpyAsync(D.meta[par], h_off, (2 * (u64)nb + 1) * 8, hipMemcpyHostToDevice, D.rs));
         NCK(hipMemsetAsync(D.words[par], 0, ROUTE_WORDS * 8, D.rs));
         RouteArgs A{};
-        A.events = D.stage[par];
+        A.events = D.ev[par];
         A.n = (u32)B.events;
         A.nb = nb;
         A.batch_off = D.meta[par];
@@ -661,12 +690,13 @@ static int node_issue_replies(TbNode* N, NodePass& P, u32 p, const NodeRoute& RT
         }
         base += P.blk[s].events;
         NCK(hipEventRecord(D.ev_replied, E->stream));
-        if (nb) {
-            hipLaunchKernelGGL(tb_reply_out, dim3(nb), dim3(64), 0, E->stream, D.meta[par], nb, D.reply_bytes, D.results,
-                               E->g, D.d_arena[tri]);
-            NCK(hipGetLastError());
-            NCK(hipEventRecord(D.ev_done[tri], E->stream));
-        }
+        // Every shard's arena, with or without a block: its head carries the shard's panic word after
+        // its whole part of the pass (home commit, owner legs, replies: one stream), so consuming the
+        // pass reads every shard's verdict and the call needs no drain at its end.
+        hipLaunchKernelGGL(tb_reply_out, dim3(std::max<u32>(nb, 1)), dim3(64), 0, E->stream, D.meta[par], nb,
+                           D.reply_bytes, D.results, E->g, D.d_arena[tri]);
+        NCK(hipGetLastError());
+        NCK(hipEventRecord(D.ev_done[tri], E->stream));
     }
     P.issued = true;
     return TBGPU_STATUS_OK;
@@ -680,7 +710,6 @@ static int node_consume(TbNode* N, NodePass& P, u32 p, void* const* outputs, u32
         NodeDev& D = N->D[s];
         const NodeBlock& B = P.blk[s];
         const u32 nb = B.k1 - B.k0;
-        if (!nb) continue;
         NCK(hipSetDevice(D.device));
         NCK(hipEventSynchronize(D.ev_done[tri]));
         if (!take || status) continue;
@@ -688,7 +717,7 @@ static int node_consume(TbNode* N, NodePass& P, u32 p, void* const* outputs, u32
         const u32* rb = (const u32*)(D.h_arena[tri] + 16);
         const u8* res = D.h_arena[tri] + 16 + (u64)nb * 4;
         float ms = 0;
-        if (latency_ms) NCK(hipEventElapsedTime(&ms, D.ev_start[tri], D.ev_done[tri]));
+        if (latency_ms && nb) NCK(hipEventElapsedTime(&ms, D.ev_start[tri], D.ev_done[tri]));
         for (u32 k = B.k0; k < B.k1; k++) {
             const u32 bytes = rb[k - B.k0];
             if (bytes) memcpy(outputs[k], res + 8 * P.off[s][k - B.k0], bytes);
@@ -714,7 +743,7 @@ static int node_split_pass(TbNode* N, NodePass& P, u32 p, const u64* ts, u64 bou
     tbgpu* X = N->X;
     auto route_args = [&](NodeDev& D, const NodeBlock& B) {
         RouteArgs A{};
-        A.events = D.stage[par];
+        A.events = D.ev[par];
         A.n = (u32)B.events;
         A.nb = B.k1 - B.k0;
         A.batch_off = D.meta[par];
@@ -832,7 +861,7 @@ static int node_split_pass(TbNode* N, NodePass& P, u32 p, const u64* ts, u64 bou
     {
         u64 at = 0;
         for (u32 d = 0; d < W; d++) {
-            G.src[d] = N->D[d].stage[par];
+            G.src[d] = N->D[d].ev[par];
             G.dep[d] = N->D[d].dep;
             G.start[d] = at;
             at += P.blk[d].events;
@@ -956,13 +985,15 @@ static int node_commit_transfers(TbNode* N, u32 n, const u64* ts, const void* co
         passes.push_back(std::move(P));
     }
     // Drain the shards and read their bounds back — unless the previous call on this handle was a
-    // create_transfers call that ended drained (nothing ran since: its read-back still holds).
+    // create_transfers call that ended with nothing in flight and nothing ran since: its bound (the
+    // host-tracked sum, conservative) still holds.
     const bool drained = N->api_calls && *N->api_calls == N->drained_at + 1;
+    h128 bound = N->bound_carry;
     if (!drained) {
         const int st0 = node_sync(N);
         if (st0) return st0;
+        bound = node_bound(N);
     }
-    h128 bound = node_bound(N);
     int status = TBGPU_STATUS_OK;
     const u32 NP = (u32)passes.size();
     u32 next_consume = 0;
@@ -1004,10 +1035,20 @@ static int node_commit_transfers(TbNode* N, u32 n, const u64* ts, const void* co
         N->passes_clean++;
     }
     consume_upto(NP);
-    const int s2 = node_sync(N);
-    if (status == TBGPU_STATUS_OK) status = s2;
+    // Every pass consumed = every shard's stream past its last reply arena (node_issue_replies), every
+    // plan read: nothing is in flight and every shard's panic word was read.  The end-of-call drain
+    // stays only after a failure (plans issued ahead) or to collect profiling events.
+    bool profiling = false;
+    for (u32 d = 0; d < W; d++) profiling |= N->D[d].E->profile;
+    if (status != TBGPU_STATUS_OK || profiling) {
+        const int s2 = node_sync(N);
+        if (status == TBGPU_STATUS_OK) status = s2;
+    }
     const int s3 = node_publish_commit_ts(N);
-    if (status == TBGPU_STATUS_OK && s3 == TBGPU_STATUS_OK && N->api_calls) N->drained_at = *N->api_calls;
+    if (status == TBGPU_STATUS_OK && s3 == TBGPU_STATUS_OK && N->api_calls) {
+        N->drained_at = *N->api_calls;
+        N->bound_carry = bound;
+    }
     return status ? status : s3;
 }
 
@@ -1388,6 +1429,10 @@ static int node_api_get_stats(TbNode* N, tbgpu_stats* s) {
         s->sweep_u64_passes += x.sweep_u64_passes;
         s->flow_exec_ms += x.flow_exec_ms;
         for (int k = 0; k < 8; k++) s->flow_phase_ms[k] += x.flow_phase_ms[k];
+        for (int k = 0; k < 3; k++) {
+            s->span_ms[k] += x.span_ms[k];
+            s->span_launches[k] += x.span_launches[k];
+        }
         s->walk_segments += x.walk_segments;
         s->walk_heavy += x.walk_heavy;
         s->walk_heavy_positions += x.walk_heavy_positions;

@@ -31,6 +31,8 @@ enum : u32 {
     HZ_AMT_HI = 1u << 18,    // amt_hi[] holds the amount's high word (else it is zero, not written)
     HZ_REC = 1u << 19,       // kernel 1 wrote the event's record (timestamped, amount as given) at
                              // log_base + event, under its claimed entry rs[]
+    HZ_LATE = 1u << 20,      // tb_resolve: an independent ok create_transfers event that is not a
+                             // balance leg — tb_apply_events applies exactly these
 };
 
 #define SUM_SHARDS 64

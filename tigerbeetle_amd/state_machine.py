@@ -241,6 +241,9 @@ class Engine:
         engine keeps registered for DMA: valid only until the next write-back."""
         counts = _lib.tbgpu_delta_counts()
         caps = list(caps) if caps else [1024, 1024, 1024]
+        if getattr(self, "_wb_inflight", None) is not None:  # its buffers belong to the engine until the wait
+            raise _lib.EngineError(_lib.STATUS_INVALID, "an asynchronous write-back is in flight "
+                                                        "(checkpoint_delta_wait first)")
         while True:
             a, before, t, p = self._delta_buffers(caps, 0)
             st = self.lib.tbgpu_checkpoint_delta(self.h, a.ctypes.data, before.ctypes.data, caps[0], t.ctypes.data,
@@ -256,10 +259,14 @@ class Engine:
         """tbgpu_checkpoint_delta_async into one of two registered buffer sets of at least `caps`
         (accounts, transfers, posted) entries — size them for a bar, as the Zig wrapper does; the
         objects land while later commits run.  checkpoint_delta_wait() returns the Delta."""
-        self._wb_set = 1 - getattr(self, "_wb_set", 1)
-        a, before, t, p = self._delta_buffers(list(caps), self._wb_set)
+        if getattr(self, "_wb_inflight", None) is not None:  # never touch a set the engine may be copying into
+            raise _lib.EngineError(_lib.STATUS_INVALID, "an asynchronous write-back is in flight "
+                                                        "(checkpoint_delta_wait first)")
+        which = 1 - getattr(self, "_wb_set", 1)
+        a, before, t, p = self._delta_buffers(list(caps), which)
         _lib.check(self.lib.tbgpu_checkpoint_delta_async(self.h, a.ctypes.data, before.ctypes.data, caps[0],
                                                          t.ctypes.data, caps[1], p.ctypes.data, caps[2]))
+        self._wb_set = which  # flipped only once the call succeeded
         self._wb_inflight = (a, before, t, p)
 
     def checkpoint_delta_wait(self, copy=True):
@@ -310,6 +317,16 @@ class Engine:
     def checkpoint_mark(self):
         """Take the current state as written back (tbgpu_bench_checkpoint_mark)."""
         _lib.check(self.lib.tbgpu_bench_checkpoint_mark(self.h))
+
+    def shard(self, d):
+        """A node engine's shard d as an Engine sharing its handle (tbgpu_bench_node_shard): device
+        buffers, copies and the generators on shard d's GPU.  Never closed on its own."""
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.tbgpu_bench_node_shard(self.h, int(d), ctypes.byref(h)))
+        view = Engine.__new__(Engine)
+        view.options, view.lib, view.h = self.options, self.lib, h
+        view.close = lambda: None
+        return view
 
     def walk_merge_max(self, segments):
         """Heavy segments the limit-check sweep walks merged on one wave at most (0: a wave each)."""
