@@ -93,8 +93,8 @@ typedef struct tbgpu_config {
     uint32_t flags;             /* TBGPU_CONFIG_* */
     /* SURVEY.md §8b device_mask.  device_count >= 2: a NODE engine over devices[0 .. device_count),
      * one shard per entry (an ordinal may repeat: logical shards sharing a GPU).  Every entry point
-     * of this header works on a node engine with the same semantics: accounts hash-partitioned (the
-     * records replicated, the balances on their owner shard), transfers on their home shard, each
+     * of this header works on a node engine with the same semantics: accounts hash-partitioned
+     * (record and balances on their owner shard only), transfers on their home shard, each
      * create_transfers pass routed across the shards by kernels reading their peers' HBM over xGMI
      * (tigerbeetle_amd/csrc/node.h).  Not on a node: tbgpu_commit_device_async and the
      * tbgpu_shard.h primitives (they take one device's engine). */
@@ -287,6 +287,11 @@ typedef struct tbgpu_stats {
      * committed by the sequencer, the rest routed), or sequenced whole (no overflow certificate);
      * events the sequencer committed. */
     uint64_t node_passes_clean, node_passes_split, node_passes_whole, node_sequenced_events;
+    /* HBM bytes of the account table (hot records, balances, cold fields, marks): this engine's; on a
+     * node engine the largest shard's, and each shard's in node_shard_account_bytes — the accounts it
+     * owns (1/N of the ledger) plus room for one routed sub-pass's imported records. */
+    uint64_t account_table_bytes;
+    uint64_t node_shard_account_bytes[16];
 } tbgpu_stats;
 
 int tbgpu_get_stats(tbgpu_t* engine, tbgpu_stats* stats);

@@ -111,6 +111,61 @@ def test_no_allocation_after_init(profile, gpu_engine_factory):
     engine.unregister_host(body)
 
 
+@pytest.mark.parametrize("profile", [False, True])
+def test_no_allocation_after_init_node(profile):
+    """The same rule on a node engine (two logical shards): every commit entry point (create_accounts
+    through the sequencer, create_transfers routed and split, one prepare and many), lookups and the
+    synchronous write-back make no device, pinned or event allocation after tbgpu_init."""
+    from tigerbeetle_amd.state_machine import Engine, Options
+    engine = Engine(Options(accounts_max=1 << 12, transfers_max=1 << 18, pass_events_max=1 << 14, pass_batches_max=16,
+                            devices=(0, 0), profile=profile))
+    try:
+        body = np.zeros(4 * 8190 * 128, dtype=np.uint8)
+        engine.register_host(body)
+        ts = 10**9
+        k = 1
+        before = None
+        for rnd in range(3):
+            a = _accounts(64)
+            a["id_lo"] += 64 * rnd
+            assert engine.commit(128, ts, a.tobytes()) == b""                   # create_accounts (sequencer)
+            n_acc = 64 * (rnd + 1)
+            t = _transfers(8190, k, n_acc)
+            k += 8190
+            ts += 10**4
+            assert engine.commit(129, ts, t.tobytes()) == b""                   # one prepare, clean pass
+            t = _transfers(8190, k, n_acc)
+            t["flags"][::7] = TransferFlags.linked
+            t["flags"][-1] = 0
+            k += 8190
+            ts += 10**4
+            assert engine.commit(129, ts, t.tobytes()) == b""                   # dirty pass: split
+            many = [_transfers(1000, k + 1000 * j, n_acc).tobytes() for j in range(3)]
+            k += 3000
+            assert engine.commit_many(129, [ts + 10**4 * (j + 1) for j in range(3)], many) == [b""] * 3
+            ts += 10**5
+            t3 = _transfers(3 * 8190, k, n_acc)
+            k += 3 * 8190
+            body[:t3.nbytes] = t3.view(np.uint8)
+            rb, _, _ = engine.commit_pipelined(129, [ts + 10**4 * (j + 1) for j in range(3)], [8190] * 3, body,
+                                               chunk_batches=1)
+            assert int(rb.sum()) == 0
+            ts += 10**5
+            ids = np.zeros((4, 2), dtype=np.uint64)
+            ids[:, 0] = [1, 2, 3, 9999]
+            assert len(engine.commit(130, ts, ids.tobytes())) == 3 * 128          # lookup_accounts
+            ts += 10**4
+            d = engine.checkpoint_delta(caps=(1 << 17, 1 << 17, 1 << 17))      # synchronous write-back
+            assert len(d.transfers) > 0
+            engine.stats()
+            if rnd == 0:  # the mirror's write-back buffers are registered by now
+                before = allocations()
+        assert allocations() == before, "a node entry point allocated after tbgpu_init"
+        engine.unregister_host(body)
+    finally:
+        engine.close()
+
+
 def test_prefetch_staging_belongs_to_the_next_commit(gpu_engine_factory):
     """A staged body is taken by the commit right after its prefetch only: any call in between drops
     it, and a re-prefetch restages the current bytes."""

@@ -2,7 +2,8 @@
 legs) at its full account count, on the GPU box's one GPU.
 
 * The node engine (include/tbgpu.h tbgpu_config.devices, csrc/node.h) with two logical shards on
-  cuda:0: 100M accounts created through the C ABI (every shard holds every record), then a sample
+  cuda:0: 100M accounts created through the C ABI (each on its owner shard only: every shard's account
+  table is half of a single engine's), then a sample
   of 64 prepares compared byte for byte with the oracle — the oracle holds exactly the accounts the
   sample touches, built from the generator's records and the create timestamps, not from the GPU —
   then two full passes of 2 x 256 prepares (every source block full: 512 prepares, 4.19M transfers
@@ -50,7 +51,8 @@ def test_c5_node_full_size():
         assert (x["debit_account_id_hi"][:n_sample] == H).all() and (x["credit_account_id_hi"][:n_sample] == H).all()
         ref = np.unique(np.concatenate([x["debit_account_id_lo"][:n_sample], x["credit_account_id_lo"][:n_sample]]))
 
-        # 100M accounts through the node (replicated create_accounts), in chunks of 2048 prepares;
+        # 100M accounts through the node (sequenced create_accounts, each to its owner), in chunks of 2048
+        # prepares;
         # the oracle gets the sample's accounts as created (generator record + create timestamp).
         a_lens = batches(N_ACCOUNTS, BATCH)
         a_ts, t = timestamps(a_lens, 10**9)
@@ -105,6 +107,12 @@ def test_c5_node_full_size():
         assert int(rb.sum()) == 0
         st = engine.stats()
         assert st["transfers"] == n_xfer and st["dependent_events"] == 0
+        # Partitioned records: each shard's account table holds its own half of the ledger (plus one
+        # routed sub-pass's imports), half of what one engine holding all 100M accounts allocates.
+        single = (1 << 28) * (32 + 64 + 32 + 4)  # pow2(2 x 100M) slots x (hot, balances, cold, mark)
+        shard_bytes = st["node_shard_account_bytes"][:2]
+        assert all(0 < b <= single // 2 for b in shard_bytes), (shard_bytes, single)
+        assert st["accounts"] == N_ACCOUNTS
         s = engine.ledger_summary()
         assert s["accounts"] == N_ACCOUNTS and s["stray"] == 0
         assert (x["amount_hi"] == 0).all()

@@ -92,6 +92,8 @@ class tbgpu_stats(ctypes.Structure):
         ("node_passes_split", ctypes.c_uint64),
         ("node_passes_whole", ctypes.c_uint64),
         ("node_sequenced_events", ctypes.c_uint64),
+        ("account_table_bytes", ctypes.c_uint64),
+        ("node_shard_account_bytes", ctypes.c_uint64 * 16),
     ]
 
 

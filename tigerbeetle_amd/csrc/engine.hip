@@ -852,7 +852,8 @@ static int engine_sync(tbgpu* E) {
 static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* events_dev, u32* results_dev,
                         u32* reply_bytes_dev, bool routed = false, u8* codes = nullptr, u32 cert_ext = 0,
                         const u8* events_src = nullptr, const u64* d_meta = nullptr,
-                        const OwnerLegArgs* owner = nullptr, const u64* inline_meta = nullptr) {
+                        const OwnerLegArgs* owner = nullptr, const u64* inline_meta = nullptr,
+                        const NodeImport* imp = nullptr) {
     const u64* d_off = d_meta ? d_meta : E->meta;
     const u64* d_ts = d_off + (nb + 1);
     u32 b0 = 0;
@@ -948,6 +949,13 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         E->dedup_prev = P.dedup_mask + 1;
         if ((st = prof_end(E, &pp))) return st;
 
+        if (imp && n > 0) {  // a node home: the foreign accounts this sub-pass names, from their owners
+            HIPCK(hipMemsetAsync(imp->count, 0, 8, E->stream));
+            const u32 ig = (u32)std::min<u64>(4096, (2 * n + 255) / 256);
+            hipLaunchKernelGGL(tb_node_import, dim3(ig), dim3(256), 0, E->stream, E->T, imp->N, events_dev + P.e0 * 128, n,
+                               imp->self, imp->list, imp->count, imp->cap);
+            HIPCK(hipGetLastError());
+        }
         if (n > 0) {
             if ((st = prof_begin(E, &pp, K_VALIDATE))) return st;
             const u32 grid = (u32)((n + VALIDATE_THREADS - 1) / VALIDATE_THREADS);
@@ -1012,6 +1020,10 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         if ((st = prof_end(E, &pp))) return st;
         if (owner && n > 0) {  // every committed transfer's legs, grouped by owner (k_route.h)
             hipLaunchKernelGGL(tb_owner_legs, dim3((u32)((n + 255) / 256)), dim3(256), 0, E->stream, P, *owner);
+            HIPCK(hipGetLastError());
+        }
+        if (imp && n > 0) {  // the owned-only table again
+            hipLaunchKernelGGL(tb_node_import_clear, dim3(1024), dim3(256), 0, E->stream, E->T, imp->list, imp->count);
             HIPCK(hipGetLastError());
         }
         if ((st = prof_end(E, &pass_pp))) return st;
@@ -2073,6 +2085,7 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     HIPCK(hipMemcpy(&g, E->g, sizeof(Globals), hipMemcpyDeviceToHost));
     memset(s, 0, sizeof(*s));
     s->passes = E->passes;
+    s->account_table_bytes = E->account_cap * (sizeof(AccountHot) + sizeof(AccountBal) + sizeof(AccountCold) + 4);
     s->events = E->events;
     s->dependent_events = g.dependent_all;
     s->accounts = g.account_count;
@@ -2334,7 +2347,7 @@ extern "C" int tbgpu_bench_ledger_summary(tbgpu_t* E, tbgpu_ledger_summary* out)
             out->sums[2 * f + 1] += v[2 * f + 1] + (lo < out->sums[2 * f] ? 1 : 0);
             out->sums[2 * f] = lo;
         }
-        if (d == 0) out->accounts = v[8];  // replicated records
+        out->accounts += v[8];  // on a node, each account on its owner only
         out->stray += v[9];
     }
     return TBGPU_STATUS_OK;

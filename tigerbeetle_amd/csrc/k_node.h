@@ -3,14 +3,18 @@
 // xGMI (hipDeviceEnablePeerAccess) — no host staging, no collective library, one host round trip
 // per pass (the route plan's counts).
 //
-// Partition (as the per-process protocol of tigerbeetle_amd/sharded.py): account
-// records replicated on every shard, an account's balances on owner(id) = tb_home(id, N) only, a
-// transfer (record, id index entry, posted state) on home(id).  A clean create_transfers pass:
+// Partition: an account (record and balances) lives on owner(id) = tb_home(id, N)
+// only, a transfer (record, id index entry, posted state) on home(id).  A clean create_transfers
+// pass:
 //   1. every source shard: tb_route_classify / _offsets / _scatter over its block of the pass's
-//      prepares (k_route.h): its events grouped by home, each with its execute timestamp;
+//      prepares (k_route.h): its events grouped by home, each with its execute timestamp (limit
+//      accounts are recognised by a replicated bitmap, tb_limit_maybe: no account probe);
 //   2. every home: tb_node_gather pulls its run from every source's send buffer (global order:
-//      sources in order, each source's run in event order), then the routed commit with owner
-//      legs (tb_owner_legs: every committed transfer's two balance legs, grouped by owner);
+//      sources in order, each source's run in event order); tb_node_import copies the hot record of
+//      every foreign account the run names from its owner's table into the home's (the reference's
+//      prefetch of the pass's accounts, src/state_machine.zig:345-506), then the routed commit with
+//      owner legs (tb_owner_legs: every committed transfer's two balance legs, grouped by owner),
+//      then tb_node_import_clear empties the imported entries again;
 //   3. every owner: tb_node_apply_legs pulls its region of every home's legs and adds them;
 //   4. every source: tb_node_replies reads each event's result code from its home's code array and
 //      compacts the sparse replies of its prepares (tb_route_replies' layout).
@@ -50,7 +54,7 @@ struct NodeLegArgs {
 
 // Owner side: every leg this shard owns, from every home (tb_apply_owner_legs' arithmetic).  The
 // sums commute, so the order of homes and legs does not matter.  A leg for an account this shard
-// lacks is an invariant failure (accounts are replicated): PANIC_ASSERT.
+// lacks is an invariant failure (the owner holds every account it owns): PANIC_ASSERT.
 __global__ __launch_bounds__(256) void tb_node_apply_legs(Tables T, NodeLegArgs A) {
     const u64 stride = (u64)gridDim.x * 256;
     for (u32 h = 0; h < A.world; h++) {
@@ -68,6 +72,73 @@ __global__ __launch_bounds__(256) void tb_node_apply_legs(Tables T, NodeLegArgs 
             if (A.cert64) tb_atomic_add_lo_noret(f, a_lo);
             else tb_atomic_add_u128(f, tb_u128(a_lo, a_hi));
         }
+    }
+}
+
+// ---- partitioned account records ----------------------------------------------------------------
+// Every limit account among n records (a load or an upsert of accounts, any owner) into this shard's
+// bitmap.
+__global__ void tb_limbits_from_records(const u8* recs, u32 n, u64* bits, u64 mask) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Account& a = *(const Account*)(recs + (u64)i * 128);
+    if (a.flags & AF_LIMITS) tb_limit_set(bits, mask, tb_lo(a.id), tb_hi(a.id));
+}
+
+struct NodeTablesArgs {
+    Tables T[NODE_WORLD_MAX];  // every shard's tables (device pointers; peers read over xGMI)
+    u32 world;
+};
+
+// Home side, before a routed sub-pass: the hot record (id, ledger, code, flags, timestamp) of every
+// foreign account the sub-pass's events name, from its owner's table, into this shard's table — what
+// validate and the ordered fallback read of an account in a routed pass (its balances are the owner's
+// and never read here: the router's certificate rules out every balance check, and limit and
+// balancing events are sequenced).  Entries go into slots empty in the owned-only table, so they
+// never sit on an owned account's probe chain, and tb_node_import_clear restores the owned-only table
+// exactly.  Two lanes importing one id concurrently may both insert it: both entries are identical,
+// every probe stops at the first, and both are cleared.
+__global__ void tb_node_import(Tables H, NodeTablesArgs N, const u8* events, u64 n, u32 self, u32* list, u64* count,
+                               u64 cap) {
+    const u64 stride = (u64)gridDim.x * blockDim.x;
+    for (u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x; g < 2 * n; g += stride) {
+        const u64* w = (const u64*)(events + (g >> 1) * 128) + 2 + 2 * (g & 1);  // debit @16, credit @32
+        const u64 lo = w[0], hi = w[1];
+        if (tb_id_reserved(lo, hi)) continue;
+        const u32 o = tb_home(lo, hi, N.world);
+        if (o == self || tb_account_find(H, lo, hi) != TB_NOT_FOUND) continue;
+        const Tables& O = N.T[o];
+        const u32 os = tb_account_find(O, lo, hi);
+        if (os == TB_NOT_FOUND) continue;  // no such account: validate answers *_account_not_found
+        const AccountHot a = O.acct_hot[os];
+        const u32 slot = tb_account_claim(H, lo, hi, a.timestamp);
+        if (slot == TB_NOT_FOUND) continue;  // PANIC_TABLE_FULL set
+        AccountHot* h = &H.acct_hot[slot];
+        h->ledger = a.ledger;
+        h->code = a.code;
+        h->flags = a.flags;
+        h->id_lo = lo;
+        h->id_hi = hi;
+        const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
+        if (k < cap) list[k] = slot;
+        else tb_panic(H.g, PANIC_TABLE_FULL);
+    }
+}
+
+// What a routed commit on a node home needs to import (engine.hip enqueue_call runs the import before
+// each of its sub-passes and the clear after it).
+struct NodeImport {
+    NodeTablesArgs N;
+    u32 self;
+    u32* list;     // [cap] slots inserted
+    u64* count;
+    u64 cap;
+};
+
+__global__ void tb_node_import_clear(Tables H, const u32* list, const u64* count) {
+    const u64 n = *count;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        H.acct_hot[list[i]] = AccountHot{};
     }
 }
 
@@ -193,13 +264,9 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_node_classify1(RouteArgs A, 
     if ((flags & TF_LINKED) || (e > A.batch_off[b] && (*(const u16*)(A.events + (e - 1) * 128 + 118) & TF_LINKED))) d |= 1;
     if (flags & (TF_POST | TF_VOID)) d |= 2;
     if (flags & (TF_BAL_DEBIT | TF_BAL_CREDIT)) d |= 4;
-    if (A.T.g->limit_accounts != 0) {
-        const u32 dr = tb_account_find(A.T, w[2], w[3]);
-        const u32 cr = tb_account_find(A.T, w[4], w[5]);
-        if ((dr != TB_NOT_FOUND && (A.T.acct_hot[dr].flags & AF_LIMITS)) ||
-            (cr != TB_NOT_FOUND && (A.T.acct_hot[cr].flags & AF_LIMITS))) {
-            d |= 8;
-        }
+    if (A.limit_any && (tb_limit_maybe(A.limbits, A.limmask, w[2], w[3]) ||
+                        tb_limit_maybe(A.limbits, A.limmask, w[4], w[5]))) {
+        d |= 8;
     }
     D.dep1[e] = d;
     if (d) {  // the ids it reads: its own, and its pending transfer's
@@ -373,11 +440,6 @@ __global__ __launch_bounds__(256) void tb_seq_gather(SeqGatherArgs A, SeqSet tse
     if (((const u16*)v)[59] & (TF_POST | TF_VOID)) tb_seq_insert(tset, w[8], w[9]);
 }
 
-struct NodeTablesArgs {
-    Tables T[NODE_WORLD_MAX];  // every shard's tables (device pointers; peers read over xGMI)
-    u32 world;
-};
-
 // The transfers the sequenced events read, from their homes: record, posted state, into the
 // sequencer's log at [0, loaded) and its index.  Their accounts go to the account set (a post / void
 // reads its pending transfer's accounts).
@@ -411,26 +473,15 @@ __global__ __launch_bounds__(256) void tb_seq_event_accounts(const u8* events, u
     tb_seq_insert(aset, w[4], w[5]);
 }
 
-// The accounts, into the sequencer: the record from the first shard's copy (records are replicated),
-// the balances from the owner's (the only true ones).
+// The accounts, into the sequencer: record and balances from the owner (the only copy).
 __global__ void tb_seq_load_accounts(NodeTablesArgs N, SeqSet aset, Tables X) {
     const u64 n = aset.count[0];
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
         SeqEntry& q = aset.e[aset.list[i]];
-        const u32 local = tb_account_find(N.T[0], q.lo, q.hi);
-        if (local == TB_NOT_FOUND) continue;
         const Tables& O = N.T[tb_home(q.lo, q.hi, N.world)];
         const u32 os = tb_account_find(O, q.lo, q.hi);
-        if (os == TB_NOT_FOUND) {
-            tb_panic(X.g, PANIC_ASSERT);  // records are replicated on every shard
-            continue;
-        }
-        Account a = tb_account_load(N.T[0], local);
-        const AccountBal b = O.acct_bal[os];
-        a.debits_pending = b.debits_pending;
-        a.debits_posted = b.debits_posted;
-        a.credits_pending = b.credits_pending;
-        a.credits_posted = b.credits_posted;
+        if (os == TB_NOT_FOUND) continue;  // no such account
+        const Account a = tb_account_load(O, os);
         const u32 xs = tb_account_claim(X, q.lo, q.hi, a.timestamp);
         if (xs == TB_NOT_FOUND) continue;  // PANIC_TABLE_FULL set
         tb_account_store_new(X, xs, a);
@@ -476,6 +527,49 @@ __global__ void tb_seq_writeback_accounts(Tables X, SeqSet aset, Tables O, u32 s
         const SeqEntry& q = aset.e[aset.list[i]];
         if (q.x == TB_NOT_FOUND || tb_home(q.lo, q.hi, world) != self) continue;
         O.acct_bal[q.home] = X.acct_bal[q.x];
+    }
+}
+
+// create_accounts on the sequencer (node.h node_commit_accounts): every event's id to the account set
+// (its existing record is loaded from its owner: create_account_exists, state_machine.zig:767-777).
+__global__ __launch_bounds__(256) void tb_seq_account_ids(const u8* events, u64 n, SeqSet aset) {
+    const u64 g = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (g >= n) return;
+    const u64* w = (const u64*)(events + g * 128);
+    tb_seq_insert(aset, w[0], w[1]);
+}
+
+#define SEQ_NEW 0xFFFFFFFEu  // SeqEntry.home: an account the sequencer created this pass
+
+// After the sequencer's create_accounts pass: the accounts its table holds that were not loaded were
+// created by the pass (a rolled-back insert is a tombstone, never found by id).
+__global__ void tb_seq_locate_new(SeqSet aset, Tables X) {
+    const u64 n = aset.count[0];
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        SeqEntry& q = aset.e[aset.list[i]];
+        if (q.x != TB_NOT_FOUND) continue;
+        const u32 xs = tb_account_find(X, q.lo, q.hi);
+        if (xs == TB_NOT_FOUND) continue;
+        q.x = xs;
+        q.home = SEQ_NEW;
+    }
+}
+
+// Write-back, on shard `self`: the accounts the sequencer created that it owns, inserted verbatim
+// (timestamp as assigned, zero balances); every created limit account into its limit bitmap.
+__global__ void tb_seq_writeback_new_accounts(Tables X, SeqSet aset, Tables O, u32 self, u32 world, u64* limbits,
+                                              u64 limmask) {
+    const u64 n = aset.count[0];
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        const SeqEntry& q = aset.e[aset.list[i]];
+        if (q.home != SEQ_NEW) continue;
+        const Account a = tb_account_load(X, q.x);
+        if (a.flags & AF_LIMITS) tb_limit_set(limbits, limmask, q.lo, q.hi);
+        if (tb_home(q.lo, q.hi, world) != self) continue;
+        const u32 slot = tb_account_claim(O, q.lo, q.hi, a.timestamp);
+        if (slot == TB_NOT_FOUND) continue;  // PANIC_TABLE_FULL set
+        tb_account_store_new(O, slot, a);
+        atomicAdd((unsigned long long*)&O.g->account_count, 1ULL);
     }
 }
 

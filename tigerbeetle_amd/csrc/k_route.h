@@ -30,6 +30,24 @@ enum : u32 { ROUTE_DIRTY_FLAGS = 1, ROUTE_DIRTY_LIMIT = 2 };
 
 // home(id) / owner(id): tb_home (tb_device.h).
 
+// Limit flags, replicated: one bit per hash bucket of ids, set for every account created or loaded
+// with debits_must_not_exceed_credits / credits_must_not_exceed_debits (tigerbeetle.zig:31-39).  A
+// source classifies its events with it instead of reading account records it does not hold; a false
+// positive (another id in the bucket) only sequences an event that could have been routed, which is
+// always exact.  The bucket hash is independent of the table position and owner bits.
+__host__ __device__ static inline u64 tb_limit_bit(u64 lo, u64 hi, u64 mask) {
+    return tb_mix64(tb_hash_id(lo, hi) ^ 0x9e3779b97f4a7c15ULL) & mask;
+}
+__device__ static inline bool tb_limit_maybe(const u64* bits, u64 mask, u64 lo, u64 hi) {
+    if (tb_id_reserved(lo, hi)) return false;
+    const u64 b = tb_limit_bit(lo, hi, mask);
+    return (bits[b >> 6] >> (b & 63)) & 1;
+}
+__device__ static inline void tb_limit_set(u64* bits, u64 mask, u64 lo, u64 hi) {
+    const u64 b = tb_limit_bit(lo, hi, mask);
+    atomicOr((unsigned long long*)&bits[b >> 6], 1ULL << (b & 63));
+}
+
 struct RouteArgs {
     const u8* events;      // this rank's events of the pass, back to back
     u32 n;
@@ -44,6 +62,12 @@ struct RouteArgs {
     u64* words;            // [2*SUM_SHARDS] S shards, [2*SUM_SHARDS] HUGE, [+1] dirty bits, [+2..] counts
     Tables T;
     const u8* skip;        // [n] or null: non-zero = a dependent event the sequencer commits (not routed)
+    // Node engines (records partitioned, node.h): limit accounts by the replicated bitmap
+    // (k_node.h tb_limit_maybe), not by this shard's records; limit_any = 0: none exists.  Null:
+    // records replicated (the per-process protocol), probe T.
+    const u64* limbits;
+    u64 limmask;
+    u32 limit_any;
 };
 #define RW_HUGE (2 * SUM_SHARDS)
 #define RW_DIRTY (2 * SUM_SHARDS + 1)
@@ -60,7 +84,7 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_route_classify(RouteArgs A) 
     if (threadIdx.x == 0) s_dirty = 0;
     __syncthreads();
     const u64 e = (u64)blockIdx.x * ROUTE_THREADS + threadIdx.x;
-    const bool limits = A.T.g->limit_accounts != 0;
+    const bool limits = A.limbits ? A.limit_any != 0 : A.T.g->limit_accounts != 0;
     u128 amount = 0;
     if (e < A.n) {
         const u64* w = (const u64*)(A.events + e * 128);
@@ -80,6 +104,10 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_route_classify(RouteArgs A) 
         u32 dirty = 0;
         if (flags & (TF_LINKED | TF_POST | TF_VOID | TF_BAL_DEBIT | TF_BAL_CREDIT)) {
             dirty = ROUTE_DIRTY_FLAGS;
+        } else if (limits && A.limbits) {
+            if (tb_limit_maybe(A.limbits, A.limmask, w[2], w[3]) || tb_limit_maybe(A.limbits, A.limmask, w[4], w[5])) {
+                dirty = ROUTE_DIRTY_LIMIT;
+            }
         } else if (limits) {  // no limit account exists (C2/C5): no account probe at all
             const u32 d = tb_account_find(A.T, w[2], w[3]);
             const u32 c = tb_account_find(A.T, w[4], w[5]);

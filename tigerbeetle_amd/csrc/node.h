@@ -7,9 +7,12 @@
 // device listed in the config) inside the library — the exchange is kernels reading their peers'
 // HBM (k_node.h), so no host staging, no collective library and no Python sit on the data path.
 //
-// Partition (the protocol of tigerbeetle_amd/sharded.py): account records replicated
-// on every shard (create_accounts commits every prepare on every shard), balances on owner(id)
-// only, a transfer on home(id).  A create_transfers call is cut into passes: pass p takes up to
+// Partition: an account — record and balances — on owner(id) only, a transfer on
+// home(id).  create_accounts prepares are committed in order by the sequencer (below) with the
+// existing records they name loaded from their owners, and each new account goes to its owner; a home
+// imports the hot records of the foreign accounts a routed pass names from their owners before it
+// validates, and drops them after (k_node.h tb_node_import).  Per-shard account memory is the owned
+// 1/N of the ledger plus one routed pass's imports.  A create_transfers call is cut into passes: pass p takes up to
 // N blocks of `chunk` prepares (block d -> source shard d, in order, so the pass's global order is
 // block-major = prepare order).  Per pass, on every device:
 //   copy stream   H2D of the source block's bodies (registered host memory: DMA)
@@ -77,6 +80,13 @@ struct NodeDev {
     u64 set_mask = 0;
     u64* wb_count = nullptr;     // sequencer write-back: records appended here
     hipEvent_t ev_cls = nullptr, ev_marked = nullptr;
+    // Partitioned account records: the foreign accounts a routed sub-pass imports (k_node.h
+    // tb_node_import), and the replicated limit-account bitmap.
+    u32* imp_list = nullptr;
+    u64* imp_count = nullptr;
+    u64 imp_cap = 0;
+    u64* limbits = nullptr;
+    u64 limmask = 0;             // bits - 1
 };
 
 struct NodeBlock {
@@ -87,9 +97,10 @@ struct NodeBlock {
 struct NodePass {
     u32 k0 = 0, k1 = 0;
     NodeBlock blk[NODE_WORLD_MAX];
-    std::vector<u64> off[NODE_WORLD_MAX];  // block-relative event offsets of its prepares
+    u64* off[NODE_WORLD_MAX] = {};  // block-relative event offsets of its prepares (pb_src + 1, init-time)
     bool issued = false, consumed = false;
 };
+#define NODE_PASS_RING 4  // passes alive at once in a call: p - 2 (replies), p - 1, p, p + 1 (planned)
 
 struct TbNode {
     u32 world = 0;
@@ -113,7 +124,11 @@ struct TbNode {
     u8* seq_codes = nullptr;     // [world * pe_src] the pass's dense codes from the sequencer
     u64* h_seq = nullptr;        // pinned scratch words
     u64 passes_clean = 0, passes_split = 0, passes_whole = 0, seq_events = 0;
+    bool limit_any = false;          // some account carries a limit flag (the bitmaps are consulted)
+    u64 x_limit_seen = 0;            // the sequencer's limit_accounts count when last read
     const u64* api_calls = nullptr;  // the node handle's entry-point count (tbgpu::api_calls)
+    NodePass ring[NODE_PASS_RING];   // a call's passes, built as they are planned (no per-call allocation)
+    std::vector<u64> ring_off;       // their offset tables
     u64 drained_at = ~0ULL;          // its value when a create_transfers call last ended drained
     unsigned __int128 bound_carry = 0;  // the node's balance bound at that point (host-tracked)
 };
@@ -144,7 +159,8 @@ static void node_free(TbNode* N) {
         void* dev[] = {D.stage[0], D.stage[1], D.send[0], D.send[1], D.slot[0], D.slot[1], D.home[0], D.home[1],
                        D.words[0], D.words[1], D.meta[0], D.meta[1], D.block_counts, D.results, D.reply_bytes,
                        D.recv, D.codes, D.legs, D.leg_counts, D.hmeta_dev[0], D.hmeta_dev[1], D.hmeta_dev[2],
-                       D.dep1, D.dep, D.dkeys, D.dbal, D.dcounts, D.keyset, D.markset, D.wb_count};
+                       D.dep1, D.dep, D.dkeys, D.dbal, D.dcounts, D.keyset, D.markset, D.wb_count,
+                       D.imp_list, D.imp_count, D.limbits};
         for (void* p : dev) if (p) (void)hipFree(p);
         void* host[] = {D.h_words[0], D.h_words[1], D.h_meta[0], D.h_meta[1], D.hmeta_host[0], D.hmeta_host[1],
                         D.hmeta_host[2], D.h_arena[0], D.h_arena[1], D.h_arena[2], D.h_dcounts};
@@ -185,15 +201,23 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
     N->pe_src = config->pass_events_max;
     N->pb_src = config->pass_batches_max;
     N->recv_cap = (u64)W * N->pe_src;
-    // Shard engines: the account table of the whole ledger (records are replicated), the transfer
-    // log of the transfers homed there (1/N of the ledger, with room for hash imbalance), routed
-    // passes of up to ~1.25x a source block (larger receipts are committed in several passes).
+    N->ring_off.assign((u64)NODE_PASS_RING * W * (N->pb_src + 1), 0);
+    for (u32 r = 0; r < NODE_PASS_RING; r++) {
+        for (u32 d = 0; d < W; d++) N->ring[r].off[d] = N->ring_off.data() + ((u64)r * W + d) * (N->pb_src + 1);
+    }
+    // Shard engines: the accounts owned there (below), the transfer log of the transfers homed there
+    // (1/N of the ledger, with room for hash imbalance), routed passes of up to ~1.25x a source
+    // block (larger receipts are committed in several passes).
     tbgpu_config sc = *config;
     sc.device_count = 0;
     sc.transfers_max = std::min<u64>(1ULL << 31, config->transfers_max / W + config->transfers_max / (8 * W) + N->recv_cap + 4096);
     sc.pass_events_max = (u32)std::min<u64>(N->recv_cap, N->pe_src + N->pe_src / 4 + 8192);
     sc.pass_batches_max = (u32)std::min<u64>(FLOW_NB_MAX, (sc.pass_events_max + BATCH_EVENTS_MAX - 2) / (BATCH_EVENTS_MAX - 1) + 2);
     sc.pass_batches_max = std::max(sc.pass_batches_max, N->pb_src);
+    // Accounts: the ones this shard owns (1/N of the ledger, with room for hash imbalance) plus the
+    // imports of one routed sub-pass (two per event).
+    const u64 owned = std::min<u64>(config->accounts_max, config->accounts_max / W + config->accounts_max / (8 * W) + 4096);
+    sc.accounts_max = std::min<u64>(1ULL << 31, owned + 2 * (u64)sc.pass_events_max);
     int st = TBGPU_STATUS_OK;
     for (u32 d = 0; d < W && st == TBGPU_STATUS_OK; d++) {
         NodeDev& D = N->D[d];
@@ -283,6 +307,15 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
         NALLOC(tbMalloc(&D.wb_count, 8));
         NALLOC(tbEventCreateWithFlags(&D.ev_cls, hipEventDisableTiming));
         NALLOC(tbEventCreateWithFlags(&D.ev_marked, hipEventDisableTiming));
+        D.imp_cap = 2 * (u64)sc.pass_events_max;
+        NALLOC(tbMalloc(&D.imp_list, D.imp_cap * 4));
+        NALLOC(tbMalloc(&D.imp_count, 8));
+        // 16 bits per account of the ledger: a false positive (which only sequences an event) is at
+        // most 1 in 16 even when every account is limited.
+        const u64 lim_bits = std::min<u64>(1ULL << 34, pow2_at_least(std::max<u64>(1ULL << 16, 16 * config->accounts_max)));
+        D.limmask = lim_bits - 1;
+        NALLOC(tbMalloc(&D.limbits, lim_bits / 8));
+        NALLOC(hipMemset(D.limbits, 0, lim_bits / 8));
     }
 #undef NALLOC
     if (e != hipSuccess) {
@@ -374,52 +407,97 @@ static int node_publish_commit_ts(TbNode* N) {
     return TBGPU_STATUS_OK;
 }
 
-// -- create_accounts: every shard commits every prepare (records are replicated) ------------------
-
-static int node_commit_replicated(TbNode* N, u8 op, u32 n, const u64* ts, const void* const* inputs, const u32* in_lens,
-                                  void* const* outputs, u32* out_lens, u32 chunk) {
-    std::vector<std::vector<u8>> outs((size_t)N->world - 1);
-    std::vector<std::vector<void*>> optrs((size_t)N->world - 1);
-    std::vector<std::vector<u32>> olens((size_t)N->world - 1, std::vector<u32>(n));
-    for (u32 d = 1; d < N->world; d++) {
-        u64 total = 0;
-        for (u32 k = 0; k < n; k++) total += (u64)(in_lens[k] / 128) * 8;
-        outs[d - 1].resize(std::max<u64>(total, 8));
-        optrs[d - 1].resize(n);
-        u64 o = 0;
-        for (u32 k = 0; k < n; k++) {
-            optrs[d - 1][k] = outs[d - 1].data() + o;
-            o += (u64)(in_lens[k] / 128) * 8;
+// -- create_accounts: committed in order by the sequencer, each new account to its owner -----------
+// The reference's create_account reads only the account's own id (exists, :757-765) and the batch's
+// earlier events (linked chains, :628-692): the sequencer gets the pass verbatim, loads from their
+// owners the existing accounts the events name (prefetch, src/state_machine.zig:345-506), commits it
+// with the normal kernels, and each shard takes the accounts it created that the shard owns; every
+// shard's limit bitmap learns the new limit accounts.  The sequencer's account table is emptied after
+// each pass (tombstones of rolled-back chains included).
+static int node_commit_accounts(TbNode* N, u32 n, const u64* ts, const void* const* inputs, const u32* lens,
+                                void* const* outputs, u32* out_lens) {
+    const u32 W = N->world;
+    tbgpu* X = N->X;
+    const int dev0 = N->D[0].device;
+    int st = node_sync(N);  // the owners' tables are read below
+    if (st) return st;
+    for (u32 k = 0; k < n; k++) ckpt_note_ids(N->D[0].E, (const u8*)inputs[k], lens[k]);  // the next write-back
+    NodeTablesArgs NT{};
+    NT.world = W;
+    for (u32 d = 0; d < W; d++) NT.T[d] = N->D[d].E->T;
+    SeqSet tset{N->tset_e, N->tset_mask, N->tset_list, N->seq_counts, N->tset_dups};
+    SeqSet aset{N->aset_e, N->aset_mask, N->aset_list, N->seq_counts + 2, N->aset_dups};
+    for (u32 k0 = 0; k0 < n;) {
+        u32 k1 = k0;
+        u64 ev = 0;
+        while (k1 < n && k1 - k0 < X->pb_max && k1 - k0 < X->meta_cap && ev + lens[k1] <= X->pe_max) ev += lens[k1++];
+        if (k1 == k0) return fail(TBGPU_STATUS_INVALID, "batch larger than pass_events_max");
+        const u32 nb = k1 - k0;
+        NCK(hipSetDevice(dev0));
+        hipStream_t xs = X->stream;
+        u64* h_off = X->h_meta;
+        u64* h_ts = X->h_meta + nb + 1;
+        h_off[0] = 0;
+        for (u32 k = k0; k < k1; k++) {
+            h_off[k - k0 + 1] = h_off[k - k0] + lens[k];
+            h_ts[k - k0] = ts[k];
         }
-    }
-    std::vector<int> st(N->world, TBGPU_STATUS_OK);
-    std::vector<std::string> err(N->world);
-    std::vector<std::thread> th;
-    for (u32 d = 0; d < N->world; d++) {
-        th.emplace_back([&, d]() {
-            tbgpu* E = N->D[d].E;
-            if (hipSetDevice(N->D[d].device) != hipSuccess) {
-                st[d] = TBGPU_STATUS_DEVICE;
-                return;
-            }
-            st[d] = commit_pipelined(E, op, n, ts, inputs, in_lens, d == 0 ? outputs : optrs[d - 1].data(),
-                                     d == 0 ? out_lens : olens[d - 1].data(), nullptr, chunk, nullptr);
-            if (st[d]) err[d] = g_err;  // g_err is thread-local
-        });
-    }
-    for (auto& t : th) t.join();
-    for (u32 d = 0; d < N->world; d++) {
-        if (st[d]) return fail(st[d], "%s", err[d].c_str());
-    }
-    for (u32 d = 1; d < N->world; d++) {  // replicas of the same deterministic commit
-        for (u32 k = 0; k < n; k++) {
-            if (olens[d - 1][k] != out_lens[k] || memcmp(optrs[d - 1][k], outputs[k], out_lens[k]) != 0) {
-                return fail(TBGPU_STATUS_PANIC, "node: shard %u replied differently to replicated prepare %u", d, k);
-            }
+        for (u32 k = k0; k < k1; k++) {
+            if (lens[k]) NCK(hipMemcpyAsync(X->staging + h_off[k - k0] * 128, inputs[k], (u64)lens[k] * 128, hipMemcpyDefault, xs));
         }
+        NCK(hipMemcpyAsync(X->meta, X->h_meta, (2 * (u64)nb + 1) * 8, hipMemcpyHostToDevice, xs));
+        NCK(hipMemsetAsync(N->seq_counts, 0, 8 * 8, xs));
+        const u64 ne = h_off[nb];
+        if (ne) {
+            hipLaunchKernelGGL(tb_seq_account_ids, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, xs, X->staging, ne, aset);
+            hipLaunchKernelGGL(tb_seq_verify, dim3(256), dim3(256), 0, xs, aset, (u64*)&X->g->panic);
+            hipLaunchKernelGGL(tb_seq_load_accounts, dim3(1024), dim3(256), 0, xs, NT, aset, X->T);
+            NCK(hipGetLastError());
+        }
+        N->h_seq[0] = N->commit_ts;
+        NCK(hipMemcpyAsync(&X->g->commit_timestamp, N->h_seq, 8, hipMemcpyHostToDevice, xs));
+        X->commit_ts = N->commit_ts;
+        X->last_batch_ts = N->commit_ts;
+        if ((st = enqueue_call(X, OP_CREATE_ACCOUNTS, nb, h_off, X->staging, X->results, X->reply_bytes, false, nullptr, 0,
+                               nullptr, X->meta))) {
+            return st;
+        }
+        hipLaunchKernelGGL(tb_seq_locate_new, dim3(1024), dim3(256), 0, xs, aset, X->T);
+        NCK(hipGetLastError());
+        NCK(hipMemcpyAsync(X->h_rb, X->reply_bytes, (u64)nb * 4, hipMemcpyDeviceToHost, xs));
+        if ((st = engine_sync(X))) return st;
+        for (u32 k = k0; k < k1; k++) {
+            const u32 bytes = X->h_rb[k - k0];
+            if (bytes) NCK(hipMemcpy(outputs[k], X->results + 2 * h_off[k - k0], bytes, hipMemcpyDeviceToHost));
+            out_lens[k] = bytes;
+        }
+        N->commit_ts = std::max(N->commit_ts, X->commit_ts);
+        if (X->h_globals->limit_accounts != N->x_limit_seen) {  // a limit account was created (or loaded)
+            N->x_limit_seen = X->h_globals->limit_accounts;
+            N->limit_any = true;
+        }
+        // Each shard takes the accounts it owns (its own stream, reading the sequencer over xGMI).
+        for (u32 d = 0; d < W; d++) {
+            NodeDev& D = N->D[d];
+            NCK(hipSetDevice(D.device));
+            hipLaunchKernelGGL(tb_seq_writeback_new_accounts, dim3(1024), dim3(256), 0, D.E->stream, X->T, aset, D.E->T, d,
+                               W, D.limbits, D.limmask);
+            NCK(hipGetLastError());
+        }
+        for (u32 d = 0; d < W; d++) {
+            NCK(hipSetDevice(N->D[d].device));
+            NCK(hipStreamSynchronize(N->D[d].E->stream));
+        }
+        // The sequencer empty again: its entries, the sets, and (by one sweep) the tombstones of
+        // rolled-back creates.
+        NCK(hipSetDevice(dev0));
+        hipLaunchKernelGGL(tb_seq_clear, dim3(1024), dim3(256), 0, xs, tset, aset, X->T);
+        NCK(hipGetLastError());
+        NCK(hipMemsetAsync(X->T.acct_hot, 0, X->account_cap * sizeof(AccountHot), xs));
+        NCK(hipStreamSynchronize(xs));
+        k0 = k1;
     }
-    for (u32 d = 0; d < N->world; d++) N->commit_ts = std::max(N->commit_ts, N->D[d].E->commit_ts);
-    return TBGPU_STATUS_OK;
+    return node_sync(N);
 }
 
 // -- create_transfers ----------------------------------------------------------------------------
@@ -502,6 +580,9 @@ static int node_issue_plan(TbNode* N, NodePass& P, u32 p, const u64* ts, const v
         A.words = D.words[par];
         A.T = E->T;
         A.skip = nullptr;
+        A.limbits = D.limbits;
+        A.limmask = D.limmask;
+        A.limit_any = N->limit_any ? 1u : 0u;
         if (B.events) {
             hipLaunchKernelGGL(tb_route_classify, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, D.rs, A);
             NCK(hipGetLastError());
@@ -633,10 +714,16 @@ static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, 
                 h_ts[k] = ts_max;
             }
             NCK(hipMemcpyAsync(D.hmeta_dev[tri], h_off, (2 * nb + 1) * 8, hipMemcpyHostToDevice, E->stream));
-            std::vector<u64> offs(h_off, h_off + nb + 1);
             OwnerLegArgs O{W, h, D.legs, 2 * nh[h], D.leg_counts};
-            const int st = enqueue_call(E, OP_CREATE_TRANSFERS, (u32)nb, offs.data(), D.recv, E->results, E->reply_bytes,
-                                        true, D.codes, cert, nullptr, D.hmeta_dev[tri], &O);
+            NodeImport imp{};
+            imp.N.world = W;
+            for (u32 d = 0; d < W; d++) imp.N.T[d] = N->D[d].E->T;
+            imp.self = h;
+            imp.list = D.imp_list;
+            imp.count = D.imp_count;
+            imp.cap = D.imp_cap;
+            const int st = enqueue_call(E, OP_CREATE_TRANSFERS, (u32)nb, h_off, D.recv, E->results, E->reply_bytes,
+                                        true, D.codes, cert, nullptr, D.hmeta_dev[tri], &O, nullptr, &imp);
             if (st) return st;
         }
         NCK(hipEventRecord(D.ev_committed, E->stream));
@@ -750,6 +837,9 @@ static int node_split_pass(TbNode* N, NodePass& P, u32 p, const u64* ts, u64 bou
         A.batch_ts = D.meta[par] + A.nb + 1;
         A.world = W;
         A.T = D.E->T;
+        A.limbits = D.limbits;
+        A.limmask = D.limmask;
+        A.limit_any = N->limit_any ? 1u : 0u;
         return A;
     };
     // -- 1. classification on every source: primary classes, then the events on balancing-marked
@@ -964,26 +1054,30 @@ static int node_commit_transfers(TbNode* N, u32 n, const u64* ts, const void* co
     typedef unsigned __int128 h128;
     const u32 W = N->world;
     const u32 per = std::max<u32>(1, std::min<u32>(chunk ? chunk : N->pb_src, N->pb_src));
-    // Passes: W blocks of up to `per` prepares and pe_src events each, in prepare order.
-    std::vector<NodePass> passes;
-    for (u32 k = 0; k < n;) {
-        NodePass P;
+    // Passes: W blocks of up to `per` prepares and pe_src events each, in prepare order, built in a
+    // ring as they are planned.  Every prepare fits a block (checked before anything runs).
+    for (u32 k = 0; k < n; k++) {
+        if (lens[k] > N->pe_src) return fail(TBGPU_STATUS_INVALID, "batch larger than pass_events_max");
+    }
+    auto build = [&](u32 p, u32 k) -> NodePass& {
+        NodePass& P = N->ring[p % NODE_PASS_RING];
         P.k0 = k;
+        P.issued = P.consumed = false;
         for (u32 d = 0; d < W; d++) {
             NodeBlock& B = P.blk[d];
             B.k0 = B.k1 = k;
-            P.off[d].assign(1, 0);
+            B.events = 0;
+            P.off[d][0] = 0;
             while (k < n && B.k1 - B.k0 < per && B.events + lens[k] <= N->pe_src) {
                 B.events += lens[k];
-                P.off[d].push_back(B.events);
+                P.off[d][B.k1 - B.k0 + 1] = B.events;
                 k++;
                 B.k1 = k;
             }
         }
-        if (k == P.k0) return fail(TBGPU_STATUS_INVALID, "batch larger than pass_events_max");
         P.k1 = k;
-        passes.push_back(std::move(P));
-    }
+        return P;
+    };
     // Drain the shards and read their bounds back — unless the previous call on this handle was a
     // create_transfers call that ended with nothing in flight and nothing ran since: its bound (the
     // host-tracked sum, conservative) still holds.
@@ -995,31 +1089,36 @@ static int node_commit_transfers(TbNode* N, u32 n, const u64* ts, const void* co
         bound = node_bound(N);
     }
     int status = TBGPU_STATUS_OK;
-    const u32 NP = (u32)passes.size();
+    u32 NP = 1;  // passes built so far (the last one planned)
     u32 next_consume = 0;
+    auto pass = [&](u32 p) -> NodePass& { return N->ring[p % NODE_PASS_RING]; };
     auto consume_upto = [&](u32 end) {  // consume every issued pass < end
         for (; next_consume < end; next_consume++) {
-            NodePass& P = passes[next_consume];
+            NodePass& P = pass(next_consume);
             if (P.issued && !P.consumed) {
                 const int c = node_consume(N, P, next_consume, outputs, out_lens, latency_ms, status == TBGPU_STATUS_OK);
                 if (status == TBGPU_STATUS_OK) status = c;
             }
         }
     };
-    if ((status = node_issue_plan(N, passes[0], 0, ts, inputs, lens))) return status;
+    if ((status = node_issue_plan(N, build(0, 0), 0, ts, inputs, lens))) return status;
     for (u32 p = 0; p < NP && status == TBGPU_STATUS_OK; p++) {
         if (p >= 2) consume_upto(p - 1);  // pass p-2: its arena slot, start event and meta are reused next
         if (status) break;
-        if (p + 1 < NP && (status = node_issue_plan(N, passes[p + 1], p + 1, ts, inputs, lens))) break;
+        if (pass(p).k1 < n) {  // the next pass: its ring slot held pass p - 3, consumed above
+            NP = p + 2;
+            if ((status = node_issue_plan(N, build(p + 1, pass(p).k1), p + 1, ts, inputs, lens))) break;
+        }
+        NodePass& Pp = pass(p);
         NodePlan PL;
-        if ((status = node_read_plan(N, passes[p], p, &PL))) break;
+        if ((status = node_read_plan(N, Pp, p, &PL))) break;
         const h128 total = bound + PL.S < bound ? ~(h128)0 : bound + PL.S;
         if (PL.dirty || PL.huge || total == ~(h128)0) {
             consume_upto(p);
             if (status) break;
             if ((status = node_sync(N))) break;
             bound = node_bound(N);
-            if ((status = node_split_pass(N, passes[p], p, ts, (u64)bound, (u64)(bound >> 64),
+            if ((status = node_split_pass(N, Pp, p, ts, (u64)bound, (u64)(bound >> 64),
                                           PL.huge || total == ~(h128)0))) {
                 break;
             }
@@ -1030,7 +1129,7 @@ static int node_commit_transfers(TbNode* N, u32 n, const u64* ts, const void* co
             continue;
         }
         const u32 cert = (total >> 64) == 0 ? TBGPU_CERT_U64 : TBGPU_CERT_U128;
-        if ((status = node_issue_commit(N, passes[p], p, PL, cert, ts[passes[p].k1 - 1]))) break;
+        if ((status = node_issue_commit(N, Pp, p, PL, cert, ts[Pp.k1 - 1]))) break;
         bound = total;
         N->passes_clean++;
     }
@@ -1085,7 +1184,7 @@ static int node_commit_pipelined(TbNode* N, u8 op, u32 n, const u64* ts, const v
         out_lens[k] = 0;
     }
     if (op == OP_CREATE_ACCOUNTS) {
-        const int st = node_commit_replicated(N, op, n, ts, inputs, input_lens, outputs, out_lens, chunk);
+        const int st = node_commit_accounts(N, n, ts, inputs, lens.data(), outputs, out_lens);
         const int s2 = node_publish_commit_ts(N);
         return st ? st : s2;
     }
@@ -1094,21 +1193,27 @@ static int node_commit_pipelined(TbNode* N, u8 op, u32 n, const u64* ts, const v
 
 // -- lookups, exports, write-back, test setup ------------------------------------------------------
 
-// Every account (identical on every shard but the balances) with the balances of its owner.
+// Every account, from its owner (the only copy), in id order.
 static int node_export_accounts(TbNode* N, std::vector<u8>& out) {
-    std::vector<std::vector<u8>> per(N->world);
+    out.clear();
     for (u32 d = 0; d < N->world; d++) {
         if (hipSetDevice(N->D[d].device) != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "hipSetDevice");
-        const int st = export_records<true>(N->D[d].E, per[d], nullptr);
+        std::vector<u8> r;
+        const int st = export_records<true>(N->D[d].E, r, nullptr);
         if (st) return st;
-        if (per[d].size() != per[0].size()) return fail(TBGPU_STATUS_PANIC, "node: shards hold different accounts");
+        const u64 m = r.size() / 128;
+        for (u64 i = 0; i < m; i++) {
+            if (node_home(&r[i * 128], N->world) != d) return fail(TBGPU_STATUS_PANIC, "node: shard %u holds a foreign account", d);
+        }
+        out.insert(out.end(), r.begin(), r.end());
     }
-    out = per[0];
     const u64 n = out.size() / 128;
-    for (u64 i = 0; i < n; i++) {
-        const u32 o = node_home(&out[i * 128], N->world);
-        if (o) memcpy(&out[i * 128 + 16], &per[o][i * 128 + 16], 64);  // dp, dpost, cp, cpost
-    }
+    std::vector<u64> idx(n);
+    for (u64 i = 0; i < n; i++) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](u64 a, u64 b) { return id_less(&out[a * 128], &out[b * 128]); });
+    std::vector<u8> sorted(out.size());
+    for (u64 i = 0; i < n; i++) memcpy(&sorted[i * 128], &out[idx[i] * 128], 128);
+    out.swap(sorted);
     return TBGPU_STATUS_OK;
 }
 
@@ -1221,16 +1326,9 @@ static int node_api_commit(TbNode* N, u8 op, u64 timestamp, const void* input, u
     return node_commit_pipelined(N, op, 1, &timestamp, ins, &input_len, outs, out_len, 1, nullptr);
 }
 
-// The setup action (state_machine.zig:1398-1407): the owner holds the balances, every other shard
-// zeros for the account.
+// The setup action (state_machine.zig:1398-1407): on the owner, the account's only copy.
 static int node_api_set_balances(TbNode* N, u64 id_lo, u64 id_hi, const u64 b[8]) {
-    const u32 o = tb_home(id_lo, id_hi, N->world);
-    const u64 zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (u32 d = 0; d < N->world; d++) {
-        const int st = tbgpu_test_set_balances(N->D[d].E, id_lo, id_hi, d == o ? b : zero);
-        if (st) return st;
-    }
-    return TBGPU_STATUS_OK;
+    return tbgpu_test_set_balances(N->D[tb_home(id_lo, id_hi, N->world)].E, id_lo, id_hi, b);
 }
 
 static int node_api_export(TbNode* N, int what, void* out, u64 cap, u64* count) {
@@ -1396,9 +1494,11 @@ static int node_api_get_stats(TbNode* N, tbgpu_stats* s) {
         if (st) return st;
         s->dependent_events += x.dependent_events;
         if (!seq) {
+            s->node_shard_account_bytes[d] = x.account_table_bytes;
+            s->account_table_bytes = std::max(s->account_table_bytes, x.account_table_bytes);
             s->passes += x.passes;
             s->events += x.events;
-            if (d == 0) s->accounts = x.accounts;  // replicated records
+            s->accounts += x.accounts;  // each on its owner only
             s->transfers += x.transfers;
         }
         s->ms_validate += x.ms_validate;
@@ -1464,21 +1564,37 @@ static int node_api_unregister_host(TbNode* N, void* ptr) {
     return TBGPU_STATUS_OK;
 }
 
-// Accounts from elsewhere (a load from the forest, an upsert): every shard gets the record, the
-// owner its balances, the others zeros.
+// Accounts from elsewhere (a load from the forest, an upsert): each to its owner; every shard's limit
+// bitmap learns the limit accounts among them.
 static int node_api_accounts_in(TbNode* N, const void* records, u32 n, bool load) {
-    std::vector<u8> zeroed((const u8*)records, (const u8*)records + (u64)n * 128);
-    for (u32 i = 0; i < n; i++) memset(&zeroed[(u64)i * 128 + 16], 0, 64);
-    for (u32 d = 0; d < N->world; d++) {
-        std::vector<u8> mine(zeroed);
-        for (u32 i = 0; i < n; i++) {
-            if (node_home((const u8*)records + (u64)i * 128, N->world) == d) {
-                memcpy(&mine[(u64)i * 128 + 16], (const u8*)records + (u64)i * 128 + 16, 64);
-            }
-        }
-        const int st = load ? tbgpu_load_accounts(N->D[d].E, mine.data(), n) : tbgpu_upsert_accounts(N->D[d].E, mine.data(), n);
+    std::vector<std::vector<u8>> recs(N->world);
+    bool limits = false;
+    for (u32 i = 0; i < n; i++) {
+        const u8* r = (const u8*)records + (u64)i * 128;
+        recs[node_home(r, N->world)].insert(recs[node_home(r, N->world)].end(), r, r + 128);
+        limits |= (*(const u16*)(r + 118) & AF_LIMITS) != 0;
+    }
+    for (u32 o = 0; o < N->world; o++) {
+        const u32 m = (u32)(recs[o].size() / 128);
+        if (!m) continue;
+        const int st = load ? tbgpu_load_accounts(N->D[o].E, recs[o].data(), m) : tbgpu_upsert_accounts(N->D[o].E, recs[o].data(), m);
         if (st) return st;
     }
+    if (!limits) return TBGPU_STATUS_OK;
+    for (u32 d = 0; d < N->world; d++) {  // through the shard's staging buffer, in slices
+        NodeDev& D = N->D[d];
+        tbgpu* E = D.E;
+        NCK(hipSetDevice(D.device));
+        for (u32 i0 = 0; i0 < n; i0 += E->pe_max) {
+            const u32 m = std::min<u32>(n - i0, E->pe_max);
+            NCK(hipMemcpyAsync(E->staging, (const u8*)records + (u64)i0 * 128, (u64)m * 128, hipMemcpyHostToDevice, E->stream));
+            hipLaunchKernelGGL(tb_limbits_from_records, dim3((m + 255) / 256), dim3(256), 0, E->stream, E->staging, m, D.limbits,
+                               D.limmask);
+            NCK(hipGetLastError());
+        }
+        NCK(hipStreamSynchronize(E->stream));
+    }
+    N->limit_any = true;
     return TBGPU_STATUS_OK;
 }
 

@@ -226,7 +226,7 @@ class Engine:
     def stats(self):
         s = _lib.tbgpu_stats()
         _lib.check(self.lib.tbgpu_get_stats(self.h, ctypes.byref(s)))
-        return {f: (list(getattr(s, f)) if f in ("flow_phase_ms", "walk_dbg", "span_ms", "span_launches") else getattr(s, f)) for f, _ in s._fields_}
+        return {f: (list(getattr(s, f)) if f in ("flow_phase_ms", "walk_dbg", "span_ms", "span_launches", "node_shard_account_bytes") else getattr(s, f)) for f, _ in s._fields_}
 
     def reset_stats(self):
         self.lib.tbgpu_reset_stats(self.h)
