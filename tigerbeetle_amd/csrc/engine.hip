@@ -853,7 +853,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
                         u32* reply_bytes_dev, bool routed = false, u8* codes = nullptr, u32 cert_ext = 0,
                         const u8* events_src = nullptr, const u64* d_meta = nullptr,
                         const OwnerLegArgs* owner = nullptr, const u64* inline_meta = nullptr,
-                        const NodeImport* imp = nullptr) {
+                        const NodeImport* imp = nullptr, const u64* ev_ts = nullptr) {
     const u64* d_off = d_meta ? d_meta : E->meta;
     const u64* d_ts = d_off + (nb + 1);
     u32 b0 = 0;
@@ -904,6 +904,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.codes = codes;
         P.cert_ext = cert_ext;
         P.seq_pv = E->balances_set ? 1u : 0u;
+        P.ev_ts = ev_ts;
         // Legs pay a fixed ~30 us (one workgroup per bucket, LDS sums) that no-return atomics in
         // the resolve kernel (~20 G/s) only cost beyond ~LEGS_MIN_EVENTS events: the replica's
         // one-prepare commits take the atomics.

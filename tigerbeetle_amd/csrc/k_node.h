@@ -250,9 +250,12 @@ struct NodeDepArgs {
     u8* dep;           // [n] final: 1 = sequenced (the route plan's skip mask)
     u64* keys;         // [2n][2] ids and pending ids of primary-dependent events
     u64* bal;          // [2n][2] accounts of balancing events
-    u64* counts;       // [0] keys, [1] balancing accounts, [2] sequenced events
+    u64* counts;       // [0] keys, [1] balancing accounts, [2] sequenced events, [3] (host),
+                       // [NODE_DC_HOME + h] sequenced events whose id is homed on h (log room there)
     u32 all;           // 1: every event is sequenced (no global certificate)
 };
+#define NODE_DC_HOME 4
+#define NODE_DC_WORDS (NODE_DC_HOME + NODE_WORLD_MAX)
 
 __global__ __launch_bounds__(ROUTE_THREADS) void tb_node_classify1(RouteArgs A, NodeDepArgs D) {
     const u64 e = (u64)blockIdx.x * ROUTE_THREADS + threadIdx.x;
@@ -339,6 +342,8 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_node_classify2(RouteArgs A, 
         const u64* w = (const u64*)(A.events + e * 128);
         seq = D.dep1[e] != 0 || tb_dedup_is_dup_or_present(keyset, keyset_mask, tb_dedup_key(w[0], w[1]));
         D.dep[e] = seq ? 1 : 0;
+        // The sequencer may create this event's transfer on its home: reserve a log position there.
+        if (seq) atomicAdd((unsigned long long*)&D.counts[NODE_DC_HOME + tb_home(w[0], w[1], A.world)], 1ULL);
     }
     const u64 m = __ballot(seq);
     if ((threadIdx.x & 63) == 0 && m) atomicAdd((unsigned long long*)&D.counts[2], (unsigned long long)__popcll(m));
@@ -356,6 +361,8 @@ struct SeqEntry {
     u32 x;         // its slot / log position in the sequencer (TB_NOT_FOUND: absent everywhere)
     u32 home;      // its slot / log position on its owner / home shard
 };
+
+#define SEQ_NEW 0xFFFFFFFEu  // SeqEntry.home: an account the sequencer created this pass
 
 struct SeqSet {
     SeqEntry* e;
@@ -400,44 +407,157 @@ __global__ void tb_seq_verify(SeqSet S, u64* panic) {
     }
 }
 
-// The pass as the sequencer commits it: every event of the pass at its place (block-major, the
-// pass's global order), the sequenced ones verbatim from their source (a peer read), every other one a
-// placeholder that fails its first check without reading any state (a reserved flag bit; never
-// linked, so no chain crosses it, and every chain member is sequenced).  Positions and prepares keep
-// their original layout, so every execute timestamp (:645) and chain boundary is the original one.
-// The ids the sequenced events read go to the transfer set.
-struct SeqGatherArgs {
-    const u8* src[NODE_WORLD_MAX];   // source s's block of the pass (its staging buffer)
-    const u8* dep[NODE_WORLD_MAX];   // its sequenced mask
-    u64 start[NODE_WORLD_MAX + 1];   // block starts in the pass
+// The pass as the sequencer commits it: only its sequenced events, in pass order (block-major =
+// prepare order), each prepare keeping its place as the run of its own sequenced events.  Every
+// chain member is sequenced and a chain never leaves its prepare, so chains stay consecutive, and a
+// chain open at its prepare's end ends its compacted prepare; each event carries its execute
+// timestamp (:645) in `out_ts` (PassArgs.ev_ts).  Three kernels: per-256-event counts, one scan,
+// the stable scatter (wave ballots) — plus the compacted prepare offsets.  The ids the sequenced
+// events read go to the transfer set.
+struct SeqCompactArgs {
+    const u8* src[NODE_WORLD_MAX];    // source s's block of the pass
+    const u8* dep[NODE_WORLD_MAX];    // its sequenced mask
+    const u64* meta[NODE_WORLD_MAX];  // its block's prepare offsets [nb + 1], then timestamps [nb]
+    u32 nb[NODE_WORLD_MAX];
+    u64 start[NODE_WORLD_MAX + 1];    // block starts in the pass (events)
+    u32 pstart[NODE_WORLD_MAX + 1];   // block starts in the pass (prepares)
     u32 world;
-    u8* out;                         // the sequencer's staging
+    u32* blk;                         // [n_pass / 256 + 1]: sequenced events per 256-event block, then
+                                      // their exclusive prefix (tb_seq_scan), blk[nblk] = the total
+    u32 nblk;
+    u8* out;                          // the sequencer's staging
+    u64* out_ts;                      // [n_seq] execute timestamps
+    u32* map;                         // [n_pass] compacted index of a sequenced event, else ~0
+    u64* xmeta;                       // the sequencer's call meta: [nb_pass + 1] compacted offsets, [nb_pass] timestamps
 };
 
-__global__ __launch_bounds__(256) void tb_seq_gather(SeqGatherArgs A, SeqSet tset) {
-    const u64 n = A.start[A.world];
-    const u64 g = (u64)blockIdx.x * 256 + threadIdx.x;
-    if (g >= n) return;
+__device__ static inline u32 tb_seq_source(const SeqCompactArgs& A, u64 g) {
     u32 s = 0;
     while (s + 1 < A.world && A.start[s + 1] <= g) s++;
-    const u64 e = g - A.start[s];
-    u32x4* dst = (u32x4*)(A.out + g * 128);
-    if (!A.dep[s][e]) {
-        const u32x4 z = {0, 0, 0, 0};
-#pragma unroll
-        for (u32 k = 0; k < 8; k++) dst[k] = z;
-        ((u16*)(A.out + g * 128))[59] = (u16)0x8000;  // flags @118: a reserved bit
+    return s;
+}
+
+__global__ __launch_bounds__(256) void tb_seq_count(SeqCompactArgs A) {
+    const u64 g = (u64)blockIdx.x * 256 + threadIdx.x;
+    bool d = false;
+    if (g < A.start[A.world]) {
+        const u32 s = tb_seq_source(A, g);
+        d = A.dep[s][g - A.start[s]] != 0;
+    }
+    __shared__ u32 s_cnt;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    const u64 m = __ballot(d);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_cnt, (u32)__popcll(m));
+    __syncthreads();
+    if (threadIdx.x == 0) A.blk[blockIdx.x] = s_cnt;
+}
+
+__global__ __launch_bounds__(1024) void tb_seq_scan(SeqCompactArgs A) {
+    __shared__ u32 s_wave[1024 / 64];
+    const u32 n = A.nblk;
+    const u32 per = (n + 1023) / 1024;
+    const u32 k0 = min(n, threadIdx.x * per), k1 = min(n, k0 + per);
+    u32 local = 0;
+    for (u32 k = k0; k < k1; k++) local += A.blk[k];
+    u32 total;
+    u32 run = tb_block_excl_sum(local, s_wave, &total);
+    for (u32 k = k0; k < k1; k++) {
+        const u32 c = A.blk[k];
+        A.blk[k] = run;
+        run += c;
+    }
+    if (threadIdx.x == 0) A.blk[n] = total;
+}
+
+__global__ __launch_bounds__(256) void tb_seq_compact(SeqCompactArgs A, SeqSet tset) {
+    __shared__ u32 s_wave[256 / 64];
+    const u64 g = (u64)blockIdx.x * 256 + threadIdx.x;
+    const bool live = g < A.start[A.world];
+    u32 s = 0;
+    u64 e = 0;
+    bool d = false;
+    if (live) {
+        s = tb_seq_source(A, g);
+        e = g - A.start[s];
+        d = A.dep[s][e] != 0;
+    }
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const u64 m = __ballot(d);
+    if (lane == 0) s_wave[wave] = (u32)__popcll(m);
+    __syncthreads();
+    u32 before = 0;
+    for (u32 w = 0; w < wave; w++) before += s_wave[w];
+    if (!live) return;
+    if (!d) {
+        A.map[g] = 0xFFFFFFFFu;
         return;
     }
+    const u32 r = A.blk[blockIdx.x] + before + (u32)__popcll(m & ((1ULL << lane) - 1));
+    A.map[g] = r;
+    const u64* off = A.meta[s];
+    const u32 b = tb_batch_search(off, 0, A.nb[s], e);
+    const u64 L = off[b + 1] - off[b];
+    A.out_ts[r] = off[A.nb[s] + 1 + b] - L + 1 + (e - off[b]);  // execute, :645
     const u32x4* in = (const u32x4*)(A.src[s] + e * 128);
     u32x4 v[8];
 #pragma unroll
     for (u32 k = 0; k < 8; k++) v[k] = in[k];
+    u32x4* dst = (u32x4*)(A.out + (u64)r * 128);
 #pragma unroll
     for (u32 k = 0; k < 8; k++) dst[k] = v[k];
     const u64* w = (const u64*)v;
     tb_seq_insert(tset, w[0], w[1]);
     if (((const u16*)v)[59] & (TF_POST | TF_VOID)) tb_seq_insert(tset, w[8], w[9]);
+}
+
+// The compacted prepare offsets: prepare k of the pass starts where its first event's compacted rank
+// would be (the sequenced events before it), and ends where prepare k + 1 starts.
+__global__ void tb_seq_meta(SeqCompactArgs A) {
+    const u32 nbp = A.pstart[A.world];
+    for (u32 k = blockIdx.x * blockDim.x + threadIdx.x; k <= nbp; k += gridDim.x * blockDim.x) {
+        u64 g;
+        u64 ts = 0;
+        if (k == nbp) {
+            g = A.start[A.world];
+        } else {
+            u32 s = 0;
+            while (s + 1 < A.world && A.pstart[s + 1] <= k) s++;
+            const u32 b = k - A.pstart[s];
+            g = A.start[s] + A.meta[s][b];
+            ts = A.meta[s][A.nb[s] + 1 + b];
+        }
+        const u64 blk = g >> 8;
+        u32 r = A.blk[blk];
+        for (u64 q = blk << 8; q < g; q++) {
+            const u32 s = tb_seq_source(A, q);
+            r += A.dep[s][q - A.start[s]] != 0;
+        }
+        A.xmeta[k] = r;
+        if (k < nbp) A.xmeta[nbp + 1 + k] = ts;
+    }
+}
+
+// The sequencer's dense codes back at their pass positions (for tb_node_replies, ROUTE_DEP).
+__global__ void tb_seq_expand(SeqCompactArgs A, const u8* xcodes, u8* codes) {
+    const u64 n = A.start[A.world];
+    for (u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (u64)gridDim.x * blockDim.x) {
+        const u32 r = A.map[g];
+        if (r != 0xFFFFFFFFu) codes[g] = xcodes[r];
+    }
+}
+
+// What the sequencer's pass leaves in its globals, into the first shard's (on that shard's stream, so
+// nothing else writes them meanwhile): its panic bits, its latest ok timestamp, and its balance growth
+// (the node's bound is the sum of the shards').  The first shard's reply arena then carries them.
+__global__ void tb_seq_fold(const Globals* xg, Globals* g0, u64 bound0_lo, u64 bound0_hi) {
+    if (blockIdx.x || threadIdx.x) return;
+    g0->panic |= xg->panic;
+    if (xg->commit_timestamp > g0->commit_timestamp) g0->commit_timestamp = xg->commit_timestamp;
+    const u128 grow = tb_u128(xg->bound_lo, xg->bound_hi) - tb_u128(bound0_lo, bound0_hi);
+    const u128 b = tb_sat_add(tb_u128(g0->bound_lo, g0->bound_hi), grow);
+    g0->bound_lo = tb_lo(b);
+    g0->bound_hi = tb_hi(b);
 }
 
 // The transfers the sequenced events read, from their homes: record, posted state, into the
@@ -473,8 +593,10 @@ __global__ __launch_bounds__(256) void tb_seq_event_accounts(const u8* events, u
     tb_seq_insert(aset, w[4], w[5]);
 }
 
-// The accounts, into the sequencer: record and balances from the owner (the only copy).
-__global__ void tb_seq_load_accounts(NodeTablesArgs N, SeqSet aset, Tables X) {
+// The accounts, into the sequencer: record and balances from the owner (the only copy); the balances
+// as loaded are kept (bal0[i]) so the write-back adds the sequencer's changes as deltas — the routed
+// part of the pass may be adding legs to the same (free) accounts meanwhile.
+__global__ void tb_seq_load_accounts(NodeTablesArgs N, SeqSet aset, Tables X, AccountBal* bal0) {
     const u64 n = aset.count[0];
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
         SeqEntry& q = aset.e[aset.list[i]];
@@ -482,6 +604,7 @@ __global__ void tb_seq_load_accounts(NodeTablesArgs N, SeqSet aset, Tables X) {
         const u32 os = tb_account_find(O, q.lo, q.hi);
         if (os == TB_NOT_FOUND) continue;  // no such account
         const Account a = tb_account_load(O, os);
+        if (bal0) bal0[i] = O.acct_bal[os];
         const u32 xs = tb_account_claim(X, q.lo, q.hi, a.timestamp);
         if (xs == TB_NOT_FOUND) continue;  // PANIC_TABLE_FULL set
         tb_account_store_new(X, xs, a);
@@ -520,13 +643,20 @@ __global__ void tb_seq_writeback_transfers(Tables X, u64 base, u64 n, SeqSet tse
     }
 }
 
-// Write-back, on owner o: the balances of every account the sequencer held that o owns.
-__global__ void tb_seq_writeback_accounts(Tables X, SeqSet aset, Tables O, u32 self, u32 world) {
+// Write-back, on owner o: what the sequencer changed in the balances of every account it held that o
+// owns, added as u128 deltas (mod 2^128, exact in aggregate): sums commute with the routed part's
+// legs on the same free accounts; a constrained account's balance only the sequencer touches.
+__global__ void tb_seq_writeback_accounts(Tables X, SeqSet aset, Tables O, u32 self, u32 world, const AccountBal* bal0) {
     const u64 n = aset.count[0];
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
         const SeqEntry& q = aset.e[aset.list[i]];
-        if (q.x == TB_NOT_FOUND || tb_home(q.lo, q.hi, world) != self) continue;
-        O.acct_bal[q.home] = X.acct_bal[q.x];
+        if (q.x == TB_NOT_FOUND || q.home == SEQ_NEW || tb_home(q.lo, q.hi, world) != self) continue;
+        const AccountBal x = X.acct_bal[q.x], b = bal0[i];
+        u8* o = (u8*)&O.acct_bal[q.home];
+        if (x.debits_pending != b.debits_pending) tb_atomic_add_u128(o + BAL_OFF_DEBITS_PENDING, x.debits_pending - b.debits_pending);
+        if (x.debits_posted != b.debits_posted) tb_atomic_add_u128(o + BAL_OFF_DEBITS_POSTED, x.debits_posted - b.debits_posted);
+        if (x.credits_pending != b.credits_pending) tb_atomic_add_u128(o + BAL_OFF_CREDITS_PENDING, x.credits_pending - b.credits_pending);
+        if (x.credits_posted != b.credits_posted) tb_atomic_add_u128(o + BAL_OFF_CREDITS_POSTED, x.credits_posted - b.credits_posted);
     }
 }
 
@@ -538,8 +668,6 @@ __global__ __launch_bounds__(256) void tb_seq_account_ids(const u8* events, u64 
     const u64* w = (const u64*)(events + g * 128);
     tb_seq_insert(aset, w[0], w[1]);
 }
-
-#define SEQ_NEW 0xFFFFFFFEu  // SeqEntry.home: an account the sequencer created this pass
 
 // After the sequencer's create_accounts pass: the accounts its table holds that were not loaded were
 // created by the pass (a rolled-back insert is a tombstone, never found by id).

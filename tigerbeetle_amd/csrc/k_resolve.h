@@ -268,7 +268,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     // The prepare's first timestamp, loaded before any global store of this kernel: on gfx950 a
     // load waits for every earlier store of its wave to complete (vmcnt counts both), so a load
     // left between the per-event stores below would serialise them.
-    const u64 ts0 = P.routed ? 0 : P.batch_ts[b] - L + 1;
+    const u64 ts0 = tb_ts_carried(P) ? 0 : P.batch_ts[b] - L + 1;
     // a. classify.  Each thread owns events tid + k*RESOLVE_THREADS; their scratch words are loaded
     // for every k before any is used (one memory round trip instead of one per k).
     u32 r_info[RESOLVE_K];
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
             panic |= code == TB_CODE_PANIC;
             const bool leg = use_legs && !(info & HZ_POSTVOID) && r_amt[k][1] == 0 && r_amt[k][0] <= LEG_AMT_MASK;
             if (valid) P.info[pe] = info | (ok ? HZ_EVAL_OK : 0) | (ok && !leg ? HZ_LATE : 0);
-            const u64 ts = P.routed ? (valid ? tb_event_ts(P, b, boff, L, i) : 0) : ts0 + i;
+            const u64 ts = tb_ts_carried(P) ? (valid ? tb_event_ts(P, b, boff, L, i) : 0) : ts0 + i;
             tsmax = ok ? ts : tsmax;
             n_app += ok;
             n_fail += valid & !ok;
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                                  r_amt[k][0] <= LEG_AMT_MASK;
                 const bool late_ev = OP == OP_CREATE_TRANSFERS && fin == R_OK && !leg;
                 P.info[pe] = (info & 0xFFFFFF00u) | fin | (eval_ok ? HZ_EVAL_OK : 0) | (late_ev ? HZ_LATE : 0);
-                const u64 ts = P.routed ? tb_event_ts(P, b, boff, L, i) : ts0 + i;
+                const u64 ts = tb_ts_carried(P) ? tb_event_ts(P, b, boff, L, i) : ts0 + i;
                 if (eval_ok) tsmax = ts;  // increasing in i
                 if (fin == R_OK) {
                     if (OP == OP_CREATE_TRANSFERS) {

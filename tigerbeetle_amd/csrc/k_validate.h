@@ -318,7 +318,7 @@ __global__ __launch_bounds__(VALIDATE_THREADS) void tb_transfers_validate(PassAr
         } else if (t.timestamp != 0) {
             code = R_TIMESTAMP_MUST_BE_ZERO;  // :643
         } else {
-            const u64 ts = P.routed ? routed_ts : P.batch_ts[b] - L + j + 1;  // :645
+            const u64 ts = P.routed ? routed_ts : P.ev_ts ? P.ev_ts[e] : P.batch_ts[b] - L + j + 1;  // :645
             code = tb_validate_transfer(P, t, ts, pe, s);
         }
         if (tb_hi(s.amount)) s.hz |= HZ_AMT_HI;

@@ -70,16 +70,18 @@ struct NodeDev {
     hipEvent_t ev_gathered = nullptr, ev_committed = nullptr, ev_applied = nullptr, ev_replied = nullptr;
     // Dirty passes (k_node.h): the block's classification and this device's key sets.
     u8* dep1 = nullptr;
-    u8* dep = nullptr;
+    u8* dep[2] = {};             // by pass parity: the sequencer reads pass p's while pass p + 1 classifies
     u64* dkeys = nullptr;        // [2 pe_src][2]
     u64* dbal = nullptr;         // [2 pe_src][2]
-    u64* dcounts = nullptr;      // [4]
+    u64* dcounts = nullptr;      // [NODE_DC_WORDS] (k_node.h NodeDepArgs)
     u64* h_dcounts = nullptr;    // pinned
     u64* keyset = nullptr;
     u64* markset = nullptr;
     u64 set_mask = 0;
     u64* wb_count = nullptr;     // sequencer write-back: records appended here
     hipEvent_t ev_cls = nullptr, ev_marked = nullptr;
+    hipEvent_t ev_pre = nullptr;  // split pass: this stream before the pass's routed part (the sequencer's loads wait)
+    hipEvent_t ev_xwb = nullptr;  // split pass: this shard's write-back of the sequencer's results done
     // Partitioned account records: the foreign accounts a routed sub-pass imports (k_node.h
     // tb_node_import), and the replicated limit-account bitmap.
     u32* imp_list = nullptr;
@@ -121,7 +123,14 @@ struct TbNode {
     u64* seq_counts = nullptr;   // [0..1] tset, [2..3] aset, [4] loaded transfers
     u64* tset_dups = nullptr;
     u64* aset_dups = nullptr;
-    u8* seq_codes = nullptr;     // [world * pe_src] the pass's dense codes from the sequencer
+    u8* seq_codes = nullptr;     // [world * pe_src] the pass's dense codes from the sequencer (pass positions)
+    u8* seq_xcodes = nullptr;    // [world * pe_src] its dense codes in compacted order
+    u32* seq_map = nullptr;      // [world * pe_src] compacted index of each sequenced event
+    u64* seq_ts = nullptr;       // [world * pe_src] execute timestamps of the compacted events
+    u32* seq_blk = nullptr;      // [world * pe_src / 256 + 2] compaction counts / prefix
+    AccountBal* seq_bal0 = nullptr;  // [6 * world * pe_src] balances as loaded (delta write-back)
+    hipEvent_t ev_xread = nullptr;   // the sequencer has read the split pass's source buffers
+    hipEvent_t ev_x = nullptr;       // the sequencer's results (codes expanded) are final
     u64* h_seq = nullptr;        // pinned scratch words
     u64 passes_clean = 0, passes_split = 0, passes_whole = 0, seq_events = 0;
     bool limit_any = false;          // some account carries a limit flag (the bitmaps are consulted)
@@ -159,7 +168,7 @@ static void node_free(TbNode* N) {
         void* dev[] = {D.stage[0], D.stage[1], D.send[0], D.send[1], D.slot[0], D.slot[1], D.home[0], D.home[1],
                        D.words[0], D.words[1], D.meta[0], D.meta[1], D.block_counts, D.results, D.reply_bytes,
                        D.recv, D.codes, D.legs, D.leg_counts, D.hmeta_dev[0], D.hmeta_dev[1], D.hmeta_dev[2],
-                       D.dep1, D.dep, D.dkeys, D.dbal, D.dcounts, D.keyset, D.markset, D.wb_count,
+                       D.dep1, D.dep[0], D.dep[1], D.dkeys, D.dbal, D.dcounts, D.keyset, D.markset, D.wb_count,
                        D.imp_list, D.imp_count, D.limbits};
         for (void* p : dev) if (p) (void)hipFree(p);
         void* host[] = {D.h_words[0], D.h_words[1], D.h_meta[0], D.h_meta[1], D.hmeta_host[0], D.hmeta_host[1],
@@ -167,7 +176,7 @@ static void node_free(TbNode* N) {
         for (void* p : host) if (p) (void)hipHostFree(p);
         hipEvent_t evs[] = {D.ev_start[0], D.ev_start[1], D.ev_start[2], D.ev_done[0], D.ev_done[1], D.ev_done[2],
                             D.ev_planned[0], D.ev_planned[1], D.ev_copied, D.ev_gathered, D.ev_committed,
-                            D.ev_applied, D.ev_replied, D.ev_cls, D.ev_marked};
+                            D.ev_applied, D.ev_replied, D.ev_cls, D.ev_marked, D.ev_pre, D.ev_xwb};
         for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
         if (D.rs) (void)hipStreamDestroy(D.rs);
         if (D.E) tbgpu_deinit(D.E);
@@ -175,8 +184,10 @@ static void node_free(TbNode* N) {
     if (N->X) {
         (void)hipSetDevice(N->D[0].device);
         void* dev[] = {N->tset_e, N->aset_e, N->tset_list, N->aset_list, N->seq_counts, N->tset_dups, N->aset_dups,
-                       N->seq_codes};
+                       N->seq_codes, N->seq_xcodes, N->seq_map, N->seq_ts, N->seq_blk, N->seq_bal0};
         for (void* p : dev) if (p) (void)hipFree(p);
+        if (N->ev_xread) (void)hipEventDestroy(N->ev_xread);
+        if (N->ev_x) (void)hipEventDestroy(N->ev_x);
         if (N->h_seq) (void)hipHostFree(N->h_seq);
         tbgpu_deinit(N->X);
     }
@@ -297,16 +308,19 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
         // sequencer write-back counter.
         D.set_mask = pow2_at_least(std::max<u64>(1024, 4 * (u64)W * pe)) - 1;
         NALLOC(tbMalloc(&D.dep1, pe));
-        NALLOC(tbMalloc(&D.dep, pe));
+        NALLOC(tbMalloc(&D.dep[0], pe));
+        NALLOC(tbMalloc(&D.dep[1], pe));
         NALLOC(tbMalloc(&D.dkeys, 2 * pe * 16));
         NALLOC(tbMalloc(&D.dbal, 2 * pe * 16));
-        NALLOC(tbMalloc(&D.dcounts, 4 * 8));
-        NALLOC(tbHostMalloc(&D.h_dcounts, 4 * 8, hipHostMallocDefault));
+        NALLOC(tbMalloc(&D.dcounts, NODE_DC_WORDS * 8));
+        NALLOC(tbHostMalloc(&D.h_dcounts, NODE_DC_WORDS * 8, hipHostMallocDefault));
         NALLOC(tbMalloc(&D.keyset, (D.set_mask + 1) * 8));
         NALLOC(tbMalloc(&D.markset, (D.set_mask + 1) * 8));
         NALLOC(tbMalloc(&D.wb_count, 8));
         NALLOC(tbEventCreateWithFlags(&D.ev_cls, hipEventDisableTiming));
         NALLOC(tbEventCreateWithFlags(&D.ev_marked, hipEventDisableTiming));
+        NALLOC(tbEventCreateWithFlags(&D.ev_pre, hipEventDisableTiming));
+        NALLOC(tbEventCreateWithFlags(&D.ev_xwb, hipEventDisableTiming));
         D.imp_cap = 2 * (u64)sc.pass_events_max;
         NALLOC(tbMalloc(&D.imp_list, D.imp_cap * 4));
         NALLOC(tbMalloc(&D.imp_count, 8));
@@ -352,6 +366,14 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
         XALLOC(tbMalloc(&N->tset_dups, 2 * pass * 24));
         XALLOC(tbMalloc(&N->aset_dups, 6 * pass * 24));
         XALLOC(tbMalloc(&N->seq_codes, pass));
+        XALLOC(tbMalloc(&N->seq_xcodes, pass));
+        XALLOC(tbMalloc(&N->seq_map, pass * 4));
+        XALLOC(tbMalloc(&N->seq_ts, pass * 8));
+        XALLOC(tbMalloc(&N->seq_blk, (pass / 256 + 2) * 4));
+        XALLOC(tbMalloc(&N->seq_bal0, 6 * pass * sizeof(AccountBal)));
+        XALLOC(tbEventCreateWithFlags(&N->ev_xread, hipEventDisableTiming));
+        XALLOC(tbEventCreateWithFlags(&N->ev_x, hipEventDisableTiming));
+        XALLOC(hipEventRecord(N->ev_xread, N->X->stream));  // "the previous split pass" exists before the first
         XALLOC(tbHostMalloc(&N->h_seq, 16 * 8, hipHostMallocDefault));
         XALLOC(hipMemset(N->tset_e, 0, (N->tset_mask + 1) * sizeof(SeqEntry)));
         XALLOC(hipMemset(N->aset_e, 0, (N->aset_mask + 1) * sizeof(SeqEntry)));
@@ -365,9 +387,13 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
     return TBGPU_STATUS_OK;
 }
 
-// Drain every device and read back its globals (panic, commit_timestamp).
+// Drain every device (and the sequencer) and read back its globals (panic, commit_timestamp).
 static int node_sync(TbNode* N) {
     int status = TBGPU_STATUS_OK;
+    if (N->X) {
+        NCK(hipSetDevice(N->D[0].device));
+        NCK(hipStreamSynchronize(N->X->stream));
+    }
     for (u32 d = 0; d < N->world; d++) {
         NodeDev& D = N->D[d];
         NCK(hipSetDevice(D.device));
@@ -451,7 +477,7 @@ static int node_commit_accounts(TbNode* N, u32 n, const u64* ts, const void* con
         if (ne) {
             hipLaunchKernelGGL(tb_seq_account_ids, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, xs, X->staging, ne, aset);
             hipLaunchKernelGGL(tb_seq_verify, dim3(256), dim3(256), 0, xs, aset, (u64*)&X->g->panic);
-            hipLaunchKernelGGL(tb_seq_load_accounts, dim3(1024), dim3(256), 0, xs, NT, aset, X->T);
+            hipLaunchKernelGGL(tb_seq_load_accounts, dim3(1024), dim3(256), 0, xs, NT, aset, X->T, (AccountBal*)nullptr);
             NCK(hipGetLastError());
         }
         N->h_seq[0] = N->commit_ts;
@@ -541,6 +567,9 @@ static int node_issue_plan(TbNode* N, NodePass& P, u32 p, const u64* ts, const v
         // prepares as one DMA; host memory over the device's own PCIe link, another device's HBM
         // over xGMI).
         NCK(hipEventRecord(D.ev_start[p % 3], E->copy_stream));
+        // The sequencer of the split pass two passes back may still be reading this parity's buffers.
+        NCK(hipStreamWaitEvent(E->copy_stream, N->ev_xread, 0));
+        NCK(hipStreamWaitEvent(D.rs, N->ev_xread, 0));
         D.ev[par] = D.stage[par];
         if (node_block_resident(D, P, d, inputs, lens)) {
             D.ev[par] = (const u8*)inputs[B.k0];
@@ -821,10 +850,13 @@ static int node_consume(TbNode* N, NodePass& P, u32 p, void* const* outputs, u32
 }
 
 // A dirty pass, SPLIT (k_node.h): the dependent subsequence is committed in order by the sequencer,
-// every other event is routed to its home as in a clean pass.  Synchronous (every earlier pass has
-// drained); the pass's bodies are in the sources' staging buffers (its plan was issued).  all: no
-// overflow certificate — every event goes to the sequencer.  One host round trip for the plan (the
-// routed part's counts, as in a clean pass) and one to learn how many records each home received.
+// every other event is routed to its home as in a clean pass.  Enqueued, nothing drained: the
+// sequencer runs on its own stream beside the routed part, on the pass's sequenced events only
+// (compacted, each with its execute timestamp), loaded with the state from before the pass (every
+// shard's stream is marked before the routed part is issued), and writes its results back as deltas
+// (balances) and into log room reserved per home; the replies wait for it.  all: no overflow
+// certificate — every event goes to the sequencer.  One host round trip: the plan (the routed part's
+// counts, the sequenced events per home), as in a clean pass.
 static int node_split_pass(TbNode* N, NodePass& P, u32 p, const u64* ts, u64 bound_lo, u64 bound_hi, bool all) {
     const u32 W = N->world, par = p & 1;
     tbgpu* X = N->X;
@@ -848,10 +880,10 @@ static int node_split_pass(TbNode* N, NodePass& P, u32 p, const u64* ts, u64 bou
         NodeDev& D = N->D[d];
         const NodeBlock& B = P.blk[d];
         NCK(hipSetDevice(D.device));
-        NCK(hipMemsetAsync(D.dcounts, 0, 4 * 8, D.rs));
+        NCK(hipMemsetAsync(D.dcounts, 0, NODE_DC_WORDS * 8, D.rs));
         if (B.events) {
             const RouteArgs A = route_args(D, B);
-            NodeDepArgs Dp{D.dep1, D.dep, D.dkeys, D.dbal, D.dcounts, all ? 1u : 0u};
+            NodeDepArgs Dp{D.dep1, D.dep[par], D.dkeys, D.dbal, D.dcounts, all ? 1u : 0u};
             hipLaunchKernelGGL(tb_node_classify1, dim3((unsigned)((B.events + ROUTE_THREADS - 1) / ROUTE_THREADS)),
                                dim3(ROUTE_THREADS), 0, D.rs, A, Dp);
             NCK(hipGetLastError());
@@ -880,7 +912,7 @@ static int node_split_pass(TbNode* N, NodePass& P, u32 p, const u64* ts, u64 bou
         hipLaunchKernelGGL(tb_node_sets, dim3(512), dim3(256), 0, D.rs, Sd);
         if (B.events) {
             const RouteArgs A = route_args(D, B);
-            NodeDepArgs Dp{D.dep1, D.dep, D.dkeys, D.dbal, D.dcounts, all ? 1u : 0u};
+            NodeDepArgs Dp{D.dep1, D.dep[par], D.dkeys, D.dbal, D.dcounts, all ? 1u : 0u};
             hipLaunchKernelGGL(tb_node_classify_marked, dim3((unsigned)((B.events + ROUTE_THREADS - 1) / ROUTE_THREADS)),
                                dim3(ROUTE_THREADS), 0, D.rs, A, Dp, D.markset, D.set_mask);
         }
@@ -906,142 +938,164 @@ static int node_split_pass(TbNode* N, NodePass& P, u32 p, const u64* ts, u64 bou
             A.block_counts = D.block_counts;
             A.block_base = D.block_counts + (u64)A.nblocks * W;
             A.words = D.words[par];
-            NodeDepArgs Dp{D.dep1, D.dep, D.dkeys, D.dbal, D.dcounts, all ? 1u : 0u};
+            NodeDepArgs Dp{D.dep1, D.dep[par], D.dkeys, D.dbal, D.dcounts, all ? 1u : 0u};
             hipLaunchKernelGGL(tb_node_classify2, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, D.rs, A, Dp, D.keyset, D.set_mask);
-            A.skip = D.dep;
+            A.skip = D.dep[par];
             hipLaunchKernelGGL(tb_route_classify, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, D.rs, A);
             hipLaunchKernelGGL(tb_route_offsets, dim3(A.world), dim3(1024), 0, D.rs, A);
             hipLaunchKernelGGL(tb_route_scatter, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, D.rs, A, D.send[par], D.slot[par]);
             NCK(hipGetLastError());
         }
         NCK(hipMemcpyAsync(D.h_words[par], D.words[par], ROUTE_WORDS * 8, hipMemcpyDeviceToHost, D.rs));
-        NCK(hipMemcpyAsync(D.h_dcounts, D.dcounts, 4 * 8, hipMemcpyDeviceToHost, D.rs));
+        NCK(hipMemcpyAsync(D.h_dcounts, D.dcounts, NODE_DC_WORDS * 8, hipMemcpyDeviceToHost, D.rs));
         NCK(hipEventRecord(D.ev_planned[par], D.rs));
     }
     NodePlan PL;
     int st = node_read_plan(N, P, p, &PL);
     if (st) return st;
-    u64 n_seq = 0, n_pass = 0;
+    u64 n_seq = 0, n_pass = 0, room[NODE_WORLD_MAX] = {};
     for (u32 d = 0; d < W; d++) {
         n_seq += N->D[d].h_dcounts[2];
         n_pass += P.blk[d].events;
+        for (u32 h = 0; h < W; h++) room[h] += N->D[d].h_dcounts[NODE_DC_HOME + h];
     }
     // -- 2. the routed part, committed by the homes (legs to the owners); its certificate covers the
-    //       whole pass's amounts.
+    //       whole pass's amounts.  First every shard's stream is marked: the sequencer's loads see the
+    //       state before the pass (every earlier pass applied), not the routed part, which touches no
+    //       id, pending transfer or constrained balance a sequenced event reads.
     typedef unsigned __int128 h128;
     const h128 bound = ((h128)bound_hi << 64) | bound_lo;
     const h128 total = bound + PL.S < bound ? ~(h128)0 : bound + PL.S;
     const u32 cert = (total >> 64) == 0 ? TBGPU_CERT_U64 : TBGPU_CERT_U128;
+    for (u32 d = 0; d < W; d++) {
+        NCK(hipSetDevice(N->D[d].device));
+        NCK(hipEventRecord(N->D[d].ev_pre, N->D[d].E->stream));
+    }
     if (!all && (st = node_issue_commit(N, P, p, PL, cert, ts[P.k1 - 1], false))) return st;
-    if ((st = node_sync(N))) return st;
-    // -- 3. the sequencer: the pass at its place (the dependent events verbatim, placeholders
-    //       elsewhere), loaded with what they read, committed in order.
+    // Log room on every home for the transfers the sequencer may create there (one per sequenced
+    // event homed there), after the routed part's.
+    u64 wb_base[NODE_WORLD_MAX];
+    for (u32 h = 0; h < W; h++) {
+        tbgpu* E = N->D[h].E;
+        if (E->log_next + room[h] > E->xlog_cap) {
+            return fail(TBGPU_STATUS_INVALID, "node: transfer log of shard %u full", h);
+        }
+        wb_base[h] = E->log_next;
+        E->log_next += room[h];
+    }
+    // -- 3. the sequencer (its own stream, beside the routed part): the pass's sequenced events
+    //       compacted, loaded with what they read, committed in order.
     const int dev0 = N->D[0].device;
     NCK(hipSetDevice(dev0));
     hipStream_t xs = X->stream;
+    for (u32 d = 0; d < W; d++) {
+        NCK(hipStreamWaitEvent(xs, N->D[d].ev_pre, 0));
+        NCK(hipStreamWaitEvent(xs, N->D[d].ev_planned[par], 0));  // the classification
+    }
     NCK(hipMemsetAsync(X->T.xidx, 0, X->xidx_cap * 8, xs));
     NCK(hipMemsetAsync(X->T.xdup, 0, X->xidx_cap, xs));
     NCK(hipMemsetAsync(X->T.xposted, 0, X->xlog_cap, xs));
     NCK(hipMemsetAsync(N->seq_counts, 0, 8 * 8, xs));
+    NCK(hipMemsetAsync(&X->g->commit_timestamp, 0, 8, xs));
     SeqSet tset{N->tset_e, N->tset_mask, N->tset_list, N->seq_counts, N->tset_dups};
     SeqSet aset{N->aset_e, N->aset_mask, N->aset_list, N->seq_counts + 2, N->aset_dups};
-    SeqGatherArgs G{};
-    G.world = W;
-    G.out = X->staging;
+    const u32 nb = P.k1 - P.k0;
+    SeqCompactArgs C{};
+    C.world = W;
     {
         u64 at = 0;
+        u32 pk = 0;
         for (u32 d = 0; d < W; d++) {
-            G.src[d] = N->D[d].ev[par];
-            G.dep[d] = N->D[d].dep;
-            G.start[d] = at;
+            C.src[d] = N->D[d].ev[par];
+            C.dep[d] = N->D[d].dep[par];
+            C.meta[d] = N->D[d].meta[par];
+            C.nb[d] = P.blk[d].k1 - P.blk[d].k0;
+            C.start[d] = at;
+            C.pstart[d] = pk;
             at += P.blk[d].events;
+            pk += C.nb[d];
         }
-        G.start[W] = at;
+        C.start[W] = at;
+        C.pstart[W] = pk;
     }
+    C.nblk = (u32)((n_pass + 255) / 256);
+    C.blk = N->seq_blk;
+    C.out = X->staging;
+    C.out_ts = N->seq_ts;
+    C.map = N->seq_map;
+    C.xmeta = X->meta;
     NodeTablesArgs NT{};
     NT.world = W;
     for (u32 d = 0; d < W; d++) NT.T[d] = N->D[d].E->T;
     if (n_pass) {
-        hipLaunchKernelGGL(tb_seq_gather, dim3((unsigned)((n_pass + 255) / 256)), dim3(256), 0, xs, G, tset);
-        hipLaunchKernelGGL(tb_seq_load_transfers, dim3(1024), dim3(256), 0, xs, NT, tset, X->T, N->seq_counts + 4, aset);
-        hipLaunchKernelGGL(tb_seq_event_accounts, dim3((unsigned)((n_pass + 255) / 256)), dim3(256), 0, xs, X->staging,
-                           n_pass, aset);
-        hipLaunchKernelGGL(tb_seq_verify, dim3(256), dim3(256), 0, xs, tset, (u64*)&X->g->panic);
-        hipLaunchKernelGGL(tb_seq_verify, dim3(256), dim3(256), 0, xs, aset, (u64*)&X->g->panic);
-        hipLaunchKernelGGL(tb_seq_load_accounts, dim3(1024), dim3(256), 0, xs, NT, aset, X->T);
+        hipLaunchKernelGGL(tb_seq_count, dim3(C.nblk), dim3(256), 0, xs, C);
+        hipLaunchKernelGGL(tb_seq_scan, dim3(1), dim3(1024), 0, xs, C);
+        hipLaunchKernelGGL(tb_seq_compact, dim3(C.nblk), dim3(256), 0, xs, C, tset);
+        hipLaunchKernelGGL(tb_seq_meta, dim3((nb + 256) / 256), dim3(256), 0, xs, C);
         NCK(hipGetLastError());
     }
-    // Its commit timestamp and balance bound: the node's.
-    N->h_seq[0] = N->commit_ts;
-    N->h_seq[1] = bound_lo;
-    N->h_seq[2] = bound_hi;
-    NCK(hipMemcpyAsync(&X->g->commit_timestamp, N->h_seq, 8, hipMemcpyHostToDevice, xs));
-    NCK(hipMemcpyAsync(&X->g->bound_lo, N->h_seq + 1, 16, hipMemcpyHostToDevice, xs));
-    X->commit_ts = N->commit_ts;
-    X->last_batch_ts = N->commit_ts;
-    X->log_next = N->seq_tcap;
-    // The pass's prepares: every block's, in order (their offsets in the pass and timestamps).
-    const u32 nb = P.k1 - P.k0;
-    u64* h_off = X->h_meta;
-    u64* h_ts = X->h_meta + nb + 1;
-    {
-        u64 at = 0;
-        u32 k = 0;
-        h_off[0] = 0;
-        for (u32 d = 0; d < W; d++) {
-            for (u32 j = 0; j < P.blk[d].k1 - P.blk[d].k0; j++, k++) {
-                h_off[k + 1] = at + P.off[d][j + 1];
-                h_ts[k] = ts[P.blk[d].k0 + j];
-            }
-            at += P.blk[d].events;
-        }
+    NCK(hipEventRecord(N->ev_xread, xs));  // the sources' buffers of this pass may be reused
+    if (n_seq) {
+        hipLaunchKernelGGL(tb_seq_load_transfers, dim3(1024), dim3(256), 0, xs, NT, tset, X->T, N->seq_counts + 4, aset);
+        hipLaunchKernelGGL(tb_seq_event_accounts, dim3((unsigned)((n_seq + 255) / 256)), dim3(256), 0, xs, X->staging,
+                           n_seq, aset);
+        hipLaunchKernelGGL(tb_seq_verify, dim3(256), dim3(256), 0, xs, tset, (u64*)&X->g->panic);
+        hipLaunchKernelGGL(tb_seq_verify, dim3(256), dim3(256), 0, xs, aset, (u64*)&X->g->panic);
+        hipLaunchKernelGGL(tb_seq_load_accounts, dim3(1024), dim3(256), 0, xs, NT, aset, X->T, N->seq_bal0);
+        NCK(hipGetLastError());
     }
-    NCK(hipMemcpyAsync(X->meta, X->h_meta, (2 * (u64)nb + 1) * 8, hipMemcpyHostToDevice, xs));
-    if (n_pass && (st = enqueue_call(X, OP_CREATE_TRANSFERS, nb, h_off, X->staging, X->results, X->reply_bytes, false,
-                                     N->seq_codes, 0, nullptr, X->meta))) {
+    // Its balance bound: the node's (its commit timestamp: from its own events, folded below).
+    u64* hs = N->h_seq + 8 * (p & 1);  // by pass parity: the previous pass's copy may be in flight
+    hs[0] = bound_lo;
+    hs[1] = bound_hi;
+    NCK(hipMemcpyAsync(&X->g->bound_lo, hs, 16, hipMemcpyHostToDevice, xs));
+    X->commit_ts = 0;
+    X->last_batch_ts = 0;
+    X->log_next = N->seq_tcap;
+    // One pass of the compacted prepares (nb of them, offsets on the device from tb_seq_meta; the
+    // host needs only the total).
+    u64* h_off = X->h_meta;
+    for (u32 k = 0; k < nb; k++) h_off[k] = 0;
+    h_off[nb] = n_seq;
+    if (n_seq && (st = enqueue_call(X, OP_CREATE_TRANSFERS, nb, h_off, X->staging, X->results, X->reply_bytes, false,
+                                    N->seq_xcodes, 0, nullptr, X->meta, nullptr, nullptr, nullptr, N->seq_ts))) {
         return st;
     }
-    if ((st = engine_sync(X))) return st;
-    const h128 xbound = ((h128)X->h_globals->bound_hi << 64) | X->h_globals->bound_lo;
-    // -- 4. write-back: the new transfers and posted states to their homes, the balances to their
-    //       owners (kernels on those devices, reading the sequencer over xGMI).
+    if (n_pass) {
+        hipLaunchKernelGGL(tb_seq_expand, dim3(1024), dim3(256), 0, xs, C, N->seq_xcodes, N->seq_codes);
+        NCK(hipGetLastError());
+    }
+    NCK(hipEventRecord(N->ev_x, xs));
+    // -- 4. write-back on every shard's stream once the sequencer is done: its new transfers and
+    //       posted states to their homes (into the room reserved above), its balance deltas to the
+    //       owners; the first shard folds in its panic bits, timestamp and bound growth.
     for (u32 d = 0; d < W; d++) {
         NodeDev& D = N->D[d];
         NCK(hipSetDevice(D.device));
-        NCK(hipMemsetAsync(D.wb_count, 0, 8, D.E->stream));
-        hipLaunchKernelGGL(tb_seq_writeback_transfers, dim3(1024), dim3(256), 0, D.E->stream, X->T, N->seq_tcap, n_pass,
-                           tset, D.E->T, d, W, D.E->log_next, D.wb_count);
-        hipLaunchKernelGGL(tb_seq_writeback_accounts, dim3(1024), dim3(256), 0, D.E->stream, X->T, aset, D.E->T, d, W);
-        NCK(hipGetLastError());
-        NCK(hipMemcpyAsync(D.h_dcounts + 3, D.wb_count, 8, hipMemcpyDeviceToHost, D.E->stream));
+        NCK(hipStreamWaitEvent(D.E->stream, N->ev_x, 0));
+        if (n_seq) {
+            NCK(hipMemsetAsync(D.wb_count, 0, 8, D.E->stream));
+            hipLaunchKernelGGL(tb_seq_writeback_transfers, dim3(1024), dim3(256), 0, D.E->stream, X->T, N->seq_tcap, n_seq,
+                               tset, D.E->T, d, W, wb_base[d], D.wb_count);
+            hipLaunchKernelGGL(tb_seq_writeback_accounts, dim3(1024), dim3(256), 0, D.E->stream, X->T, aset, D.E->T, d, W,
+                               (const AccountBal*)N->seq_bal0);
+            NCK(hipGetLastError());
+        }
+        if (d == 0) {
+            hipLaunchKernelGGL(tb_seq_fold, dim3(1), dim3(64), 0, D.E->stream, (const Globals*)X->g, D.E->g, bound_lo, bound_hi);
+            NCK(hipGetLastError());
+        }
+        NCK(hipEventRecord(D.ev_xwb, D.E->stream));
     }
-    // The sequenced part's balance growth goes to the first shard's bound (the node's bound is the
-    // shards' sum): read back below, written after the sync.
-    for (u32 d = 0; d < W; d++) {
-        NCK(hipSetDevice(N->D[d].device));
-        NCK(hipStreamSynchronize(N->D[d].E->stream));
-        N->D[d].E->log_next += N->D[d].h_dcounts[3];
-    }
-    if ((st = node_sync(N))) return st;
-    if (xbound > bound) {
-        tbgpu* E0 = N->D[0].E;
-        const h128 b0 = (((h128)E0->h_globals->bound_hi << 64) | E0->h_globals->bound_lo);
-        const h128 nb0 = b0 + (xbound - bound) < b0 ? ~(h128)0 : b0 + (xbound - bound);
-        N->h_seq[3] = (u64)nb0;
-        N->h_seq[4] = (u64)(nb0 >> 64);
-        NCK(hipSetDevice(N->D[0].device));
-        NCK(hipMemcpyAsync(&E0->g->bound_lo, N->h_seq + 3, 16, hipMemcpyHostToDevice, E0->stream));
-        NCK(hipStreamSynchronize(E0->stream));
-    }
-    N->commit_ts = std::max(N->commit_ts, X->commit_ts);
-    // -- 5. replies (the homes' codes and the sequencer's), then the sequencer's tables empty.
+    // -- 5. replies (the homes' codes and the sequencer's), then the sequencer's tables empty once
+    //       every shard has written back.
     NodeRoute RT;
     node_route(N, PL, RT);
     if ((st = node_issue_replies(N, P, p, RT, N->seq_codes))) return st;
     NCK(hipSetDevice(dev0));
+    for (u32 d = 0; d < W; d++) NCK(hipStreamWaitEvent(xs, N->D[d].ev_xwb, 0));
     hipLaunchKernelGGL(tb_seq_clear, dim3(1024), dim3(256), 0, xs, tset, aset, X->T);
     NCK(hipGetLastError());
-    NCK(hipStreamSynchronize(xs));
     if (all) N->passes_whole++;
     else N->passes_split++;
     N->seq_events += n_seq;
@@ -1114,13 +1168,13 @@ static int node_commit_transfers(TbNode* N, u32 n, const u64* ts, const void* co
         if ((status = node_read_plan(N, Pp, p, &PL))) break;
         const h128 total = bound + PL.S < bound ? ~(h128)0 : bound + PL.S;
         if (PL.dirty || PL.huge || total == ~(h128)0) {
-            consume_upto(p);
-            if (status) break;
-            if ((status = node_sync(N))) break;
-            bound = node_bound(N);
-            if ((status = node_split_pass(N, Pp, p, ts, (u64)bound, (u64)(bound >> 64),
-                                          PL.huge || total == ~(h128)0))) {
-                break;
+            // Split: issued like a clean pass, nothing drained (node_split_pass).  Without the overflow
+            // certificate every event is sequenced, and the shards' bounds are read back after it.
+            const bool all = PL.huge || total == ~(h128)0;
+            if ((status = node_split_pass(N, Pp, p, ts, (u64)bound, (u64)(bound >> 64), all))) break;
+            if (!all) {
+                bound = total;
+                continue;
             }
             consume_upto(p + 1);
             if (status) break;

@@ -83,6 +83,11 @@ struct PassArgs {
     u32 cert_ext;          // 0: certificate from this engine's bound; CERT_EXT_*: given by the caller
     u32 seq_pv;            // 1: balances were set directly (tbgpu_test_set_balances / upserts): every
                            // post / void is dependent, so the replay checks its pending-balance `-=`
+    // Compacted prepares (a node's sequencer, node.h node_split_pass): each event's execute
+    // timestamp, call-relative, instead of batch_ts - L + 1 + i — a prepare holds only its sequenced
+    // events, in order, so positions no longer give timestamps.  Their own timestamp fields are the
+    // caller's (timestamp_must_be_zero still applies).  Null: from batch_ts (or routed).
+    const u64* ev_ts;
     // Balance legs (k_apply.h): with the 64-bit certificate, the balance deltas of independent ok
     // create_transfer events are written as legs, bucketed by account slot per prepare, and summed
     // per account by tb_apply_legs instead of being added with one global atomic per leg.
@@ -154,8 +159,11 @@ static_assert((1u << (64 - LEG_AMT_BITS - 2)) >= LEG_SLOTS_MAX, "leg word: slot-
 // timestamp its source assigned (the source answered timestamp_must_be_zero itself and never
 // routed such an event).
 __device__ static inline u64 tb_event_ts(const PassArgs& P, u32 b, u64 boff, u32 L, u32 i) {
+    if (P.ev_ts) return P.ev_ts[boff + i];
     return P.routed ? *(const u64*)(P.events + (boff + i) * 128 + 120) : P.batch_ts[b] - L + 1 + i;
 }
+// Timestamps not from the prepare's position (routed, or compacted prepares).
+__device__ static inline bool tb_ts_carried(const PassArgs& P) { return P.routed || P.ev_ts; }
 
 // Timing-only ablations (A/B experiments with tools/gpu/ab.sh) exist only in a build with
 // -DTBGPU_TIMING_KNOBS; in the product build every check folds to false, so no environment
