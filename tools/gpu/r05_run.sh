@@ -8,9 +8,15 @@ mkdir -p $O
 for what in "$@"; do
   case $what in
     suite)
-      timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $O/suite.log 2>&1
+      timeout -k 10 1000 python -u -m pytest -q -rf --maxfail=25 --timeout 240 --timeout-method thread -m gpu tests \
+        > $O/suite.log 2>&1
       rc=$?; echo "suite rc=$rc"; tail -3 $O/suite.log
-      [ $rc -ne 0 ] && { grep -E "^E |FAILED|Error" $O/suite.log | head -40; exit $rc; } ;;
+      [ $rc -ne 0 ] && { grep -E "^FAILED|^ERROR" $O/suite.log | head -40; exit $rc; } ;;
+    node_tests)
+      timeout -k 10 900 python -u -m pytest -q -rf --maxfail=25 --timeout 240 --timeout-method thread -m gpu \
+        tests/test_gpu_node.py tests/test_gpu_alloc.py tests/test_gpu_c5.py > $O/node_tests.log 2>&1
+      rc=$?; echo "node tests rc=$rc"; tail -3 $O/node_tests.log
+      [ $rc -ne 0 ] && { grep -E "^FAILED|^ERROR" $O/node_tests.log | head -40; exit $rc; } ;;
     smoke)
       timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
       rc=$?; tail -3 $O/smoke.log; [ $rc -ne 0 ] && exit $rc ;;
