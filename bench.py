@@ -225,7 +225,8 @@ def run_replica_path(args, device):
     import subprocess
     exe = os.path.join(ROOT, "tigerbeetle_amd", "host", "tb_replica_bench")
     out = {}
-    for name, opts in (("in_memory", []), ("in_memory_staged", ["--stage"]), ("with_write_back", ["--write-back"])):
+    for name, opts in (("in_memory", []), ("in_memory_staged", ["--stage"]), ("with_write_back", ["--write-back"]),
+                       ("with_write_back_sync", ["--write-back-sync"])):
         cmd = [exe, "--accounts", str(args.accounts), "--prepares", str(args.replica_prepares),
                "--device", str(device)] + opts
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
@@ -747,6 +748,7 @@ def main():
 
         # 1. The headline's own timed path: the sample resident in HBM, tbgpu_commit_device_async.
         engine.reset_transfers()
+        ct0 = engine.commit_timestamp
         engine.commit_device_async(129, sample_ts, sample_lens, events_dev, res_dev, rb_dev)
         engine.sync()
         rb = engine.to_host(rb_dev, len(sample_lens) * 4).view(np.uint32)
@@ -756,8 +758,10 @@ def main():
         parity.update({"sample_transfers": n_sample, "replies_equal": got_replies(rb, results) == expected,
                        "accounts_equal": acc_equal, "transfers_equal": xfer_equal,
                        "sample_path": "tbgpu_commit_device_async, %d-prepare passes (the timed path)" % args.pass_batches})
-        # 2. The host path: tbgpu_commit_pipelined from registered host memory.
+        # 2. The host path: tbgpu_commit_pipelined from registered host memory (the same timestamps:
+        # the commit timestamp goes back to where the first run started, as a replica's would).
         engine.reset_transfers()
+        engine.set_commit_timestamp(ct0)
         sample_host = engine.to_host(events_dev, n_sample * 128)
         engine.register_host(sample_host)
         rb, results, _ = engine.commit_pipelined(129, sample_ts, sample_lens, sample_host,

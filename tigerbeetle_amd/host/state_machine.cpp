@@ -151,7 +151,9 @@ std::vector<size_t> StateMachine::commit_many(Operation operation, const std::ve
 
 void StateMachine::compact(const Callback& callback, uint64_t op) {
     // The HBM tables need no compaction; the durable copy gets each bar's changes, one bar behind.
-    if (write_back && lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0) {
+    if (write_back && lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0 && compact_sync) {
+        write_back(checkpoint_delta());  // the Zig wrapper's shape: the bar's objects before compact returns
+    } else if (write_back && lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0) {
         wb_deliver_inflight();  // the previous bar's objects: landed while this bar committed
         reserve_write_back();
         WbSet& w = wb_[wb_bar_];

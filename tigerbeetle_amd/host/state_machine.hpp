@@ -186,6 +186,9 @@ public:
     // is asynchronous, src/state_machine.zig:542-567); then calls back.  The forest so trails the
     // engine by at most one bar, and checkpoint() closes the gap.
     void compact(const Callback& callback, uint64_t op);
+    // compact's write-back synchronous instead (tbgpu_checkpoint_delta at the bar's last op, its
+    // objects handed over before compact calls back): the shape zig/state_machine_gpu.zig runs.
+    bool compact_sync = false;
     // The replica's message pool (MessagePool.init_capacity, src/message_pool.zig:98-120): buffers
     // registered once, so prefetch stages a prepare body from its message by DMA.
     void register_message_buffer(void* buffer, size_t bytes);

@@ -31,6 +31,17 @@ for what in "$@"; do
       timeout -k 10 600 python -u bench.py --gpus 2 --same-device --accounts 2000000 --transfers 8000000 --steps 2 \
         --warmup 1 --host-steps 1 > $O/node.json 2> $O/node.err
       rc=$?; echo "node rc=$rc"; tail -c 2500 $O/node.json; tail -5 $O/node.err; [ $rc -ne 0 ] && exit $rc ;;
+    passab)  # device-resident passes of 512 vs 1024 prepares
+      for pb in 512 1024; do
+        timeout -k 10 400 python -u bench.py --steps 3 --warmup 1 --secondary 0 --replica-prepares 0 --host-prepares 0 \
+          --write-back 0 --cpu-sample 0 --host-steps 0 --access-mix 0 --pass-batches $pb > $O/passab_$pb.json 2> $O/passab_$pb.err
+        rc=$?; echo "pass $pb rc=$rc"; python -c "import json,sys;d=json.loads(open('$O/passab_$pb.json').read().strip().splitlines()[-1]);print(d['value'],d['ms_per_step'],d['roofline']['frac'],d['roofline']['avg_launch_ms'],{k:v['avg_launch_ms'] for k,v in d['roofline']['kernels'].items()})"
+        [ $rc -ne 0 ] && { tail -5 $O/passab_$pb.err; exit $rc; }
+      done ;;
+    nodec3)
+      timeout -k 10 600 python -u bench.py --gpus 2 --same-device --accounts 1000000 --transfers 4000000 --steps 2 \
+        --warmup 1 --host-steps 1 --workload c3 > $O/node_c3.json 2> $O/node_c3.err
+      rc=$?; echo "node c3 rc=$rc"; tail -c 2500 $O/node_c3.json; tail -5 $O/node_c3.err; [ $rc -ne 0 ] && exit $rc ;;
     *) echo "unknown step $what"; exit 2 ;;
   esac
 done
