@@ -227,6 +227,22 @@ int tbgpu_checkpoint_delta_wait(tbgpu_t* engine, tbgpu_delta_counts* counts);
 int tbgpu_load_accounts(tbgpu_t* engine, const void* accounts, uint32_t n);
 int tbgpu_load_transfers(tbgpu_t* engine, const void* transfers, const uint8_t* posted_state, uint32_t n);
 
+/* Bounded residency.  The transfer log holds tbgpu_config.transfers_max records; a replica that
+ * outlives it evicts what its forest already holds and loads it back when a prepare names it — the
+ * reference's groove keeps every transfer reachable through its cache and LSM levels
+ * (src/lsm/groove.zig:602-898), loaded by prefetch before commit (src/state_machine.zig:419-467).
+ *   tbgpu_evict_transfers: drops the transfers the last write-back (tbgpu_checkpoint_delta) covered,
+ *     except the newest `keep` log positions; the rest of the log is compacted and re-indexed.
+ *     *evicted = transfers dropped.  Synchronous; no asynchronous write-back may be in flight.
+ *   tbgpu_transfers_maybe_cold: for n ids ({lo, hi} pairs), cold[i] = 1 when the engine does not
+ *     hold id i and may have evicted it (a Bloom filter of evicted ids: false positives only).  The
+ *     wrapper's prefetch loads the cold ids its forest holds (tbgpu_load_transfers, with their posted
+ *     state) before the commit of a prepare that names them (its ids and post / void pending ids);
+ *     an id it does not load is taken as absent, as the reference's groove would report it.
+ * Single-device engines (a node returns TBGPU_STATUS_INVALID). */
+int tbgpu_evict_transfers(tbgpu_t* engine, uint64_t keep, uint64_t* evicted);
+int tbgpu_transfers_maybe_cold(tbgpu_t* engine, const uint64_t* ids, uint32_t n, uint8_t* cold);
+
 /* The replica writes StateMachine.commit_timestamp itself: the header timestamp after every commit
  * (src/vsr/replica.zig:3664-3665) and the checkpoint's value on open / state sync.  The wrapper
  * pushes a changed value here before the next commit, so the engine asserts what the reference
@@ -292,6 +308,9 @@ typedef struct tbgpu_stats {
      * owns (1/N of the ledger) plus room for one routed sub-pass's imported records. */
     uint64_t account_table_bytes;
     uint64_t node_shard_account_bytes[16];
+    /* Bounded residency (tbgpu_evict_transfers): transfers evicted so far, transfer-log positions in
+     * use and in all (a wrapper evicts when the log fills; single-device engines). */
+    uint64_t transfers_evicted, log_used, log_capacity;
 } tbgpu_stats;
 
 int tbgpu_get_stats(tbgpu_t* engine, tbgpu_stats* stats);

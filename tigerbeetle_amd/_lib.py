@@ -94,6 +94,9 @@ class tbgpu_stats(ctypes.Structure):
         ("node_sequenced_events", ctypes.c_uint64),
         ("account_table_bytes", ctypes.c_uint64),
         ("node_shard_account_bytes", ctypes.c_uint64 * 16),
+        ("transfers_evicted", ctypes.c_uint64),
+        ("log_used", ctypes.c_uint64),
+        ("log_capacity", ctypes.c_uint64),
     ]
 
 
@@ -177,6 +180,8 @@ SIGNATURES = [
     ("tbgpu_load_accounts", ctypes.c_int, [_P, _P, _U32]),
     ("tbgpu_load_transfers", ctypes.c_int, [_P, _P, _P, _U32]),
     ("tbgpu_set_commit_timestamp", ctypes.c_int, [_P, _U64]),
+    ("tbgpu_evict_transfers", ctypes.c_int, [_P, _U64, ctypes.POINTER(_U64)]),
+    ("tbgpu_transfers_maybe_cold", ctypes.c_int, [_P, _P, _U32, _P]),
     ("tbgpu_unregister_host", ctypes.c_int, [_P, _P]),
     ("tbgpu_copy_to_device", ctypes.c_int, [_P, _P, _P, _U64]),
     ("tbgpu_marker", ctypes.c_int, [_P, _U32]),

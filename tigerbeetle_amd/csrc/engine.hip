@@ -30,6 +30,7 @@
 #include "k_route.h"
 #include "k_node.h"
 #include "k_workload.h"
+#include "k_evict.h"
 #include "checksum.h"
 
 static thread_local std::string g_err;
@@ -143,6 +144,10 @@ struct tbgpu {
     Globals* g = nullptr;
     u64 account_cap = 0, xidx_cap = 0, xlog_cap = 0;
     u64 log_next = 0;  // next free transfer-log position (host-owned)
+    // Evicted transfers (k_evict.h): the Bloom filter of their ids, its mask, how many so far.
+    u64* bloom = nullptr;
+    u64 bloom_mask = 0;
+    u64 evicted_total = 0;
 
     // Pass scratch.
     u32 pe_max = 0, pb_max = 0;
@@ -356,7 +361,9 @@ static int engine_clear(tbgpu* E) {
     HIPCK(hipMemsetAsync(E->T.xidx, 0, E->xidx_cap * sizeof(u64), E->stream));
     HIPCK(hipMemsetAsync(E->T.xdup, 0, E->xidx_cap, E->stream));
     HIPCK(hipMemsetAsync(E->T.xposted, 0, E->xlog_cap, E->stream));
+    HIPCK(hipMemsetAsync(E->bloom, 0, (E->bloom_mask + 1) / 8, E->stream));
     E->log_next = 0;
+    E->evicted_total = 0;
     HIPCK(hipMemsetAsync(E->g, 0, sizeof(Globals), E->stream));
     HIPCK(hipStreamSynchronize(E->stream));
     E->epoch = 0;
@@ -572,6 +579,13 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     INIT_CK(tbMalloc(&E->T.xposted, E->xlog_cap));
     INIT_CK(tbMalloc(&E->g, sizeof(Globals)));
     {
+        // The evicted-id filter: 8 bits per log position (about 2 % false positives at one log's worth
+        // of evicted ids with 3 hashes; more evictions raise it — extra forest lookups, never errors).
+        const u64 bits = std::min<u64>(1ULL << 34, pow2_at_least(std::max<u64>(1ULL << 16, 8 * E->xlog_cap)));
+        E->bloom_mask = bits - 1;
+        INIT_CK(tbMalloc(&E->bloom, bits / 8));
+    }
+    {
         // tb_flow: 1024-thread workgroups, all resident (see flow_grid).
         hipDeviceProp_t prop;
         int occ = 0;
@@ -768,7 +782,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
     dev_register(E, false);
     if (E->stream) (void)hipStreamSynchronize(E->stream);
     void* bufs[] = {E->ckpt_bal, E->ckpt_mark, E->T.acct_hot, E->T.acct_bal, E->T.acct_cold, E->T.account_mark, E->T.xidx, E->T.xdup, E->T.xlog,
-                    E->T.xposted, E->g, E->info, E->eflags, E->dr,
+                    E->T.xposted, E->g, E->bloom, E->info, E->eflags, E->dr,
                     E->cr, E->ps, E->rs, E->dep_list, E->dep_count, E->amt, E->kid, E->kpid, E->dedup,
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
                     E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->pf_staging, E->kclock, E->r_home,
@@ -2087,6 +2101,9 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     memset(s, 0, sizeof(*s));
     s->passes = E->passes;
     s->account_table_bytes = E->account_cap * (sizeof(AccountHot) + sizeof(AccountBal) + sizeof(AccountCold) + 4);
+    s->transfers_evicted = E->evicted_total;
+    s->log_used = E->log_next;
+    s->log_capacity = E->xlog_cap;
     s->events = E->events;
     s->dependent_events = g.dependent_all;
     s->accounts = g.account_count;
@@ -2963,6 +2980,89 @@ extern "C" int tbgpu_load_transfers(tbgpu_t* E, const void* records, const uint8
 
 // The replica writes commit_timestamp after every commit (= the prepare header's timestamp,
 // src/vsr/replica.zig:3664-3665) and on state sync; the engine's commit asserts use that value.
+// Bounded residency (k_evict.h): drop the written-back transfers older than the newest `keep` log
+// positions.  Only what the last write-back covered can go (the forest holds it); the rest slides to
+// the front of the log and the index is rebuilt from it.  Synchronous.
+extern "C" int tbgpu_evict_transfers(tbgpu_t* E, uint64_t keep, uint64_t* evicted) {
+    API_ENTER(E, true);
+    *evicted = 0;
+    if (E->node) return fail(TBGPU_STATUS_INVALID, "eviction needs a single-device engine");
+    HIPCK(hipSetDevice(E->device));
+    if (E->wb.inflight) return fail(TBGPU_STATUS_INVALID, "an asynchronous write-back is in flight");
+    int st = engine_sync(E);
+    if (st) return st;
+    const u64 written = E->ckpt_valid ? E->ckpt_pos : 0;  // positions the forest already holds
+    const u64 cut = std::min<u64>(written, E->log_next > keep ? E->log_next - keep : 0);
+    if (cut == 0) return TBGPU_STATUS_OK;
+    const u64 n = E->log_next, kept = n - cut;
+    u8* live = E->T.xdup;  // scratch (xidx_cap >= 2 x log bytes), zeroed again below
+    u64* d_evicted = E->wb.d_cnt;  // scratch word (no write-back in flight)
+    HIPCK(hipMemsetAsync(d_evicted, 0, 8, E->stream));
+    const u32 grid = (u32)std::min<u64>(4096, std::max<u64>(1, (n + 255) / 256));
+    hipLaunchKernelGGL(tb_evict_scan, dim3(grid), dim3(256), 0, E->stream, E->T, cut, n, E->bloom, E->bloom_mask, live,
+                       d_evicted);
+    HIPCK(hipGetLastError());
+    // Slide the kept records (and their posted states) to the front, in chunks that never overlap
+    // their sources, then rebuild the index over them.
+    for (u64 a = 0; a < kept; a += cut) {
+        const u64 m = std::min<u64>(cut, kept - a);
+        HIPCK(hipMemcpyAsync(E->T.xlog + a, E->T.xlog + cut + a, m * sizeof(Transfer), hipMemcpyDeviceToDevice, E->stream));
+        HIPCK(hipMemcpyAsync(E->T.xposted + a, E->T.xposted + cut + a, m, hipMemcpyDeviceToDevice, E->stream));
+    }
+    HIPCK(hipMemsetAsync(E->T.xlog + kept, 0, cut * sizeof(Transfer), E->stream));
+    HIPCK(hipMemsetAsync(E->T.xposted + kept, 0, cut, E->stream));
+    HIPCK(hipMemsetAsync(E->T.xidx, 0, E->xidx_cap * sizeof(u64), E->stream));
+    if (kept) {
+        hipLaunchKernelGGL(tb_evict_reindex, dim3((u32)std::min<u64>(4096, (kept + 255) / 256)), dim3(256), 0, E->stream,
+                           E->T, kept, (const u8*)live);
+        HIPCK(hipGetLastError());
+    }
+    HIPCK(hipMemsetAsync(E->T.xdup, 0, E->xidx_cap, E->stream));
+    u64 h_evicted = 0;
+    HIPCK(hipMemcpyAsync(&h_evicted, d_evicted, 8, hipMemcpyDeviceToHost, E->stream));
+    HIPCK(hipStreamSynchronize(E->stream));
+    E->log_next = kept;
+    E->ckpt_pos -= cut;
+    E->evicted_total += h_evicted;
+    E->dedup_force = true;
+    // Live transfers resident: the evicted ones left.
+    if (h_evicted) {
+        HIPCK(hipMemcpy(E->h_globals, E->g, sizeof(Globals), hipMemcpyDeviceToHost));
+        E->h_globals->transfer_count -= std::min<u64>(E->h_globals->transfer_count, h_evicted);
+        HIPCK(hipMemcpy(&E->g->transfer_count, &E->h_globals->transfer_count, 8, hipMemcpyHostToDevice));
+    }
+    *evicted = h_evicted;
+    return TBGPU_STATUS_OK;
+}
+
+// The replica's prefetch after an eviction: which of n ids (lo, hi pairs) the engine may have evicted
+// — not resident, maybe in the filter.  The caller loads those its forest holds (tbgpu_load_transfers)
+// before committing the prepare that names them.
+extern "C" int tbgpu_transfers_maybe_cold(tbgpu_t* E, const uint64_t* ids, uint32_t n, uint8_t* cold) {
+    API_ENTER(E, false);
+    if (E->node) return fail(TBGPU_STATUS_INVALID, "eviction needs a single-device engine");
+    if (n == 0) return TBGPU_STATUS_OK;
+    if (E->evicted_total == 0) {  // nothing ever left: nothing is cold
+        memset(cold, 0, n);
+        return TBGPU_STATUS_OK;
+    }
+    HIPCK(hipSetDevice(E->device));
+    if (E->pending) {
+        const int st = engine_sync(E);
+        if (st) return st;
+    }
+    for (u32 i0 = 0; i0 < n; i0 += E->lookup_cap) {
+        const u32 m = std::min<u32>(n - i0, E->lookup_cap);
+        HIPCK(hipMemcpyAsync(E->lookup_ids, ids + 2 * (u64)i0, (u64)m * 16, hipMemcpyHostToDevice, E->stream));
+        hipLaunchKernelGGL(tb_cold_query, dim3((m + 255) / 256), dim3(256), 0, E->stream, E->T, (const u64*)E->bloom,
+                           E->bloom_mask, E->lookup_ids, m, E->lookup_found);
+        HIPCK(hipGetLastError());
+        HIPCK(hipMemcpyAsync(cold + i0, E->lookup_found, m, hipMemcpyDeviceToHost, E->stream));
+        HIPCK(hipStreamSynchronize(E->stream));
+    }
+    return TBGPU_STATUS_OK;
+}
+
 extern "C" int tbgpu_set_commit_timestamp(tbgpu_t* E, uint64_t timestamp) {
     API_ENTER(E, true);
     if (E->node) return node_api_set_commit_timestamp(E->node, timestamp);

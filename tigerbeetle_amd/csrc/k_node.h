@@ -96,8 +96,13 @@ struct NodeTablesArgs {
 // and never read here: the router's certificate rules out every balance check, and limit and
 // balancing events are sequenced).  Entries go into slots empty in the owned-only table, so they
 // never sit on an owned account's probe chain, and tb_node_import_clear restores the owned-only table
-// exactly.  Two lanes importing one id concurrently may both insert it: both entries are identical,
-// every probe stops at the first, and both are cleared.
+// exactly.
+// One entry per id however many lanes name it (a Zipf-hot account is named by a large share of a
+// pass): a lane claims an empty slot by a CAS of its timestamp word to a marker {bit 63, the id's
+// 63-bit fingerprint} (real timestamps are below 2^63), and a lane that meets its own marker or its
+// id already there stops — the winner alone reads the owner's record, writes the entry and puts the
+// real timestamp last.  (Two ids with one 63-bit fingerprint meeting on one probe chain in one pass
+// would import one of them only: about 2^-63 per pair, the sequencer's own fingerprint bet.)
 __global__ void tb_node_import(Tables H, NodeTablesArgs N, const u8* events, u64 n, u32 self, u32* list, u64* count,
                                u64 cap) {
     const u64 stride = (u64)gridDim.x * blockDim.x;
@@ -106,22 +111,50 @@ __global__ void tb_node_import(Tables H, NodeTablesArgs N, const u8* events, u64
         const u64 lo = w[0], hi = w[1];
         if (tb_id_reserved(lo, hi)) continue;
         const u32 o = tb_home(lo, hi, N.world);
-        if (o == self || tb_account_find(H, lo, hi) != TB_NOT_FOUND) continue;
+        if (o == self) continue;  // owned here: present or absent in the owned table itself
+        const u64 mark = (1ULL << 63) | (tb_fingerprint(lo, hi) >> 1);
+        u64 pos = tb_hash_id(lo, hi) & H.account_mask;
+        u32 slot = TB_NOT_FOUND;
+        for (u64 k = 0; k <= H.account_mask; k++) {
+            u64* tw = &H.acct_hot[pos].timestamp;
+            u64 t = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t == 0) {
+                t = atomicCAS((unsigned long long*)tw, 0ULL, (unsigned long long)mark);
+                if (t == 0) {
+                    slot = (u32)pos;
+                    break;
+                }
+            }
+            if (t == mark) break;  // another lane is importing this id
+            if (!(t >> 63)) {  // a complete entry: this id already?  (a stale read only costs a duplicate entry)
+                AccountHot* e = &H.acct_hot[pos];
+                if (__hip_atomic_load(&e->id_lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == lo &&
+                    __hip_atomic_load(&e->id_hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == hi) {
+                    break;
+                }
+            }
+            pos = (pos + 1) & H.account_mask;
+        }
+        if (slot == TB_NOT_FOUND) continue;
+        const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
+        if (k < cap) list[k] = slot;
+        else tb_panic(H.g, PANIC_TABLE_FULL);
         const Tables& O = N.T[o];
         const u32 os = tb_account_find(O, lo, hi);
-        if (os == TB_NOT_FOUND) continue;  // no such account: validate answers *_account_not_found
-        const AccountHot a = O.acct_hot[os];
-        const u32 slot = tb_account_claim(H, lo, hi, a.timestamp);
-        if (slot == TB_NOT_FOUND) continue;  // PANIC_TABLE_FULL set
         AccountHot* h = &H.acct_hot[slot];
+        if (os == TB_NOT_FOUND) {  // no such account: a tombstone id (probes continue past it) under the marker
+            h->id_lo = ~0ULL;
+            h->id_hi = ~0ULL;
+            continue;
+        }
+        const AccountHot a = O.acct_hot[os];
         h->ledger = a.ledger;
         h->code = a.code;
         h->flags = a.flags;
         h->id_lo = lo;
         h->id_hi = hi;
-        const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
-        if (k < cap) list[k] = slot;
-        else tb_panic(H.g, PANIC_TABLE_FULL);
+        __threadfence();
+        __hip_atomic_store(&h->timestamp, a.timestamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

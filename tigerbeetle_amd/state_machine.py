@@ -390,6 +390,22 @@ class Engine:
             _lib.check(self.lib.tbgpu_load_transfers(self.h, records.ctypes.data, posted_state.ctypes.data,
                                                      len(records)))
 
+    def evict_transfers(self, keep):
+        """Drop the written-back transfers older than the newest `keep` log positions
+        (tbgpu_evict_transfers); returns how many left."""
+        n = ctypes.c_uint64(0)
+        _lib.check(self.lib.tbgpu_evict_transfers(self.h, int(keep), ctypes.byref(n)))
+        return n.value
+
+    def transfers_maybe_cold(self, ids):
+        """ids: uint64 [n, 2] (lo, hi).  Returns bool[n]: not resident and maybe evicted (load them
+        from the forest before the commit that names them)."""
+        ids = np.ascontiguousarray(ids, dtype=np.uint64).reshape(-1, 2)
+        out = np.zeros(len(ids), dtype=np.uint8)
+        if len(ids):
+            _lib.check(self.lib.tbgpu_transfers_maybe_cold(self.h, ids.ctypes.data, len(ids), out.ctypes.data))
+        return out.astype(bool)
+
     def set_commit_timestamp(self, timestamp):
         _lib.check(self.lib.tbgpu_set_commit_timestamp(self.h, int(timestamp)))
 
