@@ -10,6 +10,7 @@
 #   bash tools/gpu/profile.sh dkt                 -> kernel trace + stats of the same run
 #   bash tools/gpu/profile.sh mc                  -> memory-copy + kernel trace of one headline step
 #     (the copy engine's timeline: body copies, their gaps, the per-chunk metadata copies)
+#   bash tools/gpu/profile.sh nkt|nc3             -> kernel trace of the node rehearsal (2 logical shards, C2 / C3)
 #   bash tools/gpu/profile.sh c3|c3h|c4           -> kernel trace of `bench.py --workload c3|c3h|c4`
 #     (1M accounts, 10M transfers, one timed step from host memory: tb_flow's bounds / sweep / run)
 # (rocprofv3 has written its CSVs when the profiled python exits; a crash after that, in process
@@ -20,7 +21,8 @@ MODE=${1:-kt}
 OUT=$R/gpurun_out/prof
 mkdir -p "$OUT"; rm -rf "$OUT/$MODE"
 cd /tmp && export TMPDIR=/tmp
-LEG="--cpu-sample 0 --host-prepares 0 --device-steps 0 --secondary 0 --write-back 0 --replica-prepares 0"
+# The headline (round 5): device-resident passes; the host path (PCIe) is its own leg (--host-steps).
+LEG="--cpu-sample 0 --host-prepares 0 --host-steps 0 --secondary 0 --write-back 0 --replica-prepares 0"
 case $MODE in
   kt) timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 "$R/bench.py" $LEG \
         > "$OUT/bench_kt.log" 2>&1; rc=$? ;;
@@ -34,6 +36,12 @@ case $MODE in
   fetch|write) C=FETCH_SIZE; [ "$MODE" = write ] && C=WRITE_SIZE
       timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/bench.py" $LEG \
         --steps 1 --warmup 0 > "$OUT/$MODE.log" 2>&1; rc=$? ;;
+  nkt) timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/nkt" -o run -- python3 "$R/bench.py" \
+        --gpus 2 --same-device --accounts 2000000 --transfers 8000000 --steps 1 --warmup 1 $LEG --access-mix 0 \
+        > "$OUT/bench_nkt.log" 2>&1; rc=$? ;;
+  nc3) timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/nc3" -o run -- python3 "$R/bench.py" \
+        --gpus 2 --same-device --workload c3 --accounts 1000000 --transfers 4000000 --steps 1 --warmup 1 $LEG --access-mix 0 \
+        > "$OUT/bench_nc3.log" 2>&1; rc=$? ;;
   c3|c3h|c4) timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/bench.py" \
         --workload $MODE --accounts 1000000 --transfers 10000000 --steps 1 --warmup 0 $LEG --access-mix 0 \
         > "$OUT/bench_$MODE.log" 2>&1; rc=$? ;;

@@ -46,6 +46,8 @@ for what in "$@"; do
       timeout -k 10 600 python -u bench.py --gpus 2 --same-device --accounts 1000000 --transfers 4000000 --steps 2 \
         --warmup 1 --host-steps 1 --workload c3 > $O/node_c3.json 2> $O/node_c3.err
       rc=$?; echo "node c3 rc=$rc"; tail -c 2500 $O/node_c3.json; tail -5 $O/node_c3.err; [ $rc -ne 0 ] && exit $rc ;;
+    prof_*)  # a tools/gpu/profile.sh mode
+      bash tools/gpu/profile.sh ${what#prof_}; rc=$?; [ $rc -ne 0 ] && exit $rc ;;
     *) echo "unknown step $what"; exit 2 ;;
   esac
 done
