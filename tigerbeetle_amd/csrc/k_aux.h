@@ -212,19 +212,6 @@ __global__ void tb_delta_posted(Tables T, const u64* pv, const u64* npv, u64* pa
 // > ts0) or when its balances differ from the snapshot; `slots` lists every slot seen, for the
 // snapshot's advance.  n_dev (optional): the id count is 2 x *n_dev (the new transfers' two accounts,
 // counted on the device), n is then only the grid's bound.
-// A wave's lanes with `take` set get consecutive positions from one atomic on *count (one per wave,
-// not one per lane: every lane of the write-back otherwise adds to the same two words).
-__device__ static inline u64 tb_wave_claim(bool take, u64* count) {
-    const u64 m = __ballot(take);
-    if (!m) return 0;
-    const u32 lane = threadIdx.x & 63;
-    const u32 leader = __ffsll((long long)m) - 1;
-    u64 base = 0;
-    if (lane == leader) base = atomicAdd((unsigned long long*)count, (unsigned long long)__popcll(m));
-    base = __shfl(base, leader);
-    return base + __popcll(m & ((1ULL << lane) - 1));
-}
-
 __global__ __launch_bounds__(256) void tb_delta_ids(Tables T, const AccountBal* snap, u64 ts0, const u64* ids, u64 n,
                                                     u32* mark, u32 epoch, u8* out, AccountBal* before, u64* count,
                                                     u32* slots, u64* slot_count, const u64* n_dev = nullptr) {

@@ -55,23 +55,90 @@ struct NodeLegArgs {
 // Owner side: every leg this shard owns, from every home (tb_apply_owner_legs' arithmetic).  The
 // sums commute, so the order of homes and legs does not matter.  A leg for an account this shard
 // lacks is an invariant failure (the owner holds every account it owns): PANIC_ASSERT.
+// Under the 64-bit certificate a workgroup takes a chunk of NAL_CHUNK legs and sums them per (slot,
+// field) in an LDS table first, then adds each sum with one global atomic: a Zipf-hot account (C3: the
+// hottest takes about a fifth of the legs) costs one atomic per chunk, not one per leg — atomics on
+// one address serialise at its L2 channel.  A leg that finds no LDS entry within NAL_PROBES adds
+// directly.  Without the certificate, one exact u128 atomic per leg.
+#define NAL_PER 4
+#define NAL_CHUNK (256 * NAL_PER)
+#define NAL_TABLE 1024
+#define NAL_PROBES 8
 __global__ __launch_bounds__(256) void tb_node_apply_legs(Tables T, NodeLegArgs A) {
-    const u64 stride = (u64)gridDim.x * 256;
-    for (u32 h = 0; h < A.world; h++) {
-        const u64 n = *A.counts[h];
-        const u64* legs = A.legs[h];
-        for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-            const u64* w = legs + i * OWNER_LEG_WORDS;
-            const u64 id_lo = w[0], id_hi = w[1], a_lo = w[2], a_hi = w[3], field = w[4];
-            const u32 slot = tb_account_find(T, id_lo, id_hi);
-            if (slot == TB_NOT_FOUND || field > 3) {
+    __shared__ u64 start[NODE_WORLD_MAX + 1];  // exclusive prefix of the homes' leg counts
+    if (threadIdx.x == 0) {
+        u64 s = 0;
+        for (u32 h = 0; h < A.world; h++) {
+            start[h] = s;
+            s += *A.counts[h];
+        }
+        start[A.world] = s;
+    }
+    __syncthreads();
+    const u64 total = start[A.world];
+    if (!A.cert64) {
+        for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < total; i += (u64)gridDim.x * 256) {
+            u32 h = 0;
+            while (start[h + 1] <= i) h++;
+            const u64* w = A.legs[h] + (i - start[h]) * OWNER_LEG_WORDS;
+            const u32 slot = tb_account_find(T, w[0], w[1]);
+            if (slot == TB_NOT_FOUND || w[4] > 3) {
                 tb_panic(T.g, PANIC_ASSERT);
                 continue;
             }
-            u8* f = (u8*)&T.acct_bal[slot] + 16 * field;
-            if (A.cert64) tb_atomic_add_lo_noret(f, a_lo);
-            else tb_atomic_add_u128(f, tb_u128(a_lo, a_hi));
+            tb_atomic_add_u128((u8*)&T.acct_bal[slot] + 16 * w[4], tb_u128(w[2], w[3]));
         }
+        return;
+    }
+    __shared__ u64 s_key[NAL_TABLE];  // slot << 2 | field, ~0 = empty
+    __shared__ u64 s_sum[NAL_TABLE];
+    for (u64 c0 = (u64)blockIdx.x * NAL_CHUNK; c0 < total; c0 += (u64)gridDim.x * NAL_CHUNK) {
+        for (u32 k = threadIdx.x; k < NAL_TABLE; k += 256) {
+            s_key[k] = ~0ULL;
+            s_sum[k] = 0;
+        }
+        __syncthreads();
+        u64 key[NAL_PER], amt[NAL_PER];
+#pragma unroll
+        for (u32 q = 0; q < NAL_PER; q++) {  // consecutive lanes on consecutive legs; every probe in flight
+            const u64 i = c0 + q * 256 + threadIdx.x;
+            key[q] = ~0ULL;
+            amt[q] = 0;
+            if (i < total) {
+                u32 h = 0;
+                while (start[h + 1] <= i) h++;
+                const u64* w = A.legs[h] + (i - start[h]) * OWNER_LEG_WORDS;
+                const u32 slot = tb_account_find(T, w[0], w[1]);
+                if (slot == TB_NOT_FOUND || w[4] > 3) {
+                    tb_panic(T.g, PANIC_ASSERT);
+                } else {
+                    key[q] = ((u64)slot << 2) | w[4];
+                    amt[q] = w[2];
+                }
+            }
+        }
+#pragma unroll
+        for (u32 q = 0; q < NAL_PER; q++) {
+            if (key[q] == ~0ULL || amt[q] == 0) continue;
+            u32 p = (u32)(tb_mix64(key[q]) & (NAL_TABLE - 1));
+            bool placed = false;
+            for (u32 r = 0; r < NAL_PROBES; r++) {
+                const u64 prev = atomicCAS((unsigned long long*)&s_key[p], ~0ULL, (unsigned long long)key[q]);
+                if (prev == ~0ULL || prev == key[q]) {
+                    atomicAdd((unsigned long long*)&s_sum[p], (unsigned long long)amt[q]);
+                    placed = true;
+                    break;
+                }
+                p = (p + 1) & (NAL_TABLE - 1);
+            }
+            if (!placed) tb_atomic_add_lo_noret((u8*)&T.acct_bal[key[q] >> 2] + 16 * (key[q] & 3), amt[q]);
+        }
+        __syncthreads();
+        for (u32 k = threadIdx.x; k < NAL_TABLE; k += 256) {
+            const u64 kk = s_key[k];
+            if (kk != ~0ULL) tb_atomic_add_lo_noret((u8*)&T.acct_bal[kk >> 2] + 16 * (kk & 3), s_sum[k]);
+        }
+        __syncthreads();
     }
 }
 
@@ -136,7 +203,7 @@ __global__ void tb_node_import(Tables H, NodeTablesArgs N, const u8* events, u64
             pos = (pos + 1) & H.account_mask;
         }
         if (slot == TB_NOT_FOUND) continue;
-        const u64 k = atomicAdd((unsigned long long*)count, 1ULL);
+        const u64 k = tb_wave_claim(true, count);
         if (k < cap) list[k] = slot;
         else tb_panic(H.g, PANIC_TABLE_FULL);
         const Tables& O = N.T[o];
@@ -307,7 +374,7 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_node_classify1(RouteArgs A, 
     D.dep1[e] = d;
     if (d) {  // the ids it reads: its own, and its pending transfer's
         const bool pv = (flags & (TF_POST | TF_VOID)) != 0;
-        const u64 k = atomicAdd((unsigned long long*)&D.counts[0], pv ? 2ULL : 1ULL);
+        const u64 k = tb_wave_claim12(true, pv, &D.counts[0]);
         D.keys[2 * k] = w[0];
         D.keys[2 * k + 1] = w[1];
         if (pv) {
@@ -316,7 +383,7 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_node_classify1(RouteArgs A, 
         }
     }
     if (flags & (TF_BAL_DEBIT | TF_BAL_CREDIT)) {
-        const u64 k = atomicAdd((unsigned long long*)&D.counts[1], 2ULL);
+        const u64 k = tb_wave_claim(true, &D.counts[1], 2);
         D.bal[2 * k] = w[2];
         D.bal[2 * k + 1] = w[3];
         D.bal[2 * k + 2] = w[4];
@@ -361,7 +428,7 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_node_classify_marked(RouteAr
     if (tb_dedup_is_dup_or_present(markset, markset_mask, tb_dedup_key(w[2], w[3])) ||
         tb_dedup_is_dup_or_present(markset, markset_mask, tb_dedup_key(w[4], w[5]))) {
         D.dep1[e] = 16;
-        const u64 k = atomicAdd((unsigned long long*)&D.counts[0], 1ULL);
+        const u64 k = tb_wave_claim(true, &D.counts[0]);
         D.keys[2 * k] = w[0];
         D.keys[2 * k + 1] = w[1];
     }
@@ -369,17 +436,26 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_node_classify_marked(RouteAr
 
 // Final: sequenced = primary-dependent, or its id is a key (the id or pending id of a primary one).
 __global__ __launch_bounds__(ROUTE_THREADS) void tb_node_classify2(RouteArgs A, NodeDepArgs D, const u64* keyset, u64 keyset_mask) {
+    __shared__ u32 s_home[NODE_WORLD_MAX + 1];  // per home, then the block's sequenced events
+    if (threadIdx.x <= A.world) s_home[threadIdx.x] = 0;
+    __syncthreads();
     const u64 e = (u64)blockIdx.x * ROUTE_THREADS + threadIdx.x;
     bool seq = false;
     if (e < A.n) {
         const u64* w = (const u64*)(A.events + e * 128);
         seq = D.dep1[e] != 0 || tb_dedup_is_dup_or_present(keyset, keyset_mask, tb_dedup_key(w[0], w[1]));
         D.dep[e] = seq ? 1 : 0;
-        // The sequencer may create this event's transfer on its home: reserve a log position there.
-        if (seq) atomicAdd((unsigned long long*)&D.counts[NODE_DC_HOME + tb_home(w[0], w[1], A.world)], 1ULL);
+        // The sequencer may create this event's transfer on its home: reserve a log position there
+        // (counted per block in LDS, one global add per home and block).
+        if (seq) atomicAdd(&s_home[tb_home(w[0], w[1], A.world)], 1u);
     }
     const u64 m = __ballot(seq);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd((unsigned long long*)&D.counts[2], (unsigned long long)__popcll(m));
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_home[A.world], (u32)__popcll(m));
+    __syncthreads();
+    if (threadIdx.x <= A.world && s_home[threadIdx.x]) {
+        const u32 slot = threadIdx.x == A.world ? 2 : NODE_DC_HOME + threadIdx.x;
+        atomicAdd((unsigned long long*)&D.counts[slot], (unsigned long long)s_home[threadIdx.x]);
+    }
 }
 
 // The sequencer's prefetch sets: 64-bit fingerprints of 128-bit ids with the id stored by the thread
@@ -418,11 +494,17 @@ __device__ static inline void tb_seq_insert(const SeqSet& S, u64 lo, u64 hi) {
             q->hi = hi;
             q->x = TB_NOT_FOUND;
             q->home = TB_NOT_FOUND;
-            S.list[atomicAdd((unsigned long long*)&S.count[0], 1ULL)] = (u32)pos;
+            S.list[tb_wave_claim(true, &S.count[0])] = (u32)pos;
             return;
         }
         if (cur == tag) {
-            const u64 k = atomicAdd((unsigned long long*)&S.count[1], 1ULL);
+            // The claimant's id, once published, settles it here (tb_seq_clear zeroed both words, and
+            // an id is never 0): only a claim still in flight goes to the list for tb_seq_verify.
+            if (__hip_atomic_load(&q->lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == lo &&
+                __hip_atomic_load(&q->hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == hi) {
+                return;
+            }
+            const u64 k = tb_wave_claim(true, &S.count[1]);
             S.dups[3 * k] = pos;
             S.dups[3 * k + 1] = lo;
             S.dups[3 * k + 2] = hi;
@@ -604,7 +686,7 @@ __global__ void tb_seq_load_transfers(NodeTablesArgs N, SeqSet tset, Tables X, u
         const u32 pos = tb_transfer_find(H, q.lo, q.hi);
         if (pos == TB_NOT_FOUND) continue;
         const Transfer t = H.xlog[pos];
-        const u32 xp = (u32)atomicAdd((unsigned long long*)loaded, 1ULL);
+        const u32 xp = (u32)tb_wave_claim(true, loaded);
         X.xlog[xp] = t;
         X.xposted[xp] = H.xposted[pos];
         q.x = xp;
@@ -656,7 +738,7 @@ __global__ void tb_seq_writeback_transfers(Tables X, u64 base, u64 n, SeqSet tse
         const Transfer& t = X.xlog[base + i];
         if (t.timestamp == 0 || tb_home(tb_lo(t.id), tb_hi(t.id), world) != self) continue;
         if (tb_transfer_find(X, tb_lo(t.id), tb_hi(t.id)) != (u32)(base + i)) continue;  // withdrawn
-        const u64 lp = h_base + atomicAdd((unsigned long long*)h_count, 1ULL);
+        const u64 lp = h_base + tb_wave_claim(true, h_count);
         if (lp >= H.xlog_cap) {
             tb_panic(H.g, PANIC_TABLE_FULL);
             continue;
@@ -665,7 +747,7 @@ __global__ void tb_seq_writeback_transfers(Tables X, u64 base, u64 n, SeqSet tse
         H.xposted[lp] = X.xposted[base + i];
         __threadfence();
         if (tb_transfer_claim_new(H, tb_lo(t.id), tb_hi(t.id), (u32)lp) == TB_NOT_FOUND) continue;
-        atomicAdd((unsigned long long*)&H.g->transfer_count, 1ULL);
+        (void)tb_wave_claim(true, &H.g->transfer_count);
     }
     const u64 m = tset.count[0];
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
@@ -730,7 +812,7 @@ __global__ void tb_seq_writeback_new_accounts(Tables X, SeqSet aset, Tables O, u
         const u32 slot = tb_account_claim(O, q.lo, q.hi, a.timestamp);
         if (slot == TB_NOT_FOUND) continue;  // PANIC_TABLE_FULL set
         tb_account_store_new(O, slot, a);
-        atomicAdd((unsigned long long*)&O.g->account_count, 1ULL);
+        (void)tb_wave_claim(true, &O.g->account_count);
     }
 }
 
@@ -741,7 +823,10 @@ __global__ void tb_seq_clear(SeqSet tset, SeqSet aset, Tables X) {
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) {
         SeqEntry& q = aset.e[aset.list[i]];
         if (q.x != TB_NOT_FOUND) X.acct_hot[q.x] = AccountHot{};
-        q.tag = 0;
+        q.tag = q.lo = q.hi = 0;
     }
-    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nt; i += stride) tset.e[tset.list[i]].tag = 0;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nt; i += stride) {
+        SeqEntry& q = tset.e[tset.list[i]];
+        q.tag = q.lo = q.hi = 0;
+    }
 }

@@ -773,7 +773,8 @@ static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, 
             legs_max += 2 * nh[h];
         }
         if (legs_max) {
-            const u32 grid = (u32)std::min<u64>(4096, std::max<u64>(1, (legs_max / W + 255) / 256));
+            // A chunk of NAL_CHUNK legs per workgroup at twice the mean load (grid-stride past it).
+            const u32 grid = (u32)std::min<u64>(4096, std::max<u64>(1, (2 * legs_max / W + NAL_CHUNK - 1) / NAL_CHUNK));
             hipLaunchKernelGGL(tb_node_apply_legs, dim3(grid), dim3(256), 0, E->stream, E->T, L);
             NCK(hipGetLastError());
         }

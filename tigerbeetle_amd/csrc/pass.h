@@ -248,6 +248,34 @@ __device__ static inline R tb_read_staged(const u8* lds) {
     return r;
 }
 
+// Positions from one shared counter, one atomic per wave instead of one per lane (a counter every lane
+// of a kernel adds to is a single L2 address: its atomics serialise).  The lanes of the wave that are
+// active here with `take` set get consecutive positions, `k` each (a call from divergent code is
+// fine: the ballot sees only the active lanes, and the leader is one of them).
+__device__ static inline u64 tb_wave_claim(bool take, u64* count, u64 k = 1) {
+    const u64 m = __ballot(take);
+    if (!m) return 0;
+    const u32 lane = threadIdx.x & 63;
+    const u32 leader = __ffsll((long long)m) - 1;
+    u64 base = 0;
+    if (lane == leader) base = atomicAdd((unsigned long long*)count, (unsigned long long)(k * __popcll(m)));
+    base = __shfl(base, leader);
+    return base + k * __popcll(m & ((1ULL << lane) - 1));
+}
+
+// The same with a weight of 1 or 2 per lane (two = `two` set).
+__device__ static inline u64 tb_wave_claim12(bool take, bool two, u64* count) {
+    const u64 m = __ballot(take), m2 = __ballot(take && two);
+    if (!m) return 0;
+    const u32 lane = threadIdx.x & 63;
+    const u32 leader = __ffsll((long long)m) - 1;
+    u64 base = 0;
+    if (lane == leader) base = atomicAdd((unsigned long long*)count, (unsigned long long)(__popcll(m) + __popcll(m2)));
+    base = __shfl(base, leader);
+    const u64 lt = (1ULL << lane) - 1;
+    return base + __popcll(m & lt) + __popcll(m2 & lt);
+}
+
 // Wave-level sum of a u128 (64 lanes).
 __device__ static inline u128 tb_wave_sum_u128(u128 v) {
 #pragma unroll
