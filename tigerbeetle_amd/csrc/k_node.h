@@ -220,7 +220,10 @@ __global__ void tb_node_import(Tables H, NodeTablesArgs N, const u8* events, u64
         h->flags = a.flags;
         h->id_lo = lo;
         h->id_hi = hi;
-        __threadfence();
+        // No fence before the timestamp: a lane of this kernel that reads the entry before the fields
+        // reach it only imports the id once more (a duplicate entry, equal by the end), and the
+        // pass's next kernel sees everything.  (An agent-scope fence on gfx950 writes back and
+        // invalidates the XCD's whole L2, per wave: it cost this kernel 1 ms a pass.)
         __hip_atomic_store(&h->timestamp, a.timestamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -691,7 +694,8 @@ __global__ void tb_seq_load_transfers(NodeTablesArgs N, SeqSet tset, Tables X, u
         X.xposted[xp] = H.xposted[pos];
         q.x = xp;
         q.home = pos;
-        __threadfence();
+        // No fence: nothing in this kernel reads the record through the index (the ids are distinct);
+        // the next kernel sees it.
         if (tb_transfer_claim_new(X, q.lo, q.hi, xp) == TB_NOT_FOUND) continue;  // PANIC_TABLE_FULL set
         tb_seq_insert(aset, tb_lo(t.debit_account_id), tb_hi(t.debit_account_id));
         tb_seq_insert(aset, tb_lo(t.credit_account_id), tb_hi(t.credit_account_id));
@@ -744,8 +748,7 @@ __global__ void tb_seq_writeback_transfers(Tables X, u64 base, u64 n, SeqSet tse
             continue;
         }
         H.xlog[lp] = t;
-        H.xposted[lp] = X.xposted[base + i];
-        __threadfence();
+        H.xposted[lp] = X.xposted[base + i];  // read through the index from the next kernel on (no fence)
         if (tb_transfer_claim_new(H, tb_lo(t.id), tb_hi(t.id), (u32)lp) == TB_NOT_FOUND) continue;
         (void)tb_wave_claim(true, &H.g->transfer_count);
     }

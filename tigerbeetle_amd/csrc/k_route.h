@@ -360,8 +360,7 @@ __global__ void tb_upsert_transfers(Tables T, const u8* recs, const u8* state, u
     }
     T.xlog[lp] = t;
     T.xposted[lp] = st ? st - 1 : POSTED_NONE;
-    if (snap_posted) snap_posted[lp] = T.xposted[lp];
-    __threadfence();
+    if (snap_posted) snap_posted[lp] = T.xposted[lp];  // read through the index from the next kernel on (no fence)
     if (tb_transfer_claim_new(T, tb_lo(t.id), tb_hi(t.id), (u32)lp) == TB_NOT_FOUND) atomicOr(status, 1u);
     atomicAdd((unsigned long long*)&T.g->transfer_count, 1ULL);
 }
