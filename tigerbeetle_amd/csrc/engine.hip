@@ -968,7 +968,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
             HIPCK(hipMemsetAsync(imp->count, 0, 8, E->stream));
             const u32 ig = (u32)std::min<u64>(4096, (2 * n + 255) / 256);
             hipLaunchKernelGGL(tb_node_import, dim3(ig), dim3(256), 0, E->stream, E->T, imp->N, events_dev + P.e0 * 128, n,
-                               imp->self, imp->list, imp->count, imp->cap);
+                               imp->self, imp->list, imp->count, imp->cap, imp->os_of);
             HIPCK(hipGetLastError());
         }
         if (n > 0) {
@@ -2758,7 +2758,7 @@ extern "C" int tbgpu_commit_routed_owner_async(tbgpu_t* E, uint64_t n, const voi
     }
     HIPCK(hipMemcpyAsync(E->meta, E->h_meta, (2 * nb + 1) * 8, hipMemcpyHostToDevice, E->stream));
     std::vector<u64> off(h_off, h_off + nb + 1);
-    OwnerLegArgs O{world, self, (u64*)legs_dev, legs_cap, leg_counts_dev};
+    OwnerLegArgs O{world, self, (u64*)legs_dev, legs_cap, leg_counts_dev, nullptr, OWNER_LEG_WORDS};
     int st = enqueue_call(E, OP_CREATE_TRANSFERS, (u32)nb, off.data(), (const u8*)events_dev, E->results,
                           E->reply_bytes, true, codes_dev, cert, nullptr, nullptr, &O);
     if (st) return st;

@@ -52,9 +52,9 @@ struct NodeLegArgs {
     u32 cert64;                         // no balance can reach 2^64 this pass: low-word adds
 };
 
-// Owner side: every leg this shard owns, from every home (tb_apply_owner_legs' arithmetic).  The
-// sums commute, so the order of homes and legs does not matter.  A leg for an account this shard
-// lacks is an invariant failure (the owner holds every account it owns): PANIC_ASSERT.
+// Owner side: every leg this shard owns, from every home, each naming the account's slot here (k_route.h
+// NODE_LEG_WORDS: no probe).  The sums commute, so the order of homes and legs does not matter.  A leg
+// whose slot is out of range or unknown (TB_NOT_FOUND: the home panicked) is skipped.
 // Under the 64-bit certificate a workgroup takes a chunk of NAL_CHUNK legs and sums them per (slot,
 // field) in an LDS table first, then adds each sum with one global atomic: a Zipf-hot account (C3: the
 // hottest takes about a fifth of the legs) costs one atomic per chunk, not one per leg — atomics on
@@ -76,17 +76,14 @@ __global__ __launch_bounds__(256) void tb_node_apply_legs(Tables T, NodeLegArgs 
     }
     __syncthreads();
     const u64 total = start[A.world];
+    const u64 nslots = T.account_mask + 1;
     if (!A.cert64) {
         for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < total; i += (u64)gridDim.x * 256) {
             u32 h = 0;
             while (start[h + 1] <= i) h++;
-            const u64* w = A.legs[h] + (i - start[h]) * OWNER_LEG_WORDS;
-            const u32 slot = tb_account_find(T, w[0], w[1]);
-            if (slot == TB_NOT_FOUND || w[4] > 3) {
-                tb_panic(T.g, PANIC_ASSERT);
-                continue;
-            }
-            tb_atomic_add_u128((u8*)&T.acct_bal[slot] + 16 * w[4], tb_u128(w[2], w[3]));
+            const u64* w = A.legs[h] + (i - start[h]) * NODE_LEG_WORDS;
+            if ((w[0] >> 2) >= nslots || (w[0] >> 2) == TB_NOT_FOUND) continue;
+            tb_atomic_add_u128((u8*)&T.acct_bal[w[0] >> 2] + 16 * (w[0] & 3), tb_u128(w[1], w[2]));
         }
         return;
     }
@@ -100,26 +97,21 @@ __global__ __launch_bounds__(256) void tb_node_apply_legs(Tables T, NodeLegArgs 
         __syncthreads();
         u64 key[NAL_PER], amt[NAL_PER];
 #pragma unroll
-        for (u32 q = 0; q < NAL_PER; q++) {  // consecutive lanes on consecutive legs; every probe in flight
+        for (u32 q = 0; q < NAL_PER; q++) {  // consecutive lanes on consecutive legs
             const u64 i = c0 + q * 256 + threadIdx.x;
             key[q] = ~0ULL;
             amt[q] = 0;
             if (i < total) {
                 u32 h = 0;
                 while (start[h + 1] <= i) h++;
-                const u64* w = A.legs[h] + (i - start[h]) * OWNER_LEG_WORDS;
-                const u32 slot = tb_account_find(T, w[0], w[1]);
-                if (slot == TB_NOT_FOUND || w[4] > 3) {
-                    tb_panic(T.g, PANIC_ASSERT);
-                } else {
-                    key[q] = ((u64)slot << 2) | w[4];
-                    amt[q] = w[2];
-                }
+                const u64* w = A.legs[h] + (i - start[h]) * NODE_LEG_WORDS;
+                key[q] = w[0];
+                amt[q] = w[1];
             }
         }
 #pragma unroll
         for (u32 q = 0; q < NAL_PER; q++) {
-            if (key[q] == ~0ULL || amt[q] == 0) continue;
+            if ((key[q] >> 2) >= nslots || (key[q] >> 2) == TB_NOT_FOUND || amt[q] == 0) continue;
             u32 p = (u32)(tb_mix64(key[q]) & (NAL_TABLE - 1));
             bool placed = false;
             for (u32 r = 0; r < NAL_PROBES; r++) {
@@ -171,7 +163,7 @@ struct NodeTablesArgs {
 // real timestamp last.  (Two ids with one 63-bit fingerprint meeting on one probe chain in one pass
 // would import one of them only: about 2^-63 per pair, the sequencer's own fingerprint bet.)
 __global__ void tb_node_import(Tables H, NodeTablesArgs N, const u8* events, u64 n, u32 self, u32* list, u64* count,
-                               u64 cap) {
+                               u64 cap, u32* os_of) {
     const u64 stride = (u64)gridDim.x * blockDim.x;
     for (u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x; g < 2 * n; g += stride) {
         const u64* w = (const u64*)(events + (g >> 1) * 128) + 2 + 2 * (g & 1);  // debit @16, credit @32
@@ -183,8 +175,10 @@ __global__ void tb_node_import(Tables H, NodeTablesArgs N, const u8* events, u64
         u64 pos = tb_hash_id(lo, hi) & H.account_mask;
         u32 slot = TB_NOT_FOUND;
         for (u64 k = 0; k <= H.account_mask; k++) {
+            // Plain (cached) reads: a stale one costs a failed CAS (which returns the truth) or a
+            // duplicate entry, never a wrong one.
             u64* tw = &H.acct_hot[pos].timestamp;
-            u64 t = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            u64 t = *tw;
             if (t == 0) {
                 t = atomicCAS((unsigned long long*)tw, 0ULL, (unsigned long long)mark);
                 if (t == 0) {
@@ -194,11 +188,8 @@ __global__ void tb_node_import(Tables H, NodeTablesArgs N, const u8* events, u64
             }
             if (t == mark) break;  // another lane is importing this id
             if (!(t >> 63)) {  // a complete entry: this id already?  (a stale read only costs a duplicate entry)
-                AccountHot* e = &H.acct_hot[pos];
-                if (__hip_atomic_load(&e->id_lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == lo &&
-                    __hip_atomic_load(&e->id_hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == hi) {
-                    break;
-                }
+                const AccountHot* e = &H.acct_hot[pos];
+                if (e->id_lo == lo && e->id_hi == hi) break;
             }
             pos = (pos + 1) & H.account_mask;
         }
@@ -215,6 +206,7 @@ __global__ void tb_node_import(Tables H, NodeTablesArgs N, const u8* events, u64
             continue;
         }
         const AccountHot a = O.acct_hot[os];
+        os_of[slot] = os;  // the owner's slot, for this pass's owner legs
         h->ledger = a.ledger;
         h->code = a.code;
         h->flags = a.flags;
@@ -236,6 +228,7 @@ struct NodeImport {
     u32* list;     // [cap] slots inserted
     u64* count;
     u64 cap;
+    u32* os_of;    // [account_cap] imported slot -> the account's slot on its owner
 };
 
 __global__ void tb_node_import_clear(Tables H, const u32* list, const u64* count) {

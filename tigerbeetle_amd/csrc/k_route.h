@@ -377,15 +377,21 @@ __global__ void tb_upsert_transfers(Tables T, const u8* recs, const u8* state, u
 //     local table by the replay: a leg whose owner is another rank goes there and the local copy is
 //     cancelled (adds are mod 2^128; free balances feed no check in a clean pass, so the transient
 //     local value is never read).
-// Leg on the wire: {account id lo, hi, amount lo, hi, field (BAL_OFF / 16)}.
+// Leg on the wire: {account id lo, hi, amount lo, hi, field (BAL_OFF / 16)}.  The node engine
+// (os_of set) sends the account's slot on its owner instead of its id — {slot << 2 | field, amount lo,
+// hi} — so the owner adds without a probe: an owned account's slot is the home's own, an imported
+// one's is what the import read (tb_node_import's os_of).
 #define OWNER_LEG_WORDS 5
+#define NODE_LEG_WORDS 3
 
 struct OwnerLegArgs {
     u32 world;
     u32 self;
-    u64* legs;      // [world][cap][OWNER_LEG_WORDS]: owner o's legs at legs + o * cap * OWNER_LEG_WORDS
+    u64* legs;      // [world][cap][words]: owner o's legs at legs + o * cap * words
     u64 cap;        // legs per owner region
     u64* counts;    // [world] legs written per owner (zeroed by the host before the call)
+    const u32* os_of;  // node engine: [home slot] -> owner slot of an imported account (null: id legs)
+    u32 words;      // OWNER_LEG_WORDS (id legs) or NODE_LEG_WORDS (slot legs)
 };
 
 __global__ __launch_bounds__(256) void tb_owner_legs(PassArgs P, OwnerLegArgs O) {
@@ -394,13 +400,14 @@ __global__ __launch_bounds__(256) void tb_owner_legs(PassArgs P, OwnerLegArgs O)
     if (threadIdx.x < O.world) s_cnt[threadIdx.x] = 0;
     __syncthreads();
     const u32 pe = blockIdx.x * 256 + threadIdx.x;
-    u32 owner[2] = {0, 0}, pos[2] = {0, 0};
+    u32 owner[2] = {0, 0}, pos[2] = {0, 0}, oslot[2] = {0, 0};
     bool emit[2] = {false, false};
     Transfer t;
     u32 field0 = 0;
     if (pe < P.n && P.codes[P.e0 + pe] == R_OK) {
         t = P.T.xlog[P.log_base + pe];
-        const bool dep = (P.info[pe] & HZ_DEP) != 0;
+        const u32 info = P.info[pe];
+        const bool dep = (info & HZ_DEP) != 0;
         field0 = (t.flags & TF_PENDING) ? 0 : 1;  // debits_pending / debits_posted (+2: credits)
 #pragma unroll
         for (u32 s = 0; s < 2; s++) {
@@ -408,14 +415,18 @@ __global__ __launch_bounds__(256) void tb_owner_legs(PassArgs P, OwnerLegArgs O)
             owner[s] = tb_home(tb_lo(id), tb_hi(id), O.world);
             emit[s] = !(dep && owner[s] == O.self);
             if (emit[s]) pos[s] = atomicAdd(&s_cnt[owner[s]], 1u);
-            if (emit[s] && dep) {  // cancel the replay's local add: the owner applies it
-                const u32 slot = tb_account_find(P.T, tb_lo(id), tb_hi(id));
-                if (slot == TB_NOT_FOUND) {
-                    tb_panic(P.T.g, PANIC_ASSERT);
-                } else {
-                    u8* bal = (u8*)&P.T.acct_bal[slot];
-                    tb_atomic_add_u128(bal + 16 * (field0 + 2 * s), (u128)0 - t.amount);
-                }
+            if (!emit[s] || (!dep && !O.os_of)) continue;
+            // This shard's slot of the account (validate's, or a probe for an event it did not reach).
+            const u32 slot = (info & HZ_ACCTS) ? (s ? P.cr[pe] : P.dr[pe]) : tb_account_find(P.T, tb_lo(id), tb_hi(id));
+            if (slot == TB_NOT_FOUND) {  // an ok event's account is always here: invariant failure
+                tb_panic(P.T.g, PANIC_ASSERT);
+                oslot[s] = TB_NOT_FOUND;  // the owner skips it (its position in the region is taken)
+                continue;
+            }
+            if (O.os_of) oslot[s] = owner[s] == O.self ? slot : O.os_of[slot];
+            if (dep) {  // cancel the replay's local add: the owner applies it
+                u8* bal = (u8*)&P.T.acct_bal[slot];
+                tb_atomic_add_u128(bal + 16 * (field0 + 2 * s), (u128)0 - t.amount);
             }
         }
     }
@@ -433,8 +444,14 @@ __global__ __launch_bounds__(256) void tb_owner_legs(PassArgs P, OwnerLegArgs O)
             tb_panic(P.T.g, PANIC_ASSERT);
             continue;
         }
+        u64* w = O.legs + ((u64)owner[s] * O.cap + k) * O.words;
+        if (O.os_of) {
+            w[0] = ((u64)oslot[s] << 2) | (field0 + 2 * s);
+            w[1] = tb_lo(t.amount);
+            w[2] = tb_hi(t.amount);
+            continue;
+        }
         const u128 id = s ? t.credit_account_id : t.debit_account_id;
-        u64* w = O.legs + ((u64)owner[s] * O.cap + k) * OWNER_LEG_WORDS;
         w[0] = tb_lo(id);
         w[1] = tb_hi(id);
         w[2] = tb_lo(t.amount);

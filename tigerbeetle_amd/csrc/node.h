@@ -87,6 +87,7 @@ struct NodeDev {
     u32* imp_list = nullptr;
     u64* imp_count = nullptr;
     u64 imp_cap = 0;
+    u32* imp_os = nullptr;  // [account_cap] an imported slot's slot on the account's owner (owner legs)
     u64* limbits = nullptr;
     u64 limmask = 0;             // bits - 1
 };
@@ -169,7 +170,7 @@ static void node_free(TbNode* N) {
                        D.words[0], D.words[1], D.meta[0], D.meta[1], D.block_counts, D.results, D.reply_bytes,
                        D.recv, D.codes, D.legs, D.leg_counts, D.hmeta_dev[0], D.hmeta_dev[1], D.hmeta_dev[2],
                        D.dep1, D.dep[0], D.dep[1], D.dkeys, D.dbal, D.dcounts, D.keyset, D.markset, D.wb_count,
-                       D.imp_list, D.imp_count, D.limbits};
+                       D.imp_list, D.imp_count, D.imp_os, D.limbits};
         for (void* p : dev) if (p) (void)hipFree(p);
         void* host[] = {D.h_words[0], D.h_words[1], D.h_meta[0], D.h_meta[1], D.hmeta_host[0], D.hmeta_host[1],
                         D.hmeta_host[2], D.h_arena[0], D.h_arena[1], D.h_arena[2], D.h_dcounts};
@@ -284,7 +285,7 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
         NALLOC(tbMalloc(&D.reply_bytes, (u64)N->pb_src * 4));
         NALLOC(tbMalloc(&D.recv, N->recv_cap * 128));
         NALLOC(tbMalloc(&D.codes, N->recv_cap));
-        NALLOC(tbMalloc(&D.legs, legs_cap_total * OWNER_LEG_WORDS * 8));
+        NALLOC(tbMalloc(&D.legs, legs_cap_total * NODE_LEG_WORDS * 8));
         NALLOC(tbMalloc(&D.leg_counts, (u64)W * 8));
         const u64 hm = 2 * ((N->recv_cap + BATCH_EVENTS_MAX - 2) / (BATCH_EVENTS_MAX - 1) + 2) + 1;
         for (int k = 0; k < 3; k++) {
@@ -324,6 +325,7 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
         D.imp_cap = 2 * (u64)sc.pass_events_max;
         NALLOC(tbMalloc(&D.imp_list, D.imp_cap * 4));
         NALLOC(tbMalloc(&D.imp_count, 8));
+        NALLOC(tbMalloc(&D.imp_os, D.E->account_cap * 4));
         // 16 bits per account of the ledger: a false positive (which only sequences an event) is at
         // most 1 in 16 even when every account is limited.
         const u64 lim_bits = std::min<u64>(1ULL << 34, pow2_at_least(std::max<u64>(1ULL << 16, 16 * config->accounts_max)));
@@ -743,7 +745,7 @@ static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, 
                 h_ts[k] = ts_max;
             }
             NCK(hipMemcpyAsync(D.hmeta_dev[tri], h_off, (2 * nb + 1) * 8, hipMemcpyHostToDevice, E->stream));
-            OwnerLegArgs O{W, h, D.legs, 2 * nh[h], D.leg_counts};
+            OwnerLegArgs O{W, h, D.legs, 2 * nh[h], D.leg_counts, D.imp_os, NODE_LEG_WORDS};
             NodeImport imp{};
             imp.N.world = W;
             for (u32 d = 0; d < W; d++) imp.N.T[d] = N->D[d].E->T;
@@ -751,6 +753,7 @@ static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, 
             imp.list = D.imp_list;
             imp.count = D.imp_count;
             imp.cap = D.imp_cap;
+            imp.os_of = D.imp_os;
             const int st = enqueue_call(E, OP_CREATE_TRANSFERS, (u32)nb, h_off, D.recv, E->results, E->reply_bytes,
                                         true, D.codes, cert, nullptr, D.hmeta_dev[tri], &O, nullptr, &imp);
             if (st) return st;
@@ -768,7 +771,7 @@ static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, 
         u64 legs_max = 0;
         for (u32 h = 0; h < W; h++) {
             if (h != o) NCK(hipStreamWaitEvent(E->stream, N->D[h].ev_committed, 0));
-            L.legs[h] = N->D[h].legs + (u64)o * 2 * nh[h] * OWNER_LEG_WORDS;
+            L.legs[h] = N->D[h].legs + (u64)o * 2 * nh[h] * NODE_LEG_WORDS;
             L.counts[h] = N->D[h].leg_counts + o;
             legs_max += 2 * nh[h];
         }
