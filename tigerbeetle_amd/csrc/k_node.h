@@ -48,6 +48,7 @@ __global__ __launch_bounds__(256) void tb_node_gather(NodeGatherArgs A) {
 struct NodeLegArgs {
     const u64* legs[NODE_WORLD_MAX];    // home h's leg region for this owner
     const u64* counts[NODE_WORLD_MAX];  // home h's leg count for this owner
+    u64 region[NODE_WORLD_MAX];         // legs the region holds (a larger count is a panic at the home)
     u32 world;
     u32 cert64;                         // no balance can reach 2^64 this pass: low-word adds
 };
@@ -70,7 +71,12 @@ __global__ __launch_bounds__(256) void tb_node_apply_legs(Tables T, NodeLegArgs 
         u64 s = 0;
         for (u32 h = 0; h < A.world; h++) {
             start[h] = s;
-            s += *A.counts[h];
+            u64 c = *A.counts[h];
+            if (c > A.region[h]) {  // guard (0x400): never read past a home's region
+                tb_panic(T.g, PANIC_ASSERT | 0x400);
+                c = A.region[h];
+            }
+            s += c;
         }
         start[A.world] = s;
     }

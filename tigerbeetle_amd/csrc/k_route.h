@@ -423,7 +423,18 @@ __global__ __launch_bounds__(256) void tb_owner_legs(PassArgs P, OwnerLegArgs O)
                 oslot[s] = TB_NOT_FOUND;  // the owner skips it (its position in the region is taken)
                 continue;
             }
-            if (O.os_of) oslot[s] = owner[s] == O.self ? slot : O.os_of[slot];
+            if (slot > P.T.account_mask) {  // guard (diagnostic panic bit 0x100)
+                tb_panic(P.T.g, PANIC_ASSERT | 0x100);
+                oslot[s] = TB_NOT_FOUND;
+                continue;
+            }
+            if (O.os_of) {
+                oslot[s] = owner[s] == O.self ? slot : O.os_of[slot];
+                if (oslot[s] > P.T.account_mask) {  // guard (0x200): shards share one table size
+                    tb_panic(P.T.g, PANIC_ASSERT | 0x200);
+                    oslot[s] = TB_NOT_FOUND;
+                }
+            }
             if (dep) {  // cancel the replay's local add: the owner applies it
                 u8* bal = (u8*)&P.T.acct_bal[slot];
                 tb_atomic_add_u128(bal + 16 * (field0 + 2 * s), (u128)0 - t.amount);

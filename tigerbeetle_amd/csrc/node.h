@@ -772,6 +772,7 @@ static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, 
         for (u32 h = 0; h < W; h++) {
             if (h != o) NCK(hipStreamWaitEvent(E->stream, N->D[h].ev_committed, 0));
             L.legs[h] = N->D[h].legs + (u64)o * 2 * nh[h] * NODE_LEG_WORDS;
+            L.region[h] = 2 * nh[h];
             L.counts[h] = N->D[h].leg_counts + o;
             legs_max += 2 * nh[h];
         }
