@@ -88,7 +88,10 @@ __global__ __launch_bounds__(256) void tb_node_apply_legs(Tables T, NodeLegArgs 
             u32 h = 0;
             while (start[h + 1] <= i) h++;
             const u64* w = A.legs[h] + (i - start[h]) * NODE_LEG_WORDS;
-            if ((w[0] >> 2) >= nslots || (w[0] >> 2) == TB_NOT_FOUND) continue;
+            if ((w[0] >> 2) >= nslots || (w[0] >> 2) == TB_NOT_FOUND) {  // NOT_FOUND: the home panicked; else 0x800
+                if ((w[0] >> 2) != TB_NOT_FOUND) tb_panic(T.g, PANIC_ASSERT | 0x800);
+                continue;
+            }
             tb_atomic_add_u128((u8*)&T.acct_bal[w[0] >> 2] + 16 * (w[0] & 3), tb_u128(w[1], w[2]));
         }
         return;
@@ -117,6 +120,7 @@ __global__ __launch_bounds__(256) void tb_node_apply_legs(Tables T, NodeLegArgs 
         }
 #pragma unroll
         for (u32 q = 0; q < NAL_PER; q++) {
+            if (key[q] != ~0ULL && (key[q] >> 2) >= nslots && (key[q] >> 2) != TB_NOT_FOUND) tb_panic(T.g, PANIC_ASSERT | 0x800);
             if ((key[q] >> 2) >= nslots || (key[q] >> 2) == TB_NOT_FOUND || amt[q] == 0) continue;
             u32 p = (u32)(tb_mix64(key[q]) & (NAL_TABLE - 1));
             bool placed = false;
