@@ -523,6 +523,12 @@ def main():
         return launch_check(args, world, rank)
     if launched and world > 1 and world != args.gpus:
         raise SystemExit("bench.py: launched with %d ranks but --gpus %d" % (world, args.gpus))
+    if args.gpus > 1 and args.engine == "node":
+        # The node engine keeps three streams per shard (copy, route, engine) and the sequencer's on the
+        # first device: with HIP's default of 4 hardware queues per device the sequencer's stream shares
+        # a queue with shard 0's engine stream and waits behind its routed part.  Read by the HIP
+        # runtime when it starts (no HIP call has been made yet); an explicit setting is kept.
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     import torch
     import torch.distributed as dist
 

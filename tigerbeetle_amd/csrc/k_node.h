@@ -493,7 +493,10 @@ __device__ static inline void tb_seq_insert(const SeqSet& S, u64 lo, u64 hi) {
     u64 pos = tb_mix64(tag) & S.mask;
     for (u64 n = 0; n <= S.mask; n++) {
         SeqEntry* q = &S.e[pos];
-        u64 cur = __hip_atomic_load(&q->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // Plain (cached) reads: a Zipf-hot id is inserted by a large share of the lanes, and reads of
+        // one address that bypass the cache serialise.  A stale 0 costs a CAS that returns the truth;
+        // stale id words send the lane to the dups list (tb_seq_verify), never to a wrong answer.
+        u64 cur = q->tag;
         if (cur == 0) cur = atomicCAS((unsigned long long*)&q->tag, 0ULL, (unsigned long long)tag);
         if (cur == 0) {
             q->lo = lo;
@@ -506,10 +509,7 @@ __device__ static inline void tb_seq_insert(const SeqSet& S, u64 lo, u64 hi) {
         if (cur == tag) {
             // The claimant's id, once published, settles it here (tb_seq_clear zeroed both words, and
             // an id is never 0): only a claim still in flight goes to the list for tb_seq_verify.
-            if (__hip_atomic_load(&q->lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == lo &&
-                __hip_atomic_load(&q->hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == hi) {
-                return;
-            }
+            if (q->lo == lo && q->hi == hi) return;
             const u64 k = tb_wave_claim(true, &S.count[1]);
             S.dups[3 * k] = pos;
             S.dups[3 * k + 1] = lo;

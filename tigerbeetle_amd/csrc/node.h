@@ -355,6 +355,10 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
             node_free(N);
             return st2;
         }
+        // The sequencer's passes are the dependent events of a node pass: a tenth to a quarter of it
+        // in C3 / C4, Zipf-hot.  Balance legs (per-account LDS sums) from 8K events on: below the
+        // single engine's threshold, atomics on the hot accounts would serialise.
+        N->X->legs_min = 8192;
         (void)hipSetDevice(N->D[0].device);
         N->tset_mask = pow2_at_least(4 * pass) - 1;
         N->aset_mask = pow2_at_least(2 * (xc.accounts_max + 2 * pass)) - 1;
