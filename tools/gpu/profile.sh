@@ -36,10 +36,12 @@ case $MODE in
   fetch|write) C=FETCH_SIZE; [ "$MODE" = write ] && C=WRITE_SIZE
       timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/bench.py" $LEG \
         --steps 1 --warmup 0 > "$OUT/$MODE.log" 2>&1; rc=$? ;;
-  nkt) timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/nkt" -o run -- python3 "$R/bench.py" \
+  nkt) export GPU_MAX_HW_QUEUES=8  # as bench.py sets for the node engine (the profiler starts HIP first)
+      timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/nkt" -o run -- python3 "$R/bench.py" \
         --gpus 2 --same-device --accounts 2000000 --transfers 8000000 --steps 1 --warmup 1 $LEG --access-mix 0 \
         > "$OUT/bench_nkt.log" 2>&1; rc=$? ;;
-  nc3) timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/nc3" -o run -- python3 "$R/bench.py" \
+  nc3) export GPU_MAX_HW_QUEUES=8
+      timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/nc3" -o run -- python3 "$R/bench.py" \
         --gpus 2 --same-device --workload c3 --accounts 1000000 --transfers 4000000 --steps 1 --warmup 1 $LEG --access-mix 0 \
         > "$OUT/bench_nc3.log" 2>&1; rc=$? ;;
   c3|c3h|c4) timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/bench.py" \

@@ -46,6 +46,13 @@ for what in "$@"; do
       timeout -k 10 600 python -u bench.py --gpus 2 --same-device --accounts 1000000 --transfers 4000000 --steps 2 \
         --warmup 1 --host-steps 1 --workload c3 > $O/node_c3.json 2> $O/node_c3.err
       rc=$?; echo "node c3 rc=$rc"; tail -c 2500 $O/node_c3.json; tail -5 $O/node_c3.err; [ $rc -ne 0 ] && exit $rc ;;
+    nodec4)
+      timeout -k 10 600 python -u bench.py --gpus 2 --same-device --accounts 1000000 --transfers 4000000 --steps 2 \
+        --warmup 1 --host-steps 0 --workload c4 > $O/node_c4.json 2> $O/node_c4.err
+      rc=$?; echo "node c4 rc=$rc"; tail -c 1500 $O/node_c4.json; tail -5 $O/node_c4.err; [ $rc -ne 0 ] && exit $rc ;;
+    node1)  # one C2 prepare per tbgpu_commit: node (2 logical shards) and single engine
+      GPU_MAX_HW_QUEUES=8 timeout -k 10 400 python -u tools/gpu/node_one_prepare.py 400 2 > $O/node1.jsonl 2> $O/node1.err
+      rc=$?; echo "node1 rc=$rc"; cat $O/node1.jsonl; tail -5 $O/node1.err; [ $rc -ne 0 ] && exit $rc ;;
     prof_*)  # a tools/gpu/profile.sh mode
       bash tools/gpu/profile.sh ${what#prof_}; rc=$?; [ $rc -ne 0 ] && exit $rc ;;
     *) echo "unknown step $what"; exit 2 ;;
