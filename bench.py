@@ -68,6 +68,11 @@ def parse():
                    help="transfers per GPU; default: 100M (N=1, C2); 125M (N>1, C5: 1B over 8 GPUs)")
     p.add_argument("--batch", type=int, default=8190)
     p.add_argument("--pass-batches", type=int, default=512, help="prepares per device pass (device-resident leg)")
+    p.add_argument("--inplace", type=int, default=1,
+                   help="1: the device-resident prepares are placed in the engine's log window and committed in "
+                        "place (tbgpu_log_window, zero-copy); 0: committed from a separate HBM buffer")
+    p.add_argument("--staged-steps", type=int, default=2,
+                   help="steps of the same leg from a separate HBM buffer (the copy commit), reported beside it")
     p.add_argument("--chunk-prepares", type=int, default=None,
                    help="prepares per pipelined chunk (host memory -> PCIe -> commit -> reply); default per "
                         "workload: CHUNK_PREPARES")
@@ -595,16 +600,33 @@ def main():
                               limit_permille=wl["limit_permille"], hot_limited=wl.get("hot_limited", 0))
     engine.sync()
 
+    def place(dst, count=None):
+        """The same prepares (same generator, same seed) at `dst`: the log window for an in-place
+        commit (each committed record is stamped there, so every step places them afresh, untimed)."""
+        engine.generate_transfers(dst, 0, count or args.transfers, args.accounts, seed=seed, kind=KINDS[args.workload],
+                                  limit_permille=wl["limit_permille"], hot_limited=wl.get("hot_limited", 0))
+
+    def headline_input(count=None):
+        """Reset the transfer store; the prepares' device address for the next commit."""
+        engine.reset_transfers()
+        if not args.inplace:
+            return events_dev
+        window = engine.log_window(count or args.transfers)
+        place(window, count)
+        return window
+
     # -- headline: the prepares already resident in HBM (the measurement rule: inputs in HBM when
-    # the timed region starts), tbgpu_commit_device_async in passes of pass_batches prepares.  Each
-    # step commits all of them from the post-account-creation state; bracketed by barrier + sync.
+    # the timed region starts), tbgpu_commit_device_async in passes of pass_batches prepares — in
+    # place: the prepares sit at their transfer-log positions (tbgpu_log_window), where a replica's
+    # DMA or a peer would put them.  Each step commits all of them from the post-account-creation
+    # state; bracketed by barrier + sync.
     step_ms = []
     t_cursor = t_end
     engine.profile_mask(engine.PROF_ALL)  # warmup: every kernel's HIP-event time (the breakdown)
     breakdown = None
     for step in range(args.warmup + args.steps):
         timed = step >= args.warmup
-        engine.reset_transfers()
+        src = headline_input()
         ts, t_cursor = timestamps(xfer_lens, t_cursor + 10, wl["gap_every"])
         if timed and step == args.warmup:
             if args.warmup:
@@ -616,7 +638,7 @@ def main():
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        engine.commit_device_async(129, ts, xfer_lens, events_dev, res_dev, rb_dev)
+        engine.commit_device_async(129, ts, xfer_lens, src, res_dev, rb_dev)
         engine.sync()
         torch.cuda.synchronize()
         barrier()
@@ -627,6 +649,35 @@ def main():
     pass_lat = engine.pass_latencies()
     rb = engine.to_host(rb_dev, len(xfer_lens) * 4).view(np.uint32)
     n_failed = int(rb.sum()) // 8
+
+    # -- the same leg from a separate HBM buffer (the copy commit: kernel 1 stores each record) ------
+    staged = None
+    if args.inplace and args.staged_steps:
+        s_ms = []
+        engine.profile_mask(engine.PROF_APPLY | engine.PROF_PASS | engine.PROF_REPLAY)
+        s_stats0 = engine.stats()
+        for step in range(args.staged_steps):
+            engine.reset_transfers()
+            ts, t_cursor = timestamps(xfer_lens, t_cursor + 10, wl["gap_every"])
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            engine.commit_device_async(129, ts, xfer_lens, events_dev, res_dev, rb_dev)
+            engine.sync()
+            torch.cuda.synchronize()
+            barrier()
+            s_ms.append(allmax((time.perf_counter() - t0) * 1e3))
+        s_stats = engine.stats()
+        s_total = sum(s_ms)
+        s_val = max(1, s_stats["span_launches"][0] - s_stats0["span_launches"][0]) if s_stats.get("span_launches") else 0
+        staged = {"value": round(args.transfers * world * args.staged_steps / (s_total / 1e3), 1), "unit": "transfers/s",
+                  "steps": args.staged_steps, "ms_per_step": round(s_total / args.staged_steps, 3),
+                  "definition": "the same prepares committed from a separate HBM buffer (kernel 1 copies each record "
+                                "into the log) instead of in place",
+                  "validate_avg_launch_ms": round((s_stats["span_ms"][0] - s_stats0["span_ms"][0]) / s_val, 4)
+                  if s_val else None,
+                  "replies_equal_to_in_place": bool(int(engine.to_host(rb_dev, len(xfer_lens) * 4).view(np.uint32).sum())
+                                                    // 8 == n_failed)}
 
     # -- the host path: the same prepares from registered host memory, PCIe both ways (the replica's
     # batched call, tbgpu_commit_pipelined: chunk c+1 crosses PCIe while chunk c commits) ---------
@@ -695,9 +746,9 @@ def main():
 
     # -- full-run checks (size-independent properties) of the last timed step ---------------------
     # (the write-back leg committed other transfers since: re-run one untimed step to check them)
-    engine.reset_transfers()
+    src = headline_input()
     ts, t_cursor = timestamps(xfer_lens, t_cursor + 10, wl["gap_every"])
-    engine.commit_device_async(129, ts, xfer_lens, events_dev, res_dev, rb_dev)
+    engine.commit_device_async(129, ts, xfer_lens, src, res_dev, rb_dev)
     engine.sync()
     rb = engine.to_host(rb_dev, len(xfer_lens) * 4).view(np.uint32)
     accts = engine.export_accounts()
@@ -752,10 +803,11 @@ def main():
                 off += L
             return got
 
-        # 1. The headline's own timed path: the sample resident in HBM, tbgpu_commit_device_async.
-        engine.reset_transfers()
+        # 1. The headline's own timed path: the sample resident in HBM, tbgpu_commit_device_async
+        # (in place when the headline is).
         ct0 = engine.commit_timestamp
-        engine.commit_device_async(129, sample_ts, sample_lens, events_dev, res_dev, rb_dev)
+        src = headline_input(n_sample)
+        engine.commit_device_async(129, sample_ts, sample_lens, src, res_dev, rb_dev)
         engine.sync()
         rb = engine.to_host(rb_dev, len(sample_lens) * 4).view(np.uint32)
         results = engine.to_host(res_dev, n_sample * 8)
@@ -763,7 +815,8 @@ def main():
         xfer_equal = engine.export_transfers(cap=n_sample).tobytes() == oracle.export_transfers().tobytes()
         parity.update({"sample_transfers": n_sample, "replies_equal": got_replies(rb, results) == expected,
                        "accounts_equal": acc_equal, "transfers_equal": xfer_equal,
-                       "sample_path": "tbgpu_commit_device_async, %d-prepare passes (the timed path)" % args.pass_batches})
+                       "sample_path": "tbgpu_commit_device_async, %d-prepare passes%s (the timed path)" % (
+                           args.pass_batches, ", in place (tbgpu_log_window)" if args.inplace else "")})
         # 2. The host path: tbgpu_commit_pipelined from registered host memory (the same timestamps:
         # the commit timestamp goes back to where the first run started, as a replica's would).
         engine.reset_transfers()
@@ -814,8 +867,11 @@ def main():
         "data": "synthetic (generated on the GPU in the reference benchmark's shapes, resident in HBM before timing)",
         "config": {"workload": WORKLOAD_TEXT[args.workload] % (args.accounts, args.transfers, args.batch),
                    "prepares_per_step": len(xfer_lens), "pass_prepares": args.pass_batches,
-                   "input": "prepare bodies resident in HBM when the timed region starts (tbgpu_commit_device_async); "
-                            "replies written to HBM; the PCIe-inclusive rate is `host_path`",
+                   "input": ("prepare bodies resident in HBM when the timed region starts, placed at their transfer-log "
+                             "positions and committed in place (tbgpu_log_window + tbgpu_commit_device_async; the same "
+                             "leg from a separate buffer is `device_resident_staged`)" if args.inplace else
+                             "prepare bodies resident in HBM when the timed region starts (tbgpu_commit_device_async)")
+                            + "; replies written to HBM; the PCIe-inclusive rate is `host_path`",
                    "host_numa_node": args.numa_node, "parallelism": "single"},
         "p99_batch_latency_ms": round(ref_percentile(pass_lat, 99), 3),
         "batch_latency_ms": dict(deciles(pass_lat), definition=(
@@ -823,6 +879,7 @@ def main():
             "%d-prepare pass is; device clock, HIP events around each pass); percentiles by "
             "src/benchmark.zig:454-471" % args.pass_batches)),
         "host_path": host_path,
+        "device_resident_staged": staged,
         "dependent_events": stats["dependent_events"],
         "flow": {k: (round(stats[k], 3) if isinstance(stats[k], float) else stats[k])
                  for k in ("flow_units", "flow_runs", "flow_run_units", "flow_plan_ms", "flow_run_ms", "bounds_passes",
@@ -849,7 +906,8 @@ def main():
     line["headline"] = {"value": line["value"], "unit": "transfers/s", "p99_batch_latency_ms": line["p99_batch_latency_ms"],
                         "roofline_frac": roof["frac"] if roof else None,
                         "roofline_traffic": roof.get("traffic") if roof else None,
-                        "host_path_value": host_path["value"] if host_path else None}
+                        "host_path_value": host_path["value"] if host_path else None,
+                        "staged_value": staged["value"] if staged else None}
     if rank == 0:
         print(json.dumps(line), flush=True)
     engine.close()

@@ -158,6 +158,16 @@ int tbgpu_commit_device_async(tbgpu_t* engine, uint8_t operation, uint32_t n_bat
                               const void* events_dev, void* results_dev, uint32_t* reply_bytes_dev);
 int tbgpu_sync(tbgpu_t* engine);
 
+/* Zero-copy create_transfers: the device address where the next `events` transfer records will be
+ * stored (the transfer log from the engine's next position; the groove's insert,
+ * src/lsm/groove.zig:950-1014, lands here).  Prepares placed there — by DMA from the message
+ * buffers, by a peer, by a generator — and committed with tbgpu_commit_device_async(operation 129,
+ * events_dev = *window) are committed IN PLACE: a committed transfer's record is its event with its
+ * timestamp written, so the pass stores 8 bytes of it instead of copying 128 (results identical to
+ * a copy commit).  The window is valid until the next call that stores transfers; INVALID when the
+ * log cannot hold `events` more, or on a node engine. */
+int tbgpu_log_window(tbgpu_t* engine, uint64_t events, void** window);
+
 /* Host-memory registration for the replica's message pool (allocated once at init, like every
  * reference buffer): prepare bodies inside registered memory reach HBM by direct DMA. */
 int tbgpu_register_host(tbgpu_t* engine, void* ptr, uint64_t bytes);

@@ -181,6 +181,7 @@ SIGNATURES = [
     ("tbgpu_load_transfers", ctypes.c_int, [_P, _P, _P, _U32]),
     ("tbgpu_set_commit_timestamp", ctypes.c_int, [_P, _U64]),
     ("tbgpu_evict_transfers", ctypes.c_int, [_P, _U64, ctypes.POINTER(_U64)]),
+    ("tbgpu_log_window", ctypes.c_int, [_P, _U64, ctypes.POINTER(ctypes.c_void_p)]),
     ("tbgpu_transfers_maybe_cold", ctypes.c_int, [_P, _P, _U32, _P]),
     ("tbgpu_unregister_host", ctypes.c_int, [_P, _P]),
     ("tbgpu_copy_to_device", ctypes.c_int, [_P, _P, _P, _U64]),

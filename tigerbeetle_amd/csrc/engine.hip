@@ -148,6 +148,7 @@ struct tbgpu {
     u64* bloom = nullptr;
     u64 bloom_mask = 0;
     u64 evicted_total = 0;
+    bool inplace_call = false;  // the call being enqueued commits its events in place (tbgpu_log_window)
 
     // Pass scratch.
     u32 pe_max = 0, pb_max = 0;
@@ -919,6 +920,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.cert_ext = cert_ext;
         P.seq_pv = E->balances_set ? 1u : 0u;
         P.ev_ts = ev_ts;
+        P.inplace = E->inplace_call ? 1u : 0u;
         // Legs pay a fixed ~30 us (one workgroup per bucket, LDS sums) that no-return atomics in
         // the resolve kernel (~20 G/s) only cost beyond ~LEGS_MIN_EVENTS events: the replica's
         // one-prepare commits take the atomics.
@@ -1471,9 +1473,24 @@ extern "C" int tbgpu_commit_device_async(tbgpu_t* E, uint8_t operation, uint32_t
     if (st) return st;
     std::vector<u64> h_off(E->h_meta, E->h_meta + n_batches + 1);
     if (operation == OP_CREATE_ACCOUNTS) E->ckpt_scan = true;  // ids in device memory: diff the table next
+    // Prepares placed in the log window (tbgpu_log_window) are committed in place.
+    E->inplace_call = operation == OP_CREATE_TRANSFERS && (const u8*)events_dev == (const u8*)(E->T.xlog + E->log_next);
     st = enqueue_call(E, operation, n_batches, h_off.data(), (const u8*)events_dev, (u32*)results_dev, reply_bytes_dev);
+    E->inplace_call = false;
     if (st) return st;
     E->pending = true;
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_log_window(tbgpu_t* E, uint64_t events, void** window) {
+    API_ENTER(E, false);
+    *window = nullptr;
+    if (E->node) return fail(TBGPU_STATUS_INVALID, "the log window needs a single-device engine");
+    if (E->log_next + events > E->xlog_cap) {
+        return fail(TBGPU_STATUS_INVALID, "transfer log full: %llu of %llu positions used, %llu asked",
+                    (unsigned long long)E->log_next, (unsigned long long)E->xlog_cap, (unsigned long long)events);
+    }
+    *window = E->T.xlog + E->log_next;
     return TBGPU_STATUS_OK;
 }
 

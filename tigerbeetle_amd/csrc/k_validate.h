@@ -63,6 +63,26 @@ __device__ static inline u32 tb_post_void_exists(const Transfer& t, const Transf
     return CT_EXISTS;
 }
 
+// The record of a post / void (post_or_void_pending_transfer :971-985): the event's fields where it
+// gives them, the pending transfer's otherwise.
+__device__ static inline Transfer tb_compose_post_void(const Transfer& t, const Transfer& p, u64 ts) {
+    Transfer r;
+    r.id = t.id;
+    r.debit_account_id = p.debit_account_id;
+    r.credit_account_id = p.credit_account_id;
+    r.amount = t.amount > 0 ? t.amount : p.amount;
+    r.pending_id = t.pending_id;
+    r.user_data_128 = t.user_data_128 > 0 ? t.user_data_128 : p.user_data_128;
+    r.user_data_64 = t.user_data_64 > 0 ? t.user_data_64 : p.user_data_64;
+    r.user_data_32 = t.user_data_32 > 0 ? t.user_data_32 : p.user_data_32;
+    r.timeout = 0;
+    r.ledger = p.ledger;
+    r.code = p.code;
+    r.flags = t.flags;
+    r.timestamp = ts;
+    return r;
+}
+
 // The `id` existence check of create_transfer (:824) / post_or_void (:954) fused with the
 // speculative index claim.  Returns R_OK (claimed, record to be written by the caller),
 // a pseudo "exists" marker via *exists_pos, or CLAIM_COLLIDED (dependent).
@@ -165,21 +185,7 @@ __device__ static inline u32 tb_validate_post_void(const PassArgs& P, const Tran
     // A post moves <= p.amount from pending to posted: dp + dpost never grows, so no S term.
 
     // Speculative record (composed as at :971-985); kernel 2 withdraws it if the event fails.
-    Transfer r;
-    r.id = t.id;
-    r.debit_account_id = p.debit_account_id;
-    r.credit_account_id = p.credit_account_id;
-    r.amount = amount;
-    r.pending_id = t.pending_id;
-    r.user_data_128 = t.user_data_128 > 0 ? t.user_data_128 : p.user_data_128;
-    r.user_data_64 = t.user_data_64 > 0 ? t.user_data_64 : p.user_data_64;
-    r.user_data_32 = t.user_data_32 > 0 ? t.user_data_32 : p.user_data_32;
-    r.timeout = 0;
-    r.ledger = p.ledger;
-    r.code = p.code;
-    r.flags = t.flags;
-    r.timestamp = ts;
-    if (s.hz & HZ_SPEC) T.xlog[P.log_base + pe] = r;
+    if ((s.hz & HZ_SPEC) && !P.inplace) T.xlog[P.log_base + pe] = tb_compose_post_void(t, p, ts);  // in place: tb_resolve
     return R_OK;
 }
 
@@ -277,7 +283,9 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     // then the timeout check (:862) is the next possible failure.
     const u64 timeout_ns = (u64)t.timeout * 1000000000ULL;
     if (ts + timeout_ns < ts) return CT_OVERFLOWS_TIMEOUT;  // entry withdrawn by kernel 2
-    if ((s.hz & HZ_SPEC) && !TB_ABL(P, ABL_RECORD)) {
+    if ((s.hz & HZ_SPEC) && P.inplace) {
+        s.hz |= HZ_INPLACE;  // the record is the event in place: tb_resolve stamps it if it commits
+    } else if ((s.hz & HZ_SPEC) && !TB_ABL(P, ABL_RECORD)) {
         s.rec_ts = ts;
         s.hz |= HZ_REC;
     }

@@ -33,6 +33,8 @@ enum : u32 {
                              // log_base + event, under its claimed entry rs[]
     HZ_LATE = 1u << 20,      // tb_resolve: an independent ok create_transfers event that is not a
                              // balance leg — tb_apply_events applies exactly these
+    HZ_INPLACE = 1u << 21,   // in-place pass (PassArgs.inplace): the event at log_base + event is its
+                             // record but for the timestamp, which tb_resolve writes if it commits
 };
 
 #define SUM_SHARDS 64
@@ -88,6 +90,12 @@ struct PassArgs {
     // events, in order, so positions no longer give timestamps.  Their own timestamp fields are the
     // caller's (timestamp_must_be_zero still applies).  Null: from batch_ts (or routed).
     const u64* ev_ts;
+    // In-place pass (tbgpu_log_window): the events already sit at their transfer-log positions
+    // (events + (e0 + pe) * 128 == &T.xlog[log_base + pe]).  Kernel 1 writes no record; tb_resolve
+    // writes the timestamp of each independent ok create (HZ_INPLACE) and the composed record of each
+    // independent ok post / void; the ordered path stores its records as always.  No kernel reads an
+    // event's bytes after its record is written, except its id and pending id, which a record keeps.
+    u32 inplace;
     // Balance legs (k_apply.h): with the 64-bit certificate, the balance deltas of independent ok
     // create_transfer events are written as legs, bucketed by account slot per prepare, and summed
     // per account by tb_apply_legs instead of being added with one global atomic per leg.

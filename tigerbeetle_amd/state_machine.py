@@ -192,6 +192,14 @@ class Engine:
     def sync(self):
         _lib.check(self.lib.tbgpu_sync(self.h))
 
+    def log_window(self, events):
+        """Device address where the next `events` transfer records go (tbgpu_log_window): prepares
+        placed there and committed with commit_device_async(129, ..., events_dev=window) are committed
+        in place."""
+        w = ctypes.c_void_p(0)
+        _lib.check(self.lib.tbgpu_log_window(self.h, int(events), ctypes.byref(w)))
+        return int(w.value)
+
     @property
     def commit_timestamp(self):
         return self.lib.tbgpu_commit_timestamp(self.h)
