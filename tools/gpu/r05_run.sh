@@ -16,6 +16,10 @@ for what in "$@"; do
       timeout -k 10 600 python -u -m pytest -q -rf --timeout 400 --timeout-method thread -m gpu tests/test_gpu_evict.py \
         > $O/evict.log 2>&1
       rc=$?; echo "evict rc=$rc"; tail -15 $O/evict.log; [ $rc -ne 0 ] && exit $rc ;;
+    inplace)
+      timeout -k 10 600 python -u -m pytest -q -rf --timeout 400 --timeout-method thread -m gpu tests/test_gpu_inplace.py \
+        > $O/inplace.log 2>&1
+      rc=$?; echo "inplace rc=$rc"; tail -15 $O/inplace.log; [ $rc -ne 0 ] && exit $rc ;;
     node_tests)
       timeout -k 10 900 python -u -m pytest -q -rf --maxfail=25 --timeout 240 --timeout-method thread -m gpu \
         tests/test_gpu_node.py tests/test_gpu_alloc.py tests/test_gpu_c5.py > $O/node_tests.log 2>&1
