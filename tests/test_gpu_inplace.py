@@ -67,7 +67,9 @@ def run_inplace(sc, engine, per_call=4):
 
 @pytest.mark.parametrize("config", sorted(CONFIGS))
 def test_inplace_matches_oracle(config, gpu_engine_factory):
-    sc = make_scenario(7100 + sorted(CONFIGS).index(config), n_transfer_batches=12, **CONFIGS[config])
+    cfg = dict(CONFIGS[config])
+    cfg.setdefault("n_transfer_batches", 12)
+    sc = make_scenario(7100 + sorted(CONFIGS).index(config), **cfg)
     oracle = OracleEngine(4096, 1 << 17)
     engine = gpu_engine_factory(pass_events_max=8192, pass_batches_max=4)
     try:

@@ -375,6 +375,7 @@ __device__ static inline u32 fl_run_run(const PassArgs& P, const FlowArgs& F, Re
                 if (R.cert64) tb_atomic_add_lo_noret(fb + off, tb_lo(amount));
                 else tb_atomic_add_u128(fb + off, amount);
                 __hip_atomic_fetch_and(&T.xidx[crs_[j]], ~(u64)XI_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (P.inplace) T.xlog[P.log_base + pe].timestamp = tb_event_ts_pe(P, pe);  // the record is its event
                 n_ok++;
                 last_ok_pe = pe;
             } else {
@@ -2045,7 +2046,8 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
     }
 
     // Apply: the ok units' legs (both accounts; sums commute), their index entries and counts; the
-    // failed ones' codes.  Kernel 1 already wrote every record at its log position.
+    // failed ones' codes.  Kernel 1 already wrote every record at its log position (an in-place
+    // pass: the event is there, and its timestamp is written here).
     // Zipf-hot accounts put one balance word in many lanes of a wave: atomics on one address
     // serialise in L2, so the lanes sharing the first lane's word add their sum once (fl_add_lo).
     u32 n_ok = 0;
@@ -2074,7 +2076,9 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
             n_ok++;
             const u32 b = F.f_batch[f];
             const u64 boff = P.batch_off[b];
-            tsm = max(tsm, tb_event_ts(P, b, boff, (u32)(P.batch_off[b + 1] - boff), (u32)(P.e0 + pe - boff)));
+            const u64 ts = tb_event_ts(P, b, boff, (u32)(P.batch_off[b + 1] - boff), (u32)(P.e0 + pe - boff));
+            if (P.inplace) T.xlog[P.log_base + pe].timestamp = ts;
+            tsm = max(tsm, ts);
         }
         fl_add_lo(dw, a);
         fl_add_lo(cw, a);

@@ -173,6 +173,19 @@ __device__ static inline u64 tb_event_ts(const PassArgs& P, u32 b, u64 boff, u32
 // Timestamps not from the prepare's position (routed, or compacted prepares).
 __device__ static inline bool tb_ts_carried(const PassArgs& P) { return P.routed || P.ev_ts; }
 
+// The execute timestamp of pass-relative event pe (its prepare found by binary search).
+__device__ static inline u64 tb_event_ts_pe(const PassArgs& P, u32 pe) {
+    const u64 e = P.e0 + pe;
+    u32 lo = P.b0, hi = P.b1;
+    while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if (P.batch_off[mid] <= e) lo = mid;
+        else hi = mid;
+    }
+    const u64 boff = P.batch_off[lo];
+    return tb_event_ts(P, lo, boff, (u32)(P.batch_off[lo + 1] - boff), (u32)(e - boff));
+}
+
 // Timing-only ablations (A/B experiments with tools/gpu/ab.sh) exist only in a build with
 // -DTBGPU_TIMING_KNOBS; in the product build every check folds to false, so no environment
 // variable can switch off a validation step.
