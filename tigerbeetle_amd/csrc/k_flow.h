@@ -255,7 +255,8 @@ __device__ static inline u64 fl_run_unit(const PassArgs& P, const FlowArgs& F, R
         Transfer t = *(const Transfer*)ev;
         const u32 L = (u32)(bend - boff);
         const u32 i = (u32)(P.e0 + pe - boff);
-        const u64 evts = P.routed ? 0 : t.timestamp;
+        // In place, kernel 1 stamped an HZ_INPLACE event's record (= the event): its field was 0.
+        const u64 evts = (P.routed || (info & HZ_INPLACE)) ? 0 : t.timestamp;
         const bool linked = flags & TF_LINKED;
         u32 result;
         if (linked && !in_chain) {
@@ -375,7 +376,6 @@ __device__ static inline u32 fl_run_run(const PassArgs& P, const FlowArgs& F, Re
                 if (R.cert64) tb_atomic_add_lo_noret(fb + off, tb_lo(amount));
                 else tb_atomic_add_u128(fb + off, amount);
                 __hip_atomic_fetch_and(&T.xidx[crs_[j]], ~(u64)XI_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (P.inplace) T.xlog[P.log_base + pe].timestamp = tb_event_ts_pe(P, pe);  // the record is its event
                 n_ok++;
                 last_ok_pe = pe;
             } else {
@@ -2046,8 +2046,8 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
     }
 
     // Apply: the ok units' legs (both accounts; sums commute), their index entries and counts; the
-    // failed ones' codes.  Kernel 1 already wrote every record at its log position (an in-place
-    // pass: the event is there, and its timestamp is written here).
+    // failed ones' codes.  Kernel 1 already wrote every record at its log position (in place: the
+    // event is there, stamped).
     // Zipf-hot accounts put one balance word in many lanes of a wave: atomics on one address
     // serialise in L2, so the lanes sharing the first lane's word add their sum once (fl_add_lo).
     u32 n_ok = 0;
@@ -2077,7 +2077,6 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
             const u32 b = F.f_batch[f];
             const u64 boff = P.batch_off[b];
             const u64 ts = tb_event_ts(P, b, boff, (u32)(P.batch_off[b + 1] - boff), (u32)(P.e0 + pe - boff));
-            if (P.inplace) T.xlog[P.log_base + pe].timestamp = ts;
             tsm = max(tsm, ts);
         }
         fl_add_lo(dw, a);

@@ -500,7 +500,7 @@ __device__ static inline u64 rp_batch(const PassArgs& P, Replay& R, u32 b) {
         const u32 i = list[k];
         const u8* ev = P.events + (boff + i) * 128;
         const u16 flags = P.eflags[pbase + i];
-        const u64 evts = P.routed ? 0 : *(const u64*)(ev + 120);
+        const u64 evts = (P.routed || (P.info[pbase + i] & HZ_INPLACE)) ? 0 : *(const u64*)(ev + 120);  // stamped in place
         const bool linked = flags & 1;
         u32 result;
         if (linked && !in_chain) {

@@ -177,17 +177,14 @@ __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 L, 
     }
 }
 
-// In-place pass: an independent ok create's record is its event, stamped here; an independent ok
-// post / void's record is composed here over its event (kernel 1 wrote neither, so the ordered path
-// could still read the event as given).
+// In-place pass: an independent ok post / void's record is composed here over its event (kernel 1
+// did not write it, so the ordered path could still read the event as given).  A create's record is
+// its event, stamped by kernel 1 (HZ_INPLACE).
 __device__ static inline void tb_inplace_record(const PassArgs& P, u32 pe, u32 info, u64 ts) {
+    if (!(info & HZ_POSTVOID)) return;
     Transfer* rec = &P.T.xlog[P.log_base + pe];
-    if (info & HZ_INPLACE) {
-        rec->timestamp = ts;
-    } else if (info & HZ_POSTVOID) {
-        const Transfer t = *rec;
-        *rec = tb_compose_post_void(t, P.T.xlog[P.ps[pe]], ts);
-    }
+    const Transfer t = *rec;
+    *rec = tb_compose_post_void(t, P.T.xlog[P.ps[pe]], ts);
 }
 
 // Apply one independent ok account (create_account :762, groove insert).
@@ -393,7 +390,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
             tsmax = ok ? ts : tsmax;
             n_app += ok;
             n_fail += valid & !ok;
-            if (ok && P.inplace) tb_inplace_record(P, pe, info, ts);
+            if (ok && P.inplace && (info & HZ_POSTVOID)) tb_inplace_record(P, pe, info, ts);
             if (ok) {
                 if (leg) {
                     const u32 drs = r_dr[k], crs = r_cr[k];
@@ -459,7 +456,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
                 if (eval_ok) tsmax = ts;  // increasing in i
                 if (fin == R_OK) {
                     if (OP == OP_CREATE_TRANSFERS) {
-                        if (P.inplace) tb_inplace_record(P, pe, info, ts);
+                        if (P.inplace && (info & HZ_POSTVOID)) tb_inplace_record(P, pe, info, ts);
                         if (leg) {
                             const u32 drs = r_dr[k], crs = r_cr[k];
                             const u64 pend = (r_fl[k] & TF_PENDING) ? 0 : 1;  // field: pending / posted

@@ -284,7 +284,10 @@ __device__ static inline u32 tb_validate_transfer(const PassArgs& P, const Trans
     const u64 timeout_ns = (u64)t.timeout * 1000000000ULL;
     if (ts + timeout_ns < ts) return CT_OVERFLOWS_TIMEOUT;  // entry withdrawn by kernel 2
     if ((s.hz & HZ_SPEC) && P.inplace) {
-        s.hz |= HZ_INPLACE;  // the record is the event in place: tb_resolve stamps it if it commits
+        // The record is the event in place: 8 bytes of it written here (its line was just read).  The
+        // ordered path reads an HZ_INPLACE event's timestamp field as the 0 it was checked to be.
+        s.hz |= HZ_INPLACE;
+        P.T.xlog[P.log_base + pe].timestamp = ts;
     } else if ((s.hz & HZ_SPEC) && !TB_ABL(P, ABL_RECORD)) {
         s.rec_ts = ts;
         s.hz |= HZ_REC;

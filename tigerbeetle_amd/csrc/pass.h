@@ -34,7 +34,8 @@ enum : u32 {
     HZ_LATE = 1u << 20,      // tb_resolve: an independent ok create_transfers event that is not a
                              // balance leg — tb_apply_events applies exactly these
     HZ_INPLACE = 1u << 21,   // in-place pass (PassArgs.inplace): the event at log_base + event is its
-                             // record but for the timestamp, which tb_resolve writes if it commits
+                             // record, and kernel 1 wrote its timestamp there (read back as 0 by the
+                             // ordered path, which re-evaluates the event)
 };
 
 #define SUM_SHARDS 64
@@ -91,10 +92,12 @@ struct PassArgs {
     // caller's (timestamp_must_be_zero still applies).  Null: from batch_ts (or routed).
     const u64* ev_ts;
     // In-place pass (tbgpu_log_window): the events already sit at their transfer-log positions
-    // (events + (e0 + pe) * 128 == &T.xlog[log_base + pe]).  Kernel 1 writes no record; tb_resolve
-    // writes the timestamp of each independent ok create (HZ_INPLACE) and the composed record of each
-    // independent ok post / void; the ordered path stores its records as always.  No kernel reads an
-    // event's bytes after its record is written, except its id and pending id, which a record keeps.
+    // (events + (e0 + pe) * 128 == &T.xlog[log_base + pe]).  Kernel 1 writes the timestamp of each
+    // create that may commit (HZ_INPLACE: its record is the event) and no post / void record;
+    // tb_resolve composes the record of each independent ok post / void over its event; the ordered
+    // path stores its records as always.  No kernel reads an event's bytes after its record is
+    // written, except its id and pending id, which a record keeps, and an HZ_INPLACE event's
+    // timestamp, which the ordered path takes as the 0 kernel 1 checked.
     u32 inplace;
     // Balance legs (k_apply.h): with the 64-bit certificate, the balance deltas of independent ok
     // create_transfer events are written as legs, bucketed by account slot per prepare, and summed
@@ -172,19 +175,6 @@ __device__ static inline u64 tb_event_ts(const PassArgs& P, u32 b, u64 boff, u32
 }
 // Timestamps not from the prepare's position (routed, or compacted prepares).
 __device__ static inline bool tb_ts_carried(const PassArgs& P) { return P.routed || P.ev_ts; }
-
-// The execute timestamp of pass-relative event pe (its prepare found by binary search).
-__device__ static inline u64 tb_event_ts_pe(const PassArgs& P, u32 pe) {
-    const u64 e = P.e0 + pe;
-    u32 lo = P.b0, hi = P.b1;
-    while (hi - lo > 1) {
-        const u32 mid = (lo + hi) >> 1;
-        if (P.batch_off[mid] <= e) lo = mid;
-        else hi = mid;
-    }
-    const u64 boff = P.batch_off[lo];
-    return tb_event_ts(P, lo, boff, (u32)(P.batch_off[lo + 1] - boff), (u32)(e - boff));
-}
 
 // Timing-only ablations (A/B experiments with tools/gpu/ab.sh) exist only in a build with
 // -DTBGPU_TIMING_KNOBS; in the product build every check folds to false, so no environment
