@@ -1169,9 +1169,13 @@ def run_node(args, procs, rank):
         sample_x = engine.to_host(gen, n_sample * 128)
         engine.free(gen)
         x = sample_x.view(TRANSFER_DTYPE)
-        # account ids are IdPermutation.inversion: maxInt(u128) - (index + 1), one high word
-        assert (x["debit_account_id_hi"] == U64_ALL).all() and (x["credit_account_id_hi"] == U64_ALL).all()
-        lo = np.unique(np.concatenate([x["debit_account_id_lo"], x["credit_account_id_lo"]]))
+        # account ids are IdPermutation.inversion: maxInt(u128) - (index + 1), one high word (a post /
+        # void may leave them 0: its pending transfer's accounts are used)
+        ids_hi = np.concatenate([x["debit_account_id_hi"], x["credit_account_id_hi"]])
+        ids_lo = np.concatenate([x["debit_account_id_lo"], x["credit_account_id_lo"]])
+        named = (ids_hi | ids_lo) != 0
+        assert (ids_hi[named] == U64_ALL).all()
+        lo = np.unique(ids_lo[named])
         sample_idx = np.uint64(U64_ALL - 1) - lo
 
     # Accounts: generated on the first GPU in chunks, committed from host memory; the oracle gets the
