@@ -11,6 +11,7 @@
 #   bash tools/gpu/profile.sh mc                  -> memory-copy + kernel trace of one headline step
 #     (the copy engine's timeline: body copies, their gaps, the per-chunk metadata copies)
 #   bash tools/gpu/profile.sh nkt|nc3             -> kernel trace of the node rehearsal (2 logical shards, C2 / C3)
+#   bash tools/gpu/profile.sh n1kt                -> kernel + copy trace of one-prepare node calls
 #   bash tools/gpu/profile.sh c3|c3h|c4           -> kernel trace of `bench.py --workload c3|c3h|c4`
 #     (1M accounts, 10M transfers, one timed step from host memory: tb_flow's bounds / sweep / run)
 # (rocprofv3 has written its CSVs when the profiled python exits; a crash after that, in process
@@ -44,6 +45,9 @@ case $MODE in
       timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/nc3" -o run -- python3 "$R/bench.py" \
         --gpus 2 --same-device --workload c3 --accounts 1000000 --transfers 4000000 --steps 1 --warmup 1 $LEG --access-mix 0 \
         > "$OUT/bench_nc3.log" 2>&1; rc=$? ;;
+  n1kt) export GPU_MAX_HW_QUEUES=8  # one C2 prepare per tbgpu_commit on a 2-shard node (and a single engine)
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$OUT/n1kt" -o run -- \
+        python3 "$R/tools/gpu/node_one_prepare.py" 120 2 > "$OUT/n1kt.log" 2>&1; rc=$? ;;
   c3|c3h|c4) timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/bench.py" \
         --workload $MODE --accounts 1000000 --transfers 10000000 --steps 1 --warmup 0 $LEG --access-mix 0 \
         > "$OUT/bench_$MODE.log" 2>&1; rc=$? ;;
