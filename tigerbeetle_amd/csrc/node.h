@@ -814,13 +814,15 @@ static int node_issue_replies(TbNode* N, NodePass& P, u32 p, const NodeRoute& RT
             NCK(hipGetLastError());
         }
         base += P.blk[s].events;
-        NCK(hipEventRecord(D.ev_replied, E->stream));
         // Every shard's arena, with or without a block: its head carries the shard's panic word after
         // its whole part of the pass (home commit, owner legs, replies: one stream), so consuming the
         // pass reads every shard's verdict and the call needs no drain at its end.
         hipLaunchKernelGGL(tb_reply_out, dim3(std::max<u32>(nb, 1)), dim3(64), 0, E->stream, D.meta[par], nb,
                            D.reply_bytes, D.results, E->g, D.d_arena[tri]);
         NCK(hipGetLastError());
+        // After tb_reply_out too: it reads this parity's prepare offsets, which the route stream
+        // rewrites two passes on once it has waited for this event.
+        NCK(hipEventRecord(D.ev_replied, E->stream));
         NCK(hipEventRecord(D.ev_done[tri], E->stream));
     }
     P.issued = true;

@@ -20,6 +20,18 @@ for what in "$@"; do
       timeout -k 10 600 python -u -m pytest -q -rf --timeout 400 --timeout-method thread -m gpu tests/test_gpu_inplace.py \
         > $O/inplace.log 2>&1
       rc=$?; echo "inplace rc=$rc"; tail -15 $O/inplace.log; [ $rc -ne 0 ] && exit $rc ;;
+    race)  # the node engine with every stream on its own hardware queue (as on N GPUs): node tests, C3 twice
+      export GPU_MAX_HW_QUEUES=8
+      timeout -k 10 600 python -u -m pytest -q -rf --maxfail=5 --timeout 240 --timeout-method thread -m gpu \
+        tests/test_gpu_node.py -k "dirty or clean or differential or device_resident" > $O/race_tests.log 2>&1
+      rc=$?; echo "race tests rc=$rc"; tail -3 $O/race_tests.log
+      [ $rc -ne 0 ] && { grep -E "^FAILED|^ERROR|^E  " $O/race_tests.log | head -40; exit $rc; }
+      for k in 1 2; do
+        timeout -k 10 300 python -u bench.py --gpus 2 --same-device --accounts 1000000 --transfers 4000000 --steps 2 \
+          --warmup 1 --host-steps 0 --workload c3 > $O/race_c3_$k.json 2> $O/race_c3_$k.err
+        rc=$?; echo "race c3 $k rc=$rc"; grep -o '"parity": {[^}]*}' $O/race_c3_$k.json; [ $rc -ne 0 ] && exit $rc
+      done
+      unset GPU_MAX_HW_QUEUES ;;
     node_tests)
       timeout -k 10 900 python -u -m pytest -q -rf --maxfail=25 --timeout 240 --timeout-method thread -m gpu \
         tests/test_gpu_node.py tests/test_gpu_alloc.py tests/test_gpu_c5.py > $O/node_tests.log 2>&1
