@@ -726,7 +726,18 @@ __global__ void tb_seq_load_accounts(NodeTablesArgs N, SeqSet aset, Tables X, Ac
         const u32 os = tb_account_find(O, q.lo, q.hi);
         if (os == TB_NOT_FOUND) continue;  // no such account
         const Account a = tb_account_load(O, os);
-        if (bal0) bal0[i] = O.acct_bal[os];
+        if (bal0) {
+            // The balances as loaded, not read again: the routed part may be adding legs to this
+            // (free) account meanwhile, and the write-back's deltas must be against what the
+            // sequencer started from (a second read could include a leg the first did not — and
+            // the delta would cancel it).
+            AccountBal b;
+            b.debits_pending = a.debits_pending;
+            b.debits_posted = a.debits_posted;
+            b.credits_pending = a.credits_pending;
+            b.credits_posted = a.credits_posted;
+            bal0[i] = b;
+        }
         const u32 xs = tb_account_claim(X, q.lo, q.hi, a.timestamp);
         if (xs == TB_NOT_FOUND) continue;  // PANIC_TABLE_FULL set
         tb_account_store_new(X, xs, a);
