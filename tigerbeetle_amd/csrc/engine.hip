@@ -968,7 +968,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
 
         if (imp && n > 0) {  // a node home: the foreign accounts this sub-pass names, from their owners
             HIPCK(hipMemsetAsync(imp->count, 0, 8, E->stream));
-            const u32 ig = (u32)std::min<u64>(4096, (2 * n + 255) / 256);
+            const u32 ig = (u32)std::min<u64>(4096, (n + 255) / 256);
             hipLaunchKernelGGL(tb_node_import, dim3(ig), dim3(256), 0, E->stream, E->T, imp->N, events_dev + P.e0 * 128, n,
                                imp->self, imp->list, imp->count, imp->cap, imp->os_of);
             HIPCK(hipGetLastError());

@@ -154,6 +154,47 @@ __global__ void tb_limbits_from_records(const u8* recs, u32 n, u64* bits, u64 ma
     if (a.flags & AF_LIMITS) tb_limit_set(bits, mask, tb_lo(a.id), tb_hi(a.id));
 }
 
+// Workgroup-level dedup of 128-bit ids in LDS (open addressing on the fingerprint; exact: a lane that
+// meets its fingerprint compares the ids after the barrier).  A Zipf-hot id named by many lanes of a
+// workgroup then costs one lane's global work, not one per lane: global atomics on one address
+// serialise.  Every thread calls tb_wg_dedup_claim, then __syncthreads, then tb_wg_dedup_go.
+#define WGD_SLOTS 1024
+#define WGD_SKIP 0xFFFFFFFFu  // no id
+#define WGD_FIRST 0xFFFFFFFEu // this lane placed the id (or the table had no room): it does the work
+struct WgDedup {
+    u64 tag[WGD_SLOTS];
+    u64 lo[WGD_SLOTS], hi[WGD_SLOTS];
+};
+
+__device__ static inline void tb_wg_dedup_reset(WgDedup& d) {
+    for (u32 k = threadIdx.x; k < WGD_SLOTS; k += blockDim.x) d.tag[k] = 0;
+    __syncthreads();
+}
+
+// WGD_SKIP, WGD_FIRST, or the LDS slot holding the same fingerprint (compare after the barrier).
+__device__ static inline u32 tb_wg_dedup_claim(WgDedup& d, bool want, u64 lo, u64 hi) {
+    if (!want) return WGD_SKIP;
+    const u64 fp = tb_fingerprint(lo, hi) | 1;
+    u32 p = (u32)(tb_mix64(fp) & (WGD_SLOTS - 1));
+    for (u32 r = 0; r < 16; r++) {
+        const u64 prev = atomicCAS((unsigned long long*)&d.tag[p], 0ULL, (unsigned long long)fp);
+        if (prev == 0) {
+            d.lo[p] = lo;
+            d.hi[p] = hi;
+            return WGD_FIRST;
+        }
+        if (prev == fp) return p;
+        p = (p + 1) & (WGD_SLOTS - 1);
+    }
+    return WGD_FIRST;
+}
+
+__device__ static inline bool tb_wg_dedup_go(const WgDedup& d, u32 st, u64 lo, u64 hi) {
+    if (st == WGD_SKIP) return false;
+    if (st == WGD_FIRST) return true;
+    return !(d.lo[st] == lo && d.hi[st] == hi);  // another id with this fingerprint: not a duplicate
+}
+
 struct NodeTablesArgs {
     Tables T[NODE_WORLD_MAX];  // every shard's tables (device pointers; peers read over xGMI)
     u32 world;
@@ -167,66 +208,88 @@ struct NodeTablesArgs {
 // never sit on an owned account's probe chain, and tb_node_import_clear restores the owned-only table
 // exactly.
 // One entry per id however many lanes name it (a Zipf-hot account is named by a large share of a
-// pass): a lane claims an empty slot by a CAS of its timestamp word to a marker {bit 63, the id's
-// 63-bit fingerprint} (real timestamps are below 2^63), and a lane that meets its own marker or its
-// id already there stops — the winner alone reads the owner's record, writes the entry and puts the
-// real timestamp last.  (Two ids with one 63-bit fingerprint meeting on one probe chain in one pass
-// would import one of them only: about 2^-63 per pair, the sequencer's own fingerprint bet.)
-__global__ void tb_node_import(Tables H, NodeTablesArgs N, const u8* events, u64 n, u32 self, u32* list, u64* count,
-                               u64 cap, u32* os_of) {
-    const u64 stride = (u64)gridDim.x * blockDim.x;
-    for (u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x; g < 2 * n; g += stride) {
-        const u64* w = (const u64*)(events + (g >> 1) * 128) + 2 + 2 * (g & 1);  // debit @16, credit @32
-        const u64 lo = w[0], hi = w[1];
-        if (tb_id_reserved(lo, hi)) continue;
-        const u32 o = tb_home(lo, hi, N.world);
-        if (o == self) continue;  // owned here: present or absent in the owned table itself
-        const u64 mark = (1ULL << 63) | (tb_fingerprint(lo, hi) >> 1);
-        u64 pos = tb_hash_id(lo, hi) & H.account_mask;
-        u32 slot = TB_NOT_FOUND;
-        for (u64 k = 0; k <= H.account_mask; k++) {
-            // Plain (cached) reads: a stale one costs a failed CAS (which returns the truth) or a
-            // duplicate entry, never a wrong one.
-            u64* tw = &H.acct_hot[pos].timestamp;
-            u64 t = *tw;
+// pass): first the workgroup keeps one lane per distinct id (tb_wg_dedup: LDS, exact), then that lane
+// claims an empty slot by a CAS of its timestamp word to a marker {bit 63, the id's 63-bit
+// fingerprint} (real timestamps are below 2^63), and a lane that meets its own marker or its id
+// already there stops — the winner alone reads the owner's record, writes the entry and puts the real
+// timestamp last.  (Two ids with one 63-bit fingerprint meeting on one probe chain in one pass would
+// import one of them only: about 2^-63 per pair, the sequencer's own fingerprint bet.)
+__device__ static inline void tb_import_one(const Tables& H, const NodeTablesArgs& N, u64 lo, u64 hi, u32 o, u32* list,
+                                            u64* count, u64 cap, u32* os_of) {
+    const u64 mark = (1ULL << 63) | (tb_fingerprint(lo, hi) >> 1);
+    u64 pos = tb_hash_id(lo, hi) & H.account_mask;
+    u32 slot = TB_NOT_FOUND;
+    for (u64 k = 0; k <= H.account_mask; k++) {
+        // Plain (cached) reads: a stale one costs a failed CAS (which returns the truth) or a
+        // duplicate entry, never a wrong one.
+        u64* tw = &H.acct_hot[pos].timestamp;
+        u64 t = *tw;
+        if (t == 0) {
+            t = atomicCAS((unsigned long long*)tw, 0ULL, (unsigned long long)mark);
             if (t == 0) {
-                t = atomicCAS((unsigned long long*)tw, 0ULL, (unsigned long long)mark);
-                if (t == 0) {
-                    slot = (u32)pos;
-                    break;
-                }
+                slot = (u32)pos;
+                break;
             }
-            if (t == mark) break;  // another lane is importing this id
-            if (!(t >> 63)) {  // a complete entry: this id already?  (a stale read only costs a duplicate entry)
-                const AccountHot* e = &H.acct_hot[pos];
-                if (e->id_lo == lo && e->id_hi == hi) break;
+        }
+        if (t == mark) break;  // another lane is importing this id
+        if (!(t >> 63)) {  // a complete entry: this id already?  (a stale read only costs a duplicate entry)
+            const AccountHot* e = &H.acct_hot[pos];
+            if (e->id_lo == lo && e->id_hi == hi) break;
+        }
+        pos = (pos + 1) & H.account_mask;
+    }
+    if (slot == TB_NOT_FOUND) return;
+    const u64 k = tb_wave_claim(true, count);
+    if (k < cap) list[k] = slot;
+    else tb_panic(H.g, PANIC_TABLE_FULL);
+    const Tables& O = N.T[o];
+    const u32 os = tb_account_find(O, lo, hi);
+    AccountHot* h = &H.acct_hot[slot];
+    if (os == TB_NOT_FOUND) {  // no such account: a tombstone id (probes continue past it) under the marker
+        h->id_lo = ~0ULL;
+        h->id_hi = ~0ULL;
+        return;
+    }
+    const AccountHot a = O.acct_hot[os];
+    os_of[slot] = os;  // the owner's slot, for this pass's owner legs
+    h->ledger = a.ledger;
+    h->code = a.code;
+    h->flags = a.flags;
+    h->id_lo = lo;
+    h->id_hi = hi;
+    // No fence before the timestamp: a lane of this kernel that reads the entry before the fields
+    // reach it only imports the id once more (a duplicate entry, equal by the end), and the
+    // pass's next kernel sees everything.  (An agent-scope fence on gfx950 writes back and
+    // invalidates the XCD's whole L2, per wave: it cost this kernel 1 ms a pass.)
+    __hip_atomic_store(&h->timestamp, a.timestamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void tb_node_import(Tables H, NodeTablesArgs N, const u8* events, u64 n, u32 self,
+                                                      u32* list, u64* count, u64 cap, u32* os_of) {
+    __shared__ WgDedup s_d;
+    for (u64 base = (u64)blockIdx.x * 256; base < n; base += (u64)gridDim.x * 256) {  // uniform per workgroup
+        tb_wg_dedup_reset(s_d);
+        const u64 e = base + threadIdx.x;
+        u64 lo[2] = {0, 0}, hi[2] = {0, 0};
+        u32 o[2] = {0, 0}, st[2] = {WGD_SKIP, WGD_SKIP};
+#pragma unroll
+        for (u32 s = 0; s < 2; s++) {
+            if (e < n) {
+                const u64* w = (const u64*)(events + e * 128) + 2 + 2 * s;  // debit @16, credit @32
+                lo[s] = w[0];
+                hi[s] = w[1];
+                o[s] = tb_home(lo[s], hi[s], N.world);
             }
-            pos = (pos + 1) & H.account_mask;
+            // owned here: present or absent in the owned table itself
+            const bool want = e < n && !tb_id_reserved(lo[s], hi[s]) && o[s] != self;
+            st[s] = tb_wg_dedup_claim(s_d, want, lo[s], hi[s]);
         }
-        if (slot == TB_NOT_FOUND) continue;
-        const u64 k = tb_wave_claim(true, count);
-        if (k < cap) list[k] = slot;
-        else tb_panic(H.g, PANIC_TABLE_FULL);
-        const Tables& O = N.T[o];
-        const u32 os = tb_account_find(O, lo, hi);
-        AccountHot* h = &H.acct_hot[slot];
-        if (os == TB_NOT_FOUND) {  // no such account: a tombstone id (probes continue past it) under the marker
-            h->id_lo = ~0ULL;
-            h->id_hi = ~0ULL;
-            continue;
+        __syncthreads();
+#pragma unroll
+        for (u32 s = 0; s < 2; s++) {
+            if (tb_wg_dedup_go(s_d, st[s], lo[s], hi[s])) tb_import_one(H, N, lo[s], hi[s], o[s], list, count, cap, os_of);
         }
-        const AccountHot a = O.acct_hot[os];
-        os_of[slot] = os;  // the owner's slot, for this pass's owner legs
-        h->ledger = a.ledger;
-        h->code = a.code;
-        h->flags = a.flags;
-        h->id_lo = lo;
-        h->id_hi = hi;
-        // No fence before the timestamp: a lane of this kernel that reads the entry before the fields
-        // reach it only imports the id once more (a duplicate entry, equal by the end), and the
-        // pass's next kernel sees everything.  (An agent-scope fence on gfx950 writes back and
-        // invalidates the XCD's whole L2, per wave: it cost this kernel 1 ms a pass.)
-        __hip_atomic_store(&h->timestamp, a.timestamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
     }
 }
 
@@ -706,13 +769,29 @@ __global__ void tb_seq_load_transfers(NodeTablesArgs N, SeqSet tset, Tables X, u
 }
 
 // The accounts every sequenced event names, to the account set.
+// (one lane per distinct id of the workgroup: Zipf-hot accounts are most of the names)
 __global__ __launch_bounds__(256) void tb_seq_event_accounts(const u8* events, u64 n, SeqSet aset) {
+    __shared__ WgDedup s_d;
+    tb_wg_dedup_reset(s_d);
     const u64 g = (u64)blockIdx.x * 256 + threadIdx.x;
-    if (g >= n) return;
-    const u64* w = (const u64*)(events + g * 128);
-    if (((const u16*)(events + g * 128))[59] & 0x8000) return;  // a placeholder (or a reserved-flag event: no state read)
-    tb_seq_insert(aset, w[2], w[3]);
-    tb_seq_insert(aset, w[4], w[5]);
+    // a placeholder (or a reserved-flag event: no state read) names nothing
+    const bool live = g < n && !(((const u16*)(events + g * 128))[59] & 0x8000);
+    u64 lo[2] = {0, 0}, hi[2] = {0, 0};
+    u32 st[2];
+#pragma unroll
+    for (u32 s = 0; s < 2; s++) {
+        if (live) {
+            const u64* w = (const u64*)(events + g * 128) + 2 + 2 * s;
+            lo[s] = w[0];
+            hi[s] = w[1];
+        }
+        st[s] = tb_wg_dedup_claim(s_d, live && !tb_id_reserved(lo[s], hi[s]), lo[s], hi[s]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (u32 s = 0; s < 2; s++) {
+        if (tb_wg_dedup_go(s_d, st[s], lo[s], hi[s])) tb_seq_insert(aset, lo[s], hi[s]);
+    }
 }
 
 // The accounts, into the sequencer: record and balances from the owner (the only copy); the balances
