@@ -239,7 +239,7 @@ struct tbgpu {
     u64 wall_khz = 0;  // device wall clock (flow phase timing)
     WbBufs wb;
     // Groove write-back snapshot (tbgpu_checkpoint_delta).
-    AccountBal* ckpt_bal = nullptr;  // balances at the previous write-back
+    u64* ckpt_bal = nullptr;  // balances at the previous write-back: the two planes of T.bal (tb_device.h BalView)
     u32* ckpt_mark = nullptr;        // per slot: the write-back epoch that last covered it
     u32 ckpt_epoch = 0;
     u64 ckpt_pos = 0;                // log position of the first transfer not yet written back
@@ -276,6 +276,11 @@ struct tbgpu {
     u64* r_meta = nullptr;    // device [meta_cap + 1] offsets then [meta_cap] timestamps
     u64* h_rmeta = nullptr;   // pinned mirror
 };
+
+// The write-back snapshot as a balance view (its two planes, like T.bal).
+static inline BalView ckpt_view(const tbgpu* E) {
+    return BalView{E->ckpt_bal, E->ckpt_bal ? E->ckpt_bal + 4 * E->account_cap : nullptr};
+}
 
 static void ckpt_note_ids(tbgpu* E, const u8* records, u64 n);
 
@@ -356,7 +361,7 @@ static int prof_collect(tbgpu* E) {
 
 static int engine_clear(tbgpu* E) {
     HIPCK(hipMemsetAsync(E->T.acct_hot, 0, E->account_cap * sizeof(AccountHot), E->stream));
-    HIPCK(hipMemsetAsync(E->T.acct_bal, 0, E->account_cap * sizeof(AccountBal), E->stream));
+    HIPCK(hipMemsetAsync(E->T.bal.lo, 0, E->account_cap * sizeof(AccountBal), E->stream));  // both planes
     HIPCK(hipMemsetAsync(E->T.acct_cold, 0, E->account_cap * sizeof(AccountCold), E->stream));
     HIPCK(hipMemsetAsync(E->T.account_mark, 0, E->account_cap * sizeof(u32), E->stream));
     HIPCK(hipMemsetAsync(E->T.xidx, 0, E->xidx_cap * sizeof(u64), E->stream));
@@ -571,7 +576,8 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     }
 
     INIT_CK(tbMalloc(&E->T.acct_hot, E->account_cap * sizeof(AccountHot)));
-    INIT_CK(tbMalloc(&E->T.acct_bal, E->account_cap * sizeof(AccountBal)));
+    INIT_CK(tbMalloc(&E->T.bal.lo, E->account_cap * sizeof(AccountBal)));  // low plane, then high plane
+    E->T.bal.hi = E->T.bal.lo + 4 * E->account_cap;
     INIT_CK(tbMalloc(&E->T.acct_cold, E->account_cap * sizeof(AccountCold)));
     INIT_CK(tbMalloc(&E->T.account_mark, E->account_cap * sizeof(u32)));
     INIT_CK(tbMalloc(&E->T.xidx, E->xidx_cap * sizeof(u64)));
@@ -782,7 +788,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
     (void)hipSetDevice(E->device);
     dev_register(E, false);
     if (E->stream) (void)hipStreamSynchronize(E->stream);
-    void* bufs[] = {E->ckpt_bal, E->ckpt_mark, E->T.acct_hot, E->T.acct_bal, E->T.acct_cold, E->T.account_mark, E->T.xidx, E->T.xdup, E->T.xlog,
+    void* bufs[] = {E->ckpt_bal, E->ckpt_mark, E->T.acct_hot, E->T.bal.lo, E->T.acct_cold, E->T.account_mark, E->T.xidx, E->T.xdup, E->T.xlog,
                     E->T.xposted, E->g, E->bloom, E->info, E->eflags, E->dr,
                     E->cr, E->ps, E->rs, E->dep_list, E->dep_count, E->amt, E->kid, E->kpid, E->dedup,
                     E->sum_shards, E->undo, E->staging, E->results, E->reply_bytes, E->meta,
@@ -1741,7 +1747,7 @@ static int wb_gather_slice(tbgpu* E, u64 a, u64 b, bool want_records, bool poste
 static int wb_ids(tbgpu* E, const u64* d_ids, u64 n, const u64* n_dev) {
     if (E->ckpt_scan || !n) return TBGPU_STATUS_OK;
     WbBufs& W = E->wb;
-    hipLaunchKernelGGL(tb_delta_ids, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T, E->ckpt_bal, E->ckpt_ts,
+    hipLaunchKernelGGL(tb_delta_ids, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream, E->T, ckpt_view(E), E->ckpt_ts,
                        d_ids, n, E->ckpt_mark, E->ckpt_epoch, W.d_acc, W.d_before, W.d_cnt + WB_ACCOUNTS, W.d_slots,
                        W.d_cnt + WB_SLOTS, n_dev);
     HIPCK(hipGetLastError());
@@ -1792,7 +1798,7 @@ static int wb_scan(tbgpu* E, u32 world, u32 self, u8* out, u8* before_out, u64* 
     for (u64 s0 = 0; s0 < E->account_cap; s0 += E->wb.cap_a) {
         const u64 s1 = std::min<u64>(E->account_cap, s0 + E->wb.cap_a);
         hipLaunchKernelGGL(tb_delta_accounts, dim3((unsigned)((s1 - s0 + 255) / 256)), dim3(256), 0, E->stream, E->T,
-                           E->ckpt_bal, E->ckpt_ts, s0, s1, E->wb.d_acc, E->wb.cap_a, E->wb.d_cnt + WB_ACCOUNTS,
+                           ckpt_view(E), E->ckpt_ts, s0, s1, E->wb.d_acc, E->wb.cap_a, E->wb.d_cnt + WB_ACCOUNTS,
                            E->wb.d_before, world, self);
         HIPCK(hipGetLastError());
         int st = wb_read_counts(E);
@@ -1806,11 +1812,11 @@ static int wb_scan(tbgpu* E, u32 world, u32 self, u8* out, u8* before_out, u64* 
 // positions move, the lists empty.
 static int wb_advance(tbgpu* E) {
     if (E->ckpt_scan) {
-        HIPCK(hipMemcpyAsync(E->ckpt_bal, E->T.acct_bal, E->account_cap * sizeof(AccountBal), hipMemcpyDeviceToDevice,
+        HIPCK(hipMemcpyAsync(E->ckpt_bal, E->T.bal.lo, E->account_cap * sizeof(AccountBal), hipMemcpyDeviceToDevice,
                              E->stream));
     } else {
         const u32 grid = (u32)std::max<u64>(1, std::min<u64>(2048, (E->account_cap + 255) / 256));
-        hipLaunchKernelGGL(tb_delta_advance, dim3(grid), dim3(256), 0, E->stream, E->T, E->ckpt_bal, E->wb.d_slots,
+        hipLaunchKernelGGL(tb_delta_advance, dim3(grid), dim3(256), 0, E->stream, E->T, ckpt_view(E), E->wb.d_slots,
                            E->wb.d_cnt + WB_SLOTS);
         HIPCK(hipGetLastError());
     }
@@ -2044,9 +2050,9 @@ static int wb_tail(tbgpu* E, hipEvent_t after) {
     const int st = wb_gather_slice(E, W.tail_pos0, W.tail_pos1, true, true, W.stream);
     E->ckpt_ts = ts;
     if (st) return st;
-    hipLaunchKernelGGL(tb_delta_emit, dim3(1024), dim3(256), 0, W.stream, E->T, E->ckpt_bal, W.tail_ts0, W.d_slots, W.d_cap,
+    hipLaunchKernelGGL(tb_delta_emit, dim3(1024), dim3(256), 0, W.stream, E->T, ckpt_view(E), W.tail_ts0, W.d_slots, W.d_cap,
                        W.d_cnt + WB_SLOTS, W.d_acc, W.d_before, W.d_cnt + WB_ACCOUNTS);
-    hipLaunchKernelGGL(tb_delta_advance_from, dim3(1024), dim3(256), 0, W.stream, E->ckpt_bal, W.d_slots, W.d_cap,
+    hipLaunchKernelGGL(tb_delta_advance_from, dim3(1024), dim3(256), 0, W.stream, ckpt_view(E), W.d_slots, W.d_cap,
                        W.d_cnt + WB_SLOTS);
     hipLaunchKernelGGL(tb_delta_order, dim3(256), dim3(256), 0, W.stream, W.d_out, W.d_cnt + WB_RECORDS, W.d_pairs,
                        W.d_cnt + WB_PV, W.d_cnt + WB_ORDER);
@@ -2918,7 +2924,7 @@ static int upsert_accounts(tbgpu* E, const void* records, uint32_t n, bool if_ab
         HIPCK(hipMemcpyAsync(E->lookup_out, (const u8*)records + (u64)c * 128, (u64)m * 128, hipMemcpyHostToDevice,
                              E->stream));
         hipLaunchKernelGGL(tb_upsert_accounts, dim3((m + 255) / 256), dim3(256), 0, E->stream, E->T, E->lookup_out, m,
-                           E->d_status, if_absent ? 1u : 0u, if_absent ? E->ckpt_bal : nullptr);
+                           E->d_status, if_absent ? 1u : 0u, if_absent ? ckpt_view(E) : BalView{nullptr, nullptr});
         HIPCK(hipGetLastError());
         HIPCK(hipStreamSynchronize(E->stream));
     }

@@ -207,12 +207,14 @@ __device__ static inline void tb_apply_legs_body(const PassArgs& P, u64* s_acc) 
     const u32 extras = tb_bucket_extras(total);
     if (!extras) {
         tb_gather_range(P, 0, total, nb, s_start, s_pref, s_acc, s_red);
-        // Write back: thread k -> (slot k/4, field k%4), consecutive threads on consecutive 16-B fields.
-        // Every load of the thread's words is issued before any store: on gfx950 a load waits for the
-        // wave's earlier stores (vmcnt counts both), so a read-modify-write per word in turn was one
-        // memory round trip per word.
+        // Write back into the low plane (tb_device.h BalView): word k of the bucket is (slot k/4, field
+        // k%4), so consecutive threads read-modify-write consecutive 8-B words — whole lines, four
+        // accounts each, and no high word (no carry under the certificate).  Every load of the
+        // thread's words is issued before any store: on gfx950 a load waits for the wave's earlier
+        // stores (vmcnt counts both), so a read-modify-write per word in turn was one memory round
+        // trip per word.
         constexpr u32 PER = 4 * LEG_SLOTS_MAX / APPLY_THREADS;
-        u64* __restrict__ bal = (u64*)(P.T.acct_bal + (u64)g * W);
+        u64* __restrict__ bal = P.T.bal.lo + 4 * (u64)g * W;
         u64 v[PER], old[PER];
 #pragma unroll
         for (u32 q = 0; q < PER; q++) {
@@ -220,10 +222,10 @@ __device__ static inline void tb_apply_legs_body(const PassArgs& P, u64* s_acc) 
             v[q] = k < 4 * W ? s_acc[k] : 0;
         }
 #pragma unroll
-        for (u32 q = 0; q < PER; q++) old[q] = v[q] ? bal[2 * (u64)(threadIdx.x + q * APPLY_THREADS)] : 0;
+        for (u32 q = 0; q < PER; q++) old[q] = v[q] ? bal[threadIdx.x + q * APPLY_THREADS] : 0;
 #pragma unroll
         for (u32 q = 0; q < PER; q++) {
-            if (v[q]) bal[2 * (u64)(threadIdx.x + q * APPLY_THREADS)] = old[q] + v[q];  // low word: no carry (certificate)
+            if (v[q]) bal[threadIdx.x + q * APPLY_THREADS] = old[q] + v[q];  // low word: no carry (certificate)
         }
         return;
     }
@@ -233,10 +235,10 @@ __device__ static inline void tb_apply_legs_body(const PassArgs& P, u64* s_acc) 
         if (!mine) continue;
         tb_gather_range(P, q * APPLY_PART, min(total, (q + 1) * APPLY_PART), nb, s_start, s_pref, s_acc, s_red);
     }
-    u8* bal = (u8*)(P.T.acct_bal + (u64)g * W);
+    u64* bal = P.T.bal.lo + 4 * (u64)g * W;
     for (u32 k = threadIdx.x; k < 4 * W; k += APPLY_THREADS) {
         const u64 v = s_acc[k];
-        if (v != 0) tb_atomic_add_lo_noret(bal + (u64)k * 16, v);
+        if (v != 0) tb_atomic_add_lo_noret(bal + k, v);
     }
 }
 

@@ -61,13 +61,14 @@ __global__ void tb_set_balances(Tables T, u64 lo, u64 hi, u64 dp_lo, u64 dp_hi, 
         *status = 1;
         return;
     }
-    AccountBal* a = &T.acct_bal[slot];
-    a->debits_pending = tb_u128(dp_lo, dp_hi);
-    a->debits_posted = tb_u128(dpo_lo, dpo_hi);
-    a->credits_pending = tb_u128(cp_lo, cp_hi);
-    a->credits_posted = tb_u128(cpo_lo, cpo_hi);
-    const u128 d = tb_sat_add(a->debits_pending, a->debits_posted);
-    const u128 c = tb_sat_add(a->credits_pending, a->credits_posted);
+    AccountBal a;
+    a.debits_pending = tb_u128(dp_lo, dp_hi);
+    a.debits_posted = tb_u128(dpo_lo, dpo_hi);
+    a.credits_pending = tb_u128(cp_lo, cp_hi);
+    a.credits_posted = tb_u128(cpo_lo, cpo_hi);
+    tb_bal_store(T.bal, slot, a);
+    const u128 d = tb_sat_add(a.debits_pending, a.debits_posted);
+    const u128 c = tb_sat_add(a.credits_pending, a.credits_posted);
     u128 bound = tb_u128(T.g->bound_lo, T.g->bound_hi);
     if (d > bound) bound = d;
     if (c > bound) bound = c;
@@ -86,7 +87,7 @@ __global__ void tb_zero_balances(Tables T, u64 cap) {
         T.g->bound_hi = 0;
     }
     if (i >= cap) return;
-    T.acct_bal[i] = AccountBal{0, 0, 0, 0};
+    tb_bal_store(T.bal, i, AccountBal{0, 0, 0, 0});
 }
 
 // ---- groove write-back (StateMachine.checkpoint, state_machine.zig:542-582) --------------------
@@ -96,14 +97,14 @@ __global__ void tb_zero_balances(Tables T, u64 cap) {
 // tb_delta_accounts is the whole-table diff, kept for the one case the host cannot name the changed
 // accounts (create_accounts committed from device memory, tbgpu_commit_device_async, or more of them
 // than the engine lists).  Counts past `cap` are still counted (the host retries with room).
-__global__ void tb_delta_accounts(Tables T, const AccountBal* snap, u64 ts0, u64 first, u64 last, u8* out, u64 cap,
+__global__ void tb_delta_accounts(Tables T, BalView snap, u64 ts0, u64 first, u64 last, u8* out, u64 cap,
                                   u64* count, AccountBal* before, u32 world, u32 self) {
     const u64 i = first + (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= last) return;
     const AccountHot& h = T.acct_hot[i];
     if (h.timestamp == 0 || tb_id_reserved(h.id_lo, h.id_hi)) return;
     if (world > 1 && tb_home(h.id_lo, h.id_hi, world) != self) return;  // a node shard: its owned accounts
-    const AccountBal b = T.acct_bal[i], s = snap[i];
+    const AccountBal b = tb_bal_load(T.bal, i), s = tb_bal_load(snap, i);
     const bool same = b.debits_pending == s.debits_pending && b.debits_posted == s.debits_posted &&
                       b.credits_pending == s.credits_pending && b.credits_posted == s.credits_posted;
     if (h.timestamp <= ts0 && same) return;
@@ -212,7 +213,7 @@ __global__ void tb_delta_posted(Tables T, const u64* pv, const u64* npv, u64* pa
 // > ts0) or when its balances differ from the snapshot; `slots` lists every slot seen, for the
 // snapshot's advance.  n_dev (optional): the id count is 2 x *n_dev (the new transfers' two accounts,
 // counted on the device), n is then only the grid's bound.
-__global__ __launch_bounds__(256) void tb_delta_ids(Tables T, const AccountBal* snap, u64 ts0, const u64* ids, u64 n,
+__global__ __launch_bounds__(256) void tb_delta_ids(Tables T, BalView snap, u64 ts0, const u64* ids, u64 n,
                                                     u32* mark, u32 epoch, u8* out, AccountBal* before, u64* count,
                                                     u32* slots, u64* slot_count, const u64* n_dev = nullptr) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -228,8 +229,8 @@ __global__ __launch_bounds__(256) void tb_delta_ids(Tables T, const AccountBal* 
     if (slot != TB_NOT_FOUND) {
         was = atomicExch(&mark[slot], epoch);
         h = T.acct_hot[slot];
-        b = T.acct_bal[slot];
-        sn = snap[slot];
+        b = tb_bal_load(T.bal, slot);
+        sn = tb_bal_load(snap, slot);
         c = T.acct_cold[slot];
     }
     const bool first = was != epoch;  // the first copy of the id takes its slot
@@ -277,7 +278,7 @@ __global__ __launch_bounds__(256) void tb_delta_capture(Tables T, const u64* ids
     AccountBal b{};
     if (slot != TB_NOT_FOUND) {
         was = atomicExch(&mark[slot], epoch);
-        b = T.acct_bal[slot];
+        b = tb_bal_load(T.bal, slot);
     }
     const bool first = was != epoch;
     const u64 si = tb_wave_claim(first, slot_count);
@@ -313,11 +314,11 @@ __global__ __launch_bounds__(256) void tb_delta_capture_log(Tables T, u64 pos0, 
     AccountBal db{}, cb{};
     if (ds != TB_NOT_FOUND) {
         dw = atomicExch(&mark[ds], epoch);
-        db = T.acct_bal[ds];
+        db = tb_bal_load(T.bal, ds);
     }
     if (cs != TB_NOT_FOUND) {
         cw = atomicExch(&mark[cs], epoch);
-        cb = T.acct_bal[cs];
+        cb = tb_bal_load(T.bal, cs);
     }
     const bool df = dw != epoch, cf = cw != epoch;
     const u64 dsi = tb_wave_claim(df, slot_count);
@@ -332,7 +333,7 @@ __global__ __launch_bounds__(256) void tb_delta_capture_log(Tables T, u64 pos0, 
     }
 }
 
-__global__ __launch_bounds__(256) void tb_delta_emit(Tables T, const AccountBal* snap, u64 ts0, const u32* slots,
+__global__ __launch_bounds__(256) void tb_delta_emit(Tables T, BalView snap, u64 ts0, const u32* slots,
                                                      const AccountBal* cap, const u64* slot_count, u8* out,
                                                      AccountBal* before, u64* count) {
     const u64 m = *slot_count;
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(256) void tb_delta_emit(Tables T, const AccountBal*
             const u32 slot = slots[i];
             h = T.acct_hot[slot];
             c = T.acct_cold[slot];
-            sn = snap[slot];
+            sn = tb_bal_load(snap, slot);
             b = cap[i];
         }
         const bool same = b.debits_pending == sn.debits_pending && b.debits_posted == sn.debits_posted &&
@@ -374,16 +375,16 @@ __global__ __launch_bounds__(256) void tb_delta_emit(Tables T, const AccountBal*
     }
 }
 
-__global__ void tb_delta_advance_from(AccountBal* snap, const u32* slots, const AccountBal* cap, const u64* n) {
+__global__ void tb_delta_advance_from(BalView snap, const u32* slots, const AccountBal* cap, const u64* n) {
     const u64 m = *n;
-    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (u64)gridDim.x * blockDim.x) snap[slots[i]] = cap[i];
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (u64)gridDim.x * blockDim.x) tb_bal_store(snap, slots[i], cap[i]);
 }
 
 // The snapshot follows the slots a write-back covered (*n of them), grid-stride.
-__global__ void tb_delta_advance(Tables T, AccountBal* snap, const u32* slots, const u64* n) {
+__global__ void tb_delta_advance(Tables T, BalView snap, const u32* slots, const u64* n) {
     const u64 m = *n;
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (u64)gridDim.x * blockDim.x) {
-        snap[slots[i]] = T.acct_bal[slots[i]];
+        tb_bal_store(snap, slots[i], tb_bal_load(T.bal, slots[i]));
     }
 }
 

@@ -325,7 +325,7 @@ __device__ static inline u32 fl_run_run(const PassArgs& P, const FlowArgs& F, Re
                                         u32 q, u32 r, u32* count, u64* tsmax) {
     const Tables& T = P.T;
     const u32* K = F.keys[0];
-    AccountBal B = rp_load<true>(&T.acct_bal[r]);
+    AccountBal B = rp_bal_load<true>(T.bal, r);
     const u16 rflags = T.acct_hot[r].flags;
     u32 n = 0, n_ok = 0, last = u, last_ok_pe = TB_NOT_FOUND;
     bool more = true;
@@ -370,11 +370,10 @@ __device__ static inline u32 fl_run_run(const PassArgs& P, const FlowArgs& F, Re
                                  : (pend ? &B.credits_pending : &B.credits_posted);
                 *rf += amount;
                 // The free side: one field, +amount (exact in any order).
-                u8* fb = (u8*)&T.acct_bal[debit ? crs : drs];
-                const u32 off = debit ? (pend ? BAL_OFF_CREDITS_PENDING : BAL_OFF_CREDITS_POSTED)
-                                      : (pend ? BAL_OFF_DEBITS_PENDING : BAL_OFF_DEBITS_POSTED);
-                if (R.cert64) tb_atomic_add_lo_noret(fb + off, tb_lo(amount));
-                else tb_atomic_add_u128(fb + off, amount);
+                const u32 fs = debit ? crs : drs;
+                const u32 ff = debit ? (pend ? BAL_CP : BAL_CPOST) : (pend ? BAL_DP : BAL_DPOST);
+                if (R.cert64) tb_bal_add_lo(T.bal, fs, ff, tb_lo(amount));
+                else tb_bal_add(T.bal, fs, ff, amount);
                 __hip_atomic_fetch_and(&T.xidx[crs_[j]], ~(u64)XI_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 n_ok++;
                 last_ok_pe = pe;
@@ -387,7 +386,7 @@ __device__ static inline u32 fl_run_run(const PassArgs& P, const FlowArgs& F, Re
         more = j == FLOW_RUN_STEP;
         q += FLOW_RUN_STEP;
     }
-    rp_store<true>(&T.acct_bal[r], B);
+    rp_bal_store<true>(T.bal, r, B);
     R.xcount += n_ok;
     if (last_ok_pe != TB_NOT_FOUND) {  // commit_timestamp: the run's last ok event is its latest
         u32 lo = P.b0, hi = P.b1;
@@ -1600,11 +1599,10 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
         const u32 u = meta >> 3;
         if (!(meta & (BT_X | BT_Y)) || F.b_st[u] != BS_UNK) continue;
         const u32 r = K[q];
-        const AccountBal& B = T.acct_bal[r];
+        const u64* L = T.bal.lo + 4 * (u64)r;  // low words (the bounds run in u64)
         const bool dlim = T.acct_hot[r].flags & AF_DEBITS_MUST_NOT_EXCEED_CREDITS;
-        const u64 xb = dlim ? tb_lo(B.debits_pending) + tb_lo(B.debits_posted)
-                            : tb_lo(B.credits_pending) + tb_lo(B.credits_posted);
-        const u64 yb = dlim ? tb_lo(B.credits_posted) : tb_lo(B.debits_posted);
+        const u64 xb = dlim ? L[BAL_DP] + L[BAL_DPOST] : L[BAL_CP] + L[BAL_CPOST];
+        const u64 yb = dlim ? L[BAL_CPOST] : L[BAL_DPOST];
         const u32 head = (u32)v[1];
         F.b_xy[2 * q] = xb + v[0] - own[0];
         F.b_xy[2 * q + 1] = yb + v[2] - own[2];
@@ -1994,10 +1992,9 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
                 // segment.  Statuses read in the middle of a round are facts, old or new, so any mix
                 // of them still bounds the truth.
                 const u64 xmin = v[0] - own[0], xmax = v[1] - own[1], ymin = v[2] - own[2], ymax = v[3] - own[3];
-                const AccountBal& B = T.acct_bal[K[q]];
-                const u64 xb = cr_side ? tb_lo(B.credits_pending) + tb_lo(B.credits_posted)
-                                       : tb_lo(B.debits_pending) + tb_lo(B.debits_posted);
-                const u64 yb = cr_side ? tb_lo(B.debits_posted) : tb_lo(B.credits_posted);
+                const u64* L = T.bal.lo + 4 * (u64)K[q];  // low words
+                const u64 xb = cr_side ? L[BAL_CP] + L[BAL_CPOST] : L[BAL_DP] + L[BAL_DPOST];
+                const u64 yb = cr_side ? L[BAL_DPOST] : L[BAL_CPOST];
                 const u64 a = F.b_amt[q];
                 u8 verdict = BV_UNK;
                 if (xb + xmax + a <= yb + ymin) verdict = BV_PASS;
@@ -2070,8 +2067,8 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
         if (ok) {
             a = P.amt[pe];
             const bool pend = P.eflags[pe] & TF_PENDING;
-            dw = (u64*)((u8*)&T.acct_bal[P.dr[pe]] + (pend ? BAL_OFF_DEBITS_PENDING : BAL_OFF_DEBITS_POSTED));
-            cw = (u64*)((u8*)&T.acct_bal[P.cr[pe]] + (pend ? BAL_OFF_CREDITS_PENDING : BAL_OFF_CREDITS_POSTED));
+            dw = T.bal.lo + 4 * (u64)P.dr[pe] + (pend ? BAL_DP : BAL_DPOST);
+            cw = T.bal.lo + 4 * (u64)P.cr[pe] + (pend ? BAL_CP : BAL_CPOST);
             __hip_atomic_fetch_and(&T.xidx[P.rs[pe]], ~(u64)XI_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             n_ok++;
             const u32 b = F.f_batch[f];

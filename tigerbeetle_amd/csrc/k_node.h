@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void tb_node_apply_legs(Tables T, NodeLegArgs 
                 if ((w[0] >> 2) != TB_NOT_FOUND) tb_panic(T.g, PANIC_ASSERT | 0x800);
                 continue;
             }
-            tb_atomic_add_u128((u8*)&T.acct_bal[w[0] >> 2] + 16 * (w[0] & 3), tb_u128(w[1], w[2]));
+            tb_bal_add(T.bal, w[0] >> 2, (u32)(w[0] & 3), tb_u128(w[1], w[2]));
         }
         return;
     }
@@ -133,12 +133,12 @@ __global__ __launch_bounds__(256) void tb_node_apply_legs(Tables T, NodeLegArgs 
                 }
                 p = (p + 1) & (NAL_TABLE - 1);
             }
-            if (!placed) tb_atomic_add_lo_noret((u8*)&T.acct_bal[key[q] >> 2] + 16 * (key[q] & 3), amt[q]);
+            if (!placed) tb_bal_add_lo(T.bal, key[q] >> 2, (u32)(key[q] & 3), amt[q]);
         }
         __syncthreads();
         for (u32 k = threadIdx.x; k < NAL_TABLE; k += 256) {
             const u64 kk = s_key[k];
-            if (kk != ~0ULL) tb_atomic_add_lo_noret((u8*)&T.acct_bal[kk >> 2] + 16 * (kk & 3), s_sum[k]);
+            if (kk != ~0ULL) tb_bal_add_lo(T.bal, kk >> 2, (u32)(kk & 3), s_sum[k]);
         }
         __syncthreads();
     }
@@ -367,7 +367,7 @@ __global__ __launch_bounds__(256) void tb_ledger_summary(Tables T, u64 cap, u32 
     if (i < cap) {
         const AccountHot& h = T.acct_hot[i];
         if (h.timestamp != 0 && !tb_id_reserved(h.id_lo, h.id_hi)) {
-            const AccountBal b = T.acct_bal[i];
+            const AccountBal b = tb_bal_load(T.bal, i);
             v[0] = b.debits_pending;
             v[1] = b.debits_posted;
             v[2] = b.credits_pending;
@@ -862,12 +862,11 @@ __global__ void tb_seq_writeback_accounts(Tables X, SeqSet aset, Tables O, u32 s
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
         const SeqEntry& q = aset.e[aset.list[i]];
         if (q.x == TB_NOT_FOUND || q.home == SEQ_NEW || tb_home(q.lo, q.hi, world) != self) continue;
-        const AccountBal x = X.acct_bal[q.x], b = bal0[i];
-        u8* o = (u8*)&O.acct_bal[q.home];
-        if (x.debits_pending != b.debits_pending) tb_atomic_add_u128(o + BAL_OFF_DEBITS_PENDING, x.debits_pending - b.debits_pending);
-        if (x.debits_posted != b.debits_posted) tb_atomic_add_u128(o + BAL_OFF_DEBITS_POSTED, x.debits_posted - b.debits_posted);
-        if (x.credits_pending != b.credits_pending) tb_atomic_add_u128(o + BAL_OFF_CREDITS_PENDING, x.credits_pending - b.credits_pending);
-        if (x.credits_posted != b.credits_posted) tb_atomic_add_u128(o + BAL_OFF_CREDITS_POSTED, x.credits_posted - b.credits_posted);
+        const AccountBal x = tb_bal_load(X.bal, q.x), b = bal0[i];
+        if (x.debits_pending != b.debits_pending) tb_bal_add(O.bal, q.home, BAL_DP, x.debits_pending - b.debits_pending);
+        if (x.debits_posted != b.debits_posted) tb_bal_add(O.bal, q.home, BAL_DPOST, x.debits_posted - b.debits_posted);
+        if (x.credits_pending != b.credits_pending) tb_bal_add(O.bal, q.home, BAL_CP, x.credits_pending - b.credits_pending);
+        if (x.credits_posted != b.credits_posted) tb_bal_add(O.bal, q.home, BAL_CPOST, x.credits_posted - b.credits_posted);
     }
 }
 

@@ -99,6 +99,35 @@ __device__ static inline void rp_store(R* p, const R& v) {
         __hip_atomic_store((u64*)p + k, s[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
+// An account's balances (both planes, tb_device.h BalView) with the same rules.
+template <bool FLOW>
+__device__ static inline AccountBal rp_bal_load(const BalView& V, u64 slot) {
+    if (!FLOW) return tb_bal_load(V, slot);
+    const u64* l = V.lo + 4 * slot;
+    const u64* h = V.hi + 4 * slot;
+    AccountBal b;
+    b.debits_pending = tb_u128(fl_ld64(l), fl_ld64(h));
+    b.debits_posted = tb_u128(fl_ld64(l + 1), fl_ld64(h + 1));
+    b.credits_pending = tb_u128(fl_ld64(l + 2), fl_ld64(h + 2));
+    b.credits_posted = tb_u128(fl_ld64(l + 3), fl_ld64(h + 3));
+    return b;
+}
+template <bool FLOW>
+__device__ static inline void rp_bal_store(const BalView& V, u64 slot, const AccountBal& b) {
+    if (!FLOW) {
+        tb_bal_store(V, slot, b);
+        return;
+    }
+    u64* l = V.lo + 4 * slot;
+    u64* h = V.hi + 4 * slot;
+    const u128 f[4] = {b.debits_pending, b.debits_posted, b.credits_pending, b.credits_posted};
+#pragma unroll
+    for (u32 k = 0; k < 4; k++) {
+        __hip_atomic_store(l + k, tb_lo(f[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(h + k, tb_hi(f[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 template <bool FLOW>
 __device__ static inline void rp_store_posted(const Tables& T, u32 pos, u8 v) {
     if (!FLOW) {
@@ -155,18 +184,18 @@ __device__ static inline void rp_push(Replay& R, u32 kind, u32 slot, const Accou
 }
 
 __device__ static inline void rp_add_free_delta(Replay& R, u32 slot, const AccountBal& d) {
-    u8* a = (u8*)&R.T.acct_bal[slot];
+    const u128 f[4] = {d.debits_pending, d.debits_posted, d.credits_pending, d.credits_posted};
     if (R.cert64) {  // every balance stays below 2^64: the low word alone is exact, no carry to wait for
-        if (d.debits_pending) tb_atomic_add_lo_noret(a + BAL_OFF_DEBITS_PENDING, tb_lo(d.debits_pending));
-        if (d.debits_posted) tb_atomic_add_lo_noret(a + BAL_OFF_DEBITS_POSTED, tb_lo(d.debits_posted));
-        if (d.credits_pending) tb_atomic_add_lo_noret(a + BAL_OFF_CREDITS_PENDING, tb_lo(d.credits_pending));
-        if (d.credits_posted) tb_atomic_add_lo_noret(a + BAL_OFF_CREDITS_POSTED, tb_lo(d.credits_posted));
+#pragma unroll
+        for (u32 k = 0; k < 4; k++) {
+            if (f[k]) tb_bal_add_lo(R.T.bal, slot, k, tb_lo(f[k]));
+        }
         return;
     }
-    if (d.debits_pending) tb_atomic_add_u128(a + BAL_OFF_DEBITS_PENDING, d.debits_pending);
-    if (d.debits_posted) tb_atomic_add_u128(a + BAL_OFF_DEBITS_POSTED, d.debits_posted);
-    if (d.credits_pending) tb_atomic_add_u128(a + BAL_OFF_CREDITS_PENDING, d.credits_pending);
-    if (d.credits_posted) tb_atomic_add_u128(a + BAL_OFF_CREDITS_POSTED, d.credits_posted);
+#pragma unroll
+    for (u32 k = 0; k < 4; k++) {
+        if (f[k]) tb_bal_add(R.T.bal, slot, k, f[k]);
+    }
 }
 
 template <bool FLOW>
@@ -179,7 +208,7 @@ __device__ static inline void rp_scope_close(Replay& R, bool persist) {
                 tb_account_tombstone(R.T, e.slot);
                 R.T.g->account_count--;
                 break;
-            case UNDO_BALANCE_UPDATE: rp_store<FLOW>(&R.T.acct_bal[e.slot], e.before); break;
+            case UNDO_BALANCE_UPDATE: rp_bal_store<FLOW>(R.T.bal, e.slot, e.before); break;
             case UNDO_FREE_DELTA: {
                 AccountBal neg;
                 neg.debits_pending = (u128)0 - e.before.debits_pending;
@@ -217,7 +246,7 @@ template <bool FLOW>
 __device__ static inline AccountBal rp_balance_load(Replay& R, u32 slot, bool* free) {
     *free = FLOW && !fl_account_is_resource(R.T, slot, R.epoch, R.cert_global);
     if (*free) return AccountBal{};
-    return rp_load<FLOW>(&R.T.acct_bal[slot]);
+    return rp_bal_load<FLOW>(R.T.bal, slot);
 }
 
 // Write an account's balances (`before` = what rp_balance_load returned).  A free account on the
@@ -236,7 +265,7 @@ __device__ static inline void rp_balance_update(Replay& R, u32 slot, const Accou
         return;
     }
     rp_push(R, UNDO_BALANCE_UPDATE, slot, &before);
-    rp_store<FLOW>(&R.T.acct_bal[slot], next);
+    rp_bal_store<FLOW>(R.T.bal, slot, next);
 }
 
 // Insert a transfer record at the event's own log position (after an exact find said "absent").

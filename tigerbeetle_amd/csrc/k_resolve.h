@@ -42,11 +42,11 @@ __device__ static inline u32 tb_block_rank(bool pred, u32* s_wave, u32& total) {
     return wb + before;
 }
 
-__device__ static inline bool tb_account_cert_fails(const AccountBal* a, u128 S) {
+__device__ static inline bool tb_account_cert_fails(const AccountBal& a, u128 S) {
     if (S == TB_U128_MAX) return true;  // saturated: the true S is unknown (tb_pass_cert)
     u128 d, c, r;
-    if (tb_add_overflows(a->debits_pending, a->debits_posted, &d)) return true;
-    if (tb_add_overflows(a->credits_pending, a->credits_posted, &c)) return true;
+    if (tb_add_overflows(a.debits_pending, a.debits_posted, &d)) return true;
+    if (tb_add_overflows(a.credits_pending, a.credits_posted, &c)) return true;
     if (tb_add_overflows(d, S, &r)) return true;
     if (tb_add_overflows(c, S, &r)) return true;
     return false;
@@ -86,30 +86,29 @@ __device__ static inline void tb_write_replies(const PassArgs& P, u32 b, u32 L, 
 // can reach 2^64 this pass) the adds are fire-and-forget low-word atomics.
 __device__ static inline void tb_apply_transfer(const PassArgs& P, u32 pe, u32 info, u16 flags, bool cert64) {
     const Tables& T = P.T;
-    u8* dr = (u8*)&T.acct_bal[P.dr[pe]];
-    u8* cr = (u8*)&T.acct_bal[P.cr[pe]];
+    const u32 dr = P.dr[pe], cr = P.cr[pe];
     const u128 amount = tb_u128(P.amt[pe], (info & HZ_AMT_HI) ? P.amt_hi[pe] : 0ULL);
     if (info & HZ_POSTVOID) {
         const u32 pslot = P.ps[pe];
         const u128 pamount = T.xlog[pslot].amount;
         T.xposted[pslot] = (flags & TF_POST) ? POSTED_POSTED : POSTED_VOIDED;
         const u128 neg = (u128)0 - pamount;  // dp -= p.amount (mod 2^128, exact in aggregate)
-        tb_atomic_add_u128(dr + BAL_OFF_DEBITS_PENDING, neg);
-        tb_atomic_add_u128(cr + BAL_OFF_CREDITS_PENDING, neg);
+        tb_bal_add(T.bal, dr, BAL_DP, neg);
+        tb_bal_add(T.bal, cr, BAL_CP, neg);
         if (flags & TF_POST) {
-            tb_atomic_add_u128(dr + BAL_OFF_DEBITS_POSTED, amount);
-            tb_atomic_add_u128(cr + BAL_OFF_CREDITS_POSTED, amount);
+            tb_bal_add(T.bal, dr, BAL_DPOST, amount);
+            tb_bal_add(T.bal, cr, BAL_CPOST, amount);
         }
         return;
     }
-    const u32 off_d = (flags & TF_PENDING) ? BAL_OFF_DEBITS_PENDING : BAL_OFF_DEBITS_POSTED;
-    const u32 off_c = (flags & TF_PENDING) ? BAL_OFF_CREDITS_PENDING : BAL_OFF_CREDITS_POSTED;
+    const u32 fd = (flags & TF_PENDING) ? BAL_DP : BAL_DPOST;
+    const u32 fc = (flags & TF_PENDING) ? BAL_CP : BAL_CPOST;
     if (cert64) {
-        tb_atomic_add_lo_noret(dr + off_d, tb_lo(amount));
-        tb_atomic_add_lo_noret(cr + off_c, tb_lo(amount));
+        tb_bal_add_lo(T.bal, dr, fd, tb_lo(amount));
+        tb_bal_add_lo(T.bal, cr, fc, tb_lo(amount));
     } else {
-        tb_atomic_add_u128(dr + off_d, amount);
-        tb_atomic_add_u128(cr + off_c, amount);
+        tb_bal_add(T.bal, dr, fd, amount);
+        tb_bal_add(T.bal, cr, fc, amount);
     }
 }
 
@@ -234,7 +233,7 @@ __device__ static inline bool tb_classify(const PassArgs& P, u32 pe, u32 info, u
             if (info & (HZ_BAL | HZ_LIMIT)) return true;
             if (any_bal && (T.account_mark[drs] == P.epoch || T.account_mark[crs] == P.epoch)) return true;
         }
-        if (!cert_global && (tb_account_cert_fails(&T.acct_bal[drs], S) || tb_account_cert_fails(&T.acct_bal[crs], S))) {
+        if (!cert_global && (tb_account_cert_fails(tb_bal_load(T.bal, drs), S) || tb_account_cert_fails(tb_bal_load(T.bal, crs), S))) {
             return true;
         }
     }

@@ -314,7 +314,7 @@ __global__ void tb_fetch_transfers(Tables T, const u64* ids, u32 n, u8* out, u8*
 // existing one.  Ids within one call are distinct.  status: bit0 table full.
 // if_absent (tbgpu_load_accounts): only accounts the table does not hold are inserted; a resident
 // account is newer than any copy from the forest and stays as it is.
-__global__ void tb_upsert_accounts(Tables T, const u8* recs, u32 n, u32* status, u32 if_absent, AccountBal* snap) {
+__global__ void tb_upsert_accounts(Tables T, const u8* recs, u32 n, u32* status, u32 if_absent, BalView snap) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const Account a = *(const Account*)(recs + (u64)i * 128);
@@ -326,7 +326,7 @@ __global__ void tb_upsert_accounts(Tables T, const u8* recs, u32 n, u32* status,
         b.debits_posted = a.debits_posted;
         b.credits_pending = a.credits_pending;
         b.credits_posted = a.credits_posted;
-        T.acct_bal[slot] = b;
+        tb_bal_store(T.bal, slot, b);
         return;
     }
     slot = tb_account_claim(T, tb_lo(a.id), tb_hi(a.id), a.timestamp);
@@ -335,7 +335,7 @@ __global__ void tb_upsert_accounts(Tables T, const u8* recs, u32 n, u32* status,
         return;
     }
     tb_account_store_new(T, slot, a);
-    if (snap) snap[slot] = T.acct_bal[slot];  // loaded from the forest: written back already
+    if (snap.lo) tb_bal_store(snap, slot, tb_bal_load(T.bal, slot));  // loaded from the forest: written back already
     atomicAdd((unsigned long long*)&T.g->account_count, 1ULL);
 }
 
@@ -377,7 +377,7 @@ __global__ void tb_upsert_transfers(Tables T, const u8* recs, const u8* state, u
 //     local table by the replay: a leg whose owner is another rank goes there and the local copy is
 //     cancelled (adds are mod 2^128; free balances feed no check in a clean pass, so the transient
 //     local value is never read).
-// Leg on the wire: {account id lo, hi, amount lo, hi, field (BAL_OFF / 16)}.  The node engine
+// Leg on the wire: {account id lo, hi, amount lo, hi, field (BAL_DP .. BAL_CPOST)}.  The node engine
 // (os_of set) sends the account's slot on its owner instead of its id — {slot << 2 | field, amount lo,
 // hi} — so the owner adds without a probe: an owned account's slot is the home's own, an imported
 // one's is what the import read (tb_node_import's os_of).
@@ -436,8 +436,7 @@ __global__ __launch_bounds__(256) void tb_owner_legs(PassArgs P, OwnerLegArgs O)
                 }
             }
             if (dep) {  // cancel the replay's local add: the owner applies it
-                u8* bal = (u8*)&P.T.acct_bal[slot];
-                tb_atomic_add_u128(bal + 16 * (field0 + 2 * s), (u128)0 - t.amount);
+                tb_bal_add(P.T.bal, slot, field0 + 2 * s, (u128)0 - t.amount);
             }
         }
     }
@@ -483,7 +482,6 @@ __global__ __launch_bounds__(256) void tb_apply_owner_legs(Tables T, const u64* 
         atomicOr(status, 1u);
         return;
     }
-    u8* f = (u8*)&T.acct_bal[slot] + 16 * w[4];
-    if (cert64) tb_atomic_add_lo_noret(f, w[2]);
-    else tb_atomic_add_u128(f, tb_u128(w[2], w[3]));
+    if (cert64) tb_bal_add_lo(T.bal, slot, (u32)w[4], w[2]);
+    else tb_bal_add(T.bal, slot, (u32)w[4], tb_u128(w[2], w[3]));
 }

@@ -242,17 +242,27 @@ struct AccountCold {
 };
 static_assert(sizeof(AccountHot) == 32 && sizeof(AccountBal) == 64 && sizeof(AccountCold) == 32, "account split");
 
-#define BAL_OFF_DEBITS_PENDING 0
-#define BAL_OFF_DEBITS_POSTED 16
-#define BAL_OFF_CREDITS_PENDING 32
-#define BAL_OFF_CREDITS_POSTED 48
+// Balances in two planes (round 5): the low words of an account's four balances side by side, 32 B
+// per slot at lo[4 * slot + f], and their high words the same way in `hi`.  Every balance the engine
+// holds stays below 2^64 unless an event makes it larger, and the balance-leg write-back
+// (k_apply.h tb_apply_legs) adds low words only under the 64-bit certificate: it reads and writes the
+// low plane alone, four accounts to a 128-B line, and never touches a high word.  The two planes are
+// one allocation (hi = lo + 4 * account_cap), so a snapshot is one copy of it.
+#define BAL_DP 0     // debits_pending
+#define BAL_DPOST 1  // debits_posted
+#define BAL_CP 2     // credits_pending
+#define BAL_CPOST 3  // credits_posted
+struct BalView {
+    u64* lo;  // [4 * account_cap]
+    u64* hi;  // [4 * account_cap]
+};
 
 #define XI_TOMB (1ULL << 31)  // withdrawn (failed / dependent / rolled back)
 #define XI_POS_MASK 0x7FFFFFFFULL
 
 struct Tables {
     AccountHot* acct_hot;     // [account_cap]
-    AccountBal* acct_bal;     // [account_cap]
+    BalView bal;              // balances, by plane (above)
     AccountCold* acct_cold;   // [account_cap]
     u32* account_mark;        // [account_cap] pass epoch of the last balancing mark
     u64 account_mask;         // account_cap - 1
@@ -402,9 +412,38 @@ __device__ static inline void tb_account_tombstone(const Tables& T, u32 slot) {
     T.acct_hot[slot].id_hi = ~0ULL;
 }
 
+__device__ static inline AccountBal tb_bal_load(const BalView& V, u64 slot) {
+    const u64* l = V.lo + 4 * slot;
+    const u64* h = V.hi + 4 * slot;
+    AccountBal b;
+    b.debits_pending = tb_u128(l[0], h[0]);
+    b.debits_posted = tb_u128(l[1], h[1]);
+    b.credits_pending = tb_u128(l[2], h[2]);
+    b.credits_posted = tb_u128(l[3], h[3]);
+    return b;
+}
+
+__device__ static inline void tb_bal_store(const BalView& V, u64 slot, const AccountBal& b) {
+    u64* l = V.lo + 4 * slot;
+    u64* h = V.hi + 4 * slot;
+    l[0] = tb_lo(b.debits_pending);
+    l[1] = tb_lo(b.debits_posted);
+    l[2] = tb_lo(b.credits_pending);
+    l[3] = tb_lo(b.credits_posted);
+    h[0] = tb_hi(b.debits_pending);
+    h[1] = tb_hi(b.debits_posted);
+    h[2] = tb_hi(b.credits_pending);
+    h[3] = tb_hi(b.credits_posted);
+}
+
+// Balance f (BAL_*) of a slot as one u128.
+__device__ static inline u128 tb_bal_get(const BalView& V, u64 slot, u32 f) {
+    return tb_u128(V.lo[4 * slot + f], V.hi[4 * slot + f]);
+}
+
 __device__ static inline Account tb_account_load(const Tables& T, u32 slot) {
     const AccountHot h = T.acct_hot[slot];
-    const AccountBal b = T.acct_bal[slot];
+    const AccountBal b = tb_bal_load(T.bal, slot);
     const AccountCold c = T.acct_cold[slot];
     Account a;
     a.id = tb_u128(h.id_lo, h.id_hi);
@@ -436,7 +475,7 @@ __device__ static inline void tb_account_store_new(const Tables& T, u32 slot, co
     b.debits_posted = a.debits_posted;
     b.credits_pending = a.credits_pending;
     b.credits_posted = a.credits_posted;
-    T.acct_bal[slot] = b;
+    tb_bal_store(T.bal, slot, b);
     if (a.flags & AF_LIMITS) atomicAdd((unsigned long long*)&T.g->limit_accounts, 1ULL);
     AccountHot* h = &T.acct_hot[slot];
     h->ledger = a.ledger;
@@ -597,6 +636,22 @@ __device__ static inline void tb_atomic_add_u128(void* field, u128 v) {
 __device__ static inline void tb_atomic_add_lo_noret(void* field, u64 v) {
     __hip_atomic_fetch_add((unsigned long long*)field, (unsigned long long)v, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Exact u128 add to balance f of a slot (mod 2^128): the low word, then the carry into the high.
+__device__ static inline void tb_bal_add(const BalView& V, u64 slot, u32 f, u128 v) {
+    const u64 lo = tb_lo(v), hi = tb_hi(v);
+    u64 carry = 0;
+    if (lo != 0) {
+        const u64 old = atomicAdd((unsigned long long*)&V.lo[4 * slot + f], (unsigned long long)lo);
+        carry = (old + lo) < old ? 1 : 0;
+    }
+    if (hi + carry != 0) atomicAdd((unsigned long long*)&V.hi[4 * slot + f], (unsigned long long)(hi + carry));
+}
+
+// Low-word add to balance f of a slot (the certificate's no-carry case).
+__device__ static inline void tb_bal_add_lo(const BalView& V, u64 slot, u32 f, u64 v) {
+    tb_atomic_add_lo_noret(&V.lo[4 * slot + f], v);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -62,6 +62,10 @@ for what in "$@"; do
       timeout -k 10 600 python -u bench.py --gpus 2 --same-device --accounts 1000000 --transfers 4000000 --steps 2 \
         --warmup 1 --host-steps 1 --workload c3 > $O/node_c3.json 2> $O/node_c3.err
       rc=$?; echo "node c3 rc=$rc"; tail -c 2500 $O/node_c3.json; tail -5 $O/node_c3.err; [ $rc -ne 0 ] && exit $rc ;;
+    nodec3c)  # C3 on the node with 128-prepare blocks
+      timeout -k 10 600 python -u bench.py --gpus 2 --same-device --accounts 1000000 --transfers 4000000 --steps 2 \
+        --warmup 1 --host-steps 0 --workload c3 --chunk-prepares 128 > $O/node_c3_128.json 2> $O/node_c3_128.err
+      rc=$?; echo "node c3/128 rc=$rc"; grep -o '"headline": {[^}]*}' $O/node_c3_128.json; tail -3 $O/node_c3_128.err; [ $rc -ne 0 ] && exit $rc ;;
     nodec4)
       timeout -k 10 600 python -u bench.py --gpus 2 --same-device --accounts 1000000 --transfers 4000000 --steps 2 \
         --warmup 1 --host-steps 0 --workload c4 > $O/node_c4.json 2> $O/node_c4.err
