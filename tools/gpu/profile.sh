@@ -8,6 +8,8 @@
 #   bash tools/gpu/profile.sh dfetch|dwrite       -> FETCH_SIZE / WRITE_SIZE of device-resident C2 passes
 #     (tools/gpu/device_pass.py: 512-prepare passes, no host copy in flight)
 #   bash tools/gpu/profile.sh dkt                 -> kernel trace + stats of the same run
+#   bash tools/gpu/profile.sh hkt|hfetch|hwrite   -> the same for the host path (tools/gpu/host_pass.py:
+#     pipelined 64-prepare chunks from registered host memory)
 #   bash tools/gpu/profile.sh mc                  -> memory-copy + kernel trace of one headline step
 #     (the copy engine's timeline: body copies, their gaps, the per-chunk metadata copies)
 #   bash tools/gpu/profile.sh nkt|nc3             -> kernel trace of the node rehearsal (2 logical shards, C2 / C3)
@@ -45,6 +47,11 @@ case $MODE in
       timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/nc3" -o run -- python3 "$R/bench.py" \
         --gpus 2 --same-device --workload c3 --accounts 1000000 --transfers 4000000 --steps 1 --warmup 1 $LEG --access-mix 0 \
         > "$OUT/bench_nc3.log" 2>&1; rc=$? ;;
+  hfetch|hwrite) C=FETCH_SIZE; [ "$MODE" = hwrite ] && C=WRITE_SIZE
+      timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/$MODE" -o run -- python3 "$R/tools/gpu/host_pass.py" \
+        > "$OUT/$MODE.log" 2>&1; rc=$? ;;
+  hkt) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/hkt" -o run -- \
+        python3 "$R/tools/gpu/host_pass.py" > "$OUT/hkt.log" 2>&1; rc=$? ;;
   n1kt) export GPU_MAX_HW_QUEUES=8  # one C2 prepare per tbgpu_commit on a 2-shard node (and a single engine)
       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$OUT/n1kt" -o run -- \
         python3 "$R/tools/gpu/node_one_prepare.py" 120 2 > "$OUT/n1kt.log" 2>&1; rc=$? ;;

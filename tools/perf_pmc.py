@@ -1,5 +1,5 @@
 """Build perf/pmc_<round>.json — the rocprofv3 evidence bench.py's roofline reads (`traffic`,
-`rocprof_avg_launch_ms`) — from the kernel-trace and PMC runs of tools/gpu/r04_prof.sh.
+`rocprof_avg_launch_ms`) — from the kernel-trace and PMC runs of tools/gpu/r0N_prof.sh.
 
 Two legs, each from three runs of one command (kernel trace + stats; FETCH_SIZE alone; WRITE_SIZE
 alone — they do not fit in one pass on gfx950, MI355X_MICROARCH.md §HBM):
@@ -73,8 +73,8 @@ def leg(stats_csv, fetch_csv, write_csv, counter_transfers, launch_transfers):
 def main(argv):
     out, rnd = argv[0], argv[1]
     res = {"round": rnd,
-           "source": "tools/gpu/r04_prof.sh (rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE; --pmc WRITE_SIZE) "
-                     "summarised by tools/perf_pmc.py",
+           "source": "tools/gpu/%s_prof.sh (rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE; --pmc WRITE_SIZE) "
+                     "summarised by tools/perf_pmc.py" % rnd,
            "note": "bytes per committed transfer; raw = FETCH_SIZE + WRITE_SIZE; fetch_x2 doubles FETCH_SIZE "
                    "(gfx950 FETCH_SIZE counts half of a wide coalesced read)",
            "legs": {}}
