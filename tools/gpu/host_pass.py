@@ -34,7 +34,7 @@ e.free(ev)
 e.register_host(host)
 x_lens = batches(n_xfer, batch)
 x_ts, _ = timestamps(x_lens, t + 10)
-out_lens, _ = e.commit_pipelined(129, x_ts, x_lens, host, chunk_batches=chunk)
+out_lens, _, _ = e.commit_pipelined(129, x_ts, x_lens, host, chunk_batches=chunk)
 e.unregister_host(host)
 print("host passes of %d prepares: %d transfers, reply bytes %d" % (chunk, n_xfer, int(np.asarray(out_lens).sum())))
 e.close()

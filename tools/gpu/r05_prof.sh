@@ -8,7 +8,7 @@ R=${GRAFT_REPO_ROOT:-$PWD}
 cd "$R" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof
-for m in dkt dfetch dwrite hkt hfetch hwrite; do
+for m in ${MODES:-dkt dfetch dwrite hkt hfetch hwrite}; do
   bash "$R/tools/gpu/profile.sh" $m || { echo "profile $m failed"; exit 1; }
 done
 P=gpurun_out/prof
