@@ -44,6 +44,9 @@ for what in "$@"; do
       timeout -k 10 600 python -u bench.py --steps 2 --warmup 1 --secondary 0 --replica-prepares 0 --host-prepares 0 \
         --write-back 0 --cpu-sample 2000000 > $O/bench.json 2> $O/bench.err
       rc=$?; echo "bench rc=$rc"; tail -c 1500 $O/bench.json; tail -5 $O/bench.err; [ $rc -ne 0 ] && exit $rc ;;
+    driver)  # the driver's own command line
+      timeout -k 10 900 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err
+      rc=$?; echo "bench rc=$rc"; tail -c 1200 $O/bench_driver.json; tail -5 $O/bench_driver.err; [ $rc -ne 0 ] && exit $rc ;;
     benchfull)
       timeout -k 10 900 python -u bench.py > $O/bench_full.json 2> $O/bench_full.err
       rc=$?; echo "bench rc=$rc"; tail -c 1500 $O/bench_full.json; tail -5 $O/bench_full.err; [ $rc -ne 0 ] && exit $rc ;;
