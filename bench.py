@@ -226,12 +226,15 @@ def run_replica_path(args, device):
     """The replica's call path from C++ (tigerbeetle_amd/host/replica_bench.cpp, the tb::StateMachine
     mirror): per op, prepare -> prefetch (the body's DMA from the registered message pool starts)
     -> commit -> compact, serially, one C2 prepare of 8190 transfers each (src/vsr/replica.zig:
-    3045-3102); without and with the per-bar groove write-back in compact."""
+    3045-3102); without and with the groove write-back in compact: one bar behind (asynchronous), at each
+    bar's last op (synchronous, round 4's Zig wrapper) and one op behind with every bar complete at its
+    last op (the Zig wrapper's shape since round 5)."""
     import subprocess
     exe = os.path.join(ROOT, "tigerbeetle_amd", "host", "tb_replica_bench")
     out = {}
     for name, opts in (("in_memory", []), ("in_memory_staged", ["--stage"]), ("with_write_back", ["--write-back"]),
-                       ("with_write_back_sync", ["--write-back-sync"])):
+                       ("with_write_back_sync", ["--write-back-sync"]),
+                       ("with_write_back_per_op", ["--write-back-per-op"])):
         cmd = [exe, "--accounts", str(args.accounts), "--prepares", str(args.replica_prepares),
                "--device", str(device)] + opts
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)

@@ -7,9 +7,12 @@
 // commit waits for it).  With --write-back, compact hands each bar's changes to a sink (the durable
 // replica's forest; here the sink touches nothing).
 //
-// Usage: tb_replica_bench [--accounts N] [--prepares N] [--warmup N] [--write-back | --write-back-sync] [--stage]
+// Usage: tb_replica_bench [--accounts N] [--prepares N] [--warmup N] [--write-back | --write-back-sync |
+//                         --write-back-per-op] [--stage]
 //                         [--device D]
-// (--write-back-sync: compact writes each bar back synchronously, as zig/state_machine_gpu.zig does.)
+// (--write-back-sync: compact writes each bar back synchronously, as zig/state_machine_gpu.zig did in
+// round 4; --write-back-per-op: one op behind, each bar complete at its last op — the Zig wrapper's
+// shape since round 5.)
 // (--stage: prefetch stages the body by DMA; default: commit reads it straight from the message.)
 // Prints one JSON line: per-op latency (host clock around prefetch+commit+compact) and throughput.
 #include <algorithm>
@@ -45,7 +48,7 @@ double pick(const std::vector<double>& sorted, int p) {
 int main(int argc, char** argv) {
     uint64_t accounts = 1000000, prepares = 2000, warmup = 64;
     int device = 0;
-    bool write_back = false, stage = false, sync_wb = false;
+    bool write_back = false, stage = false, sync_wb = false, per_op_wb = false;
     for (int i = 1; i < argc; i++) {
         const std::string a = argv[i];
         auto next = [&]() { return i + 1 < argc ? strtoull(argv[++i], nullptr, 10) : 0ULL; };
@@ -55,6 +58,7 @@ int main(int argc, char** argv) {
         else if (a == "--device") device = (int)next();
         else if (a == "--write-back") write_back = true;
         else if (a == "--write-back-sync") write_back = sync_wb = true;
+        else if (a == "--write-back-per-op") write_back = per_op_wb = true;
         else if (a == "--no-stage") stage = false;
         else if (a == "--stage") stage = true;
     }
@@ -70,6 +74,7 @@ int main(int argc, char** argv) {
     tb::StateMachine sm(o);
     sm.stage_bodies = stage;
     sm.compact_sync = sync_wb;
+    sm.compact_per_op = per_op_wb;
     tbgpu_t* E = sm.engine();
 
     // Workload: the engine's generator (C2 shapes, tbgpu_bench.h), copied to host memory.
@@ -160,11 +165,11 @@ int main(int argc, char** argv) {
     std::vector<double> sorted(lat);
     std::sort(sorted.begin(), sorted.end());
     printf("{\"call_path\": \"prepare -> prefetch -> commit -> compact per op (tb::StateMachine, C++)\", "
-           "\"ops\": %llu, \"events_per_op\": %u, \"write_back\": %s, \"write_back_sync\": %s, \"prefetch_stages_body\": %s, \"transfers_per_s\": %.1f, "
+           "\"ops\": %llu, \"events_per_op\": %u, \"write_back\": %s, \"write_back_sync\": %s, \"write_back_per_op\": %s, \"prefetch_stages_body\": %s, \"transfers_per_s\": %.1f, "
            "\"ms_per_op\": %.4f, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"p100_ms\": %.4f, \"failed_events\": %llu, "
            "\"written_back_objects\": %llu, \"compact_ms_per_op\": %.4f, \"compact_ms_max\": %.4f}\n",
            (unsigned long long)prepares, batch, write_back ? "true" : "false", sync_wb ? "true" : "false",
-           stage ? "true" : "false",
+           per_op_wb ? "true" : "false", stage ? "true" : "false",
            prepares * batch / (total_ms / 1e3),
            total_ms / prepares, pick(sorted, 50), pick(sorted, 99), pick(sorted, 100), (unsigned long long)failed,
            (unsigned long long)wb_objects, compact_ms / prepares, compact_max);

@@ -151,7 +151,17 @@ std::vector<size_t> StateMachine::commit_many(Operation operation, const std::ve
 
 void StateMachine::compact(const Callback& callback, uint64_t op) {
     // The HBM tables need no compaction; the durable copy gets each bar's changes, one bar behind.
-    if (write_back && lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0 && compact_sync) {
+    if (write_back && lsm_batch_multiple && compact_per_op) {
+        wb_deliver_inflight();  // the previous op's objects: landed while this op committed
+        reserve_write_back();
+        WbSet& w = wb_[wb_bar_];
+        check(tbgpu_checkpoint_delta_async(engine_, w.accounts.data(), w.before.data(), w.caps[0], w.transfers.data(),
+                                           w.caps[1], (uint64_t*)w.posted.data(), w.caps[2]),
+              "checkpoint_delta_async");
+        wb_inflight_ = wb_bar_;
+        wb_bar_ ^= 1;
+        if ((op + 1) % lsm_batch_multiple == 0) wb_deliver_inflight();  // the bar ends with its own objects
+    } else if (write_back && lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0 && compact_sync) {
         write_back(checkpoint_delta());  // the Zig wrapper's shape: the bar's objects before compact returns
     } else if (write_back && lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0) {
         wb_deliver_inflight();  // the previous bar's objects: landed while this bar committed
