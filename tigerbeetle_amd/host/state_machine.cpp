@@ -151,8 +151,11 @@ std::vector<size_t> StateMachine::commit_many(Operation operation, const std::ve
 
 void StateMachine::compact(const Callback& callback, uint64_t op) {
     // The HBM tables need no compaction; the durable copy gets each bar's changes, one bar behind.
-    if (write_back && lsm_batch_multiple && compact_per_op) {
-        wb_deliver_inflight();  // the previous op's objects: landed while this op committed
+    const bool bar_end = lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0;
+    if (write_back && lsm_batch_multiple && compact_per_op && !bar_end && (op + 1) % std::max<uint32_t>(1, compact_every)) {
+        // inside a chunk: nothing to do
+    } else if (write_back && lsm_batch_multiple && compact_per_op) {
+        wb_deliver_inflight();  // the previous chunk's objects: landed while this one committed
         reserve_write_back();
         WbSet& w = wb_[wb_bar_];
         check(tbgpu_checkpoint_delta_async(engine_, w.accounts.data(), w.before.data(), w.caps[0], w.transfers.data(),
@@ -160,7 +163,7 @@ void StateMachine::compact(const Callback& callback, uint64_t op) {
               "checkpoint_delta_async");
         wb_inflight_ = wb_bar_;
         wb_bar_ ^= 1;
-        if ((op + 1) % lsm_batch_multiple == 0) wb_deliver_inflight();  // the bar ends with its own objects
+        if (bar_end) wb_deliver_inflight();  // the bar ends with its own objects
     } else if (write_back && lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0 && compact_sync) {
         write_back(checkpoint_delta());  // the Zig wrapper's shape: the bar's objects before compact returns
     } else if (write_back && lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0) {

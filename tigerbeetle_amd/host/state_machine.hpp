@@ -189,13 +189,16 @@ public:
     // compact's write-back synchronous instead (tbgpu_checkpoint_delta at the bar's last op, its
     // objects handed over before compact calls back): the shape zig/state_machine_gpu.zig runs.
     bool compact_sync = false;
-    // compact's write-back one OP behind instead of one bar: every op starts the capture of its own
+    // compact's write-back one OP (or chunk of ops) behind instead of one bar: every op starts the capture of its own
     // changes (tbgpu_checkpoint_delta_async) and hands the previous op's to write_back (they crossed
     // PCIe while this op committed); the last op of a bar waits for its own, so every bar's objects
     // reach the forest before compact calls back — each bar's table_mutable holds exactly that bar
     // (the groove's value_count_max, src/state_machine.zig:100-178), and nothing blocks for a bar.
     // The shape zig/state_machine_gpu.zig runs.
     bool compact_per_op = false;
+    // With compact_per_op: capture every this many ops (a chunk of the bar) instead of every op; the
+    // bar's last op still waits for its own chunk.
+    uint32_t compact_every = 1;
     // The replica's message pool (MessagePool.init_capacity, src/message_pool.zig:98-120): buffers
     // registered once, so prefetch stages a prepare body from its message by DMA.
     void register_message_buffer(void* buffer, size_t bytes);
