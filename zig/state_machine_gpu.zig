@@ -134,6 +134,13 @@ pub fn StateMachineType(
         /// The engine holds every object the forest holds (a freshly formatted cluster).  False
         /// after open() finds objects in the forest, for the rest of the process.
         engine_complete: bool = true,
+        /// Transfers the engine evicted (tbgpu_evict_transfers: written back, dropped when the
+        /// transfer log fills).  Non-zero: a create_transfers / lookup_transfers prefetch asks the
+        /// engine which of its ids may be cold and takes the forest path when any is.
+        engine_evicted: u64 = 0,
+        /// A node engine (engine_devices >= 2): its shards do not evict (tbgpu.h), so its transfer
+        /// log bounds the ledger it holds.
+        engine_node: bool,
 
         prefetch_input: ?[]align(16) const u8 = null,
         prefetch_operation: Operation = undefined,
@@ -158,6 +165,8 @@ pub fn StateMachineType(
         load_accounts: []Account,
         load_transfers: []Transfer,
         load_posted: []u8,
+        cold_ids: [][2]u64,
+        cold_flags: []u8,
 
         pub fn init(allocator: mem.Allocator, grid: *Grid, options: Options) !StateMachine {
             var forest = try Forest.init(allocator, grid, options.lsm_forest_node_count, forest_options(options));
@@ -192,6 +201,10 @@ pub fn StateMachineType(
             errdefer allocator.free(load_transfers);
             const load_posted = try allocator.alloc(u8, prepare_transfers_max);
             errdefer allocator.free(load_posted);
+            const cold_ids = try allocator.alloc([2]u64, prepare_transfers_max);
+            errdefer allocator.free(cold_ids);
+            const cold_flags = try allocator.alloc(u8, prepare_transfers_max);
+            errdefer allocator.free(cold_flags);
             var registered_messages: std.AutoHashMapUnmanaged(usize, void) = .{};
             try registered_messages.ensureTotalCapacity(allocator, messages_max_replica);
             errdefer registered_messages.deinit(allocator);
@@ -216,6 +229,9 @@ pub fn StateMachineType(
                 .load_accounts = load_accounts,
                 .load_transfers = load_transfers,
                 .load_posted = load_posted,
+                .cold_ids = cold_ids,
+                .cold_flags = cold_flags,
+                .engine_node = options.engine_devices.len >= 2,
                 .engine_stage_bodies = options.engine_stage_bodies,
                 .engine_register_messages = options.engine_register_messages,
                 .registered_messages = registered_messages,
@@ -229,6 +245,8 @@ pub fn StateMachineType(
             inline for (.{ self.writeback_accounts, self.writeback_accounts_before, self.writeback_transfers, self.writeback_posted }) |buffer| {
                 check(tbgpu.tbgpu_unregister_host(self.engine, mem.sliceAsBytes(buffer).ptr));
             }
+            allocator.free(self.cold_flags);
+            allocator.free(self.cold_ids);
             allocator.free(self.load_posted);
             allocator.free(self.load_transfers);
             allocator.free(self.load_accounts);
@@ -247,6 +265,7 @@ pub fn StateMachineType(
             self.commit_timestamp = 0;
             self.engine_commit_timestamp = 0;
             self.engine_complete = true;
+            self.engine_evicted = 0;
             self.prefetch_input = null;
             self.prefetch_callback = null;
             self.open_callback = null;
@@ -302,7 +321,7 @@ pub fn StateMachineType(
             _ = op;
             assert(self.prefetch_input == null);
             assert(self.prefetch_callback == null);
-            if (self.engine_complete) {
+            if (self.engine_complete and !self.transfers_cold(operation, input)) {
                 if (self.engine_stage_bodies and (operation == .create_accounts or operation == .create_transfers)) {
                     self.register_message(input);
                     check(tbgpu.tbgpu_prefetch(self.engine, @intFromEnum(operation), input.ptr, @intCast(input.len)));
@@ -345,6 +364,34 @@ pub fn StateMachineType(
                     self.forest.grooves.transfers.prefetch(prefetch_transfers_done, &self.prefetch_context.transfers);
                 },
             }
+        }
+
+        /// After an eviction: does the prepare name a transfer the engine may have dropped (its ids,
+        /// a post / void's pending id; lookup_transfers' ids)?  Then the groove prefetch below runs
+        /// and loads what the forest holds and the engine lacks (tbgpu_load_transfers), as after a
+        /// restart.  A false positive (Bloom filter) only costs that prefetch.
+        fn transfers_cold(self: *StateMachine, operation: Operation, input: []align(16) const u8) bool {
+            if (self.engine_evicted == 0) return false;
+            var n: u32 = 0;
+            switch (operation) {
+                .create_transfers => for (mem.bytesAsSlice(Transfer, input)) |*t| {
+                    self.cold_ids[n] = .{ @truncate(t.id), @truncate(t.id >> 64) };
+                    n += 1;
+                    if (t.flags.post_pending_transfer or t.flags.void_pending_transfer) {
+                        self.cold_ids[n] = .{ @truncate(t.pending_id), @truncate(t.pending_id >> 64) };
+                        n += 1;
+                    }
+                },
+                .lookup_transfers => for (mem.bytesAsSlice(u128, input)) |id| {
+                    self.cold_ids[n] = .{ @truncate(id), @truncate(id >> 64) };
+                    n += 1;
+                },
+                else => return false,
+            }
+            if (n == 0) return false;
+            check(tbgpu.tbgpu_transfers_maybe_cold(self.engine, @ptrCast(self.cold_ids.ptr), n, self.cold_flags.ptr));
+            for (self.cold_flags[0..n]) |c| if (c != 0) return true;
+            return false;
         }
 
         fn parent_of(comptime field: std.meta.FieldEnum(PrefetchContext), completion: anytype) *StateMachine {
@@ -542,6 +589,7 @@ pub fn StateMachineType(
             // larger counts would mean the engine changed more objects than a bar's commits can
             // (an invariant failure, like the reference's TableMemory.put assert), so it panics.
             check(status);
+            defer self.evict_if_full();
             const grooves = &self.forest.grooves;
             for (self.writeback_accounts[0..counts.accounts], self.writeback_accounts_before[0..counts.accounts]) |*a, before| {
                 if (a.timestamp > counts.created_after) {
@@ -568,6 +616,19 @@ pub fn StateMachineType(
                     .padding = [_]u8{0} ** 7,
                 });
             }
+        }
+
+        /// Bounded residency: once the bar is in the grooves, a transfer log three-quarters full
+        /// drops what the forest now holds, keeping the newest quarter (tbgpu_evict_transfers);
+        /// a later prefetch that names a dropped transfer loads it back (transfers_cold).
+        fn evict_if_full(self: *StateMachine) void {
+            if (self.engine_node) return;
+            var stats: tbgpu.tbgpu_stats = undefined;
+            check(tbgpu.tbgpu_get_stats(self.engine, &stats));
+            if (stats.log_capacity == 0 or stats.log_used * 4 < stats.log_capacity * 3) return;
+            var evicted: u64 = 0;
+            check(tbgpu.tbgpu_evict_transfers(self.engine, stats.log_capacity / 4, &evicted));
+            self.engine_evicted += evicted;
         }
 
         pub fn checkpoint(self: *StateMachine, callback: *const fn (*StateMachine) void) void {
