@@ -632,6 +632,16 @@ struct WalkRec {
 #define WALK_REFRESH 0  // 1: a heavy walker re-reads a window's open partner statuses before walking it (C3h: no gain, stops -5 %)
 #endif
 
+#ifndef WALK_PROF
+#define WALK_PROF 0  // A/B builds only: time the critical heavy walker's window setups and ends
+#endif
+#ifndef WALK_DEEP
+#define WALK_DEEP 0  // 1: a heavy walker loads statuses two windows ahead (records three)
+#endif
+#ifndef WALK_PEND_NOW
+#define WALK_PEND_NOW 1  // 0: a heavy walker polls an open Y leg's status before taking it as pending
+#endif
+
 #define WALK_BIG (1LL << 62)  // a position whose outcome is known: "always" (+) / "never" (−)
 
 __device__ static inline u32 fl_combine(u32 vd, u32 vc) {  // the unit's status from its two checks
@@ -701,7 +711,7 @@ __device__ static inline void fl_walk_status(const FlowArgs& F, const WalkRec& r
 }
 
 struct WalkStats {
-    u64 windows = 0, stops = 0, blocks = 0, loop_ticks = 0, block_ticks = 0;
+    u64 windows = 0, stops = 0, blocks = 0, loop_ticks = 0, block_ticks = 0, prof_ticks = 0;
 };
 
 // One step of the 32-bit chain on the scalar unit: t = v + dc; if t >= 0 { dc += e; okm |= bit }.
@@ -808,6 +818,9 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
             dl = oth == BV_FAIL ? 0 : -r.a;  // the other side failed: no delta here either way
         }
     };
+#if WALK_PROF
+    const u64 tp0 = wait ? fl_now() : 0;
+#endif
     classify();
     u64 smask = __ballot(simple);
     const u64 vmask = n == 64 ? ~0ULL : ((1ULL << n) - 1);
@@ -859,6 +872,9 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         }
         ws.block_ticks += fl_now() - w0;
     };
+#if WALK_PROF
+    if (wait) ws.loop_ticks += fl_now() - tp0;  // A/B builds: the window's setup
+#endif
     while (j < n) {
         const u64 bar = ~smask & vmask & (~0ULL << j);
         const u32 b = bar ? (u32)__builtin_ctzll(bar) : n;
@@ -907,14 +923,25 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         // loaded a window ahead; a partner walker has usually decided them since): each one decided
         // by now walks as a simple position instead of stopping the walk again.
         ws.stops++;
+        const u32 bu = __builtin_amdgcn_readlane(r.u, b), bk = __builtin_amdgcn_readlane(r.kind, b);
+        const i64 ba = (i64)fl_rl64((u64)r.a, b);
+#if WALK_PEND_NOW
+        if (wait && !(bk & BT_X)) {
+            // A waiting walker takes an open Y leg as pending at once, without polling its status: the
+            // pending statuses are read together, in one round trip, when a check needs them and at
+            // the window's end (a poll per stop was the heavy walker's main cost).
+            pmask |= 1ULL << b;
+            dp += ba;
+            j = b + 1;
+            continue;
+        }
+#endif
         const bool refresh = valid && lane > b && !simple;
         if (refresh) {
             st = fl_ld32(&F.b_st[r.u]);
             if (isx) vw = fl_ld32(&F.b_vw[r.u]);
         }
-        const u32 bu = __builtin_amdgcn_readlane(r.u, b), bk = __builtin_amdgcn_readlane(r.kind, b);
         if ((bk & BT_X) && pmask) wait_until([&]() { return !pmask; });  // a paired check needs the exact d
-        const i64 ba = (i64)fl_rl64((u64)r.a, b);
         const i64 bb = (i64)fl_rl64((u64)r.base, b);
         // The unit's status now: a paired check ORs this side's verdict in first (whoever completes
         // the pair publishes; a partner that walked its side as a plain check publishes the status,
@@ -976,6 +1003,9 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         if (fin == BS_OK) d += (bk & BT_X) ? -ba : ba;
         j = b + 1;
     }
+#if WALK_PROF
+    const u64 tp2 = wait ? fl_now() : 0;
+#endif
     if (pmask) wait_until([&]() { return !pmask; });  // the window leaves with an exact d
     ws.windows++;
     // Publish the checks walked in the scalar loop, once per window: a status poll issued after a
@@ -985,6 +1015,9 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         const u32 mine = (okm >> lane) & 1 ? BV_PASS : BV_FAIL;
         fl_st32(&F.b_st[r.u], cr ? fl_combine(oth, mine) : fl_combine(mine, oth));
     }
+#if WALK_PROF
+    if (wait) ws.prof_ticks += fl_now() - tp2;  // A/B builds: the window's end (its last wait included)
+#endif
     return m;
 }
 
@@ -1029,12 +1062,26 @@ __device__ static inline bool fl_walk_heavy(const FlowArgs& F, Globals* g, const
     if (64 + lane < n_seg) r1 = R[s0 + 64 + lane];
     u32 st0, vw0;
     fl_walk_status(F, r0, lane < n_seg, st0, vw0);
+#if WALK_DEEP
+    // Statuses two windows ahead, records three.
+    WalkRec r2 = {};
+    if (128 + lane < n_seg) r2 = R[s0 + 128 + lane];
+    u32 st1, vw1;
+    fl_walk_status(F, r1, 64 + lane < n_seg, st1, vw1);
+#endif
     for (u32 c = 0; c < n_seg; c += 64) {
         const u32 n = min(64u, n_seg - c);
+#if WALK_DEEP
+        WalkRec r3 = {};
+        if (c + 192 + lane < n_seg) r3 = R[s0 + c + 192 + lane];
+        u32 st2, vw2;
+        fl_walk_status(F, r2, c + 128 + lane < n_seg, st2, vw2);
+#else
         WalkRec r2 = {};
         if (c + 128 + lane < n_seg) r2 = R[s0 + c + 128 + lane];
         u32 st1, vw1;
         fl_walk_status(F, r1, c + 64 + lane < n_seg, st1, vw1);
+#endif
 #if WALK_REFRESH
         {   // The window's still-open partner statuses, read again right before it is walked (they were
             // read a window ago; a partner walker has often decided them since): one round trip here
@@ -1079,6 +1126,11 @@ __device__ static inline bool fl_walk_heavy(const FlowArgs& F, Globals* g, const
         r1 = r2;
         st0 = st1;
         vw0 = vw1;
+#if WALK_DEEP
+        r2 = r3;
+        st1 = st2;
+        vw1 = vw2;
+#endif
     }
     return true;
 }
@@ -1469,8 +1521,13 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
                 atomicAdd((unsigned long long*)&g->walk[2], (unsigned long long)len);
                 if (len == *(volatile u32*)&F.words[FW_WMAX]) {  // the critical walker: the longest segment
                     atomicAdd((unsigned long long*)&g->walk[8], (unsigned long long)ws.windows);
+#if WALK_PROF  // A/B builds: crit "blocks" = window-end ticks, "wait" = window-setup ticks
+                    atomicAdd((unsigned long long*)&g->walk[9], (unsigned long long)ws.prof_ticks);
+                    atomicAdd((unsigned long long*)&g->walk[10], (unsigned long long)ws.loop_ticks);
+#else
                     atomicAdd((unsigned long long*)&g->walk[9], (unsigned long long)ws.blocks);
                     atomicAdd((unsigned long long*)&g->walk[10], (unsigned long long)ws.block_ticks);
+#endif
                     atomicAdd((unsigned long long*)&g->walk[11], (unsigned long long)(fl_now() - w0));
                 }
             }
