@@ -632,6 +632,18 @@ struct WalkRec {
 #define WALK_REFRESH 0  // 1: a heavy walker re-reads a window's open partner statuses before walking it (C3h: no gain, stops -5 %)
 #endif
 
+#ifndef WALK_LIGHT_SLEEP
+#define WALK_LIGHT_SLEEP 2  // s_sleep of a light wave whose segments all stood still
+#endif
+#ifndef WALK_PRIO
+#define WALK_PRIO 0  // 1: a heavy walker's wave runs at the highest issue priority (s_setprio 3)
+#endif
+#ifndef WALK_PAR
+#define WALK_PAR 1  // 0: the 32-bit chain as a scalar step per lane
+#endif
+#ifndef WALK_CNT
+#define WALK_CNT 0  // A/B builds only: count the critical walker's positions by path (walk_dbg)
+#endif
 #ifndef WALK_PROF
 #define WALK_PROF 0  // A/B builds only: time the critical heavy walker's window setups and ends
 #endif
@@ -712,6 +724,9 @@ __device__ static inline void fl_walk_status(const FlowArgs& F, const WalkRec& r
 
 struct WalkStats {
     u64 windows = 0, stops = 0, blocks = 0, loop_ticks = 0, block_ticks = 0, prof_ticks = 0;
+#if WALK_CNT
+    u64 cnt[4] = {};  // A/B builds: the critical walker's positions by path (walk_dbg)
+#endif
 };
 
 // One step of the 32-bit chain on the scalar unit: t = v + dc; if t >= 0 { dc += e; okm |= bit }.
@@ -733,12 +748,80 @@ __device__ static inline void fl_step32(int v, int e, u64 bit, int& dc, u64& okm
 // The 32-bit chain over lanes [j, e) of one account: lane i is ok iff v32 + dc >= 0, and an ok lane
 // adds d32 to dc; okm collects the outcomes.  Four lanes a step: their inputs read ahead of the
 // chain (a readlane's result reaches the scalar unit late), then the chain itself.
+// Inclusive prefix sum over the wave's 64 lanes: within each row of 16 lanes by DPP row shifts
+// (a lane whose source is outside its row adds 0), then the rows' totals carried on.
+__device__ static inline int fl_scan32(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);  // row_shr:8
+    const int r0 = __builtin_amdgcn_readlane(x, 15), r1 = __builtin_amdgcn_readlane(x, 31);
+    const int r2 = __builtin_amdgcn_readlane(x, 47);
+    const u32 row = (threadIdx.x & 63) >> 4;
+    return x + (row >= 1 ? r0 : 0) + (row >= 2 ? r1 : 0) + (row >= 3 ? r2 : 0);
+}
+
+// The in-order walk of lanes [j, e) (lane i ok iff v32 + dc >= 0; an ok lane adds d32 to dc) in
+// parallel, by RUNS.  With P the prefix sum of the lanes' deltas (one scan) and w = v32 + P, a run of
+// ok lanes from s on base dc fails first at the first lane k >= s with w < P(s) - dc; a run of failed
+// lanes from k (their deltas left out, so dc stays) ends at the first lane with v32 + dc >= 0.  So
+// the walk costs a scan and a ballot per run, not a scalar step per lane (a lone wave issues one
+// instruction per four cycles: the scalar chain cost the critical walker ~50 ns a position).
+// p32 > 0 (pending credits): a lane that fails without them but passes with them stops the walk;
+// returns where (e: none).  Every sum stays below 2^31 in magnitude: |v32| <= 2^30, and dc plus
+// any partial sum of one window's deltas (each below 2^24) is below 2^30.
+__device__ static inline u64 fl_from(u32 s) { return s >= 64 ? 0 : ~0ULL << s; }
+__device__ static inline u32 fl_runs32(int v32, int d32, u32 j, u32 e, int& dc, u64& okm, int p32) {
+    const u32 lane = threadIdx.x & 63;
+    const bool in = lane >= j && lane < e;
+    const int x = in ? d32 : 0;
+    const int S = fl_scan32(x);
+    const int P = S - x;  // the deltas of [j, lane)
+    const int w = v32 + P;
+    const u64 inm = __ballot(in);
+    int B = __builtin_amdgcn_readfirstlane(dc);
+    u32 s = j;
+    int Ps = 0;
+    for (;;) {
+        const int c = Ps - B;  // lane k >= s of the ok run fails iff v32 + B + P(k) - P(s) < 0
+        const u64 bad = __ballot(w < c) & inm & fl_from(s);
+        if (!bad) {
+            okm |= inm & fl_from(s);
+            dc = B + (e > j ? __builtin_amdgcn_readlane(S, e - 1) : 0) - Ps;
+            return e;
+        }
+        const u32 k = (u32)__builtin_ctzll(bad);
+        okm |= inm & fl_from(s) & ~fl_from(k);
+        B += __builtin_amdgcn_readlane(P, k) - Ps;
+        if (p32 && __builtin_amdgcn_readlane(w, k) + p32 >= c) {  // the pending credits could flip it
+            dc = B;
+            return k;
+        }
+        const u64 nxt = __ballot(v32 + B + p32 >= 0) & inm & fl_from(k + 1);  // the failed run's end
+        if (!nxt) {
+            dc = B;
+            return e;
+        }
+        const u32 q = (u32)__builtin_ctzll(nxt);
+        if (p32 && __builtin_amdgcn_readlane(v32, q) + B < 0) {  // passes only with the pending credits
+            dc = B;
+            return q;
+        }
+        s = q;
+        Ps = __builtin_amdgcn_readlane(P, q);
+    }
+}
+
 __device__ static inline void fl_chain32(int v32, int d32, u32 j, u32 e, int& dc, u64& okm) {
     // Wave-uniform by construction; said so, or the compiler may keep them in vector registers.
     j = __builtin_amdgcn_readfirstlane(j);
     e = __builtin_amdgcn_readfirstlane(e);
     dc = __builtin_amdgcn_readfirstlane(dc);
     okm = fl_rl64(okm, 0);
+#if WALK_PAR
+    (void)fl_runs32(v32, d32, j, e, dc, okm, 0);
+    return;
+#endif
     for (; j + 4 <= e; j += 4) {
         const int v0 = __builtin_amdgcn_readlane(v32, j), v1 = __builtin_amdgcn_readlane(v32, j + 1);
         const int v2 = __builtin_amdgcn_readlane(v32, j + 2), v3 = __builtin_amdgcn_readlane(v32, j + 3);
@@ -760,7 +843,7 @@ __device__ static inline void fl_chain32(int v32, int d32, u32 j, u32 e, int& dc
 // v + d >= 0, and an ok lane adds dl to d; okm collects the outcomes.  When every |dl| of the run is
 // below 2^24 the run is walked in 32 bits, relative to d at its start (|sum of dl| < 2^30): each v + d0
 // is clamped to +-2^30, which keeps its sign against any partial sum, so every outcome is the same.
-__device__ static inline void fl_walk_run(i64 v, i64 dl, u32 j, u32 e, i64& d, u64& okm) {
+__device__ static inline bool fl_walk_run(i64 v, i64 dl, u32 j, u32 e, i64& d, u64& okm) {
     const u32 lane = threadIdx.x & 63;
     const bool in = lane >= j && lane < e;
     if (!__ballot(in && (dl >= (1LL << 24) || dl <= -(1LL << 24)))) {
@@ -770,7 +853,7 @@ __device__ static inline void fl_walk_run(i64 v, i64 dl, u32 j, u32 e, i64& d, u
         int dd = 0;
         fl_chain32(v32, d32, j, e, dd, okm);
         d += dd;
-        return;
+        return true;
     }
     for (; j < e; j++) {
         const u64 vj = fl_rl64((u64)v, j), dj = fl_rl64((u64)dl, j);
@@ -779,6 +862,7 @@ __device__ static inline void fl_walk_run(i64 v, i64 dl, u32 j, u32 e, i64& d, u
         d = (i64)((u64)d + (ok ? dj : 0));
         okm |= ok ? 1ULL << j : 0;
     }
+    return false;
 }
 
 // Resolves one window of n <= 64 positions (lane j: position j) in order from the running sum d
@@ -845,14 +929,14 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         const bool known = ((pmask >> lane) & 1) && sx != BS_UNK;
         const u64 km = __ballot(known);
         if (!km) return;
-        u64 okv = known && sx == BS_OK ? (u64)r.a : 0, allv = known ? (u64)r.a : 0;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            okv += __shfl_xor((unsigned long long)okv, off);
-            allv += __shfl_xor((unsigned long long)allv, off);
+        // A few lanes: summed on the scalar unit (a shuffle reduction is 12 dependent LDS permutes).
+        const u64 okm2 = __ballot(known && sx == BS_OK);
+        for (u64 m = km; m; m &= m - 1) {
+            const u32 k = (u32)__builtin_ctzll(m);
+            const i64 a = (i64)fl_rl64((u64)r.a, k);
+            if ((okm2 >> k) & 1) d += a;
+            dp -= a;
         }
-        d += (i64)fl_rl64(okv, 0);
-        dp -= (i64)fl_rl64(allv, 0);
         pmask &= ~km;
     };
     auto wait_until = [&](auto decided) {  // publish, then poll the pending units until decided()
@@ -888,6 +972,9 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
             const int d32 = (int)dl, p32 = (int)dp;
             int dd = 0;
             u32 i = j;
+#if WALK_PAR
+            i = fl_runs32(v32, d32, j, b, dd, okm, p32 > 0 ? p32 : 0);
+#else
             for (; i < b; i++) {
                 const int vi = __builtin_amdgcn_readlane(v32, i), di = __builtin_amdgcn_readlane(d32, i);
                 if (vi + dd >= 0) {
@@ -897,7 +984,11 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
                     break;  // the pending credits could flip it
                 }
             }
+#endif
             d += dd;
+#if WALK_CNT
+            if (wait) ws.cnt[2] += i - j;  // bounded, 32 bits
+#endif
             j = i;
         }
         while (pmask && j < b) {  // bounded walk: d without the pending credits, d + dp with them
@@ -913,9 +1004,18 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
                 d += dj;
                 okm |= 1ULL << j;
             }
+#if WALK_CNT
+            if (wait) ws.cnt[3]++;  // bounded, 64 bits
+#endif
             j++;
         }
+#if WALK_CNT
+        const u32 j_run = j;
+        const bool r32 = fl_walk_run(v, dl, j, b, d, okm);
+        if (wait) (r32 ? ws.cnt[0] : ws.cnt[1]) += b - j_run;  // A/B builds: positions walked in 32 / 64 bits
+#else
         fl_walk_run(v, dl, j, b, d, okm);
+#endif
         j = b;
         if (b == n) break;
         // Position b: its partner was open when the window loaded.  The window's other open
@@ -1055,6 +1155,10 @@ __device__ static inline bool fl_walk_heavy(const FlowArgs& F, Globals* g, const
     const u32 lane = threadIdx.x & 63;
     s0 = __builtin_amdgcn_readfirstlane(s0);
     n_seg = __builtin_amdgcn_readfirstlane(n_seg);
+#if WALK_PRIO
+    // The heavy walker is the sweep's critical path; the light walkers sharing its SIMD yield to it.
+    __builtin_amdgcn_s_setprio(3);
+#endif
     i64 d = 0;
     u64 wb = 0, tblock = 0;
     WalkRec r0 = {}, r1 = {};
@@ -1515,6 +1619,9 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
             const u32 s0 = seg[k];
             len = seg[k + 1] - s0;
             fl_walk_heavy(F, g, R, s0, len, ws);
+#if WALK_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
         }
         if (heavy_walker) {
             if (lane == 0) {
@@ -1529,6 +1636,9 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
                     atomicAdd((unsigned long long*)&g->walk[10], (unsigned long long)ws.block_ticks);
 #endif
                     atomicAdd((unsigned long long*)&g->walk[11], (unsigned long long)(fl_now() - w0));
+#if WALK_CNT
+                    for (int k = 0; k < 4; k++) atomicAdd((unsigned long long*)&g->walk_dbg[k], (unsigned long long)ws.cnt[k]);
+#endif
                 }
             }
         }
@@ -1571,7 +1681,7 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
                 break;
             }
             if (fl_stalled(g)) break;
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(WALK_LIGHT_SLEEP);
         }
     }
     if (heavy_walker && lane == 0) {

@@ -12,7 +12,17 @@ CHILD = r"""
 import json, sys
 sys.argv = ["bench.py", "--secondary", "10000000"]
 import bench
-print(json.dumps(bench.run_secondary(bench.parse(), "c3h", 0)))
+from tigerbeetle_amd.state_machine import Engine
+seen = {}
+_stats = Engine.stats
+def stats(self):
+    s = _stats(self)
+    seen["walk_dbg"] = s.get("walk_dbg")
+    return s
+Engine.stats = stats
+d = bench.run_secondary(bench.parse(), "c3h", 0)
+d["flow"]["walk_dbg"] = seen.get("walk_dbg")
+print(json.dumps(d))
 """
 
 
@@ -38,7 +48,7 @@ def main():
                                                                       "transfers_equal", "posted_equal")),
                               **{k: f[k] for k in ("sweep_ms", "walk_crit_ms", "walk_crit_windows", "walk_crit_blocks",
                                                    "walk_crit_wait_ms", "walk_heavy_stops", "walk_heavy_blocks",
-                                                   "walk_heavy_blocked_ms")}}), flush=True)
+                                                   "walk_heavy_blocked_ms", "walk_dbg")}}), flush=True)
 
 
 if __name__ == "__main__":
