@@ -638,6 +638,9 @@ struct WalkRec {
 #ifndef WALK_PRIO
 #define WALK_PRIO 0  // 1: a heavy walker's wave runs at the highest issue priority (s_setprio 3)
 #endif
+#ifndef WALK_CARRY
+#define WALK_CARRY 1  // 0: a heavy walker's window waits for its pending credits before it ends
+#endif
 #ifndef WALK_PAR
 #define WALK_PAR 1  // 0: the 32-bit chain as a scalar step per lane
 #endif
@@ -645,7 +648,7 @@ struct WalkRec {
 #define WALK_CNT 0  // A/B builds only: count the critical walker's positions by path (walk_dbg)
 #endif
 #ifndef WALK_PROF
-#define WALK_PROF 0  // A/B builds only: time the critical heavy walker's window setups and ends
+#define WALK_PROF 0  // A/B builds only: time the critical heavy walker's window loops and runs
 #endif
 #ifndef WALK_DEEP
 #define WALK_DEEP 0  // 1: a heavy walker loads statuses two windows ahead (records three)
@@ -771,7 +774,8 @@ __device__ static inline int fl_scan32(int x) {
 // returns where (e: none).  Every sum stays below 2^31 in magnitude: |v32| <= 2^30, and dc plus
 // any partial sum of one window's deltas (each below 2^24) is below 2^30.
 __device__ static inline u64 fl_from(u32 s) { return s >= 64 ? 0 : ~0ULL << s; }
-__device__ static inline u32 fl_runs32(int v32, int d32, u32 j, u32 e, int& dc, u64& okm, int p32) {
+__device__ static inline u32 fl_runs32(int v32, int d32, u32 j, u32 e, int& dc, u64& okm, int p32,
+                                       u64* trips = nullptr) {
     const u32 lane = threadIdx.x & 63;
     const bool in = lane >= j && lane < e;
     const int x = in ? d32 : 0;
@@ -783,6 +787,7 @@ __device__ static inline u32 fl_runs32(int v32, int d32, u32 j, u32 e, int& dc, 
     u32 s = j;
     int Ps = 0;
     for (;;) {
+        if (trips) (*trips)++;
         const int c = Ps - B;  // lane k >= s of the ok run fails iff v32 + B + P(k) - P(s) < 0
         const u64 bad = __ballot(w < c) & inm & fl_from(s);
         if (!bad) {
@@ -812,14 +817,14 @@ __device__ static inline u32 fl_runs32(int v32, int d32, u32 j, u32 e, int& dc, 
     }
 }
 
-__device__ static inline void fl_chain32(int v32, int d32, u32 j, u32 e, int& dc, u64& okm) {
+__device__ static inline void fl_chain32(int v32, int d32, u32 j, u32 e, int& dc, u64& okm, u64* trips = nullptr) {
     // Wave-uniform by construction; said so, or the compiler may keep them in vector registers.
     j = __builtin_amdgcn_readfirstlane(j);
     e = __builtin_amdgcn_readfirstlane(e);
     dc = __builtin_amdgcn_readfirstlane(dc);
     okm = fl_rl64(okm, 0);
 #if WALK_PAR
-    (void)fl_runs32(v32, d32, j, e, dc, okm, 0);
+    (void)fl_runs32(v32, d32, j, e, dc, okm, 0, trips);
     return;
 #endif
     for (; j + 4 <= e; j += 4) {
@@ -843,7 +848,7 @@ __device__ static inline void fl_chain32(int v32, int d32, u32 j, u32 e, int& dc
 // v + d >= 0, and an ok lane adds dl to d; okm collects the outcomes.  When every |dl| of the run is
 // below 2^24 the run is walked in 32 bits, relative to d at its start (|sum of dl| < 2^30): each v + d0
 // is clamped to +-2^30, which keeps its sign against any partial sum, so every outcome is the same.
-__device__ static inline bool fl_walk_run(i64 v, i64 dl, u32 j, u32 e, i64& d, u64& okm) {
+__device__ static inline bool fl_walk_run(i64 v, i64 dl, u32 j, u32 e, i64& d, u64& okm, u64* trips = nullptr) {
     const u32 lane = threadIdx.x & 63;
     const bool in = lane >= j && lane < e;
     if (!__ballot(in && (dl >= (1LL << 24) || dl <= -(1LL << 24)))) {
@@ -851,7 +856,7 @@ __device__ static inline bool fl_walk_run(i64 v, i64 dl, u32 j, u32 e, i64& d, u
         const int v32 = (int)(vv > (1LL << 30) ? (1LL << 30) : vv < -(1LL << 30) ? -(1LL << 30) : vv);
         const int d32 = (int)dl;
         int dd = 0;
-        fl_chain32(v32, d32, j, e, dd, okm);
+        fl_chain32(v32, d32, j, e, dd, okm, trips);
         d += dd;
         return true;
     }
@@ -865,13 +870,22 @@ __device__ static inline bool fl_walk_run(i64 v, i64 dl, u32 j, u32 e, i64& d, u
     return false;
 }
 
+struct WalkCarry {  // a heavy walker's pending credits, carried from one window to the next
+    u32 u = 0;        // lane i: the unit of carried leg i
+    u32 st = BS_UNK;  // lane i: its status as loaded at the window's start
+    i64 a = 0;        // lane i: its amount
+    u64 mask = 0;     // the carried legs
+    i64 dp = 0;       // their amounts' sum
+};
+
 // Resolves one window of n <= 64 positions (lane j: position j) in order from the running sum d
 // (wave-uniform), publishing the statuses its checks decide.  Returns the positions decided: n, or
 // the position of a partner that has not decided yet (the walk resumes there).
 // wait (a heavy walker: its wave walks this one segment) keeps a stopped window in place, polling the
 // partner's status, instead of returning; a light wave returns and visits its other segments.
 __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r, u32 st, u32 vw, u32 s, u32 n,
-                                            i64& d, WalkStats& ws, Globals* g = nullptr, bool wait = false) {
+                                            i64& d, WalkStats& ws, Globals* g = nullptr, bool wait = false,
+                                            WalkCarry* cw = nullptr) {
     const u32 lane = threadIdx.x & 63;
     const bool valid = lane >= s && lane < n;  // positions [s, n): the window from where it stopped
     const bool isx = r.kind & BT_X, isy = valid && !isx, cr = r.kind & BT_CR;
@@ -902,9 +916,6 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
             dl = oth == BV_FAIL ? 0 : -r.a;  // the other side failed: no delta here either way
         }
     };
-#if WALK_PROF
-    const u64 tp0 = wait ? fl_now() : 0;
-#endif
     classify();
     u64 smask = __ballot(simple);
     const u64 vmask = n == 64 ? ~0ULL : ((1ULL << n) - 1);
@@ -914,8 +925,10 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
     // amount in dp, and d stays the sum without it.  A later check is decided if it decides the same
     // way with and without every pending credit (d and d + dp); only a check that it would flip
     // waits — for the pending units, not for the first of them.
-    u64 pmask = 0;
-    i64 dp = 0;
+    // With cw (a heavy walker), the window leaves its pending credits to the next one instead of
+    // waiting for them (cmask: the ones carried in from the previous window; dp counts both).
+    u64 pmask = 0, cmask = cw ? cw->mask : 0;
+    i64 dp = cw ? cw->dp : 0;
     auto publish_to = [&](u32 upto) {  // this window's checks in [pub, upto)
         if (check && valid && lane >= pub && lane < upto) {
             const u32 mine = (okm >> lane) & 1 ? BV_PASS : BV_FAIL;
@@ -923,21 +936,37 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         }
         pub = max(pub, upto);
     };
-    auto settle = [&]() {  // the pending units decided by now: their amounts leave dp (and ok ones enter d)
-        u32 sx = BS_UNK;
-        if ((pmask >> lane) & 1) sx = fl_ld32(&F.b_st[r.u]);
+    // The pending units decided by now (sx: this window's, sc: the carried ones' statuses): their
+    // amounts leave dp, and the ok ones' enter d.
+    auto settle_with = [&](u32 sx, u32 sc) {
         const bool known = ((pmask >> lane) & 1) && sx != BS_UNK;
-        const u64 km = __ballot(known);
-        if (!km) return;
+        const bool knownc = cw && ((cmask >> lane) & 1) && sc != BS_UNK;
+        const u64 km = __ballot(known), kc = __ballot(knownc);
+        if (!(km | kc)) return;
         // A few lanes: summed on the scalar unit (a shuffle reduction is 12 dependent LDS permutes).
-        const u64 okm2 = __ballot(known && sx == BS_OK);
+        const u64 okp = __ballot(known && sx == BS_OK), okc = __ballot(knownc && sc == BS_OK);
         for (u64 m = km; m; m &= m - 1) {
             const u32 k = (u32)__builtin_ctzll(m);
             const i64 a = (i64)fl_rl64((u64)r.a, k);
-            if ((okm2 >> k) & 1) d += a;
+            if ((okp >> k) & 1) d += a;
             dp -= a;
         }
+        if (cw) {
+            for (u64 m = kc; m; m &= m - 1) {
+                const u32 k = (u32)__builtin_ctzll(m);
+                const i64 a = (i64)fl_rl64((u64)cw->a, k);
+                if ((okc >> k) & 1) d += a;
+                dp -= a;
+            }
+        }
         pmask &= ~km;
+        cmask &= ~kc;
+    };
+    auto settle = [&]() {  // polls every pending unit once
+        u32 sx = BS_UNK, sc = BS_UNK;
+        if ((pmask >> lane) & 1) sx = fl_ld32(&F.b_st[r.u]);
+        if (cw && ((cmask >> lane) & 1)) sc = fl_ld32(&F.b_st[cw->u]);
+        settle_with(sx, sc);
     };
     auto wait_until = [&](auto decided) {  // publish, then poll the pending units until decided()
         publish_to(j);
@@ -950,6 +979,7 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
             if (__builtin_amdgcn_readfirstlane(!decided() && (fl_expired(F, w0) || fl_stalled(g)))) {
                 if (lane == 0) tb_panic(g, PANIC_FLOW_STALL);
                 pmask = 0;  // give up (the pass is lost to the panic)
+                cmask = 0;
                 dp = 0;
                 break;
             }
@@ -957,7 +987,7 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         ws.block_ticks += fl_now() - w0;
     };
 #if WALK_PROF
-    if (wait) ws.loop_ticks += fl_now() - tp0;  // A/B builds: the window's setup
+    const u64 tp1 = wait ? fl_now() : 0;  // A/B builds: the loop's time, and its runs' time
 #endif
     while (j < n) {
         const u64 bar = ~smask & vmask & (~0ULL << j);
@@ -965,7 +995,7 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         // Bounded walk while credits are pending: d without them, d + dp with them.  In 32 bits when
         // the stretch's moves and the pending credits stay below 2^29 (amounts below 2^22): v + d
         // clamped to +-2^29 keeps both signs.
-        if (pmask && j < b && dp < (1LL << 28) &&
+        if ((pmask | cmask) && j < b && dp < (1LL << 28) &&
             !__ballot(lane >= j && lane < b && (dl >= (1LL << 22) || dl <= -(1LL << 22)))) {
             const i64 vv = (i64)((u64)v + (u64)d);
             const int v32 = (int)(vv > (1LL << 29) ? (1LL << 29) : vv < -(1LL << 29) ? -(1LL << 29) : vv);
@@ -973,7 +1003,11 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
             int dd = 0;
             u32 i = j;
 #if WALK_PAR
+#if WALK_CNT
+            i = fl_runs32(v32, d32, j, b, dd, okm, p32 > 0 ? p32 : 0, wait ? &ws.cnt[2] : nullptr);
+#else
             i = fl_runs32(v32, d32, j, b, dd, okm, p32 > 0 ? p32 : 0);
+#endif
 #else
             for (; i < b; i++) {
                 const int vi = __builtin_amdgcn_readlane(v32, i), di = __builtin_amdgcn_readlane(d32, i);
@@ -986,17 +1020,16 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
             }
 #endif
             d += dd;
-#if WALK_CNT
-            if (wait) ws.cnt[2] += i - j;  // bounded, 32 bits
-#endif
+
             j = i;
         }
-        while (pmask && j < b) {  // bounded walk: d without the pending credits, d + dp with them
+        while ((pmask | cmask) && j < b) {  // bounded walk: d without the pending credits, d + dp with them
             const i64 vj = (i64)fl_rl64((u64)v, j), dj = (i64)fl_rl64((u64)dl, j);
             const bool lo = (i64)((u64)vj + (u64)d) >= 0, hi = (i64)((u64)vj + (u64)d + (u64)dp) >= 0;
             if (lo != hi) {
                 wait_until([&]() {
-                    return !pmask || ((i64)((u64)vj + (u64)d) >= 0) == ((i64)((u64)vj + (u64)d + (u64)dp) >= 0);
+                    return !(pmask | cmask) ||
+                           ((i64)((u64)vj + (u64)d) >= 0) == ((i64)((u64)vj + (u64)d + (u64)dp) >= 0);
                 });
                 continue;
             }
@@ -1004,15 +1037,18 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
                 d += dj;
                 okm |= 1ULL << j;
             }
-#if WALK_CNT
-            if (wait) ws.cnt[3]++;  // bounded, 64 bits
-#endif
+
             j++;
         }
 #if WALK_CNT
-        const u32 j_run = j;
-        const bool r32 = fl_walk_run(v, dl, j, b, d, okm);
-        if (wait) (r32 ? ws.cnt[0] : ws.cnt[1]) += b - j_run;  // A/B builds: positions walked in 32 / 64 bits
+        // A/B builds: runs walked (fl_runs32 trips), loop iterations, bounded-walk trips, windows
+        const bool r32 = fl_walk_run(v, dl, j, b, d, okm, wait ? &ws.cnt[0] : nullptr);
+        (void)r32;
+        if (wait) ws.cnt[1]++;
+#elif WALK_PROF
+        const u64 tpr = wait ? fl_now() : 0;
+        fl_walk_run(v, dl, j, b, d, okm);
+        if (wait) ws.loop_ticks += fl_now() - tpr;
 #else
         fl_walk_run(v, dl, j, b, d, okm);
 #endif
@@ -1041,7 +1077,7 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
             st = fl_ld32(&F.b_st[r.u]);
             if (isx) vw = fl_ld32(&F.b_vw[r.u]);
         }
-        if ((bk & BT_X) && pmask) wait_until([&]() { return !pmask; });  // a paired check needs the exact d
+        if ((bk & BT_X) && (pmask | cmask)) wait_until([&]() { return !(pmask | cmask); });  // a paired check needs the exact d
         const i64 bb = (i64)fl_rl64((u64)r.base, b);
         // The unit's status now: a paired check ORs this side's verdict in first (whoever completes
         // the pair publishes; a partner that walked its side as a plain check publishes the status,
@@ -1104,10 +1140,26 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         j = b + 1;
     }
 #if WALK_PROF
-    const u64 tp2 = wait ? fl_now() : 0;
+    if (wait) ws.prof_ticks += fl_now() - tp1;
 #endif
-    if (pmask) wait_until([&]() { return !pmask; });  // the window leaves with an exact d
+    if (cw) {
+        // The legs carried in from the previous window, with their statuses as loaded at this
+        // window's start (fl_walk_heavy): the ones still open are polled until decided; then this
+        // window's pending legs carry on to the next (no round trip when the partners kept up).
+        if (cmask) settle_with(BS_UNK, cw->st);
+        if (cmask) wait_until([&]() { return !cmask; });
+        cw->u = r.u;
+        cw->a = r.a;
+        cw->st = BS_UNK;  // (loaded afresh at the next window's start)
+        cw->mask = pmask;
+        cw->dp = dp;
+    } else if (pmask) {
+        wait_until([&]() { return !pmask; });  // the window leaves with an exact d
+    }
     ws.windows++;
+#if WALK_CNT
+    if (wait) ws.cnt[3]++;
+#endif
     // Publish the checks walked in the scalar loop, once per window: a status poll issued after a
     // store waits for it (vmcnt counts both), so publishing in smaller pieces ahead of the stops
     // cost more than it saved partners (C3h 66.5 -> 54 M/s with 16-position pieces).
@@ -1115,9 +1167,6 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         const u32 mine = (okm >> lane) & 1 ? BV_PASS : BV_FAIL;
         fl_st32(&F.b_st[r.u], cr ? fl_combine(oth, mine) : fl_combine(mine, oth));
     }
-#if WALK_PROF
-    if (wait) ws.prof_ticks += fl_now() - tp2;  // A/B builds: the window's end (its last wait included)
-#endif
     return m;
 }
 
@@ -1161,6 +1210,9 @@ __device__ static inline bool fl_walk_heavy(const FlowArgs& F, Globals* g, const
 #endif
     i64 d = 0;
     u64 wb = 0, tblock = 0;
+#if WALK_CARRY
+    WalkCarry cw;
+#endif
     WalkRec r0 = {}, r1 = {};
     if (lane < n_seg) r0 = R[s0 + lane];
     if (64 + lane < n_seg) r1 = R[s0 + 64 + lane];
@@ -1199,8 +1251,16 @@ __device__ static inline bool fl_walk_heavy(const FlowArgs& F, Globals* g, const
             }
         }
 #endif
+#if WALK_CARRY
+        // The carried legs' statuses, loaded now and read at the window's end.
+        cw.st = BS_UNK;
+        if ((cw.mask >> lane) & 1) cw.st = fl_ld32(&F.b_st[cw.u]);
+        WalkCarry* cwp = &cw;
+#else
+        WalkCarry* cwp = nullptr;
+#endif
         for (u32 s = 0;;) {
-            const u32 m = fl_walk_window(F, r0, st0, vw0, s, n, d, ws, g, true);
+            const u32 m = fl_walk_window(F, r0, st0, vw0, s, n, d, ws, g, true, cwp);
             if (m > s && tblock) {
                 ws.block_ticks += wall_clock64() - tblock;
                 tblock = 0;
@@ -1628,7 +1688,7 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
                 atomicAdd((unsigned long long*)&g->walk[2], (unsigned long long)len);
                 if (len == *(volatile u32*)&F.words[FW_WMAX]) {  // the critical walker: the longest segment
                     atomicAdd((unsigned long long*)&g->walk[8], (unsigned long long)ws.windows);
-#if WALK_PROF  // A/B builds: crit "blocks" = window-end ticks, "wait" = window-setup ticks
+#if WALK_PROF  // A/B builds: crit "blocks" = the windows' loop ticks, "wait" = their runs' ticks
                     atomicAdd((unsigned long long*)&g->walk[9], (unsigned long long)ws.prof_ticks);
                     atomicAdd((unsigned long long*)&g->walk[10], (unsigned long long)ws.loop_ticks);
 #else
