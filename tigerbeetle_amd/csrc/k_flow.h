@@ -614,8 +614,10 @@ __device__ static inline u32 fl_sw_slot(u32* s_hk, u32 head) {
 // wave of its own; the others share the remaining waves, each wave cycling through its segments
 // and moving on from a blocked one.  A wave walks its segment 64 positions a window: the
 // records and the statuses its Y legs and paired checks need are loaded by the 64 lanes at once,
-// then the window is resolved in order on the scalar unit — one add, compare and select per
-// position — stopping at a position whose partner has not decided yet.
+// then the window is resolved in order — in parallel by runs of ok / failed positions (a prefix
+// sum and a ballot per run, fl_runs32) — stopping at a position whose partner has not decided yet.
+// A heavy walker takes an open Y leg as a pending credit and goes on, and carries the credits
+// still pending at a window's end into the next window (WalkCarry) rather than waiting for them.
 struct WalkRec {
     i64 base;  // Y − X of the account with every decided ok unit before this position (balances included)
     i64 a;     // the leg's amount
@@ -628,33 +630,26 @@ struct WalkRec {
 #define WALK_HEAVY 256
 #endif
 #define WALK_RING 8  // windows a feeder wave keeps ahead of its walker in LDS
-#ifndef WALK_REFRESH
-#define WALK_REFRESH 0  // 1: a heavy walker re-reads a window's open partner statuses before walking it (C3h: no gain, stops -5 %)
-#endif
 
-#ifndef WALK_LIGHT_SLEEP
-#define WALK_LIGHT_SLEEP 2  // s_sleep of a light wave whose segments all stood still
-#endif
-#ifndef WALK_PRIO
-#define WALK_PRIO 0  // 1: a heavy walker's wave runs at the highest issue priority (s_setprio 3)
-#endif
 #ifndef WALK_CARRY
-#define WALK_CARRY 1  // 0: a heavy walker's window waits for its pending credits before it ends
+#define WALK_CARRY 1  // windows a heavy walker carries its pending credits (0: each window waits for its own);
+                      // C3h 0: 99.5, 1: 120.1, 2: 116.9, 3: 113.2 M/s
 #endif
+#define WALK_NC (WALK_CARRY > 0 ? WALK_CARRY : 1)
 #ifndef WALK_PAR
-#define WALK_PAR 1  // 0: the 32-bit chain as a scalar step per lane
+#define WALK_PAR 1  // 0: the 32-bit chain as a scalar step per lane (C3h 73.2 M/s against 99.2)
 #endif
 #ifndef WALK_CNT
 #define WALK_CNT 0  // A/B builds only: count the critical walker's positions by path (walk_dbg)
 #endif
 #ifndef WALK_PROF
-#define WALK_PROF 0  // A/B builds only: time the critical heavy walker's window loops and runs
+#define WALK_PROF 0  // A/B builds only: time the critical heavy walker's phases (walk_dbg)
 #endif
 #ifndef WALK_DEEP
-#define WALK_DEEP 0  // 1: a heavy walker loads statuses two windows ahead (records three)
+#define WALK_DEEP 0  // 1: a heavy walker loads statuses two windows ahead, records three (C3h 121.7 M/s against 124.1)
 #endif
 #ifndef WALK_PEND_NOW
-#define WALK_PEND_NOW 1  // 0: a heavy walker polls an open Y leg's status before taking it as pending
+#define WALK_PEND_NOW 1  // 0: a heavy walker polls an open Y leg's status before taking it as pending (C3h 94.2 against 99.1)
 #endif
 
 #define WALK_BIG (1LL << 62)  // a position whose outcome is known: "always" (+) / "never" (−)
@@ -725,10 +720,41 @@ __device__ static inline void fl_walk_status(const FlowArgs& F, const WalkRec& r
     if (pair) vw = fl_ld32(&F.b_vw[r.u]);
 }
 
+// The heavy walker's loads, issued unconditionally (a clamped index: lanes past the segment read its
+// last record, a valid address) and raw, their lanes selected only where a window consumes them: a
+// load under a branch leaves the compiler unsure how many loads are in flight, so it waits for all
+// of them (vmcnt(0)) at the next use of any, and a select right after a load waits for that load —
+// either put a full memory round trip on every window of the critical walker.
+__device__ static inline WalkRec fl_walk_rec(const WalkRec* R, u32 s0, u32 n_seg, u32 i) {
+    return R[s0 + min(i, n_seg - 1)];
+}
+__device__ static inline WalkRec fl_walk_rec_valid(WalkRec x, bool ok) {  // lanes past the segment: zero
+    x.base = ok ? x.base : 0;
+    x.a = ok ? x.a : 0;
+    x.u = ok ? x.u : 0;
+    x.kind = ok ? x.kind : 0;
+    x.head = ok ? x.head : 0;
+    return x;
+}
+__device__ static inline void fl_walk_status_raw(const FlowArgs& F, const WalkRec& r, u32& st, u32& vw) {
+    st = fl_ld32(&F.b_st[r.u]);
+    vw = fl_ld32(&F.b_vw[r.u]);
+}
+__device__ static inline void fl_walk_status_sel(const WalkRec& r, bool valid, u32& st, u32& vw) {  // as fl_walk_status
+    const bool isx = r.kind & BT_X, cr = r.kind & BT_CR;
+    const bool pair = valid && isx && (cr ? (r.kind >> 8) & 15 : (r.kind >> 12) & 15) == BV_UNK;
+    st = (valid && !isx) || pair ? st : (u32)BS_UNK;
+    vw = pair ? vw : 0;
+}
+
 struct WalkStats {
-    u64 windows = 0, stops = 0, blocks = 0, loop_ticks = 0, block_ticks = 0, prof_ticks = 0;
+    u64 windows = 0, stops = 0, blocks = 0, loop_ticks = 0, block_ticks = 0;
 #if WALK_CNT
     u64 cnt[4] = {};  // A/B builds: the critical walker's positions by path (walk_dbg)
+#endif
+#if WALK_PROF
+    u64 pt[4] = {};   // A/B builds: ticks in the window's fetch, setup, loop and end (walk_dbg)
+    u64 pt_last = 0;
 #endif
 };
 
@@ -916,6 +942,13 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
             dl = oth == BV_FAIL ? 0 : -r.a;  // the other side failed: no delta here either way
         }
     };
+#if WALK_PROF
+    if (wait) {
+        const u64 t = fl_now();
+        ws.pt[0] += t - ws.pt_last;
+        ws.pt_last = t;
+    }
+#endif
     classify();
     u64 smask = __ballot(simple);
     const u64 vmask = n == 64 ? ~0ULL : ((1ULL << n) - 1);
@@ -925,10 +958,12 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
     // amount in dp, and d stays the sum without it.  A later check is decided if it decides the same
     // way with and without every pending credit (d and d + dp); only a check that it would flip
     // waits — for the pending units, not for the first of them.
-    // With cw (a heavy walker), the window leaves its pending credits to the next one instead of
-    // waiting for them (cmask: the ones carried in from the previous window; dp counts both).
-    u64 pmask = 0, cmask = cw ? cw->mask : 0;
-    i64 dp = cw ? cw->dp : 0;
+    // With cw (a heavy walker), the window leaves its pending credits to the next ones instead of
+    // waiting for them (cmask[k]: the ones carried in, set 0 the oldest; dp counts them all).
+    u64 pmask = 0, cmask[WALK_NC];
+#pragma unroll
+    for (int k = 0; k < WALK_NC; k++) cmask[k] = cw ? cw[k].mask : 0;
+    i64 dp = cw ? cw[0].dp : 0;
     auto publish_to = [&](u32 upto) {  // this window's checks in [pub, upto)
         if (check && valid && lane >= pub && lane < upto) {
             const u32 mine = (okm >> lane) & 1 ? BV_PASS : BV_FAIL;
@@ -938,35 +973,40 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
     };
     // The pending units decided by now (sx: this window's, sc: the carried ones' statuses): their
     // amounts leave dp, and the ok ones' enter d.
-    auto settle_with = [&](u32 sx, u32 sc) {
-        const bool known = ((pmask >> lane) & 1) && sx != BS_UNK;
-        const bool knownc = cw && ((cmask >> lane) & 1) && sc != BS_UNK;
-        const u64 km = __ballot(known), kc = __ballot(knownc);
-        if (!(km | kc)) return;
-        // A few lanes: summed on the scalar unit (a shuffle reduction is 12 dependent LDS permutes).
-        const u64 okp = __ballot(known && sx == BS_OK), okc = __ballot(knownc && sc == BS_OK);
+    // A few lanes: summed on the scalar unit (a shuffle reduction is 12 dependent LDS permutes).
+    auto settle_set = [&](u64& mask, u32 sx, i64 a_lane) {
+        const bool known = ((mask >> lane) & 1) && sx != BS_UNK;
+        const u64 km = __ballot(known);
+        if (!km) return;
+        const u64 okk = __ballot(known && sx == BS_OK);
         for (u64 m = km; m; m &= m - 1) {
             const u32 k = (u32)__builtin_ctzll(m);
-            const i64 a = (i64)fl_rl64((u64)r.a, k);
-            if ((okp >> k) & 1) d += a;
+            const i64 a = (i64)fl_rl64((u64)a_lane, k);
+            if ((okk >> k) & 1) d += a;
             dp -= a;
         }
-        if (cw) {
-            for (u64 m = kc; m; m &= m - 1) {
-                const u32 k = (u32)__builtin_ctzll(m);
-                const i64 a = (i64)fl_rl64((u64)cw->a, k);
-                if ((okc >> k) & 1) d += a;
-                dp -= a;
-            }
-        }
-        pmask &= ~km;
-        cmask &= ~kc;
+        mask &= ~km;
+    };
+    auto pend = [&]() {
+        u64 m = pmask;
+#pragma unroll
+        for (int k = 0; k < WALK_NC; k++) m |= cmask[k];
+        return m;
     };
     auto settle = [&]() {  // polls every pending unit once
-        u32 sx = BS_UNK, sc = BS_UNK;
+        u32 sx = BS_UNK;
         if ((pmask >> lane) & 1) sx = fl_ld32(&F.b_st[r.u]);
-        if (cw && ((cmask >> lane) & 1)) sc = fl_ld32(&F.b_st[cw->u]);
-        settle_with(sx, sc);
+        u32 sc[WALK_NC];
+#pragma unroll
+        for (int k = 0; k < WALK_NC; k++) {
+            sc[k] = BS_UNK;
+            if (cw && ((cmask[k] >> lane) & 1)) sc[k] = fl_ld32(&F.b_st[cw[k].u]);
+        }
+        settle_set(pmask, sx, r.a);
+        if (cw) {
+#pragma unroll
+            for (int k = 0; k < WALK_NC; k++) settle_set(cmask[k], sc[k], cw[k].a);
+        }
     };
     auto wait_until = [&](auto decided) {  // publish, then poll the pending units until decided()
         publish_to(j);
@@ -979,7 +1019,8 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
             if (__builtin_amdgcn_readfirstlane(!decided() && (fl_expired(F, w0) || fl_stalled(g)))) {
                 if (lane == 0) tb_panic(g, PANIC_FLOW_STALL);
                 pmask = 0;  // give up (the pass is lost to the panic)
-                cmask = 0;
+#pragma unroll
+                for (int k = 0; k < WALK_NC; k++) cmask[k] = 0;
                 dp = 0;
                 break;
             }
@@ -987,7 +1028,11 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         ws.block_ticks += fl_now() - w0;
     };
 #if WALK_PROF
-    const u64 tp1 = wait ? fl_now() : 0;  // A/B builds: the loop's time, and its runs' time
+    if (wait) {
+        const u64 t = fl_now();
+        ws.pt[1] += t - ws.pt_last;
+        ws.pt_last = t;
+    }
 #endif
     while (j < n) {
         const u64 bar = ~smask & vmask & (~0ULL << j);
@@ -995,7 +1040,7 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         // Bounded walk while credits are pending: d without them, d + dp with them.  In 32 bits when
         // the stretch's moves and the pending credits stay below 2^29 (amounts below 2^22): v + d
         // clamped to +-2^29 keeps both signs.
-        if ((pmask | cmask) && j < b && dp < (1LL << 28) &&
+        if (pend() && j < b && dp < (1LL << 28) &&
             !__ballot(lane >= j && lane < b && (dl >= (1LL << 22) || dl <= -(1LL << 22)))) {
             const i64 vv = (i64)((u64)v + (u64)d);
             const int v32 = (int)(vv > (1LL << 29) ? (1LL << 29) : vv < -(1LL << 29) ? -(1LL << 29) : vv);
@@ -1023,12 +1068,12 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
 
             j = i;
         }
-        while ((pmask | cmask) && j < b) {  // bounded walk: d without the pending credits, d + dp with them
+        while (pend() && j < b) {  // bounded walk: d without the pending credits, d + dp with them
             const i64 vj = (i64)fl_rl64((u64)v, j), dj = (i64)fl_rl64((u64)dl, j);
             const bool lo = (i64)((u64)vj + (u64)d) >= 0, hi = (i64)((u64)vj + (u64)d + (u64)dp) >= 0;
             if (lo != hi) {
                 wait_until([&]() {
-                    return !(pmask | cmask) ||
+                    return !pend() ||
                            ((i64)((u64)vj + (u64)d) >= 0) == ((i64)((u64)vj + (u64)d + (u64)dp) >= 0);
                 });
                 continue;
@@ -1045,10 +1090,6 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         const bool r32 = fl_walk_run(v, dl, j, b, d, okm, wait ? &ws.cnt[0] : nullptr);
         (void)r32;
         if (wait) ws.cnt[1]++;
-#elif WALK_PROF
-        const u64 tpr = wait ? fl_now() : 0;
-        fl_walk_run(v, dl, j, b, d, okm);
-        if (wait) ws.loop_ticks += fl_now() - tpr;
 #else
         fl_walk_run(v, dl, j, b, d, okm);
 #endif
@@ -1077,7 +1118,7 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
             st = fl_ld32(&F.b_st[r.u]);
             if (isx) vw = fl_ld32(&F.b_vw[r.u]);
         }
-        if ((bk & BT_X) && (pmask | cmask)) wait_until([&]() { return !(pmask | cmask); });  // a paired check needs the exact d
+        if ((bk & BT_X) && pend()) wait_until([&]() { return !pend(); });  // a paired check needs the exact d
         const i64 bb = (i64)fl_rl64((u64)r.base, b);
         // The unit's status now: a paired check ORs this side's verdict in first (whoever completes
         // the pair publishes; a partner that walked its side as a plain check publishes the status,
@@ -1140,19 +1181,31 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         j = b + 1;
     }
 #if WALK_PROF
-    if (wait) ws.prof_ticks += fl_now() - tp1;
+    if (wait) {
+        const u64 t = fl_now();
+        ws.pt[2] += t - ws.pt_last;
+        ws.pt_last = t;
+    }
 #endif
     if (cw) {
-        // The legs carried in from the previous window, with their statuses as loaded at this
-        // window's start (fl_walk_heavy): the ones still open are polled until decided; then this
-        // window's pending legs carry on to the next (no round trip when the partners kept up).
-        if (cmask) settle_with(BS_UNK, cw->st);
-        if (cmask) wait_until([&]() { return !cmask; });
-        cw->u = r.u;
-        cw->a = r.a;
-        cw->st = BS_UNK;  // (loaded afresh at the next window's start)
-        cw->mask = pmask;
-        cw->dp = dp;
+        // The oldest carried legs, with their statuses as loaded at the start of the window after
+        // theirs (fl_walk_heavy; WALK_NC windows ago): the ones still open are polled until
+        // decided.  The others move down, and this window's pending legs carry on (no round trip
+        // when the partners kept up).
+        settle_set(cmask[0], cw[0].st, cw[0].a);
+        if (cmask[0]) wait_until([&]() { return !cmask[0]; });
+#pragma unroll
+        for (int k = 0; k + 1 < WALK_NC; k++) {
+            cw[k].u = cw[k + 1].u;
+            cw[k].a = cw[k + 1].a;
+            cw[k].st = cw[k + 1].st;
+            cw[k].mask = cmask[k + 1];
+        }
+        cw[WALK_NC - 1].u = r.u;
+        cw[WALK_NC - 1].a = r.a;
+        cw[WALK_NC - 1].st = BS_UNK;  // (loaded at the next window's start)
+        cw[WALK_NC - 1].mask = pmask;
+        cw[0].dp = dp;
     } else if (pmask) {
         wait_until([&]() { return !pmask; });  // the window leaves with an exact d
     }
@@ -1167,6 +1220,13 @@ __device__ static inline u32 fl_walk_window(const FlowArgs& F, const WalkRec& r,
         const u32 mine = (okm >> lane) & 1 ? BV_PASS : BV_FAIL;
         fl_st32(&F.b_st[r.u], cr ? fl_combine(oth, mine) : fl_combine(mine, oth));
     }
+#if WALK_PROF
+    if (wait) {
+        const u64 t = fl_now();
+        ws.pt[3] += t - ws.pt_last;
+        ws.pt_last = t;
+    }
+#endif
     return m;
 }
 
@@ -1204,63 +1264,47 @@ __device__ static inline bool fl_walk_heavy(const FlowArgs& F, Globals* g, const
     const u32 lane = threadIdx.x & 63;
     s0 = __builtin_amdgcn_readfirstlane(s0);
     n_seg = __builtin_amdgcn_readfirstlane(n_seg);
-#if WALK_PRIO
-    // The heavy walker is the sweep's critical path; the light walkers sharing its SIMD yield to it.
-    __builtin_amdgcn_s_setprio(3);
-#endif
     i64 d = 0;
     u64 wb = 0, tblock = 0;
 #if WALK_CARRY
-    WalkCarry cw;
+    WalkCarry cw[WALK_NC];
 #endif
-    WalkRec r0 = {}, r1 = {};
-    if (lane < n_seg) r0 = R[s0 + lane];
-    if (64 + lane < n_seg) r1 = R[s0 + 64 + lane];
+#if WALK_PROF
+    ws.pt_last = fl_now();
+#endif
+    WalkRec r0 = fl_walk_rec(R, s0, n_seg, lane), r1 = fl_walk_rec(R, s0, n_seg, 64 + lane);
     u32 st0, vw0;
-    fl_walk_status(F, r0, lane < n_seg, st0, vw0);
+    fl_walk_status_raw(F, r0, st0, vw0);
 #if WALK_DEEP
     // Statuses two windows ahead, records three.
-    WalkRec r2 = {};
-    if (128 + lane < n_seg) r2 = R[s0 + 128 + lane];
+    WalkRec r2 = fl_walk_rec(R, s0, n_seg, 128 + lane);
     u32 st1, vw1;
-    fl_walk_status(F, r1, 64 + lane < n_seg, st1, vw1);
+    fl_walk_status_raw(F, r1, st1, vw1);
 #endif
     for (u32 c = 0; c < n_seg; c += 64) {
         const u32 n = min(64u, n_seg - c);
 #if WALK_DEEP
-        WalkRec r3 = {};
-        if (c + 192 + lane < n_seg) r3 = R[s0 + c + 192 + lane];
+        const WalkRec r3 = fl_walk_rec(R, s0, n_seg, c + 192 + lane);
         u32 st2, vw2;
-        fl_walk_status(F, r2, c + 128 + lane < n_seg, st2, vw2);
+        fl_walk_status_raw(F, r2, st2, vw2);
 #else
-        WalkRec r2 = {};
-        if (c + 128 + lane < n_seg) r2 = R[s0 + c + 128 + lane];
+        const WalkRec r2 = fl_walk_rec(R, s0, n_seg, c + 128 + lane);
         u32 st1, vw1;
-        fl_walk_status(F, r1, c + 64 + lane < n_seg, st1, vw1);
-#endif
-#if WALK_REFRESH
-        {   // The window's still-open partner statuses, read again right before it is walked (they were
-            // read a window ago; a partner walker has often decided them since): one round trip here
-            // instead of a stop at each of them in the walk.
-            const bool open = lane < n && st0 == BS_UNK;
-            u32 st2 = BS_UNK, vw2 = 0;
-            if (__ballot(open)) fl_walk_status(F, r0, open, st2, vw2);
-            if (open) {
-                st0 = st2;
-                vw0 = vw2 ? vw2 : vw0;
-            }
-        }
+        fl_walk_status_raw(F, r1, st1, vw1);
 #endif
 #if WALK_CARRY
-        // The carried legs' statuses, loaded now and read at the window's end.
-        cw.st = BS_UNK;
-        if ((cw.mask >> lane) & 1) cw.st = fl_ld32(&F.b_st[cw.u]);
-        WalkCarry* cwp = &cw;
+        // The newest carried legs' statuses, loaded now and read WALK_NC window ends later.
+        cw[WALK_NC - 1].st = fl_ld32(&F.b_st[cw[WALK_NC - 1].u]);  // (masked where it is read)
+        WalkCarry* cwp = cw;
 #else
         WalkCarry* cwp = nullptr;
 #endif
+        // This window's records and statuses (loaded one and two windows ago), lanes selected now.
+        const WalkRec rw = fl_walk_rec_valid(r0, c + lane < n_seg);
+        u32 stw = st0, vww = vw0;
+        fl_walk_status_sel(rw, c + lane < n_seg, stw, vww);
         for (u32 s = 0;;) {
-            const u32 m = fl_walk_window(F, r0, st0, vw0, s, n, d, ws, g, true, cwp);
+            const u32 m = fl_walk_window(F, rw, stw, vww, s, n, d, ws, g, true, cwp);
             if (m > s && tblock) {
                 ws.block_ticks += wall_clock64() - tblock;
                 tblock = 0;
@@ -1273,7 +1317,7 @@ __device__ static inline bool fl_walk_heavy(const FlowArgs& F, Globals* g, const
             if (!tblock) tblock = now;
             if (!wb) wb = now;
             if (now - wb > F.stall_ticks) {
-                const u32 bu = __builtin_amdgcn_readlane(r0.u, s), bk = __builtin_amdgcn_readlane(r0.kind, s);
+                const u32 bu = __builtin_amdgcn_readlane(rw.u, s), bk = __builtin_amdgcn_readlane(rw.kind, s);
                 if (lane == 0) {
                     g->walk_dbg[0] = 1 | ((u64)bk << 8) | ((u64)c << 32);
                     g->walk_dbg[1] = bu;
@@ -1679,21 +1723,16 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
             const u32 s0 = seg[k];
             len = seg[k + 1] - s0;
             fl_walk_heavy(F, g, R, s0, len, ws);
-#if WALK_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
         }
         if (heavy_walker) {
             if (lane == 0) {
                 atomicAdd((unsigned long long*)&g->walk[2], (unsigned long long)len);
                 if (len == *(volatile u32*)&F.words[FW_WMAX]) {  // the critical walker: the longest segment
                     atomicAdd((unsigned long long*)&g->walk[8], (unsigned long long)ws.windows);
-#if WALK_PROF  // A/B builds: crit "blocks" = the windows' loop ticks, "wait" = their runs' ticks
-                    atomicAdd((unsigned long long*)&g->walk[9], (unsigned long long)ws.prof_ticks);
-                    atomicAdd((unsigned long long*)&g->walk[10], (unsigned long long)ws.loop_ticks);
-#else
                     atomicAdd((unsigned long long*)&g->walk[9], (unsigned long long)ws.blocks);
                     atomicAdd((unsigned long long*)&g->walk[10], (unsigned long long)ws.block_ticks);
+#if WALK_PROF
+                    for (int k = 0; k < 4; k++) atomicAdd((unsigned long long*)&g->walk_dbg[k], (unsigned long long)ws.pt[k]);
 #endif
                     atomicAdd((unsigned long long*)&g->walk[11], (unsigned long long)(fl_now() - w0));
 #if WALK_CNT
@@ -1741,7 +1780,7 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
                 break;
             }
             if (fl_stalled(g)) break;
-            __builtin_amdgcn_s_sleep(WALK_LIGHT_SLEEP);
+            __builtin_amdgcn_s_sleep(2);
         }
     }
     if (heavy_walker && lane == 0) {
