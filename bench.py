@@ -227,13 +227,15 @@ def run_replica_path(args, device):
     mirror): per op, prepare -> prefetch (the body's DMA from the registered message pool starts)
     -> commit -> compact, serially, one C2 prepare of 8190 transfers each (src/vsr/replica.zig:
     3045-3102); without and with the groove write-back in compact: one bar behind (asynchronous), at each
-    bar's last op (synchronous, round 4's Zig wrapper) and one op behind with every bar complete at its
-    last op (the Zig wrapper's shape since round 5)."""
+    bar's last op (synchronous: the Zig wrapper's default), one bar behind with the bars of every
+    checkpoint op and trigger synchronous (a 1024-slot journal, src/config.zig:136; the Zig wrapper
+    with engine_write_back_behind) and one op behind with every bar complete at its last op."""
     import subprocess
     exe = os.path.join(ROOT, "tigerbeetle_amd", "host", "tb_replica_bench")
     out = {}
     for name, opts in (("in_memory", []), ("in_memory_staged", ["--stage"]), ("with_write_back", ["--write-back"]),
                        ("with_write_back_sync", ["--write-back-sync"]),
+                       ("with_write_back_behind_checkpoints", ["--write-back", "--checkpoint-journal-slots", "1024"]),
                        ("with_write_back_per_op", ["--write-back-per-op"])):
         cmd = [exe, "--accounts", str(args.accounts), "--prepares", str(args.replica_prepares),
                "--device", str(device)] + opts

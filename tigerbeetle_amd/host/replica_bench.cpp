@@ -48,8 +48,8 @@ double pick(const std::vector<double>& sorted, int p) {
 int main(int argc, char** argv) {
     uint64_t accounts = 1000000, prepares = 2000, warmup = 64;
     int device = 0;
-    bool write_back = false, stage = false, sync_wb = false, per_op_wb = false;
-    uint32_t every = 1;
+    bool write_back = false, stage = false, sync_wb = false, per_op_wb = false, trigger_sync = false;
+    uint32_t every = 1, journal_slots = 0;
     for (int i = 1; i < argc; i++) {
         const std::string a = argv[i];
         auto next = [&]() { return i + 1 < argc ? strtoull(argv[++i], nullptr, 10) : 0ULL; };
@@ -61,6 +61,8 @@ int main(int argc, char** argv) {
         else if (a == "--write-back-sync") write_back = sync_wb = true;
         else if (a == "--write-back-per-op") write_back = per_op_wb = true;
         else if (a == "--write-back-every") { write_back = per_op_wb = true; every = (uint32_t)next(); }
+        else if (a == "--checkpoint-journal-slots") { write_back = true; journal_slots = (uint32_t)next(); }
+        else if (a == "--checkpoint-trigger-sync") trigger_sync = true;
         else if (a == "--no-stage") stage = false;
         else if (a == "--stage") stage = true;
     }
@@ -78,6 +80,8 @@ int main(int argc, char** argv) {
     sm.compact_sync = sync_wb;
     sm.compact_per_op = per_op_wb;
     sm.compact_every = every;
+    sm.checkpoint_journal_slots = journal_slots;
+    sm.checkpoint_trigger_sync = trigger_sync;
     tbgpu_t* E = sm.engine();
 
     // Workload: the engine's generator (C2 shapes, tbgpu_bench.h), copied to host memory.
@@ -168,11 +172,11 @@ int main(int argc, char** argv) {
     std::vector<double> sorted(lat);
     std::sort(sorted.begin(), sorted.end());
     printf("{\"call_path\": \"prepare -> prefetch -> commit -> compact per op (tb::StateMachine, C++)\", "
-           "\"ops\": %llu, \"events_per_op\": %u, \"write_back\": %s, \"write_back_sync\": %s, \"write_back_per_op\": %s, \"write_back_every_ops\": %u, \"prefetch_stages_body\": %s, \"transfers_per_s\": %.1f, "
+           "\"ops\": %llu, \"events_per_op\": %u, \"write_back\": %s, \"write_back_sync\": %s, \"write_back_per_op\": %s, \"write_back_every_ops\": %u, \"checkpoint_journal_slots\": %u, \"prefetch_stages_body\": %s, \"transfers_per_s\": %.1f, "
            "\"ms_per_op\": %.4f, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"p100_ms\": %.4f, \"failed_events\": %llu, "
            "\"written_back_objects\": %llu, \"compact_ms_per_op\": %.4f, \"compact_ms_max\": %.4f}\n",
            (unsigned long long)prepares, batch, write_back ? "true" : "false", sync_wb ? "true" : "false",
-           per_op_wb ? "true" : "false", per_op_wb ? every : 0u, stage ? "true" : "false",
+           per_op_wb ? "true" : "false", per_op_wb ? every : 0u, journal_slots, stage ? "true" : "false",
            prepares * batch / (total_ms / 1e3),
            total_ms / prepares, pick(sorted, 50), pick(sorted, 99), pick(sorted, 100), (unsigned long long)failed,
            (unsigned long long)wb_objects, compact_ms / prepares, compact_max);

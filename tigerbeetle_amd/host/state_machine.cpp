@@ -149,6 +149,15 @@ std::vector<size_t> StateMachine::commit_many(Operation operation, const std::ve
     return std::vector<size_t>(out_lens.begin(), out_lens.end());
 }
 
+bool StateMachine::checkpoint_bar(uint64_t op, uint32_t journal_slots, uint32_t bar, bool trigger_too) {
+    if (journal_slots == 0 || journal_slots <= bar + 1) return false;
+    const uint64_t first = journal_slots - bar - 1, every = journal_slots - bar;  // checkpoint_after
+    if (op < first) return false;
+    const uint64_t r = (op - first) % every;
+    // A checkpoint op (its bar is flushed by the trigger bar's compaction); optionally the trigger too.
+    return r == 0 || (trigger_too && r == bar);
+}
+
 void StateMachine::compact(const Callback& callback, uint64_t op) {
     // The HBM tables need no compaction; the durable copy gets each bar's changes, one bar behind.
     const bool bar_end = lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0;
@@ -164,8 +173,11 @@ void StateMachine::compact(const Callback& callback, uint64_t op) {
         wb_inflight_ = wb_bar_;
         wb_bar_ ^= 1;
         if (bar_end) wb_deliver_inflight();  // the bar ends with its own objects
-    } else if (write_back && lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0 && compact_sync) {
-        write_back(checkpoint_delta());  // the Zig wrapper's shape: the bar's objects before compact returns
+    } else if (write_back && lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0 &&
+               (compact_sync || checkpoint_bar(op, checkpoint_journal_slots, lsm_batch_multiple, checkpoint_trigger_sync))) {
+        // The bar's objects before compact returns (the in-flight bar first, in checkpoint_delta):
+        // the Zig wrapper's synchronous shape, and its checkpoint bars with engine_write_back_behind.
+        write_back(checkpoint_delta());
     } else if (write_back && lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0) {
         wb_deliver_inflight();  // the previous bar's objects: landed while this bar committed
         reserve_write_back();

@@ -199,6 +199,13 @@ public:
     // With compact_per_op: capture every this many ops (a chunk of the bar) instead of every op; the
     // bar's last op still waits for its own chunk.
     uint32_t compact_every = 1;
+    // One bar behind, except the bar ending at a checkpoint op (a journal of this many slots:
+    // vsr.Checkpoint.checkpoint_after, src/vsr.zig:2009-2021), written back synchronously (the
+    // in-flight bar first): the shape zig/state_machine_gpu.zig runs with engine_write_back_behind.
+    // 0: no checkpoint bars.
+    uint32_t checkpoint_journal_slots = 0;
+    bool checkpoint_trigger_sync = false;  // the trigger's bar synchronous too (A/B)
+    static bool checkpoint_bar(uint64_t op, uint32_t journal_slots, uint32_t bar, bool trigger_too);
     // The replica's message pool (MessagePool.init_capacity, src/message_pool.zig:98-120): buffers
     // registered once, so prefetch stages a prepare body from its message by DMA.
     void register_message_buffer(void* buffer, size_t bytes);

@@ -45,7 +45,7 @@ for what in "$@"; do
         --write-back 0 --cpu-sample 2000000 > $O/bench.json 2> $O/bench.err
       rc=$?; echo "bench rc=$rc"; tail -c 1500 $O/bench.json; tail -5 $O/bench.err; [ $rc -ne 0 ] && exit $rc ;;
     replica)  # the replica call path (C++ mirror) with each write-back shape
-      for m in --write-back --write-back-sync --write-back-per-op "--write-back-every 4" "--write-back-every 8"; do
+      for m in --write-back --write-back-sync "--write-back --checkpoint-journal-slots 1024" --write-back-per-op "--write-back-every 4" "--write-back-every 8"; do
         timeout -k 10 300 tigerbeetle_amd/host/tb_replica_bench --accounts 1000000 --prepares 2000 --device 0 $m \
           > "$O/replica$m.json" 2> "$O/replica$m.err"
         rc=$?; echo "replica $m rc=$rc"; cat "$O/replica$m.json"; [ $rc -ne 0 ] && { tail -3 "$O/replica$m.err"; exit $rc; }

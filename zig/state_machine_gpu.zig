@@ -94,6 +94,18 @@ pub fn StateMachineType(
             /// pageable memory, and the engine pins nothing it does not own (test / fuzzer / replay
             /// buffers from any allocator stay safe).
             engine_register_messages: bool = false,
+            /// compact() writes each bar back ONE BAR BEHIND (tbgpu_checkpoint_delta_async: bar k's
+            /// objects cross PCIe while bar k+1 commits and reach the grooves at bar k+1's end),
+            /// except the bar ending at a checkpoint op, which drains synchronously
+            /// (write_back_synchronous): its objects must be in its own table_mutable, which the
+            /// trigger bar's compaction flushes before the checkpoint (src/lsm/tree.zig:1078-1099,
+            /// src/vsr.zig:2009-2037); a later bar in flight at the checkpoint is replayed from the
+            /// WAL.  The bound this needs: the checkpoint bar's table_mutable receives two bars of
+            /// objects (the one in flight and its own), so every groove tree must be sized for
+            /// 2 x value_count_max (src/state_machine.zig:100-178 — a constant doubled in the fork
+            /// that links this wrapper); every other bar's table receives one.  Off: each bar is
+            /// written back synchronously at its last op (one bar per table, ~4 ms per bar).
+            engine_write_back_behind: bool = false,
 
             fn base(options: Options) Base.Options {
                 return .{
@@ -117,6 +129,48 @@ pub fn StateMachineType(
         // Objects one prepare can read (the groove prefetch_entries_max, :1091-1146).
         const prepare_accounts_max = @max(constants.batch_max.create_accounts, 2 * constants.batch_max.create_transfers);
         const prepare_transfers_max = 2 * constants.batch_max.create_transfers;
+
+        /// One bar's write-back buffers (registered with the engine; the DMA target of a delta).
+        const WriteBack = struct {
+            accounts: []Account,
+            accounts_before: [][4]u128,
+            transfers: []Transfer,
+            posted: [][2]u64,
+
+            fn alloc(allocator: mem.Allocator) !WriteBack {
+                const accounts = try allocator.alloc(Account, bar_accounts_max);
+                errdefer allocator.free(accounts);
+                const accounts_before = try allocator.alloc([4]u128, bar_accounts_max);
+                errdefer allocator.free(accounts_before);
+                const transfers = try allocator.alloc(Transfer, bar_transfers_max);
+                errdefer allocator.free(transfers);
+                const posted = try allocator.alloc([2]u64, bar_transfers_max);
+                return .{ .accounts = accounts, .accounts_before = accounts_before, .transfers = transfers, .posted = posted };
+            }
+
+            fn free(set: *const WriteBack, allocator: mem.Allocator) void {
+                allocator.free(set.posted);
+                allocator.free(set.transfers);
+                allocator.free(set.accounts_before);
+                allocator.free(set.accounts);
+            }
+
+            fn register(set: *const WriteBack, engine: *tbgpu.tbgpu_t) bool {
+                inline for (.{ set.accounts, set.accounts_before, set.transfers, set.posted }) |buffer| {
+                    const bytes = mem.sliceAsBytes(buffer);
+                    if (tbgpu.tbgpu_register_host(engine, @constCast(bytes.ptr), bytes.len) != tbgpu.TBGPU_STATUS_OK) {
+                        return false;
+                    }
+                }
+                return true;
+            }
+
+            fn unregister(set: *const WriteBack, engine: *tbgpu.tbgpu_t) void {
+                inline for (.{ set.accounts, set.accounts_before, set.transfers, set.posted }) |buffer| {
+                    check(tbgpu.tbgpu_unregister_host(engine, mem.sliceAsBytes(buffer).ptr));
+                }
+            }
+        };
 
         const PrefetchContext = union(enum) {
             accounts: AccountsGroove.PrefetchContext,
@@ -157,11 +211,14 @@ pub fn StateMachineType(
         compact_callback: ?*const fn (*StateMachine) void = null,
         checkpoint_callback: ?*const fn (*StateMachine) void = null,
 
+        /// Write-back sets in use: 1 (synchronous), 2 (engine_write_back_behind: one in flight).
+        writeback_sets: u2,
+        /// The set whose delta is in flight (engine_write_back_behind), and the next free one.
+        writeback_inflight: ?u1 = null,
+        writeback_next: u1 = 0,
+
         // Static allocation (allocated in init, never resized).
-        writeback_accounts: []Account,
-        writeback_accounts_before: [][4]u128,
-        writeback_transfers: []Transfer,
-        writeback_posted: [][2]u64,
+        writeback: [2]WriteBack,
         load_accounts: []Account,
         load_transfers: []Transfer,
         load_posted: []u8,
@@ -187,14 +244,13 @@ pub fn StateMachineType(
             if (tbgpu.tbgpu_init(&engine_config, &engine) != tbgpu.TBGPU_STATUS_OK) return error.EngineInit;
             errdefer tbgpu.tbgpu_deinit(engine);
 
-            const writeback_accounts = try allocator.alloc(Account, bar_accounts_max);
-            errdefer allocator.free(writeback_accounts);
-            const writeback_accounts_before = try allocator.alloc([4]u128, bar_accounts_max);
-            errdefer allocator.free(writeback_accounts_before);
-            const writeback_transfers = try allocator.alloc(Transfer, bar_transfers_max);
-            errdefer allocator.free(writeback_transfers);
-            const writeback_posted = try allocator.alloc([2]u64, bar_transfers_max);
-            errdefer allocator.free(writeback_posted);
+            // A node engine writes back synchronously (tbgpu_checkpoint_delta_async is single-device).
+            const sets: u2 = if (options.engine_write_back_behind and options.engine_devices.len < 2) 2 else 1;
+            var writeback: [2]WriteBack = undefined;
+            writeback[0] = try WriteBack.alloc(allocator);
+            errdefer writeback[0].free(allocator);
+            writeback[1] = if (sets == 2) try WriteBack.alloc(allocator) else writeback[0];
+            errdefer if (sets == 2) writeback[1].free(allocator);
             const load_accounts = try allocator.alloc(Account, prepare_accounts_max);
             errdefer allocator.free(load_accounts);
             const load_transfers = try allocator.alloc(Transfer, prepare_transfers_max);
@@ -210,11 +266,8 @@ pub fn StateMachineType(
             errdefer registered_messages.deinit(allocator);
 
             // The write-back buffers receive each bar's delta by DMA (registered once).
-            inline for (.{ writeback_accounts, writeback_accounts_before, writeback_transfers, writeback_posted }) |buffer| {
-                const bytes = mem.sliceAsBytes(buffer);
-                if (tbgpu.tbgpu_register_host(engine.?, @constCast(bytes.ptr), bytes.len) != tbgpu.TBGPU_STATUS_OK) {
-                    return error.EngineInit;
-                }
+            for (writeback[0..sets]) |*set| {
+                if (!set.register(engine.?)) return error.EngineInit;
             }
 
             return StateMachine{
@@ -222,10 +275,8 @@ pub fn StateMachineType(
                 .commit_timestamp = 0,
                 .forest = forest,
                 .engine = engine.?,
-                .writeback_accounts = writeback_accounts,
-                .writeback_accounts_before = writeback_accounts_before,
-                .writeback_transfers = writeback_transfers,
-                .writeback_posted = writeback_posted,
+                .writeback_sets = sets,
+                .writeback = writeback,
                 .load_accounts = load_accounts,
                 .load_transfers = load_transfers,
                 .load_posted = load_posted,
@@ -242,18 +293,18 @@ pub fn StateMachineType(
             var it = self.registered_messages.keyIterator();
             while (it.next()) |address| check(tbgpu.tbgpu_unregister_host(self.engine, @ptrFromInt(address.*)));
             self.registered_messages.deinit(allocator);
-            inline for (.{ self.writeback_accounts, self.writeback_accounts_before, self.writeback_transfers, self.writeback_posted }) |buffer| {
-                check(tbgpu.tbgpu_unregister_host(self.engine, mem.sliceAsBytes(buffer).ptr));
+            if (self.writeback_inflight != null) {
+                var counts: tbgpu.tbgpu_delta_counts = undefined;
+                check(tbgpu.tbgpu_checkpoint_delta_wait(self.engine, &counts)); // its buffers go away below
+                self.writeback_inflight = null;
             }
+            for (self.writeback[0..self.writeback_sets]) |*set| set.unregister(self.engine);
             allocator.free(self.cold_flags);
             allocator.free(self.cold_ids);
             allocator.free(self.load_posted);
             allocator.free(self.load_transfers);
             allocator.free(self.load_accounts);
-            allocator.free(self.writeback_posted);
-            allocator.free(self.writeback_transfers);
-            allocator.free(self.writeback_accounts_before);
-            allocator.free(self.writeback_accounts);
+            for (self.writeback[0..self.writeback_sets]) |*set| set.free(allocator);
             tbgpu.tbgpu_deinit(self.engine);
             self.forest.deinit(allocator);
         }
@@ -556,7 +607,14 @@ pub fn StateMachineType(
         pub fn compact(self: *StateMachine, callback: *const fn (*StateMachine) void, op: u64) void {
             assert(self.compact_callback == null);
             assert(self.checkpoint_callback == null);
-            if ((op + 1) % config.lsm_batch_multiple == 0) self.write_back();
+            if ((op + 1) % config.lsm_batch_multiple == 0) {
+                if (self.writeback_sets == 2 and !write_back_synchronous(op)) {
+                    self.write_back_behind();
+                } else {
+                    self.write_back_deliver(); // the bar in flight first: the grooves take bars in order
+                    self.write_back();
+                }
+            }
             self.compact_callback = callback;
             self.forest.compact(compact_finish, op);
         }
@@ -573,25 +631,67 @@ pub fn StateMachineType(
         /// (which the groove must hold to diff the balance index trees: the engine returns the
         /// previous balances; the cache gets the old object first if it is not there).
         fn write_back(self: *StateMachine) void {
+            assert(self.writeback_inflight == null);
+            const set = &self.writeback[self.writeback_next];
             var counts: tbgpu.tbgpu_delta_counts = undefined;
             const status = tbgpu.tbgpu_checkpoint_delta(
                 self.engine,
-                self.writeback_accounts.ptr,
-                self.writeback_accounts_before.ptr,
-                self.writeback_accounts.len,
-                self.writeback_transfers.ptr,
-                self.writeback_transfers.len,
-                @ptrCast(self.writeback_posted.ptr),
-                self.writeback_posted.len,
+                set.accounts.ptr,
+                set.accounts_before.ptr,
+                set.accounts.len,
+                set.transfers.ptr,
+                set.transfers.len,
+                @ptrCast(set.posted.ptr),
+                set.posted.len,
                 &counts,
             );
             // The buffers hold one bar's worth, the most a bar can change: STATUS_INVALID with
             // larger counts would mean the engine changed more objects than a bar's commits can
             // (an invariant failure, like the reference's TableMemory.put assert), so it panics.
             check(status);
+            self.write_back_apply(set, &counts);
+        }
+
+        /// Checkpoint ops (vsr.Checkpoint.checkpoint_after: the first at journal_slot_count -
+        /// lsm_batch_multiple - 1, then every journal_slot_count - lsm_batch_multiple ops): the bar
+        /// ending there reaches the grooves before compact returns, with the bar in flight first.
+        fn write_back_synchronous(op: u64) bool {
+            const first = global_constants.journal_slot_count - global_constants.lsm_batch_multiple - 1;
+            const every = global_constants.journal_slot_count - global_constants.lsm_batch_multiple;
+            return op >= first and (op - first) % every == 0;
+        }
+
+        /// engine_write_back_behind: the previous bar's objects (landed while this bar committed)
+        /// into the grooves, then this bar's capture started into the other set.
+        fn write_back_behind(self: *StateMachine) void {
+            self.write_back_deliver();
+            const set = &self.writeback[self.writeback_next];
+            check(tbgpu.tbgpu_checkpoint_delta_async(
+                self.engine,
+                set.accounts.ptr,
+                set.accounts_before.ptr,
+                set.accounts.len,
+                set.transfers.ptr,
+                set.transfers.len,
+                @ptrCast(set.posted.ptr),
+                set.posted.len,
+            ));
+            self.writeback_inflight = self.writeback_next;
+            self.writeback_next ^= 1;
+        }
+
+        fn write_back_deliver(self: *StateMachine) void {
+            const inflight = self.writeback_inflight orelse return;
+            self.writeback_inflight = null;
+            var counts: tbgpu.tbgpu_delta_counts = undefined;
+            check(tbgpu.tbgpu_checkpoint_delta_wait(self.engine, &counts));
+            self.write_back_apply(&self.writeback[inflight], &counts);
+        }
+
+        fn write_back_apply(self: *StateMachine, set: *const WriteBack, counts: *const tbgpu.tbgpu_delta_counts) void {
             defer self.evict_if_full();
             const grooves = &self.forest.grooves;
-            for (self.writeback_accounts[0..counts.accounts], self.writeback_accounts_before[0..counts.accounts]) |*a, before| {
+            for (set.accounts[0..counts.accounts], set.accounts_before[0..counts.accounts]) |*a, before| {
                 if (a.timestamp > counts.created_after) {
                     grooves.accounts.insert(a); // created since the previous write-back
                     continue;
@@ -608,8 +708,8 @@ pub fn StateMachineType(
                 }
                 grooves.accounts.upsert(a);
             }
-            for (self.writeback_transfers[0..counts.transfers]) |*t| grooves.transfers.insert(t);
-            for (self.writeback_posted[0..counts.posted]) |pair| {
+            for (set.transfers[0..counts.transfers]) |*t| grooves.transfers.insert(t);
+            for (set.posted[0..counts.posted]) |pair| {
                 grooves.posted.insert(&PostedGrooveValue{
                     .timestamp = pair[0],
                     .fulfillment = if (pair[1] == 0) .posted else .voided,
@@ -634,6 +734,8 @@ pub fn StateMachineType(
         pub fn checkpoint(self: *StateMachine, callback: *const fn (*StateMachine) void) void {
             assert(self.compact_callback == null);
             assert(self.checkpoint_callback == null);
+            // A bar in flight here (the trigger's) is not part of this checkpoint: its ops are after
+            // the checkpoint op, so a restart replays them; it reaches the grooves one bar behind.
             self.checkpoint_callback = callback;
             self.forest.checkpoint(checkpoint_finish);
         }
