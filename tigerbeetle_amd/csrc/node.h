@@ -35,6 +35,7 @@
 // the pass is sequenced.
 #pragma once
 
+#include <chrono>
 #include <thread>
 
 #include "k_node.h"
@@ -140,6 +141,11 @@ struct TbNode {
     NodePass ring[NODE_PASS_RING];   // a call's passes, built as they are planned (no per-call allocation)
     std::vector<u64> ring_off;       // their offset tables
     u64 drained_at = ~0ULL;          // its value when a create_transfers call last ended drained
+    // TBGPU_NODE_TIMING=1 (set at init): host time per phase of create_transfers calls, printed at
+    // deinit — plan issue, plan wait, commit issue, replies issue, consume wait, whole call.
+    bool timing = false;
+    double t_us[6] = {};
+    u64 t_calls = 0;
     unsigned __int128 bound_carry = 0;  // the node's balance bound at that point (host-tracked)
 };
 
@@ -158,8 +164,27 @@ static u32 node_home(const u8* rec16, u32 world) {
     return tb_home(w[0], w[1], world);
 }
 
+struct NodeTimer {  // adds the scope's host time to N->t_us[k] when N->timing
+    TbNode* N;
+    int k;
+    std::chrono::steady_clock::time_point t0;
+    NodeTimer(TbNode* n, int kk) : N(n), k(kk) {
+        if (N->timing) t0 = std::chrono::steady_clock::now();
+    }
+    ~NodeTimer() {
+        if (N->timing) N->t_us[k] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    }
+};
+
 static void node_free(TbNode* N) {
     if (!N) return;
+    if (N->timing && N->t_calls) {
+        const double c = (double)N->t_calls;
+        fprintf(stderr, "tbgpu node timing (us per create_transfers call, %llu calls): plan_issue %.1f plan_wait %.1f "
+                        "commit_issue %.1f replies_issue %.1f consume_wait %.1f call %.1f\n",
+                (unsigned long long)N->t_calls, N->t_us[0] / c, N->t_us[1] / c, N->t_us[2] / c, N->t_us[3] / c,
+                N->t_us[4] / c, N->t_us[5] / c);
+    }
     for (u32 d = 0; d < N->world; d++) {
         NodeDev& D = N->D[d];
         if (D.E) {
@@ -209,6 +234,7 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
         }
     }
     TbNode* N = new TbNode();
+    if (const char* t = getenv("TBGPU_NODE_TIMING")) N->timing = atoi(t) != 0;
     N->world = W;
     N->pe_src = config->pass_events_max;
     N->pb_src = config->pass_batches_max;
@@ -556,6 +582,7 @@ static bool node_block_resident(const NodeDev& D, const NodePass& P, u32 d, cons
 // H2D of source d's block of pass p and its route plan (enqueued; ev_planned[p & 1] fires when the
 // plan's words are in pinned host memory).
 static int node_issue_plan(TbNode* N, NodePass& P, u32 p, const u64* ts, const void* const* inputs, const u32* lens) {
+    NodeTimer timer(N, 0);
     const u32 par = p & 1;
     for (u32 d = 0; d < N->world; d++) {
         NodeDev& D = N->D[d];
@@ -650,7 +677,10 @@ static int node_read_plan(TbNode* N, const NodePass& P, u32 p, NodePlan* out) {
         if (P.blk[d].k1 == P.blk[d].k0) continue;
         NodeDev& D = N->D[d];
         NCK(hipSetDevice(D.device));
-        NCK(hipEventSynchronize(D.ev_planned[par]));
+        {
+            NodeTimer timer(N, 1);
+            NCK(hipEventSynchronize(D.ev_planned[par]));
+        }
         const u64* w = D.h_words[par];
         if (w[RW_HUGE]) out->huge = true;
         for (int i = 0; i < SUM_SHARDS && !out->huge; i++) {
@@ -698,6 +728,7 @@ static int node_issue_replies(TbNode* N, NodePass& P, u32 p, const NodeRoute& X,
 // replies = false (a split pass): the sources' replies wait for the sequencer (node_issue_replies).
 static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, u32 cert, u64 ts_max,
                              bool replies = true) {
+    NodeTimer timer(N, 2);
     const u32 W = N->world, par = p & 1, tri = p % 3;
     NodeRoute RT;
     node_route(N, PL, RT);
@@ -795,6 +826,7 @@ static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, 
 // 3. Sources: replies from the codes their homes wrote (and, for a split pass, the sequencer's codes
 // of the events it committed: seq_codes, the whole pass block-major), into the reply arena.
 static int node_issue_replies(TbNode* N, NodePass& P, u32 p, const NodeRoute& RT, const u8* seq_codes) {
+    NodeTimer timer(N, 3);
     const u32 W = N->world, par = p & 1, tri = p % 3;
     u64 base = 0;
     for (u32 s = 0; s < W; s++) {
@@ -838,7 +870,10 @@ static int node_consume(TbNode* N, NodePass& P, u32 p, void* const* outputs, u32
         const NodeBlock& B = P.blk[s];
         const u32 nb = B.k1 - B.k0;
         NCK(hipSetDevice(D.device));
-        NCK(hipEventSynchronize(D.ev_done[tri]));
+        {
+            NodeTimer timer(N, 4);
+            NCK(hipEventSynchronize(D.ev_done[tri]));
+        }
         if (!take || status) continue;
         const u64* head = (const u64*)D.h_arena[tri];
         const u32* rb = (const u32*)(D.h_arena[tri] + 16);
@@ -1124,6 +1159,8 @@ static int node_split_pass(TbNode* N, NodePass& P, u32 p, const u64* ts, u64 bou
 // The node's commit of n create_transfers prepares from host memory.
 static int node_commit_transfers(TbNode* N, u32 n, const u64* ts, const void* const* inputs, const u32* lens,
                                  void* const* outputs, u32* out_lens, u32 chunk, double* latency_ms) {
+    NodeTimer timer(N, 5);
+    N->t_calls++;
     typedef unsigned __int128 h128;
     const u32 W = N->world;
     const u32 per = std::max<u32>(1, std::min<u32>(chunk ? chunk : N->pb_src, N->pb_src));
