@@ -151,8 +151,12 @@ enum : u32 { CERT_EXT_U128 = 1, CERT_EXT_U64 = 2 };
 // Legs limits: a bucket's accumulators live in LDS (4 fields x 8 B per slot), the per-prepare
 // bucket histogram in the resolve workgroup's LDS, the per-prepare segment table in the apply
 // workgroup's LDS.
+#ifndef LEG_SLOTS_MAX
 #define LEG_SLOTS_MAX 1024
+#endif
+#ifndef LEG_BUCKETS_PREF  // -DLEG_BUCKETS_PREF=... builds an A/B variant
 #define LEG_BUCKETS_PREF 2048
+#endif
 #define LEG_BUCKETS_MAX 4096  // u16 counters: 8 KB of tb_resolve's LDS (under 80 KB: two workgroups per CU)
 #define LEG_PREPARES_MAX 1024
 #define LEG_SPLIT_MIN 65536  // tb_apply_legs splits a bucket with at least this many legs in the pass
@@ -162,7 +166,9 @@ enum : u32 { CERT_EXT_U128 = 1, CERT_EXT_U64 = 2 };
 #endif
 // Leg word: ((slot within its bucket) << 2 | balance field (BAL_OFF / 16)) << LEG_AMT_BITS | amount.
 // An amount of 2^LEG_AMT_BITS or more is applied by the resolve kernel with an atomic instead.
+#ifndef LEG_AMT_BITS
 #define LEG_AMT_BITS 52  // leaves 12 bits: slot-in-bucket (<= 10, LEG_SLOTS_MAX) + field (2)
+#endif
 #define LEG_AMT_MASK ((1ULL << LEG_AMT_BITS) - 1)
 static_assert((1u << (64 - LEG_AMT_BITS - 2)) >= LEG_SLOTS_MAX, "leg word: slot-in-bucket field too narrow");
 
