@@ -966,14 +966,14 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         hipLaunchKernelGGL(tb_pass_clear, dim3(clear_grid), dim3(256), 0, E->stream, E->dedup, E->dedup_cap, E->sum_shards,
                            E->g, E->epoch, E->dedup_force ? 1u : 0u, E->leg_tot, E->leg_buckets, meta_dst,
                            inline_meta ? inline_meta[0] : 0, inline_meta ? inline_meta[1] : 0, inline_meta ? inline_meta[2] : 0,
-                           P.kclock);
+                           P.kclock, imp ? imp->count : nullptr, imp && b0 == 0 ? imp->leg_counts : nullptr,
+                           imp && b0 == 0 ? imp->legs_n : 0u);
         HIPCK(hipGetLastError());
         E->dedup_force = false;
         E->dedup_prev = P.dedup_mask + 1;
         if ((st = prof_end(E, &pp))) return st;
 
         if (imp && n > 0) {  // a node home: the foreign accounts this sub-pass names, from their owners
-            HIPCK(hipMemsetAsync(imp->count, 0, 8, E->stream));
             const u32 ig = (u32)std::min<u64>(4096, (n + 255) / 256);
             hipLaunchKernelGGL(tb_node_import, dim3(ig), dim3(256), 0, E->stream, E->T, imp->N, events_dev + P.e0 * 128, n,
                                imp->self, imp->list, imp->count, imp->cap, imp->os_of);

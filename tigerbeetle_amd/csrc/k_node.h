@@ -299,9 +299,11 @@ struct NodeImport {
     NodeTablesArgs N;
     u32 self;
     u32* list;     // [cap] slots inserted
-    u64* count;
+    u64* count;    // zeroed by the sub-pass's tb_pass_clear
     u64 cap;
     u32* os_of;    // [account_cap] imported slot -> the account's slot on its owner
+    u64* leg_counts = nullptr;  // the home's per-owner leg counts, zeroed by the same tb_pass_clear
+    u32 legs_n = 0;
 };
 
 __global__ void tb_node_import_clear(Tables H, const u32* list, const u64* count) {

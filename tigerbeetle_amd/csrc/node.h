@@ -144,6 +144,14 @@ struct TbNode {
     // TBGPU_NODE_TIMING=1 (set at init): host time per phase of create_transfers calls, printed at
     // deinit — plan issue, plan wait, commit issue, replies issue, consume wait, whole call.
     bool timing = false;
+    bool latency_on = false;  // the current call asked for per-prepare latencies (ev_start recorded)
+    // Host memory registered through the node (node_api_register_host): a block in it is not in
+    // HBM, known without asking the runtime per pass.
+    struct HostRegion {
+        const u8* p;
+        u64 n;
+    } host_reg[64];
+    u32 n_host_reg = 0;
     double t_us[6] = {};
     u64 t_calls = 0;
     unsigned __int128 bound_carry = 0;  // the node's balance bound at that point (host-tracked)
@@ -563,10 +571,14 @@ static int node_commit_accounts(TbNode* N, u32 n, const u64* ts, const void* con
 // Is source d's block of the pass already in d's HBM, its prepares back to back?  (Then the route
 // kernels read it in place: the node's device-resident commit, the prepares generated or received
 // on each GPU.)
-static bool node_block_resident(const NodeDev& D, const NodePass& P, u32 d, const void* const* inputs, const u32* lens) {
+static bool node_block_resident(const TbNode* N, const NodeDev& D, const NodePass& P, u32 d, const void* const* inputs,
+                                const u32* lens) {
     const NodeBlock& B = P.blk[d];
     if (B.k1 == B.k0 || B.events == 0) return false;
     const u8* base = (const u8*)inputs[B.k0];
+    for (u32 i = 0; i < N->n_host_reg; i++) {
+        if (base >= N->host_reg[i].p && base < N->host_reg[i].p + N->host_reg[i].n) return false;
+    }
     for (u32 k = B.k0; k < B.k1; k++) {
         if ((const u8*)inputs[k] != base + P.off[d][k - B.k0] * 128) return false;
     }
@@ -599,12 +611,12 @@ static int node_issue_plan(TbNode* N, NodePass& P, u32 p, const u64* ts, const v
         // read where they are.  Otherwise the copy stream moves them (runs of address-contiguous
         // prepares as one DMA; host memory over the device's own PCIe link, another device's HBM
         // over xGMI).
-        NCK(hipEventRecord(D.ev_start[p % 3], E->copy_stream));
+        if (N->latency_on) NCK(hipEventRecord(D.ev_start[p % 3], E->copy_stream));
         // The sequencer of the split pass two passes back may still be reading this parity's buffers.
         NCK(hipStreamWaitEvent(E->copy_stream, N->ev_xread, 0));
         NCK(hipStreamWaitEvent(D.rs, N->ev_xread, 0));
         D.ev[par] = D.stage[par];
-        if (node_block_resident(D, P, d, inputs, lens)) {
+        if (node_block_resident(N, D, P, d, inputs, lens)) {
             D.ev[par] = (const u8*)inputs[B.k0];
         } else {
             for (u32 k = B.k0; k < B.k1;) {
@@ -762,13 +774,15 @@ static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, 
             NCK(hipGetLastError());
         }
         NCK(hipEventRecord(D.ev_gathered, E->stream));
+        // The previous pass's readers of this home's legs and codes: every shard's owner apply and
+        // replies.  Both run on that shard's stream, the replies after the apply (node_issue_replies,
+        // also for a split pass), so its latest replies event covers both.
         for (u32 o = 0; o < W; o++) {
             NCK(hipSetDevice(D.device));
-            NCK(hipStreamWaitEvent(E->stream, N->D[o].ev_applied, 0));
             NCK(hipStreamWaitEvent(E->stream, N->D[o].ev_replied, 0));
         }
         NCK(hipSetDevice(D.device));
-        NCK(hipMemsetAsync(D.leg_counts, 0, (u64)W * 8, E->stream));
+        if (!nh[h]) NCK(hipMemsetAsync(D.leg_counts, 0, (u64)W * 8, E->stream));  // (otherwise: tb_pass_clear)
         if (nh[h]) {
             const u64 per = BATCH_EVENTS_MAX - 1;
             const u64 nb = (nh[h] + per - 1) / per;
@@ -779,7 +793,10 @@ static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, 
                 h_off[k + 1] = std::min<u64>(nh[h], h_off[k] + per);
                 h_ts[k] = ts_max;
             }
-            NCK(hipMemcpyAsync(D.hmeta_dev[tri], h_off, (2 * nb + 1) * 8, hipMemcpyHostToDevice, E->stream));
+            // One pseudo-prepare (a pass of up to 8191 routed events, the one-prepare call's): its
+            // offsets and timestamp written by tb_pass_clear from kernel arguments, no copy.
+            const u64 im[3] = {0, nh[h], ts_max};
+            if (nb > 1) NCK(hipMemcpyAsync(D.hmeta_dev[tri], h_off, (2 * nb + 1) * 8, hipMemcpyHostToDevice, E->stream));
             OwnerLegArgs O{W, h, D.legs, 2 * nh[h], D.leg_counts, D.imp_os, NODE_LEG_WORDS};
             NodeImport imp{};
             imp.N.world = W;
@@ -789,8 +806,10 @@ static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, 
             imp.count = D.imp_count;
             imp.cap = D.imp_cap;
             imp.os_of = D.imp_os;
+            imp.leg_counts = D.leg_counts;
+            imp.legs_n = W;
             const int st = enqueue_call(E, OP_CREATE_TRANSFERS, (u32)nb, h_off, D.recv, E->results, E->reply_bytes,
-                                        true, D.codes, cert, nullptr, D.hmeta_dev[tri], &O, nullptr, &imp);
+                                        true, D.codes, cert, nullptr, D.hmeta_dev[tri], &O, nb == 1 ? im : nullptr, &imp);
             if (st) return st;
         }
         NCK(hipEventRecord(D.ev_committed, E->stream));
@@ -1161,6 +1180,7 @@ static int node_commit_transfers(TbNode* N, u32 n, const u64* ts, const void* co
                                  void* const* outputs, u32* out_lens, u32 chunk, double* latency_ms) {
     NodeTimer timer(N, 5);
     N->t_calls++;
+    N->latency_on = latency_ms != nullptr;
     typedef unsigned __int128 h128;
     const u32 W = N->world;
     const u32 per = std::max<u32>(1, std::min<u32>(chunk ? chunk : N->pb_src, N->pb_src));
@@ -1667,6 +1687,7 @@ static int node_api_get_stats(TbNode* N, tbgpu_stats* s) {
 static int node_api_register_host(TbNode* N, void* ptr, u64 bytes) {
     NCK(hipSetDevice(N->D[0].device));
     NCK(hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    if (N->n_host_reg < 64) N->host_reg[N->n_host_reg++] = {(const u8*)ptr, bytes};
     return TBGPU_STATUS_OK;
 }
 
@@ -1675,6 +1696,12 @@ static int node_api_unregister_host(TbNode* N, void* ptr) {
     if (st) return st;
     NCK(hipSetDevice(N->D[0].device));
     NCK(hipHostUnregister(ptr));
+    for (u32 i = 0; i < N->n_host_reg; i++) {
+        if (N->host_reg[i].p == (const u8*)ptr) {
+            N->host_reg[i] = N->host_reg[--N->n_host_reg];
+            break;
+        }
+    }
     return TBGPU_STATUS_OK;
 }
 
