@@ -21,7 +21,7 @@ AF_DEBITS_MUST_NOT_EXCEED_CREDITS = 1 << 1
 AF_CREDITS_MUST_NOT_EXCEED_DEBITS = 1 << 2
 
 
-def mixed_limits(n_acc, n_xfer, seed):
+def mixed_limits(n_acc, n_xfer, seed, wide=False):
     rng = np.random.default_rng(seed)
     acc = np.zeros(n_acc, dtype=ACCOUNT_DTYPE)
     acc["id_lo"] = np.arange(1, n_acc + 1)
@@ -43,6 +43,11 @@ def mixed_limits(n_acc, n_xfer, seed):
     x["debit_account_id_lo"] = dr + 1
     x["credit_account_id_lo"] = cr + 1
     x["amount_lo"] = rng.integers(1, 1000, n_xfer)
+    if wide:
+        # A third of the amounts between 2^22 and 2^40: the walkers' 64-bit runs and bounded walks
+        # (fl_walk_run's wide path, pending credits of 2^28 and more carried across windows).
+        big = rng.random(n_xfer) < 0.33
+        x["amount_lo"][big] = rng.integers(1 << 22, 1 << 40, int(big.sum()))
     x["ledger"] = 1
     x["code"] = 1
     return acc.view(np.uint8), x.view(np.uint8)
@@ -94,3 +99,22 @@ def test_c3_hot_limited(bounds_sweep, walk_merge, gpu_engine_factory):
     st = engine.stats()
     assert st["bounds_passes"] == st["flow_passes"] > 0 and st["bounds_abandoned"] == 0
     assert st["bounds_swept"] > 10_000  # the hot account's checks hover at its limit
+
+
+@pytest.mark.parametrize("bounds_sweep", ["auto", "early"])
+def test_mixed_limit_flags_wide_amounts(bounds_sweep, gpu_engine_factory):
+    """Amounts up to 2^40 mixed with small ones: the walkers' 64-bit paths — the in-order walk, the
+    bounded walk with pending credits too large for 32 bits, the pending credits a heavy walker
+    carries from one window into the next (WalkCarry) — against the oracle."""
+    n_acc, n_xfer, pb = 64, 200_000, 8
+    accts, xfers = mixed_limits(n_acc, n_xfer, seed=5, wide=True)
+    engine = gpu_engine_factory(accounts_max=n_acc, transfers_max=n_xfer, pass_events_max=pb * 8190,
+                                pass_batches_max=pb, bounds_sweep=bounds_sweep)
+    engine.walk_merge_max(0)
+    expected = commit_both(engine, accts, xfers, n_acc, n_xfer)
+    codes = np.frombuffer(b"".join(expected), dtype=np.uint32).reshape(-1, 2)[:, 1]
+    assert (codes == CreateTransferResult.exceeds_credits).any() and (codes == CreateTransferResult.exceeds_debits).any()
+    st = engine.stats()
+    assert st["bounds_passes"] == st["flow_passes"] > 0 and st["bounds_abandoned"] == 0
+    if bounds_sweep == "early":
+        assert st["bounds_swept"] > 0 and st["walk_heavy"] > 0  # heavy segments (a wave each) walked
