@@ -913,6 +913,64 @@ __global__ void tb_seq_writeback_new_accounts(Tables X, SeqSet aset, Tables O, u
     }
 }
 
+// The sequencer's transfer index emptied entry by entry instead of by a whole-table memset (64 MB at
+// C3's pass size, 0.13 ms a split pass): every entry of X's index was claimed for one of its log
+// positions under that position's id — a loaded transfer at [0, loaded) (tb_seq_load_transfers), a
+// sequenced event at [base, base + n) (validate, the ordered run; a withdrawn claim is tombstoned,
+// never emptied) — so scanning each id's chain for the entries naming its position finds them all.
+// Pass 1 lists them with the chains intact; pass 2 empties them, their collision marks and the
+// positions' posted states.  A list past `cap` (it holds 2 entries per position) makes pass 2 empty
+// the whole index instead.
+__global__ void tb_seq_xidx_list(Tables X, const u64* loaded, const u8* events, u64 base, u64 n, u32* list, u64* count,
+                                 u64 cap) {
+    const u64 L = *loaded, total = L + n;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (u64)gridDim.x * blockDim.x) {
+        u64 lo, hi, pos;
+        if (i < L) {
+            lo = tb_lo(X.xlog[i].id);
+            hi = tb_hi(X.xlog[i].id);
+            pos = i;
+        } else {
+            const u64* w = (const u64*)(events + (i - L) * 128);
+            lo = w[0];
+            hi = w[1];
+            pos = base + (i - L);
+        }
+        if (tb_id_reserved(lo, hi)) continue;  // no claim: the event failed before its id check
+        const u64 fp = tb_fp32(lo, hi);
+        u64 p = tb_hash_id(lo, hi) & X.xidx_mask;
+        for (u64 k = 0; k <= X.xidx_mask; k++) {
+            const u64 e = X.xidx[p];
+            if (e == 0) break;
+            if ((e >> 32) == fp && (e & XI_POS_MASK) == pos + 1) {
+                const u64 at = atomicAdd((unsigned long long*)&count[0], 1ULL);
+                if (at < cap) list[at] = (u32)p;
+            }
+            p = (p + 1) & X.xidx_mask;
+        }
+    }
+}
+
+__global__ void tb_seq_xidx_zero(Tables X, const u32* list, const u64* count, const u64* loaded, u64 base, u64 n,
+                                 u64 cap) {
+    const u64 stride = (u64)gridDim.x * blockDim.x, t0 = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u64 m = count[0];
+    if (m > cap) {  // the list overflowed: the whole index
+        for (u64 i = t0; i <= X.xidx_mask; i += stride) {
+            X.xidx[i] = 0;
+            X.xdup[i] = 0;
+        }
+    } else {
+        for (u64 i = t0; i < m; i += stride) {
+            X.xidx[list[i]] = 0;
+            X.xdup[list[i]] = 0;
+        }
+    }
+    const u64 L = *loaded;
+    for (u64 i = t0; i < L; i += stride) X.xposted[i] = 0;
+    for (u64 i = t0; i < n; i += stride) X.xposted[base + i] = 0;
+}
+
 // Empties what the pass put in the sequencer's account table and both sets (by their lists).
 __global__ void tb_seq_clear(SeqSet tset, SeqSet aset, Tables X) {
     const u64 stride = (u64)gridDim.x * blockDim.x;

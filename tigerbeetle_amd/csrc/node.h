@@ -131,6 +131,10 @@ struct TbNode {
     u64* seq_ts = nullptr;       // [world * pe_src] execute timestamps of the compacted events
     u32* seq_blk = nullptr;      // [world * pe_src / 256 + 2] compaction counts / prefix
     AccountBal* seq_bal0 = nullptr;  // [6 * world * pe_src] balances as loaded (delta write-back)
+    u32* xclr_list = nullptr;    // [xclr_cap] the sequencer's index entries a split pass claimed (tb_seq_xidx_list)
+    u64* xclr_count = nullptr;
+    u64 xclr_cap = 0;
+    bool x_index_clean = true;   // the sequencer's transfer index, collision marks and posted states are empty
     hipEvent_t ev_xread = nullptr;   // the sequencer has read the split pass's source buffers
     hipEvent_t ev_x = nullptr;       // the sequencer's results (codes expanded) are final
     u64* h_seq = nullptr;        // pinned scratch words
@@ -218,7 +222,8 @@ static void node_free(TbNode* N) {
     if (N->X) {
         (void)hipSetDevice(N->D[0].device);
         void* dev[] = {N->tset_e, N->aset_e, N->tset_list, N->aset_list, N->seq_counts, N->tset_dups, N->aset_dups,
-                       N->seq_codes, N->seq_xcodes, N->seq_map, N->seq_ts, N->seq_blk, N->seq_bal0};
+                       N->seq_codes, N->seq_xcodes, N->seq_map, N->seq_ts, N->seq_blk, N->seq_bal0, N->xclr_list,
+                       N->xclr_count};
         for (void* p : dev) if (p) (void)hipFree(p);
         if (N->ev_xread) (void)hipEventDestroy(N->ev_xread);
         if (N->ev_x) (void)hipEventDestroy(N->ev_x);
@@ -411,6 +416,9 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
         XALLOC(tbMalloc(&N->seq_ts, pass * 8));
         XALLOC(tbMalloc(&N->seq_blk, (pass / 256 + 2) * 4));
         XALLOC(tbMalloc(&N->seq_bal0, 6 * pass * sizeof(AccountBal)));
+        N->xclr_cap = 2 * (N->seq_tcap + pass);  // two entries per log position (a withdrawn claim and a new one)
+        XALLOC(tbMalloc(&N->xclr_list, N->xclr_cap * 4));
+        XALLOC(tbMalloc(&N->xclr_count, 8));
         XALLOC(tbEventCreateWithFlags(&N->ev_xread, hipEventDisableTiming));
         XALLOC(tbEventCreateWithFlags(&N->ev_x, hipEventDisableTiming));
         XALLOC(hipEventRecord(N->ev_xread, N->X->stream));  // "the previous split pass" exists before the first
@@ -1065,9 +1073,12 @@ static int node_split_pass(TbNode* N, NodePass& P, u32 p, const u64* ts, u64 bou
         NCK(hipStreamWaitEvent(xs, N->D[d].ev_pre, 0));
         NCK(hipStreamWaitEvent(xs, N->D[d].ev_planned[par], 0));  // the classification
     }
-    NCK(hipMemsetAsync(X->T.xidx, 0, X->xidx_cap * 8, xs));
-    NCK(hipMemsetAsync(X->T.xdup, 0, X->xidx_cap, xs));
-    NCK(hipMemsetAsync(X->T.xposted, 0, X->xlog_cap, xs));
+    if (!N->x_index_clean) {  // an earlier split pass ended before its clear (tb_seq_xidx_zero)
+        NCK(hipMemsetAsync(X->T.xidx, 0, X->xidx_cap * 8, xs));
+        NCK(hipMemsetAsync(X->T.xdup, 0, X->xidx_cap, xs));
+        NCK(hipMemsetAsync(X->T.xposted, 0, X->xlog_cap, xs));
+    }
+    N->x_index_clean = false;
     NCK(hipMemsetAsync(N->seq_counts, 0, 8 * 8, xs));
     NCK(hipMemsetAsync(&X->g->commit_timestamp, 0, 8, xs));
     SeqSet tset{N->tset_e, N->tset_mask, N->tset_list, N->seq_counts, N->tset_dups};
@@ -1169,6 +1180,14 @@ static int node_split_pass(TbNode* N, NodePass& P, u32 p, const u64* ts, u64 bou
     for (u32 d = 0; d < W; d++) NCK(hipStreamWaitEvent(xs, N->D[d].ev_xwb, 0));
     hipLaunchKernelGGL(tb_seq_clear, dim3(1024), dim3(256), 0, xs, tset, aset, X->T);
     NCK(hipGetLastError());
+    // The sequencer's transfer index, entry by entry (its claims; the next split pass needs it empty).
+    NCK(hipMemsetAsync(N->xclr_count, 0, 8, xs));
+    hipLaunchKernelGGL(tb_seq_xidx_list, dim3(1024), dim3(256), 0, xs, X->T, (const u64*)(N->seq_counts + 4), X->staging,
+                       N->seq_tcap, n_seq, N->xclr_list, N->xclr_count, N->xclr_cap);
+    hipLaunchKernelGGL(tb_seq_xidx_zero, dim3(1024), dim3(256), 0, xs, X->T, N->xclr_list, N->xclr_count,
+                       (const u64*)(N->seq_counts + 4), N->seq_tcap, n_seq, N->xclr_cap);
+    NCK(hipGetLastError());
+    N->x_index_clean = true;
     if (all) N->passes_whole++;
     else N->passes_split++;
     N->seq_events += n_seq;
