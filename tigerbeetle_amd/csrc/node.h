@@ -35,7 +35,10 @@
 // the pass is sequenced.
 #pragma once
 
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 
 #include "k_node.h"
@@ -106,6 +109,28 @@ struct NodePass {
 };
 #define NODE_PASS_RING 4  // passes alive at once in a call: p - 2 (replies), p - 1, p, p + 1 (planned)
 
+struct TbNode;
+// The node's issue pool: one host thread per shard beyond the first (created at init), so a pass's
+// per-shard work — a source's route plan, a home's routed commit, an owner's legs and a source's
+// replies, each a chain of launches and event operations on that shard's streams — is issued for
+// every shard at once instead of shard after shard (on N GPUs the host would otherwise issue ~N x
+// the work of one pass per pass).  A phase runs its function for every shard and returns when all
+// have; phases that wait on another shard's events of the same pass come after the phase that
+// records them.  Idle workers spin briefly, then sleep on a condition variable.
+typedef int (*NodeShardFn)(TbNode* N, u32 shard, void* ctx);
+struct NodePool {
+    std::vector<std::thread> threads;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<u64> gen{0};
+    std::atomic<u32> done{0};
+    std::atomic<bool> stop{false};
+    NodeShardFn fn = nullptr;
+    void* ctx = nullptr;
+    int status[NODE_WORLD_MAX] = {};
+    std::string err[NODE_WORLD_MAX];
+};
+
 struct TbNode {
     u32 world = 0;
     NodeDev D[NODE_WORLD_MAX];
@@ -148,6 +173,7 @@ struct TbNode {
     // TBGPU_NODE_TIMING=1 (set at init): host time per phase of create_transfers calls, printed at
     // deinit — plan issue, plan wait, commit issue, replies issue, consume wait, whole call.
     bool timing = false;
+    NodePool* pool = nullptr;  // null: every phase issued shard after shard (TBGPU_NODE_THREADS=0)
     bool latency_on = false;  // the current call asked for per-prepare latencies (ev_start recorded)
     // Host memory registered through the node (node_api_register_host): a block in it is not in
     // HBM, known without asking the runtime per pass.
@@ -188,8 +214,69 @@ struct NodeTimer {  // adds the scope's host time to N->t_us[k] when N->timing
     }
 };
 
+static void node_pool_worker(TbNode* N, u32 d) {
+    NodePool& Q = *N->pool;
+    u64 seen = 0;
+    for (;;) {
+        // A job (gen past `seen`) or stop: spin ~50 us, then sleep until notified.
+        for (u32 spin = 0; spin < 20000 && Q.gen.load(std::memory_order_acquire) == seen && !Q.stop.load(); spin++) {
+            __builtin_ia32_pause();
+        }
+        if (Q.gen.load(std::memory_order_acquire) == seen && !Q.stop.load()) {
+            std::unique_lock<std::mutex> lk(Q.mu);
+            Q.cv.wait(lk, [&] { return Q.gen.load(std::memory_order_acquire) != seen || Q.stop.load(); });
+        }
+        if (Q.stop.load()) return;
+        seen = Q.gen.load(std::memory_order_acquire);
+        const int st = Q.fn(N, d, Q.ctx);
+        Q.status[d] = st;
+        if (st) Q.err[d] = g_err;  // (the error text is per thread)
+        Q.done.fetch_add(1, std::memory_order_acq_rel);
+    }
+}
+
+// fn for every shard: shard 0 on the calling thread, the others on the pool.  The first failure's
+// status and text come back to the caller.
+static int node_run(TbNode* N, NodeShardFn fn, void* ctx) {
+    const u32 W = N->world;
+    if (!N->pool) {
+        for (u32 d = 0; d < W; d++) {
+            const int st = fn(N, d, ctx);
+            if (st) return st;
+        }
+        return TBGPU_STATUS_OK;
+    }
+    NodePool& Q = *N->pool;
+    Q.fn = fn;
+    Q.ctx = ctx;
+    Q.done.store(0, std::memory_order_relaxed);
+    Q.gen.fetch_add(1, std::memory_order_acq_rel);
+    { std::lock_guard<std::mutex> lk(Q.mu); }  // a worker checking its wait predicate sees the new gen
+    Q.cv.notify_all();
+    int status = fn(N, 0, ctx);
+    while (Q.done.load(std::memory_order_acquire) < W - 1) __builtin_ia32_pause();
+    for (u32 d = 1; d < W; d++) {
+        if (Q.status[d] && !status) {
+            status = Q.status[d];
+            g_err = Q.err[d];
+        }
+    }
+    return status;
+}
+
+static void node_pool_stop(TbNode* N) {
+    if (!N->pool) return;
+    N->pool->stop.store(true);
+    { std::lock_guard<std::mutex> lk(N->pool->mu); }
+    N->pool->cv.notify_all();
+    for (std::thread& t : N->pool->threads) t.join();
+    delete N->pool;
+    N->pool = nullptr;
+}
+
 static void node_free(TbNode* N) {
     if (!N) return;
+    node_pool_stop(N);
     if (N->timing && N->t_calls) {
         const double c = (double)N->t_calls;
         fprintf(stderr, "tbgpu node timing (us per create_transfers call, %llu calls): plan_issue %.1f plan_wait %.1f "
@@ -248,6 +335,13 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
     }
     TbNode* N = new TbNode();
     if (const char* t = getenv("TBGPU_NODE_TIMING")) N->timing = atoi(t) != 0;
+    {
+        const char* t = getenv("TBGPU_NODE_THREADS");
+        if (!(t && atoi(t) == 0) && W >= 2) {
+            N->pool = new NodePool();
+            for (u32 d = 1; d < W; d++) N->pool->threads.emplace_back(node_pool_worker, N, d);
+        }
+    }
     N->world = W;
     N->pe_src = config->pass_events_max;
     N->pb_src = config->pass_batches_max;
@@ -601,14 +695,26 @@ static bool node_block_resident(const TbNode* N, const NodeDev& D, const NodePas
 
 // H2D of source d's block of pass p and its route plan (enqueued; ev_planned[p & 1] fires when the
 // plan's words are in pinned host memory).
-static int node_issue_plan(TbNode* N, NodePass& P, u32 p, const u64* ts, const void* const* inputs, const u32* lens) {
-    NodeTimer timer(N, 0);
-    const u32 par = p & 1;
-    for (u32 d = 0; d < N->world; d++) {
+struct NodePlanJob {
+    NodePass* P;
+    u32 p;
+    const u64* ts;
+    const void* const* inputs;
+    const u32* lens;
+};
+
+static int node_plan_one(TbNode* N, u32 d, void* ctx) {
+    const NodePlanJob& J = *(const NodePlanJob*)ctx;
+    NodePass& P = *J.P;
+    const u32 p = J.p, par = p & 1;
+    const u64* ts = J.ts;
+    const void* const* inputs = J.inputs;
+    const u32* lens = J.lens;
+    {
         NodeDev& D = N->D[d];
         const NodeBlock& B = P.blk[d];
         const u32 nb = B.k1 - B.k0;
-        if (nb == 0) continue;
+        if (nb == 0) return TBGPU_STATUS_OK;
         tbgpu* E = D.E;
         NCK(hipSetDevice(D.device));
         u64* h_off = D.h_meta[par];
@@ -679,6 +785,12 @@ static int node_issue_plan(TbNode* N, NodePass& P, u32 p, const u64* ts, const v
     return TBGPU_STATUS_OK;
 }
 
+static int node_issue_plan(TbNode* N, NodePass& P, u32 p, const u64* ts, const void* const* inputs, const u32* lens) {
+    NodeTimer timer(N, 0);
+    NodePlanJob J{&P, p, ts, inputs, lens};
+    return node_run(N, node_plan_one, &J);
+}
+
 struct NodePlan {
     u64 C[NODE_WORLD_MAX][NODE_WORLD_MAX];  // events of source s for home h
     unsigned __int128 S = 0;                // saturating sum of every amount of the pass
@@ -744,28 +856,32 @@ static void node_route(const TbNode* N, const NodePlan& PL, NodeRoute& X) {
 
 static int node_issue_replies(TbNode* N, NodePass& P, u32 p, const NodeRoute& X, const u8* seq_codes);
 
-// Gather, routed commit with owner legs, legs to owners, replies to sources — every device, enqueued.
-// replies = false (a split pass): the sources' replies wait for the sequencer (node_issue_replies).
-static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, u32 cert, u64 ts_max,
-                             bool replies = true) {
-    NodeTimer timer(N, 2);
-    const u32 W = N->world, par = p & 1, tri = p % 3;
-    NodeRoute RT;
-    node_route(N, PL, RT);
-    const auto& R = RT.R;
-    const auto& off = RT.off;
-    const auto& nh = RT.nh;
-    for (u32 h = 0; h < W; h++) {
-        if (nh[h] > N->recv_cap) return fail(TBGPU_STATUS_INVALID, "node: home %u receives %llu events > %llu", h,
-                                             (unsigned long long)nh[h], (unsigned long long)N->recv_cap);
-        if (N->D[h].E->log_next + nh[h] > N->D[h].E->xlog_cap) {
-            return fail(TBGPU_STATUS_INVALID, "node: transfer log of shard %u full (%llu + %llu > %llu)", h,
-                        (unsigned long long)N->D[h].E->log_next, (unsigned long long)nh[h],
-                        (unsigned long long)N->D[h].E->xlog_cap);
-        }
-    }
-    // 1. Homes: gather, then (after the previous pass's readers of codes / legs) the routed commit.
-    for (u32 h = 0; h < W; h++) {
+struct NodeCommitJob {
+    NodePass* P;
+    u32 p;
+    const NodeRoute* RT;
+    u32 cert;
+    u64 ts_max;
+    bool replies;
+};
+struct NodeReplyJob {
+    NodePass* P;
+    u32 p;
+    const NodeRoute* RT;
+    const u8* seq_codes;
+};
+static int node_reply_one(TbNode* N, u32 s, void* ctx);
+
+// 1. Home h: gather, then (after the previous pass's readers of codes / legs) the routed commit.
+static int node_home_one(TbNode* N, u32 h, void* ctx) {
+    const NodeCommitJob& J = *(const NodeCommitJob*)ctx;
+    const u32 W = N->world, par = J.p & 1, tri = J.p % 3;
+    const u32 cert = J.cert;
+    const u64 ts_max = J.ts_max;
+    const auto& R = J.RT->R;
+    const auto& off = J.RT->off;
+    const auto& nh = J.RT->nh;
+    {
         NodeDev& D = N->D[h];
         tbgpu* E = D.E;
         NCK(hipSetDevice(D.device));
@@ -822,8 +938,17 @@ static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, 
         }
         NCK(hipEventRecord(D.ev_committed, E->stream));
     }
-    // 2. Owners: the legs they own, from every home.
-    for (u32 o = 0; o < W; o++) {
+    return TBGPU_STATUS_OK;
+}
+
+// 2. Owner o: the legs it owns, from every home (after every home's commit of the pass); then, unless
+// the pass is split, source o's replies (the same stream: after the homes' codes).
+static int node_owner_one(TbNode* N, u32 o, void* ctx) {
+    const NodeCommitJob& J = *(const NodeCommitJob*)ctx;
+    const u32 W = N->world;
+    const u32 cert = J.cert;
+    const auto& nh = J.RT->nh;
+    {
         NodeDev& D = N->D[o];
         tbgpu* E = D.E;
         NCK(hipSetDevice(D.device));
@@ -846,17 +971,50 @@ static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, 
         }
         NCK(hipEventRecord(D.ev_applied, E->stream));
     }
+    if (!J.replies) return TBGPU_STATUS_OK;
+    NodeReplyJob RJ{J.P, J.p, J.RT, nullptr};
+    return node_reply_one(N, o, &RJ);
+}
+
+// Gather, routed commit with owner legs, legs to owners, replies to sources — every device, enqueued.
+// replies = false (a split pass): the sources' replies wait for the sequencer (node_issue_replies).
+static int node_issue_commit(TbNode* N, NodePass& P, u32 p, const NodePlan& PL, u32 cert, u64 ts_max,
+                             bool replies = true) {
+    NodeTimer timer(N, 2);
+    const u32 W = N->world;
+    NodeRoute RT;
+    node_route(N, PL, RT);
+    const auto& nh = RT.nh;
+    for (u32 h = 0; h < W; h++) {
+        if (nh[h] > N->recv_cap) return fail(TBGPU_STATUS_INVALID, "node: home %u receives %llu events > %llu", h,
+                                             (unsigned long long)nh[h], (unsigned long long)N->recv_cap);
+        if (N->D[h].E->log_next + nh[h] > N->D[h].E->xlog_cap) {
+            return fail(TBGPU_STATUS_INVALID, "node: transfer log of shard %u full (%llu + %llu > %llu)", h,
+                        (unsigned long long)N->D[h].E->log_next, (unsigned long long)nh[h],
+                        (unsigned long long)N->D[h].E->xlog_cap);
+        }
+    }
+    NodeCommitJob J{&P, p, &RT, cert, ts_max, replies};
+    int st = node_run(N, node_home_one, &J);
+    if (st) return st;
+    // Every home's commit event is recorded: the owners may wait on them.
+    st = node_run(N, node_owner_one, &J);
+    if (st) return st;
     P.issued = true;
-    return replies ? node_issue_replies(N, P, p, RT, nullptr) : TBGPU_STATUS_OK;
+    return TBGPU_STATUS_OK;
 }
 
 // 3. Sources: replies from the codes their homes wrote (and, for a split pass, the sequencer's codes
 // of the events it committed: seq_codes, the whole pass block-major), into the reply arena.
-static int node_issue_replies(TbNode* N, NodePass& P, u32 p, const NodeRoute& RT, const u8* seq_codes) {
-    NodeTimer timer(N, 3);
-    const u32 W = N->world, par = p & 1, tri = p % 3;
-    u64 base = 0;
-    for (u32 s = 0; s < W; s++) {
+static int node_reply_one(TbNode* N, u32 s, void* ctx) {
+    const NodeReplyJob& J = *(const NodeReplyJob*)ctx;
+    const NodePass& P = *J.P;
+    const NodeRoute& RT = *J.RT;
+    const u8* seq_codes = J.seq_codes;
+    const u32 W = N->world, par = J.p & 1, tri = J.p % 3;
+    u64 base = 0;  // the pass's events of the sources before s (seq_codes is the whole pass, block-major)
+    for (u32 d = 0; d < s; d++) base += P.blk[d].events;
+    {
         NodeDev& D = N->D[s];
         tbgpu* E = D.E;
         const u32 nb = P.blk[s].k1 - P.blk[s].k0;
@@ -872,7 +1030,6 @@ static int node_issue_replies(TbNode* N, NodePass& P, u32 p, const NodeRoute& RT
                                D.results, D.reply_bytes);
             NCK(hipGetLastError());
         }
-        base += P.blk[s].events;
         // Every shard's arena, with or without a block: its head carries the shard's panic word after
         // its whole part of the pass (home commit, owner legs, replies: one stream), so consuming the
         // pass reads every shard's verdict and the call needs no drain at its end.
@@ -884,6 +1041,14 @@ static int node_issue_replies(TbNode* N, NodePass& P, u32 p, const NodeRoute& RT
         NCK(hipEventRecord(D.ev_replied, E->stream));
         NCK(hipEventRecord(D.ev_done[tri], E->stream));
     }
+    return TBGPU_STATUS_OK;
+}
+
+static int node_issue_replies(TbNode* N, NodePass& P, u32 p, const NodeRoute& RT, const u8* seq_codes) {
+    NodeTimer timer(N, 3);
+    NodeReplyJob J{&P, p, &RT, seq_codes};
+    const int st = node_run(N, node_reply_one, &J);
+    if (st) return st;
     P.issued = true;
     return TBGPU_STATUS_OK;
 }
