@@ -221,3 +221,12 @@ def test_node_device_resident_blocks(shards, node_factory):
     finally:
         for sh, dev in bufs:
             sh.free(dev)
+
+
+@pytest.mark.parametrize("config", ["mixed", "two_phase", "limits"])
+def test_node_without_issue_pool(config, node_factory, monkeypatch):
+    """TBGPU_NODE_THREADS=0: every phase issued shard after shard on the calling thread (no issue
+    pool) — the same bytes as the oracle, as with the pool (test_node_differential)."""
+    monkeypatch.setenv("TBGPU_NODE_THREADS", "0")
+    sc = make_scenario(5003 + sum(map(ord, config)), **CONFIGS[config])
+    _run(sc, OracleEngine(), node_factory(devices=(0, 0, 0)), True)
