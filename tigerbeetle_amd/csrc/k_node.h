@@ -219,11 +219,17 @@ __device__ static inline void tb_import_one(const Tables& H, const NodeTablesArg
     const u64 mark = (1ULL << 63) | (tb_fingerprint(lo, hi) >> 1);
     u64 pos = tb_hash_id(lo, hi) & H.account_mask;
     u32 slot = TB_NOT_FOUND;
+    // The owner's first probe entry is loaded beside this table's (independent; a lane that finds
+    // the id being imported by another lane wasted one load): one round trip off the chain.
+    const Tables& O = N.T[o];
+    const u64 opos = tb_hash_id(lo, hi) & O.account_mask;
+    const AccountHot o0 = O.acct_hot[opos];
+    u64 t_first = H.acct_hot[pos].timestamp;
     for (u64 k = 0; k <= H.account_mask; k++) {
         // Plain (cached) reads: a stale one costs a failed CAS (which returns the truth) or a
         // duplicate entry, never a wrong one.
         u64* tw = &H.acct_hot[pos].timestamp;
-        u64 t = *tw;
+        u64 t = k == 0 ? t_first : *tw;
         if (t == 0) {
             t = atomicCAS((unsigned long long*)tw, 0ULL, (unsigned long long)mark);
             if (t == 0) {
@@ -242,15 +248,14 @@ __device__ static inline void tb_import_one(const Tables& H, const NodeTablesArg
     const u64 k = tb_wave_claim(true, count);
     if (k < cap) list[k] = slot;
     else tb_panic(H.g, PANIC_TABLE_FULL);
-    const Tables& O = N.T[o];
-    const u32 os = tb_account_find(O, lo, hi);
+    AccountHot a;
+    const u32 os = tb_account_find_from(O, lo, hi, opos, o0, &a);
     AccountHot* h = &H.acct_hot[slot];
     if (os == TB_NOT_FOUND) {  // no such account: a tombstone id (probes continue past it) under the marker
         h->id_lo = ~0ULL;
         h->id_hi = ~0ULL;
         return;
     }
-    const AccountHot a = O.acct_hot[os];
     os_of[slot] = os;  // the owner's slot, for this pass's owner legs
     h->ledger = a.ledger;
     h->code = a.code;
@@ -321,38 +326,56 @@ struct NodeReplyArgs {
 
 // Per-prepare sparse replies of a source's block (tb_route_replies with the codes read from their
 // homes): ascending index, non-ok only.  One workgroup per prepare.
+// A prepare (up to 8 x 1024 events) is one group: every event's home and slot are loaded first, then
+// every code (one dependent round trip each, not one per 1024 events), then one barrier ranks all.
+#define NR_K 8
 __global__ __launch_bounds__(1024) void tb_node_replies(const u64* batch_off, const u8* home, const u32* slot,
                                                         NodeReplyArgs A, u32* results, u32* reply_bytes) {
-    __shared__ u32 s_wave[1024 / 64];
+    __shared__ u32 s_cnt[NR_K][1024 / 64];
     const u32 b = blockIdx.x;
     const u64 boff = batch_off[b];
     const u32 L = (u32)(batch_off[b + 1] - boff);
     u32* out = results + 2 * boff;
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     u32 running = 0;
-    for (u32 c = 0; c < L; c += blockDim.x) {
-        const u32 i = c + threadIdx.x;
-        u32 code = R_OK;
-        if (i < L) {
-            const u32 h = home[boff + i];
-            code = h == ROUTE_LOCAL ? (u32)R_TIMESTAMP_MUST_BE_ZERO
-                   : h == ROUTE_DEP   ? (u32)A.seq[boff + i]
-                                      : (u32)A.codes[h][(i64)slot[boff + i] + A.delta[h]];
+    for (u32 c0 = 0; c0 < L; c0 += NR_K * blockDim.x) {
+        u32 h[NR_K], sl[NR_K], code[NR_K];
+#pragma unroll
+        for (u32 q = 0; q < NR_K; q++) {
+            const u32 i = c0 + q * blockDim.x + threadIdx.x;
+            h[q] = i < L ? home[boff + i] : (u32)ROUTE_LOCAL;
+            sl[q] = i < L ? slot[boff + i] : 0u;
         }
-        const u64 m = __ballot(code != R_OK);
-        const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        if (lane == 0) s_wave[wave] = __popcll(m);
+#pragma unroll
+        for (u32 q = 0; q < NR_K; q++) {
+            const u32 i = c0 + q * blockDim.x + threadIdx.x;
+            code[q] = i >= L                 ? (u32)R_OK
+                      : h[q] == ROUTE_LOCAL ? (u32)R_TIMESTAMP_MUST_BE_ZERO
+                      : h[q] == ROUTE_DEP   ? (u32)A.seq[boff + i]
+                                            : (u32)A.codes[h[q]][(i64)sl[q] + A.delta[h[q]]];
+        }
+        u64 m[NR_K];
+#pragma unroll
+        for (u32 q = 0; q < NR_K; q++) {
+            m[q] = __ballot(code[q] != R_OK);
+            if (lane == 0) s_cnt[q][wave] = __popcll(m[q]);
+        }
         __syncthreads();
-        u32 wb = 0, tot = 0;
-        for (u32 k = 0; k < blockDim.x / 64; k++) {
-            wb += k < wave ? s_wave[k] : 0;
-            tot += s_wave[k];
+#pragma unroll
+        for (u32 q = 0; q < NR_K; q++) {
+            u32 wb = 0, tot = 0;
+            for (u32 k = 0; k < nw; k++) {
+                const u32 v = s_cnt[q][k];
+                wb += k < wave ? v : 0;
+                tot += v;
+            }
+            if (code[q] != R_OK) {
+                const u32 r = running + wb + __popcll(m[q] & ((1ULL << lane) - 1));
+                out[2 * r] = c0 + q * blockDim.x + threadIdx.x;
+                out[2 * r + 1] = code[q];
+            }
+            running += tot;
         }
-        if (code != R_OK) {
-            const u32 r = running + wb + __popcll(m & ((1ULL << lane) - 1));
-            out[2 * r] = i;
-            out[2 * r + 1] = code;
-        }
-        running += tot;
         __syncthreads();
     }
     if (threadIdx.x == 0) reply_bytes[b] = running * 8;

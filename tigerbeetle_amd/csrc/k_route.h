@@ -68,6 +68,10 @@ struct RouteArgs {
     const u64* limbits;
     u64 limmask;
     u32 limit_any;
+    // Non-null (a one-prepare block of a node call): tb_route_classify writes the block's metadata
+    // {0, n, im_ts} here (= batch_off / batch_ts) from its arguments, instead of a host copy.
+    u64* im_meta;
+    u64 im_ts;
 };
 #define RW_HUGE (2 * SUM_SHARDS)
 #define RW_DIRTY (2 * SUM_SHARDS + 1)
@@ -82,6 +86,11 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_route_classify(RouteArgs A) 
     __shared__ u32 s_dirty;
     if (threadIdx.x < A.world) s_cnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) s_dirty = 0;
+    if (A.im_meta && blockIdx.x == 0 && threadIdx.x == 0) {  // read by the kernels after this one
+        A.im_meta[0] = 0;
+        A.im_meta[1] = A.n;
+        A.im_meta[2] = A.im_ts;
+    }
     __syncthreads();
     const u64 e = (u64)blockIdx.x * ROUTE_THREADS + threadIdx.x;
     const bool limits = A.limbits ? A.limit_any != 0 : A.T.g->limit_accounts != 0;
@@ -166,6 +175,31 @@ __global__ __launch_bounds__(1024) void tb_route_offsets(RouteArgs A) {
         run += A.block_counts[(u64)b * A.world + h];
     }
     if (threadIdx.x == 0) A.words[RW_COUNTS + h] = home_total;
+}
+
+// After a plan (node engines): its words into the source's mapped host copy, the device words
+// zeroed for the plan after next of this parity (so no memset precedes a plan), then `seq` into the
+// word at `done` with system scope — the host spins on it instead of waiting for the route stream.
+// One wave: every load is issued before the first store into mapped memory (gfx950's vmcnt counts
+// stores too), and its stores drain before the flag.
+__global__ __launch_bounds__(64) void tb_route_publish(u64* words, u64* host_words, u32* done, u32 seq) {
+    constexpr u32 R = (ROUTE_WORDS + 63) / 64;
+    u64 v[R];
+#pragma unroll
+    for (u32 r = 0; r < R; r++) {
+        const u32 i = r * 64 + threadIdx.x;
+        v[r] = i < ROUTE_WORDS ? words[i] : 0;
+    }
+#pragma unroll
+    for (u32 r = 0; r < R; r++) {
+        const u32 i = r * 64 + threadIdx.x;
+        if (i < ROUTE_WORDS) {
+            host_words[i] = v[r];
+            words[i] = 0;
+        }
+    }
+    __threadfence_system();
+    if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Pass 3: stable scatter into the send buffer, with the execute timestamp of every event.

@@ -53,8 +53,16 @@ struct NodeDev {
     u8* send[2] = {};
     u32* slot[2] = {};
     u8* home[2] = {};
-    u64* words[2] = {};
-    u64* h_words[2] = {};        // pinned: the plan words back on the host
+    u64* words[2] = {};          // zero between plans (tb_route_publish clears them)
+    u64* h_words[2] = {};        // pinned, device-mapped: the plan words back on the host
+    u64* d_words_host[2] = {};   // h_words' device address
+    // Completion words (pinned, device-mapped) the host spins on: [par] a plan's words published,
+    // [2 + tri] a one-workgroup reply arena written.  Each use gets a new non-zero sequence number.
+    u32* h_flags = nullptr;
+    u32* d_flags = nullptr;
+    u32 flag_seq = 0;
+    u32 plan_seq[2] = {};
+    u32 reply_seq[3] = {};       // 0: the arena of that slot is waited for by its event
     u64* meta[2] = {};           // device: the block's offsets then timestamps
     u64* h_meta[2] = {};         // pinned mirror
     u32* block_counts = nullptr;
@@ -125,6 +133,7 @@ struct NodePool {
     std::atomic<u64> gen{0};
     std::atomic<u32> done{0};
     std::atomic<bool> stop{false};
+    u32 spin_us = 50;  // TBGPU_NODE_SPIN_US
     NodeShardFn fn = nullptr;
     void* ctx = nullptr;
     int status[NODE_WORLD_MAX] = {};
@@ -218,9 +227,11 @@ static void node_pool_worker(TbNode* N, u32 d) {
     NodePool& Q = *N->pool;
     u64 seen = 0;
     for (;;) {
-        // A job (gen past `seen`) or stop: spin ~50 us, then sleep until notified.
-        for (u32 spin = 0; spin < 20000 && Q.gen.load(std::memory_order_acquire) == seen && !Q.stop.load(); spin++) {
+        // A job (gen past `seen`) or stop: spin Q.spin_us, then sleep until notified.
+        const auto t0 = std::chrono::steady_clock::now();
+        for (u32 spin = 0; Q.gen.load(std::memory_order_acquire) == seen && !Q.stop.load(); spin++) {
             __builtin_ia32_pause();
+            if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(Q.spin_us)) break;
         }
         if (Q.gen.load(std::memory_order_acquire) == seen && !Q.stop.load()) {
             std::unique_lock<std::mutex> lk(Q.mu);
@@ -297,7 +308,7 @@ static void node_free(TbNode* N) {
                        D.imp_list, D.imp_count, D.imp_os, D.limbits};
         for (void* p : dev) if (p) (void)hipFree(p);
         void* host[] = {D.h_words[0], D.h_words[1], D.h_meta[0], D.h_meta[1], D.hmeta_host[0], D.hmeta_host[1],
-                        D.hmeta_host[2], D.h_arena[0], D.h_arena[1], D.h_arena[2], D.h_dcounts};
+                        D.hmeta_host[2], D.h_arena[0], D.h_arena[1], D.h_arena[2], D.h_dcounts, D.h_flags};
         for (void* p : host) if (p) (void)hipHostFree(p);
         hipEvent_t evs[] = {D.ev_start[0], D.ev_start[1], D.ev_start[2], D.ev_done[0], D.ev_done[1], D.ev_done[2],
                             D.ev_planned[0], D.ev_planned[1], D.ev_copied, D.ev_gathered, D.ev_committed,
@@ -339,6 +350,7 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
         const char* t = getenv("TBGPU_NODE_THREADS");
         if (!(t && atoi(t) == 0) && W >= 2) {
             N->pool = new NodePool();
+            if (const char* us = getenv("TBGPU_NODE_SPIN_US")) N->pool->spin_us = (u32)atoi(us);
             for (u32 d = 1; d < W; d++) N->pool->threads.emplace_back(node_pool_worker, N, d);
         }
     }
@@ -408,7 +420,9 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
             NALLOC(tbMalloc(&D.slot[k], pe * 4));
             NALLOC(tbMalloc(&D.home[k], pe));
             NALLOC(tbMalloc(&D.words[k], ROUTE_WORDS * 8));
-            NALLOC(tbHostMalloc(&D.h_words[k], ROUTE_WORDS * 8, hipHostMallocDefault));
+            NALLOC(hipMemsetAsync(D.words[k], 0, ROUTE_WORDS * 8, D.rs));
+            NALLOC(tbHostMalloc(&D.h_words[k], ROUTE_WORDS * 8, hipHostMallocMapped));
+            if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&D.d_words_host[k], D.h_words[k], 0);
             NALLOC(tbMalloc(&D.meta[k], (2 * (u64)N->pb_src + 1) * 8));
             NALLOC(tbHostMalloc(&D.h_meta[k], (2 * (u64)N->pb_src + 1) * 8, hipHostMallocDefault));
             NALLOC(tbEventCreateWithFlags(&D.ev_planned[k], hipEventDisableTiming));
@@ -428,6 +442,11 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
             if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&D.d_arena[k], D.h_arena[k], 0);
             NALLOC(tbEventCreate(&D.ev_start[k]));
             NALLOC(tbEventCreate(&D.ev_done[k]));
+        }
+        NALLOC(tbHostMalloc(&D.h_flags, 64, hipHostMallocMapped));
+        if (e == hipSuccess) {
+            memset(D.h_flags, 0, 64);
+            e = hipHostGetDevicePointer((void**)&D.d_flags, D.h_flags, 0);
         }
         NALLOC(tbEventCreateWithFlags(&D.ev_copied, hipEventDisableTiming));
         NALLOC(tbEventCreateWithFlags(&D.ev_gathered, hipEventDisableTiming));
@@ -693,14 +712,33 @@ static bool node_block_resident(const TbNode* N, const NodeDev& D, const NodePas
     return attr.type == hipMemoryTypeDevice && attr.device == D.device;
 }
 
-// H2D of source d's block of pass p and its route plan (enqueued; ev_planned[p & 1] fires when the
-// plan's words are in pinned host memory).
+static u32 node_next_seq(NodeDev& D) {
+    if (++D.flag_seq == 0) ++D.flag_seq;
+    return D.flag_seq;
+}
+
+// Spin until a kernel wrote `seq` into a completion word (a stream's completion signal reaches a
+// waiting host thread later).  False after 2 s: the caller waits on the stream's event instead,
+// which reports a fault.
+static bool node_spin(const u32* word, u32 seq) {
+    volatile const u32* w = word;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (u32 spin = 0; *w != seq; spin++) {
+        if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) return false;
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return true;
+}
+
+// H2D of source d's block of pass p and its route plan (enqueued; ev_planned[p & 1] fires, and the
+// plan flag takes plan_seq[p & 1], when the plan's words are in pinned host memory).
 struct NodePlanJob {
     NodePass* P;
     u32 p;
     const u64* ts;
     const void* const* inputs;
     const u32* lens;
+    bool single;  // the call is this one pass: its bodies cross on the route stream (no event hop)
 };
 
 static int node_plan_one(TbNode* N, u32 d, void* ctx) {
@@ -725,9 +763,12 @@ static int node_plan_one(TbNode* N, u32 d, void* ctx) {
         // read where they are.  Otherwise the copy stream moves them (runs of address-contiguous
         // prepares as one DMA; host memory over the device's own PCIe link, another device's HBM
         // over xGMI).
-        if (N->latency_on) NCK(hipEventRecord(D.ev_start[p % 3], E->copy_stream));
+        // A one-pass call has no next plan to overlap: its copy goes on the route stream itself (a
+        // cross-stream event hop costs ~15 us on the device between the copy and the plan).
+        hipStream_t cs = J.single ? D.rs : E->copy_stream;
+        if (N->latency_on) NCK(hipEventRecord(D.ev_start[p % 3], cs));
         // The sequencer of the split pass two passes back may still be reading this parity's buffers.
-        NCK(hipStreamWaitEvent(E->copy_stream, N->ev_xread, 0));
+        if (!J.single) NCK(hipStreamWaitEvent(E->copy_stream, N->ev_xread, 0));
         NCK(hipStreamWaitEvent(D.rs, N->ev_xread, 0));
         D.ev[par] = D.stage[par];
         if (node_block_resident(N, D, P, d, inputs, lens)) {
@@ -738,23 +779,30 @@ static int node_plan_one(TbNode* N, u32 d, void* ctx) {
                 const u8* base = (const u8*)inputs[k];
                 u64 bytes = (u64)lens[k] * 128;
                 while (j < B.k1 && (const u8*)inputs[j] == base + bytes) bytes += (u64)lens[j++] * 128;
-                if (bytes) NCK(hipMemcpyAsync(D.stage[par] + P.off[d][k - B.k0] * 128, base, bytes, hipMemcpyDefault,
-                                              E->copy_stream));
+                if (bytes) NCK(hipMemcpyAsync(D.stage[par] + P.off[d][k - B.k0] * 128, base, bytes, hipMemcpyDefault, cs));
                 k = j;
             }
         }
-        NCK(hipEventRecord(D.ev_copied, E->copy_stream));
+        if (!J.single) {
+            NCK(hipEventRecord(D.ev_copied, E->copy_stream));
+            NCK(hipStreamWaitEvent(D.rs, D.ev_copied, 0));
+        }
         // Route stream: wait for the buffers' previous users (pass p-2's gathers on every home and
         // this source's replies), then the plan.
-        NCK(hipStreamWaitEvent(D.rs, D.ev_copied, 0));
         NCK(hipStreamWaitEvent(D.rs, D.ev_replied, 0));
         for (u32 h = 0; h < N->world; h++) {
             NCK(hipSetDevice(D.device));
             NCK(hipStreamWaitEvent(D.rs, N->D[h].ev_gathered, 0));
         }
-        NCK(hipMemcpyAsync(D.meta[par], h_off, (2 * (u64)nb + 1) * 8, hipMemcpyHostToDevice, D.rs));
-        NCK(hipMemsetAsync(D.words[par], 0, ROUTE_WORDS * 8, D.rs));
+        // One prepare with events (the replica's commit): its metadata written by the classification
+        // from kernel arguments, no copy.  The words are zero already (tb_route_publish).
+        const bool im = nb == 1 && B.events > 0;
+        if (!im) NCK(hipMemcpyAsync(D.meta[par], h_off, (2 * (u64)nb + 1) * 8, hipMemcpyHostToDevice, D.rs));
         RouteArgs A{};
+        if (im) {
+            A.im_meta = D.meta[par];
+            A.im_ts = h_ts[0];
+        }
         A.events = D.ev[par];
         A.n = (u32)B.events;
         A.nb = nb;
@@ -779,15 +827,19 @@ static int node_plan_one(TbNode* N, u32 d, void* ctx) {
             hipLaunchKernelGGL(tb_route_scatter, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, D.rs, A, D.send[par], D.slot[par]);
             NCK(hipGetLastError());
         }
-        NCK(hipMemcpyAsync(D.h_words[par], D.words[par], ROUTE_WORDS * 8, hipMemcpyDeviceToHost, D.rs));
+        D.plan_seq[par] = node_next_seq(D);
+        hipLaunchKernelGGL(tb_route_publish, dim3(1), dim3(64), 0, D.rs, D.words[par], D.d_words_host[par], D.d_flags + par,
+                           D.plan_seq[par]);
+        NCK(hipGetLastError());
         NCK(hipEventRecord(D.ev_planned[par], D.rs));
     }
     return TBGPU_STATUS_OK;
 }
 
-static int node_issue_plan(TbNode* N, NodePass& P, u32 p, const u64* ts, const void* const* inputs, const u32* lens) {
+static int node_issue_plan(TbNode* N, NodePass& P, u32 p, const u64* ts, const void* const* inputs, const u32* lens,
+                           bool single) {
     NodeTimer timer(N, 0);
-    NodePlanJob J{&P, p, ts, inputs, lens};
+    NodePlanJob J{&P, p, ts, inputs, lens, single};
     return node_run(N, node_plan_one, &J);
 }
 
@@ -798,7 +850,9 @@ struct NodePlan {
     bool huge = false;
 };
 
-static int node_read_plan(TbNode* N, const NodePass& P, u32 p, NodePlan* out) {
+// spin: the words are all the caller reads (a clean plan); otherwise (a split pass, which reads its
+// classification counts too) the route stream's event is waited for.
+static int node_read_plan(TbNode* N, const NodePass& P, u32 p, NodePlan* out, bool spin = true) {
     typedef unsigned __int128 h128;
     memset(out->C, 0, sizeof(out->C));
     out->S = 0;
@@ -811,7 +865,7 @@ static int node_read_plan(TbNode* N, const NodePass& P, u32 p, NodePlan* out) {
         NCK(hipSetDevice(D.device));
         {
             NodeTimer timer(N, 1);
-            NCK(hipEventSynchronize(D.ev_planned[par]));
+            if (!spin || !node_spin(D.h_flags + par, D.plan_seq[par])) NCK(hipEventSynchronize(D.ev_planned[par]));
         }
         const u64* w = D.h_words[par];
         if (w[RW_HUGE]) out->huge = true;
@@ -1033,8 +1087,10 @@ static int node_reply_one(TbNode* N, u32 s, void* ctx) {
         // Every shard's arena, with or without a block: its head carries the shard's panic word after
         // its whole part of the pass (home commit, owner legs, replies: one stream), so consuming the
         // pass reads every shard's verdict and the call needs no drain at its end.
+        // One workgroup (a block of at most one prepare): it flags its arena for the host to spin on.
+        D.reply_seq[tri] = nb <= 1 ? node_next_seq(D) : 0;
         hipLaunchKernelGGL(tb_reply_out, dim3(std::max<u32>(nb, 1)), dim3(64), 0, E->stream, D.meta[par], nb,
-                           D.reply_bytes, D.results, E->g, D.d_arena[tri]);
+                           D.reply_bytes, D.results, E->g, D.d_arena[tri], D.d_flags + 2 + tri, D.reply_seq[tri]);
         NCK(hipGetLastError());
         // After tb_reply_out too: it reads this parity's prepare offsets, which the route stream
         // rewrites two passes on once it has waited for this event.
@@ -1064,7 +1120,9 @@ static int node_consume(TbNode* N, NodePass& P, u32 p, void* const* outputs, u32
         NCK(hipSetDevice(D.device));
         {
             NodeTimer timer(N, 4);
-            NCK(hipEventSynchronize(D.ev_done[tri]));
+            // The arena's flag when it has one (and no device-clock latency is asked for).
+            const bool spun = D.reply_seq[tri] && !(latency_ms && nb) && node_spin(D.h_flags + 2 + tri, D.reply_seq[tri]);
+            if (!spun) NCK(hipEventSynchronize(D.ev_done[tri]));
         }
         if (!take || status) continue;
         const u64* head = (const u64*)D.h_arena[tri];
@@ -1191,14 +1249,17 @@ static int node_split_pass(TbNode* N, NodePass& P, u32 p, const u64* ts, u64 bou
             hipLaunchKernelGGL(tb_route_scatter, dim3(A.nblocks), dim3(ROUTE_THREADS), 0, D.rs, A, D.send[par], D.slot[par]);
             NCK(hipGetLastError());
         }
-        NCK(hipMemcpyAsync(D.h_words[par], D.words[par], ROUTE_WORDS * 8, hipMemcpyDeviceToHost, D.rs));
+        D.plan_seq[par] = node_next_seq(D);
+        hipLaunchKernelGGL(tb_route_publish, dim3(1), dim3(64), 0, D.rs, D.words[par], D.d_words_host[par], D.d_flags + par,
+                           D.plan_seq[par]);
+        NCK(hipGetLastError());
         NCK(hipMemcpyAsync(D.h_dcounts, D.dcounts, NODE_DC_WORDS * 8, hipMemcpyDeviceToHost, D.rs));
         NCK(hipEventRecord(D.ev_planned[par], D.rs));
     }
     int st = plan_next();
     if (st) return st;
     NodePlan PL;
-    if ((st = node_read_plan(N, P, p, &PL))) return st;
+    if ((st = node_read_plan(N, P, p, &PL, false))) return st;
     u64 n_seq = 0, n_pass = 0, room[NODE_WORLD_MAX] = {};
     for (u32 d = 0; d < W; d++) {
         n_seq += N->D[d].h_dcounts[2];
@@ -1415,7 +1476,10 @@ static int node_commit_transfers(TbNode* N, u32 n, const u64* ts, const void* co
             }
         }
     };
-    if ((status = node_issue_plan(N, build(0, 0), 0, ts, inputs, lens))) return status;
+    {
+        NodePass& P0 = build(0, 0);
+        if ((status = node_issue_plan(N, P0, 0, ts, inputs, lens, P0.k1 >= n))) return status;
+    }
     for (u32 p = 0; p < NP && status == TBGPU_STATUS_OK; p++) {
         if (p >= 2) consume_upto(p - 1);  // pass p-2: its arena slot, start event and meta are reused next
         if (status) break;
@@ -1427,7 +1491,7 @@ static int node_commit_transfers(TbNode* N, u32 n, const u64* ts, const void* co
         auto plan_next = [&]() -> int {
             if (pass(p).k1 >= n) return TBGPU_STATUS_OK;
             NP = p + 2;  // its ring slot held pass p - 3, consumed above
-            return node_issue_plan(N, build(p + 1, pass(p).k1), p + 1, ts, inputs, lens);
+            return node_issue_plan(N, build(p + 1, pass(p).k1), p + 1, ts, inputs, lens, false);
         };
         const h128 total = bound + PL.S < bound ? ~(h128)0 : bound + PL.S;
         if (PL.dirty || PL.huge || total == ~(h128)0) {
