@@ -1045,6 +1045,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
             hipLaunchKernelGGL(tb_owner_legs, dim3((u32)((n + 255) / 256)), dim3(256), 0, E->stream, P, *owner);
             HIPCK(hipGetLastError());
         }
+        if (imp && imp->ev_legs) HIPCK(hipEventRecord((hipEvent_t)imp->ev_legs, E->stream));
         if (imp && n > 0) {  // the owned-only table again
             hipLaunchKernelGGL(tb_node_import_clear, dim3(1024), dim3(256), 0, E->stream, E->T, imp->list, imp->count);
             HIPCK(hipGetLastError());

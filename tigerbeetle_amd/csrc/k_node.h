@@ -309,6 +309,9 @@ struct NodeImport {
     u32* os_of;    // [account_cap] imported slot -> the account's slot on its owner
     u64* leg_counts = nullptr;  // the home's per-owner leg counts, zeroed by the same tb_pass_clear
     u32 legs_n = 0;
+    // Recorded after each sub-pass's owner legs (before the table's import clear): what the owners
+    // wait for (the legs and codes are final there).  Host-side only (hipEvent_t).
+    void* ev_legs = nullptr;
 };
 
 __global__ void tb_node_import_clear(Tables H, const u32* list, const u64* count) {

@@ -986,11 +986,13 @@ static int node_home_one(TbNode* N, u32 h, void* ctx) {
             imp.os_of = D.imp_os;
             imp.leg_counts = D.leg_counts;
             imp.legs_n = W;
+            imp.ev_legs = (void*)D.ev_committed;  // the owners need not wait for the import clear
             const int st = enqueue_call(E, OP_CREATE_TRANSFERS, (u32)nb, h_off, D.recv, E->results, E->reply_bytes,
                                         true, D.codes, cert, nullptr, D.hmeta_dev[tri], &O, nb == 1 ? im : nullptr, &imp);
             if (st) return st;
+        } else {
+            NCK(hipEventRecord(D.ev_committed, E->stream));
         }
-        NCK(hipEventRecord(D.ev_committed, E->stream));
     }
     return TBGPU_STATUS_OK;
 }
