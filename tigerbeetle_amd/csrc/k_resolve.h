@@ -374,6 +374,15 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     // in s_code; the loop below without its chain and dependent cases, branch-light.
     if (OP == OP_CREATE_TRANSFERS && !any_linked && !any_dep) {
         u32 panic = 0;
+        // Carried timestamps (a routed pass reads each from its event) loaded before the loop's
+        // first store: a load after a store of the same wave waits for it (gfx950 vmcnt), which cost
+        // a routed one-prepare pass one memory round trip per k.
+        u64 r_ts[RESOLVE_K];
+#pragma unroll
+        for (u32 k = 0; k < RESOLVE_K; k++) {
+            const u32 i = k * RESOLVE_THREADS + threadIdx.x;
+            r_ts[k] = tb_ts_carried(P) ? (i < L ? tb_event_ts(P, b, boff, L, i) : 0) : ts0 + i;
+        }
 #pragma unroll
         for (u32 k = 0; k < RESOLVE_K; k++) {
             const u32 i = k * RESOLVE_THREADS + threadIdx.x;
@@ -385,7 +394,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
             panic |= code == TB_CODE_PANIC;
             const bool leg = use_legs && !(info & HZ_POSTVOID) && r_amt[k][1] == 0 && r_amt[k][0] <= LEG_AMT_MASK;
             if (valid) P.info[pe] = info | (ok ? HZ_EVAL_OK : 0) | (ok && !leg ? HZ_LATE : 0);
-            const u64 ts = tb_ts_carried(P) ? (valid ? tb_event_ts(P, b, boff, L, i) : 0) : ts0 + i;
+            const u64 ts = r_ts[k];
             tsmax = ok ? ts : tsmax;
             n_app += ok;
             n_fail += valid & !ok;
