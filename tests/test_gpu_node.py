@@ -230,3 +230,53 @@ def test_node_without_issue_pool(config, node_factory, monkeypatch):
     monkeypatch.setenv("TBGPU_NODE_THREADS", "0")
     sc = make_scenario(5003 + sum(map(ord, config)), **CONFIGS[config])
     _run(sc, OracleEngine(), node_factory(devices=(0, 0, 0)), True)
+
+
+@pytest.mark.parametrize("shards", [2, 3])
+def test_node_one_prepare_calls(shards, node_factory):
+    """The replica's call on a node: one prepare per call from registered host memory (a one-pass
+    call: the body's copy on the route stream, the block's metadata from the classification's
+    arguments, the plan words and the reply arena read once their completion words flip), clean
+    calls with duplicate ids, non-zero timestamps and missing accounts, interleaved with dirty
+    calls (a linked chain: a split pass, whose classification rewrites the plan words) — every
+    reply, account and transfer equals the oracle's."""
+    n_acc, batch, n_prep = 6000, 8190, 16
+    n_xfer = batch * n_prep
+    engine = node_factory(devices=(0,) * shards, accounts_max=n_acc, transfers_max=n_xfer,
+                          pass_events_max=4 * batch, pass_batches_max=4)
+    accts, xfers = generate(engine, "c2", n_acc, n_xfer, seed=23 + shards)
+    x = xfers.view(TRANSFER_DTYPE).copy()
+    rng = np.random.default_rng(40 + shards)
+    dup = rng.choice(np.arange(batch, n_xfer), 400, replace=False)
+    src = rng.integers(0, batch, 400)
+    x["id_lo"][dup] = x["id_lo"][src]
+    x["id_hi"][dup] = x["id_hi"][src]
+    x["timestamp"][rng.choice(n_xfer, 100, replace=False)] = 9
+    x["debit_account_id_lo"][rng.choice(n_xfer, 100, replace=False)] ^= 0x5A5A
+    for k in (3, 4, 9):  # dirty calls: a 6-event linked chain inside the prepare
+        x["flags"][k * batch + 100:k * batch + 105] |= 1
+    xfers = x.view(np.uint8).reshape(-1)
+    a_lens, x_lens = batches(n_acc, batch), [batch] * n_prep
+    a_ts, t = timestamps(a_lens, 10**12)
+    x_ts, _ = timestamps(x_lens, t + 10)
+    oracle = OracleEngine(n_acc, n_xfer)
+    assert all(r == b"" for r in oracle.commit_many(128, a_ts, split(accts, a_lens)))
+    expected = oracle.commit_many(129, x_ts, split(xfers, x_lens))
+    rb, _, _ = engine.commit_pipelined(128, a_ts, a_lens, np.ascontiguousarray(accts), chunk_batches=4)
+    assert int(rb.sum()) == 0
+    host = np.ascontiguousarray(xfers)
+    engine.register_host(host)
+    try:
+        got = []
+        for k in range(n_prep):
+            body = host[k * batch * 128:(k + 1) * batch * 128]
+            nb, rep, _ = engine.commit_pipelined(129, [x_ts[k]], [batch], body)
+            got.append(bytes(rep[:int(nb[0])]))
+    finally:
+        engine.unregister_host(host)
+    for k, (e, a) in enumerate(zip(expected, got)):
+        assert e == a, "reply of prepare %d differs" % k
+    assert sum(len(r) for r in expected) > 0
+    assert_same_state(oracle, engine)
+    st = engine.stats()
+    assert st["node_passes_split"] >= 3, st
