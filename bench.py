@@ -537,8 +537,12 @@ def main():
         # The node engine keeps three streams per shard (copy, route, engine) and the sequencer's on the
         # first device: with HIP's default of 4 hardware queues per device the sequencer's stream shares
         # a queue with shard 0's engine stream and waits behind its routed part.  Read by the HIP
-        # runtime when it starts (no HIP call has been made yet); an explicit setting is kept.
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+        # runtime when it starts (no HIP call has been made yet); an explicit setting is kept, except
+        # below 8 for logical shards on one device (their streams all share that device's queues: C3
+        # on two logical shards ran at 253 M/s with the box's exported 4, 356 with 8).
+        cur = os.environ.get("GPU_MAX_HW_QUEUES")
+        if cur is None or (args.same_device and cur.isdigit() and int(cur) < 8):
+            os.environ["GPU_MAX_HW_QUEUES"] = "8"
     import torch
     import torch.distributed as dist
 
