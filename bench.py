@@ -1471,6 +1471,11 @@ def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=No
            "avg_launch_ms": round(avg_ms, 4), "avg_launch_ms_hip_events": round(hip_avg, 4) if hip_avg else None,
            "transfers_per_launch": round(per_launch_transfers, 1),
            "alg_bytes_per_transfer": round(alg_bytes / per_launch_transfers, 1), "timing": timing}
+    if dom == "tb_transfers_validate":
+        # One build's validate mean moves with the box it lands on (each gpurun call gets a fresh one):
+        # round 5's driver runs of unchanged kernels read frac 0.276-0.285, round 4's same-build A/B
+        # lines 0.59-0.70 ms.  The frac above is this box's.
+        out["frac_box_spread"] = "about +-8% box to box for one build (DESIGN.md §4); this line is one box"
     if pmc_leg:  # the C2 launches the PMC runs profiled (not the C3/C4 lines)
         out.update(load_pmc(pmc_leg, dom, per_launch_transfers))
     if out.get("rocprof_avg_launch_ms"):
