@@ -232,14 +232,18 @@ def test_node_without_issue_pool(config, node_factory, monkeypatch):
     _run(sc, OracleEngine(), node_factory(devices=(0, 0, 0)), True)
 
 
-@pytest.mark.parametrize("shards", [2, 3])
-def test_node_one_prepare_calls(shards, node_factory):
+@pytest.mark.parametrize("shards,spin_us", [(2, None), (3, None), (3, "0")], ids=["2", "3", "3-pool-sleeps"])
+def test_node_one_prepare_calls(shards, spin_us, node_factory, monkeypatch):
     """The replica's call on a node: one prepare per call from registered host memory (a one-pass
     call: the body's copy on the route stream, the block's metadata from the classification's
     arguments, the plan words and the reply arena read once their completion words flip), clean
     calls with duplicate ids, non-zero timestamps and missing accounts, interleaved with dirty
     calls (a linked chain: a split pass, whose classification rewrites the plan words) — every
-    reply, account and transfer equals the oracle's."""
+    reply, account and transfer equals the oracle's.  TBGPU_NODE_SPIN_US=0: the issue pool's
+    threads sleep between every phase (each phase's job reaches them through the condition
+    variable)."""
+    if spin_us is not None:
+        monkeypatch.setenv("TBGPU_NODE_SPIN_US", spin_us)
     n_acc, batch, n_prep = 6000, 8190, 16
     n_xfer = batch * n_prep
     engine = node_factory(devices=(0,) * shards, accounts_max=n_acc, transfers_max=n_xfer,
