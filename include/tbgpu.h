@@ -243,7 +243,10 @@ int tbgpu_load_transfers(tbgpu_t* engine, const void* transfers, const uint8_t* 
  * (src/lsm/groove.zig:602-898), loaded by prefetch before commit (src/state_machine.zig:419-467).
  *   tbgpu_evict_transfers: drops the transfers the last write-back (tbgpu_checkpoint_delta) covered,
  *     except the newest `keep` log positions; the rest of the log is compacted and re-indexed.
- *     *evicted = transfers dropped.  Synchronous; no asynchronous write-back may be in flight.
+ *     *evicted = transfers dropped.  Synchronous.  Only right after a write-back: with an
+ *     asynchronous write-back in flight, or any log position written since the last one (a commit,
+ *     a load), it returns TBGPU_STATUS_INVALID and changes nothing (an unwritten post / void may name
+ *     a pending transfer the cut would drop, and the next write-back needs that record).
  *   tbgpu_transfers_maybe_cold: for n ids ({lo, hi} pairs), cold[i] = 1 when the engine does not
  *     hold id i and may have evicted it (a Bloom filter of evicted ids: false positives only).  The
  *     wrapper's prefetch loads the cold ids its forest holds (tbgpu_load_transfers, with their posted

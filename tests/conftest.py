@@ -9,6 +9,16 @@ if ROOT not in sys.path:
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# Every stream of the node engine on its own hardware queue, as on N real devices (HIP's default is
+# 4 per process, under which a 2-shard node's 7 streams share queues and serialise; round 5's
+# sequencer balance race showed only with 8). Set here, before any test module imports torch or
+# loads libtbgpu.so, i.e. before HIP reads it. `GPU_MAX_HW_QUEUES=4 pytest ...` keeps the old case.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
+
+def pytest_report_header(config):
+    return "GPU_MAX_HW_QUEUES=%s (set before HIP initialises)" % os.environ.get("GPU_MAX_HW_QUEUES")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs on the GPU box)")

@@ -23,7 +23,15 @@ def _ids(body):
     return list(dict.fromkeys(ids))
 
 
-def test_commit_past_the_log_with_eviction(gpu_engine_factory):
+@pytest.mark.parametrize("behind", [False, True], ids=["sync", "behind"])
+def test_commit_past_the_log_with_eviction(behind, gpu_engine_factory):
+    """behind: the Zig wrapper's engine_write_back_behind shape — each bar's delta captured
+    asynchronously and delivered to the forest while the next bar commits (its posts and voids of
+    the previous bars' pending transfers included); eviction is refused while a delta is in flight
+    and while any commit is unwritten, so the wrapper writes a bar back synchronously when the log
+    is three-quarters full and evicts then (an eviction one bar behind could drop a
+    pending transfer the bar in flight posts)."""
+    from tigerbeetle_amd._lib import EngineError
     cap = 1 << 14
     engine = gpu_engine_factory(accounts_max=4096, transfers_max=cap, pass_events_max=8192, pass_batches_max=16)
     sc = make_scenario(2024, n_accounts=64, n_transfer_batches=320, batch_len=(100, 400), p_pending=0.3,
@@ -31,9 +39,18 @@ def test_commit_past_the_log_with_eviction(gpu_engine_factory):
                        id_space=1 << 40)
     oracle = OracleEngine(4096, 1 << 17)
     forest, forest_posted = {}, {}  # the durable copy, built from the write-backs only
-    loads = evictions = committed = 0
+    loads = evictions = committed = refused = 0
     codes = set()
     bar = 16
+    inflight = False
+
+    def apply(d):
+        for rec in d.transfers:
+            key = (int(rec["id_lo"]), int(rec["id_hi"]))
+            forest[key] = rec.tobytes()
+        for pts, voided in d.posted:
+            forest_posted[int(pts)] = 2 if voided else 1
+
     for k, (_, op, ts, events) in enumerate(sc.steps):
         body = b"".join(events)
         if op == 129:
@@ -52,18 +69,28 @@ def test_commit_past_the_log_with_eviction(gpu_engine_factory):
             committed += len(events)
             codes.update(np.frombuffer(expected, dtype=np.uint32)[1::2].tolist())
         if k % bar == bar - 1:
-            d = engine.checkpoint_delta()
-            for rec in d.transfers:
-                key = (int(rec["id_lo"]), int(rec["id_hi"]))
-                forest[key] = rec.tobytes()
-            for pts, voided in d.posted:
-                forest_posted[int(pts)] = 2 if voided else 1
-            st = engine.stats()
-            if st["log_used"] > cap // 2:
+            full = engine.stats()["log_used"] > cap // 2
+            if behind and inflight:
+                with pytest.raises(EngineError):  # a delta in flight
+                    engine.evict_transfers(cap // 4)
+                apply(engine.checkpoint_delta_wait())
+                inflight = False
+                with pytest.raises(EngineError):  # this bar's commits are not written back
+                    engine.evict_transfers(cap // 4)
+                refused += 2
+            if behind and not full:
+                engine.checkpoint_delta_async((1 << 14, 1 << 14, 1 << 14))
+                inflight = True
+                continue
+            apply(engine.checkpoint_delta())
+            if full:
                 evictions += engine.evict_transfers(cap // 4)
+    if inflight:
+        apply(engine.checkpoint_delta_wait())
     st = engine.stats()
     assert committed > 3 * cap and st["log_capacity"] == cap
     assert evictions > 0 and st["transfers_evicted"] == evictions and loads > 0
+    assert refused > 0 or not behind
     # The evicted transfers were named again: duplicates and two-phase results against them.
     assert 46 in codes or any(c in codes for c in range(36, 46)), codes  # exists / exists_with_different_*
     assert 33 in codes or 34 in codes, codes  # already posted / voided

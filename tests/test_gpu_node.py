@@ -115,17 +115,15 @@ def test_node_refuses_device_resident(node_factory):
         engine.commit_device_async(129, [10], [1], 0, 0, 0)
 
 
-@pytest.mark.parametrize("config,shards", [("c3", 2), ("c3", 4), ("c4", 2), ("c4", 4)])
-def test_node_dirty_passes_split(config, shards, node_factory):
-    """BASELINE C3 / C4 shapes at 1M accounts and 2M transfers, through 2 and 4 shards in
-    64-prepare blocks: every dirty pass is SPLIT — the dependent subsequence committed in order by
-    the sequencer, the rest routed — never sequenced whole (no host code walks the events); every
-    reply, account, transfer and posted entry equals the oracle's."""
+def _commit_generated(config, shards, chunk, n_acc, n_xfer, seed, node_factory):
+    """Commit a BASELINE shape (the device generator's accounts, then its transfers from registered
+    host memory in `chunk`-prepare blocks) on a node of `shards` logical shards and the oracle; every
+    reply, account, transfer and posted entry must be equal. Returns the node's stats."""
     from tests.harness.configs import SETTINGS
-    n_acc, n_xfer, batch, chunk = 1_000_000, 2_000_000, 8190, 64
+    batch = 8190
     engine = node_factory(devices=(0,) * shards, accounts_max=n_acc, transfers_max=n_xfer,
                           pass_events_max=chunk * batch, pass_batches_max=chunk)
-    accts, xfers = generate(engine, config, n_acc, n_xfer, seed=11 + shards)
+    accts, xfers = generate(engine, config, n_acc, n_xfer, seed=seed)
     a_lens, x_lens = batches(n_acc, batch), batches(n_xfer, batch)
     a_ts, t = timestamps(a_lens, 10**12)
     x_ts, _ = timestamps(x_lens, t + 10, gap_every=SETTINGS[config]["gap_every"])
@@ -147,11 +145,50 @@ def test_node_dirty_passes_split(config, shards, node_factory):
         off += L
     for k, (e, a) in enumerate(zip(expected, got)):
         assert e == a, "reply of prepare %d differs" % k
-    assert sum(len(r) for r in expected) > 0
     assert_same_state(oracle, engine)
     st = engine.stats()
+    led = engine.ledger_summary()
+    assert led["stray"] == 0, led
+    return expected, st
+
+
+@pytest.mark.parametrize("config,shards", [("c3", 2), ("c3", 4), ("c4", 2), ("c4", 4)])
+def test_node_dirty_passes_split(config, shards, node_factory):
+    """BASELINE C3 / C4 shapes at 1M accounts and 2M transfers, through 2 and 4 shards in
+    64-prepare blocks: every dirty pass is SPLIT — the dependent subsequence committed in order by
+    the sequencer, the rest routed — never sequenced whole (no host code walks the events); every
+    reply, account, transfer and posted entry equals the oracle's."""
+    n_xfer = 2_000_000
+    expected, st = _commit_generated(config, shards, 64, 1_000_000, n_xfer, 11 + shards, node_factory)
+    assert sum(len(r) for r in expected) > 0
     assert st["node_passes_whole"] == 0 and st["node_passes_split"] > 0, st
     assert 0 < st["node_sequenced_events"] < n_xfer, st  # only the dependent subsequence is sequenced
+
+
+def test_node_hw_queues_env():
+    """The suite runs the node with every stream on its own hardware queue (tests/conftest.py), the
+    concurrency of N real devices; GPU_MAX_HW_QUEUES=4 (HIP's default) is the case that hid round 5's
+    sequencer race."""
+    import os
+    print("GPU_MAX_HW_QUEUES=%s" % os.environ.get("GPU_MAX_HW_QUEUES"))
+    assert int(os.environ.get("GPU_MAX_HW_QUEUES", "0")) >= 8
+
+
+@pytest.mark.parametrize("config", ["c2", "c3", "c4"])
+def test_node_eight_shards(config, node_factory):
+    """BASELINE configs[4]'s shard count: eight logical shards (devices = (0,) * 8), 16-prepare
+    blocks so that every pass has all eight sources busy (128 prepares, 1.05M transfers a pass).
+    c2 is C5's clean shape (uniform accounts, 7/8 of the legs cross shards), c3 / c4 its dirty
+    shapes (limit accounts under Zipf; chains and two-phase): byte-exact against the oracle, the
+    ledger's stray balance zero, and every dirty pass split, never sequenced whole."""
+    n_xfer = 2_500_000
+    expected, st = _commit_generated(config, 8, 16, 1_000_000, n_xfer, 31, node_factory)
+    if config == "c2":
+        assert st["node_passes_split"] == 0 and st["node_passes_whole"] == 0, st
+    else:
+        assert sum(len(r) for r in expected) > 0
+        assert st["node_passes_whole"] == 0 and st["node_passes_split"] > 0, st
+        assert 0 < st["node_sequenced_events"] < n_xfer, st
 
 
 @pytest.mark.parametrize("shards", [2, 3])

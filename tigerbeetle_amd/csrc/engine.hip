@@ -3015,6 +3015,11 @@ extern "C" int tbgpu_evict_transfers(tbgpu_t* E, uint64_t keep, uint64_t* evicte
     if (E->wb.inflight) return fail(TBGPU_STATUS_INVALID, "an asynchronous write-back is in flight");
     int st = engine_sync(E);
     if (st) return st;
+    // Only right after a write-back: a commit since then may post or void a pending transfer before
+    // the cut, and the next write-back reads that record (tb_delta_posted) and its posted state.
+    if (E->ckpt_valid && E->ckpt_pos != E->log_next)
+        return fail(TBGPU_STATUS_INVALID, "%llu log positions written since the last write-back",
+                    (unsigned long long)(E->log_next - E->ckpt_pos));
     const u64 written = E->ckpt_valid ? E->ckpt_pos : 0;  // positions the forest already holds
     const u64 cut = std::min<u64>(written, E->log_next > keep ? E->log_next - keep : 0);
     if (cut == 0) return TBGPU_STATUS_OK;

@@ -198,6 +198,9 @@ pub fn StateMachineType(
 
         prefetch_input: ?[]align(16) const u8 = null,
         prefetch_operation: Operation = undefined,
+        /// The prefetch in flight loads only the ids transfers_cold flagged (cold_ids[0..n]); the
+        /// engine resolves the rest from HBM and the body is staged as on the fast path.
+        prefetch_cold: u32 = 0,
         prefetch_callback: ?*const fn (*StateMachine) void = null,
         prefetch_context: PrefetchContext = undefined,
 
@@ -240,6 +243,12 @@ pub fn StateMachineType(
                 engine_config.device_count = @intCast(options.engine_devices.len);
                 for (options.engine_devices, 0..) |d, i| engine_config.devices[i] = d;
             }
+            // Eviction (evict_if_full) runs at a bar boundary once the log is three-quarters full
+            // and keeps the newest quarter: the rest must hold a bar of commits plus the transfers
+            // its prefetches load back (an id and a pending id per event), or a commit could find
+            // the log full in the middle of a bar.
+            if (options.engine_devices.len < 2 and
+                options.engine_transfers_max / 4 < 3 * bar_transfers_max) return error.EngineInit;
             var engine: ?*tbgpu.tbgpu_t = null;
             if (tbgpu.tbgpu_init(&engine_config, &engine) != tbgpu.TBGPU_STATUS_OK) return error.EngineInit;
             errdefer tbgpu.tbgpu_deinit(engine);
@@ -372,12 +381,27 @@ pub fn StateMachineType(
             _ = op;
             assert(self.prefetch_input == null);
             assert(self.prefetch_callback == null);
-            if (self.engine_complete and !self.transfers_cold(operation, input)) {
-                if (self.engine_stage_bodies and (operation == .create_accounts or operation == .create_transfers)) {
-                    self.register_message(input);
-                    check(tbgpu.tbgpu_prefetch(self.engine, @intFromEnum(operation), input.ptr, @intCast(input.len)));
+            if (self.engine_complete) {
+                const cold = self.transfers_cold(operation, input);
+                if (cold == 0) {
+                    self.stage_body(operation, input);
+                    return callback(self);
                 }
-                return callback(self);
+                // Only the flagged ids go through the groove (a Bloom false positive costs one
+                // groove lookup, as the reference's own prefetch does for every id); the accounts
+                // are resident (never evicted).
+                self.prefetch_input = input;
+                self.prefetch_operation = operation;
+                self.prefetch_callback = callback;
+                self.prefetch_cold = cold;
+                self.forest.grooves.transfers.prefetch_setup(null);
+                self.forest.grooves.posted.prefetch_setup(null);
+                for (self.cold_ids[0..cold]) |pair| {
+                    self.forest.grooves.transfers.prefetch_enqueue(@as(u128, pair[1]) << 64 | pair[0]);
+                }
+                self.prefetch_context = .{ .transfers = undefined };
+                self.forest.grooves.transfers.prefetch(prefetch_transfers_done, &self.prefetch_context.transfers);
+                return;
             }
 
             self.prefetch_input = input;
@@ -417,12 +441,21 @@ pub fn StateMachineType(
             }
         }
 
-        /// After an eviction: does the prepare name a transfer the engine may have dropped (its ids,
-        /// a post / void's pending id; lookup_transfers' ids)?  Then the groove prefetch below runs
-        /// and loads what the forest holds and the engine lacks (tbgpu_load_transfers), as after a
-        /// restart.  A false positive (Bloom filter) only costs that prefetch.
-        fn transfers_cold(self: *StateMachine, operation: Operation, input: []align(16) const u8) bool {
-            if (self.engine_evicted == 0) return false;
+        fn stage_body(self: *StateMachine, operation: Operation, input: []align(16) const u8) void {
+            if (self.engine_stage_bodies and (operation == .create_accounts or operation == .create_transfers)) {
+                self.register_message(input);
+                check(tbgpu.tbgpu_prefetch(self.engine, @intFromEnum(operation), input.ptr, @intCast(input.len)));
+            }
+        }
+
+        /// After an eviction: which transfers the prepare names may the engine have dropped (its ids,
+        /// a post / void's pending id; lookup_transfers' ids)?  Compacts them into cold_ids and
+        /// returns how many: only those go through the groove prefetch and are loaded
+        /// (tbgpu_load_transfers) when the forest holds them.  A false positive (Bloom filter) only
+        /// costs that id's groove lookup; a saturated filter degrades to the reference's own
+        /// prefetch of every id, never to a wrong answer.
+        fn transfers_cold(self: *StateMachine, operation: Operation, input: []align(16) const u8) u32 {
+            if (self.engine_evicted == 0) return 0;
             var n: u32 = 0;
             switch (operation) {
                 .create_transfers => for (mem.bytesAsSlice(Transfer, input)) |*t| {
@@ -437,12 +470,17 @@ pub fn StateMachineType(
                     self.cold_ids[n] = .{ @truncate(id), @truncate(id >> 64) };
                     n += 1;
                 },
-                else => return false,
+                else => return 0,
             }
-            if (n == 0) return false;
+            if (n == 0) return 0;
             check(tbgpu.tbgpu_transfers_maybe_cold(self.engine, @ptrCast(self.cold_ids.ptr), n, self.cold_flags.ptr));
-            for (self.cold_flags[0..n]) |c| if (c != 0) return true;
-            return false;
+            var cold: u32 = 0;
+            for (self.cold_ids[0..n], self.cold_flags[0..n]) |pair, c| {
+                if (c == 0) continue;
+                self.cold_ids[cold] = pair;
+                cold += 1;
+            }
+            return cold;
         }
 
         fn parent_of(comptime field: std.meta.FieldEnum(PrefetchContext), completion: anytype) *StateMachine {
@@ -452,6 +490,17 @@ pub fn StateMachineType(
 
         fn prefetch_transfers_done(completion: *TransfersGroove.PrefetchContext) void {
             const self = parent_of(.transfers, completion);
+            if (self.prefetch_cold > 0) {
+                // The loaded transfers' posted entries (push_transfer reads them).
+                for (self.cold_ids[0..self.prefetch_cold]) |pair| {
+                    if (self.forest.grooves.transfers.get(@as(u128, pair[1]) << 64 | pair[0])) |t| {
+                        self.forest.grooves.posted.prefetch_enqueue(t.timestamp);
+                    }
+                }
+                self.prefetch_context = .{ .posted = undefined };
+                self.forest.grooves.posted.prefetch(prefetch_posted_done, &self.prefetch_context.posted);
+                return;
+            }
             if (self.prefetch_operation == .lookup_transfers) return self.prefetch_finish();
             // src/state_machine.zig:434-458: the pending transfer's posted entry and accounts.
             for (mem.bytesAsSlice(Transfer, self.prefetch_input.?)) |*t| {
@@ -488,6 +537,21 @@ pub fn StateMachineType(
             var na: u32 = 0;
             var nt: u32 = 0;
             const grooves = &self.forest.grooves;
+            if (self.prefetch_cold > 0) {
+                for (self.cold_ids[0..self.prefetch_cold]) |pair| {
+                    if (grooves.transfers.get(@as(u128, pair[1]) << 64 | pair[0])) |t| self.push_transfer(&nt, t);
+                }
+                if (nt > 0) {
+                    check(tbgpu.tbgpu_load_transfers(self.engine, self.load_transfers.ptr, self.load_posted.ptr, nt));
+                }
+                self.prefetch_cold = 0;
+                self.stage_body(self.prefetch_operation, input); // after the loads: the next commit's
+                const callback_cold = self.prefetch_callback.?;
+                self.prefetch_input = null;
+                self.prefetch_callback = null;
+                self.prefetch_context = undefined;
+                return callback_cold(self);
+            }
             switch (self.prefetch_operation) {
                 .create_accounts => for (mem.bytesAsSlice(Account, input)) |*a| {
                     if (grooves.accounts.get(a.id)) |found| self.push_account(&na, found);
@@ -608,11 +672,15 @@ pub fn StateMachineType(
             assert(self.compact_callback == null);
             assert(self.checkpoint_callback == null);
             if ((op + 1) % config.lsm_batch_multiple == 0) {
-                if (self.writeback_sets == 2 and !write_back_synchronous(op)) {
+                if (self.writeback_sets == 2 and !write_back_synchronous(op) and !self.log_needs_eviction()) {
                     self.write_back_behind();
                 } else {
                     self.write_back_deliver(); // the bar in flight first: the grooves take bars in order
                     self.write_back();
+                    // Only here may transfers leave: every commit is written back and no delta is
+                    // in flight (tbgpu_evict_transfers refuses otherwise). One bar behind, a post /
+                    // void of the bar in flight could name a pending transfer an eviction dropped.
+                    self.evict_if_full();
                 }
             }
             self.compact_callback = callback;
@@ -689,7 +757,6 @@ pub fn StateMachineType(
         }
 
         fn write_back_apply(self: *StateMachine, set: *const WriteBack, counts: *const tbgpu.tbgpu_delta_counts) void {
-            defer self.evict_if_full();
             const grooves = &self.forest.grooves;
             for (set.accounts[0..counts.accounts], set.accounts_before[0..counts.accounts]) |*a, before| {
                 if (a.timestamp > counts.created_after) {
@@ -718,14 +785,22 @@ pub fn StateMachineType(
             }
         }
 
-        /// Bounded residency: once the bar is in the grooves, a transfer log three-quarters full
-        /// drops what the forest now holds, keeping the newest quarter (tbgpu_evict_transfers);
-        /// a later prefetch that names a dropped transfer loads it back (transfers_cold).
-        fn evict_if_full(self: *StateMachine) void {
-            if (self.engine_node) return;
+        /// The transfer log is three-quarters full: this bar writes back synchronously and evicts.
+        fn log_needs_eviction(self: *StateMachine) bool {
+            if (self.engine_node) return false;
             var stats: tbgpu.tbgpu_stats = undefined;
             check(tbgpu.tbgpu_get_stats(self.engine, &stats));
-            if (stats.log_capacity == 0 or stats.log_used * 4 < stats.log_capacity * 3) return;
+            return stats.log_capacity != 0 and stats.log_used * 4 >= stats.log_capacity * 3;
+        }
+
+        /// Bounded residency: once the bar is in the grooves (synchronously, nothing committed
+        /// since), a transfer log three-quarters full drops what the forest now holds, keeping the
+        /// newest quarter (tbgpu_evict_transfers); a later prefetch that names a dropped transfer
+        /// loads it back (transfers_cold).
+        fn evict_if_full(self: *StateMachine) void {
+            if (!self.log_needs_eviction()) return;
+            var stats: tbgpu.tbgpu_stats = undefined;
+            check(tbgpu.tbgpu_get_stats(self.engine, &stats));
             var evicted: u64 = 0;
             check(tbgpu.tbgpu_evict_transfers(self.engine, stats.log_capacity / 4, &evicted));
             self.engine_evicted += evicted;
