@@ -80,6 +80,9 @@ def parse():
                    help="timed steps of the host path (prepares in registered host memory, PCIe inclusive; 0: skip)")
     p.add_argument("--secondary", type=int, default=10_000_000,
                    help="transfers of the C3 / C4 secondary lines (0: skip)")
+    p.add_argument("--secondary-device", type=int, default=100_000_000,
+                   help="transfers of the C3 / C4 secondary lines' device-resident leg (in place, as the headline; "
+                        "BASELINE.md's 100M; 0: skip)")
     p.add_argument("--cpu-sample", type=int, default=12_285_000, help="transfers in the CPU baseline / parity sample (0: skip)")
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--walk-merge", type=int, default=-1,
@@ -363,6 +366,11 @@ def run_secondary(args, kind, device):
               "posted_equal": bool(np.array_equal(eng.export_posted(), oracle.export_posted())),
               "failed_events": sum(len(r) for r in expected) // 8}
     eng.close()
+    device_resident = None
+    if args.secondary_device:
+        device_resident = run_secondary_device(args, kind, device, accts, a_lens, a_ts, t_cursor, oracle, expected,
+                                               p_lens, p_ts)
+        parity["device_sample_equal"] = device_resident["parity"]["sample_equal"]
     return {"workload": WORKLOAD_TEXT[kind] % (n_acct, n_xfer, args.batch),
             "value": round(n_xfer / (step_ms[0] / 1e3), 1), "unit": "transfers/s", "ms_per_step": round(step_ms[0], 3),
             "input": "registered host memory, %d-prepare pipelined chunks, PCIe inclusive" % args.chunk_prepares,
@@ -375,7 +383,105 @@ def run_secondary(args, kind, device):
                                "walk_heavy_blocked_ms", "walk_longest", "walk_crit_windows",
                                "walk_crit_blocks", "walk_crit_wait_ms", "walk_crit_ms")},
             "flow_phases_ms": flow_phases(stats),
-            "roofline": roof, "parity": parity}
+            "roofline": roof, "device_resident": device_resident, "parity": parity}
+
+
+def run_secondary_device(args, kind, device, accts, a_lens, a_ts, t_cursor, oracle, expected, p_lens, p_ts):
+    """The C3 / C4 line with its prepares resident in HBM, as the headline measures C2: BASELINE.md's
+    100M transfers generated at their transfer-log positions (tbgpu_log_window, untimed) and committed
+    in place with tbgpu_commit_device_async in passes of the line's chunk size; one warmup step and
+    one timed step, validate on the device clock, tb_flow (the ordered fallback) timed beside it.
+    Parity: the oracle's sample (the first 1M transfers, the same generator indices and timestamps)
+    committed in place from the post-account-creation state on the same engine."""
+    from tests.harness.configs import KINDS, SETTINGS
+    from tigerbeetle_amd.state_machine import Engine, Options
+
+    wl = SETTINGS[kind]
+    n_acct, n = 1_000_000, args.secondary_device
+    chunk = args.chunk_prepares
+    eng = Engine(Options(accounts_max=n_acct, transfers_max=n, pass_events_max=chunk * args.batch,
+                         pass_batches_max=chunk, device=device, profile=True))
+    try:
+        if args.walk_merge >= 0:
+            eng.walk_merge_max(args.walk_merge)
+        rb, _, _ = eng.commit_pipelined(128, a_ts, a_lens, accts, chunk_batches=chunk)
+        assert int(rb.sum()) == 0, "account creation returned errors"
+        ct_accounts = eng.commit_timestamp
+        lens = batches(n, args.batch)
+        res_dev = eng.alloc(n * 8)
+        rb_dev = eng.alloc((len(lens) + 2) * 4)
+        gen = dict(seed=args.seed, kind=KINDS[kind], limit_permille=wl["limit_permille"],
+                   hot_limited=wl.get("hot_limited", 0))
+
+        def place(count):
+            eng.reset_transfers()
+            window = eng.log_window(count)
+            eng.generate_transfers(window, 0, count, n_acct, **gen)
+            eng.sync()
+            return window
+
+        step_ms = []
+        for step in range(2):  # one warmup, one timed
+            window = place(n)
+            ts, t_cursor = timestamps(lens, t_cursor + 10, wl["gap_every"])
+            if step == 1:
+                breakdown = eng.stats()
+                eng.reset_stats()
+                eng.profile_mask(eng.PROF_APPLY | eng.PROF_PASS | eng.PROF_REPLAY)
+            else:
+                eng.profile_mask(eng.PROF_ALL)
+            t0 = time.perf_counter()
+            eng.commit_device_async(129, ts, lens, window, res_dev, rb_dev)
+            eng.sync()
+            if step == 1:
+                step_ms.append((time.perf_counter() - t0) * 1e3)
+        stats = eng.stats()
+        n_failed = int(eng.to_host(rb_dev, len(lens) * 4).view(np.uint32).sum()) // 8
+        accs = eng.export_accounts()
+
+        def total(field):
+            return sum(int(x) for x in accs[field + "_lo"]) + (sum(int(x) for x in accs[field + "_hi"]) << 64)
+
+        full_ok = bool(stats["transfers"] == n - n_failed and total("debits_posted") == total("credits_posted")
+                       and total("debits_pending") == total("credits_pending"))
+        n_val = (stats.get("span_launches") or [0])[0] or stats["launches_validate"]
+        per_launch = n / max(1, n_val)
+        roof = roofline(stats, expected_unique(n_acct, 2 * per_launch) / per_launch, per_launch,
+                        argparse.Namespace(transfers=n, steps=1), step_ms[0], breakdown, kernel="tb_transfers_validate")
+        pass_lat = np.sort(np.array(eng.pass_latencies()))
+
+        # Parity: the oracle's sample, in place, from the post-account-creation state.
+        n_par = sum(p_lens)
+        window = place(n_par)
+        eng.set_commit_timestamp(ct_accounts)
+        eng.commit_device_async(129, p_ts, p_lens, window, res_dev, rb_dev)
+        eng.sync()
+        rbp = eng.to_host(rb_dev, len(p_lens) * 4).view(np.uint32)
+        results = eng.to_host(res_dev, n_par * 8)
+        got, off = [], 0
+        for L, nb in zip(p_lens, rbp):
+            got.append(bytes(results[off * 8:off * 8 + int(nb)]))
+            off += L
+        sample_equal = bool(got == expected
+                            and eng.export_accounts().tobytes() == oracle.export_accounts().tobytes()
+                            and eng.export_transfers(cap=n_par).tobytes() == oracle.export_transfers().tobytes()
+                            and np.array_equal(eng.export_posted(), oracle.export_posted()))
+        for ptr in (res_dev, rb_dev):
+            eng.free(ptr)
+    finally:
+        eng.close()
+    return {"value": round(n / (step_ms[0] / 1e3), 1), "unit": "transfers/s", "ms_per_step": round(step_ms[0], 3),
+            "transfers": n, "pass_prepares": chunk,
+            "input": "prepares resident in HBM at their transfer-log positions, committed in place "
+                     "(tbgpu_log_window + tbgpu_commit_device_async), %d-prepare passes" % chunk,
+            "p99_batch_latency_ms": round(ref_percentile(pass_lat, 99), 3) if len(pass_lat) else None,
+            "dependent_events": stats["dependent_events"], "failed_events": n_failed,
+            "validate_ms": round(stats["span_ms"][0], 3) if stats.get("span_ms") else None,
+            "tb_flow_ms": round(stats["ms_replay"], 3),
+            "flow_ms_share": round(stats["ms_replay"] / step_ms[0], 4),
+            "flow_phases_ms": flow_phases(stats),
+            "roofline": roof,
+            "parity": {"sample_transfers": n_par, "sample_equal": sample_equal, "full_run_properties": full_ok}}
 
 
 def run_cpu_c1(engine, args):
@@ -911,6 +1017,8 @@ def main():
         sp = sec["parity"]
         parity[kind + "_sample_equal"] = bool(sp["replies_equal"] and sp["accounts_equal"] and sp["transfers_equal"]
                                               and sp["posted_equal"])
+        if sec.get("device_resident"):
+            parity[kind + "_device_sample_equal"] = sec["device_resident"]["parity"]["sample_equal"]
     line["parity"] = parity
     line["headline"] = {"value": line["value"], "unit": "transfers/s", "p99_batch_latency_ms": line["p99_batch_latency_ms"],
                         "roofline_frac": roof["frac"] if roof else None,

@@ -224,7 +224,9 @@ int tbgpu_checkpoint_delta(tbgpu_t* engine, void* accounts_out, void* accounts_b
  * to the engine, and no other write-back may start.  Needs buffers registered with
  * tbgpu_register_host and large enough for the bounds above; otherwise (or past one slice of the
  * engine's write-back buffers) the call runs the synchronous write-back and the wait returns at
- * once.  Single-device engines only. */
+ * once.  A node engine (device_count >= 2) merges its shards' objects at the call (owners'
+ * balances, homes' records, on the host) and its wait returns at once: the same contract, without the
+ * single device's overlap with the next commits. */
 int tbgpu_checkpoint_delta_async(tbgpu_t* engine, void* accounts_out, void* accounts_before_out, uint64_t accounts_cap,
                                  void* transfers_out, uint64_t transfers_cap, uint64_t* posted_out, uint64_t posted_cap);
 int tbgpu_checkpoint_delta_wait(tbgpu_t* engine, tbgpu_delta_counts* counts);
@@ -252,7 +254,9 @@ int tbgpu_load_transfers(tbgpu_t* engine, const void* transfers, const uint8_t* 
  *     wrapper's prefetch loads the cold ids its forest holds (tbgpu_load_transfers, with their posted
  *     state) before the commit of a prepare that names them (its ids and post / void pending ids);
  *     an id it does not load is taken as absent, as the reference's groove would report it.
- * Single-device engines (a node returns TBGPU_STATUS_INVALID). */
+ * A node engine evicts per home shard (each shard's log keeps its share of `keep`; log_used in
+ * tbgpu_stats is the fullest shard's fill in units of the node's capacity) and answers each id's
+ * cold query on its home shard. */
 int tbgpu_evict_transfers(tbgpu_t* engine, uint64_t keep, uint64_t* evicted);
 int tbgpu_transfers_maybe_cold(tbgpu_t* engine, const uint64_t* ids, uint32_t n, uint8_t* cold);
 
@@ -322,7 +326,8 @@ typedef struct tbgpu_stats {
     uint64_t account_table_bytes;
     uint64_t node_shard_account_bytes[16];
     /* Bounded residency (tbgpu_evict_transfers): transfers evicted so far, transfer-log positions in
-     * use and in all (a wrapper evicts when the log fills; single-device engines). */
+     * use and in all (a wrapper evicts when the log fills; a node: the sums over its shards, log_used
+     * the fullest shard's fill times the node's capacity). */
     uint64_t transfers_evicted, log_used, log_capacity;
 } tbgpu_stats;
 

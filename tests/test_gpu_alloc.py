@@ -265,10 +265,12 @@ def test_kernel_spans_on_the_device_clock(gpu_engine_factory):
         assert 0 < per_span <= per_hip * 1.25 + 0.005, (k, per_span, per_hip)
 
 
+@pytest.mark.parametrize("devices", [None, (0, 0)], ids=["single", "node2"])
 @pytest.mark.parametrize("config", ["mixed", "two_phase", "chains"])
-def test_async_write_back_equals_sync(config, gpu_engine_factory):
+def test_async_write_back_equals_sync(config, devices, gpu_engine_factory):
     """Each segment's write-back through tbgpu_checkpoint_delta_async, waited for only after the
-    next segment committed, equals the synchronous write-back of an engine committing the same."""
+    next segment committed, equals the synchronous write-back of an engine committing the same
+    (node2: a two-shard node, whose asynchronous write-back merges the shards at the call)."""
     sc = make_scenario(707 + sum(map(ord, config)), **CONFIGS[config])
     cut = np.linspace(0, len(sc.steps), 5).astype(int)
     segs = []
@@ -276,7 +278,8 @@ def test_async_write_back_equals_sync(config, gpu_engine_factory):
         s = Scenario()
         s.steps = sc.steps[a:b]
         segs.append(s)
-    e_sync, e_async = gpu_engine_factory(), gpu_engine_factory()
+    kw = dict(devices=devices) if devices else {}
+    e_sync, e_async = gpu_engine_factory(**kw), gpu_engine_factory(**kw)
     caps = (1 << 14, 1 << 14, 1 << 14)
 
     def rows(arr):

@@ -39,10 +39,11 @@ def _posted(arr):
     return {int(ts): int(f) for ts, f in np.asarray(arr, dtype=np.uint64).reshape(-1, 2)}
 
 
+@pytest.mark.parametrize("devices", [None, (0, 0)], ids=["single", "node2"])
 @pytest.mark.parametrize("config", ["mixed", "two_phase", "chains", "limits"])
-def test_checkpoint_deltas(config, gpu_engine_factory):
+def test_checkpoint_deltas(config, devices, gpu_engine_factory):
     sc = make_scenario(99 + sum(map(ord, config)), **CONFIGS[config])
-    oracle, engine = OracleEngine(), gpu_engine_factory()
+    oracle, engine = OracleEngine(), gpu_engine_factory(**(dict(devices=devices) if devices else {}))
     forest_a, forest_t, forest_p = {}, {}, {}
     prev = (oracle.export_accounts(), oracle.export_transfers(), oracle.export_posted())
     for seg in _segments(sc, 3):

@@ -23,21 +23,31 @@ def _ids(body):
     return list(dict.fromkeys(ids))
 
 
+@pytest.mark.parametrize("devices", [None, (0, 0)], ids=["single", "node2"])
 @pytest.mark.parametrize("behind", [False, True], ids=["sync", "behind"])
-def test_commit_past_the_log_with_eviction(behind, gpu_engine_factory):
+def test_commit_past_the_log_with_eviction(behind, devices, gpu_engine_factory):
     """behind: the Zig wrapper's engine_write_back_behind shape — each bar's delta captured
     asynchronously and delivered to the forest while the next bar commits (its posts and voids of
     the previous bars' pending transfers included); eviction is refused while a delta is in flight
     and while any commit is unwritten, so the wrapper writes a bar back synchronously when the log
     is three-quarters full and evicts then (an eviction one bar behind could drop a
-    pending transfer the bar in flight posts)."""
+    pending transfer the bar in flight posts).
+
+    node2: a node of two logical shards (include/tbgpu.h: every home shard evicts from its own log and
+    answers the cold queries of the ids it homes; the node's write-back merges the shards)."""
     from tigerbeetle_amd._lib import EngineError
-    cap = 1 << 14
-    engine = gpu_engine_factory(accounts_max=4096, transfers_max=cap, pass_events_max=8192, pass_batches_max=16)
-    sc = make_scenario(2024, n_accounts=64, n_transfer_batches=320, batch_len=(100, 400), p_pending=0.3,
+    if devices:
+        engine = gpu_engine_factory(accounts_max=4096, transfers_max=1 << 14, pass_events_max=2048, pass_batches_max=16,
+                                    devices=devices)
+        n_batches = 520
+    else:
+        engine = gpu_engine_factory(accounts_max=4096, transfers_max=1 << 14, pass_events_max=8192, pass_batches_max=16)
+        n_batches = 320
+    cap = engine.stats()["log_capacity"]
+    sc = make_scenario(2024, n_accounts=64, n_transfer_batches=n_batches, batch_len=(100, 400), p_pending=0.3,
                        p_post_void=0.25, p_dup=0.08, p_linked=0.05, p_limit=0.05, p_balancing=0.02, p_invalid=0.03,
                        id_space=1 << 40)
-    oracle = OracleEngine(4096, 1 << 17)
+    oracle = OracleEngine(4096, 1 << 18)
     forest, forest_posted = {}, {}  # the durable copy, built from the write-backs only
     loads = evictions = committed = refused = 0
     codes = set()
@@ -89,6 +99,8 @@ def test_commit_past_the_log_with_eviction(behind, gpu_engine_factory):
         apply(engine.checkpoint_delta_wait())
     st = engine.stats()
     assert committed > 3 * cap and st["log_capacity"] == cap
+    if devices:
+        assert st["node_passes_split"] > 0  # the sequencer's passes ran against evicted homes too
     assert evictions > 0 and st["transfers_evicted"] == evictions and loads > 0
     assert refused > 0 or not behind
     # The evicted transfers were named again: duplicates and two-phase results against them.

@@ -106,7 +106,7 @@ def test_node_checkpoint_and_lookups(node_factory):
     """Write-back of a node equals the oracle's state diff (merged over the shards: each account's
     owner copy, each transfer from its home), and lookups read each object where it lives."""
     from tests.test_gpu_checkpoint import test_checkpoint_deltas
-    test_checkpoint_deltas("two_phase", lambda **kw: node_factory(devices=(0, 0, 0), **kw))
+    test_checkpoint_deltas("two_phase", None, lambda **kw: node_factory(devices=(0, 0, 0), **kw))
 
 
 def test_node_refuses_device_resident(node_factory):

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -484,6 +485,11 @@ static int node_sync(TbNode* N);
 static u64 node_commit_ts(TbNode* N);
 static int node_api_set_balances(TbNode* N, u64 id_lo, u64 id_hi, const u64 b[8]);
 static int node_api_export(TbNode* N, int what, void* out, u64 cap, u64* count);
+static int node_api_evict(TbNode* N, uint64_t keep, uint64_t* evicted);
+static int node_api_checkpoint_delta_async(TbNode* N, void* accounts_out, void* accounts_before_out, u64 accounts_cap,
+                                           void* transfers_out, u64 transfers_cap, u64* posted_out, u64 posted_cap);
+static int node_api_checkpoint_delta_wait(TbNode* N, tbgpu_delta_counts* counts);
+static int node_api_maybe_cold(TbNode* N, const uint64_t* ids, uint32_t n, uint8_t* cold);
 static int node_api_checkpoint_delta(TbNode* N, void* accounts_out, void* accounts_before_out, u64 accounts_cap,
                                      void* transfers_out, u64 transfers_cap, u64* posted_out, u64 posted_cap,
                                      tbgpu_delta_counts* counts);
@@ -1942,7 +1948,8 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
                                             uint64_t accounts_cap, void* transfers_out, uint64_t transfers_cap,
                                             uint64_t* posted_out, uint64_t posted_cap) {
     API_ENTER(E, true);
-    if (E->node) return fail(TBGPU_STATUS_INVALID, "asynchronous write-back needs a single-device engine");
+    if (E->node) return node_api_checkpoint_delta_async(E->node, accounts_out, accounts_before_out, accounts_cap,
+                                                        transfers_out, transfers_cap, posted_out, posted_cap);
     HIPCK(hipSetDevice(E->device));
     WbBufs& W = E->wb;
     if (W.inflight) return fail(TBGPU_STATUS_INVALID, "an asynchronous write-back is in flight (tbgpu_checkpoint_delta_wait)");
@@ -2107,7 +2114,7 @@ static int wb_pump(tbgpu* E, u64 budget, hipEvent_t after) {
 extern "C" int tbgpu_checkpoint_delta_wait(tbgpu_t* E, tbgpu_delta_counts* counts) {
     API_ENTER(E, false);
     memset(counts, 0, sizeof(*counts));
-    if (E->node) return fail(TBGPU_STATUS_INVALID, "asynchronous write-back needs a single-device engine");
+    if (E->node) return node_api_checkpoint_delta_wait(E->node, counts);
     HIPCK(hipSetDevice(E->device));
     return wb_wait(E, counts);
 }
@@ -3007,10 +3014,8 @@ extern "C" int tbgpu_load_transfers(tbgpu_t* E, const void* records, const uint8
 // Bounded residency (k_evict.h): drop the written-back transfers older than the newest `keep` log
 // positions.  Only what the last write-back covered can go (the forest holds it); the rest slides to
 // the front of the log and the index is rebuilt from it.  Synchronous.
-extern "C" int tbgpu_evict_transfers(tbgpu_t* E, uint64_t keep, uint64_t* evicted) {
-    API_ENTER(E, true);
+static int engine_evict(tbgpu_t* E, uint64_t keep, uint64_t* evicted) {
     *evicted = 0;
-    if (E->node) return fail(TBGPU_STATUS_INVALID, "eviction needs a single-device engine");
     HIPCK(hipSetDevice(E->device));
     if (E->wb.inflight) return fail(TBGPU_STATUS_INVALID, "an asynchronous write-back is in flight");
     int st = engine_sync(E);
@@ -3064,12 +3069,18 @@ extern "C" int tbgpu_evict_transfers(tbgpu_t* E, uint64_t keep, uint64_t* evicte
     return TBGPU_STATUS_OK;
 }
 
+
+extern "C" int tbgpu_evict_transfers(tbgpu_t* E, uint64_t keep, uint64_t* evicted) {
+    API_ENTER(E, true);
+    *evicted = 0;
+    if (E->node) return node_api_evict(E->node, keep, evicted);
+    return engine_evict(E, keep, evicted);
+}
+
 // The replica's prefetch after an eviction: which of n ids (lo, hi pairs) the engine may have evicted
 // — not resident, maybe in the filter.  The caller loads those its forest holds (tbgpu_load_transfers)
 // before committing the prepare that names them.
-extern "C" int tbgpu_transfers_maybe_cold(tbgpu_t* E, const uint64_t* ids, uint32_t n, uint8_t* cold) {
-    API_ENTER(E, false);
-    if (E->node) return fail(TBGPU_STATUS_INVALID, "eviction needs a single-device engine");
+static int engine_maybe_cold(tbgpu_t* E, const uint64_t* ids, uint32_t n, uint8_t* cold) {
     if (n == 0) return TBGPU_STATUS_OK;
     if (E->evicted_total == 0) {  // nothing ever left: nothing is cold
         memset(cold, 0, n);
@@ -3090,6 +3101,12 @@ extern "C" int tbgpu_transfers_maybe_cold(tbgpu_t* E, const uint64_t* ids, uint3
         HIPCK(hipStreamSynchronize(E->stream));
     }
     return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_transfers_maybe_cold(tbgpu_t* E, const uint64_t* ids, uint32_t n, uint8_t* cold) {
+    API_ENTER(E, false);
+    if (E->node) return node_api_maybe_cold(E->node, ids, n, cold);
+    return engine_maybe_cold(E, ids, n, cold);
 }
 
 extern "C" int tbgpu_set_commit_timestamp(tbgpu_t* E, uint64_t timestamp) {

@@ -174,6 +174,10 @@ struct TbNode {
     u64* h_seq = nullptr;        // pinned scratch words
     u64 passes_clean = 0, passes_split = 0, passes_whole = 0, seq_events = 0;
     bool limit_any = false;          // some account carries a limit flag (the bitmaps are consulted)
+    // tbgpu_checkpoint_delta_async on a node: the merged delta is produced at the call (the shards'
+    // objects are merged on the host, node_api_checkpoint_delta); the wait returns its counts.
+    bool wb_inflight = false;
+    tbgpu_delta_counts wb_counts{};
     u64 x_limit_seen = 0;            // the sequencer's limit_accounts count when last read
     const u64* api_calls = nullptr;  // the node handle's entry-point count (tbgpu::api_calls)
     NodePass ring[NODE_PASS_RING];   // a call's passes, built as they are planned (no per-call allocation)
@@ -1752,6 +1756,7 @@ static int node_api_checkpoint_delta(TbNode* N, void* accounts_out, void* accoun
                                      tbgpu_delta_counts* counts) {
     memset(counts, 0, sizeof(*counts));
     const u32 W = N->world;
+    if (N->wb_inflight) return fail(TBGPU_STATUS_INVALID, "an asynchronous write-back is in flight (tbgpu_checkpoint_delta_wait)");
     int st = node_sync(N);
     if (st) return st;
     WbBounds bd{0, 0, 0};
@@ -1871,6 +1876,7 @@ static int node_api_get_stats(TbNode* N, tbgpu_stats* s) {
     s->node_passes_split = N->passes_split;
     s->node_passes_whole = N->passes_whole;
     s->node_sequenced_events = N->seq_events;
+    double fill = 0;
     for (u32 d = 0; d <= N->world; d++) {  // every shard, then the sequencer (its ordered-path work)
         const bool seq = d == N->world;
         tbgpu_stats x;
@@ -1878,6 +1884,11 @@ static int node_api_get_stats(TbNode* N, tbgpu_stats* s) {
         if (st) return st;
         s->dependent_events += x.dependent_events;
         if (!seq) {
+            // Bounded residency per home shard: the log is as full as its fullest shard (a commit that
+            // overruns any shard's log is refused), in units of the node's total capacity.
+            s->transfers_evicted += x.transfers_evicted;
+            s->log_capacity += x.log_capacity;
+            if (x.log_capacity) fill = std::max(fill, (double)x.log_used / (double)x.log_capacity);
             s->node_shard_account_bytes[d] = x.account_table_bytes;
             s->account_table_bytes = std::max(s->account_table_bytes, x.account_table_bytes);
             s->passes += x.passes;
@@ -1930,6 +1941,7 @@ static int node_api_get_stats(TbNode* N, tbgpu_stats* s) {
         s->walk_crit_wait_ms += x.walk_crit_wait_ms;
         s->walk_crit_ms += x.walk_crit_ms;
     }
+    s->log_used = (u64)std::ceil(fill * (double)s->log_capacity);
     return TBGPU_STATUS_OK;
 }
 
@@ -2018,4 +2030,82 @@ static int node_api_set_commit_timestamp(TbNode* N, u64 timestamp) {
     if (st) return st;
     N->commit_ts = timestamp;
     return node_publish_commit_ts(N);
+}
+
+// Bounded residency on a node (include/tbgpu.h tbgpu_evict_transfers): every home shard evicts from
+// its own log what the last write-back covered, keeping its share of `keep` (its log's fraction of
+// the node's).  Refused as a whole, before any shard moves, while any shard has a log position the
+// last write-back did not cover (the node's write-back covers every shard at once).
+static int node_api_evict(TbNode* N, uint64_t keep, uint64_t* evicted) {
+    *evicted = 0;
+    if (N->wb_inflight) return fail(TBGPU_STATUS_INVALID, "an asynchronous write-back is in flight");
+    int st = node_sync(N);
+    if (st) return st;
+    u64 cap = 0;
+    for (u32 d = 0; d < N->world; d++) {
+        const tbgpu* E = N->D[d].E;
+        if (E->wb.inflight) return fail(TBGPU_STATUS_INVALID, "an asynchronous write-back is in flight");
+        if (E->ckpt_valid && E->ckpt_pos != E->log_next) {
+            return fail(TBGPU_STATUS_INVALID, "shard %u: %llu log positions written since the last write-back", d,
+                        (unsigned long long)(E->log_next - E->ckpt_pos));
+        }
+        cap += E->xlog_cap;
+    }
+    for (u32 d = 0; d < N->world; d++) {
+        tbgpu* E = N->D[d].E;
+        const u64 k = cap ? (u64)((unsigned __int128)keep * E->xlog_cap / cap) : 0;
+        u64 ev = 0;
+        if ((st = engine_evict(E, k, &ev))) return st;
+        *evicted += ev;
+    }
+    return TBGPU_STATUS_OK;
+}
+
+// tbgpu_transfers_maybe_cold on a node: each id asks its home shard (the one that would hold it and
+// whose filter holds it if it left).
+static int node_api_maybe_cold(TbNode* N, const uint64_t* ids, uint32_t n, uint8_t* cold) {
+    memset(cold, 0, n);
+    int st = node_sync(N);
+    if (st) return st;
+    const u32 W = N->world;
+    std::vector<u64> per[NODE_WORLD_MAX];
+    std::vector<u32> where[NODE_WORLD_MAX];
+    for (u32 i = 0; i < n; i++) {
+        const u32 h = tb_home(ids[2 * i], ids[2 * i + 1], W);
+        per[h].push_back(ids[2 * i]);
+        per[h].push_back(ids[2 * i + 1]);
+        where[h].push_back(i);
+    }
+    std::vector<u8> c;
+    for (u32 h = 0; h < W; h++) {
+        const u32 m = (u32)where[h].size();
+        if (!m) continue;
+        c.assign(m, 0);
+        if ((st = engine_maybe_cold(N->D[h].E, per[h].data(), m, c.data()))) return st;
+        for (u32 j = 0; j < m; j++) cold[where[h][j]] = c[j];
+    }
+    return TBGPU_STATUS_OK;
+}
+
+// tbgpu_checkpoint_delta_async / _wait on a node: the same contract (the buffers belong to the engine
+// until the wait; no other write-back may start), with the merged delta produced at the call.  The
+// overlap with the next bar's commits that a single device gets (its capture in stream order, the
+// objects crossing PCIe beside the commits) is not built for a node: its objects are merged over the
+// shards on the host (owners' balances, homes' records).
+static int node_api_checkpoint_delta_async(TbNode* N, void* accounts_out, void* accounts_before_out, u64 accounts_cap,
+                                           void* transfers_out, u64 transfers_cap, u64* posted_out, u64 posted_cap) {
+    tbgpu_delta_counts c;
+    const int st = node_api_checkpoint_delta(N, accounts_out, accounts_before_out, accounts_cap, transfers_out,
+                                             transfers_cap, posted_out, posted_cap, &c);
+    if (st) return st;
+    N->wb_counts = c;
+    N->wb_inflight = true;
+    return TBGPU_STATUS_OK;
+}
+
+static int node_api_checkpoint_delta_wait(TbNode* N, tbgpu_delta_counts* counts) {
+    if (!N->wb_inflight) return fail(TBGPU_STATUS_INVALID, "no asynchronous write-back in flight");
+    N->wb_inflight = false;
+    *counts = N->wb_counts;
+    return TBGPU_STATUS_OK;
 }

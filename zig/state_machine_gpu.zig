@@ -192,9 +192,6 @@ pub fn StateMachineType(
         /// transfer log fills).  Non-zero: a create_transfers / lookup_transfers prefetch asks the
         /// engine which of its ids may be cold and takes the forest path when any is.
         engine_evicted: u64 = 0,
-        /// A node engine (engine_devices >= 2): its shards do not evict (tbgpu.h), so its transfer
-        /// log bounds the ledger it holds.
-        engine_node: bool,
 
         prefetch_input: ?[]align(16) const u8 = null,
         prefetch_operation: Operation = undefined,
@@ -247,14 +244,14 @@ pub fn StateMachineType(
             // and keeps the newest quarter: the rest must hold a bar of commits plus the transfers
             // its prefetches load back (an id and a pending id per event), or a commit could find
             // the log full in the middle of a bar.
-            if (options.engine_devices.len < 2 and
-                options.engine_transfers_max / 4 < 3 * bar_transfers_max) return error.EngineInit;
+            if (options.engine_transfers_max / 4 < 3 * bar_transfers_max) return error.EngineInit;
             var engine: ?*tbgpu.tbgpu_t = null;
             if (tbgpu.tbgpu_init(&engine_config, &engine) != tbgpu.TBGPU_STATUS_OK) return error.EngineInit;
             errdefer tbgpu.tbgpu_deinit(engine);
 
-            // A node engine writes back synchronously (tbgpu_checkpoint_delta_async is single-device).
-            const sets: u2 = if (options.engine_write_back_behind and options.engine_devices.len < 2) 2 else 1;
+            // A node engine's asynchronous write-back merges its shards at the call (tbgpu.h); the
+            // contract, and so this wrapper, is the same as a single device's.
+            const sets: u2 = if (options.engine_write_back_behind) 2 else 1;
             var writeback: [2]WriteBack = undefined;
             writeback[0] = try WriteBack.alloc(allocator);
             errdefer writeback[0].free(allocator);
@@ -291,7 +288,6 @@ pub fn StateMachineType(
                 .load_posted = load_posted,
                 .cold_ids = cold_ids,
                 .cold_flags = cold_flags,
-                .engine_node = options.engine_devices.len >= 2,
                 .engine_stage_bodies = options.engine_stage_bodies,
                 .engine_register_messages = options.engine_register_messages,
                 .registered_messages = registered_messages,
@@ -787,7 +783,6 @@ pub fn StateMachineType(
 
         /// The transfer log is three-quarters full: this bar writes back synchronously and evicts.
         fn log_needs_eviction(self: *StateMachine) bool {
-            if (self.engine_node) return false;
             var stats: tbgpu.tbgpu_stats = undefined;
             check(tbgpu.tbgpu_get_stats(self.engine, &stats));
             return stats.log_capacity != 0 and stats.log_used * 4 >= stats.log_capacity * 3;
