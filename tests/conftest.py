@@ -12,8 +12,9 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 # Every stream of the node engine on its own hardware queue, as on N real devices (HIP's default is
 # 4 per process, under which a 2-shard node's 7 streams share queues and serialise; round 5's
 # sequencer balance race showed only with 8). Set here, before any test module imports torch or
-# loads libtbgpu.so, i.e. before HIP reads it. `GPU_MAX_HW_QUEUES=4 pytest ...` keeps the old case.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# loads libtbgpu.so, i.e. before HIP reads it. The GPU box exports its own value (4), so it is
+# overridden; `TBGPU_TEST_HW_QUEUES=4 pytest ...` runs the old case.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("TBGPU_TEST_HW_QUEUES", "8")
 
 
 def pytest_report_header(config):

@@ -165,7 +165,8 @@ struct tbgpu {
     // Balance legs (k_apply.h); legs_ok = false: resolve applies every leg with atomics.
     bool legs_ok = false;
     u32 leg_shift = 0, leg_buckets = 0;
-    u64* leg_ev = nullptr;
+    u32* resolve_slow = nullptr;  // [pb_max] tb_resolve_lean's verdict per prepare of a legs pass
+    bool lean_ok = true;          // legs passes run tb_resolve_lean first (TBGPU_NO_LEAN=1: tb_resolve alone)
     u64* leg_w = nullptr;
     u32* leg_off = nullptr;
     u32* leg_tot = nullptr;  // [leg_buckets] legs per bucket of the current pass
@@ -556,6 +557,7 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     E->xidx_cap = pow2_at_least(std::max<u64>(2 * E->xlog_cap, 2048));
     E->pe_max = config->pass_events_max;
     E->pb_max = config->pass_batches_max;
+    if (const char* v = getenv("TBGPU_NO_LEAN")) E->lean_ok = atoi(v) == 0;
     E->dedup_cap = pow2_at_least(std::max<u64>(4ULL * E->pe_max, 64));
     E->undo_cap = 4 * (BATCH_EVENTS_MAX + 1);
     E->meta_cap = std::max<u64>(E->pb_max, 1 << 16);
@@ -656,7 +658,7 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     INIT_CK(tbMalloc(&E->sum_shards, SUM_WORDS * 8));
     INIT_CK(tbMalloc(&E->undo, (u64)E->undo_cap * sizeof(UndoEntry)));
     if (E->legs_ok) {
-        INIT_CK(tbMalloc(&E->leg_ev, pe * 2 * 8));
+        INIT_CK(tbMalloc(&E->resolve_slow, (u64)E->pb_max * 4));
         INIT_CK(tbMalloc(&E->leg_w, pe * 2 * 8));
         INIT_CK(tbMalloc(&E->leg_off, (u64)std::min<u32>(E->pb_max, LEG_PREPARES_MAX) * (E->leg_buckets + 1) * 4));
         INIT_CK(tbMalloc(&E->leg_tot, ((u64)E->leg_buckets + 1) * 4));
@@ -801,7 +803,7 @@ extern "C" void tbgpu_deinit(tbgpu_t* E) {
                     E->lookup_ids, E->lookup_out, E->lookup_found, E->d_status, E->pf_staging, E->kclock, E->r_home,
                     E->wb.d_bc, E->wb.d_base, E->wb.d_out, E->wb.d_ids, E->wb.d_pv, E->wb.d_pairs, E->wb.d_hids,
                     E->wb.d_acc, E->wb.d_before, E->wb.d_slots, E->wb.d_cap, E->wb.d_cnt,
-                    E->r_block_counts, E->r_words, E->r_meta, E->leg_ev, E->leg_w, E->leg_off, E->leg_tot,
+                    E->r_block_counts, E->r_words, E->r_meta, E->resolve_slow, E->leg_w, E->leg_off, E->leg_tot,
                     E->F.f_pe, E->F.f_batch, E->F.f_len, E->F.need, E->F.nsucc, E->F.queue, E->F.uflags, E->F.nacct, E->F.rpos, E->F.succ,
                     E->F.run, E->F.keys[0], E->F.keys[1], E->F.vals[0], E->F.vals[1], E->F.hist, E->F.words, E->F.undo,
                     E->F.b_st, E->F.b_vd, E->F.b_vc, E->F.b_amt, E->F.b_meta, E->F.b_blk,
@@ -941,7 +943,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.apply_late = (op == OP_CREATE_TRANSFERS && !P.legs) ? 1 : 0;
         P.leg_shift = E->leg_shift;
         P.leg_buckets = E->leg_buckets;
-        P.leg_ev = E->leg_ev;
+        P.resolve_slow = P.legs && E->lean_ok ? E->resolve_slow : nullptr;
         P.leg_w = E->leg_w;
         P.leg_off = E->leg_off;
         P.leg_tot = E->leg_tot;
@@ -981,8 +983,9 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
 
         if (imp && n > 0) {  // a node home: the foreign accounts this sub-pass names, from their owners
             const u32 ig = (u32)std::min<u64>(4096, (n + 255) / 256);
+            if (2 * n > imp->cap) return fail(TBGPU_STATUS_INVALID, "node import list: %llu events", (unsigned long long)n);
             hipLaunchKernelGGL(tb_node_import, dim3(ig), dim3(256), 0, E->stream, E->T, imp->N, events_dev + P.e0 * 128, n,
-                               imp->self, imp->list, imp->count, imp->cap, imp->os_of);
+                               imp->self, imp->list, imp->os_of);
             HIPCK(hipGetLastError());
         }
         if (n > 0) {
@@ -1008,6 +1011,10 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         }
         if ((st = prof_begin(E, &pp, K_RESOLVE))) return st;
         if (op == OP_CREATE_TRANSFERS) {
+            // A legs pass: the lean kernel first (the common case), tb_resolve for the prepares it left.
+            if (P.resolve_slow) {
+                hipLaunchKernelGGL(tb_resolve_lean, dim3(b1 - b0), dim3(RESOLVE_THREADS), 0, E->stream, P);
+            }
             hipLaunchKernelGGL(tb_resolve<OP_CREATE_TRANSFERS>, dim3(b1 - b0), dim3(RESOLVE_THREADS), 0, E->stream, P);
         } else {
             hipLaunchKernelGGL(tb_resolve<OP_CREATE_ACCOUNTS>, dim3(b1 - b0), dim3(RESOLVE_THREADS), 0, E->stream, P);
@@ -1053,7 +1060,8 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         }
         if (imp && imp->ev_legs) HIPCK(hipEventRecord((hipEvent_t)imp->ev_legs, E->stream));
         if (imp && n > 0) {  // the owned-only table again
-            hipLaunchKernelGGL(tb_node_import_clear, dim3(1024), dim3(256), 0, E->stream, E->T, imp->list, imp->count);
+            hipLaunchKernelGGL(tb_node_import_clear, dim3((u32)std::min<u64>(1024, (2 * n + 255) / 256)), dim3(256), 0,
+                               E->stream, E->T, imp->list, 2 * n);
             HIPCK(hipGetLastError());
         }
         if ((st = prof_end(E, &pass_pp))) return st;

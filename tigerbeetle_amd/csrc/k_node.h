@@ -214,8 +214,11 @@ struct NodeTablesArgs {
 // already there stops — the winner alone reads the owner's record, writes the entry and puts the real
 // timestamp last.  (Two ids with one 63-bit fingerprint meeting on one probe chain in one pass would
 // import one of them only: about 2^-63 per pair, the sequencer's own fingerprint bet.)
-__device__ static inline void tb_import_one(const Tables& H, const NodeTablesArgs& N, u64 lo, u64 hi, u32 o, u32* list,
-                                            u64* count, u64 cap, u32* os_of) {
+// The slot it claimed (TB_NOT_FOUND: none — another lane imports the id, or it is here already) goes
+// to *list_at: one entry per event side, no shared counter (a counter every importing wave added to
+// serialised at its L2 channel: 16K atomics on one word, ~0.3 ms of a 2-shard C2 pass).
+__device__ static inline void tb_import_one(const Tables& H, const NodeTablesArgs& N, u64 lo, u64 hi, u32 o, u32* list_at,
+                                            u32* os_of) {
     const u64 mark = (1ULL << 63) | (tb_fingerprint(lo, hi) >> 1);
     u64 pos = tb_hash_id(lo, hi) & H.account_mask;
     u32 slot = TB_NOT_FOUND;
@@ -244,10 +247,8 @@ __device__ static inline void tb_import_one(const Tables& H, const NodeTablesArg
         }
         pos = (pos + 1) & H.account_mask;
     }
+    *list_at = slot;
     if (slot == TB_NOT_FOUND) return;
-    const u64 k = tb_wave_claim(true, count);
-    if (k < cap) list[k] = slot;
-    else tb_panic(H.g, PANIC_TABLE_FULL);
     AccountHot a;
     const u32 os = tb_account_find_from(O, lo, hi, opos, o0, &a);
     AccountHot* h = &H.acct_hot[slot];
@@ -269,8 +270,9 @@ __device__ static inline void tb_import_one(const Tables& H, const NodeTablesArg
     __hip_atomic_store(&h->timestamp, a.timestamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// list: [2n] the slot each event side imported into (TB_NOT_FOUND: none), for tb_node_import_clear.
 __global__ __launch_bounds__(256) void tb_node_import(Tables H, NodeTablesArgs N, const u8* events, u64 n, u32 self,
-                                                      u32* list, u64* count, u64 cap, u32* os_of) {
+                                                      u32* list, u32* os_of) {
     __shared__ WgDedup s_d;
     for (u64 base = (u64)blockIdx.x * 256; base < n; base += (u64)gridDim.x * 256) {  // uniform per workgroup
         tb_wg_dedup_reset(s_d);
@@ -292,7 +294,8 @@ __global__ __launch_bounds__(256) void tb_node_import(Tables H, NodeTablesArgs N
         __syncthreads();
 #pragma unroll
         for (u32 s = 0; s < 2; s++) {
-            if (tb_wg_dedup_go(s_d, st[s], lo[s], hi[s])) tb_import_one(H, N, lo[s], hi[s], o[s], list, count, cap, os_of);
+            if (tb_wg_dedup_go(s_d, st[s], lo[s], hi[s])) tb_import_one(H, N, lo[s], hi[s], o[s], list + 2 * e + s, os_of);
+            else if (e < n) list[2 * e + s] = TB_NOT_FOUND;
         }
         __syncthreads();
     }
@@ -303,9 +306,9 @@ __global__ __launch_bounds__(256) void tb_node_import(Tables H, NodeTablesArgs N
 struct NodeImport {
     NodeTablesArgs N;
     u32 self;
-    u32* list;     // [cap] slots inserted
-    u64* count;    // zeroed by the sub-pass's tb_pass_clear
-    u64 cap;
+    u32* list;     // [cap] the slot each event side of a sub-pass imported into (TB_NOT_FOUND: none)
+    u64* count;    // zeroed by the sub-pass's tb_pass_clear (unused since the per-side list)
+    u64 cap;       // 2 x the sub-pass's events at most
     u32* os_of;    // [account_cap] imported slot -> the account's slot on its owner
     u64* leg_counts = nullptr;  // the home's per-owner leg counts, zeroed by the same tb_pass_clear
     u32 legs_n = 0;
@@ -314,10 +317,10 @@ struct NodeImport {
     void* ev_legs = nullptr;
 };
 
-__global__ void tb_node_import_clear(Tables H, const u32* list, const u64* count) {
-    const u64 n = *count;
+__global__ void tb_node_import_clear(Tables H, const u32* list, u64 n) {
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-        H.acct_hot[list[i]] = AccountHot{};
+        const u32 slot = list[i];
+        if (slot != TB_NOT_FOUND) H.acct_hot[slot] = AccountHot{};
     }
 }
 

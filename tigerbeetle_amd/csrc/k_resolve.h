@@ -117,10 +117,11 @@ __device__ static inline void tb_apply_transfer(const PassArgs& P, u32 pe, u32 i
 // independent ok create_transfer into the prepare's leg region [2*pbase, 2*pbase + 2L), grouped by
 // bucket: debit side into debits_pending / debits_posted, credit side into credits_pending /
 // credits_posted (:870-880).  The order inside a bucket is unspecified: the sums commute.
-// The final-results loop wrote each leg word in event order (leg_ev, coalesced); the counting sort
-// runs in LDS (s_perm: sorted position -> event << 1 | side, 2 B per leg) and the grouped copy is
-// stored in order, coalesced (scattering the words straight to their sorted places cost 4x the
-// whole sort: partial-line stores).
+// A leg word never leaves the registers of the thread that classified its event until it is stored
+// in bucket order: each leg takes its sorted position from its bucket's LDS cursor (the counting
+// sort), and the words go out through an LDS window of LEG_WIN words (the dead s_key array), each
+// window stored coalesced.  (Round 5 wrote the words in event order to a global array and gathered
+// them back through a 2-B LDS permutation: 32 B of traffic per transfer more.)
 // Per-bucket leg counter of a prepare: 16 bits each, two per LDS word (a prepare has at most
 // 16382 legs), so 4096 buckets fit in 8 KB.  Returns the counter's previous value.
 __device__ static inline u32 tb_hist16_inc(u32* s_hist, u32 bucket) {
@@ -129,11 +130,17 @@ __device__ static inline u32 tb_hist16_inc(u32* s_hist, u32 bucket) {
 }
 
 #define RESOLVE_K (BATCH_LDS / RESOLVE_THREADS)  // events per thread of a prepare
+#define LEG_WIN (BATCH_LDS / 2)                  // u64 words of the store window (s_key's 32 KB)
 
-__device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 L, u32 legmask, const u32* r_dr,
-                                           const u32* r_cr, u32* s_hist, u16* s_perm, u32* s_wave) {
+__device__ static inline u64 tb_leg_word(u32 slot, u32 leg_shift, u32 side, bool pending, u64 amount) {
+    const u32 mask = (1u << leg_shift) - 1;
+    return ((((u64)(slot & mask) << 2) | (side << 1) | (pending ? 0u : 1u)) << LEG_AMT_BITS) | amount;
+}
+
+__device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 legmask, u32 pendmask, const u32* r_dr,
+                                           const u32* r_cr, const u64* r_amt, u32* s_hist, u64* s_win, u32* s_wave) {
     if (TB_ABL(P, ABL_LEG_WORK)) return;
-    __syncthreads();  // every count is in; s_perm's LDS is free
+    __syncthreads();  // every count is in
     tb_block_scan_lds((u16*)s_hist, P.leg_buckets, s_wave);
     const u16* h = (const u16*)s_hist;
     const u32 nlegs = h[P.leg_buckets];
@@ -148,31 +155,28 @@ __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 L, 
         }
     }
     __syncthreads();  // the row is read before the starts advance as cursors
+    u32 r_pos[RESOLVE_K];  // sorted positions: debit leg in the low half, credit leg in the high half
 #pragma unroll
     for (u32 k = 0; k < RESOLVE_K; k++) {
+        r_pos[k] = 0;
         if (!((legmask >> k) & 1)) continue;
-        const u32 i = k * RESOLVE_THREADS + threadIdx.x;
-        s_perm[tb_hist16_inc(s_hist, r_dr[k] >> P.leg_shift)] = (u16)(i << 1);
-        s_perm[tb_hist16_inc(s_hist, r_cr[k] >> P.leg_shift)] = (u16)((i << 1) | 1);
+        r_pos[k] = tb_hist16_inc(s_hist, r_dr[k] >> P.leg_shift) | (tb_hist16_inc(s_hist, r_cr[k] >> P.leg_shift) << 16);
     }
-    __syncthreads();
     if (TB_ABL(P, ABL_LEG_STORES)) return;
-    // Gather in groups of four (the loads of a group are in flight together: leg_w and leg_ev are
-    // both u64 arrays, so the compiler would otherwise order each load after the previous store).
-    const u64* __restrict__ ev = P.leg_ev + 2ULL * pbase;
     u64* __restrict__ w = P.leg_w + 2ULL * pbase;
-    for (u32 j0 = 0; j0 < nlegs; j0 += 4 * blockDim.x) {
-        u64 v[4];
+    for (u32 w0 = 0; w0 < nlegs; w0 += LEG_WIN) {
+        __syncthreads();  // the window is free (the previous one stored; before the first: s_key is dead)
 #pragma unroll
-        for (u32 q = 0; q < 4; q++) {
-            const u32 j = j0 + q * blockDim.x + threadIdx.x;
-            v[q] = j < nlegs ? ev[s_perm[j]] : 0;
+        for (u32 k = 0; k < RESOLVE_K; k++) {
+            if (!((legmask >> k) & 1)) continue;
+            const bool pend = (pendmask >> k) & 1;
+            const u32 pd = (r_pos[k] & 0xFFFF) - w0, pc = (r_pos[k] >> 16) - w0;
+            if (pd < LEG_WIN) s_win[pd] = tb_leg_word(r_dr[k], P.leg_shift, 0, pend, r_amt[k]);
+            if (pc < LEG_WIN) s_win[pc] = tb_leg_word(r_cr[k], P.leg_shift, 1, pend, r_amt[k]);
         }
-#pragma unroll
-        for (u32 q = 0; q < 4; q++) {
-            const u32 j = j0 + q * blockDim.x + threadIdx.x;
-            if (j < nlegs) w[j] = v[q];
-        }
+        __syncthreads();
+        const u32 m = min((u32)LEG_WIN, nlegs - w0);
+        for (u32 j = threadIdx.x; j < m; j += blockDim.x) w[w0 + j] = s_win[j];
     }
 }
 
@@ -245,13 +249,14 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     __shared__ u8 s_code[BATCH_LDS];
     __shared__ u8 s_fl[BATCH_LDS];   // bit0 linked, bit1 dependent
     __shared__ u16 s_seg[BATCH_LDS]; // segment (chain) start
-    __shared__ u32 s_key[BATCH_LDS]; // per segment start: min over members (0 = dependent member)
+    __shared__ __attribute__((aligned(8))) u32 s_key[BATCH_LDS]; // per segment start: min over members (0 = dependent member)
     __shared__ u32 s_wave[RESOLVE_THREADS / 64];
     __shared__ u64 s_tsmax[RESOLVE_THREADS / 64];
     __shared__ u32 s_applied;
     __shared__ u32 s_failed;  // non-ok final results of independent events
     __shared__ u32 s_hist[OP == OP_CREATE_TRANSFERS ? LEG_BUCKETS_MAX / 2 + 1 : 1];  // legs per bucket (u16 pairs)
 
+    if (P.resolve_slow && !P.resolve_slow[blockIdx.x]) return;  // tb_resolve_lean resolved this prepare
     const Tables& T = P.T;
     const u32 b = P.b0 + blockIdx.x;
     const u64 boff = P.batch_off[b];
@@ -279,16 +284,22 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     // left between the per-event stores below would serialise them.
     const u64 ts0 = tb_ts_carried(P) ? 0 : P.batch_ts[b] - L + 1;
     // a. classify.  Each thread owns events tid + k*RESOLVE_THREADS; their scratch words are loaded
-    // for every k before any is used (one memory round trip instead of one per k).
+    // for every k before any is used (one memory round trip instead of one per k).  The event
+    // flags the kernel needs are kept as bit masks over k (linked, pending): at 1024 threads a
+    // workgroup, 64 VGPRs a lane is what lets two prepares share a CU (one round of workgroups
+    // for a 512-prepare pass instead of two).
     u32 r_info[RESOLVE_K];
-    u16 r_fl[RESOLVE_K];
+    u32 linkmask = 0, pendmask = 0;
 #pragma unroll
     for (u32 k = 0; k < RESOLVE_K; k++) {
         const u32 i = k * RESOLVE_THREADS + threadIdx.x;
         r_info[k] = i < L ? P.info[pbase + i] : 0u;
-        r_fl[k] = i < L ? P.eflags[pbase + i] : (u16)0;
+        const u16 fl = i < L ? P.eflags[pbase + i] : (u16)0;
+        linkmask |= (fl & 1u) << k;
+        pendmask |= ((fl & TF_PENDING) ? 1u : 0u) << k;
     }
-    bool local_linked = false, local_dep = false;
+    bool local_dep = false;
+    const bool local_linked = linkmask != 0;
     // With every pass-wide condition of tb_classify off (uniform), what is left of it is a test of
     // the event's own bits, computed without branches (a 1024-thread workgroup's divergent branches
     // cost scalar instructions on its CU's one scalar unit).  Lanes past L hold info 0: not
@@ -304,8 +315,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         const bool dep = fast_cls ? ((info & HZ_SELFDEP) != 0) |
                                         (((info & HZ_ACCTS) != 0) & (code == R_OK) & ((info & (HZ_BAL | HZ_LIMIT)) != 0))
                                   : tb_classify<OP>(P, pe, info, code, S, cert_global, any_dup, any_bal, any_pv);
-        const bool linked = r_fl[k] & 1;
-        local_linked |= linked;
+        const bool linked = (linkmask >> k) & 1;
         local_dep |= dep;
         s_code[i] = (u8)code;
         s_fl[i] = (linked ? 1 : 0) | (dep ? 2 : 0);
@@ -349,9 +359,11 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     }
 
     // Final results, dependent list, apply.  The account slots and amounts of every event of the
-    // thread are loaded up front as well.
+    // thread are loaded up front as well (the amount's high word only as "non-zero": a leg needs
+    // an amount below 2^LEG_AMT_BITS).
     u32 r_dr[RESOLVE_K], r_cr[RESOLVE_K];
-    u64 r_amt[RESOLVE_K][2];
+    u64 r_amt[RESOLVE_K];
+    u32 wide = 0;  // bit k: event k's amount has a non-zero high word
 #pragma unroll
     for (u32 k = 0; k < RESOLVE_K; k++) {
         const u32 i = k * RESOLVE_THREADS + threadIdx.x;
@@ -359,30 +371,22 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         const u32 pe = pbase + i;
         r_dr[k] = want ? P.dr[pe] : 0u;
         r_cr[k] = want ? P.cr[pe] : 0u;
-        r_amt[k][0] = want ? P.amt[pe] : 0ULL;
-        r_amt[k][1] = want && (r_info[k] & HZ_AMT_HI) ? P.amt_hi[pe] : 0ULL;
+        r_amt[k] = want ? P.amt[pe] : 0ULL;
+        wide |= (want && (r_info[k] & HZ_AMT_HI) && P.amt_hi[pe] != 0 ? 1u : 0u) << k;
     }
-    u64 tsmax = 0;
     u32 ndep = 0, n_app = 0, n_fail = 0;  // per thread, summed per wave below (one LDS atomic per wave)
     u32 legmask = 0;  // bit k: this thread's event k contributes two legs
+    u32 last_ok = ~0u;  // the thread's last event (largest i) that returned ok when evaluated
     // An independent ok transfer that is not a leg is applied by tb_apply_events after this kernel:
     // no balance changes while any workgroup classifies, so the per-account certificate checks read
     // the pre-pass balances and the classification is a function of the input alone.
     bool late = false;
     u32* dep_out = P.dep_list + pbase;
     // No chain and no dependent event (uniform): every final result is the intrinsic code, already
-    // in s_code; the loop below without its chain and dependent cases, branch-light.
+    // in s_code; the loop below without its chain and dependent cases, branch-light.  Only a late
+    // event's info word is rewritten (tb_apply_events reads HZ_LATE; the code byte is unchanged).
     if (OP == OP_CREATE_TRANSFERS && !any_linked && !any_dep) {
         u32 panic = 0;
-        // Carried timestamps (a routed pass reads each from its event) loaded before the loop's
-        // first store: a load after a store of the same wave waits for it (gfx950 vmcnt), which cost
-        // a routed one-prepare pass one memory round trip per k.
-        u64 r_ts[RESOLVE_K];
-#pragma unroll
-        for (u32 k = 0; k < RESOLVE_K; k++) {
-            const u32 i = k * RESOLVE_THREADS + threadIdx.x;
-            r_ts[k] = tb_ts_carried(P) ? (i < L ? tb_event_ts(P, b, boff, L, i) : 0) : ts0 + i;
-        }
 #pragma unroll
         for (u32 k = 0; k < RESOLVE_K; k++) {
             const u32 i = k * RESOLVE_THREADS + threadIdx.x;
@@ -392,23 +396,19 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
             const u32 code = info & 0xFF;
             const bool ok = valid & (code == R_OK);
             panic |= code == TB_CODE_PANIC;
-            const bool leg = use_legs && !(info & HZ_POSTVOID) && r_amt[k][1] == 0 && r_amt[k][0] <= LEG_AMT_MASK;
-            if (valid) P.info[pe] = info | (ok ? HZ_EVAL_OK : 0) | (ok && !leg ? HZ_LATE : 0);
-            const u64 ts = r_ts[k];
-            tsmax = ok ? ts : tsmax;
+            const bool leg = use_legs && !(info & HZ_POSTVOID) && !((wide >> k) & 1) && r_amt[k] <= LEG_AMT_MASK;
+            if (ok && !leg) P.info[pe] = info | HZ_EVAL_OK | HZ_LATE;
+            last_ok = ok ? i : last_ok;
             n_app += ok;
             n_fail += valid & !ok;
-            if (ok && P.inplace && (info & HZ_POSTVOID)) tb_inplace_record(P, pe, info, ts);
+            if (ok && P.inplace && (info & HZ_POSTVOID)) {
+                tb_inplace_record(P, pe, info, tb_ts_carried(P) ? tb_event_ts(P, b, boff, L, i) : ts0 + i);
+            }
             if (ok) {
                 if (leg) {
-                    const u32 drs = r_dr[k], crs = r_cr[k];
-                    const u64 pend = (r_fl[k] & TF_PENDING) ? 0 : 1;  // field: pending / posted
-                    const u32 mask = (1u << P.leg_shift) - 1;
-                    P.leg_ev[2 * (u64)pe] = ((((u64)(drs & mask) << 2) | pend) << LEG_AMT_BITS) | r_amt[k][0];
-                    P.leg_ev[2 * (u64)pe + 1] = ((((u64)(crs & mask) << 2) | 2 | pend) << LEG_AMT_BITS) | r_amt[k][0];
                     if (!TB_ABL(P, ABL_LEG_WORK)) {
-                        tb_hist16_inc(s_hist, drs >> P.leg_shift);
-                        tb_hist16_inc(s_hist, crs >> P.leg_shift);
+                        tb_hist16_inc(s_hist, r_dr[k] >> P.leg_shift);
+                        tb_hist16_inc(s_hist, r_cr[k] >> P.leg_shift);
                     }
                     legmask |= 1u << k;
                 } else {
@@ -456,31 +456,27 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
             if (!dep) {
                 if (fin == TB_CODE_PANIC) tb_panic(T.g, PANIC_ASSERT);
                 s_code[i] = (u8)fin;
-                const bool leg = OP == OP_CREATE_TRANSFERS && use_legs && !(info & HZ_POSTVOID) && r_amt[k][1] == 0 &&
-                                 r_amt[k][0] <= LEG_AMT_MASK;
+                const bool leg = OP == OP_CREATE_TRANSFERS && use_legs && !(info & HZ_POSTVOID) && !((wide >> k) & 1) &&
+                                 r_amt[k] <= LEG_AMT_MASK;
                 const bool late_ev = OP == OP_CREATE_TRANSFERS && fin == R_OK && !leg;
                 P.info[pe] = (info & 0xFFFFFF00u) | fin | (eval_ok ? HZ_EVAL_OK : 0) | (late_ev ? HZ_LATE : 0);
-                const u64 ts = tb_ts_carried(P) ? tb_event_ts(P, b, boff, L, i) : ts0 + i;
-                if (eval_ok) tsmax = ts;  // increasing in i
+                if (eval_ok) last_ok = i;  // increasing in i
                 if (fin == R_OK) {
                     if (OP == OP_CREATE_TRANSFERS) {
-                        if (P.inplace && (info & HZ_POSTVOID)) tb_inplace_record(P, pe, info, ts);
+                        if (P.inplace && (info & HZ_POSTVOID)) {
+                            tb_inplace_record(P, pe, info, tb_ts_carried(P) ? tb_event_ts(P, b, boff, L, i) : ts0 + i);
+                        }
                         if (leg) {
-                            const u32 drs = r_dr[k], crs = r_cr[k];
-                            const u64 pend = (r_fl[k] & TF_PENDING) ? 0 : 1;  // field: pending / posted
-                            const u32 mask = (1u << P.leg_shift) - 1;
-                            P.leg_ev[2 * (u64)pe] = ((((u64)(drs & mask) << 2) | pend) << LEG_AMT_BITS) | r_amt[k][0];
-                            P.leg_ev[2 * (u64)pe + 1] = ((((u64)(crs & mask) << 2) | 2 | pend) << LEG_AMT_BITS) | r_amt[k][0];
                             if (!TB_ABL(P, ABL_LEG_WORK)) {
-                                tb_hist16_inc(s_hist, drs >> P.leg_shift);
-                                tb_hist16_inc(s_hist, crs >> P.leg_shift);
+                                tb_hist16_inc(s_hist, r_dr[k] >> P.leg_shift);
+                                tb_hist16_inc(s_hist, r_cr[k] >> P.leg_shift);
                             }
                             legmask |= 1u << k;
                         } else {
                             late = true;
                         }
                     } else {
-                        tb_apply_account(P, pe, ts);
+                        tb_apply_account(P, pe, tb_ts_carried(P) ? tb_event_ts(P, b, boff, L, i) : ts0 + i);
                     }
                     n_app++;
                 } else {
@@ -505,8 +501,9 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     }
 
     if (P.legs && __ballot(late) && (threadIdx.x & 63) == 0) P.pass_words[PW_LATE] = 1;
-    // commit_timestamp: max over events that returned ok when evaluated (:763, :882, :1012).
-    u64 m = tsmax;
+    // commit_timestamp: max over events that returned ok when evaluated (:763, :882, :1012) — the
+    // timestamps increase with the event index, so each thread's last such event holds its maximum.
+    u64 m = last_ok == ~0u ? 0 : tb_ts_carried(P) ? tb_event_ts(P, b, boff, L, last_ok) : ts0 + last_ok;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         m = max(m, (u64)__shfl_xor((unsigned long long)m, off));
@@ -534,7 +531,148 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         P.dep_count[blockIdx.x] = ndep;
         if (ndep) atomicAdd((unsigned long long*)&T.g->dependent_total, (unsigned long long)ndep);
     }
-    if (use_legs) tb_emit_legs(P, pbase, L, legmask, r_dr, r_cr, s_hist, (u16*)s_key, s_wave);  // s_key is dead here
+    if (use_legs) tb_emit_legs(P, pbase, legmask, pendmask, r_dr, r_cr, r_amt, s_hist, (u64*)s_key, s_wave);  // s_key is dead here
     if (ndep == 0) tb_write_replies(P, b, L, s_code, s_wave, s_failed);
+    tb_kclock_end(P, 1);
+}
+
+// tb_resolve's common case on a legs pass, in a lean kernel: no pass-wide condition (no
+// duplicate id, post / void or balancing event in the pass, the 64-bit certificate) and, in the
+// prepare, no linked chain and no dependent event.  Every final result is then the intrinsic code,
+// and what is left is the legs' counting sort, the commit timestamp and the sparse reply.  Holding
+// only what that needs (64 VGPRs a lane: the info words, the slots and amounts, the legs' sorted
+// positions) lets two 1024-thread workgroups share a CU, so a 512-prepare pass is one round of
+// workgroups; tb_resolve needs 128 VGPRs (one workgroup a CU: two rounds).  A prepare outside the
+// common case is flagged in P.resolve_slow and tb_resolve, launched after this kernel, resolves it
+// whole (this kernel changed nothing for it); the others tb_resolve skips.
+__global__ __launch_bounds__(RESOLVE_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void tb_resolve_lean(PassArgs P) {
+    __shared__ u8 s_code[BATCH_LDS];
+    __shared__ __attribute__((aligned(8))) u64 s_win[LEG_WIN];
+    __shared__ u32 s_wave[RESOLVE_THREADS / 64];
+    __shared__ u64 s_tsmax[RESOLVE_THREADS / 64];
+    __shared__ u32 s_applied;
+    __shared__ u32 s_failed;
+    __shared__ u32 s_hist[LEG_BUCKETS_MAX / 2 + 1];
+
+    const Tables& T = P.T;
+    const u32 b = P.b0 + blockIdx.x;
+    const u64 boff = P.batch_off[b];
+    const u32 L = (u32)(P.batch_off[b + 1] - boff);
+    const u32 pbase = (u32)(boff - P.e0);
+    tb_kclock_start(P, 1);
+    u128 S = 0;
+    bool cert_global = true, cert64 = true;
+    tb_pass_cert(P, S, cert_global, cert64);
+    const bool lean = P.legs && !P.seq_pv && P.pass_words[PW_DUP] == 0 && P.pass_words[PW_PV] == 0 &&
+                      P.pass_words[PW_BAL] == 0 && cert_global && cert64;
+    if (!lean) {  // uniform: the whole pass goes to tb_resolve
+        if (threadIdx.x == 0) P.resolve_slow[blockIdx.x] = 1;
+        return;
+    }
+    for (u32 k = threadIdx.x; k <= P.leg_buckets / 2; k += RESOLVE_THREADS) s_hist[k] = 0;
+    if (threadIdx.x == 0) {
+        s_applied = 0;
+        s_failed = 0;
+    }
+    const u64 ts0 = tb_ts_carried(P) ? 0 : P.batch_ts[b] - L + 1;
+    u32 r_info[RESOLVE_K];
+    u32 linkmask = 0, pendmask = 0;
+#pragma unroll
+    for (u32 k = 0; k < RESOLVE_K; k++) {
+        const u32 i = k * RESOLVE_THREADS + threadIdx.x;
+        r_info[k] = i < L ? P.info[pbase + i] : 0u;
+        const u16 fl = i < L ? P.eflags[pbase + i] : (u16)0;
+        linkmask |= (fl & 1u) << k;
+        pendmask |= ((fl & TF_PENDING) ? 1u : 0u) << k;
+    }
+    bool local_dep = false;
+#pragma unroll
+    for (u32 k = 0; k < RESOLVE_K; k++) {
+        const u32 info = r_info[k];
+        local_dep |= ((info & HZ_SELFDEP) != 0) |
+                     (((info & HZ_ACCTS) != 0) & ((info & 0xFF) == R_OK) & ((info & (HZ_BAL | HZ_LIMIT)) != 0));
+    }
+    const bool any_linked = __syncthreads_or(linkmask != 0);
+    const bool any_dep = __syncthreads_or(local_dep);
+    if (any_linked || any_dep) {  // uniform
+        if (threadIdx.x == 0) P.resolve_slow[blockIdx.x] = 1;
+        return;
+    }
+    if (threadIdx.x == 0) P.resolve_slow[blockIdx.x] = 0;
+    u32 r_dr[RESOLVE_K], r_cr[RESOLVE_K];
+    u64 r_amt[RESOLVE_K];
+    u32 wide = 0;
+#pragma unroll
+    for (u32 k = 0; k < RESOLVE_K; k++) {
+        const u32 i = k * RESOLVE_THREADS + threadIdx.x;
+        const bool want = i < L && (r_info[k] & HZ_ACCTS);
+        const u32 pe = pbase + i;
+        r_dr[k] = want ? P.dr[pe] : 0u;
+        r_cr[k] = want ? P.cr[pe] : 0u;
+        r_amt[k] = want ? P.amt[pe] : 0ULL;
+        wide |= (want && (r_info[k] & HZ_AMT_HI) && P.amt_hi[pe] != 0 ? 1u : 0u) << k;
+    }
+    u32 n_app = 0, n_fail = 0, legmask = 0, last_ok = ~0u, panic = 0;
+    bool late = false;
+#pragma unroll
+    for (u32 k = 0; k < RESOLVE_K; k++) {
+        const u32 i = k * RESOLVE_THREADS + threadIdx.x;
+        const bool valid = i < L;
+        const u32 pe = pbase + i;
+        const u32 info = r_info[k];
+        const u32 code = info & 0xFF;
+        if (valid) s_code[i] = (u8)code;
+        const bool ok = valid & (code == R_OK);
+        panic |= code == TB_CODE_PANIC;
+        const bool leg = !(info & HZ_POSTVOID) && !((wide >> k) & 1) && r_amt[k] <= LEG_AMT_MASK;
+        if (ok && !leg) P.info[pe] = info | HZ_EVAL_OK | HZ_LATE;
+        last_ok = ok ? i : last_ok;
+        n_app += ok;
+        n_fail += valid & !ok;
+        if (ok && P.inplace && (info & HZ_POSTVOID)) {
+            tb_inplace_record(P, pe, info, tb_ts_carried(P) ? tb_event_ts(P, b, boff, L, i) : ts0 + i);
+        }
+        if (ok) {
+            if (leg) {
+                if (!TB_ABL(P, ABL_LEG_WORK)) {
+                    tb_hist16_inc(s_hist, r_dr[k] >> P.leg_shift);
+                    tb_hist16_inc(s_hist, r_cr[k] >> P.leg_shift);
+                }
+                legmask |= 1u << k;
+            } else {
+                late = true;
+            }
+        } else if (valid && (info & HZ_SPEC)) {
+            tb_xindex_tombstone(T, P.rs[pe]);  // a failed event's speculative record
+        }
+    }
+    if (panic) tb_panic(T.g, PANIC_ASSERT);
+    if (__ballot(late) && (threadIdx.x & 63) == 0) P.pass_words[PW_LATE] = 1;
+    u64 m = last_ok == ~0u ? 0 : tb_ts_carried(P) ? tb_event_ts(P, b, boff, L, last_ok) : ts0 + last_ok;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        m = max(m, (u64)__shfl_xor((unsigned long long)m, off));
+        n_app += __shfl_xor(n_app, off);
+        n_fail += __shfl_xor(n_fail, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_tsmax[threadIdx.x >> 6] = m;
+        if (n_app) atomicAdd(&s_applied, n_app);
+        if (n_fail) atomicAdd(&s_failed, n_fail);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (blockIdx.x == 0) {  // the replay kernel's per-pass counters (k_flow.h), after every load
+            for (u32 k = 0; k < FL_BAR_GROUPS + 2; k++) T.g->flow_bar[FL_BAR_STRIDE * k] = 0;
+            if (P.flow_words) for (u32 k = 0; k < FLOW_WORDS; k++) P.flow_words[k] = 0;
+        }
+        u64 mm = 0;
+        for (u32 k = 0; k < RESOLVE_THREADS / 64; k++) mm = max(mm, s_tsmax[k]);
+        if (mm) atomicMax((unsigned long long*)&T.g->commit_timestamp, (unsigned long long)mm);
+        if (s_applied) atomicAdd((unsigned long long*)&T.g->transfer_count, (unsigned long long)s_applied);
+        P.dep_count[blockIdx.x] = 0;
+    }
+    tb_emit_legs(P, pbase, legmask, pendmask, r_dr, r_cr, r_amt, s_hist, s_win, s_wave);
+    tb_write_replies(P, b, L, s_code, s_wave, s_failed);
     tb_kclock_end(P, 1);
 }

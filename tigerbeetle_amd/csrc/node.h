@@ -1268,6 +1268,11 @@ static int node_split_pass(TbNode* N, NodePass& P, u32 p, const u64* ts, u64 bou
     if ((st = node_read_plan(N, P, p, &PL, false))) return st;
     u64 n_seq = 0, n_pass = 0, room[NODE_WORLD_MAX] = {};
     for (u32 d = 0; d < W; d++) {
+        // A source with an empty block (the call's last pass) sequences nothing; its counts' copy is
+        // not waited for (node_read_plan waits for the sources with events), so its host words may
+        // still hold an earlier pass's counts: reading them reserved too little log room on the
+        // homes and sized the sequencer's pass wrong (8-shard C3 / C4, tests/test_gpu_node.py).
+        if (P.blk[d].k1 == P.blk[d].k0) continue;
         n_seq += N->D[d].h_dcounts[2];
         n_pass += P.blk[d].events;
         for (u32 h = 0; h < W; h++) room[h] += N->D[d].h_dcounts[NODE_DC_HOME + h];

@@ -108,7 +108,8 @@ struct PassArgs {
     u32* leg_tot;          // [leg_buckets + 1] legs per bucket in the pass (tb_emit_legs; zeroed by tb_pass_clear),
                            // then the number of buckets that reached APPLY_SPLIT_MIN
     u32 leg_buckets;       // account_cap >> leg_shift
-    u64* leg_ev;           // [2 * pass events] leg word of event pe's side s at 2*pe+s (event order)
+    u32* resolve_slow;     // [pass prepares] or null: 1 = the prepare is tb_resolve's (tb_resolve_lean did not
+                           // resolve it); null: tb_resolve resolves every prepare
     u64* leg_w;            // [2 * pass events] the same leg words grouped by bucket per prepare
 
     u32* leg_off;          // [prepares of the pass][leg_buckets + 1] bucket starts in the prepare's legs

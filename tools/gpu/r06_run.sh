@@ -54,6 +54,20 @@ for what in "$@"; do
         rc=$?; echo "node chunk $pb rc=$rc"; [ $rc -ne 0 ] && { tail -5 $O/ab_node_$pb.err; exit $rc; }
         python -c "import json;d=json.loads(open('$O/ab_node_$pb.json').read().strip().splitlines()[-1]);print('node',d['value'],d['ms_per_step'],d.get('parity'))"
       done ;;
+    resab)  # resolve variants on device-resident C2 passes, rocprofv3 kernel trace each: base (libtbgpu_base.so),
+            # cur, cur with TBGPU_NO_LEAN=1
+      export TMPDIR=/tmp
+      for v in ${RESAB_VARIANTS:-base cur nolean}; do
+        unset TBGPU_AB_LIB TBGPU_NO_LEAN
+        [ $v = base ] && export TBGPU_AB_LIB=$PWD/tigerbeetle_amd/libtbgpu_base.so
+        [ $v = nolean ] && export TBGPU_NO_LEAN=1
+        rm -rf $O/rk_$v
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rk_$v -o run -- \
+          python3 tools/gpu/device_pass.py 100000000 > $O/rk_$v.log 2>&1
+        rc=$?; echo "resab $v rc=$rc"; [ $rc -ne 0 ] && { tail -5 $O/rk_$v.log; exit $rc; }
+        python3 tools/gpu/kstats.py $(find $O/rk_$v -name '*kernel_stats.csv' | head -1) tb_transfers_validate tb_resolve tb_apply_legs tb_flow tb_pass_clear
+      done
+      unset TBGPU_AB_LIB TBGPU_NO_LEAN ;;
     smoke)
       timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
       rc=$?; tail -3 $O/smoke.log; [ $rc -ne 0 ] && exit $rc ;;
