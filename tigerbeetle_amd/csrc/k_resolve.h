@@ -372,7 +372,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
         r_dr[k] = want ? P.dr[pe] : 0u;
         r_cr[k] = want ? P.cr[pe] : 0u;
         r_amt[k] = want ? P.amt[pe] : 0ULL;
-        wide |= (want && (r_info[k] & HZ_AMT_HI) && P.amt_hi[pe] != 0 ? 1u : 0u) << k;
+        wide |= (want && (r_info[k] & HZ_AMT_HI) ? 1u : 0u) << k;  // HZ_AMT_HI: the high word is non-zero
     }
     u32 ndep = 0, n_app = 0, n_fail = 0;  // per thread, summed per wave below (one LDS atomic per wave)
     u32 legmask = 0;  // bit k: this thread's event k contributes two legs
@@ -575,21 +575,31 @@ __global__ __launch_bounds__(RESOLVE_THREADS) __attribute__((amdgpu_waves_per_eu
         s_failed = 0;
     }
     const u64 ts0 = tb_ts_carried(P) ? 0 : P.batch_ts[b] - L + 1;
+    // The prepare's scratch rows from workgroup-uniform bases: a lane's address is a 32-bit offset
+    // from a scalar base (no 64-bit address per event held in VGPRs across the kernel).
+    u32* __restrict__ info_b = P.info + pbase;
+    const u16* __restrict__ fl_b = P.eflags + pbase;
+    const u32* __restrict__ dr_b = P.dr + pbase;
+    const u32* __restrict__ cr_b = P.cr + pbase;
+    const u64* __restrict__ amt_b = P.amt + pbase;
+    const u32* __restrict__ rs_b = P.rs + pbase;
     u32 r_info[RESOLVE_K];
     u32 linkmask = 0, pendmask = 0;
 #pragma unroll
     for (u32 k = 0; k < RESOLVE_K; k++) {
         const u32 i = k * RESOLVE_THREADS + threadIdx.x;
-        r_info[k] = i < L ? P.info[pbase + i] : 0u;
-        const u16 fl = i < L ? P.eflags[pbase + i] : (u16)0;
+        r_info[k] = i < L ? info_b[i] : 0u;
+        const u16 fl = i < L ? fl_b[i] : (u16)0;
         linkmask |= (fl & 1u) << k;
         pendmask |= ((fl & TF_PENDING) ? 1u : 0u) << k;
     }
+    // Dependent events, and post / voids (an in-place one composes its record here: tb_resolve's), send
+    // the prepare to tb_resolve.
     bool local_dep = false;
 #pragma unroll
     for (u32 k = 0; k < RESOLVE_K; k++) {
         const u32 info = r_info[k];
-        local_dep |= ((info & HZ_SELFDEP) != 0) |
+        local_dep |= ((info & (HZ_SELFDEP | HZ_POSTVOID)) != 0) |
                      (((info & HZ_ACCTS) != 0) & ((info & 0xFF) == R_OK) & ((info & (HZ_BAL | HZ_LIMIT)) != 0));
     }
     const bool any_linked = __syncthreads_or(linkmask != 0);
@@ -606,11 +616,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) __attribute__((amdgpu_waves_per_eu
     for (u32 k = 0; k < RESOLVE_K; k++) {
         const u32 i = k * RESOLVE_THREADS + threadIdx.x;
         const bool want = i < L && (r_info[k] & HZ_ACCTS);
-        const u32 pe = pbase + i;
-        r_dr[k] = want ? P.dr[pe] : 0u;
-        r_cr[k] = want ? P.cr[pe] : 0u;
-        r_amt[k] = want ? P.amt[pe] : 0ULL;
-        wide |= (want && (r_info[k] & HZ_AMT_HI) && P.amt_hi[pe] != 0 ? 1u : 0u) << k;
+        r_dr[k] = want ? dr_b[i] : 0u;
+        r_cr[k] = want ? cr_b[i] : 0u;
+        r_amt[k] = want ? amt_b[i] : 0ULL;
+        wide |= (want && (r_info[k] & HZ_AMT_HI) ? 1u : 0u) << k;  // HZ_AMT_HI: the high word is non-zero
     }
     u32 n_app = 0, n_fail = 0, legmask = 0, last_ok = ~0u, panic = 0;
     bool late = false;
@@ -618,20 +627,16 @@ __global__ __launch_bounds__(RESOLVE_THREADS) __attribute__((amdgpu_waves_per_eu
     for (u32 k = 0; k < RESOLVE_K; k++) {
         const u32 i = k * RESOLVE_THREADS + threadIdx.x;
         const bool valid = i < L;
-        const u32 pe = pbase + i;
         const u32 info = r_info[k];
         const u32 code = info & 0xFF;
         if (valid) s_code[i] = (u8)code;
         const bool ok = valid & (code == R_OK);
         panic |= code == TB_CODE_PANIC;
-        const bool leg = !(info & HZ_POSTVOID) && !((wide >> k) & 1) && r_amt[k] <= LEG_AMT_MASK;
-        if (ok && !leg) P.info[pe] = info | HZ_EVAL_OK | HZ_LATE;
+        const bool leg = !((wide >> k) & 1) && r_amt[k] <= LEG_AMT_MASK;
+        if (ok && !leg) info_b[i] = info | HZ_EVAL_OK | HZ_LATE;
         last_ok = ok ? i : last_ok;
         n_app += ok;
         n_fail += valid & !ok;
-        if (ok && P.inplace && (info & HZ_POSTVOID)) {
-            tb_inplace_record(P, pe, info, tb_ts_carried(P) ? tb_event_ts(P, b, boff, L, i) : ts0 + i);
-        }
         if (ok) {
             if (leg) {
                 if (!TB_ABL(P, ABL_LEG_WORK)) {
@@ -643,7 +648,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) __attribute__((amdgpu_waves_per_eu
                 late = true;
             }
         } else if (valid && (info & HZ_SPEC)) {
-            tb_xindex_tombstone(T, P.rs[pe]);  // a failed event's speculative record
+            tb_xindex_tombstone(T, rs_b[i]);  // a failed event's speculative record
         }
     }
     if (panic) tb_panic(T.g, PANIC_ASSERT);
