@@ -947,8 +947,12 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         P.leg_w = E->leg_w;
         P.leg_off = E->leg_off;
         P.leg_tot = E->leg_tot;
+        // A node home's routed pass (owner legs) holds no chain, post / void, balancing or limit event:
+        // its only dependent events are same-pass duplicate ids, which the one-workgroup replay
+        // orders at a fraction of tb_flow's launch (a grid of whole-CU workgroups that must wait for
+        // every CU it lands on to drain: ~45 us a pass on a node's shared device).
         const bool flow = op == OP_CREATE_TRANSFERS && E->flow_ok && !E->balances_set && !(E->ablate & ABL_FLOW) &&
-                          b1 - b0 <= FLOW_NB_MAX;
+                          b1 - b0 <= FLOW_NB_MAX && !owner;
         P.flow_words = E->flow_ok ? E->F.words : nullptr;
 
         // Launch spans of this pass's kernels on the device clock (profiling only).

@@ -31,18 +31,28 @@ struct NodeGatherArgs {
     u8* recv;                         // [start[world]] events, back to back
 };
 
-// One 16-B chunk per thread: consecutive lanes copy consecutive chunks of a record (coalesced on
-// both sides; the source side crosses xGMI when the source is another GPU).
+// Consecutive lanes copy consecutive 16-B chunks of the records (coalesced on both sides; the source
+// side crosses xGMI when the source is another GPU); each thread has GATHER_PER chunks in flight,
+// their loads issued before any store.
+#define GATHER_PER 4
 __global__ __launch_bounds__(256) void tb_node_gather(NodeGatherArgs A) {
-    const u64 n = A.start[A.world];
-    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
-    if (idx >= n * 8) return;
-    const u64 i = idx >> 3;
-    const u32 c = (u32)(idx & 7);
-    u32 s = 0;
-    while (s + 1 < A.world && A.start[s + 1] <= i) s++;
-    const u32x4* in = (const u32x4*)(A.src[s] + (i - A.start[s]) * 128) + c;
-    ((u32x4*)(A.recv + i * 128))[c] = *in;
+    const u64 n8 = A.start[A.world] * 8;
+    const u64 base = (u64)blockIdx.x * 256 * GATHER_PER + threadIdx.x;
+    u32x4 v[GATHER_PER];
+#pragma unroll
+    for (u32 q = 0; q < GATHER_PER; q++) {
+        const u64 idx = base + q * 256;
+        if (idx >= n8) continue;
+        const u64 i = idx >> 3;
+        u32 s = 0;
+        while (s + 1 < A.world && A.start[s + 1] <= i) s++;
+        v[q] = ((const u32x4*)(A.src[s] + (i - A.start[s]) * 128))[idx & 7];
+    }
+#pragma unroll
+    for (u32 q = 0; q < GATHER_PER; q++) {
+        const u64 idx = base + q * 256;
+        if (idx < n8) ((u32x4*)A.recv)[idx] = v[q];
+    }
 }
 
 struct NodeLegArgs {

@@ -434,7 +434,6 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
         NALLOC(tbMalloc(&D.block_counts, 2 * nblocks * W * 4));
         NALLOC(tbMalloc(&D.results, pe * 8));
         NALLOC(tbMalloc(&D.reply_bytes, (u64)N->pb_src * 4));
-        NALLOC(tbMalloc(&D.recv, N->recv_cap * 128));
         NALLOC(tbMalloc(&D.codes, N->recv_cap));
         NALLOC(tbMalloc(&D.legs, legs_cap_total * NODE_LEG_WORDS * 8));
         NALLOC(tbMalloc(&D.leg_counts, (u64)W * 8));
@@ -943,16 +942,21 @@ static int node_home_one(TbNode* N, u32 h, void* ctx) {
         NodeDev& D = N->D[h];
         tbgpu* E = D.E;
         NCK(hipSetDevice(D.device));
+        // The home's run lands at its transfer-log positions (the log window) and is committed in
+        // place: validate stamps each committed record's timestamp instead of storing the record
+        // (128 B an event less), as the single engine's in-place commit does.
+        u8* window = (u8*)(E->T.xlog + E->log_next);
         if (nh[h]) {
             NodeGatherArgs G{};
             G.world = W;
-            G.recv = D.recv;
+            G.recv = window;
             for (u32 s = 0; s < W; s++) {
                 G.src[s] = N->D[s].send[par] + off[s][h] * 128;
                 G.start[s] = R[h][s];
             }
             G.start[W] = nh[h];
-            hipLaunchKernelGGL(tb_node_gather, dim3((unsigned)((nh[h] * 8 + 255) / 256)), dim3(256), 0, E->stream, G);
+            hipLaunchKernelGGL(tb_node_gather, dim3((unsigned)((nh[h] * 8 + 256 * GATHER_PER - 1) / (256 * GATHER_PER))),
+                               dim3(256), 0, E->stream, G);
             NCK(hipGetLastError());
         }
         NCK(hipEventRecord(D.ev_gathered, E->stream));
@@ -991,8 +995,10 @@ static int node_home_one(TbNode* N, u32 h, void* ctx) {
             imp.leg_counts = D.leg_counts;
             imp.legs_n = W;
             imp.ev_legs = (void*)D.ev_committed;  // the owners need not wait for the import clear
-            const int st = enqueue_call(E, OP_CREATE_TRANSFERS, (u32)nb, h_off, D.recv, E->results, E->reply_bytes,
+            E->inplace_call = true;
+            const int st = enqueue_call(E, OP_CREATE_TRANSFERS, (u32)nb, h_off, window, E->results, E->reply_bytes,
                                         true, D.codes, cert, nullptr, D.hmeta_dev[tri], &O, nb == 1 ? im : nullptr, &imp);
+            E->inplace_call = false;
             if (st) return st;
         } else {
             NCK(hipEventRecord(D.ev_committed, E->stream));
