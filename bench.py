@@ -56,6 +56,11 @@ PCIE_MEASURED_GBS = 57.3
 # larger chunks amortise it (10M C4 transfers: 282M/s at 64, 352M/s at 128, 351M/s at 256, with
 # p99 submit-to-reply 5.4 / 7.0 / 9.8 ms; tools/gpu/chunks.sh).
 CHUNK_PREPARES = {"c2": 64, "c3": 64, "c3h": 64, "c4": 128}
+# The node engine (--gpus N > 1): prepares per source block of a pass.  A node pass has fixed costs a
+# single engine's has not (the route plan's host round trip, per-shard import, owner legs, replies,
+# each a launch per shard): C2 on two logical shards of one GPU ran at 625 M/s in 64-prepare blocks
+# and 1.13 G/s in 512-prepare blocks (round 6, profiles/r06/node/).
+NODE_CHUNK_PREPARES = {"c2": 256, "c3": 64, "c3h": 64, "c4": 128}
 
 
 def parse():
@@ -628,7 +633,8 @@ def launch_check(args, world, rank):
 def main():
     args = parse()
     if args.chunk_prepares is None:
-        args.chunk_prepares = CHUNK_PREPARES[args.workload]
+        node = args.gpus > 1 and args.engine == "node"
+        args.chunk_prepares = (NODE_CHUNK_PREPARES if node else CHUNK_PREPARES)[args.workload]
     launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

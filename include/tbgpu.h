@@ -10,7 +10,7 @@
  *   StateMachine.init(allocator, grid, options)            tbgpu_init
  *     (src/state_machine.zig:264-278)
  *   StateMachine.deinit / reset (:280-299)                 tbgpu_deinit / tbgpu_reset
- *   StateMachine.prefetch (:345-506)                       tbgpu_prefetch (stages the body by DMA)
+ *   StateMachine.prefetch (:345-506)                       tbgpu_prefetch (stages a pageable body)
  *   StateMachine.commit(client, op, timestamp, operation,  tbgpu_commit (one prepare) and
  *     input, output) -> usize (:508-540)                     tbgpu_commit_many (N prepares, one
  *                                                             device pass; same bytes as N commits)
@@ -117,9 +117,11 @@ int tbgpu_commit(tbgpu_t* engine, uint8_t operation, uint64_t timestamp, const v
                  uint32_t input_len, void* output, uint32_t output_cap, uint32_t* out_len);
 
 /* StateMachine.prefetch (src/state_machine.zig:345-506) for the prepare about to be committed.  The
- * objects are HBM-resident; what is staged is the body: a create body in registered host memory
- * (tbgpu_register_host: the message pool) starts crossing PCIe by DMA at once, and the following
- * tbgpu_commit of the same body (same pointer and length) only waits for the copy.  Completes
+ * objects are HBM-resident; what is staged is the body: a pageable create body starts its copy to
+ * HBM at once, and the following tbgpu_commit of the same body (same pointer and length) only waits
+ * for it.  A body in registered host memory (tbgpu_register_host: the message pool) is not staged:
+ * the commit's first kernel reads it through, which measured faster than a DMA the replica's serial
+ * prefetch -> commit leaves nothing to overlap with.  Completes
  * immediately (the reference allows the callback inside the call, src/lsm/groove.zig:723-742).
  * The staged copy belongs to the very next call only, if that call is tbgpu_commit of this body
  * (the replica's prefetch(op) -> commit(op)); any other call drops it.  The body must not change

@@ -211,13 +211,29 @@ def test_prefetch_staging_belongs_to_the_next_commit(gpu_engine_factory):
     buf[:] = bad3.view(np.uint8)
     ts += 100
     expect_bad(_commit_raw(engine, 129, ts, buf))
-    # 4. the staged path itself: prefetch -> commit of the same bytes.
+    # 4. a registered body: prefetch stages nothing (the commit reads it through) -> the same bytes.
     good4 = _transfers(64, 20000, 8)
     buf[:] = good4.view(np.uint8)
     _prefetch(engine, 129, buf)
     ts += 100
     assert _commit_raw(engine, 129, ts, buf) == b""
     engine.unregister_host(buf)
+    # 5. the staged path itself (a pageable body): prefetch -> commit of the same bytes; and a
+    #    re-prefetch after the bytes changed restages them.
+    page = np.zeros(64 * 128, dtype=np.uint8)
+    page[:] = _transfers(64, 30000, 8).view(np.uint8)
+    _prefetch(engine, 129, page)
+    ts += 100
+    assert _commit_raw(engine, 129, ts, page) == b""
+    good6 = _transfers(64, 40000, 8)
+    bad6 = good6.copy()
+    bad6["ledger"][::2] = 0
+    page[:] = good6.view(np.uint8)
+    _prefetch(engine, 129, page)
+    page[:] = bad6.view(np.uint8)
+    _prefetch(engine, 129, page)
+    ts += 100
+    expect_bad(_commit_raw(engine, 129, ts, page))
 
 
 def test_device_panic_stops_the_engine_until_reset(gpu_engine_factory):

@@ -1445,9 +1445,9 @@ extern "C" int tbgpu_commit(tbgpu_t* E, uint8_t operation, uint64_t timestamp, c
 }
 
 // StateMachine.prefetch (src/state_machine.zig:345-506): every object is HBM-resident, so what is
-// left to stage is the prepare body itself — a create body in registered host memory (the message
-// pool) starts crossing PCIe by DMA now, on the copy stream, and the commit of the same body only
-// waits for it.  Anything else needs no staging.
+// left to stage is the prepare body itself — a pageable create body starts its copy to HBM now, on
+// the copy stream, and the commit of the same body only waits for it.  A registered body (the
+// message pool) is not staged: the commit reads it through (below).  Anything else needs nothing.
 extern "C" int tbgpu_prefetch(tbgpu_t* E, uint8_t operation, const void* input, uint32_t input_len) {
     if (E->node) return TBGPU_STATUS_OK;
     HIPCK(hipSetDevice(E->device));
@@ -1460,7 +1460,12 @@ extern "C" int tbgpu_prefetch(tbgpu_t* E, uint8_t operation, const void* input, 
     for (const auto& r : E->host_regions) {
         if ((const u8*)input >= r.ptr && (const u8*)input + input_len <= r.ptr + r.bytes) registered = true;
     }
-    if (!registered) return TBGPU_STATUS_OK;  // pageable: commit copies it (a DMA needs pinned pages)
+    // A registered body is read by the commit's first kernel straight over PCIe (and written through
+    // to HBM): faster than a DMA ahead of it, which the replica's serial prefetch -> commit leaves
+    // nothing to overlap with (round 5: 95 M/s staged against 123 M/s read through,
+    // `replica_path`).  So only a pageable body is staged here: its copy, which the commit would
+    // otherwise make itself, happens at prefetch.
+    if (registered) return TBGPU_STATUS_OK;
     // The staging slot's previous reader (the last commit) has finished: commits are synchronous.
     HIPCK(hipMemcpyAsync(E->pf_staging, input, input_len, hipMemcpyHostToDevice, E->copy_stream));
     HIPCK(hipEventRecord(E->pf_done, E->copy_stream));

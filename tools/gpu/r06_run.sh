@@ -68,6 +68,13 @@ for what in "$@"; do
         python3 tools/gpu/kstats.py $(find $O/rk_$v -name '*kernel_stats.csv' | head -1) tb_transfers_validate tb_resolve tb_apply_legs tb_flow tb_pass_clear
       done
       unset TBGPU_AB_LIB TBGPU_NO_LEAN ;;
+    mbj)  # the sort + join microbenchmark, with a kernel trace (per-phase times)
+      export TMPDIR=/tmp
+      rm -rf $O/mbj_kt
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/mbj_kt -o run -- tools/bin/microbench_join \
+        > $O/mbj.json 2> $O/mbj.err
+      rc=$?; echo "mbj rc=$rc"; cat $O/mbj.json; [ $rc -ne 0 ] && { tail -5 $O/mbj.err; exit $rc; }
+      python3 tools/gpu/kstats.py $(find $O/mbj_kt -name '*kernel_stats.csv' | head -1) cas hist scan scatter bucket_sort dups probe append ;;
     smoke)
       timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
       rc=$?; tail -3 $O/smoke.log; [ $rc -ne 0 ] && exit $rc ;;
