@@ -74,7 +74,7 @@ for what in "$@"; do
       timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/mbj_kt -o run -- tools/bin/microbench_join \
         > $O/mbj.json 2> $O/mbj.err
       rc=$?; echo "mbj rc=$rc"; cat $O/mbj.json; [ $rc -ne 0 ] && { tail -5 $O/mbj.err; exit $rc; }
-      python3 tools/gpu/kstats.py $(find $O/mbj_kt -name '*kernel_stats.csv' | head -1) cas hist scan scatter bucket_sort dups probe append ;;
+      python3 tools/gpu/kstats.py $(find $O/mbj_kt -name "*kernel_stats.csv" | head -1) cas hist bucket_totals scan_totals bucket_runs scatter bucket_sort dups probe append ;;
     smoke)
       timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
       rc=$?; tail -3 $O/smoke.log; [ $rc -ne 0 ] && exit $rc ;;

@@ -5,9 +5,9 @@
 // duplicates) against an index holding R = 100M ids (the end of a 100M-transfer step).
 //   cas        the engine's claim: one random 8-B CAS per id into a 2^28-entry (2-GB) hash index
 //   sort       a hand-written device sort of the pass's (hash, event) pairs: one partition pass by
-//              the top 12 hash bits (LDS histograms of 128 workgroups, one scan, a scatter ranked per
-//              workgroup so each workgroup's run of a bucket is contiguous), then every bucket
-//              (~1K pairs) sorted in LDS (bitonic, 2048 slots)
+//              the top 12 hash bits (LDS histograms of 128 workgroups, a three-kernel scan, a scatter
+//              ranked per workgroup so each workgroup's run of a bucket is contiguous), then every
+//              bucket (~1K pairs) sorted in LDS (bitonic, 2048 slots)
 //   dups       same-pass duplicates: adjacent equal hashes in sorted order
 //   probe_sorted / probe_random
 //              the sorted runs' exists filter: a blocked Bloom filter of the R ids (2^22 64-B
@@ -95,27 +95,47 @@ __global__ void hist(const u64* keys, u64 n, u32* counts) {
     for (u32 k = threadIdx.x; k < NBUCKETS; k += blockDim.x) counts[(u64)k * gridDim.x + blockIdx.x] = s[k];
 }
 
-__global__ void scan(u32* counts, u64 m, u32* bucket_start) {  // one workgroup of 1024
+// The exclusive scan of the [bucket][workgroup] counts in three short kernels: each bucket's total
+// (one thread per bucket), the scan of the 4096 totals (one workgroup), each bucket's run rewritten.
+__global__ void bucket_totals(const u32* counts, u32 nwg, u32* totals) {
+    const u32 k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= NBUCKETS) return;
+    u32 t = 0;
+    for (u32 w = 0; w < nwg; w++) t += counts[(u64)k * nwg + w];
+    totals[k] = t;
+}
+
+__global__ void scan_totals(u32* totals) {  // one workgroup of 1024, 4 buckets per thread
     __shared__ u32 s_part[1024];
-    const u64 per = (m + 1023) / 1024;
-    const u64 a = threadIdx.x * per, b = a + per < m ? a + per : m;
-    u32 sum = 0;
-    for (u64 i = a; i < b; i++) sum += counts[i];
+    u32 v[4], sum = 0;
+    for (u32 q = 0; q < 4; q++) {
+        v[q] = totals[threadIdx.x * 4 + q];
+        sum += v[q];
+    }
     s_part[threadIdx.x] = sum;
     __syncthreads();
     for (u32 off = 1; off < 1024; off <<= 1) {
-        const u32 v = threadIdx.x >= off ? s_part[threadIdx.x - off] : 0;
+        const u32 x = threadIdx.x >= off ? s_part[threadIdx.x - off] : 0;
         __syncthreads();
-        s_part[threadIdx.x] += v;
+        s_part[threadIdx.x] += x;
         __syncthreads();
     }
     u32 run = s_part[threadIdx.x] - sum;
-    for (u64 i = a; i < b; i++) {
-        const u32 c = counts[i];
-        counts[i] = run;
+    for (u32 q = 0; q < 4; q++) {
+        totals[threadIdx.x * 4 + q] = run;
+        run += v[q];
+    }
+}
+
+__global__ void bucket_runs(u32* counts, u32 nwg, const u32* starts) {
+    const u32 k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= NBUCKETS) return;
+    u32 run = starts[k];
+    for (u32 w = 0; w < nwg; w++) {
+        const u32 c = counts[(u64)k * nwg + w];
+        counts[(u64)k * nwg + w] = run;
         run += c;
     }
-    (void)bucket_start;
 }
 
 __global__ void scatter(const u64* keys, const u32* vals, u64 n, const u32* base, u64* okeys, u32* ovals) {
@@ -198,7 +218,7 @@ int main() {
     const u64 table_n = 1ULL << 28, filter_words = (1ULL << FILTER_BLOCK_BITS) * 8;
     const u32 grid = 2048, nwg = 128;
     u64 *keys, *keys2, *table, *filter, *run_keys;
-    u32 *vals, *vals2, *counts, *run_pos, *cas_out;
+    u32 *vals, *vals2, *counts, *totals, *run_pos, *cas_out;
     unsigned char *flag, *hit;
     CK(hipMalloc(&keys, N * 8));
     CK(hipMalloc(&keys2, N * 8));
@@ -210,6 +230,7 @@ int main() {
     CK(hipMalloc(&run_pos, N * 4));
     CK(hipMalloc(&cas_out, N * 4));
     CK(hipMalloc(&counts, (u64)NBUCKETS * nwg * 4));
+    CK(hipMalloc(&totals, NBUCKETS * 4));
     CK(hipMalloc(&flag, N));
     CK(hipMalloc(&hit, N));
     CK(hipMemset(filter, 0, filter_words * 8));
@@ -234,7 +255,9 @@ int main() {
 
         CK(hipEventRecord(e0, 0));
         hipLaunchKernelGGL(hist, dim3(nwg), dim3(256), 0, 0, keys, N, counts);
-        hipLaunchKernelGGL(scan, dim3(1), dim3(1024), 0, 0, counts, (u64)NBUCKETS * nwg, nullptr);
+        hipLaunchKernelGGL(bucket_totals, dim3(NBUCKETS / 256), dim3(256), 0, 0, counts, nwg, totals);
+        hipLaunchKernelGGL(scan_totals, dim3(1), dim3(1024), 0, 0, totals);
+        hipLaunchKernelGGL(bucket_runs, dim3(NBUCKETS / 256), dim3(256), 0, 0, counts, nwg, totals);
         hipLaunchKernelGGL(scatter, dim3(nwg), dim3(256), 0, 0, keys, vals, N, counts, keys2, vals2);
         hipLaunchKernelGGL(bucket_sort, dim3(NBUCKETS), dim3(1024), 0, 0, keys2, vals2, counts, nwg, N);
         CK(hipEventRecord(e1, 0));

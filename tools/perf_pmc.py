@@ -23,8 +23,8 @@ import csv
 import json
 import sys
 
-PASS_KERNELS = ("tb_transfers_validate", "tb_resolve<129>", "tb_apply_legs", "tb_flow", "tb_pass_clear",
-                "tb_reply_out")
+PASS_KERNELS = ("tb_transfers_validate", "tb_resolve_lean", "tb_resolve<129>", "tb_apply_legs", "tb_flow",
+                "tb_pass_clear", "tb_reply_out")
 
 
 def short(name):
