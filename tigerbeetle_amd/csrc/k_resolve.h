@@ -137,6 +137,8 @@ __device__ static inline u64 tb_leg_word(u32 slot, u32 leg_shift, u32 side, bool
     return ((((u64)(slot & mask) << 2) | (side << 1) | (pending ? 0u : 1u)) << LEG_AMT_BITS) | amount;
 }
 
+// r_amt null: each leg's amount is loaded from the prepare's scratch row when its word is stored
+// (tb_resolve_lean: its 64 VGPRs hold no amounts; the row was just read by this workgroup).
 __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 legmask, u32 pendmask, const u32* r_dr,
                                            const u32* r_cr, const u64* r_amt, u32* s_hist, u64* s_win, u32* s_wave) {
     if (TB_ABL(P, ABL_LEG_WORK)) return;
@@ -164,6 +166,7 @@ __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 leg
     }
     if (TB_ABL(P, ABL_LEG_STORES)) return;
     u64* __restrict__ w = P.leg_w + 2ULL * pbase;
+    const u64* __restrict__ amt_b = P.amt + pbase;
     for (u32 w0 = 0; w0 < nlegs; w0 += LEG_WIN) {
         __syncthreads();  // the window is free (the previous one stored; before the first: s_key is dead)
 #pragma unroll
@@ -171,8 +174,10 @@ __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 leg
             if (!((legmask >> k) & 1)) continue;
             const bool pend = (pendmask >> k) & 1;
             const u32 pd = (r_pos[k] & 0xFFFF) - w0, pc = (r_pos[k] >> 16) - w0;
-            if (pd < LEG_WIN) s_win[pd] = tb_leg_word(r_dr[k], P.leg_shift, 0, pend, r_amt[k]);
-            if (pc < LEG_WIN) s_win[pc] = tb_leg_word(r_cr[k], P.leg_shift, 1, pend, r_amt[k]);
+            if (pd >= LEG_WIN && pc >= LEG_WIN) continue;
+            const u64 a = r_amt ? r_amt[k] : amt_b[k * RESOLVE_THREADS + threadIdx.x];
+            if (pd < LEG_WIN) s_win[pd] = tb_leg_word(r_dr[k], P.leg_shift, 0, pend, a);
+            if (pc < LEG_WIN) s_win[pc] = tb_leg_word(r_cr[k], P.leg_shift, 1, pend, a);
         }
         __syncthreads();
         const u32 m = min((u32)LEG_WIN, nlegs - w0);
@@ -609,17 +614,18 @@ __global__ __launch_bounds__(RESOLVE_THREADS) __attribute__((amdgpu_waves_per_eu
         return;
     }
     if (threadIdx.x == 0) P.resolve_slow[blockIdx.x] = 0;
+    // The slots stay in registers until the legs are stored; an amount is needed here only against
+    // LEG_AMT_MASK (tb_emit_legs loads it again from the row when it stores the word).
     u32 r_dr[RESOLVE_K], r_cr[RESOLVE_K];
-    u64 r_amt[RESOLVE_K];
-    u32 wide = 0;
+    u32 wide = 0;  // bit k: event k's amount is not a leg amount (a non-zero high word, or >= 2^LEG_AMT_BITS)
 #pragma unroll
     for (u32 k = 0; k < RESOLVE_K; k++) {
         const u32 i = k * RESOLVE_THREADS + threadIdx.x;
         const bool want = i < L && (r_info[k] & HZ_ACCTS);
         r_dr[k] = want ? dr_b[i] : 0u;
         r_cr[k] = want ? cr_b[i] : 0u;
-        r_amt[k] = want ? amt_b[i] : 0ULL;
-        wide |= (want && (r_info[k] & HZ_AMT_HI) ? 1u : 0u) << k;  // HZ_AMT_HI: the high word is non-zero
+        const u64 a = want ? amt_b[i] : 0ULL;
+        wide |= (want && ((r_info[k] & HZ_AMT_HI) || a > LEG_AMT_MASK) ? 1u : 0u) << k;  // HZ_AMT_HI: high word non-zero
     }
     u32 n_app = 0, n_fail = 0, legmask = 0, last_ok = ~0u, panic = 0;
     bool late = false;
@@ -632,7 +638,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) __attribute__((amdgpu_waves_per_eu
         if (valid) s_code[i] = (u8)code;
         const bool ok = valid & (code == R_OK);
         panic |= code == TB_CODE_PANIC;
-        const bool leg = !((wide >> k) & 1) && r_amt[k] <= LEG_AMT_MASK;
+        const bool leg = !((wide >> k) & 1);
         if (ok && !leg) info_b[i] = info | HZ_EVAL_OK | HZ_LATE;
         last_ok = ok ? i : last_ok;
         n_app += ok;
@@ -677,7 +683,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) __attribute__((amdgpu_waves_per_eu
         if (s_applied) atomicAdd((unsigned long long*)&T.g->transfer_count, (unsigned long long)s_applied);
         P.dep_count[blockIdx.x] = 0;
     }
-    tb_emit_legs(P, pbase, legmask, pendmask, r_dr, r_cr, r_amt, s_hist, s_win, s_wave);
+    tb_emit_legs(P, pbase, legmask, pendmask, r_dr, r_cr, (const u64*)nullptr, s_hist, s_win, s_wave);
     tb_write_replies(P, b, L, s_code, s_wave, s_failed);
     tb_kclock_end(P, 1);
 }

@@ -75,6 +75,12 @@ for what in "$@"; do
         > $O/mbj.json 2> $O/mbj.err
       rc=$?; echo "mbj rc=$rc"; cat $O/mbj.json; [ $rc -ne 0 ] && { tail -5 $O/mbj.err; exit $rc; }
       python3 tools/gpu/kstats.py $(find $O/mbj_kt -name "*kernel_stats.csv" | head -1) cas hist bucket_totals scan_totals bucket_runs scatter bucket_sort dups probe append ;;
+    nodeq)  # C2 on two logical shards with NODEQ hardware queues (bench.py keeps an explicit setting >= 8)
+      GPU_MAX_HW_QUEUES=${NODEQ:-16} timeout -k 10 400 python -u bench.py --gpus 2 --same-device --accounts 2000000 \
+        --transfers 4000000 --steps 3 --warmup 1 --secondary 0 --replica-prepares 0 --host-prepares 0 --write-back 0 \
+        --cpu-sample 0 --host-steps 0 --access-mix 0 --chunk-prepares ${NODEQ_CHUNK:-64} > $O/nodeq_${NODEQ:-16}.json 2> $O/nodeq.err
+      rc=$?; echo "nodeq ${NODEQ:-16} rc=$rc"; [ $rc -ne 0 ] && { tail -5 $O/nodeq.err; exit $rc; }
+      python -c "import json;d=json.loads(open('$O/nodeq_${NODEQ:-16}.json').read().strip().splitlines()[-1]);print('node q${NODEQ:-16}',d['value'],d['ms_per_step'])" ;;
     smoke)
       timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
       rc=$?; tail -3 $O/smoke.log; [ $rc -ne 0 ] && exit $rc ;;
