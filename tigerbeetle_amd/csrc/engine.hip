@@ -954,6 +954,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         const bool flow = op == OP_CREATE_TRANSFERS && E->flow_ok && !E->balances_set && !(E->ablate & ABL_FLOW) &&
                           b1 - b0 <= FLOW_NB_MAX && !owner;
         P.flow_words = E->flow_ok ? E->F.words : nullptr;
+        P.late_in_flow = (flow && (P.apply_late || P.legs)) ? 1u : 0u;  // tb_flow applies the late events itself
 
         // Launch spans of this pass's kernels on the device clock (profiling only).
         P.kclock = nullptr;
@@ -1031,7 +1032,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
                 hipLaunchKernelGGL(tb_apply_legs, dim3(E->leg_buckets + APPLY_EXTRA), dim3(APPLY_THREADS),
                                    tb_apply_lds_bytes(E->leg_shift, b1 - b0), E->stream, P);
             }
-            if (n > 0 && !owner) {  // owner-partitioned: the owners apply the legs instead
+            if (n > 0 && !owner && !P.late_in_flow) {  // owner-partitioned: the owners apply the legs instead
                 const u32 grid = (u32)std::min<u64>((n + 255) / 256, P.legs ? 2048 : 1u << 20);
                 hipLaunchKernelGGL(tb_apply_events, dim3(grid), dim3(256), 0, E->stream, P);
             }

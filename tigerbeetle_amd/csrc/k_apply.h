@@ -248,12 +248,13 @@ __device__ static inline void tb_apply_legs_body(const PassArgs& P, u64* s_acc) 
 // from a single CU), the post / voids and the wide amounts in a legs pass (none at all when the pass
 // word says so: the launch exits at once).  The resolve kernel applies nothing itself, so its
 // classification reads the pre-pass balances.
-__global__ __launch_bounds__(256) void tb_apply_events(PassArgs P) {
+// The body, shared with tb_flow (PassArgs.late_in_flow): every thread of the grid calls it.
+__device__ static inline void tb_apply_late(const PassArgs& P) {
     if (P.legs && !P.pass_words[PW_LATE]) return;
     u128 S;
     bool cert_global, cert64;
     tb_pass_cert(P, S, cert_global, cert64);  // every lane (a wave-wide sum)
-    for (u32 pe = blockIdx.x * 256 + threadIdx.x; pe < P.n; pe += gridDim.x * 256) {
+    for (u32 pe = blockIdx.x * blockDim.x + threadIdx.x; pe < P.n; pe += gridDim.x * blockDim.x) {
         const u32 info = P.info[pe];
         // Exactly the events the resolve kernel marked: independent, ok, and not a balance leg (the
         // legs went to tb_apply_legs) — one decision, made once, so no event is applied twice or never.
@@ -261,3 +262,5 @@ __global__ __launch_bounds__(256) void tb_apply_events(PassArgs P) {
         tb_apply_transfer(P, pe, info, P.eflags[pe], cert64);
     }
 }
+
+__global__ __launch_bounds__(256) void tb_apply_events(PassArgs P) { tb_apply_late(P); }

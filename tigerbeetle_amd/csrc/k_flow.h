@@ -2395,6 +2395,10 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     Globals* g = P.T.g;
     const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid;
     const u32 nb = P.b1 - P.b0;
+    // tb_apply_events' work first, when this launch replaces it (one launch a pass fewer): the
+    // independent ok transfers that are not legs touch no constrained account, id or pending transfer
+    // a dependent unit reads, so their balance adds commute with everything below.
+    if (P.late_in_flow) tb_apply_late(P);
     if (__hip_atomic_load(&g->dependent_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
         if (blockIdx.x == 0) fl_finish(P, s_code, s_wave, s_list, 0, false);
         return;

@@ -104,6 +104,7 @@ struct PassArgs {
     // per account by tb_apply_legs instead of being added with one global atomic per leg.
     u32 legs;              // 1: the legs path is enabled for this pass (the host checked the sizes)
     u32 apply_late;        // 1: no legs; tb_apply_events applies the independent ok transfers (small passes)
+    u32 late_in_flow;      // 1: tb_flow applies them (tb_apply_events' work) before its own; no separate launch
     u32 leg_shift;         // bucket of an account slot = slot >> leg_shift (2^leg_shift slots each)
     u32* leg_tot;          // [leg_buckets + 1] legs per bucket in the pass (tb_emit_legs; zeroed by tb_pass_clear),
                            // then the number of buckets that reached APPLY_SPLIT_MIN
