@@ -129,6 +129,10 @@ struct WbBufs {
     u8* dst[4] = {};
     u64 len[4] = {}, at[4] = {};
     u64 slice = 0;
+    // Commits between an asynchronous write-back's start and its wait: this one's so far, and the
+    // previous one's — the slices of the next copy-out are spread over that many commits (a bar
+    // written back one bar behind: ~64; a replica writing back every 4 ops: 4).
+    u32 calls = 0, calls_prev = 0;
     tbgpu_delta_counts counts{};
     u8* out_t = nullptr;          // the in-flight write-back's caller buffers (sorted by the wait)
     u64* out_p = nullptr;
@@ -1215,6 +1219,7 @@ static int commit_host(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const
             hipLaunchKernelGGL(tb_reply_out, dim3(1), dim3(64), 0, E->stream, E->meta, 1u, E->reply_bytes, E->results, E->g,
                                S.d_reply, (u32*)(S.d_reply + pipe_reply_bytes(E)), seq);
             HIPCK(hipGetLastError());
+            if (E->wb.inflight) E->wb.calls++;
             if ((st = wb_pump(E, 0, E->wb.read_done))) return st;  // one slice of a write-back in flight
             if (!E->profile) {
                 const auto t0 = std::chrono::steady_clock::now();
@@ -1879,6 +1884,7 @@ static int wb_wait(tbgpu* E, tbgpu_delta_counts* counts) {
         if (st) return st;
     }
     W.inflight = false;
+    W.calls_prev = W.calls;
     HIPCK(hipEventSynchronize(W.done));
     *counts = W.counts;
     counts->transfers = W.h_cnt[WB_RECORDS];
@@ -2013,6 +2019,7 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
     }
     memset(&W.counts, 0, sizeof(W.counts));
     W.counts.created_after = E->ckpt_ts;
+    W.calls = 0;
     if ((st = wb_next_epoch(E))) return st;
     HIPCK(hipMemsetAsync(W.d_cnt, 0, WB_COUNT_WORDS * 8, E->stream));
     // In stream order (the next commits follow): each account the bar's log range names, its slot and
@@ -2108,7 +2115,12 @@ static int wb_pump(tbgpu* E, u64 budget, hipEvent_t after) {
             W.at[r] = 0;
             total += W.len[r];
         }
-        W.slice = std::max<u64>(512 << 10, (total / WB_SLICE_CALLS + 65535) & ~65535ULL);
+        // Spread over the commits the previous write-back saw before its wait, less the one that
+        // enqueued the gather and the one that learns its sizes (a chunked write-back every few ops
+        // would otherwise leave most of its bytes to a synchronous copy at the wait).
+        const u32 spread = W.calls_prev ? std::max<u32>(1, std::min<u32>(WB_SLICE_CALLS, W.calls_prev > 2 ? W.calls_prev - 2 : 1))
+                                         : WB_SLICE_CALLS;
+        W.slice = std::max<u64>(512 << 10, (total / spread + 65535) & ~65535ULL);
         W.counts_known = true;
     }
     if (budget != ~0ULL) budget = W.slice;

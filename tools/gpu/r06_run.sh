@@ -61,6 +61,7 @@ for what in "$@"; do
         unset TBGPU_AB_LIB TBGPU_NO_LEAN
         [ $v = base ] && export TBGPU_AB_LIB=$PWD/tigerbeetle_amd/libtbgpu_base.so
         [ $v = nolean ] && export TBGPU_NO_LEAN=1
+        [ $v = spill ] && export TBGPU_AB_LIB=$PWD/tigerbeetle_amd/libtbgpu_spill.so
         rm -rf $O/rk_$v
         timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rk_$v -o run -- \
           python3 tools/gpu/device_pass.py 100000000 > $O/rk_$v.log 2>&1
