@@ -137,8 +137,9 @@ __device__ static inline u64 tb_leg_word(u32 slot, u32 leg_shift, u32 side, bool
     return ((((u64)(slot & mask) << 2) | (side << 1) | (pending ? 0u : 1u)) << LEG_AMT_BITS) | amount;
 }
 
-// r_amt null: each leg's amount is loaded from the prepare's scratch row when its word is stored
-// (tb_resolve_lean: its 64 VGPRs hold no amounts; the row was just read by this workgroup).
+// r_amt null: the legs' amounts are loaded again from the prepare's scratch row once the positions
+// are known (tb_resolve_lean: its 64 VGPRs hold no amounts through the classification; the row was
+// just read by this workgroup).
 __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 legmask, u32 pendmask, const u32* r_dr,
                                            const u32* r_cr, const u64* r_amt, u32* s_hist, u64* s_win, u32* s_wave) {
     if (TB_ABL(P, ABL_LEG_WORK)) return;
@@ -166,7 +167,13 @@ __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 leg
     }
     if (TB_ABL(P, ABL_LEG_STORES)) return;
     u64* __restrict__ w = P.leg_w + 2ULL * pbase;
+    // The amounts, all loaded together (one round trip) once the classification's registers are free.
+    u64 amt[RESOLVE_K];
     const u64* __restrict__ amt_b = P.amt + pbase;
+#pragma unroll
+    for (u32 k = 0; k < RESOLVE_K; k++) {
+        amt[k] = r_amt ? r_amt[k] : ((legmask >> k) & 1) ? amt_b[k * RESOLVE_THREADS + threadIdx.x] : 0ULL;
+    }
     for (u32 w0 = 0; w0 < nlegs; w0 += LEG_WIN) {
         __syncthreads();  // the window is free (the previous one stored; before the first: s_key is dead)
 #pragma unroll
@@ -174,10 +181,8 @@ __device__ static inline void tb_emit_legs(const PassArgs& P, u32 pbase, u32 leg
             if (!((legmask >> k) & 1)) continue;
             const bool pend = (pendmask >> k) & 1;
             const u32 pd = (r_pos[k] & 0xFFFF) - w0, pc = (r_pos[k] >> 16) - w0;
-            if (pd >= LEG_WIN && pc >= LEG_WIN) continue;
-            const u64 a = r_amt ? r_amt[k] : amt_b[k * RESOLVE_THREADS + threadIdx.x];
-            if (pd < LEG_WIN) s_win[pd] = tb_leg_word(r_dr[k], P.leg_shift, 0, pend, a);
-            if (pc < LEG_WIN) s_win[pc] = tb_leg_word(r_cr[k], P.leg_shift, 1, pend, a);
+            if (pd < LEG_WIN) s_win[pd] = tb_leg_word(r_dr[k], P.leg_shift, 0, pend, amt[k]);
+            if (pc < LEG_WIN) s_win[pc] = tb_leg_word(r_cr[k], P.leg_shift, 1, pend, amt[k]);
         }
         __syncthreads();
         const u32 m = min((u32)LEG_WIN, nlegs - w0);
