@@ -557,7 +557,7 @@ def cpu_model():
 # kernel, HBM bytes per committed transfer from FETCH_SIZE / WRITE_SIZE passes and rocprof's mean
 # launch time, for the headline leg (64-prepare chunks from host memory) and for device-resident
 # passes.  It lives outside profiles/ so it travels to the GPU box with the tree.
-PMC_FILE = os.path.join("perf", "pmc_r05.json")
+PMC_FILE = os.path.join("perf", "pmc_r06.json")
 
 
 def load_pmc(leg, kernel, transfers_per_launch):
