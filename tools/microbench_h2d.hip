@@ -4,6 +4,7 @@
 //   pull<W>  a kernel on W workgroups reading mapped host memory (16 B per lane per load, 8 loads in
 //            flight per lane) and storing to HBM
 //   reg      hipMemcpyAsync from malloc'd memory registered with hipHostRegister (the engine's case)
+//   d2h, d2h_8m, duplex_d2h / duplex_h2d: the other direction, sliced, and both at once
 //   busy     `copy` while a kernel holding every CU spins on another stream: a copy engine (SDMA)
 //            keeps its rate, a blit kernel waits for CUs
 // usage: microbench_h2d [MiB]
@@ -12,6 +13,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <utility>
 
 #define CK(x)                                                                      \
     do {                                                                           \
@@ -126,6 +129,52 @@ int main(int argc, char** argv) {
         CK(hipEventSynchronize(b));
         report("busy");
         CK(hipStreamSynchronize(s[1]));
+        // d2h: the write-back's direction (device -> registered host memory), whole and in 8-MiB
+        // slices; duplex: d2h on stream 0 while the same bytes go h2d on stream 1 (the replica's
+        // copy-out beside the next prepares' bodies).
+        for (int warm = 0; warm < 2; warm++) {
+            CK(hipEventRecord(a, s[0]));
+            for (int r2 = 0; r2 < reps; r2++) CK(hipMemcpyAsync(r, d, bytes, hipMemcpyDeviceToHost, s[0]));
+            CK(hipEventRecord(b, s[0]));
+            CK(hipEventSynchronize(b));
+        }
+        report("d2h");
+        const size_t sl = std::min<size_t>(bytes, 8 << 20);
+        CK(hipEventRecord(a, s[0]));
+        for (int r2 = 0; r2 < reps; r2++)
+            for (size_t o = 0; o < bytes; o += sl)
+                CK(hipMemcpyAsync((char*)r + o, (char*)d + o, std::min(sl, bytes - o), hipMemcpyDeviceToHost, s[0]));
+        CK(hipEventRecord(b, s[0]));
+        CK(hipEventSynchronize(b));
+        report("d2h_8m");
+        void* r3 = malloc(bytes);
+        memset(r3, 2, bytes);
+        CK(hipHostRegister(r3, bytes, hipHostRegisterDefault));
+        void* d3 = nullptr;
+        CK(hipMalloc(&d3, bytes));
+        hipEvent_t a1, b1;
+        CK(hipEventCreate(&a1));
+        CK(hipEventCreate(&b1));
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a, s[0]));
+        CK(hipEventRecord(a1, s[1]));
+        for (int r2 = 0; r2 < reps; r2++) {
+            CK(hipMemcpyAsync(r, d, bytes, hipMemcpyDeviceToHost, s[0]));
+            CK(hipMemcpyAsync(d3, r3, bytes, hipMemcpyHostToDevice, s[1]));
+        }
+        CK(hipEventRecord(b, s[0]));
+        CK(hipEventRecord(b1, s[1]));
+        CK(hipEventSynchronize(b));
+        CK(hipEventSynchronize(b1));
+        report("duplex_d2h");
+        std::swap(a, a1);
+        std::swap(b, b1);
+        report("duplex_h2d");
+        std::swap(a, a1);
+        std::swap(b, b1);
+        CK(hipHostUnregister(r3));
+        free(r3);
+        CK(hipFree(d3));
         CK(hipHostUnregister(r));
         free(r);
     }
