@@ -331,6 +331,10 @@ typedef struct tbgpu_stats {
      * use and in all (a wrapper evicts when the log fills; a node: the sums over its shards, log_used
      * the fullest shard's fill times the node's capacity). */
     uint64_t transfers_evicted, log_used, log_capacity;
+    /* Asynchronous write-backs started (tbgpu_checkpoint_delta_async), and of them those whose
+     * copy-out was sent at its bounds from the first commit after it (a write-back every few ops;
+     * the bytes past the counts land in the caller's buffers unread); since tbgpu_init. */
+    uint64_t write_backs_async, write_backs_bound;
 } tbgpu_stats;
 
 int tbgpu_get_stats(tbgpu_t* engine, tbgpu_stats* stats);

@@ -320,3 +320,83 @@ def test_async_write_back_equals_sync(config, devices, gpu_engine_factory):
     oracle = OracleEngine()
     run_oracle(sc, oracle)
     assert e_async.export_accounts().tobytes() == oracle.export_accounts().tobytes()
+
+
+def _chunk_ops(rng, n_acc, per_op, ops, first_id):
+    """`ops` create_transfers bodies of `per_op` events over `n_acc` accounts: an eighth pending,
+    and from the second op on a sixteenth posting or voiding a pending transfer of an earlier op."""
+    bodies, pending, next_id = [], [], first_id
+    for k in range(ops):
+        t = np.zeros(per_op, dtype=TRANSFER_DTYPE)
+        t["id_lo"] = np.arange(next_id, next_id + per_op)
+        next_id += per_op
+        dr = rng.integers(1, n_acc + 1, per_op)
+        cr = 1 + (dr + rng.integers(0, n_acc - 1, per_op)) % n_acc
+        t["debit_account_id_lo"], t["credit_account_id_lo"] = dr, cr
+        t["amount_lo"] = rng.integers(1, 100, per_op)
+        t["ledger"], t["code"] = 1, 1
+        pend = rng.random(per_op) < 1 / 8
+        t["flags"][pend] = int(TransferFlags.pending)
+        if pending:
+            for i in rng.choice(per_op, per_op // 16, replace=False):
+                if not pending or pend[i]:
+                    continue
+                p = pending.pop(int(rng.integers(0, len(pending))))
+                t["flags"][i] = int(TransferFlags.post_pending_transfer if i % 2 else TransferFlags.void_pending_transfer)
+                t["pending_id_lo"][i] = p["id_lo"]
+                for f in ("debit_account_id_lo", "credit_account_id_lo", "amount_lo"):
+                    t[f][i] = p[f]
+        pending.extend(t[pend])
+        bodies.append(t)
+    return bodies
+
+
+@pytest.mark.parametrize("stage", [False, True], ids=["read_through", "staged"])
+def test_chunked_write_back_bound_copy_out(stage, gpu_engine_factory):
+    """A write-back every two one-prepare commits, as a replica writing back every few ops does.
+    Once a write-back's objects fill their bounds, the next copy-outs are sent at their bounds from
+    the first commit after (`write_backs_bound`); with prefetch staging the bodies while a copy-out
+    is in flight (`staged`) no slice waits for a commit's reads.  Every delta equals the synchronous
+    write-back of an engine committing the same prepares, the posted pairs (which cross at the wait)
+    included, and the replies and balances equal the oracle's."""
+    n_acc, per_op, ops = 1 << 16, 512, 24
+    kw = dict(accounts_max=n_acc, transfers_max=1 << 16, pass_events_max=1 << 13, pass_batches_max=8)
+    e_sync, e_async = gpu_engine_factory(**kw), gpu_engine_factory(**kw)
+    oracle = OracleEngine(n_acc, ops * per_op)
+    ts = 10**9
+    for a0 in range(0, n_acc, 8190):
+        body = _accounts(min(8190, n_acc - a0))
+        body["id_lo"] += a0
+        ts += 10**6
+        for e in (e_sync, e_async, oracle):
+            assert e.commit(128, ts, body.tobytes()) == b""
+    caps = (1 << 14, 1 << 14, 1 << 14)
+    e_sync.checkpoint_delta(caps=caps)
+    e_async.checkpoint_delta(caps=caps)
+    buf = np.zeros(per_op * 128, dtype=np.uint8)
+    e_async.register_host(buf)
+    expected, got = [], []
+    for k, t in enumerate(_chunk_ops(np.random.default_rng(5), n_acc, per_op, ops, 1 << 20)):
+        ts += 10**6
+        buf[:] = t.view(np.uint8)
+        if stage:
+            _prefetch(e_async, 129, buf)
+        reply = _commit_raw(e_async, 129, ts, buf)
+        assert reply == e_sync.commit(129, ts, t.tobytes()) == oracle.commit(129, ts, t.tobytes())
+        if k % 2 == 1:
+            expected.append(e_sync.checkpoint_delta(caps=caps))
+            if k > 1:
+                got.append(e_async.checkpoint_delta_wait())
+            e_async.checkpoint_delta_async(caps)
+    got.append(e_async.checkpoint_delta_wait())
+    st = e_async.stats()
+    assert st["write_backs_async"] == ops // 2 and st["write_backs_bound"] == ops // 2 - 1, st
+    assert sum(len(d.posted) for d in expected[1:]) > 0
+    for d_s, d_a in zip(expected, got, strict=True):
+        assert np.array_equal(d_s.transfers, d_a.transfers)
+        assert np.array_equal(d_s.posted, d_a.posted)
+        assert d_s.created_after == d_a.created_after
+        assert sorted(zip(map(bytes, d_s.accounts.view(np.uint8).reshape(-1, 128)), map(bytes, d_s.accounts_before))) == \
+            sorted(zip(map(bytes, d_a.accounts.view(np.uint8).reshape(-1, 128)), map(bytes, d_a.accounts_before)))
+    e_async.unregister_host(buf)
+    assert e_async.export_accounts().tobytes() == oracle.export_accounts().tobytes()

@@ -30,8 +30,14 @@ def test_committed_pmc_file_covers_the_rooflines():
         kernels = d["legs"][leg]["kernels"]
         for k in ("tb_transfers_validate", "tb_resolve<129>", "tb_apply_legs"):
             e = kernels[k]
-            assert e["raw_per_transfer"] > 0 and e["rocprof_calls"] > 0 and e["rocprof_avg_ms"] > 0
+            assert e["rocprof_calls"] > 0 and e["rocprof_avg_ms"] > 0
             assert e["fetch_x2_per_transfer"] >= e["raw_per_transfer"]
+        # the resolve stage's bytes: tb_resolve_lean's on a clean legs pass (round 6: tb_resolve<129>
+        # then only exits early), tb_resolve<129>'s otherwise
+        for k in ("tb_transfers_validate", "tb_apply_legs"):
+            assert kernels[k]["raw_per_transfer"] > 0
+        lean = kernels.get("tb_resolve_lean", {})
+        assert max(lean.get("raw_per_transfer", 0), kernels["tb_resolve<129>"]["raw_per_transfer"]) > 0
     # the gitignore / gpurunignore must let it travel to the GPU box
     ignore = open(os.path.join(ROOT, ".gpurunignore")).read().split()
     assert not any(p.strip("./") in ("perf", "perf/", name) for p in ignore)

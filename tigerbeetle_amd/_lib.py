@@ -97,6 +97,8 @@ class tbgpu_stats(ctypes.Structure):
         ("transfers_evicted", ctypes.c_uint64),
         ("log_used", ctypes.c_uint64),
         ("log_capacity", ctypes.c_uint64),
+        ("write_backs_async", ctypes.c_uint64),
+        ("write_backs_bound", ctypes.c_uint64),
     ]
 
 

@@ -133,6 +133,18 @@ struct WbBufs {
     // previous one's — the slices of the next copy-out are spread over that many commits (a bar
     // written back one bar behind: ~64; a replica writing back every 4 ops: 4).
     u32 calls = 0, calls_prev = 0;
+    // Bound-sized copy-out: the regions are sent at their bounds (every log position, two accounts
+    // per position plus the listed ids), so the first commit after the write-back starts sending
+    // without waiting for the gather's counts; the bytes past the counts are never read by the
+    // caller.  Taken when the previous write-back's objects filled their bounds to within ~1/8
+    // and it saw two commits or more (a replica writing back every few ops), never for a whole
+    // bar (far fewer accounts than two a transfer) nor every op (measured slower: the copy-out then
+    // beside every commit instead of at the wait).
+    bool bound = false, bound_ok = false;
+    bool posted_late = false;     // bound mode: the posted pairs cross at the wait, by their count
+    u64 bound_len[2] = {};        // bound mode: the transfers and accounts the regions were sized for
+    u64 n_async = 0, n_bound = 0;  // tbgpu_stats write_backs_async / _bound
+    bool staged_reads = false;    // the commit this slice follows read a staged body (no PCIe reads)
     tbgpu_delta_counts counts{};
     u8* out_t = nullptr;          // the in-flight write-back's caller buffers (sorted by the wait)
     u64* out_p = nullptr;
@@ -171,6 +183,8 @@ struct tbgpu {
     u32 leg_shift = 0, leg_buckets = 0;
     u32* resolve_slow = nullptr;  // [pb_max] tb_resolve_lean's verdict per prepare of a legs pass
     bool lean_ok = true;          // legs passes run tb_resolve_lean first (TBGPU_NO_LEAN=1: tb_resolve alone)
+    bool wb_bound_ok = true;      // bound-sized copy-outs allowed (TBGPU_WB_BOUND=0: counts always)
+    bool wb_stage = true;         // prefetch stages registered bodies during a copy-out (TBGPU_WB_STAGE=0: never)
     u64* leg_w = nullptr;
     u32* leg_off = nullptr;
     u32* leg_tot = nullptr;  // [leg_buckets] legs per bucket of the current pass
@@ -562,6 +576,8 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
     E->pe_max = config->pass_events_max;
     E->pb_max = config->pass_batches_max;
     if (const char* v = getenv("TBGPU_NO_LEAN")) E->lean_ok = atoi(v) == 0;
+    if (const char* v = getenv("TBGPU_WB_BOUND")) E->wb_bound_ok = atoi(v) != 0;
+    if (const char* v = getenv("TBGPU_WB_STAGE")) E->wb_stage = atoi(v) != 0;
     E->dedup_cap = pow2_at_least(std::max<u64>(4ULL * E->pe_max, 64));
     E->undo_cap = 4 * (BATCH_EVENTS_MAX + 1);
     E->meta_cap = std::max<u64>(E->pb_max, 1 << 16);
@@ -1220,7 +1236,10 @@ static int commit_host(tbgpu* E, u8 op, u32 n, const uint64_t* timestamps, const
                                S.d_reply, (u32*)(S.d_reply + pipe_reply_bytes(E)), seq);
             HIPCK(hipGetLastError());
             if (E->wb.inflight) E->wb.calls++;
-            if ((st = wb_pump(E, 0, E->wb.read_done))) return st;  // one slice of a write-back in flight
+            E->wb.staged_reads = events == E->pf_staging;
+            st = wb_pump(E, 0, E->wb.read_done);  // one slice of a write-back in flight
+            E->wb.staged_reads = false;
+            if (st) return st;
             if (!E->profile) {
                 const auto t0 = std::chrono::steady_clock::now();
                 for (u32 spin = 0; *done != seq; spin++) {
@@ -1471,7 +1490,11 @@ extern "C" int tbgpu_prefetch(tbgpu_t* E, uint8_t operation, const void* input, 
     // nothing to overlap with (round 5: 95 M/s staged against 123 M/s read through,
     // `replica_path`).  So only a pageable body is staged here: its copy, which the commit would
     // otherwise make itself, happens at prefetch.
-    if (registered) return TBGPU_STATUS_OK;
+    // Except while a write-back's copy-out is in flight: then the body crosses by DMA (the link carries
+    // both directions at ~50 GB/s each, tools/microbench_h2d `duplex`), the commit reads HBM, and the
+    // copy-out needs not wait for the commit's PCIe reads (wb_pump).
+    // (Not for a write-back every op: the body's DMA then only lengthens each serial prepare.)
+    if (registered && !(E->wb_stage && E->wb.copying && E->wb.calls_prev >= 2)) return TBGPU_STATUS_OK;
     // The staging slot's previous reader (the last commit) has finished: commits are synchronous.
     HIPCK(hipMemcpyAsync(E->pf_staging, input, input_len, hipMemcpyHostToDevice, E->copy_stream));
     HIPCK(hipEventRecord(E->pf_done, E->copy_stream));
@@ -1884,12 +1907,22 @@ static int wb_wait(tbgpu* E, tbgpu_delta_counts* counts) {
         if (st) return st;
     }
     W.inflight = false;
-    W.calls_prev = W.calls;
+    if (W.calls) W.calls_prev = W.calls;  // (one waited for at once, a bar's last op, says nothing)
     HIPCK(hipEventSynchronize(W.done));
     *counts = W.counts;
     counts->transfers = W.h_cnt[WB_RECORDS];
     counts->posted = W.h_cnt[WB_PV];
     counts->accounts = W.h_cnt[WB_ACCOUNTS];
+    if (W.posted_late && counts->posted) {
+        HIPCK(hipMemcpyAsync(W.dst[3], W.src[3], counts->posted * 16, hipMemcpyDeviceToHost, W.stream));
+        HIPCK(hipStreamSynchronize(W.stream));
+    }
+    W.posted_late = false;
+    if (W.dst[1]) {  // an asynchronous copy-out ran: did its objects fill their bounds (within 1/8)?
+        const u64 actual = counts->transfers * 128 + counts->accounts * (128 + sizeof(AccountBal));
+        const u64 bound = W.bound_len[0] * 128 + W.bound_len[1] * (128 + sizeof(AccountBal));
+        W.bound_ok = actual * 8 >= bound * 7;
+    }
     if (W.h_cnt[WB_STATUS]) {
         E->poisoned = true;
         return fail(TBGPU_STATUS_PANIC, "checkpoint delta: a posted pending transfer is missing");
@@ -1899,6 +1932,8 @@ static int wb_wait(tbgpu* E, tbgpu_delta_counts* counts) {
     if (W.out_p && (W.h_cnt[WB_ORDER] & 2)) delta_sort_pairs(W.out_p, counts->posted);
     return TBGPU_STATUS_OK;
 }
+
+static void wb_set_slice(tbgpu* E, u64 total);  // the copy-out's slice (below)
 
 static int wb_checkpoint_sync(tbgpu* E, u8* accounts_out, u8* before_out, u64 accounts_cap, u8* transfers_out,
                               u64 transfers_cap, u64* posted_out, u64 posted_cap, tbgpu_delta_counts* counts) {
@@ -2057,6 +2092,22 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
     W.dst[3] = (u8*)posted_out;
     W.copying = true;
     W.counts_known = false;
+    W.bound_len[0] = bd.transfers;
+    W.bound_len[1] = bd.accounts;
+    W.bound = E->wb_bound_ok && W.bound_ok && W.calls_prev >= 2;
+    W.posted_late = false;
+    W.n_async++;
+    if (W.bound) {
+        W.n_bound++;  // the sizes are known now: wb_pump sends from the first commit on
+        W.len[0] = bd.transfers * 128;
+        W.len[1] = bd.accounts * 128;
+        W.len[2] = W.src[2] ? bd.accounts * sizeof(AccountBal) : 0;
+        W.len[3] = 0;  // posted pairs (usually none) cross at the wait, by their count
+        W.posted_late = true;
+        for (u32 r = 0; r < 4; r++) W.at[r] = 0;
+        wb_set_slice(E, W.len[0] + W.len[1] + W.len[2]);
+        W.counts_known = true;
+    }
     W.inflight = true;
     return TBGPU_STATUS_OK;
 }
@@ -2070,6 +2121,16 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
 // resolve, apply, flow and reply and the host's turn), sized to spread the bar's objects over about
 // WB_SLICE_CALLS commits.  The sizes come from the gather's counts, known once it completed.
 #define WB_SLICE_CALLS 56
+// The slice: the copy-out spread over the commits the previous write-back saw before its wait, less
+// the one that enqueues the gather and (counts mode) the one that learns its sizes — a chunked
+// write-back every few ops would otherwise leave most of its bytes to a synchronous copy at the wait.
+static void wb_set_slice(tbgpu* E, u64 total) {
+    WbBufs& W = E->wb;
+    const u32 skip = W.bound ? 1 : 2;
+    const u32 spread = W.calls_prev ? std::max<u32>(1, std::min<u32>(WB_SLICE_CALLS, W.calls_prev > skip ? W.calls_prev - skip : 1))
+                                     : WB_SLICE_CALLS;
+    W.slice = std::max<u64>(512 << 10, (total / spread + 65535) & ~65535ULL);
+}
 // The asynchronous write-back's work beside the commits, after the in-order capture (and `after`):
 // the records of the log range (immutable now), the emission, the snapshot's advance, the order
 // check, the counts back to the host.
@@ -2100,7 +2161,7 @@ static int wb_pump(tbgpu* E, u64 budget, hipEvent_t after) {
     if (!W.copying) return TBGPU_STATUS_OK;
     if (W.tail) {
         const int st = wb_tail(E, after);
-        if (st || budget != ~0ULL) return st;  // its counts come back by the next commit
+        if (st || (budget != ~0ULL && !W.counts_known)) return st;  // its counts come back by the next commit
     }
     if (!W.counts_known) {
         if (budget != ~0ULL && hipEventQuery(W.gathered) != hipSuccess) return TBGPU_STATUS_OK;  // next call
@@ -2115,16 +2176,13 @@ static int wb_pump(tbgpu* E, u64 budget, hipEvent_t after) {
             W.at[r] = 0;
             total += W.len[r];
         }
-        // Spread over the commits the previous write-back saw before its wait, less the one that
-        // enqueued the gather and the one that learns its sizes (a chunked write-back every few ops
-        // would otherwise leave most of its bytes to a synchronous copy at the wait).
-        const u32 spread = W.calls_prev ? std::max<u32>(1, std::min<u32>(WB_SLICE_CALLS, W.calls_prev > 2 ? W.calls_prev - 2 : 1))
-                                         : WB_SLICE_CALLS;
-        W.slice = std::max<u64>(512 << 10, (total / spread + 65535) & ~65535ULL);
+        wb_set_slice(E, total);
         W.counts_known = true;
     }
-    if (budget != ~0ULL) budget = W.slice;
-    if (after) HIPCK(hipStreamWaitEvent(W.stream, after, 0));
+    // A commit that read no host memory (its body staged in HBM) leaves the link's upstream side to
+    // the copy-out: everything goes now.  Otherwise one slice, after the commit's reads.
+    if (budget != ~0ULL) budget = W.staged_reads ? ~0ULL : W.slice;
+    if (after && !W.staged_reads) HIPCK(hipStreamWaitEvent(W.stream, after, 0));
     for (u32 r = 0; r < 4 && budget; r++) {
         const u64 n = std::min<u64>(budget, W.len[r] - W.at[r]);
         if (!n) continue;
@@ -2165,6 +2223,8 @@ extern "C" int tbgpu_get_stats(tbgpu_t* E, tbgpu_stats* s) {
     s->transfers_evicted = E->evicted_total;
     s->log_used = E->log_next;
     s->log_capacity = E->xlog_cap;
+    s->write_backs_async = E->wb.n_async;
+    s->write_backs_bound = E->wb.n_bound;
     s->events = E->events;
     s->dependent_events = g.dependent_all;
     s->accounts = g.account_count;

@@ -158,10 +158,22 @@ bool StateMachine::checkpoint_bar(uint64_t op, uint32_t journal_slots, uint32_t 
     return r == 0 || (trigger_too && r == bar);
 }
 
+// In chunks of compact_every ops; the bar's last compact_every ops in chunks halving down to its
+// last op alone (e.g. of 4: 2, 1, 1).  The bar's last chunk is waited for at once (its objects
+// land before compact returns) and each chunk's copy-out overlaps the next chunk's commits, so a
+// chunk shorter than the one before it waits for the difference: halving keeps both waits to about
+// one op's objects.
+bool StateMachine::chunk_end(uint64_t op) const {
+    const uint64_t bar = lsm_batch_multiple, r = op % bar, rem = bar - 1 - r;
+    const uint64_t every = std::max<uint32_t>(1, compact_every);
+    if (rem < every) return rem == 0 || (rem & (rem - 1)) == 0;
+    return (r + 1) % every == 0;
+}
+
 void StateMachine::compact(const Callback& callback, uint64_t op) {
     // The HBM tables need no compaction; the durable copy gets each bar's changes, one bar behind.
     const bool bar_end = lsm_batch_multiple && (op + 1) % lsm_batch_multiple == 0;
-    if (write_back && lsm_batch_multiple && compact_per_op && !bar_end && (op + 1) % std::max<uint32_t>(1, compact_every)) {
+    if (write_back && lsm_batch_multiple && compact_per_op && !chunk_end(op)) {
         // inside a chunk: nothing to do
     } else if (write_back && lsm_batch_multiple && compact_per_op) {
         wb_deliver_inflight();  // the previous chunk's objects: landed while this one committed

@@ -197,8 +197,9 @@ public:
     // The shape zig/state_machine_gpu.zig runs.
     bool compact_per_op = false;
     // With compact_per_op: capture every this many ops (a chunk of the bar) instead of every op; the
-    // bar's last op still waits for its own chunk.
+    // bar's last ops in chunks halving down to its last op alone, which waits for its own.
     uint32_t compact_every = 1;
+    bool chunk_end(uint64_t op) const;
     // One bar behind, except the bar ending at a checkpoint op (a journal of this many slots:
     // vsr.Checkpoint.checkpoint_after, src/vsr.zig:2009-2021), written back synchronously (the
     // in-flight bar first): the shape zig/state_machine_gpu.zig runs with engine_write_back_behind.

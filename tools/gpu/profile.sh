@@ -13,6 +13,7 @@
 #   bash tools/gpu/profile.sh mc                  -> memory-copy + kernel trace of one headline step
 #     (the copy engine's timeline: body copies, their gaps, the per-chunk metadata copies)
 #   bash tools/gpu/profile.sh nkt|nc3             -> kernel trace of the node rehearsal (2 logical shards, C2 / C3)
+#   bash tools/gpu/profile.sh nkt1                -> the same C2 trace on one hardware queue (kernels serialised)
 #   bash tools/gpu/profile.sh n1kt                -> kernel + copy trace of one-prepare node calls
 #   bash tools/gpu/profile.sh c3|c3h|c4           -> kernel trace of `bench.py --workload c3|c3h|c4`
 #     (1M accounts, 10M transfers, one timed step from host memory: tb_flow's bounds / sweep / run)
@@ -43,6 +44,10 @@ case $MODE in
       timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/nkt" -o run -- python3 "$R/bench.py" \
         --gpus 2 --same-device --accounts 2000000 --transfers 8000000 --steps 1 --warmup 1 $LEG --access-mix 0 \
         > "$OUT/bench_nkt.log" 2>&1; rc=$? ;;
+  nkt1) export GPU_MAX_HW_QUEUES=1  # every stream on one hardware queue: each kernel's duration its own
+      timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/nkt1" -o run -- python3 "$R/bench.py" \
+        --gpus 2 --same-device --accounts 2000000 --transfers 8000000 --steps 1 --warmup 1 $LEG --access-mix 0 \
+        --chunk-prepares ${NKT_CHUNK:-512} > "$OUT/bench_nkt1.log" 2>&1; rc=$? ;;
   nc3) export GPU_MAX_HW_QUEUES=8
       timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/nc3" -o run -- python3 "$R/bench.py" \
         --gpus 2 --same-device --workload c3 --accounts 1000000 --transfers 4000000 --steps 1 --warmup 1 $LEG --access-mix 0 \

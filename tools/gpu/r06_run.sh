@@ -89,6 +89,22 @@ for what in "$@"; do
       timeout -k 10 600 python -u bench.py --steps 2 --warmup 1 --secondary 0 --replica-prepares 0 --host-prepares 0 \
         --write-back 0 --cpu-sample 2000000 > $O/bench.json 2> $O/bench.err
       rc=$?; echo "bench rc=$rc"; tail -c 1500 $O/bench.json; tail -5 $O/bench.err; [ $rc -ne 0 ] && exit $rc ;;
+    wbab)  # write-back copy-out A/B on one box: counts-sized vs bound-sized, read through vs staged bodies
+      for v in ${WBAB_VARIANTS:-base bound stage both}; do
+        case $v in
+          base) env_="TBGPU_WB_BOUND=0 TBGPU_WB_STAGE=0"; st="" ;;
+          bound) env_="TBGPU_WB_BOUND=1 TBGPU_WB_STAGE=0"; st="" ;;
+          stage) env_="TBGPU_WB_BOUND=0 TBGPU_WB_STAGE=1"; st="--stage" ;;
+          both) env_="TBGPU_WB_BOUND=1 TBGPU_WB_STAGE=1"; st="--stage" ;;
+        esac
+        for m in ${WBAB_SHAPES:-"--write-back-every 4" "--write-back-every 8" --write-back --write-back-per-op}; do
+          f="$O/wbab_${v}_$(echo $m | tr -d ' -')"
+          env $env_ timeout -k 10 300 tigerbeetle_amd/host/tb_replica_bench --accounts 1000000 --prepares 2000 --device 0 \
+            $m $st > "$f.json" 2> "$f.err"
+          rc=$?; [ $rc -ne 0 ] && { echo "wbab $v $m rc=$rc"; tail -3 "$f.err"; exit $rc; }
+          python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print('wbab',sys.argv[2],sys.argv[3],round(d['transfers_per_s']/1e6,1),'M/s p99',d['p99_ms'],'compact',d['compact_ms_per_op'])" "$f.json" "$v" "$m"
+        done
+      done ;;
     replica)  # the replica call path (C++ mirror) with each write-back shape
       for m in --write-back --write-back-sync "--write-back --checkpoint-journal-slots 1024" --write-back-per-op "--write-back-every 4" "--write-back-every 8"; do
         timeout -k 10 300 tigerbeetle_amd/host/tb_replica_bench --accounts 1000000 --prepares 2000 --device 0 $m \
