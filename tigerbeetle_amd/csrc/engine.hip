@@ -996,10 +996,12 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         const u32 clear_grid = (u32)std::min<u64>(1024, std::max<u64>(1, clear_n / 2048));
         // inline_meta: a one-prepare call's metadata, written into E->meta by this first kernel.
         u64* meta_dst = inline_meta && b0 == 0 ? (u64*)d_off : nullptr;
+        ImportGate gate{};
+        if (imp && n > 0) gate = ImportGate{imp->count, imp->room, 2 * n, imp->flag};
         hipLaunchKernelGGL(tb_pass_clear, dim3(clear_grid), dim3(256), 0, E->stream, E->dedup, E->dedup_cap, E->sum_shards,
                            E->g, E->epoch, E->dedup_force ? 1u : 0u, E->leg_tot, E->leg_buckets, meta_dst,
                            inline_meta ? inline_meta[0] : 0, inline_meta ? inline_meta[1] : 0, inline_meta ? inline_meta[2] : 0,
-                           P.kclock, imp ? imp->count : nullptr, imp && b0 == 0 ? imp->leg_counts : nullptr,
+                           P.kclock, gate, imp && b0 == 0 ? imp->leg_counts : nullptr,
                            imp && b0 == 0 ? imp->legs_n : 0u);
         HIPCK(hipGetLastError());
         E->dedup_force = false;
@@ -1008,9 +1010,13 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
 
         if (imp && n > 0) {  // a node home: the foreign accounts this sub-pass names, from their owners
             const u32 ig = (u32)std::min<u64>(4096, (n + 255) / 256);
-            if (2 * n > imp->cap) return fail(TBGPU_STATUS_INVALID, "node import list: %llu events", (unsigned long long)n);
+            if (2 * n > imp->room) return fail(TBGPU_STATUS_INVALID, "node import room: %llu events", (unsigned long long)n);
+            // The imports of earlier passes stay, unless this sub-pass could overfill the room (the
+            // gate in tb_pass_clear above).
+            hipLaunchKernelGGL(tb_node_import_flush, dim3((u32)std::min<u64>(1024, (E->account_cap + 255) / 256)), dim3(256), 0,
+                               E->stream, E->T, E->account_cap, imp->N.world, imp->self, (const u32*)imp->flag);
             hipLaunchKernelGGL(tb_node_import, dim3(ig), dim3(256), 0, E->stream, E->T, imp->N, events_dev + P.e0 * 128, n,
-                               imp->self, imp->list, imp->os_of);
+                               imp->self, imp->count, imp->os_of);
             HIPCK(hipGetLastError());
         }
         if (n > 0) {
@@ -1084,11 +1090,6 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
             HIPCK(hipGetLastError());
         }
         if (imp && imp->ev_legs) HIPCK(hipEventRecord((hipEvent_t)imp->ev_legs, E->stream));
-        if (imp && n > 0) {  // the owned-only table again
-            hipLaunchKernelGGL(tb_node_import_clear, dim3((u32)std::min<u64>(1024, (2 * n + 255) / 256)), dim3(256), 0,
-                               E->stream, E->T, imp->list, 2 * n);
-            HIPCK(hipGetLastError());
-        }
         if ((st = prof_end(E, &pass_pp))) return st;
         E->passes++;
         E->events += n;

@@ -13,8 +13,10 @@
 //      sources in order, each source's run in event order); tb_node_import copies the hot record of
 //      every foreign account the run names from its owner's table into the home's (the reference's
 //      prefetch of the pass's accounts, src/state_machine.zig:345-506), then the routed commit with
-//      owner legs (tb_owner_legs: every committed transfer's two balance legs, grouped by owner),
-//      then tb_node_import_clear empties the imported entries again;
+//      owner legs (tb_owner_legs: every committed transfer's two balance legs, grouped by owner).
+//      The imported entries stay for the next passes (account hot records never change after
+//      create_account) until the import room fills or an account is inserted on the shard
+//      (tb_pass_clear's import gate, tb_node_import_flush);
 //   3. every owner: tb_node_apply_legs pulls its region of every home's legs and adds them;
 //   4. every source: tb_node_replies reads each event's result code from its home's code array and
 //      compacts the sparse replies of its prepares (tb_route_replies' layout).
@@ -214,9 +216,12 @@ struct NodeTablesArgs {
 // foreign account the sub-pass's events name, from its owner's table, into this shard's table — what
 // validate and the ordered fallback read of an account in a routed pass (its balances are the owner's
 // and never read here: the router's certificate rules out every balance check, and limit and
-// balancing events are sequenced).  Entries go into slots empty in the owned-only table, so they
-// never sit on an owned account's probe chain, and tb_node_import_clear restores the owned-only table
-// exactly.
+// balancing events are sequenced).  Entries go into empty slots and stay: the next passes find them
+// with one probe instead of importing again (a hot record never changes after create_account; an id
+// no owner holds gets a tombstone entry, which also stays — only a create could change that, and
+// every insert of an account flushes the imports first).  So an import never sits on an owned
+// account's probe chain (owned accounts are only inserted while no import exists), and
+// tb_node_import_flush restores the owned-only table exactly.
 // One entry per id however many lanes name it (a Zipf-hot account is named by a large share of a
 // pass): first the workgroup keeps one lane per distinct id (tb_wg_dedup: LDS, exact), then that lane
 // claims an empty slot by a CAS of its timestamp word to a marker {bit 63, the id's 63-bit
@@ -224,11 +229,8 @@ struct NodeTablesArgs {
 // already there stops — the winner alone reads the owner's record, writes the entry and puts the real
 // timestamp last.  (Two ids with one 63-bit fingerprint meeting on one probe chain in one pass would
 // import one of them only: about 2^-63 per pair, the sequencer's own fingerprint bet.)
-// The slot it claimed (TB_NOT_FOUND: none — another lane imports the id, or it is here already) goes
-// to *list_at: one entry per event side, no shared counter (a counter every importing wave added to
-// serialised at its L2 channel: 16K atomics on one word, ~0.3 ms of a 2-shard C2 pass).
-__device__ static inline void tb_import_one(const Tables& H, const NodeTablesArgs& N, u64 lo, u64 hi, u32 o, u32* list_at,
-                                            u32* os_of) {
+// Returns whether it claimed a slot (false: another lane imports the id, or it is here already).
+__device__ static inline bool tb_import_one(const Tables& H, const NodeTablesArgs& N, u64 lo, u64 hi, u32 o, u32* os_of) {
     const u64 mark = (1ULL << 63) | (tb_fingerprint(lo, hi) >> 1);
     u64 pos = tb_hash_id(lo, hi) & H.account_mask;
     u32 slot = TB_NOT_FOUND;
@@ -257,15 +259,14 @@ __device__ static inline void tb_import_one(const Tables& H, const NodeTablesArg
         }
         pos = (pos + 1) & H.account_mask;
     }
-    *list_at = slot;
-    if (slot == TB_NOT_FOUND) return;
+    if (slot == TB_NOT_FOUND) return false;
     AccountHot a;
     const u32 os = tb_account_find_from(O, lo, hi, opos, o0, &a);
     AccountHot* h = &H.acct_hot[slot];
     if (os == TB_NOT_FOUND) {  // no such account: a tombstone id (probes continue past it) under the marker
         h->id_lo = ~0ULL;
         h->id_hi = ~0ULL;
-        return;
+        return true;
     }
     os_of[slot] = os;  // the owner's slot, for this pass's owner legs
     h->ledger = a.ledger;
@@ -278,12 +279,17 @@ __device__ static inline void tb_import_one(const Tables& H, const NodeTablesArg
     // pass's next kernel sees everything.  (An agent-scope fence on gfx950 writes back and
     // invalidates the XCD's whole L2, per wave: it cost this kernel 1 ms a pass.)
     __hip_atomic_store(&h->timestamp, a.timestamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
 }
 
-// list: [2n] the slot each event side imported into (TB_NOT_FOUND: none), for tb_node_import_clear.
+// count: the shard's live imports (tb_pass_clear's import gate), one add per workgroup that claimed any —
+// none once the pass's accounts are all here (a counter every importing wave added to serialised at
+// its L2 channel: 16K atomics on one word, ~0.3 ms of a 2-shard C2 pass).
 __global__ __launch_bounds__(256) void tb_node_import(Tables H, NodeTablesArgs N, const u8* events, u64 n, u32 self,
-                                                      u32* list, u32* os_of) {
+                                                      u64* count, u32* os_of) {
     __shared__ WgDedup s_d;
+    __shared__ u32 s_claimed;
+    if (threadIdx.x == 0) s_claimed = 0;
     for (u64 base = (u64)blockIdx.x * 256; base < n; base += (u64)gridDim.x * 256) {  // uniform per workgroup
         tb_wg_dedup_reset(s_d);
         const u64 e = base + threadIdx.x;
@@ -302,37 +308,48 @@ __global__ __launch_bounds__(256) void tb_node_import(Tables H, NodeTablesArgs N
             st[s] = tb_wg_dedup_claim(s_d, want, lo[s], hi[s]);
         }
         __syncthreads();
+        u32 claimed = 0;
 #pragma unroll
         for (u32 s = 0; s < 2; s++) {
-            if (tb_wg_dedup_go(s_d, st[s], lo[s], hi[s])) tb_import_one(H, N, lo[s], hi[s], o[s], list + 2 * e + s, os_of);
-            else if (e < n) list[2 * e + s] = TB_NOT_FOUND;
+            if (tb_wg_dedup_go(s_d, st[s], lo[s], hi[s]) && tb_import_one(H, N, lo[s], hi[s], o[s], os_of)) claimed++;
         }
+        if (claimed) atomicAdd(&s_claimed, claimed);
         __syncthreads();
+    }
+    if (threadIdx.x == 0 && s_claimed) atomicAdd((unsigned long long*)count, (unsigned long long)s_claimed);
+}
+
+// Every import out of the table (each entry whose id another shard owns, or the tombstone of an id no
+// owner held, under its marker): the owned-only table again.  flag: only if *flag (tb_pass_clear's
+// import gate), null: always (before
+// an account is inserted on this shard, or the table is read whole).
+__global__ __launch_bounds__(256) void tb_node_import_flush(Tables H, u64 cap, u32 world, u32 self, const u32* flag) {
+    if (flag && !*flag) return;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (u64)gridDim.x * blockDim.x) {
+        const AccountHot& h = H.acct_hot[i];
+        if (h.timestamp == 0) continue;
+        // A tombstone id: an import's (its timestamp the import marker, bit 63) or a withdrawn create's
+        // (a real timestamp: it stays, on an owned probe chain).
+        const bool tomb = h.id_lo == ~0ULL && h.id_hi == ~0ULL;
+        if (tomb ? (h.timestamp >> 63) != 0 : tb_home(h.id_lo, h.id_hi, world) != self) H.acct_hot[i] = AccountHot{};
     }
 }
 
-// What a routed commit on a node home needs to import (engine.hip enqueue_call runs the import before
-// each of its sub-passes and the clear after it).
+// What a routed commit on a node home needs to import (engine.hip enqueue_call: the gate in
+// tb_pass_clear, then the flush and the import, before each of its sub-passes).
 struct NodeImport {
     NodeTablesArgs N;
     u32 self;
-    u32* list;     // [cap] the slot each event side of a sub-pass imported into (TB_NOT_FOUND: none)
-    u64* count;    // zeroed by the sub-pass's tb_pass_clear (unused since the per-side list)
-    u64 cap;       // 2 x the sub-pass's events at most
+    u64* count;    // the shard's live imports (persistent across passes)
+    u64 room;      // imports the table has room for (2 x a sub-pass's events at most)
+    u32* flag;     // tb_pass_clear's gate -> tb_node_import_flush
     u32* os_of;    // [account_cap] imported slot -> the account's slot on its owner
-    u64* leg_counts = nullptr;  // the home's per-owner leg counts, zeroed by the same tb_pass_clear
+    u64* leg_counts = nullptr;  // the home's per-owner leg counts, zeroed by the sub-pass's tb_pass_clear
     u32 legs_n = 0;
-    // Recorded after each sub-pass's owner legs (before the table's import clear): what the owners
-    // wait for (the legs and codes are final there).  Host-side only (hipEvent_t).
+    // Recorded after each sub-pass's owner legs: what the owners wait for (the legs and codes are
+    // final there).  Host-side only (hipEvent_t).
     void* ev_legs = nullptr;
 };
-
-__global__ void tb_node_import_clear(Tables H, const u32* list, u64 n) {
-    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-        const u32 slot = list[i];
-        if (slot != TB_NOT_FOUND) H.acct_hot[slot] = AccountHot{};
-    }
-}
 
 struct NodeReplyArgs {
     const u8* codes[NODE_WORLD_MAX];  // home h's result codes (one byte per received event)
@@ -413,8 +430,9 @@ __global__ __launch_bounds__(256) void tb_ledger_summary(Tables T, u64 cap, u32 
             v[1] = b.debits_posted;
             v[2] = b.credits_pending;
             v[3] = b.credits_posted;
-            live = 1;
-            if (world && tb_home(h.id_lo, h.id_hi, world) != self && (v[0] | v[1] | v[2] | v[3]) != 0) stray = 1;
+            const bool owned = !world || tb_home(h.id_lo, h.id_hi, world) == self;
+            live = owned ? 1 : 0;  // (a node home's imports are not its accounts)
+            if (!owned && (v[0] | v[1] | v[2] | v[3]) != 0) stray = 1;
         }
     }
     const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

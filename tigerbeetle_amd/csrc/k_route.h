@@ -202,11 +202,16 @@ __global__ __launch_bounds__(64) void tb_route_publish(u64* words, u64* host_wor
     if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Pass 3: stable scatter into the send buffer, with the execute timestamp of every event.
+// Pass 3: stable scatter into the send buffer, with the execute timestamp of every event.  A tile's
+// events for one home land at consecutive send positions, so the tile is written cooperatively: eight
+// lanes per event, each a 16-B chunk, the events in tile order — a wave's store covers eight whole
+// records, mostly contiguous (one store per lane per record would put 64 records' partial lines in
+// every store instruction).
 __global__ __launch_bounds__(ROUTE_THREADS) void tb_route_scatter(RouteArgs A, u8* send_events, u32* slot) {
     __shared__ __attribute__((aligned(16))) u8 stage[ROUTE_THREADS * STAGE_STRIDE];
     __shared__ u32 s_wcnt[ROUTE_THREADS / 64][ROUTE_WORLD_MAX];
     __shared__ u32 s_range[2];
+    __shared__ u32 s_pos[ROUTE_THREADS];  // each event's send position (SLOT_LOCAL: not routed)
     const u64 tile0 = (u64)blockIdx.x * ROUTE_THREADS;
     const u32 count = (u32)min((u64)ROUTE_THREADS, A.n - tile0);
     tb_stage_events(A.events + tile0 * 128, count, stage);
@@ -226,21 +231,28 @@ __global__ __launch_bounds__(ROUTE_THREADS) void tb_route_scatter(RouteArgs A, u
         s_range[1] = tb_batch_search(A.batch_off, s_range[0], A.nb, tile0 + count - 1) + 1;
     }
     __syncthreads();
-    if (!live) return;
-    if (h == ROUTE_LOCAL || h == ROUTE_DEP) {
+    u32 pos = SLOT_LOCAL;
+    if (live && (h == ROUTE_LOCAL || h == ROUTE_DEP)) {
         slot[e] = h == ROUTE_LOCAL ? SLOT_LOCAL : SLOT_DEP;
-        return;
+    } else if (live) {
+        pos = A.block_base[(u64)blockIdx.x * A.world + h] + before;
+        for (u32 w = 0; w < wave; w++) pos += s_wcnt[w][h];
+        const u32 b = tb_batch_search(A.batch_off, s_range[0], s_range[1], e);
+        const u64 boff = A.batch_off[b];
+        const u32 L = (u32)(A.batch_off[b + 1] - boff);
+        slot[e] = pos;
+        *(u64*)(stage + tb_stage_off(threadIdx.x, 7) + 8) = A.batch_ts[b] - L + 1 + (e - boff);  // execute, :645
     }
-    u32 pos = A.block_base[(u64)blockIdx.x * A.world + h] + before;
-    for (u32 w = 0; w < wave; w++) pos += s_wcnt[w][h];
-    const u32 b = tb_batch_search(A.batch_off, s_range[0], s_range[1], e);
-    const u64 boff = A.batch_off[b];
-    const u32 L = (u32)(A.batch_off[b + 1] - boff);
-    slot[e] = pos;
-    *(u64*)(stage + tb_stage_off(threadIdx.x, 7) + 8) = A.batch_ts[b] - L + 1 + (e - boff);  // execute, :645
-    u32x4* dst = (u32x4*)(send_events + (u64)pos * 128);
+    s_pos[threadIdx.x] = pos;
+    __syncthreads();
 #pragma unroll
-    for (u32 k = 0; k < 8; k++) dst[k] = *(const u32x4*)(stage + tb_stage_off(threadIdx.x, k));
+    for (u32 r = 0; r < 8; r++) {
+        const u32 c = threadIdx.x + r * ROUTE_THREADS;  // chunk c: event c / 8, part c % 8
+        const u32 j = c >> 3, part = c & 7;
+        if (j < count && s_pos[j] != SLOT_LOCAL) {
+            ((u32x4*)(send_events + (u64)s_pos[j] * 128))[part] = *(const u32x4*)(stage + tb_stage_off(j, part));
+        }
+    }
 }
 
 // Dependency classes of every event of a dirty pass (its source's share), for the split commit

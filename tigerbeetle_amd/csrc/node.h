@@ -96,9 +96,9 @@ struct NodeDev {
     hipEvent_t ev_xwb = nullptr;  // split pass: this shard's write-back of the sequencer's results done
     // Partitioned account records: the foreign accounts a routed sub-pass imports (k_node.h
     // tb_node_import), and the replicated limit-account bitmap.
-    u32* imp_list = nullptr;
-    u64* imp_count = nullptr;
-    u64 imp_cap = 0;
+    u32* imp_flag = nullptr;   // tb_pass_clear's import gate -> tb_node_import_flush
+    u64* imp_count = nullptr;  // live imports (they stay across passes)
+    u64 imp_cap = 0;           // the table's import room
     u32* imp_os = nullptr;  // [account_cap] an imported slot's slot on the account's owner (owner legs)
     u64* limbits = nullptr;
     u64 limmask = 0;             // bits - 1
@@ -309,7 +309,7 @@ static void node_free(TbNode* N) {
                        D.words[0], D.words[1], D.meta[0], D.meta[1], D.block_counts, D.results, D.reply_bytes,
                        D.recv, D.codes, D.legs, D.leg_counts, D.hmeta_dev[0], D.hmeta_dev[1], D.hmeta_dev[2],
                        D.dep1, D.dep[0], D.dep[1], D.dkeys, D.dbal, D.dcounts, D.keyset, D.markset, D.wb_count,
-                       D.imp_list, D.imp_count, D.imp_os, D.limbits};
+                       D.imp_flag, D.imp_count, D.imp_os, D.limbits};
         for (void* p : dev) if (p) (void)hipFree(p);
         void* host[] = {D.h_words[0], D.h_words[1], D.h_meta[0], D.h_meta[1], D.hmeta_host[0], D.hmeta_host[1],
                         D.hmeta_host[2], D.h_arena[0], D.h_arena[1], D.h_arena[2], D.h_dcounts, D.h_flags};
@@ -478,8 +478,9 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
         NALLOC(tbEventCreateWithFlags(&D.ev_pre, hipEventDisableTiming));
         NALLOC(tbEventCreateWithFlags(&D.ev_xwb, hipEventDisableTiming));
         D.imp_cap = 2 * (u64)sc.pass_events_max;
-        NALLOC(tbMalloc(&D.imp_list, D.imp_cap * 4));
+        NALLOC(tbMalloc(&D.imp_flag, 4));
         NALLOC(tbMalloc(&D.imp_count, 8));
+        NALLOC(hipMemset(D.imp_count, 0, 8));
         NALLOC(tbMalloc(&D.imp_os, D.E->account_cap * 4));
         // 16 bits per account of the ledger: a false positive (which only sequences an event) is at
         // most 1 in 16 even when every account is limited.
@@ -570,6 +571,22 @@ static int node_sync(TbNode* N) {
     return status;
 }
 
+// Every shard's imports out of its table (k_node.h tb_node_import_flush), on its engine stream:
+// before an account is inserted on a shard (so no import sits on an owned probe chain) and before a
+// table is read whole.  Routed passes import again what they name.
+static int node_imports_flush(TbNode* N) {
+    for (u32 d = 0; d < N->world; d++) {
+        NodeDev& D = N->D[d];
+        tbgpu* E = D.E;
+        NCK(hipSetDevice(D.device));
+        hipLaunchKernelGGL(tb_node_import_flush, dim3((u32)std::min<u64>(1024, (E->account_cap + 255) / 256)), dim3(256), 0,
+                           E->stream, E->T, E->account_cap, N->world, d, (const u32*)nullptr);
+        NCK(hipGetLastError());
+        NCK(hipMemsetAsync(D.imp_count, 0, 8, E->stream));
+    }
+    return TBGPU_STATUS_OK;
+}
+
 // Sum of the shards' balance bounds (every true, owner-held balance is below it).
 static unsigned __int128 node_bound(TbNode* N) {
     typedef unsigned __int128 h128;
@@ -609,7 +626,8 @@ static int node_commit_accounts(TbNode* N, u32 n, const u64* ts, const void* con
     const u32 W = N->world;
     tbgpu* X = N->X;
     const int dev0 = N->D[0].device;
-    int st = node_sync(N);  // the owners' tables are read below
+    int st = node_imports_flush(N);  // new accounts go into the owners' tables below
+    if (!st) st = node_sync(N);      // the owners' tables are read below
     if (st) return st;
     for (u32 k = 0; k < n; k++) ckpt_note_ids(N->D[0].E, (const u8*)inputs[k], lens[k]);  // the next write-back
     NodeTablesArgs NT{};
@@ -988,9 +1006,9 @@ static int node_home_one(TbNode* N, u32 h, void* ctx) {
             imp.N.world = W;
             for (u32 d = 0; d < W; d++) imp.N.T[d] = N->D[d].E->T;
             imp.self = h;
-            imp.list = D.imp_list;
             imp.count = D.imp_count;
-            imp.cap = D.imp_cap;
+            imp.room = D.imp_cap;
+            imp.flag = D.imp_flag;
             imp.os_of = D.imp_os;
             imp.leg_counts = D.leg_counts;
             imp.legs_n = W;
@@ -1595,6 +1613,7 @@ static int node_commit_pipelined(TbNode* N, u8 op, u32 n, const u64* ts, const v
 // Every account, from its owner (the only copy), in id order.
 static int node_export_accounts(TbNode* N, std::vector<u8>& out) {
     out.clear();
+    if (const int st = node_imports_flush(N)) return st;  // each table read whole: its own accounts only
     for (u32 d = 0; d < N->world; d++) {
         if (hipSetDevice(N->D[d].device) != hipSuccess) return fail(TBGPU_STATUS_DEVICE, "hipSetDevice");
         std::vector<u8> r;
@@ -1700,6 +1719,8 @@ static int node_api_reset(TbNode* N) {
     for (u32 d = 0; d < N->world; d++) {
         const int st = tbgpu_reset(N->D[d].E);
         if (st) return st;
+        NCK(hipSetDevice(N->D[d].device));
+        NCK(hipMemset(N->D[d].imp_count, 0, 8));  // (the tables are empty again)
     }
     N->commit_ts = 0;
     return TBGPU_STATUS_OK;
@@ -1981,6 +2002,7 @@ static int node_api_unregister_host(TbNode* N, void* ptr) {
 // Accounts from elsewhere (a load from the forest, an upsert): each to its owner; every shard's limit
 // bitmap learns the limit accounts among them.
 static int node_api_accounts_in(TbNode* N, const void* records, u32 n, bool load) {
+    if (const int st = node_imports_flush(N)) return st;  // accounts are inserted on their owners below
     std::vector<std::vector<u8>> recs(N->world);
     bool limits = false;
     for (u32 i = 0; i < n; i++) {

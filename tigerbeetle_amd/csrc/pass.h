@@ -339,15 +339,26 @@ __device__ static inline void tb_dedup_mark(const PassArgs& P) {
 // previous pass may have written (all `cap` entries when `force`).
 // meta (optional): a one-prepare call's metadata {offset 0, offset 1, timestamp}, carried here as
 // kernel arguments instead of a copy ahead of the pass (the replica's one-prepare commits).
-// zero / zero_b (optional): counters of the caller zeroed here instead of by a copy each (a node
-// home's import count and leg counts, k_node.h).
+// zero_b (optional): counters of the caller zeroed here instead of by a copy each (a node home's leg
+// counts, k_node.h).  imp (optional): a node home's import gate (k_node.h tb_node_import_flush):
+// when its live imports plus what this sub-pass may add would pass the room, flag the flush and
+// restart the count.
+struct ImportGate {
+    u64* count;
+    u64 room, need;
+    u32* flag;
+};
 __global__ __launch_bounds__(256) void tb_pass_clear(u64* dedup, u64 cap, u64* sum_shards, const Globals* g, u32 epoch,
                                                      u32 force, u32* leg_tot, u32 leg_buckets, u64* meta, u64 m0, u64 m1,
-                                                     u64 m2, u64* kclock, u64* zero = nullptr, u64* zero_b = nullptr,
+                                                     u64 m2, u64* kclock, ImportGate imp, u64* zero_b = nullptr,
                                                      u32 zero_b_n = 0) {
     const u64 w = g->dedup_dirty;  // before the stores (a load after them waits for them)
     if (blockIdx.x == 0 && threadIdx.x < SUM_WORDS) sum_shards[threadIdx.x] = 0;
-    if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;
+    if (imp.count && blockIdx.x == 0 && threadIdx.x == 0) {
+        const bool full = *imp.count + imp.need > imp.room;
+        *imp.flag = full ? 1u : 0u;
+        if (full) *imp.count = 0;
+    }
     if (zero_b && blockIdx.x == 0 && threadIdx.x < zero_b_n) zero_b[threadIdx.x] = 0;
     if (kclock && blockIdx.x == 0) {
         for (u32 k = threadIdx.x; k < KCLOCK_WORDS; k += 256) kclock[k] = k % KCLOCK_STRIDE ? 0 : ~0ULL;
