@@ -997,7 +997,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
         // inline_meta: a one-prepare call's metadata, written into E->meta by this first kernel.
         u64* meta_dst = inline_meta && b0 == 0 ? (u64*)d_off : nullptr;
         ImportGate gate{};
-        if (imp && n > 0) gate = ImportGate{imp->count, imp->room, 2 * n, imp->flag};
+        if (imp && n > 0) gate = ImportGate{imp->count, imp->room, 0, imp->flag};
         hipLaunchKernelGGL(tb_pass_clear, dim3(clear_grid), dim3(256), 0, E->stream, E->dedup, E->dedup_cap, E->sum_shards,
                            E->g, E->epoch, E->dedup_force ? 1u : 0u, E->leg_tot, E->leg_buckets, meta_dst,
                            inline_meta ? inline_meta[0] : 0, inline_meta ? inline_meta[1] : 0, inline_meta ? inline_meta[2] : 0,
@@ -1010,9 +1010,8 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
 
         if (imp && n > 0) {  // a node home: the foreign accounts this sub-pass names, from their owners
             const u32 ig = (u32)std::min<u64>(4096, (n + 255) / 256);
-            if (2 * n > imp->room) return fail(TBGPU_STATUS_INVALID, "node import room: %llu events", (unsigned long long)n);
-            // The imports of earlier passes stay, unless this sub-pass could overfill the room (the
-            // gate in tb_pass_clear above).
+            // The imports of earlier passes stay, unless they passed the room (the gate in
+            // tb_pass_clear above).
             hipLaunchKernelGGL(tb_node_import_flush, dim3((u32)std::min<u64>(1024, (E->account_cap + 255) / 256)), dim3(256), 0,
                                E->stream, E->T, E->account_cap, imp->N.world, imp->self, (const u32*)imp->flag);
             hipLaunchKernelGGL(tb_node_import, dim3(ig), dim3(256), 0, E->stream, E->T, imp->N, events_dev + P.e0 * 128, n,

@@ -217,11 +217,10 @@ struct NodeTablesArgs {
 // validate and the ordered fallback read of an account in a routed pass (its balances are the owner's
 // and never read here: the router's certificate rules out every balance check, and limit and
 // balancing events are sequenced).  Entries go into empty slots and stay: the next passes find them
-// with one probe instead of importing again (a hot record never changes after create_account; an id
-// no owner holds gets a tombstone entry, which also stays — only a create could change that, and
-// every insert of an account flushes the imports first).  So an import never sits on an owned
-// account's probe chain (owned accounts are only inserted while no import exists), and
-// tb_node_import_flush restores the owned-only table exactly.
+// with one probe instead of importing again (a hot record never changes after create_account, and
+// every insert of an account flushes the imports first).  An id no owner holds takes no entry
+// (validate answers account_not_found), so the imports are at most the ledger's accounts.  An import never sits on an owned account's probe chain (owned accounts are only
+// inserted while no import exists), and tb_node_import_flush restores the owned-only table exactly.
 // One entry per id however many lanes name it (a Zipf-hot account is named by a large share of a
 // pass): first the workgroup keeps one lane per distinct id (tb_wg_dedup: LDS, exact), then that lane
 // claims an empty slot by a CAS of its timestamp word to a marker {bit 63, the id's 63-bit
@@ -229,7 +228,8 @@ struct NodeTablesArgs {
 // already there stops — the winner alone reads the owner's record, writes the entry and puts the real
 // timestamp last.  (Two ids with one 63-bit fingerprint meeting on one probe chain in one pass would
 // import one of them only: about 2^-63 per pair, the sequencer's own fingerprint bet.)
-// Returns whether it claimed a slot (false: another lane imports the id, or it is here already).
+// Returns whether it imported the id (false: another lane imports it, it is here already, or no
+// owner holds it).
 __device__ static inline bool tb_import_one(const Tables& H, const NodeTablesArgs& N, u64 lo, u64 hi, u32 o, u32* os_of) {
     const u64 mark = (1ULL << 63) | (tb_fingerprint(lo, hi) >> 1);
     u64 pos = tb_hash_id(lo, hi) & H.account_mask;
@@ -240,12 +240,22 @@ __device__ static inline bool tb_import_one(const Tables& H, const NodeTablesArg
     const u64 opos = tb_hash_id(lo, hi) & O.account_mask;
     const AccountHot o0 = O.acct_hot[opos];
     u64 t_first = H.acct_hot[pos].timestamp;
+    // The owner's verdict comes before any claim: an id no owner holds never takes a slot (a slot
+    // claimed and released would leave a hole in the probe chain of an id imported past it).
+    AccountHot a;
+    u32 os = TB_NOT_FOUND;
+    bool looked = false;
     for (u64 k = 0; k <= H.account_mask; k++) {
         // Plain (cached) reads: a stale one costs a failed CAS (which returns the truth) or a
         // duplicate entry, never a wrong one.
         u64* tw = &H.acct_hot[pos].timestamp;
         u64 t = k == 0 ? t_first : *tw;
         if (t == 0) {
+            if (!looked) {
+                os = tb_account_find_from(O, lo, hi, opos, o0, &a);
+                looked = true;
+                if (os == TB_NOT_FOUND) return false;  // validate finds no entry: account_not_found
+            }
             t = atomicCAS((unsigned long long*)tw, 0ULL, (unsigned long long)mark);
             if (t == 0) {
                 slot = (u32)pos;
@@ -260,14 +270,7 @@ __device__ static inline bool tb_import_one(const Tables& H, const NodeTablesArg
         pos = (pos + 1) & H.account_mask;
     }
     if (slot == TB_NOT_FOUND) return false;
-    AccountHot a;
-    const u32 os = tb_account_find_from(O, lo, hi, opos, o0, &a);
     AccountHot* h = &H.acct_hot[slot];
-    if (os == TB_NOT_FOUND) {  // no such account: a tombstone id (probes continue past it) under the marker
-        h->id_lo = ~0ULL;
-        h->id_hi = ~0ULL;
-        return true;
-    }
     os_of[slot] = os;  // the owner's slot, for this pass's owner legs
     h->ledger = a.ledger;
     h->code = a.code;

@@ -440,24 +440,36 @@ struct OwnerLegArgs {
     u32 words;      // OWNER_LEG_WORDS (id legs) or NODE_LEG_WORDS (slot legs)
 };
 
+// The tile's records are staged through LDS (coalesced 16-B chunks) and each thread reads the fields
+// it needs (accounts, amount, flags) from there: a per-thread 128-B record load would put 64
+// records' partial lines in every load instruction.
 __global__ __launch_bounds__(256) void tb_owner_legs(PassArgs P, OwnerLegArgs O) {
+    static_assert(VALIDATE_THREADS == 256, "tb_stage_events stages 256 records");
+    __shared__ __attribute__((aligned(16))) u8 stage[256 * STAGE_STRIDE];
     __shared__ u32 s_cnt[ROUTE_WORLD_MAX];
     __shared__ u64 s_base[ROUTE_WORLD_MAX];
     if (threadIdx.x < O.world) s_cnt[threadIdx.x] = 0;
-    __syncthreads();
-    const u32 pe = blockIdx.x * 256 + threadIdx.x;
+    const u32 tile0 = blockIdx.x * 256;
+    tb_stage_events((const u8*)(P.T.xlog + P.log_base + tile0), (u32)min((u64)256, P.n - tile0), stage);  // (syncs)
+    const u32 pe = tile0 + threadIdx.x;
     u32 owner[2] = {0, 0}, pos[2] = {0, 0}, oslot[2] = {0, 0};
     bool emit[2] = {false, false};
-    Transfer t;
+    u128 acct[2] = {0, 0}, amount = 0;
     u32 field0 = 0;
     if (pe < P.n && P.codes[P.e0 + pe] == R_OK) {
-        t = P.T.xlog[P.log_base + pe];
+        const u64* c1 = (const u64*)(stage + tb_stage_off(threadIdx.x, 1));  // debit account id
+        const u64* c2 = (const u64*)(stage + tb_stage_off(threadIdx.x, 2));  // credit account id
+        const u64* c3 = (const u64*)(stage + tb_stage_off(threadIdx.x, 3));  // amount
+        const u16 flags = *(const u16*)(stage + tb_stage_off(threadIdx.x, 7) + 6);  // @118
+        acct[0] = tb_u128(c1[0], c1[1]);
+        acct[1] = tb_u128(c2[0], c2[1]);
+        amount = tb_u128(c3[0], c3[1]);
         const u32 info = P.info[pe];
         const bool dep = (info & HZ_DEP) != 0;
-        field0 = (t.flags & TF_PENDING) ? 0 : 1;  // debits_pending / debits_posted (+2: credits)
+        field0 = (flags & TF_PENDING) ? 0 : 1;  // debits_pending / debits_posted (+2: credits)
 #pragma unroll
         for (u32 s = 0; s < 2; s++) {
-            const u128 id = s ? t.credit_account_id : t.debit_account_id;
+            const u128 id = acct[s];
             owner[s] = tb_home(tb_lo(id), tb_hi(id), O.world);
             emit[s] = !(dep && owner[s] == O.self);
             if (emit[s]) pos[s] = atomicAdd(&s_cnt[owner[s]], 1u);
@@ -482,7 +494,7 @@ __global__ __launch_bounds__(256) void tb_owner_legs(PassArgs P, OwnerLegArgs O)
                 }
             }
             if (dep) {  // cancel the replay's local add: the owner applies it
-                tb_bal_add(P.T.bal, slot, field0 + 2 * s, (u128)0 - t.amount);
+                tb_bal_add(P.T.bal, slot, field0 + 2 * s, (u128)0 - amount);
             }
         }
     }
@@ -503,15 +515,14 @@ __global__ __launch_bounds__(256) void tb_owner_legs(PassArgs P, OwnerLegArgs O)
         u64* w = O.legs + ((u64)owner[s] * O.cap + k) * O.words;
         if (O.os_of) {
             w[0] = ((u64)oslot[s] << 2) | (field0 + 2 * s);
-            w[1] = tb_lo(t.amount);
-            w[2] = tb_hi(t.amount);
+            w[1] = tb_lo(amount);
+            w[2] = tb_hi(amount);
             continue;
         }
-        const u128 id = s ? t.credit_account_id : t.debit_account_id;
-        w[0] = tb_lo(id);
-        w[1] = tb_hi(id);
-        w[2] = tb_lo(t.amount);
-        w[3] = tb_hi(t.amount);
+        w[0] = tb_lo(acct[s]);
+        w[1] = tb_hi(acct[s]);
+        w[2] = tb_lo(amount);
+        w[3] = tb_hi(amount);
         w[4] = field0 + 2 * s;
     }
 }

@@ -376,9 +376,12 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
     sc.pass_batches_max = (u32)std::min<u64>(FLOW_NB_MAX, (sc.pass_events_max + BATCH_EVENTS_MAX - 2) / (BATCH_EVENTS_MAX - 1) + 2);
     sc.pass_batches_max = std::max(sc.pass_batches_max, N->pb_src);
     // Accounts: the ones this shard owns (1/N of the ledger, with room for hash imbalance) plus the
-    // imports of one routed sub-pass (two per event).
+    // import room — every account of the ledger when that is smaller than a routed sub-pass's two per
+    // event (imports then never need a flush, and the table stays as dense as the ledger allows: its
+    // random probes hit the MALL), else the sub-pass's two per event (k_node.h tb_node_import_flush).
     const u64 owned = std::min<u64>(config->accounts_max, config->accounts_max / W + config->accounts_max / (8 * W) + 4096);
-    sc.accounts_max = std::min<u64>(1ULL << 31, owned + 2 * (u64)sc.pass_events_max);
+    const u64 import_room = std::min<u64>(config->accounts_max, 2 * (u64)sc.pass_events_max);
+    sc.accounts_max = std::min<u64>(1ULL << 31, owned + import_room);
     int st = TBGPU_STATUS_OK;
     for (u32 d = 0; d < W && st == TBGPU_STATUS_OK; d++) {
         NodeDev& D = N->D[d];
@@ -477,7 +480,7 @@ static int node_init(const tbgpu_config* config, TbNode** out) {
         NALLOC(tbEventCreateWithFlags(&D.ev_marked, hipEventDisableTiming));
         NALLOC(tbEventCreateWithFlags(&D.ev_pre, hipEventDisableTiming));
         NALLOC(tbEventCreateWithFlags(&D.ev_xwb, hipEventDisableTiming));
-        D.imp_cap = 2 * (u64)sc.pass_events_max;
+        D.imp_cap = import_room;
         NALLOC(tbMalloc(&D.imp_flag, 4));
         NALLOC(tbMalloc(&D.imp_count, 8));
         NALLOC(hipMemset(D.imp_count, 0, 8));
