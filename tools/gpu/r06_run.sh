@@ -89,6 +89,18 @@ for what in "$@"; do
       timeout -k 10 600 python -u bench.py --steps 2 --warmup 1 --secondary 0 --replica-prepares 0 --host-prepares 0 \
         --write-back 0 --cpu-sample 2000000 > $O/bench.json 2> $O/bench.err
       rc=$?; echo "bench rc=$rc"; tail -c 1500 $O/bench.json; tail -5 $O/bench.err; [ $rc -ne 0 ] && exit $rc ;;
+    nodelib)  # same box: node C2 (2 logical shards) with library builds in turn (NODELIB_VARIANTS: cur or a
+      # tigerbeetle_amd/libtbgpu_<name>.so), NODELIB_CHUNKS prepare blocks
+      LEGS="--secondary 0 --replica-prepares 0 --host-prepares 0 --write-back 0 --cpu-sample 0 --host-steps 0 --access-mix 0"
+      for v in ${NODELIB_VARIANTS:-r06a cur r06a cur}; do
+        lib=""; [ "$v" != cur ] && lib="$R/tigerbeetle_amd/libtbgpu_$v.so"
+        for pb in ${NODELIB_CHUNKS:-64 512}; do
+          TBGPU_AB_LIB=$lib timeout -k 10 400 python -u bench.py --gpus 2 --same-device --accounts 2000000 --transfers 4000000 \
+            --steps 3 --warmup 1 $LEGS --chunk-prepares $pb > $O/nodelib_${v}_$pb.json 2> $O/nodelib_${v}_$pb.err
+          rc=$?; [ $rc -ne 0 ] && { echo "nodelib $v $pb rc=$rc"; tail -5 $O/nodelib_${v}_$pb.err; exit $rc; }
+          python -c "import json;d=json.loads(open('$O/nodelib_${v}_$pb.json').read().strip().splitlines()[-1]);print('nodelib $v $pb',round(d['value']/1e6,1),'M/s',d['ms_per_step'],'ms')"
+        done
+      done ;;
     wbab)  # write-back copy-out A/B on one box: counts-sized vs bound-sized, read through vs staged bodies
       for v in ${WBAB_VARIANTS:-base bound stage both}; do
         case $v in
