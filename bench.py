@@ -58,9 +58,10 @@ PCIE_MEASURED_GBS = 57.3
 CHUNK_PREPARES = {"c2": 64, "c3": 64, "c3h": 64, "c4": 128}
 # The node engine (--gpus N > 1): prepares per source block of a pass.  A node pass has fixed costs a
 # single engine's has not (the route plan's host round trip, per-shard import, owner legs, replies,
-# each a launch per shard): C2 on two logical shards of one GPU ran at 625 M/s in 64-prepare blocks
-# and 1.13 G/s in 512-prepare blocks (round 6, profiles/r06/node/).
-NODE_CHUNK_PREPARES = {"c2": 256, "c3": 64, "c3h": 64, "c4": 128}
+# each a launch per shard): C2 on two logical shards of one GPU ran at 0.76 / 1.52 / 1.76 G/s in
+# 64- / 256- / 512-prepare blocks (1024: 1.76; round 6, profiles/r06/node/lib_ab/).  Per GPU a
+# 512-prepare block costs ~1 GB of send buffer and 2 GB of owner-leg regions at N = 8.
+NODE_CHUNK_PREPARES = {"c2": 512, "c3": 64, "c3h": 64, "c4": 128}
 
 
 def parse():
@@ -237,14 +238,19 @@ def run_replica_path(args, device):
     3045-3102); without and with the groove write-back in compact: one bar behind (asynchronous), at each
     bar's last op (synchronous: the Zig wrapper's default), one bar behind with the bars of every
     checkpoint op and trigger synchronous (a 1024-slot journal, src/config.zig:136; the Zig wrapper
-    with engine_write_back_behind) and one op behind with every bar complete at its last op."""
+    with engine_write_back_behind), and one op / a chunk of 4 or 8 ops behind with every bar complete
+    at its last op (the reference's one-bar table_mutable bound)."""
     import subprocess
     exe = os.path.join(ROOT, "tigerbeetle_amd", "host", "tb_replica_bench")
     out = {}
-    for name, opts in (("in_memory", []), ("in_memory_staged", ["--stage"]), ("with_write_back", ["--write-back"]),
-                       ("with_write_back_sync", ["--write-back-sync"]),
-                       ("with_write_back_behind_checkpoints", ["--write-back", "--checkpoint-journal-slots", "1024"]),
-                       ("with_write_back_per_op", ["--write-back-per-op"])):
+    # The write-back shapes call tbgpu_prefetch (--stage) as the replica does before every commit: with a
+    # copy-out in flight it stages the body by DMA (DESIGN.md §7b).
+    for name, opts in (("in_memory", []), ("in_memory_staged", ["--stage"]), ("with_write_back", ["--write-back", "--stage"]),
+                       ("with_write_back_sync", ["--write-back-sync", "--stage"]),
+                       ("with_write_back_behind_checkpoints", ["--write-back", "--checkpoint-journal-slots", "1024", "--stage"]),
+                       ("with_write_back_per_op", ["--write-back-per-op", "--stage"]),
+                       ("with_write_back_every_4", ["--write-back-every", "4", "--stage"]),
+                       ("with_write_back_every_8", ["--write-back-every", "8", "--stage"])):
         cmd = [exe, "--accounts", str(args.accounts), "--prepares", str(args.replica_prepares),
                "--device", str(device)] + opts
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
