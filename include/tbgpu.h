@@ -121,7 +121,9 @@ int tbgpu_commit(tbgpu_t* engine, uint8_t operation, uint64_t timestamp, const v
  * HBM at once, and the following tbgpu_commit of the same body (same pointer and length) only waits
  * for it.  A body in registered host memory (tbgpu_register_host: the message pool) is not staged:
  * the commit's first kernel reads it through, which measured faster than a DMA the replica's serial
- * prefetch -> commit leaves nothing to overlap with.  Completes
+ * prefetch -> commit leaves nothing to overlap with — except while the copy-out of an
+ * asynchronous write-back written every few commits is in flight: then it is staged, so the commit
+ * reads HBM and the copy-out need not wait for the commit's PCIe reads.  Completes
  * immediately (the reference allows the callback inside the call, src/lsm/groove.zig:723-742).
  * The staged copy belongs to the very next call only, if that call is tbgpu_commit of this body
  * (the replica's prefetch(op) -> commit(op)); any other call drops it.  The body must not change
@@ -220,7 +222,10 @@ int tbgpu_checkpoint_delta(tbgpu_t* engine, void* accounts_out, void* accounts_b
  * state it describes is captured in stream order with the commits (the accounts the bar's transfers
  * name, with their balances; the next commits follow the capture), the rest is gathered on a
  * low-priority stream beside them, and the objects cross PCIe into the caller's buffers by DMA,
- * one slice after each one-prepare tbgpu_commit's body read (or all at the wait).
+ * one slice after each one-prepare tbgpu_commit's body read (all at once after a commit whose body
+ * tbgpu_prefetch staged; the rest at the wait).  A write-back every few commits whose objects
+ * filled those bounds is sent at the bounds from the first commit after it (the bytes past the
+ * counts land in the caller's buffers, unread; tbgpu_stats.write_backs_bound).
  * tbgpu_checkpoint_delta_wait returns the counts once the
  * objects have landed (transfers and posted entries sorted as above); until then the buffers belong
  * to the engine, and no other write-back may start.  Needs buffers registered with
