@@ -38,12 +38,14 @@
  *     never reaches, so the engine stops: every later call that changes state returns
  *     TBGPU_STATUS_PANIC until tbgpu_reset (or tbgpu_deinit).  Reads (exports, stats) still work.
  *   - Device exclusivity: the ordered fallback kernel (tb_flow) synchronises its workgroups with a
- *     software grid barrier, so its grid (at most a quarter of the CUs, shared among this process's
- *     engines on the device) must be resident at once.  tbgpu_init checks that once (a probe grid
- *     of the same shape must become co-resident within 200 ms) and fails with TBGPU_STATUS_DEVICE
- *     on a device other work holds; one engine process per device is the supported deployment.
- *     A co-tenant that arrives later and starves the grid makes a pass end in PANIC (every wait is
- *     bounded, PANIC_FLOW_STALL), never a hang.
+ *     software grid barrier among the workgroups it ADMITS at its start — those resident within
+ *     ~50 us of the first one (at most a quarter of the CUs, shared among this process's engines on
+ *     the device); a workgroup that starts later exits, and the admitted ones cover the pass.  So a
+ *     co-tenant that holds CUs makes a pass slower, never a stall (tests/test_gpu_liveness.py
+ *     launches tb_flow 8x over what the device holds).  tbgpu_init still checks once that a grid
+ *     of that shape can be co-resident (within 200 ms) and fails with TBGPU_STATUS_DEVICE on a
+ *     device other work holds; one engine process per device is the supported deployment.  Every
+ *     wait stays bounded (PANIC_FLOW_STALL: an engine bug, never a hang).
  */
 #ifndef TBGPU_H
 #define TBGPU_H

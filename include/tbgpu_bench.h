@@ -56,6 +56,10 @@ int tbgpu_bench_legs_min_events(tbgpu_t* engine, uint32_t events);
 /* The limit-check sweep's walkers (k_flow.h fl_walk): up to this many heavy segments are walked
  * merged by one wave (default 63); 0: every heavy segment on a wave of its own. */
 int tbgpu_bench_walk_merge_max(tbgpu_t* engine, uint32_t segments);
+/* Liveness tests: launch the ordered fallback (tb_flow) with this many workgroups (0: its own
+ * grid), more than the device can hold at once — the ones that are not resident when its admission
+ * closes exit (k_flow.h fl_admit), as under a co-tenant. */
+int tbgpu_bench_flow_launch(tbgpu_t* engine, uint32_t workgroups);
 
 /* The memory-access mix of tb_transfers_validate without its logic, on scratch buffers sized like
  * this engine's account table and transfer index, for `transfers` events (one pass): mean ms of

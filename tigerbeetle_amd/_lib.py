@@ -168,6 +168,7 @@ SIGNATURES = [
     ("tbgpu_bench_profile_mask", ctypes.c_int, [_P, _U32]),
     ("tbgpu_bench_legs_min_events", ctypes.c_int, [_P, _U32]),
     ("tbgpu_bench_walk_merge_max", ctypes.c_int, [_P, _U32]),
+    ("tbgpu_bench_flow_launch", ctypes.c_int, [_P, _U32]),
     ("tbgpu_bench_access_mix", ctypes.c_int, [_P, _U64, ctypes.POINTER(ctypes.c_double)]),
     ("tbgpu_bench_ledger_summary", ctypes.c_int, [_P, ctypes.POINTER(tbgpu_ledger_summary)]),
     ("tbgpu_bench_checkpoint_mark", ctypes.c_int, [_P]),

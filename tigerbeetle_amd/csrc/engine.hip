@@ -185,6 +185,7 @@ struct tbgpu {
     bool lean_ok = true;          // legs passes run tb_resolve_lean first (TBGPU_NO_LEAN=1: tb_resolve alone)
     bool wb_bound_ok = true;      // bound-sized copy-outs allowed (TBGPU_WB_BOUND=0: counts always)
     bool wb_stage = true;         // prefetch stages registered bodies during a copy-out (TBGPU_WB_STAGE=0: never)
+    u32 flow_launch = 0;          // tbgpu_bench_flow_launch (tests): tb_flow launched with this many workgroups
     u64* leg_w = nullptr;
     u32* leg_off = nullptr;
     u32* leg_tot = nullptr;  // [leg_buckets] legs per bucket of the current pass
@@ -639,6 +640,7 @@ extern "C" int tbgpu_init(const tbgpu_config* config, tbgpu_t** out) {
             E->flow_capacity = (u64)occ * prop.multiProcessorCount;
             E->flow_occ = (u32)occ;
             E->F.grid = (u32)std::min<u64>(E->F.grid, E->flow_capacity);
+            E->F.grid_alloc = E->F.grid;
             int khz = 0;
             if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, E->device) != hipSuccess) khz = 0;
             khz = std::max(khz, 100000);  // s_memrealtime: 100 MHz on gfx9 parts; never trust a lower figure
@@ -1074,6 +1076,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
             // A small pass (the replica's one-prepare commit) has at most n dependent events: a grid
             // of one workgroup per 512 of them holds every unit and launches faster.
             if (n <= 65536) F.grid = std::min<u32>(F.grid, std::max<u32>(4, (u32)((n + 511) / 512)));
+            if (E->flow_launch) F.grid = E->flow_launch;  // tbgpu_bench_flow_launch (tests)
             hipLaunchKernelGGL(tb_flow, dim3(F.grid), dim3(FLOW_THREADS), 0, E->stream, P, F, seq_undo, seq_cap);
         } else if (op == OP_CREATE_TRANSFERS) {
             hipLaunchKernelGGL(tb_replay<OP_CREATE_TRANSFERS>, dim3(1), dim3(REPLAY_THREADS), 0, E->stream, P,
@@ -2368,6 +2371,16 @@ extern "C" int tbgpu_bench_walk_merge_max(tbgpu_t* E, uint32_t segments) {
         return TBGPU_STATUS_OK;
     }
     E->F.walk_merge = std::min<u32>(segments, WALK_MERGE_MAX);
+    return TBGPU_STATUS_OK;
+}
+
+extern "C" int tbgpu_bench_flow_launch(tbgpu_t* E, uint32_t workgroups) {
+    API_ENTER(E, false);
+    if (E->node) {
+        for (u32 d = 0; d < node_world(E->node); d++) tbgpu_bench_flow_launch(node_engine(E->node, d), workgroups);
+        return TBGPU_STATUS_OK;
+    }
+    E->flow_launch = workgroups;
     return TBGPU_STATUS_OK;
 }
 

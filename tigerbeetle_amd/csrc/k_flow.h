@@ -27,8 +27,11 @@
 //          queueing those with no predecessor left.  The result equals the sequential replay's:
 //          every unit sees exactly the effects of the units before it on its resources, and
 //          nothing else it reads can differ.
-// Grid-wide phases are separated by a counter barrier (every workgroup is resident: the host
-// launches at most its device budget of workgroups, engine.hip flow_grid).  Cases the planner does not cover (a chain longer than FLOW_CHAIN_MAX, a pending id
+// Grid-wide phases are separated by a counter barrier among the workgroups ADMITTED at the start
+// (fl_admit): the first one waits briefly for the launch's others, then closes admission; the ones
+// that started by then are the grid the pass is partitioned over (FL_B of FL_G), and a workgroup
+// that starts later — the device was shared and it could not be resident — exits at once.  So a
+// co-tenant holding CUs makes the pass slower, never a stall.  Cases the planner does not cover (a chain longer than FLOW_CHAIN_MAX, a pending id
 // whose creator in this pass is ambiguous) set a flag, and workgroup 0 runs the sequential replay
 // for the pass instead.  Every wait is bounded: a stall raises PANIC_FLOW_STALL, never a hang.
 #pragma once
@@ -40,6 +43,13 @@
 #define FLOW_CHAIN_MAX 64       // longer chains: sequential replay
 #define FLOW_NB_MAX 4096        // prepares per pass the planner handles (LDS prefix)
 #define FLOW_SENT 0xFFFFFFFFu   // empty pair slot
+// This workgroup's index among the admitted ones, and their number (fl_admit); ~0: not admitted.
+__shared__ u32 s_fl_b, s_fl_g;
+#define FL_B s_fl_b
+#define FL_G s_fl_g
+#define FL_ADM_CLOSED 0x80000000u
+#define FL_ADMIT_TICKS 5000  // wall-clock ticks (50 us at 100 MHz) the first workgroup waits for the others
+
 #ifndef FLOW_POLL_SLEEP
 #define FLOW_POLL_SLEEP 16      // s_sleep units (64 cycles) between a waiting lane's polls
 #endif
@@ -83,6 +93,7 @@ struct FlowArgs {
     u32* words;     // [FW_WORDS], zeroed by tb_resolve every pass
     UndoEntry* undo;  // [4 * pass events] chain of head u: [4u, 4u + 4 * len)
     u32 grid;
+    u32 grid_alloc;  // workgroups the per-workgroup arrays (hist, b_blk) hold: at most this many are admitted
     u64 stall_ticks;  // wall_clock64 ticks after which a wait is taken as an engine bug (PANIC_FLOW_STALL)
     // Bounds certification of limit checks (fl_bounds): per unit head its state and the verdicts of
     // its debit-side / credit-side limit check; per account-resource position its leg.
@@ -120,7 +131,7 @@ __device__ static inline u64 fl_now() {
 // FP_REPLIES.
 enum : u32 { FP_PLAN = 0, FP_SORT, FP_LINK, FP_BSETUP, FP_BROUNDS, FP_SWEEP, FP_RUN, FP_REPLIES };
 __device__ static inline void fl_mark(Globals* g, u64& t, u32 k) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    if (FL_B != 0 || threadIdx.x != 0) return;
     const u64 now = (u64)wall_clock64();
     atomicAdd((unsigned long long*)&g->flow_phase_ticks[k], (unsigned long long)(now - t));
     t = now;
@@ -136,8 +147,50 @@ __device__ static inline u32 fl_key_id(u64 lo, u64 hi) {
     return 0x80000000u | (u32)(tb_mix64(lo ^ tb_mix64(hi ^ 0x9e3779b97f4a7c15ULL)) % 0x7FFFFFFFu);
 }
 
+// Admission (tb_flow's first step): every workgroup takes a ticket on the entry counter; the first
+// waits until the whole launch (at most grid_alloc workgroups) has entered or FL_ADMIT_TICKS passed,
+// closes the counter and publishes how many entered.  Those are the grid: indices FL_B = their
+// tickets, FL_G = the number published.  A workgroup whose ticket comes after the close returns false (the host launches at
+// most its share of the device, engine.hip flow_grid, so on a device this process owns every
+// workgroup enters within microseconds; one a co-tenant kept off the device enters late).  The
+// counters are zeroed with the barrier's by tb_resolve every pass.
+__device__ static inline bool fl_admit(Globals* g, const FlowArgs& F) {
+    if (threadIdx.x == 0) {
+        u32* entry = &g->flow_bar[FL_BAR_STRIDE * (FL_BAR_GROUPS + 2)];
+        u32* grid = &g->flow_bar[FL_BAR_STRIDE * (FL_BAR_GROUPS + 3)];
+        const u32 cap = min(gridDim.x, F.grid_alloc);
+        const u32 t = __hip_atomic_fetch_add(entry, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_fl_b = (t & FL_ADM_CLOSED) || t >= cap ? ~0u : t;
+        if (t == 0) {
+            const u64 w0 = fl_now();
+            while ((__hip_atomic_load(entry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~FL_ADM_CLOSED) < cap) {
+                __builtin_amdgcn_s_sleep(2);
+                const u64 now = fl_now();
+                if (now > w0 && now - w0 > FL_ADMIT_TICKS) break;
+            }
+            const u32 n = __hip_atomic_fetch_or(entry, FL_ADM_CLOSED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(grid, min(n & ~FL_ADM_CLOSED, cap), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (s_fl_b != ~0u) {
+            const u64 w0 = fl_now();
+            u32 n;
+            while ((n = __hip_atomic_load(grid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+                __builtin_amdgcn_s_sleep(2);
+                if (fl_expired(F, w0)) {
+                    tb_panic(g, PANIC_FLOW_STALL);
+                    break;
+                }
+            }
+            s_fl_g = n;
+            if (n == 0 || s_fl_b >= n) s_fl_b = ~0u;  // (a stall: leave)
+        }
+    }
+    __syncthreads();
+    return s_fl_b != ~0u;
+}
+
 // Grid barrier of the co-resident grid (engine.hip flow_grid).  Two levels, so arrivals do not all
-// serialise on one word: the workgroups of each of FL_BAR_GROUPS groups (blockIdx mod groups)
+// serialise on one word: the workgroups of each of FL_BAR_GROUPS groups (FL_B mod groups)
 // count on their group's word, the last of a group counts on the root word, and the last group
 // publishes the generation, which every workgroup polls.  Every counter only grows (generation gen
 // waits for gen * members); tb_resolve zeroes them each pass.  Each workgroup writes its L2 back
@@ -149,7 +202,7 @@ __device__ static inline void fl_grid_sync(Globals* g, u32 nblocks, u32& gen, co
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const u32 groups = min(nblocks, (u32)FL_BAR_GROUPS), grp = blockIdx.x % groups;
+        const u32 groups = min(nblocks, (u32)FL_BAR_GROUPS), grp = FL_B % groups;
         const u32 members = (nblocks - grp + groups - 1) / groups;
         u32* bar = g->flow_bar;
         const u32 a = __hip_atomic_fetch_add(&bar[FL_BAR_STRIDE * grp], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -672,22 +725,22 @@ __device__ static inline void fl_st32(u32* p, u32 v) {
 template <class Pred, class Emit>
 __device__ static inline bool fl_compact(const FlowArgs& F, Globals* g, u32 n, u32& gen, u32* s_wf, u32& total,
                                          Pred pred, Emit emit) {
-    const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid, lane = tid & 63, wave = tid >> 6;
+    const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = FL_G, lane = tid & 63, wave = tid >> 6;
     const u32 ut = ((n + G - 1) / G + NT - 1) / NT * NT;
-    const u32 u0 = min(n, blockIdx.x * ut), u1 = min(n, u0 + ut);
+    const u32 u0 = min(n, FL_B * ut), u1 = min(n, u0 + ut);
     u32 cnt = 0;
     for (u32 c0 = u0; c0 < u1; c0 += NT) {
         const u32 i = c0 + tid;
         cnt += __syncthreads_count(i < u1 && pred(i));
     }
-    if (tid == 0) F.b_blk[5 * blockIdx.x] = cnt;
+    if (tid == 0) F.b_blk[5 * FL_B] = cnt;
     fl_grid_sync(g, G, gen, F);
     if (fl_stalled(g)) return false;
     u32 off = 0;
     total = 0;
     for (u32 b = 0; b < G; b++) {
         const u32 c = (u32)F.b_blk[5 * b];
-        off += b < blockIdx.x ? c : 0;
+        off += b < FL_B ? c : 0;
         total += c;
     }
     for (u32 c0 = u0; c0 < u1; c0 += NT) {
@@ -1585,7 +1638,7 @@ __device__ static inline void fl_walk_merged(const FlowArgs& F, Globals* g, cons
 __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 ndep, u32 NA, u32& gen, u32* s_wf,
                                        u32* s_ctl, HotRec* s_ring) {
     Globals* g = P.T.g;
-    const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid;
+    const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = FL_G;
     const u32 lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     WalkRec* R = (WalkRec*)F.b_ex;                 // [2 * ndep] position records (sorted order)
     const u32 segcap = 2 * ndep + 2;
@@ -1596,7 +1649,7 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
 
     // W1. Units: the verdict words; the undecided count (stats).
     u32 nu = 0;
-    for (u32 f = blockIdx.x * NT + tid; f < ndep; f += G * NT) {
+    for (u32 f = FL_B * NT + tid; f < ndep; f += G * NT) {
         if (F.f_len[f] && F.b_st[f] == BS_UNK) {
             F.b_vw[f] = (u32)F.b_vd[f] | ((u32)F.b_vc[f] << 2);
             nu++;
@@ -1648,7 +1701,7 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
                     },
                     [&](u32 k, u32 i) { hv[i] = k; }))
         return false;
-    if (blockIdx.x == 0 && tid == 0) {
+    if (FL_B == 0 && tid == 0) {
         atomicAdd((unsigned long long*)&g->walk[0], (unsigned long long)NS);
         atomicAdd((unsigned long long*)&g->walk[1], (unsigned long long)NH);
     }
@@ -1665,7 +1718,7 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
         // Tag the heavy positions with their heavy index, then list the units with a heavy leg.
         for (u32 i = 0; i < NH; i++) {
             const u32 k = hv[i], s0 = seg[k], len = seg[k + 1] - s0;
-            for (u32 p = blockIdx.x * NT + tid; p < len; p += G * NT) R[s0 + p].pad = i + 1;
+            for (u32 p = FL_B * NT + tid; p < len; p += G * NT) R[s0 + p].pad = i + 1;
         }
         fl_grid_sync(g, G, gen, F);
         if (fl_stalled(g)) return false;
@@ -1699,9 +1752,9 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
     WalkStats ws;
     const u64 w0 = fl_now();
     bool heavy_walker = false, light_wave = true;
-    u32 lw = blockIdx.x * (NT / 64) + wave, LW = G * (NT / 64);
+    u32 lw = FL_B * (NT / 64) + wave, LW = G * (NT / 64);
     if (merged) {
-        if (blockIdx.x == 0) {
+        if (FL_B == 0) {
             // The walker (wave 0) and its feeder (wave 1); the ring lives in the planner's LDS.
             if (tid == 0) {
                 s_ctl[0] = 0;
@@ -1712,14 +1765,14 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
             fl_walk_merged(F, g, H, NHU, ws, s_ctl, s_ring);
             if (heavy_walker && lane == 0) atomicAdd((unsigned long long*)&g->walk[2], (unsigned long long)NHU);
         }
-        light_wave = G >= 2 ? blockIdx.x >= 1 : wave >= 2;  // (waves 0, 1 of workgroup 0: the walker, its feeder)
-        lw = G >= 2 ? (blockIdx.x - 1) * (NT / 64) + wave : wave - 2;
+        light_wave = G >= 2 ? FL_B >= 1 : wave >= 2;  // (waves 0, 1 of workgroup 0: the walker, its feeder)
+        lw = G >= 2 ? (FL_B - 1) * (NT / 64) + wave : wave - 2;
         LW = G >= 2 ? (G - 1) * (NT / 64) : NT / 64 - 2;
     } else if (split) {
         u32 len = 0;
-        if (blockIdx.x < NH && wave == 0) {
+        if (FL_B < NH && wave == 0) {
             heavy_walker = true;
-            const u32 k = hv[blockIdx.x];
+            const u32 k = hv[FL_B];
             const u32 s0 = seg[k];
             len = seg[k + 1] - s0;
             fl_walk_heavy(F, g, R, s0, len, ws);
@@ -1741,8 +1794,8 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
                 }
             }
         }
-        light_wave = blockIdx.x >= NH;
-        lw = (blockIdx.x - NH) * (NT / 64) + wave;
+        light_wave = FL_B >= NH;
+        lw = (FL_B - NH) * (NT / 64) + wave;
         LW = (G - NH) * (NT / 64);
     }
     if (light_wave) {
@@ -1790,7 +1843,7 @@ __device__ static inline bool fl_walk(const PassArgs& P, const FlowArgs& F, u32 
         atomicAdd((unsigned long long*)&g->walk[5], (unsigned long long)ws.blocks);
         atomicAdd((unsigned long long*)&g->walk[6], (unsigned long long)ws.block_ticks);
 
-        if (blockIdx.x == 0) {
+        if (FL_B == 0) {
             atomicAdd((unsigned long long*)&g->sweep_ticks[1], (unsigned long long)ws.loop_ticks);
             atomicAdd((unsigned long long*)&g->sweep_ticks[2], (unsigned long long)(t - ws.loop_ticks));
         }
@@ -1803,10 +1856,10 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
                                        u64 (*s_wv)[4], u32* s_wf, u32* s_cnt, u32* s_hk, u64* s_hx) {
     Globals* g = P.T.g;
     const Tables& T = P.T;
-    const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid;
+    const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = FL_G;
     const u32 lane = tid & 63, wave = tid >> 6;
     const u32* K = F.keys[0];
-    const u64 t_all = (blockIdx.x == 0 && tid == 0) ? fl_now() : 0;
+    const u64 t_all = (FL_B == 0 && tid == 0) ? fl_now() : 0;
 
     // Every balance, amount and sum below 2^63 (bound + S, the certificate's own numbers): the
     // signed slack form; below 2^62: the per-account walkers (fl_walk), whose "always" / "never"
@@ -1820,13 +1873,13 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
     const bool walk = F.walk && slack && (tb_lo(bs) >> 62) == 0;
 
     // 1a. Units: no legs yet.
-    for (u32 f = blockIdx.x * NT + tid; f < ndep; f += G * NT) {
+    for (u32 f = FL_B * NT + tid; f < ndep; f += G * NT) {
         F.b_qd[f] = FLOW_SENT;
         F.b_qc[f] = FLOW_SENT;
     }
     // 1b. The record scan (statuses are fixed from here to the sweep).
     const u32 tile = ((NA + G - 1) / G + NT - 1) / NT * NT;
-    const u32 t0 = min(NA, blockIdx.x * tile), t1 = min(NA, t0 + tile);
+    const u32 t0 = min(NA, FL_B * tile), t1 = min(NA, t0 + tile);
     u64 carry[4] = {0, 0, 0, 0};
     u32 any_start = 0;
     for (u32 c0 = t0; c0 < t1; c0 += NT) {
@@ -1838,14 +1891,14 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
         fl_seg_scan4(v, f, carry, s_wv, s_wf);
     }
     if (tid == 0) {
-        F.b_blk[5 * blockIdx.x] = any_start;
+        F.b_blk[5 * FL_B] = any_start;
 #pragma unroll
-        for (u32 k = 0; k < 4; k++) F.b_blk[5 * blockIdx.x + 1 + k] = carry[k];
+        for (u32 k = 0; k < 4; k++) F.b_blk[5 * FL_B + 1 + k] = carry[k];
     }
     fl_grid_sync(g, G, gen, F);
     if (fl_stalled(g)) return false;
     u64 cin[4] = {0, 0, 0, 0};
-    for (int b = (int)blockIdx.x - 1; b >= 0; b--) {
+    for (int b = (int)FL_B - 1; b >= 0; b--) {
 #pragma unroll
         for (u32 k = 0; k < 4; k++) cin[k] += F.b_blk[5 * b + 1 + k];
         if (F.b_blk[5 * b]) break;
@@ -1884,25 +1937,25 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
         fl_grid_sync(g, G, gen, F);
         if (fl_stalled(g)) return false;
         const bool done = fl_walk(P, F, ndep, NA, gen, s_wf, s_hk, (HotRec*)s_hx);
-        if (blockIdx.x == 0 && tid == 0)
+        if (FL_B == 0 && tid == 0)
             atomicAdd((unsigned long long*)&g->sweep_ticks[0], (unsigned long long)(fl_now() - t_all));
         return done;
     }
     // 1c. The undecided units in event order: per workgroup tile of units its count, then its offset.
     const u32 ut = ((ndep + G - 1) / G + NT - 1) / NT * NT;
-    const u32 u0 = min(ndep, blockIdx.x * ut), u1 = min(ndep, u0 + ut);
+    const u32 u0 = min(ndep, FL_B * ut), u1 = min(ndep, u0 + ut);
     u32 cnt = 0;
     for (u32 c0 = u0; c0 < u1; c0 += NT) {
         const u32 f = c0 + tid;
         cnt += __syncthreads_count(f < u1 && F.f_len[f] && F.b_st[f] == BS_UNK);
     }
-    if (tid == 0) F.b_blk[5 * blockIdx.x] = cnt;
+    if (tid == 0) F.b_blk[5 * FL_B] = cnt;
     fl_grid_sync(g, G, gen, F);
     if (fl_stalled(g)) return false;
     u32 off = 0, nu = 0;
     for (u32 b = 0; b < G; b++) {
         const u32 c = (u32)F.b_blk[5 * b];
-        off += b < blockIdx.x ? c : 0;
+        off += b < FL_B ? c : 0;
         nu += c;
     }
     for (u32 c0 = u0; c0 < u1; c0 += NT) {
@@ -1950,7 +2003,7 @@ __device__ static inline bool fl_sweep(const PassArgs& P, const FlowArgs& F, u32
     // swept ok units of earlier windows (b_ex); the window is resolved in lane order, each ok unit
     // adding its legs to the later lanes that share an account (branch-free: one wave, so every
     // instruction's latency is on the critical path).
-    if (blockIdx.x == 0 && wave == 0) {
+    if (FL_B == 0 && wave == 0) {
         SweepRec nx = {};
         if (lane < nu) nx = F.b_rec[lane];
         for (u32 k = lane; k < SW_CAP; k += 64) {
@@ -2132,7 +2185,7 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
                                         u64* s_hx) {
     Globals* g = P.T.g;
     const Tables& T = P.T;
-    const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid;
+    const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = FL_G;
     const u32* K = F.keys[0];
     if (!cert64 || F.bounds_rounds_max == 0) return false;
     // Account positions are the prefix of the sorted list (keys < 2^31).
@@ -2144,7 +2197,7 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
     const u32 NA = lo;
 
     // S1: units — eligibility, static failures, no check yet.
-    for (u32 f = blockIdx.x * NT + tid; f < ndep; f += G * NT) {
+    for (u32 f = FL_B * NT + tid; f < ndep; f += G * NT) {
         if (!F.f_len[f]) continue;
         const u32 pe = F.f_pe[f];
         const u32 info = P.info[pe];
@@ -2166,12 +2219,12 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
     fl_grid_sync(g, G, gen, F);
     if (fl_stalled(g)) return false;
     if (*(volatile u32*)&F.words[FW_BNO]) {
-        if (blockIdx.x == 0 && tid == 0) atomicAdd((unsigned long long*)&g->bounds_skipped, 1ULL);
+        if (FL_B == 0 && tid == 0) atomicAdd((unsigned long long*)&g->bounds_skipped, 1ULL);
         return false;
     }
 
     // S2: positions — the leg each holds, and which checks are open.
-    for (u32 q = blockIdx.x * NT + tid; q < NA; q += G * NT) {
+    for (u32 q = FL_B * NT + tid; q < NA; q += G * NT) {
         const RunEntry x = F.run[q];
         const u32 r = K[q];
         const u16 rf = T.acct_hot[r].flags;
@@ -2189,7 +2242,7 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
     fl_grid_sync(g, G, gen, F);
     if (fl_stalled(g)) return false;
     // S3: units with no open check (a credit to a debits-limited account, ...) are ok.
-    for (u32 f = blockIdx.x * NT + tid; f < ndep; f += G * NT) {
+    for (u32 f = FL_B * NT + tid; f < ndep; f += G * NT) {
         if (F.f_len[f] && F.b_st[f] == BS_UNK && F.b_vd[f] == BV_PASS && F.b_vc[f] == BV_PASS) {
             F.b_st[f] = BS_OK;
             atomicSub(&F.words[FW_BUND], 1u);
@@ -2200,12 +2253,12 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
 
     fl_mark(g, tp, FP_BSETUP);
     const u32 tile = ((NA + G - 1) / G + NT - 1) / NT * NT;
-    const u32 t0 = min(NA, blockIdx.x * tile), t1 = min(NA, t0 + tile);
+    const u32 t0 = min(NA, FL_B * tile), t1 = min(NA, t0 + tile);
     bool converged = *(volatile u32*)&F.words[FW_BUND] == 0;
     u32 rounds = 0;
     for (; !converged && rounds < F.bounds_rounds_max; rounds++) {
         u32* dec = &F.words[FW_BDEC + rounds % 3];
-        if (blockIdx.x == 0 && tid == 0) F.words[FW_BDEC + (rounds + 1) % 3] = 0;
+        if (FL_B == 0 && tid == 0) F.words[FW_BDEC + (rounds + 1) % 3] = 0;
         // Phase A: this tile's aggregate (sums since its last segment start; start flag).
         u64 carry[4] = {0, 0, 0, 0};
         u32 any_start = 0;
@@ -2221,15 +2274,15 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
             fl_seg_scan4(v, f, carry, s_wv, s_wf);
         }
         if (tid == 0) {
-            F.b_blk[5 * blockIdx.x] = any_start;
+            F.b_blk[5 * FL_B] = any_start;
 #pragma unroll
-            for (u32 k = 0; k < 4; k++) F.b_blk[5 * blockIdx.x + 1 + k] = carry[k];
+            for (u32 k = 0; k < 4; k++) F.b_blk[5 * FL_B + 1 + k] = carry[k];
         }
         fl_grid_sync(g, G, gen, F);
         if (fl_stalled(g)) return false;
         // Phase B: carry-in from the preceding tiles, then the scan again with the decisions.
         u64 cin[4] = {0, 0, 0, 0};
-        for (int b = (int)blockIdx.x - 1; b >= 0; b--) {
+        for (int b = (int)FL_B - 1; b >= 0; b--) {
 #pragma unroll
             for (u32 k = 0; k < 4; k++) cin[k] += F.b_blk[5 * b + 1 + k];
             if (F.b_blk[5 * b]) break;
@@ -2301,7 +2354,7 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
         fl_mark(g, tp, FP_SWEEP);
     }
     if (!converged) {
-        if (blockIdx.x == 0 && tid == 0) {
+        if (FL_B == 0 && tid == 0) {
             atomicAdd((unsigned long long*)&g->bounds_abandoned, 1ULL);
             atomicAdd((unsigned long long*)&g->bounds_rounds, (unsigned long long)rounds);
         }
@@ -2315,7 +2368,7 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
     // serialise in L2, so the lanes sharing the first lane's word add their sum once (fl_add_lo).
     u32 n_ok = 0;
     u64 tsm = 0;
-    for (u32 f0 = blockIdx.x * NT; f0 < ndep; f0 += G * NT) {  // whole waves iterate together
+    for (u32 f0 = FL_B * NT; f0 < ndep; f0 += G * NT) {  // whole waves iterate together
         const u32 f = f0 + tid;
         bool ok = false;
         u32 pe = 0;
@@ -2350,7 +2403,7 @@ __device__ static inline bool fl_bounds(const PassArgs& P, const FlowArgs& F, u3
     for (int off = 32; off > 0; off >>= 1) nw += __shfl_xor((unsigned long long)nw, off);
     if ((tid & 63) == 0 && nw) atomicAdd((unsigned long long*)&g->transfer_count, (unsigned long long)nw);
     tsmax = max(tsmax, tsm);
-    if (blockIdx.x == 0 && tid == 0) {
+    if (FL_B == 0 && tid == 0) {
         atomicAdd((unsigned long long*)&g->bounds_passes, 1ULL);
         atomicAdd((unsigned long long*)&g->bounds_units, (unsigned long long)ndep);
         atomicAdd((unsigned long long*)&g->bounds_rounds, (unsigned long long)rounds);
@@ -2393,21 +2446,23 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     __shared__ u64 s_tsmax[FLOW_THREADS / 64];
 
     Globals* g = P.T.g;
-    const u32 NT = FLOW_THREADS, tid = threadIdx.x, G = F.grid;
+    const u32 NT = FLOW_THREADS, tid = threadIdx.x;
     const u32 nb = P.b1 - P.b0;
     // tb_apply_events' work first, when this launch replaces it (one launch a pass fewer): the
     // independent ok transfers that are not legs touch no constrained account, id or pending transfer
     // a dependent unit reads, so their balance adds commute with everything below.
     if (P.late_in_flow) tb_apply_late(P);
     if (__hip_atomic_load(&g->dependent_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        if (blockIdx.x == 0) fl_finish(P, s_code, s_wave, s_list, 0, false);
+        if (blockIdx.x == 0) fl_finish(P, s_code, s_wave, s_list, 0, false);  // (before any admission)
         return;
     }
+    if (!fl_admit(g, F)) return;  // started after admission closed: the admitted workgroups cover the pass
+    const u32 G = FL_G;
     u128 S;
     bool cert_global, cert64;
     tb_pass_cert(P, S, cert_global, cert64);
     u32 gen = 0;
-    const u64 ft0 = (blockIdx.x == 0 && tid == 0) ? fl_now() : 0;
+    const u64 ft0 = (FL_B == 0 && tid == 0) ? fl_now() : 0;
     u64 tp = ft0;
 
     // ---- plan 1: flat list of dependent events, units, resource pairs ------------------------
@@ -2419,7 +2474,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     // slots per event in keys[1] / vals[1] first, and are compacted (in order) into keys[0] /
     // vals[0] below, so the sort sees only real pairs (C4: ~1.3 of the 6 slots per event).
     const u32 ftile = ((ndep + G - 1) / G + NT - 1) / NT * NT;
-    const u32 fa = min(ndep, blockIdx.x * ftile), fb = min(ndep, fa + ftile);
+    const u32 fa = min(ndep, FL_B * ftile), fb = min(ndep, fa + ftile);
     u32 my_pairs = 0;
     for (u32 c0 = fa; c0 < fb; c0 += NT) {
         const u32 f = c0 + tid;
@@ -2482,7 +2537,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     {
         u32 total;
         (void)fl_block_excl(my_pairs, s_wave, total);
-        if (tid == 0) F.b_blk[blockIdx.x] = total;
+        if (tid == 0) F.b_blk[FL_B] = total;
     }
     fl_grid_sync(g, G, gen, F);
     if (fl_stalled(g)) return;
@@ -2491,7 +2546,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     u32 N = 0, base = 0;
     for (u32 w = 0; w < G; w++) {
         const u32 c = (u32)F.b_blk[w];
-        base += w < blockIdx.x ? c : 0;
+        base += w < FL_B ? c : 0;
         N += c;
     }
     if (!sequential) {
@@ -2527,7 +2582,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     if (!sequential) {
         // ---- plan 2: stable LSD radix sort of the pairs by key (4 x 8 bits) ---------------------
         const u32 tile = ((N + G - 1) / G + NT - 1) / NT * NT;
-        const u32 t0 = min(N, blockIdx.x * tile), t1 = min(N, t0 + tile);
+        const u32 t0 = min(N, FL_B * tile), t1 = min(N, t0 + tile);
         const u32 lane = tid & 63, wave = tid >> 6;
         for (u32 pass = 0; pass < 4; pass++) {
             const u32 shift = 8 * pass;
@@ -2539,7 +2594,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
             __syncthreads();
             for (u32 q = t0 + tid; q < t1; q += NT) atomicAdd(&s_hist[(sk[q] >> shift) & 255], 1u);
             __syncthreads();
-            if (tid < 256) F.hist[blockIdx.x * 256 + tid] = s_hist[tid];
+            if (tid < 256) F.hist[FL_B * 256 + tid] = s_hist[tid];
             fl_grid_sync(g, G, gen, F);
             if (fl_stalled(g)) return;
             // Digit totals over the grid and the counts of the workgroups before this one: every
@@ -2556,7 +2611,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
 #pragma unroll
                     for (u32 k = 0; k < 8; k++) {
                         tot += c[k];
-                        before += w + k < blockIdx.x ? c[k] : 0;
+                        before += w + k < FL_B ? c[k] : 0;
                     }
                 }
                 s_wcnt[qt][d] = tot;
@@ -2621,7 +2676,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
         // ---- plan 3: link each unit to its successor on every resource --------------------------
         const u32* K = F.keys[0];
         const u32* V = F.vals[0];
-        for (u32 q = blockIdx.x * NT + tid; q < N; q += G * NT) {
+        for (u32 q = FL_B * NT + tid; q < N; q += G * NT) {
             const u32 key = K[q];
             if (key == FLOW_SENT) continue;
             const bool first = q == 0 || K[q - 1] != key;
@@ -2662,14 +2717,14 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
         }
         fl_grid_sync(g, G, gen, F);
         if (fl_stalled(g)) return;
-        for (u32 f = blockIdx.x * NT + tid; f < ndep; f += G * NT) {
+        for (u32 f = FL_B * NT + tid; f < ndep; f += G * NT) {
             if (F.f_len[f] && F.need[f] == 0) {
                 const u32 pos = atomicAdd(&F.words[FW_QTAIL], 1u);
                 F.queue[pos] = f + 1;
             }
         }
         // Pack the run walker's view of every account-resource position (unit flags are final now).
-        for (u32 q = blockIdx.x * NT + tid; q < N; q += G * NT) {
+        for (u32 q = FL_B * NT + tid; q < N; q += G * NT) {
             const u32 key = K[q];
             if (key == FLOW_SENT || (key & 0x80000000u)) continue;
             const u32 u = V[q];
@@ -2693,7 +2748,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
         fl_grid_sync(g, G, gen, F);
         if (fl_stalled(g)) return;
     }
-    const u64 ft1 = (blockIdx.x == 0 && tid == 0) ? fl_now() : 0;
+    const u64 ft1 = (FL_B == 0 && tid == 0) ? fl_now() : 0;
     fl_mark(g, tp, FP_LINK);
     if (!sequential) {
         __shared__ u64 s_bwv[FLOW_THREADS / 64][4];
@@ -2706,14 +2761,14 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
             // workgroups' writes.
             if (tsb) atomicMax((unsigned long long*)&g->commit_timestamp, (unsigned long long)tsb);
             fl_grid_sync(g, G, gen, F);
-            if (blockIdx.x == 0 && tid == 0) {
+            if (FL_B == 0 && tid == 0) {
                 const u64 ft2 = fl_now();
                 atomicAdd((unsigned long long*)&g->flow_plan_ticks, (unsigned long long)(ft1 - ft0));
                 atomicAdd((unsigned long long*)&g->flow_run_ticks, (unsigned long long)(ft2 - ft1));
                 atomicAdd(&g->flow_passes, 1u);
             }
             fl_mark(g, tp, FP_RUN);
-            fl_finish(P, s_code, s_wave, s_list, 0, true, blockIdx.x, G, blockIdx.x == 0);
+            fl_finish(P, s_code, s_wave, s_list, 0, true, FL_B, G, FL_B == 0);
             fl_mark(g, tp, FP_REPLIES);  // workgroup 0's share
             return;
         }
@@ -2724,7 +2779,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     // ---- run --------------------------------------------------------------------------------------
     u64 tsmax = 0;
     if (sequential) {
-        if (blockIdx.x != 0) return;
+        if (FL_B != 0) return;
         Replay R;
         R.T = P.T;
         R.undo = seq_undo;
@@ -2850,7 +2905,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
             atomicAdd((unsigned long long*)&g->flow_runs, (unsigned long long)runs);
             atomicAdd((unsigned long long*)&g->flow_run_units, (unsigned long long)run_units);
         }
-        if (blockIdx.x == 0 && tid == 0) {
+        if (FL_B == 0 && tid == 0) {
             atomicAdd(&g->flow_passes, 1u);
             atomicAdd((unsigned long long*)&g->flow_units, (unsigned long long)nunits);
         }
@@ -2871,7 +2926,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     __syncthreads();
     u64 mm = 0;
     for (u32 k = 0; k < NT / 64; k++) mm = max(mm, s_tsmax[k]);
-    if (blockIdx.x == 0 && tid == 0) {
+    if (FL_B == 0 && tid == 0) {
         const u64 ft2 = fl_now();
         atomicAdd((unsigned long long*)&g->flow_plan_ticks, (unsigned long long)(ft1 - ft0));
         atomicAdd((unsigned long long*)&g->flow_run_ticks, (unsigned long long)(ft2 - ft1));
@@ -2880,6 +2935,6 @@ __global__ __launch_bounds__(FLOW_THREADS) void tb_flow(PassArgs P, FlowArgs F, 
     // 0 alone after the sequential one (the others have left).
     const u32 parts = sequential ? 1u : G;
     fl_mark(g, tp, FP_RUN);
-    fl_finish(P, s_code, s_wave, s_list, mm, true, blockIdx.x, parts, blockIdx.x == 0);
+    fl_finish(P, s_code, s_wave, s_list, mm, true, FL_B, parts, FL_B == 0);
     fl_mark(g, tp, FP_REPLIES);  // workgroup 0's share
 }

@@ -528,7 +528,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void tb_resolve(PassArgs P) {
     __syncthreads();
     if (threadIdx.x == 0) {
         if (blockIdx.x == 0) {  // the replay kernel's per-pass counters (k_flow.h), after every load
-            for (u32 k = 0; k < FL_BAR_GROUPS + 2; k++) T.g->flow_bar[FL_BAR_STRIDE * k] = 0;
+            for (u32 k = 0; k < FL_BAR_WORDS; k++) T.g->flow_bar[FL_BAR_STRIDE * k] = 0;
             if (P.flow_words) for (u32 k = 0; k < FLOW_WORDS; k++) P.flow_words[k] = 0;
         }
         u64 mm = 0;
@@ -679,7 +679,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) __attribute__((amdgpu_waves_per_eu
     __syncthreads();
     if (threadIdx.x == 0) {
         if (blockIdx.x == 0) {  // the replay kernel's per-pass counters (k_flow.h), after every load
-            for (u32 k = 0; k < FL_BAR_GROUPS + 2; k++) T.g->flow_bar[FL_BAR_STRIDE * k] = 0;
+            for (u32 k = 0; k < FL_BAR_WORDS; k++) T.g->flow_bar[FL_BAR_STRIDE * k] = 0;
             if (P.flow_words) for (u32 k = 0; k < FLOW_WORDS; k++) P.flow_words[k] = 0;
         }
         u64 mm = 0;

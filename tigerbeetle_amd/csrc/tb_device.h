@@ -186,6 +186,7 @@ __device__ static inline u128 tb_sat_add(u128 a, u128 b) {
 #define FL_BAR_GROUPS 8
 #endif
 #define FL_BAR_STRIDE 32  // u32 words: one 128-B line per counter
+#define FL_BAR_WORDS (FL_BAR_GROUPS + 4)
 struct Globals {
     u64 commit_timestamp;     // max timestamp of an event that returned ok when evaluated
     u64 panic;                // PANIC_* bits
@@ -220,8 +221,9 @@ struct Globals {
     u64 sweep_u64_passes;     // sweeps that ran in the u64 X/Y form (bound + S >= 2^63)
     u64 bounds_abandoned;     // passes whose bounds did not converge in FLOW_BOUNDS_ROUNDS_MAX rounds
     // tb_flow's two-level grid barrier (k_flow.h fl_grid_sync): FL_BAR_GROUPS group counters, the
-    // root counter, the published generation; one 128-B line each.  Zeroed by tb_resolve every pass.
-    u32 flow_bar[FL_BAR_STRIDE * (FL_BAR_GROUPS + 2)];
+    // root counter, the published generation; then its admission (fl_admit): the entry counter and
+    // the admitted grid.  One 128-B line each.  Zeroed by tb_resolve every pass.
+    u32 flow_bar[FL_BAR_STRIDE * FL_BAR_WORDS];
 };
 
 struct AccountHot {

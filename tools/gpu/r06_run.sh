@@ -101,6 +101,18 @@ for what in "$@"; do
           python -c "import json;d=json.loads(open('$O/nodelib_${v}_$pb.json').read().strip().splitlines()[-1]);print('nodelib $v $pb',round(d['value']/1e6,1),'M/s',d['ms_per_step'],'ms')"
         done
       done ;;
+    flowab)  # same box: the C3 / C3h / C4 lines (host 10M + device-resident 100M) with library builds in turn
+      for v in ${FLOWAB_VARIANTS:-preadm cur preadm cur}; do
+        lib=""; [ "$v" != cur ] && lib="$R/tigerbeetle_amd/libtbgpu_$v.so"
+        TBGPU_AB_LIB=$lib timeout -k 10 600 python -u bench.py --steps 1 --warmup 1 --host-prepares 0 --replica-prepares 0 \
+          --write-back 0 --cpu-sample 0 --host-steps 0 --access-mix 0 --staged-steps 0 > $O/flowab_$v.json 2> $O/flowab_$v.err
+        rc=$?; [ $rc -ne 0 ] && { echo "flowab $v rc=$rc"; tail -5 $O/flowab_$v.err; exit $rc; }
+        python3 -c "
+import json,sys
+d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print('flowab', sys.argv[2], ' '.join('%s %.1f/%.1f' % (k, v['value']/1e6, v['device_resident']['value']/1e6) for k, v in d['secondary'].items()))
+" $O/flowab_$v.json $v
+      done ;;
     wbab)  # write-back copy-out A/B on one box: counts-sized vs bound-sized, read through vs staged bodies
       for v in ${WBAB_VARIANTS:-base bound stage both}; do
         case $v in
