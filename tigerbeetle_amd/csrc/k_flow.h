@@ -45,8 +45,8 @@
 #define FLOW_SENT 0xFFFFFFFFu   // empty pair slot
 // This workgroup's index among the admitted ones, and their number (fl_admit); ~0: not admitted.
 __shared__ u32 s_fl_b, s_fl_g;
-#define FL_B s_fl_b
-#define FL_G s_fl_g
+#define FL_B ((u32)__builtin_amdgcn_readfirstlane(s_fl_b))  // uniform: a scalar register, as blockIdx.x was
+#define FL_G ((u32)__builtin_amdgcn_readfirstlane(s_fl_g))
 #define FL_ADM_CLOSED 0x80000000u
 #define FL_ADMIT_TICKS 5000  // wall-clock ticks (50 us at 100 MHz) the first workgroup waits for the others
 
