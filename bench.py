@@ -559,7 +559,7 @@ def cpu_model():
     return "nproc %d" % os.cpu_count()
 
 
-# The rocprofv3 evidence behind `roofline.traffic` (tools/gpu/r04_prof.sh -> tools/perf_pmc.py): per
+# The rocprofv3 evidence behind `roofline.traffic` (tools/gpu/archive/r04_prof.sh -> tools/perf_pmc.py): per
 # kernel, HBM bytes per committed transfer from FETCH_SIZE / WRITE_SIZE passes and rocprof's mean
 # launch time, for the headline leg (64-prepare chunks from host memory) and for device-resident
 # passes.  It lives outside profiles/ so it travels to the GPU box with the tree.
