@@ -1476,6 +1476,8 @@ extern "C" int tbgpu_commit(tbgpu_t* E, uint8_t operation, uint64_t timestamp, c
 // left to stage is the prepare body itself — a pageable create body starts its copy to HBM now, on
 // the copy stream, and the commit of the same body only waits for it.  A registered body (the
 // message pool) is not staged: the commit reads it through (below).  Anything else needs nothing.
+static bool wb_copy_in_flight(tbgpu* E);  // (below)
+
 extern "C" int tbgpu_prefetch(tbgpu_t* E, uint8_t operation, const void* input, uint32_t input_len) {
     if (E->node) return TBGPU_STATUS_OK;
     HIPCK(hipSetDevice(E->device));
@@ -1497,7 +1499,11 @@ extern "C" int tbgpu_prefetch(tbgpu_t* E, uint8_t operation, const void* input, 
     // both directions at ~50 GB/s each, tools/microbench_h2d `duplex`), the commit reads HBM, and the
     // copy-out needs not wait for the commit's PCIe reads (wb_pump).
     // (Not for a write-back every op: the body's DMA then only lengthens each serial prepare.)
-    if (registered && !(E->wb_stage && E->wb.copying && E->wb.calls_prev >= 2)) return TBGPU_STATUS_OK;
+    // (A bound-sized copy-out is issued whole at its write-back: staged while it crosses.  A counts-
+    // sized one, a slice per commit: while slices are still to be sent — measured: staging every
+    // body of a bar while its copy-out crosses cost one bar behind 97 -> 86 M/s.)
+    const bool stage = E->wb.bound ? wb_copy_in_flight(E) : E->wb.copying;
+    if (registered && !(E->wb_stage && E->wb.calls_prev >= 2 && stage)) return TBGPU_STATUS_OK;
     // The staging slot's previous reader (the last commit) has finished: commits are synchronous.
     HIPCK(hipMemcpyAsync(E->pf_staging, input, input_len, hipMemcpyHostToDevice, E->copy_stream));
     HIPCK(hipEventRecord(E->pf_done, E->copy_stream));
@@ -1937,6 +1943,7 @@ static int wb_wait(tbgpu* E, tbgpu_delta_counts* counts) {
 }
 
 static void wb_set_slice(tbgpu* E, u64 total);  // the copy-out's slice (below)
+static int wb_tail(tbgpu* E, hipEvent_t after);  // the gather beside the commits (below)
 
 static int wb_checkpoint_sync(tbgpu* E, u8* accounts_out, u8* before_out, u64 accounts_cap, u8* transfers_out,
                               u64 transfers_cap, u64* posted_out, u64 posted_cap, tbgpu_delta_counts* counts) {
@@ -2110,9 +2117,22 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
         for (u32 r = 0; r < 4; r++) W.at[r] = 0;
         wb_set_slice(E, W.len[0] + W.len[1] + W.len[2]);
         W.counts_known = true;
+        W.inflight = true;
+        // The gather and the whole copy-out now, on the write-back stream: the sizes need no counts,
+        // and a replica writing back every few ops stages its next bodies while the copy-out is in
+        // flight (tbgpu_prefetch), so its commits read nothing over the link the copy-out fills.
+        st = wb_tail(E, nullptr);
+        if (!st) st = wb_pump(E, ~0ULL, nullptr);
+        return st;
     }
     W.inflight = true;
     return TBGPU_STATUS_OK;
+}
+
+// A write-back's copy-out still issuing or still crossing the link.
+static bool wb_copy_in_flight(tbgpu* E) {
+    const WbBufs& W = E->wb;
+    return W.inflight && (W.copying || hipEventQuery(W.done) == hipErrorNotReady);
 }
 
 // The copy-out of an asynchronous write-back, a slice at a time (up to `budget` bytes; ~0: all of

@@ -113,6 +113,18 @@ d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 print('flowab', sys.argv[2], ' '.join('%s %.1f/%.1f' % (k, v['value']/1e6, v['device_resident']['value']/1e6) for k, v in d['secondary'].items()))
 " $O/flowab_$v.json $v
       done ;;
+    wblib)  # same box: the replica's write-back shapes with library builds in turn (WBLIB_VARIANTS: cur, or a
+      # directory tigerbeetle_amd/<name>/ holding a libtbgpu.so the bench's RUNPATH is overridden to)
+      for v in ${WBLIB_VARIANTS:-ab_wbprev cur ab_wbprev cur}; do
+        ld=""; [ "$v" != cur ] && ld="$R/tigerbeetle_amd/$v"
+        for m in "--write-back-every 4" "--write-back-every 8" --write-back; do
+          f="$O/wblib_${v}_$(echo $m | tr -d ' -')"
+          LD_LIBRARY_PATH=$ld timeout -k 10 300 tigerbeetle_amd/host/tb_replica_bench --accounts 1000000 --prepares 2000 \
+            --device 0 $m --stage > "$f.json" 2> "$f.err"
+          rc=$?; [ $rc -ne 0 ] && { echo "wblib $v $m rc=$rc"; tail -3 "$f.err"; exit $rc; }
+          python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print('wblib',sys.argv[2],sys.argv[3],round(d['transfers_per_s']/1e6,1),'M/s p99',d['p99_ms'])" "$f.json" "$v" "$m"
+        done
+      done ;;
     wbab)  # write-back copy-out A/B on one box: counts-sized vs bound-sized, read through vs staged bodies
       for v in ${WBAB_VARIANTS:-base bound stage both}; do
         case $v in
