@@ -1784,12 +1784,16 @@ static WbBounds wb_bounds(tbgpu* E, u64 live_accounts) {
 // Slice [a, b) of the log range: gather its new transfers (records, their account ids, their post /
 // void records and posted pairs) into the write-back buffers and look their accounts up.  Enqueued
 // only; the slice's counts land in d_cnt (records, post / void records, accounts emitted).
-static int wb_gather_slice(tbgpu* E, u64 a, u64 b, bool want_records, bool posted = true, hipStream_t stream = nullptr) {
+// zero_counts = false: the caller zeroed them in stream order already (the asynchronous write-back).
+static int wb_gather_slice(tbgpu* E, u64 a, u64 b, bool want_records, bool posted = true, hipStream_t stream = nullptr,
+                           bool zero_counts = true) {
     WbBufs& W = E->wb;
     if (!stream) stream = E->stream;
     const u64 n = b - a, nblocks = (n + DELTA_THREADS - 1) / DELTA_THREADS;
-    HIPCK(hipMemsetAsync(W.d_cnt + WB_ACCOUNTS, 0, 8, stream));
-    HIPCK(hipMemsetAsync(W.d_cnt + WB_PV, 0, 16, stream));  // WB_PV, WB_RECORDS
+    if (zero_counts) {
+        HIPCK(hipMemsetAsync(W.d_cnt + WB_ACCOUNTS, 0, 8, stream));
+        HIPCK(hipMemsetAsync(W.d_cnt + WB_PV, 0, 16, stream));  // WB_PV, WB_RECORDS
+    }
     if (!n) return TBGPU_STATUS_OK;
     hipLaunchKernelGGL(tb_delta_log_count, dim3((unsigned)nblocks), dim3(DELTA_THREADS), 0, stream, E->T, a, n, E->ckpt_ts,
                        W.d_bc);
@@ -1943,7 +1947,7 @@ static int wb_wait(tbgpu* E, tbgpu_delta_counts* counts) {
 }
 
 static void wb_set_slice(tbgpu* E, u64 total);  // the copy-out's slice (below)
-static int wb_tail(tbgpu* E, hipEvent_t after);  // the gather beside the commits (below)
+static int wb_tail(tbgpu* E, hipEvent_t after, bool counts);  // the gather beside the commits (below)
 
 static int wb_checkpoint_sync(tbgpu* E, u8* accounts_out, u8* before_out, u64 accounts_cap, u8* transfers_out,
                               u64 transfers_cap, u64* posted_out, u64 posted_cap, tbgpu_delta_counts* counts) {
@@ -2121,9 +2125,12 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
         // The gather and the whole copy-out now, on the write-back stream: the sizes need no counts,
         // and a replica writing back every few ops stages its next bodies while the copy-out is in
         // flight (tbgpu_prefetch), so its commits read nothing over the link the copy-out fills.
-        st = wb_tail(E, nullptr);
+        st = wb_tail(E, nullptr, false);
         if (!st) st = wb_pump(E, ~0ULL, nullptr);
-        return st;
+        if (st) return st;
+        HIPCK(hipMemcpyAsync(W.h_cnt, W.d_cnt, WB_COUNT_WORDS * 8, hipMemcpyDeviceToHost, W.stream));  // for the wait
+        HIPCK(hipEventRecord(W.done, W.stream));
+        return TBGPU_STATUS_OK;
     }
     W.inflight = true;
     return TBGPU_STATUS_OK;
@@ -2156,15 +2163,16 @@ static void wb_set_slice(tbgpu* E, u64 total) {
 }
 // The asynchronous write-back's work beside the commits, after the in-order capture (and `after`):
 // the records of the log range (immutable now), the emission, the snapshot's advance, the order
-// check, the counts back to the host.
-static int wb_tail(tbgpu* E, hipEvent_t after) {
+// check, the counts back to the host (counts = false: the caller copies them after the objects —
+// a bound-sized copy-out needs them only at the wait).
+static int wb_tail(tbgpu* E, hipEvent_t after, bool counts) {
     WbBufs& W = E->wb;
     W.tail = false;
     HIPCK(hipStreamWaitEvent(W.stream, W.captured, 0));
     if (after) HIPCK(hipStreamWaitEvent(W.stream, after, 0));
     const u64 ts = E->ckpt_ts;  // wb_gather_slice reads the previous write-back's timestamp
     E->ckpt_ts = W.tail_ts0;
-    const int st = wb_gather_slice(E, W.tail_pos0, W.tail_pos1, true, true, W.stream);
+    const int st = wb_gather_slice(E, W.tail_pos0, W.tail_pos1, true, true, W.stream, false);  // (zeroed at the call)
     E->ckpt_ts = ts;
     if (st) return st;
     hipLaunchKernelGGL(tb_delta_emit, dim3(1024), dim3(256), 0, W.stream, E->T, ckpt_view(E), W.tail_ts0, W.d_slots, W.d_cap,
@@ -2174,8 +2182,10 @@ static int wb_tail(tbgpu* E, hipEvent_t after) {
     hipLaunchKernelGGL(tb_delta_order, dim3(256), dim3(256), 0, W.stream, W.d_out, W.d_cnt + WB_RECORDS, W.d_pairs,
                        W.d_cnt + WB_PV, W.d_cnt + WB_ORDER);
     HIPCK(hipGetLastError());
-    HIPCK(hipMemcpyAsync(W.h_cnt, W.d_cnt, WB_COUNT_WORDS * 8, hipMemcpyDeviceToHost, W.stream));
-    HIPCK(hipEventRecord(W.gathered, W.stream));
+    if (counts) {
+        HIPCK(hipMemcpyAsync(W.h_cnt, W.d_cnt, WB_COUNT_WORDS * 8, hipMemcpyDeviceToHost, W.stream));
+        HIPCK(hipEventRecord(W.gathered, W.stream));
+    }
     return TBGPU_STATUS_OK;
 }
 
@@ -2183,7 +2193,7 @@ static int wb_pump(tbgpu* E, u64 budget, hipEvent_t after) {
     WbBufs& W = E->wb;
     if (!W.copying) return TBGPU_STATUS_OK;
     if (W.tail) {
-        const int st = wb_tail(E, after);
+        const int st = wb_tail(E, after, true);
         if (st || (budget != ~0ULL && !W.counts_known)) return st;  // its counts come back by the next commit
     }
     if (!W.counts_known) {
