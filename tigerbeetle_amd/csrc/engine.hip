@@ -2121,16 +2121,10 @@ extern "C" int tbgpu_checkpoint_delta_async(tbgpu_t* E, void* accounts_out, void
         for (u32 r = 0; r < 4; r++) W.at[r] = 0;
         wb_set_slice(E, W.len[0] + W.len[1] + W.len[2]);
         W.counts_known = true;
-        W.inflight = true;
-        // The gather and the whole copy-out now, on the write-back stream: the sizes need no counts,
-        // and a replica writing back every few ops stages its next bodies while the copy-out is in
-        // flight (tbgpu_prefetch), so its commits read nothing over the link the copy-out fills.
-        st = wb_tail(E, nullptr, false);
-        if (!st) st = wb_pump(E, ~0ULL, nullptr);
-        if (st) return st;
-        HIPCK(hipMemcpyAsync(W.h_cnt, W.d_cnt, WB_COUNT_WORDS * 8, hipMemcpyDeviceToHost, W.stream));  // for the wait
-        HIPCK(hipEventRecord(W.done, W.stream));
-        return TBGPU_STATUS_OK;
+        // The gather and the whole copy-out are enqueued by the next commit, right after its own
+        // kernels (the host issues them while the device runs that commit): the sizes need no
+        // counts, nothing waits for the commit's reads — a replica writing back every few ops stages
+        // its bodies while the copy-out crosses (tbgpu_prefetch) — and the counts cross last.
     }
     W.inflight = true;
     return TBGPU_STATUS_OK;
@@ -2192,8 +2186,8 @@ static int wb_tail(tbgpu* E, hipEvent_t after, bool counts) {
 static int wb_pump(tbgpu* E, u64 budget, hipEvent_t after) {
     WbBufs& W = E->wb;
     if (!W.copying) return TBGPU_STATUS_OK;
-    if (W.tail) {
-        const int st = wb_tail(E, after, true);
+    if (W.tail) {  // (bound-sized: nothing waits for the commit's reads, the counts go last)
+        const int st = wb_tail(E, W.bound ? nullptr : after, !W.bound);
         if (st || (budget != ~0ULL && !W.counts_known)) return st;  // its counts come back by the next commit
     }
     if (!W.counts_known) {
@@ -2214,8 +2208,8 @@ static int wb_pump(tbgpu* E, u64 budget, hipEvent_t after) {
     }
     // A commit that read no host memory (its body staged in HBM) leaves the link's upstream side to
     // the copy-out: everything goes now.  Otherwise one slice, after the commit's reads.
-    if (budget != ~0ULL) budget = W.staged_reads ? ~0ULL : W.slice;
-    if (after && !W.staged_reads) HIPCK(hipStreamWaitEvent(W.stream, after, 0));
+    if (budget != ~0ULL) budget = W.staged_reads || W.bound ? ~0ULL : W.slice;
+    if (after && !W.staged_reads && !W.bound) HIPCK(hipStreamWaitEvent(W.stream, after, 0));
     for (u32 r = 0; r < 4 && budget; r++) {
         const u64 n = std::min<u64>(budget, W.len[r] - W.at[r]);
         if (!n) continue;
@@ -2226,6 +2220,7 @@ static int wb_pump(tbgpu* E, u64 budget, hipEvent_t after) {
     bool left = false;
     for (u32 r = 0; r < 4; r++) left |= W.at[r] < W.len[r];
     if (!left) {
+        if (W.bound) HIPCK(hipMemcpyAsync(W.h_cnt, W.d_cnt, WB_COUNT_WORDS * 8, hipMemcpyDeviceToHost, W.stream));  // for the wait
         HIPCK(hipEventRecord(W.done, W.stream));
         W.copying = false;
     }
