@@ -331,7 +331,8 @@ typedef struct tbgpu_stats {
     uint64_t node_passes_clean, node_passes_split, node_passes_whole, node_sequenced_events;
     /* HBM bytes of the account table (hot records, balances, cold fields, marks): this engine's; on a
      * node engine the largest shard's, and each shard's in node_shard_account_bytes — the accounts it
-     * owns (1/N of the ledger) plus room for one routed sub-pass's imported records. */
+     * owns (1/N of the ledger) plus an import room for foreign accounts' hot records (the ledger's
+     * accounts, or two per event of a routed sub-pass when that is fewer). */
     uint64_t account_table_bytes;
     uint64_t node_shard_account_bytes[16];
     /* Bounded residency (tbgpu_evict_transfers): transfers evicted so far, transfer-log positions in

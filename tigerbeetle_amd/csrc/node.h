@@ -11,8 +11,10 @@
 // home(id).  create_accounts prepares are committed in order by the sequencer (below) with the
 // existing records they name loaded from their owners, and each new account goes to its owner; a home
 // imports the hot records of the foreign accounts a routed pass names from their owners before it
-// validates, and drops them after (k_node.h tb_node_import).  Per-shard account memory is the owned
-// 1/N of the ledger plus one routed pass's imports.  A create_transfers call is cut into passes: pass p takes up to
+// validates and keeps them for later passes, until an account is inserted on a shard or the room
+// fills (k_node.h tb_node_import, tb_node_import_flush).  Per-shard account memory is the owned 1/N
+// of the ledger plus the import room (the ledger's accounts, or a routed sub-pass's two per event
+// when fewer).  A create_transfers call is cut into passes: pass p takes up to
 // N blocks of `chunk` prepares (block d -> source shard d, in order, so the pass's global order is
 // block-major = prepare order).  Per pass, on every device:
 //   copy stream   H2D of the source block's bodies (registered host memory: DMA)
