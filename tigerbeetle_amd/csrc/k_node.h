@@ -234,11 +234,9 @@ __device__ static inline bool tb_import_one(const Tables& H, const NodeTablesArg
     const u64 mark = (1ULL << 63) | (tb_fingerprint(lo, hi) >> 1);
     u64 pos = tb_hash_id(lo, hi) & H.account_mask;
     u32 slot = TB_NOT_FOUND;
-    // The owner's first probe entry is loaded beside this table's (independent; a lane that finds
-    // the id being imported by another lane wasted one load): one round trip off the chain.
+    // The owner's table is read only when this one lacks the id (an import is needed once per id and
+    // kept: most lookups find the entry of an earlier pass and read nothing of the owner's).
     const Tables& O = N.T[o];
-    const u64 opos = tb_hash_id(lo, hi) & O.account_mask;
-    const AccountHot o0 = O.acct_hot[opos];
     u64 t_first = H.acct_hot[pos].timestamp;
     // The owner's verdict comes before any claim: an id no owner holds never takes a slot (a slot
     // claimed and released would leave a hole in the probe chain of an id imported past it).
@@ -252,7 +250,8 @@ __device__ static inline bool tb_import_one(const Tables& H, const NodeTablesArg
         u64 t = k == 0 ? t_first : *tw;
         if (t == 0) {
             if (!looked) {
-                os = tb_account_find_from(O, lo, hi, opos, o0, &a);
+                const u64 opos = tb_hash_id(lo, hi) & O.account_mask;
+                os = tb_account_find_from(O, lo, hi, opos, O.acct_hot[opos], &a);
                 looked = true;
                 if (os == TB_NOT_FOUND) return false;  // validate finds no entry: account_not_found
             }
