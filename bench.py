@@ -458,7 +458,8 @@ def run_secondary_device(args, kind, device, accts, a_lens, a_ts, t_cursor, orac
         n_val = (stats.get("span_launches") or [0])[0] or stats["launches_validate"]
         per_launch = n / max(1, n_val)
         roof = roofline(stats, expected_unique(n_acct, 2 * per_launch) / per_launch, per_launch,
-                        argparse.Namespace(transfers=n, steps=1), step_ms[0], breakdown, kernel="tb_transfers_validate")
+                        argparse.Namespace(transfers=n, steps=1), step_ms[0], breakdown, kernel="tb_transfers_validate",
+                        in_place=True)
         pass_lat = np.sort(np.array(eng.pass_latencies()))
 
         # Parity: the oracle's sample, in place, from the post-account-creation state.
@@ -903,7 +904,7 @@ def main():
     # The ordered fallback (tb_flow) has no byte roofline (its dependency rounds bound it): the
     # roofline is the validate kernel's, with tb_flow's share of the time beside it.
     roof = roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown, kernel="tb_transfers_validate",
-                    pmc_leg="device")
+                    pmc_leg="device", in_place=bool(args.inplace))
     if roof is not None and args.workload != "c2":
         roof["flow_ms_share"] = round(stats["ms_replay"] / total_ms, 4)
 
@@ -1034,6 +1035,7 @@ def main():
     line["parity"] = parity
     line["headline"] = {"value": line["value"], "unit": "transfers/s", "p99_batch_latency_ms": line["p99_batch_latency_ms"],
                         "roofline_frac": roof["frac"] if roof else None,
+                        "roofline_frac_in_place_bytes": roof["in_place"]["frac"] if roof and "in_place" in roof else None,
                         "roofline_traffic": roof.get("traffic") if roof else None,
                         "host_path_value": host_path["value"] if host_path else None,
                         "staged_value": staged["value"] if staged else None}
@@ -1538,10 +1540,12 @@ def access_mix(engine, transfers, kernel_ms):
 
 
 def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=None, steps=None, kernel=None,
-             pmc_leg=None):
+             pmc_leg=None, in_place=False):
     """The dominant kernel of the timed steps against the HBM peak; `kernels` = every kernel's mean
     launch time (from the warmup steps when given: the timed steps time only validate, replay/flow
-    and whole passes)."""
+    and whole passes).  `in_place`: the prepares were committed at their transfer-log positions, so
+    validate stamps each record's 8-B timestamp instead of writing the 128-B record; the line then
+    also carries `in_place` (the same launch priced at the bytes that kernel must move)."""
     def kernel_table(stats):
         return {
             "tb_transfers_validate": (stats["ms_validate"], stats["launches_validate"]),
@@ -1596,6 +1600,16 @@ def roofline(stats, u_over_t, per_launch_transfers, args, total_ms, breakdown=No
         # round 5's driver runs of unchanged kernels read frac 0.276-0.285, round 4's same-build A/B
         # lines 0.59-0.70 ms.  The frac above is this box's.
         out["frac_box_spread"] = "about +-8% box to box for one build (DESIGN.md §4); this line is one box"
+        if in_place:
+            # §8(d)'s figure counts the groove insert's 128-B record write; committed in place the record
+            # is already at its log position (placed before the timed region, as a replica's receive DMA
+            # would) and the kernel writes only its timestamp: 128 - 8 = 120 B fewer per transfer.
+            b_ip = b_validate - 120
+            out["in_place"] = {"alg_bytes_per_transfer": round(b_ip, 1),
+                               "achieved": round(b_ip * per_launch_transfers / avg_s / 1e9, 1),
+                               "frac": round(b_ip * per_launch_transfers / avg_s / 1e9 / HBM_PEAK_GBS, 4),
+                               "definition": "the in-place launch's own minimum: event read 128, id probe + claim "
+                                             "32, timestamp stamp 8, each touched account read once (128 U/T)"}
     if pmc_leg:  # the C2 launches the PMC runs profiled (not the C3/C4 lines)
         out.update(load_pmc(pmc_leg, dom, per_launch_transfers))
     if out.get("rocprof_avg_launch_ms"):
