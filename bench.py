@@ -68,6 +68,8 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--latency-steps", type=int, default=2,
+                   help="headline steps run again after the timed ones with every pass timed (batch latency)")
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--accounts", type=int, default=None, help="default: 1M (N=1, C2); 100M (N>1, C5)")
     p.add_argument("--transfers", type=int, default=None,
@@ -760,9 +762,12 @@ def main():
             if args.warmup:
                 breakdown = engine.stats()
             engine.reset_stats()
-            # validate on the device clock only (no HIP event pair inside its span); whole passes
-            # timed for the batch latency
-            engine.profile_mask(engine.PROF_APPLY | engine.PROF_PASS | engine.PROF_REPLAY)
+            # The timed steps stamp validate's, resolve's and apply's launch spans on the device
+            # clock and record no HIP event pair: a pair on the stream holds the next launch back by a
+            # few microseconds (the bench's former pass / apply / flow pairs cost 3.8 % of a step,
+            # tools/gpu/prof_cost.py, profiles/r06/prof_cost.log).
+            # (C3 / C4: tb_flow's pair stays — its share of the step is part of the line.)
+            engine.profile_mask(engine.PROF_SPANS | (engine.PROF_REPLAY if args.workload != "c2" else 0))
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -774,6 +779,14 @@ def main():
         if timed:
             step_ms.append(allmax(dt * 1e3))
     stats = engine.stats()
+    # The batch latency: the same steps again, each pass between a HIP event pair (not timed).
+    engine.reset_stats()
+    engine.profile_mask(engine.PROF_PASS)
+    for _ in range(args.latency_steps):
+        src = headline_input()
+        ts, t_cursor = timestamps(xfer_lens, t_cursor + 10, wl["gap_every"])
+        engine.commit_device_async(129, ts, xfer_lens, src, res_dev, rb_dev)
+        engine.sync()
     pass_lat = engine.pass_latencies()
     rb = engine.to_host(rb_dev, len(xfer_lens) * 4).view(np.uint32)
     n_failed = int(rb.sum()) // 8
@@ -1004,8 +1017,9 @@ def main():
         "p99_batch_latency_ms": round(ref_percentile(pass_lat, 99), 3),
         "batch_latency_ms": dict(deciles(pass_lat), definition=(
             "per prepare, commit to reply: its device pass's duration (a prepare's reply is complete when its "
-            "%d-prepare pass is; device clock, HIP events around each pass); percentiles by "
-            "src/benchmark.zig:454-471" % args.pass_batches)),
+            "%d-prepare pass is; device clock, HIP events around each pass, in %d steps run after the timed "
+            "ones so that no event pair sits among the timed launches); percentiles by "
+            "src/benchmark.zig:454-471" % (args.pass_batches, args.latency_steps))),
         "host_path": host_path,
         "device_resident_staged": staged,
         "dependent_events": stats["dependent_events"],

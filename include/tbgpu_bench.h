@@ -45,9 +45,11 @@ int tbgpu_bench_pass_latencies(tbgpu_t* engine, double* out_ms, uint64_t cap, ui
 
 /* Which kernels TBGPU_CONFIG_PROFILE times with HIP events (every event pair on the stream costs
  * a little): bit 1 << kind, kinds 0 validate, 1 resolve, 2 replay/flow, 3 clears, 4 whole pass,
- * 5 apply_legs.  Default: all. */
+ * 5 apply_legs.  Default: all.  Any of validate, resolve, apply or TBGPU_PROF_SPANS also stamps the
+ * launch spans of validate, resolve and apply on the device clock (tbgpu_stats.span_ms); SPANS alone
+ * records no event pair (each pair on the stream separates two launches by a few microseconds). */
 enum { TBGPU_PROF_VALIDATE = 1, TBGPU_PROF_RESOLVE = 2, TBGPU_PROF_REPLAY = 4, TBGPU_PROF_CLEAR = 8,
-       TBGPU_PROF_PASS = 16, TBGPU_PROF_APPLY = 32, TBGPU_PROF_ALL = 63 };
+       TBGPU_PROF_PASS = 16, TBGPU_PROF_APPLY = 32, TBGPU_PROF_ALL = 63, TBGPU_PROF_SPANS = 64 };
 int tbgpu_bench_profile_mask(tbgpu_t* engine, uint32_t mask);
 /* Passes of at least this many create_transfers events apply balances through sorted legs
  * (k_apply.h), smaller ones with atomics (default 262144; tests set 0 to cover legs on small

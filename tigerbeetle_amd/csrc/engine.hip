@@ -87,6 +87,8 @@ static u64 pow2_at_least(u64 v) {
 #define KCLOCK_SLOTS 2048  // profiled passes between two collects (a full ring is collected early)
 
 enum { K_VALIDATE = 0, K_RESOLVE = 1, K_REPLAY = 2, K_CLEAR = 3, K_PASS = 4, K_APPLY = 5, K_COUNT = 6 };
+// prof_mask bit without an event pair: the launch spans on the device clock only (TBGPU_PROF_SPANS).
+#define K_SPANS 6
 
 struct ProfilePair {
     int kind;
@@ -980,7 +982,7 @@ static int enqueue_call(tbgpu* E, u8 op, u32 nb, const u64* h_off, const u8* eve
 
         // Launch spans of this pass's kernels on the device clock (profiling only).
         P.kclock = nullptr;
-        if (E->profile && !E->kclock_off && (E->prof_mask & ((1u << K_VALIDATE) | (1u << K_RESOLVE) | (1u << K_APPLY))) &&
+        if (E->profile && !E->kclock_off && (E->prof_mask & ((1u << K_VALIDATE) | (1u << K_RESOLVE) | (1u << K_APPLY) | (1u << K_SPANS))) &&
             E->kclock_next < KCLOCK_SLOTS) {
             const u32 slot = E->kclock_next++;
             P.kclock = E->kclock + (u64)slot * KCLOCK_WORDS;

@@ -240,6 +240,7 @@ class Engine:
         self.lib.tbgpu_reset_stats(self.h)
 
     PROF_VALIDATE, PROF_RESOLVE, PROF_REPLAY, PROF_CLEAR, PROF_PASS, PROF_APPLY, PROF_ALL = 1, 2, 4, 8, 16, 32, 63
+    PROF_SPANS = 64  # the device-clock launch spans only (no HIP event pair)
 
     def checkpoint_delta(self, caps=None, copy=True):
         """Objects changed since the previous call (groove write-back): a Delta of accounts (in no
