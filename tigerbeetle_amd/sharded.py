@@ -87,6 +87,15 @@ def _key64(ids):
     return ids[:, 0] ^ (ids[:, 1] * -7046029254386353131)  # 0x9E3779B97F4A7C15 as int64
 
 
+def _host_array(values, dtype, ctype):
+    """values as a C array for the engine (at least one element): numpy's conversion, and the array
+    object with it so that the buffer outlives the call."""
+    import ctypes
+    a = np.zeros(max(len(values), 1), dtype=dtype)
+    a[:len(values)] = np.asarray(values, dtype=dtype)
+    return a.ctypes.data_as(ctypes.POINTER(ctype))
+
+
 def _stream_sync(device):
     """Wait for torch's current stream on `device` (its work, and the RCCL collectives it waits
     on), not the whole device: a copy of the next pass on another stream keeps running."""
@@ -132,8 +141,8 @@ class GpuShard:
         send_events = torch.empty_like(events)
         slots = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
         p = _lib.tbgpu_route_plan()
-        ts = (ctypes.c_uint64 * max(nb, 1))(*[int(t) for t in timestamps])
-        ls = (ctypes.c_uint32 * max(nb, 1))(*[int(x) for x in lens])
+        ts = _host_array(timestamps, np.uint64, ctypes.c_uint64)
+        ls = _host_array(lens, np.uint32, ctypes.c_uint32)
         _stream_sync(self.device)
         _lib.check(self.lib.tbgpu_route_plan_build(self.engine.h, nb, ts, ls, events.data_ptr(),
                                                    skip.data_ptr() if skip is not None else None,
@@ -158,7 +167,7 @@ class GpuShard:
         n, nb = events.shape[0], len(lens)
         dep = torch.zeros(max(n, 1), dtype=torch.uint8, device=self.device)
         if n:
-            ls = (ctypes.c_uint32 * nb)(*[int(x) for x in lens])
+            ls = _host_array(lens, np.uint32, ctypes.c_uint32)
             marked = np.ascontiguousarray(marked, dtype=np.uint64).reshape(-1, 2)
             _stream_sync(self.device)
             _lib.check(self.lib.tbgpu_route_dependents(self.engine.h, nb, ls, events.data_ptr(),
@@ -205,7 +214,7 @@ class GpuShard:
         results = torch.empty(2 * max(n, 1), dtype=torch.int32, device=self.device)
         reply_bytes = torch.zeros(max(nb, 1), dtype=torch.int32, device=self.device)
         if nb:
-            ls = (ctypes.c_uint32 * nb)(*[int(x) for x in lens])
+            ls = _host_array(lens, np.uint32, ctypes.c_uint32)
             _stream_sync(self.device)
             _lib.check(self.lib.tbgpu_route_replies_async(self.engine.h, nb, ls, slots.data_ptr(), codes_back.data_ptr(),
                                                           results.data_ptr(), reply_bytes.data_ptr()))
