@@ -750,7 +750,7 @@ def main():
     # place: the prepares sit at their transfer-log positions (tbgpu_log_window), where a replica's
     # DMA or a peer would put them.  Each step commits all of them from the post-account-creation
     # state; bracketed by barrier + sync.
-    step_ms, issue_ms = [], []
+    step_ms, issue_ms, sync_ms = [], [], []
     t_cursor = t_end
     engine.profile_mask(engine.PROF_ALL)  # warmup: every kernel's HIP-event time (the breakdown)
     breakdown = None
@@ -774,12 +774,14 @@ def main():
         engine.commit_device_async(129, ts, xfer_lens, src, res_dev, rb_dev)
         t_issue = time.perf_counter()
         engine.sync()
+        t_sync = time.perf_counter()
         torch.cuda.synchronize()
         barrier()
         dt = time.perf_counter() - t0
         if timed:
             step_ms.append(allmax(dt * 1e3))
             issue_ms.append((t_issue - t0) * 1e3)
+            sync_ms.append((t_sync - t0) * 1e3)
     stats = engine.stats()
     # The batch latency: the same steps again, each pass between a HIP event pair (not timed).
     engine.reset_stats()
@@ -1004,6 +1006,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(total_ms / args.steps, 3),
         "step_ms": [round(x, 3) for x in step_ms], "issue_ms": [round(x, 3) for x in issue_ms],
+        "engine_sync_ms": [round(x, 3) for x in sync_ms],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -39,6 +39,7 @@ for r in range(rounds + 1):
         e.sync()
         ts, t = timestamps(x_lens, t + 10)
         e.profile_mask(mask)
+        e.reset_stats()
         t0 = time.perf_counter()
         e.commit_device_async(129, ts, x_lens, win, res, rb)
         t_issue = time.perf_counter()
@@ -46,9 +47,12 @@ for r in range(rounds + 1):
         ms = (time.perf_counter() - t0) * 1e3
         issue_ms = (t_issue - t0) * 1e3
         fails = int(e.to_host(rb, len(x_lens) * 4).view(np.uint32).sum())
+        st = e.stats()
+        val_ms = st["span_ms"][0] / st["span_launches"][0] if st.get("span_launches") and st["span_launches"][0] else None
         if r:  # round 0 warms up every mask
             out[name].append(ms)
-            print(json.dumps({"mask": name, "round": r, "ms": round(ms, 3), "issue_ms": round(issue_ms, 3), "reply_bytes": fails}), flush=True)
+            print(json.dumps({"mask": name, "round": r, "ms": round(ms, 3), "issue_ms": round(issue_ms, 3), "validate_span_ms": round(val_ms, 4) if val_ms else None,
+                              "reply_bytes": fails}), flush=True)
 print(json.dumps({"summary_ms_per_step": {k: [round(min(v), 3), round(float(np.median(v)), 3)] for k, v in out.items()},
                   "transfers": n_xfer}), flush=True)
 e.close()
